@@ -1,0 +1,121 @@
+"""Pin the CPU oracle (oracle/unet_ref_cpu.py) against the reference's own outputs.
+
+The fixtures in tests/golden/ were written by tools/gen_golden.py, which imports the
+unmodified reference (models/model.py, models/loss.py, torch AdamW as
+utils/trainer.py:41 builds it) in the build container.  On the same machine the
+restatement is bit-identical; elsewhere (different CPU, different oneDNN kernels) it
+agrees to fp32 rounding, which is what these tolerances allow.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import unet_ref_cpu as O
+from oracle import weights as W
+
+
+def _load(golden_dir, name):
+    return np.load(os.path.join(golden_dir, name), allow_pickle=False)
+
+
+def _grad_stats(grads, spec):
+    norms, sums, samp = [], [], []
+    for t, item in enumerate(spec):
+        g = grads[item[0]].double().reshape(-1)
+        idx = np.floor(W.uniform(7, 3000 + t, 64) * g.numel()).astype(np.int64)
+        norms.append(g.norm().item())
+        sums.append(g.sum().item())
+        samp.append(g[torch.from_numpy(idx)].numpy())
+    return np.array(norms), np.array(sums), np.stack(samp)
+
+
+def _check_grads(g, norms, sums, samp, rtol):
+    n, s, sm = g
+    np.testing.assert_allclose(n, norms, rtol=rtol, atol=0)
+    scale = norms[:, None]
+    assert np.all(np.abs(sm - samp) <= rtol * scale + 1e-30)
+    assert np.all(np.abs(s - sums) <= rtol * norms * 100)
+
+
+def test_param_spec_and_count():
+    spec = O.param_spec()
+    assert len(spec) == 82
+    assert sum(int(np.prod(s[1])) for s in spec) == 31_042_369
+    assert O.train_flops_per_image(256, 256) == 288_475_840_512
+
+
+def test_oracle_b2_64_three_steps(golden_dir):
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    f = _load(golden_dir, "unet_b2_64.npz")
+    P = O.make_params(42)
+    B = O.init_buffers()
+    opt = O.AdamWState(P, lr=1e-5)
+    x, t = torch.from_numpy(f["x"]), torch.from_numpy(f["t"])
+    np.testing.assert_array_equal(f["x"], W.make_input(1, 2, 1, 64, 64))
+    np.testing.assert_array_equal(f["t"], W.make_target(1, 2, 64, 64))
+    spec = O.param_spec()
+    for s in range(3):
+        r = O.train_step(P, B, opt, x, t)
+        ref = f[f"s{s}_logits"]
+        assert np.max(np.abs(r["logits"].numpy() - ref)) <= 1e-5 * np.max(np.abs(ref))
+        np.testing.assert_array_equal(O.mask_readout(r["logits"]).numpy(), f[f"s{s}_mask"])
+        assert abs(r["bce"].item() - float(f[f"s{s}_bce"])) < 1e-6
+        assert abs(r["dice"].item() - float(f[f"s{s}_dice"])) < 1e-6
+        _check_grads(_grad_stats(r["grads"], spec), f[f"s{s}_grad_norm"], f[f"s{s}_grad_sum"],
+                     f[f"s{s}_grad_samp"], rtol=1e-4)
+        psamp = np.stack([P[it[0]].reshape(-1)[torch.from_numpy(
+            np.floor(W.uniform(7, 3000 + ti, 64) * P[it[0]].numel()).astype(np.int64))].numpy()
+            for ti, it in enumerate(spec)])
+        np.testing.assert_allclose(psamp, f[f"s{s}_params_samp"], rtol=0, atol=1e-7)
+        rm = np.concatenate([B[f"{n}.running_mean"].numpy() for n in O.BN_LAYERS])
+        rv = np.concatenate([B[f"{n}.running_var"].numpy() for n in O.BN_LAYERS])
+        np.testing.assert_allclose(rm, f[f"s{s}_running_mean"], rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(rv, f[f"s{s}_running_var"], rtol=1e-5, atol=1e-6)
+        assert [B[f"{n}.num_batches_tracked"].item() for n in O.BN_LAYERS] == list(f[f"s{s}_nbt"])
+    with torch.no_grad():
+        ev = O.forward(x, P, B, training=False).numpy()
+    assert np.max(np.abs(ev - f["eval_logits"])) <= 1e-5 * np.max(np.abs(f["eval_logits"]))
+
+
+def test_oracle_b2_256(golden_dir):
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    f = _load(golden_dir, "unet_b2_256.npz")
+    P = O.make_params(42)
+    B = O.init_buffers()
+    x = torch.from_numpy(W.make_input(2, 2, 1, 256, 256))
+    t = torch.from_numpy(W.make_target(2, 2, 256, 256))
+    r = O.train_step(P, B, None, x, t)
+    flat = r["logits"].reshape(-1).numpy()
+    assert np.max(np.abs(flat[f["logit_idx"]] - f["logit_samp"])) <= 1e-5 * float(f["logit_max_abs"])
+    bits = np.packbits(O.mask_readout(r["logits"]).numpy().reshape(-1))
+    np.testing.assert_array_equal(bits, f["mask_bits"])
+    assert abs(r["loss"].item() - float(f["loss"])) < 1e-6
+    _check_grads(_grad_stats(r["grads"], O.param_spec()), f["grad_norm"], f["grad_sum"],
+                 f["grad_samp"], rtol=1e-4)
+
+
+def test_oracle_dp2_64(golden_dir):
+    f = _load(golden_dir, "unet_dp2_64.npz")
+    P = O.make_params(42)
+    B = O.init_buffers()
+    x = torch.from_numpy(W.make_input(3, 4, 1, 64, 64))
+    t = torch.from_numpy(W.make_target(3, 4, 64, 64))
+    r = O.train_step(P, B, None, x, t, shards=2)
+    assert abs(r["loss"].item() - float(f["loss"])) < 1e-6
+    _check_grads(_grad_stats(r["grads"], O.param_spec()), f["grad_norm"], f["grad_sum"],
+                 f["grad_samp"], rtol=1e-4)
+
+
+def test_oracle_negative_gamma(golden_dir):
+    f = _load(golden_dir, "unet_neg_32.npz")
+    P = O.make_params(5, -1.0, 1.0)
+    B = O.init_buffers()
+    x = torch.from_numpy(W.make_input(4, 2, 1, 32, 32))
+    t = torch.from_numpy(W.make_target(4, 2, 32, 32))
+    r = O.train_step(P, B, None, x, t)
+    ref = f["logits"]
+    assert np.max(np.abs(r["logits"].numpy() - ref)) <= 1e-5 * np.max(np.abs(ref))
+    _check_grads(_grad_stats(r["grads"], O.param_spec()), f["grad_norm"], f["grad_sum"],
+                 f["grad_samp"], rtol=1e-4)

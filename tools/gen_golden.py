@@ -1,0 +1,189 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures under tests/golden/ from the REAL reference.
+
+Runs only in the build container (it imports /root/reference, which never travels
+to the GPU box).  The reference modules used are imported unmodified:
+
+* ``models/model.py``  UNet                     (the network)
+* ``models/loss.py``   DiceLoss                 (Dice term)
+* ``torch.nn.BCEWithLogitsLoss``                (utils/trainer.py:37)
+* ``torch.optim.AdamW(params, lr)``             (utils/trainer.py:41)
+
+The step body mirrors ``utils/trainer.py:81-93`` (zero_grad, forward, losses,
+weighted sum with bce_ratio=dice_ratio=1, backward, optimizer.step).  Weights and
+inputs come from ``oracle/weights.py`` (counter hash), so the fixtures can be
+re-derived anywhere without the reference; only the *outputs* need it.
+
+Fixtures (all float64 statistics computed from fp32 results):
+  unet_b2_64.npz    B=2, 1x64x64, 3 AdamW steps: full logits, masks, losses, per-tensor
+                    grad norm/sum/samples, param samples after every step, running stats,
+                    eval-mode logits after step 3.
+  unet_b2_256.npz   B=2, 1x256x256, one step: logit samples/stats, packed mask, losses,
+                    grad norm/sum/samples.
+  unet_dp2_64.npz   B=4, 1x64x64 split into 2 DataParallel-style shards (per-shard BN,
+                    full-batch loss): losses and grad norm/sum/samples.
+  unet_neg_32.npz   B=2, 1x32x32 with BN gamma in [-1, 1] (max-pool after a sign flip),
+                    one step: full logits, grad norm/sum/samples.
+"""
+import os
+import sys
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF = "/root/reference"
+sys.path.insert(0, REPO)
+sys.path.insert(0, REF)
+
+from models.model import UNet as RefUNet  # noqa: E402  (reference)
+from models.loss import DiceLoss as RefDice  # noqa: E402  (reference)
+
+from oracle import weights as W  # noqa: E402
+from oracle import unet_ref_cpu as O  # noqa: E402
+
+OUT = os.path.join(REPO, "tests", "golden")
+NSAMP = 64
+
+
+def sample_idx(t, n):
+    return np.floor(W.uniform(7, 3000 + t, NSAMP) * n).astype(np.int64)
+
+
+def build(seed=42, gamma_lo=0.5, gamma_hi=1.5):
+    torch.manual_seed(0)
+    m = RefUNet(1, 1)
+    params = O.make_params(seed, gamma_lo, gamma_hi)
+    names = [n for n, _ in m.named_parameters()]
+    assert names == [s[0] for s in O.param_spec()], "param order mismatch"
+    sd = m.state_dict()
+    for k, v in params.items():
+        sd[k] = v.clone()
+    m.load_state_dict(sd)
+    return m
+
+
+def grad_stats(m, prefix, out):
+    names, norms, sums, samp = [], [], [], []
+    for t, (n, p) in enumerate(m.named_parameters()):
+        g = p.grad.detach().double().reshape(-1)
+        names.append(n)
+        norms.append(g.norm().item())
+        sums.append(g.sum().item())
+        samp.append(g[torch.from_numpy(sample_idx(t, g.numel()))].numpy())
+    out[f"{prefix}grad_norm"] = np.array(norms)
+    out[f"{prefix}grad_sum"] = np.array(sums)
+    out[f"{prefix}grad_samp"] = np.stack(samp)
+
+
+def param_samples(m):
+    return np.stack([p.detach().reshape(-1)[torch.from_numpy(sample_idx(t, p.numel()))].numpy()
+                     for t, (_, p) in enumerate(m.named_parameters())])
+
+
+def step(m, opt, x, t, dice):
+    bce = torch.nn.BCEWithLogitsLoss()
+    opt.zero_grad()
+    logits = m(x)
+    lb = bce(logits, t)
+    ld = dice(logits, t)
+    loss = 1.0 * lb + 1.0 * ld
+    loss.backward()
+    opt.step()
+    return logits.detach(), lb.item(), ld.item(), loss.item()
+
+
+def case_b2_64():
+    m = build()
+    m.train()
+    x = torch.from_numpy(W.make_input(1, 2, 1, 64, 64))
+    t = torch.from_numpy(W.make_target(1, 2, 64, 64))
+    opt = torch.optim.AdamW(m.parameters(), lr=1e-5)
+    dice = RefDice()
+    out = dict(x=x.numpy(), t=t.numpy(), param_names=np.array([n for n, _ in m.named_parameters()]))
+    out["params0_samp"] = param_samples(m)
+    for s in range(3):
+        logits, lb, ld, loss = step(m, opt, x, t, dice)
+        out[f"s{s}_logits"] = logits.numpy()
+        out[f"s{s}_mask"] = (torch.sigmoid(logits) > 0.5).numpy().astype(np.uint8)
+        out[f"s{s}_bce"], out[f"s{s}_dice"], out[f"s{s}_loss"] = lb, ld, loss
+        grad_stats(m, f"s{s}_", out)
+        out[f"s{s}_params_samp"] = param_samples(m)
+        bufs = dict(m.named_buffers())
+        out[f"s{s}_running_mean"] = np.concatenate([bufs[f"{n}.running_mean"].numpy() for n in O.BN_LAYERS])
+        out[f"s{s}_running_var"] = np.concatenate([bufs[f"{n}.running_var"].numpy() for n in O.BN_LAYERS])
+        out[f"s{s}_nbt"] = np.array([bufs[f"{n}.num_batches_tracked"].item() for n in O.BN_LAYERS])
+    m.eval()
+    with torch.no_grad():
+        out["eval_logits"] = m(x).numpy()
+    np.savez_compressed(os.path.join(OUT, "unet_b2_64.npz"), **out)
+
+
+def case_b2_256():
+    m = build()
+    m.train()
+    x = torch.from_numpy(W.make_input(2, 2, 1, 256, 256))
+    t = torch.from_numpy(W.make_target(2, 2, 256, 256))
+    opt = torch.optim.AdamW(m.parameters(), lr=1e-5)
+    logits, lb, ld, loss = step(m, opt, x, t, RefDice())
+    flat = logits.reshape(-1)
+    li = np.floor(W.uniform(9, 4000, 4096) * flat.numel()).astype(np.int64)
+    out = dict(logit_idx=li, logit_samp=flat[torch.from_numpy(li)].numpy(),
+               logit_max_abs=flat.abs().max().item(), logit_sum=flat.double().sum().item(),
+               logit_norm=flat.double().norm().item(),
+               mask_bits=np.packbits((torch.sigmoid(logits) > 0.5).numpy().astype(np.uint8).reshape(-1)),
+               bce=lb, dice=ld, loss=loss)
+    grad_stats(m, "", out)
+    np.savez_compressed(os.path.join(OUT, "unet_b2_256.npz"), **out)
+
+
+def case_dp2_64():
+    """nn.DataParallel numerics (utils/trainer.py:28-30): scatter dim 0, per-replica BN,
+    gather logits, loss on the full batch, grads summed over replicas."""
+    m = build()
+    m.train()
+    x = torch.from_numpy(W.make_input(3, 4, 1, 64, 64))
+    t = torch.from_numpy(W.make_target(3, 4, 64, 64))
+    bns = [mod for mod in m.modules() if isinstance(mod, torch.nn.BatchNorm2d)]
+    bufs0 = [(b.running_mean.clone(), b.running_var.clone(), b.num_batches_tracked.clone()) for b in bns]
+    outs = []
+    for s, xs in enumerate(torch.chunk(x, 2, 0)):
+        if s > 0:  # replica s>0 gets its own broadcast copy of the buffers; replica 0's are kept
+            keep = [(b.running_mean, b.running_var, b.num_batches_tracked) for b in bns]
+            for b, (rm, rv, nb) in zip(bns, bufs0):
+                b.running_mean, b.running_var, b.num_batches_tracked = rm.clone(), rv.clone(), nb.clone()
+        outs.append(m(xs))
+        if s > 0:
+            for b, (rm, rv, nb) in zip(bns, keep):
+                b.running_mean, b.running_var, b.num_batches_tracked = rm, rv, nb
+    logits = torch.cat(outs, 0)
+    lb = torch.nn.BCEWithLogitsLoss()(logits, t)
+    ld = RefDice()(logits, t)
+    loss = lb + ld
+    loss.backward()
+    out = dict(bce=lb.item(), dice=ld.item(), loss=loss.item(), logits=logits.detach().numpy())
+    grad_stats(m, "", out)
+    np.savez_compressed(os.path.join(OUT, "unet_dp2_64.npz"), **out)
+
+
+def case_neg_32():
+    m = build(seed=5, gamma_lo=-1.0, gamma_hi=1.0)
+    m.train()
+    x = torch.from_numpy(W.make_input(4, 2, 1, 32, 32))
+    t = torch.from_numpy(W.make_target(4, 2, 32, 32))
+    opt = torch.optim.AdamW(m.parameters(), lr=1e-5)
+    logits, lb, ld, loss = step(m, opt, x, t, RefDice())
+    out = dict(logits=logits.numpy(), bce=lb, dice=ld, loss=loss)
+    grad_stats(m, "", out)
+    np.savez_compressed(os.path.join(OUT, "unet_neg_32.npz"), **out)
+
+
+if __name__ == "__main__":
+    torch.set_num_threads(8)
+    os.makedirs(OUT, exist_ok=True)
+    case_b2_64()
+    case_b2_256()
+    case_dp2_64()
+    case_neg_32()
+    for f in sorted(os.listdir(OUT)):
+        print(f, os.path.getsize(os.path.join(OUT, f)))
