@@ -1,0 +1,154 @@
+/*
+ * unet_hip.h - C ABI of libunet_hip.so, the MI355X-native (gfx950) UNet training /
+ * inference path for the DDTI thyroid-nodule workload.
+ *
+ * The reference (WuJiaqiii/Thyroid-nodule-image-segmentation-UNet-DDTI) is pure Python;
+ * its hot path is PyTorch autograd over models/model.py:UNet plus the losses and the
+ * optimizer step driven by utils/trainer.py.  Each entry point below replaces one
+ * call site of that path (file:line in the reference):
+ *
+ *   unet_create / unet_destroy      models/model.py:6-31   UNet.__init__ (topology only;
+ *                                                           parameters stay torch-owned)
+ *   unet_param_info / unet_bn_info  models/model.py:6-31   named_parameters()/named_buffers()
+ *                                                           order, shapes and flat offsets
+ *   unet_workspace_size             (new)                  device scratch the caller allocates
+ *   unet_forward                    models/model.py:53-73  UNet.forward (train: batch-stat BN
+ *                                                           + running-stat update; eval:
+ *                                                           running-stat BN), called from
+ *                                                           utils/trainer.py:84,139,216
+ *   unet_backward                   utils/trainer.py:91    loss.backward() through the UNet
+ *   unet_loss_fwd                   utils/trainer.py:85-87 BCEWithLogitsLoss, models/loss.py:13-24
+ *                                                           DiceLoss, models/loss.py:34-46
+ *                                                           FocalTverskyLoss
+ *   unet_loss_bwd                   utils/trainer.py:90-91 d(weighted loss)/d(logits)
+ *   unet_adamw                      utils/trainer.py:41,92 AdamW.step (torch optim/adam.py
+ *                                                           _single_tensor_adam, decoupled wd)
+ *   unet_mask_counts                utils/trainer.py:217,236-242  sigmoid(x)>0.5 masks and
+ *                                                           TP/FP/FN/TN counts
+ *   unet_bucket_* / unet_stream_wait_bucket   utils/trainer.py:28-30 nn.DataParallel grad
+ *                                   reduction -> per-bucket readiness for an RCCL all-reduce
+ *                                   overlapped with the rest of the backward pass
+ *
+ * Conventions: every function returns 0 (UNET_OK) or a negative unet_status and never
+ * throws across the ABI; unet_last_error() returns the text of the last failure on that
+ * context.  All pointers are device pointers owned by the caller (PyTorch) unless noted;
+ * the library only borrows them for the duration of the call.  Work is enqueued on the
+ * caller's stream with no host synchronisation.  A context is not re-entrant.
+ *
+ * Tensor layouts at the boundary are the reference's: x (N, Cin, H, W), logits
+ * (N, Cout, H, W), parameters in torch layout (Conv2d [Cout,Cin,kh,kw],
+ * ConvTranspose2d [Cin,Cout,2,2]) packed back to back in named_parameters() order in one
+ * flat fp32 arena (offsets from unet_param_info).  BN buffers: running_mean and
+ * running_var in one fp32 arena (layer i: mean at bn_off[i], var at bn_off[i]+C_i) and
+ * num_batches_tracked in an int64 array, one per BN layer.
+ */
+#ifndef UNET_HIP_H
+#define UNET_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct unet_ctx unet_ctx;
+typedef void* unet_stream_t; /* hipStream_t (0 = legacy default stream) */
+
+typedef enum {
+    UNET_OK = 0,
+    UNET_ERR_INVALID = -1,     /* null pointer / bad argument */
+    UNET_ERR_SHAPE = -2,       /* H or W not divisible by 16, N < 1, ... */
+    UNET_ERR_HIP = -3,         /* a HIP runtime call failed */
+    UNET_ERR_WORKSPACE = -4,   /* workspace too small */
+    UNET_ERR_UNSUPPORTED = -5  /* configuration not implemented */
+} unet_status;
+
+typedef struct {
+    int in_channels;   /* models/model.py:6 in_channels (default 1)  */
+    int out_channels;  /* models/model.py:6 out_channels (default 1) */
+} unet_cfg;
+
+/* models/model.py:6-31.  device = HIP ordinal the context will launch on. */
+int unet_create(const unet_cfg* cfg, int device, unet_ctx** out);
+int unet_destroy(unet_ctx* ctx);
+const char* unet_last_error(const unet_ctx* ctx);
+
+/* Parameter table in named_parameters() order.  n_floats = size of the flat arena. */
+int unet_num_params(const unet_ctx* ctx, int* n_tensors, int64_t* n_floats);
+/* name: static string owned by the library; shape: up to 4 dims. */
+int unet_param_info(const unet_ctx* ctx, int i, const char** name, int* ndim, int64_t shape[4],
+                    int64_t* offset);
+/* BN layer table: n_layers, total floats of the running-stat arena (mean|var per layer). */
+int unet_num_bn(const unet_ctx* ctx, int* n_layers, int64_t* n_floats);
+int unet_bn_info(const unet_ctx* ctx, int i, const char** name, int* channels, int64_t* offset);
+
+/* Bytes of device workspace for one forward (+backward when training) at (N, H, W). */
+int unet_workspace_size(unet_ctx* ctx, int N, int H, int W, int training, size_t* bytes);
+
+/* Forward.  params: flat arena; bn_running: running-stat arena (updated when training);
+ * bn_count: int64[n_bn] num_batches_tracked (incremented when training); x: (N,Cin,H,W);
+ * logits: (N,Cout,H,W).  The workspace keeps what backward needs; pass the same one. */
+int unet_forward(unet_ctx* ctx, const float* params, float* bn_running, int64_t* bn_count,
+                 const float* x, float* logits, void* workspace, size_t ws_bytes, int N, int H,
+                 int W, int training, unet_stream_t stream);
+
+/* Backward of the last training forward run with this workspace.  dlogits: (N,Cout,H,W).
+ * grads: flat arena laid out like params; every entry is overwritten (zero_grad -> None
+ * semantics, utils/trainer.py:81). */
+int unet_backward(unet_ctx* ctx, const float* params, const float* dlogits, float* grads,
+                  void* workspace, size_t ws_bytes, int N, int H, int W, unet_stream_t stream);
+
+/* Losses over logits/targets (N, C, H, W) (targets may be soft, e.g. mixup).
+ * stats: device fp32[4*N + 8] scratch the caller keeps for unet_loss_bwd.
+ * losses: device fp32[3] <- {bce_mean, dice_loss, focal_tversky_loss}.
+ * focal uses (alpha, beta, gamma) of utils/trainer.py:38 / models/loss.py:27 defaults. */
+int unet_loss_fwd(unet_ctx* ctx, const float* logits, const float* targets, int N, int C, int H,
+                  int W, float* stats, float* losses, float focal_alpha, float focal_beta,
+                  float focal_gamma, unet_stream_t stream);
+/* dlogits = w[0]*dBCE + w[1]*dDice + w[2]*dFocal, w a device fp32[3]. */
+int unet_loss_bwd(unet_ctx* ctx, const float* logits, const float* targets, int N, int C, int H,
+                  int W, const float* stats, const float* w, float* dlogits, float focal_alpha,
+                  float focal_beta, float focal_gamma, unet_stream_t stream);
+
+/* AdamW over flat arenas of n floats (one launch for all 82 tensors).
+ * grads are multiplied by grad_scale first (1/world_size after an RCCL sum). */
+int unet_adamw(unet_ctx* ctx, float* params, const float* grads, float* exp_avg,
+               float* exp_avg_sq, int64_t n, int step, float lr, float beta1, float beta2,
+               float eps, float weight_decay, float grad_scale, unet_stream_t stream);
+
+/* Mask readout + confusion counts: counts (device int64[4]) += {TP, FP, FN, TN} of
+ * (sigmoid(logits) > 0.5) vs (targets cast to uint8 == 1), utils/trainer.py:217-242.
+ * mask (optional, may be null): uint8 (N,C,H,W). */
+int unet_mask_counts(unet_ctx* ctx, const float* logits, const float* targets, int64_t n,
+                     uint8_t* mask, int64_t* counts, unet_stream_t stream);
+
+/* Gradient buckets for data-parallel overlap.  Bucket b covers grads[offset, offset+len)
+ * and is complete once the event recorded by unet_backward for it has fired; buckets
+ * become ready in order 0, 1, ... (decoder first). */
+int unet_num_buckets(const unet_ctx* ctx, int* n);
+int unet_bucket_range(const unet_ctx* ctx, int b, int64_t* offset, int64_t* len);
+/* Make `stream` wait (device-side) until bucket b of the last backward is complete. */
+int unet_stream_wait_bucket(unet_ctx* ctx, int b, unet_stream_t stream);
+
+/* Per-kernel timing: when enabled, unet_forward/unet_backward bracket every launch with
+ * HIP events; unet_timing_read synchronises and returns, per kernel family, the launch
+ * count, total ms and algorithmic FLOP of the last call(s) since the last reset. */
+int unet_timing_enable(unet_ctx* ctx, int enable);
+int unet_timing_reset(unet_ctx* ctx);
+int unet_timing_count(unet_ctx* ctx, int* n_families);
+int unet_timing_read(unet_ctx* ctx, int i, const char** family, int64_t* launches,
+                     double* total_ms, double* flop);
+
+/* Debug/test view into a workspace: byte offset of an intermediate tensor.
+ * kind: 0 y[i] (post-ReLU conv output, NHWC, channel stride *ld, channel offset *off),
+ *       1 BN scale[i], 2 BN shift[i], 3 BN batch mean[i], 4 BN invstd[i],
+ *       5 pooled[l] (NHWC dense), 6 concat buffer[l] (NHWC, 2*64<<l channels),
+ *       7 d(concat)[l] of the last backward.  *count = elements (pixels*ld for NHWC). */
+int unet_debug_view(unet_ctx* ctx, int N, int H, int W, int training, int kind, int index,
+                    int64_t* byte_offset, int64_t* count, int* ld, int* off);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* UNET_HIP_H */

@@ -103,13 +103,20 @@ def _bn(x, P, B, name, training):
                         P[f"{name}.weight"], P[f"{name}.bias"], training, BN_MOMENTUM, BN_EPS)
 
 
+_RECORD = None  # test hook: list collecting the post-ReLU (pre-BN) output of every conv
+
+
 def _conv_block(x, P, B, prefix, training):
     # models/model.py:33-43
     x = F.conv2d(x, P[f"{prefix}.0.weight"], P[f"{prefix}.0.bias"], padding=1)
     x = F.relu(x)
+    if _RECORD is not None:
+        _RECORD.append(x.detach())
     x = _bn(x, P, B, f"{prefix}.2", training)
     x = F.conv2d(x, P[f"{prefix}.3.weight"], P[f"{prefix}.3.bias"], padding=1)
     x = F.relu(x)
+    if _RECORD is not None:
+        _RECORD.append(x.detach())
     x = _bn(x, P, B, f"{prefix}.5", training)
     return x
 
@@ -118,8 +125,18 @@ def _convT(x, P, name):
     return F.conv_transpose2d(x, P[f"{name}.weight"], P[f"{name}.bias"], stride=2)
 
 
-def forward(x, P, B, training=True):
-    """models/model.py:53-73.  P: params (name -> tensor), B: buffers (mutated in train mode)."""
+def forward(x, P, B, training=True, record=None):
+    """models/model.py:53-73.  P: params (name -> tensor), B: buffers (mutated in train mode).
+    record: optional list that receives the 18 post-ReLU conv outputs (test diagnostics)."""
+    global _RECORD
+    _RECORD = record
+    try:
+        return _forward(x, P, B, training)
+    finally:
+        _RECORD = None
+
+
+def _forward(x, P, B, training):
     enc1 = _conv_block(x, P, B, "encoder1", training)
     enc2 = _conv_block(F.max_pool2d(enc1, 2), P, B, "encoder2", training)
     enc3 = _conv_block(F.max_pool2d(enc2, 2), P, B, "encoder3", training)

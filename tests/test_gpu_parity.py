@@ -1,0 +1,260 @@
+"""GPU parity of the HIP path (libunet_hip.so through its C ABI) against the CPU oracle and
+the reference-generated golden fixtures.
+
+Tolerances (north star / SURVEY.md §8c):
+* forward logits: max|d| <= 1e-4 * max|ref|   ("1e-4 relative fp32")
+* losses: |d| <= 1e-5 (absolute, losses are O(1))
+* masks: bit-exact except where |ref logit| <= 1e-3 * max|ref| (forward error bound)
+* gradients: norm-relative <= 1e-2 per tensor (the reference's own fp32-vs-fp64 error is
+  ~4e-3); in practice the kernels land around 1e-5..1e-4
+* AdamW-updated params: |d| <= 1e-7 absolute at lr 1e-5 (identical op order)
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from _helpers import grad_errors, hip_model, inputs, masks_agree, norm_rel, rel_max
+from oracle import unet_ref_cpu as O
+from oracle import weights as Wt
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda:0")
+LOGIT_TOL = 1e-4
+GRAD_TOL = 1e-2
+
+
+@pytest.fixture(autouse=True, scope="module")
+def _threads():
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+
+
+def _golden(golden_dir, name):
+    return np.load(os.path.join(golden_dir, name), allow_pickle=False)
+
+
+def _step(m, opt, x, t, w_bce=1.0, w_dice=1.0):
+    import unet_hip
+    opt.zero_grad()
+    logits = m(x)
+    losses = unet_hip.seg_losses(logits, t)
+    loss = w_bce * losses[0] + w_dice * losses[1]
+    loss.backward()
+    opt.step()
+    return logits.detach(), losses.detach(), loss.detach()
+
+
+def test_forward_layers_match_oracle():
+    """Every conv layer's post-ReLU output (pre-BN) vs the oracle, train-mode BN, B=2 64x64."""
+    P = O.make_params(42)
+    x, _ = inputs(1, 2, 64, 64)
+    rec = []
+    ref = O.forward(x, P, O.init_buffers(), True, record=rec)
+    m = hip_model(P, DEV)
+    st = m.flatten_()
+    with torch.no_grad():
+        logits, ws = st.rt.forward(st.param_arena, st.bn_arena, st.nbt_arena, x.to(DEV), training=True)
+    torch.cuda.synchronize()
+    errs = []
+    for i in range(18):
+        v, off = st.rt.debug_view(ws, 2, 64, 64, True, 0, i)
+        C = rec[i].shape[1]
+        got = v[:, off:off + C].cpu().numpy()
+        want = rec[i].permute(0, 2, 3, 1).reshape(-1, C).numpy()
+        errs.append(rel_max(got, want))
+    assert max(errs) <= LOGIT_TOL, f"per-layer rel errors: {np.array(errs)}"
+    assert rel_max(logits.cpu().numpy(), ref.numpy()) <= LOGIT_TOL
+
+
+def test_train_steps_match_golden(golden_dir):
+    """Three full training steps (fwd, BCE+Dice, bwd, AdamW) vs the reference's own outputs."""
+    import unet_hip
+    f = _golden(golden_dir, "unet_b2_64.npz")
+    m = hip_model(O.make_params(42), DEV)
+    opt = unet_hip.HipAdamW(m.parameters(), lr=1e-5)
+    x, t = torch.from_numpy(f["x"]).to(DEV), torch.from_numpy(f["t"]).to(DEV)
+    spec = O.param_spec()
+    for s in range(3):
+        logits, losses, loss = _step(m, opt, x, t)
+        ref = f[f"s{s}_logits"]
+        lg = logits.cpu().numpy()
+        assert rel_max(lg, ref) <= LOGIT_TOL, f"step {s} logits"
+        ok, nd = masks_agree((torch.sigmoid(logits) > 0.5).cpu().numpy().astype(np.uint8),
+                             f[f"s{s}_mask"], ref, 1e-3 * np.abs(ref).max())
+        assert ok, f"step {s}: {nd} mask bits differ away from the decision boundary"
+        assert abs(losses[0].item() - float(f[f"s{s}_bce"])) <= 1e-5
+        assert abs(losses[1].item() - float(f[f"s{s}_dice"])) <= 1e-5
+        # gradients: per-tensor norm and the 64 fixed samples, relative to the tensor norm
+        norms = f[f"s{s}_grad_norm"]
+        samp = f[f"s{s}_grad_samp"]
+        for ti, item in enumerate(spec):
+            g = dict(m.named_parameters())[item[0]].grad.detach().double().cpu().reshape(-1)
+            idx = np.floor(Wt.uniform(7, 3000 + ti, 64) * g.numel()).astype(np.int64)
+            assert abs(g.norm().item() - norms[ti]) <= GRAD_TOL * norms[ti], item[0]
+            assert np.max(np.abs(g[idx].numpy() - samp[ti])) <= GRAD_TOL * norms[ti], item[0]
+        # post-AdamW parameters
+        pnow = dict(m.named_parameters())
+        ps = np.stack([pnow[it[0]].detach().cpu().reshape(-1)[torch.from_numpy(
+            np.floor(Wt.uniform(7, 3000 + ti, 64) * pnow[it[0]].numel()).astype(np.int64))].numpy()
+            for ti, it in enumerate(spec)])
+        np.testing.assert_allclose(ps, f[f"s{s}_params_samp"], rtol=0, atol=1e-7)
+        rm = torch.cat([m.state_dict()[f"{n}.running_mean"].cpu() for n in O.BN_LAYERS]).numpy()
+        rv = torch.cat([m.state_dict()[f"{n}.running_var"].cpu() for n in O.BN_LAYERS]).numpy()
+        np.testing.assert_allclose(rm, f[f"s{s}_running_mean"], rtol=1e-4, atol=1e-5)
+        np.testing.assert_allclose(rv, f[f"s{s}_running_var"], rtol=1e-4, atol=1e-5)
+        nbt = [int(m.state_dict()[f"{n}.num_batches_tracked"]) for n in O.BN_LAYERS]
+        assert nbt == list(f[f"s{s}_nbt"])
+    m.eval()
+    with torch.no_grad():
+        ev = m(x).cpu().numpy()
+    assert rel_max(ev, f["eval_logits"]) <= LOGIT_TOL
+
+
+def test_full_grads_vs_oracle_64():
+    """Every element of every gradient vs the oracle (not just the fixture samples)."""
+    P = O.make_params(42)
+    x, t = inputs(1, 2, 64, 64)
+    ref = O.train_step(P, O.init_buffers(), None, x, t)
+    m = hip_model(P, DEV)
+    import unet_hip
+    logits = m(x.to(DEV))
+    losses = unet_hip.seg_losses(logits, t.to(DEV))
+    (losses[0] + losses[1]).backward()
+    errs = grad_errors(m, ref["grads"])
+    worst = max(errs, key=errs.get)
+    assert errs[worst] <= GRAD_TOL, f"{worst}: {errs[worst]:.3e}"
+
+
+def test_b2_256_matches_golden(golden_dir):
+    import unet_hip
+    f = _golden(golden_dir, "unet_b2_256.npz")
+    m = hip_model(O.make_params(42), DEV)
+    x, t = inputs(2, 2, 256, 256)
+    logits = m(x.to(DEV))
+    losses = unet_hip.seg_losses(logits, t.to(DEV))
+    loss = losses[0] + losses[1]
+    loss.backward()
+    flat = logits.detach().reshape(-1).cpu().numpy()
+    mx = float(f["logit_max_abs"])
+    assert np.max(np.abs(flat[f["logit_idx"]] - f["logit_samp"])) <= LOGIT_TOL * mx
+    assert abs(np.abs(flat).max() - mx) <= LOGIT_TOL * mx
+    bits = np.unpackbits(f["mask_bits"])[:flat.size]
+    mask = (1 / (1 + np.exp(-flat.astype(np.float64))) > 0.5).astype(np.uint8)
+    diff = mask != bits
+    assert diff.sum() == 0 or np.all(np.abs(flat[diff]) <= 1e-3 * mx), f"{diff.sum()} mask bits"
+    assert abs(loss.item() - float(f["loss"])) <= 1e-5
+    for ti, (name, p) in enumerate(m.named_parameters()):
+        n = p.grad.detach().double().norm().item()
+        assert abs(n - f["grad_norm"][ti]) <= GRAD_TOL * f["grad_norm"][ti], name
+
+
+def test_negative_gamma_matches_golden(golden_dir):
+    """BN gamma < 0 before max-pool (max of BN(y), not BN of max(y)) and 2x2 bottleneck."""
+    import unet_hip
+    f = _golden(golden_dir, "unet_neg_32.npz")
+    m = hip_model(O.make_params(5, -1.0, 1.0), DEV)
+    x, t = inputs(4, 2, 32, 32)
+    logits = m(x.to(DEV))
+    losses = unet_hip.seg_losses(logits, t.to(DEV))
+    (losses[0] + losses[1]).backward()
+    assert rel_max(logits.detach().cpu().numpy(), f["logits"]) <= LOGIT_TOL
+    for ti, (name, p) in enumerate(m.named_parameters()):
+        n = p.grad.detach().double().norm().item()
+        assert abs(n - f["grad_norm"][ti]) <= GRAD_TOL * f["grad_norm"][ti], name
+
+
+def test_losses_and_grads_vs_torch():
+    """Fused BCE/Dice/FocalTversky kernel vs torch fp32 ops (incl. soft targets, mixup)."""
+    import unet_hip
+    g = torch.Generator().manual_seed(3)
+    x = (torch.randn(4, 1, 96, 80, generator=g) * 4).to(DEV)
+    t = torch.rand(4, 1, 96, 80, generator=g).to(DEV)  # soft targets
+    w = torch.tensor([0.7, 1.3, 0.5], device=DEV)
+    xr = x.clone().requires_grad_(True)
+    pr = torch.sigmoid(xr)
+    bce = torch.nn.functional.binary_cross_entropy_with_logits(xr, t)
+    pf, tf = pr.view(4, -1), t.view(4, -1)
+    dice = 1 - ((2 * (pf * tf).sum(1) + 1) / (pf.sum(1) + tf.sum(1) + 1)).mean()
+    TP = (pr * t).sum()
+    FP = (pr * (1 - t)).sum()
+    FN = ((1 - pr) * t).sum()
+    ti = (TP + 1e-6) / (TP + 0.4 * FP + 0.6 * FN + 1e-6)
+    focal = (1 - ti) ** 2.0
+    (w[0] * bce + w[1] * dice + w[2] * focal).backward()
+    xh = x.clone().requires_grad_(True)
+    l = unet_hip.seg_losses(xh, t)
+    (w * l).sum().backward()
+    ref = torch.stack([bce, dice, focal]).detach()
+    assert torch.allclose(l.detach(), ref, rtol=1e-5, atol=1e-6), (l, ref)
+    assert norm_rel(xh.grad.cpu(), xr.grad.cpu()) <= 1e-4
+
+
+def test_adamw_vs_torch():
+    import unet_hip
+    g = torch.Generator().manual_seed(5)
+    p0 = torch.randn(1000003, generator=g).to(DEV)
+    pa = torch.nn.Parameter(p0.clone())
+    pb = torch.nn.Parameter(p0.clone())
+    oa = torch.optim.AdamW([pa], lr=1e-3, foreach=False)
+    ob = unet_hip.HipAdamW([pb], lr=1e-3)
+    for _ in range(4):
+        gr = torch.randn(1000003, generator=g).to(DEV)
+        pa.grad = gr.clone()
+        pb.grad = gr.clone()
+        oa.step()
+        ob.step()
+    assert torch.max(torch.abs(pa - pb)).item() <= 1e-6
+
+
+def test_mask_counts():
+    import unet_hip
+    g = torch.Generator().manual_seed(9)
+    x = torch.randn(3, 1, 64, 48, generator=g).to(DEV)
+    t = (torch.rand(3, 1, 64, 48, generator=g) > 0.6).float().to(DEV)
+    rt = unet_hip.UNetRuntime.get(DEV)
+    counts = torch.zeros(4, dtype=torch.int64, device=DEV)
+    mask = torch.empty(x.shape, dtype=torch.uint8, device=DEV)
+    rt.mask_counts(x, t, counts, mask)
+    pm = (torch.sigmoid(x) > 0.5)
+    tm = t.to(torch.uint8) == 1
+    want = [int((pm & tm).sum()), int((pm & ~tm).sum()), int((~pm & tm).sum()), int((~pm & ~tm).sum())]
+    assert counts.cpu().tolist() == want
+    assert torch.equal(mask.bool(), pm)
+
+
+def test_full_size_vs_torch_gpu_reference():
+    """bs=32, 1x256x256 (BASELINE config 2): forward and gradients vs the oracle's functional
+    graph evaluated by torch fp32 on the same GPU (the CPU oracle would take ~20 s/step)."""
+    import unet_hip
+    P = O.make_params(42)
+    x, t = inputs(11, 32, 256, 256)
+    Pd = {k: v.to(DEV) for k, v in P.items()}
+    Bd = {k: v.to(DEV) for k, v in O.init_buffers().items()}
+    ref = O.train_step(Pd, Bd, None, x.to(DEV), t.to(DEV))
+    m = hip_model(P, DEV)
+    logits = m(x.to(DEV))
+    losses = unet_hip.seg_losses(logits, t.to(DEV))
+    (losses[0] + losses[1]).backward()
+    assert rel_max(logits.detach().cpu().numpy(), ref["logits"].cpu().numpy()) <= LOGIT_TOL
+    errs = grad_errors(m, {k: v.cpu() for k, v in ref["grads"].items()})
+    worst = max(errs, key=errs.get)
+    assert errs[worst] <= GRAD_TOL, f"{worst}: {errs[worst]:.3e}"
+
+
+def test_determinism_full_size():
+    """Two identical training forwards+backwards are bit-identical (no float atomics)."""
+    import unet_hip
+    P = O.make_params(42)
+    x, t = inputs(12, 8, 256, 256)
+    outs = []
+    for _ in range(2):
+        m = hip_model(P, DEV)
+        logits = m(x.to(DEV))
+        l = unet_hip.seg_losses(logits, t.to(DEV))
+        (l[0] + l[1]).backward()
+        outs.append((logits.detach().clone(), m.flat_params.grad if False else
+                     m._state.grad_arena.clone()))
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])

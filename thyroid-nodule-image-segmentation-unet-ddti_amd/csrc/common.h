@@ -1,0 +1,67 @@
+// Shared definitions for the gfx950 UNet kernels (internal; the public ABI is
+// include/unet_hip.h).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// How the rows of a GEMM operand are gathered from an NHWC activation.
+//   G_CONV3: 3x3 / pad 1 taps on the row grid (tap t -> dy = t/3-1, dx = t%3-1),
+//            out-of-image taps read as zero (post-BN zero padding, models/model.py:36).
+//   G_IDENT: one tap, row = pixel.
+//   G_UP2  : four taps (a,b) = (t>>1, t&1) reading pixel (2y+a, 2x+b) of a grid twice
+//            the row grid (ConvTranspose2d k2 s2, models/model.py:19,49).
+enum GatherMode { G_CONV3 = 0, G_IDENT = 1, G_UP2 = 2 };
+
+static inline int gather_taps(int mode) { return mode == G_CONV3 ? 9 : (mode == G_UP2 ? 4 : 1); }
+
+// Epilogues of the pixel-row GEMM.
+//   E_STORE          : out[m][n] = acc            (dgrad)
+//   E_BIAS_RELU_STATS: out[m][n] = relu(acc+b[n]) + per-block column sum / sum of squares
+//                      for the following BatchNorm (models/model.py:36-38)
+//   E_CONVT          : ConvTranspose2d scatter, n = (a*2+b)*cout + co ->
+//                      out[(2y+a, 2x+b)][co] = acc + b[co]  (models/model.py:19)
+enum EpiMode { E_STORE = 0, E_BIAS_RELU_STATS = 1, E_CONVT = 2 };
+
+struct RowGemmArgs {
+    int H, W;        // row grid (rows = Nimg*H*W pixels)
+    int M, N, K;     // GEMM sizes; K = taps * C
+    const float* a;  // NHWC source of A rows
+    int lda, aoff, C, amode;
+    const float* ascale;  // per-channel affine applied to valid A values (BN fused in the
+    const float* ashift;  // consumer's prologue); null = identity
+    const float* bt;      // B^T, row-major [N][K]
+    float* out;
+    int ldo, ooff;
+    const float* bias;
+    float* stats;  // [M/BM][2][N] partial (sum, sumsq)
+    int cout;      // E_CONVT
+    int emode;
+};
+
+struct WgradArgs {
+    int H, W;   // pixel grid of the reduction rows (P = Nimg*H*W)
+    int P;
+    const float* a;  // A' rows: gather(a, amode, tapA) channels [ca0, ca0+BM)
+    int lda, aoff, CA, amode;
+    const float* ascale;
+    const float* ashift;
+    const float* b;  // B' rows: gather(b, bmode, tapB) channels [cb0, cb0+BN)
+    int ldb, boff, CB, bmode;
+    int Mw, Nw;      // tapsA*CA, tapsB*CB
+    int pps;         // pixels per split (multiple of the pixel chunk)
+    int splits;
+    float* slab;     // [splits][Mw][Nw]
+};
+
+#define HIP_OK(x)                                   \
+    do {                                            \
+        hipError_t e_ = (x);                        \
+        if (e_ != hipSuccess) return (int)e_;       \
+    } while (0)
+
+// host launchers (kernels_gemm.hip)
+int launch_rowgemm(const RowGemmArgs& a, int bm, int bn, hipStream_t s);
+int launch_wgrad(const WgradArgs& a, int bm, int bn, hipStream_t s);

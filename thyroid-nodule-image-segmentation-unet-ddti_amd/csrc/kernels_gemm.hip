@@ -1,0 +1,382 @@
+// Implicit-GEMM kernels for the UNet convolutions on gfx950, fp32 in / fp32 accumulate on
+// the matrix cores (v_mfma_f32_32x32x2_f32: exact f32 fmaf chains at 64 FLOP/clk/SIMD).
+//
+// Two families cover every conv-shaped op of models/model.py:UNet:
+//
+//  rowgemm  C[m][n] = sum_k A[m][k] * Bt[n][k], rows m = output pixels (NHWC), k = (tap, c)
+//           * Conv2d 3x3 pad 1 forward        (model.py:36,39)  A = gather G_CONV3 of the
+//             BN-normalised input (affine applied in the load, zero padding kept zero),
+//             Bt = weights packed [Cout][tap][Cin]; epilogue bias + ReLU (model.py:37,40)
+//             + BatchNorm batch-stat partials.
+//           * Conv2d 3x3 dgrad                 A = gather G_CONV3 of dZ, Bt = flipped weights
+//             packed [Cin][tap'][Cout].
+//           * ConvTranspose2d k2 s2 forward    (model.py:19,49) A = G_IDENT, Bt = [(a,b,co)][ci],
+//             epilogue scatters the 2x2 output pixels into the concat buffer's channel slice
+//             (torch.cat([up, skip]) of model.py:64-70 costs no copy).
+//           * ConvTranspose2d dgrad            A = gather G_UP2 of dOut, Bt = [ci][(a,b,co)].
+//  wgrad    C[m][n] = sum_p A'[p][m] * B'[p][n], reduction over pixels p, split over `splits`
+//           slices into fp32 slabs (deterministic: the slab reducer adds them in order).
+//
+// Tiling: 256 threads = 4 waves (2x2), block tile BM x BN, wave tile (BM/2) x (BN/2) made of
+// 32x32 MFMA accumulators.  Operands go HBM/L2 -> registers (issued one K-chunk ahead) ->
+// LDS -> registers.  K-order inside an 8-wide chunk is permuted so each lane fetches its
+// four k values with one ds_read_b128: lane half h owns k = 4h..4h+3 and MFMA step s sums
+// k = s (h=0) and k = 4+s (h=1) -- A and B use the same permutation, so the product is the
+// same sum in a different order.
+#include "common.h"
+
+namespace {
+
+__device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+struct Pix {
+    int img, y, x;
+};
+
+__device__ __forceinline__ Pix decode(int m, int H, int W) {
+    Pix r;
+    int t = m / W;
+    r.x = m - t * W;
+    r.img = t / H;
+    r.y = t - r.img * H;
+    return r;
+}
+
+// Source pixel of row pixel `q` (on grid HxW) for `tap` in `mode`; `valid` false for
+// zero-padding taps (the returned index is then the row pixel itself, always in range).
+__device__ __forceinline__ int gather_src(int mode, int tap, int m, Pix q, int H, int W,
+                                          bool& valid) {
+    if (mode == G_CONV3) {
+        int yy = q.y + tap / 3 - 1, xx = q.x + tap % 3 - 1;
+        valid = (yy >= 0) & (yy < H) & (xx >= 0) & (xx < W);
+        return valid ? (q.img * H + yy) * W + xx : m;
+    }
+    valid = true;
+    if (mode == G_UP2) {
+        int a = tap >> 1, b = tap & 1;
+        return (q.img * 2 * H + 2 * q.y + a) * (2 * W) + 2 * q.x + b;
+    }
+    return m;
+}
+
+template <int BM, int BN, int BK, int WM, int WN>
+__global__ __launch_bounds__(256, 2) void rowgemm_kernel(RowGemmArgs p) {
+    constexpr int LDK = BK + 4;  // 16-B pad: conflict-free ds_read_b128 (row stride 144 B)
+    constexpr int MT = WM / 32, NT = WN / 32;
+    constexpr int WAVES_N = BN / WN;
+    constexpr int F4R = BK / 4;
+    constexpr int RPP = 256 / F4R;
+    constexpr int AP = BM / RPP, BP = BN / RPP;
+    static_assert((BM / WM) * (BN / WN) == 4, "4 waves");
+    __shared__ __attribute__((aligned(16))) float smem[(BM + BN) * LDK];
+    float* As = smem;
+    float* Bs = smem + BM * LDK;
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+    const int ntn = p.N / BN;
+    const int tile_m = blockIdx.x / ntn, tile_n = blockIdx.x - (blockIdx.x / ntn) * ntn;
+    const int m0 = tile_m * BM, n0 = tile_n * BN;
+    const int H = p.H, W = p.W;
+
+    const int lrow = tid / F4R, lc4 = tid % F4R;
+    Pix rq[AP];
+#pragma unroll
+    for (int i = 0; i < AP; ++i) rq[i] = decode(m0 + lrow + i * RPP, H, W);
+
+    f32x4 ra[AP], rb[BP];
+    const bool affine = p.ascale != nullptr;
+
+    auto load_chunk = [&](int kc) {
+        const int k0 = kc * BK;
+        const int tap = k0 / p.C;
+        const int c = k0 - tap * p.C + lc4 * 4;
+        f32x4 sc = {1.f, 1.f, 1.f, 1.f}, sh = {0.f, 0.f, 0.f, 0.f};
+        if (affine) {
+            sc = *(const f32x4*)(p.ascale + c);
+            sh = *(const f32x4*)(p.ashift + c);
+        }
+#pragma unroll
+        for (int i = 0; i < AP; ++i) {
+            bool valid;
+            const int m = m0 + lrow + i * RPP;
+            const int src = gather_src(p.amode, tap, m, rq[i], H, W, valid);
+            f32x4 v = *(const f32x4*)(p.a + (size_t)src * p.lda + p.aoff + c);
+            if (affine) v = v * sc + sh;
+            ra[i] = valid ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int i = 0; i < BP; ++i)
+            rb[i] = *(const f32x4*)(p.bt + (size_t)(n0 + lrow + i * RPP) * p.K + k0 + lc4 * 4);
+    };
+    auto store_chunk = [&]() {
+#pragma unroll
+        for (int i = 0; i < AP; ++i) *(f32x4*)&As[(lrow + i * RPP) * LDK + lc4 * 4] = ra[i];
+#pragma unroll
+        for (int i = 0; i < BP; ++i) *(f32x4*)&Bs[(lrow + i * RPP) * LDK + lc4 * 4] = rb[i];
+    };
+
+    f32x16 acc[MT][NT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    const int li = lane & 31, lh = lane >> 5;
+    const int nk = p.K / BK;
+    load_chunk(0);
+    store_chunk();
+    __syncthreads();
+    for (int kc = 0; kc < nk; ++kc) {
+        if (kc + 1 < nk) load_chunk(kc + 1);
+#pragma unroll
+        for (int kk = 0; kk < BK / 8; ++kk) {
+            f32x4 af[MT], bf[NT];
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt)
+                af[mt] = *(const f32x4*)&As[(wm * WM + mt * 32 + li) * LDK + kk * 8 + lh * 4];
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt)
+                bf[nt] = *(const f32x4*)&Bs[(wn * WN + nt * 32 + li) * LDK + kk * 8 + lh * 4];
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+#pragma unroll
+                for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                    for (int nt = 0; nt < NT; ++nt)
+                        acc[mt][nt] = mfma32(af[mt][s], bf[nt][s], acc[mt][nt]);
+        }
+        __syncthreads();
+        if (kc + 1 < nk) {
+            store_chunk();
+            __syncthreads();
+        }
+    }
+
+    // ---------------- epilogue ----------------
+    if (p.emode == E_BIAS_RELU_STATS) {
+        float s1[NT], s2[NT];
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+            const int n = n0 + wn * WN + nt * 32 + li;
+            const float b = p.bias[n];
+            s1[nt] = 0.f;
+            s2[nt] = 0.f;
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int m = m0 + wm * WM + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                    float v = fmaxf(acc[mt][nt][r] + b, 0.f);
+                    p.out[(size_t)m * p.ldo + p.ooff + n] = v;
+                    s1[nt] += v;
+                    s2[nt] += v * v;
+                }
+            s1[nt] += __shfl_xor(s1[nt], 32);
+            s2[nt] += __shfl_xor(s2[nt], 32);
+        }
+        // combine the BM/WM waves that share these columns (smem is free after the loop)
+        float* red = smem;  // [BM/WM][2][BN]
+        if (lh == 0) {
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) {
+                red[(wm * 2 + 0) * BN + wn * WN + nt * 32 + li] = s1[nt];
+                red[(wm * 2 + 1) * BN + wn * WN + nt * 32 + li] = s2[nt];
+            }
+        }
+        __syncthreads();
+        if (tid < BN) {
+            float a = 0.f, q = 0.f;
+#pragma unroll
+            for (int w = 0; w < BM / WM; ++w) {
+                a += red[(w * 2 + 0) * BN + tid];
+                q += red[(w * 2 + 1) * BN + tid];
+            }
+            p.stats[(size_t)tile_m * 2 * p.N + n0 + tid] = a;
+            p.stats[(size_t)tile_m * 2 * p.N + p.N + n0 + tid] = q;
+        }
+    } else if (p.emode == E_CONVT) {
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+            const int n = n0 + wn * WN + nt * 32 + li;
+            const int ab = n / p.cout, co = n - ab * p.cout;
+            const int a = ab >> 1, b = ab & 1;
+            const float bb = p.bias[co];
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int m = m0 + wm * WM + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                    const Pix q = decode(m, H, W);
+                    const size_t op = (size_t)(q.img * 2 * H + 2 * q.y + a) * (2 * W) + 2 * q.x + b;
+                    p.out[op * p.ldo + p.ooff + co] = acc[mt][nt][r] + bb;
+                }
+        }
+    } else {
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+            const int n = n0 + wn * WN + nt * 32 + li;
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int m = m0 + wm * WM + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                    p.out[(size_t)m * p.ldo + p.ooff + n] = acc[mt][nt][r];
+                }
+        }
+    }
+}
+
+template <int BM, int BN, int BKP, int WM, int WN>
+__global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
+    constexpr int LDA = BM + 4, LDB = BN + 4;
+    constexpr int MT = WM / 32, NT = WN / 32;
+    constexpr int WAVES_N = BN / WN;
+    constexpr int AF = BM / 4, BF = BN / 4;        // float4 per pixel row
+    constexpr int ARPP = 256 / AF, BRPP = 256 / BF;  // rows per pass
+    constexpr int AP = BKP / ARPP, BP = BKP / BRPP;
+    static_assert((BM / WM) * (BN / WN) == 4, "4 waves");
+    __shared__ __attribute__((aligned(16))) float As[BKP * LDA];
+    __shared__ __attribute__((aligned(16))) float Bs[BKP * LDB];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+    const int tiles_n = p.Nw / BN, tiles_m = p.Mw / BM;
+    int idx = blockIdx.x;
+    const int tn = idx % tiles_n;
+    idx /= tiles_n;
+    const int tm = idx % tiles_m;
+    const int split = idx / tiles_m;
+    const int tapA = (tm * BM) / p.CA, ca0 = tm * BM - tapA * p.CA;
+    const int tapB = (tn * BN) / p.CB, cb0 = tn * BN - tapB * p.CB;
+    const int H = p.H, W = p.W;
+
+    const int ac4 = tid % AF, arow = tid / AF;
+    const int bc4 = tid % BF, brow = tid / BF;
+    const bool affine = p.ascale != nullptr;
+    f32x4 sc = {1.f, 1.f, 1.f, 1.f}, sh = {0.f, 0.f, 0.f, 0.f};
+    if (affine) {
+        sc = *(const f32x4*)(p.ascale + ca0 + ac4 * 4);
+        sh = *(const f32x4*)(p.ashift + ca0 + ac4 * 4);
+    }
+
+    const int pbeg = split * p.pps;
+    int pend = pbeg + p.pps;
+    if (pend > p.P) pend = p.P;
+    const int nchunks = (pend - pbeg) / BKP;
+
+    f32x4 ra[AP], rb[BP];
+    auto load_chunk = [&](int pc) {
+#pragma unroll
+        for (int i = 0; i < AP; ++i) {
+            const int m = pc + arow + i * ARPP;
+            bool valid;
+            const int src = gather_src(p.amode, tapA, m, decode(m, H, W), H, W, valid);
+            f32x4 v = *(const f32x4*)(p.a + (size_t)src * p.lda + p.aoff + ca0 + ac4 * 4);
+            if (affine) v = v * sc + sh;
+            ra[i] = valid ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int i = 0; i < BP; ++i) {
+            const int m = pc + brow + i * BRPP;
+            bool valid;
+            const int src = gather_src(p.bmode, tapB, m, decode(m, H, W), H, W, valid);
+            f32x4 v = *(const f32x4*)(p.b + (size_t)src * p.ldb + p.boff + cb0 + bc4 * 4);
+            rb[i] = valid ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+    };
+    auto store_chunk = [&]() {
+#pragma unroll
+        for (int i = 0; i < AP; ++i) *(f32x4*)&As[(arow + i * ARPP) * LDA + ac4 * 4] = ra[i];
+#pragma unroll
+        for (int i = 0; i < BP; ++i) *(f32x4*)&Bs[(brow + i * BRPP) * LDB + bc4 * 4] = rb[i];
+    };
+
+    f32x16 acc[MT][NT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    const int li = lane & 31, lh = lane >> 5;
+    if (nchunks > 0) {
+        load_chunk(pbeg);
+        store_chunk();
+        __syncthreads();
+    }
+    for (int c = 0; c < nchunks; ++c) {
+        if (c + 1 < nchunks) load_chunk(pbeg + (c + 1) * BKP);
+#pragma unroll
+        for (int kk = 0; kk < BKP / 8; ++kk)
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const int pr = kk * 8 + lh * 4 + s;
+                float af[MT], bf[NT];
+#pragma unroll
+                for (int mt = 0; mt < MT; ++mt) af[mt] = As[pr * LDA + wm * WM + mt * 32 + li];
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt) bf[nt] = Bs[pr * LDB + wn * WN + nt * 32 + li];
+#pragma unroll
+                for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                    for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma32(af[mt], bf[nt], acc[mt][nt]);
+            }
+        __syncthreads();
+        if (c + 1 < nchunks) {
+            store_chunk();
+            __syncthreads();
+        }
+    }
+
+    float* slab = p.slab + (size_t)split * p.Mw * p.Nw;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = tm * BM + wm * WM + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                const int n = tn * BN + wn * WN + nt * 32 + li;
+                slab[(size_t)m * p.Nw + n] = acc[mt][nt][r];
+            }
+}
+
+}  // namespace
+
+int launch_rowgemm(const RowGemmArgs& a, int bm, int bn, hipStream_t s) {
+    constexpr int BK = 32;
+    if (a.M % bm || a.N % bn || a.K % BK || a.C % BK || a.K != gather_taps(a.amode) * a.C)
+        return -1;
+    if (a.emode == E_CONVT && (a.cout % bn)) return -1;
+    dim3 grid((a.M / bm) * (a.N / bn)), block(256);
+    if (bm == 128 && bn == 128)
+        hipLaunchKernelGGL((rowgemm_kernel<128, 128, BK, 64, 64>), grid, block, 0, s, a);
+    else if (bm == 128 && bn == 64)
+        hipLaunchKernelGGL((rowgemm_kernel<128, 64, BK, 64, 32>), grid, block, 0, s, a);
+    else
+        return -1;
+    return (int)hipGetLastError();
+}
+
+int launch_wgrad(const WgradArgs& a, int bm, int bn, hipStream_t s) {
+    constexpr int BKP = 32;
+    if (a.Mw % bm || a.Nw % bn || a.CA % bm || a.CB % bn || a.P % BKP || a.pps % BKP) return -1;
+    dim3 grid((a.Mw / bm) * (a.Nw / bn) * a.splits), block(256);
+    if (bm == 128 && bn == 128)
+        hipLaunchKernelGGL((wgrad_kernel<128, 128, BKP, 64, 64>), grid, block, 0, s, a);
+    else if (bm == 64 && bn == 64)
+        hipLaunchKernelGGL((wgrad_kernel<64, 64, BKP, 32, 32>), grid, block, 0, s, a);
+    else if (bm == 128 && bn == 64)
+        hipLaunchKernelGGL((wgrad_kernel<128, 64, BKP, 64, 32>), grid, block, 0, s, a);
+    else if (bm == 64 && bn == 128)
+        hipLaunchKernelGGL((wgrad_kernel<64, 128, BKP, 32, 64>), grid, block, 0, s, a);
+    else
+        return -1;
+    return (int)hipGetLastError();
+}

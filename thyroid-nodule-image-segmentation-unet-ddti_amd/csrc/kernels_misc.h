@@ -1,0 +1,47 @@
+// Host launchers of kernels_misc.hip (internal).
+#pragma once
+#include "common.h"
+
+int k_pack_conv3(const float* w, float* wf, float* wd, int cin, int cout, hipStream_t s);
+int k_pack_convT(const float* w, float* tf, float* td, int cin, int cout, hipStream_t s);
+int k_conv_first_fwd(const float* x, const float* w, const float* b, float* y, int P, int H, int W,
+                     int C, float* partial, int G, hipStream_t s);
+int k_conv_first_wgrad(const float* x, const float* dz, int P, int H, int W, int C, float* partial,
+                       int G, float* gw, float* gb, hipStream_t s);
+int k_reduce_rows(const float* in, int R, int ncols, float* out, int G, hipStream_t s);
+int k_bn_finalize_train(const float* part, int G, int C, double count, const float* gamma,
+                        const float* beta, float* rmean, float* rvar, int64_t* nbt, float momentum,
+                        float eps, float* scale, float* shift, float* mean, float* invstd,
+                        hipStream_t s);
+int k_bn_finalize_eval(int C, const float* gamma, const float* beta, const float* rmean,
+                       const float* rvar, float eps, float* scale, float* shift, hipStream_t s);
+int k_maxpool_bn(const float* y, int ld, int off, const float* scale, const float* shift, int N,
+                 int H, int W, int C, float* out, uint8_t* idx, hipStream_t s);
+int k_maxpool_bwd(const float* dp, const uint8_t* idx, const float* dskip, int ldskip, int offskip,
+                  int N, int H, int W, int C, float* dout, hipStream_t s);
+int k_bn_bwd_reduce(const float* dout, const float* y, int ld, int off, int P, int C,
+                    float* partial, int G, hipStream_t s);
+int k_bn_bwd_finalize(const float* part, int G, int C, double count, const float* gamma,
+                      const float* mean, const float* invstd, float* coef, float* dgamma,
+                      float* dbeta, hipStream_t s);
+int k_bn_bwd_apply(float* dz, const float* y, int ld, int off, int P, int C, const float* coef,
+                   float* partial, int G, hipStream_t s);
+int k_chan_sum(const float* v, int ld, int off, int P, int C, float* partial, int G, hipStream_t s);
+int k_sum_partials(const float* part, int G, int ncols, float* out, hipStream_t s);
+int k_slab_reduce(const float* slab, int S, int Mw, int Nw, int kind, int cin, int cout,
+                  float* grad, hipStream_t s);
+int k_head_fwd(const float* y, int C, const float* scale, const float* shift, const float* w,
+               const float* b, int O, int P, int HW, float* logits, hipStream_t s);
+int k_head_bwd(const float* y, int C, const float* scale, const float* shift, const float* w,
+               int O, int P, int HW, const float* dlog, float* dout, float* partial, int G,
+               hipStream_t s);
+int k_loss_fwd(const float* x, const float* t, int N, int64_t per, float* stats, float* losses,
+               float alpha, float beta, float gamma, hipStream_t s);
+int k_loss_bwd(const float* x, const float* t, int N, int64_t per, const float* stats,
+               const float* w, float alpha, float beta, float gamma, float* dx, hipStream_t s);
+int k_adamw(float* p, const float* g, float* m, float* v, int64_t n, float lr, float b1, float b2,
+            float eps, float wd, float step_size, float bc2_sqrt, float gscale, hipStream_t s);
+int k_mask_counts(const float* x, const float* t, int64_t n, uint8_t* mask, int64_t* counts,
+                  hipStream_t s);
+int k_nchw_to_nhwc(const float* x, int N, int C, int HW, float* y, hipStream_t s);
+int k_fill(float* p, int64_t n, float v, hipStream_t s);

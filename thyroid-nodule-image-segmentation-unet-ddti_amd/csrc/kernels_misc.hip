@@ -1,0 +1,821 @@
+// Bandwidth-bound kernels around the MFMA convolutions: weight repacking, the Cin=1 first
+// conv, BatchNorm statistics / finalisation / backward, 2x2 max-pool, the 1x1 head, the
+// BCE + Dice + FocalTversky loss, AdamW and the eval mask readout.
+//
+// All reductions are deterministic: fixed per-block partial sums followed by fixed-order
+// reductions (no float atomics), so two runs of the same inputs are bit-identical.
+// Layout everywhere: NHWC, channel stride `ld`, channel offset `off` (concat slices).
+#include "kernels_misc.h"
+
+namespace {
+
+// -------------------------------------------------------------------------------------
+// Weight packing.  torch Conv2d weight W[co][ci][ky][kx] (models/model.py:36,39):
+//   fwd  : Wf[co][tap][ci]                    (Bt of the forward row-GEMM, k = tap*Cin+ci)
+//   dgrad: Wd[ci][tap'][co] = W[co][ci][8-tap'] (flipped taps, k = tap'*Cout+co)
+// torch ConvTranspose2d weight W[ci][co][a][b] (models/model.py:19,49):
+//   fwd  : Tf[(ab*Cout+co)][ci]
+//   dgrad: Td[ci][ab*Cout+co]
+// -------------------------------------------------------------------------------------
+__global__ void pack_conv3_kernel(const float* __restrict__ w, float* __restrict__ wf,
+                                  float* __restrict__ wd, int cin, int cout) {
+    const int64_t n = (int64_t)cin * cout * 9;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int tap = (int)(i % 9);
+        const int64_t t = i / 9;
+        const int ci = (int)(t % cin), co = (int)(t / cin);
+        const float v = w[i];
+        wf[((int64_t)co * 9 + tap) * cin + ci] = v;
+        if (wd) wd[((int64_t)ci * 9 + (8 - tap)) * cout + co] = v;
+    }
+}
+
+__global__ void pack_convT_kernel(const float* __restrict__ w, float* __restrict__ tf,
+                                  float* __restrict__ td, int cin, int cout) {
+    const int64_t n = (int64_t)cin * cout * 4;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int ab = (int)(i & 3);
+        const int64_t t = i >> 2;
+        const int co = (int)(t % cout), ci = (int)(t / cout);
+        const float v = w[i];
+        tf[((int64_t)ab * cout + co) * cin + ci] = v;
+        if (td) td[(int64_t)ci * 4 * cout + ab * cout + co] = v;
+    }
+}
+
+// Block-level combine of per-thread channel partials.  Threads are laid out as
+// (row group g = tid / tpr, channel quad q = tid % tpr); acc[NV] holds NV quantities per
+// channel-quad.  Writes out[v*C + 4q + j] for row group 0.  smem: 256*NV*4 floats.
+template <int NV>
+__device__ void block_combine(const f32x4 (&acc)[NV], int tpr, int C, float* out, float* smem) {
+    const int tid = threadIdx.x;
+    const int g = tid / tpr, q = tid % tpr;
+    const int groups = blockDim.x / tpr;
+    f32x4* s = (f32x4*)smem;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) s[v * blockDim.x + tid] = acc[v];
+    __syncthreads();
+    if (g == 0) {
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            f32x4 a = s[v * blockDim.x + q];
+            for (int k = 1; k < groups; ++k) a += s[v * blockDim.x + k * tpr + q];
+            *(f32x4*)(out + v * C + 4 * q) = a;
+        }
+    }
+}
+
+// -------------------------------------------------------------------------------------
+// Conv2d(1 -> C, 3x3, pad 1) + bias + ReLU + BN partials (encoder1.0, model.py:10,36-37).
+// K = 9 is too small for MFMA; one thread computes 4 channels of one pixel.
+// -------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void conv_first_fwd_kernel(const float* __restrict__ x,
+                                                            const float* __restrict__ w,
+                                                            const float* __restrict__ bias,
+                                                            float* __restrict__ y, int P, int H,
+                                                            int W, int C, float* partial) {
+    __shared__ __attribute__((aligned(16))) float smem[256 * 2 * 4];
+    const int tpr = C / 4, rpp = 256 / tpr;
+    const int q = threadIdx.x % tpr, g = threadIdx.x / tpr;
+    float wr[4][9];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int t = 0; t < 9; ++t) wr[j][t] = w[(4 * q + j) * 9 + t];
+    const f32x4 b = *(const f32x4*)(bias + 4 * q);
+    f32x4 acc[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+    const int per = (P + gridDim.x - 1) / gridDim.x;
+    const int r0 = blockIdx.x * per;
+    const int r1 = min(P, r0 + per);
+    for (int m = r0 + g; m < r1; m += rpp) {
+        const int xx = m % W, t = m / W, yy = t % H, img = t / H;
+        float xv[9];
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap) {
+            const int sy = yy + tap / 3 - 1, sx = xx + tap % 3 - 1;
+            const bool ok = sy >= 0 && sy < H && sx >= 0 && sx < W;
+            xv[tap] = ok ? x[((int64_t)img * H + sy) * W + sx] : 0.f;
+        }
+        f32x4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            float s = 0.f;
+#pragma unroll
+            for (int tap = 0; tap < 9; ++tap) s = fmaf(xv[tap], wr[j][tap], s);
+            o[j] = fmaxf(s + b[j], 0.f);
+        }
+        *(f32x4*)(y + (int64_t)m * C + 4 * q) = o;
+        acc[0] += o;
+        acc[1] += o * o;
+    }
+    block_combine<2>(acc, tpr, C, partial + (int64_t)blockIdx.x * 2 * C, smem);
+}
+
+// dW[co][tap] = sum_p x_tap(p) dz[p][co], db[co] = sum_p dz[p][co]; partial [G][10*C]
+// laid out as [tap][C] for tap 0..8 then bias.
+__global__ __launch_bounds__(256) void conv_first_wgrad_kernel(const float* __restrict__ x,
+                                                              const float* __restrict__ dz,
+                                                              int P, int H, int W, int C,
+                                                              float* partial) {
+    __shared__ __attribute__((aligned(16))) float smem[256 * 10 * 4];
+    const int tpr = C / 4, rpp = 256 / tpr;
+    const int q = threadIdx.x % tpr, g = threadIdx.x / tpr;
+    f32x4 acc[10];
+#pragma unroll
+    for (int v = 0; v < 10; ++v) acc[v] = f32x4{0, 0, 0, 0};
+    const int per = (P + gridDim.x - 1) / gridDim.x;
+    const int r0 = blockIdx.x * per;
+    const int r1 = min(P, r0 + per);
+    for (int m = r0 + g; m < r1; m += rpp) {
+        const int xx = m % W, t = m / W, yy = t % H, img = t / H;
+        const f32x4 d = *(const f32x4*)(dz + (int64_t)m * C + 4 * q);
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap) {
+            const int sy = yy + tap / 3 - 1, sx = xx + tap % 3 - 1;
+            const bool ok = sy >= 0 && sy < H && sx >= 0 && sx < W;
+            const float xv = ok ? x[((int64_t)img * H + sy) * W + sx] : 0.f;
+            acc[tap] += xv * d;
+        }
+        acc[9] += d;
+    }
+    block_combine<10>(acc, tpr, C, partial + (int64_t)blockIdx.x * 10 * C, smem);
+}
+
+// -------------------------------------------------------------------------------------
+// Deterministic reductions of partial rows.
+// -------------------------------------------------------------------------------------
+// out[g][c] = sum_{r in slice g} in[r][c], c < ncols.  grid (ceil(ncols/256), G).
+__global__ void reduce_rows_kernel(const float* __restrict__ in, int R, int ncols,
+                                   float* __restrict__ out) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= ncols) return;
+    const int G = gridDim.y, g = blockIdx.y;
+    const int per = (R + G - 1) / G;
+    const int r0 = g * per, r1 = min(R, r0 + per);
+    float s = 0.f;
+    for (int r = r0; r < r1; ++r) s += in[(int64_t)r * ncols + c];
+    out[(int64_t)g * ncols + c] = s;
+}
+
+// BatchNorm2d train finalisation (torch/nn/modules/batchnorm.py semantics): batch mean,
+// biased var for normalisation, running stats r = (1-m) r + m * stat with unbiased var.
+// Emits the fused affine (scale, shift) consumers apply in their load path, and keeps
+// mean / invstd for the backward.
+__global__ void bn_finalize_train_kernel(const float* __restrict__ part, int G, int C,
+                                         double count, const float* __restrict__ gamma,
+                                         const float* __restrict__ beta, float* rmean,
+                                         float* rvar, int64_t* nbt, float momentum, float eps,
+                                         float* __restrict__ scale, float* __restrict__ shift,
+                                         float* __restrict__ mean_out,
+                                         float* __restrict__ invstd_out) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c == 0 && nbt) *nbt += 1;
+    if (c >= C) return;
+    double s = 0.0, q = 0.0;
+    for (int g = 0; g < G; ++g) {
+        s += part[(int64_t)g * 2 * C + c];
+        q += part[(int64_t)g * 2 * C + C + c];
+    }
+    const double mean = s / count;
+    double var = q / count - mean * mean;
+    if (var < 0) var = 0;
+    const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+    const float sc = gamma[c] * invstd;
+    scale[c] = sc;
+    shift[c] = beta[c] - (float)mean * sc;
+    mean_out[c] = (float)mean;
+    invstd_out[c] = invstd;
+    if (rmean) {
+        const double unb = count > 1 ? var * count / (count - 1) : var;
+        rmean[c] = (1.f - momentum) * rmean[c] + momentum * (float)mean;
+        rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)unb;
+    }
+}
+
+__global__ void bn_finalize_eval_kernel(int C, const float* __restrict__ gamma,
+                                        const float* __restrict__ beta,
+                                        const float* __restrict__ rmean,
+                                        const float* __restrict__ rvar, float eps,
+                                        float* __restrict__ scale, float* __restrict__ shift) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    const float invstd = 1.f / sqrtf(rvar[c] + eps);
+    const float sc = gamma[c] * invstd;
+    scale[c] = sc;
+    shift[c] = beta[c] - rmean[c] * sc;
+}
+
+// -------------------------------------------------------------------------------------
+// MaxPool2d(2) of BN(y) (model.py:17,56-58).  BN is applied before the max (the two do not
+// commute when gamma < 0).  idx keeps the winning window position with torch's tie rule:
+// scan order (0,0),(0,1),(1,0),(1,1), first strict maximum wins.
+// -------------------------------------------------------------------------------------
+__global__ void maxpool_bn_kernel(const float* __restrict__ y, int ld, int off,
+                                  const float* __restrict__ scale,
+                                  const float* __restrict__ shift, int N, int H, int W, int C,
+                                  float* __restrict__ out, uint8_t* __restrict__ idx) {
+    const int Ho = H / 2, Wo = W / 2, c4n = C / 4;
+    const int64_t total = (int64_t)N * Ho * Wo * c4n;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int c4 = (int)(i % c4n);
+        const int64_t po = i / c4n;
+        const int xo = (int)(po % Wo);
+        const int64_t t = po / Wo;
+        const int yo = (int)(t % Ho), img = (int)(t / Ho);
+        const f32x4 sc = *(const f32x4*)(scale + 4 * c4), sh = *(const f32x4*)(shift + 4 * c4);
+        f32x4 best;
+        uint32_t bi = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int64_t pin = ((int64_t)img * H + 2 * yo + (k >> 1)) * W + 2 * xo + (k & 1);
+            const f32x4 v = *(const f32x4*)(y + pin * ld + off + 4 * c4) * sc + sh;
+            if (k == 0) {
+                best = v;
+            } else {
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    if (v[j] > best[j] || v[j] != v[j]) {
+                        best[j] = v[j];
+                        bi = (bi & ~(0xFFu << (8 * j))) | ((uint32_t)k << (8 * j));
+                    }
+            }
+        }
+        *(f32x4*)(out + po * C + 4 * c4) = best;
+        *(uint32_t*)(idx + po * C + 4 * c4) = bi;
+    }
+}
+
+// do[p][c] = (idx routes dpool to p) + dskip[p][c]  (skip grad comes from the decoder's
+// concat slice, model.py:64-70, so the encoder output's two consumers are summed here).
+__global__ void maxpool_bwd_kernel(const float* __restrict__ dp, const uint8_t* __restrict__ idx,
+                                   const float* __restrict__ dskip, int ldskip, int offskip,
+                                   int N, int H, int W, int C, float* __restrict__ dout) {
+    const int Ho = H / 2, Wo = W / 2, c4n = C / 4;
+    const int64_t total = (int64_t)N * Ho * Wo * c4n;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int c4 = (int)(i % c4n);
+        const int64_t po = i / c4n;
+        const int xo = (int)(po % Wo);
+        const int64_t t = po / Wo;
+        const int yo = (int)(t % Ho), img = (int)(t / Ho);
+        const f32x4 g = *(const f32x4*)(dp + po * C + 4 * c4);
+        const uint32_t bi = *(const uint32_t*)(idx + po * C + 4 * c4);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int64_t pin = ((int64_t)img * H + 2 * yo + (k >> 1)) * W + 2 * xo + (k & 1);
+            f32x4 v = {0, 0, 0, 0};
+            if (dskip) v = *(const f32x4*)(dskip + pin * ldskip + offskip + 4 * c4);
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (((bi >> (8 * j)) & 0xFF) == (uint32_t)k) v[j] += g[j];
+            *(f32x4*)(dout + pin * C + 4 * c4) = v;
+        }
+    }
+}
+
+// -------------------------------------------------------------------------------------
+// BatchNorm backward (train mode) through the preceding ReLU (model.py:37-38,40-41):
+//   sums:  S1 = sum do, S2 = sum do*y                      (bn_bwd_reduce)
+//   coefs: dz = [y>0] (A do + B y + Cc)                     (bn_bwd_finalize)
+//          dgamma = invstd (S2 - mean S1), dbeta = S1
+//   apply: dz in place of do, plus per-channel sum dz for the conv bias (bn_bwd_apply)
+// -------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restrict__ dout,
+                                                           const float* __restrict__ y, int ld,
+                                                           int off, int P, int C,
+                                                           float* partial) {
+    __shared__ __attribute__((aligned(16))) float smem[256 * 2 * 4];
+    const int tpr = C / 4 < 256 ? C / 4 : 256, rpp = 256 / tpr;
+    f32x4 acc[2];
+    for (int c0 = 0; c0 < C; c0 += 4 * tpr) {
+        const int q = threadIdx.x % tpr, g = threadIdx.x / tpr;
+        acc[0] = acc[1] = f32x4{0, 0, 0, 0};
+        const int per = (P + gridDim.x - 1) / gridDim.x;
+        const int r0 = blockIdx.x * per, r1 = min(P, r0 + per);
+        for (int m = r0 + g; m < r1; m += rpp) {
+            const f32x4 d = *(const f32x4*)(dout + (int64_t)m * C + c0 + 4 * q);
+            const f32x4 v = *(const f32x4*)(y + (int64_t)m * ld + off + c0 + 4 * q);
+            acc[0] += d;
+            acc[1] += d * v;
+        }
+        block_combine<2>(acc, tpr, C, partial + (int64_t)blockIdx.x * 2 * C + c0, smem);
+        __syncthreads();
+    }
+}
+
+__global__ void bn_bwd_finalize_kernel(const float* __restrict__ part, int G, int C, double count,
+                                       const float* __restrict__ gamma,
+                                       const float* __restrict__ mean,
+                                       const float* __restrict__ invstd, float* __restrict__ coef,
+                                       float* __restrict__ dgamma, float* __restrict__ dbeta) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    double s1 = 0.0, s2 = 0.0;
+    for (int g = 0; g < G; ++g) {
+        s1 += part[(int64_t)g * 2 * C + c];
+        s2 += part[(int64_t)g * 2 * C + C + c];
+    }
+    const double is = invstd[c], mu = mean[c];
+    const double sdxh = is * (s2 - mu * s1);  // sum do * xhat
+    const double k = (double)gamma[c] * is;
+    coef[c] = (float)k;                                         // A
+    coef[C + c] = (float)(-k * is * sdxh / count);              // B
+    coef[2 * C + c] = (float)(-k * s1 / count + k * is * mu * sdxh / count);  // Cc
+    dgamma[c] = (float)sdxh;
+    dbeta[c] = (float)s1;
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(float* __restrict__ dz,
+                                                          const float* __restrict__ y, int ld,
+                                                          int off, int P, int C,
+                                                          const float* __restrict__ coef,
+                                                          float* partial) {
+    __shared__ __attribute__((aligned(16))) float smem[256 * 1 * 4];
+    const int tpr = C / 4 < 256 ? C / 4 : 256, rpp = 256 / tpr;
+    f32x4 acc[1];
+    for (int c0 = 0; c0 < C; c0 += 4 * tpr) {
+        const int q = threadIdx.x % tpr, g = threadIdx.x / tpr;
+        const int c = c0 + 4 * q;
+        const f32x4 A = *(const f32x4*)(coef + c), B = *(const f32x4*)(coef + C + c),
+                    Cc = *(const f32x4*)(coef + 2 * C + c);
+        acc[0] = f32x4{0, 0, 0, 0};
+        const int per = (P + gridDim.x - 1) / gridDim.x;
+        const int r0 = blockIdx.x * per, r1 = min(P, r0 + per);
+        for (int m = r0 + g; m < r1; m += rpp) {
+            f32x4* pd = (f32x4*)(dz + (int64_t)m * C + c);
+            const f32x4 v = *(const f32x4*)(y + (int64_t)m * ld + off + c);
+            f32x4 d = A * (*pd) + B * v + Cc;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) d[j] = v[j] > 0.f ? d[j] : 0.f;
+            *pd = d;
+            acc[0] += d;
+        }
+        block_combine<1>(acc, tpr, C, partial + (int64_t)blockIdx.x * C + c0, smem);
+        __syncthreads();
+    }
+}
+
+// per-channel sum over pixels of a strided NHWC slice (ConvTranspose2d bias grad)
+__global__ __launch_bounds__(256) void chan_sum_kernel(const float* __restrict__ v, int ld, int off,
+                                                      int P, int C, float* partial) {
+    __shared__ __attribute__((aligned(16))) float smem[256 * 1 * 4];
+    const int tpr = C / 4 < 256 ? C / 4 : 256, rpp = 256 / tpr;
+    f32x4 acc[1];
+    for (int c0 = 0; c0 < C; c0 += 4 * tpr) {
+        const int q = threadIdx.x % tpr, g = threadIdx.x / tpr;
+        acc[0] = f32x4{0, 0, 0, 0};
+        const int per = (P + gridDim.x - 1) / gridDim.x;
+        const int r0 = blockIdx.x * per, r1 = min(P, r0 + per);
+        for (int m = r0 + g; m < r1; m += rpp)
+            acc[0] += *(const f32x4*)(v + (int64_t)m * ld + off + c0 + 4 * q);
+        block_combine<1>(acc, tpr, C, partial + (int64_t)blockIdx.x * C + c0, smem);
+        __syncthreads();
+    }
+}
+
+// out[c] = sum over G partial rows (fixed order), optional scatter stride
+__global__ void sum_partials_kernel(const float* __restrict__ part, int G, int ncols,
+                                    float* __restrict__ out) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= ncols) return;
+    float s = 0.f;
+    for (int g = 0; g < G; ++g) s += part[(int64_t)g * ncols + c];
+    out[c] = s;
+}
+
+// Sum the split-K slabs of a wgrad and scatter into the torch weight layout.
+//   conv3 : slab [S][tap*Cin+ci][co] -> grad[co][ci][tap]
+//   convT : slab [S][ci][ab*Cout+co] -> grad[ci][co][ab]
+__global__ void slab_reduce_kernel(const float* __restrict__ slab, int S, int Mw, int Nw,
+                                   int kind, int cin, int cout, float* __restrict__ grad) {
+    const int64_t total = (int64_t)Mw * Nw;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        float s = 0.f;
+        for (int k = 0; k < S; ++k) s += slab[(int64_t)k * total + i];
+        const int n = (int)(i % Nw), m = (int)(i / Nw);
+        int64_t o;
+        if (kind == 0) {
+            const int tap = m / cin, ci = m - tap * cin;
+            o = ((int64_t)n * cin + ci) * 9 + tap;
+        } else {
+            const int ab = n / cout, co = n - ab * cout;
+            o = ((int64_t)m * cout + co) * 4 + ab;
+        }
+        grad[o] = s;
+    }
+}
+
+// conv-first wgrad partials [G][10][C] -> grad w[co][0][tap], b[co]
+__global__ void conv_first_wgrad_finalize_kernel(const float* __restrict__ part, int G, int C,
+                                                 float* __restrict__ gw, float* __restrict__ gb) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= 10 * C) return;
+    float s = 0.f;
+    for (int g = 0; g < G; ++g) s += part[(int64_t)g * 10 * C + i];
+    const int tap = i / C, c = i - tap * C;
+    if (tap < 9)
+        gw[c * 9 + tap] = s;
+    else
+        gb[c] = s;
+}
+
+// -------------------------------------------------------------------------------------
+// 1x1 head Conv2d(C -> O) (model.py:30) on BN(y), fused BN affine.  16 lanes per pixel.
+// logits are NCHW (N, O, H, W).
+// -------------------------------------------------------------------------------------
+__global__ void head_fwd_kernel(const float* __restrict__ y, int C, const float* __restrict__ scale,
+                                const float* __restrict__ shift, const float* __restrict__ w,
+                                const float* __restrict__ b, int O, int P, int HW,
+                                float* __restrict__ logits) {
+    const int lpp = C / 4;  // lanes per pixel (C == 64 -> 16)
+    const int64_t gt = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    const int64_t pix = gt / lpp;
+    const int q = (int)(gt % lpp);
+    const bool ok = pix < P;
+    f32x4 v = {0, 0, 0, 0};
+    if (ok) v = *(const f32x4*)(y + pix * C + 4 * q) * *(const f32x4*)(scale + 4 * q) +
+                *(const f32x4*)(shift + 4 * q);
+    for (int o = 0; o < O; ++o) {
+        const f32x4 wv = *(const f32x4*)(w + o * C + 4 * q);
+        float s = v[0] * wv[0] + v[1] * wv[1] + v[2] * wv[2] + v[3] * wv[3];
+        for (int d = lpp / 2; d >= 1; d >>= 1) s += __shfl_xor(s, d);
+        if (ok && q == 0) {
+            const int64_t img = pix / HW, hw = pix % HW;
+            logits[(img * O + o) * HW + hw] = s + b[o];
+        }
+    }
+}
+
+// do[p][c] = sum_o dl[p][o] w[o][c];  partial dW[o][c] = sum dl * BN(y)_c, db[o] = sum dl.
+// partial layout [G][O*C + O].
+__global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__ y, int C,
+                                                      const float* __restrict__ scale,
+                                                      const float* __restrict__ shift,
+                                                      const float* __restrict__ w, int O, int P,
+                                                      int HW, const float* __restrict__ dlog,
+                                                      float* __restrict__ dout, float* partial) {
+    __shared__ float red[256 * 5];
+    const int lpp = C / 4, rpp = 256 / lpp;
+    const int q = threadIdx.x % lpp, g = threadIdx.x / lpp;
+    const f32x4 sc = *(const f32x4*)(scale + 4 * q), sh = *(const f32x4*)(shift + 4 * q);
+    // O <= 4 supported for the fused partials
+    f32x4 aw[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
+    float ab[4] = {0, 0, 0, 0};
+    const int per = (P + gridDim.x - 1) / gridDim.x;
+    const int r0 = blockIdx.x * per, r1 = min(P, r0 + per);
+    for (int m = r0 + g; m < r1; m += rpp) {
+        const f32x4 v = *(const f32x4*)(y + (int64_t)m * C + 4 * q) * sc + sh;
+        const int64_t img = m / HW, hw = m % HW;
+        f32x4 d = {0, 0, 0, 0};
+        for (int o = 0; o < O; ++o) {
+            const float dl = dlog[(img * O + o) * HW + hw];
+            d += dl * *(const f32x4*)(w + o * C + 4 * q);
+            aw[o] += dl * v;
+            ab[o] += dl;
+        }
+        *(f32x4*)(dout + (int64_t)m * C + 4 * q) = d;
+    }
+    // combine over row groups through LDS, one quantity at a time
+    float* out = partial + (int64_t)blockIdx.x * (O * C + O);
+    for (int o = 0; o < O; ++o) {
+        for (int j = 0; j < 4; ++j) {
+            red[threadIdx.x] = aw[o][j];
+            __syncthreads();
+            if (g == 0) {
+                float s = 0.f;
+                for (int k = 0; k < rpp; ++k) s += red[k * lpp + q];
+                out[o * C + 4 * q + j] = s;
+            }
+            __syncthreads();
+        }
+        red[threadIdx.x] = ab[o];
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            float s = 0.f;
+            for (int k = 0; k < rpp; ++k) s += red[k * lpp];  // q == 0 lanes carry the sum
+            out[O * C + o] = s;
+        }
+        __syncthreads();
+    }
+}
+
+// -------------------------------------------------------------------------------------
+// Losses (utils/trainer.py:85-88; models/loss.py:13-46).  One block per sample:
+//   stats[n] = {I = sum p t, Sp = sum p, St = sum t, Sbce = sum bce_elem}
+// bce_elem = (1 - t) x - log_sigmoid(x), log_sigmoid(x) = min(x,0) - log1p(exp(-|x|))
+// (ATen binary_cross_entropy_with_logits), p = 1 / (1 + exp(-x)).
+// -------------------------------------------------------------------------------------
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + expf(-x)); }
+
+__global__ __launch_bounds__(1024) void loss_stats_kernel(const float* __restrict__ x,
+                                                         const float* __restrict__ t, int64_t per,
+                                                         float* __restrict__ stats) {
+    __shared__ float red[4][32];
+    const int n = blockIdx.x;
+    const float* xs = x + n * per;
+    const float* ts = t + n * per;
+    float a[4] = {0, 0, 0, 0};
+    for (int64_t i = threadIdx.x; i < per; i += blockDim.x) {
+        const float xv = xs[i], tv = ts[i];
+        const float pv = sigmoidf_(xv);
+        a[0] += pv * tv;
+        a[1] += pv;
+        a[2] += tv;
+        a[3] += (1.f - tv) * xv - (fminf(xv, 0.f) - log1pf(expf(-fabsf(xv))));
+    }
+    for (int k = 0; k < 4; ++k)
+        for (int d = 32; d >= 1; d >>= 1) a[k] += __shfl_xor(a[k], d);
+    const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+    if (ln == 0)
+        for (int k = 0; k < 4; ++k) red[k][wv] = a[k];
+    __syncthreads();
+    if (threadIdx.x < 4) {
+        float s = 0.f;
+        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) s += red[threadIdx.x][w];
+        stats[4 * n + threadIdx.x] = s;
+    }
+}
+
+// stats[4N + 0..] = {TP, Sp, St} globals; losses = {bce_mean, dice_loss, focal}
+__global__ void loss_finalize_kernel(float* __restrict__ stats, int N, double total, float alpha,
+                                     float beta, float gamma, float* __restrict__ losses) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    double bce = 0, dice = 0, tp = 0, sp = 0, st = 0;
+    for (int n = 0; n < N; ++n) {
+        const double I = stats[4 * n], P = stats[4 * n + 1], T = stats[4 * n + 2];
+        bce += stats[4 * n + 3];
+        dice += (2.0 * I + 1.0) / (P + T + 1.0);
+        tp += I;
+        sp += P;
+        st += T;
+    }
+    const double fp = sp - tp, fn = st - tp, sm = 1e-6;
+    const double ti = (tp + sm) / (tp + alpha * fp + beta * fn + sm);
+    stats[4 * N + 0] = (float)tp;
+    stats[4 * N + 1] = (float)sp;
+    stats[4 * N + 2] = (float)st;
+    losses[0] = (float)(bce / total);
+    losses[1] = (float)(1.0 - dice / N);
+    losses[2] = (float)pow(1.0 - ti, (double)gamma);
+}
+
+__global__ void loss_bwd_kernel(const float* __restrict__ x, const float* __restrict__ t,
+                                int64_t per, int N, const float* __restrict__ stats,
+                                const float* __restrict__ w, float alpha, float beta,
+                                float gamma, float* __restrict__ dx) {
+    const int64_t total = per * N;
+    const float wb = w[0], wd = w[1], wf = w[2];
+    const float inv_total = (float)(1.0 / (double)total);
+    // focal-tversky scalars
+    const float tp = stats[4 * N], sp = stats[4 * N + 1], st = stats[4 * N + 2];
+    const float fp = sp - tp, fn = st - tp, sm = 1e-6f;
+    const float A = tp + sm, Bd = tp + alpha * fp + beta * fn + sm;
+    const float ti = A / Bd;
+    const float dLdti = (wf != 0.f) ? -gamma * powf(fmaxf(1.f - ti, 0.f), gamma - 1.f) : 0.f;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int n = (int)(i / per);
+        const float xv = x[i], tv = t[i];
+        const float pv = sigmoidf_(xv);
+        float g = wb * (pv - tv) * inv_total;  // d bce_mean / dx
+        const float I = stats[4 * n], U = stats[4 * n + 1] + stats[4 * n + 2];
+        const float dd = (2.f * tv * (U + 1.f) - (2.f * I + 1.f)) / ((U + 1.f) * (U + 1.f));
+        float gp = -wd * dd / (float)N;  // d dice_loss / dp
+        if (wf != 0.f) {
+            const float dti = (tv * Bd - A * (tv + alpha * (1.f - tv) - beta * tv)) / (Bd * Bd);
+            gp += wf * dLdti * dti;
+        }
+        g += gp * pv * (1.f - pv);
+        dx[i] = g;
+    }
+}
+
+// -------------------------------------------------------------------------------------
+// AdamW (utils/trainer.py:41,92; torch optim/adam.py _single_tensor_adam, decoupled wd).
+// Same op order as the CPU reference; __f*_rn keeps the compiler from contracting.
+// -------------------------------------------------------------------------------------
+__global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
+                             float* __restrict__ m, float* __restrict__ v, int64_t n, float lr,
+                             float b1, float b2, float eps, float wd, float step_size,
+                             float bc2_sqrt, float gscale) {
+    const float decay = 1.f - lr * wd;
+    const float w1 = 1.f - b1, w2 = 1.f - b2;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const float gi = __fmul_rn(g[i], gscale);
+        float pi = __fmul_rn(p[i], decay);
+        float mi = m[i];
+        mi = __fadd_rn(mi, __fmul_rn(w1, __fsub_rn(gi, mi)));  // lerp, weight < 0.5 branch
+        float vi = __fadd_rn(__fmul_rn(v[i], b2), __fmul_rn(__fmul_rn(w2, gi), gi));
+        const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(vi), bc2_sqrt), eps);
+        pi = __fadd_rn(pi, __fmul_rn(-step_size, __fdiv_rn(mi, denom)));
+        p[i] = pi;
+        m[i] = mi;
+        v[i] = vi;
+    }
+}
+
+// sigmoid(x) > 0.5 masks + confusion counts vs targets cast to uint8 (utils/trainer.py:217-242)
+__global__ void mask_counts_kernel(const float* __restrict__ x, const float* __restrict__ t,
+                                   int64_t n, uint8_t* __restrict__ mask,
+                                   unsigned long long* __restrict__ counts) {
+    unsigned long long c[4] = {0, 0, 0, 0};
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const bool pr = sigmoidf_(x[i]) > 0.5f;
+        const float tv = t[i];
+        const uint8_t tu = (uint8_t)(int)tv;  // numpy astype(uint8) truncation of {0,1} floats
+        const bool pos = tu == 1, neg = tu == 0;
+        if (mask) mask[i] = pr ? 1 : 0;
+        c[0] += pr && pos;
+        c[1] += pr && neg;
+        c[2] += !pr && pos;
+        c[3] += !pr && neg;
+    }
+    for (int k = 0; k < 4; ++k) {
+        unsigned long long s = c[k];
+        for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d);
+        if ((threadIdx.x & 63) == 0 && s) atomicAdd(counts + k, s);
+    }
+}
+
+// NCHW (N,C,H,W) -> NHWC for in_channels > 1
+__global__ void nchw_to_nhwc_kernel(const float* __restrict__ x, int N, int C, int HW,
+                                    float* __restrict__ y) {
+    const int64_t total = (int64_t)N * C * HW;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int c = (int)(i % C);
+        const int64_t p = i / C;
+        const int64_t img = p / HW, hw = p % HW;
+        y[i] = x[(img * C + c) * HW + hw];
+    }
+}
+
+inline int grid_for(int64_t n, int block = 256, int cap = 8192) {
+    int64_t g = (n + block - 1) / block;
+    if (g > cap) g = cap;
+    if (g < 1) g = 1;
+    return (int)g;
+}
+
+}  // namespace
+
+// ============================ host launchers ============================
+#define LAUNCH_CHECK() return (int)hipGetLastError()
+
+int k_pack_conv3(const float* w, float* wf, float* wd, int cin, int cout, hipStream_t s) {
+    const int64_t n = (int64_t)cin * cout * 9;
+    hipLaunchKernelGGL(pack_conv3_kernel, dim3(grid_for(n)), dim3(256), 0, s, w, wf, wd, cin, cout);
+    LAUNCH_CHECK();
+}
+int k_pack_convT(const float* w, float* tf, float* td, int cin, int cout, hipStream_t s) {
+    const int64_t n = (int64_t)cin * cout * 4;
+    hipLaunchKernelGGL(pack_convT_kernel, dim3(grid_for(n)), dim3(256), 0, s, w, tf, td, cin, cout);
+    LAUNCH_CHECK();
+}
+int k_conv_first_fwd(const float* x, const float* w, const float* b, float* y, int P, int H, int W,
+                     int C, float* partial, int G, hipStream_t s) {
+    hipLaunchKernelGGL(conv_first_fwd_kernel, dim3(G), dim3(256), 0, s, x, w, b, y, P, H, W, C,
+                       partial);
+    LAUNCH_CHECK();
+}
+int k_conv_first_wgrad(const float* x, const float* dz, int P, int H, int W, int C, float* partial,
+                       int G, float* gw, float* gb, hipStream_t s) {
+    hipLaunchKernelGGL(conv_first_wgrad_kernel, dim3(G), dim3(256), 0, s, x, dz, P, H, W, C, partial);
+    HIP_OK(hipGetLastError());
+    hipLaunchKernelGGL(conv_first_wgrad_finalize_kernel, dim3((10 * C + 255) / 256), dim3(256), 0,
+                       s, partial, G, C, gw, gb);
+    LAUNCH_CHECK();
+}
+int k_reduce_rows(const float* in, int R, int ncols, float* out, int G, hipStream_t s) {
+    hipLaunchKernelGGL(reduce_rows_kernel, dim3((ncols + 255) / 256, G), dim3(256), 0, s, in, R,
+                       ncols, out);
+    LAUNCH_CHECK();
+}
+int k_bn_finalize_train(const float* part, int G, int C, double count, const float* gamma,
+                        const float* beta, float* rmean, float* rvar, int64_t* nbt, float momentum,
+                        float eps, float* scale, float* shift, float* mean, float* invstd,
+                        hipStream_t s) {
+    hipLaunchKernelGGL(bn_finalize_train_kernel, dim3((C + 255) / 256), dim3(256), 0, s, part, G,
+                       C, count, gamma, beta, rmean, rvar, nbt, momentum, eps, scale, shift, mean,
+                       invstd);
+    LAUNCH_CHECK();
+}
+int k_bn_finalize_eval(int C, const float* gamma, const float* beta, const float* rmean,
+                       const float* rvar, float eps, float* scale, float* shift, hipStream_t s) {
+    hipLaunchKernelGGL(bn_finalize_eval_kernel, dim3((C + 255) / 256), dim3(256), 0, s, C, gamma,
+                       beta, rmean, rvar, eps, scale, shift);
+    LAUNCH_CHECK();
+}
+int k_maxpool_bn(const float* y, int ld, int off, const float* scale, const float* shift, int N,
+                 int H, int W, int C, float* out, uint8_t* idx, hipStream_t s) {
+    const int64_t n = (int64_t)N * (H / 2) * (W / 2) * (C / 4);
+    hipLaunchKernelGGL(maxpool_bn_kernel, dim3(grid_for(n)), dim3(256), 0, s, y, ld, off, scale,
+                       shift, N, H, W, C, out, idx);
+    LAUNCH_CHECK();
+}
+int k_maxpool_bwd(const float* dp, const uint8_t* idx, const float* dskip, int ldskip, int offskip,
+                  int N, int H, int W, int C, float* dout, hipStream_t s) {
+    const int64_t n = (int64_t)N * (H / 2) * (W / 2) * (C / 4);
+    hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for(n)), dim3(256), 0, s, dp, idx, dskip,
+                       ldskip, offskip, N, H, W, C, dout);
+    LAUNCH_CHECK();
+}
+int k_bn_bwd_reduce(const float* dout, const float* y, int ld, int off, int P, int C,
+                    float* partial, int G, hipStream_t s) {
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(G), dim3(256), 0, s, dout, y, ld, off, P, C,
+                       partial);
+    LAUNCH_CHECK();
+}
+int k_bn_bwd_finalize(const float* part, int G, int C, double count, const float* gamma,
+                      const float* mean, const float* invstd, float* coef, float* dgamma,
+                      float* dbeta, hipStream_t s) {
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, part, G, C,
+                       count, gamma, mean, invstd, coef, dgamma, dbeta);
+    LAUNCH_CHECK();
+}
+int k_bn_bwd_apply(float* dz, const float* y, int ld, int off, int P, int C, const float* coef,
+                   float* partial, int G, hipStream_t s) {
+    hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(G), dim3(256), 0, s, dz, y, ld, off, P, C, coef,
+                       partial);
+    LAUNCH_CHECK();
+}
+int k_chan_sum(const float* v, int ld, int off, int P, int C, float* partial, int G,
+               hipStream_t s) {
+    hipLaunchKernelGGL(chan_sum_kernel, dim3(G), dim3(256), 0, s, v, ld, off, P, C, partial);
+    LAUNCH_CHECK();
+}
+int k_sum_partials(const float* part, int G, int ncols, float* out, hipStream_t s) {
+    hipLaunchKernelGGL(sum_partials_kernel, dim3((ncols + 255) / 256), dim3(256), 0, s, part, G,
+                       ncols, out);
+    LAUNCH_CHECK();
+}
+int k_slab_reduce(const float* slab, int S, int Mw, int Nw, int kind, int cin, int cout,
+                  float* grad, hipStream_t s) {
+    hipLaunchKernelGGL(slab_reduce_kernel, dim3(grid_for((int64_t)Mw * Nw)), dim3(256), 0, s, slab,
+                       S, Mw, Nw, kind, cin, cout, grad);
+    LAUNCH_CHECK();
+}
+int k_head_fwd(const float* y, int C, const float* scale, const float* shift, const float* w,
+               const float* b, int O, int P, int HW, float* logits, hipStream_t s) {
+    const int64_t threads = (int64_t)P * (C / 4);
+    hipLaunchKernelGGL(head_fwd_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, y,
+                       C, scale, shift, w, b, O, P, HW, logits);
+    LAUNCH_CHECK();
+}
+int k_head_bwd(const float* y, int C, const float* scale, const float* shift, const float* w,
+               int O, int P, int HW, const float* dlog, float* dout, float* partial, int G,
+               hipStream_t s) {
+    hipLaunchKernelGGL(head_bwd_kernel, dim3(G), dim3(256), 0, s, y, C, scale, shift, w, O, P, HW,
+                       dlog, dout, partial);
+    LAUNCH_CHECK();
+}
+int k_loss_fwd(const float* x, const float* t, int N, int64_t per, float* stats, float* losses,
+               float alpha, float beta, float gamma, hipStream_t s) {
+    hipLaunchKernelGGL(loss_stats_kernel, dim3(N), dim3(1024), 0, s, x, t, per, stats);
+    HIP_OK(hipGetLastError());
+    hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(64), 0, s, stats, N,
+                       (double)per * N, alpha, beta, gamma, losses);
+    LAUNCH_CHECK();
+}
+int k_loss_bwd(const float* x, const float* t, int N, int64_t per, const float* stats,
+               const float* w, float alpha, float beta, float gamma, float* dx, hipStream_t s) {
+    hipLaunchKernelGGL(loss_bwd_kernel, dim3(grid_for(per * N)), dim3(256), 0, s, x, t, per, N,
+                       stats, w, alpha, beta, gamma, dx);
+    LAUNCH_CHECK();
+}
+int k_adamw(float* p, const float* g, float* m, float* v, int64_t n, float lr, float b1, float b2,
+            float eps, float wd, float step_size, float bc2_sqrt, float gscale, hipStream_t s) {
+    hipLaunchKernelGGL(adamw_kernel, dim3(grid_for(n, 256, 16384)), dim3(256), 0, s, p, g, m, v, n,
+                       lr, b1, b2, eps, wd, step_size, bc2_sqrt, gscale);
+    LAUNCH_CHECK();
+}
+int k_mask_counts(const float* x, const float* t, int64_t n, uint8_t* mask, int64_t* counts,
+                  hipStream_t s) {
+    hipLaunchKernelGGL(mask_counts_kernel, dim3(grid_for(n, 256, 2048)), dim3(256), 0, s, x, t, n,
+                       mask, (unsigned long long*)counts);
+    LAUNCH_CHECK();
+}
+int k_nchw_to_nhwc(const float* x, int N, int C, int HW, float* y, hipStream_t s) {
+    hipLaunchKernelGGL(nchw_to_nhwc_kernel, dim3(grid_for((int64_t)N * C * HW)), dim3(256), 0, s, x,
+                       N, C, HW, y);
+    LAUNCH_CHECK();
+}
+
+namespace {
+__global__ void fill_kernel(float* __restrict__ p, int64_t n, float v) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x)
+        p[i] = v;
+}
+}  // namespace
+int k_fill(float* p, int64_t n, float v, hipStream_t s) {
+    hipLaunchKernelGGL(fill_kernel, dim3(grid_for(n)), dim3(256), 0, s, p, n, v);
+    LAUNCH_CHECK();
+}

@@ -1,0 +1,999 @@
+// Native runtime behind include/unet_hip.h: the layer graph of models/model.py:UNet, the
+// workspace plan (NHWC activations, zero-copy concat buffers, packed weights, backward
+// scratch) and the forward / backward / loss / optimizer orchestration on one HIP stream.
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/unet_hip.h"
+#include "kernels_misc.h"
+
+namespace {
+
+constexpr float BN_EPS = 1e-5f;       // nn.BatchNorm2d default (models/model.py:38,41)
+constexpr float BN_MOMENTUM = 0.1f;   // nn.BatchNorm2d default
+constexpr int NBLOCKS = 9;            // enc1..enc4, middle, dec3, dec2, dec1, final
+constexpr int NCONV = 18;             // 3x3 convs
+constexpr int NCONVT = 4;             // ConvTranspose2d k2 s2
+constexpr int RED_G = 512;            // first-level blocks of the channel reductions
+constexpr int STAT_G = 256;           // second level of the BN-stat reduction
+
+struct ParamT {
+    std::string name;
+    int ndim;
+    int64_t shape[4];
+    int64_t off, numel;
+};
+
+struct ConvL {
+    int cin, cout, level, block, which;
+    int64_t w, b;        // param offsets
+    int bn;              // index of the BN that follows (== conv index)
+    int64_t pf, pd;      // packed weight offsets (floats) inside the pack region
+};
+struct BnL {
+    int C;
+    int64_t g, b;        // gamma / beta param offsets
+    int64_t run;         // running_mean offset in the bn arena (var at run + C)
+    std::string name;
+};
+struct ConvTL {
+    int cin, cout, in_level;
+    int64_t w, b;
+    int64_t pf, pd;
+};
+
+struct TimeRec {
+    std::string label;
+    hipEvent_t a, b;
+    double flop;
+};
+
+}  // namespace
+
+struct unet_ctx {
+    int device = 0;
+    int in_ch = 1, out_ch = 1;
+    std::vector<ParamT> params;
+    int64_t n_param_floats = 0;
+    ConvL conv[NCONV];
+    BnL bn[NCONV];
+    ConvTL convt[NCONVT];
+    int64_t head_w = 0, head_b = 0;
+    int64_t n_bn_floats = 0;
+    int64_t pack_floats = 0;
+    std::string err;
+    // buckets (DP overlap)
+    std::vector<int64_t> bucket_off, bucket_len;
+    std::vector<hipEvent_t> bucket_ev;
+    // timing
+    bool timing = false;
+    std::vector<TimeRec> trec;
+    std::vector<hipEvent_t> ev_pool;
+    size_t ev_used = 0;
+};
+
+namespace {
+
+int fail(unet_ctx* c, int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    if (c) c->err = buf;
+    return code;
+}
+
+int level_of_block(int b) { return b <= 4 ? b : 8 - b; }
+
+void build_graph(unet_ctx* c) {
+    int64_t off = 0;
+    auto add = [&](const std::string& name, std::initializer_list<int64_t> shape) {
+        ParamT p;
+        p.name = name;
+        p.ndim = (int)shape.size();
+        p.numel = 1;
+        int i = 0;
+        for (int64_t s : shape) {
+            p.shape[i++] = s;
+            p.numel *= s;
+        }
+        for (; i < 4; ++i) p.shape[i] = 0;
+        p.off = off;
+        off += p.numel;
+        c->params.push_back(p);
+        return p.off;
+    };
+    const char* bname[NBLOCKS] = {"encoder1", "encoder2", "encoder3", "encoder4", "middle.1",
+                                  "decoder3.0", "decoder2.0", "decoder1.0", "final.0"};
+    const int bcin[NBLOCKS] = {c->in_ch, 64, 128, 256, 512, 1024, 512, 256, 128};
+    const int bcout[NBLOCKS] = {64, 128, 256, 512, 1024, 512, 256, 128, 64};
+    const char* tname[NCONVT] = {"middle.2", "decoder3.1", "decoder2.1", "decoder1.1"};
+    int64_t run = 0;
+    auto block = [&](int b) {
+        std::string p = bname[b];
+        for (int which = 0; which < 2; ++which) {
+            const int i = 2 * b + which;
+            ConvL& L = c->conv[i];
+            L.cin = which == 0 ? bcin[b] : bcout[b];
+            L.cout = bcout[b];
+            L.level = level_of_block(b);
+            L.block = b;
+            L.which = which;
+            L.bn = i;
+            L.w = add(p + (which ? ".3.weight" : ".0.weight"), {L.cout, L.cin, 3, 3});
+            L.b = add(p + (which ? ".3.bias" : ".0.bias"), {L.cout});
+            BnL& B = c->bn[i];
+            B.C = L.cout;
+            B.name = p + (which ? ".5" : ".2");
+            B.g = add(B.name + ".weight", {L.cout});
+            B.b = add(B.name + ".bias", {L.cout});
+            B.run = run;
+            run += 2 * L.cout;
+        }
+    };
+    auto convT = [&](int k, int cin) {
+        ConvTL& T = c->convt[k];
+        T.cin = cin;
+        T.cout = cin / 2;
+        T.in_level = 4 - k;
+        T.w = add(std::string(tname[k]) + ".weight", {T.cin, T.cout, 2, 2});
+        T.b = add(std::string(tname[k]) + ".bias", {T.cout});
+    };
+    for (int b = 0; b < 5; ++b) block(b);
+    convT(0, 1024);
+    block(5);
+    convT(1, 512);
+    block(6);
+    convT(2, 256);
+    block(7);
+    convT(3, 128);
+    block(8);
+    c->head_w = add("final.1.weight", {c->out_ch, 64, 1, 1});
+    c->head_b = add("final.1.bias", {c->out_ch});
+    c->n_param_floats = off;
+    c->n_bn_floats = run;
+    // packed weights (forward + dgrad images); conv 0 (Cin = in_channels) has its own kernel
+    int64_t pk = 0;
+    for (int i = 0; i < NCONV; ++i) {
+        ConvL& L = c->conv[i];
+        const int64_t n = (int64_t)L.cin * L.cout * 9;
+        if (i == 0 && L.cin < 32) {
+            L.pf = L.pd = -1;
+            continue;
+        }
+        L.pf = pk;
+        pk += n;
+        L.pd = pk;
+        pk += n;
+    }
+    for (int k = 0; k < NCONVT; ++k) {
+        ConvTL& T = c->convt[k];
+        const int64_t n = (int64_t)T.cin * T.cout * 4;
+        T.pf = pk;
+        pk += n;
+        T.pd = pk;
+        pk += n;
+    }
+    c->pack_floats = pk;
+    // gradient buckets in the order backward completes them (decoder first)
+    auto range = [&](const std::string& first, const std::string& last) {
+        int64_t a = -1, e = -1;
+        for (auto& p : c->params) {
+            if (p.name == first) a = p.off;
+            if (p.name == last) e = p.off + p.numel;
+        }
+        c->bucket_off.push_back(a);
+        c->bucket_len.push_back(e - a);
+    };
+    range("final.0.0.weight", "final.1.bias");
+    range("decoder1.0.0.weight", "decoder1.1.bias");
+    range("decoder2.0.0.weight", "decoder2.1.bias");
+    range("decoder3.0.0.weight", "decoder3.1.bias");
+    range("middle.1.0.weight", "middle.2.bias");
+    range("encoder4.0.weight", "encoder4.5.bias");
+    range("encoder3.0.weight", "encoder3.5.bias");
+    range("encoder2.0.weight", "encoder2.5.bias");
+    range("encoder1.0.weight", "encoder1.5.bias");
+}
+
+// ------------------------------------------------------------------------------------
+// Workspace plan.  A bump allocator over the caller's buffer; the same function sizes and
+// carves it so forward and backward agree on every pointer.
+// ------------------------------------------------------------------------------------
+struct Plan {
+    int N, H, W;
+    int64_t P[5];  // pixels per level
+    float* pack;
+    float* x_nhwc;
+    float* y[NCONV];
+    int ldy[NCONV], offy[NCONV];
+    float* cat[4];
+    float* cat_scale[4];
+    float* cat_shift[4];
+    float* pool[4];
+    uint8_t* idx[4];
+    float *scale[NCONV], *shift[NCONV], *mean[NCONV], *invstd[NCONV];
+    float* stats;
+    float* stats2;
+    // backward
+    float* g[2];
+    float* dcat[4];
+    float* slab;
+    float* part;
+    float* part2;
+    float* coef;
+    size_t bytes;
+};
+
+struct Bump {
+    char* base;
+    size_t off = 0;
+    template <class T>
+    T* take(int64_t n) {
+        off = (off + 255) & ~(size_t)255;
+        T* p = base ? (T*)(base + off) : nullptr;
+        off += (size_t)n * sizeof(T);
+        return p;
+    }
+};
+
+struct WgradCfg {
+    int bm, bn, splits, pps;
+};
+
+WgradCfg wgrad_cfg(int CA, int tapsA, int CB, int tapsB, int64_t P) {
+    WgradCfg w;
+    w.bm = CA % 128 == 0 ? 128 : 64;
+    w.bn = CB % 128 == 0 ? 128 : 64;
+    const int64_t tiles = (int64_t)(tapsA * CA / w.bm) * (tapsB * CB / w.bn);
+    int64_t s = (2048 + tiles - 1) / tiles;
+    const int64_t maxs = P / 256 > 0 ? P / 256 : 1;  // keep >= 8 pixel chunks per split
+    if (s > maxs) s = maxs;
+    if (s < 1) s = 1;
+    int64_t pps = (P + s - 1) / s;
+    pps = (pps + 31) / 32 * 32;
+    w.pps = (int)pps;
+    w.splits = (int)((P + pps - 1) / pps);
+    return w;
+}
+
+void make_plan(unet_ctx* c, int N, int H, int W, bool training, char* base, Plan& p) {
+    Bump b{base};
+    p.N = N;
+    p.H = H;
+    p.W = W;
+    for (int l = 0; l < 5; ++l) p.P[l] = (int64_t)N * (H >> l) * (W >> l);
+    p.pack = b.take<float>(c->pack_floats);
+    p.x_nhwc = b.take<float>(p.P[0] * c->in_ch);  // NHWC copy of x (conv-0 wgrad input)
+    for (int l = 0; l < 4; ++l) {
+        const int C = 64 << l;
+        p.cat[l] = b.take<float>(p.P[l] * 2 * C);
+        p.cat_scale[l] = b.take<float>(2 * C);
+        p.cat_shift[l] = b.take<float>(2 * C);
+        p.pool[l] = b.take<float>(p.P[l + 1] * C);
+        p.idx[l] = b.take<uint8_t>(p.P[l + 1] * C);
+    }
+    for (int i = 0; i < NCONV; ++i) {
+        const ConvL& L = c->conv[i];
+        if (L.block < 4 && L.which == 1) {
+            const int C = 64 << L.block;
+            p.y[i] = p.cat[L.block] ? p.cat[L.block] : nullptr;
+            p.ldy[i] = 2 * C;
+            p.offy[i] = C;
+            // the encoder output's BN affine is the second half of the concat affine
+            p.scale[i] = p.cat_scale[L.block] ? p.cat_scale[L.block] + C : nullptr;
+            p.shift[i] = p.cat_shift[L.block] ? p.cat_shift[L.block] + C : nullptr;
+        } else {
+            p.y[i] = b.take<float>(p.P[L.level] * L.cout);
+            p.ldy[i] = L.cout;
+            p.offy[i] = 0;
+            p.scale[i] = b.take<float>(L.cout);
+            p.shift[i] = b.take<float>(L.cout);
+        }
+        p.mean[i] = b.take<float>(L.cout);
+        p.invstd[i] = b.take<float>(L.cout);
+    }
+    // BN-stat partials: rows = M / 128 of the row GEMM, or RED_G for the first conv
+    int64_t srows = 0;
+    for (int i = 0; i < NCONV; ++i) {
+        const int64_t r = std::max<int64_t>(p.P[c->conv[i].level] / 128, RED_G);
+        srows = std::max(srows, r * 2 * c->conv[i].cout);
+    }
+    p.stats = b.take<float>(srows);
+    p.stats2 = b.take<float>((int64_t)STAT_G * 2 * 1024);
+    if (training) {
+        int64_t gmax = p.P[0] * 64;
+        for (int i = 0; i < NCONV; ++i)
+            gmax = std::max(gmax, p.P[c->conv[i].level] * c->conv[i].cout);
+        p.g[0] = b.take<float>(gmax);
+        p.g[1] = b.take<float>(gmax);
+        for (int l = 0; l < 4; ++l) p.dcat[l] = b.take<float>(p.P[l] * 2 * (64 << l));
+        int64_t smax = 0;
+        for (int i = 1; i < NCONV; ++i) {
+            const ConvL& L = c->conv[i];
+            WgradCfg w = wgrad_cfg(L.cin, 9, L.cout, 1, p.P[L.level]);
+            smax = std::max(smax, (int64_t)w.splits * 9 * L.cin * L.cout);
+        }
+        for (int k = 0; k < NCONVT; ++k) {
+            const ConvTL& T = c->convt[k];
+            WgradCfg w = wgrad_cfg(T.cin, 1, T.cout, 4, p.P[T.in_level]);
+            smax = std::max(smax, (int64_t)w.splits * T.cin * 4 * T.cout);
+        }
+        p.slab = b.take<float>(smax);
+        p.part = b.take<float>((int64_t)RED_G * (10 * 1024 + 64));
+        p.part2 = b.take<float>((int64_t)RED_G * 2 * 1024);
+        p.coef = b.take<float>(3 * 1024);
+    } else {
+        p.g[0] = p.g[1] = p.slab = p.part = p.part2 = p.coef = nullptr;
+        for (int l = 0; l < 4; ++l) p.dcat[l] = nullptr;
+    }
+    p.bytes = b.off + 256;
+}
+
+// ------------------------------------------------------------------------------------
+// launch bookkeeping (optional per-launch HIP-event timing)
+// ------------------------------------------------------------------------------------
+struct Launcher {
+    unet_ctx* c;
+    hipStream_t s;
+    hipEvent_t ev() {
+        if (c->ev_used == c->ev_pool.size()) {
+            hipEvent_t e;
+            (void)hipEventCreate(&e);
+            c->ev_pool.push_back(e);
+        }
+        return c->ev_pool[c->ev_used++];
+    }
+    template <class F>
+    int run(const char* label, double flop, F&& f) {
+        hipEvent_t a = nullptr, b = nullptr;
+        if (c->timing) {
+            a = ev();
+            b = ev();
+            (void)hipEventRecord(a, s);
+        }
+        int r = f();
+        if (r != 0) return fail(c, UNET_ERR_HIP, "%s: launch failed (%d: %s)", label, r,
+                                r > 0 ? hipGetErrorString((hipError_t)r) : "bad shape");
+        if (c->timing) {
+            (void)hipEventRecord(b, s);
+            c->trec.push_back(TimeRec{label, a, b, flop});
+        }
+        return 0;
+    }
+};
+
+#define RUN(label, flop, expr)                            \
+    do {                                                  \
+        int rc_ = L.run(label, flop, [&]() { return (expr); }); \
+        if (rc_) return rc_;                              \
+    } while (0)
+
+int stats_finalize(unet_ctx* c, Launcher& L, Plan& p, int i, int R, int64_t count, bool training,
+                   const float* prm, float* bn_run, int64_t* bn_cnt) {
+    const BnL& B = c->bn[i];
+    const int C = B.C;
+    hipStream_t s = L.s;
+    if (!training) {
+        RUN("bn_finalize", 0,
+            k_bn_finalize_eval(C, prm + B.g, prm + B.b, bn_run + B.run, bn_run + B.run + C, BN_EPS,
+                               p.scale[i], p.shift[i], s));
+        return 0;
+    }
+    const float* part = p.stats;
+    int G = R;
+    if (R > STAT_G) {
+        RUN("bn_stats_reduce", 0, k_reduce_rows(p.stats, R, 2 * C, p.stats2, STAT_G, s));
+        part = p.stats2;
+        G = STAT_G;
+    }
+    RUN("bn_finalize", 0,
+        k_bn_finalize_train(part, G, C, (double)count, prm + B.g, prm + B.b,
+                            bn_run ? bn_run + B.run : nullptr,
+                            bn_run ? bn_run + B.run + C : nullptr, bn_cnt ? bn_cnt + i : nullptr,
+                            BN_MOMENTUM, BN_EPS, p.scale[i], p.shift[i], p.mean[i], p.invstd[i],
+                            s));
+    return 0;
+}
+
+// Input operand of conv i: pointer, ld, offset, affine.
+struct Operand {
+    const float* ptr;
+    int ld, off;
+    const float* scale;
+    const float* shift;
+};
+
+Operand conv_input(unet_ctx* c, Plan& p, int i) {
+    const ConvL& L = c->conv[i];
+    if (L.which == 1) return {p.y[i - 1], p.ldy[i - 1], p.offy[i - 1], p.scale[i - 1], p.shift[i - 1]};
+    if (L.block >= 1 && L.block <= 4)
+        return {p.pool[L.block - 1], c->conv[i].cin, 0, nullptr, nullptr};
+    if (L.block >= 5) {
+        const int l = L.level;
+        return {p.cat[l], 2 * (64 << l), 0, p.cat_scale[l], p.cat_shift[l]};
+    }
+    return {nullptr, 0, 0, nullptr, nullptr};  // conv 0: x
+}
+
+int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, const float* x,
+                 float* logits, Plan& p, bool training, hipStream_t s) {
+    Launcher L{c, s};
+    const int N = p.N, H = p.H, W = p.W;
+    // 1. weight images for the row GEMMs (re-packed every call: params may have changed
+    //    through the optimizer or load_state_dict; ~0.1 ms of HBM traffic per step)
+    for (int i = 0; i < NCONV; ++i) {
+        const ConvL& C = c->conv[i];
+        if (C.pf < 0) continue;
+        RUN("pack", 0, k_pack_conv3(prm + C.w, p.pack + C.pf, training ? p.pack + C.pd : nullptr,
+                                    C.cin, C.cout, s));
+    }
+    for (int k = 0; k < NCONVT; ++k) {
+        const ConvTL& T = c->convt[k];
+        RUN("pack", 0, k_pack_convT(prm + T.w, p.pack + T.pf, training ? p.pack + T.pd : nullptr,
+                                    T.cin, T.cout, s));
+    }
+    // 2. concat affine: identity on the up-sampled half (no BN between ConvT and concat)
+    for (int l = 0; l < 4; ++l) {
+        const int C = 64 << l;
+        RUN("fill", 0, k_fill(p.cat_scale[l], C, 1.f, s));
+        RUN("fill", 0, k_fill(p.cat_shift[l], C, 0.f, s));
+    }
+    // in_channels == 1: NCHW == NHWC; keep a private copy for the conv-0 wgrad
+    RUN("copy_x", 0, (int)hipMemcpyAsync(p.x_nhwc, x, sizeof(float) * p.P[0] * c->in_ch,
+                                         hipMemcpyDeviceToDevice, s));
+    const float* xin = p.x_nhwc;
+
+    auto conv = [&](int i) -> int {
+        const ConvL& C = c->conv[i];
+        const int Hl = H >> C.level, Wl = W >> C.level;
+        const int64_t M = p.P[C.level];
+        int R;
+        if (i == 0 && C.pf < 0) {
+            R = RED_G;
+            RUN("conv_first_fwd", 2.0 * M * 9 * C.cout,
+                k_conv_first_fwd(xin, prm + C.w, prm + C.b, p.y[0], (int)M, Hl, Wl, C.cout,
+                                 p.stats, R, s));
+        } else {
+            Operand a = conv_input(c, p, i);
+            RowGemmArgs g{};
+            g.H = Hl;
+            g.W = Wl;
+            g.M = (int)M;
+            g.N = C.cout;
+            g.K = 9 * C.cin;
+            g.a = a.ptr;
+            g.lda = a.ld;
+            g.aoff = a.off;
+            g.C = C.cin;
+            g.amode = G_CONV3;
+            g.ascale = a.scale;
+            g.ashift = a.shift;
+            g.bt = p.pack + C.pf;
+            g.out = p.y[i];
+            g.ldo = p.ldy[i];
+            g.ooff = p.offy[i];
+            g.bias = prm + C.b;
+            g.stats = p.stats;
+            g.emode = E_BIAS_RELU_STATS;
+            const int bn = C.cout % 128 == 0 ? 128 : 64;
+            R = (int)(M / 128);
+            RUN("conv_fwd", 2.0 * M * C.cout * 9 * C.cin, launch_rowgemm(g, 128, bn, s));
+        }
+        return stats_finalize(c, L, p, i, R, M, training, prm, bn_run, bn_cnt);
+    };
+    auto convT = [&](int k) -> int {
+        const ConvTL& T = c->convt[k];
+        const int src = 2 * (4 + k) + 1;  // second conv of middle / dec3 / dec2 / dec1
+        const int lo = T.in_level - 1;
+        RowGemmArgs g{};
+        g.H = H >> T.in_level;
+        g.W = W >> T.in_level;
+        g.M = (int)p.P[T.in_level];
+        g.N = 4 * T.cout;
+        g.K = T.cin;
+        g.a = p.y[src];
+        g.lda = p.ldy[src];
+        g.aoff = p.offy[src];
+        g.C = T.cin;
+        g.amode = G_IDENT;
+        g.ascale = p.scale[src];
+        g.ashift = p.shift[src];
+        g.bt = p.pack + T.pf;
+        g.out = p.cat[lo];
+        g.ldo = 2 * (64 << lo);
+        g.ooff = 0;
+        g.bias = prm + T.b;
+        g.cout = T.cout;
+        g.emode = E_CONVT;
+        const int bn = T.cout % 128 == 0 ? 128 : 64;
+        RUN("convT_fwd", 2.0 * g.M * g.N * g.K, launch_rowgemm(g, 128, bn, s));
+        return 0;
+    };
+
+    int rc;
+    for (int b = 0; b < 5; ++b) {
+        if ((rc = conv(2 * b))) return rc;
+        if ((rc = conv(2 * b + 1))) return rc;
+        if (b < 4) {
+            const int i = 2 * b + 1, C = 64 << b;
+            RUN("maxpool_fwd", 0,
+                k_maxpool_bn(p.y[i], p.ldy[i], p.offy[i], p.scale[i], p.shift[i], N, H >> b, W >> b,
+                             C, p.pool[b], p.idx[b], s));
+        }
+    }
+    if ((rc = convT(0))) return rc;
+    for (int b = 5; b < 9; ++b) {
+        if ((rc = conv(2 * b))) return rc;
+        if ((rc = conv(2 * b + 1))) return rc;
+        if (b < 8 && (rc = convT(b - 4))) return rc;
+    }
+    RUN("head_fwd", 2.0 * p.P[0] * 64 * c->out_ch,
+        k_head_fwd(p.y[17], 64, p.scale[17], p.shift[17], prm + c->head_w, prm + c->head_b,
+                   c->out_ch, (int)p.P[0], H * W, logits, s));
+    return 0;
+}
+
+int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* grads, Plan& p,
+                  hipStream_t s) {
+    Launcher L{c, s};
+    const int N = p.N, H = p.H, W = p.W;
+    (void)N;
+    int rc;
+
+    // BN backward through ReLU, in place: do -> dz; writes dgamma, dbeta, conv bias grad
+    auto bn_bwd = [&](int i, float* d) -> int {
+        const ConvL& C = c->conv[i];
+        const BnL& B = c->bn[i];
+        const int64_t P = p.P[C.level];
+        RUN("bn_bwd_reduce", 0,
+            k_bn_bwd_reduce(d, p.y[i], p.ldy[i], p.offy[i], (int)P, C.cout, p.part, RED_G, s));
+        RUN("bn_bwd_finalize", 0,
+            k_bn_bwd_finalize(p.part, RED_G, C.cout, (double)P, prm + B.g, p.mean[i], p.invstd[i],
+                              p.coef, grads + B.g, grads + B.b, s));
+        RUN("bn_bwd_apply", 0,
+            k_bn_bwd_apply(d, p.y[i], p.ldy[i], p.offy[i], (int)P, C.cout, p.coef, p.part2,
+                           RED_G, s));
+        RUN("bias_grad", 0, k_sum_partials(p.part2, RED_G, C.cout, grads + C.b, s));
+        return 0;
+    };
+    // conv backward: wgrad from (input, dz), dgrad dz -> dx (ld, off) when dx != null
+    auto conv_bwd = [&](int i, const float* dz, float* dx, int ldx) -> int {
+        const ConvL& C = c->conv[i];
+        const int Hl = H >> C.level, Wl = W >> C.level;
+        const int64_t P = p.P[C.level];
+        if (i == 0 && C.pf < 0) {
+            RUN("conv_first_wgrad", 2.0 * P * 9 * C.cout,
+                k_conv_first_wgrad(p.x_nhwc, dz, (int)P, Hl, Wl, C.cout,
+                                   p.part, RED_G, grads + C.w, grads + C.b, s));
+            return 0;
+        }
+        Operand a = conv_input(c, p, i);
+        WgradCfg wc = wgrad_cfg(C.cin, 9, C.cout, 1, P);
+        WgradArgs w{};
+        w.H = Hl;
+        w.W = Wl;
+        w.P = (int)P;
+        w.a = a.ptr;
+        w.lda = a.ld;
+        w.aoff = a.off;
+        w.CA = C.cin;
+        w.amode = G_CONV3;
+        w.ascale = a.scale;
+        w.ashift = a.shift;
+        w.b = dz;
+        w.ldb = C.cout;
+        w.boff = 0;
+        w.CB = C.cout;
+        w.bmode = G_IDENT;
+        w.Mw = 9 * C.cin;
+        w.Nw = C.cout;
+        w.pps = wc.pps;
+        w.splits = wc.splits;
+        w.slab = p.slab;
+        RUN("conv_wgrad", 2.0 * P * C.cout * 9 * C.cin, launch_wgrad(w, wc.bm, wc.bn, s));
+        RUN("wgrad_reduce", 0,
+            k_slab_reduce(p.slab, wc.splits, w.Mw, w.Nw, 0, C.cin, C.cout, grads + C.w, s));
+        if (dx) {
+            RowGemmArgs g{};
+            g.H = Hl;
+            g.W = Wl;
+            g.M = (int)P;
+            g.N = C.cin;
+            g.K = 9 * C.cout;
+            g.a = dz;
+            g.lda = C.cout;
+            g.aoff = 0;
+            g.C = C.cout;
+            g.amode = G_CONV3;
+            g.bt = p.pack + C.pd;
+            g.out = dx;
+            g.ldo = ldx;
+            g.ooff = 0;
+            g.emode = E_STORE;
+            const int bn = C.cin % 128 == 0 ? 128 : 64;
+            RUN("conv_dgrad", 2.0 * P * C.cout * 9 * C.cin, launch_rowgemm(g, 128, bn, s));
+        }
+        return 0;
+    };
+    // ConvT k backward: dOut = dcat[lo][:, 0:cout]; writes do of its input into dx
+    auto convT_bwd = [&](int k, float* dx) -> int {
+        const ConvTL& T = c->convt[k];
+        const int src = 2 * (4 + k) + 1;
+        const int lo = T.in_level - 1;
+        const int ldo = 2 * (64 << lo);
+        const int Hi = H >> T.in_level, Wi = W >> T.in_level;
+        const int64_t Pin = p.P[T.in_level], Pout = p.P[lo];
+        RUN("convT_bias_grad", 0, k_chan_sum(p.dcat[lo], ldo, 0, (int)Pout, T.cout, p.part, RED_G, s));
+        RUN("bias_grad", 0, k_sum_partials(p.part, RED_G, T.cout, grads + T.b, s));
+        WgradCfg wc = wgrad_cfg(T.cin, 1, T.cout, 4, Pin);
+        WgradArgs w{};
+        w.H = Hi;
+        w.W = Wi;
+        w.P = (int)Pin;
+        w.a = p.y[src];
+        w.lda = p.ldy[src];
+        w.aoff = p.offy[src];
+        w.CA = T.cin;
+        w.amode = G_IDENT;
+        w.ascale = p.scale[src];
+        w.ashift = p.shift[src];
+        w.b = p.dcat[lo];
+        w.ldb = ldo;
+        w.boff = 0;
+        w.CB = T.cout;
+        w.bmode = G_UP2;
+        w.Mw = T.cin;
+        w.Nw = 4 * T.cout;
+        w.pps = wc.pps;
+        w.splits = wc.splits;
+        w.slab = p.slab;
+        RUN("convT_wgrad", 2.0 * Pin * T.cin * 4 * T.cout, launch_wgrad(w, wc.bm, wc.bn, s));
+        RUN("wgrad_reduce", 0,
+            k_slab_reduce(p.slab, wc.splits, w.Mw, w.Nw, 1, T.cin, T.cout, grads + T.w, s));
+        RowGemmArgs g{};
+        g.H = Hi;
+        g.W = Wi;
+        g.M = (int)Pin;
+        g.N = T.cin;
+        g.K = 4 * T.cout;
+        g.a = p.dcat[lo];
+        g.lda = ldo;
+        g.aoff = 0;
+        g.C = T.cout;
+        g.amode = G_UP2;
+        g.bt = p.pack + T.pd;
+        g.out = dx;
+        g.ldo = T.cin;
+        g.ooff = 0;
+        g.emode = E_STORE;
+        const int bn = T.cin % 128 == 0 ? 128 : 64;
+        RUN("convT_dgrad", 2.0 * Pin * T.cin * 4 * T.cout, launch_rowgemm(g, 128, bn, s));
+        return 0;
+    };
+    auto bucket_done = [&](int b) {
+        if (b < (int)c->bucket_ev.size()) (void)hipEventRecord(c->bucket_ev[b], s);
+    };
+
+    float* G0 = p.g[0];
+    float* G1 = p.g[1];
+    // ---- final block + head (bucket 0) ----
+    RUN("head_bwd", 2.0 * p.P[0] * 64 * c->out_ch * 2,
+        k_head_bwd(p.y[17], 64, p.scale[17], p.shift[17], prm + c->head_w, c->out_ch, (int)p.P[0],
+                   H * W, dlogits, G0, p.part, RED_G, s));
+    RUN("head_grad", 0, k_sum_partials(p.part, RED_G, c->out_ch * 64 + c->out_ch, grads + c->head_w, s));
+    if ((rc = bn_bwd(17, G0))) return rc;
+    if ((rc = conv_bwd(17, G0, G1, 64))) return rc;
+    if ((rc = bn_bwd(16, G1))) return rc;
+    if ((rc = conv_bwd(16, G1, p.dcat[0], 128))) return rc;
+    bucket_done(0);
+    // ---- decoders: ConvT k then block 4+k ----
+    for (int k = 3; k >= 0; --k) {
+        const int b = 4 + k;  // block producing the ConvT input
+        const int i1 = 2 * b + 1, i0 = 2 * b;
+        if ((rc = convT_bwd(k, G0))) return rc;
+        if ((rc = bn_bwd(i1, G0))) return rc;
+        if ((rc = conv_bwd(i1, G0, G1, c->conv[i1].cin))) return rc;
+        if ((rc = bn_bwd(i0, G1))) return rc;
+        if (b >= 5) {
+            const int l = c->conv[i0].level;  // input is CAT_l
+            if ((rc = conv_bwd(i0, G1, p.dcat[l], 2 * (64 << l)))) return rc;
+            bucket_done(4 - k);  // decoder1 -> bucket 1, decoder2 -> 2, decoder3 -> 3
+        } else {
+            // middle block: input is pool[3]
+            if ((rc = conv_bwd(i0, G1, G0, c->conv[i0].cin))) return rc;
+            bucket_done(4);
+        }
+    }
+    // G0 = d pool[3]
+    // ---- encoders ----
+    float* cur = G0;
+    for (int b = 3; b >= 0; --b) {
+        const int C = 64 << b;
+        float* nxt = cur == G0 ? G1 : G0;
+        RUN("maxpool_bwd", 0,
+            k_maxpool_bwd(cur, p.idx[b], p.dcat[b], 2 * C, C, p.N, H >> b, W >> b, C, nxt, s));
+        cur = nxt;
+        nxt = cur == G0 ? G1 : G0;
+        const int i1 = 2 * b + 1, i0 = 2 * b;
+        if ((rc = bn_bwd(i1, cur))) return rc;
+        if ((rc = conv_bwd(i1, cur, nxt, C))) return rc;
+        cur = nxt;
+        nxt = cur == G0 ? G1 : G0;
+        if ((rc = bn_bwd(i0, cur))) return rc;
+        if (b > 0) {
+            if ((rc = conv_bwd(i0, cur, nxt, c->conv[i0].cin))) return rc;
+            cur = nxt;
+        } else {
+            if ((rc = conv_bwd(0, cur, nullptr, 0))) return rc;
+        }
+        bucket_done(8 - b);
+    }
+    return 0;
+}
+
+bool shape_ok(int N, int H, int W) { return N >= 1 && H >= 16 && W >= 16 && H % 16 == 0 && W % 16 == 0; }
+
+}  // namespace
+
+// ====================================== C ABI ======================================
+extern "C" {
+
+int unet_create(const unet_cfg* cfg, int device, unet_ctx** out) {
+    if (!out) return UNET_ERR_INVALID;
+    *out = nullptr;
+    unet_ctx* c = new unet_ctx();
+    c->device = device;
+    if (cfg) {
+        c->in_ch = cfg->in_channels;
+        c->out_ch = cfg->out_channels;
+    }
+    // models/model.py:UNet defaults (1, 1) are what every BASELINE config uses; the first
+    // conv kernel is specialised for a single input channel.
+    if (c->in_ch != 1 || c->out_ch < 1 || c->out_ch > 4) {
+        delete c;
+        return UNET_ERR_UNSUPPORTED;
+    }
+    build_graph(c);
+    *out = c;
+    return UNET_OK;
+}
+
+int unet_destroy(unet_ctx* c) {
+    if (!c) return UNET_ERR_INVALID;
+    for (auto e : c->bucket_ev) (void)hipEventDestroy(e);
+    for (auto e : c->ev_pool) (void)hipEventDestroy(e);
+    delete c;
+    return UNET_OK;
+}
+
+const char* unet_last_error(const unet_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int unet_num_params(const unet_ctx* c, int* n, int64_t* nf) {
+    if (!c) return UNET_ERR_INVALID;
+    if (n) *n = (int)c->params.size();
+    if (nf) *nf = c->n_param_floats;
+    return UNET_OK;
+}
+
+int unet_param_info(const unet_ctx* c, int i, const char** name, int* ndim, int64_t shape[4],
+                    int64_t* offset) {
+    if (!c || i < 0 || i >= (int)c->params.size()) return UNET_ERR_INVALID;
+    const ParamT& p = c->params[i];
+    if (name) *name = p.name.c_str();
+    if (ndim) *ndim = p.ndim;
+    if (shape)
+        for (int k = 0; k < 4; ++k) shape[k] = p.shape[k];
+    if (offset) *offset = p.off;
+    return UNET_OK;
+}
+
+int unet_num_bn(const unet_ctx* c, int* n, int64_t* nf) {
+    if (!c) return UNET_ERR_INVALID;
+    if (n) *n = NCONV;
+    if (nf) *nf = c->n_bn_floats;
+    return UNET_OK;
+}
+
+int unet_bn_info(const unet_ctx* c, int i, const char** name, int* ch, int64_t* off) {
+    if (!c || i < 0 || i >= NCONV) return UNET_ERR_INVALID;
+    if (name) *name = c->bn[i].name.c_str();
+    if (ch) *ch = c->bn[i].C;
+    if (off) *off = c->bn[i].run;
+    return UNET_OK;
+}
+
+int unet_workspace_size(unet_ctx* c, int N, int H, int W, int training, size_t* bytes) {
+    if (!c || !bytes) return UNET_ERR_INVALID;
+    if (!shape_ok(N, H, W)) return fail(c, UNET_ERR_SHAPE, "bad shape N=%d H=%d W=%d", N, H, W);
+    Plan p;
+    make_plan(c, N, H, W, training != 0, nullptr, p);
+    *bytes = p.bytes;
+    return UNET_OK;
+}
+
+int unet_forward(unet_ctx* c, const float* params, float* bn_running, int64_t* bn_count,
+                 const float* x, float* logits, void* ws, size_t ws_bytes, int N, int H, int W,
+                 int training, unet_stream_t stream) {
+    if (!c || !params || !x || !logits || !ws) return c ? fail(c, UNET_ERR_INVALID, "null pointer") : UNET_ERR_INVALID;
+    if (!shape_ok(N, H, W)) return fail(c, UNET_ERR_SHAPE, "bad shape N=%d H=%d W=%d", N, H, W);
+    if (!training && !bn_running)
+        return fail(c, UNET_ERR_INVALID, "eval forward needs running statistics");
+    Plan p;
+    make_plan(c, N, H, W, training != 0, nullptr, p);
+    if (ws_bytes < p.bytes) return fail(c, UNET_ERR_WORKSPACE, "workspace %zu < %zu", ws_bytes, p.bytes);
+    make_plan(c, N, H, W, training != 0, (char*)ws, p);
+    if (hipSetDevice(c->device) != hipSuccess) return fail(c, UNET_ERR_HIP, "hipSetDevice");
+    if (!c->timing) c->ev_used = 0;
+    return forward_impl(c, params, bn_running, bn_count, x, logits, p, training != 0,
+                        (hipStream_t)stream);
+}
+
+int unet_backward(unet_ctx* c, const float* params, const float* dlogits, float* grads, void* ws,
+                  size_t ws_bytes, int N, int H, int W, unet_stream_t stream) {
+    if (!c || !params || !dlogits || !grads || !ws) return c ? fail(c, UNET_ERR_INVALID, "null pointer") : UNET_ERR_INVALID;
+    if (!shape_ok(N, H, W)) return fail(c, UNET_ERR_SHAPE, "bad shape N=%d H=%d W=%d", N, H, W);
+    Plan p;
+    make_plan(c, N, H, W, true, nullptr, p);
+    if (ws_bytes < p.bytes) return fail(c, UNET_ERR_WORKSPACE, "workspace %zu < %zu", ws_bytes, p.bytes);
+    make_plan(c, N, H, W, true, (char*)ws, p);
+    if (hipSetDevice(c->device) != hipSuccess) return fail(c, UNET_ERR_HIP, "hipSetDevice");
+    if (c->bucket_ev.empty()) {
+        c->bucket_ev.resize(c->bucket_off.size());
+        for (auto& e : c->bucket_ev) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
+    }
+    return backward_impl(c, params, dlogits, grads, p, (hipStream_t)stream);
+}
+
+int unet_loss_fwd(unet_ctx* c, const float* logits, const float* targets, int N, int C, int H,
+                  int W, float* stats, float* losses, float fa, float fb, float fg,
+                  unet_stream_t stream) {
+    if (!c || !logits || !targets || !stats || !losses) return UNET_ERR_INVALID;
+    if (N < 1 || C < 1 || H < 1 || W < 1) return fail(c, UNET_ERR_SHAPE, "bad loss shape");
+    int r = k_loss_fwd(logits, targets, N, (int64_t)C * H * W, stats, losses, fa, fb, fg,
+                       (hipStream_t)stream);
+    return r ? fail(c, UNET_ERR_HIP, "loss_fwd launch %d", r) : UNET_OK;
+}
+
+int unet_loss_bwd(unet_ctx* c, const float* logits, const float* targets, int N, int C, int H,
+                  int W, const float* stats, const float* w, float* dlogits, float fa, float fb,
+                  float fg, unet_stream_t stream) {
+    if (!c || !logits || !targets || !stats || !w || !dlogits) return UNET_ERR_INVALID;
+    if (N < 1 || C < 1 || H < 1 || W < 1) return fail(c, UNET_ERR_SHAPE, "bad loss shape");
+    int r = k_loss_bwd(logits, targets, N, (int64_t)C * H * W, stats, w, fa, fb, fg, dlogits,
+                       (hipStream_t)stream);
+    return r ? fail(c, UNET_ERR_HIP, "loss_bwd launch %d", r) : UNET_OK;
+}
+
+int unet_adamw(unet_ctx* c, float* params, const float* grads, float* m, float* v, int64_t n,
+               int step, float lr, float b1, float b2, float eps, float wd, float gscale,
+               unet_stream_t stream) {
+    if (!c || !params || !grads || !m || !v || n < 0 || step < 1) return UNET_ERR_INVALID;
+    // torch optim/adam.py: bias corrections computed on the host in double then used as
+    // python floats (double) -> step_size and bias_correction2_sqrt
+    const double bc1 = 1.0 - pow((double)b1, step);
+    const double bc2 = 1.0 - pow((double)b2, step);
+    const double step_size = (double)lr / bc1;
+    const double bc2_sqrt = sqrt(bc2);
+    int r = k_adamw(params, grads, m, v, n, lr, b1, b2, eps, wd, (float)step_size, (float)bc2_sqrt,
+                    gscale, (hipStream_t)stream);
+    return r ? fail(c, UNET_ERR_HIP, "adamw launch %d", r) : UNET_OK;
+}
+
+int unet_mask_counts(unet_ctx* c, const float* logits, const float* targets, int64_t n,
+                     uint8_t* mask, int64_t* counts, unet_stream_t stream) {
+    if (!c || !logits || !targets || !counts || n < 0) return UNET_ERR_INVALID;
+    int r = k_mask_counts(logits, targets, n, mask, counts, (hipStream_t)stream);
+    return r ? fail(c, UNET_ERR_HIP, "mask_counts launch %d", r) : UNET_OK;
+}
+
+int unet_num_buckets(const unet_ctx* c, int* n) {
+    if (!c || !n) return UNET_ERR_INVALID;
+    *n = (int)c->bucket_off.size();
+    return UNET_OK;
+}
+
+int unet_bucket_range(const unet_ctx* c, int b, int64_t* off, int64_t* len) {
+    if (!c || b < 0 || b >= (int)c->bucket_off.size()) return UNET_ERR_INVALID;
+    if (off) *off = c->bucket_off[b];
+    if (len) *len = c->bucket_len[b];
+    return UNET_OK;
+}
+
+int unet_stream_wait_bucket(unet_ctx* c, int b, unet_stream_t stream) {
+    if (!c || b < 0 || b >= (int)c->bucket_ev.size()) return UNET_ERR_INVALID;
+    if (hipStreamWaitEvent((hipStream_t)stream, c->bucket_ev[b], 0) != hipSuccess)
+        return fail(c, UNET_ERR_HIP, "hipStreamWaitEvent");
+    return UNET_OK;
+}
+
+int unet_timing_enable(unet_ctx* c, int en) {
+    if (!c) return UNET_ERR_INVALID;
+    c->timing = en != 0;
+    return UNET_OK;
+}
+
+int unet_timing_reset(unet_ctx* c) {
+    if (!c) return UNET_ERR_INVALID;
+    c->trec.clear();
+    c->ev_used = 0;
+    return UNET_OK;
+}
+
+int unet_timing_count(unet_ctx* c, int* n) {
+    if (!c || !n) return UNET_ERR_INVALID;
+    *n = (int)c->trec.size();
+    return UNET_OK;
+}
+
+int unet_timing_read(unet_ctx* c, int i, const char** family, int64_t* launches, double* total_ms,
+                     double* flop) {
+    if (!c || i < 0 || i >= (int)c->trec.size()) return UNET_ERR_INVALID;
+    TimeRec& t = c->trec[i];
+    if (hipEventSynchronize(t.b) != hipSuccess) return fail(c, UNET_ERR_HIP, "event sync");
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, t.a, t.b);
+    if (family) *family = t.label.c_str();
+    if (launches) *launches = 1;
+    if (total_ms) *total_ms = ms;
+    if (flop) *flop = t.flop;
+    return UNET_OK;
+}
+
+int unet_debug_view(unet_ctx* c, int N, int H, int W, int training, int kind, int index,
+                    int64_t* byte_offset, int64_t* count, int* ld, int* off) {
+    if (!c || !byte_offset || !count) return UNET_ERR_INVALID;
+    if (!shape_ok(N, H, W)) return fail(c, UNET_ERR_SHAPE, "bad shape");
+    Plan p;
+    char* const base = (char*)(uintptr_t)4096;  // fake base: offsets only
+    make_plan(c, N, H, W, training != 0, base, p);
+    const void* q = nullptr;
+    int64_t n = 0;
+    int l = 1, o = 0;
+    if (kind <= 4) {
+        if (index < 0 || index >= NCONV) return UNET_ERR_INVALID;
+        const ConvL& L = c->conv[index];
+        const int C = L.cout;
+        if (kind == 0) {
+            q = p.y[index];
+            l = p.ldy[index];
+            o = p.offy[index];
+            n = p.P[L.level] * l;
+        } else {
+            q = kind == 1 ? p.scale[index] : kind == 2 ? p.shift[index] : kind == 3 ? p.mean[index] : p.invstd[index];
+            n = C;
+        }
+    } else {
+        if (index < 0 || index >= 4) return UNET_ERR_INVALID;
+        const int C = 64 << index;
+        if (kind == 5) {
+            q = p.pool[index];
+            n = p.P[index + 1] * C;
+            l = C;
+        } else if (kind == 6) {
+            q = p.cat[index];
+            n = p.P[index] * 2 * C;
+            l = 2 * C;
+        } else if (kind == 7) {
+            if (!training) return UNET_ERR_INVALID;
+            q = p.dcat[index];
+            n = p.P[index] * 2 * C;
+            l = 2 * C;
+        } else {
+            return UNET_ERR_INVALID;
+        }
+    }
+    *byte_offset = (int64_t)((const char*)q - base);
+    *count = n;
+    if (ld) *ld = l;
+    if (off) *off = o;
+    return UNET_OK;
+}
+
+}  // extern "C"

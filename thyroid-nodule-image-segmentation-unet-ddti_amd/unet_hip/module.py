@@ -1,0 +1,165 @@
+"""Drop-in ``UNet`` (models/model.py:5-73) whose forward/backward run on libunet_hip.so.
+
+The module keeps the reference's exact submodule tree (encoder1..4, middle, decoder3..1,
+final; Conv2d / ReLU / BatchNorm2d / ConvTranspose2d in the same Sequential slots), so
+
+* ``state_dict()`` keys, shapes and torch layouts are identical and checkpoints move
+  freely between this module and the reference (``main.py:141-142`` style loading);
+* construction consumes the torch RNG exactly like the reference, so ``set_seed(42)``
+  (utils/utils.py:47-51) gives the same initial weights.
+
+The submodules are never *executed*: on the first forward on a GPU the parameters and
+BN buffers are re-pointed into flat device arenas in the native table's order (one
+arena for parameters, one for running_mean|running_var, one int64 vector for
+num_batches_tracked) and the whole network runs as one native call.  Moving the module
+(``.to()``, ``.cuda()``) re-flattens lazily.  CPU tensors raise ``HipUnavailable``:
+there is no silent CPU fallback.
+"""
+import torch
+import torch.nn as nn
+
+from ._lib import HipUnavailable
+from .functional import UNetFunction
+from .runtime import UNetRuntime
+
+
+def _conv_block(cin, cout):
+    # models/model.py:33-43: Conv3x3(bias) -> ReLU -> BN -> Conv3x3 -> ReLU -> BN
+    layers = []
+    for a, b in ((cin, cout), (cout, cout)):
+        layers += [nn.Conv2d(a, b, kernel_size=3, padding=1), nn.ReLU(inplace=True), nn.BatchNorm2d(b)]
+    return nn.Sequential(*layers)
+
+
+def _upconv_block(cin, cout):
+    # models/model.py:45-51
+    return nn.Sequential(_conv_block(cin, cin // 2),
+                         nn.ConvTranspose2d(cin // 2, cout, kernel_size=2, stride=2))
+
+
+class _ArenaState:
+    """Flat device arenas shared by the module and the autograd function."""
+
+    def __init__(self, rt, params, param_arena, bn_arena, nbt_arena):
+        self.rt = rt
+        self.params = params            # [(Parameter, offset, shape)]
+        self.param_arena = param_arena
+        self.bn_arena = bn_arena
+        self.nbt_arena = nbt_arena
+        self.grad_arena = None
+
+    def grad_arena_for_backward(self):
+        # gradients are written with '=' semantics (zero_grad(set_to_none) is the reference's
+        # pattern, utils/trainer.py:81).  If .grad still aliases the arena (accumulation
+        # across backward calls), hand autograd a fresh arena so it can add.
+        if self.grad_arena is None:
+            self.grad_arena = torch.empty_like(self.param_arena)
+            return self.grad_arena
+        p0 = self.params[0][0]
+        if p0.grad is not None and p0.grad.data_ptr() == self.grad_arena.data_ptr():
+            return torch.empty_like(self.param_arena)
+        return self.grad_arena
+
+    def grad_views(self, arena):
+        return [arena[off:off + p.numel()].view(p.shape) for p, off, _ in self.params]
+
+
+class UNet(nn.Module):
+    def __init__(self, in_channels=1, out_channels=1):
+        super().__init__()
+        self.in_channels, self.out_channels = in_channels, out_channels
+        self.encoder1 = _conv_block(in_channels, 64)
+        self.encoder2 = _conv_block(64, 128)
+        self.encoder3 = _conv_block(128, 256)
+        self.encoder4 = _conv_block(256, 512)
+        self.middle = nn.Sequential(nn.MaxPool2d(kernel_size=2, stride=2), _conv_block(512, 1024),
+                                    nn.ConvTranspose2d(1024, 512, kernel_size=2, stride=2))
+        self.decoder3 = _upconv_block(1024, 256)
+        self.decoder2 = _upconv_block(512, 128)
+        self.decoder1 = _upconv_block(256, 64)
+        self.final = nn.Sequential(_conv_block(128, 64), nn.Conv2d(64, out_channels, kernel_size=1))
+        self._state = None
+
+    # ---------------------------------------------------------------- arenas
+    def _bn_modules(self):
+        return {n: m for n, m in self.named_modules() if isinstance(m, nn.BatchNorm2d)}
+
+    def _arenas_valid(self, rt):
+        st = self._state
+        if st is None or st.rt is not rt:
+            return False
+        base = st.param_arena.data_ptr()
+        for p, off, _ in st.params:
+            if p.data_ptr() != base + 4 * off or not p.is_contiguous() or p.device != st.param_arena.device:
+                return False
+        bns = self._bn_modules()
+        bbase = st.bn_arena.data_ptr()
+        for name, ch, off in rt.bn:
+            if bns[name].running_mean.data_ptr() != bbase + 4 * off:
+                return False
+        return True
+
+    def flatten_(self):
+        """Re-point parameters and BN buffers into flat device arenas (idempotent)."""
+        p0 = next(self.parameters())
+        dev = p0.device
+        if dev.type != "cuda":
+            raise HipUnavailable("models.model.UNet runs on the MI355X HIP path only; move it to a "
+                                 "GPU with .cuda() / .to('cuda') (no CPU fallback)")
+        rt = UNetRuntime.get(dev, self.in_channels, self.out_channels)
+        if self._arenas_valid(rt):
+            return self._state
+        named = dict(self.named_parameters())
+        table = [n for n, _, _ in rt.params]
+        if list(named.keys()) != table:
+            raise RuntimeError("parameter table mismatch between module and native graph")
+        arena = torch.empty(rt.n_param_floats, dtype=torch.float32, device=dev)
+        plist = []
+        with torch.no_grad():
+            for name, shape, off in rt.params:
+                p = named[name]
+                if tuple(p.shape) != tuple(shape):
+                    raise RuntimeError(f"{name}: shape {tuple(p.shape)} != native {shape}")
+                n = p.numel()
+                arena[off:off + n].copy_(p.detach().reshape(-1).to(dev, torch.float32))
+                p.data = arena[off:off + n].view(shape)
+                plist.append((p, off, shape))
+            bns = self._bn_modules()
+            bn_arena = torch.empty(rt.n_bn_floats, dtype=torch.float32, device=dev)
+            nbt = torch.zeros(len(rt.bn), dtype=torch.int64, device=dev)
+            for i, (name, ch, off) in enumerate(rt.bn):
+                m = bns[name]
+                bn_arena[off:off + ch].copy_(m.running_mean.reshape(-1).float())
+                bn_arena[off + ch:off + 2 * ch].copy_(m.running_var.reshape(-1).float())
+                nbt[i].copy_(m.num_batches_tracked.reshape(()))
+                m.running_mean = bn_arena[off:off + ch]
+                m.running_var = bn_arena[off + ch:off + 2 * ch]
+                m.num_batches_tracked = nbt[i]
+        self._state = _ArenaState(rt, plist, arena, bn_arena, nbt)
+        return self._state
+
+    def _apply(self, fn, *args, **kwargs):
+        self._state = None  # any device / dtype move invalidates the arenas
+        return super()._apply(fn, *args, **kwargs)
+
+    # ---------------------------------------------------------------- forward
+    def forward(self, x):
+        """models/model.py:53-73: (N, in_channels, H, W) fp32 -> logits (N, out_channels, H, W).
+        H and W must be multiples of 16 (four 2x2 pools)."""
+        st = self.flatten_()
+        if x.dim() != 4 or x.shape[1] != self.in_channels:
+            raise ValueError(f"expected (N, {self.in_channels}, H, W), got {tuple(x.shape)}")
+        if x.device != st.param_arena.device:
+            raise ValueError(f"input on {x.device}, model on {st.param_arena.device}")
+        x = x.contiguous().float()
+        need_grad = self.training and torch.is_grad_enabled() and any(
+            p.requires_grad for p, _, _ in st.params)
+        if need_grad:
+            return UNetFunction.apply(x, st, *[p for p, _, _ in st.params])
+        logits, _ = st.rt.forward(st.param_arena, st.bn_arena, st.nbt_arena, x,
+                                  training=self.training)
+        return logits
+
+    @property
+    def flat_params(self):
+        return self.flatten_().param_arena
