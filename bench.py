@@ -1,0 +1,212 @@
+#!/usr/bin/env python3
+"""Throughput of the HIP UNet training step (BASELINE.json metric).
+
+One step = zero_grad -> forward (models/model.py:53-73) -> BCEWithLogits + Dice
+(utils/trainer.py:85-90, ratios 1/1) -> backward -> AdamW (utils/trainer.py:41,92), on a
+synthetic bs=32 x 1x256x256 batch per GPU (BASELINE config 2; config 3 = 8 ranks x 32),
+inputs resident in HBM before the timed region.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU, RCCL)
+
+Prints ONE JSON line on rank 0.  ``value`` = images/s of the whole job (sum over ranks,
+time = max over ranks).  ``roofline`` is for the dominant kernel (most GPU time in the
+timed region), from per-launch HIP events recorded on the launch stream inside the
+library: achieved = algorithmic FLOP of its launches / their summed duration.
+``cpu_baseline`` times the CPU oracle (oracle/unet_ref_cpu.py, a torch-CPU restatement
+of the reference's step) on a bounded sample (bs=4) on rank 0 only.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(REPO, "thyroid-nodule-image-segmentation-unet-ddti_amd")
+for _p in (REPO, PKG):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md chip table, dense fp32 matrix
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=32, help="images per GPU")
+    ap.add_argument("--size", type=int, default=256)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--verbose", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(steps, size):
+    """Oracle step on the host CPU, bs=4 (BASELINE config 1 shape), median of `steps`."""
+    import torch
+    from oracle import unet_ref_cpu as O
+    from oracle import weights as Wt
+    threads = os.cpu_count() or 1
+    torch.set_num_threads(threads)
+    P = O.make_params(42)
+    B = O.init_buffers()
+    opt = O.AdamWState(P, lr=1e-5)
+    x = torch.from_numpy(Wt.make_input(21, 4, 1, size, size))
+    t = torch.from_numpy(Wt.make_target(21, 4, size, size))
+    O.train_step(P, B, opt, x, t)  # warm-up
+    ts = []
+    for _ in range(steps):
+        t0 = time.perf_counter()
+        O.train_step(P, B, opt, x, t)
+        ts.append(time.perf_counter() - t0)
+    ts.sort()
+    med = ts[len(ts) // 2]
+    cpu_model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu_model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": round(4 / med, 4), "unit": "images/sec", "cores": threads, "kind": "port",
+            "sample": f"oracle/unet_ref_cpu.py train step (fwd+BCE+Dice+bwd+AdamW), bs=4, "
+                      f"1x{size}x{size}, median of {steps} steps after 1 warm-up, "
+                      f"torch CPU {threads} threads, {cpu_model}"}
+
+
+def load_pmc(kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary, if any."""
+    path = os.path.join(REPO, "profiles", "pmc_summary.json")
+    try:
+        d = json.load(open(path))
+        return d.get("kernels", {}).get(kernel, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    dev = torch.device(f"cuda:{local}")
+    torch.cuda.set_device(dev)
+
+    import unet_hip
+    from unet_hip.dist import DistributedUNet
+    from oracle import unet_ref_cpu as O  # analytic FLOP count only
+
+    torch.manual_seed(42)
+    model = unet_hip.UNet(1, 1).to(dev).train()
+    opt = unet_hip.HipAdamW(model.parameters(), lr=1e-5)
+    ddp = DistributedUNet(model, opt) if world > 1 else None
+
+    g = torch.Generator(device="cpu").manual_seed(1000 + rank)
+    B, S = args.batch, args.size
+    x = torch.rand(B, 1, S, S, generator=g).to(dev)
+    t = (torch.rand(B, 1, S, S, generator=g) > 0.5).float().to(dev)
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        logits = model(x)
+        losses = unet_hip.seg_losses(logits, t)
+        loss = losses[0] + losses[1]
+        loss.backward()
+        if ddp is not None:
+            ddp.reduce_gradients()
+        opt.step()
+        return loss
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    rt = model._state.rt
+    rt.timing(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    recs = rt.timing_records()
+    rt.timing(False)
+    if world > 1:
+        te = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(te, op=dist.ReduceOp.MAX)
+        elapsed = te.item()
+    if not torch.isfinite(loss).item():
+        raise RuntimeError("non-finite loss")
+
+    images = B * world * args.steps
+    value = images / elapsed
+    ms = 1000 * elapsed / args.steps
+
+    # per-kernel aggregation (label = family/kernel instance)
+    fam, kern = {}, {}
+    for label, t_ms, flop in recs:
+        f, _, k = label.partition("/")
+        for d, key in ((fam, f), (kern, k or f)):
+            e = d.setdefault(key, [0, 0.0, 0.0])
+            e[0] += 1
+            e[1] += t_ms
+            e[2] += flop
+    dom = max(kern, key=lambda k: kern[k][1])
+    n_l, t_l, f_l = kern[dom]
+    achieved = f_l / (t_l * 1e-3) / 1e12 if t_l > 0 else 0.0
+    per_launch_flop = f_l / n_l
+    pmc = load_pmc(dom)
+    conv_flop = O.train_flops_per_image(S, S) * B
+    roofline = {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 3),
+                "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
+                "traffic": pmc, "launches": n_l, "avg_launch_ms": round(t_l / n_l, 4),
+                "flop_per_launch": per_launch_flop,
+                "kernel_share_of_gpu_time": round(t_l / max(1e-9, sum(v[1] for v in kern.values())), 4),
+                "step_conv_tflops": round(conv_flop / (ms * 1e-3) / 1e12, 3),
+                "step_conv_frac": round(conv_flop / (ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4)}
+
+    out = {"metric": "images/sec fwd+bwd, UNet 256x256x1 bs=32/GPU (Dice+BCE, AdamW)",
+           "value": round(value, 3), "unit": "images/sec", "n_gpus": world, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
+           "config": {"workload": f"models/model.py UNet depth-4 base-64, 1x{S}x{S}, bs={B}/GPU, "
+                                  f"fwd+BCE+Dice+bwd+AdamW (BASELINE config {'2' if world == 1 else '3'})",
+                      "model": "UNet(in=1,out=1) 31,042,369 params", "global_batch": B * world,
+                      "image": [1, S, S], "parallelism": f"dp{world}"},
+           "roofline": roofline}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args.cpu_steps, S)
+    elif rank == 0:
+        out["cpu_baseline"] = None
+    if rank == 0:
+        if args.verbose:
+            for k, (n, tm, fl) in sorted(fam.items(), key=lambda kv: -kv[1][1]):
+                tf = fl / (tm * 1e-3) / 1e12 if tm > 0 and fl > 0 else 0
+                print(f"  {k:22s} n={n:5d} {tm / args.steps:9.3f} ms/step  {tf:7.2f} TF/s",
+                      file=sys.stderr)
+            for k, (n, tm, fl) in sorted(kern.items(), key=lambda kv: -kv[1][1])[:8]:
+                print(f"  [{k}] n={n} {tm / args.steps:.3f} ms/step", file=sys.stderr)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -83,8 +83,13 @@ __global__ __launch_bounds__(256, 2) void rowgemm_kernel(RowGemmArgs p) {
 
     const int lrow = tid / F4R, lc4 = tid % F4R;
     Pix rq[AP];
+    bool rok[AP];  // row inside M (the last M tile may be partial)
 #pragma unroll
-    for (int i = 0; i < AP; ++i) rq[i] = decode(m0 + lrow + i * RPP, H, W);
+    for (int i = 0; i < AP; ++i) {
+        const int m = m0 + lrow + i * RPP;
+        rok[i] = m < p.M;
+        rq[i] = decode(rok[i] ? m : p.M - 1, H, W);
+    }
 
     f32x4 ra[AP], rb[BP];
     const bool affine = p.ascale != nullptr;
@@ -101,11 +106,11 @@ __global__ __launch_bounds__(256, 2) void rowgemm_kernel(RowGemmArgs p) {
 #pragma unroll
         for (int i = 0; i < AP; ++i) {
             bool valid;
-            const int m = m0 + lrow + i * RPP;
+            const int m = rok[i] ? m0 + lrow + i * RPP : p.M - 1;
             const int src = gather_src(p.amode, tap, m, rq[i], H, W, valid);
             f32x4 v = *(const f32x4*)(p.a + (size_t)src * p.lda + p.aoff + c);
             if (affine) v = v * sc + sh;
-            ra[i] = valid ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+            ra[i] = (valid && rok[i]) ? v : f32x4{0.f, 0.f, 0.f, 0.f};
         }
 #pragma unroll
         for (int i = 0; i < BP; ++i)
@@ -171,10 +176,12 @@ __global__ __launch_bounds__(256, 2) void rowgemm_kernel(RowGemmArgs p) {
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     const int m = m0 + wm * WM + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-                    float v = fmaxf(acc[mt][nt][r] + b, 0.f);
-                    p.out[(size_t)m * p.ldo + p.ooff + n] = v;
-                    s1[nt] += v;
-                    s2[nt] += v * v;
+                    if (m < p.M) {
+                        float v = fmaxf(acc[mt][nt][r] + b, 0.f);
+                        p.out[(size_t)m * p.ldo + p.ooff + n] = v;
+                        s1[nt] += v;
+                        s2[nt] += v * v;
+                    }
                 }
             s1[nt] += __shfl_xor(s1[nt], 32);
             s2[nt] += __shfl_xor(s2[nt], 32);
@@ -211,6 +218,7 @@ __global__ __launch_bounds__(256, 2) void rowgemm_kernel(RowGemmArgs p) {
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     const int m = m0 + wm * WM + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                    if (m >= p.M) continue;
                     const Pix q = decode(m, H, W);
                     const size_t op = (size_t)(q.img * 2 * H + 2 * q.y + a) * (2 * W) + 2 * q.x + b;
                     p.out[op * p.ldo + p.ooff + co] = acc[mt][nt][r] + bb;
@@ -225,7 +233,7 @@ __global__ __launch_bounds__(256, 2) void rowgemm_kernel(RowGemmArgs p) {
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     const int m = m0 + wm * WM + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-                    p.out[(size_t)m * p.ldo + p.ooff + n] = acc[mt][nt][r];
+                    if (m < p.M) p.out[(size_t)m * p.ldo + p.ooff + n] = acc[mt][nt][r];
                 }
         }
     }
@@ -267,26 +275,30 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
     const int pbeg = split * p.pps;
     int pend = pbeg + p.pps;
     if (pend > p.P) pend = p.P;
-    const int nchunks = (pend - pbeg) / BKP;
+    const int nchunks = (pend - pbeg + BKP - 1) / BKP;
 
     f32x4 ra[AP], rb[BP];
     auto load_chunk = [&](int pc) {
 #pragma unroll
         for (int i = 0; i < AP; ++i) {
-            const int m = pc + arow + i * ARPP;
+            int m = pc + arow + i * ARPP;
+            const bool in = m < pend;
+            m = in ? m : pend - 1;
             bool valid;
             const int src = gather_src(p.amode, tapA, m, decode(m, H, W), H, W, valid);
             f32x4 v = *(const f32x4*)(p.a + (size_t)src * p.lda + p.aoff + ca0 + ac4 * 4);
             if (affine) v = v * sc + sh;
-            ra[i] = valid ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+            ra[i] = (valid && in) ? v : f32x4{0.f, 0.f, 0.f, 0.f};
         }
 #pragma unroll
         for (int i = 0; i < BP; ++i) {
-            const int m = pc + brow + i * BRPP;
+            int m = pc + brow + i * BRPP;
+            const bool in = m < pend;
+            m = in ? m : pend - 1;
             bool valid;
             const int src = gather_src(p.bmode, tapB, m, decode(m, H, W), H, W, valid);
             f32x4 v = *(const f32x4*)(p.b + (size_t)src * p.ldb + p.boff + cb0 + bc4 * 4);
-            rb[i] = valid ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+            rb[i] = (valid && in) ? v : f32x4{0.f, 0.f, 0.f, 0.f};
         }
     };
     auto store_chunk = [&]() {
@@ -351,10 +363,10 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
 
 int launch_rowgemm(const RowGemmArgs& a, int bm, int bn, hipStream_t s) {
     constexpr int BK = 32;
-    if (a.M % bm || a.N % bn || a.K % BK || a.C % BK || a.K != gather_taps(a.amode) * a.C)
+    if (a.M < 1 || a.N % bn || a.K % BK || a.C % BK || a.K != gather_taps(a.amode) * a.C)
         return -1;
     if (a.emode == E_CONVT && (a.cout % bn)) return -1;
-    dim3 grid((a.M / bm) * (a.N / bn)), block(256);
+    dim3 grid(((a.M + bm - 1) / bm) * (a.N / bn)), block(256);
     if (bm == 128 && bn == 128)
         hipLaunchKernelGGL((rowgemm_kernel<128, 128, BK, 64, 64>), grid, block, 0, s, a);
     else if (bm == 128 && bn == 64)
@@ -366,7 +378,7 @@ int launch_rowgemm(const RowGemmArgs& a, int bm, int bn, hipStream_t s) {
 
 int launch_wgrad(const WgradArgs& a, int bm, int bn, hipStream_t s) {
     constexpr int BKP = 32;
-    if (a.Mw % bm || a.Nw % bn || a.CA % bm || a.CB % bn || a.P % BKP || a.pps % BKP) return -1;
+    if (a.Mw % bm || a.Nw % bn || a.CA % bm || a.CB % bn || a.P < 1 || a.pps % BKP) return -1;
     dim3 grid((a.Mw / bm) * (a.Nw / bn) * a.splits), block(256);
     if (bm == 128 && bn == 128)
         hipLaunchKernelGGL((wgrad_kernel<128, 128, BKP, 64, 64>), grid, block, 0, s, a);

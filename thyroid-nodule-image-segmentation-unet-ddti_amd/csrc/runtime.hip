@@ -254,6 +254,7 @@ WgradCfg wgrad_cfg(int CA, int tapsA, int CB, int tapsB, int64_t P) {
     const int64_t tiles = (int64_t)(tapsA * CA / w.bm) * (tapsB * CB / w.bn);
     int64_t s = (2048 + tiles - 1) / tiles;
     const int64_t maxs = P / 256 > 0 ? P / 256 : 1;  // keep >= 8 pixel chunks per split
+    // (P need not be a multiple of the 32-pixel chunk: the kernel zero-fills the tail)
     if (s > maxs) s = maxs;
     if (s < 1) s = 1;
     int64_t pps = (P + s - 1) / s;
@@ -302,7 +303,7 @@ void make_plan(unet_ctx* c, int N, int H, int W, bool training, char* base, Plan
     // BN-stat partials: rows = M / 128 of the row GEMM, or RED_G for the first conv
     int64_t srows = 0;
     for (int i = 0; i < NCONV; ++i) {
-        const int64_t r = std::max<int64_t>(p.P[c->conv[i].level] / 128, RED_G);
+        const int64_t r = std::max<int64_t>((p.P[c->conv[i].level] + 127) / 128, RED_G);
         srows = std::max(srows, r * 2 * c->conv[i].cout);
     }
     p.stats = b.take<float>(srows);
@@ -351,7 +352,7 @@ struct Launcher {
         return c->ev_pool[c->ev_used++];
     }
     template <class F>
-    int run(const char* label, double flop, F&& f) {
+    int run(const std::string& label, double flop, F&& f) {
         hipEvent_t a = nullptr, b = nullptr;
         if (c->timing) {
             a = ev();
@@ -359,7 +360,7 @@ struct Launcher {
             (void)hipEventRecord(a, s);
         }
         int r = f();
-        if (r != 0) return fail(c, UNET_ERR_HIP, "%s: launch failed (%d: %s)", label, r,
+        if (r != 0) return fail(c, UNET_ERR_HIP, "%s: launch failed (%d: %s)", label.c_str(), r,
                                 r > 0 ? hipGetErrorString((hipError_t)r) : "bad shape");
         if (c->timing) {
             (void)hipEventRecord(b, s);
@@ -368,6 +369,13 @@ struct Launcher {
         return 0;
     }
 };
+
+// timing label "family/kernel-instance" (the instance is what rocprofv3 reports)
+std::string glabel(const char* fam, const char* kern, int bm, int bn) {
+    char b[96];
+    snprintf(b, sizeof b, "%s/%s_%dx%d", fam, kern, bm, bn);
+    return b;
+}
 
 #define RUN(label, flop, expr)                            \
     do {                                                  \
@@ -483,8 +491,9 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
             g.stats = p.stats;
             g.emode = E_BIAS_RELU_STATS;
             const int bn = C.cout % 128 == 0 ? 128 : 64;
-            R = (int)(M / 128);
-            RUN("conv_fwd", 2.0 * M * C.cout * 9 * C.cin, launch_rowgemm(g, 128, bn, s));
+            R = (int)((M + 127) / 128);
+            RUN(glabel("conv_fwd", "rowgemm", 128, bn), 2.0 * M * C.cout * 9 * C.cin,
+                launch_rowgemm(g, 128, bn, s));
         }
         return stats_finalize(c, L, p, i, R, M, training, prm, bn_run, bn_cnt);
     };
@@ -513,7 +522,8 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
         g.cout = T.cout;
         g.emode = E_CONVT;
         const int bn = T.cout % 128 == 0 ? 128 : 64;
-        RUN("convT_fwd", 2.0 * g.M * g.N * g.K, launch_rowgemm(g, 128, bn, s));
+        RUN(glabel("convT_fwd", "rowgemm", 128, bn), 2.0 * g.M * g.N * g.K,
+            launch_rowgemm(g, 128, bn, s));
         return 0;
     };
 
@@ -597,7 +607,8 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         w.pps = wc.pps;
         w.splits = wc.splits;
         w.slab = p.slab;
-        RUN("conv_wgrad", 2.0 * P * C.cout * 9 * C.cin, launch_wgrad(w, wc.bm, wc.bn, s));
+        RUN(glabel("conv_wgrad", "wgrad", wc.bm, wc.bn), 2.0 * P * C.cout * 9 * C.cin,
+            launch_wgrad(w, wc.bm, wc.bn, s));
         RUN("wgrad_reduce", 0,
             k_slab_reduce(p.slab, wc.splits, w.Mw, w.Nw, 0, C.cin, C.cout, grads + C.w, s));
         if (dx) {
@@ -618,7 +629,8 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
             g.ooff = 0;
             g.emode = E_STORE;
             const int bn = C.cin % 128 == 0 ? 128 : 64;
-            RUN("conv_dgrad", 2.0 * P * C.cout * 9 * C.cin, launch_rowgemm(g, 128, bn, s));
+            RUN(glabel("conv_dgrad", "rowgemm", 128, bn), 2.0 * P * C.cout * 9 * C.cin,
+                launch_rowgemm(g, 128, bn, s));
         }
         return 0;
     };
@@ -654,7 +666,8 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         w.pps = wc.pps;
         w.splits = wc.splits;
         w.slab = p.slab;
-        RUN("convT_wgrad", 2.0 * Pin * T.cin * 4 * T.cout, launch_wgrad(w, wc.bm, wc.bn, s));
+        RUN(glabel("convT_wgrad", "wgrad", wc.bm, wc.bn), 2.0 * Pin * T.cin * 4 * T.cout,
+            launch_wgrad(w, wc.bm, wc.bn, s));
         RUN("wgrad_reduce", 0,
             k_slab_reduce(p.slab, wc.splits, w.Mw, w.Nw, 1, T.cin, T.cout, grads + T.w, s));
         RowGemmArgs g{};
@@ -674,7 +687,8 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         g.ooff = 0;
         g.emode = E_STORE;
         const int bn = T.cin % 128 == 0 ? 128 : 64;
-        RUN("convT_dgrad", 2.0 * Pin * T.cin * 4 * T.cout, launch_rowgemm(g, 128, bn, s));
+        RUN(glabel("convT_dgrad", "rowgemm", 128, bn), 2.0 * Pin * T.cin * 4 * T.cout,
+            launch_rowgemm(g, 128, bn, s));
         return 0;
     };
     auto bucket_done = [&](int b) {
