@@ -117,9 +117,10 @@ int unet_adamw(unet_ctx* ctx, float* params, const float* grads, float* exp_avg,
                float* exp_avg_sq, int64_t n, int step, float lr, float beta1, float beta2,
                float eps, float weight_decay, float grad_scale, unet_stream_t stream);
 
-/* Mask readout + confusion counts: counts (device int64[4]) += {TP, FP, FN, TN} of
- * (sigmoid(logits) > 0.5) vs (targets cast to uint8 == 1), utils/trainer.py:217-242.
- * mask (optional, may be null): uint8 (N,C,H,W). */
+/* Mask readout + confusion counts, utils/trainer.py:101-107,217-242, utils/utils.py:225-251.
+ * counts (device int64[6]) += {TP, FP, FN, TN} of (sigmoid(logits) > 0.5) vs targets cast to
+ * an integer (== 1 is positive), then {|pred AND t!=0|, |pred OR t!=0|} (the bool cast of
+ * calculate_iou).  mask (optional, may be null): uint8 (N,C,H,W). */
 int unet_mask_counts(unet_ctx* ctx, const float* logits, const float* targets, int64_t n,
                      uint8_t* mask, int64_t* counts, unet_stream_t stream);
 

@@ -224,12 +224,14 @@ def test_mask_counts():
     x = torch.randn(3, 1, 64, 48, generator=g).to(DEV)
     t = (torch.rand(3, 1, 64, 48, generator=g) > 0.6).float().to(DEV)
     rt = unet_hip.UNetRuntime.get(DEV)
-    counts = torch.zeros(4, dtype=torch.int64, device=DEV)
+    counts = torch.zeros(6, dtype=torch.int64, device=DEV)
     mask = torch.empty(x.shape, dtype=torch.uint8, device=DEV)
     rt.mask_counts(x, t, counts, mask)
     pm = (torch.sigmoid(x) > 0.5)
     tm = t.to(torch.uint8) == 1
-    want = [int((pm & tm).sum()), int((pm & ~tm).sum()), int((~pm & tm).sum()), int((~pm & ~tm).sum())]
+    tb = t != 0
+    want = [int((pm & tm).sum()), int((pm & ~tm).sum()), int((~pm & tm).sum()), int((~pm & ~tm).sum()),
+            int((pm & tb).sum()), int((pm | tb).sum())]
     assert counts.cpu().tolist() == want
     assert torch.equal(mask.bool(), pm)
 

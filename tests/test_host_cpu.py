@@ -1,0 +1,73 @@
+"""Host-side mirror modules (no GPU): metrics-from-counts == the reference's array metrics,
+transforms, synthetic data, CLI parsing, loss-module plumbing."""
+import numpy as np
+import pytest
+import torch
+
+
+def _counts(pred, target):
+    p = pred.astype(bool)
+    ti = target.astype(np.uint8)
+    tb = target != 0
+    return [int((p & (ti == 1)).sum()), int((p & (ti == 0)).sum()), int((~p & (ti == 1)).sum()),
+            int((~p & (ti == 0)).sum()), int((p & tb).sum()), int((p | tb).sum())]
+
+
+@pytest.mark.parametrize("soft", [False, True])
+def test_metrics_from_counts_match_array_metrics(soft):
+    from utils.utils import (calculate_acc, calculate_iou, calculate_precision_recall_f1,
+                             metrics_from_counts)
+    rng = np.random.default_rng(0)
+    pred = (rng.random((4, 1, 32, 32)) > 0.5).astype(np.uint8)
+    target = (rng.random((4, 1, 32, 32)) > 0.6).astype(np.float32)
+    if soft:  # mixup soft labels (utils/trainer.py:77-78)
+        target = 0.3 * target + 0.7 * (rng.random(target.shape) > 0.5)
+    acc, p, r, f1, iou = metrics_from_counts(_counts(pred, target))
+    assert acc == pytest.approx(calculate_acc(pred, target))
+    pp, rr, ff = calculate_precision_recall_f1(pred, target)
+    assert (p, r, f1) == pytest.approx((pp, rr, ff))
+    assert iou == pytest.approx(calculate_iou(pred, target))
+
+
+def test_global_metrics():
+    from utils.utils import global_metrics_from_counts
+    m = global_metrics_from_counts([10, 5, 3, 82])
+    assert m["IoU"] == pytest.approx(10 / 18, rel=1e-6)
+    assert m["F1"] == pytest.approx(2 * (10 / 15) * (10 / 13) / (10 / 15 + 10 / 13), rel=1e-6)
+
+
+def test_transforms_and_synthetic():
+    from PIL import Image
+    from data.data_loader import SyntheticSegmentation
+    from utils.transforms import Compose, Resize, ToTensor
+    img = Image.fromarray((np.arange(40 * 30) % 256).astype(np.uint8).reshape(40, 30))
+    mask = Image.fromarray(((np.arange(40 * 30) % 7) == 0).astype(np.uint8).reshape(40, 30) * 255)
+    a, m = Compose([Resize((64, 48)), ToTensor()])(img, mask)
+    assert a.shape == (1, 64, 48) and m.shape == (1, 64, 48)
+    assert 0 <= a.min() and a.max() <= 1 and set(torch.unique(m).tolist()) <= {0.0, 1.0}
+    ds = SyntheticSegmentation(3, 64)
+    x, y = ds[1]
+    assert x.shape == (1, 64, 64) and y.shape == (1, 64, 64) and y.sum() > 0
+    assert torch.equal(ds[1][0], x)
+
+
+def test_cli_flags_match_reference():
+    import main
+    a = main.get_parser([])
+    for k, v in dict(bce_ratio=1, dice_ratio=0, focal_ratio=1, boundary_ratio=0, lr=1e-5,
+                     batch_size=16, epochs=10000, mixup_alpha=0.2, mixup_prob=0.3,
+                     early_stop_patience=50, use_data_parallel=True, use_amp_autocast=False).items():
+        assert getattr(a, k) == v, k
+
+
+def test_boundary_loss_matches_reference_formula():
+    import scipy.ndimage as nd
+    from models.loss import BoundaryLoss
+    rng = np.random.default_rng(1)
+    x = torch.from_numpy(rng.standard_normal((2, 1, 16, 16)).astype(np.float32))
+    t = torch.from_numpy((rng.random((2, 1, 16, 16)) > 0.7).astype(np.float32))
+    ref = 0.0
+    for b in range(2):
+        d = torch.from_numpy(nd.distance_transform_edt(1 - t[b, 0].numpy().astype(np.uint8))).float()
+        ref += torch.mean(torch.abs(torch.sigmoid(x[b, 0]) - t[b, 0]) * d)
+    assert float(BoundaryLoss()(x, t)) == pytest.approx(float(ref / 2), rel=1e-6)

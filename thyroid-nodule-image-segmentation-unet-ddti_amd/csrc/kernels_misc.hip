@@ -159,6 +159,47 @@ __global__ void reduce_rows_kernel(const float* __restrict__ in, int R, int ncol
     out[(int64_t)g * ncols + c] = s;
 }
 
+// Column sums of G partial rows for the 64 columns of this block: thread (cx, ry) sums rows
+// ry, ry+16, ... (8 loads in flight), then the 16 row groups are added in fixed order.
+// Returns the column total in threads ry == 0 (others return 0).  blockDim = (64, 16).
+template <int NQ>
+__device__ void colsum16(const float* __restrict__ part, int G, int stride, int qstride, int col,
+                         bool ok, double (&out)[NQ]) {
+    __shared__ double red[NQ][16][64];
+    const int cx = threadIdx.x, ry = threadIdx.y;
+    double acc[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) acc[q] = 0.0;
+    if (ok) {
+        int g = ry;
+        for (; g + 16 * 7 < G; g += 16 * 8) {
+            float v[NQ][8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+#pragma unroll
+                for (int q = 0; q < NQ; ++q)
+                    v[q][u] = part[(int64_t)(g + 16 * u) * stride + q * qstride + col];
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) acc[q] += v[q][u];
+        }
+        for (; g < G; g += 16)
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) acc[q] += part[(int64_t)g * stride + q * qstride + col];
+    }
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) red[q][ry][cx] = acc[q];
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        double t = 0.0;
+        if (ry == 0)
+            for (int k = 0; k < 16; ++k) t += red[q][k][cx];
+        out[q] = t;
+    }
+}
+
 // BatchNorm2d train finalisation (torch/nn/modules/batchnorm.py semantics): batch mean,
 // biased var for normalisation, running stats r = (1-m) r + m * stat with unbiased var.
 // Emits the fused affine (scale, shift) consumers apply in their load path, and keeps
@@ -170,14 +211,13 @@ __global__ void bn_finalize_train_kernel(const float* __restrict__ part, int G, 
                                          float* __restrict__ scale, float* __restrict__ shift,
                                          float* __restrict__ mean_out,
                                          float* __restrict__ invstd_out) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    const int c = blockIdx.x * 64 + threadIdx.x;
+    double sq[2];
+    colsum16<2>(part, G, 2 * C, C, c, c < C, sq);
+    if (threadIdx.y != 0) return;
     if (c == 0 && nbt) *nbt += 1;
     if (c >= C) return;
-    double s = 0.0, q = 0.0;
-    for (int g = 0; g < G; ++g) {
-        s += part[(int64_t)g * 2 * C + c];
-        q += part[(int64_t)g * 2 * C + C + c];
-    }
+    const double s = sq[0], q = sq[1];
     const double mean = s / count;
     double var = q / count - mean * mean;
     if (var < 0) var = 0;
@@ -312,13 +352,11 @@ __global__ void bn_bwd_finalize_kernel(const float* __restrict__ part, int G, in
                                        const float* __restrict__ mean,
                                        const float* __restrict__ invstd, float* __restrict__ coef,
                                        float* __restrict__ dgamma, float* __restrict__ dbeta) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= C) return;
-    double s1 = 0.0, s2 = 0.0;
-    for (int g = 0; g < G; ++g) {
-        s1 += part[(int64_t)g * 2 * C + c];
-        s2 += part[(int64_t)g * 2 * C + C + c];
-    }
+    const int c = blockIdx.x * 64 + threadIdx.x;
+    double ss[2];
+    colsum16<2>(part, G, 2 * C, C, c, c < C, ss);
+    if (threadIdx.y != 0 || c >= C) return;
+    const double s1 = ss[0], s2 = ss[1];
     const double is = invstd[c], mu = mean[c];
     const double sdxh = is * (s2 - mu * s1);  // sum do * xhat
     const double k = (double)gamma[c] * is;
@@ -380,11 +418,10 @@ __global__ __launch_bounds__(256) void chan_sum_kernel(const float* __restrict__
 // out[c] = sum over G partial rows (fixed order), optional scatter stride
 __global__ void sum_partials_kernel(const float* __restrict__ part, int G, int ncols,
                                     float* __restrict__ out) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= ncols) return;
-    float s = 0.f;
-    for (int g = 0; g < G; ++g) s += part[(int64_t)g * ncols + c];
-    out[c] = s;
+    const int c = blockIdx.x * 64 + threadIdx.x;
+    double s[1];
+    colsum16<1>(part, G, ncols, 0, c, c < ncols, s);
+    if (threadIdx.y == 0 && c < ncols) out[c] = (float)s[0];
 }
 
 // Sum the split-K slabs of a wgrad and scatter into the torch weight layout.
@@ -413,10 +450,11 @@ __global__ void slab_reduce_kernel(const float* __restrict__ slab, int S, int Mw
 // conv-first wgrad partials [G][10][C] -> grad w[co][0][tap], b[co]
 __global__ void conv_first_wgrad_finalize_kernel(const float* __restrict__ part, int G, int C,
                                                  float* __restrict__ gw, float* __restrict__ gb) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= 10 * C) return;
-    float s = 0.f;
-    for (int g = 0; g < G; ++g) s += part[(int64_t)g * 10 * C + i];
+    const int i = blockIdx.x * 64 + threadIdx.x;
+    double sv[1];
+    colsum16<1>(part, G, 10 * C, 0, i, i < 10 * C, sv);
+    if (threadIdx.y != 0 || i >= 10 * C) return;
+    const float s = (float)sv[0];
     const int tap = i / C, c = i - tap * C;
     if (tap < 9)
         gw[c * 9 + tap] = s;
@@ -620,11 +658,15 @@ __global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
     }
 }
 
-// sigmoid(x) > 0.5 masks + confusion counts vs targets cast to uint8 (utils/trainer.py:217-242)
+// sigmoid(x) > 0.5 masks + confusion counts (utils/trainer.py:101-107,217-242):
+//   counts[0..3] = TP, FP, FN, TN with targets cast to an integer (astype(int)/astype(uint8):
+//                  only t == 1 is positive, utils/utils.py:233-251, trainer.py:220)
+//   counts[4..5] = |pred & t!=0|, |pred | t!=0| (astype(bool), calculate_iou utils.py:225-231)
+// Integer counts: atomics are exact, the result is deterministic.
 __global__ void mask_counts_kernel(const float* __restrict__ x, const float* __restrict__ t,
                                    int64_t n, uint8_t* __restrict__ mask,
                                    unsigned long long* __restrict__ counts) {
-    unsigned long long c[4] = {0, 0, 0, 0};
+    unsigned long long c[6] = {0, 0, 0, 0, 0, 0};
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * blockDim.x) {
         const bool pr = sigmoidf_(x[i]) > 0.5f;
@@ -636,8 +678,10 @@ __global__ void mask_counts_kernel(const float* __restrict__ x, const float* __r
         c[1] += pr && neg;
         c[2] += !pr && pos;
         c[3] += !pr && neg;
+        c[4] += pr && (tv != 0.f);
+        c[5] += pr || (tv != 0.f);
     }
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < 6; ++k) {
         unsigned long long s = c[k];
         for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d);
         if ((threadIdx.x & 63) == 0 && s) atomicAdd(counts + k, s);
@@ -689,7 +733,7 @@ int k_conv_first_wgrad(const float* x, const float* dz, int P, int H, int W, int
                        int G, float* gw, float* gb, hipStream_t s) {
     hipLaunchKernelGGL(conv_first_wgrad_kernel, dim3(G), dim3(256), 0, s, x, dz, P, H, W, C, partial);
     HIP_OK(hipGetLastError());
-    hipLaunchKernelGGL(conv_first_wgrad_finalize_kernel, dim3((10 * C + 255) / 256), dim3(256), 0,
+    hipLaunchKernelGGL(conv_first_wgrad_finalize_kernel, dim3((10 * C + 63) / 64), dim3(64, 16), 0,
                        s, partial, G, C, gw, gb);
     LAUNCH_CHECK();
 }
@@ -702,7 +746,7 @@ int k_bn_finalize_train(const float* part, int G, int C, double count, const flo
                         const float* beta, float* rmean, float* rvar, int64_t* nbt, float momentum,
                         float eps, float* scale, float* shift, float* mean, float* invstd,
                         hipStream_t s) {
-    hipLaunchKernelGGL(bn_finalize_train_kernel, dim3((C + 255) / 256), dim3(256), 0, s, part, G,
+    hipLaunchKernelGGL(bn_finalize_train_kernel, dim3((C + 63) / 64), dim3(64, 16), 0, s, part, G,
                        C, count, gamma, beta, rmean, rvar, nbt, momentum, eps, scale, shift, mean,
                        invstd);
     LAUNCH_CHECK();
@@ -736,7 +780,7 @@ int k_bn_bwd_reduce(const float* dout, const float* y, int ld, int off, int P, i
 int k_bn_bwd_finalize(const float* part, int G, int C, double count, const float* gamma,
                       const float* mean, const float* invstd, float* coef, float* dgamma,
                       float* dbeta, hipStream_t s) {
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, part, G, C,
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(64, 16), 0, s, part, G, C,
                        count, gamma, mean, invstd, coef, dgamma, dbeta);
     LAUNCH_CHECK();
 }
@@ -752,7 +796,7 @@ int k_chan_sum(const float* v, int ld, int off, int P, int C, float* partial, in
     LAUNCH_CHECK();
 }
 int k_sum_partials(const float* part, int G, int ncols, float* out, hipStream_t s) {
-    hipLaunchKernelGGL(sum_partials_kernel, dim3((ncols + 255) / 256), dim3(256), 0, s, part, G,
+    hipLaunchKernelGGL(sum_partials_kernel, dim3((ncols + 63) / 64), dim3(64, 16), 0, s, part, G,
                        ncols, out);
     LAUNCH_CHECK();
 }

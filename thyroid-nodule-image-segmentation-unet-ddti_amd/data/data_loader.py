@@ -1,0 +1,60 @@
+"""Data loading (mirror of the reference's data/data_loader.py).
+
+``MedicalDataset(img_dir, mask_dir, transform)`` pairs ``<name>.jpg`` with
+``<stem>_mask.jpg`` exactly like the reference (:9-27); ``create_dataloader`` is the same
+plain DataLoader (:29-33).  ``SyntheticSegmentation`` provides device-free synthetic
+batches (images in [0, 1), binary nodule-like disc masks) for benchmarks and tests, since
+the DDTI data is not distributed with the code.
+"""
+import os
+from pathlib import Path
+
+import numpy as np
+import torch
+from torch.utils.data import DataLoader, Dataset
+
+
+class MedicalDataset(Dataset):
+    def __init__(self, img_dir, mask_dir, transform=None):
+        self.img_dir, self.mask_dir, self.transform = img_dir, mask_dir, transform
+        self.img_names = [p.name for p in Path(img_dir).rglob("*")]
+        self.mask_names = [n.split(".jpg")[0] + "_mask.jpg" for n in self.img_names]
+
+    def __len__(self):
+        return len(self.img_names)
+
+    def __getitem__(self, idx):
+        from PIL import Image
+        img = Image.open(os.path.join(self.img_dir, self.img_names[idx]))
+        mask = Image.open(os.path.join(self.mask_dir, self.mask_names[idx]))
+        if self.transform:
+            img, mask = self.transform(img, mask)
+        return img, mask
+
+
+class SyntheticSegmentation(Dataset):
+    """n samples of (1, H, W) float images in [0, 1) and {0, 1} masks of 1-3 discs."""
+
+    def __init__(self, n, size=256, seed=0):
+        self.n, self.size, self.seed = n, size, seed
+
+    def __len__(self):
+        return self.n
+
+    def __getitem__(self, idx):
+        rng = np.random.default_rng(self.seed * 1_000_003 + idx)
+        S = self.size
+        img = rng.random((1, S, S), dtype=np.float32)
+        yy, xx = np.mgrid[0:S, 0:S]
+        m = np.zeros((S, S), bool)
+        for _ in range(rng.integers(1, 4)):
+            cy, cx = rng.random(2) * S
+            r = (0.08 + 0.17 * rng.random()) * S
+            m |= (yy - cy) ** 2 + (xx - cx) ** 2 <= r * r
+        img[0][m] = 0.5 * img[0][m] + 0.4  # brighter nodule
+        return torch.from_numpy(img), torch.from_numpy(m[None].astype(np.float32))
+
+
+def create_dataloader(dataset, config, shuffle):
+    return DataLoader(dataset=dataset, batch_size=config.batch_size, shuffle=shuffle,
+                      num_workers=config.num_workers)

@@ -1,0 +1,117 @@
+"""CLI entry (mirror of the reference's main.py:17-161) on the HIP UNet path.
+
+Same flags as the reference (``--dataset_path``, ``--checkpoint_path``, ``--bce_ratio`` ...
+``--use_data_parallel``), with three additions: ``--model_type UNet`` is the model actually
+built (the reference hard-codes ResUNet at main.py:120-122; only the UNet of
+models/model.py has a HIP path), ``--mode {train,test,both}`` replaces the commented-out
+``trainer.train()`` / hard-wired ``trainer.test()`` (:156-157), and ``--synthetic N`` runs
+on N synthetic samples per split when the DDTI images are not on disk.
+
+Multi-GPU: launch one process per GPU, e.g.
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 main.py --mode train ...
+(RCCL backend; replaces nn.DataParallel of utils/trainer.py:28-30).
+"""
+import argparse
+import os
+import sys
+
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+if HERE not in sys.path:
+    sys.path.insert(0, HERE)
+
+from data.data_loader import MedicalDataset, SyntheticSegmentation, create_dataloader  # noqa: E402
+from models.model import UNet  # noqa: E402
+from utils.trainer import Trainer  # noqa: E402
+from utils.transforms import Compose, Resize, ToTensor  # noqa: E402
+from utils.utils import Config, create_logger, set_seed  # noqa: E402
+
+
+def _flag(v):
+    # the reference uses type=bool (main.py:59-60), which turns any string into True
+    return bool(v)
+
+
+def get_parser(argv=None):
+    p = argparse.ArgumentParser(formatter_class=argparse.ArgumentDefaultsHelpFormatter)
+    p.add_argument("--dataset_path", default="data/dataset", type=str)
+    p.add_argument("--dataset", default="DDTI", type=str)
+    p.add_argument("--checkpoint_path", default="", type=str)
+    p.add_argument("--config_path", default=None, type=str)
+    p.add_argument("--p_crop", default=0, type=float)
+    for f in ("--use_elastic", "--use_speckle", "--use_tgc", "--use_clahe", "--use_mixup"):
+        p.add_argument(f, action="store_true")
+    p.add_argument("--mixup_alpha", type=float, default=0.2)
+    p.add_argument("--mixup_prob", type=float, default=0.3)
+    p.add_argument("--model_type", default="UNet", type=str)
+    p.add_argument("--bce_ratio", type=float, default=1)
+    p.add_argument("--dice_ratio", type=float, default=0)
+    p.add_argument("--focal_ratio", type=float, default=1)
+    p.add_argument("--boundary_ratio", type=float, default=0)
+    p.add_argument("--num_workers", default=4, type=int)
+    p.add_argument("--epochs", type=int, default=10000)
+    p.add_argument("--batch_size", default=16, type=int)
+    p.add_argument("--lr", type=float, default=1e-5)
+    p.add_argument("--weight_decay", type=float, default=1e-2)  # unused, as in the reference
+    p.add_argument("--save_interval", default=20, type=int)
+    p.add_argument("--early_stop_patience", default=50, type=int)
+    p.add_argument("--alpha", type=float, default=2)
+    p.add_argument("--use_data_parallel", type=_flag, default=True)
+    p.add_argument("--use_amp_autocast", type=_flag, default=False)
+    p.add_argument("--mode", choices=["train", "test", "both"], default="test")
+    p.add_argument("--image_size", type=int, default=512)
+    p.add_argument("--synthetic", type=int, default=0, help="synthetic samples per split")
+    return p.parse_args(argv)
+
+
+def main(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1 and not torch.distributed.is_initialized():
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        torch.cuda.set_device(local)
+        torch.distributed.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    set_seed(seed=42)
+    config = Config(args)
+    if torch.cuda.is_available():
+        config.device = torch.device("cuda", torch.cuda.current_device())
+    logger = create_logger(os.path.join(config.log_dir, "train_log.log"))
+    if args.model_type != "UNet":
+        raise SystemExit(f"model_type {args.model_type!r}: only the models/model.py UNet has a HIP path")
+    if args.use_elastic or args.use_speckle or args.use_tgc or args.use_clahe:
+        raise SystemExit("ultrasound augmentations need OpenCV/torchvision (not in this image)")
+
+    S = args.image_size
+    if args.synthetic:
+        splits = [SyntheticSegmentation(args.synthetic, S, seed=s) for s in range(3)]
+    else:
+        tf = Compose([Resize((S, S)), ToTensor()])
+        root = config.dataset_path
+        splits = [MedicalDataset(os.path.join(root, d), os.path.join(root, d + "_mask"), tf)
+                  for d in ("train", "val", "test")]
+    sampler_kw = {}
+    loaders = []
+    for i, ds in enumerate(splits):
+        if world > 1:
+            sampler_kw = dict(sampler=torch.utils.data.distributed.DistributedSampler(ds, shuffle=(i != 1)))
+            loaders.append(torch.utils.data.DataLoader(ds, batch_size=config.batch_size,
+                                                       num_workers=config.num_workers, **sampler_kw))
+        else:
+            loaders.append(create_dataloader(ds, config, shuffle=(i != 1)))
+
+    model = UNet()
+    if config.checkpoint_path and os.path.isfile(config.checkpoint_path):
+        model.load_state_dict(torch.load(config.checkpoint_path, weights_only=True))
+    n = sum(p.numel() for p in model.parameters() if p.requires_grad)
+    logger.info(f"Model: {config.model_type} | Trainable params: {n / 1e6:.2f}M ({n:,})")
+    print(f"[PARAMS] {config.model_type},{n}")
+
+    trainer = Trainer(config, tuple(loaders), logger, model)
+    if args.mode in ("train", "both"):
+        trainer.train()
+    if args.mode in ("test", "both"):
+        trainer.test()
+
+
+if __name__ == "__main__":
+    main(get_parser())
