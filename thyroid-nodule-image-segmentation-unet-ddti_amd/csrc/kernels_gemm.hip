@@ -23,6 +23,8 @@
 // four k values with one ds_read_b128: lane half h owns k = 4h..4h+3 and MFMA step s sums
 // k = s (h=0) and k = 4+s (h=1) -- A and B use the same permutation, so the product is the
 // same sum in a different order.
+#include <stdlib.h>
+
 #include "common.h"
 
 namespace {
@@ -61,16 +63,17 @@ __device__ __forceinline__ int gather_src(int mode, int tap, int m, Pix q, int H
     return m;
 }
 
-template <int BM, int BN, int BK, int WM, int WN>
+template <int BM, int BN, int BK, int WM, int WN, bool DBUF>
 __global__ __launch_bounds__(256, 2) void rowgemm_kernel(RowGemmArgs p) {
     constexpr int LDK = BK + 4;  // 16-B pad: conflict-free ds_read_b128 (row stride 144 B)
+    constexpr int NBUF = DBUF ? 2 : 1;  // DBUF: two LDS images, one barrier per K-chunk
     constexpr int MT = WM / 32, NT = WN / 32;
     constexpr int WAVES_N = BN / WN;
     constexpr int F4R = BK / 4;
     constexpr int RPP = 256 / F4R;
     constexpr int AP = BM / RPP, BP = BN / RPP;
     static_assert((BM / WM) * (BN / WN) == 4, "4 waves");
-    __shared__ __attribute__((aligned(16))) float smem[(BM + BN) * LDK];
+    __shared__ __attribute__((aligned(16))) float smem[NBUF * (BM + BN) * LDK];
     float* As = smem;
     float* Bs = smem + BM * LDK;
 
@@ -116,11 +119,13 @@ __global__ __launch_bounds__(256, 2) void rowgemm_kernel(RowGemmArgs p) {
         for (int i = 0; i < BP; ++i)
             rb[i] = *(const f32x4*)(p.bt + (size_t)(n0 + lrow + i * RPP) * p.K + k0 + lc4 * 4);
     };
-    auto store_chunk = [&]() {
+    auto store_chunk = [&](int buf) {
+        float* as = As + buf * (BM + BN) * LDK;
+        float* bs = Bs + buf * (BM + BN) * LDK;
 #pragma unroll
-        for (int i = 0; i < AP; ++i) *(f32x4*)&As[(lrow + i * RPP) * LDK + lc4 * 4] = ra[i];
+        for (int i = 0; i < AP; ++i) *(f32x4*)&as[(lrow + i * RPP) * LDK + lc4 * 4] = ra[i];
 #pragma unroll
-        for (int i = 0; i < BP; ++i) *(f32x4*)&Bs[(lrow + i * RPP) * LDK + lc4 * 4] = rb[i];
+        for (int i = 0; i < BP; ++i) *(f32x4*)&bs[(lrow + i * RPP) * LDK + lc4 * 4] = rb[i];
     };
 
     f32x16 acc[MT][NT];
@@ -134,19 +139,22 @@ __global__ __launch_bounds__(256, 2) void rowgemm_kernel(RowGemmArgs p) {
     const int li = lane & 31, lh = lane >> 5;
     const int nk = p.K / BK;
     load_chunk(0);
-    store_chunk();
+    store_chunk(0);
     __syncthreads();
     for (int kc = 0; kc < nk; ++kc) {
+        const int cur = DBUF ? (kc & 1) : 0;
         if (kc + 1 < nk) load_chunk(kc + 1);
+        const float* as = As + cur * (BM + BN) * LDK;
+        const float* bs = Bs + cur * (BM + BN) * LDK;
 #pragma unroll
         for (int kk = 0; kk < BK / 8; ++kk) {
             f32x4 af[MT], bf[NT];
 #pragma unroll
             for (int mt = 0; mt < MT; ++mt)
-                af[mt] = *(const f32x4*)&As[(wm * WM + mt * 32 + li) * LDK + kk * 8 + lh * 4];
+                af[mt] = *(const f32x4*)&as[(wm * WM + mt * 32 + li) * LDK + kk * 8 + lh * 4];
 #pragma unroll
             for (int nt = 0; nt < NT; ++nt)
-                bf[nt] = *(const f32x4*)&Bs[(wn * WN + nt * 32 + li) * LDK + kk * 8 + lh * 4];
+                bf[nt] = *(const f32x4*)&bs[(wn * WN + nt * 32 + li) * LDK + kk * 8 + lh * 4];
 #pragma unroll
             for (int s = 0; s < 4; ++s)
 #pragma unroll
@@ -155,10 +163,17 @@ __global__ __launch_bounds__(256, 2) void rowgemm_kernel(RowGemmArgs p) {
                     for (int nt = 0; nt < NT; ++nt)
                         acc[mt][nt] = mfma32(af[mt][s], bf[nt][s], acc[mt][nt]);
         }
-        __syncthreads();
-        if (kc + 1 < nk) {
-            store_chunk();
+        if (DBUF) {
+            // the other image was last read in iteration kc-1, which every wave finished
+            // before the barrier that ended it
+            if (kc + 1 < nk) store_chunk(cur ^ 1);
             __syncthreads();
+        } else {
+            __syncthreads();
+            if (kc + 1 < nk) {
+                store_chunk(0);
+                __syncthreads();
+            }
         }
     }
 
@@ -361,18 +376,32 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
 
 }  // namespace
 
+static int g_rowgemm_dbuf = -1;
+
 int launch_rowgemm(const RowGemmArgs& a, int bm, int bn, hipStream_t s) {
     constexpr int BK = 32;
+    if (g_rowgemm_dbuf < 0) {
+        const char* e = getenv("UNET_ROWGEMM_DBUF");
+        g_rowgemm_dbuf = e ? atoi(e) : 1;
+    }
     if (a.M < 1 || a.N % bn || a.K % BK || a.C % BK || a.K != gather_taps(a.amode) * a.C)
         return -1;
     if (a.emode == E_CONVT && (a.cout % bn)) return -1;
     dim3 grid(((a.M + bm - 1) / bm) * (a.N / bn)), block(256);
-    if (bm == 128 && bn == 128)
-        hipLaunchKernelGGL((rowgemm_kernel<128, 128, BK, 64, 64>), grid, block, 0, s, a);
-    else if (bm == 128 && bn == 64)
-        hipLaunchKernelGGL((rowgemm_kernel<128, 64, BK, 64, 32>), grid, block, 0, s, a);
-    else
+    if (bm == 128 && bn == 128) {
+        if (g_rowgemm_dbuf)
+            hipLaunchKernelGGL((rowgemm_kernel<128, 128, BK, 64, 64, true>), grid, block, 0, s, a);
+        else
+            hipLaunchKernelGGL((rowgemm_kernel<128, 128, BK, 64, 64, false>), grid, block, 0, s, a);
+    } else if (bm == 128 && bn == 64) {
+        // 55 KB of double-buffered LDS would halve this tile's occupancy (4 -> 2 waves/SIMD)
+        if (g_rowgemm_dbuf >= 2)
+            hipLaunchKernelGGL((rowgemm_kernel<128, 64, BK, 64, 32, true>), grid, block, 0, s, a);
+        else
+            hipLaunchKernelGGL((rowgemm_kernel<128, 64, BK, 64, 32, false>), grid, block, 0, s, a);
+    } else {
         return -1;
+    }
     return (int)hipGetLastError();
 }
 
