@@ -162,10 +162,13 @@ def main():
     ms = 1000 * elapsed / args.steps
 
     # per-kernel aggregation (label = family/kernel instance)
-    fam, kern = {}, {}
+    fam, kern, layer = {}, {}, {}
     for label, t_ms, flop in recs:
-        f, _, k = label.partition("/")
-        for d, key in ((fam, f), (kern, k or f)):
+        f, _, rest = label.partition("/")
+        k, _, li = rest.partition("|")
+        for d, key in ((fam, f), (kern, k or f), (layer, f"{f}|{li}" if li else None)):
+            if key is None:
+                continue
             e = d.setdefault(key, [0, 0.0, 0.0])
             e[0] += 1
             e[1] += t_ms
@@ -206,6 +209,10 @@ def main():
                       file=sys.stderr)
             for k, (n, tm, fl) in sorted(kern.items(), key=lambda kv: -kv[1][1])[:8]:
                 print(f"  [{k}] n={n} {tm / args.steps:.3f} ms/step", file=sys.stderr)
+            print("  per layer (conv i = 0..17, convT 100..103):", file=sys.stderr)
+            for k, (n, tm, fl) in sorted(layer.items(), key=lambda kv: -kv[1][1]):
+                tf = fl / (tm * 1e-3) / 1e12 if tm > 0 else 0
+                print(f"    {k:18s} {tm / args.steps:8.3f} ms/step {tf:7.2f} TF/s", file=sys.stderr)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -371,9 +371,12 @@ struct Launcher {
 };
 
 // timing label "family/kernel-instance" (the instance is what rocprofv3 reports)
-std::string glabel(const char* fam, const char* kern, int bm, int bn) {
-    char b[96];
-    snprintf(b, sizeof b, "%s/%s_%dx%d", fam, kern, bm, bn);
+std::string glabel(const char* fam, const char* kern, int bm, int bn, int layer = -1) {
+    char b[112];
+    if (layer >= 0)
+        snprintf(b, sizeof b, "%s/%s_%dx%d|%d", fam, kern, bm, bn, layer);
+    else
+        snprintf(b, sizeof b, "%s/%s_%dx%d", fam, kern, bm, bn);
     return b;
 }
 
@@ -492,7 +495,7 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
             g.emode = E_BIAS_RELU_STATS;
             const int bn = C.cout % 128 == 0 ? 128 : 64;
             R = (int)((M + 127) / 128);
-            RUN(glabel("conv_fwd", "rowgemm", 128, bn), 2.0 * M * C.cout * 9 * C.cin,
+            RUN(glabel("conv_fwd", "rowgemm", 128, bn, i), 2.0 * M * C.cout * 9 * C.cin,
                 launch_rowgemm(g, 128, bn, s));
         }
         return stats_finalize(c, L, p, i, R, M, training, prm, bn_run, bn_cnt);
@@ -522,7 +525,7 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
         g.cout = T.cout;
         g.emode = E_CONVT;
         const int bn = T.cout % 128 == 0 ? 128 : 64;
-        RUN(glabel("convT_fwd", "rowgemm", 128, bn), 2.0 * g.M * g.N * g.K,
+        RUN(glabel("convT_fwd", "rowgemm", 128, bn, 100 + k), 2.0 * g.M * g.N * g.K,
             launch_rowgemm(g, 128, bn, s));
         return 0;
     };
@@ -607,7 +610,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         w.pps = wc.pps;
         w.splits = wc.splits;
         w.slab = p.slab;
-        RUN(glabel("conv_wgrad", "wgrad", wc.bm, wc.bn), 2.0 * P * C.cout * 9 * C.cin,
+        RUN(glabel("conv_wgrad", "wgrad", wc.bm, wc.bn, i), 2.0 * P * C.cout * 9 * C.cin,
             launch_wgrad(w, wc.bm, wc.bn, s));
         RUN("wgrad_reduce", 0,
             k_slab_reduce(p.slab, wc.splits, w.Mw, w.Nw, 0, C.cin, C.cout, grads + C.w, s));
@@ -629,7 +632,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
             g.ooff = 0;
             g.emode = E_STORE;
             const int bn = C.cin % 128 == 0 ? 128 : 64;
-            RUN(glabel("conv_dgrad", "rowgemm", 128, bn), 2.0 * P * C.cout * 9 * C.cin,
+            RUN(glabel("conv_dgrad", "rowgemm", 128, bn, i), 2.0 * P * C.cout * 9 * C.cin,
                 launch_rowgemm(g, 128, bn, s));
         }
         return 0;
@@ -666,7 +669,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         w.pps = wc.pps;
         w.splits = wc.splits;
         w.slab = p.slab;
-        RUN(glabel("convT_wgrad", "wgrad", wc.bm, wc.bn), 2.0 * Pin * T.cin * 4 * T.cout,
+        RUN(glabel("convT_wgrad", "wgrad", wc.bm, wc.bn, 100 + k), 2.0 * Pin * T.cin * 4 * T.cout,
             launch_wgrad(w, wc.bm, wc.bn, s));
         RUN("wgrad_reduce", 0,
             k_slab_reduce(p.slab, wc.splits, w.Mw, w.Nw, 1, T.cin, T.cout, grads + T.w, s));
@@ -687,7 +690,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         g.ooff = 0;
         g.emode = E_STORE;
         const int bn = T.cin % 128 == 0 ? 128 : 64;
-        RUN(glabel("convT_dgrad", "rowgemm", 128, bn), 2.0 * Pin * T.cin * 4 * T.cout,
+        RUN(glabel("convT_dgrad", "rowgemm", 128, bn, 100 + k), 2.0 * Pin * T.cin * 4 * T.cout,
             launch_rowgemm(g, 128, bn, s));
         return 0;
     };
