@@ -23,8 +23,6 @@
 // four k values with one ds_read_b128: lane half h owns k = 4h..4h+3 and MFMA step s sums
 // k = s (h=0) and k = 4+s (h=1) -- A and B use the same permutation, so the product is the
 // same sum in a different order.
-#include <stdlib.h>
-
 #include "common.h"
 
 namespace {
@@ -46,84 +44,96 @@ __device__ __forceinline__ Pix decode(int m, int H, int W) {
     return r;
 }
 
-// Source pixel of row pixel `q` (on grid HxW) for `tap` in `mode`; `valid` false for
+// Source pixel of row pixel `q` (on grid HxW) for `tap` in MODE; `valid` false for
 // zero-padding taps (the returned index is then the row pixel itself, always in range).
-__device__ __forceinline__ int gather_src(int mode, int tap, int m, Pix q, int H, int W,
-                                          bool& valid) {
-    if (mode == G_CONV3) {
-        int yy = q.y + tap / 3 - 1, xx = q.x + tap % 3 - 1;
+template <int MODE>
+__device__ __forceinline__ int gather_src(int tap, int m, Pix q, int H, int W, bool& valid) {
+    if constexpr (MODE == G_CONV3) {
+        const int yy = q.y + tap / 3 - 1, xx = q.x + tap % 3 - 1;
         valid = (yy >= 0) & (yy < H) & (xx >= 0) & (xx < W);
         return valid ? (q.img * H + yy) * W + xx : m;
-    }
-    valid = true;
-    if (mode == G_UP2) {
-        int a = tap >> 1, b = tap & 1;
+    } else if constexpr (MODE == G_UP2) {
+        valid = true;
+        const int a = tap >> 1, b = tap & 1;
         return (q.img * 2 * H + 2 * q.y + a) * (2 * W) + 2 * q.x + b;
+    } else {
+        valid = true;
+        return m;
     }
-    return m;
 }
 
-template <int BM, int BN, int BK, int WM, int WN, bool DBUF>
+// ------------------------------------------------------------------------------------
+// Row GEMM.  Pipeline per K-chunk: issue the NEXT chunk's global loads into registers
+// (raw: no arithmetic depends on them, so nothing waits for them here), run the MFMAs of
+// the current chunk from LDS, then apply the BN affine / zero padding to the landed
+// registers and write them to the other LDS image, one barrier.
+// ------------------------------------------------------------------------------------
+template <int AMODE, bool AFFINE, int EMODE, int BM, int BN>
 __global__ __launch_bounds__(256, 2) void rowgemm_kernel(RowGemmArgs p) {
-    constexpr int LDK = BK + 4;  // 16-B pad: conflict-free ds_read_b128 (row stride 144 B)
-    constexpr int NBUF = DBUF ? 2 : 1;  // DBUF: two LDS images, one barrier per K-chunk
+    constexpr int BK = 32;
+    constexpr int WM = BM / 2, WN = BN / 2;
+    constexpr bool DBUF = BN == 128;     // 2 LDS images when it does not cost occupancy
+    constexpr int NBUF = DBUF ? 2 : 1;
+    constexpr int LDK = BK + 4;          // 16-B pad: conflict-free ds_read_b128 (144-B rows)
     constexpr int MT = WM / 32, NT = WN / 32;
-    constexpr int WAVES_N = BN / WN;
     constexpr int F4R = BK / 4;
     constexpr int RPP = 256 / F4R;
     constexpr int AP = BM / RPP, BP = BN / RPP;
-    static_assert((BM / WM) * (BN / WN) == 4, "4 waves");
-    __shared__ __attribute__((aligned(16))) float smem[NBUF * (BM + BN) * LDK];
-    float* As = smem;
-    float* Bs = smem + BM * LDK;
+    constexpr int IMG = (BM + BN) * LDK;
+    __shared__ __attribute__((aligned(16))) float smem[NBUF * IMG];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+    const int wm = wave >> 1, wn = wave & 1;
     const int ntn = p.N / BN;
-    const int tile_m = blockIdx.x / ntn, tile_n = blockIdx.x - (blockIdx.x / ntn) * ntn;
+    const int tile_m = blockIdx.x / ntn, tile_n = blockIdx.x - tile_m * ntn;
     const int m0 = tile_m * BM, n0 = tile_n * BN;
     const int H = p.H, W = p.W;
 
     const int lrow = tid / F4R, lc4 = tid % F4R;
     Pix rq[AP];
+    int rm[AP];
     bool rok[AP];  // row inside M (the last M tile may be partial)
 #pragma unroll
     for (int i = 0; i < AP; ++i) {
         const int m = m0 + lrow + i * RPP;
         rok[i] = m < p.M;
-        rq[i] = decode(rok[i] ? m : p.M - 1, H, W);
+        rm[i] = rok[i] ? m : p.M - 1;
+        rq[i] = decode(rm[i], H, W);
     }
 
-    f32x4 ra[AP], rb[BP];
-    const bool affine = p.ascale != nullptr;
+    f32x4 ra[AP], rb[BP], rsc, rsh;
+    unsigned vmask = 0;
 
-    auto load_chunk = [&](int kc) {
+    auto issue = [&](int kc) {
         const int k0 = kc * BK;
         const int tap = k0 / p.C;
         const int c = k0 - tap * p.C + lc4 * 4;
-        f32x4 sc = {1.f, 1.f, 1.f, 1.f}, sh = {0.f, 0.f, 0.f, 0.f};
-        if (affine) {
-            sc = *(const f32x4*)(p.ascale + c);
-            sh = *(const f32x4*)(p.ashift + c);
+        if constexpr (AFFINE) {
+            rsc = *(const f32x4*)(p.ascale + c);
+            rsh = *(const f32x4*)(p.ashift + c);
         }
+        vmask = 0;
 #pragma unroll
         for (int i = 0; i < AP; ++i) {
             bool valid;
-            const int m = rok[i] ? m0 + lrow + i * RPP : p.M - 1;
-            const int src = gather_src(p.amode, tap, m, rq[i], H, W, valid);
-            f32x4 v = *(const f32x4*)(p.a + (size_t)src * p.lda + p.aoff + c);
-            if (affine) v = v * sc + sh;
-            ra[i] = (valid && rok[i]) ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+            const int src = gather_src<AMODE>(tap, rm[i], rq[i], H, W, valid);
+            vmask |= (valid && rok[i]) ? (1u << i) : 0u;
+            ra[i] = *(const f32x4*)(p.a + (size_t)src * p.lda + p.aoff + c);
         }
 #pragma unroll
         for (int i = 0; i < BP; ++i)
             rb[i] = *(const f32x4*)(p.bt + (size_t)(n0 + lrow + i * RPP) * p.K + k0 + lc4 * 4);
     };
-    auto store_chunk = [&](int buf) {
-        float* as = As + buf * (BM + BN) * LDK;
-        float* bs = Bs + buf * (BM + BN) * LDK;
+    auto commit = [&](int buf) {
+        float* as = smem + buf * IMG;
+        float* bs = as + BM * LDK;
 #pragma unroll
-        for (int i = 0; i < AP; ++i) *(f32x4*)&as[(lrow + i * RPP) * LDK + lc4 * 4] = ra[i];
+        for (int i = 0; i < AP; ++i) {
+            f32x4 v = ra[i];
+            if constexpr (AFFINE) v = v * rsc + rsh;
+            if (!((vmask >> i) & 1u)) v = f32x4{0.f, 0.f, 0.f, 0.f};
+            *(f32x4*)&as[(lrow + i * RPP) * LDK + lc4 * 4] = v;
+        }
 #pragma unroll
         for (int i = 0; i < BP; ++i) *(f32x4*)&bs[(lrow + i * RPP) * LDK + lc4 * 4] = rb[i];
     };
@@ -138,14 +148,14 @@ __global__ __launch_bounds__(256, 2) void rowgemm_kernel(RowGemmArgs p) {
 
     const int li = lane & 31, lh = lane >> 5;
     const int nk = p.K / BK;
-    load_chunk(0);
-    store_chunk(0);
+    issue(0);
+    commit(0);
     __syncthreads();
     for (int kc = 0; kc < nk; ++kc) {
         const int cur = DBUF ? (kc & 1) : 0;
-        if (kc + 1 < nk) load_chunk(kc + 1);
-        const float* as = As + cur * (BM + BN) * LDK;
-        const float* bs = Bs + cur * (BM + BN) * LDK;
+        if (kc + 1 < nk) issue(kc + 1);
+        const float* as = smem + cur * IMG;
+        const float* bs = as + BM * LDK;
 #pragma unroll
         for (int kk = 0; kk < BK / 8; ++kk) {
             f32x4 af[MT], bf[NT];
@@ -163,22 +173,22 @@ __global__ __launch_bounds__(256, 2) void rowgemm_kernel(RowGemmArgs p) {
                     for (int nt = 0; nt < NT; ++nt)
                         acc[mt][nt] = mfma32(af[mt][s], bf[nt][s], acc[mt][nt]);
         }
-        if (DBUF) {
+        if constexpr (DBUF) {
             // the other image was last read in iteration kc-1, which every wave finished
             // before the barrier that ended it
-            if (kc + 1 < nk) store_chunk(cur ^ 1);
+            if (kc + 1 < nk) commit(cur ^ 1);
             __syncthreads();
         } else {
             __syncthreads();
             if (kc + 1 < nk) {
-                store_chunk(0);
+                commit(0);
                 __syncthreads();
             }
         }
     }
 
     // ---------------- epilogue ----------------
-    if (p.emode == E_BIAS_RELU_STATS) {
+    if constexpr (EMODE == E_BIAS_RELU_STATS) {
         float s1[NT], s2[NT];
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) {
@@ -192,7 +202,7 @@ __global__ __launch_bounds__(256, 2) void rowgemm_kernel(RowGemmArgs p) {
                 for (int r = 0; r < 16; ++r) {
                     const int m = m0 + wm * WM + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
                     if (m < p.M) {
-                        float v = fmaxf(acc[mt][nt][r] + b, 0.f);
+                        const float v = fmaxf(acc[mt][nt][r] + b, 0.f);
                         p.out[(size_t)m * p.ldo + p.ooff + n] = v;
                         s1[nt] += v;
                         s2[nt] += v * v;
@@ -201,8 +211,9 @@ __global__ __launch_bounds__(256, 2) void rowgemm_kernel(RowGemmArgs p) {
             s1[nt] += __shfl_xor(s1[nt], 32);
             s2[nt] += __shfl_xor(s2[nt], 32);
         }
-        // combine the BM/WM waves that share these columns (smem is free after the loop)
-        float* red = smem;  // [BM/WM][2][BN]
+        // combine the two M-waves that share these columns (LDS is free after the loop)
+        __syncthreads();
+        float* red = smem;  // [2][2][BN]
         if (lh == 0) {
 #pragma unroll
             for (int nt = 0; nt < NT; ++nt) {
@@ -212,16 +223,12 @@ __global__ __launch_bounds__(256, 2) void rowgemm_kernel(RowGemmArgs p) {
         }
         __syncthreads();
         if (tid < BN) {
-            float a = 0.f, q = 0.f;
-#pragma unroll
-            for (int w = 0; w < BM / WM; ++w) {
-                a += red[(w * 2 + 0) * BN + tid];
-                q += red[(w * 2 + 1) * BN + tid];
-            }
+            const float a = red[0 * BN + tid] + red[2 * BN + tid];
+            const float q = red[1 * BN + tid] + red[3 * BN + tid];
             p.stats[(size_t)tile_m * 2 * p.N + n0 + tid] = a;
             p.stats[(size_t)tile_m * 2 * p.N + p.N + n0 + tid] = q;
         }
-    } else if (p.emode == E_CONVT) {
+    } else if constexpr (EMODE == E_CONVT) {
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) {
             const int n = n0 + wn * WN + nt * 32 + li;
@@ -254,20 +261,23 @@ __global__ __launch_bounds__(256, 2) void rowgemm_kernel(RowGemmArgs p) {
     }
 }
 
-template <int BM, int BN, int BKP, int WM, int WN>
+// ------------------------------------------------------------------------------------
+// Weight-gradient GEMM (reduction over pixels), same issue / compute / commit pipeline.
+// ------------------------------------------------------------------------------------
+template <int AMODE, bool AFFINE, int BMODE, int BM, int BN>
 __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
+    constexpr int BKP = 32;
+    constexpr int WM = BM / 2, WN = BN / 2;
     constexpr int LDA = BM + 4, LDB = BN + 4;
     constexpr int MT = WM / 32, NT = WN / 32;
-    constexpr int WAVES_N = BN / WN;
-    constexpr int AF = BM / 4, BF = BN / 4;        // float4 per pixel row
+    constexpr int AF = BM / 4, BF = BN / 4;          // float4 per pixel row
     constexpr int ARPP = 256 / AF, BRPP = 256 / BF;  // rows per pass
     constexpr int AP = BKP / ARPP, BP = BKP / BRPP;
-    static_assert((BM / WM) * (BN / WN) == 4, "4 waves");
     __shared__ __attribute__((aligned(16))) float As[BKP * LDA];
     __shared__ __attribute__((aligned(16))) float Bs[BKP * LDB];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+    const int wm = wave >> 1, wn = wave & 1;
     const int tiles_n = p.Nw / BN, tiles_m = p.Mw / BM;
     int idx = blockIdx.x;
     const int tn = idx % tiles_n;
@@ -280,9 +290,8 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
 
     const int ac4 = tid % AF, arow = tid / AF;
     const int bc4 = tid % BF, brow = tid / BF;
-    const bool affine = p.ascale != nullptr;
     f32x4 sc = {1.f, 1.f, 1.f, 1.f}, sh = {0.f, 0.f, 0.f, 0.f};
-    if (affine) {
+    if constexpr (AFFINE) {
         sc = *(const f32x4*)(p.ascale + ca0 + ac4 * 4);
         sh = *(const f32x4*)(p.ashift + ca0 + ac4 * 4);
     }
@@ -293,17 +302,18 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
     const int nchunks = (pend - pbeg + BKP - 1) / BKP;
 
     f32x4 ra[AP], rb[BP];
-    auto load_chunk = [&](int pc) {
+    unsigned amask = 0, bmask = 0;
+    auto issue = [&](int pc) {
+        amask = bmask = 0;
 #pragma unroll
         for (int i = 0; i < AP; ++i) {
             int m = pc + arow + i * ARPP;
             const bool in = m < pend;
             m = in ? m : pend - 1;
             bool valid;
-            const int src = gather_src(p.amode, tapA, m, decode(m, H, W), H, W, valid);
-            f32x4 v = *(const f32x4*)(p.a + (size_t)src * p.lda + p.aoff + ca0 + ac4 * 4);
-            if (affine) v = v * sc + sh;
-            ra[i] = (valid && in) ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+            const int src = gather_src<AMODE>(tapA, m, decode(m, H, W), H, W, valid);
+            amask |= (valid && in) ? (1u << i) : 0u;
+            ra[i] = *(const f32x4*)(p.a + (size_t)src * p.lda + p.aoff + ca0 + ac4 * 4);
         }
 #pragma unroll
         for (int i = 0; i < BP; ++i) {
@@ -311,16 +321,25 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
             const bool in = m < pend;
             m = in ? m : pend - 1;
             bool valid;
-            const int src = gather_src(p.bmode, tapB, m, decode(m, H, W), H, W, valid);
-            f32x4 v = *(const f32x4*)(p.b + (size_t)src * p.ldb + p.boff + cb0 + bc4 * 4);
-            rb[i] = (valid && in) ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+            const int src = gather_src<BMODE>(tapB, m, decode(m, H, W), H, W, valid);
+            bmask |= (valid && in) ? (1u << i) : 0u;
+            rb[i] = *(const f32x4*)(p.b + (size_t)src * p.ldb + p.boff + cb0 + bc4 * 4);
         }
     };
-    auto store_chunk = [&]() {
+    auto commit = [&]() {
 #pragma unroll
-        for (int i = 0; i < AP; ++i) *(f32x4*)&As[(arow + i * ARPP) * LDA + ac4 * 4] = ra[i];
+        for (int i = 0; i < AP; ++i) {
+            f32x4 v = ra[i];
+            if constexpr (AFFINE) v = v * sc + sh;
+            if (!((amask >> i) & 1u)) v = f32x4{0.f, 0.f, 0.f, 0.f};
+            *(f32x4*)&As[(arow + i * ARPP) * LDA + ac4 * 4] = v;
+        }
 #pragma unroll
-        for (int i = 0; i < BP; ++i) *(f32x4*)&Bs[(brow + i * BRPP) * LDB + bc4 * 4] = rb[i];
+        for (int i = 0; i < BP; ++i) {
+            f32x4 v = rb[i];
+            if (!((bmask >> i) & 1u)) v = f32x4{0.f, 0.f, 0.f, 0.f};
+            *(f32x4*)&Bs[(brow + i * BRPP) * LDB + bc4 * 4] = v;
+        }
     };
 
     f32x16 acc[MT][NT];
@@ -333,12 +352,12 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
 
     const int li = lane & 31, lh = lane >> 5;
     if (nchunks > 0) {
-        load_chunk(pbeg);
-        store_chunk();
+        issue(pbeg);
+        commit();
         __syncthreads();
     }
     for (int c = 0; c < nchunks; ++c) {
-        if (c + 1 < nchunks) load_chunk(pbeg + (c + 1) * BKP);
+        if (c + 1 < nchunks) issue(pbeg + (c + 1) * BKP);
 #pragma unroll
         for (int kk = 0; kk < BKP / 8; ++kk)
 #pragma unroll
@@ -356,7 +375,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
             }
         __syncthreads();
         if (c + 1 < nchunks) {
-            store_chunk();
+            commit();
             __syncthreads();
         }
     }
@@ -376,48 +395,65 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
 
 }  // namespace
 
-static int g_rowgemm_dbuf = -1;
+// ------------------------------------------------------------------------------------
+// host dispatch
+// ------------------------------------------------------------------------------------
+template <int AMODE, bool AFFINE, int EMODE>
+static int rowgemm_tile(const RowGemmArgs& a, int bn, dim3 grid, hipStream_t s) {
+    if (bn == 128)
+        hipLaunchKernelGGL((rowgemm_kernel<AMODE, AFFINE, EMODE, 128, 128>), grid, dim3(256), 0, s, a);
+    else if (bn == 64)
+        hipLaunchKernelGGL((rowgemm_kernel<AMODE, AFFINE, EMODE, 128, 64>), grid, dim3(256), 0, s, a);
+    else
+        return -1;
+    return (int)hipGetLastError();
+}
 
 int launch_rowgemm(const RowGemmArgs& a, int bm, int bn, hipStream_t s) {
     constexpr int BK = 32;
-    if (g_rowgemm_dbuf < 0) {
-        const char* e = getenv("UNET_ROWGEMM_DBUF");
-        g_rowgemm_dbuf = e ? atoi(e) : 1;
-    }
-    if (a.M < 1 || a.N % bn || a.K % BK || a.C % BK || a.K != gather_taps(a.amode) * a.C)
+    if (bm != 128 || a.M < 1 || a.N % bn || a.K % BK || a.C % BK ||
+        a.K != gather_taps(a.amode) * a.C)
         return -1;
     if (a.emode == E_CONVT && (a.cout % bn)) return -1;
-    dim3 grid(((a.M + bm - 1) / bm) * (a.N / bn)), block(256);
-    if (bm == 128 && bn == 128) {
-        if (g_rowgemm_dbuf)
-            hipLaunchKernelGGL((rowgemm_kernel<128, 128, BK, 64, 64, true>), grid, block, 0, s, a);
-        else
-            hipLaunchKernelGGL((rowgemm_kernel<128, 128, BK, 64, 64, false>), grid, block, 0, s, a);
-    } else if (bm == 128 && bn == 64) {
-        // 55 KB of double-buffered LDS would halve this tile's occupancy (4 -> 2 waves/SIMD)
-        if (g_rowgemm_dbuf >= 2)
-            hipLaunchKernelGGL((rowgemm_kernel<128, 64, BK, 64, 32, true>), grid, block, 0, s, a);
-        else
-            hipLaunchKernelGGL((rowgemm_kernel<128, 64, BK, 64, 32, false>), grid, block, 0, s, a);
-    } else {
-        return -1;
+    const dim3 grid(((a.M + bm - 1) / bm) * (a.N / bn));
+    const bool aff = a.ascale != nullptr;
+    if (a.amode == G_CONV3 && a.emode == E_BIAS_RELU_STATS)
+        return aff ? rowgemm_tile<G_CONV3, true, E_BIAS_RELU_STATS>(a, bn, grid, s)
+                   : rowgemm_tile<G_CONV3, false, E_BIAS_RELU_STATS>(a, bn, grid, s);
+    if (a.amode == G_CONV3 && a.emode == E_STORE && !aff)
+        return rowgemm_tile<G_CONV3, false, E_STORE>(a, bn, grid, s);
+    if (a.amode == G_IDENT && a.emode == E_CONVT && aff)
+        return rowgemm_tile<G_IDENT, true, E_CONVT>(a, bn, grid, s);
+    if (a.amode == G_UP2 && a.emode == E_STORE && !aff)
+        return rowgemm_tile<G_UP2, false, E_STORE>(a, bn, grid, s);
+    return -1;  // combination not instantiated
+}
+
+template <int AMODE, bool AFFINE, int BMODE>
+static int wgrad_tile(const WgradArgs& a, int bm, int bn, dim3 grid, hipStream_t s) {
+#define WG_CASE(M_, N_)                                                                    \
+    if (bm == M_ && bn == N_) {                                                            \
+        hipLaunchKernelGGL((wgrad_kernel<AMODE, AFFINE, BMODE, M_, N_>), grid, dim3(256), 0, \
+                           s, a);                                                          \
+        return (int)hipGetLastError();                                                     \
     }
-    return (int)hipGetLastError();
+    WG_CASE(128, 128)
+    WG_CASE(64, 64)
+    WG_CASE(128, 64)
+    WG_CASE(64, 128)
+#undef WG_CASE
+    return -1;
 }
 
 int launch_wgrad(const WgradArgs& a, int bm, int bn, hipStream_t s) {
     constexpr int BKP = 32;
     if (a.Mw % bm || a.Nw % bn || a.CA % bm || a.CB % bn || a.P < 1 || a.pps % BKP) return -1;
-    dim3 grid((a.Mw / bm) * (a.Nw / bn) * a.splits), block(256);
-    if (bm == 128 && bn == 128)
-        hipLaunchKernelGGL((wgrad_kernel<128, 128, BKP, 64, 64>), grid, block, 0, s, a);
-    else if (bm == 64 && bn == 64)
-        hipLaunchKernelGGL((wgrad_kernel<64, 64, BKP, 32, 32>), grid, block, 0, s, a);
-    else if (bm == 128 && bn == 64)
-        hipLaunchKernelGGL((wgrad_kernel<128, 64, BKP, 64, 32>), grid, block, 0, s, a);
-    else if (bm == 64 && bn == 128)
-        hipLaunchKernelGGL((wgrad_kernel<64, 128, BKP, 32, 64>), grid, block, 0, s, a);
-    else
-        return -1;
-    return (int)hipGetLastError();
+    const dim3 grid((a.Mw / bm) * (a.Nw / bn) * a.splits);
+    const bool aff = a.ascale != nullptr;
+    if (a.amode == G_CONV3 && a.bmode == G_IDENT)
+        return aff ? wgrad_tile<G_CONV3, true, G_IDENT>(a, bm, bn, grid, s)
+                   : wgrad_tile<G_CONV3, false, G_IDENT>(a, bm, bn, grid, s);
+    if (a.amode == G_IDENT && a.bmode == G_UP2 && aff)
+        return wgrad_tile<G_IDENT, true, G_UP2>(a, bm, bn, grid, s);
+    return -1;
 }
