@@ -113,7 +113,7 @@ def test_train_steps_match_golden(golden_dir):
         rms = (norms / np.sqrt(sizes))[:, None]
         tiny = tiny | (np.abs(samp) < 1e-2 * rms) if s else (np.abs(samp) < 1e-2 * rms)
         d = np.abs(ps - f[f"s{s}_params_samp"])
-        bound = 3e-7 if s == 0 else 3e-6
+        bound = 3e-7 if s == 0 else 1e-5  # after step 0: within one lr (no sign flips)
         assert np.all(d[~tiny] <= bound), f"step {s}: max {d[~tiny].max():.3e}"
         assert np.all(d[tiny] <= 2 * 1e-5 * (s + 1) * 1.01)
         assert tiny.mean() < 0.02

@@ -63,5 +63,7 @@ struct WgradArgs {
     } while (0)
 
 // host launchers (kernels_gemm.hip)
-int launch_rowgemm(const RowGemmArgs& a, int bm, int bn, hipStream_t s);
+// tile ids: 0 = 128x128 (DBUF), 1 = 128x64, 2 = 256x64, 3 = 128x128 BK64 (kernels_gemm.hip)
+int launch_rowgemm(const RowGemmArgs& a, int tile, hipStream_t s);
+int rowgemm_tile_dims(int tile, int* bm, int* bn, int* bk);
 int launch_wgrad(const WgradArgs& a, int bm, int bn, hipStream_t s);

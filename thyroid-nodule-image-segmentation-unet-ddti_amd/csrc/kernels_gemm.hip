@@ -68,22 +68,34 @@ __device__ __forceinline__ int gather_src(int tap, int m, Pix q, int H, int W, b
 // the current chunk from LDS, then apply the BN affine / zero padding to the landed
 // registers and write them to the other LDS image, one barrier.
 // ------------------------------------------------------------------------------------
-template <int AMODE, bool AFFINE, int EMODE, int BM, int BN>
-__global__ __launch_bounds__(256, 2) void rowgemm_kernel(RowGemmArgs p) {
-    constexpr int BK = 32;
-    constexpr int WM = BM / 2, WN = BN / 2;
-    constexpr bool DBUF = BN == 128;     // 2 LDS images when it does not cost occupancy
+// Tile configuration of the row GEMM: block tile BM x BN, wave tile WM x WN (32x32 MFMA
+// accumulators), K-chunk BK, DBUF = two LDS images (one barrier per chunk).
+template <int BM_, int BN_, int WM_, int WN_, int BK_, bool DBUF_>
+struct RowTile {
+    static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, BK = BK_;
+    static constexpr bool DBUF = DBUF_;
+    static constexpr int WAVES = (BM / WM) * (BN / WN);
+    static constexpr int THREADS = 64 * WAVES;
+};
+
+template <int AMODE, bool AFFINE, int EMODE, class T>
+__global__ __launch_bounds__(T::THREADS, 1) void rowgemm_kernel(RowGemmArgs p) {
+    constexpr int BM = T::BM, BN = T::BN, WM = T::WM, WN = T::WN, BK = T::BK;
+    constexpr bool DBUF = T::DBUF;
+    constexpr int NTH = T::THREADS;
+    constexpr int WAVES_N = BN / WN, WAVES_M = BM / WM;
     constexpr int NBUF = DBUF ? 2 : 1;
-    constexpr int LDK = BK + 4;          // 16-B pad: conflict-free ds_read_b128 (144-B rows)
+    constexpr int LDK = BK + 4;          // 16-B pad: conflict-free ds_read_b128
     constexpr int MT = WM / 32, NT = WN / 32;
     constexpr int F4R = BK / 4;
-    constexpr int RPP = 256 / F4R;
+    constexpr int RPP = NTH / F4R;
     constexpr int AP = BM / RPP, BP = BN / RPP;
+    static_assert(AP * RPP == BM && BP * RPP == BN, "loader shape");
     constexpr int IMG = (BM + BN) * LDK;
     __shared__ __attribute__((aligned(16))) float smem[NBUF * IMG];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wm = wave >> 1, wn = wave & 1;
+    const int wm = wave / WAVES_N, wn = wave % WAVES_N;
     const int ntn = p.N / BN;
     const int tile_m = blockIdx.x / ntn, tile_n = blockIdx.x - tile_m * ntn;
     const int m0 = tile_m * BM, n0 = tile_n * BN;
@@ -211,9 +223,9 @@ __global__ __launch_bounds__(256, 2) void rowgemm_kernel(RowGemmArgs p) {
             s1[nt] += __shfl_xor(s1[nt], 32);
             s2[nt] += __shfl_xor(s2[nt], 32);
         }
-        // combine the two M-waves that share these columns (LDS is free after the loop)
+        // combine the M-waves that share these columns (LDS is free after the loop)
         __syncthreads();
-        float* red = smem;  // [2][2][BN]
+        float* red = smem;  // [WAVES_M][2][BN]
         if (lh == 0) {
 #pragma unroll
             for (int nt = 0; nt < NT; ++nt) {
@@ -223,8 +235,12 @@ __global__ __launch_bounds__(256, 2) void rowgemm_kernel(RowGemmArgs p) {
         }
         __syncthreads();
         if (tid < BN) {
-            const float a = red[0 * BN + tid] + red[2 * BN + tid];
-            const float q = red[1 * BN + tid] + red[3 * BN + tid];
+            float a = 0.f, q = 0.f;
+#pragma unroll
+            for (int w = 0; w < WAVES_M; ++w) {
+                a += red[(w * 2 + 0) * BN + tid];
+                q += red[(w * 2 + 1) * BN + tid];
+            }
             p.stats[(size_t)tile_m * 2 * p.N + n0 + tid] = a;
             p.stats[(size_t)tile_m * 2 * p.N + p.N + n0 + tid] = q;
         }
@@ -398,34 +414,60 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
 // ------------------------------------------------------------------------------------
 // host dispatch
 // ------------------------------------------------------------------------------------
-template <int AMODE, bool AFFINE, int EMODE>
-static int rowgemm_tile(const RowGemmArgs& a, int bn, dim3 grid, hipStream_t s) {
-    if (bn == 128)
-        hipLaunchKernelGGL((rowgemm_kernel<AMODE, AFFINE, EMODE, 128, 128>), grid, dim3(256), 0, s, a);
-    else if (bn == 64)
-        hipLaunchKernelGGL((rowgemm_kernel<AMODE, AFFINE, EMODE, 128, 64>), grid, dim3(256), 0, s, a);
-    else
-        return -1;
+// Tile table (tuned on MI355X with tools/gemm_tune.hip).  The runtime picks a tile id per
+// layer; ROWGEMM_TILES lists what is instantiated.
+using RowTile0 = RowTile<128, 128, 64, 64, 32, true>;
+using RowTile1 = RowTile<128, 64, 64, 32, 32, false>;
+using RowTile2 = RowTile<256, 64, 64, 64, 32, false>;
+using RowTile3 = RowTile<128, 128, 64, 64, 64, false>;
+using RowTile4 = RowTile<128, 128, 64, 64, 32, false>;
+using RowTile5 = RowTile<256, 128, 64, 64, 32, false>;
+#define ROWGEMM_TILES(X) \
+    X(0, RowTile0) X(1, RowTile1) X(2, RowTile2) X(3, RowTile3) X(4, RowTile4) X(5, RowTile5)
+
+template <int AMODE, bool AFFINE, int EMODE, class T>
+static int rowgemm_go(const RowGemmArgs& a, hipStream_t s) {
+    if (a.N % T::BN || a.K % T::BK || a.C % T::BK) return -1;
+    if (EMODE == E_CONVT && (a.cout % T::BN)) return -1;
+    const dim3 grid(((a.M + T::BM - 1) / T::BM) * (a.N / T::BN));
+    hipLaunchKernelGGL((rowgemm_kernel<AMODE, AFFINE, EMODE, T>), grid, dim3(T::THREADS), 0, s, a);
     return (int)hipGetLastError();
 }
 
-int launch_rowgemm(const RowGemmArgs& a, int bm, int bn, hipStream_t s) {
-    constexpr int BK = 32;
-    if (bm != 128 || a.M < 1 || a.N % bn || a.K % BK || a.C % BK ||
-        a.K != gather_taps(a.amode) * a.C)
-        return -1;
-    if (a.emode == E_CONVT && (a.cout % bn)) return -1;
-    const dim3 grid(((a.M + bm - 1) / bm) * (a.N / bn));
+template <int AMODE, bool AFFINE, int EMODE>
+static int rowgemm_tile(const RowGemmArgs& a, int tile, hipStream_t s) {
+#define RG_CASE(id, T) \
+    if (tile == id) return rowgemm_go<AMODE, AFFINE, EMODE, T>(a, s);
+    ROWGEMM_TILES(RG_CASE)
+#undef RG_CASE
+    return -1;
+}
+
+int rowgemm_tile_dims(int tile, int* bm, int* bn, int* bk) {
+#define RG_DIMS(id, T)   \
+    if (tile == id) {    \
+        *bm = T::BM;     \
+        *bn = T::BN;     \
+        *bk = T::BK;     \
+        return 0;        \
+    }
+    ROWGEMM_TILES(RG_DIMS)
+#undef RG_DIMS
+    return -1;
+}
+
+int launch_rowgemm(const RowGemmArgs& a, int tile, hipStream_t s) {
+    if (a.M < 1 || a.K != gather_taps(a.amode) * a.C) return -1;
     const bool aff = a.ascale != nullptr;
     if (a.amode == G_CONV3 && a.emode == E_BIAS_RELU_STATS)
-        return aff ? rowgemm_tile<G_CONV3, true, E_BIAS_RELU_STATS>(a, bn, grid, s)
-                   : rowgemm_tile<G_CONV3, false, E_BIAS_RELU_STATS>(a, bn, grid, s);
+        return aff ? rowgemm_tile<G_CONV3, true, E_BIAS_RELU_STATS>(a, tile, s)
+                   : rowgemm_tile<G_CONV3, false, E_BIAS_RELU_STATS>(a, tile, s);
     if (a.amode == G_CONV3 && a.emode == E_STORE && !aff)
-        return rowgemm_tile<G_CONV3, false, E_STORE>(a, bn, grid, s);
+        return rowgemm_tile<G_CONV3, false, E_STORE>(a, tile, s);
     if (a.amode == G_IDENT && a.emode == E_CONVT && aff)
-        return rowgemm_tile<G_IDENT, true, E_CONVT>(a, bn, grid, s);
+        return rowgemm_tile<G_IDENT, true, E_CONVT>(a, tile, s);
     if (a.amode == G_UP2 && a.emode == E_STORE && !aff)
-        return rowgemm_tile<G_UP2, false, E_STORE>(a, bn, grid, s);
+        return rowgemm_tile<G_UP2, false, E_STORE>(a, tile, s);
     return -1;  // combination not instantiated
 }
 

@@ -2,6 +2,7 @@
 // workspace plan (NHWC activations, zero-copy concat buffers, packed weights, backward
 // scratch) and the forward / backward / loss / optimizer orchestration on one HIP stream.
 #include <math.h>
+#include <stdlib.h>
 #include <stdarg.h>
 #include <stdio.h>
 #include <string.h>
@@ -303,7 +304,7 @@ void make_plan(unet_ctx* c, int N, int H, int W, bool training, char* base, Plan
     // BN-stat partials: rows = M / 128 of the row GEMM, or RED_G for the first conv
     int64_t srows = 0;
     for (int i = 0; i < NCONV; ++i) {
-        const int64_t r = std::max<int64_t>((p.P[c->conv[i].level] + 127) / 128, RED_G);
+        const int64_t r = std::max<int64_t>((p.P[c->conv[i].level] + 63) / 64, RED_G);
         srows = std::max(srows, r * 2 * c->conv[i].cout);
     }
     p.stats = b.take<float>(srows);
@@ -369,6 +370,27 @@ struct Launcher {
         return 0;
     }
 };
+
+// Row-GEMM tile choice for an output width N (tile ids: kernels_gemm.hip ROWGEMM_TILES).
+// UNET_TILE_N128 / UNET_TILE_N64 override the choice (tuning runs).
+int pick_tile(int N) {
+    static int t128 = -2, t64 = -2;
+    if (t128 == -2) {
+        const char* e = getenv("UNET_TILE_N128");
+        t128 = e ? atoi(e) : 0;
+        e = getenv("UNET_TILE_N64");
+        t64 = e ? atoi(e) : 1;
+    }
+    return N % 128 == 0 ? t128 : t64;
+}
+
+std::string tlabel(const char* fam, int tile, int layer) {
+    int bm = 0, bn = 0, bk = 0;
+    rowgemm_tile_dims(tile, &bm, &bn, &bk);
+    char b[112];
+    snprintf(b, sizeof b, "%s/rowgemm_%dx%dx%d|%d", fam, bm, bn, bk, layer);
+    return b;
+}
 
 // timing label "family/kernel-instance" (the instance is what rocprofv3 reports)
 std::string glabel(const char* fam, const char* kern, int bm, int bn, int layer = -1) {
@@ -493,10 +515,11 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
             g.bias = prm + C.b;
             g.stats = p.stats;
             g.emode = E_BIAS_RELU_STATS;
-            const int bn = C.cout % 128 == 0 ? 128 : 64;
-            R = (int)((M + 127) / 128);
-            RUN(glabel("conv_fwd", "rowgemm", 128, bn, i), 2.0 * M * C.cout * 9 * C.cin,
-                launch_rowgemm(g, 128, bn, s));
+            const int tile = pick_tile(C.cout);
+            int bm, bn, bk;
+            rowgemm_tile_dims(tile, &bm, &bn, &bk);
+            R = (int)((M + bm - 1) / bm);
+            RUN(tlabel("conv_fwd", tile, i), 2.0 * M * C.cout * 9 * C.cin, launch_rowgemm(g, tile, s));
         }
         return stats_finalize(c, L, p, i, R, M, training, prm, bn_run, bn_cnt);
     };
@@ -524,9 +547,8 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
         g.bias = prm + T.b;
         g.cout = T.cout;
         g.emode = E_CONVT;
-        const int bn = T.cout % 128 == 0 ? 128 : 64;
-        RUN(glabel("convT_fwd", "rowgemm", 128, bn, 100 + k), 2.0 * g.M * g.N * g.K,
-            launch_rowgemm(g, 128, bn, s));
+        const int tile = pick_tile(T.cout);
+        RUN(tlabel("convT_fwd", tile, 100 + k), 2.0 * g.M * g.N * g.K, launch_rowgemm(g, tile, s));
         return 0;
     };
 
@@ -631,9 +653,8 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
             g.ldo = ldx;
             g.ooff = 0;
             g.emode = E_STORE;
-            const int bn = C.cin % 128 == 0 ? 128 : 64;
-            RUN(glabel("conv_dgrad", "rowgemm", 128, bn, i), 2.0 * P * C.cout * 9 * C.cin,
-                launch_rowgemm(g, 128, bn, s));
+            const int tile = pick_tile(C.cin);
+            RUN(tlabel("conv_dgrad", tile, i), 2.0 * P * C.cout * 9 * C.cin, launch_rowgemm(g, tile, s));
         }
         return 0;
     };
@@ -689,9 +710,8 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         g.ldo = T.cin;
         g.ooff = 0;
         g.emode = E_STORE;
-        const int bn = T.cin % 128 == 0 ? 128 : 64;
-        RUN(glabel("convT_dgrad", "rowgemm", 128, bn, 100 + k), 2.0 * Pin * T.cin * 4 * T.cout,
-            launch_rowgemm(g, 128, bn, s));
+        const int tile = pick_tile(T.cin);
+        RUN(tlabel("convT_dgrad", tile, 100 + k), 2.0 * Pin * T.cin * 4 * T.cout, launch_rowgemm(g, tile, s));
         return 0;
     };
     auto bucket_done = [&](int b) {

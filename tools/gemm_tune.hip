@@ -1,0 +1,144 @@
+// Tile tuning harness for the implicit-GEMM conv kernels (run on the GPU box).
+// Includes kernels_gemm.hip directly, allocates one layer's operands with random data and
+// times every instantiated tile on it, interleaved over rounds in ONE process
+// (cdna_hip_programming.md §5.4 rule 24).  Prints TF/s per (shape, variant).
+//   build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/gemm_tune.hip -o gemm_tune
+#include <stdio.h>
+#include <stdlib.h>
+#include <vector>
+
+#include "../thyroid-nodule-image-segmentation-unet-ddti_amd/csrc/kernels_gemm.hip"
+
+#define CK(x)                                                                    \
+    do {                                                                         \
+        hipError_t e = (x);                                                      \
+        if (e != hipSuccess) {                                                   \
+            fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e)); \
+            exit(1);                                                             \
+        }                                                                        \
+    } while (0)
+
+__global__ void fill_rand(float* p, size_t n, unsigned seed, float scale) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        unsigned x = (unsigned)i * 2654435761u ^ seed;
+        x ^= x >> 13; x *= 0x5bd1e995u; x ^= x >> 15;
+        p[i] = scale * ((x & 0xFFFFFF) / 16777216.0f - 0.5f);
+    }
+}
+
+static float* dalloc(size_t n, unsigned seed, float scale) {
+    float* p;
+    CK(hipMalloc(&p, n * sizeof(float)));
+    hipLaunchKernelGGL(fill_rand, dim3(4096), dim3(256), 0, 0, p, n, seed, scale);
+    return p;
+}
+
+struct Shape { const char* name; int N, H, W, Cin, Cout; };
+
+int main(int argc, char** argv) {
+    const int rounds = argc > 1 ? atoi(argv[1]) : 3;
+    const int iters = 5;
+    Shape shapes[] = {
+        {"L0 64->64 @256", 32, 256, 256, 64, 64},
+        {"L0 128->64 @256", 32, 256, 256, 128, 64},
+        {"L1 128->128 @128", 32, 128, 128, 128, 128},
+        {"L2 256->256 @64", 32, 64, 64, 256, 256},
+        {"L3 512->512 @32", 32, 32, 32, 512, 512},
+        {"L4 1024->1024 @16", 32, 16, 16, 1024, 1024},
+    };
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    for (const Shape& sh : shapes) {
+        const int M = sh.N * sh.H * sh.W;
+        float* x = dalloc((size_t)M * sh.Cin, 1, 2.f);
+        float* w = dalloc((size_t)sh.Cout * 9 * sh.Cin, 2, 0.1f);
+        float* sc = dalloc(sh.Cin, 3, 1.f);
+        float* shf = dalloc(sh.Cin, 4, 1.f);
+        float* bias = dalloc(sh.Cout, 5, 1.f);
+        float* y = dalloc((size_t)M * sh.Cout, 6, 0.f);
+        float* st = dalloc((size_t)(M / 64 + 1) * 2 * sh.Cout, 7, 0.f);
+        float* dz = dalloc((size_t)M * sh.Cout, 8, 1.f);
+        const double flop = 2.0 * M * sh.Cout * 9.0 * sh.Cin;
+        // forward (CONV3 + affine + stats) per tile, dgrad (CONV3 store) per tile
+        std::vector<std::vector<double>> best(2, std::vector<double>(6, 0));
+        for (int r = 0; r < rounds; ++r) {
+            for (int tile = 0; tile < 6; ++tile) {
+                for (int op = 0; op < 2; ++op) {
+                    RowGemmArgs g{};
+                    g.H = sh.H; g.W = sh.W; g.M = M;
+                    if (op == 0) {
+                        g.N = sh.Cout; g.K = 9 * sh.Cin; g.a = x; g.lda = sh.Cin; g.C = sh.Cin;
+                        g.ascale = sc; g.ashift = shf; g.emode = E_BIAS_RELU_STATS; g.bias = bias;
+                        g.stats = st; g.out = y; g.ldo = sh.Cout;
+                    } else {
+                        g.N = sh.Cin; g.K = 9 * sh.Cout; g.a = dz; g.lda = sh.Cout; g.C = sh.Cout;
+                        g.emode = E_STORE; g.out = x; g.ldo = sh.Cin;
+                    }
+                    g.amode = G_CONV3; g.bt = w;
+                    if (launch_rowgemm(g, tile, 0) != 0) continue;
+                    CK(hipEventRecord(e0, 0));
+                    for (int it = 0; it < iters; ++it) launch_rowgemm(g, tile, 0);
+                    CK(hipEventRecord(e1, 0));
+                    CK(hipEventSynchronize(e1));
+                    float ms;
+                    CK(hipEventElapsedTime(&ms, e0, e1));
+                    const double tf = flop * iters / (ms * 1e-3) / 1e12;
+                    if (tf > best[op][tile]) best[op][tile] = tf;
+                }
+            }
+            // wgrad tiles
+        }
+        for (int op = 0; op < 2; ++op) {
+            printf("%-20s %-5s", sh.name, op ? "dgrad" : "fwd");
+            for (int tile = 0; tile < 6; ++tile) printf("  t%d %6.1f", tile, best[op][tile]);
+            printf("\n");
+        }
+        // wgrad
+        const int bms[4] = {128, 64, 128, 64}, bns[4] = {128, 64, 64, 128};
+        double wb[4] = {0, 0, 0, 0};
+        int wsplit[4] = {0, 0, 0, 0};
+        float* slab = nullptr;
+        size_t slab_n = 0;
+        for (int r = 0; r < rounds; ++r)
+            for (int v = 0; v < 4; ++v) {
+                const int bm = bms[v], bn = bns[v];
+                if (sh.Cin % bm || sh.Cout % bn) continue;
+                const long tiles = (long)(9 * sh.Cin / bm) * (sh.Cout / bn);
+                long sp = (2048 + tiles - 1) / tiles;
+                if (sp > M / 256) sp = M / 256;
+                if (sp < 1) sp = 1;
+                long pps = ((M + sp - 1) / sp + 31) / 32 * 32;
+                const int splits = (int)((M + pps - 1) / pps);
+                const size_t need = (size_t)splits * 9 * sh.Cin * sh.Cout;
+                if (need > slab_n) {
+                    if (slab) CK(hipFree(slab));
+                    CK(hipMalloc(&slab, need * 4));
+                    slab_n = need;
+                }
+                WgradArgs a{};
+                a.H = sh.H; a.W = sh.W; a.P = M; a.a = x; a.lda = sh.Cin; a.CA = sh.Cin;
+                a.amode = G_CONV3; a.ascale = sc; a.ashift = shf; a.b = dz; a.ldb = sh.Cout;
+                a.CB = sh.Cout; a.bmode = G_IDENT; a.Mw = 9 * sh.Cin; a.Nw = sh.Cout;
+                a.pps = (int)pps; a.splits = splits; a.slab = slab;
+                if (launch_wgrad(a, bm, bn, 0) != 0) continue;
+                CK(hipEventRecord(e0, 0));
+                for (int it = 0; it < iters; ++it) launch_wgrad(a, bm, bn, 0);
+                CK(hipEventRecord(e1, 0));
+                CK(hipEventSynchronize(e1));
+                float ms;
+                CK(hipEventElapsedTime(&ms, e0, e1));
+                const double tf = flop * iters / (ms * 1e-3) / 1e12;
+                if (tf > wb[v]) wb[v] = tf;
+                wsplit[v] = splits;
+            }
+        printf("%-20s wgrad", sh.name);
+        for (int v = 0; v < 4; ++v) printf("  %dx%d/s%d %6.1f", bms[v], bns[v], wsplit[v], wb[v]);
+        printf("\n");
+        fflush(stdout);
+        CK(hipFree(x)); CK(hipFree(w)); CK(hipFree(sc)); CK(hipFree(shf)); CK(hipFree(bias));
+        CK(hipFree(y)); CK(hipFree(st)); CK(hipFree(dz));
+        if (slab) CK(hipFree(slab));
+    }
+    return 0;
+}
