@@ -66,4 +66,8 @@ struct WgradArgs {
 // tile ids: 0 = 128x128 (DBUF), 1 = 128x64, 2 = 256x64, 3 = 128x128 BK64 (kernels_gemm.hip)
 int launch_rowgemm(const RowGemmArgs& a, int tile, hipStream_t s);
 int rowgemm_tile_dims(int tile, int* bm, int* bn, int* bk);
-int launch_wgrad(const WgradArgs& a, int bm, int bn, hipStream_t s);
+int rowgemm_tile_dbuf(int tile);
+// wgrad tile ids: 0 = 128x128/32px, 1 = 64x64/128px, 2 = 128x64/64px, 3 = 64x128/64px,
+// 4 = 64x64/32px, 5 = 128x64/32px
+int launch_wgrad(const WgradArgs& a, int tile, hipStream_t s);
+int wgrad_tile_dims(int tile, int* bm, int* bn, int* bkp);

@@ -280,9 +280,14 @@ __global__ __launch_bounds__(T::THREADS, 1) void rowgemm_kernel(RowGemmArgs p) {
 // ------------------------------------------------------------------------------------
 // Weight-gradient GEMM (reduction over pixels), same issue / compute / commit pipeline.
 // ------------------------------------------------------------------------------------
-template <int AMODE, bool AFFINE, int BMODE, int BM, int BN>
-__global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
-    constexpr int BKP = 32;
+template <int BM_, int BN_, int BKP_>
+struct WgTile {
+    static constexpr int BM = BM_, BN = BN_, BKP = BKP_;
+};
+
+template <int AMODE, bool AFFINE, int BMODE, class T>
+__global__ __launch_bounds__(256, 1) void wgrad_kernel(WgradArgs p) {
+    constexpr int BM = T::BM, BN = T::BN, BKP = T::BKP;
     constexpr int WM = BM / 2, WN = BN / 2;
     constexpr int LDA = BM + 4, LDB = BN + 4;
     constexpr int MT = WM / 32, NT = WN / 32;
@@ -456,6 +461,14 @@ int rowgemm_tile_dims(int tile, int* bm, int* bn, int* bk) {
     return -1;
 }
 
+int rowgemm_tile_dbuf(int tile) {
+#define RG_DB(id, T) \
+    if (tile == id) return T::DBUF ? 1 : 0;
+    ROWGEMM_TILES(RG_DB)
+#undef RG_DB
+    return 0;
+}
+
 int launch_rowgemm(const RowGemmArgs& a, int tile, hipStream_t s) {
     if (a.M < 1 || a.K != gather_taps(a.amode) * a.C) return -1;
     const bool aff = a.ascale != nullptr;
@@ -471,31 +484,52 @@ int launch_rowgemm(const RowGemmArgs& a, int tile, hipStream_t s) {
     return -1;  // combination not instantiated
 }
 
-template <int AMODE, bool AFFINE, int BMODE>
-static int wgrad_tile(const WgradArgs& a, int bm, int bn, dim3 grid, hipStream_t s) {
-#define WG_CASE(M_, N_)                                                                    \
-    if (bm == M_ && bn == N_) {                                                            \
-        hipLaunchKernelGGL((wgrad_kernel<AMODE, AFFINE, BMODE, M_, N_>), grid, dim3(256), 0, \
-                           s, a);                                                          \
-        return (int)hipGetLastError();                                                     \
+// wgrad tiles: (BM, BN, pixels per chunk).  Narrow tiles take deeper pixel chunks so the
+// per-chunk staging cost is spread over as many MFMAs as the 128x128 tile's.
+using WgTile0 = WgTile<128, 128, 32>;
+using WgTile1 = WgTile<64, 64, 128>;
+using WgTile2 = WgTile<128, 64, 64>;
+using WgTile3 = WgTile<64, 128, 64>;
+using WgTile4 = WgTile<64, 64, 32>;
+using WgTile5 = WgTile<128, 64, 32>;
+#define WGRAD_TILES(X) \
+    X(0, WgTile0) X(1, WgTile1) X(2, WgTile2) X(3, WgTile3) X(4, WgTile4) X(5, WgTile5)
+
+int wgrad_tile_dims(int tile, int* bm, int* bn, int* bkp) {
+#define WG_DIMS(id, T) \
+    if (tile == id) {  \
+        *bm = T::BM;   \
+        *bn = T::BN;   \
+        *bkp = T::BKP; \
+        return 0;      \
     }
-    WG_CASE(128, 128)
-    WG_CASE(64, 64)
-    WG_CASE(128, 64)
-    WG_CASE(64, 128)
+    WGRAD_TILES(WG_DIMS)
+#undef WG_DIMS
+    return -1;
+}
+
+template <int AMODE, bool AFFINE, int BMODE>
+static int wgrad_tile(const WgradArgs& a, int tile, hipStream_t s) {
+#define WG_CASE(id, T)                                                                        \
+    if (tile == id) {                                                                         \
+        if (a.Mw % T::BM || a.Nw % T::BN || a.CA % T::BM || a.CB % T::BN || a.pps % T::BKP) \
+            return -1;                                                                        \
+        const dim3 grid((a.Mw / T::BM) * (a.Nw / T::BN) * a.splits);                          \
+        hipLaunchKernelGGL((wgrad_kernel<AMODE, AFFINE, BMODE, T>), grid, dim3(256), 0, s, a); \
+        return (int)hipGetLastError();                                                        \
+    }
+    WGRAD_TILES(WG_CASE)
 #undef WG_CASE
     return -1;
 }
 
-int launch_wgrad(const WgradArgs& a, int bm, int bn, hipStream_t s) {
-    constexpr int BKP = 32;
-    if (a.Mw % bm || a.Nw % bn || a.CA % bm || a.CB % bn || a.P < 1 || a.pps % BKP) return -1;
-    const dim3 grid((a.Mw / bm) * (a.Nw / bn) * a.splits);
+int launch_wgrad(const WgradArgs& a, int tile, hipStream_t s) {
+    if (a.P < 1) return -1;
     const bool aff = a.ascale != nullptr;
     if (a.amode == G_CONV3 && a.bmode == G_IDENT)
-        return aff ? wgrad_tile<G_CONV3, true, G_IDENT>(a, bm, bn, grid, s)
-                   : wgrad_tile<G_CONV3, false, G_IDENT>(a, bm, bn, grid, s);
+        return aff ? wgrad_tile<G_CONV3, true, G_IDENT>(a, tile, s)
+                   : wgrad_tile<G_CONV3, false, G_IDENT>(a, tile, s);
     if (a.amode == G_IDENT && a.bmode == G_UP2 && aff)
-        return wgrad_tile<G_IDENT, true, G_UP2>(a, bm, bn, grid, s);
+        return wgrad_tile<G_IDENT, true, G_UP2>(a, tile, s);
     return -1;
 }

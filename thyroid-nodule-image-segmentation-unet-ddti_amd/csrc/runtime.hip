@@ -245,21 +245,35 @@ struct Bump {
 };
 
 struct WgradCfg {
-    int bm, bn, splits, pps;
+    int tile, bm, bn, bkp, splits, pps;
 };
 
+// wgrad tile (kernels_gemm.hip WGRAD_TILES) + split-K over pixels so that every layer
+// launches >= 2048 blocks; UNET_WGRAD_TILE_{W,N} override (tuning runs).
 WgradCfg wgrad_cfg(int CA, int tapsA, int CB, int tapsB, int64_t P) {
+    static int tw = -2, tn = -2;
+    if (tw == -2) {
+        const char* e = getenv("UNET_WGRAD_TILE_W");
+        tw = e ? atoi(e) : 0;
+        e = getenv("UNET_WGRAD_TILE_N");
+        tn = e ? atoi(e) : 1;
+    }
     WgradCfg w;
-    w.bm = CA % 128 == 0 ? 128 : 64;
-    w.bn = CB % 128 == 0 ? 128 : 64;
+    if (CA % 128 == 0 && CB % 128 == 0)
+        w.tile = tw;
+    else if (CA % 64 == 0 && CB % 64 == 0 && (CA % 128 || CB % 128) && tn >= 0)
+        w.tile = (CA % 128 == 0) ? 2 : (CB % 128 == 0 ? 3 : tn);
+    else
+        w.tile = 4;
+    wgrad_tile_dims(w.tile, &w.bm, &w.bn, &w.bkp);
     const int64_t tiles = (int64_t)(tapsA * CA / w.bm) * (tapsB * CB / w.bn);
     int64_t s = (2048 + tiles - 1) / tiles;
-    const int64_t maxs = P / 256 > 0 ? P / 256 : 1;  // keep >= 8 pixel chunks per split
-    // (P need not be a multiple of the 32-pixel chunk: the kernel zero-fills the tail)
+    const int64_t maxs = P / (8 * w.bkp) > 0 ? P / (8 * w.bkp) : 1;  // >= 8 chunks per split
+    // (P need not be a multiple of the pixel chunk: the kernel zero-fills the tail)
     if (s > maxs) s = maxs;
     if (s < 1) s = 1;
     int64_t pps = (P + s - 1) / s;
-    pps = (pps + 31) / 32 * 32;
+    pps = (pps + 127) / 128 * 128;
     w.pps = (int)pps;
     w.splits = (int)((P + pps - 1) / pps);
     return w;
@@ -373,22 +387,33 @@ struct Launcher {
 
 // Row-GEMM tile choice for an output width N (tile ids: kernels_gemm.hip ROWGEMM_TILES).
 // UNET_TILE_N128 / UNET_TILE_N64 override the choice (tuning runs).
-int pick_tile(int N) {
-    static int t128 = -2, t64 = -2;
+// Defaults from tools/gemm_tune (r01): forward-type ops 128x128/BK32 single LDS image
+// (4 waves/SIMD), dgrad-type 128x128 double-buffered, N = 64 outputs 128x64.
+int pick_tile(int N, bool dgrad = false) {
+    static int t128 = -2, t128d = -2, t64 = -2;
     if (t128 == -2) {
         const char* e = getenv("UNET_TILE_N128");
-        t128 = e ? atoi(e) : 0;
+        t128 = e ? atoi(e) : 4;
+        e = getenv("UNET_TILE_N128_DGRAD");
+        t128d = e ? atoi(e) : 0;
         e = getenv("UNET_TILE_N64");
         t64 = e ? atoi(e) : 1;
     }
-    return N % 128 == 0 ? t128 : t64;
+    return N % 128 == 0 ? (dgrad ? t128d : t128) : t64;
 }
 
 std::string tlabel(const char* fam, int tile, int layer) {
     int bm = 0, bn = 0, bk = 0;
     rowgemm_tile_dims(tile, &bm, &bn, &bk);
     char b[112];
-    snprintf(b, sizeof b, "%s/rowgemm_%dx%dx%d|%d", fam, bm, bn, bk, layer);
+    snprintf(b, sizeof b, "%s/rowgemm_%dx%dx%d%s|%d", fam, bm, bn, bk,
+             rowgemm_tile_dbuf(tile) ? "d" : "", layer);
+    return b;
+}
+
+std::string wlabel(const char* fam, const WgradCfg& w, int layer) {
+    char b[112];
+    snprintf(b, sizeof b, "%s/wgrad_%dx%dx%d|%d", fam, w.bm, w.bn, w.bkp, layer);
     return b;
 }
 
@@ -632,8 +657,8 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         w.pps = wc.pps;
         w.splits = wc.splits;
         w.slab = p.slab;
-        RUN(glabel("conv_wgrad", "wgrad", wc.bm, wc.bn, i), 2.0 * P * C.cout * 9 * C.cin,
-            launch_wgrad(w, wc.bm, wc.bn, s));
+        RUN(wlabel("conv_wgrad", wc, i), 2.0 * P * C.cout * 9 * C.cin,
+            launch_wgrad(w, wc.tile, s));
         RUN("wgrad_reduce", 0,
             k_slab_reduce(p.slab, wc.splits, w.Mw, w.Nw, 0, C.cin, C.cout, grads + C.w, s));
         if (dx) {
@@ -653,7 +678,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
             g.ldo = ldx;
             g.ooff = 0;
             g.emode = E_STORE;
-            const int tile = pick_tile(C.cin);
+            const int tile = pick_tile(C.cin, true);
             RUN(tlabel("conv_dgrad", tile, i), 2.0 * P * C.cout * 9 * C.cin, launch_rowgemm(g, tile, s));
         }
         return 0;
@@ -690,8 +715,8 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         w.pps = wc.pps;
         w.splits = wc.splits;
         w.slab = p.slab;
-        RUN(glabel("convT_wgrad", "wgrad", wc.bm, wc.bn, 100 + k), 2.0 * Pin * T.cin * 4 * T.cout,
-            launch_wgrad(w, wc.bm, wc.bn, s));
+        RUN(wlabel("convT_wgrad", wc, 100 + k), 2.0 * Pin * T.cin * 4 * T.cout,
+            launch_wgrad(w, wc.tile, s));
         RUN("wgrad_reduce", 0,
             k_slab_reduce(p.slab, wc.splits, w.Mw, w.Nw, 1, T.cin, T.cout, grads + T.w, s));
         RowGemmArgs g{};
@@ -710,7 +735,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         g.ldo = T.cin;
         g.ooff = 0;
         g.emode = E_STORE;
-        const int tile = pick_tile(T.cin);
+        const int tile = pick_tile(T.cin, true);
         RUN(tlabel("convT_dgrad", tile, 100 + k), 2.0 * Pin * T.cin * 4 * T.cout, launch_rowgemm(g, tile, s));
         return 0;
     };

@@ -94,21 +94,21 @@ int main(int argc, char** argv) {
             for (int tile = 0; tile < 6; ++tile) printf("  t%d %6.1f", tile, best[op][tile]);
             printf("\n");
         }
-        // wgrad
-        const int bms[4] = {128, 64, 128, 64}, bns[4] = {128, 64, 64, 128};
-        double wb[4] = {0, 0, 0, 0};
-        int wsplit[4] = {0, 0, 0, 0};
+        // wgrad over the tile table
+        double wb[6] = {0, 0, 0, 0, 0, 0};
+        int wsplit[6] = {0, 0, 0, 0, 0, 0};
         float* slab = nullptr;
         size_t slab_n = 0;
         for (int r = 0; r < rounds; ++r)
-            for (int v = 0; v < 4; ++v) {
-                const int bm = bms[v], bn = bns[v];
+            for (int v = 0; v < 6; ++v) {
+                int bm, bn, bkp;
+                wgrad_tile_dims(v, &bm, &bn, &bkp);
                 if (sh.Cin % bm || sh.Cout % bn) continue;
                 const long tiles = (long)(9 * sh.Cin / bm) * (sh.Cout / bn);
                 long sp = (2048 + tiles - 1) / tiles;
-                if (sp > M / 256) sp = M / 256;
+                if (sp > M / (8 * bkp)) sp = M / (8 * bkp);
                 if (sp < 1) sp = 1;
-                long pps = ((M + sp - 1) / sp + 31) / 32 * 32;
+                long pps = ((M + sp - 1) / sp + 127) / 128 * 128;
                 const int splits = (int)((M + pps - 1) / pps);
                 const size_t need = (size_t)splits * 9 * sh.Cin * sh.Cout;
                 if (need > slab_n) {
@@ -121,9 +121,9 @@ int main(int argc, char** argv) {
                 a.amode = G_CONV3; a.ascale = sc; a.ashift = shf; a.b = dz; a.ldb = sh.Cout;
                 a.CB = sh.Cout; a.bmode = G_IDENT; a.Mw = 9 * sh.Cin; a.Nw = sh.Cout;
                 a.pps = (int)pps; a.splits = splits; a.slab = slab;
-                if (launch_wgrad(a, bm, bn, 0) != 0) continue;
+                if (launch_wgrad(a, v, 0) != 0) continue;
                 CK(hipEventRecord(e0, 0));
-                for (int it = 0; it < iters; ++it) launch_wgrad(a, bm, bn, 0);
+                for (int it = 0; it < iters; ++it) launch_wgrad(a, v, 0);
                 CK(hipEventRecord(e1, 0));
                 CK(hipEventSynchronize(e1));
                 float ms;
@@ -133,7 +133,7 @@ int main(int argc, char** argv) {
                 wsplit[v] = splits;
             }
         printf("%-20s wgrad", sh.name);
-        for (int v = 0; v < 4; ++v) printf("  %dx%d/s%d %6.1f", bms[v], bns[v], wsplit[v], wb[v]);
+        for (int v = 0; v < 6; ++v) printf("  w%d/s%d %6.1f", v, wsplit[v], wb[v]);
         printf("\n");
         fflush(stdout);
         CK(hipFree(x)); CK(hipFree(w)); CK(hipFree(sc)); CK(hipFree(shf)); CK(hipFree(bias));

@@ -22,9 +22,13 @@ from collections import defaultdict
 
 
 def short(name):
-    m = re.search(r"(rowgemm|wgrad)_kernel<(\d+), (\d+)", name)
+    """rocprofv3 kernel name -> bench.py label (rowgemm_BMxBNxBK / wgrad_BMxBNxBKP)."""
+    m = re.search(r"RowTile<(\d+), (\d+), \d+, \d+, (\d+), (true|false)", name)
     if m:
-        return f"{m.group(1)}_{m.group(2)}x{m.group(3)}"
+        return f"rowgemm_{m.group(1)}x{m.group(2)}x{m.group(3)}{'d' if m.group(4) == 'true' else ''}"
+    m = re.search(r"WgTile<(\d+), (\d+), (\d+)", name)
+    if m:
+        return f"wgrad_{m.group(1)}x{m.group(2)}x{m.group(3)}"
     m = re.search(r"::(\w+?)_kernel", name)
     return m.group(1) if m else name[:60]
 
