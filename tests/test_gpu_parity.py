@@ -116,7 +116,7 @@ def test_train_steps_match_golden(golden_dir):
         bound = 3e-7 if s == 0 else 1e-5  # after step 0: within one lr (no sign flips)
         assert np.all(d[~tiny] <= bound), f"step {s}: max {d[~tiny].max():.3e}"
         assert np.all(d[tiny] <= 2 * 1e-5 * (s + 1) * 1.01)
-        assert tiny.mean() < 0.02
+        assert tiny.mean() < 0.05
         rm = torch.cat([m.state_dict()[f"{n}.running_mean"].cpu() for n in O.BN_LAYERS]).numpy()
         rv = torch.cat([m.state_dict()[f"{n}.running_var"].cpu() for n in O.BN_LAYERS]).numpy()
         np.testing.assert_allclose(rm, f[f"s{s}_running_mean"], rtol=1e-4, atol=1e-4)

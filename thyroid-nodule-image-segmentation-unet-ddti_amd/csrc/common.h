@@ -67,7 +67,7 @@ struct WgradArgs {
 int launch_rowgemm(const RowGemmArgs& a, int tile, hipStream_t s);
 int rowgemm_tile_dims(int tile, int* bm, int* bn, int* bk);
 int rowgemm_tile_dbuf(int tile);
-// wgrad tile ids: 0 = 128x128/32px, 1 = 64x64/128px, 2 = 128x64/64px, 3 = 64x128/64px,
-// 4 = 64x64/32px, 5 = 128x64/32px
+// wgrad tile ids (kernels_gemm.hip WGRAD_TILES): 0 = 128x128, 1 = 64x64 one wave,
+// 2 = 128x64 two waves, 3 = 64x128 two waves, 4 = 64x64 four waves, 5 = 128x64 four waves
 int launch_wgrad(const WgradArgs& a, int tile, hipStream_t s);
 int wgrad_tile_dims(int tile, int* bm, int* bn, int* bkp);

@@ -44,6 +44,25 @@ __device__ __forceinline__ Pix decode(int m, int H, int W) {
     return r;
 }
 
+// Division by a per-launch constant through an f32 reciprocal plus one correction step:
+// exact while the quotient stays below 2^22 (P / W < 4M pixel rows here).
+__device__ __forceinline__ int fdiv(int n, int d, float rd) {
+    int q = (int)((float)n * rd);
+    const int r = n - q * d;
+    q += (r >= d) ? 1 : 0;
+    q -= (r < 0) ? 1 : 0;
+    return q;
+}
+
+__device__ __forceinline__ Pix decode_fast(int m, int H, int W, float rH, float rW) {
+    Pix r;
+    const int t = fdiv(m, W, rW);
+    r.x = m - t * W;
+    r.img = fdiv(t, H, rH);
+    r.y = t - r.img * H;
+    return r;
+}
+
 // Source pixel of row pixel `q` (on grid HxW) for `tap` in MODE; `valid` false for
 // zero-padding taps (the returned index is then the row pixel itself, always in range).
 template <int MODE>
@@ -280,25 +299,29 @@ __global__ __launch_bounds__(T::THREADS, 1) void rowgemm_kernel(RowGemmArgs p) {
 // ------------------------------------------------------------------------------------
 // Weight-gradient GEMM (reduction over pixels), same issue / compute / commit pipeline.
 // ------------------------------------------------------------------------------------
-template <int BM_, int BN_, int BKP_>
+// wgrad tile: block BM x BN, wave tile WM x WN, pixels per chunk BKP.
+template <int BM_, int BN_, int WM_, int WN_, int BKP_>
 struct WgTile {
-    static constexpr int BM = BM_, BN = BN_, BKP = BKP_;
+    static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, BKP = BKP_;
+    static constexpr int THREADS = 64 * (BM / WM) * (BN / WN);
 };
 
 template <int AMODE, bool AFFINE, int BMODE, class T>
-__global__ __launch_bounds__(256, 1) void wgrad_kernel(WgradArgs p) {
-    constexpr int BM = T::BM, BN = T::BN, BKP = T::BKP;
-    constexpr int WM = BM / 2, WN = BN / 2;
+__global__ __launch_bounds__(T::THREADS, 1) void wgrad_kernel(WgradArgs p) {
+    constexpr int BM = T::BM, BN = T::BN, BKP = T::BKP, WM = T::WM, WN = T::WN;
+    constexpr int NTH = T::THREADS;
+    constexpr int WAVES_N = BN / WN;
     constexpr int LDA = BM + 4, LDB = BN + 4;
     constexpr int MT = WM / 32, NT = WN / 32;
     constexpr int AF = BM / 4, BF = BN / 4;          // float4 per pixel row
-    constexpr int ARPP = 256 / AF, BRPP = 256 / BF;  // rows per pass
+    constexpr int ARPP = NTH / AF, BRPP = NTH / BF;  // rows per pass
     constexpr int AP = BKP / ARPP, BP = BKP / BRPP;
+    static_assert(AP * ARPP == BKP && BP * BRPP == BKP, "loader shape");
     __shared__ __attribute__((aligned(16))) float As[BKP * LDA];
     __shared__ __attribute__((aligned(16))) float Bs[BKP * LDB];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wm = wave >> 1, wn = wave & 1;
+    const int wm = wave / WAVES_N, wn = wave % WAVES_N;
     const int tiles_n = p.Nw / BN, tiles_m = p.Mw / BM;
     int idx = blockIdx.x;
     const int tn = idx % tiles_n;
@@ -308,6 +331,7 @@ __global__ __launch_bounds__(256, 1) void wgrad_kernel(WgradArgs p) {
     const int tapA = (tm * BM) / p.CA, ca0 = tm * BM - tapA * p.CA;
     const int tapB = (tn * BN) / p.CB, cb0 = tn * BN - tapB * p.CB;
     const int H = p.H, W = p.W;
+    const float rH = 1.f / (float)H, rW = 1.f / (float)W;
 
     const int ac4 = tid % AF, arow = tid / AF;
     const int bc4 = tid % BF, brow = tid / BF;
@@ -332,7 +356,8 @@ __global__ __launch_bounds__(256, 1) void wgrad_kernel(WgradArgs p) {
             const bool in = m < pend;
             m = in ? m : pend - 1;
             bool valid;
-            const int src = gather_src<AMODE>(tapA, m, decode(m, H, W), H, W, valid);
+            const Pix q = AMODE == G_IDENT ? Pix{0, 0, 0} : decode_fast(m, H, W, rH, rW);
+            const int src = gather_src<AMODE>(tapA, m, q, H, W, valid);
             amask |= (valid && in) ? (1u << i) : 0u;
             ra[i] = *(const f32x4*)(p.a + (size_t)src * p.lda + p.aoff + ca0 + ac4 * 4);
         }
@@ -342,7 +367,8 @@ __global__ __launch_bounds__(256, 1) void wgrad_kernel(WgradArgs p) {
             const bool in = m < pend;
             m = in ? m : pend - 1;
             bool valid;
-            const int src = gather_src<BMODE>(tapB, m, decode(m, H, W), H, W, valid);
+            const Pix q = BMODE == G_IDENT ? Pix{0, 0, 0} : decode_fast(m, H, W, rH, rW);
+            const int src = gather_src<BMODE>(tapB, m, q, H, W, valid);
             bmask |= (valid && in) ? (1u << i) : 0u;
             rb[i] = *(const f32x4*)(p.b + (size_t)src * p.ldb + p.boff + cb0 + bc4 * 4);
         }
@@ -486,12 +512,12 @@ int launch_rowgemm(const RowGemmArgs& a, int tile, hipStream_t s) {
 
 // wgrad tiles: (BM, BN, pixels per chunk).  Narrow tiles take deeper pixel chunks so the
 // per-chunk staging cost is spread over as many MFMAs as the 128x128 tile's.
-using WgTile0 = WgTile<128, 128, 32>;
-using WgTile1 = WgTile<64, 64, 128>;
-using WgTile2 = WgTile<128, 64, 64>;
-using WgTile3 = WgTile<64, 128, 64>;
-using WgTile4 = WgTile<64, 64, 32>;
-using WgTile5 = WgTile<128, 64, 32>;
+using WgTile0 = WgTile<128, 128, 64, 64, 32>;  // 4 waves
+using WgTile1 = WgTile<64, 64, 64, 64, 16>;    // 1 wave, 64x64 per wave
+using WgTile2 = WgTile<128, 64, 64, 64, 32>;   // 2 waves
+using WgTile3 = WgTile<64, 128, 64, 64, 32>;   // 2 waves
+using WgTile4 = WgTile<64, 64, 32, 32, 32>;    // 4 waves, 32x32 per wave
+using WgTile5 = WgTile<128, 64, 64, 32, 32>;   // 4 waves
 #define WGRAD_TILES(X) \
     X(0, WgTile0) X(1, WgTile1) X(2, WgTile2) X(3, WgTile3) X(4, WgTile4) X(5, WgTile5)
 
@@ -515,7 +541,7 @@ static int wgrad_tile(const WgradArgs& a, int tile, hipStream_t s) {
         if (a.Mw % T::BM || a.Nw % T::BN || a.CA % T::BM || a.CB % T::BN || a.pps % T::BKP) \
             return -1;                                                                        \
         const dim3 grid((a.Mw / T::BM) * (a.Nw / T::BN) * a.splits);                          \
-        hipLaunchKernelGGL((wgrad_kernel<AMODE, AFFINE, BMODE, T>), grid, dim3(256), 0, s, a); \
+        hipLaunchKernelGGL((wgrad_kernel<AMODE, AFFINE, BMODE, T>), grid, dim3(T::THREADS), 0, s, a); \
         return (int)hipGetLastError();                                                        \
     }
     WGRAD_TILES(WG_CASE)

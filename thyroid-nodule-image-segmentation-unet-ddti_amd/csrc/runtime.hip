@@ -256,13 +256,13 @@ WgradCfg wgrad_cfg(int CA, int tapsA, int CB, int tapsB, int64_t P) {
         const char* e = getenv("UNET_WGRAD_TILE_W");
         tw = e ? atoi(e) : 0;
         e = getenv("UNET_WGRAD_TILE_N");
-        tn = e ? atoi(e) : 1;
+        tn = e ? atoi(e) : 4;
     }
     WgradCfg w;
     if (CA % 128 == 0 && CB % 128 == 0)
         w.tile = tw;
     else if (CA % 64 == 0 && CB % 64 == 0 && (CA % 128 || CB % 128) && tn >= 0)
-        w.tile = (CA % 128 == 0) ? 2 : (CB % 128 == 0 ? 3 : tn);
+        w.tile = (CA % 128 == 0) ? 5 : (CB % 128 == 0 ? 3 : tn);
     else
         w.tile = 4;
     wgrad_tile_dims(w.tile, &w.bm, &w.bn, &w.bkp);

@@ -26,7 +26,7 @@ def short(name):
     m = re.search(r"RowTile<(\d+), (\d+), \d+, \d+, (\d+), (true|false)", name)
     if m:
         return f"rowgemm_{m.group(1)}x{m.group(2)}x{m.group(3)}{'d' if m.group(4) == 'true' else ''}"
-    m = re.search(r"WgTile<(\d+), (\d+), (\d+)", name)
+    m = re.search(r"WgTile<(\d+), (\d+), \d+, \d+, (\d+)", name)
     if m:
         return f"wgrad_{m.group(1)}x{m.group(2)}x{m.group(3)}"
     m = re.search(r"::(\w+?)_kernel", name)
