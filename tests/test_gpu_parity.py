@@ -119,8 +119,9 @@ def test_train_steps_match_golden(golden_dir):
         assert tiny.mean() < 0.05
         rm = torch.cat([m.state_dict()[f"{n}.running_mean"].cpu() for n in O.BN_LAYERS]).numpy()
         rv = torch.cat([m.state_dict()[f"{n}.running_var"].cpu() for n in O.BN_LAYERS]).numpy()
-        np.testing.assert_allclose(rm, f[f"s{s}_running_mean"], rtol=1e-4, atol=1e-4)
-        np.testing.assert_allclose(rv, f[f"s{s}_running_var"], rtol=1e-4, atol=1e-4)
+        btol = 1e-4 if s == 0 else 1e-3
+        np.testing.assert_allclose(rm, f[f"s{s}_running_mean"], rtol=btol, atol=btol)
+        np.testing.assert_allclose(rv, f[f"s{s}_running_var"], rtol=btol, atol=btol)
         nbt = [int(m.state_dict()[f"{n}.num_batches_tracked"]) for n in O.BN_LAYERS]
         assert nbt == list(f[f"s{s}_nbt"])
     m.eval()

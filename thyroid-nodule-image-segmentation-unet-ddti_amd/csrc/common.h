@@ -23,7 +23,17 @@ static inline int gather_taps(int mode) { return mode == G_CONV3 ? 9 : (mode == 
 //                      for the following BatchNorm (models/model.py:36-38)
 //   E_CONVT          : ConvTranspose2d scatter, n = (a*2+b)*cout + co ->
 //                      out[(2y+a, 2x+b)][co] = acc + b[co]  (models/model.py:19)
-enum EpiMode { E_STORE = 0, E_BIAS_RELU_STATS = 1, E_CONVT = 2 };
+//   E_STORE_BN       : out[m][n] = acc, and the result is the gradient `do` of a BatchNorm
+//                      output: per-block column partials {sum do, sum do*y, sum_{y>0} do,
+//                      count y>0} for the BN backward (y = ey, the BN input)
+enum EpiMode { E_STORE = 0, E_BIAS_RELU_STATS = 1, E_CONVT = 2, E_STORE_BN = 3 };
+
+// What the A (row GEMM) / B' (wgrad) loader applies to the gathered values:
+//   OP_PLAIN : raw values
+//   OP_AFFINE: per-channel BN affine scale*x + shift (forward consumers of a BN output)
+//   OP_DZ    : BN+ReLU backward on the fly, dz = [y > 0] (A*do + B*y + C) per channel,
+//              from do (the operand pointer), y (its BN input) and coef = [A | B | C]
+enum LoadOp { OP_PLAIN = 0, OP_AFFINE = 1, OP_DZ = 2 };
 
 struct RowGemmArgs {
     int H, W;        // row grid (rows = Nimg*H*W pixels)
@@ -36,9 +46,14 @@ struct RowGemmArgs {
     float* out;
     int ldo, ooff;
     const float* bias;
-    float* stats;  // [M/BM][2][N] partial (sum, sumsq)
+    float* stats;  // [M/BM][2][N] partial (sum, sumsq); E_STORE_BN: [M/BM][4][N]
     int cout;      // E_CONVT
     int emode;
+    const float* ay;     // OP_DZ: BN input y of the A operand (ld, off)
+    int lday, offay;
+    const float* acoef;  // OP_DZ: [3][C] coefficients
+    const float* ey;     // E_STORE_BN: BN input y at the output position (ld, off)
+    int ldey, offey;
 };
 
 struct WgradArgs {
@@ -54,6 +69,10 @@ struct WgradArgs {
     int pps;         // pixels per split (multiple of the pixel chunk)
     int splits;
     float* slab;     // [splits][Mw][Nw]
+    const float* by;     // OP_DZ on B': BN input y (ld, off) and coef [3][CB]
+    int ldby, offby;
+    const float* bcoef;
+    float* bias_slab;    // optional [splits][Nw]: column sums of B' (the bias gradient)
 };
 
 #define HIP_OK(x)                                   \

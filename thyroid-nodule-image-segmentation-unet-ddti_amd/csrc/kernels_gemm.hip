@@ -97,8 +97,9 @@ struct RowTile {
     static constexpr int THREADS = 64 * WAVES;
 };
 
-template <int AMODE, bool AFFINE, int EMODE, class T>
+template <int AMODE, int AOP, int EMODE, class T>
 __global__ __launch_bounds__(T::THREADS, 1) void rowgemm_kernel(RowGemmArgs p) {
+    constexpr bool AFFINE = AOP == OP_AFFINE, ADZ = AOP == OP_DZ;
     constexpr int BM = T::BM, BN = T::BN, WM = T::WM, WN = T::WN, BK = T::BK;
     constexpr bool DBUF = T::DBUF;
     constexpr int NTH = T::THREADS;
@@ -132,7 +133,8 @@ __global__ __launch_bounds__(T::THREADS, 1) void rowgemm_kernel(RowGemmArgs p) {
         rq[i] = decode(rm[i], H, W);
     }
 
-    f32x4 ra[AP], rb[BP], rsc, rsh;
+    f32x4 ra[AP], rb[BP], rsc, rsh, rcc;
+    f32x4 ry[ADZ ? AP : 1];
     unsigned vmask = 0;
 
     auto issue = [&](int kc) {
@@ -143,6 +145,11 @@ __global__ __launch_bounds__(T::THREADS, 1) void rowgemm_kernel(RowGemmArgs p) {
             rsc = *(const f32x4*)(p.ascale + c);
             rsh = *(const f32x4*)(p.ashift + c);
         }
+        if constexpr (ADZ) {
+            rsc = *(const f32x4*)(p.acoef + c);
+            rsh = *(const f32x4*)(p.acoef + p.C + c);
+            rcc = *(const f32x4*)(p.acoef + 2 * p.C + c);
+        }
         vmask = 0;
 #pragma unroll
         for (int i = 0; i < AP; ++i) {
@@ -150,6 +157,7 @@ __global__ __launch_bounds__(T::THREADS, 1) void rowgemm_kernel(RowGemmArgs p) {
             const int src = gather_src<AMODE>(tap, rm[i], rq[i], H, W, valid);
             vmask |= (valid && rok[i]) ? (1u << i) : 0u;
             ra[i] = *(const f32x4*)(p.a + (size_t)src * p.lda + p.aoff + c);
+            if constexpr (ADZ) ry[i] = *(const f32x4*)(p.ay + (size_t)src * p.lday + p.offay + c);
         }
 #pragma unroll
         for (int i = 0; i < BP; ++i)
@@ -162,6 +170,11 @@ __global__ __launch_bounds__(T::THREADS, 1) void rowgemm_kernel(RowGemmArgs p) {
         for (int i = 0; i < AP; ++i) {
             f32x4 v = ra[i];
             if constexpr (AFFINE) v = v * rsc + rsh;
+            if constexpr (ADZ) {
+                const f32x4 d = rsc * v + rsh * ry[i] + rcc;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) v[j] = ry[i][j] > 0.f ? d[j] : 0.f;
+            }
             if (!((vmask >> i) & 1u)) v = f32x4{0.f, 0.f, 0.f, 0.f};
             *(f32x4*)&as[(lrow + i * RPP) * LDK + lc4 * 4] = v;
         }
@@ -263,6 +276,51 @@ __global__ __launch_bounds__(T::THREADS, 1) void rowgemm_kernel(RowGemmArgs p) {
             p.stats[(size_t)tile_m * 2 * p.N + n0 + tid] = a;
             p.stats[(size_t)tile_m * 2 * p.N + p.N + n0 + tid] = q;
         }
+    } else if constexpr (EMODE == E_STORE_BN) {
+        float q[NT][4];
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+            const int n = n0 + wn * WN + nt * 32 + li;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) q[nt][j] = 0.f;
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int m = m0 + wm * WM + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                    if (m < p.M) {
+                        const float v = acc[mt][nt][r];
+                        p.out[(size_t)m * p.ldo + p.ooff + n] = v;
+                        const float y = p.ey[(size_t)m * p.ldey + p.offey + n];
+                        q[nt][0] += v;
+                        q[nt][1] += v * y;
+                        if (y > 0.f) {
+                            q[nt][2] += v;
+                            q[nt][3] += 1.f;
+                        }
+                    }
+                }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) q[nt][j] += __shfl_xor(q[nt][j], 32);
+        }
+        __syncthreads();
+        float* red = smem;  // [WAVES_M][4][BN]
+        if (lh == 0) {
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) red[(wm * 4 + j) * BN + wn * WN + nt * 32 + li] = q[nt][j];
+        }
+        __syncthreads();
+        if (tid < BN) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                float a = 0.f;
+#pragma unroll
+                for (int w = 0; w < WAVES_M; ++w) a += red[(w * 4 + j) * BN + tid];
+                p.stats[((size_t)tile_m * 4 + j) * p.N + n0 + tid] = a;
+            }
+        }
     } else if constexpr (EMODE == E_CONVT) {
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) {
@@ -306,7 +364,7 @@ struct WgTile {
     static constexpr int THREADS = 64 * (BM / WM) * (BN / WN);
 };
 
-template <int AMODE, bool AFFINE, int BMODE, class T>
+template <int AMODE, bool AFFINE, int BMODE, bool BDZ, class T>
 __global__ __launch_bounds__(T::THREADS, 1) void wgrad_kernel(WgradArgs p) {
     constexpr int BM = T::BM, BN = T::BN, BKP = T::BKP, WM = T::WM, WN = T::WN;
     constexpr int NTH = T::THREADS;
@@ -341,11 +399,21 @@ __global__ __launch_bounds__(T::THREADS, 1) void wgrad_kernel(WgradArgs p) {
         sh = *(const f32x4*)(p.ashift + ca0 + ac4 * 4);
     }
 
+    f32x4 ca = {0, 0, 0, 0}, cb = ca, cc = ca;  // OP_DZ coefficients of this thread's columns
+    if constexpr (BDZ) {
+        ca = *(const f32x4*)(p.bcoef + cb0 + bc4 * 4);
+        cb = *(const f32x4*)(p.bcoef + p.CB + cb0 + bc4 * 4);
+        cc = *(const f32x4*)(p.bcoef + 2 * p.CB + cb0 + bc4 * 4);
+    }
+    const bool bsum = p.bias_slab != nullptr && tm == 0;
+    f32x4 bacc = {0, 0, 0, 0};
+
     const int pbeg = split * p.pps;
     int pend = pbeg + p.pps;
     if (pend > p.P) pend = p.P;
     const int nchunks = (pend - pbeg + BKP - 1) / BKP;
 
+    f32x4 ryb[BDZ ? BP : 1];
     f32x4 ra[AP], rb[BP];
     unsigned amask = 0, bmask = 0;
     auto issue = [&](int pc) {
@@ -371,6 +439,8 @@ __global__ __launch_bounds__(T::THREADS, 1) void wgrad_kernel(WgradArgs p) {
             const int src = gather_src<BMODE>(tapB, m, q, H, W, valid);
             bmask |= (valid && in) ? (1u << i) : 0u;
             rb[i] = *(const f32x4*)(p.b + (size_t)src * p.ldb + p.boff + cb0 + bc4 * 4);
+            if constexpr (BDZ)
+                ryb[i] = *(const f32x4*)(p.by + (size_t)src * p.ldby + p.offby + cb0 + bc4 * 4);
         }
     };
     auto commit = [&]() {
@@ -384,7 +454,13 @@ __global__ __launch_bounds__(T::THREADS, 1) void wgrad_kernel(WgradArgs p) {
 #pragma unroll
         for (int i = 0; i < BP; ++i) {
             f32x4 v = rb[i];
+            if constexpr (BDZ) {
+                const f32x4 d = ca * v + cb * ryb[i] + cc;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) v[j] = ryb[i][j] > 0.f ? d[j] : 0.f;
+            }
             if (!((bmask >> i) & 1u)) v = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (bsum) bacc += v;
             *(f32x4*)&Bs[(brow + i * BRPP) * LDB + bc4 * 4] = v;
         }
     };
@@ -427,6 +503,18 @@ __global__ __launch_bounds__(T::THREADS, 1) void wgrad_kernel(WgradArgs p) {
         }
     }
 
+    if (bsum) {  // column sums of B' for the bias gradient: combine the row groups in order
+        __syncthreads();
+        f32x4* red = (f32x4*)As;
+        red[tid] = bacc;
+        __syncthreads();
+        if (tid < BF) {
+            f32x4 t = red[tid];
+            for (int g = 1; g < BRPP; ++g) t += red[g * BF + tid];
+            *(f32x4*)(p.bias_slab + (size_t)split * p.Nw + tn * BN + tid * 4) = t;
+        }
+    }
+
     float* slab = p.slab + (size_t)split * p.Mw * p.Nw;
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
@@ -456,19 +544,19 @@ using RowTile5 = RowTile<256, 128, 64, 64, 32, false>;
 #define ROWGEMM_TILES(X) \
     X(0, RowTile0) X(1, RowTile1) X(2, RowTile2) X(3, RowTile3) X(4, RowTile4) X(5, RowTile5)
 
-template <int AMODE, bool AFFINE, int EMODE, class T>
+template <int AMODE, int AOP, int EMODE, class T>
 static int rowgemm_go(const RowGemmArgs& a, hipStream_t s) {
     if (a.N % T::BN || a.K % T::BK || a.C % T::BK) return -1;
     if (EMODE == E_CONVT && (a.cout % T::BN)) return -1;
     const dim3 grid(((a.M + T::BM - 1) / T::BM) * (a.N / T::BN));
-    hipLaunchKernelGGL((rowgemm_kernel<AMODE, AFFINE, EMODE, T>), grid, dim3(T::THREADS), 0, s, a);
+    hipLaunchKernelGGL((rowgemm_kernel<AMODE, AOP, EMODE, T>), grid, dim3(T::THREADS), 0, s, a);
     return (int)hipGetLastError();
 }
 
-template <int AMODE, bool AFFINE, int EMODE>
+template <int AMODE, int AOP, int EMODE>
 static int rowgemm_tile(const RowGemmArgs& a, int tile, hipStream_t s) {
 #define RG_CASE(id, T) \
-    if (tile == id) return rowgemm_go<AMODE, AFFINE, EMODE, T>(a, s);
+    if (tile == id) return rowgemm_go<AMODE, AOP, EMODE, T>(a, s);
     ROWGEMM_TILES(RG_CASE)
 #undef RG_CASE
     return -1;
@@ -497,16 +585,20 @@ int rowgemm_tile_dbuf(int tile) {
 
 int launch_rowgemm(const RowGemmArgs& a, int tile, hipStream_t s) {
     if (a.M < 1 || a.K != gather_taps(a.amode) * a.C) return -1;
-    const bool aff = a.ascale != nullptr;
+    const bool aff = a.ascale != nullptr, dz = a.acoef != nullptr;
+    if (aff && dz) return -1;
+    if ((a.emode == E_STORE_BN) != (a.ey != nullptr)) return -1;
     if (a.amode == G_CONV3 && a.emode == E_BIAS_RELU_STATS)
-        return aff ? rowgemm_tile<G_CONV3, true, E_BIAS_RELU_STATS>(a, tile, s)
-                   : rowgemm_tile<G_CONV3, false, E_BIAS_RELU_STATS>(a, tile, s);
-    if (a.amode == G_CONV3 && a.emode == E_STORE && !aff)
-        return rowgemm_tile<G_CONV3, false, E_STORE>(a, tile, s);
+        return aff ? rowgemm_tile<G_CONV3, OP_AFFINE, E_BIAS_RELU_STATS>(a, tile, s)
+                   : rowgemm_tile<G_CONV3, OP_PLAIN, E_BIAS_RELU_STATS>(a, tile, s);
+    if (a.amode == G_CONV3 && dz && a.emode == E_STORE)
+        return rowgemm_tile<G_CONV3, OP_DZ, E_STORE>(a, tile, s);
+    if (a.amode == G_CONV3 && dz && a.emode == E_STORE_BN)
+        return rowgemm_tile<G_CONV3, OP_DZ, E_STORE_BN>(a, tile, s);
     if (a.amode == G_IDENT && a.emode == E_CONVT && aff)
-        return rowgemm_tile<G_IDENT, true, E_CONVT>(a, tile, s);
-    if (a.amode == G_UP2 && a.emode == E_STORE && !aff)
-        return rowgemm_tile<G_UP2, false, E_STORE>(a, tile, s);
+        return rowgemm_tile<G_IDENT, OP_AFFINE, E_CONVT>(a, tile, s);
+    if (a.amode == G_UP2 && !aff && !dz && a.emode == E_STORE_BN)
+        return rowgemm_tile<G_UP2, OP_PLAIN, E_STORE_BN>(a, tile, s);
     return -1;  // combination not instantiated
 }
 
@@ -534,14 +626,14 @@ int wgrad_tile_dims(int tile, int* bm, int* bn, int* bkp) {
     return -1;
 }
 
-template <int AMODE, bool AFFINE, int BMODE>
+template <int AMODE, bool AFFINE, int BMODE, bool BDZ>
 static int wgrad_tile(const WgradArgs& a, int tile, hipStream_t s) {
 #define WG_CASE(id, T)                                                                        \
     if (tile == id) {                                                                         \
         if (a.Mw % T::BM || a.Nw % T::BN || a.CA % T::BM || a.CB % T::BN || a.pps % T::BKP) \
             return -1;                                                                        \
         const dim3 grid((a.Mw / T::BM) * (a.Nw / T::BN) * a.splits);                          \
-        hipLaunchKernelGGL((wgrad_kernel<AMODE, AFFINE, BMODE, T>), grid, dim3(T::THREADS), 0, s, a); \
+        hipLaunchKernelGGL((wgrad_kernel<AMODE, AFFINE, BMODE, BDZ, T>), grid, dim3(T::THREADS), 0, s, a); \
         return (int)hipGetLastError();                                                        \
     }
     WGRAD_TILES(WG_CASE)
@@ -551,11 +643,11 @@ static int wgrad_tile(const WgradArgs& a, int tile, hipStream_t s) {
 
 int launch_wgrad(const WgradArgs& a, int tile, hipStream_t s) {
     if (a.P < 1) return -1;
-    const bool aff = a.ascale != nullptr;
-    if (a.amode == G_CONV3 && a.bmode == G_IDENT)
-        return aff ? wgrad_tile<G_CONV3, true, G_IDENT>(a, tile, s)
-                   : wgrad_tile<G_CONV3, false, G_IDENT>(a, tile, s);
-    if (a.amode == G_IDENT && a.bmode == G_UP2 && aff)
-        return wgrad_tile<G_IDENT, true, G_UP2>(a, tile, s);
+    const bool aff = a.ascale != nullptr, dz = a.bcoef != nullptr;
+    if (a.amode == G_CONV3 && a.bmode == G_IDENT && dz)
+        return aff ? wgrad_tile<G_CONV3, true, G_IDENT, true>(a, tile, s)
+                   : wgrad_tile<G_CONV3, false, G_IDENT, true>(a, tile, s);
+    if (a.amode == G_IDENT && a.bmode == G_UP2 && aff && !dz)
+        return wgrad_tile<G_IDENT, true, G_UP2, false>(a, tile, s);
     return -1;
 }

@@ -6,8 +6,9 @@ int k_pack_conv3(const float* w, float* wf, float* wd, int cin, int cout, hipStr
 int k_pack_convT(const float* w, float* tf, float* td, int cin, int cout, hipStream_t s);
 int k_conv_first_fwd(const float* x, const float* w, const float* b, float* y, int P, int H, int W,
                      int C, float* partial, int G, hipStream_t s);
-int k_conv_first_wgrad(const float* x, const float* dz, int P, int H, int W, int C, float* partial,
-                       int G, float* gw, float* gb, hipStream_t s);
+int k_conv_first_wgrad(const float* x, const float* dout, const float* y, const float* coef, int P,
+                       int H, int W, int C, float* partial, int G, float* gw, float* gb,
+                       hipStream_t s);
 int k_reduce_rows(const float* in, int R, int ncols, float* out, int G, hipStream_t s);
 int k_bn_finalize_train(const float* part, int G, int C, double count, const float* gamma,
                         const float* beta, float* rmean, float* rvar, int64_t* nbt, float momentum,
@@ -18,7 +19,12 @@ int k_bn_finalize_eval(int C, const float* gamma, const float* beta, const float
 int k_maxpool_bn(const float* y, int ld, int off, const float* scale, const float* shift, int N,
                  int H, int W, int C, float* out, uint8_t* idx, hipStream_t s);
 int k_maxpool_bwd(const float* dp, const uint8_t* idx, const float* dskip, int ldskip, int offskip,
-                  int N, int H, int W, int C, float* dout, hipStream_t s);
+                  const float* y, int ldy, int offy, int N, int H, int W, int C, float* dout,
+                  float* partial, int G, hipStream_t s);
+int k_bn_bwd_finalize4(const float* part, int G, int C, double count, const float* gamma,
+                       const float* mean, const float* invstd, float* coef, float* dgamma,
+                       float* dbeta, hipStream_t s);
+int k_bias_reduce(const float* slab, int S, int taps, int C, float* out, hipStream_t s);
 int k_bn_bwd_reduce(const float* dout, const float* y, int ld, int off, int P, int C,
                     float* partial, int G, hipStream_t s);
 int k_bn_bwd_finalize(const float* part, int G, int C, double count, const float* gamma,
@@ -33,8 +39,8 @@ int k_slab_reduce(const float* slab, int S, int Mw, int Nw, int kind, int cin, i
 int k_head_fwd(const float* y, int C, const float* scale, const float* shift, const float* w,
                const float* b, int O, int P, int HW, float* logits, hipStream_t s);
 int k_head_bwd(const float* y, int C, const float* scale, const float* shift, const float* w,
-               int O, int P, int HW, const float* dlog, float* dout, float* partial, int G,
-               hipStream_t s);
+               int O, int P, int HW, const float* dlog, float* dout, float* partial,
+               float* bnpart, int G, hipStream_t s);
 int k_loss_fwd(const float* x, const float* t, int N, int64_t per, float* stats, float* losses,
                float alpha, float beta, float gamma, hipStream_t s);
 int k_loss_bwd(const float* x, const float* t, int N, int64_t per, const float* stats,

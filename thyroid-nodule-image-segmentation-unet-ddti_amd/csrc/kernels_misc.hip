@@ -116,7 +116,9 @@ __global__ __launch_bounds__(256) void conv_first_fwd_kernel(const float* __rest
 // dW[co][tap] = sum_p x_tap(p) dz[p][co], db[co] = sum_p dz[p][co]; partial [G][10*C]
 // laid out as [tap][C] for tap 0..8 then bias.
 __global__ __launch_bounds__(256) void conv_first_wgrad_kernel(const float* __restrict__ x,
-                                                              const float* __restrict__ dz,
+                                                              const float* __restrict__ dout,
+                                                              const float* __restrict__ y,
+                                                              const float* __restrict__ coef,
                                                               int P, int H, int W, int C,
                                                               float* partial) {
     __shared__ __attribute__((aligned(16))) float smem[256 * 10 * 4];
@@ -130,7 +132,14 @@ __global__ __launch_bounds__(256) void conv_first_wgrad_kernel(const float* __re
     const int r1 = min(P, r0 + per);
     for (int m = r0 + g; m < r1; m += rpp) {
         const int xx = m % W, t = m / W, yy = t % H, img = t / H;
-        const f32x4 d = *(const f32x4*)(dz + (int64_t)m * C + 4 * q);
+        // dz = [y > 0] (A do + B y + C): BN + ReLU backward fused into the load
+        const f32x4 dv = *(const f32x4*)(dout + (int64_t)m * C + 4 * q);
+        const f32x4 yv = *(const f32x4*)(y + (int64_t)m * C + 4 * q);
+        const f32x4 dd = *(const f32x4*)(coef + 4 * q) * dv + *(const f32x4*)(coef + C + 4 * q) * yv +
+                         *(const f32x4*)(coef + 2 * C + 4 * q);
+        f32x4 d;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) d[j] = yv[j] > 0.f ? dd[j] : 0.f;
 #pragma unroll
         for (int tap = 0; tap < 9; ++tap) {
             const int sy = yy + tap / 3 - 1, sx = xx + tap % 3 - 1;
@@ -289,31 +298,56 @@ __global__ void maxpool_bn_kernel(const float* __restrict__ y, int ld, int off,
 }
 
 // do[p][c] = (idx routes dpool to p) + dskip[p][c]  (skip grad comes from the decoder's
-// concat slice, model.py:64-70, so the encoder output's two consumers are summed here).
-__global__ void maxpool_bwd_kernel(const float* __restrict__ dp, const uint8_t* __restrict__ idx,
-                                   const float* __restrict__ dskip, int ldskip, int offskip,
-                                   int N, int H, int W, int C, float* __restrict__ dout) {
-    const int Ho = H / 2, Wo = W / 2, c4n = C / 4;
-    const int64_t total = (int64_t)N * Ho * Wo * c4n;
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
-         i += (int64_t)gridDim.x * blockDim.x) {
-        const int c4 = (int)(i % c4n);
-        const int64_t po = i / c4n;
-        const int xo = (int)(po % Wo);
-        const int64_t t = po / Wo;
-        const int yo = (int)(t % Ho), img = (int)(t / Ho);
-        const f32x4 g = *(const f32x4*)(dp + po * C + 4 * c4);
-        const uint32_t bi = *(const uint32_t*)(idx + po * C + 4 * c4);
+// concat slice, model.py:64-70, so the encoder output's two consumers are summed here), plus
+// the BN-backward column partials of do against the BN input y (same NHWC slice as the
+// skip): partial[G][4][C] = {sum do, sum do*y, sum_{y>0} do, count y>0}.
+// One thread per channel quad, pooled pixels strided over the block's row groups.
+__global__ __launch_bounds__(256) void maxpool_bwd_kernel(const float* __restrict__ dp,
+                                                         const uint8_t* __restrict__ idx,
+                                                         const float* __restrict__ dskip, int ldskip,
+                                                         int offskip, const float* __restrict__ y,
+                                                         int ldy, int offy, int N, int H, int W,
+                                                         int C, float* __restrict__ dout,
+                                                         float* partial) {
+    __shared__ __attribute__((aligned(16))) float smem[256 * 4 * 4];
+    const int Ho = H / 2, Wo = W / 2;
+    const int tpr = C / 4 < 256 ? C / 4 : 256, rpp = 256 / tpr;
+    const int64_t PO = (int64_t)N * Ho * Wo;
+    f32x4 acc[4];
+    for (int c0 = 0; c0 < C; c0 += 4 * tpr) {
+        const int q = threadIdx.x % tpr, g = threadIdx.x / tpr;
+        const int c = c0 + 4 * q;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int64_t pin = ((int64_t)img * H + 2 * yo + (k >> 1)) * W + 2 * xo + (k & 1);
-            f32x4 v = {0, 0, 0, 0};
-            if (dskip) v = *(const f32x4*)(dskip + pin * ldskip + offskip + 4 * c4);
+        for (int v = 0; v < 4; ++v) acc[v] = f32x4{0, 0, 0, 0};
+        const int64_t per = (PO + gridDim.x - 1) / gridDim.x;
+        const int64_t r0 = blockIdx.x * per, r1 = r0 + per < PO ? r0 + per : PO;
+        for (int64_t po = r0 + g; po < r1; po += rpp) {
+            const int xo = (int)(po % Wo);
+            const int64_t t = po / Wo;
+            const int yo = (int)(t % Ho), img = (int)(t / Ho);
+            const f32x4 gp = *(const f32x4*)(dp + po * C + c);
+            const uint32_t bi = *(const uint32_t*)(idx + po * C + c);
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
-                if (((bi >> (8 * j)) & 0xFF) == (uint32_t)k) v[j] += g[j];
-            *(f32x4*)(dout + pin * C + 4 * c4) = v;
+            for (int k = 0; k < 4; ++k) {
+                const int64_t pin = ((int64_t)img * H + 2 * yo + (k >> 1)) * W + 2 * xo + (k & 1);
+                f32x4 v = *(const f32x4*)(dskip + pin * ldskip + offskip + c);
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    if (((bi >> (8 * j)) & 0xFF) == (uint32_t)k) v[j] += gp[j];
+                *(f32x4*)(dout + pin * C + c) = v;
+                const f32x4 yv = *(const f32x4*)(y + pin * ldy + offy + c);
+                acc[0] += v;
+                acc[1] += v * yv;
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    if (yv[j] > 0.f) {
+                        acc[2][j] += v[j];
+                        acc[3][j] += 1.f;
+                    }
+            }
         }
+        block_combine<4>(acc, tpr, C, partial + (int64_t)blockIdx.x * 4 * C + c0, smem);
+        __syncthreads();
     }
 }
 
@@ -365,6 +399,43 @@ __global__ void bn_bwd_finalize_kernel(const float* __restrict__ part, int G, in
     coef[2 * C + c] = (float)(-k * s1 / count + k * is * mu * sdxh / count);  // Cc
     dgamma[c] = (float)sdxh;
     dbeta[c] = (float)s1;
+}
+
+// From the 4-quantity partials of the producer of `do` ({S1 = sum do, S2 = sum do*y,
+// S3, S4}; only S1, S2 are needed here): dz = [y>0](A do + B y + Cc) coefficients for the
+// fused consumers, and dgamma = invstd (S2 - mean S1), dbeta = S1.
+__global__ void bn_bwd_finalize4_kernel(const float* __restrict__ part, int G, int C, double count,
+                                        const float* __restrict__ gamma,
+                                        const float* __restrict__ mean,
+                                        const float* __restrict__ invstd, float* __restrict__ coef,
+                                        float* __restrict__ dgamma, float* __restrict__ dbeta) {
+    const int c = blockIdx.x * 64 + threadIdx.x;
+    double ss[2];
+    colsum16<2>(part, G, 4 * C, C, c, c < C, ss);
+    if (threadIdx.y != 0 || c >= C) return;
+    const double s1 = ss[0], s2 = ss[1];
+    const double is = invstd[c], mu = mean[c];
+    const double sdxh = is * (s2 - mu * s1);
+    const double k = (double)gamma[c] * is;
+    coef[c] = (float)k;
+    coef[C + c] = (float)(-k * is * sdxh / count);
+    coef[2 * C + c] = (float)(-k * s1 / count + k * is * mu * sdxh / count);
+    dgamma[c] = (float)sdxh;
+    dbeta[c] = (float)s1;
+}
+
+// bias gradient from the wgrad kernels' column sums: out[co] = sum_s sum_tap slab[s][tap*C+co]
+__global__ void bias_reduce_kernel(const float* __restrict__ slab, int S, int taps, int C,
+                                   float* __restrict__ out) {
+    const int c = blockIdx.x * 64 + threadIdx.x;
+    double t = 0.0;
+    for (int tap = 0; tap < taps; ++tap) {
+        double v[1];
+        colsum16<1>(slab + tap * C, S, taps * C, 0, c, c < C, v);
+        t += v[0];
+        __syncthreads();
+    }
+    if (threadIdx.y == 0 && c < C) out[c] = (float)t;
 }
 
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(float* __restrict__ dz,
@@ -429,21 +500,42 @@ __global__ void sum_partials_kernel(const float* __restrict__ part, int G, int n
 //   convT : slab [S][ci][ab*Cout+co] -> grad[ci][co][ab]
 __global__ void slab_reduce_kernel(const float* __restrict__ slab, int S, int Mw, int Nw,
                                    int kind, int cin, int cout, float* __restrict__ grad) {
+    // 4 consecutive n per thread (float4 loads); the S slabs are summed in a fixed
+    // association (four interleaved partial sums, then combined) with 8 loads in flight.
     const int64_t total = (int64_t)Mw * Nw;
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
-         i += (int64_t)gridDim.x * blockDim.x) {
-        float s = 0.f;
-        for (int k = 0; k < S; ++k) s += slab[(int64_t)k * total + i];
-        const int n = (int)(i % Nw), m = (int)(i / Nw);
-        int64_t o;
-        if (kind == 0) {
-            const int tap = m / cin, ci = m - tap * cin;
-            o = ((int64_t)n * cin + ci) * 9 + tap;
-        } else {
-            const int ab = n / cout, co = n - ab * cout;
-            o = ((int64_t)m * cout + co) * 4 + ab;
+    const int64_t nq = total / 4;
+    for (int64_t iq = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; iq < nq;
+         iq += (int64_t)gridDim.x * blockDim.x) {
+        const f32x4* sp = (const f32x4*)slab + iq;
+        const int64_t stride = total / 4;
+        f32x4 a0 = {0, 0, 0, 0}, a1 = a0, a2 = a0, a3 = a0;
+        int k = 0;
+        for (; k + 8 <= S; k += 8) {
+            f32x4 v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = sp[(int64_t)(k + u) * stride];
+            a0 += v[0] + v[4];
+            a1 += v[1] + v[5];
+            a2 += v[2] + v[6];
+            a3 += v[3] + v[7];
         }
-        grad[o] = s;
+        for (; k < S; ++k) a0 += sp[(int64_t)k * stride];
+        const f32x4 s4 = (a0 + a1) + (a2 + a3);
+        const int64_t i0 = iq * 4;
+        const int m = (int)(i0 / Nw), n0 = (int)(i0 % Nw);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int n = n0 + j;
+            int64_t o;
+            if (kind == 0) {
+                const int tap = m / cin, ci = m - tap * cin;
+                o = ((int64_t)n * cin + ci) * 9 + tap;
+            } else {
+                const int ab = n / cout, co = n - ab * cout;
+                o = ((int64_t)m * cout + co) * 4 + ab;
+            }
+            grad[o] = s4[j];
+        }
     }
 }
 
@@ -496,8 +588,11 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__
                                                       const float* __restrict__ shift,
                                                       const float* __restrict__ w, int O, int P,
                                                       int HW, const float* __restrict__ dlog,
-                                                      float* __restrict__ dout, float* partial) {
+                                                      float* __restrict__ dout, float* partial,
+                                                      float* bnpart) {
     __shared__ float red[256 * 5];
+    __shared__ __attribute__((aligned(16))) float smem4[256 * 4 * 4];
+    f32x4 bq[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
     const int lpp = C / 4, rpp = 256 / lpp;
     const int q = threadIdx.x % lpp, g = threadIdx.x / lpp;
     const f32x4 sc = *(const f32x4*)(scale + 4 * q), sh = *(const f32x4*)(shift + 4 * q);
@@ -507,7 +602,8 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__
     const int per = (P + gridDim.x - 1) / gridDim.x;
     const int r0 = blockIdx.x * per, r1 = min(P, r0 + per);
     for (int m = r0 + g; m < r1; m += rpp) {
-        const f32x4 v = *(const f32x4*)(y + (int64_t)m * C + 4 * q) * sc + sh;
+        const f32x4 yr = *(const f32x4*)(y + (int64_t)m * C + 4 * q);
+        const f32x4 v = yr * sc + sh;
         const int64_t img = m / HW, hw = m % HW;
         f32x4 d = {0, 0, 0, 0};
         for (int o = 0; o < O; ++o) {
@@ -517,7 +613,17 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__
             ab[o] += dl;
         }
         *(f32x4*)(dout + (int64_t)m * C + 4 * q) = d;
+        bq[0] += d;
+        bq[1] += d * yr;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (yr[j] > 0.f) {
+                bq[2][j] += d[j];
+                bq[3][j] += 1.f;
+            }
     }
+    block_combine<4>(bq, lpp, C, bnpart + (int64_t)blockIdx.x * 4 * C, smem4);
+    __syncthreads();
     // combine over row groups through LDS, one quantity at a time
     float* out = partial + (int64_t)blockIdx.x * (O * C + O);
     for (int o = 0; o < O; ++o) {
@@ -729,9 +835,11 @@ int k_conv_first_fwd(const float* x, const float* w, const float* b, float* y, i
                        partial);
     LAUNCH_CHECK();
 }
-int k_conv_first_wgrad(const float* x, const float* dz, int P, int H, int W, int C, float* partial,
-                       int G, float* gw, float* gb, hipStream_t s) {
-    hipLaunchKernelGGL(conv_first_wgrad_kernel, dim3(G), dim3(256), 0, s, x, dz, P, H, W, C, partial);
+int k_conv_first_wgrad(const float* x, const float* dout, const float* y, const float* coef, int P,
+                       int H, int W, int C, float* partial, int G, float* gw, float* gb,
+                       hipStream_t s) {
+    hipLaunchKernelGGL(conv_first_wgrad_kernel, dim3(G), dim3(256), 0, s, x, dout, y, coef, P, H, W,
+                       C, partial);
     HIP_OK(hipGetLastError());
     hipLaunchKernelGGL(conv_first_wgrad_finalize_kernel, dim3((10 * C + 63) / 64), dim3(64, 16), 0,
                        s, partial, G, C, gw, gb);
@@ -765,10 +873,10 @@ int k_maxpool_bn(const float* y, int ld, int off, const float* scale, const floa
     LAUNCH_CHECK();
 }
 int k_maxpool_bwd(const float* dp, const uint8_t* idx, const float* dskip, int ldskip, int offskip,
-                  int N, int H, int W, int C, float* dout, hipStream_t s) {
-    const int64_t n = (int64_t)N * (H / 2) * (W / 2) * (C / 4);
-    hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for(n)), dim3(256), 0, s, dp, idx, dskip,
-                       ldskip, offskip, N, H, W, C, dout);
+                  const float* y, int ldy, int offy, int N, int H, int W, int C, float* dout,
+                  float* partial, int G, hipStream_t s) {
+    hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(G), dim3(256), 0, s, dp, idx, dskip, ldskip,
+                       offskip, y, ldy, offy, N, H, W, C, dout, partial);
     LAUNCH_CHECK();
 }
 int k_bn_bwd_reduce(const float* dout, const float* y, int ld, int off, int P, int C,
@@ -782,6 +890,18 @@ int k_bn_bwd_finalize(const float* part, int G, int C, double count, const float
                       float* dbeta, hipStream_t s) {
     hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(64, 16), 0, s, part, G, C,
                        count, gamma, mean, invstd, coef, dgamma, dbeta);
+    LAUNCH_CHECK();
+}
+int k_bn_bwd_finalize4(const float* part, int G, int C, double count, const float* gamma,
+                       const float* mean, const float* invstd, float* coef, float* dgamma,
+                       float* dbeta, hipStream_t s) {
+    hipLaunchKernelGGL(bn_bwd_finalize4_kernel, dim3((C + 63) / 64), dim3(64, 16), 0, s, part, G, C,
+                       count, gamma, mean, invstd, coef, dgamma, dbeta);
+    LAUNCH_CHECK();
+}
+int k_bias_reduce(const float* slab, int S, int taps, int C, float* out, hipStream_t s) {
+    hipLaunchKernelGGL(bias_reduce_kernel, dim3((C + 63) / 64), dim3(64, 16), 0, s, slab, S, taps, C,
+                       out);
     LAUNCH_CHECK();
 }
 int k_bn_bwd_apply(float* dz, const float* y, int ld, int off, int P, int C, const float* coef,
@@ -802,8 +922,9 @@ int k_sum_partials(const float* part, int G, int ncols, float* out, hipStream_t 
 }
 int k_slab_reduce(const float* slab, int S, int Mw, int Nw, int kind, int cin, int cout,
                   float* grad, hipStream_t s) {
-    hipLaunchKernelGGL(slab_reduce_kernel, dim3(grid_for((int64_t)Mw * Nw)), dim3(256), 0, s, slab,
-                       S, Mw, Nw, kind, cin, cout, grad);
+    if (Nw % 4) return -1;
+    hipLaunchKernelGGL(slab_reduce_kernel, dim3(grid_for((int64_t)Mw * Nw / 4)), dim3(256), 0, s,
+                       slab, S, Mw, Nw, kind, cin, cout, grad);
     LAUNCH_CHECK();
 }
 int k_head_fwd(const float* y, int C, const float* scale, const float* shift, const float* w,
@@ -814,10 +935,10 @@ int k_head_fwd(const float* y, int C, const float* scale, const float* shift, co
     LAUNCH_CHECK();
 }
 int k_head_bwd(const float* y, int C, const float* scale, const float* shift, const float* w,
-               int O, int P, int HW, const float* dlog, float* dout, float* partial, int G,
-               hipStream_t s) {
+               int O, int P, int HW, const float* dlog, float* dout, float* partial,
+               float* bnpart, int G, hipStream_t s) {
     hipLaunchKernelGGL(head_bwd_kernel, dim3(G), dim3(256), 0, s, y, C, scale, shift, w, O, P, HW,
-                       dlog, dout, partial);
+                       dlog, dout, partial, bnpart);
     LAUNCH_CHECK();
 }
 int k_loss_fwd(const float* x, const float* t, int N, int64_t per, float* stats, float* losses,

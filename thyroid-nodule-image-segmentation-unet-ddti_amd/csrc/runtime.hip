@@ -226,8 +226,10 @@ struct Plan {
     float* g[2];
     float* dcat[4];
     float* slab;
-    float* part;
-    float* part2;
+    float* part;   // BN-backward column partials [rows][4][C]
+    float* part2;  // second-level reduction of part
+    float* hpart;  // head / conv-first weight-gradient partials
+    float* bslab;  // [splits][Nw] bias-gradient column sums from the wgrad kernels
     float* coef;
     size_t bytes;
 };
@@ -342,11 +344,27 @@ void make_plan(unet_ctx* c, int N, int H, int W, bool training, char* base, Plan
             smax = std::max(smax, (int64_t)w.splits * T.cin * 4 * T.cout);
         }
         p.slab = b.take<float>(smax);
-        p.part = b.take<float>((int64_t)RED_G * (10 * 1024 + 64));
-        p.part2 = b.take<float>((int64_t)RED_G * 2 * 1024);
+        int64_t pmax = (int64_t)RED_G * 4 * 1024;
+        for (int i = 0; i < NCONV; ++i)  // dgrad epilogues: ceil(P/64) rows of 4*C (BM >= 64)
+            pmax = std::max(pmax, (p.P[c->conv[i].level] / 64 + 1) * 4 * c->conv[i].cout);
+        p.part = b.take<float>(pmax);
+        p.part2 = b.take<float>((int64_t)STAT_G * 4 * 1024);
+        p.hpart = b.take<float>((int64_t)RED_G * (10 * 1024 + 64));
+        int64_t bmax = 0;
+        for (int i = 1; i < NCONV; ++i) {
+            const ConvL& L = c->conv[i];
+            WgradCfg w = wgrad_cfg(L.cin, 9, L.cout, 1, p.P[L.level]);
+            bmax = std::max(bmax, (int64_t)w.splits * L.cout);
+        }
+        for (int k = 0; k < NCONVT; ++k) {
+            const ConvTL& T = c->convt[k];
+            WgradCfg w = wgrad_cfg(T.cin, 1, T.cout, 4, p.P[T.in_level]);
+            bmax = std::max(bmax, (int64_t)w.splits * 4 * T.cout);
+        }
+        p.bslab = b.take<float>(bmax);
         p.coef = b.take<float>(3 * 1024);
     } else {
-        p.g[0] = p.g[1] = p.slab = p.part = p.part2 = p.coef = nullptr;
+        p.g[0] = p.g[1] = p.slab = p.part = p.part2 = p.hpart = p.bslab = p.coef = nullptr;
         for (int l = 0; l < 4; ++l) p.dcat[l] = nullptr;
     }
     p.bytes = b.off + 256;
@@ -603,35 +621,40 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
 int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* grads, Plan& p,
                   hipStream_t s) {
     Launcher L{c, s};
-    const int N = p.N, H = p.H, W = p.W;
-    (void)N;
+    const int H = p.H, W = p.W;
     int rc;
 
-    // BN backward through ReLU, in place: do -> dz; writes dgamma, dbeta, conv bias grad
-    auto bn_bwd = [&](int i, float* d) -> int {
+    // BatchNorm (+ReLU) backward is fused: the producer of `do` (head_bwd, a dgrad epilogue,
+    // maxpool_bwd) leaves {sum do, sum do*y, ...} column partials in p.part; this finalize
+    // turns them into dgamma, dbeta and the per-channel coefficients of
+    // dz = [y>0](A do + B y + C), which the conv's wgrad / dgrad loaders apply on the fly.
+    auto bn_finalize = [&](int i, int R) -> int {
         const ConvL& C = c->conv[i];
         const BnL& B = c->bn[i];
-        const int64_t P = p.P[C.level];
-        RUN("bn_bwd_reduce", 0,
-            k_bn_bwd_reduce(d, p.y[i], p.ldy[i], p.offy[i], (int)P, C.cout, p.part, RED_G, s));
+        const float* part = p.part;
+        int G = R;
+        if (R > STAT_G) {
+            RUN("bn_bwd_reduce", 0, k_reduce_rows(p.part, R, 4 * C.cout, p.part2, STAT_G, s));
+            part = p.part2;
+            G = STAT_G;
+        }
         RUN("bn_bwd_finalize", 0,
-            k_bn_bwd_finalize(p.part, RED_G, C.cout, (double)P, prm + B.g, p.mean[i], p.invstd[i],
-                              p.coef, grads + B.g, grads + B.b, s));
-        RUN("bn_bwd_apply", 0,
-            k_bn_bwd_apply(d, p.y[i], p.ldy[i], p.offy[i], (int)P, C.cout, p.coef, p.part2,
-                           RED_G, s));
-        RUN("bias_grad", 0, k_sum_partials(p.part2, RED_G, C.cout, grads + C.b, s));
+            k_bn_bwd_finalize4(part, G, C.cout, (double)p.P[C.level], prm + B.g, p.mean[i],
+                               p.invstd[i], p.coef, grads + B.g, grads + B.b, s));
         return 0;
     };
-    // conv backward: wgrad from (input, dz), dgrad dz -> dx (ld, off) when dx != null
-    auto conv_bwd = [&](int i, const float* dz, float* dx, int ldx) -> int {
+    // conv i backward from do_i (dense [P][cout]); dz is formed in the loaders.
+    // dgrad -> dx (ld ldx).  bn_next: dx is the `do` of BN layer i-1 (second conv of a
+    // block), so the epilogue also emits that layer's partials; *rows = their count.
+    auto conv_bwd = [&](int i, const float* dout, float* dx, int ldx, bool bn_next,
+                        int* rows) -> int {
         const ConvL& C = c->conv[i];
         const int Hl = H >> C.level, Wl = W >> C.level;
         const int64_t P = p.P[C.level];
         if (i == 0 && C.pf < 0) {
             RUN("conv_first_wgrad", 2.0 * P * 9 * C.cout,
-                k_conv_first_wgrad(p.x_nhwc, dz, (int)P, Hl, Wl, C.cout,
-                                   p.part, RED_G, grads + C.w, grads + C.b, s));
+                k_conv_first_wgrad(p.x_nhwc, dout, p.y[0], p.coef, (int)P, Hl, Wl, C.cout,
+                                   p.hpart, RED_G, grads + C.w, grads + C.b, s));
             return 0;
         }
         Operand a = conv_input(c, p, i);
@@ -647,11 +670,16 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         w.amode = G_CONV3;
         w.ascale = a.scale;
         w.ashift = a.shift;
-        w.b = dz;
+        w.b = dout;
         w.ldb = C.cout;
         w.boff = 0;
         w.CB = C.cout;
         w.bmode = G_IDENT;
+        w.by = p.y[i];
+        w.ldby = p.ldy[i];
+        w.offby = p.offy[i];
+        w.bcoef = p.coef;
+        w.bias_slab = p.bslab;
         w.Mw = 9 * C.cin;
         w.Nw = C.cout;
         w.pps = wc.pps;
@@ -661,6 +689,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
             launch_wgrad(w, wc.tile, s));
         RUN("wgrad_reduce", 0,
             k_slab_reduce(p.slab, wc.splits, w.Mw, w.Nw, 0, C.cin, C.cout, grads + C.w, s));
+        RUN("bias_grad", 0, k_bias_reduce(p.bslab, wc.splits, 1, C.cout, grads + C.b, s));
         if (dx) {
             RowGemmArgs g{};
             g.H = Hl;
@@ -668,31 +697,43 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
             g.M = (int)P;
             g.N = C.cin;
             g.K = 9 * C.cout;
-            g.a = dz;
+            g.a = dout;
             g.lda = C.cout;
             g.aoff = 0;
             g.C = C.cout;
             g.amode = G_CONV3;
+            g.ay = p.y[i];
+            g.lday = p.ldy[i];
+            g.offay = p.offy[i];
+            g.acoef = p.coef;
             g.bt = p.pack + C.pd;
             g.out = dx;
             g.ldo = ldx;
             g.ooff = 0;
             g.emode = E_STORE;
+            if (bn_next) {
+                g.emode = E_STORE_BN;
+                g.ey = p.y[i - 1];
+                g.ldey = p.ldy[i - 1];
+                g.offey = p.offy[i - 1];
+                g.stats = p.part;
+            }
             const int tile = pick_tile(C.cin, true);
+            int bm, bn, bk;
+            rowgemm_tile_dims(tile, &bm, &bn, &bk);
+            if (rows) *rows = (int)((P + bm - 1) / bm);
             RUN(tlabel("conv_dgrad", tile, i), 2.0 * P * C.cout * 9 * C.cin, launch_rowgemm(g, tile, s));
         }
         return 0;
     };
-    // ConvT k backward: dOut = dcat[lo][:, 0:cout]; writes do of its input into dx
-    auto convT_bwd = [&](int k, float* dx) -> int {
+    // ConvT k backward: dOut = dcat[lo][:, 0:cout]; dx = `do` of its input's BN (partials -> rows)
+    auto convT_bwd = [&](int k, float* dx, int* rows) -> int {
         const ConvTL& T = c->convt[k];
         const int src = 2 * (4 + k) + 1;
         const int lo = T.in_level - 1;
         const int ldo = 2 * (64 << lo);
         const int Hi = H >> T.in_level, Wi = W >> T.in_level;
-        const int64_t Pin = p.P[T.in_level], Pout = p.P[lo];
-        RUN("convT_bias_grad", 0, k_chan_sum(p.dcat[lo], ldo, 0, (int)Pout, T.cout, p.part, RED_G, s));
-        RUN("bias_grad", 0, k_sum_partials(p.part, RED_G, T.cout, grads + T.b, s));
+        const int64_t Pin = p.P[T.in_level];
         WgradCfg wc = wgrad_cfg(T.cin, 1, T.cout, 4, Pin);
         WgradArgs w{};
         w.H = Hi;
@@ -710,6 +751,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         w.boff = 0;
         w.CB = T.cout;
         w.bmode = G_UP2;
+        w.bias_slab = p.bslab;
         w.Mw = T.cin;
         w.Nw = 4 * T.cout;
         w.pps = wc.pps;
@@ -719,6 +761,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
             launch_wgrad(w, wc.tile, s));
         RUN("wgrad_reduce", 0,
             k_slab_reduce(p.slab, wc.splits, w.Mw, w.Nw, 1, T.cin, T.cout, grads + T.w, s));
+        RUN("bias_grad", 0, k_bias_reduce(p.bslab, wc.splits, 4, T.cout, grads + T.b, s));
         RowGemmArgs g{};
         g.H = Hi;
         g.W = Wi;
@@ -734,8 +777,15 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         g.out = dx;
         g.ldo = T.cin;
         g.ooff = 0;
-        g.emode = E_STORE;
+        g.emode = E_STORE_BN;
+        g.ey = p.y[src];
+        g.ldey = p.ldy[src];
+        g.offey = p.offy[src];
+        g.stats = p.part;
         const int tile = pick_tile(T.cin, true);
+        int bm, bn, bk;
+        rowgemm_tile_dims(tile, &bm, &bn, &bk);
+        *rows = (int)((Pin + bm - 1) / bm);
         RUN(tlabel("convT_dgrad", tile, 100 + k), 2.0 * Pin * T.cin * 4 * T.cout, launch_rowgemm(g, tile, s));
         return 0;
     };
@@ -745,55 +795,56 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
 
     float* G0 = p.g[0];
     float* G1 = p.g[1];
-    // ---- final block + head (bucket 0) ----
+    int R = 0;
+    // ---- head + final block (bucket 0) ----
     RUN("head_bwd", 2.0 * p.P[0] * 64 * c->out_ch * 2,
         k_head_bwd(p.y[17], 64, p.scale[17], p.shift[17], prm + c->head_w, c->out_ch, (int)p.P[0],
-                   H * W, dlogits, G0, p.part, RED_G, s));
-    RUN("head_grad", 0, k_sum_partials(p.part, RED_G, c->out_ch * 64 + c->out_ch, grads + c->head_w, s));
-    if ((rc = bn_bwd(17, G0))) return rc;
-    if ((rc = conv_bwd(17, G0, G1, 64))) return rc;
-    if ((rc = bn_bwd(16, G1))) return rc;
-    if ((rc = conv_bwd(16, G1, p.dcat[0], 128))) return rc;
+                   H * W, dlogits, G0, p.hpart, p.part, RED_G, s));
+    RUN("head_grad", 0, k_sum_partials(p.hpart, RED_G, c->out_ch * 64 + c->out_ch, grads + c->head_w, s));
+    if ((rc = bn_finalize(17, RED_G))) return rc;
+    if ((rc = conv_bwd(17, G0, G1, 64, true, &R))) return rc;
+    if ((rc = bn_finalize(16, R))) return rc;
+    if ((rc = conv_bwd(16, G1, p.dcat[0], 128, false, nullptr))) return rc;
     bucket_done(0);
-    // ---- decoders: ConvT k then block 4+k ----
+    // ---- decoders: ConvT k, then block 4+k ----
     for (int k = 3; k >= 0; --k) {
-        const int b = 4 + k;  // block producing the ConvT input
+        const int b = 4 + k;
         const int i1 = 2 * b + 1, i0 = 2 * b;
-        if ((rc = convT_bwd(k, G0))) return rc;
-        if ((rc = bn_bwd(i1, G0))) return rc;
-        if ((rc = conv_bwd(i1, G0, G1, c->conv[i1].cin))) return rc;
-        if ((rc = bn_bwd(i0, G1))) return rc;
+        if ((rc = convT_bwd(k, G0, &R))) return rc;
+        if ((rc = bn_finalize(i1, R))) return rc;
+        if ((rc = conv_bwd(i1, G0, G1, c->conv[i1].cin, true, &R))) return rc;
+        if ((rc = bn_finalize(i0, R))) return rc;
         if (b >= 5) {
             const int l = c->conv[i0].level;  // input is CAT_l
-            if ((rc = conv_bwd(i0, G1, p.dcat[l], 2 * (64 << l)))) return rc;
+            if ((rc = conv_bwd(i0, G1, p.dcat[l], 2 * (64 << l), false, nullptr))) return rc;
             bucket_done(4 - k);  // decoder1 -> bucket 1, decoder2 -> 2, decoder3 -> 3
         } else {
-            // middle block: input is pool[3]
-            if ((rc = conv_bwd(i0, G1, G0, c->conv[i0].cin))) return rc;
+            // middle block: its input is pool[3]; G0 <- d pool[3]
+            if ((rc = conv_bwd(i0, G1, G0, c->conv[i0].cin, false, nullptr))) return rc;
             bucket_done(4);
         }
     }
-    // G0 = d pool[3]
     // ---- encoders ----
     float* cur = G0;
     for (int b = 3; b >= 0; --b) {
         const int C = 64 << b;
+        const int i1 = 2 * b + 1, i0 = 2 * b;
         float* nxt = cur == G0 ? G1 : G0;
         RUN("maxpool_bwd", 0,
-            k_maxpool_bwd(cur, p.idx[b], p.dcat[b], 2 * C, C, p.N, H >> b, W >> b, C, nxt, s));
+            k_maxpool_bwd(cur, p.idx[b], p.dcat[b], 2 * C, C, p.y[i1], p.ldy[i1], p.offy[i1], p.N,
+                          H >> b, W >> b, C, nxt, p.part, RED_G, s));
         cur = nxt;
         nxt = cur == G0 ? G1 : G0;
-        const int i1 = 2 * b + 1, i0 = 2 * b;
-        if ((rc = bn_bwd(i1, cur))) return rc;
-        if ((rc = conv_bwd(i1, cur, nxt, C))) return rc;
+        if ((rc = bn_finalize(i1, RED_G))) return rc;
+        if ((rc = conv_bwd(i1, cur, nxt, C, true, &R))) return rc;
         cur = nxt;
         nxt = cur == G0 ? G1 : G0;
-        if ((rc = bn_bwd(i0, cur))) return rc;
+        if ((rc = bn_finalize(i0, R))) return rc;
         if (b > 0) {
-            if ((rc = conv_bwd(i0, cur, nxt, c->conv[i0].cin))) return rc;
+            if ((rc = conv_bwd(i0, cur, nxt, c->conv[i0].cin, false, nullptr))) return rc;
             cur = nxt;
         } else {
-            if ((rc = conv_bwd(0, cur, nullptr, 0))) return rc;
+            if ((rc = conv_bwd(0, cur, nullptr, 0, false, nullptr))) return rc;
         }
         bucket_done(8 - b);
     }
