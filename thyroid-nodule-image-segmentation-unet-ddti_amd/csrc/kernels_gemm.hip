@@ -591,10 +591,12 @@ int launch_rowgemm(const RowGemmArgs& a, int tile, hipStream_t s) {
     if (a.amode == G_CONV3 && a.emode == E_BIAS_RELU_STATS)
         return aff ? rowgemm_tile<G_CONV3, OP_AFFINE, E_BIAS_RELU_STATS>(a, tile, s)
                    : rowgemm_tile<G_CONV3, OP_PLAIN, E_BIAS_RELU_STATS>(a, tile, s);
-    if (a.amode == G_CONV3 && dz && a.emode == E_STORE)
-        return rowgemm_tile<G_CONV3, OP_DZ, E_STORE>(a, tile, s);
-    if (a.amode == G_CONV3 && dz && a.emode == E_STORE_BN)
-        return rowgemm_tile<G_CONV3, OP_DZ, E_STORE_BN>(a, tile, s);
+    if (a.amode == G_CONV3 && a.emode == E_STORE)
+        return dz ? rowgemm_tile<G_CONV3, OP_DZ, E_STORE>(a, tile, s)
+                  : rowgemm_tile<G_CONV3, OP_PLAIN, E_STORE>(a, tile, s);
+    if (a.amode == G_CONV3 && a.emode == E_STORE_BN)
+        return dz ? rowgemm_tile<G_CONV3, OP_DZ, E_STORE_BN>(a, tile, s)
+                  : rowgemm_tile<G_CONV3, OP_PLAIN, E_STORE_BN>(a, tile, s);
     if (a.amode == G_IDENT && a.emode == E_CONVT && aff)
         return rowgemm_tile<G_IDENT, OP_AFFINE, E_CONVT>(a, tile, s);
     if (a.amode == G_UP2 && !aff && !dz && a.emode == E_STORE_BN)
@@ -647,6 +649,9 @@ int launch_wgrad(const WgradArgs& a, int tile, hipStream_t s) {
     if (a.amode == G_CONV3 && a.bmode == G_IDENT && dz)
         return aff ? wgrad_tile<G_CONV3, true, G_IDENT, true>(a, tile, s)
                    : wgrad_tile<G_CONV3, false, G_IDENT, true>(a, tile, s);
+    if (a.amode == G_CONV3 && a.bmode == G_IDENT && !dz)
+        return aff ? wgrad_tile<G_CONV3, true, G_IDENT, false>(a, tile, s)
+                   : wgrad_tile<G_CONV3, false, G_IDENT, false>(a, tile, s);
     if (a.amode == G_IDENT && a.bmode == G_UP2 && aff && !dz)
         return wgrad_tile<G_IDENT, true, G_UP2, false>(a, tile, s);
     return -1;

@@ -24,6 +24,8 @@ int k_maxpool_bwd(const float* dp, const uint8_t* idx, const float* dskip, int l
 int k_bn_bwd_finalize4(const float* part, int G, int C, double count, const float* gamma,
                        const float* mean, const float* invstd, float* coef, float* dgamma,
                        float* dbeta, hipStream_t s);
+int k_bn_dz(float* d, const float* y, int ld, int off, int64_t P, int C, const float* coef,
+            hipStream_t s);
 int k_bias_reduce(const float* slab, int S, int taps, int C, float* out, hipStream_t s);
 int k_bn_bwd_reduce(const float* dout, const float* y, int ld, int off, int P, int C,
                     float* partial, int G, hipStream_t s);

@@ -424,6 +424,26 @@ __global__ void bn_bwd_finalize4_kernel(const float* __restrict__ part, int G, i
     dbeta[c] = (float)s1;
 }
 
+// dz = [y>0](A do + B y + C) in place (BN + ReLU backward as one elementwise pass).
+__global__ void bn_dz_kernel(float* __restrict__ d, const float* __restrict__ y, int ld, int off,
+                             int64_t P, int C, const float* __restrict__ coef) {
+    const int c4n = C / 4;
+    const int64_t total = P * c4n;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int c = (int)(i % c4n) * 4;
+        const int64_t m = i / c4n;
+        f32x4* pd = (f32x4*)(d + m * C + c);
+        const f32x4 v = *(const f32x4*)(y + m * ld + off + c);
+        const f32x4 r = *(const f32x4*)(coef + c) * (*pd) + *(const f32x4*)(coef + C + c) * v +
+                        *(const f32x4*)(coef + 2 * C + c);
+        f32x4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = v[j] > 0.f ? r[j] : 0.f;
+        *pd = o;
+    }
+}
+
 // bias gradient from the wgrad kernels' column sums: out[co] = sum_s sum_tap slab[s][tap*C+co]
 __global__ void bias_reduce_kernel(const float* __restrict__ slab, int S, int taps, int C,
                                    float* __restrict__ out) {
@@ -897,6 +917,12 @@ int k_bn_bwd_finalize4(const float* part, int G, int C, double count, const floa
                        float* dbeta, hipStream_t s) {
     hipLaunchKernelGGL(bn_bwd_finalize4_kernel, dim3((C + 63) / 64), dim3(64, 16), 0, s, part, G, C,
                        count, gamma, mean, invstd, coef, dgamma, dbeta);
+    LAUNCH_CHECK();
+}
+int k_bn_dz(float* d, const float* y, int ld, int off, int64_t P, int C, const float* coef,
+            hipStream_t s) {
+    hipLaunchKernelGGL(bn_dz_kernel, dim3(grid_for(P * (C / 4))), dim3(256), 0, s, d, y, ld, off, P, C,
+                       coef);
     LAUNCH_CHECK();
 }
 int k_bias_reduce(const float* slab, int S, int taps, int C, float* out, hipStream_t s) {

@@ -643,7 +643,15 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
                                p.invstd[i], p.coef, grads + B.g, grads + B.b, s));
         return 0;
     };
-    // conv i backward from do_i (dense [P][cout]); dz is formed in the loaders.
+    // dz = [y>0](A do + B y + C) either as one elementwise pass over do (default) or inside
+    // the wgrad / dgrad loaders (UNET_DZ_IN_LOADERS=1: fewer passes, but every 3x3 tap
+    // re-gathers both do and y -- measured slower on MI355X, kept for A/B runs)
+    static int dz_in_loaders = -1;
+    if (dz_in_loaders < 0) {
+        const char* e = getenv("UNET_DZ_IN_LOADERS");
+        dz_in_loaders = e ? atoi(e) : 0;
+    }
+    // conv i backward from do_i (dense [P][cout]).
     // dgrad -> dx (ld ldx).  bn_next: dx is the `do` of BN layer i-1 (second conv of a
     // block), so the epilogue also emits that layer's partials; *rows = their count.
     auto conv_bwd = [&](int i, const float* dout, float* dx, int ldx, bool bn_next,
@@ -657,6 +665,10 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
                                    p.hpart, RED_G, grads + C.w, grads + C.b, s));
             return 0;
         }
+        if (!dz_in_loaders)
+            RUN("bn_dz", 0, k_bn_dz(const_cast<float*>(dout), p.y[i], p.ldy[i], p.offy[i], P, C.cout,
+                                    p.coef, s));
+        const float* dzc = dz_in_loaders ? p.coef : nullptr;
         Operand a = conv_input(c, p, i);
         WgradCfg wc = wgrad_cfg(C.cin, 9, C.cout, 1, P);
         WgradArgs w{};
@@ -678,7 +690,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         w.by = p.y[i];
         w.ldby = p.ldy[i];
         w.offby = p.offy[i];
-        w.bcoef = p.coef;
+        w.bcoef = dzc;
         w.bias_slab = p.bslab;
         w.Mw = 9 * C.cin;
         w.Nw = C.cout;
@@ -705,7 +717,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
             g.ay = p.y[i];
             g.lday = p.ldy[i];
             g.offay = p.offy[i];
-            g.acoef = p.coef;
+            g.acoef = dzc;
             g.bt = p.pack + C.pd;
             g.out = dx;
             g.ldo = ldx;
