@@ -130,9 +130,18 @@ def test_train_steps_match_golden(golden_dir):
     assert rel_max(ev, f["eval_logits"]) <= 2e-3
 
 
+def _to64(d):
+    return {k: (v.double() if v.is_floating_point() else v.clone()) for k, v in d.items()}
+
+
 def test_train_steps_strict_resync():
-    """Per-step strict parity over 3 steps: before every step the oracle restarts from this
-    path's current parameters, BN buffers and Adam moments (no trajectory drift)."""
+    """Per-step parity over 3 steps at lr 1e-4: before every step the oracle restarts from
+    this path's current parameters, BN buffers and Adam moments (no trajectory drift).
+
+    Gradients are judged against the fp64 evaluation of the same graph: per tensor the HIP
+    error must stay within 2x the fp32 reference's own error (+2e-4 floor) -- the criterion
+    of SURVEY.md §8c.  (Small bias / BN-beta gradients are sums of +/- terms that cancel to
+    ~1e-3 of their magnitude, so any two fp32 evaluations differ there by ~1e-3..1e-2.)"""
     import unet_hip
     P = O.make_params(42)
     x, t = inputs(1, 2, 64, 64)
@@ -142,6 +151,7 @@ def test_train_steps_strict_resync():
     for s in range(3):
         Pc = {k: v.detach().cpu().clone() for k, v in m.named_parameters()}
         Bc = {k: v.detach().cpu().clone() for k, v in m.named_buffers()}
+        r64 = O.train_step(_to64(Pc), _to64(Bc), None, x.double(), t.double())
         if s:
             for k, p in m.named_parameters():
                 ref_opt.m[k] = opt.state[p]["exp_avg"].detach().cpu().clone()
@@ -151,8 +161,10 @@ def test_train_steps_strict_resync():
         logits, losses, loss = _step(m, opt, x.to(DEV), t.to(DEV))
         assert rel_max(logits.cpu().numpy(), ref["logits"].numpy()) <= LOGIT_TOL, f"step {s}"
         assert abs(loss.item() - ref["loss"].item()) <= 1e-5
-        errs = grad_errors(m, ref["grads"])
-        assert max(errs.values()) <= GRAD_TOL, f"step {s}"
+        e_hip = grad_errors(m, r64["grads"])
+        for k, g in ref["grads"].items():
+            e32 = norm_rel(g, r64["grads"][k])
+            assert e_hip[k] <= 2 * e32 + 2e-4, f"step {s} {k}: hip {e_hip[k]:.2e} vs fp32 ref {e32:.2e}"
 
 
 def test_full_grads_vs_oracle_64():

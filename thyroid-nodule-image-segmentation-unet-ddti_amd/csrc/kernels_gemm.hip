@@ -277,12 +277,14 @@ __global__ __launch_bounds__(T::THREADS, 1) void rowgemm_kernel(RowGemmArgs p) {
             p.stats[(size_t)tile_m * 2 * p.N + p.N + n0 + tid] = q;
         }
     } else if constexpr (EMODE == E_STORE_BN) {
-        float q[NT][4];
+        // BN-backward partials are differences of nearly equal sums downstream (sum do can be
+        // 1e-3 of sum |do|): accumulate in f64, round once per block.
+        double q[NT][4];
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) {
             const int n = n0 + wn * WN + nt * 32 + li;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) q[nt][j] = 0.f;
+            for (int j = 0; j < 4; ++j) q[nt][j] = 0.0;
 #pragma unroll
             for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
@@ -293,10 +295,10 @@ __global__ __launch_bounds__(T::THREADS, 1) void rowgemm_kernel(RowGemmArgs p) {
                         p.out[(size_t)m * p.ldo + p.ooff + n] = v;
                         const float y = p.ey[(size_t)m * p.ldey + p.offey + n];
                         q[nt][0] += v;
-                        q[nt][1] += v * y;
+                        q[nt][1] += (double)v * y;
                         if (y > 0.f) {
                             q[nt][2] += v;
-                            q[nt][3] += 1.f;
+                            q[nt][3] += 1.0;
                         }
                     }
                 }
@@ -304,7 +306,7 @@ __global__ __launch_bounds__(T::THREADS, 1) void rowgemm_kernel(RowGemmArgs p) {
             for (int j = 0; j < 4; ++j) q[nt][j] += __shfl_xor(q[nt][j], 32);
         }
         __syncthreads();
-        float* red = smem;  // [WAVES_M][4][BN]
+        double* red = (double*)smem;  // [WAVES_M][4][BN]
         if (lh == 0) {
 #pragma unroll
             for (int nt = 0; nt < NT; ++nt)
@@ -315,10 +317,10 @@ __global__ __launch_bounds__(T::THREADS, 1) void rowgemm_kernel(RowGemmArgs p) {
         if (tid < BN) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                float a = 0.f;
+                double a = 0.0;
 #pragma unroll
                 for (int w = 0; w < WAVES_M; ++w) a += red[(w * 4 + j) * BN + tid];
-                p.stats[((size_t)tile_m * 4 + j) * p.N + n0 + tid] = a;
+                p.stats[((size_t)tile_m * 4 + j) * p.N + n0 + tid] = (float)a;
             }
         }
     } else if constexpr (EMODE == E_CONVT) {
@@ -406,7 +408,7 @@ __global__ __launch_bounds__(T::THREADS, 1) void wgrad_kernel(WgradArgs p) {
         cc = *(const f32x4*)(p.bcoef + 2 * p.CB + cb0 + bc4 * 4);
     }
     const bool bsum = p.bias_slab != nullptr && tm == 0;
-    f32x4 bacc = {0, 0, 0, 0};
+    double bacc[4] = {0.0, 0.0, 0.0, 0.0};  // f64: the bias gradient is a small sum of +/- terms
 
     const int pbeg = split * p.pps;
     int pend = pbeg + p.pps;
@@ -460,7 +462,9 @@ __global__ __launch_bounds__(T::THREADS, 1) void wgrad_kernel(WgradArgs p) {
                 for (int j = 0; j < 4; ++j) v[j] = ryb[i][j] > 0.f ? d[j] : 0.f;
             }
             if (!((bmask >> i) & 1u)) v = f32x4{0.f, 0.f, 0.f, 0.f};
-            if (bsum) bacc += v;
+            if (bsum)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) bacc[j] += v[j];
             *(f32x4*)&Bs[(brow + i * BRPP) * LDB + bc4 * 4] = v;
         }
     };
@@ -505,13 +509,17 @@ __global__ __launch_bounds__(T::THREADS, 1) void wgrad_kernel(WgradArgs p) {
 
     if (bsum) {  // column sums of B' for the bias gradient: combine the row groups in order
         __syncthreads();
-        f32x4* red = (f32x4*)As;
-        red[tid] = bacc;
+        double* red = (double*)As;  // [NTH][4]; As holds >= BKP*LDA floats >= 8*NTH
+#pragma unroll
+        for (int j = 0; j < 4; ++j) red[tid * 4 + j] = bacc[j];
         __syncthreads();
         if (tid < BF) {
-            f32x4 t = red[tid];
-            for (int g = 1; g < BRPP; ++g) t += red[g * BF + tid];
-            *(f32x4*)(p.bias_slab + (size_t)split * p.Nw + tn * BN + tid * 4) = t;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                double t = 0.0;
+                for (int g = 0; g < BRPP; ++g) t += red[(g * BF + tid) * 4 + j];
+                p.bias_slab[(size_t)split * p.Nw + tn * BN + tid * 4 + j] = (float)t;
+            }
         }
     }
 

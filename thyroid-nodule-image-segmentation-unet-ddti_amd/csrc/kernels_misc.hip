@@ -67,6 +67,30 @@ __device__ void block_combine(const f32x4 (&acc)[NV], int tpr, int C, float* out
     }
 }
 
+// f64 variant (BN-backward partials, where downstream differences of the sums cancel)
+template <int NV>
+__device__ void block_combine_d(const double (&acc)[NV][4], int tpr, int C, float* out,
+                                double* smem) {
+    const int tid = threadIdx.x;
+    const int g = tid / tpr, q = tid % tpr;
+    const int groups = blockDim.x / tpr;
+#pragma unroll
+    for (int v = 0; v < NV; ++v)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) smem[(v * blockDim.x + tid) * 4 + j] = acc[v][j];
+    __syncthreads();
+    if (g == 0) {
+#pragma unroll
+        for (int v = 0; v < NV; ++v)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                double a = 0.0;
+                for (int k = 0; k < groups; ++k) a += smem[(v * blockDim.x + k * tpr + q) * 4 + j];
+                out[v * C + 4 * q + j] = (float)a;
+            }
+    }
+}
+
 // -------------------------------------------------------------------------------------
 // Conv2d(1 -> C, 3x3, pad 1) + bias + ReLU + BN partials (encoder1.0, model.py:10,36-37).
 // K = 9 is too small for MFMA; one thread computes 4 channels of one pixel.
@@ -309,16 +333,18 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const float* __restric
                                                          int ldy, int offy, int N, int H, int W,
                                                          int C, float* __restrict__ dout,
                                                          float* partial) {
-    __shared__ __attribute__((aligned(16))) float smem[256 * 4 * 4];
+    __shared__ double smem[256 * 4 * 4];
     const int Ho = H / 2, Wo = W / 2;
     const int tpr = C / 4 < 256 ? C / 4 : 256, rpp = 256 / tpr;
     const int64_t PO = (int64_t)N * Ho * Wo;
-    f32x4 acc[4];
+    double acc[4][4];
     for (int c0 = 0; c0 < C; c0 += 4 * tpr) {
         const int q = threadIdx.x % tpr, g = threadIdx.x / tpr;
         const int c = c0 + 4 * q;
 #pragma unroll
-        for (int v = 0; v < 4; ++v) acc[v] = f32x4{0, 0, 0, 0};
+        for (int v = 0; v < 4; ++v)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[v][j] = 0.0;
         const int64_t per = (PO + gridDim.x - 1) / gridDim.x;
         const int64_t r0 = blockIdx.x * per, r1 = r0 + per < PO ? r0 + per : PO;
         for (int64_t po = r0 + g; po < r1; po += rpp) {
@@ -336,17 +362,18 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const float* __restric
                     if (((bi >> (8 * j)) & 0xFF) == (uint32_t)k) v[j] += gp[j];
                 *(f32x4*)(dout + pin * C + c) = v;
                 const f32x4 yv = *(const f32x4*)(y + pin * ldy + offy + c);
-                acc[0] += v;
-                acc[1] += v * yv;
 #pragma unroll
-                for (int j = 0; j < 4; ++j)
+                for (int j = 0; j < 4; ++j) {
+                    acc[0][j] += v[j];
+                    acc[1][j] += (double)v[j] * yv[j];
                     if (yv[j] > 0.f) {
                         acc[2][j] += v[j];
-                        acc[3][j] += 1.f;
+                        acc[3][j] += 1.0;
                     }
+                }
             }
         }
-        block_combine<4>(acc, tpr, C, partial + (int64_t)blockIdx.x * 4 * C + c0, smem);
+        block_combine_d<4>(acc, tpr, C, partial + (int64_t)blockIdx.x * 4 * C + c0, smem);
         __syncthreads();
     }
 }
@@ -611,8 +638,8 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__
                                                       float* __restrict__ dout, float* partial,
                                                       float* bnpart) {
     __shared__ float red[256 * 5];
-    __shared__ __attribute__((aligned(16))) float smem4[256 * 4 * 4];
-    f32x4 bq[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
+    __shared__ double smem4[256 * 4 * 4];
+    double bq[4][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
     const int lpp = C / 4, rpp = 256 / lpp;
     const int q = threadIdx.x % lpp, g = threadIdx.x / lpp;
     const f32x4 sc = *(const f32x4*)(scale + 4 * q), sh = *(const f32x4*)(shift + 4 * q);
@@ -633,16 +660,17 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__
             ab[o] += dl;
         }
         *(f32x4*)(dout + (int64_t)m * C + 4 * q) = d;
-        bq[0] += d;
-        bq[1] += d * yr;
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < 4; ++j) {
+            bq[0][j] += d[j];
+            bq[1][j] += (double)d[j] * yr[j];
             if (yr[j] > 0.f) {
                 bq[2][j] += d[j];
-                bq[3][j] += 1.f;
+                bq[3][j] += 1.0;
             }
+        }
     }
-    block_combine<4>(bq, lpp, C, bnpart + (int64_t)blockIdx.x * 4 * C, smem4);
+    block_combine_d<4>(bq, lpp, C, bnpart + (int64_t)blockIdx.x * 4 * C, smem4);
     __syncthreads();
     // combine over row groups through LDS, one quantity at a time
     float* out = partial + (int64_t)blockIdx.x * (O * C + O);
