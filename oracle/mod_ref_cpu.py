@@ -1,0 +1,141 @@
+"""torch-CPU restatement of ``models/mod.py:UNet`` (test infra only).
+
+The variant ``main.py``-style configs reach through ``models/mod.py:9-66`` (SURVEY.md §8
+row a19, BASELINE config 4).  Differences from ``models/model.py:UNet`` that the
+restatement follows:
+
+* ``_block`` (``mod.py:43-51``): Conv3x3 **without bias** -> BN -> ReLU -> Conv3x3 (no
+  bias) -> BN -> ReLU (BN before ReLU).
+* ``depth`` encoders of ``base_filters * 2**i`` channels, each followed by MaxPool2d(2)
+  (``mod.py:25-30``); bottleneck ``_block(C, 2C)`` (``:32``).
+* decoder step (``:59-65``): ConvTranspose2d(k2, s2, bias) **first**, then the concat
+  ``[skip, up]`` (skip first), then ``_block(2C, C)``; ``F.interpolate`` only when the
+  shapes differ (never for H, W divisible by 2**depth, which the path requires).
+* head: ``final_conv`` Conv2d(base, out, 1) with bias (``:41``).
+
+Parameters are named and ordered exactly like ``named_parameters()`` of the reference
+module (encoders.*, bottleneck.*, upconvs.*, decoders.*, final_conv.*).  Losses, the
+train step and AdamW are shared with ``unet_ref_cpu``.
+"""
+import torch
+import torch.nn.functional as F
+
+from . import unet_ref_cpu as O
+from . import weights as W
+
+
+def _block_spec(spec, prefix, cin, cout):
+    spec.append((f"{prefix}.0.weight", (cout, cin, 3, 3), "conv_w"))
+    spec.append((f"{prefix}.1.weight", (cout,), "bn_w"))
+    spec.append((f"{prefix}.1.bias", (cout,), "bn_b"))
+    spec.append((f"{prefix}.3.weight", (cout, cout, 3, 3), "conv_w"))
+    spec.append((f"{prefix}.4.weight", (cout,), "bn_w"))
+    spec.append((f"{prefix}.4.bias", (cout,), "bn_b"))
+
+
+def param_spec(in_channels=1, out_channels=1, base=64, depth=5):
+    """(name, shape, kind[, fan_in]) in named_parameters() order of mod.py:UNet."""
+    spec = []
+    ch = [base * (2 ** i) for i in range(depth)]
+    prev = in_channels
+    for i, c in enumerate(ch):                       # mod.py:27-30
+        _block_spec(spec, f"encoders.{i}", prev, c)
+        prev = c
+    _block_spec(spec, "bottleneck", prev, 2 * prev)  # mod.py:32
+    prev = ch[-1] * 2
+    ups = []
+    for j, c in enumerate(ch[::-1]):                 # mod.py:37-40
+        ups.append((j, prev, c))
+        prev = c
+    for j, cin, cout in ups:                         # ModuleList `upconvs` registers first
+        spec.append((f"upconvs.{j}.weight", (cin, cout, 2, 2), "convT_w"))
+        spec.append((f"upconvs.{j}.bias", (cout,), "convT_b", cout * 4))
+    for j, cin, cout in ups:
+        _block_spec(spec, f"decoders.{j}", cin, cout)
+    spec.append(("final_conv.weight", (out_channels, base, 1, 1), "conv_w"))
+    spec.append(("final_conv.bias", (out_channels,), "conv_b", base))
+    return spec
+
+
+def bn_layers(base=64, depth=5):
+    """[(name, channels)] in named_buffers() order."""
+    ch = [base * (2 ** i) for i in range(depth)]
+    out = []
+    for i, c in enumerate(ch):
+        out += [(f"encoders.{i}.1", c), (f"encoders.{i}.4", c)]
+    out += [("bottleneck.1", 2 * ch[-1]), ("bottleneck.4", 2 * ch[-1])]
+    for j, c in enumerate(ch[::-1]):
+        out += [(f"decoders.{j}.1", c), (f"decoders.{j}.4", c)]
+    return out
+
+
+def init_buffers(base=64, depth=5):
+    buf = {}
+    for name, c in bn_layers(base, depth):
+        buf[f"{name}.running_mean"] = torch.zeros(c)
+        buf[f"{name}.running_var"] = torch.ones(c)
+        buf[f"{name}.num_batches_tracked"] = torch.tensor(0, dtype=torch.long)
+    return buf
+
+
+def make_params(seed=42, base=64, depth=5, gamma_lo=0.5, gamma_hi=1.5, in_channels=1,
+                out_channels=1):
+    p = W.make_params(param_spec(in_channels, out_channels, base, depth), seed, gamma_lo, gamma_hi)
+    return {k: torch.from_numpy(v) for k, v in p.items()}
+
+
+def _block(x, P, B, prefix, training):
+    # mod.py:43-51
+    x = F.conv2d(x, P[f"{prefix}.0.weight"], None, padding=1)
+    x = F.relu(O._bn(x, P, B, f"{prefix}.1", training))
+    x = F.conv2d(x, P[f"{prefix}.3.weight"], None, padding=1)
+    return F.relu(O._bn(x, P, B, f"{prefix}.4", training))
+
+
+def make_forward(depth):
+    """forward(x, P, B, training) of mod.py:UNet with `depth` levels (mod.py:53-66)."""
+
+    def forward(x, P, B, training=True):
+        skips = []
+        for i in range(depth):
+            x = _block(x, P, B, f"encoders.{i}", training)
+            skips.append(x)
+            x = F.max_pool2d(x, 2, 2)
+        x = _block(x, P, B, "bottleneck", training)
+        for j, skip in enumerate(reversed(skips)):
+            x = F.conv_transpose2d(x, P[f"upconvs.{j}.weight"], P[f"upconvs.{j}.bias"], stride=2)
+            if x.shape != skip.shape:
+                x = F.interpolate(x, size=skip.shape[2:], mode="bilinear", align_corners=False)
+            x = torch.cat([skip, x], dim=1)
+            x = _block(x, P, B, f"decoders.{j}", training)
+        return F.conv2d(x, P["final_conv.weight"], P["final_conv.bias"])
+
+    return forward
+
+
+def train_step(P, B, opt, x, t, depth, w_bce=1.0, w_dice=1.0, shards=1):
+    """utils/trainer.py:81-93 with mod.py:UNet as the model."""
+    return O.train_step(P, B, opt, x, t, w_bce, w_dice, shards, forward_fn=make_forward(depth))
+
+
+def conv_macs_per_image(H, W, in_channels=1, out_channels=1, base=64, depth=5):
+    macs = 0
+    prev = in_channels
+    for i in range(depth + 1):                    # encoders + bottleneck
+        c = base << i
+        hw = (H >> i) * (W >> i)
+        macs += hw * 9 * (prev * c + c * c)
+        prev = c
+    for l in range(depth - 1, -1, -1):            # upconv into level l, then the block
+        c = base << l
+        hw_in = (H >> (l + 1)) * (W >> (l + 1))
+        macs += hw_in * (2 * c) * c * 4
+        hw = (H >> l) * (W >> l)
+        macs += hw * 9 * (2 * c * c + c * c)
+    macs += H * W * base * out_channels
+    return macs
+
+
+def train_flops_per_image(H, W, base=64, depth=5):
+    """fwd + dgrad + wgrad minus the first conv's unneeded dgrad."""
+    return 6 * conv_macs_per_image(H, W, base=base, depth=depth) - 2 * (H * W * 9 * base)

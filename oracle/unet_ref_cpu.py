@@ -203,20 +203,22 @@ class AdamWState:
                 p.addcdiv_(self.m[k], denom, value=-step_size)
 
 
-def train_step(P, B, opt, x, t, w_bce=1.0, w_dice=1.0, shards=1):
+def train_step(P, B, opt, x, t, w_bce=1.0, w_dice=1.0, shards=1, forward_fn=None):
     """utils/trainer.py:81-93 for one batch.  ``shards`` > 1 emulates nn.DataParallel
     (utils/trainer.py:28-30): the batch is split on dim 0, every shard runs its own
     train-mode BN, logits are gathered and the loss is taken on the full batch.
     (Only shard 0's running stats are kept, as DP keeps replica 0's.)
+    ``forward_fn`` replaces models/model.py's graph (e.g. mod_ref_cpu.make_forward).
     Returns dict(logits, loss, bce, dice, grads)."""
+    fwd = forward if forward_fn is None else forward_fn
     Pg = {k: v.detach().clone().requires_grad_(True) for k, v in P.items()}
     if shards == 1:
-        logits = forward(x, Pg, B, True)
+        logits = fwd(x, Pg, B, True)
     else:
         outs = []
         for s, xs in enumerate(torch.chunk(x, shards, dim=0)):
             Bs = B if s == 0 else {k: v.clone() for k, v in B.items()}
-            outs.append(forward(xs, Pg, Bs, True))
+            outs.append(fwd(xs, Pg, Bs, True))
         logits = torch.cat(outs, 0)
     bce = bce_with_logits(logits, t)
     dice = dice_loss(logits, t)

@@ -119,3 +119,53 @@ def test_oracle_negative_gamma(golden_dir):
     assert np.max(np.abs(r["logits"].numpy() - ref)) <= 1e-5 * np.max(np.abs(ref))
     _check_grads(_grad_stats(r["grads"], O.param_spec()), f["grad_norm"], f["grad_sum"],
                  f["grad_samp"], rtol=1e-4)
+
+
+def test_mod_param_spec_and_flops():
+    from oracle import mod_ref_cpu as MO
+    spec = MO.param_spec(1, 1, 128, 5)
+    assert sum(int(np.prod(s[1])) for s in spec) == 497_438_849
+    assert MO.train_flops_per_image(512, 512, 128, 5) == 5_709_420_822_528  # §8d config 4
+
+
+@pytest.mark.parametrize("tag,seed,lo,hi", [("", 42, 0.5, 1.5), ("neg_", 5, -1.0, 1.0)])
+def test_oracle_mod_d3_two_steps(golden_dir, tag, seed, lo, hi):
+    """models/mod.py UNet(base 64, depth 3): BN->ReLU, [skip, up], bias-free convs."""
+    from oracle import mod_ref_cpu as MO
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    f = _load(golden_dir, "mod_d3_64.npz")
+    P = MO.make_params(seed, 64, 3, lo, hi)
+    B = MO.init_buffers(64, 3)
+    opt = O.AdamWState(P, lr=1e-4)
+    x = torch.from_numpy(W.make_input(11, 2, 1, 64, 64))
+    t = torch.from_numpy(W.make_target(11, 2, 64, 64))
+    spec = MO.param_spec(1, 1, 64, 3)
+    names = [n for n, _ in MO.bn_layers(64, 3)]
+    for s in range(2):
+        p = f"{tag}s{s}_"
+        r = MO.train_step(P, B, opt, x, t, depth=3)
+        ref = f[p + "logits"]
+        assert np.max(np.abs(r["logits"].numpy() - ref)) <= 1e-5 * np.max(np.abs(ref))
+        assert abs(r["loss"].item() - float(f[p + "loss"])) < 1e-6
+        _check_grads(_grad_stats(r["grads"], spec), f[p + "grad_norm"], f[p + "grad_sum"],
+                     f[p + "grad_samp"], rtol=1e-4)
+        rm = np.concatenate([B[f"{n}.running_mean"].numpy() for n in names])
+        np.testing.assert_allclose(rm, f[p + "running_mean"], rtol=1e-5, atol=1e-6)
+    with torch.no_grad():
+        ev = MO.make_forward(3)(x, P, B, training=False).numpy()
+    assert np.max(np.abs(ev - f[tag + "eval_logits"])) <= 1e-5 * np.max(np.abs(f[tag + "eval_logits"]))
+
+
+def test_oracle_mod_config4_arch(golden_dir):
+    """The config-4 architecture (base 128, depth 5, 497 M params) at B=2 64x64."""
+    from oracle import mod_ref_cpu as MO
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    f = _load(golden_dir, "mod_c4_64.npz")
+    P = MO.make_params(42, 128, 5)
+    x = torch.from_numpy(W.make_input(12, 2, 1, 64, 64))
+    t = torch.from_numpy(W.make_target(12, 2, 64, 64))
+    r = MO.train_step(P, MO.init_buffers(128, 5), None, x, t, depth=5)
+    assert np.max(np.abs(r["logits"].numpy() - f["logits"])) <= 1e-5 * np.max(np.abs(f["logits"]))
+    assert abs(r["loss"].item() - float(f["loss"])) < 1e-6
+    _check_grads(_grad_stats(r["grads"], MO.param_spec(1, 1, 128, 5)), f["grad_norm"],
+                 f["grad_sum"], f["grad_samp"], rtol=1e-4)

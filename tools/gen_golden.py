@@ -24,6 +24,12 @@ Fixtures (all float64 statistics computed from fp32 results):
                     full-batch loss): losses and grad norm/sum/samples.
   unet_neg_32.npz   B=2, 1x32x32 with BN gamma in [-1, 1] (max-pool after a sign flip),
                     one step: full logits, grad norm/sum/samples.
+  mod_d3_64.npz     models/mod.py UNet(base 64, depth 3), B=2 1x64x64, 2 AdamW steps
+                    (lr 1e-4): full logits, masks, losses, grad norm/sum/samples, param
+                    samples, running stats; gamma in [-1, 1] on a second case (neg_*).
+  mod_c4_64.npz     models/mod.py UNet(base 128, depth 5) -- the config-4 architecture,
+                    497,438,849 params -- at B=2 1x64x64, one step: full logits, losses,
+                    grad norm/sum/samples.
 """
 import os
 import sys
@@ -38,9 +44,11 @@ sys.path.insert(0, REF)
 
 from models.model import UNet as RefUNet  # noqa: E402  (reference)
 from models.loss import DiceLoss as RefDice  # noqa: E402  (reference)
+from models.mod import UNet as RefModUNet  # noqa: E402  (reference, models/mod.py:9-66)
 
 from oracle import weights as W  # noqa: E402
 from oracle import unet_ref_cpu as O  # noqa: E402
+from oracle import mod_ref_cpu as MO  # noqa: E402
 
 OUT = os.path.join(REPO, "tests", "golden")
 NSAMP = 64
@@ -178,6 +186,62 @@ def case_neg_32():
     np.savez_compressed(os.path.join(OUT, "unet_neg_32.npz"), **out)
 
 
+def build_mod(base, depth, seed=42, gamma_lo=0.5, gamma_hi=1.5):
+    torch.manual_seed(0)
+    m = RefModUNet(1, 1, base_filters=base, depth=depth)
+    spec = MO.param_spec(1, 1, base, depth)
+    assert [n for n, _ in m.named_parameters()] == [s[0] for s in spec], "mod param order"
+    assert [n for n, _ in m.named_buffers() if n.endswith("running_mean")] == \
+        [f"{n}.running_mean" for n, _ in MO.bn_layers(base, depth)], "mod buffer order"
+    params = MO.make_params(seed, base, depth, gamma_lo, gamma_hi)
+    sd = m.state_dict()
+    for k, v in params.items():
+        sd[k] = v.clone()
+    m.load_state_dict(sd)
+    return m
+
+
+def case_mod_d3_64():
+    out = {}
+    for tag, (seed, lo, hi) in (("", (42, 0.5, 1.5)), ("neg_", (5, -1.0, 1.0))):
+        m = build_mod(64, 3, seed, lo, hi)
+        m.train()
+        x = torch.from_numpy(W.make_input(11, 2, 1, 64, 64))
+        t = torch.from_numpy(W.make_target(11, 2, 64, 64))
+        opt = torch.optim.AdamW(m.parameters(), lr=1e-4)
+        names = [n for n, _ in MO.bn_layers(64, 3)]
+        for s in range(2):
+            logits, lb, ld, loss = step(m, opt, x, t, RefDice())
+            p = f"{tag}s{s}_"
+            out[p + "logits"] = logits.numpy()
+            out[p + "mask"] = (torch.sigmoid(logits) > 0.5).numpy().astype(np.uint8)
+            out[p + "bce"], out[p + "dice"], out[p + "loss"] = lb, ld, loss
+            grad_stats(m, p, out)
+            out[p + "params_samp"] = param_samples(m)
+            bufs = dict(m.named_buffers())
+            out[p + "running_mean"] = np.concatenate([bufs[f"{n}.running_mean"].numpy() for n in names])
+            out[p + "running_var"] = np.concatenate([bufs[f"{n}.running_var"].numpy() for n in names])
+        m.eval()
+        with torch.no_grad():
+            out[tag + "eval_logits"] = m(x).numpy()
+    np.savez_compressed(os.path.join(OUT, "mod_d3_64.npz"), **out)
+
+
+def case_mod_c4_64():
+    m = build_mod(128, 5)
+    m.train()
+    x = torch.from_numpy(W.make_input(12, 2, 1, 64, 64))
+    t = torch.from_numpy(W.make_target(12, 2, 64, 64))
+    logits = m(x)
+    lb = torch.nn.BCEWithLogitsLoss()(logits, t)
+    ld = RefDice()(logits, t)
+    loss = lb + ld
+    loss.backward()
+    out = dict(logits=logits.detach().numpy(), bce=lb.item(), dice=ld.item(), loss=loss.item())
+    grad_stats(m, "", out)
+    np.savez_compressed(os.path.join(OUT, "mod_c4_64.npz"), **out)
+
+
 if __name__ == "__main__":
     torch.set_num_threads(8)
     os.makedirs(OUT, exist_ok=True)
@@ -185,5 +249,7 @@ if __name__ == "__main__":
     case_b2_256()
     case_dp2_64()
     case_neg_32()
+    case_mod_d3_64()
+    case_mod_c4_64()
     for f in sorted(os.listdir(OUT)):
         print(f, os.path.getsize(os.path.join(OUT, f)))
