@@ -64,12 +64,24 @@ typedef enum {
     UNET_ERR_UNSUPPORTED = -5  /* configuration not implemented */
 } unet_status;
 
+/* Which reference network the context runs. */
+typedef enum {
+    UNET_VARIANT_MODEL = 0, /* models/model.py:UNet -- Conv(+bias) -> ReLU -> BN blocks,
+                               concat [up, skip], depth 4, base 64 (fixed) */
+    UNET_VARIANT_MOD = 1    /* models/mod.py:9-66 UNet -- Conv(no bias) -> BN -> ReLU blocks,
+                               concat [skip, up], base_filters / depth configurable */
+} unet_variant;
+
 typedef struct {
-    int in_channels;   /* models/model.py:6 in_channels (default 1)  */
-    int out_channels;  /* models/model.py:6 out_channels (default 1) */
+    int in_channels;   /* models/model.py:6 / mod.py:11 in_channels (default 1; must be 1) */
+    int out_channels;  /* models/model.py:6 / mod.py:12 out_channels (default 1; 1..4)   */
+    int variant;       /* unet_variant (0 = models/model.py)                               */
+    int base_filters;  /* mod.py:13 (0 = default 64); a multiple of 64, <= 256             */
+    int depth;         /* mod.py:14 (0 = default 5 for mod, 4 for model); 1..6             */
 } unet_cfg;
 
-/* models/model.py:6-31.  device = HIP ordinal the context will launch on. */
+/* models/model.py:6-31 / models/mod.py:10-41.  device = HIP ordinal the context will
+ * launch on.  Zero-initialised fields take the reference defaults. */
 int unet_create(const unet_cfg* cfg, int device, unet_ctx** out);
 int unet_destroy(unet_ctx* ctx);
 const char* unet_last_error(const unet_ctx* ctx);
@@ -83,7 +95,8 @@ int unet_param_info(const unet_ctx* ctx, int i, const char** name, int* ndim, in
 int unet_num_bn(const unet_ctx* ctx, int* n_layers, int64_t* n_floats);
 int unet_bn_info(const unet_ctx* ctx, int i, const char** name, int* channels, int64_t* offset);
 
-/* Bytes of device workspace for one forward (+backward when training) at (N, H, W). */
+/* Bytes of device workspace for one forward (+backward when training) at (N, H, W).
+ * H and W must be multiples of max(16, 2**depth). */
 int unet_workspace_size(unet_ctx* ctx, int N, int H, int W, int training, size_t* bytes);
 
 /* Forward.  params: flat arena; bn_running: running-stat arena (updated when training);

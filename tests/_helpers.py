@@ -47,3 +47,17 @@ def masks_agree(mask, ref_mask, ref_logits, tol):
 def inputs(seed, B, H, W):
     return (torch.from_numpy(Wt.make_input(seed, B, 1, H, W)),
             torch.from_numpy(Wt.make_target(seed, B, H, W)))
+
+
+def hip_mod_model(P, dev, base, depth, buffers=None):
+    """models/mod.py UNet(base_filters=base, depth=depth) on the HIP path with params P."""
+    import unet_hip
+    from oracle import mod_ref_cpu as MO
+    m = unet_hip.ModUNet(1, 1, base_filters=base, depth=depth)
+    sd = m.state_dict()
+    for k, v in P.items():
+        sd[k] = v.clone()
+    for k, v in (buffers or MO.init_buffers(base, depth)).items():
+        sd[k] = v.clone()
+    m.load_state_dict(sd)
+    return m.to(dev).train()

@@ -1,0 +1,151 @@
+"""GPU parity of the models/mod.py UNet variant (bias-free Conv ->
+BN -> ReLU blocks, concat [skip, up], configurable base / depth) against the CPU oracle
+(oracle/mod_ref_cpu.py) and the reference-generated fixtures (tests/golden/mod_*.npz).
+
+Same bars as tests/test_gpu_parity.py: logits max|d| <= 1e-4 max|ref|, losses <= 1e-5,
+gradients <= 1e-2 norm-relative per tensor at step 0."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from _helpers import grad_errors, hip_mod_model, inputs, masks_agree, norm_rel, rel_max
+from oracle import mod_ref_cpu as MO
+from oracle import weights as Wt
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda:0")
+LOGIT_TOL = 1e-4
+GRAD_TOL = 1e-2
+
+
+@pytest.fixture(autouse=True, scope="module")
+def _threads():
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+
+
+def _golden(golden_dir, name):
+    return np.load(os.path.join(golden_dir, name), allow_pickle=False)
+
+
+def _step(m, opt, x, t):
+    import unet_hip
+    opt.zero_grad()
+    logits = m(x)
+    losses = unet_hip.seg_losses(logits, t)
+    loss = losses[0] + losses[1]
+    loss.backward()
+    opt.step()
+    return logits.detach(), losses.detach()
+
+
+def _check_grad_stats(m, spec, norms, samp, tol, tag):
+    named = dict(m.named_parameters())
+    for ti, item in enumerate(spec):
+        g = named[item[0]].grad.detach().double().cpu().reshape(-1)
+        idx = np.floor(Wt.uniform(7, 3000 + ti, 64) * g.numel()).astype(np.int64)
+        assert abs(g.norm().item() - norms[ti]) <= tol * norms[ti], f"{tag} {item[0]} norm"
+        assert np.max(np.abs(g[idx].numpy() - samp[ti])) <= tol * norms[ti], f"{tag} {item[0]}"
+
+
+def test_mod_forward_layers_match_oracle():
+    """Train-mode forward of UNet(base 64, depth 3), B=2 64x64, logits vs the oracle."""
+    P = MO.make_params(42, 64, 3)
+    x, _ = inputs(1, 2, 64, 64)
+    ref = MO.make_forward(3)(x, P, MO.init_buffers(64, 3), True)
+    m = hip_mod_model(P, DEV, 64, 3)
+    with torch.no_grad():
+        lg = m(x.to(DEV)).cpu()
+    assert rel_max(lg.numpy(), ref.numpy()) <= LOGIT_TOL
+
+
+@pytest.mark.parametrize("tag,seed,lo,hi", [("", 42, 0.5, 1.5), ("neg_", 5, -1.0, 1.0)])
+def test_mod_train_steps_match_golden(golden_dir, tag, seed, lo, hi):
+    """Two AdamW steps (lr 1e-4) of UNet(base 64, depth 3) vs the reference's own outputs;
+    the gamma in [-1, 1] case exercises the max-pool / ReLU masks after a sign flip."""
+    import unet_hip
+    f = _golden(golden_dir, "mod_d3_64.npz")
+    m = hip_mod_model(MO.make_params(seed, 64, 3, lo, hi), DEV, 64, 3)
+    opt = unet_hip.HipAdamW(m.parameters(), lr=1e-4)
+    x = torch.from_numpy(Wt.make_input(11, 2, 1, 64, 64)).to(DEV)
+    t = torch.from_numpy(Wt.make_target(11, 2, 64, 64)).to(DEV)
+    spec = MO.param_spec(1, 1, 64, 3)
+    names = [n for n, _ in MO.bn_layers(64, 3)]
+    for s in range(2):
+        p = f"{tag}s{s}_"
+        tol = LOGIT_TOL if s == 0 else 2e-3
+        logits, losses = _step(m, opt, x, t)
+        ref = f[p + "logits"]
+        assert rel_max(logits.cpu().numpy(), ref) <= tol, f"{p} logits"
+        ok, nd = masks_agree((torch.sigmoid(logits) > 0.5).cpu().numpy().astype(np.uint8),
+                             f[p + "mask"], ref, 10 * tol * np.abs(ref).max())
+        assert ok, f"{p}: {nd} mask bits differ away from the decision boundary"
+        assert abs(losses[0].item() - float(f[p + "bce"])) <= (1e-5 if s == 0 else 1e-4)
+        assert abs(losses[1].item() - float(f[p + "dice"])) <= (1e-5 if s == 0 else 1e-4)
+        _check_grad_stats(m, spec, f[p + "grad_norm"], f[p + "grad_samp"],
+                          GRAD_TOL if s == 0 else 10 * GRAD_TOL, p)
+        sd = m.state_dict()
+        rm = torch.cat([sd[f"{n}.running_mean"].cpu() for n in names]).numpy()
+        btol = 1e-4 if s == 0 else 1e-3
+        np.testing.assert_allclose(rm, f[p + "running_mean"], rtol=btol, atol=btol)
+    m.eval()
+    with torch.no_grad():
+        ev = m(x).cpu().numpy()
+    assert rel_max(ev, f[tag + "eval_logits"]) <= 2e-3
+
+
+def test_mod_full_grads_vs_oracle():
+    """Every element of every gradient of UNet(base 64, depth 3) vs the oracle."""
+    import unet_hip
+    P = MO.make_params(42, 64, 3)
+    x, t = inputs(3, 2, 64, 64)
+    ref = MO.train_step(P, MO.init_buffers(64, 3), None, x, t, depth=3)
+    m = hip_mod_model(P, DEV, 64, 3)
+    logits = m(x.to(DEV))
+    losses = unet_hip.seg_losses(logits, t.to(DEV))
+    (losses[0] + losses[1]).backward()
+    assert rel_max(logits.detach().cpu().numpy(), ref["logits"].numpy()) <= LOGIT_TOL
+    errs = grad_errors(m, ref["grads"])
+    worst = max(errs, key=errs.get)
+    assert errs[worst] <= GRAD_TOL, f"{worst}: {errs[worst]:.3e}"
+
+
+def test_mod_config4_architecture(golden_dir):
+    """The config-4 network (base 128, depth 5, 497 M params; 2048 / 4096-channel
+    bottleneck) at B=2 64x64, one step vs the reference's fixture."""
+    import unet_hip
+    f = _golden(golden_dir, "mod_c4_64.npz")
+    m = hip_mod_model(MO.make_params(42, 128, 5), DEV, 128, 5)
+    x = torch.from_numpy(Wt.make_input(12, 2, 1, 64, 64)).to(DEV)
+    t = torch.from_numpy(Wt.make_target(12, 2, 64, 64)).to(DEV)
+    logits = m(x)
+    losses = unet_hip.seg_losses(logits, t)
+    (losses[0] + losses[1]).backward()
+    assert rel_max(logits.detach().cpu().numpy(), f["logits"]) <= LOGIT_TOL
+    assert abs((losses[0] + losses[1]).item() - float(f["loss"])) <= 1e-5
+    _check_grad_stats(m, MO.param_spec(1, 1, 128, 5), f["grad_norm"], f["grad_samp"], GRAD_TOL,
+                      "c4")
+
+
+def test_mod_config4_full_size_smoke():
+    """Config 4 at its own size (512x512, bs 2): finite loss, and the BN batch statistics
+    of the first layer match a torch evaluation of the same conv on the GPU."""
+    import unet_hip
+    torch.manual_seed(0)
+    m = unet_hip.ModUNet(1, 1, base_filters=128, depth=5).to(DEV).train()
+    x = torch.rand(2, 1, 512, 512, device=DEV)
+    t = (torch.rand(2, 1, 512, 512, device=DEV) > 0.5).float()
+    logits = m(x)
+    losses = unet_hip.seg_losses(logits, t)
+    (losses[0] + losses[1]).backward()
+    assert torch.isfinite(logits).all() and torch.isfinite(losses).all()
+    g = torch.cat([p.grad.reshape(-1) for p in m.parameters()])
+    assert torch.isfinite(g).all() and g.abs().sum() > 0
+    w = m.encoders[0][0].weight.detach()
+    z = torch.nn.functional.conv2d(x, w, None, padding=1)
+    bn = m.encoders[0][1]
+    mean = z.mean((0, 2, 3))
+    # running_mean after one step = 0.1 * batch mean
+    assert norm_rel(bn.running_mean.cpu(), 0.1 * mean.cpu()) <= 1e-4

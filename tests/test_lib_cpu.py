@@ -134,3 +134,82 @@ def test_init_consumes_rng_like_reference():
     b = unet_hip.UNet(1, 1)
     for (na, pa), (nb, pb) in zip(a.state_dict().items(), b.state_dict().items()):
         assert na == nb and torch.equal(pa, pb), na
+
+
+# ---------------------------------------------------------------- models/mod.py:UNet
+MOD_CFGS = [(64, 3), (64, 5), (128, 5)]
+
+
+def _mod_rt(base, depth):
+    from unet_hip import _lib
+    from unet_hip.runtime import UNetRuntime
+    return UNetRuntime.get("cuda:0", 1, 1, _lib.VARIANT_MOD, base, depth)
+
+
+@pytest.mark.parametrize("base,depth", MOD_CFGS)
+def test_mod_tables_match_reference_layout(base, depth):
+    from oracle import mod_ref_cpu as MO
+    rt = _mod_rt(base, depth)
+    spec = MO.param_spec(1, 1, base, depth)
+    assert [p[0] for p in rt.params] == [s[0] for s in spec]
+    off = 0
+    for (name, shape, o), s in zip(rt.params, spec):
+        assert tuple(shape) == tuple(s[1]), name
+        assert o == off
+        off += int(np.prod(shape))
+    assert rt.n_param_floats == off
+    assert [(b[0], b[1]) for b in rt.bn] == MO.bn_layers(base, depth)
+    spans = sorted(rt.buckets)
+    pos = 0
+    for o, n in spans:
+        assert o == pos and n > 0
+        pos += n
+    assert pos == rt.n_param_floats
+    offs = [o for o, _ in rt.buckets]
+    assert offs == sorted(offs, reverse=True)
+    if (base, depth) == (128, 5):
+        assert rt.n_param_floats == 497_438_849
+
+
+def test_mod_config4_workspace():
+    rt = _mod_rt(128, 5)
+    # BASELINE config 4: 512^2, bs >= 8 fits easily in 288 GB
+    b = rt.workspace_bytes(8, 512, 512, True)
+    assert 10e9 < b < 120e9
+    from unet_hip._lib import HipError
+    with pytest.raises(HipError):
+        rt.workspace_bytes(2, 48, 48, True)  # not a multiple of 2**5
+
+
+def test_unsupported_configs_rejected():
+    from unet_hip import _lib
+    from unet_hip.runtime import UNetRuntime
+    for args in [(1, 1, _lib.VARIANT_MOD, 32, 5), (1, 1, _lib.VARIANT_MODEL, 64, 5),
+                 (3, 1, _lib.VARIANT_MOD, 64, 4), (1, 1, 7, 64, 4)]:
+        with pytest.raises(_lib.HipError):
+            UNetRuntime("cuda:0", *args)
+
+
+def test_mod_state_dict_and_rng_like_reference():
+    import torch
+    import unet_hip
+    from oracle import mod_ref_cpu as MO
+    m = unet_hip.ModUNet(1, 1, base_filters=64, depth=3)
+    assert [n for n, _ in m.named_parameters()] == [s[0] for s in MO.param_spec(1, 1, 64, 3)]
+    want = []
+    for n, _ in MO.bn_layers(64, 3):
+        want += [f"{n}.running_mean", f"{n}.running_var", f"{n}.num_batches_tracked"]
+    assert [n for n, _ in m.named_buffers()] == want
+    ref_dir = "/root/reference"
+    if not os.path.isdir(ref_dir):
+        pytest.skip("reference not present (GPU box)")
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("_ref_mod", os.path.join(ref_dir, "models", "mod.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    torch.manual_seed(42)
+    a = mod.UNet(1, 1, base_filters=64, depth=3)
+    torch.manual_seed(42)
+    b = unet_hip.ModUNet(1, 1, base_filters=64, depth=3)
+    for (na, pa), (nb, pb) in zip(a.state_dict().items(), b.state_dict().items()):
+        assert na == nb and torch.equal(pa, pb), na

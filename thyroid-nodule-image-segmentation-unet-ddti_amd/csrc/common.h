@@ -24,16 +24,22 @@ static inline int gather_taps(int mode) { return mode == G_CONV3 ? 9 : (mode == 
 //   E_CONVT          : ConvTranspose2d scatter, n = (a*2+b)*cout + co ->
 //                      out[(2y+a, 2x+b)][co] = acc + b[co]  (models/model.py:19)
 //   E_STORE_BN       : out[m][n] = acc, and the result is the gradient `do` of a BatchNorm
-//                      output: per-block column partials {sum do, sum do*y, sum_{y>0} do,
-//                      count y>0} for the BN backward (y = ey, the BN input)
-enum EpiMode { E_STORE = 0, E_BIAS_RELU_STATS = 1, E_CONVT = 2, E_STORE_BN = 3 };
+//                      output: per-block column partials {sum do, sum do*y} for the BN
+//                      backward (y = ey, the BN input).  With escale/eshift set (BN -> ReLU
+//                      order, models/mod.py:46-47) do is first masked by the ReLU that
+//                      follows the BN: do *= [escale*y + eshift > 0], stored masked.
+//   E_STATS          : out[m][n] = acc + per-block column sum / sum of squares (a bias-free
+//                      conv feeding BN directly, models/mod.py:45-46)
+enum EpiMode { E_STORE = 0, E_BIAS_RELU_STATS = 1, E_CONVT = 2, E_STORE_BN = 3, E_STATS = 4 };
 
 // What the A (row GEMM) / B' (wgrad) loader applies to the gathered values:
 //   OP_PLAIN : raw values
 //   OP_AFFINE: per-channel BN affine scale*x + shift (forward consumers of a BN output)
+//   OP_AFFINE_RELU: the same followed by ReLU on channels [0, arelu) (BN -> ReLU order,
+//              models/mod.py:46-47; a concat [skip, up] has ReLU on the skip half only)
 //   OP_DZ    : BN+ReLU backward on the fly, dz = [y > 0] (A*do + B*y + C) per channel,
 //              from do (the operand pointer), y (its BN input) and coef = [A | B | C]
-enum LoadOp { OP_PLAIN = 0, OP_AFFINE = 1, OP_DZ = 2 };
+enum LoadOp { OP_PLAIN = 0, OP_AFFINE = 1, OP_DZ = 2, OP_AFFINE_RELU = 3 };
 
 struct RowGemmArgs {
     int H, W;        // row grid (rows = Nimg*H*W pixels)
@@ -42,11 +48,12 @@ struct RowGemmArgs {
     int lda, aoff, C, amode;
     const float* ascale;  // per-channel affine applied to valid A values (BN fused in the
     const float* ashift;  // consumer's prologue); null = identity
+    int arelu;            // OP_AFFINE: ReLU after the affine on channels [0, arelu)
     const float* bt;      // B^T, row-major [N][K]
     float* out;
     int ldo, ooff;
     const float* bias;
-    float* stats;  // [M/BM][2][N] partial (sum, sumsq); E_STORE_BN: [M/BM][4][N]
+    float* stats;  // [M/BM][2][N] partial (sum, sumsq) or, E_STORE_BN, (sum do, sum do*y)
     int cout;      // E_CONVT
     int emode;
     const float* ay;     // OP_DZ: BN input y of the A operand (ld, off)
@@ -54,6 +61,8 @@ struct RowGemmArgs {
     const float* acoef;  // OP_DZ: [3][C] coefficients
     const float* ey;     // E_STORE_BN: BN input y at the output position (ld, off)
     int ldey, offey;
+    const float* escale;  // E_STORE_BN, BN -> ReLU order: affine of that BN (ReLU mask)
+    const float* eshift;
 };
 
 struct WgradArgs {
@@ -63,6 +72,7 @@ struct WgradArgs {
     int lda, aoff, CA, amode;
     const float* ascale;
     const float* ashift;
+    int arelu;       // ReLU after the affine on A' channels [0, arelu)
     const float* b;  // B' rows: gather(b, bmode, tapB) channels [cb0, cb0+BN)
     int ldb, boff, CB, bmode;
     int Mw, Nw;      // tapsA*CA, tapsB*CB

@@ -99,7 +99,8 @@ struct RowTile {
 
 template <int AMODE, int AOP, int EMODE, class T>
 __global__ __launch_bounds__(T::THREADS, 1) void rowgemm_kernel(RowGemmArgs p) {
-    constexpr bool AFFINE = AOP == OP_AFFINE, ADZ = AOP == OP_DZ;
+    constexpr bool AFFINE = AOP == OP_AFFINE || AOP == OP_AFFINE_RELU, ADZ = AOP == OP_DZ;
+    constexpr bool ARELU = AOP == OP_AFFINE_RELU;
     constexpr int BM = T::BM, BN = T::BN, WM = T::WM, WN = T::WN, BK = T::BK;
     constexpr bool DBUF = T::DBUF;
     constexpr int NTH = T::THREADS;
@@ -136,6 +137,7 @@ __global__ __launch_bounds__(T::THREADS, 1) void rowgemm_kernel(RowGemmArgs p) {
     f32x4 ra[AP], rb[BP], rsc, rsh, rcc;
     f32x4 ry[ADZ ? AP : 1];
     unsigned vmask = 0;
+    bool rrelu = false;
 
     auto issue = [&](int kc) {
         const int k0 = kc * BK;
@@ -144,6 +146,7 @@ __global__ __launch_bounds__(T::THREADS, 1) void rowgemm_kernel(RowGemmArgs p) {
         if constexpr (AFFINE) {
             rsc = *(const f32x4*)(p.ascale + c);
             rsh = *(const f32x4*)(p.ashift + c);
+            if constexpr (ARELU) rrelu = c < p.arelu;
         }
         if constexpr (ADZ) {
             rsc = *(const f32x4*)(p.acoef + c);
@@ -169,7 +172,12 @@ __global__ __launch_bounds__(T::THREADS, 1) void rowgemm_kernel(RowGemmArgs p) {
 #pragma unroll
         for (int i = 0; i < AP; ++i) {
             f32x4 v = ra[i];
-            if constexpr (AFFINE) v = v * rsc + rsh;
+            if constexpr (AFFINE) {
+                v = v * rsc + rsh;
+                if (ARELU && rrelu)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
+            }
             if constexpr (ADZ) {
                 const f32x4 d = rsc * v + rsh * ry[i] + rcc;
 #pragma unroll
@@ -232,12 +240,13 @@ __global__ __launch_bounds__(T::THREADS, 1) void rowgemm_kernel(RowGemmArgs p) {
     }
 
     // ---------------- epilogue ----------------
-    if constexpr (EMODE == E_BIAS_RELU_STATS) {
+    if constexpr (EMODE == E_BIAS_RELU_STATS || EMODE == E_STATS) {
+        constexpr bool BR = EMODE == E_BIAS_RELU_STATS;
         float s1[NT], s2[NT];
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) {
             const int n = n0 + wn * WN + nt * 32 + li;
-            const float b = p.bias[n];
+            const float b = BR ? p.bias[n] : 0.f;
             s1[nt] = 0.f;
             s2[nt] = 0.f;
 #pragma unroll
@@ -246,7 +255,7 @@ __global__ __launch_bounds__(T::THREADS, 1) void rowgemm_kernel(RowGemmArgs p) {
                 for (int r = 0; r < 16; ++r) {
                     const int m = m0 + wm * WM + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
                     if (m < p.M) {
-                        const float v = fmaxf(acc[mt][nt][r] + b, 0.f);
+                        const float v = BR ? fmaxf(acc[mt][nt][r] + b, 0.f) : acc[mt][nt][r];
                         p.out[(size_t)m * p.ldo + p.ooff + n] = v;
                         s1[nt] += v;
                         s2[nt] += v * v;
@@ -279,48 +288,46 @@ __global__ __launch_bounds__(T::THREADS, 1) void rowgemm_kernel(RowGemmArgs p) {
     } else if constexpr (EMODE == E_STORE_BN) {
         // BN-backward partials are differences of nearly equal sums downstream (sum do can be
         // 1e-3 of sum |do|): accumulate in f64, round once per block.
-        double q[NT][4];
+        const bool emask = p.escale != nullptr;
+        double q[NT][2];
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) {
             const int n = n0 + wn * WN + nt * 32 + li;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) q[nt][j] = 0.0;
+            const float es = emask ? p.escale[n] : 0.f, eb = emask ? p.eshift[n] : 0.f;
+            q[nt][0] = q[nt][1] = 0.0;
 #pragma unroll
             for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     const int m = m0 + wm * WM + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
                     if (m < p.M) {
-                        const float v = acc[mt][nt][r];
-                        p.out[(size_t)m * p.ldo + p.ooff + n] = v;
+                        float v = acc[mt][nt][r];
                         const float y = p.ey[(size_t)m * p.ldey + p.offey + n];
+                        if (emask && !(es * y + eb > 0.f)) v = 0.f;
+                        p.out[(size_t)m * p.ldo + p.ooff + n] = v;
                         q[nt][0] += v;
                         q[nt][1] += (double)v * y;
-                        if (y > 0.f) {
-                            q[nt][2] += v;
-                            q[nt][3] += 1.0;
-                        }
                     }
                 }
 #pragma unroll
-            for (int j = 0; j < 4; ++j) q[nt][j] += __shfl_xor(q[nt][j], 32);
+            for (int j = 0; j < 2; ++j) q[nt][j] += __shfl_xor(q[nt][j], 32);
         }
         __syncthreads();
-        double* red = (double*)smem;  // [WAVES_M][4][BN]
+        double* red = (double*)smem;  // [WAVES_M][2][BN]
         if (lh == 0) {
 #pragma unroll
             for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
-                for (int j = 0; j < 4; ++j) red[(wm * 4 + j) * BN + wn * WN + nt * 32 + li] = q[nt][j];
+                for (int j = 0; j < 2; ++j) red[(wm * 2 + j) * BN + wn * WN + nt * 32 + li] = q[nt][j];
         }
         __syncthreads();
         if (tid < BN) {
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
+            for (int j = 0; j < 2; ++j) {
                 double a = 0.0;
 #pragma unroll
-                for (int w = 0; w < WAVES_M; ++w) a += red[(w * 4 + j) * BN + tid];
-                p.stats[((size_t)tile_m * 4 + j) * p.N + n0 + tid] = (float)a;
+                for (int w = 0; w < WAVES_M; ++w) a += red[(w * 2 + j) * BN + tid];
+                p.stats[((size_t)tile_m * 2 + j) * p.N + n0 + tid] = (float)a;
             }
         }
     } else if constexpr (EMODE == E_CONVT) {
@@ -366,8 +373,10 @@ struct WgTile {
     static constexpr int THREADS = 64 * (BM / WM) * (BN / WN);
 };
 
-template <int AMODE, bool AFFINE, int BMODE, bool BDZ, class T>
+template <int AMODE, int AOP, int BMODE, bool BDZ, class T>
 __global__ __launch_bounds__(T::THREADS, 1) void wgrad_kernel(WgradArgs p) {
+    constexpr bool AFFINE = AOP == OP_AFFINE || AOP == OP_AFFINE_RELU;
+    constexpr bool ARELU = AOP == OP_AFFINE_RELU;
     constexpr int BM = T::BM, BN = T::BN, BKP = T::BKP, WM = T::WM, WN = T::WN;
     constexpr int NTH = T::THREADS;
     constexpr int WAVES_N = BN / WN;
@@ -396,9 +405,11 @@ __global__ __launch_bounds__(T::THREADS, 1) void wgrad_kernel(WgradArgs p) {
     const int ac4 = tid % AF, arow = tid / AF;
     const int bc4 = tid % BF, brow = tid / BF;
     f32x4 sc = {1.f, 1.f, 1.f, 1.f}, sh = {0.f, 0.f, 0.f, 0.f};
+    bool arl = false;
     if constexpr (AFFINE) {
         sc = *(const f32x4*)(p.ascale + ca0 + ac4 * 4);
         sh = *(const f32x4*)(p.ashift + ca0 + ac4 * 4);
+        if constexpr (ARELU) arl = ca0 + ac4 * 4 < p.arelu;
     }
 
     f32x4 ca = {0, 0, 0, 0}, cb = ca, cc = ca;  // OP_DZ coefficients of this thread's columns
@@ -449,7 +460,12 @@ __global__ __launch_bounds__(T::THREADS, 1) void wgrad_kernel(WgradArgs p) {
 #pragma unroll
         for (int i = 0; i < AP; ++i) {
             f32x4 v = ra[i];
-            if constexpr (AFFINE) v = v * sc + sh;
+            if constexpr (AFFINE) {
+                v = v * sc + sh;
+                if (ARELU && arl)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
+            }
             if (!((amask >> i) & 1u)) v = f32x4{0.f, 0.f, 0.f, 0.f};
             *(f32x4*)&As[(arow + i * ARPP) * LDA + ac4 * 4] = v;
         }
@@ -596,6 +612,12 @@ int launch_rowgemm(const RowGemmArgs& a, int tile, hipStream_t s) {
     const bool aff = a.ascale != nullptr, dz = a.acoef != nullptr;
     if (aff && dz) return -1;
     if ((a.emode == E_STORE_BN) != (a.ey != nullptr)) return -1;
+    if ((a.escale != nullptr) != (a.eshift != nullptr) || (a.arelu && !aff)) return -1;
+    if (a.amode == G_CONV3 && a.emode == E_STATS) {  // BN -> ReLU order (models/mod.py)
+        if (a.arelu) return rowgemm_tile<G_CONV3, OP_AFFINE_RELU, E_STATS>(a, tile, s);
+        if (!aff) return rowgemm_tile<G_CONV3, OP_PLAIN, E_STATS>(a, tile, s);
+        return -1;
+    }
     if (a.amode == G_CONV3 && a.emode == E_BIAS_RELU_STATS)
         return aff ? rowgemm_tile<G_CONV3, OP_AFFINE, E_BIAS_RELU_STATS>(a, tile, s)
                    : rowgemm_tile<G_CONV3, OP_PLAIN, E_BIAS_RELU_STATS>(a, tile, s);
@@ -606,7 +628,8 @@ int launch_rowgemm(const RowGemmArgs& a, int tile, hipStream_t s) {
         return dz ? rowgemm_tile<G_CONV3, OP_DZ, E_STORE_BN>(a, tile, s)
                   : rowgemm_tile<G_CONV3, OP_PLAIN, E_STORE_BN>(a, tile, s);
     if (a.amode == G_IDENT && a.emode == E_CONVT && aff)
-        return rowgemm_tile<G_IDENT, OP_AFFINE, E_CONVT>(a, tile, s);
+        return a.arelu ? rowgemm_tile<G_IDENT, OP_AFFINE_RELU, E_CONVT>(a, tile, s)
+                       : rowgemm_tile<G_IDENT, OP_AFFINE, E_CONVT>(a, tile, s);
     if (a.amode == G_UP2 && !aff && !dz && a.emode == E_STORE_BN)
         return rowgemm_tile<G_UP2, OP_PLAIN, E_STORE_BN>(a, tile, s);
     return -1;  // combination not instantiated
@@ -636,14 +659,14 @@ int wgrad_tile_dims(int tile, int* bm, int* bn, int* bkp) {
     return -1;
 }
 
-template <int AMODE, bool AFFINE, int BMODE, bool BDZ>
+template <int AMODE, int AOP, int BMODE, bool BDZ>
 static int wgrad_tile(const WgradArgs& a, int tile, hipStream_t s) {
 #define WG_CASE(id, T)                                                                        \
     if (tile == id) {                                                                         \
         if (a.Mw % T::BM || a.Nw % T::BN || a.CA % T::BM || a.CB % T::BN || a.pps % T::BKP) \
             return -1;                                                                        \
         const dim3 grid((a.Mw / T::BM) * (a.Nw / T::BN) * a.splits);                          \
-        hipLaunchKernelGGL((wgrad_kernel<AMODE, AFFINE, BMODE, BDZ, T>), grid, dim3(T::THREADS), 0, s, a); \
+        hipLaunchKernelGGL((wgrad_kernel<AMODE, AOP, BMODE, BDZ, T>), grid, dim3(T::THREADS), 0, s, a); \
         return (int)hipGetLastError();                                                        \
     }
     WGRAD_TILES(WG_CASE)
@@ -654,13 +677,18 @@ static int wgrad_tile(const WgradArgs& a, int tile, hipStream_t s) {
 int launch_wgrad(const WgradArgs& a, int tile, hipStream_t s) {
     if (a.P < 1) return -1;
     const bool aff = a.ascale != nullptr, dz = a.bcoef != nullptr;
+    if (a.arelu && !aff) return -1;
+    if (a.arelu && dz) return -1;  // OP_DZ loaders are the ReLU -> BN order only
     if (a.amode == G_CONV3 && a.bmode == G_IDENT && dz)
-        return aff ? wgrad_tile<G_CONV3, true, G_IDENT, true>(a, tile, s)
-                   : wgrad_tile<G_CONV3, false, G_IDENT, true>(a, tile, s);
-    if (a.amode == G_CONV3 && a.bmode == G_IDENT && !dz)
-        return aff ? wgrad_tile<G_CONV3, true, G_IDENT, false>(a, tile, s)
-                   : wgrad_tile<G_CONV3, false, G_IDENT, false>(a, tile, s);
+        return aff ? wgrad_tile<G_CONV3, OP_AFFINE, G_IDENT, true>(a, tile, s)
+                   : wgrad_tile<G_CONV3, OP_PLAIN, G_IDENT, true>(a, tile, s);
+    if (a.amode == G_CONV3 && a.bmode == G_IDENT && !dz) {
+        if (a.arelu) return wgrad_tile<G_CONV3, OP_AFFINE_RELU, G_IDENT, false>(a, tile, s);
+        return aff ? wgrad_tile<G_CONV3, OP_AFFINE, G_IDENT, false>(a, tile, s)
+                   : wgrad_tile<G_CONV3, OP_PLAIN, G_IDENT, false>(a, tile, s);
+    }
     if (a.amode == G_IDENT && a.bmode == G_UP2 && aff && !dz)
-        return wgrad_tile<G_IDENT, true, G_UP2, false>(a, tile, s);
+        return a.arelu ? wgrad_tile<G_IDENT, OP_AFFINE_RELU, G_UP2, false>(a, tile, s)
+                       : wgrad_tile<G_IDENT, OP_AFFINE, G_UP2, false>(a, tile, s);
     return -1;
 }

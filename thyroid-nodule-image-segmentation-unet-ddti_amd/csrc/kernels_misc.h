@@ -4,10 +4,12 @@
 
 int k_pack_conv3(const float* w, float* wf, float* wd, int cin, int cout, hipStream_t s);
 int k_pack_convT(const float* w, float* tf, float* td, int cin, int cout, hipStream_t s);
+// conv_first: relu = ReLU after (+bias) (model.py order); b may be null (mod.py, bias-free).
+// wgrad: mask = dz masked by [y > 0] (ReLU before the BN, model.py order); gb may be null.
 int k_conv_first_fwd(const float* x, const float* w, const float* b, float* y, int P, int H, int W,
-                     int C, float* partial, int G, hipStream_t s);
+                     int C, int relu, float* partial, int G, hipStream_t s);
 int k_conv_first_wgrad(const float* x, const float* dout, const float* y, const float* coef, int P,
-                       int H, int W, int C, float* partial, int G, float* gw, float* gb,
+                       int H, int W, int C, int mask, float* partial, int G, float* gw, float* gb,
                        hipStream_t s);
 int k_reduce_rows(const float* in, int R, int ncols, float* out, int G, hipStream_t s);
 int k_bn_finalize_train(const float* part, int G, int C, double count, const float* gamma,
@@ -16,32 +18,25 @@ int k_bn_finalize_train(const float* part, int G, int C, double count, const flo
                         hipStream_t s);
 int k_bn_finalize_eval(int C, const float* gamma, const float* beta, const float* rmean,
                        const float* rvar, float eps, float* scale, float* shift, hipStream_t s);
-int k_maxpool_bn(const float* y, int ld, int off, const float* scale, const float* shift, int N,
-                 int H, int W, int C, float* out, uint8_t* idx, hipStream_t s);
+// relu / mscale+mshift: BN -> ReLU order (mod.py:46-47), see the kernels.
+int k_maxpool_bn(const float* y, int ld, int off, const float* scale, const float* shift, int relu,
+                 int N, int H, int W, int C, float* out, uint8_t* idx, hipStream_t s);
 int k_maxpool_bwd(const float* dp, const uint8_t* idx, const float* dskip, int ldskip, int offskip,
-                  const float* y, int ldy, int offy, int N, int H, int W, int C, float* dout,
-                  float* partial, int G, hipStream_t s);
-int k_bn_bwd_finalize4(const float* part, int G, int C, double count, const float* gamma,
+                  const float* y, int ldy, int offy, const float* mscale, const float* mshift,
+                  int N, int H, int W, int C, float* dout, float* partial, int G, hipStream_t s);
+int k_bn_bwd_finalize2(const float* part, int G, int C, double count, const float* gamma,
                        const float* mean, const float* invstd, float* coef, float* dgamma,
                        float* dbeta, hipStream_t s);
-int k_bn_dz(float* d, const float* y, int ld, int off, int64_t P, int C, const float* coef,
+int k_bn_dz(float* d, const float* y, int ld, int off, int64_t P, int C, const float* coef, int mask,
             hipStream_t s);
 int k_bias_reduce(const float* slab, int S, int taps, int C, float* out, hipStream_t s);
-int k_bn_bwd_reduce(const float* dout, const float* y, int ld, int off, int P, int C,
-                    float* partial, int G, hipStream_t s);
-int k_bn_bwd_finalize(const float* part, int G, int C, double count, const float* gamma,
-                      const float* mean, const float* invstd, float* coef, float* dgamma,
-                      float* dbeta, hipStream_t s);
-int k_bn_bwd_apply(float* dz, const float* y, int ld, int off, int P, int C, const float* coef,
-                   float* partial, int G, hipStream_t s);
-int k_chan_sum(const float* v, int ld, int off, int P, int C, float* partial, int G, hipStream_t s);
 int k_sum_partials(const float* part, int G, int ncols, float* out, hipStream_t s);
 int k_slab_reduce(const float* slab, int S, int Mw, int Nw, int kind, int cin, int cout,
                   float* grad, hipStream_t s);
-int k_head_fwd(const float* y, int C, const float* scale, const float* shift, const float* w,
-               const float* b, int O, int P, int HW, float* logits, hipStream_t s);
-int k_head_bwd(const float* y, int C, const float* scale, const float* shift, const float* w,
-               int O, int P, int HW, const float* dlog, float* dout, float* partial,
+int k_head_fwd(const float* y, int C, const float* scale, const float* shift, int relu,
+               const float* w, const float* b, int O, int P, int HW, float* logits, hipStream_t s);
+int k_head_bwd(const float* y, int C, const float* scale, const float* shift, int relu,
+               const float* w, int O, int P, int HW, const float* dlog, float* dout, float* partial,
                float* bnpart, int G, hipStream_t s);
 int k_loss_fwd(const float* x, const float* t, int N, int64_t per, float* stats, float* losses,
                float alpha, float beta, float gamma, hipStream_t s);

@@ -92,14 +92,16 @@ __device__ void block_combine_d(const double (&acc)[NV][4], int tpr, int C, floa
 }
 
 // -------------------------------------------------------------------------------------
-// Conv2d(1 -> C, 3x3, pad 1) + bias + ReLU + BN partials (encoder1.0, model.py:10,36-37).
-// K = 9 is too small for MFMA; one thread computes 4 channels of one pixel.
+// Conv2d(1 -> C, 3x3, pad 1) + bias + ReLU + BN partials (encoder1.0, model.py:10,36-37),
+// or bias-free without ReLU (encoders.0.0 of mod.py:45).  K = 9 is too small for MFMA;
+// one thread computes 4 channels of one pixel.
 // -------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void conv_first_fwd_kernel(const float* __restrict__ x,
                                                             const float* __restrict__ w,
                                                             const float* __restrict__ bias,
                                                             float* __restrict__ y, int P, int H,
-                                                            int W, int C, float* partial) {
+                                                            int W, int C, int relu,
+                                                            float* partial) {
     __shared__ __attribute__((aligned(16))) float smem[256 * 2 * 4];
     const int tpr = C / 4, rpp = 256 / tpr;
     const int q = threadIdx.x % tpr, g = threadIdx.x / tpr;
@@ -108,7 +110,7 @@ __global__ __launch_bounds__(256) void conv_first_fwd_kernel(const float* __rest
     for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int t = 0; t < 9; ++t) wr[j][t] = w[(4 * q + j) * 9 + t];
-    const f32x4 b = *(const f32x4*)(bias + 4 * q);
+    const f32x4 b = bias ? *(const f32x4*)(bias + 4 * q) : f32x4{0, 0, 0, 0};
     f32x4 acc[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
     const int per = (P + gridDim.x - 1) / gridDim.x;
     const int r0 = blockIdx.x * per;
@@ -128,7 +130,7 @@ __global__ __launch_bounds__(256) void conv_first_fwd_kernel(const float* __rest
             float s = 0.f;
 #pragma unroll
             for (int tap = 0; tap < 9; ++tap) s = fmaf(xv[tap], wr[j][tap], s);
-            o[j] = fmaxf(s + b[j], 0.f);
+            o[j] = relu ? fmaxf(s + b[j], 0.f) : s + b[j];
         }
         *(f32x4*)(y + (int64_t)m * C + 4 * q) = o;
         acc[0] += o;
@@ -144,7 +146,7 @@ __global__ __launch_bounds__(256) void conv_first_wgrad_kernel(const float* __re
                                                               const float* __restrict__ y,
                                                               const float* __restrict__ coef,
                                                               int P, int H, int W, int C,
-                                                              float* partial) {
+                                                              int mask, float* partial) {
     __shared__ __attribute__((aligned(16))) float smem[256 * 10 * 4];
     const int tpr = C / 4, rpp = 256 / tpr;
     const int q = threadIdx.x % tpr, g = threadIdx.x / tpr;
@@ -156,14 +158,14 @@ __global__ __launch_bounds__(256) void conv_first_wgrad_kernel(const float* __re
     const int r1 = min(P, r0 + per);
     for (int m = r0 + g; m < r1; m += rpp) {
         const int xx = m % W, t = m / W, yy = t % H, img = t / H;
-        // dz = [y > 0] (A do + B y + C): BN + ReLU backward fused into the load
+        // dz = [y > 0] (A do + B y + C) (or unmasked, BN -> ReLU order): BN backward fused
         const f32x4 dv = *(const f32x4*)(dout + (int64_t)m * C + 4 * q);
         const f32x4 yv = *(const f32x4*)(y + (int64_t)m * C + 4 * q);
         const f32x4 dd = *(const f32x4*)(coef + 4 * q) * dv + *(const f32x4*)(coef + C + 4 * q) * yv +
                          *(const f32x4*)(coef + 2 * C + 4 * q);
         f32x4 d;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) d[j] = yv[j] > 0.f ? dd[j] : 0.f;
+        for (int j = 0; j < 4; ++j) d[j] = (!mask || yv[j] > 0.f) ? dd[j] : 0.f;
 #pragma unroll
         for (int tap = 0; tap < 9; ++tap) {
             const int sy = yy + tap / 3 - 1, sx = xx + tap % 3 - 1;
@@ -285,10 +287,12 @@ __global__ void bn_finalize_eval_kernel(int C, const float* __restrict__ gamma,
 // commute when gamma < 0).  idx keeps the winning window position with torch's tie rule:
 // scan order (0,0),(0,1),(1,0),(1,1), first strict maximum wins.
 // -------------------------------------------------------------------------------------
+// relu: BN -> ReLU order (mod.py:46-47); the max of ReLU(v) is ReLU(max v) and the winner
+// only differs where every candidate is <= 0, where the ReLU blocks its gradient anyway.
 __global__ void maxpool_bn_kernel(const float* __restrict__ y, int ld, int off,
                                   const float* __restrict__ scale,
-                                  const float* __restrict__ shift, int N, int H, int W, int C,
-                                  float* __restrict__ out, uint8_t* __restrict__ idx) {
+                                  const float* __restrict__ shift, int relu, int N, int H, int W,
+                                  int C, float* __restrict__ out, uint8_t* __restrict__ idx) {
     const int Ho = H / 2, Wo = W / 2, c4n = C / 4;
     const int64_t total = (int64_t)N * Ho * Wo * c4n;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
@@ -316,33 +320,44 @@ __global__ void maxpool_bn_kernel(const float* __restrict__ y, int ld, int off,
                     }
             }
         }
+        if (relu)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) best[j] = fmaxf(best[j], 0.f);
         *(f32x4*)(out + po * C + 4 * c4) = best;
         *(uint32_t*)(idx + po * C + 4 * c4) = bi;
     }
 }
 
 // do[p][c] = (idx routes dpool to p) + dskip[p][c]  (skip grad comes from the decoder's
-// concat slice, model.py:64-70, so the encoder output's two consumers are summed here), plus
-// the BN-backward column partials of do against the BN input y (same NHWC slice as the
-// skip): partial[G][4][C] = {sum do, sum do*y, sum_{y>0} do, count y>0}.
+// concat slice, model.py:64-70 / mod.py:64, so the encoder output's two consumers are
+// summed here), plus the BN-backward column partials of do against the BN input y (same
+// NHWC slice as the skip): partial[G][2][C] = {sum do, sum do*y}.  With mscale/mshift
+// (BN -> ReLU order) do is first masked by the ReLU, [mscale*y + mshift > 0].
 // One thread per channel quad, pooled pixels strided over the block's row groups.
 __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const float* __restrict__ dp,
                                                          const uint8_t* __restrict__ idx,
                                                          const float* __restrict__ dskip, int ldskip,
                                                          int offskip, const float* __restrict__ y,
-                                                         int ldy, int offy, int N, int H, int W,
-                                                         int C, float* __restrict__ dout,
-                                                         float* partial) {
-    __shared__ double smem[256 * 4 * 4];
+                                                         int ldy, int offy,
+                                                         const float* __restrict__ mscale,
+                                                         const float* __restrict__ mshift, int N,
+                                                         int H, int W, int C,
+                                                         float* __restrict__ dout, float* partial) {
+    __shared__ double smem[256 * 2 * 4];
     const int Ho = H / 2, Wo = W / 2;
     const int tpr = C / 4 < 256 ? C / 4 : 256, rpp = 256 / tpr;
     const int64_t PO = (int64_t)N * Ho * Wo;
-    double acc[4][4];
+    double acc[2][4];
     for (int c0 = 0; c0 < C; c0 += 4 * tpr) {
         const int q = threadIdx.x % tpr, g = threadIdx.x / tpr;
         const int c = c0 + 4 * q;
+        f32x4 ms = {0, 0, 0, 0}, mb = ms;
+        if (mscale) {
+            ms = *(const f32x4*)(mscale + c);
+            mb = *(const f32x4*)(mshift + c);
+        }
 #pragma unroll
-        for (int v = 0; v < 4; ++v)
+        for (int v = 0; v < 2; ++v)
 #pragma unroll
             for (int j = 0; j < 4; ++j) acc[v][j] = 0.0;
         const int64_t per = (PO + gridDim.x - 1) / gridDim.x;
@@ -357,88 +372,40 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const float* __restric
             for (int k = 0; k < 4; ++k) {
                 const int64_t pin = ((int64_t)img * H + 2 * yo + (k >> 1)) * W + 2 * xo + (k & 1);
                 f32x4 v = *(const f32x4*)(dskip + pin * ldskip + offskip + c);
-#pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    if (((bi >> (8 * j)) & 0xFF) == (uint32_t)k) v[j] += gp[j];
-                *(f32x4*)(dout + pin * C + c) = v;
                 const f32x4 yv = *(const f32x4*)(y + pin * ldy + offy + c);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    if (((bi >> (8 * j)) & 0xFF) == (uint32_t)k) v[j] += gp[j];
+                    if (mscale && !(ms[j] * yv[j] + mb[j] > 0.f)) v[j] = 0.f;
+                }
+                *(f32x4*)(dout + pin * C + c) = v;
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     acc[0][j] += v[j];
                     acc[1][j] += (double)v[j] * yv[j];
-                    if (yv[j] > 0.f) {
-                        acc[2][j] += v[j];
-                        acc[3][j] += 1.0;
-                    }
                 }
             }
         }
-        block_combine_d<4>(acc, tpr, C, partial + (int64_t)blockIdx.x * 4 * C + c0, smem);
+        block_combine_d<2>(acc, tpr, C, partial + (int64_t)blockIdx.x * 2 * C + c0, smem);
         __syncthreads();
     }
 }
 
 // -------------------------------------------------------------------------------------
-// BatchNorm backward (train mode) through the preceding ReLU (model.py:37-38,40-41):
-//   sums:  S1 = sum do, S2 = sum do*y                      (bn_bwd_reduce)
-//   coefs: dz = [y>0] (A do + B y + Cc)                     (bn_bwd_finalize)
-//          dgamma = invstd (S2 - mean S1), dbeta = S1
-//   apply: dz in place of do, plus per-channel sum dz for the conv bias (bn_bwd_apply)
+// BatchNorm backward (train mode).  The producer of the BN-output gradient leaves column
+// partials [G][2][C] = {S1 = sum do, S2 = sum do*y} (y = BN input; with BN -> ReLU order
+// do is already masked by the ReLU).  From them: dgamma = invstd (S2 - mean S1),
+// dbeta = S1 and the coefficients of dz = A do + B y + Cc (model.py order additionally
+// masks dz by [y > 0], the ReLU in front of the BN: model.py:37-38,40-41).
 // -------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restrict__ dout,
-                                                           const float* __restrict__ y, int ld,
-                                                           int off, int P, int C,
-                                                           float* partial) {
-    __shared__ __attribute__((aligned(16))) float smem[256 * 2 * 4];
-    const int tpr = C / 4 < 256 ? C / 4 : 256, rpp = 256 / tpr;
-    f32x4 acc[2];
-    for (int c0 = 0; c0 < C; c0 += 4 * tpr) {
-        const int q = threadIdx.x % tpr, g = threadIdx.x / tpr;
-        acc[0] = acc[1] = f32x4{0, 0, 0, 0};
-        const int per = (P + gridDim.x - 1) / gridDim.x;
-        const int r0 = blockIdx.x * per, r1 = min(P, r0 + per);
-        for (int m = r0 + g; m < r1; m += rpp) {
-            const f32x4 d = *(const f32x4*)(dout + (int64_t)m * C + c0 + 4 * q);
-            const f32x4 v = *(const f32x4*)(y + (int64_t)m * ld + off + c0 + 4 * q);
-            acc[0] += d;
-            acc[1] += d * v;
-        }
-        block_combine<2>(acc, tpr, C, partial + (int64_t)blockIdx.x * 2 * C + c0, smem);
-        __syncthreads();
-    }
-}
-
-__global__ void bn_bwd_finalize_kernel(const float* __restrict__ part, int G, int C, double count,
-                                       const float* __restrict__ gamma,
-                                       const float* __restrict__ mean,
-                                       const float* __restrict__ invstd, float* __restrict__ coef,
-                                       float* __restrict__ dgamma, float* __restrict__ dbeta) {
-    const int c = blockIdx.x * 64 + threadIdx.x;
-    double ss[2];
-    colsum16<2>(part, G, 2 * C, C, c, c < C, ss);
-    if (threadIdx.y != 0 || c >= C) return;
-    const double s1 = ss[0], s2 = ss[1];
-    const double is = invstd[c], mu = mean[c];
-    const double sdxh = is * (s2 - mu * s1);  // sum do * xhat
-    const double k = (double)gamma[c] * is;
-    coef[c] = (float)k;                                         // A
-    coef[C + c] = (float)(-k * is * sdxh / count);              // B
-    coef[2 * C + c] = (float)(-k * s1 / count + k * is * mu * sdxh / count);  // Cc
-    dgamma[c] = (float)sdxh;
-    dbeta[c] = (float)s1;
-}
-
-// From the 4-quantity partials of the producer of `do` ({S1 = sum do, S2 = sum do*y,
-// S3, S4}; only S1, S2 are needed here): dz = [y>0](A do + B y + Cc) coefficients for the
-// fused consumers, and dgamma = invstd (S2 - mean S1), dbeta = S1.
-__global__ void bn_bwd_finalize4_kernel(const float* __restrict__ part, int G, int C, double count,
+__global__ void bn_bwd_finalize2_kernel(const float* __restrict__ part, int G, int C, double count,
                                         const float* __restrict__ gamma,
                                         const float* __restrict__ mean,
                                         const float* __restrict__ invstd, float* __restrict__ coef,
                                         float* __restrict__ dgamma, float* __restrict__ dbeta) {
     const int c = blockIdx.x * 64 + threadIdx.x;
     double ss[2];
-    colsum16<2>(part, G, 4 * C, C, c, c < C, ss);
+    colsum16<2>(part, G, 2 * C, C, c, c < C, ss);
     if (threadIdx.y != 0 || c >= C) return;
     const double s1 = ss[0], s2 = ss[1];
     const double is = invstd[c], mu = mean[c];
@@ -451,9 +418,9 @@ __global__ void bn_bwd_finalize4_kernel(const float* __restrict__ part, int G, i
     dbeta[c] = (float)s1;
 }
 
-// dz = [y>0](A do + B y + C) in place (BN + ReLU backward as one elementwise pass).
+// dz = A do + B y + C in place, masked by [y > 0] when `mask` (ReLU before the BN).
 __global__ void bn_dz_kernel(float* __restrict__ d, const float* __restrict__ y, int ld, int off,
-                             int64_t P, int C, const float* __restrict__ coef) {
+                             int64_t P, int C, const float* __restrict__ coef, int mask) {
     const int c4n = C / 4;
     const int64_t total = P * c4n;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
@@ -466,7 +433,7 @@ __global__ void bn_dz_kernel(float* __restrict__ d, const float* __restrict__ y,
                         *(const f32x4*)(coef + 2 * C + c);
         f32x4 o;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) o[j] = v[j] > 0.f ? r[j] : 0.f;
+        for (int j = 0; j < 4; ++j) o[j] = (!mask || v[j] > 0.f) ? r[j] : 0.f;
         *pd = o;
     }
 }
@@ -483,54 +450,6 @@ __global__ void bias_reduce_kernel(const float* __restrict__ slab, int S, int ta
         __syncthreads();
     }
     if (threadIdx.y == 0 && c < C) out[c] = (float)t;
-}
-
-__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(float* __restrict__ dz,
-                                                          const float* __restrict__ y, int ld,
-                                                          int off, int P, int C,
-                                                          const float* __restrict__ coef,
-                                                          float* partial) {
-    __shared__ __attribute__((aligned(16))) float smem[256 * 1 * 4];
-    const int tpr = C / 4 < 256 ? C / 4 : 256, rpp = 256 / tpr;
-    f32x4 acc[1];
-    for (int c0 = 0; c0 < C; c0 += 4 * tpr) {
-        const int q = threadIdx.x % tpr, g = threadIdx.x / tpr;
-        const int c = c0 + 4 * q;
-        const f32x4 A = *(const f32x4*)(coef + c), B = *(const f32x4*)(coef + C + c),
-                    Cc = *(const f32x4*)(coef + 2 * C + c);
-        acc[0] = f32x4{0, 0, 0, 0};
-        const int per = (P + gridDim.x - 1) / gridDim.x;
-        const int r0 = blockIdx.x * per, r1 = min(P, r0 + per);
-        for (int m = r0 + g; m < r1; m += rpp) {
-            f32x4* pd = (f32x4*)(dz + (int64_t)m * C + c);
-            const f32x4 v = *(const f32x4*)(y + (int64_t)m * ld + off + c);
-            f32x4 d = A * (*pd) + B * v + Cc;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) d[j] = v[j] > 0.f ? d[j] : 0.f;
-            *pd = d;
-            acc[0] += d;
-        }
-        block_combine<1>(acc, tpr, C, partial + (int64_t)blockIdx.x * C + c0, smem);
-        __syncthreads();
-    }
-}
-
-// per-channel sum over pixels of a strided NHWC slice (ConvTranspose2d bias grad)
-__global__ __launch_bounds__(256) void chan_sum_kernel(const float* __restrict__ v, int ld, int off,
-                                                      int P, int C, float* partial) {
-    __shared__ __attribute__((aligned(16))) float smem[256 * 1 * 4];
-    const int tpr = C / 4 < 256 ? C / 4 : 256, rpp = 256 / tpr;
-    f32x4 acc[1];
-    for (int c0 = 0; c0 < C; c0 += 4 * tpr) {
-        const int q = threadIdx.x % tpr, g = threadIdx.x / tpr;
-        acc[0] = f32x4{0, 0, 0, 0};
-        const int per = (P + gridDim.x - 1) / gridDim.x;
-        const int r0 = blockIdx.x * per, r1 = min(P, r0 + per);
-        for (int m = r0 + g; m < r1; m += rpp)
-            acc[0] += *(const f32x4*)(v + (int64_t)m * ld + off + c0 + 4 * q);
-        block_combine<1>(acc, tpr, C, partial + (int64_t)blockIdx.x * C + c0, smem);
-        __syncthreads();
-    }
 }
 
 // out[c] = sum over G partial rows (fixed order), optional scatter stride
@@ -597,7 +516,7 @@ __global__ void conv_first_wgrad_finalize_kernel(const float* __restrict__ part,
     const int tap = i / C, c = i - tap * C;
     if (tap < 9)
         gw[c * 9 + tap] = s;
-    else
+    else if (gb)
         gb[c] = s;
 }
 
@@ -606,7 +525,8 @@ __global__ void conv_first_wgrad_finalize_kernel(const float* __restrict__ part,
 // logits are NCHW (N, O, H, W).
 // -------------------------------------------------------------------------------------
 __global__ void head_fwd_kernel(const float* __restrict__ y, int C, const float* __restrict__ scale,
-                                const float* __restrict__ shift, const float* __restrict__ w,
+                                const float* __restrict__ shift, int relu,
+                                const float* __restrict__ w,
                                 const float* __restrict__ b, int O, int P, int HW,
                                 float* __restrict__ logits) {
     const int lpp = C / 4;  // lanes per pixel (C == 64 -> 16)
@@ -617,6 +537,9 @@ __global__ void head_fwd_kernel(const float* __restrict__ y, int C, const float*
     f32x4 v = {0, 0, 0, 0};
     if (ok) v = *(const f32x4*)(y + pix * C + 4 * q) * *(const f32x4*)(scale + 4 * q) +
                 *(const f32x4*)(shift + 4 * q);
+    if (relu)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
     for (int o = 0; o < O; ++o) {
         const f32x4 wv = *(const f32x4*)(w + o * C + 4 * q);
         float s = v[0] * wv[0] + v[1] * wv[1] + v[2] * wv[2] + v[3] * wv[3];
@@ -628,18 +551,19 @@ __global__ void head_fwd_kernel(const float* __restrict__ y, int C, const float*
     }
 }
 
-// do[p][c] = sum_o dl[p][o] w[o][c];  partial dW[o][c] = sum dl * BN(y)_c, db[o] = sum dl.
-// partial layout [G][O*C + O].
+// do[p][c] = sum_o dl[p][o] w[o][c];  partial dW[o][c] = sum dl * act(y)_c, db[o] = sum dl.
+// partial layout [G][O*C + O]; bnpart [G][2][C] = {sum do, sum do*y} for the BN backward.
+// relu (BN -> ReLU order): act = ReLU(BN(y)) and do is masked by that ReLU.
 __global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__ y, int C,
                                                       const float* __restrict__ scale,
-                                                      const float* __restrict__ shift,
+                                                      const float* __restrict__ shift, int relu,
                                                       const float* __restrict__ w, int O, int P,
                                                       int HW, const float* __restrict__ dlog,
                                                       float* __restrict__ dout, float* partial,
                                                       float* bnpart) {
     __shared__ float red[256 * 5];
-    __shared__ double smem4[256 * 4 * 4];
-    double bq[4][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
+    __shared__ double smem4[256 * 2 * 4];
+    double bq[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
     const int lpp = C / 4, rpp = 256 / lpp;
     const int q = threadIdx.x % lpp, g = threadIdx.x / lpp;
     const f32x4 sc = *(const f32x4*)(scale + 4 * q), sh = *(const f32x4*)(shift + 4 * q);
@@ -650,7 +574,10 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__
     const int r0 = blockIdx.x * per, r1 = min(P, r0 + per);
     for (int m = r0 + g; m < r1; m += rpp) {
         const f32x4 yr = *(const f32x4*)(y + (int64_t)m * C + 4 * q);
-        const f32x4 v = yr * sc + sh;
+        f32x4 v = yr * sc + sh;
+        if (relu)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
         const int64_t img = m / HW, hw = m % HW;
         f32x4 d = {0, 0, 0, 0};
         for (int o = 0; o < O; ++o) {
@@ -659,18 +586,17 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__
             aw[o] += dl * v;
             ab[o] += dl;
         }
+        if (relu)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) d[j] = v[j] > 0.f ? d[j] : 0.f;
         *(f32x4*)(dout + (int64_t)m * C + 4 * q) = d;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             bq[0][j] += d[j];
             bq[1][j] += (double)d[j] * yr[j];
-            if (yr[j] > 0.f) {
-                bq[2][j] += d[j];
-                bq[3][j] += 1.0;
-            }
         }
     }
-    block_combine_d<4>(bq, lpp, C, bnpart + (int64_t)blockIdx.x * 4 * C, smem4);
+    block_combine_d<2>(bq, lpp, C, bnpart + (int64_t)blockIdx.x * 2 * C, smem4);
     __syncthreads();
     // combine over row groups through LDS, one quantity at a time
     float* out = partial + (int64_t)blockIdx.x * (O * C + O);
@@ -878,16 +804,18 @@ int k_pack_convT(const float* w, float* tf, float* td, int cin, int cout, hipStr
     LAUNCH_CHECK();
 }
 int k_conv_first_fwd(const float* x, const float* w, const float* b, float* y, int P, int H, int W,
-                     int C, float* partial, int G, hipStream_t s) {
+                     int C, int relu, float* partial, int G, hipStream_t s) {
+    if (C % 4 || C > 1024) return -1;
     hipLaunchKernelGGL(conv_first_fwd_kernel, dim3(G), dim3(256), 0, s, x, w, b, y, P, H, W, C,
-                       partial);
+                       relu, partial);
     LAUNCH_CHECK();
 }
 int k_conv_first_wgrad(const float* x, const float* dout, const float* y, const float* coef, int P,
-                       int H, int W, int C, float* partial, int G, float* gw, float* gb,
+                       int H, int W, int C, int mask, float* partial, int G, float* gw, float* gb,
                        hipStream_t s) {
+    if (C % 4 || C > 1024) return -1;
     hipLaunchKernelGGL(conv_first_wgrad_kernel, dim3(G), dim3(256), 0, s, x, dout, y, coef, P, H, W,
-                       C, partial);
+                       C, mask, partial);
     HIP_OK(hipGetLastError());
     hipLaunchKernelGGL(conv_first_wgrad_finalize_kernel, dim3((10 * C + 63) / 64), dim3(64, 16), 0,
                        s, partial, G, C, gw, gb);
@@ -913,60 +841,36 @@ int k_bn_finalize_eval(int C, const float* gamma, const float* beta, const float
                        beta, rmean, rvar, eps, scale, shift);
     LAUNCH_CHECK();
 }
-int k_maxpool_bn(const float* y, int ld, int off, const float* scale, const float* shift, int N,
-                 int H, int W, int C, float* out, uint8_t* idx, hipStream_t s) {
+int k_maxpool_bn(const float* y, int ld, int off, const float* scale, const float* shift, int relu,
+                 int N, int H, int W, int C, float* out, uint8_t* idx, hipStream_t s) {
     const int64_t n = (int64_t)N * (H / 2) * (W / 2) * (C / 4);
     hipLaunchKernelGGL(maxpool_bn_kernel, dim3(grid_for(n)), dim3(256), 0, s, y, ld, off, scale,
-                       shift, N, H, W, C, out, idx);
+                       shift, relu, N, H, W, C, out, idx);
     LAUNCH_CHECK();
 }
 int k_maxpool_bwd(const float* dp, const uint8_t* idx, const float* dskip, int ldskip, int offskip,
-                  const float* y, int ldy, int offy, int N, int H, int W, int C, float* dout,
-                  float* partial, int G, hipStream_t s) {
+                  const float* y, int ldy, int offy, const float* mscale, const float* mshift,
+                  int N, int H, int W, int C, float* dout, float* partial, int G, hipStream_t s) {
     hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(G), dim3(256), 0, s, dp, idx, dskip, ldskip,
-                       offskip, y, ldy, offy, N, H, W, C, dout, partial);
+                       offskip, y, ldy, offy, mscale, mshift, N, H, W, C, dout, partial);
     LAUNCH_CHECK();
 }
-int k_bn_bwd_reduce(const float* dout, const float* y, int ld, int off, int P, int C,
-                    float* partial, int G, hipStream_t s) {
-    hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(G), dim3(256), 0, s, dout, y, ld, off, P, C,
-                       partial);
-    LAUNCH_CHECK();
-}
-int k_bn_bwd_finalize(const float* part, int G, int C, double count, const float* gamma,
-                      const float* mean, const float* invstd, float* coef, float* dgamma,
-                      float* dbeta, hipStream_t s) {
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(64, 16), 0, s, part, G, C,
-                       count, gamma, mean, invstd, coef, dgamma, dbeta);
-    LAUNCH_CHECK();
-}
-int k_bn_bwd_finalize4(const float* part, int G, int C, double count, const float* gamma,
+int k_bn_bwd_finalize2(const float* part, int G, int C, double count, const float* gamma,
                        const float* mean, const float* invstd, float* coef, float* dgamma,
                        float* dbeta, hipStream_t s) {
-    hipLaunchKernelGGL(bn_bwd_finalize4_kernel, dim3((C + 63) / 64), dim3(64, 16), 0, s, part, G, C,
+    hipLaunchKernelGGL(bn_bwd_finalize2_kernel, dim3((C + 63) / 64), dim3(64, 16), 0, s, part, G, C,
                        count, gamma, mean, invstd, coef, dgamma, dbeta);
     LAUNCH_CHECK();
 }
-int k_bn_dz(float* d, const float* y, int ld, int off, int64_t P, int C, const float* coef,
+int k_bn_dz(float* d, const float* y, int ld, int off, int64_t P, int C, const float* coef, int mask,
             hipStream_t s) {
     hipLaunchKernelGGL(bn_dz_kernel, dim3(grid_for(P * (C / 4))), dim3(256), 0, s, d, y, ld, off, P, C,
-                       coef);
+                       coef, mask);
     LAUNCH_CHECK();
 }
 int k_bias_reduce(const float* slab, int S, int taps, int C, float* out, hipStream_t s) {
     hipLaunchKernelGGL(bias_reduce_kernel, dim3((C + 63) / 64), dim3(64, 16), 0, s, slab, S, taps, C,
                        out);
-    LAUNCH_CHECK();
-}
-int k_bn_bwd_apply(float* dz, const float* y, int ld, int off, int P, int C, const float* coef,
-                   float* partial, int G, hipStream_t s) {
-    hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(G), dim3(256), 0, s, dz, y, ld, off, P, C, coef,
-                       partial);
-    LAUNCH_CHECK();
-}
-int k_chan_sum(const float* v, int ld, int off, int P, int C, float* partial, int G,
-               hipStream_t s) {
-    hipLaunchKernelGGL(chan_sum_kernel, dim3(G), dim3(256), 0, s, v, ld, off, P, C, partial);
     LAUNCH_CHECK();
 }
 int k_sum_partials(const float* part, int G, int ncols, float* out, hipStream_t s) {
@@ -981,18 +885,20 @@ int k_slab_reduce(const float* slab, int S, int Mw, int Nw, int kind, int cin, i
                        slab, S, Mw, Nw, kind, cin, cout, grad);
     LAUNCH_CHECK();
 }
-int k_head_fwd(const float* y, int C, const float* scale, const float* shift, const float* w,
-               const float* b, int O, int P, int HW, float* logits, hipStream_t s) {
+int k_head_fwd(const float* y, int C, const float* scale, const float* shift, int relu,
+               const float* w, const float* b, int O, int P, int HW, float* logits, hipStream_t s) {
+    if (C % 4 || C / 4 > 64 || (C / 4 & (C / 4 - 1))) return -1;  // lanes per pixel: pow2 <= 64
     const int64_t threads = (int64_t)P * (C / 4);
     hipLaunchKernelGGL(head_fwd_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, y,
-                       C, scale, shift, w, b, O, P, HW, logits);
+                       C, scale, shift, relu, w, b, O, P, HW, logits);
     LAUNCH_CHECK();
 }
-int k_head_bwd(const float* y, int C, const float* scale, const float* shift, const float* w,
-               int O, int P, int HW, const float* dlog, float* dout, float* partial,
+int k_head_bwd(const float* y, int C, const float* scale, const float* shift, int relu,
+               const float* w, int O, int P, int HW, const float* dlog, float* dout, float* partial,
                float* bnpart, int G, hipStream_t s) {
-    hipLaunchKernelGGL(head_bwd_kernel, dim3(G), dim3(256), 0, s, y, C, scale, shift, w, O, P, HW,
-                       dlog, dout, partial, bnpart);
+    if (C % 4 || C / 4 > 256 || O > 4) return -1;
+    hipLaunchKernelGGL(head_bwd_kernel, dim3(G), dim3(256), 0, s, y, C, scale, shift, relu, w, O, P,
+                       HW, dlog, dout, partial, bnpart);
     LAUNCH_CHECK();
 }
 int k_loss_fwd(const float* x, const float* t, int N, int64_t per, float* stats, float* losses,

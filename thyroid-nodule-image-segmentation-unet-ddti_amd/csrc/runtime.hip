@@ -1,12 +1,25 @@
-// Native runtime behind include/unet_hip.h: the layer graph of models/model.py:UNet, the
-// workspace plan (NHWC activations, zero-copy concat buffers, packed weights, backward
-// scratch) and the forward / backward / loss / optimizer orchestration on one HIP stream.
+// Native runtime behind include/unet_hip.h: the layer graph of the reference UNets
+// (models/model.py:UNet and models/mod.py:UNet), the workspace plan (NHWC activations,
+// zero-copy concat buffers, packed weights, backward scratch) and the forward / backward /
+// loss / optimizer orchestration on one HIP stream.
+//
+// Both reference networks are the same encoder / bottleneck / decoder topology over
+// depth D levels of C_l = base << l channels:
+//   block l < D      encoder at level l          (model.py encoder{l+1}; mod.py encoders.l)
+//   block D          bottleneck at level D       (model.py middle.1;     mod.py bottleneck)
+//   block D+1+j      decoder at level D-1-j      (model.py decoder*/final.0; mod.py decoders.j)
+//   ConvT k          level D-k -> D-k-1, reads block D+k's output, feeds block D+1+k through
+//                    the concat CAT_{D-k-1}      (model.py middle.2/decoder*.1; mod.py upconvs.k)
+// and they differ in the order inside a block (model.py:36-41 Conv(+bias) -> ReLU -> BN;
+// mod.py:45-50 Conv(no bias) -> BN -> ReLU), the concat order (model.py:64 [up, skip];
+// mod.py:64 [skip, up]) and the parameter names / registration order.
 #include <math.h>
 #include <stdlib.h>
 #include <stdarg.h>
 #include <stdio.h>
 #include <string.h>
 
+#include <algorithm>
 #include <string>
 #include <vector>
 
@@ -17,23 +30,21 @@ namespace {
 
 constexpr float BN_EPS = 1e-5f;       // nn.BatchNorm2d default (models/model.py:38,41)
 constexpr float BN_MOMENTUM = 0.1f;   // nn.BatchNorm2d default
-constexpr int NBLOCKS = 9;            // enc1..enc4, middle, dec3, dec2, dec1, final
-constexpr int NCONV = 18;             // 3x3 convs
-constexpr int NCONVT = 4;             // ConvTranspose2d k2 s2
 constexpr int RED_G = 512;            // first-level blocks of the channel reductions
 constexpr int STAT_G = 256;           // second level of the BN-stat reduction
+constexpr int MAX_DEPTH = 6;
 
 struct ParamT {
     std::string name;
     int ndim;
     int64_t shape[4];
     int64_t off, numel;
+    int stage;           // backward stage after which its gradient is final
 };
 
 struct ConvL {
     int cin, cout, level, block, which;
-    int64_t w, b;        // param offsets
-    int bn;              // index of the BN that follows (== conv index)
+    int64_t w, b;        // param offsets (b < 0: bias-free conv)
     int64_t pf, pd;      // packed weight offsets (floats) inside the pack region
 };
 struct BnL {
@@ -59,23 +70,34 @@ struct TimeRec {
 struct unet_ctx {
     int device = 0;
     int in_ch = 1, out_ch = 1;
+    int variant = UNET_VARIANT_MODEL;
+    int base = 64, depth = 4;
+    bool bn_relu = false;    // BN -> ReLU (mod.py) instead of ReLU -> BN (model.py)
+    bool skip_first = false; // concat [skip, up] (mod.py) instead of [up, skip] (model.py)
     std::vector<ParamT> params;
     int64_t n_param_floats = 0;
-    ConvL conv[NCONV];
-    BnL bn[NCONV];
-    ConvTL convt[NCONVT];
+    std::vector<ConvL> conv;
+    std::vector<BnL> bn;
+    std::vector<ConvTL> convt;
     int64_t head_w = 0, head_b = 0;
     int64_t n_bn_floats = 0;
     int64_t pack_floats = 0;
+    int cmax = 0;
     std::string err;
-    // buckets (DP overlap)
+    // buckets (DP overlap): contiguous grad ranges, ready after backward stage bucket_stage
     std::vector<int64_t> bucket_off, bucket_len;
+    std::vector<int> bucket_stage;
     std::vector<hipEvent_t> bucket_ev;
     // timing
     bool timing = false;
     std::vector<TimeRec> trec;
     std::vector<hipEvent_t> ev_pool;
     size_t ev_used = 0;
+
+    int nconv() const { return (int)conv.size(); }
+    int ch(int level) const { return base << level; }
+    int up_off(int l) const { return skip_first ? ch(l) : 0; }    // CAT_l channel offsets
+    int skip_off(int l) const { return skip_first ? 0 : ch(l); }
 };
 
 namespace {
@@ -90,11 +112,16 @@ int fail(unet_ctx* c, int code, const char* fmt, ...) {
     return code;
 }
 
-int level_of_block(int b) { return b <= 4 ? b : 8 - b; }
-
+// Parameter table in the reference's named_parameters() order, layer tables, packing
+// offsets and gradient buckets.
 void build_graph(unet_ctx* c) {
+    const int D = c->depth;
+    const int nb = 2 * D + 1;
+    c->conv.assign(2 * nb, ConvL{});
+    c->bn.assign(2 * nb, BnL{});
+    c->convt.assign(D, ConvTL{});
     int64_t off = 0;
-    auto add = [&](const std::string& name, std::initializer_list<int64_t> shape) {
+    auto add = [&](const std::string& name, std::initializer_list<int64_t> shape, int stage) {
         ParamT p;
         p.name = name;
         p.ndim = (int)shape.size();
@@ -106,62 +133,89 @@ void build_graph(unet_ctx* c) {
         }
         for (; i < 4; ++i) p.shape[i] = 0;
         p.off = off;
+        p.stage = stage;
         off += p.numel;
         c->params.push_back(p);
         return p.off;
     };
-    const char* bname[NBLOCKS] = {"encoder1", "encoder2", "encoder3", "encoder4", "middle.1",
-                                  "decoder3.0", "decoder2.0", "decoder1.0", "final.0"};
-    const int bcin[NBLOCKS] = {c->in_ch, 64, 128, 256, 512, 1024, 512, 256, 128};
-    const int bcout[NBLOCKS] = {64, 128, 256, 512, 1024, 512, 256, 128, 64};
-    const char* tname[NCONVT] = {"middle.2", "decoder3.1", "decoder2.1", "decoder1.1"};
-    int64_t run = 0;
-    auto block = [&](int b) {
-        std::string p = bname[b];
-        for (int which = 0; which < 2; ++which) {
-            const int i = 2 * b + which;
-            ConvL& L = c->conv[i];
-            L.cin = which == 0 ? bcin[b] : bcout[b];
-            L.cout = bcout[b];
-            L.level = level_of_block(b);
-            L.block = b;
-            L.which = which;
-            L.bn = i;
-            L.w = add(p + (which ? ".3.weight" : ".0.weight"), {L.cout, L.cin, 3, 3});
-            L.b = add(p + (which ? ".3.bias" : ".0.bias"), {L.cout});
-            BnL& B = c->bn[i];
-            B.C = L.cout;
-            B.name = p + (which ? ".5" : ".2");
-            B.g = add(B.name + ".weight", {L.cout});
-            B.b = add(B.name + ".bias", {L.cout});
-            B.run = run;
-            run += 2 * L.cout;
+    auto level_of = [&](int b) { return b <= D ? b : 2 * D - b; };
+    auto block_cin = [&](int b) {
+        if (b == 0) return c->in_ch;
+        if (b <= D) return c->ch(b - 1);
+        return 2 * c->ch(level_of(b));
+    };
+    // backward stage after which a block's gradients are final: 0 = head + last decoder,
+    // then ConvT k together with block D+k (k = D-1 .. 0), then the encoders
+    auto stage_of_block = [&](int b) { return 2 * D - b; };
+    // 3x3 conv + BN pair `which` of block b; names per variant
+    auto conv_pair = [&](int b, int which, const std::string& pfx) {
+        const int i = 2 * b + which;
+        ConvL& L = c->conv[i];
+        L.cout = c->ch(level_of(b));
+        L.cin = which == 0 ? block_cin(b) : L.cout;
+        L.level = level_of(b);
+        L.block = b;
+        L.which = which;
+        BnL& B = c->bn[i];
+        B.C = L.cout;
+        const int st = stage_of_block(b);
+        L.w = add(pfx + (which ? ".3.weight" : ".0.weight"), {L.cout, L.cin, 3, 3}, st);
+        if (c->variant == UNET_VARIANT_MODEL) {  // model.py:33-43: 0 conv, 2 BN, 3 conv, 5 BN
+            L.b = add(pfx + (which ? ".3.bias" : ".0.bias"), {L.cout}, st);
+            B.name = pfx + (which ? ".5" : ".2");
+        } else {  // mod.py:43-51: 0 conv (no bias), 1 BN, 3 conv, 4 BN
+            L.b = -1;
+            B.name = pfx + (which ? ".4" : ".1");
         }
+        B.g = add(B.name + ".weight", {L.cout}, st);
+        B.b = add(B.name + ".bias", {L.cout}, st);
     };
-    auto convT = [&](int k, int cin) {
+    auto block = [&](int b, const std::string& pfx) {
+        conv_pair(b, 0, pfx);
+        conv_pair(b, 1, pfx);
+    };
+    auto convT = [&](int k, const std::string& name) {
         ConvTL& T = c->convt[k];
-        T.cin = cin;
-        T.cout = cin / 2;
-        T.in_level = 4 - k;
-        T.w = add(std::string(tname[k]) + ".weight", {T.cin, T.cout, 2, 2});
-        T.b = add(std::string(tname[k]) + ".bias", {T.cout});
+        T.in_level = D - k;
+        T.cin = c->ch(D - k);
+        T.cout = c->ch(D - k - 1);
+        const int st = stage_of_block(D + k);
+        T.w = add(name + ".weight", {T.cin, T.cout, 2, 2}, st);
+        T.b = add(name + ".bias", {T.cout}, st);
     };
-    for (int b = 0; b < 5; ++b) block(b);
-    convT(0, 1024);
-    block(5);
-    convT(1, 512);
-    block(6);
-    convT(2, 256);
-    block(7);
-    convT(3, 128);
-    block(8);
-    c->head_w = add("final.1.weight", {c->out_ch, 64, 1, 1});
-    c->head_b = add("final.1.bias", {c->out_ch});
+    if (c->variant == UNET_VARIANT_MODEL) {
+        // models/model.py:6-31 registration order (D = 4, base 64)
+        const char* bname[9] = {"encoder1", "encoder2", "encoder3", "encoder4", "middle.1",
+                                "decoder3.0", "decoder2.0", "decoder1.0", "final.0"};
+        const char* tname[4] = {"middle.2", "decoder3.1", "decoder2.1", "decoder1.1"};
+        for (int b = 0; b <= D; ++b) block(b, bname[b]);
+        for (int k = 0; k < D; ++k) {
+            convT(k, tname[k]);
+            block(D + 1 + k, bname[D + 1 + k]);
+        }
+        c->head_w = add("final.1.weight", {c->out_ch, c->base, 1, 1}, 0);
+        c->head_b = add("final.1.bias", {c->out_ch}, 0);
+    } else {
+        // models/mod.py:21-41: encoders, (pools), bottleneck, upconvs, decoders, final_conv
+        for (int l = 0; l < D; ++l) block(l, "encoders." + std::to_string(l));
+        block(D, "bottleneck");
+        for (int k = 0; k < D; ++k) convT(k, "upconvs." + std::to_string(k));
+        for (int k = 0; k < D; ++k) block(D + 1 + k, "decoders." + std::to_string(k));
+        c->head_w = add("final_conv.weight", {c->out_ch, c->base, 1, 1}, 0);
+        c->head_b = add("final_conv.bias", {c->out_ch}, 0);
+    }
     c->n_param_floats = off;
+    int64_t run = 0;
+    for (auto& B : c->bn) {  // named_buffers() order == conv order in both variants
+        B.run = run;
+        run += 2 * B.C;
+    }
     c->n_bn_floats = run;
+    c->cmax = 0;
+    for (auto& L : c->conv) c->cmax = std::max(c->cmax, std::max(L.cin, L.cout));
     // packed weights (forward + dgrad images); conv 0 (Cin = in_channels) has its own kernel
     int64_t pk = 0;
-    for (int i = 0; i < NCONV; ++i) {
+    for (int i = 0; i < c->nconv(); ++i) {
         ConvL& L = c->conv[i];
         const int64_t n = (int64_t)L.cin * L.cout * 9;
         if (i == 0 && L.cin < 32) {
@@ -173,8 +227,7 @@ void build_graph(unet_ctx* c) {
         L.pd = pk;
         pk += n;
     }
-    for (int k = 0; k < NCONVT; ++k) {
-        ConvTL& T = c->convt[k];
+    for (auto& T : c->convt) {
         const int64_t n = (int64_t)T.cin * T.cout * 4;
         T.pf = pk;
         pk += n;
@@ -182,25 +235,28 @@ void build_graph(unet_ctx* c) {
         pk += n;
     }
     c->pack_floats = pk;
-    // gradient buckets in the order backward completes them (decoder first)
-    auto range = [&](const std::string& first, const std::string& last) {
-        int64_t a = -1, e = -1;
-        for (auto& p : c->params) {
-            if (p.name == first) a = p.off;
-            if (p.name == last) e = p.off + p.numel;
+    // gradient buckets: walk the arena from its end (what backward finishes first), open a
+    // new bucket whenever a tensor finishes later than everything already in the current one
+    // (so buckets become ready in order 0, 1, ...); tensors that finish earlier join it
+    c->bucket_off.clear();
+    c->bucket_len.clear();
+    c->bucket_stage.clear();
+    int64_t end = c->n_param_floats;
+    int cur = -1;
+    for (int t = (int)c->params.size() - 1; t >= 0; --t) {
+        const ParamT& p = c->params[t];
+        if (cur >= 0 && p.stage > cur) {
+            c->bucket_off.push_back(p.off + p.numel);
+            c->bucket_len.push_back(end - (p.off + p.numel));
+            c->bucket_stage.push_back(cur);
+            end = p.off + p.numel;
+            cur = -1;
         }
-        c->bucket_off.push_back(a);
-        c->bucket_len.push_back(e - a);
-    };
-    range("final.0.0.weight", "final.1.bias");
-    range("decoder1.0.0.weight", "decoder1.1.bias");
-    range("decoder2.0.0.weight", "decoder2.1.bias");
-    range("decoder3.0.0.weight", "decoder3.1.bias");
-    range("middle.1.0.weight", "middle.2.bias");
-    range("encoder4.0.weight", "encoder4.5.bias");
-    range("encoder3.0.weight", "encoder3.5.bias");
-    range("encoder2.0.weight", "encoder2.5.bias");
-    range("encoder1.0.weight", "encoder1.5.bias");
+        cur = std::max(cur, p.stage);
+    }
+    c->bucket_off.push_back(0);
+    c->bucket_len.push_back(end);
+    c->bucket_stage.push_back(cur);
 }
 
 // ------------------------------------------------------------------------------------
@@ -209,24 +265,24 @@ void build_graph(unet_ctx* c) {
 // ------------------------------------------------------------------------------------
 struct Plan {
     int N, H, W;
-    int64_t P[5];  // pixels per level
+    int64_t P[MAX_DEPTH + 1];  // pixels per level
     float* pack;
     float* x_nhwc;
-    float* y[NCONV];
-    int ldy[NCONV], offy[NCONV];
-    float* cat[4];
-    float* cat_scale[4];
-    float* cat_shift[4];
-    float* pool[4];
-    uint8_t* idx[4];
-    float *scale[NCONV], *shift[NCONV], *mean[NCONV], *invstd[NCONV];
+    std::vector<float*> y;
+    std::vector<int> ldy, offy;
+    std::vector<float*> scale, shift, mean, invstd;
+    float* cat[MAX_DEPTH];
+    float* cat_scale[MAX_DEPTH];
+    float* cat_shift[MAX_DEPTH];
+    float* pool[MAX_DEPTH];
+    uint8_t* idx[MAX_DEPTH];
     float* stats;
     float* stats2;
     // backward
     float* g[2];
-    float* dcat[4];
+    float* dcat[MAX_DEPTH];
     float* slab;
-    float* part;   // BN-backward column partials [rows][4][C]
+    float* part;   // BN-backward column partials [rows][2][C]
     float* part2;  // second-level reduction of part
     float* hpart;  // head / conv-first weight-gradient partials
     float* bslab;  // [splits][Nw] bias-gradient column sums from the wgrad kernels
@@ -283,30 +339,39 @@ WgradCfg wgrad_cfg(int CA, int tapsA, int CB, int tapsB, int64_t P) {
 
 void make_plan(unet_ctx* c, int N, int H, int W, bool training, char* base, Plan& p) {
     Bump b{base};
+    const int D = c->depth, NC = c->nconv();
     p.N = N;
     p.H = H;
     p.W = W;
-    for (int l = 0; l < 5; ++l) p.P[l] = (int64_t)N * (H >> l) * (W >> l);
+    for (int l = 0; l <= D; ++l) p.P[l] = (int64_t)N * (H >> l) * (W >> l);
+    p.y.assign(NC, nullptr);
+    p.ldy.assign(NC, 0);
+    p.offy.assign(NC, 0);
+    p.scale.assign(NC, nullptr);
+    p.shift.assign(NC, nullptr);
+    p.mean.assign(NC, nullptr);
+    p.invstd.assign(NC, nullptr);
     p.pack = b.take<float>(c->pack_floats);
     p.x_nhwc = b.take<float>(p.P[0] * c->in_ch);  // NHWC copy of x (conv-0 wgrad input)
-    for (int l = 0; l < 4; ++l) {
-        const int C = 64 << l;
+    for (int l = 0; l < D; ++l) {
+        const int C = c->ch(l);
         p.cat[l] = b.take<float>(p.P[l] * 2 * C);
         p.cat_scale[l] = b.take<float>(2 * C);
         p.cat_shift[l] = b.take<float>(2 * C);
         p.pool[l] = b.take<float>(p.P[l + 1] * C);
         p.idx[l] = b.take<uint8_t>(p.P[l + 1] * C);
     }
-    for (int i = 0; i < NCONV; ++i) {
+    for (int i = 0; i < NC; ++i) {
         const ConvL& L = c->conv[i];
-        if (L.block < 4 && L.which == 1) {
-            const int C = 64 << L.block;
-            p.y[i] = p.cat[L.block] ? p.cat[L.block] : nullptr;
-            p.ldy[i] = 2 * C;
-            p.offy[i] = C;
-            // the encoder output's BN affine is the second half of the concat affine
-            p.scale[i] = p.cat_scale[L.block] ? p.cat_scale[L.block] + C : nullptr;
-            p.shift[i] = p.cat_shift[L.block] ? p.cat_shift[L.block] + C : nullptr;
+        if (L.block < D && L.which == 1) {
+            // the encoder output lives in the skip half of its concat buffer, and its BN
+            // affine is that half of the concat affine
+            const int l = L.block, so = c->skip_off(l);
+            p.y[i] = p.cat[l];
+            p.ldy[i] = 2 * c->ch(l);
+            p.offy[i] = so;
+            p.scale[i] = p.cat_scale[l] ? p.cat_scale[l] + so : nullptr;
+            p.shift[i] = p.cat_shift[l] ? p.cat_shift[l] + so : nullptr;
         } else {
             p.y[i] = b.take<float>(p.P[L.level] * L.cout);
             p.ldy[i] = L.cout;
@@ -317,55 +382,49 @@ void make_plan(unet_ctx* c, int N, int H, int W, bool training, char* base, Plan
         p.mean[i] = b.take<float>(L.cout);
         p.invstd[i] = b.take<float>(L.cout);
     }
-    // BN-stat partials: rows = M / 128 of the row GEMM, or RED_G for the first conv
+    // BN-stat partials: rows = M / 64 (smallest row tile) of the row GEMM, or RED_G for the
+    // first conv
     int64_t srows = 0;
-    for (int i = 0; i < NCONV; ++i) {
+    for (int i = 0; i < NC; ++i) {
         const int64_t r = std::max<int64_t>((p.P[c->conv[i].level] + 63) / 64, RED_G);
         srows = std::max(srows, r * 2 * c->conv[i].cout);
     }
     p.stats = b.take<float>(srows);
-    p.stats2 = b.take<float>((int64_t)STAT_G * 2 * 1024);
+    p.stats2 = b.take<float>((int64_t)STAT_G * 2 * c->cmax);
     if (training) {
-        int64_t gmax = p.P[0] * 64;
-        for (int i = 0; i < NCONV; ++i)
+        int64_t gmax = p.P[0] * c->base;
+        for (int i = 0; i < NC; ++i) {
             gmax = std::max(gmax, p.P[c->conv[i].level] * c->conv[i].cout);
+            gmax = std::max(gmax, p.P[c->conv[i].level] * c->conv[i].cin);
+        }
         p.g[0] = b.take<float>(gmax);
         p.g[1] = b.take<float>(gmax);
-        for (int l = 0; l < 4; ++l) p.dcat[l] = b.take<float>(p.P[l] * 2 * (64 << l));
-        int64_t smax = 0;
-        for (int i = 1; i < NCONV; ++i) {
+        for (int l = 0; l < D; ++l) p.dcat[l] = b.take<float>(p.P[l] * 2 * c->ch(l));
+        int64_t smax = 0, bmax = 0;
+        for (int i = 1; i < NC; ++i) {
             const ConvL& L = c->conv[i];
             WgradCfg w = wgrad_cfg(L.cin, 9, L.cout, 1, p.P[L.level]);
             smax = std::max(smax, (int64_t)w.splits * 9 * L.cin * L.cout);
-        }
-        for (int k = 0; k < NCONVT; ++k) {
-            const ConvTL& T = c->convt[k];
-            WgradCfg w = wgrad_cfg(T.cin, 1, T.cout, 4, p.P[T.in_level]);
-            smax = std::max(smax, (int64_t)w.splits * T.cin * 4 * T.cout);
-        }
-        p.slab = b.take<float>(smax);
-        int64_t pmax = (int64_t)RED_G * 4 * 1024;
-        for (int i = 0; i < NCONV; ++i)  // dgrad epilogues: ceil(P/64) rows of 4*C (BM >= 64)
-            pmax = std::max(pmax, (p.P[c->conv[i].level] / 64 + 1) * 4 * c->conv[i].cout);
-        p.part = b.take<float>(pmax);
-        p.part2 = b.take<float>((int64_t)STAT_G * 4 * 1024);
-        p.hpart = b.take<float>((int64_t)RED_G * (10 * 1024 + 64));
-        int64_t bmax = 0;
-        for (int i = 1; i < NCONV; ++i) {
-            const ConvL& L = c->conv[i];
-            WgradCfg w = wgrad_cfg(L.cin, 9, L.cout, 1, p.P[L.level]);
             bmax = std::max(bmax, (int64_t)w.splits * L.cout);
         }
-        for (int k = 0; k < NCONVT; ++k) {
-            const ConvTL& T = c->convt[k];
+        for (const ConvTL& T : c->convt) {
             WgradCfg w = wgrad_cfg(T.cin, 1, T.cout, 4, p.P[T.in_level]);
+            smax = std::max(smax, (int64_t)w.splits * T.cin * 4 * T.cout);
             bmax = std::max(bmax, (int64_t)w.splits * 4 * T.cout);
         }
-        p.bslab = b.take<float>(bmax);
-        p.coef = b.take<float>(3 * 1024);
+        p.slab = b.take<float>(smax);
+        int64_t pmax = (int64_t)RED_G * 2 * c->cmax;
+        for (int i = 0; i < NC; ++i)  // dgrad epilogues: ceil(P/64) rows of 2*C (BM >= 64)
+            pmax = std::max(pmax, (p.P[c->conv[i].level] / 64 + 1) * 2 * c->conv[i].cout);
+        p.part = b.take<float>(pmax);
+        p.part2 = b.take<float>((int64_t)STAT_G * 2 * c->cmax);
+        p.hpart = b.take<float>((int64_t)RED_G *
+                                std::max<int64_t>(10 * c->base, (int64_t)c->out_ch * (c->base + 1)));
+        p.bslab = b.take<float>(std::max<int64_t>(bmax, 1));
+        p.coef = b.take<float>(3 * (int64_t)c->cmax);
     } else {
         p.g[0] = p.g[1] = p.slab = p.part = p.part2 = p.hpart = p.bslab = p.coef = nullptr;
-        for (int l = 0; l < 4; ++l) p.dcat[l] = nullptr;
+        for (int l = 0; l < D; ++l) p.dcat[l] = nullptr;
     }
     p.bytes = b.off + 256;
 }
@@ -435,16 +494,6 @@ std::string wlabel(const char* fam, const WgradCfg& w, int layer) {
     return b;
 }
 
-// timing label "family/kernel-instance" (the instance is what rocprofv3 reports)
-std::string glabel(const char* fam, const char* kern, int bm, int bn, int layer = -1) {
-    char b[112];
-    if (layer >= 0)
-        snprintf(b, sizeof b, "%s/%s_%dx%d|%d", fam, kern, bm, bn, layer);
-    else
-        snprintf(b, sizeof b, "%s/%s_%dx%d", fam, kern, bm, bn);
-    return b;
-}
-
 #define RUN(label, flop, expr)                            \
     do {                                                  \
         int rc_ = L.run(label, flop, [&]() { return (expr); }); \
@@ -478,48 +527,54 @@ int stats_finalize(unet_ctx* c, Launcher& L, Plan& p, int i, int R, int64_t coun
     return 0;
 }
 
-// Input operand of conv i: pointer, ld, offset, affine.
+// Input operand of conv i: pointer, ld, offset, affine and the ReLU span (channels
+// [0, relu) get ReLU after the affine: BN -> ReLU order).
 struct Operand {
     const float* ptr;
     int ld, off;
     const float* scale;
     const float* shift;
+    int relu;
 };
 
 Operand conv_input(unet_ctx* c, Plan& p, int i) {
     const ConvL& L = c->conv[i];
-    if (L.which == 1) return {p.y[i - 1], p.ldy[i - 1], p.offy[i - 1], p.scale[i - 1], p.shift[i - 1]};
-    if (L.block >= 1 && L.block <= 4)
-        return {p.pool[L.block - 1], c->conv[i].cin, 0, nullptr, nullptr};
-    if (L.block >= 5) {
+    const int D = c->depth;
+    if (L.which == 1)
+        return {p.y[i - 1], p.ldy[i - 1], p.offy[i - 1], p.scale[i - 1], p.shift[i - 1],
+                c->bn_relu ? L.cin : 0};
+    if (L.block >= 1 && L.block <= D)  // after a max-pool (already normalised + activated)
+        return {p.pool[L.block - 1], L.cin, 0, nullptr, nullptr, 0};
+    if (L.block > D) {  // concat: the skip half carries the encoder's BN (+ReLU) affine
         const int l = L.level;
-        return {p.cat[l], 2 * (64 << l), 0, p.cat_scale[l], p.cat_shift[l]};
+        return {p.cat[l], 2 * c->ch(l), 0, p.cat_scale[l], p.cat_shift[l],
+                c->bn_relu ? c->ch(l) : 0};
     }
-    return {nullptr, 0, 0, nullptr, nullptr};  // conv 0: x
+    return {nullptr, 0, 0, nullptr, nullptr, 0};  // conv 0: x
 }
+
+const float* bias_ptr(const float* prm, int64_t off) { return off >= 0 ? prm + off : nullptr; }
 
 int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, const float* x,
                  float* logits, Plan& p, bool training, hipStream_t s) {
     Launcher L{c, s};
-    const int N = p.N, H = p.H, W = p.W;
+    const int H = p.H, W = p.W, D = c->depth, NC = c->nconv();
     // 1. weight images for the row GEMMs (re-packed every call: params may have changed
     //    through the optimizer or load_state_dict; ~0.1 ms of HBM traffic per step)
-    for (int i = 0; i < NCONV; ++i) {
+    for (int i = 0; i < NC; ++i) {
         const ConvL& C = c->conv[i];
         if (C.pf < 0) continue;
         RUN("pack", 0, k_pack_conv3(prm + C.w, p.pack + C.pf, training ? p.pack + C.pd : nullptr,
                                     C.cin, C.cout, s));
     }
-    for (int k = 0; k < NCONVT; ++k) {
-        const ConvTL& T = c->convt[k];
+    for (const ConvTL& T : c->convt)
         RUN("pack", 0, k_pack_convT(prm + T.w, p.pack + T.pf, training ? p.pack + T.pd : nullptr,
                                     T.cin, T.cout, s));
-    }
     // 2. concat affine: identity on the up-sampled half (no BN between ConvT and concat)
-    for (int l = 0; l < 4; ++l) {
-        const int C = 64 << l;
-        RUN("fill", 0, k_fill(p.cat_scale[l], C, 1.f, s));
-        RUN("fill", 0, k_fill(p.cat_shift[l], C, 0.f, s));
+    for (int l = 0; l < D; ++l) {
+        const int C = c->ch(l), uo = c->up_off(l);
+        RUN("fill", 0, k_fill(p.cat_scale[l] + uo, C, 1.f, s));
+        RUN("fill", 0, k_fill(p.cat_shift[l] + uo, C, 0.f, s));
     }
     // in_channels == 1: NCHW == NHWC; keep a private copy for the conv-0 wgrad
     RUN("copy_x", 0, (int)hipMemcpyAsync(p.x_nhwc, x, sizeof(float) * p.P[0] * c->in_ch,
@@ -534,8 +589,8 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
         if (i == 0 && C.pf < 0) {
             R = RED_G;
             RUN("conv_first_fwd", 2.0 * M * 9 * C.cout,
-                k_conv_first_fwd(xin, prm + C.w, prm + C.b, p.y[0], (int)M, Hl, Wl, C.cout,
-                                 p.stats, R, s));
+                k_conv_first_fwd(xin, prm + C.w, bias_ptr(prm, C.b), p.y[0], (int)M, Hl, Wl, C.cout,
+                                 c->bn_relu ? 0 : 1, p.stats, R, s));
         } else {
             Operand a = conv_input(c, p, i);
             RowGemmArgs g{};
@@ -551,13 +606,14 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
             g.amode = G_CONV3;
             g.ascale = a.scale;
             g.ashift = a.shift;
+            g.arelu = a.relu;
             g.bt = p.pack + C.pf;
             g.out = p.y[i];
             g.ldo = p.ldy[i];
             g.ooff = p.offy[i];
-            g.bias = prm + C.b;
+            g.bias = bias_ptr(prm, C.b);
             g.stats = p.stats;
-            g.emode = E_BIAS_RELU_STATS;
+            g.emode = c->bn_relu ? E_STATS : E_BIAS_RELU_STATS;
             const int tile = pick_tile(C.cout);
             int bm, bn, bk;
             rowgemm_tile_dims(tile, &bm, &bn, &bk);
@@ -568,7 +624,7 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
     };
     auto convT = [&](int k) -> int {
         const ConvTL& T = c->convt[k];
-        const int src = 2 * (4 + k) + 1;  // second conv of middle / dec3 / dec2 / dec1
+        const int src = 2 * (D + k) + 1;  // second conv of the bottleneck / decoder block
         const int lo = T.in_level - 1;
         RowGemmArgs g{};
         g.H = H >> T.in_level;
@@ -583,10 +639,11 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
         g.amode = G_IDENT;
         g.ascale = p.scale[src];
         g.ashift = p.shift[src];
+        g.arelu = c->bn_relu ? T.cin : 0;
         g.bt = p.pack + T.pf;
         g.out = p.cat[lo];
-        g.ldo = 2 * (64 << lo);
-        g.ooff = 0;
+        g.ldo = 2 * c->ch(lo);
+        g.ooff = c->up_off(lo);
         g.bias = prm + T.b;
         g.cout = T.cout;
         g.emode = E_CONVT;
@@ -596,61 +653,65 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
     };
 
     int rc;
-    for (int b = 0; b < 5; ++b) {
+    for (int b = 0; b <= D; ++b) {
         if ((rc = conv(2 * b))) return rc;
         if ((rc = conv(2 * b + 1))) return rc;
-        if (b < 4) {
-            const int i = 2 * b + 1, C = 64 << b;
+        if (b < D) {
+            const int i = 2 * b + 1, C = c->ch(b);
             RUN("maxpool_fwd", 0,
-                k_maxpool_bn(p.y[i], p.ldy[i], p.offy[i], p.scale[i], p.shift[i], N, H >> b, W >> b,
-                             C, p.pool[b], p.idx[b], s));
+                k_maxpool_bn(p.y[i], p.ldy[i], p.offy[i], p.scale[i], p.shift[i], c->bn_relu ? 1 : 0,
+                             p.N, H >> b, W >> b, C, p.pool[b], p.idx[b], s));
         }
     }
-    if ((rc = convT(0))) return rc;
-    for (int b = 5; b < 9; ++b) {
+    for (int k = 0; k < D; ++k) {
+        if ((rc = convT(k))) return rc;
+        const int b = D + 1 + k;
         if ((rc = conv(2 * b))) return rc;
         if ((rc = conv(2 * b + 1))) return rc;
-        if (b < 8 && (rc = convT(b - 4))) return rc;
     }
-    RUN("head_fwd", 2.0 * p.P[0] * 64 * c->out_ch,
-        k_head_fwd(p.y[17], 64, p.scale[17], p.shift[17], prm + c->head_w, prm + c->head_b,
-                   c->out_ch, (int)p.P[0], H * W, logits, s));
+    const int last = NC - 1;
+    RUN("head_fwd", 2.0 * p.P[0] * c->base * c->out_ch,
+        k_head_fwd(p.y[last], c->base, p.scale[last], p.shift[last], c->bn_relu ? 1 : 0,
+                   prm + c->head_w, prm + c->head_b, c->out_ch, (int)p.P[0], H * W, logits, s));
     return 0;
 }
 
 int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* grads, Plan& p,
                   hipStream_t s) {
     Launcher L{c, s};
-    const int H = p.H, W = p.W;
+    const int H = p.H, W = p.W, D = c->depth, NC = c->nconv();
     int rc;
 
-    // BatchNorm (+ReLU) backward is fused: the producer of `do` (head_bwd, a dgrad epilogue,
-    // maxpool_bwd) leaves {sum do, sum do*y, ...} column partials in p.part; this finalize
-    // turns them into dgamma, dbeta and the per-channel coefficients of
-    // dz = [y>0](A do + B y + C), which the conv's wgrad / dgrad loaders apply on the fly.
+    // BatchNorm backward is fused: the producer of `do` (head_bwd, a dgrad epilogue,
+    // maxpool_bwd) leaves {sum do, sum do*y} column partials in p.part (do already masked by
+    // the following ReLU in BN -> ReLU order); this finalize turns them into dgamma, dbeta
+    // and the per-channel coefficients of dz = A do + B y + C (masked by [y > 0] in
+    // ReLU -> BN order).
     auto bn_finalize = [&](int i, int R) -> int {
         const ConvL& C = c->conv[i];
         const BnL& B = c->bn[i];
         const float* part = p.part;
         int G = R;
         if (R > STAT_G) {
-            RUN("bn_bwd_reduce", 0, k_reduce_rows(p.part, R, 4 * C.cout, p.part2, STAT_G, s));
+            RUN("bn_bwd_reduce", 0, k_reduce_rows(p.part, R, 2 * C.cout, p.part2, STAT_G, s));
             part = p.part2;
             G = STAT_G;
         }
         RUN("bn_bwd_finalize", 0,
-            k_bn_bwd_finalize4(part, G, C.cout, (double)p.P[C.level], prm + B.g, p.mean[i],
+            k_bn_bwd_finalize2(part, G, C.cout, (double)p.P[C.level], prm + B.g, p.mean[i],
                                p.invstd[i], p.coef, grads + B.g, grads + B.b, s));
         return 0;
     };
-    // dz = [y>0](A do + B y + C) either as one elementwise pass over do (default) or inside
-    // the wgrad / dgrad loaders (UNET_DZ_IN_LOADERS=1: fewer passes, but every 3x3 tap
-    // re-gathers both do and y -- measured slower on MI355X, kept for A/B runs)
-    static int dz_in_loaders = -1;
-    if (dz_in_loaders < 0) {
+    // dz = A do + B y + C either as one elementwise pass over do (default) or inside the
+    // wgrad / dgrad loaders (UNET_DZ_IN_LOADERS=1, ReLU -> BN order only: fewer passes, but
+    // every 3x3 tap re-gathers both do and y -- measured slower on MI355X, kept for A/B runs)
+    static int dz_env = -1;
+    if (dz_env < 0) {
         const char* e = getenv("UNET_DZ_IN_LOADERS");
-        dz_in_loaders = e ? atoi(e) : 0;
+        dz_env = e ? atoi(e) : 0;
     }
+    const bool dz_in_loaders = dz_env && !c->bn_relu;
+    const int dz_mask = c->bn_relu ? 0 : 1;
     // conv i backward from do_i (dense [P][cout]).
     // dgrad -> dx (ld ldx).  bn_next: dx is the `do` of BN layer i-1 (second conv of a
     // block), so the epilogue also emits that layer's partials; *rows = their count.
@@ -661,13 +722,14 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         const int64_t P = p.P[C.level];
         if (i == 0 && C.pf < 0) {
             RUN("conv_first_wgrad", 2.0 * P * 9 * C.cout,
-                k_conv_first_wgrad(p.x_nhwc, dout, p.y[0], p.coef, (int)P, Hl, Wl, C.cout,
-                                   p.hpart, RED_G, grads + C.w, grads + C.b, s));
+                k_conv_first_wgrad(p.x_nhwc, dout, p.y[0], p.coef, (int)P, Hl, Wl, C.cout, dz_mask,
+                                   p.hpart, RED_G, grads + C.w,
+                                   C.b >= 0 ? grads + C.b : nullptr, s));
             return 0;
         }
         if (!dz_in_loaders)
             RUN("bn_dz", 0, k_bn_dz(const_cast<float*>(dout), p.y[i], p.ldy[i], p.offy[i], P, C.cout,
-                                    p.coef, s));
+                                    p.coef, dz_mask, s));
         const float* dzc = dz_in_loaders ? p.coef : nullptr;
         Operand a = conv_input(c, p, i);
         WgradCfg wc = wgrad_cfg(C.cin, 9, C.cout, 1, P);
@@ -682,6 +744,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         w.amode = G_CONV3;
         w.ascale = a.scale;
         w.ashift = a.shift;
+        w.arelu = a.relu;
         w.b = dout;
         w.ldb = C.cout;
         w.boff = 0;
@@ -691,7 +754,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         w.ldby = p.ldy[i];
         w.offby = p.offy[i];
         w.bcoef = dzc;
-        w.bias_slab = p.bslab;
+        w.bias_slab = C.b >= 0 ? p.bslab : nullptr;
         w.Mw = 9 * C.cin;
         w.Nw = C.cout;
         w.pps = wc.pps;
@@ -701,7 +764,8 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
             launch_wgrad(w, wc.tile, s));
         RUN("wgrad_reduce", 0,
             k_slab_reduce(p.slab, wc.splits, w.Mw, w.Nw, 0, C.cin, C.cout, grads + C.w, s));
-        RUN("bias_grad", 0, k_bias_reduce(p.bslab, wc.splits, 1, C.cout, grads + C.b, s));
+        if (C.b >= 0)
+            RUN("bias_grad", 0, k_bias_reduce(p.bslab, wc.splits, 1, C.cout, grads + C.b, s));
         if (dx) {
             RowGemmArgs g{};
             g.H = Hl;
@@ -728,6 +792,10 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
                 g.ey = p.y[i - 1];
                 g.ldey = p.ldy[i - 1];
                 g.offey = p.offy[i - 1];
+                if (c->bn_relu) {
+                    g.escale = p.scale[i - 1];
+                    g.eshift = p.shift[i - 1];
+                }
                 g.stats = p.part;
             }
             const int tile = pick_tile(C.cin, true);
@@ -738,12 +806,13 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         }
         return 0;
     };
-    // ConvT k backward: dOut = dcat[lo][:, 0:cout]; dx = `do` of its input's BN (partials -> rows)
+    // ConvT k backward: dOut = up half of dcat[lo]; dx = `do` of its input's BN (partials ->
+    // rows)
     auto convT_bwd = [&](int k, float* dx, int* rows) -> int {
         const ConvTL& T = c->convt[k];
-        const int src = 2 * (4 + k) + 1;
+        const int src = 2 * (D + k) + 1;
         const int lo = T.in_level - 1;
-        const int ldo = 2 * (64 << lo);
+        const int ldo = 2 * c->ch(lo), uo = c->up_off(lo);
         const int Hi = H >> T.in_level, Wi = W >> T.in_level;
         const int64_t Pin = p.P[T.in_level];
         WgradCfg wc = wgrad_cfg(T.cin, 1, T.cout, 4, Pin);
@@ -758,9 +827,10 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         w.amode = G_IDENT;
         w.ascale = p.scale[src];
         w.ashift = p.shift[src];
+        w.arelu = c->bn_relu ? T.cin : 0;
         w.b = p.dcat[lo];
         w.ldb = ldo;
-        w.boff = 0;
+        w.boff = uo;
         w.CB = T.cout;
         w.bmode = G_UP2;
         w.bias_slab = p.bslab;
@@ -782,7 +852,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         g.K = 4 * T.cout;
         g.a = p.dcat[lo];
         g.lda = ldo;
-        g.aoff = 0;
+        g.aoff = uo;
         g.C = T.cout;
         g.amode = G_UP2;
         g.bt = p.pack + T.pd;
@@ -793,6 +863,10 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         g.ey = p.y[src];
         g.ldey = p.ldy[src];
         g.offey = p.offy[src];
+        if (c->bn_relu) {
+            g.escale = p.scale[src];
+            g.eshift = p.shift[src];
+        }
         g.stats = p.part;
         const int tile = pick_tile(T.cin, true);
         int bm, bn, bk;
@@ -801,50 +875,55 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         RUN(tlabel("convT_dgrad", tile, 100 + k), 2.0 * Pin * T.cin * 4 * T.cout, launch_rowgemm(g, tile, s));
         return 0;
     };
-    auto bucket_done = [&](int b) {
-        if (b < (int)c->bucket_ev.size()) (void)hipEventRecord(c->bucket_ev[b], s);
+    auto stage_done = [&](int st) {
+        for (size_t b = 0; b < c->bucket_stage.size(); ++b)
+            if (c->bucket_stage[b] == st) (void)hipEventRecord(c->bucket_ev[b], s);
     };
 
     float* G0 = p.g[0];
     float* G1 = p.g[1];
     int R = 0;
-    // ---- head + final block (bucket 0) ----
-    RUN("head_bwd", 2.0 * p.P[0] * 64 * c->out_ch * 2,
-        k_head_bwd(p.y[17], 64, p.scale[17], p.shift[17], prm + c->head_w, c->out_ch, (int)p.P[0],
-                   H * W, dlogits, G0, p.hpart, p.part, RED_G, s));
-    RUN("head_grad", 0, k_sum_partials(p.hpart, RED_G, c->out_ch * 64 + c->out_ch, grads + c->head_w, s));
-    if ((rc = bn_finalize(17, RED_G))) return rc;
-    if ((rc = conv_bwd(17, G0, G1, 64, true, &R))) return rc;
-    if ((rc = bn_finalize(16, R))) return rc;
-    if ((rc = conv_bwd(16, G1, p.dcat[0], 128, false, nullptr))) return rc;
-    bucket_done(0);
-    // ---- decoders: ConvT k, then block 4+k ----
-    for (int k = 3; k >= 0; --k) {
-        const int b = 4 + k;
+    // ---- head + last decoder block (stage 0) ----
+    const int last = NC - 1;
+    RUN("head_bwd", 2.0 * p.P[0] * c->base * c->out_ch * 2,
+        k_head_bwd(p.y[last], c->base, p.scale[last], p.shift[last], c->bn_relu ? 1 : 0,
+                   prm + c->head_w, c->out_ch, (int)p.P[0], H * W, dlogits, G0, p.hpart, p.part,
+                   RED_G, s));
+    RUN("head_grad", 0, k_sum_partials(p.hpart, RED_G, c->out_ch * c->base + c->out_ch,
+                                       grads + c->head_w, s));
+    if ((rc = bn_finalize(last, RED_G))) return rc;
+    if ((rc = conv_bwd(last, G0, G1, c->base, true, &R))) return rc;
+    if ((rc = bn_finalize(last - 1, R))) return rc;
+    if ((rc = conv_bwd(last - 1, G1, p.dcat[0], 2 * c->base, false, nullptr))) return rc;
+    stage_done(0);
+    // ---- ConvT k, then block D+k (the block whose output it up-samples) ----
+    for (int k = D - 1; k >= 0; --k) {
+        const int b = D + k;
         const int i1 = 2 * b + 1, i0 = 2 * b;
         if ((rc = convT_bwd(k, G0, &R))) return rc;
         if ((rc = bn_finalize(i1, R))) return rc;
         if ((rc = conv_bwd(i1, G0, G1, c->conv[i1].cin, true, &R))) return rc;
         if ((rc = bn_finalize(i0, R))) return rc;
-        if (b >= 5) {
+        if (b > D) {
             const int l = c->conv[i0].level;  // input is CAT_l
-            if ((rc = conv_bwd(i0, G1, p.dcat[l], 2 * (64 << l), false, nullptr))) return rc;
-            bucket_done(4 - k);  // decoder1 -> bucket 1, decoder2 -> 2, decoder3 -> 3
+            if ((rc = conv_bwd(i0, G1, p.dcat[l], 2 * c->ch(l), false, nullptr))) return rc;
         } else {
-            // middle block: its input is pool[3]; G0 <- d pool[3]
+            // bottleneck: its input is pool[D-1]; G0 <- d pool[D-1]
             if ((rc = conv_bwd(i0, G1, G0, c->conv[i0].cin, false, nullptr))) return rc;
-            bucket_done(4);
         }
+        stage_done(D - k);
     }
     // ---- encoders ----
     float* cur = G0;
-    for (int b = 3; b >= 0; --b) {
-        const int C = 64 << b;
+    for (int b = D - 1; b >= 0; --b) {
+        const int C = c->ch(b);
         const int i1 = 2 * b + 1, i0 = 2 * b;
         float* nxt = cur == G0 ? G1 : G0;
         RUN("maxpool_bwd", 0,
-            k_maxpool_bwd(cur, p.idx[b], p.dcat[b], 2 * C, C, p.y[i1], p.ldy[i1], p.offy[i1], p.N,
-                          H >> b, W >> b, C, nxt, p.part, RED_G, s));
+            k_maxpool_bwd(cur, p.idx[b], p.dcat[b], 2 * C, c->skip_off(b), p.y[i1], p.ldy[i1],
+                          p.offy[i1], c->bn_relu ? p.scale[i1] : nullptr,
+                          c->bn_relu ? p.shift[i1] : nullptr, p.N, H >> b, W >> b, C, nxt, p.part,
+                          RED_G, s));
         cur = nxt;
         nxt = cur == G0 ? G1 : G0;
         if ((rc = bn_finalize(i1, RED_G))) return rc;
@@ -858,12 +937,15 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         } else {
             if ((rc = conv_bwd(0, cur, nullptr, 0, false, nullptr))) return rc;
         }
-        bucket_done(8 - b);
+        stage_done(2 * D - b);
     }
     return 0;
 }
 
-bool shape_ok(int N, int H, int W) { return N >= 1 && H >= 16 && W >= 16 && H % 16 == 0 && W % 16 == 0; }
+bool shape_ok(const unet_ctx* c, int N, int H, int W) {
+    const int q = 1 << std::max(c->depth, 4);  // every level even; >= 16 (model.py contract)
+    return N >= 1 && H >= q && W >= q && H % q == 0 && W % q == 0;
+}
 
 }  // namespace
 
@@ -878,13 +960,27 @@ int unet_create(const unet_cfg* cfg, int device, unet_ctx** out) {
     if (cfg) {
         c->in_ch = cfg->in_channels;
         c->out_ch = cfg->out_channels;
+        c->variant = cfg->variant;
+        if (c->variant == UNET_VARIANT_MOD) {  // mod.py:13-14 defaults base 64, depth 5
+            c->base = cfg->base_filters > 0 ? cfg->base_filters : 64;
+            c->depth = cfg->depth > 0 ? cfg->depth : 5;
+        } else if ((cfg->base_filters > 0 && cfg->base_filters != 64) ||
+                   (cfg->depth > 0 && cfg->depth != 4)) {
+            delete c;  // models/model.py:UNet has a fixed topology
+            return UNET_ERR_UNSUPPORTED;
+        }
     }
-    // models/model.py:UNet defaults (1, 1) are what every BASELINE config uses; the first
-    // conv kernel is specialised for a single input channel.
-    if (c->in_ch != 1 || c->out_ch < 1 || c->out_ch > 4) {
+    // The first conv kernel is specialised for a single input channel (every BASELINE
+    // config); the GEMM tiles need 64-multiples of channels at every level; the head's
+    // fused BN-partials path handles up to 4 classes.
+    if ((c->variant != UNET_VARIANT_MODEL && c->variant != UNET_VARIANT_MOD) || c->in_ch != 1 ||
+        c->out_ch < 1 || c->out_ch > 4 || c->base % 64 || c->base > 256 || c->depth < 1 ||
+        c->depth > MAX_DEPTH || (c->base << c->depth) > 8192) {
         delete c;
         return UNET_ERR_UNSUPPORTED;
     }
+    c->bn_relu = c->variant == UNET_VARIANT_MOD;
+    c->skip_first = c->bn_relu;
     build_graph(c);
     *out = c;
     return UNET_OK;
@@ -921,13 +1017,13 @@ int unet_param_info(const unet_ctx* c, int i, const char** name, int* ndim, int6
 
 int unet_num_bn(const unet_ctx* c, int* n, int64_t* nf) {
     if (!c) return UNET_ERR_INVALID;
-    if (n) *n = NCONV;
+    if (n) *n = c->nconv();
     if (nf) *nf = c->n_bn_floats;
     return UNET_OK;
 }
 
 int unet_bn_info(const unet_ctx* c, int i, const char** name, int* ch, int64_t* off) {
-    if (!c || i < 0 || i >= NCONV) return UNET_ERR_INVALID;
+    if (!c || i < 0 || i >= c->nconv()) return UNET_ERR_INVALID;
     if (name) *name = c->bn[i].name.c_str();
     if (ch) *ch = c->bn[i].C;
     if (off) *off = c->bn[i].run;
@@ -936,7 +1032,7 @@ int unet_bn_info(const unet_ctx* c, int i, const char** name, int* ch, int64_t* 
 
 int unet_workspace_size(unet_ctx* c, int N, int H, int W, int training, size_t* bytes) {
     if (!c || !bytes) return UNET_ERR_INVALID;
-    if (!shape_ok(N, H, W)) return fail(c, UNET_ERR_SHAPE, "bad shape N=%d H=%d W=%d", N, H, W);
+    if (!shape_ok(c, N, H, W)) return fail(c, UNET_ERR_SHAPE, "bad shape N=%d H=%d W=%d", N, H, W);
     Plan p;
     make_plan(c, N, H, W, training != 0, nullptr, p);
     *bytes = p.bytes;
@@ -947,7 +1043,7 @@ int unet_forward(unet_ctx* c, const float* params, float* bn_running, int64_t* b
                  const float* x, float* logits, void* ws, size_t ws_bytes, int N, int H, int W,
                  int training, unet_stream_t stream) {
     if (!c || !params || !x || !logits || !ws) return c ? fail(c, UNET_ERR_INVALID, "null pointer") : UNET_ERR_INVALID;
-    if (!shape_ok(N, H, W)) return fail(c, UNET_ERR_SHAPE, "bad shape N=%d H=%d W=%d", N, H, W);
+    if (!shape_ok(c, N, H, W)) return fail(c, UNET_ERR_SHAPE, "bad shape N=%d H=%d W=%d", N, H, W);
     if (!training && !bn_running)
         return fail(c, UNET_ERR_INVALID, "eval forward needs running statistics");
     Plan p;
@@ -963,7 +1059,7 @@ int unet_forward(unet_ctx* c, const float* params, float* bn_running, int64_t* b
 int unet_backward(unet_ctx* c, const float* params, const float* dlogits, float* grads, void* ws,
                   size_t ws_bytes, int N, int H, int W, unet_stream_t stream) {
     if (!c || !params || !dlogits || !grads || !ws) return c ? fail(c, UNET_ERR_INVALID, "null pointer") : UNET_ERR_INVALID;
-    if (!shape_ok(N, H, W)) return fail(c, UNET_ERR_SHAPE, "bad shape N=%d H=%d W=%d", N, H, W);
+    if (!shape_ok(c, N, H, W)) return fail(c, UNET_ERR_SHAPE, "bad shape N=%d H=%d W=%d", N, H, W);
     Plan p;
     make_plan(c, N, H, W, true, nullptr, p);
     if (ws_bytes < p.bytes) return fail(c, UNET_ERR_WORKSPACE, "workspace %zu < %zu", ws_bytes, p.bytes);
@@ -1074,7 +1170,7 @@ int unet_timing_read(unet_ctx* c, int i, const char** family, int64_t* launches,
 int unet_debug_view(unet_ctx* c, int N, int H, int W, int training, int kind, int index,
                     int64_t* byte_offset, int64_t* count, int* ld, int* off) {
     if (!c || !byte_offset || !count) return UNET_ERR_INVALID;
-    if (!shape_ok(N, H, W)) return fail(c, UNET_ERR_SHAPE, "bad shape");
+    if (!shape_ok(c, N, H, W)) return fail(c, UNET_ERR_SHAPE, "bad shape");
     Plan p;
     char* const base = (char*)(uintptr_t)4096;  // fake base: offsets only
     make_plan(c, N, H, W, training != 0, base, p);
@@ -1082,7 +1178,7 @@ int unet_debug_view(unet_ctx* c, int N, int H, int W, int training, int kind, in
     int64_t n = 0;
     int l = 1, o = 0;
     if (kind <= 4) {
-        if (index < 0 || index >= NCONV) return UNET_ERR_INVALID;
+        if (index < 0 || index >= c->nconv()) return UNET_ERR_INVALID;
         const ConvL& L = c->conv[index];
         const int C = L.cout;
         if (kind == 0) {
@@ -1095,8 +1191,8 @@ int unet_debug_view(unet_ctx* c, int N, int H, int W, int training, int kind, in
             n = C;
         }
     } else {
-        if (index < 0 || index >= 4) return UNET_ERR_INVALID;
-        const int C = 64 << index;
+        if (index < 0 || index >= c->depth) return UNET_ERR_INVALID;
+        const int C = c->ch(index);
         if (kind == 5) {
             q = p.pool[index];
             n = p.P[index + 1] * C;

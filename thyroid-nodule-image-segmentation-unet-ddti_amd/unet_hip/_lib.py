@@ -37,7 +37,12 @@ P = ctypes.POINTER
 
 
 class UnetCfg(ctypes.Structure):
-    _fields_ = [("in_channels", c_int), ("out_channels", c_int)]
+    _fields_ = [("in_channels", c_int), ("out_channels", c_int), ("variant", c_int),
+                ("base_filters", c_int), ("depth", c_int)]
+
+
+VARIANT_MODEL = 0  # models/model.py:UNet
+VARIANT_MOD = 1    # models/mod.py:UNet
 
 
 # name -> (restype, argtypes); mirrors include/unet_hip.h

@@ -1,7 +1,11 @@
-"""Drop-in ``UNet`` (models/model.py:5-73) whose forward/backward run on libunet_hip.so.
+"""Drop-in ``UNet`` modules whose forward/backward run on libunet_hip.so:
 
-The module keeps the reference's exact submodule tree (encoder1..4, middle, decoder3..1,
-final; Conv2d / ReLU / BatchNorm2d / ConvTranspose2d in the same Sequential slots), so
+* ``UNet``    -- models/model.py:5-73
+* ``ModUNet`` -- models/mod.py:9-66 (``UNet(in, out, base_filters, depth)``)
+
+Each keeps its reference's exact submodule tree (model.py: encoder1..4, middle,
+decoder3..1, final; mod.py: encoders, pools, bottleneck, upconvs, decoders, final_conv;
+Conv2d / ReLU / BatchNorm2d / ConvTranspose2d in the same Sequential slots), so
 
 * ``state_dict()`` keys, shapes and torch layouts are identical and checkpoints move
   freely between this module and the reference (``main.py:141-142`` style loading);
@@ -18,6 +22,7 @@ there is no silent CPU fallback.
 import torch
 import torch.nn as nn
 
+from . import _lib
 from ._lib import HipUnavailable
 from .functional import UNetFunction
 from .runtime import UNetRuntime
@@ -64,21 +69,14 @@ class _ArenaState:
         return [arena[off:off + p.numel()].view(p.shape) for p, off, _ in self.params]
 
 
-class UNet(nn.Module):
-    def __init__(self, in_channels=1, out_channels=1):
-        super().__init__()
-        self.in_channels, self.out_channels = in_channels, out_channels
-        self.encoder1 = _conv_block(in_channels, 64)
-        self.encoder2 = _conv_block(64, 128)
-        self.encoder3 = _conv_block(128, 256)
-        self.encoder4 = _conv_block(256, 512)
-        self.middle = nn.Sequential(nn.MaxPool2d(kernel_size=2, stride=2), _conv_block(512, 1024),
-                                    nn.ConvTranspose2d(1024, 512, kernel_size=2, stride=2))
-        self.decoder3 = _upconv_block(1024, 256)
-        self.decoder2 = _upconv_block(512, 128)
-        self.decoder1 = _upconv_block(256, 64)
-        self.final = nn.Sequential(_conv_block(128, 64), nn.Conv2d(64, out_channels, kernel_size=1))
-        self._state = None
+class _HipUNet(nn.Module):
+    """Arena management and the native forward shared by both reference networks."""
+
+    _name = "UNet"
+
+    def _native_cfg(self):
+        """(in_channels, out_channels, variant, base_filters, depth) of the native graph."""
+        raise NotImplementedError
 
     # ---------------------------------------------------------------- arenas
     def _bn_modules(self):
@@ -104,9 +102,9 @@ class UNet(nn.Module):
         p0 = next(self.parameters())
         dev = p0.device
         if dev.type != "cuda":
-            raise HipUnavailable("models.model.UNet runs on the MI355X HIP path only; move it to a "
+            raise HipUnavailable(f"{self._name} runs on the MI355X HIP path only; move it to a "
                                  "GPU with .cuda() / .to('cuda') (no CPU fallback)")
-        rt = UNetRuntime.get(dev, self.in_channels, self.out_channels)
+        rt = UNetRuntime.get(dev, *self._native_cfg())
         if self._arenas_valid(rt):
             return self._state
         named = dict(self.named_parameters())
@@ -144,8 +142,8 @@ class UNet(nn.Module):
 
     # ---------------------------------------------------------------- forward
     def forward(self, x):
-        """models/model.py:53-73: (N, in_channels, H, W) fp32 -> logits (N, out_channels, H, W).
-        H and W must be multiples of 16 (four 2x2 pools)."""
+        """(N, in_channels, H, W) fp32 -> logits (N, out_channels, H, W) (models/model.py:53-73,
+        models/mod.py:53-66).  H and W must be multiples of max(16, 2**depth)."""
         st = self.flatten_()
         if x.dim() != 4 or x.shape[1] != self.in_channels:
             raise ValueError(f"expected (N, {self.in_channels}, H, W), got {tuple(x.shape)}")
@@ -163,3 +161,71 @@ class UNet(nn.Module):
     @property
     def flat_params(self):
         return self.flatten_().param_arena
+
+
+class UNet(_HipUNet):
+    """models/model.py:5-73."""
+
+    _name = "models.model.UNet"
+
+    def __init__(self, in_channels=1, out_channels=1):
+        super().__init__()
+        self.in_channels, self.out_channels = in_channels, out_channels
+        self.encoder1 = _conv_block(in_channels, 64)
+        self.encoder2 = _conv_block(64, 128)
+        self.encoder3 = _conv_block(128, 256)
+        self.encoder4 = _conv_block(256, 512)
+        self.middle = nn.Sequential(nn.MaxPool2d(kernel_size=2, stride=2), _conv_block(512, 1024),
+                                    nn.ConvTranspose2d(1024, 512, kernel_size=2, stride=2))
+        self.decoder3 = _upconv_block(1024, 256)
+        self.decoder2 = _upconv_block(512, 128)
+        self.decoder1 = _upconv_block(256, 64)
+        self.final = nn.Sequential(_conv_block(128, 64), nn.Conv2d(64, out_channels, kernel_size=1))
+        self._state = None
+
+    def _native_cfg(self):
+        return self.in_channels, self.out_channels, _lib.VARIANT_MODEL, 0, 0
+
+
+def _mod_block(cin, cout):
+    # models/mod.py:43-51: Conv3x3(no bias) -> BN -> ReLU -> Conv3x3(no bias) -> BN -> ReLU
+    return nn.Sequential(nn.Conv2d(cin, cout, kernel_size=3, padding=1, bias=False),
+                         nn.BatchNorm2d(cout), nn.ReLU(inplace=True),
+                         nn.Conv2d(cout, cout, kernel_size=3, padding=1, bias=False),
+                         nn.BatchNorm2d(cout), nn.ReLU(inplace=True))
+
+
+class ModUNet(_HipUNet):
+    """models/mod.py:9-66 ``UNet(in_channels, out_channels, base_filters, depth)``.
+
+    Supported here: in_channels 1, out_channels 1..4, base_filters a multiple of 64
+    (<= 256), depth 1..6 (the native GEMM tiles work on 64-channel multiples)."""
+
+    _name = "models.mod.UNet"
+
+    def __init__(self, in_channels=1, out_channels=1, base_filters=64, depth=5, **kwargs):
+        super().__init__()
+        self.in_channels, self.out_channels = in_channels, out_channels
+        self.base_filters, self.depth = base_filters, depth
+        # same construction (and RNG consumption) order as mod.py:21-41
+        self.encoders = nn.ModuleList()
+        self.pools = nn.ModuleList()
+        prev = in_channels
+        channels = [base_filters * (2 ** i) for i in range(depth)]
+        for ch in channels:
+            self.encoders.append(_mod_block(prev, ch))
+            self.pools.append(nn.MaxPool2d(2, 2))
+            prev = ch
+        self.bottleneck = _mod_block(prev, prev * 2)
+        self.upconvs = nn.ModuleList()
+        self.decoders = nn.ModuleList()
+        prev = channels[-1] * 2
+        for ch in channels[::-1]:
+            self.upconvs.append(nn.ConvTranspose2d(prev, ch, kernel_size=2, stride=2))
+            self.decoders.append(_mod_block(prev, ch))
+            prev = ch
+        self.final_conv = nn.Conv2d(base_filters, out_channels, kernel_size=1)
+        self._state = None
+
+    def _native_cfg(self):
+        return self.in_channels, self.out_channels, _lib.VARIANT_MOD, self.base_filters, self.depth

@@ -1,6 +1,6 @@
 """Python handle on a native UNet context (libunet_hip.so).
 
-One ``UNetRuntime`` per (device, in_channels, out_channels).  It exposes the native
+One ``UNetRuntime`` per (device, network configuration).  It exposes the native
 parameter / BN-buffer tables (so the ``nn.Module`` can lay its tensors out in the flat
 arenas the kernels read) and thin, shape-checked wrappers of the C entry points that
 take torch tensors and enqueue on torch's current stream.
@@ -15,11 +15,12 @@ _RUNTIMES = {}
 
 
 class UNetRuntime:
-    def __init__(self, device, in_channels=1, out_channels=1):
+    def __init__(self, device, in_channels=1, out_channels=1, variant=_lib.VARIANT_MODEL,
+                 base_filters=0, depth=0):
         lib = _lib.load()
         self.lib = lib
         self.device = torch.device(device)
-        cfg = _lib.UnetCfg(in_channels, out_channels)
+        cfg = _lib.UnetCfg(in_channels, out_channels, variant, base_filters, depth)
         h = ctypes.c_void_p()
         _lib.check(lib.unet_create(ctypes.byref(cfg), self.device.index or 0, ctypes.byref(h)),
                    None, "unet_create")
@@ -57,11 +58,12 @@ class UNetRuntime:
             pass
 
     @staticmethod
-    def get(device, in_channels=1, out_channels=1):
-        key = (str(torch.device(device)), in_channels, out_channels)
+    def get(device, in_channels=1, out_channels=1, variant=_lib.VARIANT_MODEL, base_filters=0,
+            depth=0):
+        key = (str(torch.device(device)), in_channels, out_channels, variant, base_filters, depth)
         rt = _RUNTIMES.get(key)
         if rt is None:
-            rt = UNetRuntime(device, in_channels, out_channels)
+            rt = UNetRuntime(device, in_channels, out_channels, variant, base_filters, depth)
             _RUNTIMES[key] = rt
         return rt
 
