@@ -8,6 +8,8 @@ inputs resident in HBM before the timed region.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU, RCCL)
+    python bench.py --config 4      models/mod.py UNet(base 128, depth 5), 512x512, bs 8
+                                    (BASELINE config 4; not the headline metric)
 
 Prints ONE JSON line on rank 0.  ``value`` = images/s of the whole job (sum over ranks,
 time = max over ranks).  ``roofline`` is for the dominant kernel (most GPU time in the
@@ -29,6 +31,7 @@ for _p in (REPO, PKG):
         sys.path.insert(0, _p)
 
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md chip table, dense fp32 matrix
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # dense bf16 matrix (no 2:1 sparsity)
 HBM_PEAK_GBS = 8000.0
 
 
@@ -37,17 +40,25 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=32, help="images per GPU")
-    ap.add_argument("--size", type=int, default=256)
+    ap.add_argument("--config", type=int, default=2, choices=(2, 4),
+                    help="BASELINE config: 2 = models/model.py UNet (3 = 2 on N ranks), "
+                         "4 = models/mod.py UNet(base 128, depth 5) at 512x512")
+    ap.add_argument("--mfma", default="fp32", choices=("fp32", "bf16"),
+                    help="config 4 only: conv GEMM arithmetic (BASELINE config 4 is bf16)")
+    ap.add_argument("--batch", type=int, default=0, help="images per GPU (default 32 / 8)")
+    ap.add_argument("--size", type=int, default=0, help="image side (default 256 / 512)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=2)
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args()
 
 
-def cpu_baseline(steps, size):
-    """Oracle step on the host CPU, bs=4 (BASELINE config 1 shape), median of `steps`."""
+def cpu_baseline(steps, size, config=2):
+    """Oracle step on the host CPU, median of `steps`: bs=4 (BASELINE config 1 shape) for
+    models/model.py; for config 4 one 256x256 image of mod.py UNet(128, 5) (a quarter of one
+    512x512 image's work, scaled to images/s of the 512x512 workload)."""
     import torch
+    from oracle import mod_ref_cpu as MO
     from oracle import unet_ref_cpu as O
     from oracle import weights as Wt
     # the GPU box exposes every host CPU in os.cpu_count() but gives a job a 16-CPU share
@@ -55,16 +66,28 @@ def cpu_baseline(steps, size):
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
     threads = max(1, min(threads, 16, os.cpu_count() or 1))
     torch.set_num_threads(threads)
-    P = O.make_params(42)
-    B = O.init_buffers()
+    if config == 4:
+        nb, side, scale = 1, size // 2, 0.25
+        P = MO.make_params(42, 128, 5)
+        B = MO.init_buffers(128, 5)
+
+        def run(P, B, opt, x, t):
+            return MO.train_step(P, B, opt, x, t, depth=5)
+        what = "oracle/mod_ref_cpu.py UNet(128, 5) train step"
+    else:
+        nb, side, scale = 4, size, 1.0
+        P = O.make_params(42)
+        B = O.init_buffers()
+        run = O.train_step
+        what = "oracle/unet_ref_cpu.py train step"
     opt = O.AdamWState(P, lr=1e-5)
-    x = torch.from_numpy(Wt.make_input(21, 4, 1, size, size))
-    t = torch.from_numpy(Wt.make_target(21, 4, size, size))
-    O.train_step(P, B, opt, x, t)  # warm-up
+    x = torch.from_numpy(Wt.make_input(21, nb, 1, side, side))
+    t = torch.from_numpy(Wt.make_target(21, nb, side, side))
+    run(P, B, opt, x, t)  # warm-up
     ts = []
     for _ in range(steps):
         t0 = time.perf_counter()
-        O.train_step(P, B, opt, x, t)
+        run(P, B, opt, x, t)
         ts.append(time.perf_counter() - t0)
     ts.sort()
     med = ts[len(ts) // 2]
@@ -76,10 +99,11 @@ def cpu_baseline(steps, size):
                 break
     except OSError:
         pass
-    return {"value": round(4 / med, 4), "unit": "images/sec", "cores": threads, "kind": "port",
-            "sample": f"oracle/unet_ref_cpu.py train step (fwd+BCE+Dice+bwd+AdamW), bs=4, "
-                      f"1x{size}x{size}, median of {steps} steps after 1 warm-up, "
-                      f"torch CPU {threads} threads, {cpu_model}"}
+    return {"value": round(nb * scale / med, 4), "unit": "images/sec", "cores": threads,
+            "kind": "port",
+            "sample": f"{what} (fwd+BCE+Dice+bwd+AdamW), bs={nb}, 1x{side}x{side}"
+                      f"{' (scaled x0.25 to 512x512 images)' if scale != 1.0 else ''}, median of "
+                      f"{steps} steps after 1 warm-up, torch CPU {threads} threads, {cpu_model}"}
 
 
 def load_pmc(kernel):
@@ -109,10 +133,18 @@ def main():
 
     import unet_hip
     from unet_hip.dist import DistributedUNet
-    from oracle import unet_ref_cpu as O  # analytic FLOP count only
+    from oracle import mod_ref_cpu as MO  # analytic FLOP counts only
+    from oracle import unet_ref_cpu as O
 
+    c4 = args.config == 4
+    args.batch = args.batch or (8 if c4 else 32)
+    args.size = args.size or (512 if c4 else 256)
     torch.manual_seed(42)
-    model = unet_hip.UNet(1, 1).to(dev).train()
+    if c4:
+        model = unet_hip.ModUNet(1, 1, base_filters=128, depth=5,
+                                 mfma_dtype=args.mfma).to(dev).train()
+    else:
+        model = unet_hip.UNet(1, 1).to(dev).train()
     opt = unet_hip.HipAdamW(model.parameters(), lr=1e-5)
     ddp = DistributedUNet(model, opt) if world > 1 else None
 
@@ -178,27 +210,42 @@ def main():
     achieved = f_l / (t_l * 1e-3) / 1e12 if t_l > 0 else 0.0
     per_launch_flop = f_l / n_l
     pmc = load_pmc(dom)
-    conv_flop = O.train_flops_per_image(S, S) * B
+    conv_flop = (MO.train_flops_per_image(S, S, 128, 5) if c4 else O.train_flops_per_image(S, S)) * B
+    bf16 = c4 and args.mfma == "bf16"
+    peak = BF16_MFMA_PEAK_TFLOPS if bf16 else FP32_MFMA_PEAK_TFLOPS
     roofline = {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 3),
-                "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
+                "peak": peak, "unit": "TFLOP/s",
+                "frac": round(achieved / peak, 4),
                 "traffic": pmc, "launches": n_l, "avg_launch_ms": round(t_l / n_l, 4),
                 "flop_per_launch": per_launch_flop,
                 "kernel_share_of_gpu_time": round(t_l / max(1e-9, sum(v[1] for v in kern.values())), 4),
                 "step_conv_tflops": round(conv_flop / (ms * 1e-3) / 1e12, 3),
-                "step_conv_frac": round(conv_flop / (ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4)}
+                "step_conv_frac": round(conv_flop / (ms * 1e-3) / 1e12 / peak, 4)}
 
-    out = {"metric": "images/sec fwd+bwd, UNet 256x256x1 bs=32/GPU (Dice+BCE, AdamW)",
+    if c4:
+        metric = f"images/sec fwd+bwd, mod.UNet(base 128, depth 5) {S}x{S}x1 bs={B}/GPU"
+        if bf16:
+            workload_note = " (conv GEMMs bf16 MFMA, f32 accumulate)"
+        else:
+            workload_note = " (conv GEMMs f32 MFMA)"
+        workload = (f"models/mod.py UNet base-128 depth-5, 1x{S}x{S}, bs={B}/GPU, "
+                    f"fwd+BCE+Dice+bwd+AdamW (BASELINE config 4){workload_note}")
+        mname = "mod.UNet(in=1,out=1,base_filters=128,depth=5) 497,438,849 params"
+    else:
+        metric = "images/sec fwd+bwd, UNet 256x256x1 bs=32/GPU (Dice+BCE, AdamW)"
+        workload = (f"models/model.py UNet depth-4 base-64, 1x{S}x{S}, bs={B}/GPU, "
+                    f"fwd+BCE+Dice+bwd+AdamW (BASELINE config {'2' if world == 1 else '3'})")
+        mname = "UNet(in=1,out=1) 31,042,369 params"
+    out = {"metric": metric,
            "value": round(value, 3), "unit": "images/sec", "n_gpus": world, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
-           "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
-           "config": {"workload": f"models/model.py UNet depth-4 base-64, 1x{S}x{S}, bs={B}/GPU, "
-                                  f"fwd+BCE+Dice+bwd+AdamW (BASELINE config {'2' if world == 1 else '3'})",
-                      "model": "UNet(in=1,out=1) 31,042,369 params", "global_batch": B * world,
+           "scaling": "weak", "vs_baseline": None, "dtype": "bf16" if bf16 else "fp32",
+           "data": "synthetic",
+           "config": {"workload": workload, "model": mname, "global_batch": B * world,
                       "image": [1, S, S], "parallelism": f"dp{world}"},
            "roofline": roofline}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(args.cpu_steps, S)
+        out["cpu_baseline"] = cpu_baseline(args.cpu_steps, S, args.config)
     elif rank == 0:
         out["cpu_baseline"] = None
     if rank == 0:

@@ -72,12 +72,20 @@ typedef enum {
                                concat [skip, up], base_filters / depth configurable */
 } unet_variant;
 
+/* Arithmetic of the convolution GEMMs. */
+typedef enum {
+    UNET_MATH_F32 = 0,  /* v_mfma_f32_32x32x2_f32: exact f32 products (the reference's fp32) */
+    UNET_MATH_BF16 = 1  /* v_mfma_f32_32x32x16_bf16: operands rounded to bf16, f32 accumulate
+                           (BASELINE config 4; models/mod.py variant only) */
+} unet_math;
+
 typedef struct {
     int in_channels;   /* models/model.py:6 / mod.py:11 in_channels (default 1; must be 1) */
     int out_channels;  /* models/model.py:6 / mod.py:12 out_channels (default 1; 1..4)   */
     int variant;       /* unet_variant (0 = models/model.py)                               */
     int base_filters;  /* mod.py:13 (0 = default 64); a multiple of 64, <= 256             */
     int depth;         /* mod.py:14 (0 = default 5 for mod, 4 for model); 1..6             */
+    int math;          /* unet_math of the conv GEMMs (0 = f32)                            */
 } unet_cfg;
 
 /* models/model.py:6-31 / models/mod.py:10-41.  device = HIP ordinal the context will

@@ -16,6 +16,14 @@ restatement follows:
 Parameters are named and ordered exactly like ``named_parameters()`` of the reference
 module (encoders.*, bottleneck.*, upconvs.*, decoders.*, final_conv.*).  Losses, the
 train step and AdamW are shared with ``unet_ref_cpu``.
+
+``make_forward(depth, bf16=True)`` is the checker of the bf16-MFMA build of BASELINE
+config 4: every 3x3 conv except the first (Cin = 1) and every ConvTranspose takes its
+activation and weight rounded to bf16 (round to nearest even) and, in backward, its output
+gradient rounded to bf16 before both the input- and the weight-gradient products; all
+sums, BN, ReLU, pooling, the head and the losses stay in the evaluation dtype.  That is
+the arithmetic of the HIP bf16 GEMMs (operands rounded when staged into LDS, f32
+accumulate), so the two agree to fp32 accumulation-order noise.
 """
 import torch
 import torch.nn.functional as F
@@ -84,38 +92,77 @@ def make_params(seed=42, base=64, depth=5, gamma_lo=0.5, gamma_hi=1.5, in_channe
     return {k: torch.from_numpy(v) for k, v in p.items()}
 
 
-def _block(x, P, B, prefix, training):
-    # mod.py:43-51
-    x = F.conv2d(x, P[f"{prefix}.0.weight"], None, padding=1)
+def _rnd(t):
+    """Round to bf16 (nearest even) and back to t's dtype."""
+    return t.to(torch.bfloat16).to(t.dtype)
+
+
+class _BF16Operands(torch.autograd.Function):
+    """fn(rnd(x), rnd(w)) with backward products on rnd(grad) (see module docstring)."""
+
+    @staticmethod
+    def forward(ctx, fn, x, w):
+        xr, wr = _rnd(x), _rnd(w)
+        ctx.fn = fn
+        ctx.save_for_backward(xr, wr)
+        return fn(xr, wr)
+
+    @staticmethod
+    def backward(ctx, g):
+        xr, wr = ctx.saved_tensors
+        with torch.enable_grad():
+            a = xr.detach().requires_grad_(True)
+            b = wr.detach().requires_grad_(True)
+            dx, dw = torch.autograd.grad(ctx.fn(a, b), (a, b), _rnd(g))
+        return None, dx, dw
+
+
+def _conv3(x, w, bf16):
+    if not bf16:
+        return F.conv2d(x, w, None, padding=1)
+    return _BF16Operands.apply(lambda a, b: F.conv2d(a, b, None, padding=1), x, w)
+
+
+def _convT(x, w, b, bf16):
+    if not bf16:
+        return F.conv_transpose2d(x, w, b, stride=2)
+    return _BF16Operands.apply(lambda a, ww: F.conv_transpose2d(a, ww, None, stride=2), x, w) + \
+        b.view(1, -1, 1, 1)
+
+
+def _block(x, P, B, prefix, training, bf16=False, first=False):
+    # mod.py:43-51 (the Cin = 1 first conv runs in f32 on the HIP path too)
+    x = _conv3(x, P[f"{prefix}.0.weight"], bf16 and not first)
     x = F.relu(O._bn(x, P, B, f"{prefix}.1", training))
-    x = F.conv2d(x, P[f"{prefix}.3.weight"], None, padding=1)
+    x = _conv3(x, P[f"{prefix}.3.weight"], bf16)
     return F.relu(O._bn(x, P, B, f"{prefix}.4", training))
 
 
-def make_forward(depth):
+def make_forward(depth, bf16=False):
     """forward(x, P, B, training) of mod.py:UNet with `depth` levels (mod.py:53-66)."""
 
     def forward(x, P, B, training=True):
         skips = []
         for i in range(depth):
-            x = _block(x, P, B, f"encoders.{i}", training)
+            x = _block(x, P, B, f"encoders.{i}", training, bf16, first=(i == 0))
             skips.append(x)
             x = F.max_pool2d(x, 2, 2)
-        x = _block(x, P, B, "bottleneck", training)
+        x = _block(x, P, B, "bottleneck", training, bf16)
         for j, skip in enumerate(reversed(skips)):
-            x = F.conv_transpose2d(x, P[f"upconvs.{j}.weight"], P[f"upconvs.{j}.bias"], stride=2)
+            x = _convT(x, P[f"upconvs.{j}.weight"], P[f"upconvs.{j}.bias"], bf16)
             if x.shape != skip.shape:
                 x = F.interpolate(x, size=skip.shape[2:], mode="bilinear", align_corners=False)
             x = torch.cat([skip, x], dim=1)
-            x = _block(x, P, B, f"decoders.{j}", training)
+            x = _block(x, P, B, f"decoders.{j}", training, bf16)
         return F.conv2d(x, P["final_conv.weight"], P["final_conv.bias"])
 
     return forward
 
 
-def train_step(P, B, opt, x, t, depth, w_bce=1.0, w_dice=1.0, shards=1):
+def train_step(P, B, opt, x, t, depth, w_bce=1.0, w_dice=1.0, shards=1, bf16=False):
     """utils/trainer.py:81-93 with mod.py:UNet as the model."""
-    return O.train_step(P, B, opt, x, t, w_bce, w_dice, shards, forward_fn=make_forward(depth))
+    return O.train_step(P, B, opt, x, t, w_bce, w_dice, shards,
+                        forward_fn=make_forward(depth, bf16))
 
 
 def conv_macs_per_image(H, W, in_channels=1, out_channels=1, base=64, depth=5):

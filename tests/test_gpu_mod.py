@@ -149,3 +149,52 @@ def test_mod_config4_full_size_smoke():
     mean = z.mean((0, 2, 3))
     # running_mean after one step = 0.1 * batch mean
     assert norm_rel(bn.running_mean.cpu(), 0.1 * mean.cpu()) <= 1e-4
+
+
+# ---------------------------------------------------------------- bf16 MFMA (config 4)
+def _to64(d):
+    return {k: (v.double() if v.is_floating_point() else v.clone()) for k, v in d.items()}
+
+
+@pytest.mark.parametrize("base,depth", [(64, 3), (128, 5)])
+def test_mod_bf16_matches_bf16_oracle(base, depth):
+    """mfma_dtype="bf16": one step at B=2 64x64 vs the oracle that rounds exactly the GEMM
+    operands the HIP bf16 kernels round (oracle/mod_ref_cpu.py, bf16=True).
+
+    Rounding to bf16 is discontinuous: a 1e-7 difference upstream moves an operand across a
+    rounding boundary with probability ~1e-5 per element, and the flips compound through
+    BN.  The oracle itself shows it: evaluated in fp32 and in fp64 (same bf16 roundings of
+    its own values) it differs by ~6e-3 in the logits and up to ~15 % on small BN-bias
+    gradients.  The bar is 2x that spread of the oracle against itself."""
+    import unet_hip
+    P = MO.make_params(42, base, depth)
+    x, t = inputs(5, 2, 64, 64)
+    ref = MO.train_step(P, MO.init_buffers(base, depth), None, x, t, depth=depth, bf16=True)
+    r64 = MO.train_step(_to64(P), _to64(MO.init_buffers(base, depth)), None, x.double(),
+                        t.double(), depth=depth, bf16=True)
+    ref32 = MO.train_step(P, MO.init_buffers(base, depth), None, x, t, depth=depth)
+    m = unet_hip.ModUNet(1, 1, base_filters=base, depth=depth, mfma_dtype="bf16")
+    sd = m.state_dict()
+    for k, v in P.items():
+        sd[k] = v.clone()
+    m.load_state_dict(sd)
+    m = m.to(DEV).train()
+    logits = m(x.to(DEV))
+    losses = unet_hip.seg_losses(logits, t.to(DEV))
+    (losses[0] + losses[1]).backward()
+    lg = logits.detach().cpu().numpy()
+    spread_l = rel_max(ref["logits"].numpy(), r64["logits"].numpy())
+    e_l = rel_max(lg, ref["logits"].numpy())
+    e_l32 = rel_max(lg, ref32["logits"].numpy())
+    spread = {k: norm_rel(ref["grads"][k], r64["grads"][k]) for k in ref["grads"]}
+    errs = grad_errors(m, ref["grads"])
+    worst = max(errs, key=errs.get)
+    env = 2 * max(spread.values())
+    print(f"bf16 base {base} depth {depth}: logits vs bf16 oracle {e_l:.2e} (oracle spread "
+          f"{spread_l:.2e}), vs fp32 oracle {e_l32:.2e}; worst grad {worst} {errs[worst]:.2e} "
+          f"(envelope {env:.2e})")
+    assert e_l <= 2 * spread_l + 1e-4
+    assert abs((losses[0] + losses[1]).item() - ref["loss"].item()) <= 1e-3
+    assert errs[worst] <= env, f"{worst}: {errs[worst]:.3e}"
+    # and bf16 stays a bf16-sized perturbation of the fp32 network
+    assert e_l32 <= 5e-2

@@ -213,3 +213,13 @@ def test_mod_state_dict_and_rng_like_reference():
     b = unet_hip.ModUNet(1, 1, base_filters=64, depth=3)
     for (na, pa), (nb, pb) in zip(a.state_dict().items(), b.state_dict().items()):
         assert na == nb and torch.equal(pa, pb), na
+
+
+def test_bf16_math_only_for_mod_variant():
+    from unet_hip import _lib
+    from unet_hip.runtime import UNetRuntime
+    with pytest.raises(_lib.HipError):
+        UNetRuntime("cuda:0", 1, 1, _lib.VARIANT_MODEL, 0, 0, _lib.MATH_BF16)
+    a = UNetRuntime("cuda:0", 1, 1, _lib.VARIANT_MOD, 128, 5, _lib.MATH_BF16)
+    b = _mod_rt(128, 5)
+    assert a.params == b.params and a.bn == b.bn and a.buckets == b.buckets

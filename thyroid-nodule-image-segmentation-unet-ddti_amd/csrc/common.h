@@ -48,8 +48,9 @@ struct RowGemmArgs {
     int lda, aoff, C, amode;
     const float* ascale;  // per-channel affine applied to valid A values (BN fused in the
     const float* ashift;  // consumer's prologue); null = identity
-    int arelu;            // OP_AFFINE: ReLU after the affine on channels [0, arelu)
-    const float* bt;      // B^T, row-major [N][K]
+    int arelu;            // OP_AFFINE_RELU: ReLU after the affine on channels [0, arelu)
+    const float* bt;      // B^T, row-major [N][K] (f32 MFMA)
+    const uint16_t* bt16; // or: B^T as bf16 (bf16 MFMA, f32 accumulate); exactly one is set
     float* out;
     int ldo, ooff;
     const float* bias;
@@ -83,6 +84,7 @@ struct WgradArgs {
     int ldby, offby;
     const float* bcoef;
     float* bias_slab;    // optional [splits][Nw]: column sums of B' (the bias gradient)
+    int bf16;            // bf16 MFMA (operands rounded to bf16 in LDS, f32 accumulate)
 };
 
 #define HIP_OK(x)                                   \
@@ -100,3 +102,6 @@ int rowgemm_tile_dbuf(int tile);
 // 2 = 128x64 two waves, 3 = 64x128 two waves, 4 = 64x64 four waves, 5 = 128x64 four waves
 int launch_wgrad(const WgradArgs& a, int tile, hipStream_t s);
 int wgrad_tile_dims(int tile, int* bm, int* bn, int* bkp);
+// bf16 wgrad tile ids (a.bf16): 0 = 128x128/32 px, 1 = 128x128/64, 2 = 64x64/64,
+// 3 = 128x64/64, 4 = 64x128/64
+int wgrad16_tile_dims(int tile, int* bm, int* bn, int* bkp);

@@ -31,6 +31,19 @@ __device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
 
+// bf16 operands (BF kernels): 8 bf16 per lane, k = 8 * (lane >> 5) + j
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x16 mfma32_bf16(bf16x8 a, bf16x8 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// f32x4 -> 4 bf16 (round to nearest even; v_cvt_pk_bf16_f32)
+__device__ __forceinline__ bf16x4 to_bf16x4(f32x4 v) {
+    return bf16x4{(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+}
+
 struct Pix {
     int img, y, x;
 };
@@ -97,7 +110,11 @@ struct RowTile {
     static constexpr int THREADS = 64 * WAVES;
 };
 
-template <int AMODE, int AOP, int EMODE, class T>
+// BF: bf16 MFMA (v_mfma_f32_32x32x16_bf16, f32 accumulate).  A is still gathered as f32
+// (activations stay f32 in HBM) and rounded to bf16 when it is written to LDS; Bt is a bf16
+// weight image (p.bt16).  LDS rows are K-contiguous bf16 with an 8-element pad (80 B /
+// 144 B row stride: the 16 lanes of a ds_read_b128 phase hit disjoint banks).
+template <int AMODE, int AOP, int EMODE, class T, bool BF>
 __global__ __launch_bounds__(T::THREADS, 1) void rowgemm_kernel(RowGemmArgs p) {
     constexpr bool AFFINE = AOP == OP_AFFINE || AOP == OP_AFFINE_RELU, ADZ = AOP == OP_DZ;
     constexpr bool ARELU = AOP == OP_AFFINE_RELU;
@@ -106,14 +123,18 @@ __global__ __launch_bounds__(T::THREADS, 1) void rowgemm_kernel(RowGemmArgs p) {
     constexpr int NTH = T::THREADS;
     constexpr int WAVES_N = BN / WN, WAVES_M = BM / WM;
     constexpr int NBUF = DBUF ? 2 : 1;
-    constexpr int LDK = BK + 4;          // 16-B pad: conflict-free ds_read_b128
+    constexpr int LDK = BF ? BK + 8 : BK + 4;  // row stride in elements (bf16 or f32)
     constexpr int MT = WM / 32, NT = WN / 32;
     constexpr int F4R = BK / 4;
     constexpr int RPP = NTH / F4R;
-    constexpr int AP = BM / RPP, BP = BN / RPP;
-    static_assert(AP * RPP == BM && BP * RPP == BN, "loader shape");
-    constexpr int IMG = (BM + BN) * LDK;
-    __shared__ __attribute__((aligned(16))) float smem[NBUF * IMG];
+    constexpr int AP = BM / RPP, BP = BF ? 1 : BN / RPP;
+    static_assert(AP * RPP == BM && (BF || BP * RPP == BN), "loader shape");
+    constexpr int F8R = BK / 8, RPP8 = NTH / F8R;  // bf16 B image: 8 elements per lane
+    constexpr int BP8 = BF ? BN / RPP8 : 1;
+    static_assert(!BF || BP8 * RPP8 == BN, "bf16 B loader shape");
+    constexpr int IMG = (BM + BN) * LDK;  // elements per LDS image
+    constexpr int SMEM_F = BF ? (NBUF * IMG + 1) / 2 : NBUF * IMG;
+    __shared__ __attribute__((aligned(16))) float smem[SMEM_F];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave / WAVES_N, wn = wave % WAVES_N;
@@ -135,9 +156,11 @@ __global__ __launch_bounds__(T::THREADS, 1) void rowgemm_kernel(RowGemmArgs p) {
     }
 
     f32x4 ra[AP], rb[BP], rsc, rsh, rcc;
+    uint4 rb8[BP8];
     f32x4 ry[ADZ ? AP : 1];
     unsigned vmask = 0;
     bool rrelu = false;
+    const int brow8 = tid / F8R, bc8 = tid % F8R;
 
     auto issue = [&](int kc) {
         const int k0 = kc * BK;
@@ -162,13 +185,21 @@ __global__ __launch_bounds__(T::THREADS, 1) void rowgemm_kernel(RowGemmArgs p) {
             ra[i] = *(const f32x4*)(p.a + (size_t)src * p.lda + p.aoff + c);
             if constexpr (ADZ) ry[i] = *(const f32x4*)(p.ay + (size_t)src * p.lday + p.offay + c);
         }
+        if constexpr (BF) {
 #pragma unroll
-        for (int i = 0; i < BP; ++i)
-            rb[i] = *(const f32x4*)(p.bt + (size_t)(n0 + lrow + i * RPP) * p.K + k0 + lc4 * 4);
+            for (int i = 0; i < BP8; ++i)
+                rb8[i] = *(const uint4*)(p.bt16 + (size_t)(n0 + brow8 + i * RPP8) * p.K + k0 + bc8 * 8);
+        } else {
+#pragma unroll
+            for (int i = 0; i < BP; ++i)
+                rb[i] = *(const f32x4*)(p.bt + (size_t)(n0 + lrow + i * RPP) * p.K + k0 + lc4 * 4);
+        }
     };
     auto commit = [&](int buf) {
         float* as = smem + buf * IMG;
         float* bs = as + BM * LDK;
+        __bf16* as16 = (__bf16*)smem + buf * IMG;
+        __bf16* bs16 = as16 + BM * LDK;
 #pragma unroll
         for (int i = 0; i < AP; ++i) {
             f32x4 v = ra[i];
@@ -184,10 +215,18 @@ __global__ __launch_bounds__(T::THREADS, 1) void rowgemm_kernel(RowGemmArgs p) {
                 for (int j = 0; j < 4; ++j) v[j] = ry[i][j] > 0.f ? d[j] : 0.f;
             }
             if (!((vmask >> i) & 1u)) v = f32x4{0.f, 0.f, 0.f, 0.f};
-            *(f32x4*)&as[(lrow + i * RPP) * LDK + lc4 * 4] = v;
+            if constexpr (BF)
+                *(bf16x4*)&as16[(lrow + i * RPP) * LDK + lc4 * 4] = to_bf16x4(v);
+            else
+                *(f32x4*)&as[(lrow + i * RPP) * LDK + lc4 * 4] = v;
         }
+        if constexpr (BF) {
 #pragma unroll
-        for (int i = 0; i < BP; ++i) *(f32x4*)&bs[(lrow + i * RPP) * LDK + lc4 * 4] = rb[i];
+            for (int i = 0; i < BP8; ++i) *(uint4*)&bs16[(brow8 + i * RPP8) * LDK + bc8 * 8] = rb8[i];
+        } else {
+#pragma unroll
+            for (int i = 0; i < BP; ++i) *(f32x4*)&bs[(lrow + i * RPP) * LDK + lc4 * 4] = rb[i];
+        }
     };
 
     f32x16 acc[MT][NT];
@@ -206,24 +245,44 @@ __global__ __launch_bounds__(T::THREADS, 1) void rowgemm_kernel(RowGemmArgs p) {
     for (int kc = 0; kc < nk; ++kc) {
         const int cur = DBUF ? (kc & 1) : 0;
         if (kc + 1 < nk) issue(kc + 1);
-        const float* as = smem + cur * IMG;
-        const float* bs = as + BM * LDK;
+        if constexpr (BF) {
+            const __bf16* as16 = (const __bf16*)smem + cur * IMG;
+            const __bf16* bs16 = as16 + BM * LDK;
 #pragma unroll
-        for (int kk = 0; kk < BK / 8; ++kk) {
-            f32x4 af[MT], bf[NT];
+            for (int kk = 0; kk < BK / 16; ++kk) {
+                bf16x8 af[MT], bf[NT];
 #pragma unroll
-            for (int mt = 0; mt < MT; ++mt)
-                af[mt] = *(const f32x4*)&as[(wm * WM + mt * 32 + li) * LDK + kk * 8 + lh * 4];
+                for (int mt = 0; mt < MT; ++mt)
+                    af[mt] = *(const bf16x8*)&as16[(wm * WM + mt * 32 + li) * LDK + kk * 16 + lh * 8];
 #pragma unroll
-            for (int nt = 0; nt < NT; ++nt)
-                bf[nt] = *(const f32x4*)&bs[(wn * WN + nt * 32 + li) * LDK + kk * 8 + lh * 4];
-#pragma unroll
-            for (int s = 0; s < 4; ++s)
+                for (int nt = 0; nt < NT; ++nt)
+                    bf[nt] = *(const bf16x8*)&bs16[(wn * WN + nt * 32 + li) * LDK + kk * 16 + lh * 8];
 #pragma unroll
                 for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
                     for (int nt = 0; nt < NT; ++nt)
-                        acc[mt][nt] = mfma32(af[mt][s], bf[nt][s], acc[mt][nt]);
+                        acc[mt][nt] = mfma32_bf16(af[mt], bf[nt], acc[mt][nt]);
+            }
+        } else {
+            const float* as = smem + cur * IMG;
+            const float* bs = as + BM * LDK;
+#pragma unroll
+            for (int kk = 0; kk < BK / 8; ++kk) {
+                f32x4 af[MT], bf[NT];
+#pragma unroll
+                for (int mt = 0; mt < MT; ++mt)
+                    af[mt] = *(const f32x4*)&as[(wm * WM + mt * 32 + li) * LDK + kk * 8 + lh * 4];
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt)
+                    bf[nt] = *(const f32x4*)&bs[(wn * WN + nt * 32 + li) * LDK + kk * 8 + lh * 4];
+#pragma unroll
+                for (int s = 0; s < 4; ++s)
+#pragma unroll
+                    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                        for (int nt = 0; nt < NT; ++nt)
+                            acc[mt][nt] = mfma32(af[mt][s], bf[nt][s], acc[mt][nt]);
+            }
         }
         if constexpr (DBUF) {
             // the other image was last read in iteration kc-1, which every wave finished
@@ -552,6 +611,198 @@ __global__ __launch_bounds__(T::THREADS, 1) void wgrad_kernel(WgradArgs p) {
             }
 }
 
+// ------------------------------------------------------------------------------------
+// Weight-gradient GEMM on bf16 MFMA.  The MFMA operands need 8 consecutive PIXELS of one
+// channel per lane, so the loader works on 4-pixel x 4-channel units: four f32x4 loads (one
+// per pixel), the BN affine / ReLU / padding applied in f32, then a register transpose into
+// four 8-B rows of channel-major, pixel-contiguous bf16 LDS images ([BM][BKP+8] and
+// [BN][BKP+8]).  Bias column sums of B' are taken from the f32 values.
+// ------------------------------------------------------------------------------------
+template <int AMODE, int AOP, int BMODE, class T>
+__global__ __launch_bounds__(T::THREADS, 1) void wgrad16_kernel(WgradArgs p) {
+    constexpr bool AFFINE = AOP == OP_AFFINE || AOP == OP_AFFINE_RELU;
+    constexpr bool ARELU = AOP == OP_AFFINE_RELU;
+    constexpr int BM = T::BM, BN = T::BN, BKP = T::BKP, WM = T::WM, WN = T::WN;
+    constexpr int NTH = T::THREADS;
+    constexpr int WAVES_N = BN / WN;
+    constexpr int LDP = BKP + 8;                      // bf16 per LDS row (pixels)
+    constexpr int MT = WM / 32, NT = WN / 32;
+    constexpr int AQ = BM / 4, BQ = BN / 4;           // channel quads
+    constexpr int APQ = NTH / AQ, BPQ = NTH / BQ;     // pixel quads per pass
+    constexpr int AP = (BKP / 4) / APQ, BP = (BKP / 4) / BPQ;
+    static_assert(AP * APQ == BKP / 4 && BP * BPQ == BKP / 4 && AP >= 1 && BP >= 1, "loader");
+    constexpr int SMEM_F = ((BM + BN) * LDP + 1) / 2 > 8 * NTH ? ((BM + BN) * LDP + 1) / 2 : 8 * NTH;
+    __shared__ __attribute__((aligned(16))) float smem[SMEM_F];
+    __bf16* As = (__bf16*)smem;
+    __bf16* Bs = As + BM * LDP;
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+    const int tiles_n = p.Nw / BN, tiles_m = p.Mw / BM;
+    int idx = blockIdx.x;
+    const int tn = idx % tiles_n;
+    idx /= tiles_n;
+    const int tm = idx % tiles_m;
+    const int split = idx / tiles_m;
+    const int tapA = (tm * BM) / p.CA, ca0 = tm * BM - tapA * p.CA;
+    const int tapB = (tn * BN) / p.CB, cb0 = tn * BN - tapB * p.CB;
+    const int H = p.H, W = p.W;
+    const float rH = 1.f / (float)H, rW = 1.f / (float)W;
+
+    const int aq = tid % AQ, apq = tid / AQ;
+    const int bq = tid % BQ, bpq = tid / BQ;
+    f32x4 sc = {1.f, 1.f, 1.f, 1.f}, sh = {0.f, 0.f, 0.f, 0.f};
+    bool arl = false;
+    if constexpr (AFFINE) {
+        sc = *(const f32x4*)(p.ascale + ca0 + aq * 4);
+        sh = *(const f32x4*)(p.ashift + ca0 + aq * 4);
+        if constexpr (ARELU) arl = ca0 + aq * 4 < p.arelu;
+    }
+    const bool bsum = p.bias_slab != nullptr && tm == 0;
+    double bacc[4] = {0.0, 0.0, 0.0, 0.0};
+
+    const int pbeg = split * p.pps;
+    int pend = pbeg + p.pps;
+    if (pend > p.P) pend = p.P;
+    const int nchunks = (pend - pbeg + BKP - 1) / BKP;
+
+    f32x4 ra[AP][4], rb[BP][4];
+    unsigned amask = 0, bmask = 0;
+    auto issue = [&](int pc) {
+        amask = bmask = 0;
+#pragma unroll
+        for (int i = 0; i < AP; ++i)
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                int m = pc + 4 * (apq + i * APQ) + u;
+                const bool in = m < pend;
+                m = in ? m : pend - 1;
+                bool valid;
+                const Pix q = AMODE == G_IDENT ? Pix{0, 0, 0} : decode_fast(m, H, W, rH, rW);
+                const int src = gather_src<AMODE>(tapA, m, q, H, W, valid);
+                amask |= (valid && in) ? (1u << (4 * i + u)) : 0u;
+                ra[i][u] = *(const f32x4*)(p.a + (size_t)src * p.lda + p.aoff + ca0 + aq * 4);
+            }
+#pragma unroll
+        for (int i = 0; i < BP; ++i)
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                int m = pc + 4 * (bpq + i * BPQ) + u;
+                const bool in = m < pend;
+                m = in ? m : pend - 1;
+                bool valid;
+                const Pix q = BMODE == G_IDENT ? Pix{0, 0, 0} : decode_fast(m, H, W, rH, rW);
+                const int src = gather_src<BMODE>(tapB, m, q, H, W, valid);
+                bmask |= (valid && in) ? (1u << (4 * i + u)) : 0u;
+                rb[i][u] = *(const f32x4*)(p.b + (size_t)src * p.ldb + p.boff + cb0 + bq * 4);
+            }
+    };
+    auto commit = [&]() {
+#pragma unroll
+        for (int i = 0; i < AP; ++i) {
+            f32x4 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                v[u] = ra[i][u];
+                if constexpr (AFFINE) {
+                    v[u] = v[u] * sc + sh;
+                    if (ARELU && arl)
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) v[u][j] = fmaxf(v[u][j], 0.f);
+                }
+                if (!((amask >> (4 * i + u)) & 1u)) v[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+            const int pp = 4 * (apq + i * APQ);
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                *(bf16x4*)&As[(aq * 4 + j) * LDP + pp] =
+                    bf16x4{(__bf16)v[0][j], (__bf16)v[1][j], (__bf16)v[2][j], (__bf16)v[3][j]};
+        }
+#pragma unroll
+        for (int i = 0; i < BP; ++i) {
+            f32x4 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                v[u] = rb[i][u];
+                if (!((bmask >> (4 * i + u)) & 1u)) v[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+                if (bsum)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) bacc[j] += v[u][j];
+            }
+            const int pp = 4 * (bpq + i * BPQ);
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                *(bf16x4*)&Bs[(bq * 4 + j) * LDP + pp] =
+                    bf16x4{(__bf16)v[0][j], (__bf16)v[1][j], (__bf16)v[2][j], (__bf16)v[3][j]};
+        }
+    };
+
+    f32x16 acc[MT][NT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    const int li = lane & 31, lh = lane >> 5;
+    if (nchunks > 0) {
+        issue(pbeg);
+        commit();
+        __syncthreads();
+    }
+    for (int c = 0; c < nchunks; ++c) {
+        if (c + 1 < nchunks) issue(pbeg + (c + 1) * BKP);
+#pragma unroll
+        for (int kk = 0; kk < BKP / 16; ++kk) {
+            bf16x8 af[MT], bf[NT];
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt)
+                af[mt] = *(const bf16x8*)&As[(wm * WM + mt * 32 + li) * LDP + kk * 16 + lh * 8];
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt)
+                bf[nt] = *(const bf16x8*)&Bs[(wn * WN + nt * 32 + li) * LDP + kk * 16 + lh * 8];
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma32_bf16(af[mt], bf[nt], acc[mt][nt]);
+        }
+        __syncthreads();
+        if (c + 1 < nchunks) {
+            commit();
+            __syncthreads();
+        }
+    }
+
+    if (bsum) {  // column sums of B' for the bias gradient: combine the pixel groups in order
+        __syncthreads();
+        double* red = (double*)smem;  // [NTH][4]
+#pragma unroll
+        for (int j = 0; j < 4; ++j) red[tid * 4 + j] = bacc[j];
+        __syncthreads();
+        if (tid < BQ) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                double t = 0.0;
+                for (int g = 0; g < BPQ; ++g) t += red[(g * BQ + tid) * 4 + j];
+                p.bias_slab[(size_t)split * p.Nw + tn * BN + tid * 4 + j] = (float)t;
+            }
+        }
+    }
+
+    float* slab = p.slab + (size_t)split * p.Mw * p.Nw;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = tm * BM + wm * WM + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                const int n = tn * BN + wn * WN + nt * 32 + li;
+                slab[(size_t)m * p.Nw + n] = acc[mt][nt][r];
+            }
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------------------------
@@ -565,22 +816,24 @@ using RowTile2 = RowTile<256, 64, 64, 64, 32, false>;
 using RowTile3 = RowTile<128, 128, 64, 64, 64, false>;
 using RowTile4 = RowTile<128, 128, 64, 64, 32, false>;
 using RowTile5 = RowTile<256, 128, 64, 64, 32, false>;
+using RowTile6 = RowTile<128, 128, 64, 64, 64, true>;  // bf16: 4 MFMA k-steps per barrier
 #define ROWGEMM_TILES(X) \
-    X(0, RowTile0) X(1, RowTile1) X(2, RowTile2) X(3, RowTile3) X(4, RowTile4) X(5, RowTile5)
+    X(0, RowTile0) X(1, RowTile1) X(2, RowTile2) X(3, RowTile3) X(4, RowTile4) X(5, RowTile5) \
+    X(6, RowTile6)
 
-template <int AMODE, int AOP, int EMODE, class T>
+template <int AMODE, int AOP, int EMODE, class T, bool BF>
 static int rowgemm_go(const RowGemmArgs& a, hipStream_t s) {
     if (a.N % T::BN || a.K % T::BK || a.C % T::BK) return -1;
     if (EMODE == E_CONVT && (a.cout % T::BN)) return -1;
     const dim3 grid(((a.M + T::BM - 1) / T::BM) * (a.N / T::BN));
-    hipLaunchKernelGGL((rowgemm_kernel<AMODE, AOP, EMODE, T>), grid, dim3(T::THREADS), 0, s, a);
+    hipLaunchKernelGGL((rowgemm_kernel<AMODE, AOP, EMODE, T, BF>), grid, dim3(T::THREADS), 0, s, a);
     return (int)hipGetLastError();
 }
 
-template <int AMODE, int AOP, int EMODE>
+template <int AMODE, int AOP, int EMODE, bool BF>
 static int rowgemm_tile(const RowGemmArgs& a, int tile, hipStream_t s) {
 #define RG_CASE(id, T) \
-    if (tile == id) return rowgemm_go<AMODE, AOP, EMODE, T>(a, s);
+    if (tile == id) return rowgemm_go<AMODE, AOP, EMODE, T, BF>(a, s);
     ROWGEMM_TILES(RG_CASE)
 #undef RG_CASE
     return -1;
@@ -607,32 +860,45 @@ int rowgemm_tile_dbuf(int tile) {
     return 0;
 }
 
+// BF (bf16 MFMA) is instantiated for the combinations of the BN -> ReLU network
+// (models/mod.py) only; the ReLU -> BN network runs f32.
+template <bool BF>
+static int rowgemm_dispatch(const RowGemmArgs& a, int tile, hipStream_t s) {
+    const bool aff = a.ascale != nullptr, dz = a.acoef != nullptr;
+    if (a.amode == G_CONV3 && a.emode == E_STATS) {  // BN -> ReLU order (models/mod.py)
+        if (a.arelu) return rowgemm_tile<G_CONV3, OP_AFFINE_RELU, E_STATS, BF>(a, tile, s);
+        if (!aff) return rowgemm_tile<G_CONV3, OP_PLAIN, E_STATS, BF>(a, tile, s);
+        return -1;
+    }
+    if (a.amode == G_CONV3 && (a.emode == E_STORE || a.emode == E_STORE_BN) && !dz)
+        return a.emode == E_STORE ? rowgemm_tile<G_CONV3, OP_PLAIN, E_STORE, BF>(a, tile, s)
+                                  : rowgemm_tile<G_CONV3, OP_PLAIN, E_STORE_BN, BF>(a, tile, s);
+    if (a.amode == G_IDENT && a.emode == E_CONVT && aff && a.arelu)
+        return rowgemm_tile<G_IDENT, OP_AFFINE_RELU, E_CONVT, BF>(a, tile, s);
+    if (a.amode == G_UP2 && !aff && !dz && a.emode == E_STORE_BN)
+        return rowgemm_tile<G_UP2, OP_PLAIN, E_STORE_BN, BF>(a, tile, s);
+    if constexpr (!BF) {
+        if (a.amode == G_CONV3 && a.emode == E_BIAS_RELU_STATS)
+            return aff ? rowgemm_tile<G_CONV3, OP_AFFINE, E_BIAS_RELU_STATS, false>(a, tile, s)
+                       : rowgemm_tile<G_CONV3, OP_PLAIN, E_BIAS_RELU_STATS, false>(a, tile, s);
+        if (a.amode == G_CONV3 && a.emode == E_STORE && dz)
+            return rowgemm_tile<G_CONV3, OP_DZ, E_STORE, false>(a, tile, s);
+        if (a.amode == G_CONV3 && a.emode == E_STORE_BN && dz)
+            return rowgemm_tile<G_CONV3, OP_DZ, E_STORE_BN, false>(a, tile, s);
+        if (a.amode == G_IDENT && a.emode == E_CONVT && aff && !a.arelu)
+            return rowgemm_tile<G_IDENT, OP_AFFINE, E_CONVT, false>(a, tile, s);
+    }
+    return -1;  // combination not instantiated
+}
+
 int launch_rowgemm(const RowGemmArgs& a, int tile, hipStream_t s) {
     if (a.M < 1 || a.K != gather_taps(a.amode) * a.C) return -1;
     const bool aff = a.ascale != nullptr, dz = a.acoef != nullptr;
     if (aff && dz) return -1;
     if ((a.emode == E_STORE_BN) != (a.ey != nullptr)) return -1;
     if ((a.escale != nullptr) != (a.eshift != nullptr) || (a.arelu && !aff)) return -1;
-    if (a.amode == G_CONV3 && a.emode == E_STATS) {  // BN -> ReLU order (models/mod.py)
-        if (a.arelu) return rowgemm_tile<G_CONV3, OP_AFFINE_RELU, E_STATS>(a, tile, s);
-        if (!aff) return rowgemm_tile<G_CONV3, OP_PLAIN, E_STATS>(a, tile, s);
-        return -1;
-    }
-    if (a.amode == G_CONV3 && a.emode == E_BIAS_RELU_STATS)
-        return aff ? rowgemm_tile<G_CONV3, OP_AFFINE, E_BIAS_RELU_STATS>(a, tile, s)
-                   : rowgemm_tile<G_CONV3, OP_PLAIN, E_BIAS_RELU_STATS>(a, tile, s);
-    if (a.amode == G_CONV3 && a.emode == E_STORE)
-        return dz ? rowgemm_tile<G_CONV3, OP_DZ, E_STORE>(a, tile, s)
-                  : rowgemm_tile<G_CONV3, OP_PLAIN, E_STORE>(a, tile, s);
-    if (a.amode == G_CONV3 && a.emode == E_STORE_BN)
-        return dz ? rowgemm_tile<G_CONV3, OP_DZ, E_STORE_BN>(a, tile, s)
-                  : rowgemm_tile<G_CONV3, OP_PLAIN, E_STORE_BN>(a, tile, s);
-    if (a.amode == G_IDENT && a.emode == E_CONVT && aff)
-        return a.arelu ? rowgemm_tile<G_IDENT, OP_AFFINE_RELU, E_CONVT>(a, tile, s)
-                       : rowgemm_tile<G_IDENT, OP_AFFINE, E_CONVT>(a, tile, s);
-    if (a.amode == G_UP2 && !aff && !dz && a.emode == E_STORE_BN)
-        return rowgemm_tile<G_UP2, OP_PLAIN, E_STORE_BN>(a, tile, s);
-    return -1;  // combination not instantiated
+    if ((a.bt != nullptr) == (a.bt16 != nullptr)) return -1;  // exactly one weight image
+    return a.bt16 ? rowgemm_dispatch<true>(a, tile, s) : rowgemm_dispatch<false>(a, tile, s);
 }
 
 // wgrad tiles: (BM, BN, pixels per chunk).  Narrow tiles take deeper pixel chunks so the
@@ -674,8 +940,55 @@ static int wgrad_tile(const WgradArgs& a, int tile, hipStream_t s) {
     return -1;
 }
 
+// bf16 wgrad tiles (wgrad16_kernel): 4-pixel x 4-channel loader units
+using Wg16Tile0 = WgTile<128, 128, 64, 64, 32>;
+using Wg16Tile1 = WgTile<128, 128, 64, 64, 64>;
+using Wg16Tile2 = WgTile<64, 64, 32, 32, 64>;
+using Wg16Tile3 = WgTile<128, 64, 64, 32, 64>;
+using Wg16Tile4 = WgTile<64, 128, 32, 64, 64>;
+#define WGRAD16_TILES(X) \
+    X(0, Wg16Tile0) X(1, Wg16Tile1) X(2, Wg16Tile2) X(3, Wg16Tile3) X(4, Wg16Tile4)
+
+int wgrad16_tile_dims(int tile, int* bm, int* bn, int* bkp) {
+#define WG16_DIMS(id, T) \
+    if (tile == id) {    \
+        *bm = T::BM;     \
+        *bn = T::BN;     \
+        *bkp = T::BKP;   \
+        return 0;        \
+    }
+    WGRAD16_TILES(WG16_DIMS)
+#undef WG16_DIMS
+    return -1;
+}
+
+template <int AMODE, int AOP, int BMODE>
+static int wgrad16_tile(const WgradArgs& a, int tile, hipStream_t s) {
+#define WG16_CASE(id, T)                                                                      \
+    if (tile == id) {                                                                         \
+        if (a.Mw % T::BM || a.Nw % T::BN || a.CA % T::BM || a.CB % T::BN || a.pps % T::BKP) \
+            return -1;                                                                        \
+        const dim3 grid((a.Mw / T::BM) * (a.Nw / T::BN) * a.splits);                          \
+        hipLaunchKernelGGL((wgrad16_kernel<AMODE, AOP, BMODE, T>), grid, dim3(T::THREADS), 0, s, a); \
+        return (int)hipGetLastError();                                                        \
+    }
+    WGRAD16_TILES(WG16_CASE)
+#undef WG16_CASE
+    return -1;
+}
+
 int launch_wgrad(const WgradArgs& a, int tile, hipStream_t s) {
     if (a.P < 1) return -1;
+    if (a.bf16) {  // BN -> ReLU network only (no OP_DZ loaders)
+        const bool aff = a.ascale != nullptr;
+        if (a.bcoef || (a.arelu && !aff) || (aff && !a.arelu)) return -1;
+        if (a.amode == G_CONV3 && a.bmode == G_IDENT)
+            return aff ? wgrad16_tile<G_CONV3, OP_AFFINE_RELU, G_IDENT>(a, tile, s)
+                       : wgrad16_tile<G_CONV3, OP_PLAIN, G_IDENT>(a, tile, s);
+        if (a.amode == G_IDENT && a.bmode == G_UP2 && aff)
+            return wgrad16_tile<G_IDENT, OP_AFFINE_RELU, G_UP2>(a, tile, s);
+        return -1;
+    }
     const bool aff = a.ascale != nullptr, dz = a.bcoef != nullptr;
     if (a.arelu && !aff) return -1;
     if (a.arelu && dz) return -1;  // OP_DZ loaders are the ReLU -> BN order only

@@ -4,6 +4,9 @@
 
 int k_pack_conv3(const float* w, float* wf, float* wd, int cin, int cout, hipStream_t s);
 int k_pack_convT(const float* w, float* tf, float* td, int cin, int cout, hipStream_t s);
+// bf16 weight images (round to nearest even) for the bf16-MFMA GEMMs
+int k_pack_conv3_bf16(const float* w, uint16_t* wf, uint16_t* wd, int cin, int cout, hipStream_t s);
+int k_pack_convT_bf16(const float* w, uint16_t* tf, uint16_t* td, int cin, int cout, hipStream_t s);
 // conv_first: relu = ReLU after (+bias) (model.py order); b may be null (mod.py, bias-free).
 // wgrad: mask = dz masked by [y > 0] (ReLU before the BN, model.py order); gb may be null.
 int k_conv_first_fwd(const float* x, const float* w, const float* b, float* y, int P, int H, int W,

@@ -17,29 +17,32 @@ namespace {
 //   fwd  : Tf[(ab*Cout+co)][ci]
 //   dgrad: Td[ci][ab*Cout+co]
 // -------------------------------------------------------------------------------------
-__global__ void pack_conv3_kernel(const float* __restrict__ w, float* __restrict__ wf,
-                                  float* __restrict__ wd, int cin, int cout) {
+// OUT = float (f32 MFMA images) or __bf16 (bf16 MFMA images, round to nearest even)
+template <class OUT>
+__global__ void pack_conv3_kernel(const float* __restrict__ w, OUT* __restrict__ wf,
+                                  OUT* __restrict__ wd, int cin, int cout) {
     const int64_t n = (int64_t)cin * cout * 9;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * blockDim.x) {
         const int tap = (int)(i % 9);
         const int64_t t = i / 9;
         const int ci = (int)(t % cin), co = (int)(t / cin);
-        const float v = w[i];
+        const OUT v = (OUT)w[i];
         wf[((int64_t)co * 9 + tap) * cin + ci] = v;
         if (wd) wd[((int64_t)ci * 9 + (8 - tap)) * cout + co] = v;
     }
 }
 
-__global__ void pack_convT_kernel(const float* __restrict__ w, float* __restrict__ tf,
-                                  float* __restrict__ td, int cin, int cout) {
+template <class OUT>
+__global__ void pack_convT_kernel(const float* __restrict__ w, OUT* __restrict__ tf,
+                                  OUT* __restrict__ td, int cin, int cout) {
     const int64_t n = (int64_t)cin * cout * 4;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * blockDim.x) {
         const int ab = (int)(i & 3);
         const int64_t t = i >> 2;
         const int co = (int)(t % cout), ci = (int)(t / cout);
-        const float v = w[i];
+        const OUT v = (OUT)w[i];
         tf[((int64_t)ab * cout + co) * cin + ci] = v;
         if (td) td[(int64_t)ci * 4 * cout + ab * cout + co] = v;
     }
@@ -795,12 +798,26 @@ inline int grid_for(int64_t n, int block = 256, int cap = 8192) {
 
 int k_pack_conv3(const float* w, float* wf, float* wd, int cin, int cout, hipStream_t s) {
     const int64_t n = (int64_t)cin * cout * 9;
-    hipLaunchKernelGGL(pack_conv3_kernel, dim3(grid_for(n)), dim3(256), 0, s, w, wf, wd, cin, cout);
+    hipLaunchKernelGGL(pack_conv3_kernel<float>, dim3(grid_for(n)), dim3(256), 0, s, w, wf, wd, cin,
+                       cout);
+    LAUNCH_CHECK();
+}
+int k_pack_conv3_bf16(const float* w, uint16_t* wf, uint16_t* wd, int cin, int cout, hipStream_t s) {
+    const int64_t n = (int64_t)cin * cout * 9;
+    hipLaunchKernelGGL(pack_conv3_kernel<__bf16>, dim3(grid_for(n)), dim3(256), 0, s, w,
+                       (__bf16*)wf, (__bf16*)wd, cin, cout);
     LAUNCH_CHECK();
 }
 int k_pack_convT(const float* w, float* tf, float* td, int cin, int cout, hipStream_t s) {
     const int64_t n = (int64_t)cin * cout * 4;
-    hipLaunchKernelGGL(pack_convT_kernel, dim3(grid_for(n)), dim3(256), 0, s, w, tf, td, cin, cout);
+    hipLaunchKernelGGL(pack_convT_kernel<float>, dim3(grid_for(n)), dim3(256), 0, s, w, tf, td, cin,
+                       cout);
+    LAUNCH_CHECK();
+}
+int k_pack_convT_bf16(const float* w, uint16_t* tf, uint16_t* td, int cin, int cout, hipStream_t s) {
+    const int64_t n = (int64_t)cin * cout * 4;
+    hipLaunchKernelGGL(pack_convT_kernel<__bf16>, dim3(grid_for(n)), dim3(256), 0, s, w,
+                       (__bf16*)tf, (__bf16*)td, cin, cout);
     LAUNCH_CHECK();
 }
 int k_conv_first_fwd(const float* x, const float* w, const float* b, float* y, int P, int H, int W,

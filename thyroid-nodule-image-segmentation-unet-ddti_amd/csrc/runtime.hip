@@ -74,6 +74,7 @@ struct unet_ctx {
     int base = 64, depth = 4;
     bool bn_relu = false;    // BN -> ReLU (mod.py) instead of ReLU -> BN (model.py)
     bool skip_first = false; // concat [skip, up] (mod.py) instead of [up, skip] (model.py)
+    bool bf16 = false;       // conv GEMMs on bf16 MFMA (f32 accumulate), BASELINE config 4
     std::vector<ParamT> params;
     int64_t n_param_floats = 0;
     std::vector<ConvL> conv;
@@ -308,22 +309,29 @@ struct WgradCfg {
 
 // wgrad tile (kernels_gemm.hip WGRAD_TILES) + split-K over pixels so that every layer
 // launches >= 2048 blocks; UNET_WGRAD_TILE_{W,N} override (tuning runs).
-WgradCfg wgrad_cfg(int CA, int tapsA, int CB, int tapsB, int64_t P) {
-    static int tw = -2, tn = -2;
+WgradCfg wgrad_cfg(int CA, int tapsA, int CB, int tapsB, int64_t P, bool bf16) {
+    static int tw = -2, tn = -2, t16 = -2;
     if (tw == -2) {
         const char* e = getenv("UNET_WGRAD_TILE_W");
         tw = e ? atoi(e) : 0;
         e = getenv("UNET_WGRAD_TILE_N");
         tn = e ? atoi(e) : 4;
+        e = getenv("UNET_WGRAD16_TILE");
+        t16 = e ? atoi(e) : 0;
     }
     WgradCfg w;
-    if (CA % 128 == 0 && CB % 128 == 0)
-        w.tile = tw;
-    else if (CA % 64 == 0 && CB % 64 == 0 && (CA % 128 || CB % 128) && tn >= 0)
-        w.tile = (CA % 128 == 0) ? 5 : (CB % 128 == 0 ? 3 : tn);
-    else
-        w.tile = 4;
-    wgrad_tile_dims(w.tile, &w.bm, &w.bn, &w.bkp);
+    if (bf16) {  // kernels_gemm.hip WGRAD16_TILES
+        w.tile = (CA % 128 == 0 && CB % 128 == 0) ? t16 : CA % 128 == 0 ? 3 : CB % 128 == 0 ? 4 : 2;
+        wgrad16_tile_dims(w.tile, &w.bm, &w.bn, &w.bkp);
+    } else {
+        if (CA % 128 == 0 && CB % 128 == 0)
+            w.tile = tw;
+        else if (CA % 64 == 0 && CB % 64 == 0 && (CA % 128 || CB % 128) && tn >= 0)
+            w.tile = (CA % 128 == 0) ? 5 : (CB % 128 == 0 ? 3 : tn);
+        else
+            w.tile = 4;
+        wgrad_tile_dims(w.tile, &w.bm, &w.bn, &w.bkp);
+    }
     const int64_t tiles = (int64_t)(tapsA * CA / w.bm) * (tapsB * CB / w.bn);
     int64_t s = (2048 + tiles - 1) / tiles;
     const int64_t maxs = P / (8 * w.bkp) > 0 ? P / (8 * w.bkp) : 1;  // >= 8 chunks per split
@@ -403,12 +411,12 @@ void make_plan(unet_ctx* c, int N, int H, int W, bool training, char* base, Plan
         int64_t smax = 0, bmax = 0;
         for (int i = 1; i < NC; ++i) {
             const ConvL& L = c->conv[i];
-            WgradCfg w = wgrad_cfg(L.cin, 9, L.cout, 1, p.P[L.level]);
+            WgradCfg w = wgrad_cfg(L.cin, 9, L.cout, 1, p.P[L.level], c->bf16);
             smax = std::max(smax, (int64_t)w.splits * 9 * L.cin * L.cout);
             bmax = std::max(bmax, (int64_t)w.splits * L.cout);
         }
         for (const ConvTL& T : c->convt) {
-            WgradCfg w = wgrad_cfg(T.cin, 1, T.cout, 4, p.P[T.in_level]);
+            WgradCfg w = wgrad_cfg(T.cin, 1, T.cout, 4, p.P[T.in_level], c->bf16);
             smax = std::max(smax, (int64_t)w.splits * T.cin * 4 * T.cout);
             bmax = std::max(bmax, (int64_t)w.splits * 4 * T.cout);
         }
@@ -466,16 +474,22 @@ struct Launcher {
 // UNET_TILE_N128 / UNET_TILE_N64 override the choice (tuning runs).
 // Defaults from tools/gemm_tune (r01): forward-type ops 128x128/BK32 single LDS image
 // (4 waves/SIMD), dgrad-type 128x128 double-buffered, N = 64 outputs 128x64.
-int pick_tile(int N, bool dgrad = false) {
-    static int t128 = -2, t128d = -2, t64 = -2;
+// bf16 MFMA (UNET_TILE16_*): a chunk of 64 K per barrier (4 MFMA k-steps) by default.
+int pick_tile(int N, bool dgrad, bool bf16) {
+    static int t128 = -2, t128d = -2, t64 = -2, b128 = -2, b128d = -2, b64 = -2;
     if (t128 == -2) {
-        const char* e = getenv("UNET_TILE_N128");
-        t128 = e ? atoi(e) : 4;
-        e = getenv("UNET_TILE_N128_DGRAD");
-        t128d = e ? atoi(e) : 0;
-        e = getenv("UNET_TILE_N64");
-        t64 = e ? atoi(e) : 1;
+        auto env = [](const char* n, int d) {
+            const char* e = getenv(n);
+            return e ? atoi(e) : d;
+        };
+        t128 = env("UNET_TILE_N128", 4);
+        t128d = env("UNET_TILE_N128_DGRAD", 0);
+        t64 = env("UNET_TILE_N64", 1);
+        b128 = env("UNET_TILE16_N128", 6);
+        b128d = env("UNET_TILE16_N128_DGRAD", 6);
+        b64 = env("UNET_TILE16_N64", 1);
     }
+    if (bf16) return N % 128 == 0 ? (dgrad ? b128d : b128) : b64;
     return N % 128 == 0 ? (dgrad ? t128d : t128) : t64;
 }
 
@@ -555,6 +569,14 @@ Operand conv_input(unet_ctx* c, Plan& p, int i) {
 
 const float* bias_ptr(const float* prm, int64_t off) { return off >= 0 ? prm + off : nullptr; }
 
+// weight image of a row GEMM: f32, or bf16 packed into the same slot (half its size)
+void set_weights(const unet_ctx* c, RowGemmArgs& g, const float* img) {
+    if (c->bf16)
+        g.bt16 = (const uint16_t*)img;
+    else
+        g.bt = img;
+}
+
 int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, const float* x,
                  float* logits, Plan& p, bool training, hipStream_t s) {
     Launcher L{c, s};
@@ -564,12 +586,23 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
     for (int i = 0; i < NC; ++i) {
         const ConvL& C = c->conv[i];
         if (C.pf < 0) continue;
-        RUN("pack", 0, k_pack_conv3(prm + C.w, p.pack + C.pf, training ? p.pack + C.pd : nullptr,
-                                    C.cin, C.cout, s));
+        if (c->bf16)
+            RUN("pack", 0, k_pack_conv3_bf16(prm + C.w, (uint16_t*)(p.pack + C.pf),
+                                             training ? (uint16_t*)(p.pack + C.pd) : nullptr, C.cin,
+                                             C.cout, s));
+        else
+            RUN("pack", 0, k_pack_conv3(prm + C.w, p.pack + C.pf, training ? p.pack + C.pd : nullptr,
+                                        C.cin, C.cout, s));
     }
-    for (const ConvTL& T : c->convt)
-        RUN("pack", 0, k_pack_convT(prm + T.w, p.pack + T.pf, training ? p.pack + T.pd : nullptr,
-                                    T.cin, T.cout, s));
+    for (const ConvTL& T : c->convt) {
+        if (c->bf16)
+            RUN("pack", 0, k_pack_convT_bf16(prm + T.w, (uint16_t*)(p.pack + T.pf),
+                                             training ? (uint16_t*)(p.pack + T.pd) : nullptr, T.cin,
+                                             T.cout, s));
+        else
+            RUN("pack", 0, k_pack_convT(prm + T.w, p.pack + T.pf, training ? p.pack + T.pd : nullptr,
+                                        T.cin, T.cout, s));
+    }
     // 2. concat affine: identity on the up-sampled half (no BN between ConvT and concat)
     for (int l = 0; l < D; ++l) {
         const int C = c->ch(l), uo = c->up_off(l);
@@ -607,14 +640,14 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
             g.ascale = a.scale;
             g.ashift = a.shift;
             g.arelu = a.relu;
-            g.bt = p.pack + C.pf;
+            set_weights(c, g, p.pack + C.pf);
             g.out = p.y[i];
             g.ldo = p.ldy[i];
             g.ooff = p.offy[i];
             g.bias = bias_ptr(prm, C.b);
             g.stats = p.stats;
             g.emode = c->bn_relu ? E_STATS : E_BIAS_RELU_STATS;
-            const int tile = pick_tile(C.cout);
+            const int tile = pick_tile(C.cout, false, c->bf16);
             int bm, bn, bk;
             rowgemm_tile_dims(tile, &bm, &bn, &bk);
             R = (int)((M + bm - 1) / bm);
@@ -640,14 +673,14 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
         g.ascale = p.scale[src];
         g.ashift = p.shift[src];
         g.arelu = c->bn_relu ? T.cin : 0;
-        g.bt = p.pack + T.pf;
+        set_weights(c, g, p.pack + T.pf);
         g.out = p.cat[lo];
         g.ldo = 2 * c->ch(lo);
         g.ooff = c->up_off(lo);
         g.bias = prm + T.b;
         g.cout = T.cout;
         g.emode = E_CONVT;
-        const int tile = pick_tile(T.cout);
+        const int tile = pick_tile(T.cout, false, c->bf16);
         RUN(tlabel("convT_fwd", tile, 100 + k), 2.0 * g.M * g.N * g.K, launch_rowgemm(g, tile, s));
         return 0;
     };
@@ -732,7 +765,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
                                     p.coef, dz_mask, s));
         const float* dzc = dz_in_loaders ? p.coef : nullptr;
         Operand a = conv_input(c, p, i);
-        WgradCfg wc = wgrad_cfg(C.cin, 9, C.cout, 1, P);
+        WgradCfg wc = wgrad_cfg(C.cin, 9, C.cout, 1, P, c->bf16);
         WgradArgs w{};
         w.H = Hl;
         w.W = Wl;
@@ -760,6 +793,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         w.pps = wc.pps;
         w.splits = wc.splits;
         w.slab = p.slab;
+        w.bf16 = c->bf16;
         RUN(wlabel("conv_wgrad", wc, i), 2.0 * P * C.cout * 9 * C.cin,
             launch_wgrad(w, wc.tile, s));
         RUN("wgrad_reduce", 0,
@@ -782,7 +816,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
             g.lday = p.ldy[i];
             g.offay = p.offy[i];
             g.acoef = dzc;
-            g.bt = p.pack + C.pd;
+            set_weights(c, g, p.pack + C.pd);
             g.out = dx;
             g.ldo = ldx;
             g.ooff = 0;
@@ -798,7 +832,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
                 }
                 g.stats = p.part;
             }
-            const int tile = pick_tile(C.cin, true);
+            const int tile = pick_tile(C.cin, true, c->bf16);
             int bm, bn, bk;
             rowgemm_tile_dims(tile, &bm, &bn, &bk);
             if (rows) *rows = (int)((P + bm - 1) / bm);
@@ -815,7 +849,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         const int ldo = 2 * c->ch(lo), uo = c->up_off(lo);
         const int Hi = H >> T.in_level, Wi = W >> T.in_level;
         const int64_t Pin = p.P[T.in_level];
-        WgradCfg wc = wgrad_cfg(T.cin, 1, T.cout, 4, Pin);
+        WgradCfg wc = wgrad_cfg(T.cin, 1, T.cout, 4, Pin, c->bf16);
         WgradArgs w{};
         w.H = Hi;
         w.W = Wi;
@@ -839,6 +873,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         w.pps = wc.pps;
         w.splits = wc.splits;
         w.slab = p.slab;
+        w.bf16 = c->bf16;
         RUN(wlabel("convT_wgrad", wc, 100 + k), 2.0 * Pin * T.cin * 4 * T.cout,
             launch_wgrad(w, wc.tile, s));
         RUN("wgrad_reduce", 0,
@@ -855,7 +890,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         g.aoff = uo;
         g.C = T.cout;
         g.amode = G_UP2;
-        g.bt = p.pack + T.pd;
+        set_weights(c, g, p.pack + T.pd);
         g.out = dx;
         g.ldo = T.cin;
         g.ooff = 0;
@@ -868,7 +903,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
             g.eshift = p.shift[src];
         }
         g.stats = p.part;
-        const int tile = pick_tile(T.cin, true);
+        const int tile = pick_tile(T.cin, true, c->bf16);
         int bm, bn, bk;
         rowgemm_tile_dims(tile, &bm, &bn, &bk);
         *rows = (int)((Pin + bm - 1) / bm);
@@ -961,6 +996,11 @@ int unet_create(const unet_cfg* cfg, int device, unet_ctx** out) {
         c->in_ch = cfg->in_channels;
         c->out_ch = cfg->out_channels;
         c->variant = cfg->variant;
+        c->bf16 = cfg->math == UNET_MATH_BF16;
+        if (cfg->math != UNET_MATH_F32 && cfg->math != UNET_MATH_BF16) {
+            delete c;
+            return UNET_ERR_UNSUPPORTED;
+        }
         if (c->variant == UNET_VARIANT_MOD) {  // mod.py:13-14 defaults base 64, depth 5
             c->base = cfg->base_filters > 0 ? cfg->base_filters : 64;
             c->depth = cfg->depth > 0 ? cfg->depth : 5;
@@ -981,6 +1021,10 @@ int unet_create(const unet_cfg* cfg, int device, unet_ctx** out) {
     }
     c->bn_relu = c->variant == UNET_VARIANT_MOD;
     c->skip_first = c->bn_relu;
+    if (c->bf16 && !c->bn_relu) {  // bf16 GEMMs are built for models/mod.py (config 4) only
+        delete c;
+        return UNET_ERR_UNSUPPORTED;
+    }
     build_graph(c);
     *out = c;
     return UNET_OK;

@@ -38,11 +38,13 @@ P = ctypes.POINTER
 
 class UnetCfg(ctypes.Structure):
     _fields_ = [("in_channels", c_int), ("out_channels", c_int), ("variant", c_int),
-                ("base_filters", c_int), ("depth", c_int)]
+                ("base_filters", c_int), ("depth", c_int), ("math", c_int)]
 
 
 VARIANT_MODEL = 0  # models/model.py:UNet
 VARIANT_MOD = 1    # models/mod.py:UNet
+MATH_F32 = 0       # conv GEMMs on f32 MFMA (exact f32 products)
+MATH_BF16 = 1      # conv GEMMs on bf16 MFMA, f32 accumulate (BASELINE config 4)
 
 
 # name -> (restype, argtypes); mirrors include/unet_hip.h

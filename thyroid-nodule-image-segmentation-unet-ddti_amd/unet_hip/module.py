@@ -75,7 +75,7 @@ class _HipUNet(nn.Module):
     _name = "UNet"
 
     def _native_cfg(self):
-        """(in_channels, out_channels, variant, base_filters, depth) of the native graph."""
+        """(in_channels, out_channels, variant, base_filters, depth, math) of the native graph."""
         raise NotImplementedError
 
     # ---------------------------------------------------------------- arenas
@@ -184,7 +184,7 @@ class UNet(_HipUNet):
         self._state = None
 
     def _native_cfg(self):
-        return self.in_channels, self.out_channels, _lib.VARIANT_MODEL, 0, 0
+        return self.in_channels, self.out_channels, _lib.VARIANT_MODEL, 0, 0, _lib.MATH_F32
 
 
 def _mod_block(cin, cout):
@@ -199,14 +199,22 @@ class ModUNet(_HipUNet):
     """models/mod.py:9-66 ``UNet(in_channels, out_channels, base_filters, depth)``.
 
     Supported here: in_channels 1, out_channels 1..4, base_filters a multiple of 64
-    (<= 256), depth 1..6 (the native GEMM tiles work on 64-channel multiples)."""
+    (<= 256), depth 1..6 (the native GEMM tiles work on 64-channel multiples).
+
+    ``mfma_dtype``: "fp32" (default; exact f32 products like the reference) or "bf16"
+    (BASELINE config 4: conv GEMM operands rounded to bf16, f32 accumulate; parameters,
+    activations, BN and the optimizer stay f32)."""
 
     _name = "models.mod.UNet"
 
-    def __init__(self, in_channels=1, out_channels=1, base_filters=64, depth=5, **kwargs):
+    def __init__(self, in_channels=1, out_channels=1, base_filters=64, depth=5,
+                 mfma_dtype="fp32", **kwargs):
         super().__init__()
+        if str(mfma_dtype) not in ("fp32", "bf16", "torch.float32", "torch.bfloat16"):
+            raise ValueError(f"mfma_dtype must be 'fp32' or 'bf16', got {mfma_dtype!r}")
         self.in_channels, self.out_channels = in_channels, out_channels
         self.base_filters, self.depth = base_filters, depth
+        self.mfma_dtype = "bf16" if "bf" in str(mfma_dtype) else "fp32"
         # same construction (and RNG consumption) order as mod.py:21-41
         self.encoders = nn.ModuleList()
         self.pools = nn.ModuleList()
@@ -228,4 +236,5 @@ class ModUNet(_HipUNet):
         self._state = None
 
     def _native_cfg(self):
-        return self.in_channels, self.out_channels, _lib.VARIANT_MOD, self.base_filters, self.depth
+        return (self.in_channels, self.out_channels, _lib.VARIANT_MOD, self.base_filters,
+                self.depth, _lib.MATH_BF16 if self.mfma_dtype == "bf16" else _lib.MATH_F32)

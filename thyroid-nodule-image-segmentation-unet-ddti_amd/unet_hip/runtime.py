@@ -16,11 +16,11 @@ _RUNTIMES = {}
 
 class UNetRuntime:
     def __init__(self, device, in_channels=1, out_channels=1, variant=_lib.VARIANT_MODEL,
-                 base_filters=0, depth=0):
+                 base_filters=0, depth=0, math=_lib.MATH_F32):
         lib = _lib.load()
         self.lib = lib
         self.device = torch.device(device)
-        cfg = _lib.UnetCfg(in_channels, out_channels, variant, base_filters, depth)
+        cfg = _lib.UnetCfg(in_channels, out_channels, variant, base_filters, depth, math)
         h = ctypes.c_void_p()
         _lib.check(lib.unet_create(ctypes.byref(cfg), self.device.index or 0, ctypes.byref(h)),
                    None, "unet_create")
@@ -59,11 +59,12 @@ class UNetRuntime:
 
     @staticmethod
     def get(device, in_channels=1, out_channels=1, variant=_lib.VARIANT_MODEL, base_filters=0,
-            depth=0):
-        key = (str(torch.device(device)), in_channels, out_channels, variant, base_filters, depth)
+            depth=0, math=_lib.MATH_F32):
+        key = (str(torch.device(device)), in_channels, out_channels, variant, base_filters, depth,
+               math)
         rt = _RUNTIMES.get(key)
         if rt is None:
-            rt = UNetRuntime(device, in_channels, out_channels, variant, base_filters, depth)
+            rt = UNetRuntime(device, in_channels, out_channels, variant, base_filters, depth, math)
             _RUNTIMES[key] = rt
         return rt
 
