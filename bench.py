@@ -124,10 +124,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # BENCH_DIST_BACKEND=gloo: rehearsal of the N>1 path with several ranks on one GPU
+    # (RCCL refuses two ranks per device); the real runs use "nccl" (= RCCL over xGMI)
+    backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    local = local % ndev if backend != "nccl" and ndev else local
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device(f"cuda:{local}")
     torch.cuda.set_device(dev)
 

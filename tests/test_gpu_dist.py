@@ -1,0 +1,95 @@
+"""The data-parallel product path on a real GPU: two ranks (gloo, both on cuda:0 -- the
+pool's boxes have one GPU, and RCCL refuses two ranks on one device) run the HIP UNet
+through ``unet_hip.dist.DistributedUNet``: parameters broadcast from rank 0, per-rank
+train-mode BN on its shard, the native per-bucket events gating the side-stream
+all-reduce, the 1/world mean folded into HipAdamW.  The averaged gradients must match the
+reference's own nn.DataParallel fixture (tests/golden/unet_dp2_64.npz), and both ranks
+must hold identical parameters after the AdamW step."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(REPO, "thyroid-nodule-image-segmentation-unet-ddti_amd")
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import sys
+    for p in (REPO, PKG, os.path.join(REPO, "tests")):
+        sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import unet_hip
+        from _helpers import hip_model
+        from oracle import unet_ref_cpu as O
+        from oracle import weights as Wt
+        from unet_hip.dist import DistributedUNet
+        dev = torch.device("cuda:0")
+        # rank 1 starts from different weights: the broadcast must replace them
+        m = hip_model(O.make_params(42 if rank == 0 else 7), dev)
+        opt = unet_hip.HipAdamW(m.parameters(), lr=1e-5)
+        ddp = DistributedUNet(m, opt)
+        x = torch.from_numpy(Wt.make_input(3, 4, 1, 64, 64))
+        t = torch.from_numpy(Wt.make_target(3, 4, 64, 64))
+        xs, ts = torch.chunk(x, world)[rank].to(dev), torch.chunk(t, world)[rank].to(dev)
+        opt.zero_grad(set_to_none=True)
+        logits = ddp(xs)
+        losses = unet_hip.seg_losses(logits, ts)
+        (losses[0] + losses[1]).backward()
+        scale = ddp.reduce_gradients()
+        grads = m._state.grad_arena.detach().clone() * scale
+        opt.step()
+        params = m._state.param_arena.detach().clone()
+        loss = (losses[0] + losses[1]).detach().reshape(1).cpu()
+        dist.all_reduce(loss)
+        pd = params.cpu()
+        dist.broadcast(pd, src=0)
+        same = bool(torch.equal(pd, params.cpu()))
+        if rank == 0:
+            rt = m._state.rt
+            norms = [float(grads[off:off + int(np.prod(shape))].double().norm())
+                     for name, shape, off in rt.params]
+            q.put((float(loss) / world, norms, scale, same))
+        else:
+            q.put(("rank1", same))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+def test_dp2_on_gpu_matches_dataparallel_golden(golden_dir):
+    f = np.load(os.path.join(golden_dir, "unet_dp2_64.npz"), allow_pickle=False)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=500), q.get(timeout=500)]
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    r0 = [r for r in res if r[0] != "rank1"][0]
+    r1 = [r for r in res if r[0] == "rank1"][0]
+    loss, norms, scale, same0 = r0
+    assert scale == 0.5
+    assert same0 and r1[1], "ranks diverged after the AdamW step"
+    assert abs(loss - float(f["loss"])) < 1e-5
+    np.testing.assert_allclose(norms, f["grad_norm"], rtol=1e-2)
