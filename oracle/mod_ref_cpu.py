@@ -165,6 +165,98 @@ def train_step(P, B, opt, x, t, depth, w_bce=1.0, w_dice=1.0, shards=1, bf16=Fal
                         forward_fn=make_forward(depth, bf16))
 
 
+# ---------------------------------------------------------------- ResUNet (mod.py:71-131)
+def _res_block_spec(spec, prefix, cin, cout):
+    # ResidualBlock registers `conv` (Sequential) then `skip` (mod.py:73-83)
+    spec.append((f"{prefix}.conv.0.weight", (cout, cin, 3, 3), "conv_w"))
+    spec.append((f"{prefix}.conv.1.weight", (cout,), "bn_w"))
+    spec.append((f"{prefix}.conv.1.bias", (cout,), "bn_b"))
+    spec.append((f"{prefix}.conv.3.weight", (cout, cout, 3, 3), "conv_w"))
+    spec.append((f"{prefix}.conv.4.weight", (cout,), "bn_w"))
+    spec.append((f"{prefix}.conv.4.bias", (cout,), "bn_b"))
+    spec.append((f"{prefix}.skip.weight", (cout, cin, 1, 1), "conv_w"))
+
+
+def res_param_spec(in_channels=1, out_channels=1, base=64, depth=5):
+    """named_parameters() order of mod.py:ResUNet (same layout as UNet, residual blocks)."""
+    spec = []
+    ch = [base * (2 ** i) for i in range(depth)]
+    prev = in_channels
+    for i, c in enumerate(ch):
+        _res_block_spec(spec, f"encoders.{i}", prev, c)
+        prev = c
+    _res_block_spec(spec, "bottleneck", prev, 2 * prev)
+    prev = ch[-1] * 2
+    ups = []
+    for j, c in enumerate(ch[::-1]):
+        ups.append((j, prev, c))
+        prev = c
+    for j, cin, cout in ups:
+        spec.append((f"upconvs.{j}.weight", (cin, cout, 2, 2), "convT_w"))
+        spec.append((f"upconvs.{j}.bias", (cout,), "convT_b", cout * 4))
+    for j, cin, cout in ups:
+        _res_block_spec(spec, f"decoders.{j}", cin, cout)
+    spec.append(("final_conv.weight", (out_channels, base, 1, 1), "conv_w"))
+    spec.append(("final_conv.bias", (out_channels,), "conv_b", base))
+    return spec
+
+
+def res_bn_layers(base=64, depth=5):
+    """[(name, channels)] in named_buffers() order of mod.py:ResUNet."""
+    return [(n[:-2] + ".conv" + n[-2:], c) for n, c in bn_layers(base, depth)]
+
+
+def res_init_buffers(base=64, depth=5):
+    buf = {}
+    for name, c in res_bn_layers(base, depth):
+        buf[f"{name}.running_mean"] = torch.zeros(c)
+        buf[f"{name}.running_var"] = torch.ones(c)
+        buf[f"{name}.num_batches_tracked"] = torch.tensor(0, dtype=torch.long)
+    return buf
+
+
+def res_make_params(seed=42, base=64, depth=5, gamma_lo=0.5, gamma_hi=1.5, in_channels=1,
+                    out_channels=1):
+    p = W.make_params(res_param_spec(in_channels, out_channels, base, depth), seed, gamma_lo,
+                      gamma_hi)
+    return {k: torch.from_numpy(v) for k, v in p.items()}
+
+
+def _res_block(x, P, B, prefix, training):
+    # mod.py:85-86: relu(conv(x) + skip(x)), conv = Conv-BN-ReLU-Conv-BN (mod.py:75-81)
+    y = F.conv2d(x, P[f"{prefix}.conv.0.weight"], None, padding=1)
+    y = F.relu(O._bn(y, P, B, f"{prefix}.conv.1", training))
+    y = F.conv2d(y, P[f"{prefix}.conv.3.weight"], None, padding=1)
+    y = O._bn(y, P, B, f"{prefix}.conv.4", training)
+    return F.relu(y + F.conv2d(x, P[f"{prefix}.skip.weight"]))
+
+
+def make_res_forward(depth):
+    """forward(x, P, B, training) of mod.py:ResUNet (mod.py:112-124)."""
+
+    def forward(x, P, B, training=True):
+        skips = []
+        for i in range(depth):
+            x = _res_block(x, P, B, f"encoders.{i}", training)
+            skips.append(x)
+            x = F.max_pool2d(x, 2, 2)
+        x = _res_block(x, P, B, "bottleneck", training)
+        for j, skip in enumerate(reversed(skips)):
+            x = F.conv_transpose2d(x, P[f"upconvs.{j}.weight"], P[f"upconvs.{j}.bias"], stride=2)
+            if x.shape != skip.shape:
+                x = F.interpolate(x, size=skip.shape[2:], mode="bilinear", align_corners=False)
+            x = torch.cat([skip, x], dim=1)
+            x = _res_block(x, P, B, f"decoders.{j}", training)
+        return F.conv2d(x, P["final_conv.weight"], P["final_conv.bias"])
+
+    return forward
+
+
+def res_train_step(P, B, opt, x, t, depth, w_bce=1.0, w_dice=1.0, shards=1):
+    """utils/trainer.py:81-93 with mod.py:ResUNet (the model main.py:122 builds)."""
+    return O.train_step(P, B, opt, x, t, w_bce, w_dice, shards, forward_fn=make_res_forward(depth))
+
+
 def conv_macs_per_image(H, W, in_channels=1, out_channels=1, base=64, depth=5):
     macs = 0
     prev = in_channels

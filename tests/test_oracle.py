@@ -169,3 +169,30 @@ def test_oracle_mod_config4_arch(golden_dir):
     assert abs(r["loss"].item() - float(f["loss"])) < 1e-6
     _check_grads(_grad_stats(r["grads"], MO.param_spec(1, 1, 128, 5)), f["grad_norm"],
                  f["grad_sum"], f["grad_samp"], rtol=1e-4)
+
+
+def test_oracle_res_d3_two_steps(golden_dir):
+    """models/mod.py ResUNet(base 64, depth 3) -- residual blocks relu(conv(x) + skip(x))."""
+    from oracle import mod_ref_cpu as MO
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    f = _load(golden_dir, "res_d3_64.npz")
+    P = MO.res_make_params(42, 64, 3)
+    B = MO.res_init_buffers(64, 3)
+    opt = O.AdamWState(P, lr=1e-4)
+    x = torch.from_numpy(W.make_input(13, 2, 1, 64, 64))
+    t = torch.from_numpy(W.make_target(13, 2, 64, 64))
+    spec = MO.res_param_spec(1, 1, 64, 3)
+    names = [n for n, _ in MO.res_bn_layers(64, 3)]
+    for s in range(2):
+        p = f"s{s}_"
+        r = MO.res_train_step(P, B, opt, x, t, depth=3)
+        ref = f[p + "logits"]
+        assert np.max(np.abs(r["logits"].numpy() - ref)) <= 1e-5 * np.max(np.abs(ref))
+        assert abs(r["loss"].item() - float(f[p + "loss"])) < 1e-6
+        _check_grads(_grad_stats(r["grads"], spec), f[p + "grad_norm"], f[p + "grad_sum"],
+                     f[p + "grad_samp"], rtol=1e-4)
+        rm = np.concatenate([B[f"{n}.running_mean"].numpy() for n in names])
+        np.testing.assert_allclose(rm, f[p + "running_mean"], rtol=1e-5, atol=1e-6)
+    with torch.no_grad():
+        ev = MO.make_res_forward(3)(x, P, B, training=False).numpy()
+    assert np.max(np.abs(ev - f["eval_logits"])) <= 1e-5 * np.max(np.abs(f["eval_logits"]))

@@ -27,6 +27,8 @@ Fixtures (all float64 statistics computed from fp32 results):
   mod_d3_64.npz     models/mod.py UNet(base 64, depth 3), B=2 1x64x64, 2 AdamW steps
                     (lr 1e-4): full logits, masks, losses, grad norm/sum/samples, param
                     samples, running stats; gamma in [-1, 1] on a second case (neg_*).
+  res_d3_64.npz     models/mod.py ResUNet(base 64, depth 3) (what main.py:122 builds, at
+                    reduced depth), B=2 1x64x64, 2 AdamW steps (lr 1e-4): as mod_d3_64.
   mod_c4_64.npz     models/mod.py UNet(base 128, depth 5) -- the config-4 architecture,
                     497,438,849 params -- at B=2 1x64x64, one step: full logits, losses,
                     grad norm/sum/samples.
@@ -45,6 +47,7 @@ sys.path.insert(0, REF)
 from models.model import UNet as RefUNet  # noqa: E402  (reference)
 from models.loss import DiceLoss as RefDice  # noqa: E402  (reference)
 from models.mod import UNet as RefModUNet  # noqa: E402  (reference, models/mod.py:9-66)
+from models.mod import ResUNet as RefResUNet  # noqa: E402  (reference, models/mod.py:88-131)
 
 from oracle import weights as W  # noqa: E402
 from oracle import unet_ref_cpu as O  # noqa: E402
@@ -227,6 +230,40 @@ def case_mod_d3_64():
     np.savez_compressed(os.path.join(OUT, "mod_d3_64.npz"), **out)
 
 
+def case_res_d3_64():
+    torch.manual_seed(0)
+    m = RefResUNet(1, 1, base_filters=64, depth=3)
+    spec = MO.res_param_spec(1, 1, 64, 3)
+    assert [n for n, _ in m.named_parameters()] == [s[0] for s in spec], "res param order"
+    names = [n for n, _ in MO.res_bn_layers(64, 3)]
+    assert [n for n, _ in m.named_buffers() if n.endswith("running_mean")] == \
+        [f"{n}.running_mean" for n in names], "res buffer order"
+    sd = m.state_dict()
+    for k, v in MO.res_make_params(42, 64, 3).items():
+        sd[k] = v.clone()
+    m.load_state_dict(sd)
+    m.train()
+    x = torch.from_numpy(W.make_input(13, 2, 1, 64, 64))
+    t = torch.from_numpy(W.make_target(13, 2, 64, 64))
+    opt = torch.optim.AdamW(m.parameters(), lr=1e-4)
+    out = {}
+    for s in range(2):
+        logits, lb, ld, loss = step(m, opt, x, t, RefDice())
+        p = f"s{s}_"
+        out[p + "logits"] = logits.numpy()
+        out[p + "mask"] = (torch.sigmoid(logits) > 0.5).numpy().astype(np.uint8)
+        out[p + "bce"], out[p + "dice"], out[p + "loss"] = lb, ld, loss
+        grad_stats(m, p, out)
+        out[p + "params_samp"] = param_samples(m)
+        bufs = dict(m.named_buffers())
+        out[p + "running_mean"] = np.concatenate([bufs[f"{n}.running_mean"].numpy() for n in names])
+        out[p + "running_var"] = np.concatenate([bufs[f"{n}.running_var"].numpy() for n in names])
+    m.eval()
+    with torch.no_grad():
+        out["eval_logits"] = m(x).numpy()
+    np.savez_compressed(os.path.join(OUT, "res_d3_64.npz"), **out)
+
+
 def case_mod_c4_64():
     m = build_mod(128, 5)
     m.train()
@@ -250,6 +287,7 @@ if __name__ == "__main__":
     case_dp2_64()
     case_neg_32()
     case_mod_d3_64()
+    case_res_d3_64()
     case_mod_c4_64()
     for f in sorted(os.listdir(OUT)):
         print(f, os.path.getsize(os.path.join(OUT, f)))
