@@ -68,8 +68,11 @@ typedef enum {
 typedef enum {
     UNET_VARIANT_MODEL = 0, /* models/model.py:UNet -- Conv(+bias) -> ReLU -> BN blocks,
                                concat [up, skip], depth 4, base 64 (fixed) */
-    UNET_VARIANT_MOD = 1    /* models/mod.py:9-66 UNet -- Conv(no bias) -> BN -> ReLU blocks,
+    UNET_VARIANT_MOD = 1,   /* models/mod.py:9-66 UNet -- Conv(no bias) -> BN -> ReLU blocks,
                                concat [skip, up], base_filters / depth configurable */
+    UNET_VARIANT_RES = 2    /* models/mod.py:71-131 ResUNet -- residual blocks
+                               ReLU(Conv-BN-ReLU-Conv-BN(x) + Conv1x1(x)), otherwise as MOD
+                               (the network main.py:122 builds) */
 } unet_variant;
 
 /* Arithmetic of the convolution GEMMs. */

@@ -1,0 +1,117 @@
+"""GPU parity of models/mod.py:ResUNet (mod.py:71-131, the network the reference's
+main.py:122 builds): residual blocks ReLU(Conv-BN-ReLU-Conv-BN(x) + Conv1x1(x)), closed by
+the skip GEMM's E_RESID epilogue, with the skip's input gradient added to conv1's (E_ADD).
+Oracle: oracle/mod_ref_cpu.py (make_res_forward), pinned by tests/golden/res_d3_64.npz
+from the reference module.  Bars as tests/test_gpu_parity.py."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from _helpers import grad_errors, inputs, masks_agree, norm_rel, rel_max
+from oracle import mod_ref_cpu as MO
+from oracle import weights as Wt
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda:0")
+LOGIT_TOL = 1e-4
+GRAD_TOL = 1e-2
+
+
+@pytest.fixture(autouse=True, scope="module")
+def _threads():
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+
+
+def _model(P, base, depth):
+    import unet_hip
+    m = unet_hip.ResUNet(1, 1, base_filters=base, depth=depth)
+    sd = m.state_dict()
+    for k, v in P.items():
+        sd[k] = v.clone()
+    for k, v in MO.res_init_buffers(base, depth).items():
+        sd[k] = v.clone()
+    m.load_state_dict(sd)
+    return m.to(DEV).train()
+
+
+def test_res_train_steps_match_golden(golden_dir):
+    import unet_hip
+    f = np.load(os.path.join(golden_dir, "res_d3_64.npz"), allow_pickle=False)
+    m = _model(MO.res_make_params(42, 64, 3), 64, 3)
+    opt = unet_hip.HipAdamW(m.parameters(), lr=1e-4)
+    x = torch.from_numpy(Wt.make_input(13, 2, 1, 64, 64)).to(DEV)
+    t = torch.from_numpy(Wt.make_target(13, 2, 64, 64)).to(DEV)
+    spec = MO.res_param_spec(1, 1, 64, 3)
+    names = [n for n, _ in MO.res_bn_layers(64, 3)]
+    for s in range(2):
+        p = f"s{s}_"
+        tol = LOGIT_TOL if s == 0 else 2e-3
+        opt.zero_grad()
+        logits = m(x)
+        losses = unet_hip.seg_losses(logits, t)
+        (losses[0] + losses[1]).backward()
+        opt.step()
+        ref = f[p + "logits"]
+        lg = logits.detach().cpu().numpy()
+        assert rel_max(lg, ref) <= tol, f"{p} logits {rel_max(lg, ref):.2e}"
+        ok, nd = masks_agree((torch.sigmoid(logits) > 0.5).cpu().numpy().astype(np.uint8),
+                             f[p + "mask"], ref, 10 * tol * np.abs(ref).max())
+        assert ok, f"{p}: {nd} mask bits differ away from the decision boundary"
+        assert abs(losses[0].item() - float(f[p + "bce"])) <= (1e-5 if s == 0 else 1e-4)
+        assert abs(losses[1].item() - float(f[p + "dice"])) <= (1e-5 if s == 0 else 1e-4)
+        gtol = GRAD_TOL if s == 0 else 10 * GRAD_TOL
+        named = dict(m.named_parameters())
+        norms, samp = f[p + "grad_norm"], f[p + "grad_samp"]
+        for ti, item in enumerate(spec):
+            g = named[item[0]].grad.detach().double().cpu().reshape(-1)
+            idx = np.floor(Wt.uniform(7, 3000 + ti, 64) * g.numel()).astype(np.int64)
+            assert abs(g.norm().item() - norms[ti]) <= gtol * norms[ti], f"{p} {item[0]} norm"
+            assert np.max(np.abs(g[idx].numpy() - samp[ti])) <= gtol * norms[ti], f"{p} {item[0]}"
+        sd = m.state_dict()
+        rm = torch.cat([sd[f"{n}.running_mean"].cpu() for n in names]).numpy()
+        btol = 1e-4 if s == 0 else 1e-3
+        np.testing.assert_allclose(rm, f[p + "running_mean"], rtol=btol, atol=btol)
+    m.eval()
+    with torch.no_grad():
+        ev = m(x).cpu().numpy()
+    assert rel_max(ev, f["eval_logits"]) <= 2e-3
+
+
+def _to64(d):
+    return {k: (v.double() if v.is_floating_point() else v.clone()) for k, v in d.items()}
+
+
+@pytest.mark.parametrize("base,depth,size", [(64, 3, 64), (64, 5, 128)])
+def test_res_full_grads_vs_oracle(base, depth, size):
+    """Every element of every gradient vs the oracle (depth 5 = the reference default).
+
+    Deep levels are small: at depth 5 the bottleneck's BatchNorm sees (size/32)^2 pixels x
+    2 images per channel (8 values at 64x64, where two of its ReLU inputs lie within 1e-5
+    of zero and a single fp32 mask flip moves that BN's bias gradient by ~1e-2), so depth 5
+    runs at 128x128 and gradients are judged against the fp64 oracle, within 2x the fp32
+    oracle's own worst per-tensor error, floored at the usual 1e-2.  That
+    fp32 error is taken over two evaluations, of x and of x * (1 + 1e-7): a 1-ulp-scale
+    input change flips such near-zero masks too (base 64 depth 3: the bottleneck's
+    conv.1 bias gradient goes from 2.7e-3 to 1.5e-2 off fp64 in the oracle itself)."""
+    import unet_hip
+    P = MO.res_make_params(9, base, depth)
+    x, t = inputs(4, 2, size, size)
+    ref = MO.res_train_step(P, MO.res_init_buffers(base, depth), None, x, t, depth=depth)
+    refp = MO.res_train_step(P, MO.res_init_buffers(base, depth), None, x * (1 + 1e-7), t,
+                             depth=depth)
+    r64 = MO.res_train_step(_to64(P), _to64(MO.res_init_buffers(base, depth)), None, x.double(),
+                            t.double(), depth=depth)
+    m = _model(P, base, depth)
+    logits = m(x.to(DEV))
+    losses = unet_hip.seg_losses(logits, t.to(DEV))
+    (losses[0] + losses[1]).backward()
+    assert rel_max(logits.detach().cpu().numpy(), ref["logits"].numpy()) <= LOGIT_TOL
+    e32 = {k: max(norm_rel(g, r64["grads"][k]), norm_rel(refp["grads"][k], r64["grads"][k]))
+           for k, g in ref["grads"].items()}
+    env = max(2 * max(e32.values()), GRAD_TOL)
+    errs = grad_errors(m, r64["grads"])
+    worst = max(errs, key=errs.get)
+    assert errs[worst] <= env, f"{worst}: {errs[worst]:.3e} (fp32 oracle {e32[worst]:.3e})"

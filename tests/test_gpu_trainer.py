@@ -96,3 +96,16 @@ def test_main_cli_synthetic(tmp_path, monkeypatch):
     runs = os.listdir(tmp_path / "experiments")
     assert len(runs) == 1
     assert os.path.exists(tmp_path / "experiments" / runs[0] / "models" / "UNet_last.pth")
+
+
+def test_main_cli_resunet(tmp_path, monkeypatch):
+    """The network the reference's main.py:122 builds (mod.py:ResUNet), through main.py."""
+    import main
+    monkeypatch.chdir(tmp_path)
+    args = main.get_parser(["--mode", "both", "--synthetic", "4", "--epochs", "1", "--batch_size", "2",
+                            "--image_size", "64", "--num_workers", "0", "--dice_ratio", "1",
+                            "--model_type", "ResUNet", "--depth", "3"])
+    main.main(args)
+    runs = os.listdir(tmp_path / "experiments")
+    assert len(runs) == 1
+    assert os.path.exists(tmp_path / "experiments" / runs[0] / "models" / "ResUNet_last.pth")

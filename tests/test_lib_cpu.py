@@ -223,3 +223,38 @@ def test_bf16_math_only_for_mod_variant():
     a = UNetRuntime("cuda:0", 1, 1, _lib.VARIANT_MOD, 128, 5, _lib.MATH_BF16)
     b = _mod_rt(128, 5)
     assert a.params == b.params and a.bn == b.bn and a.buckets == b.buckets
+
+
+def test_res_tables_and_rng_like_reference():
+    import torch
+    import unet_hip
+    from unet_hip import _lib
+    from unet_hip.runtime import UNetRuntime
+    from oracle import mod_ref_cpu as MO
+    rt = UNetRuntime.get("cuda:0", 1, 1, _lib.VARIANT_RES, 64, 3)
+    spec = MO.res_param_spec(1, 1, 64, 3)
+    assert [p[0] for p in rt.params] == [s[0] for s in spec]
+    assert [tuple(p[1]) for p in rt.params] == [tuple(s[1]) for s in spec]
+    assert [(b[0], b[1]) for b in rt.bn] == MO.res_bn_layers(64, 3)
+    spans = sorted(rt.buckets)
+    pos = 0
+    for o, n in spans:
+        assert o == pos and n > 0
+        pos += n
+    assert pos == rt.n_param_floats
+    m = unet_hip.ResUNet(1, 1, base_filters=64, depth=3)
+    assert [n for n, _ in m.named_parameters()] == [s[0] for s in spec]
+    assert rt.workspace_bytes(2, 64, 64, True) > 0
+    ref_dir = "/root/reference"
+    if not os.path.isdir(ref_dir):
+        pytest.skip("reference not present (GPU box)")
+    import importlib.util
+    sp = importlib.util.spec_from_file_location("_ref_mod2", os.path.join(ref_dir, "models", "mod.py"))
+    mod = importlib.util.module_from_spec(sp)
+    sp.loader.exec_module(mod)
+    torch.manual_seed(42)
+    a = mod.ResUNet(1, 1, base_filters=64, depth=3)
+    torch.manual_seed(42)
+    b = unet_hip.ResUNet(1, 1, base_filters=64, depth=3)
+    for (na, pa), (nb, pb) in zip(a.state_dict().items(), b.state_dict().items()):
+        assert na == nb and torch.equal(pa, pb), na

@@ -30,7 +30,14 @@ static inline int gather_taps(int mode) { return mode == G_CONV3 ? 9 : (mode == 
 //                      follows the BN: do *= [escale*y + eshift > 0], stored masked.
 //   E_STATS          : out[m][n] = acc + per-block column sum / sum of squares (a bias-free
 //                      conv feeding BN directly, models/mod.py:45-46)
-enum EpiMode { E_STORE = 0, E_BIAS_RELU_STATS = 1, E_CONVT = 2, E_STORE_BN = 3, E_STATS = 4 };
+//   E_RESID          : out[m][n] = ReLU(acc + escale[n] * ey[m][n] + eshift[n]): the 1x1 skip
+//                      conv of a residual block closing the block, ReLU(BN2(z2) + skip(x))
+//                      (models/mod.py:86)
+//   E_ADD            : out[m][n] += acc (the skip conv's input gradient already there)
+enum EpiMode {
+    E_STORE = 0, E_BIAS_RELU_STATS = 1, E_CONVT = 2, E_STORE_BN = 3, E_STATS = 4, E_RESID = 5,
+    E_ADD = 6
+};
 
 // What the A (row GEMM) / B' (wgrad) loader applies to the gathered values:
 //   OP_PLAIN : raw values

@@ -407,6 +407,26 @@ __global__ __launch_bounds__(T::THREADS, 1) void rowgemm_kernel(RowGemmArgs p) {
                     p.out[op * p.ldo + p.ooff + co] = acc[mt][nt][r] + bb;
                 }
         }
+    } else if constexpr (EMODE == E_RESID || EMODE == E_ADD) {
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+            const int n = n0 + wn * WN + nt * 32 + li;
+            const float es = EMODE == E_RESID ? p.escale[n] : 0.f;
+            const float eb = EMODE == E_RESID ? p.eshift[n] : 0.f;
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int m = m0 + wm * WM + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                    if (m >= p.M) continue;
+                    float* o = p.out + (size_t)m * p.ldo + p.ooff + n;
+                    if constexpr (EMODE == E_RESID)
+                        *o = fmaxf(acc[mt][nt][r] + (es * p.ey[(size_t)m * p.ldey + p.offey + n] + eb),
+                                   0.f);
+                    else
+                        *o += acc[mt][nt][r];
+                }
+        }
     } else {
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) {
@@ -878,6 +898,19 @@ static int rowgemm_dispatch(const RowGemmArgs& a, int tile, hipStream_t s) {
     if (a.amode == G_UP2 && !aff && !dz && a.emode == E_STORE_BN)
         return rowgemm_tile<G_UP2, OP_PLAIN, E_STORE_BN, BF>(a, tile, s);
     if constexpr (!BF) {
+        // residual network (models/mod.py:ResUNet): plain operands everywhere
+        if (!aff && !dz) {
+            if (a.amode == G_IDENT && a.emode == E_RESID)
+                return rowgemm_tile<G_IDENT, OP_PLAIN, E_RESID, false>(a, tile, s);
+            if (a.amode == G_IDENT && a.emode == E_STORE)
+                return rowgemm_tile<G_IDENT, OP_PLAIN, E_STORE, false>(a, tile, s);
+            if (a.amode == G_CONV3 && a.emode == E_ADD)
+                return rowgemm_tile<G_CONV3, OP_PLAIN, E_ADD, false>(a, tile, s);
+            if (a.amode == G_IDENT && a.emode == E_CONVT)
+                return rowgemm_tile<G_IDENT, OP_PLAIN, E_CONVT, false>(a, tile, s);
+            if (a.amode == G_UP2 && a.emode == E_STORE)
+                return rowgemm_tile<G_UP2, OP_PLAIN, E_STORE, false>(a, tile, s);
+        }
         if (a.amode == G_CONV3 && a.emode == E_BIAS_RELU_STATS)
             return aff ? rowgemm_tile<G_CONV3, OP_AFFINE, E_BIAS_RELU_STATS, false>(a, tile, s)
                        : rowgemm_tile<G_CONV3, OP_PLAIN, E_BIAS_RELU_STATS, false>(a, tile, s);
@@ -895,8 +928,9 @@ int launch_rowgemm(const RowGemmArgs& a, int tile, hipStream_t s) {
     if (a.M < 1 || a.K != gather_taps(a.amode) * a.C) return -1;
     const bool aff = a.ascale != nullptr, dz = a.acoef != nullptr;
     if (aff && dz) return -1;
-    if ((a.emode == E_STORE_BN) != (a.ey != nullptr)) return -1;
+    if ((a.emode == E_STORE_BN || a.emode == E_RESID) != (a.ey != nullptr)) return -1;
     if ((a.escale != nullptr) != (a.eshift != nullptr) || (a.arelu && !aff)) return -1;
+    if (a.emode == E_RESID && !a.escale) return -1;
     if ((a.bt != nullptr) == (a.bt16 != nullptr)) return -1;  // exactly one weight image
     return a.bt16 ? rowgemm_dispatch<true>(a, tile, s) : rowgemm_dispatch<false>(a, tile, s);
 }
@@ -1003,5 +1037,10 @@ int launch_wgrad(const WgradArgs& a, int tile, hipStream_t s) {
     if (a.amode == G_IDENT && a.bmode == G_UP2 && aff && !dz)
         return a.arelu ? wgrad_tile<G_IDENT, OP_AFFINE_RELU, G_UP2, false>(a, tile, s)
                        : wgrad_tile<G_IDENT, OP_AFFINE, G_UP2, false>(a, tile, s);
+    // residual network: plain operands (skip 1x1 conv; ConvT of a materialised block output)
+    if (a.amode == G_IDENT && a.bmode == G_IDENT && !aff && !dz)
+        return wgrad_tile<G_IDENT, OP_PLAIN, G_IDENT, false>(a, tile, s);
+    if (a.amode == G_IDENT && a.bmode == G_UP2 && !aff && !dz)
+        return wgrad_tile<G_IDENT, OP_PLAIN, G_UP2, false>(a, tile, s);
     return -1;
 }

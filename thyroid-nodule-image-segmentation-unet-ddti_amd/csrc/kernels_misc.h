@@ -41,6 +41,15 @@ int k_head_fwd(const float* y, int C, const float* scale, const float* shift, in
 int k_head_bwd(const float* y, int C, const float* scale, const float* shift, int relu,
                const float* w, int O, int P, int HW, const float* dlog, float* dout, float* partial,
                float* bnpart, int G, hipStream_t s);
+int k_pack_1x1_t(const float* w, float* wt, int cin, int cout, hipStream_t s);
+// Residual blocks (models/mod.py:ResUNet): first-block forward with the Cin = 1 skip,
+// backward entry (ReLU mask + BN2 partials), first-block skip weight gradient.
+int k_res_first_fwd(const float* x, const float* ws, const float* z, const float* sc,
+                    const float* sh, int64_t P, int C, float* out, int ldo, int offo, hipStream_t s);
+int k_res_bwd_prep(float* d, const float* out, int ldo, int offo, const float* z, int64_t P, int C,
+                   float* partial, int G, hipStream_t s);
+int k_res_first_wgrad(const float* x, const float* du, int P, int C, float* partial, int G,
+                      float* gw, hipStream_t s);
 int k_loss_fwd(const float* x, const float* t, int N, int64_t per, float* stats, float* losses,
                float alpha, float beta, float gamma, hipStream_t s);
 int k_loss_bwd(const float* x, const float* t, int N, int64_t per, const float* stats,

@@ -48,6 +48,17 @@ __global__ void pack_convT_kernel(const float* __restrict__ w, OUT* __restrict__
     }
 }
 
+// 1x1 conv weight W[co][ci] -> its dgrad image Wt[ci][co] (models/mod.py:83 skip)
+__global__ void pack_1x1_t_kernel(const float* __restrict__ w, float* __restrict__ wt, int cin,
+                                  int cout) {
+    const int64_t n = (int64_t)cin * cout;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int ci = (int)(i % cin), co = (int)(i / cin);
+        wt[(int64_t)ci * cout + co] = w[i];
+    }
+}
+
 // Block-level combine of per-thread channel partials.  Threads are laid out as
 // (row group g = tid / tpr, channel quad q = tid % tpr); acc[NV] holds NV quantities per
 // channel-quad.  Writes out[v*C + 4q + j] for row group 0.  smem: 256*NV*4 floats.
@@ -305,7 +316,8 @@ __global__ void maxpool_bn_kernel(const float* __restrict__ y, int ld, int off,
         const int xo = (int)(po % Wo);
         const int64_t t = po / Wo;
         const int yo = (int)(t % Ho), img = (int)(t / Ho);
-        const f32x4 sc = *(const f32x4*)(scale + 4 * c4), sh = *(const f32x4*)(shift + 4 * c4);
+        const f32x4 sc = scale ? *(const f32x4*)(scale + 4 * c4) : f32x4{1.f, 1.f, 1.f, 1.f};
+        const f32x4 sh = shift ? *(const f32x4*)(shift + 4 * c4) : f32x4{0.f, 0.f, 0.f, 0.f};
         f32x4 best;
         uint32_t bi = 0;
 #pragma unroll
@@ -375,7 +387,7 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const float* __restric
             for (int k = 0; k < 4; ++k) {
                 const int64_t pin = ((int64_t)img * H + 2 * yo + (k >> 1)) * W + 2 * xo + (k & 1);
                 f32x4 v = *(const f32x4*)(dskip + pin * ldskip + offskip + c);
-                const f32x4 yv = *(const f32x4*)(y + pin * ldy + offy + c);
+                const f32x4 yv = y ? *(const f32x4*)(y + pin * ldy + offy + c) : f32x4{0, 0, 0, 0};
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     if (((bi >> (8 * j)) & 0xFF) == (uint32_t)k) v[j] += gp[j];
@@ -389,7 +401,7 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const float* __restric
                 }
             }
         }
-        block_combine_d<2>(acc, tpr, C, partial + (int64_t)blockIdx.x * 2 * C + c0, smem);
+        if (partial) block_combine_d<2>(acc, tpr, C, partial + (int64_t)blockIdx.x * 2 * C + c0, smem);
         __syncthreads();
     }
 }
@@ -466,6 +478,7 @@ __global__ void sum_partials_kernel(const float* __restrict__ part, int G, int n
 
 // Sum the split-K slabs of a wgrad and scatter into the torch weight layout.
 //   conv3 : slab [S][tap*Cin+ci][co] -> grad[co][ci][tap]
+//   conv1 : slab [S][ci][co]         -> grad[co][ci]         (kind 2)
 //   convT : slab [S][ci][ab*Cout+co] -> grad[ci][co][ab]
 __global__ void slab_reduce_kernel(const float* __restrict__ slab, int S, int Mw, int Nw,
                                    int kind, int cin, int cout, float* __restrict__ grad) {
@@ -499,6 +512,8 @@ __global__ void slab_reduce_kernel(const float* __restrict__ slab, int S, int Mw
             if (kind == 0) {
                 const int tap = m / cin, ci = m - tap * cin;
                 o = ((int64_t)n * cin + ci) * 9 + tap;
+            } else if (kind == 2) {  // 1x1 conv: slab [ci][co] -> grad[co][ci]
+                o = (int64_t)n * cin + m;
             } else {
                 const int ab = n / cout, co = n - ab * cout;
                 o = ((int64_t)m * cout + co) * 4 + ab;
@@ -538,8 +553,10 @@ __global__ void head_fwd_kernel(const float* __restrict__ y, int C, const float*
     const int q = (int)(gt % lpp);
     const bool ok = pix < P;
     f32x4 v = {0, 0, 0, 0};
-    if (ok) v = *(const f32x4*)(y + pix * C + 4 * q) * *(const f32x4*)(scale + 4 * q) +
-                *(const f32x4*)(shift + 4 * q);
+    if (ok) {
+        v = *(const f32x4*)(y + pix * C + 4 * q);
+        if (scale) v = v * *(const f32x4*)(scale + 4 * q) + *(const f32x4*)(shift + 4 * q);
+    }
     if (relu)
 #pragma unroll
         for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
@@ -569,7 +586,8 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__
     double bq[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
     const int lpp = C / 4, rpp = 256 / lpp;
     const int q = threadIdx.x % lpp, g = threadIdx.x / lpp;
-    const f32x4 sc = *(const f32x4*)(scale + 4 * q), sh = *(const f32x4*)(shift + 4 * q);
+    const f32x4 sc = scale ? *(const f32x4*)(scale + 4 * q) : f32x4{1.f, 1.f, 1.f, 1.f};
+    const f32x4 sh = shift ? *(const f32x4*)(shift + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
     // O <= 4 supported for the fused partials
     f32x4 aw[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
     float ab[4] = {0, 0, 0, 0};
@@ -599,7 +617,7 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__
             bq[1][j] += (double)d[j] * yr[j];
         }
     }
-    block_combine_d<2>(bq, lpp, C, bnpart + (int64_t)blockIdx.x * 2 * C, smem4);
+    if (bnpart) block_combine_d<2>(bq, lpp, C, bnpart + (int64_t)blockIdx.x * 2 * C, smem4);
     __syncthreads();
     // combine over row groups through LDS, one quantity at a time
     float* out = partial + (int64_t)blockIdx.x * (O * C + O);
@@ -623,6 +641,80 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__
         }
         __syncthreads();
     }
+}
+
+// -------------------------------------------------------------------------------------
+// Residual block of models/mod.py:ResUNet (:73-86): out = ReLU(BN2(z2) + skip(x)).
+// -------------------------------------------------------------------------------------
+// First block (Cin = 1): skip is a per-channel scale of the image, out[p][c] =
+// ReLU(s[c] z[p][c] + t[c] + ws[c] x[p]).  One thread per (pixel, channel quad).
+__global__ void res_first_fwd_kernel(const float* __restrict__ x, const float* __restrict__ ws,
+                                     const float* __restrict__ z, const float* __restrict__ sc,
+                                     const float* __restrict__ sh, int64_t P, int C,
+                                     float* __restrict__ out, int ldo, int offo) {
+    const int c4n = C / 4;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < P * c4n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int c = (int)(i % c4n) * 4;
+        const int64_t m = i / c4n;
+        const float xv = x[m];
+        const f32x4 zv = *(const f32x4*)(z + m * C + c);
+        f32x4 o = zv * *(const f32x4*)(sc + c) + *(const f32x4*)(sh + c) + xv * *(const f32x4*)(ws + c);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = fmaxf(o[j], 0.f);
+        *(f32x4*)(out + m * ldo + offo + c) = o;
+    }
+}
+
+// Backward entry of a residual block: du = dout [out > 0] (in place) and the BN2 partials
+// partial[G][2][C] = {sum du, sum du z2} (z2 = conv output before BN2, dense [P][C]).
+__global__ __launch_bounds__(256) void res_bwd_prep_kernel(float* __restrict__ d,
+                                                          const float* __restrict__ out, int ldo,
+                                                          int offo, const float* __restrict__ z,
+                                                          int64_t P, int C, float* partial) {
+    __shared__ double smem[256 * 2 * 4];
+    const int tpr = C / 4 < 256 ? C / 4 : 256, rpp = 256 / tpr;
+    double acc[2][4];
+    for (int c0 = 0; c0 < C; c0 += 4 * tpr) {
+        const int q = threadIdx.x % tpr, g = threadIdx.x / tpr;
+        const int c = c0 + 4 * q;
+#pragma unroll
+        for (int v = 0; v < 2; ++v)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[v][j] = 0.0;
+        const int64_t per = (P + gridDim.x - 1) / gridDim.x;
+        const int64_t r0 = blockIdx.x * per, r1 = r0 + per < P ? r0 + per : P;
+        for (int64_t m = r0 + g; m < r1; m += rpp) {
+            f32x4* pd = (f32x4*)(d + m * C + c);
+            f32x4 v = *pd;
+            const f32x4 ov = *(const f32x4*)(out + m * ldo + offo + c);
+            const f32x4 zv = *(const f32x4*)(z + m * C + c);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                v[j] = ov[j] > 0.f ? v[j] : 0.f;
+                acc[0][j] += v[j];
+                acc[1][j] += (double)v[j] * zv[j];
+            }
+            *pd = v;
+        }
+        block_combine_d<2>(acc, tpr, C, partial + (int64_t)blockIdx.x * 2 * C + c0, smem);
+        __syncthreads();
+    }
+}
+
+// First block's skip weight gradient: partial[G][C] = sum_p x[p] du[p][c].
+__global__ __launch_bounds__(256) void res_first_wgrad_kernel(const float* __restrict__ x,
+                                                             const float* __restrict__ du, int P,
+                                                             int C, float* partial) {
+    __shared__ __attribute__((aligned(16))) float smem[256 * 1 * 4];
+    const int tpr = C / 4, rpp = 256 / tpr;
+    const int q = threadIdx.x % tpr, g = threadIdx.x / tpr;
+    f32x4 acc[1] = {{0, 0, 0, 0}};
+    const int per = (P + gridDim.x - 1) / gridDim.x;
+    const int r0 = blockIdx.x * per, r1 = min(P, r0 + per);
+    for (int m = r0 + g; m < r1; m += rpp)
+        acc[0] += x[m] * *(const f32x4*)(du + (int64_t)m * C + 4 * q);
+    block_combine<1>(acc, tpr, C, partial + (int64_t)blockIdx.x * C, smem);
 }
 
 // -------------------------------------------------------------------------------------
@@ -900,6 +992,34 @@ int k_slab_reduce(const float* slab, int S, int Mw, int Nw, int kind, int cin, i
     if (Nw % 4) return -1;
     hipLaunchKernelGGL(slab_reduce_kernel, dim3(grid_for((int64_t)Mw * Nw / 4)), dim3(256), 0, s,
                        slab, S, Mw, Nw, kind, cin, cout, grad);
+    LAUNCH_CHECK();
+}
+int k_pack_1x1_t(const float* w, float* wt, int cin, int cout, hipStream_t s) {
+    hipLaunchKernelGGL(pack_1x1_t_kernel, dim3(grid_for((int64_t)cin * cout)), dim3(256), 0, s, w, wt,
+                       cin, cout);
+    LAUNCH_CHECK();
+}
+int k_res_first_fwd(const float* x, const float* ws, const float* z, const float* sc,
+                    const float* sh, int64_t P, int C, float* out, int ldo, int offo, hipStream_t s) {
+    if (C % 4) return -1;
+    hipLaunchKernelGGL(res_first_fwd_kernel, dim3(grid_for(P * (C / 4))), dim3(256), 0, s, x, ws, z,
+                       sc, sh, P, C, out, ldo, offo);
+    LAUNCH_CHECK();
+}
+int k_res_bwd_prep(float* d, const float* out, int ldo, int offo, const float* z, int64_t P, int C,
+                   float* partial, int G, hipStream_t s) {
+    if (C % 4) return -1;
+    hipLaunchKernelGGL(res_bwd_prep_kernel, dim3(G), dim3(256), 0, s, d, out, ldo, offo, z, P, C,
+                       partial);
+    LAUNCH_CHECK();
+}
+int k_res_first_wgrad(const float* x, const float* du, int P, int C, float* partial, int G,
+                      float* gw, hipStream_t s) {
+    if (C % 4 || C > 1024) return -1;
+    hipLaunchKernelGGL(res_first_wgrad_kernel, dim3(G), dim3(256), 0, s, x, du, P, C, partial);
+    HIP_OK(hipGetLastError());
+    hipLaunchKernelGGL(sum_partials_kernel, dim3((C + 63) / 64), dim3(64, 16), 0, s, partial, G, C,
+                       gw);
     LAUNCH_CHECK();
 }
 int k_head_fwd(const float* y, int C, const float* scale, const float* shift, int relu,

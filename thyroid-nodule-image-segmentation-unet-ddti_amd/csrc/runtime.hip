@@ -12,7 +12,10 @@
 //                    the concat CAT_{D-k-1}      (model.py middle.2/decoder*.1; mod.py upconvs.k)
 // and they differ in the order inside a block (model.py:36-41 Conv(+bias) -> ReLU -> BN;
 // mod.py:45-50 Conv(no bias) -> BN -> ReLU), the concat order (model.py:64 [up, skip];
-// mod.py:64 [skip, up]) and the parameter names / registration order.
+// mod.py:64 [skip, up]) and the parameter names / registration order.  mod.py:ResUNet
+// (:71-131) has the same skeleton with residual blocks ReLU(conv(x) + skip(x)): there the
+// block output is materialised by the 1x1 skip GEMM's epilogue (E_RESID) and every
+// consumer reads it plainly.
 #include <math.h>
 #include <stdlib.h>
 #include <stdarg.h>
@@ -75,11 +78,13 @@ struct unet_ctx {
     bool bn_relu = false;    // BN -> ReLU (mod.py) instead of ReLU -> BN (model.py)
     bool skip_first = false; // concat [skip, up] (mod.py) instead of [up, skip] (model.py)
     bool bf16 = false;       // conv GEMMs on bf16 MFMA (f32 accumulate), BASELINE config 4
+    bool res = false;        // residual blocks (mod.py:ResUNet): block outputs materialised
     std::vector<ParamT> params;
     int64_t n_param_floats = 0;
     std::vector<ConvL> conv;
     std::vector<BnL> bn;
     std::vector<ConvTL> convt;
+    std::vector<int64_t> skip_w, skip_pd;  // per block: 1x1 skip weight, its dgrad image
     int64_t head_w = 0, head_b = 0;
     int64_t n_bn_floats = 0;
     int64_t pack_floats = 0;
@@ -160,20 +165,26 @@ void build_graph(unet_ctx* c) {
         BnL& B = c->bn[i];
         B.C = L.cout;
         const int st = stage_of_block(b);
-        L.w = add(pfx + (which ? ".3.weight" : ".0.weight"), {L.cout, L.cin, 3, 3}, st);
+        const std::string cp = c->res ? pfx + ".conv" : pfx;  // ResidualBlock.conv (mod.py:75)
+        L.w = add(cp + (which ? ".3.weight" : ".0.weight"), {L.cout, L.cin, 3, 3}, st);
         if (c->variant == UNET_VARIANT_MODEL) {  // model.py:33-43: 0 conv, 2 BN, 3 conv, 5 BN
             L.b = add(pfx + (which ? ".3.bias" : ".0.bias"), {L.cout}, st);
             B.name = pfx + (which ? ".5" : ".2");
-        } else {  // mod.py:43-51: 0 conv (no bias), 1 BN, 3 conv, 4 BN
+        } else {  // mod.py:43-51 / :75-81: 0 conv (no bias), 1 BN, 3 conv, 4 BN
             L.b = -1;
-            B.name = pfx + (which ? ".4" : ".1");
+            B.name = cp + (which ? ".4" : ".1");
         }
         B.g = add(B.name + ".weight", {L.cout}, st);
         B.b = add(B.name + ".bias", {L.cout}, st);
     };
+    c->skip_w.assign(nb, -1);
+    c->skip_pd.assign(nb, -1);
     auto block = [&](int b, const std::string& pfx) {
         conv_pair(b, 0, pfx);
         conv_pair(b, 1, pfx);
+        if (c->res)  // ResidualBlock.skip, Conv2d(in, out, 1, bias=False) (mod.py:83)
+            c->skip_w[b] = add(pfx + ".skip.weight", {c->conv[2 * b].cout, c->conv[2 * b].cin, 1, 1},
+                               stage_of_block(b));
     };
     auto convT = [&](int k, const std::string& name) {
         ConvTL& T = c->convt[k];
@@ -235,6 +246,10 @@ void build_graph(unet_ctx* c) {
         T.pd = pk;
         pk += n;
     }
+    for (int b = 1; b < nb && c->res; ++b) {  // transposed skip images for the dgrad
+        c->skip_pd[b] = pk;
+        pk += (int64_t)c->conv[2 * b].cin * c->conv[2 * b].cout;
+    }
     c->pack_floats = pk;
     // gradient buckets: walk the arena from its end (what backward finishes first), open a
     // new bucket whenever a tensor finishes later than everything already in the current one
@@ -277,10 +292,12 @@ struct Plan {
     float* cat_shift[MAX_DEPTH];
     float* pool[MAX_DEPTH];
     uint8_t* idx[MAX_DEPTH];
+    std::vector<float*> out;  // residual network: block outputs (ld, off)
+    std::vector<int> ldout, offout;
     float* stats;
     float* stats2;
     // backward
-    float* g[2];
+    float* g[3];
     float* dcat[MAX_DEPTH];
     float* slab;
     float* part;   // BN-backward column partials [rows][2][C]
@@ -371,7 +388,7 @@ void make_plan(unet_ctx* c, int N, int H, int W, bool training, char* base, Plan
     }
     for (int i = 0; i < NC; ++i) {
         const ConvL& L = c->conv[i];
-        if (L.block < D && L.which == 1) {
+        if (L.block < D && L.which == 1 && !c->res) {
             // the encoder output lives in the skip half of its concat buffer, and its BN
             // affine is that half of the concat affine
             const int l = L.block, so = c->skip_off(l);
@@ -390,6 +407,20 @@ void make_plan(unet_ctx* c, int N, int H, int W, bool training, char* base, Plan
         p.mean[i] = b.take<float>(L.cout);
         p.invstd[i] = b.take<float>(L.cout);
     }
+    p.out.assign(2 * D + 1, nullptr);
+    p.ldout.assign(2 * D + 1, 0);
+    p.offout.assign(2 * D + 1, 0);
+    for (int blk = 0; blk <= 2 * D && c->res; ++blk) {
+        const ConvL& L = c->conv[2 * blk + 1];
+        if (blk < D) {  // encoder output: the skip half of its concat buffer
+            p.out[blk] = p.cat[blk];
+            p.ldout[blk] = 2 * L.cout;
+            p.offout[blk] = c->skip_off(blk);
+        } else {
+            p.out[blk] = b.take<float>(p.P[L.level] * L.cout);
+            p.ldout[blk] = L.cout;
+        }
+    }
     // BN-stat partials: rows = M / 64 (smallest row tile) of the row GEMM, or RED_G for the
     // first conv
     int64_t srows = 0;
@@ -407,6 +438,7 @@ void make_plan(unet_ctx* c, int N, int H, int W, bool training, char* base, Plan
         }
         p.g[0] = b.take<float>(gmax);
         p.g[1] = b.take<float>(gmax);
+        p.g[2] = c->res ? b.take<float>(gmax) : nullptr;
         for (int l = 0; l < D; ++l) p.dcat[l] = b.take<float>(p.P[l] * 2 * c->ch(l));
         int64_t smax = 0, bmax = 0;
         for (int i = 1; i < NC; ++i) {
@@ -414,6 +446,11 @@ void make_plan(unet_ctx* c, int N, int H, int W, bool training, char* base, Plan
             WgradCfg w = wgrad_cfg(L.cin, 9, L.cout, 1, p.P[L.level], c->bf16);
             smax = std::max(smax, (int64_t)w.splits * 9 * L.cin * L.cout);
             bmax = std::max(bmax, (int64_t)w.splits * L.cout);
+        }
+        for (int blk = 1; blk <= 2 * D && c->res; ++blk) {
+            const ConvL& L = c->conv[2 * blk];
+            WgradCfg w = wgrad_cfg(L.cin, 1, L.cout, 1, p.P[L.level], c->bf16);
+            smax = std::max(smax, (int64_t)w.splits * L.cin * L.cout);
         }
         for (const ConvTL& T : c->convt) {
             WgradCfg w = wgrad_cfg(T.cin, 1, T.cout, 4, p.P[T.in_level], c->bf16);
@@ -431,7 +468,7 @@ void make_plan(unet_ctx* c, int N, int H, int W, bool training, char* base, Plan
         p.bslab = b.take<float>(std::max<int64_t>(bmax, 1));
         p.coef = b.take<float>(3 * (int64_t)c->cmax);
     } else {
-        p.g[0] = p.g[1] = p.slab = p.part = p.part2 = p.hpart = p.bslab = p.coef = nullptr;
+        p.g[0] = p.g[1] = p.g[2] = p.slab = p.part = p.part2 = p.hpart = p.bslab = p.coef = nullptr;
         for (int l = 0; l < D; ++l) p.dcat[l] = nullptr;
     }
     p.bytes = b.off + 256;
@@ -561,6 +598,7 @@ Operand conv_input(unet_ctx* c, Plan& p, int i) {
         return {p.pool[L.block - 1], L.cin, 0, nullptr, nullptr, 0};
     if (L.block > D) {  // concat: the skip half carries the encoder's BN (+ReLU) affine
         const int l = L.level;
+        if (c->res) return {p.cat[l], 2 * c->ch(l), 0, nullptr, nullptr, 0};  // materialised
         return {p.cat[l], 2 * c->ch(l), 0, p.cat_scale[l], p.cat_shift[l],
                 c->bn_relu ? c->ch(l) : 0};
     }
@@ -603,6 +641,9 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
             RUN("pack", 0, k_pack_convT(prm + T.w, p.pack + T.pf, training ? p.pack + T.pd : nullptr,
                                         T.cin, T.cout, s));
     }
+    for (int b = 1; b <= 2 * D && c->res && training; ++b)
+        RUN("pack", 0, k_pack_1x1_t(prm + c->skip_w[b], p.pack + c->skip_pd[b], c->conv[2 * b].cin,
+                                    c->conv[2 * b].cout, s));
     // 2. concat affine: identity on the up-sampled half (no BN between ConvT and concat)
     for (int l = 0; l < D; ++l) {
         const int C = c->ch(l), uo = c->up_off(l);
@@ -665,14 +706,20 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
         g.M = (int)p.P[T.in_level];
         g.N = 4 * T.cout;
         g.K = T.cin;
-        g.a = p.y[src];
-        g.lda = p.ldy[src];
-        g.aoff = p.offy[src];
+        if (c->res) {  // the materialised output of block D+k
+            g.a = p.out[D + k];
+            g.lda = p.ldout[D + k];
+            g.aoff = p.offout[D + k];
+        } else {
+            g.a = p.y[src];
+            g.lda = p.ldy[src];
+            g.aoff = p.offy[src];
+            g.ascale = p.scale[src];
+            g.ashift = p.shift[src];
+            g.arelu = c->bn_relu ? T.cin : 0;
+        }
         g.C = T.cin;
         g.amode = G_IDENT;
-        g.ascale = p.scale[src];
-        g.ashift = p.shift[src];
-        g.arelu = c->bn_relu ? T.cin : 0;
         set_weights(c, g, p.pack + T.pf);
         g.out = p.cat[lo];
         g.ldo = 2 * c->ch(lo);
@@ -685,15 +732,59 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
         return 0;
     };
 
+    // residual block b closes with out = ReLU(BN2(z2) + skip(x)) (mod.py:86)
+    auto block_out = [&](int b) -> int {
+        const ConvL& CL = c->conv[2 * b];
+        const int i2 = 2 * b + 1;
+        const int64_t M = p.P[CL.level];
+        if (CL.pf < 0) {  // Cin = 1: the skip is a per-channel scale of the image
+            RUN("res_out", 0, k_res_first_fwd(xin, prm + c->skip_w[b], p.y[i2], p.scale[i2],
+                                              p.shift[i2], M, CL.cout, p.out[b], p.ldout[b],
+                                              p.offout[b], s));
+            return 0;
+        }
+        Operand a = conv_input(c, p, 2 * b);
+        RowGemmArgs g{};
+        g.H = H >> CL.level;
+        g.W = W >> CL.level;
+        g.M = (int)M;
+        g.N = CL.cout;
+        g.K = CL.cin;
+        g.a = a.ptr;
+        g.lda = a.ld;
+        g.aoff = a.off;
+        g.C = CL.cin;
+        g.amode = G_IDENT;
+        g.bt = prm + c->skip_w[b];  // torch layout [co][ci] is already Bt[n][k]
+        g.out = p.out[b];
+        g.ldo = p.ldout[b];
+        g.ooff = p.offout[b];
+        g.emode = E_RESID;
+        g.ey = p.y[i2];
+        g.ldey = p.ldy[i2];
+        g.offey = p.offy[i2];
+        g.escale = p.scale[i2];
+        g.eshift = p.shift[i2];
+        const int tile = pick_tile(CL.cout, false, false);
+        RUN(tlabel("skip_fwd", tile, b), 2.0 * M * CL.cout * CL.cin, launch_rowgemm(g, tile, s));
+        return 0;
+    };
+
     int rc;
     for (int b = 0; b <= D; ++b) {
         if ((rc = conv(2 * b))) return rc;
         if ((rc = conv(2 * b + 1))) return rc;
+        if (c->res && (rc = block_out(b))) return rc;
         if (b < D) {
             const int i = 2 * b + 1, C = c->ch(b);
-            RUN("maxpool_fwd", 0,
-                k_maxpool_bn(p.y[i], p.ldy[i], p.offy[i], p.scale[i], p.shift[i], c->bn_relu ? 1 : 0,
-                             p.N, H >> b, W >> b, C, p.pool[b], p.idx[b], s));
+            if (c->res)
+                RUN("maxpool_fwd", 0,
+                    k_maxpool_bn(p.out[b], p.ldout[b], p.offout[b], nullptr, nullptr, 0, p.N, H >> b,
+                                 W >> b, C, p.pool[b], p.idx[b], s));
+            else
+                RUN("maxpool_fwd", 0,
+                    k_maxpool_bn(p.y[i], p.ldy[i], p.offy[i], p.scale[i], p.shift[i],
+                                 c->bn_relu ? 1 : 0, p.N, H >> b, W >> b, C, p.pool[b], p.idx[b], s));
         }
     }
     for (int k = 0; k < D; ++k) {
@@ -701,11 +792,17 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
         const int b = D + 1 + k;
         if ((rc = conv(2 * b))) return rc;
         if ((rc = conv(2 * b + 1))) return rc;
+        if (c->res && (rc = block_out(b))) return rc;
     }
     const int last = NC - 1;
-    RUN("head_fwd", 2.0 * p.P[0] * c->base * c->out_ch,
-        k_head_fwd(p.y[last], c->base, p.scale[last], p.shift[last], c->bn_relu ? 1 : 0,
-                   prm + c->head_w, prm + c->head_b, c->out_ch, (int)p.P[0], H * W, logits, s));
+    if (c->res)
+        RUN("head_fwd", 2.0 * p.P[0] * c->base * c->out_ch,
+            k_head_fwd(p.out[2 * D], c->base, nullptr, nullptr, 0, prm + c->head_w, prm + c->head_b,
+                       c->out_ch, (int)p.P[0], H * W, logits, s));
+    else
+        RUN("head_fwd", 2.0 * p.P[0] * c->base * c->out_ch,
+            k_head_fwd(p.y[last], c->base, p.scale[last], p.shift[last], c->bn_relu ? 1 : 0,
+                       prm + c->head_w, prm + c->head_b, c->out_ch, (int)p.P[0], H * W, logits, s));
     return 0;
 }
 
@@ -749,7 +846,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
     // dgrad -> dx (ld ldx).  bn_next: dx is the `do` of BN layer i-1 (second conv of a
     // block), so the epilogue also emits that layer's partials; *rows = their count.
     auto conv_bwd = [&](int i, const float* dout, float* dx, int ldx, bool bn_next,
-                        int* rows) -> int {
+                        int* rows, bool accumulate = false) -> int {
         const ConvL& C = c->conv[i];
         const int Hl = H >> C.level, Wl = W >> C.level;
         const int64_t P = p.P[C.level];
@@ -820,7 +917,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
             g.out = dx;
             g.ldo = ldx;
             g.ooff = 0;
-            g.emode = E_STORE;
+            g.emode = accumulate ? E_ADD : E_STORE;
             if (bn_next) {
                 g.emode = E_STORE_BN;
                 g.ey = p.y[i - 1];
@@ -854,14 +951,20 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         w.H = Hi;
         w.W = Wi;
         w.P = (int)Pin;
-        w.a = p.y[src];
-        w.lda = p.ldy[src];
-        w.aoff = p.offy[src];
+        if (c->res) {
+            w.a = p.out[D + k];
+            w.lda = p.ldout[D + k];
+            w.aoff = p.offout[D + k];
+        } else {
+            w.a = p.y[src];
+            w.lda = p.ldy[src];
+            w.aoff = p.offy[src];
+            w.ascale = p.scale[src];
+            w.ashift = p.shift[src];
+            w.arelu = c->bn_relu ? T.cin : 0;
+        }
         w.CA = T.cin;
         w.amode = G_IDENT;
-        w.ascale = p.scale[src];
-        w.ashift = p.shift[src];
-        w.arelu = c->bn_relu ? T.cin : 0;
         w.b = p.dcat[lo];
         w.ldb = ldo;
         w.boff = uo;
@@ -894,15 +997,19 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         g.out = dx;
         g.ldo = T.cin;
         g.ooff = 0;
-        g.emode = E_STORE_BN;
-        g.ey = p.y[src];
-        g.ldey = p.ldy[src];
-        g.offey = p.offy[src];
-        if (c->bn_relu) {
-            g.escale = p.scale[src];
-            g.eshift = p.shift[src];
+        if (c->res) {  // d(block output); the block's own backward entry masks it
+            g.emode = E_STORE;
+        } else {
+            g.emode = E_STORE_BN;
+            g.ey = p.y[src];
+            g.ldey = p.ldy[src];
+            g.offey = p.offy[src];
+            if (c->bn_relu) {
+                g.escale = p.scale[src];
+                g.eshift = p.shift[src];
+            }
+            g.stats = p.part;
         }
-        g.stats = p.part;
         const int tile = pick_tile(T.cin, true, c->bf16);
         int bm, bn, bk;
         rowgemm_tile_dims(tile, &bm, &bn, &bk);
@@ -918,6 +1025,95 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
     float* G0 = p.g[0];
     float* G1 = p.g[1];
     int R = 0;
+    if (c->res) {
+        // Residual block b from d(out) in G0: du = d(out)[out > 0] (+ BN2 partials); the skip
+        // conv's weight / input gradients from du; BN2 + conv2, then BN1-ReLU + conv1 whose
+        // input gradient is ADDED to the skip's in dx (ld ldx; null for the first block).
+        auto block_bwd = [&](int b, float* dx, int ldx) -> int {
+            const ConvL& CL = c->conv[2 * b];
+            const int i1 = 2 * b, i2 = 2 * b + 1;
+            const int64_t P = p.P[CL.level];
+            RUN("res_bwd_prep", 0, k_res_bwd_prep(G0, p.out[b], p.ldout[b], p.offout[b], p.y[i2], P,
+                                                  CL.cout, p.part, RED_G, s));
+            if (CL.pf < 0) {
+                RUN("skip_wgrad", 2.0 * P * CL.cout,
+                    k_res_first_wgrad(p.x_nhwc, G0, (int)P, CL.cout, p.hpart, RED_G,
+                                      grads + c->skip_w[b], s));
+            } else {
+                Operand a = conv_input(c, p, i1);
+                WgradCfg wc = wgrad_cfg(CL.cin, 1, CL.cout, 1, P, false);
+                WgradArgs w{};
+                w.H = H >> CL.level;
+                w.W = W >> CL.level;
+                w.P = (int)P;
+                w.a = a.ptr;
+                w.lda = a.ld;
+                w.aoff = a.off;
+                w.CA = CL.cin;
+                w.amode = G_IDENT;
+                w.b = G0;
+                w.ldb = CL.cout;
+                w.CB = CL.cout;
+                w.bmode = G_IDENT;
+                w.Mw = CL.cin;
+                w.Nw = CL.cout;
+                w.pps = wc.pps;
+                w.splits = wc.splits;
+                w.slab = p.slab;
+                RUN(wlabel("skip_wgrad", wc, b), 2.0 * P * CL.cin * CL.cout, launch_wgrad(w, wc.tile, s));
+                RUN("wgrad_reduce", 0, k_slab_reduce(p.slab, wc.splits, w.Mw, w.Nw, 2, CL.cin, CL.cout,
+                                                     grads + c->skip_w[b], s));
+                RowGemmArgs g{};
+                g.H = H >> CL.level;
+                g.W = W >> CL.level;
+                g.M = (int)P;
+                g.N = CL.cin;
+                g.K = CL.cout;
+                g.a = G0;
+                g.lda = CL.cout;
+                g.C = CL.cout;
+                g.amode = G_IDENT;
+                g.bt = p.pack + c->skip_pd[b];
+                g.out = dx;
+                g.ldo = ldx;
+                g.emode = E_STORE;
+                const int tile = pick_tile(CL.cin, true, false);
+                RUN(tlabel("skip_dgrad", tile, b), 2.0 * P * CL.cin * CL.cout, launch_rowgemm(g, tile, s));
+            }
+            if ((rc = bn_finalize(i2, RED_G))) return rc;
+            if ((rc = conv_bwd(i2, G0, G1, CL.cout, true, &R))) return rc;
+            if ((rc = bn_finalize(i1, R))) return rc;
+            return conv_bwd(i1, G1, dx, ldx, false, nullptr, dx != nullptr);
+        };
+        RUN("head_bwd", 2.0 * p.P[0] * c->base * c->out_ch * 2,
+            k_head_bwd(p.out[2 * D], c->base, nullptr, nullptr, 0, prm + c->head_w, c->out_ch,
+                       (int)p.P[0], H * W, dlogits, G0, p.hpart, nullptr, RED_G, s));
+        RUN("head_grad", 0, k_sum_partials(p.hpart, RED_G, c->out_ch * c->base + c->out_ch,
+                                           grads + c->head_w, s));
+        if ((rc = block_bwd(2 * D, p.dcat[0], 2 * c->base))) return rc;
+        stage_done(0);
+        for (int k = D - 1; k >= 0; --k) {
+            const int b = D + k;
+            if ((rc = convT_bwd(k, G0, &R))) return rc;
+            const int l = c->conv[2 * b].level;
+            if (b > D) {
+                if ((rc = block_bwd(b, p.dcat[l], 2 * c->ch(l)))) return rc;
+            } else if ((rc = block_bwd(b, p.g[2], c->conv[2 * b].cin))) {
+                return rc;
+            }
+            stage_done(D - k);
+        }
+        for (int b = D - 1; b >= 0; --b) {
+            const int C = c->ch(b);
+            RUN("maxpool_bwd", 0,
+                k_maxpool_bwd(p.g[2], p.idx[b], p.dcat[b], 2 * C, c->skip_off(b), nullptr, 0, 0,
+                              nullptr, nullptr, p.N, H >> b, W >> b, C, G0, nullptr, RED_G, s));
+            if ((rc = block_bwd(b, b > 0 ? p.g[2] : nullptr, b > 0 ? c->conv[2 * b].cin : 0)))
+                return rc;
+            stage_done(2 * D - b);
+        }
+        return 0;
+    }
     // ---- head + last decoder block (stage 0) ----
     const int last = NC - 1;
     RUN("head_bwd", 2.0 * p.P[0] * c->base * c->out_ch * 2,
@@ -1001,7 +1197,8 @@ int unet_create(const unet_cfg* cfg, int device, unet_ctx** out) {
             delete c;
             return UNET_ERR_UNSUPPORTED;
         }
-        if (c->variant == UNET_VARIANT_MOD) {  // mod.py:13-14 defaults base 64, depth 5
+        if (c->variant == UNET_VARIANT_MOD || c->variant == UNET_VARIANT_RES) {
+            // mod.py:13-14 / :91-92 defaults base 64, depth 5
             c->base = cfg->base_filters > 0 ? cfg->base_filters : 64;
             c->depth = cfg->depth > 0 ? cfg->depth : 5;
         } else if ((cfg->base_filters > 0 && cfg->base_filters != 64) ||
@@ -1013,15 +1210,17 @@ int unet_create(const unet_cfg* cfg, int device, unet_ctx** out) {
     // The first conv kernel is specialised for a single input channel (every BASELINE
     // config); the GEMM tiles need 64-multiples of channels at every level; the head's
     // fused BN-partials path handles up to 4 classes.
-    if ((c->variant != UNET_VARIANT_MODEL && c->variant != UNET_VARIANT_MOD) || c->in_ch != 1 ||
+    if ((c->variant != UNET_VARIANT_MODEL && c->variant != UNET_VARIANT_MOD &&
+         c->variant != UNET_VARIANT_RES) || c->in_ch != 1 ||
         c->out_ch < 1 || c->out_ch > 4 || c->base % 64 || c->base > 256 || c->depth < 1 ||
         c->depth > MAX_DEPTH || (c->base << c->depth) > 8192) {
         delete c;
         return UNET_ERR_UNSUPPORTED;
     }
-    c->bn_relu = c->variant == UNET_VARIANT_MOD;
+    c->res = c->variant == UNET_VARIANT_RES;
+    c->bn_relu = c->variant != UNET_VARIANT_MODEL;
     c->skip_first = c->bn_relu;
-    if (c->bf16 && !c->bn_relu) {  // bf16 GEMMs are built for models/mod.py (config 4) only
+    if (c->bf16 && c->variant != UNET_VARIANT_MOD) {  // bf16 GEMMs: mod.py UNet (config 4) only
         delete c;
         return UNET_ERR_UNSUPPORTED;
     }

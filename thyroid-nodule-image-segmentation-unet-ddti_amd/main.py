@@ -1,9 +1,11 @@
 """CLI entry (mirror of the reference's main.py:17-161) on the HIP UNet path.
 
 Same flags as the reference (``--dataset_path``, ``--checkpoint_path``, ``--bce_ratio`` ...
-``--use_data_parallel``), with three additions: ``--model_type UNet`` is the model actually
-built (the reference hard-codes ResUNet at main.py:120-122; only the UNet of
-models/model.py has a HIP path), ``--mode {train,test,both}`` replaces the commented-out
+``--use_data_parallel``), with three additions: ``--model_type`` picks the network
+(``ResUNet``: models/mod.py:88-131, what the reference hard-codes at main.py:120-122;
+``ModUNet``: models/mod.py:9-66; ``UNet``: models/model.py, the BASELINE network and the
+default here; ``--base_filters`` / ``--depth`` for the mod.py ones, default 64 / 5 as
+there), ``--mode {train,test,both}`` replaces the commented-out
 ``trainer.train()`` / hard-wired ``trainer.test()`` (:156-157), and ``--synthetic N`` runs
 on N synthetic samples per split when the DDTI images are not on disk.
 
@@ -22,6 +24,8 @@ if HERE not in sys.path:
     sys.path.insert(0, HERE)
 
 from data.data_loader import MedicalDataset, SyntheticSegmentation, create_dataloader  # noqa: E402
+from models.mod import ResUNet  # noqa: E402
+from models.mod import UNet as ModUNet  # noqa: E402
 from models.model import UNet  # noqa: E402
 from utils.trainer import Trainer  # noqa: E402
 from utils.transforms import Compose, Resize, ToTensor  # noqa: E402
@@ -44,7 +48,9 @@ def get_parser(argv=None):
         p.add_argument(f, action="store_true")
     p.add_argument("--mixup_alpha", type=float, default=0.2)
     p.add_argument("--mixup_prob", type=float, default=0.3)
-    p.add_argument("--model_type", default="UNet", type=str)
+    p.add_argument("--model_type", default="UNet", type=str, help="UNet | ModUNet | ResUNet")
+    p.add_argument("--base_filters", default=64, type=int, help="ModUNet / ResUNet (mod.py:13)")
+    p.add_argument("--depth", default=5, type=int, help="ModUNet / ResUNet (mod.py:14)")
     p.add_argument("--bce_ratio", type=float, default=1)
     p.add_argument("--dice_ratio", type=float, default=0)
     p.add_argument("--focal_ratio", type=float, default=1)
@@ -76,8 +82,9 @@ def main(args):
     if torch.cuda.is_available():
         config.device = torch.device("cuda", torch.cuda.current_device())
     logger = create_logger(os.path.join(config.log_dir, "train_log.log"))
-    if args.model_type != "UNet":
-        raise SystemExit(f"model_type {args.model_type!r}: only the models/model.py UNet has a HIP path")
+    if args.model_type not in ("UNet", "ModUNet", "ResUNet"):
+        raise SystemExit(f"model_type {args.model_type!r}: the HIP path has UNet (models/model.py), "
+                         "ModUNet and ResUNet (models/mod.py)")
     if args.use_elastic or args.use_speckle or args.use_tgc or args.use_clahe:
         raise SystemExit("ultrasound augmentations need OpenCV/torchvision (not in this image)")
 
@@ -99,7 +106,12 @@ def main(args):
         else:
             loaders.append(create_dataloader(ds, config, shuffle=(i != 1)))
 
-    model = UNet()
+    if args.model_type == "ResUNet":
+        model = ResUNet(base_filters=args.base_filters, depth=args.depth)
+    elif args.model_type == "ModUNet":
+        model = ModUNet(base_filters=args.base_filters, depth=args.depth)
+    else:
+        model = UNet()
     if config.checkpoint_path and os.path.isfile(config.checkpoint_path):
         model.load_state_dict(torch.load(config.checkpoint_path, weights_only=True))
     n = sum(p.numel() for p in model.parameters() if p.requires_grad)

@@ -10,6 +10,6 @@ fallback: without the built library every entry point raises ``HipUnavailable``.
 """
 from ._lib import HipError, HipUnavailable, LIB_PATH, load  # noqa: F401
 from .functional import seg_losses  # noqa: F401
-from .module import ModUNet, UNet  # noqa: F401
+from .module import ModUNet, ResUNet, UNet  # noqa: F401
 from .optim import HipAdamW  # noqa: F401
 from .runtime import UNetRuntime  # noqa: F401

@@ -43,6 +43,7 @@ class UnetCfg(ctypes.Structure):
 
 VARIANT_MODEL = 0  # models/model.py:UNet
 VARIANT_MOD = 1    # models/mod.py:UNet
+VARIANT_RES = 2    # models/mod.py:ResUNet
 MATH_F32 = 0       # conv GEMMs on f32 MFMA (exact f32 products)
 MATH_BF16 = 1      # conv GEMMs on bf16 MFMA, f32 accumulate (BASELINE config 4)
 

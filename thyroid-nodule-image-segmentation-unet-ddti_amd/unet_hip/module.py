@@ -2,6 +2,7 @@
 
 * ``UNet``    -- models/model.py:5-73
 * ``ModUNet`` -- models/mod.py:9-66 (``UNet(in, out, base_filters, depth)``)
+* ``ResUNet`` -- models/mod.py:71-131 (residual blocks; what the reference main.py:122 builds)
 
 Each keeps its reference's exact submodule tree (model.py: encoder1..4, middle,
 decoder3..1, final; mod.py: encoders, pools, bottleneck, upconvs, decoders, final_conv;
@@ -238,3 +239,51 @@ class ModUNet(_HipUNet):
     def _native_cfg(self):
         return (self.in_channels, self.out_channels, _lib.VARIANT_MOD, self.base_filters,
                 self.depth, _lib.MATH_BF16 if self.mfma_dtype == "bf16" else _lib.MATH_F32)
+
+
+class _ResidualBlock(nn.Module):
+    # models/mod.py:71-86 (module tree only; the block runs natively)
+    def __init__(self, in_ch, out_ch):
+        super().__init__()
+        self.conv = nn.Sequential(
+            nn.Conv2d(in_ch, out_ch, 3, padding=1, bias=False), nn.BatchNorm2d(out_ch),
+            nn.ReLU(inplace=True),
+            nn.Conv2d(out_ch, out_ch, 3, padding=1, bias=False), nn.BatchNorm2d(out_ch))
+        self.skip = nn.Conv2d(in_ch, out_ch, 1, bias=False)
+        self.relu = nn.ReLU(inplace=True)
+
+
+class ResUNet(_HipUNet):
+    """models/mod.py:88-131 ``ResUNet(in_channels, out_channels, base_filters, depth)``:
+    every block is ReLU(conv(x) + skip(x)) with conv = Conv-BN-ReLU-Conv-BN and a bias-free
+    1x1 skip.  Same support limits as ``ModUNet`` (f32 GEMMs)."""
+
+    _name = "models.mod.ResUNet"
+
+    def __init__(self, in_channels=1, out_channels=1, base_filters=64, depth=5, **kwargs):
+        super().__init__()
+        self.in_channels, self.out_channels = in_channels, out_channels
+        self.base_filters, self.depth = base_filters, depth
+        # construction (and RNG) order of mod.py:96-115
+        self.encoders = nn.ModuleList()
+        self.pools = nn.ModuleList()
+        prev = in_channels
+        channels = [base_filters * (2 ** i) for i in range(depth)]
+        for ch in channels:
+            self.encoders.append(_ResidualBlock(prev, ch))
+            self.pools.append(nn.MaxPool2d(2, 2))
+            prev = ch
+        self.bottleneck = _ResidualBlock(prev, prev * 2)
+        self.upconvs = nn.ModuleList()
+        self.decoders = nn.ModuleList()
+        prev = channels[-1] * 2
+        for ch in channels[::-1]:
+            self.upconvs.append(nn.ConvTranspose2d(prev, ch, 2, 2))
+            self.decoders.append(_ResidualBlock(prev, ch))
+            prev = ch
+        self.final_conv = nn.Conv2d(base_filters, out_channels, 1)
+        self._state = None
+
+    def _native_cfg(self):
+        return (self.in_channels, self.out_channels, _lib.VARIANT_RES, self.base_filters,
+                self.depth, _lib.MATH_F32)
