@@ -25,6 +25,8 @@
  *                                                           _single_tensor_adam, decoupled wd)
  *   unet_mask_counts                utils/trainer.py:217,236-242  sigmoid(x)>0.5 masks and
  *                                                           TP/FP/FN/TN counts
+ *   unet_resize_plan / unet_resize_u8  utils/transforms.py:143-156 Resize + ToTensor of the
+ *                                   data loader (data/data_loader.py:20-27), on the device
  *   unet_bucket_* / unet_stream_wait_bucket   utils/trainer.py:28-30 nn.DataParallel grad
  *                                   reduction -> per-bucket readiness for an RCCL all-reduce
  *                                   overlapped with the rest of the backward pass
@@ -155,6 +157,20 @@ int unet_num_buckets(const unet_ctx* ctx, int* n);
 int unet_bucket_range(const unet_ctx* ctx, int b, int64_t* offset, int64_t* len);
 /* Make `stream` wait (device-side) until bucket b of the last backward is complete. */
 int unet_stream_wait_bucket(unet_ctx* ctx, int b, unet_stream_t stream);
+
+/* Input pipeline (data/data_loader.py:20-27 + utils/transforms.py:143-156): the reference
+ * resizes every PIL image and mask with TF.resize (= Pillow Image.resize(size, BILINEAR))
+ * and scales with TF.to_tensor (float(u8) / 255).  unet_resize_plan is a HOST function:
+ * Pillow's resampling coefficients (22-bit fixed point) and source bounds for one axis,
+ * coeffs[out_size * ksize], bounds[2 * out_size] = {first, count}; pass coeffs = bounds =
+ * NULL to get *ksize only.  unet_resize_u8 resizes one (h, w) uint8 image on the device
+ * into dst (oh, ow) fp32, divided by `divisor` (255 for ToTensor), bit-identical to
+ * Pillow + torch; kh/bh (width: w -> ow) and kv/bv (height: h -> oh) are device copies of the
+ * plans (ignored for an axis whose size does not change). */
+int unet_resize_plan(int in_size, int out_size, int32_t* coeffs, int32_t* bounds, int* ksize);
+int unet_resize_u8(unet_ctx* ctx, const uint8_t* src, int h, int w, float* dst, int oh, int ow,
+                   const int32_t* kh, const int32_t* bh, int ksh, const int32_t* kv,
+                   const int32_t* bv, int ksv, float divisor, unet_stream_t stream);
 
 /* Per-kernel timing: when enabled, unet_forward/unet_backward bracket every launch with
  * HIP events; unet_timing_read synchronises and returns, per kernel family, the launch

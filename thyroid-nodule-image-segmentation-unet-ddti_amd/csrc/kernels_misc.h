@@ -50,6 +50,10 @@ int k_res_bwd_prep(float* d, const float* out, int ldo, int offo, const float* z
                    float* partial, int G, hipStream_t s);
 int k_res_first_wgrad(const float* x, const float* du, int P, int C, float* partial, int G,
                       float* gw, hipStream_t s);
+// Pillow-exact 8-bit bilinear resize + scale (input pipeline, utils/transforms.py:143-156)
+int k_resize_u8(const uint8_t* src, int H, int W, float* dst, int OH, int OW, const int* kh,
+                const int* bh, int ksh, const int* kv, const int* bv, int ksv, int need_h,
+                int need_v, float divisor, hipStream_t s);
 int k_loss_fwd(const float* x, const float* t, int N, int64_t per, float* stats, float* losses,
                float alpha, float beta, float gamma, hipStream_t s);
 int k_loss_bwd(const float* x, const float* t, int N, int64_t per, const float* stats,

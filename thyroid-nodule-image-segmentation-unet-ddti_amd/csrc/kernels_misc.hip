@@ -1081,3 +1081,61 @@ int k_fill(float* p, int64_t n, float v, hipStream_t s) {
     hipLaunchKernelGGL(fill_kernel, dim3(grid_for(n)), dim3(256), 0, s, p, n, v);
     LAUNCH_CHECK();
 }
+
+// -------------------------------------------------------------------------------------
+// Input pipeline: PIL-exact bilinear resize of a uint8 image + ToTensor scaling
+// (utils/transforms.py:143-156: TF.resize on a PIL image = Image.resize(size, BILINEAR),
+// then TF.to_tensor = float(u8) / 255).  Pillow's 8-bit resampler (libImaging/Resample.c)
+// is two separable passes with fixed-point coefficients (22 fraction bits) and a clip to
+// uint8 after EACH pass, horizontal first.  One thread per output pixel recomputes the
+// horizontal-pass values of the rows it needs (identical integers to Pillow's temporary
+// image), so the result is bit-exact.  Coefficients / bounds come from the host
+// (runtime.hip: pil_resample_plan), in Pillow's layout: k[out][ksize], b[out] = {min, n}.
+// -------------------------------------------------------------------------------------
+namespace {
+constexpr int PIL_PRECISION_BITS = 32 - 8 - 2;
+
+__device__ __forceinline__ int pil_clip8(int v) {
+    if (v >= (1 << PIL_PRECISION_BITS << 8)) return 255;
+    if (v <= 0) return 0;
+    return v >> PIL_PRECISION_BITS;
+}
+
+__global__ void resize_u8_pil_kernel(const uint8_t* __restrict__ src, int H, int W,
+                                     float* __restrict__ dst, int OH, int OW,
+                                     const int* __restrict__ kh, const int* __restrict__ bh, int ksh,
+                                     const int* __restrict__ kv, const int* __restrict__ bv, int ksv,
+                                     int need_h, int need_v, float divisor) {
+    const int64_t n = (int64_t)OH * OW;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int yy = (int)(i / OW), xx = (int)(i % OW);
+        // horizontal pass value of source row y at output column xx
+        auto hval = [&](int y) -> int {
+            if (!need_h) return src[(int64_t)y * W + xx];
+            const int xmin = bh[2 * xx], xn = bh[2 * xx + 1];
+            int ss = 1 << (PIL_PRECISION_BITS - 1);
+            for (int x = 0; x < xn; ++x) ss += (int)src[(int64_t)y * W + xmin + x] * kh[xx * ksh + x];
+            return pil_clip8(ss);
+        };
+        int v;
+        if (need_v) {
+            const int ymin = bv[2 * yy], yn = bv[2 * yy + 1];
+            int ss = 1 << (PIL_PRECISION_BITS - 1);
+            for (int y = 0; y < yn; ++y) ss += hval(ymin + y) * kv[yy * ksv + y];
+            v = pil_clip8(ss);
+        } else {
+            v = hval(yy);
+        }
+        dst[i] = (float)v / divisor;  // TF.to_tensor divides (torch div), not x * (1/255)
+    }
+}
+}  // namespace
+
+int k_resize_u8(const uint8_t* src, int H, int W, float* dst, int OH, int OW, const int* kh,
+                const int* bh, int ksh, const int* kv, const int* bv, int ksv, int need_h,
+                int need_v, float divisor, hipStream_t s) {
+    hipLaunchKernelGGL(resize_u8_pil_kernel, dim3(grid_for((int64_t)OH * OW)), dim3(256), 0, s, src,
+                       H, W, dst, OH, OW, kh, bh, ksh, kv, bv, ksv, need_h, need_v, divisor);
+    LAUNCH_CHECK();
+}

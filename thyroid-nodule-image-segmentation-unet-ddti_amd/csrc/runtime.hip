@@ -1173,6 +1173,47 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
     return 0;
 }
 
+// Pillow's precompute_coeffs + normalize_coeffs_8bpc (libImaging/Resample.c) for the
+// BILINEAR filter (support 1) over the full source extent [0, in_size): same double
+// arithmetic in the same order, then the 22-bit fixed-point conversion.
+int pil_resample_plan(int in_size, int out_size, int32_t* kk, int32_t* bounds) {
+    const double in0 = 0.0, in1 = (double)(float)in_size;
+    double filterscale, scale;
+    filterscale = scale = (double)(in1 - in0) / out_size;
+    if (filterscale < 1.0) filterscale = 1.0;
+    const double support = 1.0 * filterscale;
+    const int ksize = (int)ceil(support) * 2 + 1;
+    if (!kk || !bounds) return ksize;
+    std::vector<double> k(ksize);
+    for (int xx = 0; xx < out_size; ++xx) {
+        const double center = in0 + (xx + 0.5) * scale;
+        double ww = 0.0;
+        const double ss = 1.0 / filterscale;
+        int xmin = (int)(center - support + 0.5);
+        if (xmin < 0) xmin = 0;
+        int xmax = (int)(center + support + 0.5);
+        if (xmax > in_size) xmax = in_size;
+        xmax -= xmin;
+        int x = 0;
+        for (; x < xmax; ++x) {
+            double a = (x + xmin - center + 0.5) * ss;
+            if (a < 0.0) a = -a;
+            const double w = a < 1.0 ? 1.0 - a : 0.0;
+            k[x] = w;
+            ww += w;
+        }
+        for (x = 0; x < xmax; ++x)
+            if (ww != 0.0) k[x] /= ww;
+        for (; x < ksize; ++x) k[x] = 0;
+        for (x = 0; x < ksize; ++x)
+            kk[(int64_t)xx * ksize + x] = k[x] < 0 ? (int32_t)(-0.5 + k[x] * (1 << (32 - 8 - 2)))
+                                                   : (int32_t)(0.5 + k[x] * (1 << (32 - 8 - 2)));
+        bounds[2 * xx] = xmin;
+        bounds[2 * xx + 1] = xmax;
+    }
+    return ksize;
+}
+
 bool shape_ok(const unet_ctx* c, int N, int H, int W) {
     const int q = 1 << std::max(c->depth, 4);  // every level even; >= 16 (model.py contract)
     return N >= 1 && H >= q && W >= q && H % q == 0 && W % q == 0;
@@ -1408,6 +1449,25 @@ int unet_timing_read(unet_ctx* c, int i, const char** family, int64_t* launches,
     if (total_ms) *total_ms = ms;
     if (flop) *flop = t.flop;
     return UNET_OK;
+}
+
+int unet_resize_plan(int in_size, int out_size, int32_t* coeffs, int32_t* bounds, int* ksize) {
+    if (in_size < 1 || out_size < 1 || !ksize) return UNET_ERR_INVALID;
+    *ksize = pil_resample_plan(in_size, out_size, coeffs, bounds);
+    return UNET_OK;
+}
+
+int unet_resize_u8(unet_ctx* c, const uint8_t* src, int h, int w, float* dst, int oh, int ow,
+                   const int32_t* kh, const int32_t* bh, int ksh, const int32_t* kv,
+                   const int32_t* bv, int ksv, float divisor, unet_stream_t stream) {
+    if (!c || !src || !dst || h < 1 || w < 1 || oh < 1 || ow < 1 || !(divisor > 0.f))
+        return UNET_ERR_INVALID;
+    const int need_h = ow != w, need_v = oh != h;
+    if ((need_h && (!kh || !bh || ksh < 1)) || (need_v && (!kv || !bv || ksv < 1)))
+        return fail(c, UNET_ERR_INVALID, "resize: missing coefficient tables");
+    int r = k_resize_u8(src, h, w, dst, oh, ow, kh, bh, ksh, kv, bv, ksv, need_h, need_v, divisor,
+                        (hipStream_t)stream);
+    return r ? fail(c, UNET_ERR_HIP, "resize launch %d", r) : UNET_OK;
 }
 
 int unet_debug_view(unet_ctx* c, int N, int H, int W, int training, int kind, int index,

@@ -5,6 +5,11 @@
 plain DataLoader (:29-33).  ``SyntheticSegmentation`` provides device-free synthetic
 batches (images in [0, 1), binary nodule-like disc masks) for benchmarks and tests, since
 the DDTI data is not distributed with the code.
+
+Device-side transforms: ``MedicalDataset(..., transform=DecodeU8())`` + ``u8_collate``
+keep the host to JPEG decoding; ``DeviceResizeLoader`` then runs the reference's
+Resize + ToTensor (utils/transforms.py:143-156) on the GPU (unet_hip.GpuResizeToTensor,
+bit-identical to the Pillow path) and yields device batches.
 """
 import os
 from pathlib import Path
@@ -58,3 +63,33 @@ class SyntheticSegmentation(Dataset):
 def create_dataloader(dataset, config, shuffle):
     return DataLoader(dataset=dataset, batch_size=config.batch_size, shuffle=shuffle,
                       num_workers=config.num_workers)
+
+
+class DecodeU8:
+    """Transform that only decodes: (PIL image, PIL mask) -> two (H, W) uint8 arrays."""
+
+    def __call__(self, img, mask):
+        return (np.asarray(img.convert("L"), dtype=np.uint8),
+                np.asarray(mask.convert("L"), dtype=np.uint8))
+
+
+def u8_collate(batch):
+    """Keep variable-size uint8 planes as lists (resized on the device)."""
+    return [b[0] for b in batch], [b[1] for b in batch]
+
+
+class DeviceResizeLoader:
+    """Wraps a DataLoader of uint8 (image, mask) lists; yields (N, 1, H, W) fp32 device
+    batches resized + scaled on the GPU exactly like Resize + ToTensor."""
+
+    def __init__(self, loader, size, device="cuda"):
+        from unet_hip import GpuResizeToTensor
+        self.loader = loader
+        self.pipe = GpuResizeToTensor(size, device)
+
+    def __len__(self):
+        return len(self.loader)
+
+    def __iter__(self):
+        for imgs, masks in self.loader:
+            yield self.pipe(imgs, masks)

@@ -23,7 +23,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 if HERE not in sys.path:
     sys.path.insert(0, HERE)
 
-from data.data_loader import MedicalDataset, SyntheticSegmentation, create_dataloader  # noqa: E402
+from data.data_loader import (DecodeU8, DeviceResizeLoader, MedicalDataset,  # noqa: E402
+                              SyntheticSegmentation, create_dataloader, u8_collate)
 from models.mod import ResUNet  # noqa: E402
 from models.mod import UNet as ModUNet  # noqa: E402
 from models.model import UNet  # noqa: E402
@@ -50,6 +51,8 @@ def get_parser(argv=None):
     p.add_argument("--mixup_prob", type=float, default=0.3)
     p.add_argument("--model_type", default="UNet", type=str, help="UNet | ModUNet | ResUNet")
     p.add_argument("--base_filters", default=64, type=int, help="ModUNet / ResUNet (mod.py:13)")
+    p.add_argument("--gpu_transforms", action="store_true",
+                   help="decode on the host, Resize + ToTensor on the GPU (bit-identical)")
     p.add_argument("--depth", default=5, type=int, help="ModUNet / ResUNet (mod.py:14)")
     p.add_argument("--bce_ratio", type=float, default=1)
     p.add_argument("--dice_ratio", type=float, default=0)
@@ -89,22 +92,27 @@ def main(args):
         raise SystemExit("ultrasound augmentations need OpenCV/torchvision (not in this image)")
 
     S = args.image_size
+    gpu_tf = args.gpu_transforms and not args.synthetic
     if args.synthetic:
         splits = [SyntheticSegmentation(args.synthetic, S, seed=s) for s in range(3)]
     else:
-        tf = Compose([Resize((S, S)), ToTensor()])
+        tf = DecodeU8() if gpu_tf else Compose([Resize((S, S)), ToTensor()])
         root = config.dataset_path
         splits = [MedicalDataset(os.path.join(root, d), os.path.join(root, d + "_mask"), tf)
                   for d in ("train", "val", "test")]
-    sampler_kw = {}
     loaders = []
     for i, ds in enumerate(splits):
+        kw = dict(batch_size=config.batch_size, num_workers=config.num_workers)
+        if gpu_tf:
+            kw["collate_fn"] = u8_collate
         if world > 1:
-            sampler_kw = dict(sampler=torch.utils.data.distributed.DistributedSampler(ds, shuffle=(i != 1)))
-            loaders.append(torch.utils.data.DataLoader(ds, batch_size=config.batch_size,
-                                                       num_workers=config.num_workers, **sampler_kw))
+            kw["sampler"] = torch.utils.data.distributed.DistributedSampler(ds, shuffle=(i != 1))
+            dl = torch.utils.data.DataLoader(ds, **kw)
+        elif gpu_tf:
+            dl = torch.utils.data.DataLoader(ds, shuffle=(i != 1), **kw)
         else:
-            loaders.append(create_dataloader(ds, config, shuffle=(i != 1)))
+            dl = create_dataloader(ds, config, shuffle=(i != 1))
+        loaders.append(DeviceResizeLoader(dl, (S, S), config.device) if gpu_tf else dl)
 
     if args.model_type == "ResUNet":
         model = ResUNet(base_filters=args.base_filters, depth=args.depth)

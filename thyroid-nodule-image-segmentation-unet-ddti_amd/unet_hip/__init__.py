@@ -9,6 +9,7 @@ include/unet_hip.h); this package is the PyTorch-facing host side.  There is no 
 fallback: without the built library every entry point raises ``HipUnavailable``.
 """
 from ._lib import HipError, HipUnavailable, LIB_PATH, load  # noqa: F401
+from .data import GpuResizeToTensor  # noqa: F401
 from .functional import seg_losses  # noqa: F401
 from .module import ModUNet, ResUNet, UNet  # noqa: F401
 from .optim import HipAdamW  # noqa: F401

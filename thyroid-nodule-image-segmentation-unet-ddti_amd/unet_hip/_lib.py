@@ -75,6 +75,9 @@ SIGNATURES = {
     "unet_stream_wait_bucket": (c_int, [c_void_p, c_int, c_void_p]),
     "unet_debug_view": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, P(c_int64),
                                 P(c_int64), P(c_int), P(c_int)]),
+    "unet_resize_plan": (c_int, [c_int, c_int, c_void_p, c_void_p, P(c_int)]),
+    "unet_resize_u8": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p,
+                               c_void_p, c_int, c_void_p, c_void_p, c_int, c_float, c_void_p]),
     "unet_timing_enable": (c_int, [c_void_p, c_int]),
     "unet_timing_reset": (c_int, [c_void_p]),
     "unet_timing_count": (c_int, [c_void_p, P(c_int)]),

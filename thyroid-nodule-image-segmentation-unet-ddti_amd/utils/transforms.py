@@ -1,6 +1,8 @@
 """Paired (image, mask) transforms used by main.py (subset of the reference's
 utils/transforms.py).  ``Compose``, ``Resize`` and ``ToTensor`` behave like the
-reference's (:143-165: PIL bilinear/nearest resize, [0, 1] float tensors).  The ultrasound
+reference's (:143-165: ``TF.resize`` of both PIL images = Pillow BILINEAR, the mask
+included; [0, 1] float tensors).  ``unet_hip.GpuResizeToTensor`` does the same two steps
+on the device, bit-identically.  The ultrasound
 augmentations (Elastic, Speckle, TGC, CLAHE, Rotate, Flip, Brightness; :15-141) need
 OpenCV / torchvision, which are not part of this image, and are host-side data
 augmentation outside the accelerated path: constructing them raises NotImplementedError.
@@ -26,7 +28,8 @@ class Resize:
     def __call__(self, img, mask):
         from PIL import Image
         h, w = self.size
-        return img.resize((w, h), Image.BILINEAR), mask.resize((w, h), Image.NEAREST)
+        # TF.resize's default interpolation is BILINEAR for the mask too (soft targets)
+        return img.resize((w, h), Image.BILINEAR), mask.resize((w, h), Image.BILINEAR)
 
 
 class ToTensor:
