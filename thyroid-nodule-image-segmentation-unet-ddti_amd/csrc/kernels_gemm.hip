@@ -102,10 +102,12 @@ __device__ __forceinline__ int gather_src(int tap, int m, Pix q, int H, int W, b
 // ------------------------------------------------------------------------------------
 // Tile configuration of the row GEMM: block tile BM x BN, wave tile WM x WN (32x32 MFMA
 // accumulators), K-chunk BK, DBUF = two LDS images (one barrier per chunk).
-template <int BM_, int BN_, int WM_, int WN_, int BK_, bool DBUF_>
+// OCC = waves per SIMD the register allocation must allow (launch_bounds' second argument).
+template <int BM_, int BN_, int WM_, int WN_, int BK_, bool DBUF_, int OCC_ = 1>
 struct RowTile {
     static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, BK = BK_;
     static constexpr bool DBUF = DBUF_;
+    static constexpr int OCC = OCC_;
     static constexpr int WAVES = (BM / WM) * (BN / WN);
     static constexpr int THREADS = 64 * WAVES;
 };
@@ -115,7 +117,7 @@ struct RowTile {
 // weight image (p.bt16).  LDS rows are K-contiguous bf16 with an 8-element pad (80 B /
 // 144 B row stride: the 16 lanes of a ds_read_b128 phase hit disjoint banks).
 template <int AMODE, int AOP, int EMODE, class T, bool BF>
-__global__ __launch_bounds__(T::THREADS, 1) void rowgemm_kernel(RowGemmArgs p) {
+__global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_kernel(RowGemmArgs p) {
     constexpr bool AFFINE = AOP == OP_AFFINE || AOP == OP_AFFINE_RELU, ADZ = AOP == OP_DZ;
     constexpr bool ARELU = AOP == OP_AFFINE_RELU;
     constexpr int BM = T::BM, BN = T::BN, WM = T::WM, WN = T::WN, BK = T::BK;
@@ -446,14 +448,15 @@ __global__ __launch_bounds__(T::THREADS, 1) void rowgemm_kernel(RowGemmArgs p) {
 // Weight-gradient GEMM (reduction over pixels), same issue / compute / commit pipeline.
 // ------------------------------------------------------------------------------------
 // wgrad tile: block BM x BN, wave tile WM x WN, pixels per chunk BKP.
-template <int BM_, int BN_, int WM_, int WN_, int BKP_>
+template <int BM_, int BN_, int WM_, int WN_, int BKP_, int OCC_ = 1>
 struct WgTile {
     static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, BKP = BKP_;
     static constexpr int THREADS = 64 * (BM / WM) * (BN / WN);
+    static constexpr int OCC = OCC_;
 };
 
 template <int AMODE, int AOP, int BMODE, bool BDZ, class T>
-__global__ __launch_bounds__(T::THREADS, 1) void wgrad_kernel(WgradArgs p) {
+__global__ __launch_bounds__(T::THREADS, T::OCC) void wgrad_kernel(WgradArgs p) {
     constexpr bool AFFINE = AOP == OP_AFFINE || AOP == OP_AFFINE_RELU;
     constexpr bool ARELU = AOP == OP_AFFINE_RELU;
     constexpr int BM = T::BM, BN = T::BN, BKP = T::BKP, WM = T::WM, WN = T::WN;
@@ -837,9 +840,12 @@ using RowTile3 = RowTile<128, 128, 64, 64, 64, false>;
 using RowTile4 = RowTile<128, 128, 64, 64, 32, false>;
 using RowTile5 = RowTile<256, 128, 64, 64, 32, false>;
 using RowTile6 = RowTile<128, 128, 64, 64, 64, true>;  // bf16: 4 MFMA k-steps per barrier
+using RowTile7 = RowTile<128, 128, 64, 64, 32, false, 3>;  // 3 waves / SIMD
+using RowTile8 = RowTile<128, 64, 64, 32, 32, false, 3>;
+using RowTile9 = RowTile<128, 128, 64, 64, 16, true, 3>;
 #define ROWGEMM_TILES(X) \
     X(0, RowTile0) X(1, RowTile1) X(2, RowTile2) X(3, RowTile3) X(4, RowTile4) X(5, RowTile5) \
-    X(6, RowTile6)
+    X(6, RowTile6) X(7, RowTile7) X(8, RowTile8) X(9, RowTile9)
 
 template <int AMODE, int AOP, int EMODE, class T, bool BF>
 static int rowgemm_go(const RowGemmArgs& a, hipStream_t s) {
@@ -943,8 +949,11 @@ using WgTile2 = WgTile<128, 64, 64, 64, 32>;   // 2 waves
 using WgTile3 = WgTile<64, 128, 64, 64, 32>;   // 2 waves
 using WgTile4 = WgTile<64, 64, 32, 32, 32>;    // 4 waves, 32x32 per wave
 using WgTile5 = WgTile<128, 64, 64, 32, 32>;   // 4 waves
+using WgTile6 = WgTile<128, 128, 64, 64, 32, 3>;  // 3 waves / SIMD
+using WgTile7 = WgTile<64, 64, 32, 32, 32, 3>;
 #define WGRAD_TILES(X) \
-    X(0, WgTile0) X(1, WgTile1) X(2, WgTile2) X(3, WgTile3) X(4, WgTile4) X(5, WgTile5)
+    X(0, WgTile0) X(1, WgTile1) X(2, WgTile2) X(3, WgTile3) X(4, WgTile4) X(5, WgTile5) \
+    X(6, WgTile6) X(7, WgTile7)
 
 int wgrad_tile_dims(int tile, int* bm, int* bn, int* bkp) {
 #define WG_DIMS(id, T) \

@@ -332,7 +332,7 @@ WgradCfg wgrad_cfg(int CA, int tapsA, int CB, int tapsB, int64_t P, bool bf16) {
         const char* e = getenv("UNET_WGRAD_TILE_W");
         tw = e ? atoi(e) : 0;
         e = getenv("UNET_WGRAD_TILE_N");
-        tn = e ? atoi(e) : 4;
+        tn = e ? atoi(e) : 7;  // 64x64, 3 waves/SIMD (tools/gemm_tune: +1 % over w4)
         e = getenv("UNET_WGRAD16_TILE");
         t16 = e ? atoi(e) : 0;
     }
@@ -346,7 +346,7 @@ WgradCfg wgrad_cfg(int CA, int tapsA, int CB, int tapsB, int64_t P, bool bf16) {
         else if (CA % 64 == 0 && CB % 64 == 0 && (CA % 128 || CB % 128) && tn >= 0)
             w.tile = (CA % 128 == 0) ? 5 : (CB % 128 == 0 ? 3 : tn);
         else
-            w.tile = 4;
+            w.tile = 7;
         wgrad_tile_dims(w.tile, &w.bm, &w.bn, &w.bkp);
     }
     const int64_t tiles = (int64_t)(tapsA * CA / w.bm) * (tapsB * CB / w.bn);
@@ -511,23 +511,34 @@ struct Launcher {
 // UNET_TILE_N128 / UNET_TILE_N64 override the choice (tuning runs).
 // Defaults from tools/gemm_tune (r01): forward-type ops 128x128/BK32 single LDS image
 // (4 waves/SIMD), dgrad-type 128x128 double-buffered, N = 64 outputs 128x64.
+// Defaults from tools/gemm_tune (r01, 15 rounds, profiles/r01_gemm_tune.txt):
+//  * forward-type, N % 128 == 0: 128x128/BK32 single LDS image; at >= 2048 blocks the
+//    3-waves/SIMD variant (t7) is 2-4 % faster, below that its partial last round of
+//    blocks costs more than it gains (L3: 103 vs 125 TF/s), so t4;
+//  * dgrad-type, N % 128 == 0: double-buffered 128x128 (t0) except on the big grids
+//    (>= 4096 blocks) where the single-image t4 is 2-4 % faster;
+//  * N = 64 outputs: 128x64 (t1).
 // bf16 MFMA (UNET_TILE16_*): a chunk of 64 K per barrier (4 MFMA k-steps) by default.
-int pick_tile(int N, bool dgrad, bool bf16) {
+// UNET_TILE_* environment variables override (tuning runs; -1 = automatic).
+int pick_tile(int N, bool dgrad, bool bf16, int64_t M = 0) {
     static int t128 = -2, t128d = -2, t64 = -2, b128 = -2, b128d = -2, b64 = -2;
     if (t128 == -2) {
         auto env = [](const char* n, int d) {
             const char* e = getenv(n);
             return e ? atoi(e) : d;
         };
-        t128 = env("UNET_TILE_N128", 4);
-        t128d = env("UNET_TILE_N128_DGRAD", 0);
+        t128 = env("UNET_TILE_N128", -1);
+        t128d = env("UNET_TILE_N128_DGRAD", -1);
         t64 = env("UNET_TILE_N64", 1);
         b128 = env("UNET_TILE16_N128", 6);
         b128d = env("UNET_TILE16_N128_DGRAD", 6);
         b64 = env("UNET_TILE16_N64", 1);
     }
     if (bf16) return N % 128 == 0 ? (dgrad ? b128d : b128) : b64;
-    return N % 128 == 0 ? (dgrad ? t128d : t128) : t64;
+    if (N % 128) return t64;
+    const int64_t blocks = (M + 127) / 128 * (N / 128);
+    if (dgrad) return t128d >= 0 ? t128d : (blocks >= 4096 ? 4 : 0);
+    return t128 >= 0 ? t128 : (blocks >= 2048 ? 7 : 4);
 }
 
 std::string tlabel(const char* fam, int tile, int layer) {
@@ -688,7 +699,7 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
             g.bias = bias_ptr(prm, C.b);
             g.stats = p.stats;
             g.emode = c->bn_relu ? E_STATS : E_BIAS_RELU_STATS;
-            const int tile = pick_tile(C.cout, false, c->bf16);
+            const int tile = pick_tile(C.cout, false, c->bf16, M);
             int bm, bn, bk;
             rowgemm_tile_dims(tile, &bm, &bn, &bk);
             R = (int)((M + bm - 1) / bm);
@@ -727,7 +738,7 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
         g.bias = prm + T.b;
         g.cout = T.cout;
         g.emode = E_CONVT;
-        const int tile = pick_tile(T.cout, false, c->bf16);
+        const int tile = pick_tile(T.cout, false, c->bf16, 4 * (int64_t)g.M);  // grid N = 4 cout
         RUN(tlabel("convT_fwd", tile, 100 + k), 2.0 * g.M * g.N * g.K, launch_rowgemm(g, tile, s));
         return 0;
     };
@@ -765,7 +776,7 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
         g.offey = p.offy[i2];
         g.escale = p.scale[i2];
         g.eshift = p.shift[i2];
-        const int tile = pick_tile(CL.cout, false, false);
+        const int tile = pick_tile(CL.cout, false, false, M);
         RUN(tlabel("skip_fwd", tile, b), 2.0 * M * CL.cout * CL.cin, launch_rowgemm(g, tile, s));
         return 0;
     };
@@ -929,7 +940,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
                 }
                 g.stats = p.part;
             }
-            const int tile = pick_tile(C.cin, true, c->bf16);
+            const int tile = pick_tile(C.cin, true, c->bf16, P);
             int bm, bn, bk;
             rowgemm_tile_dims(tile, &bm, &bn, &bk);
             if (rows) *rows = (int)((P + bm - 1) / bm);
@@ -1010,7 +1021,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
             }
             g.stats = p.part;
         }
-        const int tile = pick_tile(T.cin, true, c->bf16);
+        const int tile = pick_tile(T.cin, true, c->bf16, Pin);
         int bm, bn, bk;
         rowgemm_tile_dims(tile, &bm, &bn, &bk);
         *rows = (int)((Pin + bm - 1) / bm);
@@ -1077,7 +1088,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
                 g.out = dx;
                 g.ldo = ldx;
                 g.emode = E_STORE;
-                const int tile = pick_tile(CL.cin, true, false);
+                const int tile = pick_tile(CL.cin, true, false, P);
                 RUN(tlabel("skip_dgrad", tile, b), 2.0 * P * CL.cin * CL.cout, launch_rowgemm(g, tile, s));
             }
             if ((rc = bn_finalize(i2, RED_G))) return rc;

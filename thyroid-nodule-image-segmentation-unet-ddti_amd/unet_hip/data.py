@@ -52,6 +52,8 @@ class GpuResizeToTensor:
 
     def resize(self, img, out=None):
         """One HxW uint8 image -> (oh, ow) fp32 in [0, 1] on the device."""
+        if isinstance(img, np.ndarray):  # PIL-backed arrays are read-only views
+            img = np.require(img, requirements=["C", "W"])
         t = torch.as_tensor(img)
         if t.dtype != torch.uint8 or t.dim() != 2:
             raise ValueError("expected an (H, W) uint8 image (decoded 'L' mode)")

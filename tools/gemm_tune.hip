@@ -61,9 +61,11 @@ int main(int argc, char** argv) {
         float* dz = dalloc((size_t)M * sh.Cout, 8, 1.f);
         const double flop = 2.0 * M * sh.Cout * 9.0 * sh.Cin;
         // forward (CONV3 + affine + stats) per tile, dgrad (CONV3 store) per tile
-        std::vector<std::vector<double>> best(2, std::vector<double>(6, 0));
+        const int NT = 10, NW = 8;
+        std::vector<std::vector<double>> best(2, std::vector<double>(NT, 0));
         for (int r = 0; r < rounds; ++r) {
-            for (int tile = 0; tile < 6; ++tile) {
+            for (int tile = 0; tile < NT; ++tile) {
+                if (tile == 6) continue;  // bf16-oriented BK64 tile
                 for (int op = 0; op < 2; ++op) {
                     RowGemmArgs g{};
                     g.H = sh.H; g.W = sh.W; g.M = M;
@@ -91,16 +93,16 @@ int main(int argc, char** argv) {
         }
         for (int op = 0; op < 2; ++op) {
             printf("%-20s %-5s", sh.name, op ? "dgrad" : "fwd");
-            for (int tile = 0; tile < 6; ++tile) printf("  t%d %6.1f", tile, best[op][tile]);
+            for (int tile = 0; tile < NT; ++tile) printf("  t%d %6.1f", tile, best[op][tile]);
             printf("\n");
         }
         // wgrad over the tile table
-        double wb[6] = {0, 0, 0, 0, 0, 0};
-        int wsplit[6] = {0, 0, 0, 0, 0, 0};
+        double wb[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        int wsplit[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         float* slab = nullptr;
         size_t slab_n = 0;
         for (int r = 0; r < rounds; ++r)
-            for (int v = 0; v < 6; ++v) {
+            for (int v = 0; v < NW; ++v) {
                 int bm, bn, bkp;
                 wgrad_tile_dims(v, &bm, &bn, &bkp);
                 if (sh.Cin % bm || sh.Cout % bn) continue;
@@ -133,7 +135,7 @@ int main(int argc, char** argv) {
                 wsplit[v] = splits;
             }
         printf("%-20s wgrad", sh.name);
-        for (int v = 0; v < 6; ++v) printf("  w%d/s%d %6.1f", v, wsplit[v], wb[v]);
+        for (int v = 0; v < NW; ++v) printf("  w%d/s%d %6.1f", v, wsplit[v], wb[v]);
         printf("\n");
         fflush(stdout);
         CK(hipFree(x)); CK(hipFree(w)); CK(hipFree(sc)); CK(hipFree(shf)); CK(hipFree(bias));
