@@ -12,9 +12,10 @@ inputs resident in HBM before the timed region.
                                     (BASELINE config 4; not the headline metric)
 
 Prints ONE JSON line on rank 0.  ``value`` = images/s of the whole job (sum over ranks,
-time = max over ranks).  ``roofline`` is for the dominant kernel (most GPU time in the
-timed region), from per-launch HIP events recorded on the launch stream inside the
-library: achieved = algorithmic FLOP of its launches / their summed duration.
+time = max over ranks).  ``roofline`` is for the dominant kernel (most GPU time in one extra untimed
+profiling step), from per-launch HIP events recorded on the launch stream inside the
+library around that kernel's launches in the timed region: achieved = algorithmic FLOP
+of its launches / their summed duration.
 ``cpu_baseline`` times the CPU oracle (oracle/unet_ref_cpu.py, a torch-CPU restatement
 of the reference's step) on a bounded sample (bs=4) on rank 0 only.
 """
@@ -50,6 +51,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=2)
     ap.add_argument("--verbose", action="store_true")
+    ap.add_argument("--timing", default="dominant", choices=("dominant", "all"),
+                    help="per-launch events in the timed region: around the dominant kernel "
+                         "only (default) or around every launch")
     return ap.parse_args()
 
 
@@ -177,7 +181,33 @@ def main():
     torch.cuda.synchronize()
 
     rt = model._state.rt
+
+    def aggregate(recs):
+        """label = family/kernel instance|layer -> per family, kernel instance, layer."""
+        fam, kern, layer = {}, {}, {}
+        for label, t_ms, flop in recs:
+            f, _, rest = label.partition("/")
+            k, _, li = rest.partition("|")
+            for d, key in ((fam, f), (kern, k or f), (layer, f"{f}|{li}" if li else None)):
+                if key is None:
+                    continue
+                e = d.setdefault(key, [0, 0.0, 0.0])
+                e[0] += 1
+                e[1] += t_ms
+                e[2] += flop
+        return fam, kern, layer
+
+    # 1. one untimed profiling step with an event pair around every launch: the per-kernel
+    #    breakdown and which kernel instance dominates the GPU time
     rt.timing(True)
+    step()
+    torch.cuda.synchronize()
+    fam, kern, layer = aggregate(rt.timing_records())
+    rt.timing(False)
+    dom = max(kern, key=lambda k: kern[k][1])
+    # 2. the timed region: events only around the dominant kernel's launches (so the
+    #    per-launch markers of ~400 other launches do not inflate the step time)
+    rt.timing(True, only=None if args.timing == "all" else f"/{dom}|")
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -200,21 +230,9 @@ def main():
     images = B * world * args.steps
     value = images / elapsed
     ms = 1000 * elapsed / args.steps
-
-    # per-kernel aggregation (label = family/kernel instance)
-    fam, kern, layer = {}, {}, {}
-    for label, t_ms, flop in recs:
-        f, _, rest = label.partition("/")
-        k, _, li = rest.partition("|")
-        for d, key in ((fam, f), (kern, k or f), (layer, f"{f}|{li}" if li else None)):
-            if key is None:
-                continue
-            e = d.setdefault(key, [0, 0.0, 0.0])
-            e[0] += 1
-            e[1] += t_ms
-            e[2] += flop
-    dom = max(kern, key=lambda k: kern[k][1])
-    n_l, t_l, f_l = kern[dom]
+    _, kern_t, _ = aggregate(recs)
+    prof_steps = 1
+    n_l, t_l, f_l = kern_t[dom]
     achieved = f_l / (t_l * 1e-3) / 1e12 if t_l > 0 else 0.0
     per_launch_flop = f_l / n_l
     pmc = load_pmc(dom)
@@ -226,7 +244,7 @@ def main():
                 "frac": round(achieved / peak, 4),
                 "traffic": pmc, "launches": n_l, "avg_launch_ms": round(t_l / n_l, 4),
                 "flop_per_launch": per_launch_flop,
-                "kernel_share_of_gpu_time": round(t_l / max(1e-9, sum(v[1] for v in kern.values())), 4),
+                "kernel_share_of_gpu_time": round(kern[dom][1] / max(1e-9, sum(v[1] for v in kern.values())), 4),
                 "step_conv_tflops": round(conv_flop / (ms * 1e-3) / 1e12, 3),
                 "step_conv_frac": round(conv_flop / (ms * 1e-3) / 1e12 / peak, 4)}
 
@@ -260,14 +278,14 @@ def main():
         if args.verbose:
             for k, (n, tm, fl) in sorted(fam.items(), key=lambda kv: -kv[1][1]):
                 tf = fl / (tm * 1e-3) / 1e12 if tm > 0 and fl > 0 else 0
-                print(f"  {k:22s} n={n:5d} {tm / args.steps:9.3f} ms/step  {tf:7.2f} TF/s",
+                print(f"  {k:22s} n={n:5d} {tm / prof_steps:9.3f} ms/step  {tf:7.2f} TF/s",
                       file=sys.stderr)
             for k, (n, tm, fl) in sorted(kern.items(), key=lambda kv: -kv[1][1])[:8]:
-                print(f"  [{k}] n={n} {tm / args.steps:.3f} ms/step", file=sys.stderr)
+                print(f"  [{k}] n={n} {tm / prof_steps:.3f} ms/step", file=sys.stderr)
             print("  per layer (conv i = 0..17, convT 100..103):", file=sys.stderr)
             for k, (n, tm, fl) in sorted(layer.items(), key=lambda kv: -kv[1][1]):
                 tf = fl / (tm * 1e-3) / 1e12 if tm > 0 else 0
-                print(f"    {k:18s} {tm / args.steps:8.3f} ms/step {tf:7.2f} TF/s", file=sys.stderr)
+                print(f"    {k:18s} {tm / prof_steps:8.3f} ms/step {tf:7.2f} TF/s", file=sys.stderr)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

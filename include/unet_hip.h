@@ -176,6 +176,9 @@ int unet_resize_u8(unet_ctx* ctx, const uint8_t* src, int h, int w, float* dst, 
  * HIP events; unet_timing_read synchronises and returns, per kernel family, the launch
  * count, total ms and algorithmic FLOP of the last call(s) since the last reset. */
 int unet_timing_enable(unet_ctx* ctx, int enable);
+/* Time only the launches whose label ("family/kernel|layer") contains `substring`
+ * (NULL or "" = every launch): keeps the event overhead off the rest of the step. */
+int unet_timing_filter(unet_ctx* ctx, const char* substring);
 int unet_timing_reset(unet_ctx* ctx);
 int unet_timing_count(unet_ctx* ctx, int* n_families);
 int unet_timing_read(unet_ctx* ctx, int i, const char** family, int64_t* launches,

@@ -96,6 +96,7 @@ struct unet_ctx {
     std::vector<hipEvent_t> bucket_ev;
     // timing
     bool timing = false;
+    std::string tfilter;  // time only launches whose label contains this (empty = all)
     std::vector<TimeRec> trec;
     std::vector<hipEvent_t> ev_pool;
     size_t ev_used = 0;
@@ -491,7 +492,8 @@ struct Launcher {
     template <class F>
     int run(const std::string& label, double flop, F&& f) {
         hipEvent_t a = nullptr, b = nullptr;
-        if (c->timing) {
+        const bool timed = c->timing && (c->tfilter.empty() || label.find(c->tfilter) != std::string::npos);
+        if (timed) {
             a = ev();
             b = ev();
             (void)hipEventRecord(a, s);
@@ -499,7 +501,7 @@ struct Launcher {
         int r = f();
         if (r != 0) return fail(c, UNET_ERR_HIP, "%s: launch failed (%d: %s)", label.c_str(), r,
                                 r > 0 ? hipGetErrorString((hipError_t)r) : "bad shape");
-        if (c->timing) {
+        if (timed) {
             (void)hipEventRecord(b, s);
             c->trec.push_back(TimeRec{label, a, b, flop});
         }
@@ -1432,6 +1434,12 @@ int unet_stream_wait_bucket(unet_ctx* c, int b, unet_stream_t stream) {
 int unet_timing_enable(unet_ctx* c, int en) {
     if (!c) return UNET_ERR_INVALID;
     c->timing = en != 0;
+    return UNET_OK;
+}
+
+int unet_timing_filter(unet_ctx* c, const char* substring) {
+    if (!c) return UNET_ERR_INVALID;
+    c->tfilter = substring ? substring : "";
     return UNET_OK;
 }
 

@@ -79,6 +79,7 @@ SIGNATURES = {
     "unet_resize_u8": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p,
                                c_void_p, c_int, c_void_p, c_void_p, c_int, c_float, c_void_p]),
     "unet_timing_enable": (c_int, [c_void_p, c_int]),
+    "unet_timing_filter": (c_int, [c_void_p, c_char_p]),
     "unet_timing_reset": (c_int, [c_void_p]),
     "unet_timing_count": (c_int, [c_void_p, P(c_int)]),
     "unet_timing_read": (c_int, [c_void_p, c_int, P(c_char_p), P(c_int64), P(c_double),

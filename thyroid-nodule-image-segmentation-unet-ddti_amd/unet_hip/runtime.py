@@ -132,8 +132,10 @@ class UNetRuntime:
         _lib.check(rc, self.ctx, "unet_stream_wait_bucket")
 
     # ------------------------------------------------------------------ timing
-    def timing(self, enable):
+    def timing(self, enable, only=None):
+        """Per-launch HIP-event timing; `only`: time just the labels containing it."""
         self.lib.unet_timing_enable(self.ctx, int(enable))
+        self.lib.unet_timing_filter(self.ctx, only.encode() if only else None)
         self.lib.unet_timing_reset(self.ctx)
 
     def timing_records(self):
