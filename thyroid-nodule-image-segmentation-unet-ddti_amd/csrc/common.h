@@ -71,6 +71,7 @@ struct RowGemmArgs {
     int ldey, offey;
     const float* escale;  // E_STORE_BN, BN -> ReLU order: affine of that BN (ReLU mask)
     const float* eshift;
+    int xcd;              // remap blocks so each XCD gets a contiguous range of tiles
 };
 
 struct WgradArgs {
@@ -92,6 +93,7 @@ struct WgradArgs {
     const float* bcoef;
     float* bias_slab;    // optional [splits][Nw]: column sums of B' (the bias gradient)
     int bf16;            // bf16 MFMA (operands rounded to bf16 in LDS, f32 accumulate)
+    int xcd;             // remap blocks so each XCD gets a contiguous range of tiles
 };
 
 #define HIP_OK(x)                                   \

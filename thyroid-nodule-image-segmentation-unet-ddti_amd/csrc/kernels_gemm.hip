@@ -48,6 +48,15 @@ struct Pix {
     int img, y, x;
 };
 
+// Blocks are dispatched round-robin over the 8 XCDs (block b -> XCD b % 8), each with its
+// own L2.  Give XCD x the contiguous logical tiles [x*n/8, (x+1)*n/8) instead, so tiles
+// that share input rows (3x3 halos, the taps and channel slices of one pixel range) hit
+// the same L2.
+__device__ __forceinline__ int xcd_remap(int b, int n) {
+    const int q = n >> 3, r = n & 7, x = b & 7, i = b >> 3;
+    return x < r ? x * (q + 1) + i : r * (q + 1) + (x - r) * q + i;
+}
+
 __device__ __forceinline__ Pix decode(int m, int H, int W) {
     Pix r;
     int t = m / W;
@@ -141,7 +150,8 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_kernel(RowGemmArgs
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave / WAVES_N, wn = wave % WAVES_N;
     const int ntn = p.N / BN;
-    const int tile_m = blockIdx.x / ntn, tile_n = blockIdx.x - tile_m * ntn;
+    const int bid = p.xcd ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+    const int tile_m = bid / ntn, tile_n = bid - tile_m * ntn;
     const int m0 = tile_m * BM, n0 = tile_n * BN;
     const int H = p.H, W = p.W;
 
@@ -474,7 +484,7 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void wgrad_kernel(WgradArgs p) 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave / WAVES_N, wn = wave % WAVES_N;
     const int tiles_n = p.Nw / BN, tiles_m = p.Mw / BM;
-    int idx = blockIdx.x;
+    int idx = p.xcd ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
     const int tn = idx % tiles_n;
     idx /= tiles_n;
     const int tm = idx % tiles_m;
@@ -662,7 +672,7 @@ __global__ __launch_bounds__(T::THREADS, 1) void wgrad16_kernel(WgradArgs p) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave / WAVES_N, wn = wave % WAVES_N;
     const int tiles_n = p.Nw / BN, tiles_m = p.Mw / BM;
-    int idx = blockIdx.x;
+    int idx = p.xcd ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
     const int tn = idx % tiles_n;
     idx /= tiles_n;
     const int tm = idx % tiles_m;

@@ -620,8 +620,22 @@ Operand conv_input(unet_ctx* c, Plan& p, int i) {
 
 const float* bias_ptr(const float* prm, int64_t off) { return off >= 0 ? prm + off : nullptr; }
 
+// XCD-aware block order for the GEMMs (UNET_XCD_REMAP: 0 none, 1 both, 2 row GEMMs only,
+// 3 wgrad only; A/B runs)
+int xcd_mode() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("UNET_XCD_REMAP");
+        v = e ? atoi(e) : 0;
+    }
+    return v;
+}
+int xcd_remap_on() { return xcd_mode() == 1 || xcd_mode() == 2; }
+int xcd_remap_wgrad() { return xcd_mode() == 1 || xcd_mode() == 3; }
+
 // weight image of a row GEMM: f32, or bf16 packed into the same slot (half its size)
 void set_weights(const unet_ctx* c, RowGemmArgs& g, const float* img) {
+    g.xcd = xcd_remap_on();
     if (c->bf16)
         g.bt16 = (const uint16_t*)img;
     else
@@ -769,6 +783,7 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
         g.C = CL.cin;
         g.amode = G_IDENT;
         g.bt = prm + c->skip_w[b];  // torch layout [co][ci] is already Bt[n][k]
+        g.xcd = xcd_remap_on();
         g.out = p.out[b];
         g.ldo = p.ldout[b];
         g.ooff = p.offout[b];
@@ -877,6 +892,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         Operand a = conv_input(c, p, i);
         WgradCfg wc = wgrad_cfg(C.cin, 9, C.cout, 1, P, c->bf16);
         WgradArgs w{};
+        w.xcd = xcd_remap_wgrad();
         w.H = Hl;
         w.W = Wl;
         w.P = (int)P;
@@ -961,6 +977,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         const int64_t Pin = p.P[T.in_level];
         WgradCfg wc = wgrad_cfg(T.cin, 1, T.cout, 4, Pin, c->bf16);
         WgradArgs w{};
+        w.xcd = xcd_remap_wgrad();
         w.H = Hi;
         w.W = Wi;
         w.P = (int)Pin;
@@ -1056,6 +1073,8 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
                 Operand a = conv_input(c, p, i1);
                 WgradCfg wc = wgrad_cfg(CL.cin, 1, CL.cout, 1, P, false);
                 WgradArgs w{};
+                w.xcd = xcd_remap_wgrad();
+        w.xcd = xcd_remap_wgrad();
                 w.H = H >> CL.level;
                 w.W = W >> CL.level;
                 w.P = (int)P;
@@ -1087,6 +1106,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
                 g.C = CL.cout;
                 g.amode = G_IDENT;
                 g.bt = p.pack + c->skip_pd[b];
+                g.xcd = xcd_remap_on();
                 g.out = dx;
                 g.ldo = ldx;
                 g.emode = E_STORE;
