@@ -325,3 +325,38 @@ def test_determinism_full_size():
                      m._state.grad_arena.clone()))
     assert torch.equal(outs[0][0], outs[1][0])
     assert torch.equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.parametrize("out_ch,B,H,W", [(2, 2, 64, 128), (1, 1, 48, 80), (4, 3, 32, 32)])
+def test_shapes_and_classes_vs_oracle(out_ch, B, H, W):
+    """Non-square images, batch 1, H/W multiples of 16 that are not powers of two, and the
+    multi-class head (models/model.py:6 out_channels; the losses flatten all classes like
+    models/loss.py:19-20).  Small images at batch 1 leave the deep BatchNorms a handful of
+    values per channel (15 at level 4 for 48x80), where a near-zero ReLU input flips under
+    any fp32 rounding change: gradients are judged against fp64 within 2x the fp32
+    oracle's own error over x and x * (1 + 1e-7) (as tests/test_gpu_res.py), floor 1e-2."""
+    import unet_hip
+    P = O.make_params(3, out_channels=out_ch)
+    x, _ = inputs(6, B, H, W)
+    t = (torch.rand(B, out_ch, H, W, generator=torch.Generator().manual_seed(1)) > 0.7).float()
+    ref = O.train_step(P, O.init_buffers(), None, x, t)
+    refp = O.train_step(P, O.init_buffers(), None, x * (1 + 1e-7), t)
+    r64 = O.train_step(_to64(P), _to64(O.init_buffers()), None, x.double(), t.double())
+    m = unet_hip.UNet(1, out_ch)
+    sd = m.state_dict()
+    for k, v in P.items():
+        sd[k] = v.clone()
+    m.load_state_dict(sd)
+    m = m.to(DEV).train()
+    logits = m(x.to(DEV))
+    assert logits.shape == (B, out_ch, H, W)
+    losses = unet_hip.seg_losses(logits, t.to(DEV))
+    (losses[0] + losses[1]).backward()
+    assert rel_max(logits.detach().cpu().numpy(), ref["logits"].numpy()) <= LOGIT_TOL
+    assert abs((losses[0] + losses[1]).item() - ref["loss"].item()) <= 1e-5
+    e32 = {k: max(norm_rel(g, r64["grads"][k]), norm_rel(refp["grads"][k], r64["grads"][k]))
+           for k, g in ref["grads"].items()}
+    env = max(2 * max(e32.values()), GRAD_TOL)
+    errs = grad_errors(m, r64["grads"])
+    worst = max(errs, key=errs.get)
+    assert errs[worst] <= env, f"{worst}: {errs[worst]:.3e} (fp32 oracle {e32[worst]:.3e})"
