@@ -23,6 +23,8 @@
 // four k values with one ds_read_b128: lane half h owns k = 4h..4h+3 and MFMA step s sums
 // k = s (h=0) and k = 4+s (h=1) -- A and B use the same permutation, so the product is the
 // same sum in a different order.
+#include <type_traits>
+
 #include "common.h"
 
 namespace {
@@ -645,29 +647,35 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void wgrad_kernel(WgradArgs p) 
 }
 
 // ------------------------------------------------------------------------------------
-// Weight-gradient GEMM on bf16 MFMA.  The MFMA operands need 8 consecutive PIXELS of one
-// channel per lane, so the loader works on 4-pixel x 4-channel units: four f32x4 loads (one
-// per pixel), the BN affine / ReLU / padding applied in f32, then a register transpose into
-// four 8-B rows of channel-major, pixel-contiguous bf16 LDS images ([BM][BKP+8] and
-// [BN][BKP+8]).  Bias column sums of B' are taken from the f32 values.
+// Weight-gradient GEMM with a channel-major LDS image ("transposed" loader).  The MFMA
+// operands of the pixel reduction are consecutive PIXELS of one channel per lane, so the
+// loader works on 4-pixel x 4-channel units: four f32x4 loads (one per pixel), the BN
+// affine / ReLU / padding applied in f32, then a register transpose into four 16-B
+// (f32) or 8-B (bf16) rows of channel-major, pixel-contiguous LDS images ([BM][BKP+pad]
+// and [BN][BKP+pad]).  f32 (BF = false): each lane then reads its 4 pixels of a k-group
+// with one ds_read_b128 and feeds 4 v_mfma_f32_32x32x2_f32 (the row GEMM's K permutation,
+// applied to both operands); bf16 (BF = true): 8 pixels, one v_mfma_f32_32x32x16_bf16.
+// Bias column sums of B' are taken from the f32 values.
 // ------------------------------------------------------------------------------------
-template <int AMODE, int AOP, int BMODE, class T>
-__global__ __launch_bounds__(T::THREADS, 1) void wgrad16_kernel(WgradArgs p) {
+template <int AMODE, int AOP, int BMODE, class T, bool BF>
+__global__ __launch_bounds__(T::THREADS, T::OCC) void wgradT_kernel(WgradArgs p) {
     constexpr bool AFFINE = AOP == OP_AFFINE || AOP == OP_AFFINE_RELU;
     constexpr bool ARELU = AOP == OP_AFFINE_RELU;
     constexpr int BM = T::BM, BN = T::BN, BKP = T::BKP, WM = T::WM, WN = T::WN;
     constexpr int NTH = T::THREADS;
     constexpr int WAVES_N = BN / WN;
-    constexpr int LDP = BKP + 8;                      // bf16 per LDS row (pixels)
+    constexpr int LDP = BF ? BKP + 8 : BKP + 4;       // LDS row (pixels) in elements
     constexpr int MT = WM / 32, NT = WN / 32;
     constexpr int AQ = BM / 4, BQ = BN / 4;           // channel quads
     constexpr int APQ = NTH / AQ, BPQ = NTH / BQ;     // pixel quads per pass
     constexpr int AP = (BKP / 4) / APQ, BP = (BKP / 4) / BPQ;
     static_assert(AP * APQ == BKP / 4 && BP * BPQ == BKP / 4 && AP >= 1 && BP >= 1, "loader");
-    constexpr int SMEM_F = ((BM + BN) * LDP + 1) / 2 > 8 * NTH ? ((BM + BN) * LDP + 1) / 2 : 8 * NTH;
+    using E = typename std::conditional<BF, __bf16, float>::type;
+    constexpr int IMG_F = BF ? ((BM + BN) * LDP + 1) / 2 : (BM + BN) * LDP;
+    constexpr int SMEM_F = IMG_F > 8 * NTH ? IMG_F : 8 * NTH;
     __shared__ __attribute__((aligned(16))) float smem[SMEM_F];
-    __bf16* As = (__bf16*)smem;
-    __bf16* Bs = As + BM * LDP;
+    E* As = (E*)smem;
+    E* Bs = As + BM * LDP;
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave / WAVES_N, wn = wave % WAVES_N;
@@ -747,9 +755,13 @@ __global__ __launch_bounds__(T::THREADS, 1) void wgrad16_kernel(WgradArgs p) {
             }
             const int pp = 4 * (apq + i * APQ);
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
-                *(bf16x4*)&As[(aq * 4 + j) * LDP + pp] =
-                    bf16x4{(__bf16)v[0][j], (__bf16)v[1][j], (__bf16)v[2][j], (__bf16)v[3][j]};
+            for (int j = 0; j < 4; ++j) {
+                if constexpr (BF)
+                    *(bf16x4*)&As[(aq * 4 + j) * LDP + pp] =
+                        bf16x4{(__bf16)v[0][j], (__bf16)v[1][j], (__bf16)v[2][j], (__bf16)v[3][j]};
+                else
+                    *(f32x4*)&As[(aq * 4 + j) * LDP + pp] = f32x4{v[0][j], v[1][j], v[2][j], v[3][j]};
+            }
         }
 #pragma unroll
         for (int i = 0; i < BP; ++i) {
@@ -764,9 +776,13 @@ __global__ __launch_bounds__(T::THREADS, 1) void wgrad16_kernel(WgradArgs p) {
             }
             const int pp = 4 * (bpq + i * BPQ);
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
-                *(bf16x4*)&Bs[(bq * 4 + j) * LDP + pp] =
-                    bf16x4{(__bf16)v[0][j], (__bf16)v[1][j], (__bf16)v[2][j], (__bf16)v[3][j]};
+            for (int j = 0; j < 4; ++j) {
+                if constexpr (BF)
+                    *(bf16x4*)&Bs[(bq * 4 + j) * LDP + pp] =
+                        bf16x4{(__bf16)v[0][j], (__bf16)v[1][j], (__bf16)v[2][j], (__bf16)v[3][j]};
+                else
+                    *(f32x4*)&Bs[(bq * 4 + j) * LDP + pp] = f32x4{v[0][j], v[1][j], v[2][j], v[3][j]};
+            }
         }
     };
 
@@ -786,19 +802,40 @@ __global__ __launch_bounds__(T::THREADS, 1) void wgrad16_kernel(WgradArgs p) {
     }
     for (int c = 0; c < nchunks; ++c) {
         if (c + 1 < nchunks) issue(pbeg + (c + 1) * BKP);
+        if constexpr (BF) {
 #pragma unroll
-        for (int kk = 0; kk < BKP / 16; ++kk) {
-            bf16x8 af[MT], bf[NT];
+            for (int kk = 0; kk < BKP / 16; ++kk) {
+                bf16x8 af[MT], bf[NT];
 #pragma unroll
-            for (int mt = 0; mt < MT; ++mt)
-                af[mt] = *(const bf16x8*)&As[(wm * WM + mt * 32 + li) * LDP + kk * 16 + lh * 8];
+                for (int mt = 0; mt < MT; ++mt)
+                    af[mt] = *(const bf16x8*)&As[(wm * WM + mt * 32 + li) * LDP + kk * 16 + lh * 8];
 #pragma unroll
-            for (int nt = 0; nt < NT; ++nt)
-                bf[nt] = *(const bf16x8*)&Bs[(wn * WN + nt * 32 + li) * LDP + kk * 16 + lh * 8];
+                for (int nt = 0; nt < NT; ++nt)
+                    bf[nt] = *(const bf16x8*)&Bs[(wn * WN + nt * 32 + li) * LDP + kk * 16 + lh * 8];
 #pragma unroll
-            for (int mt = 0; mt < MT; ++mt)
+                for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-                for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma32_bf16(af[mt], bf[nt], acc[mt][nt]);
+                    for (int nt = 0; nt < NT; ++nt)
+                        acc[mt][nt] = mfma32_bf16(af[mt], bf[nt], acc[mt][nt]);
+            }
+        } else {
+#pragma unroll
+            for (int kk = 0; kk < BKP / 8; ++kk) {
+                f32x4 af[MT], bf[NT];
+#pragma unroll
+                for (int mt = 0; mt < MT; ++mt)
+                    af[mt] = *(const f32x4*)&As[(wm * WM + mt * 32 + li) * LDP + kk * 8 + lh * 4];
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt)
+                    bf[nt] = *(const f32x4*)&Bs[(wn * WN + nt * 32 + li) * LDP + kk * 8 + lh * 4];
+#pragma unroll
+                for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+                    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                        for (int nt = 0; nt < NT; ++nt)
+                            acc[mt][nt] = mfma32(af[mt][s4], bf[nt][s4], acc[mt][nt]);
+            }
         }
         __syncthreads();
         if (c + 1 < nchunks) {
@@ -966,6 +1003,7 @@ using WgTile7 = WgTile<64, 64, 32, 32, 32, 3>;
     X(6, WgTile6) X(7, WgTile7)
 
 int wgrad_tile_dims(int tile, int* bm, int* bn, int* bkp) {
+    if (tile == 10 || tile == 15) return wgrad16_tile_dims(tile - 10, bm, bn, bkp);
 #define WG_DIMS(id, T) \
     if (tile == id) {  \
         *bm = T::BM;   \
@@ -993,14 +1031,18 @@ static int wgrad_tile(const WgradArgs& a, int tile, hipStream_t s) {
     return -1;
 }
 
-// bf16 wgrad tiles (wgrad16_kernel): 4-pixel x 4-channel loader units
+// channel-major wgrad tiles (wgradT_kernel; bf16 ids 0.., f32 ids 10..): 4-pixel x
+// 4-channel loader units
 using Wg16Tile0 = WgTile<128, 128, 64, 64, 32>;
 using Wg16Tile1 = WgTile<128, 128, 64, 64, 64>;
 using Wg16Tile2 = WgTile<64, 64, 32, 32, 64>;
 using Wg16Tile3 = WgTile<128, 64, 64, 32, 64>;
 using Wg16Tile4 = WgTile<64, 128, 32, 64, 64>;
+using Wg16Tile5 = WgTile<128, 128, 64, 64, 32, 2>;
+using Wg16Tile6 = WgTile<64, 64, 32, 32, 64, 3>;
 #define WGRAD16_TILES(X) \
-    X(0, Wg16Tile0) X(1, Wg16Tile1) X(2, Wg16Tile2) X(3, Wg16Tile3) X(4, Wg16Tile4)
+    X(0, Wg16Tile0) X(1, Wg16Tile1) X(2, Wg16Tile2) X(3, Wg16Tile3) X(4, Wg16Tile4) \
+    X(5, Wg16Tile5) X(6, Wg16Tile6)
 
 int wgrad16_tile_dims(int tile, int* bm, int* bn, int* bkp) {
 #define WG16_DIMS(id, T) \
@@ -1015,20 +1057,32 @@ int wgrad16_tile_dims(int tile, int* bm, int* bn, int* bkp) {
     return -1;
 }
 
-template <int AMODE, int AOP, int BMODE>
-static int wgrad16_tile(const WgradArgs& a, int tile, hipStream_t s) {
-#define WG16_CASE(id, T)                                                                      \
+#define WGT_CASE(id, T, BF)                                                                   \
     if (tile == id) {                                                                         \
         if (a.Mw % T::BM || a.Nw % T::BN || a.CA % T::BM || a.CB % T::BN || a.pps % T::BKP) \
             return -1;                                                                        \
         const dim3 grid((a.Mw / T::BM) * (a.Nw / T::BN) * a.splits);                          \
-        hipLaunchKernelGGL((wgrad16_kernel<AMODE, AOP, BMODE, T>), grid, dim3(T::THREADS), 0, s, a); \
+        hipLaunchKernelGGL((wgradT_kernel<AMODE, AOP, BMODE, T, BF>), grid, dim3(T::THREADS), 0, s, a); \
         return (int)hipGetLastError();                                                        \
     }
-    WGRAD16_TILES(WG16_CASE)
-#undef WG16_CASE
+#define WG16_CASE(id, T) WGT_CASE(id, T, true)
+#define WG32_CASE(id, T) WGT_CASE(id, T, false)
+// f32 channel-major tiles: measured ~3% below the pixel-major wgrad_kernel on every
+// layer shape (tools/gemm_tune), kept as a tuner/env alternative (ids 10 + t)
+#define WGRADT32_TILES(X) X(0, Wg16Tile0) X(5, Wg16Tile5)
+
+template <int AMODE, int AOP, int BMODE, bool BF>
+static int wgradT_tile(const WgradArgs& a, int tile, hipStream_t s) {
+    if constexpr (BF) {
+        WGRAD16_TILES(WG16_CASE)
+    } else {
+        WGRADT32_TILES(WG32_CASE)
+    }
     return -1;
 }
+#undef WG16_CASE
+#undef WG32_CASE
+#undef WGT_CASE
 
 int launch_wgrad(const WgradArgs& a, int tile, hipStream_t s) {
     if (a.P < 1) return -1;
@@ -1036,15 +1090,31 @@ int launch_wgrad(const WgradArgs& a, int tile, hipStream_t s) {
         const bool aff = a.ascale != nullptr;
         if (a.bcoef || (a.arelu && !aff) || (aff && !a.arelu)) return -1;
         if (a.amode == G_CONV3 && a.bmode == G_IDENT)
-            return aff ? wgrad16_tile<G_CONV3, OP_AFFINE_RELU, G_IDENT>(a, tile, s)
-                       : wgrad16_tile<G_CONV3, OP_PLAIN, G_IDENT>(a, tile, s);
+            return aff ? wgradT_tile<G_CONV3, OP_AFFINE_RELU, G_IDENT, true>(a, tile, s)
+                       : wgradT_tile<G_CONV3, OP_PLAIN, G_IDENT, true>(a, tile, s);
         if (a.amode == G_IDENT && a.bmode == G_UP2 && aff)
-            return wgrad16_tile<G_IDENT, OP_AFFINE_RELU, G_UP2>(a, tile, s);
+            return wgradT_tile<G_IDENT, OP_AFFINE_RELU, G_UP2, true>(a, tile, s);
         return -1;
     }
     const bool aff = a.ascale != nullptr, dz = a.bcoef != nullptr;
     if (a.arelu && !aff) return -1;
     if (a.arelu && dz) return -1;  // OP_DZ loaders are the ReLU -> BN order only
+    if (tile >= 10 && !dz) {  // f32, channel-major LDS image (wgradT_kernel)
+        const int t = tile - 10;
+        if (a.amode == G_CONV3 && a.bmode == G_IDENT) {
+            if (a.arelu) return wgradT_tile<G_CONV3, OP_AFFINE_RELU, G_IDENT, false>(a, t, s);
+            return aff ? wgradT_tile<G_CONV3, OP_AFFINE, G_IDENT, false>(a, t, s)
+                       : wgradT_tile<G_CONV3, OP_PLAIN, G_IDENT, false>(a, t, s);
+        }
+        if (a.amode == G_IDENT && a.bmode == G_UP2) {
+            if (a.arelu) return wgradT_tile<G_IDENT, OP_AFFINE_RELU, G_UP2, false>(a, t, s);
+            return aff ? wgradT_tile<G_IDENT, OP_AFFINE, G_UP2, false>(a, t, s)
+                       : wgradT_tile<G_IDENT, OP_PLAIN, G_UP2, false>(a, t, s);
+        }
+        if (a.amode == G_IDENT && a.bmode == G_IDENT && !aff)
+            return wgradT_tile<G_IDENT, OP_PLAIN, G_IDENT, false>(a, t, s);
+        return -1;
+    }
     if (a.amode == G_CONV3 && a.bmode == G_IDENT && dz)
         return aff ? wgrad_tile<G_CONV3, OP_AFFINE, G_IDENT, true>(a, tile, s)
                    : wgrad_tile<G_CONV3, OP_PLAIN, G_IDENT, true>(a, tile, s);

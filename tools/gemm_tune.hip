@@ -5,6 +5,8 @@
 //   build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/gemm_tune.hip -o gemm_tune
 #include <stdio.h>
 #include <stdlib.h>
+#include <algorithm>
+#include <cmath>
 #include <vector>
 
 #include "../thyroid-nodule-image-segmentation-unet-ddti_amd/csrc/kernels_gemm.hip"
@@ -61,7 +63,7 @@ int main(int argc, char** argv) {
         float* dz = dalloc((size_t)M * sh.Cout, 8, 1.f);
         const double flop = 2.0 * M * sh.Cout * 9.0 * sh.Cin;
         // forward (CONV3 + affine + stats) per tile, dgrad (CONV3 store) per tile
-        const int NT = 10, NW = 8;
+        const int NT = 10, NW = 10;
         std::vector<std::vector<double>> best(2, std::vector<double>(NT, 0));
         for (int r = 0; r < rounds; ++r) {
             for (int tile = 0; tile < NT; ++tile) {
@@ -97,14 +99,18 @@ int main(int argc, char** argv) {
             printf("\n");
         }
         // wgrad over the tile table
-        double wb[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        int wsplit[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        // ids 0..7: pixel-major LDS (wgrad_kernel); 10, 15: channel-major (wgradT_kernel)
+        const int wids[NW] = {0, 1, 2, 3, 4, 5, 6, 7, 10, 15};
+        double wb[NW] = {};
+        double werr[NW] = {};
+        int wsplit[NW] = {};
+        std::vector<double> wref;
         float* slab = nullptr;
         size_t slab_n = 0;
         for (int r = 0; r < rounds; ++r)
             for (int v = 0; v < NW; ++v) {
                 int bm, bn, bkp;
-                wgrad_tile_dims(v, &bm, &bn, &bkp);
+                if (wgrad_tile_dims(wids[v], &bm, &bn, &bkp) != 0) continue;
                 if (sh.Cin % bm || sh.Cout % bn) continue;
                 const long tiles = (long)(9 * sh.Cin / bm) * (sh.Cout / bn);
                 long sp = (2048 + tiles - 1) / tiles;
@@ -123,9 +129,28 @@ int main(int argc, char** argv) {
                 a.amode = G_CONV3; a.ascale = sc; a.ashift = shf; a.b = dz; a.ldb = sh.Cout;
                 a.CB = sh.Cout; a.bmode = G_IDENT; a.Mw = 9 * sh.Cin; a.Nw = sh.Cout;
                 a.pps = (int)pps; a.splits = splits; a.slab = slab;
-                if (launch_wgrad(a, v, 0) != 0) continue;
+                if (launch_wgrad(a, wids[v], 0) != 0) continue;
+                if (r == 0) {  // split-reduced result vs the first tile that ran
+                    CK(hipDeviceSynchronize());
+                    const size_t nw = (size_t)9 * sh.Cin * sh.Cout;
+                    std::vector<float> h((size_t)splits * nw);
+                    CK(hipMemcpy(h.data(), slab, h.size() * 4, hipMemcpyDeviceToHost));
+                    std::vector<double> red(nw, 0.0);
+                    for (int sp2 = 0; sp2 < splits; ++sp2)
+                        for (size_t i = 0; i < nw; ++i) red[i] += h[(size_t)sp2 * nw + i];
+                    if (wref.empty()) {
+                        wref = red;
+                    } else {
+                        double md = 0, mx = 0;
+                        for (size_t i = 0; i < nw; ++i) {
+                            md = std::max(md, std::abs(red[i] - wref[i]));
+                            mx = std::max(mx, std::abs(wref[i]));
+                        }
+                        werr[v] = md / (mx > 0 ? mx : 1);
+                    }
+                }
                 CK(hipEventRecord(e0, 0));
-                for (int it = 0; it < iters; ++it) launch_wgrad(a, v, 0);
+                for (int it = 0; it < iters; ++it) launch_wgrad(a, wids[v], 0);
                 CK(hipEventRecord(e1, 0));
                 CK(hipEventSynchronize(e1));
                 float ms;
@@ -135,7 +160,9 @@ int main(int argc, char** argv) {
                 wsplit[v] = splits;
             }
         printf("%-20s wgrad", sh.name);
-        for (int v = 0; v < NW; ++v) printf("  w%d/s%d %6.1f", v, wsplit[v], wb[v]);
+        for (int v = 0; v < NW; ++v) printf("  w%d/s%d %6.1f", wids[v], wsplit[v], wb[v]);
+        printf("\n%-20s wgrad rel.err vs first tile:", sh.name);
+        for (int v = 0; v < NW; ++v) printf("  w%d %.1e", wids[v], werr[v]);
         printf("\n");
         fflush(stdout);
         CK(hipFree(x)); CK(hipFree(w)); CK(hipFree(sc)); CK(hipFree(shf)); CK(hipFree(bias));
