@@ -65,6 +65,9 @@ int main(int argc, char** argv) {
         // forward (CONV3 + affine + stats) per tile, dgrad (CONV3 store) per tile
         const int NT = 10, NW = 10;
         std::vector<std::vector<double>> best(2, std::vector<double>(NT, 0));
+        std::vector<std::vector<double>> rerr(2, std::vector<double>(NT, 0));
+        std::vector<float> rref[2];
+        float* xo = dalloc((size_t)M * sh.Cin, 9, 0.f);
         for (int r = 0; r < rounds; ++r) {
             for (int tile = 0; tile < NT; ++tile) {
                 if (tile == 6) continue;  // bf16-oriented BK64 tile
@@ -77,10 +80,26 @@ int main(int argc, char** argv) {
                         g.stats = st; g.out = y; g.ldo = sh.Cout;
                     } else {
                         g.N = sh.Cin; g.K = 9 * sh.Cout; g.a = dz; g.lda = sh.Cout; g.C = sh.Cout;
-                        g.emode = E_STORE; g.out = x; g.ldo = sh.Cin;
+                        g.emode = E_STORE; g.out = xo; g.ldo = sh.Cin;
                     }
                     g.amode = G_CONV3; g.bt = w;
                     if (launch_rowgemm(g, tile, 0) != 0) continue;
+                    if (r == 0) {  // output vs the first tile that ran
+                        CK(hipDeviceSynchronize());
+                        const size_t no = (size_t)M * (op ? sh.Cin : sh.Cout);
+                        std::vector<float> h(no);
+                        CK(hipMemcpy(h.data(), op ? xo : y, no * 4, hipMemcpyDeviceToHost));
+                        if (rref[op].empty()) {
+                            rref[op] = h;
+                        } else {
+                            double md = 0, mx = 0;
+                            for (size_t i = 0; i < no; ++i) {
+                                md = std::max(md, (double)std::abs(h[i] - rref[op][i]));
+                                mx = std::max(mx, (double)std::abs(rref[op][i]));
+                            }
+                            rerr[op][tile] = md / (mx > 0 ? mx : 1);
+                        }
+                    }
                     CK(hipEventRecord(e0, 0));
                     for (int it = 0; it < iters; ++it) launch_rowgemm(g, tile, 0);
                     CK(hipEventRecord(e1, 0));
@@ -96,6 +115,8 @@ int main(int argc, char** argv) {
         for (int op = 0; op < 2; ++op) {
             printf("%-20s %-5s", sh.name, op ? "dgrad" : "fwd");
             for (int tile = 0; tile < NT; ++tile) printf("  t%d %6.1f", tile, best[op][tile]);
+            printf("\n%-20s %-5s rel.err:", sh.name, op ? "dgrad" : "fwd");
+            for (int tile = 0; tile < NT; ++tile) printf("  t%d %.1e", tile, rerr[op][tile]);
             printf("\n");
         }
         // wgrad over the tile table
@@ -166,7 +187,7 @@ int main(int argc, char** argv) {
         printf("\n");
         fflush(stdout);
         CK(hipFree(x)); CK(hipFree(w)); CK(hipFree(sc)); CK(hipFree(shf)); CK(hipFree(bias));
-        CK(hipFree(y)); CK(hipFree(st)); CK(hipFree(dz));
+        CK(hipFree(y)); CK(hipFree(st)); CK(hipFree(dz)); CK(hipFree(xo));
         if (slab) CK(hipFree(slab));
     }
     return 0;
