@@ -327,6 +327,32 @@ def test_determinism_full_size():
     assert torch.equal(outs[0][1], outs[1][1])
 
 
+@pytest.mark.parametrize("variant", ["model", "mod"])
+def test_wgrad_stream_bit_identical(variant, monkeypatch):
+    """UNET_WGRAD_STREAM=1 moves the weight gradients to a second stream (runtime.hip
+    backward_impl); every kernel still sees the same inputs, so logits and the whole grad
+    arena must be bit-identical to the single-stream schedule, also for the bucket-event
+    path a DP run waits on."""
+    import unet_hip
+    from _helpers import hip_mod_model
+    x, t = inputs(13, 8, 256, 256)
+    outs = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("UNET_WGRAD_STREAM", flag)
+        if variant == "model":
+            m = hip_model(O.make_params(42), DEV)
+        else:
+            from oracle import mod_ref_cpu as MO
+            m = hip_mod_model(MO.make_params(5, base=64, depth=4), DEV, 64, 4)
+        logits = m(x.to(DEV))
+        l = unet_hip.seg_losses(logits, t.to(DEV))
+        (l[0] + l[1]).backward()
+        torch.cuda.synchronize()
+        outs.append((logits.detach().clone(), m._state.grad_arena.clone()))
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
+
+
 @pytest.mark.parametrize("out_ch,B,H,W", [(2, 2, 64, 128), (1, 1, 48, 80), (4, 3, 32, 32)])
 def test_shapes_and_classes_vs_oracle(out_ch, B, H, W):
     """Non-square images, batch 1, H/W multiples of 16 that are not powers of two, and the

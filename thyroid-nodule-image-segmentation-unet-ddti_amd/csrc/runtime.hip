@@ -100,6 +100,10 @@ struct unet_ctx {
     std::vector<TimeRec> trec;
     std::vector<hipEvent_t> ev_pool;
     size_t ev_used = 0;
+    // backward: weight-gradient stream (wgrad + slab reduce run beside the dgrad chain)
+    hipStream_t side = nullptr;
+    std::vector<hipEvent_t> sync_pool;
+    size_t sync_used = 0;
 
     int nconv() const { return (int)conv.size(); }
     int ch(int level) const { return base << level; }
@@ -633,6 +637,15 @@ int xcd_mode() {
 int xcd_remap_on() { return xcd_mode() == 1 || xcd_mode() == 2; }
 int xcd_remap_wgrad() { return xcd_mode() == 1 || xcd_mode() == 3; }
 
+// UNET_WGRAD_STREAM=1: weight gradients on a second stream.  Off by default: measured
+// 1 % slower at bs = 32 (370 vs 374 img/s, r01 A/B) -- the GEMMs fill the chip on their
+// own, so the overlap only wins the tails back, and the ~50 cross-stream waits cost more.
+// (read per backward call, so a test can compare both schedules in one process)
+bool wgrad_stream_env() {
+    const char* e = getenv("UNET_WGRAD_STREAM");
+    return e && atoi(e) != 0;
+}
+
 // weight image of a row GEMM: f32, or bf16 packed into the same slot (half its size)
 void set_weights(const unet_ctx* c, RowGemmArgs& g, const float* img) {
     g.xcd = xcd_remap_on();
@@ -839,6 +852,70 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
     Launcher L{c, s};
     const int H = p.H, W = p.W, D = c->depth, NC = c->nconv();
     int rc;
+    static int dz_env = -1;
+    if (dz_env < 0) {
+        const char* e = getenv("UNET_DZ_IN_LOADERS");
+        dz_env = e ? atoi(e) : 0;
+    }
+    const bool dz_in_loaders = dz_env && !c->bn_relu;
+
+    // Weight gradients (wgrad GEMM + slab reduce + bias sums) go to a second stream: they
+    // only read the layer input (forward buffers, never written in backward) and dz, and
+    // only write their own grads + the slabs (side-stream only), so they can run beside the
+    // dgrad chain, which fills the MFMA gaps of its bandwidth kernels (bn_dz, pool, BN
+    // finalize) and of the GEMM tails.  Ordering:
+    //  * side waits for the event after bn_dz (conv) / after the dgrad that wrote dcat (ConvT);
+    //  * a main-stream kernel that overwrites a gradient buffer first waits for the side
+    //    wgrad that read it (before_write);
+    //  * bucket events are recorded on the side stream after it joined the main stream;
+    //  * the main stream joins the side stream before returning.
+    // Off for the residual network (its skip wgrad shares the slabs on the main stream), for
+    // the loader-fused dz (the coefficients are rewritten per layer on the main stream) and
+    // when every launch is timed (a clean per-kernel breakdown needs serial launches).
+    const bool async_w = wgrad_stream_env() && !c->res && !dz_in_loaders &&
+                         !(c->timing && c->tfilter.empty());
+    if (async_w && !c->side &&
+        hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess)
+        return fail(c, UNET_ERR_HIP, "cannot create the weight-gradient stream");
+    hipStream_t sw = async_w ? c->side : s;
+    Launcher LW{c, sw};
+    c->sync_used = 0;
+    auto sev = [&]() {
+        if (c->sync_used == c->sync_pool.size()) {
+            hipEvent_t e;
+            (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
+            c->sync_pool.push_back(e);
+        }
+        return c->sync_pool[c->sync_used++];
+    };
+    std::vector<std::pair<const void*, hipEvent_t>> readers;  // side-stream reads pending
+    auto side_after_main = [&]() {  // side waits for everything enqueued on s so far
+        if (!async_w) return;
+        hipEvent_t e = sev();
+        (void)hipEventRecord(e, s);
+        (void)hipStreamWaitEvent(sw, e, 0);
+    };
+    auto side_read = [&](const void* buf) {  // the side stream's last enqueued op reads buf
+        if (!async_w) return;
+        hipEvent_t e = sev();
+        (void)hipEventRecord(e, sw);
+        readers.emplace_back(buf, e);
+    };
+    auto before_write = [&](const void* buf) {
+        for (size_t k = 0; k < readers.size();) {
+            if (readers[k].first == buf) {
+                (void)hipStreamWaitEvent(s, readers[k].second, 0);
+                readers.erase(readers.begin() + k);
+            } else {
+                ++k;
+            }
+        }
+    };
+#define RUNW(label, flop, expr)                                    \
+    do {                                                           \
+        int rc_ = LW.run(label, flop, [&]() { return (expr); });   \
+        if (rc_) return rc_;                                       \
+    } while (0)
 
     // BatchNorm backward is fused: the producer of `do` (head_bwd, a dgrad epilogue,
     // maxpool_bwd) leaves {sum do, sum do*y} column partials in p.part (do already masked by
@@ -863,12 +940,6 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
     // dz = A do + B y + C either as one elementwise pass over do (default) or inside the
     // wgrad / dgrad loaders (UNET_DZ_IN_LOADERS=1, ReLU -> BN order only: fewer passes, but
     // every 3x3 tap re-gathers both do and y -- measured slower on MI355X, kept for A/B runs)
-    static int dz_env = -1;
-    if (dz_env < 0) {
-        const char* e = getenv("UNET_DZ_IN_LOADERS");
-        dz_env = e ? atoi(e) : 0;
-    }
-    const bool dz_in_loaders = dz_env && !c->bn_relu;
     const int dz_mask = c->bn_relu ? 0 : 1;
     // conv i backward from do_i (dense [P][cout]).
     // dgrad -> dx (ld ldx).  bn_next: dx is the `do` of BN layer i-1 (second conv of a
@@ -885,9 +956,12 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
                                    C.b >= 0 ? grads + C.b : nullptr, s));
             return 0;
         }
-        if (!dz_in_loaders)
+        if (!dz_in_loaders) {
+            before_write(dout);
             RUN("bn_dz", 0, k_bn_dz(const_cast<float*>(dout), p.y[i], p.ldy[i], p.offy[i], P, C.cout,
                                     p.coef, dz_mask, s));
+        }
+        side_after_main();
         const float* dzc = dz_in_loaders ? p.coef : nullptr;
         Operand a = conv_input(c, p, i);
         WgradCfg wc = wgrad_cfg(C.cin, 9, C.cout, 1, P, c->bf16);
@@ -920,13 +994,15 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         w.splits = wc.splits;
         w.slab = p.slab;
         w.bf16 = c->bf16;
-        RUN(wlabel("conv_wgrad", wc, i), 2.0 * P * C.cout * 9 * C.cin,
-            launch_wgrad(w, wc.tile, s));
-        RUN("wgrad_reduce", 0,
-            k_slab_reduce(p.slab, wc.splits, w.Mw, w.Nw, 0, C.cin, C.cout, grads + C.w, s));
+        RUNW(wlabel("conv_wgrad", wc, i), 2.0 * P * C.cout * 9 * C.cin,
+             launch_wgrad(w, wc.tile, sw));
+        side_read(dout);
+        RUNW("wgrad_reduce", 0,
+             k_slab_reduce(p.slab, wc.splits, w.Mw, w.Nw, 0, C.cin, C.cout, grads + C.w, sw));
         if (C.b >= 0)
-            RUN("bias_grad", 0, k_bias_reduce(p.bslab, wc.splits, 1, C.cout, grads + C.b, s));
+            RUNW("bias_grad", 0, k_bias_reduce(p.bslab, wc.splits, 1, C.cout, grads + C.b, sw));
         if (dx) {
+            before_write(dx);
             RowGemmArgs g{};
             g.H = Hl;
             g.W = Wl;
@@ -1007,11 +1083,14 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         w.splits = wc.splits;
         w.slab = p.slab;
         w.bf16 = c->bf16;
-        RUN(wlabel("convT_wgrad", wc, 100 + k), 2.0 * Pin * T.cin * 4 * T.cout,
-            launch_wgrad(w, wc.tile, s));
-        RUN("wgrad_reduce", 0,
-            k_slab_reduce(p.slab, wc.splits, w.Mw, w.Nw, 1, T.cin, T.cout, grads + T.w, s));
-        RUN("bias_grad", 0, k_bias_reduce(p.bslab, wc.splits, 4, T.cout, grads + T.b, s));
+        side_after_main();
+        RUNW(wlabel("convT_wgrad", wc, 100 + k), 2.0 * Pin * T.cin * 4 * T.cout,
+             launch_wgrad(w, wc.tile, sw));
+        side_read(p.dcat[lo]);
+        RUNW("wgrad_reduce", 0,
+             k_slab_reduce(p.slab, wc.splits, w.Mw, w.Nw, 1, T.cin, T.cout, grads + T.w, sw));
+        RUNW("bias_grad", 0, k_bias_reduce(p.bslab, wc.splits, 4, T.cout, grads + T.b, sw));
+        before_write(dx);
         RowGemmArgs g{};
         g.H = Hi;
         g.W = Wi;
@@ -1048,8 +1127,18 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         return 0;
     };
     auto stage_done = [&](int st) {
+        bool any = false;
+        for (size_t b = 0; b < c->bucket_stage.size(); ++b) any |= c->bucket_stage[b] == st;
+        if (!any) return;
+        side_after_main();  // BN / head grads of the stage come from the main stream
         for (size_t b = 0; b < c->bucket_stage.size(); ++b)
-            if (c->bucket_stage[b] == st) (void)hipEventRecord(c->bucket_ev[b], s);
+            if (c->bucket_stage[b] == st) (void)hipEventRecord(c->bucket_ev[b], sw);
+    };
+    auto join = [&]() {
+        if (!async_w) return;
+        hipEvent_t e = sev();
+        (void)hipEventRecord(e, sw);
+        (void)hipStreamWaitEvent(s, e, 0);
     };
 
     float* G0 = p.g[0];
@@ -1074,7 +1163,6 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
                 WgradCfg wc = wgrad_cfg(CL.cin, 1, CL.cout, 1, P, false);
                 WgradArgs w{};
                 w.xcd = xcd_remap_wgrad();
-        w.xcd = xcd_remap_wgrad();
                 w.H = H >> CL.level;
                 w.W = W >> CL.level;
                 w.P = (int)P;
@@ -1183,6 +1271,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         const int C = c->ch(b);
         const int i1 = 2 * b + 1, i0 = 2 * b;
         float* nxt = cur == G0 ? G1 : G0;
+        before_write(nxt);
         RUN("maxpool_bwd", 0,
             k_maxpool_bwd(cur, p.idx[b], p.dcat[b], 2 * C, c->skip_off(b), p.y[i1], p.ldy[i1],
                           p.offy[i1], c->bn_relu ? p.scale[i1] : nullptr,
@@ -1203,7 +1292,9 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         }
         stage_done(2 * D - b);
     }
+    join();
     return 0;
+#undef RUNW
 }
 
 // Pillow's precompute_coeffs + normalize_coeffs_8bpc (libImaging/Resample.c) for the
@@ -1307,6 +1398,8 @@ int unet_destroy(unet_ctx* c) {
     if (!c) return UNET_ERR_INVALID;
     for (auto e : c->bucket_ev) (void)hipEventDestroy(e);
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
+    for (auto e : c->sync_pool) (void)hipEventDestroy(e);
+    if (c->side) (void)hipStreamDestroy(c->side);
     delete c;
     return UNET_OK;
 }
