@@ -109,8 +109,11 @@ int rowgemm_tile_dims(int tile, int* bm, int* bn, int* bk);
 int rowgemm_tile_dbuf(int tile);
 // wgrad tile ids (kernels_gemm.hip WGRAD_TILES): 0 = 128x128, 1 = 64x64 one wave,
 // 2 = 128x64 two waves, 3 = 64x128 two waves, 4 = 64x64 four waves, 5 = 128x64 four waves
+// 20.. = one row of 3x3 taps per block (3 accumulator sets; BM = channels of ONE tap):
+// 20 = 64x64, 21 = 128x64, 22 = 64x128, 23 = 128x128, 24 = 64x64 with 64-pixel chunks
 int launch_wgrad(const WgradArgs& a, int tile, hipStream_t s);
 int wgrad_tile_dims(int tile, int* bm, int* bn, int* bkp);
+int wgrad_tile_taps(int tile);  // taps of the M dimension one block covers (3 for 20..)
 // bf16 wgrad tile ids (a.bf16): 0 = 128x128/32 px, 1 = 128x128/64, 2 = 64x64/64,
 // 3 = 128x64/64, 4 = 64x128/64
 int wgrad16_tile_dims(int tile, int* bm, int* bn, int* bkp);

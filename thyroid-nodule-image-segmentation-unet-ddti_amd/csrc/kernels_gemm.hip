@@ -647,6 +647,209 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void wgrad_kernel(WgradArgs p) 
 }
 
 // ------------------------------------------------------------------------------------
+// Weight gradient of a 3x3 conv, one ROW of taps per block (dy fixed, dx = 0..2).
+// dW[(dy,dx)][ci][co] = sum_p x[p + (dy-1, dx-1)][ci] * dz[p][co]: for a chunk of BKP
+// pixels of one image row (W % BKP == 0, so a chunk never crosses a row) the three dx
+// taps read the same input row shifted by one pixel.  The block stages that row ONCE
+// with a one-pixel halo on each side (BKP + 2 LDS rows, zero outside the image), stages
+// the dz chunk once, and feeds three accumulator sets from it: A' of tap dx at chunk
+// pixel k is LDS row k + dx.  Against the one-tap tiles this reads each dz chunk 3x
+// instead of 9x per layer and does a third of the staging per MFMA.  Same K order,
+// split-K slabs, bias column sums and loaders (OP_AFFINE / OP_AFFINE_RELU on x, OP_DZ on
+// dz) as wgrad_kernel; slab rows m = (3*dy + dx)*CA + ci, the one-tap layout.
+// ------------------------------------------------------------------------------------
+template <int AOP, bool BDZ, class T>
+__global__ __launch_bounds__(T::THREADS, T::OCC) void wgrad_row3_kernel(WgradArgs p) {
+    constexpr bool AFFINE = AOP == OP_AFFINE || AOP == OP_AFFINE_RELU;
+    constexpr bool ARELU = AOP == OP_AFFINE_RELU;
+    constexpr int BM = T::BM, BN = T::BN, BKP = T::BKP, WM = T::WM, WN = T::WN;
+    constexpr int NTH = T::THREADS;
+    constexpr int WAVES_N = BN / WN;
+    constexpr int LDA = BM + 4, LDB = BN + 4;
+    constexpr int MT = WM / 32, NT = WN / 32;
+    constexpr int AF = BM / 4, BF = BN / 4;          // float4 per pixel row
+    constexpr int ARPP = NTH / AF, BRPP = NTH / BF;  // rows per pass
+    constexpr int AROWS = BKP + 2;                   // chunk + halo
+    constexpr int AP = (AROWS + ARPP - 1) / ARPP, BP = BKP / BRPP;
+    static_assert(ARPP * AF == NTH && BP * BRPP == BKP, "loader shape");
+    __shared__ __attribute__((aligned(16))) float As[AROWS * LDA];
+    __shared__ __attribute__((aligned(16))) float Bs[BKP * LDB];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+    const int ctm = p.CA / BM;                       // channel tiles per tap row
+    const int tiles_n = p.Nw / BN, tiles_m = 3 * ctm;
+    int idx = p.xcd ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+    const int tn = idx % tiles_n;
+    idx /= tiles_n;
+    const int tm = idx % tiles_m;
+    const int split = idx / tiles_m;
+    const int dy = tm / ctm, ca0 = (tm - dy * ctm) * BM;
+    const int tapB = (tn * BN) / p.CB, cb0 = tn * BN - tapB * p.CB;
+    const int H = p.H, W = p.W;
+
+    const int ac4 = tid % AF, arow = tid / AF;
+    const int bc4 = tid % BF, brow = tid / BF;
+    f32x4 sc = {1.f, 1.f, 1.f, 1.f}, sh = {0.f, 0.f, 0.f, 0.f};
+    bool arl = false;
+    if constexpr (AFFINE) {
+        sc = *(const f32x4*)(p.ascale + ca0 + ac4 * 4);
+        sh = *(const f32x4*)(p.ashift + ca0 + ac4 * 4);
+        if constexpr (ARELU) arl = ca0 + ac4 * 4 < p.arelu;
+    }
+    f32x4 ca = {0, 0, 0, 0}, cb = ca, cc = ca;
+    if constexpr (BDZ) {
+        ca = *(const f32x4*)(p.bcoef + cb0 + bc4 * 4);
+        cb = *(const f32x4*)(p.bcoef + p.CB + cb0 + bc4 * 4);
+        cc = *(const f32x4*)(p.bcoef + 2 * p.CB + cb0 + bc4 * 4);
+    }
+    const bool bsum = p.bias_slab != nullptr && tm == 0;
+    double bacc[4] = {0.0, 0.0, 0.0, 0.0};
+
+    const int pbeg = split * p.pps;
+    int pend = pbeg + p.pps;
+    if (pend > p.P) pend = p.P;
+    const int nchunks = (pend - pbeg + BKP - 1) / BKP;
+
+    f32x4 ryb[BDZ ? BP : 1];
+    f32x4 ra[AP], rb[BP];
+    unsigned amask = 0, bmask = 0;
+    auto issue = [&](int pc) {
+        amask = bmask = 0;
+        const Pix q = decode(pc, H, W);  // chunk start; the chunk stays on this row
+        const int yy = q.y + dy - 1;
+        const bool rowok = (yy >= 0) & (yy < H);
+        const int rbase = (q.img * H + (rowok ? yy : q.y)) * W;
+#pragma unroll
+        for (int i = 0; i < AP; ++i) {
+            const int r = arow + i * ARPP;
+            const int xx = q.x + r - 1;
+            const bool valid = rowok & (r < AROWS) & (xx >= 0) & (xx < W);
+            amask |= valid ? (1u << i) : 0u;
+            const int src = valid ? rbase + xx : pc;
+            ra[i] = *(const f32x4*)(p.a + (size_t)src * p.lda + p.aoff + ca0 + ac4 * 4);
+        }
+#pragma unroll
+        for (int i = 0; i < BP; ++i) {
+            int m = pc + brow + i * BRPP;
+            const bool in = m < pend;
+            m = in ? m : pend - 1;
+            bmask |= in ? (1u << i) : 0u;
+            rb[i] = *(const f32x4*)(p.b + (size_t)m * p.ldb + p.boff + cb0 + bc4 * 4);
+            if constexpr (BDZ)
+                ryb[i] = *(const f32x4*)(p.by + (size_t)m * p.ldby + p.offby + cb0 + bc4 * 4);
+        }
+    };
+    auto commit = [&]() {
+#pragma unroll
+        for (int i = 0; i < AP; ++i) {
+            const int r = arow + i * ARPP;
+            if (AP * ARPP > AROWS && r >= AROWS) break;
+            f32x4 v = ra[i];
+            if constexpr (AFFINE) {
+                v = v * sc + sh;
+                if (ARELU && arl)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
+            }
+            if (!((amask >> i) & 1u)) v = f32x4{0.f, 0.f, 0.f, 0.f};
+            *(f32x4*)&As[r * LDA + ac4 * 4] = v;
+        }
+#pragma unroll
+        for (int i = 0; i < BP; ++i) {
+            f32x4 v = rb[i];
+            if constexpr (BDZ) {
+                const f32x4 d = ca * v + cb * ryb[i] + cc;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) v[j] = ryb[i][j] > 0.f ? d[j] : 0.f;
+            }
+            if (!((bmask >> i) & 1u)) v = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (bsum)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) bacc[j] += v[j];
+            *(f32x4*)&Bs[(brow + i * BRPP) * LDB + bc4 * 4] = v;
+        }
+    };
+
+    f32x16 acc[3][MT][NT];
+#pragma unroll
+    for (int d = 0; d < 3; ++d)
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+#pragma unroll
+            for (int j = 0; j < NT; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[d][i][j][r] = 0.f;
+
+    const int li = lane & 31, lh = lane >> 5;
+    if (nchunks > 0) {
+        issue(pbeg);
+        commit();
+        __syncthreads();
+    }
+    for (int c = 0; c < nchunks; ++c) {
+        if (c + 1 < nchunks) issue(pbeg + (c + 1) * BKP);
+#pragma unroll
+        for (int kk = 0; kk < BKP / 8; ++kk)
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const int pr = kk * 8 + lh * 4 + s;
+                float bf[NT];
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt) bf[nt] = Bs[pr * LDB + wn * WN + nt * 32 + li];
+#pragma unroll
+                for (int d = 0; d < 3; ++d) {
+                    float af[MT];
+#pragma unroll
+                    for (int mt = 0; mt < MT; ++mt) af[mt] = As[(pr + d) * LDA + wm * WM + mt * 32 + li];
+#pragma unroll
+                    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                        for (int nt = 0; nt < NT; ++nt)
+                            acc[d][mt][nt] = mfma32(af[mt], bf[nt], acc[d][mt][nt]);
+                }
+            }
+        __syncthreads();
+        if (c + 1 < nchunks) {
+            commit();
+            __syncthreads();
+        }
+    }
+
+    if (bsum) {  // column sums of B' for the bias gradient: combine the row groups in order
+        __syncthreads();
+        double* red = (double*)As;  // [NTH][4]
+        static_assert(AROWS * LDA >= 8 * NTH, "bias reduction scratch");
+#pragma unroll
+        for (int j = 0; j < 4; ++j) red[tid * 4 + j] = bacc[j];
+        __syncthreads();
+        if (tid < BF) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                double t = 0.0;
+                for (int g = 0; g < BRPP; ++g) t += red[(g * BF + tid) * 4 + j];
+                p.bias_slab[(size_t)split * p.Nw + tn * BN + tid * 4 + j] = (float)t;
+            }
+        }
+    }
+
+    float* slab = p.slab + (size_t)split * p.Mw * p.Nw;
+#pragma unroll
+    for (int d = 0; d < 3; ++d)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int m = (3 * dy + d) * p.CA + ca0 + wm * WM + mt * 32 + (r & 3) +
+                                  8 * (r >> 2) + 4 * lh;
+                    const int n = tn * BN + wn * WN + nt * 32 + li;
+                    slab[(size_t)m * p.Nw + n] = acc[d][mt][nt][r];
+                }
+}
+
+// ------------------------------------------------------------------------------------
 // Weight-gradient GEMM with a channel-major LDS image ("transposed" loader).  The MFMA
 // operands of the pixel reduction are consecutive PIXELS of one channel per lane, so the
 // loader works on 4-pixel x 4-channel units: four f32x4 loads (one per pixel), the BN
@@ -1002,8 +1205,27 @@ using WgTile7 = WgTile<64, 64, 32, 32, 32, 3>;
     X(0, WgTile0) X(1, WgTile1) X(2, WgTile2) X(3, WgTile3) X(4, WgTile4) X(5, WgTile5) \
     X(6, WgTile6) X(7, WgTile7)
 
+#define WG_DIMS_R3(id, T) \
+    if (tile == id) {     \
+        *bm = T::BM;      \
+        *bn = T::BN;      \
+        *bkp = T::BKP;    \
+        return 0;         \
+    }
+// one-row-of-taps tiles (wgrad_row3_kernel, ids 20..): BM x BN per tap, 3 taps per block
+using Wr3Tile0 = WgTile<64, 64, 32, 32, 32>;    // 4 waves, 3 x 32x32 per wave
+using Wr3Tile1 = WgTile<128, 64, 64, 32, 32>;   // 4 waves, 3 x 64x32
+using Wr3Tile2 = WgTile<64, 128, 32, 64, 32>;   // 4 waves, 3 x 32x64
+using Wr3Tile3 = WgTile<128, 128, 64, 64, 32>;  // 4 waves, 3 x 64x64 (192 accumulators)
+using Wr3Tile4 = WgTile<64, 64, 32, 32, 64>;    // 64-pixel chunks
+#define WGRAD_ROW3_TILES(X) \
+    X(20, Wr3Tile0) X(21, Wr3Tile1) X(22, Wr3Tile2) X(23, Wr3Tile3) X(24, Wr3Tile4)
+
+int wgrad_tile_taps(int tile) { return tile >= 20 ? 3 : 1; }
+
 int wgrad_tile_dims(int tile, int* bm, int* bn, int* bkp) {
     if (tile == 10 || tile == 15) return wgrad16_tile_dims(tile - 10, bm, bn, bkp);
+    WGRAD_ROW3_TILES(WG_DIMS_R3)
 #define WG_DIMS(id, T) \
     if (tile == id) {  \
         *bm = T::BM;   \
@@ -1013,6 +1235,22 @@ int wgrad_tile_dims(int tile, int* bm, int* bn, int* bkp) {
     }
     WGRAD_TILES(WG_DIMS)
 #undef WG_DIMS
+    return -1;
+}
+
+template <int AOP, bool BDZ>
+static int wgrad_row3_tile(const WgradArgs& a, int tile, hipStream_t s) {
+#define WR3_CASE(id, T)                                                                       \
+    if (tile == id) {                                                                         \
+        if (a.Mw != 9 * a.CA || a.CA % T::BM || a.Nw % T::BN || a.CB % T::BN ||               \
+            a.pps % T::BKP || a.W % T::BKP)                                                   \
+            return -1;                                                                        \
+        const dim3 grid(3 * (a.CA / T::BM) * (a.Nw / T::BN) * a.splits);                      \
+        hipLaunchKernelGGL((wgrad_row3_kernel<AOP, BDZ, T>), grid, dim3(T::THREADS), 0, s, a); \
+        return (int)hipGetLastError();                                                        \
+    }
+    WGRAD_ROW3_TILES(WR3_CASE)
+#undef WR3_CASE
     return -1;
 }
 
@@ -1099,6 +1337,14 @@ int launch_wgrad(const WgradArgs& a, int tile, hipStream_t s) {
     const bool aff = a.ascale != nullptr, dz = a.bcoef != nullptr;
     if (a.arelu && !aff) return -1;
     if (a.arelu && dz) return -1;  // OP_DZ loaders are the ReLU -> BN order only
+    if (tile >= 20) {  // one row of 3x3 taps per block (wgrad_row3_kernel)
+        if (a.amode != G_CONV3 || a.bmode != G_IDENT) return -1;
+        if (dz) return aff ? wgrad_row3_tile<OP_AFFINE, true>(a, tile, s)
+                           : wgrad_row3_tile<OP_PLAIN, true>(a, tile, s);
+        if (a.arelu) return wgrad_row3_tile<OP_AFFINE_RELU, false>(a, tile, s);
+        return aff ? wgrad_row3_tile<OP_AFFINE, false>(a, tile, s)
+                   : wgrad_row3_tile<OP_PLAIN, false>(a, tile, s);
+    }
     if (tile >= 10 && !dz) {  // f32, channel-major LDS image (wgradT_kernel)
         const int t = tile - 10;
         if (a.amode == G_CONV3 && a.bmode == G_IDENT) {

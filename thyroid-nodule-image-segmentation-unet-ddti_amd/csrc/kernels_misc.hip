@@ -17,19 +17,41 @@ namespace {
 //   fwd  : Tf[(ab*Cout+co)][ci]
 //   dgrad: Td[ci][ab*Cout+co]
 // -------------------------------------------------------------------------------------
-// OUT = float (f32 MFMA images) or __bf16 (bf16 MFMA images, round to nearest even)
+// OUT = float (f32 MFMA images) or __bf16 (bf16 MFMA images, round to nearest even).
+// 3x3: one block per LDS tile of 32 co x 32 ci x 9 taps: the torch rows (ci, tap
+// contiguous) are read with unit stride, and both images are written as 32-element runs
+// (ci runs of Wf, co runs of Wd) rather than an element-wise stride-9 / stride-9*Cout
+// scatter.  Row stride 289 floats: both LDS read patterns are conflict-free.
 template <class OUT>
-__global__ void pack_conv3_kernel(const float* __restrict__ w, OUT* __restrict__ wf,
-                                  OUT* __restrict__ wd, int cin, int cout) {
-    const int64_t n = (int64_t)cin * cout * 9;
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
-         i += (int64_t)gridDim.x * blockDim.x) {
-        const int tap = (int)(i % 9);
-        const int64_t t = i / 9;
-        const int ci = (int)(t % cin), co = (int)(t / cin);
-        const OUT v = (OUT)w[i];
-        wf[((int64_t)co * 9 + tap) * cin + ci] = v;
-        if (wd) wd[((int64_t)ci * 9 + (8 - tap)) * cout + co] = v;
+__global__ __launch_bounds__(256) void pack_conv3_tiled_kernel(const float* __restrict__ w,
+                                                               OUT* __restrict__ wf,
+                                                               OUT* __restrict__ wd, int cin,
+                                                               int cout) {
+    constexpr int T = 32, RS = T * 9 + 1;
+    __shared__ float tile[T * RS];
+    const int ci0 = blockIdx.x * T, co0 = blockIdx.y * T;
+    const int nci = min(T, cin - ci0), nco = min(T, cout - co0);
+    const int tid = threadIdx.x;
+    for (int e = tid; e < T * T * 9; e += 256) {  // e = co_l * 288 + (ci_l * 9 + tap)
+        const int co_l = e / (T * 9), r = e - co_l * (T * 9);
+        if (co_l < nco && r < nci * 9)
+            tile[co_l * RS + r] = w[((int64_t)(co0 + co_l) * cin + ci0) * 9 + r];
+    }
+    __syncthreads();
+    const int l = tid & 31, g = tid >> 5;  // 8 groups of 32 lanes
+    // Wf[co][tap][ci]: rows (co_l, tap), lanes over ci
+    for (int row = g; row < T * 9; row += 8) {
+        const int co_l = row / 9, tap = row - co_l * 9;
+        if (co_l < nco && l < nci)
+            wf[((int64_t)(co0 + co_l) * 9 + tap) * cin + ci0 + l] = (OUT)tile[co_l * RS + l * 9 + tap];
+    }
+    if (!wd) return;
+    // Wd[ci][8-tap][co]: rows (ci_l, tap), lanes over co
+    for (int row = g; row < T * 9; row += 8) {
+        const int ci_l = row / 9, tap = row - ci_l * 9;
+        if (ci_l < nci && l < nco)
+            wd[((int64_t)(ci0 + ci_l) * 9 + (8 - tap)) * cout + co0 + l] =
+                (OUT)tile[l * RS + ci_l * 9 + tap];
     }
 }
 
@@ -889,15 +911,14 @@ inline int grid_for(int64_t n, int block = 256, int cap = 8192) {
 #define LAUNCH_CHECK() return (int)hipGetLastError()
 
 int k_pack_conv3(const float* w, float* wf, float* wd, int cin, int cout, hipStream_t s) {
-    const int64_t n = (int64_t)cin * cout * 9;
-    hipLaunchKernelGGL(pack_conv3_kernel<float>, dim3(grid_for(n)), dim3(256), 0, s, w, wf, wd, cin,
-                       cout);
+    const dim3 grid((cin + 31) / 32, (cout + 31) / 32);
+    hipLaunchKernelGGL(pack_conv3_tiled_kernel<float>, grid, dim3(256), 0, s, w, wf, wd, cin, cout);
     LAUNCH_CHECK();
 }
 int k_pack_conv3_bf16(const float* w, uint16_t* wf, uint16_t* wd, int cin, int cout, hipStream_t s) {
-    const int64_t n = (int64_t)cin * cout * 9;
-    hipLaunchKernelGGL(pack_conv3_kernel<__bf16>, dim3(grid_for(n)), dim3(256), 0, s, w,
-                       (__bf16*)wf, (__bf16*)wd, cin, cout);
+    const dim3 grid((cin + 31) / 32, (cout + 31) / 32);
+    hipLaunchKernelGGL(pack_conv3_tiled_kernel<__bf16>, grid, dim3(256), 0, s, w, (__bf16*)wf,
+                       (__bf16*)wd, cin, cout);
     LAUNCH_CHECK();
 }
 int k_pack_convT(const float* w, float* tf, float* td, int cin, int cout, hipStream_t s) {

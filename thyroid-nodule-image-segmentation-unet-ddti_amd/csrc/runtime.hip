@@ -331,8 +331,18 @@ struct WgradCfg {
 
 // wgrad tile (kernels_gemm.hip WGRAD_TILES) + split-K over pixels so that every layer
 // launches >= 2048 blocks; UNET_WGRAD_TILE_{W,N} override (tuning runs).
-WgradCfg wgrad_cfg(int CA, int tapsA, int CB, int tapsB, int64_t P, bool bf16) {
-    static int tw = -2, tn = -2, t16 = -2;
+// row_w: row width of a 3x3 conv's pixel grid (0 otherwise).  3x3 weight gradients on
+// rows that are a multiple of 32 pixels take the one-row-of-taps tiles (ids 20..,
+// wgrad_row3_kernel) when UNET_WGRAD_ROW3 selects them: 1 = every eligible layer,
+// 2 = only layers with a 64-channel operand (the 256x256 / 128x128 levels), 0 = never.
+WgradCfg wgrad_cfg(int CA, int tapsA, int CB, int tapsB, int64_t P, bool bf16, int row_w = 0) {
+    static int tw = -2, tn = -2, t16 = -2, r3 = -2, r3t = -2;
+    if (r3 == -2) {
+        const char* e = getenv("UNET_WGRAD_ROW3");
+        r3 = e ? atoi(e) : 0;
+        e = getenv("UNET_WGRAD_ROW3_TILE");
+        r3t = e ? atoi(e) : -1;
+    }
     if (tw == -2) {
         const char* e = getenv("UNET_WGRAD_TILE_W");
         tw = e ? atoi(e) : 0;
@@ -352,9 +362,16 @@ WgradCfg wgrad_cfg(int CA, int tapsA, int CB, int tapsB, int64_t P, bool bf16) {
             w.tile = (CA % 128 == 0) ? 5 : (CB % 128 == 0 ? 3 : tn);
         else
             w.tile = 7;
+        const bool row3 = tapsA == 9 && tapsB == 1 && row_w > 0 && row_w % 32 == 0 &&
+                          CA % 64 == 0 && CB % 64 == 0 &&
+                          (r3 == 1 || (r3 == 2 && (CA == 64 || CB == 64)));
+        if (row3)
+            w.tile = r3t >= 20 ? r3t
+                               : (CA % 128 == 0 ? (CB % 128 == 0 ? 23 : 21) : (CB % 128 == 0 ? 22 : 20));
         wgrad_tile_dims(w.tile, &w.bm, &w.bn, &w.bkp);
     }
-    const int64_t tiles = (int64_t)(tapsA * CA / w.bm) * (tapsB * CB / w.bn);
+    const int64_t tiles =
+        (int64_t)(tapsA * CA / (w.bm * wgrad_tile_taps(w.tile))) * (tapsB * CB / w.bn);
     int64_t s = (2048 + tiles - 1) / tiles;
     const int64_t maxs = P / (8 * w.bkp) > 0 ? P / (8 * w.bkp) : 1;  // >= 8 chunks per split
     // (P need not be a multiple of the pixel chunk: the kernel zero-fills the tail)
@@ -448,7 +465,7 @@ void make_plan(unet_ctx* c, int N, int H, int W, bool training, char* base, Plan
         int64_t smax = 0, bmax = 0;
         for (int i = 1; i < NC; ++i) {
             const ConvL& L = c->conv[i];
-            WgradCfg w = wgrad_cfg(L.cin, 9, L.cout, 1, p.P[L.level], c->bf16);
+            WgradCfg w = wgrad_cfg(L.cin, 9, L.cout, 1, p.P[L.level], c->bf16, W >> L.level);
             smax = std::max(smax, (int64_t)w.splits * 9 * L.cin * L.cout);
             bmax = std::max(bmax, (int64_t)w.splits * L.cout);
         }
@@ -558,7 +575,8 @@ std::string tlabel(const char* fam, int tile, int layer) {
 
 std::string wlabel(const char* fam, const WgradCfg& w, int layer) {
     char b[112];
-    snprintf(b, sizeof b, "%s/wgrad_%dx%dx%d|%d", fam, w.bm, w.bn, w.bkp, layer);
+    snprintf(b, sizeof b, "%s/wgrad%s_%dx%dx%d|%d", fam, w.tile >= 20 ? "3" : "", w.bm, w.bn,
+             w.bkp, layer);
     return b;
 }
 
@@ -964,7 +982,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         side_after_main();
         const float* dzc = dz_in_loaders ? p.coef : nullptr;
         Operand a = conv_input(c, p, i);
-        WgradCfg wc = wgrad_cfg(C.cin, 9, C.cout, 1, P, c->bf16);
+        WgradCfg wc = wgrad_cfg(C.cin, 9, C.cout, 1, P, c->bf16, Wl);
         WgradArgs w{};
         w.xcd = xcd_remap_wgrad();
         w.H = Hl;

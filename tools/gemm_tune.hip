@@ -63,7 +63,7 @@ int main(int argc, char** argv) {
         float* dz = dalloc((size_t)M * sh.Cout, 8, 1.f);
         const double flop = 2.0 * M * sh.Cout * 9.0 * sh.Cin;
         // forward (CONV3 + affine + stats) per tile, dgrad (CONV3 store) per tile
-        const int NT = 10, NW = 10;
+        const int NT = 10, NW = 17;
         std::vector<std::vector<double>> best(2, std::vector<double>(NT, 0));
         std::vector<std::vector<double>> rerr(2, std::vector<double>(NT, 0));
         std::vector<float> rref[2];
@@ -120,8 +120,10 @@ int main(int argc, char** argv) {
             printf("\n");
         }
         // wgrad over the tile table
-        // ids 0..7: pixel-major LDS (wgrad_kernel); 10, 15: channel-major (wgradT_kernel)
-        const int wids[NW] = {0, 1, 2, 3, 4, 5, 6, 7, 10, 15};
+        // ids 0..7: pixel-major LDS (wgrad_kernel); 10, 15: channel-major (wgradT_kernel);
+        // 20..24: one row of taps per block (wgrad_row3_kernel); wx: XCD-contiguous order
+        const int wids[NW] = {0, 1, 2, 3, 4, 5, 6, 7, 10, 15, 20, 21, 22, 23, 24, 7, 0};
+        const int wx[NW] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1};
         double wb[NW] = {};
         double werr[NW] = {};
         int wsplit[NW] = {};
@@ -133,7 +135,7 @@ int main(int argc, char** argv) {
                 int bm, bn, bkp;
                 if (wgrad_tile_dims(wids[v], &bm, &bn, &bkp) != 0) continue;
                 if (sh.Cin % bm || sh.Cout % bn) continue;
-                const long tiles = (long)(9 * sh.Cin / bm) * (sh.Cout / bn);
+                const long tiles = (long)(9 * sh.Cin / (bm * wgrad_tile_taps(wids[v]))) * (sh.Cout / bn);
                 long sp = (2048 + tiles - 1) / tiles;
                 if (sp > M / (8 * bkp)) sp = M / (8 * bkp);
                 if (sp < 1) sp = 1;
@@ -149,7 +151,7 @@ int main(int argc, char** argv) {
                 a.H = sh.H; a.W = sh.W; a.P = M; a.a = x; a.lda = sh.Cin; a.CA = sh.Cin;
                 a.amode = G_CONV3; a.ascale = sc; a.ashift = shf; a.b = dz; a.ldb = sh.Cout;
                 a.CB = sh.Cout; a.bmode = G_IDENT; a.Mw = 9 * sh.Cin; a.Nw = sh.Cout;
-                a.pps = (int)pps; a.splits = splits; a.slab = slab;
+                a.pps = (int)pps; a.splits = splits; a.slab = slab; a.xcd = wx[v];
                 if (launch_wgrad(a, wids[v], 0) != 0) continue;
                 if (r == 0) {  // split-reduced result vs the first tile that ran
                     CK(hipDeviceSynchronize());
@@ -181,7 +183,8 @@ int main(int argc, char** argv) {
                 wsplit[v] = splits;
             }
         printf("%-20s wgrad", sh.name);
-        for (int v = 0; v < NW; ++v) printf("  w%d/s%d %6.1f", wids[v], wsplit[v], wb[v]);
+        for (int v = 0; v < NW; ++v)
+            printf("  w%d%s/s%d %6.1f", wids[v], wx[v] ? "x" : "", wsplit[v], wb[v]);
         printf("\n%-20s wgrad rel.err vs first tile:", sh.name);
         for (int v = 0; v < NW; ++v) printf("  w%d %.1e", wids[v], werr[v]);
         printf("\n");
