@@ -386,3 +386,36 @@ def test_shapes_and_classes_vs_oracle(out_ch, B, H, W):
     errs = grad_errors(m, r64["grads"])
     worst = max(errs, key=errs.get)
     assert errs[worst] <= env, f"{worst}: {errs[worst]:.3e} (fp32 oracle {e32[worst]:.3e})"
+
+
+@pytest.mark.parametrize("variant", ["model", "mod"])
+def test_wgrad_row3_matches_one_tap_tiles(variant, monkeypatch):
+    """UNET_WGRAD_ROW3=1 computes every eligible 3x3 weight gradient with the
+    one-row-of-taps kernel (kernels_gemm.hip wgrad_row3_kernel: three taps per block from
+    a halo-staged input row, a different split-K partition).  Same products, different
+    summation grouping: every weight / bias gradient within 1e-5 norm-relative of the
+    one-tap schedule, logits bit-identical (the forward does not change)."""
+    import unet_hip
+    from _helpers import hip_mod_model
+    x, t = inputs(17, 8, 256, 256)
+    outs = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("UNET_WGRAD_ROW3", flag)
+        if variant == "model":
+            m = hip_model(O.make_params(42), DEV)
+        else:
+            from oracle import mod_ref_cpu as MO
+            m = hip_mod_model(MO.make_params(5, base=64, depth=4), DEV, 64, 4)
+        logits = m(x.to(DEV))
+        l = unet_hip.seg_losses(logits, t.to(DEV))
+        (l[0] + l[1]).backward()
+        torch.cuda.synchronize()
+        outs.append((logits.detach().clone(),
+                     {k: p.grad.detach().clone() for k, p in m.named_parameters()}))
+    assert torch.equal(outs[0][0], outs[1][0])
+    worst = 0.0
+    for k, g0 in outs[0][1].items():
+        d = float((outs[1][1][k] - g0).norm() / max(float(g0.norm()), 1e-30))
+        worst = max(worst, d)
+        assert d <= 1e-5, (k, d)
+    print(f"row3 vs one-tap worst grad norm-rel {worst:.2e}")

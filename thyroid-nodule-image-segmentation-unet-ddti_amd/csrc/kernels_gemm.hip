@@ -114,11 +114,15 @@ __device__ __forceinline__ int gather_src(int tap, int m, Pix q, int H, int W, b
 // Tile configuration of the row GEMM: block tile BM x BN, wave tile WM x WN (32x32 MFMA
 // accumulators), K-chunk BK, DBUF = two LDS images (one barrier per chunk).
 // OCC = waves per SIMD the register allocation must allow (launch_bounds' second argument).
-template <int BM_, int BN_, int WM_, int WN_, int BK_, bool DBUF_, int OCC_ = 1>
+// PRIO: raise the wave's issue priority (s_setprio 1) for its MFMA phase of each K-chunk
+// and drop it for the commit phase, so a SIMD's matrix pipe is fed first when its co-
+// resident waves (other blocks) are staging.
+template <int BM_, int BN_, int WM_, int WN_, int BK_, bool DBUF_, int OCC_ = 1, bool PRIO_ = false>
 struct RowTile {
     static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, BK = BK_;
     static constexpr bool DBUF = DBUF_;
     static constexpr int OCC = OCC_;
+    static constexpr bool PRIO = PRIO_;
     static constexpr int WAVES = (BM / WM) * (BN / WN);
     static constexpr int THREADS = 64 * WAVES;
 };
@@ -259,6 +263,7 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_kernel(RowGemmArgs
     for (int kc = 0; kc < nk; ++kc) {
         const int cur = DBUF ? (kc & 1) : 0;
         if (kc + 1 < nk) issue(kc + 1);
+        if constexpr (T::PRIO) __builtin_amdgcn_s_setprio(1);
         if constexpr (BF) {
             const __bf16* as16 = (const __bf16*)smem + cur * IMG;
             const __bf16* bs16 = as16 + BM * LDK;
@@ -298,6 +303,7 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_kernel(RowGemmArgs
                             acc[mt][nt] = mfma32(af[mt][s], bf[nt][s], acc[mt][nt]);
             }
         }
+        if constexpr (T::PRIO) __builtin_amdgcn_s_setprio(0);
         if constexpr (DBUF) {
             // the other image was last read in iteration kc-1, which every wave finished
             // before the barrier that ended it
@@ -1093,9 +1099,13 @@ using RowTile6 = RowTile<128, 128, 64, 64, 64, true>;  // bf16: 4 MFMA k-steps p
 using RowTile7 = RowTile<128, 128, 64, 64, 32, false, 3>;  // 3 waves / SIMD
 using RowTile8 = RowTile<128, 64, 64, 32, 32, false, 3>;
 using RowTile9 = RowTile<128, 128, 64, 64, 16, true, 3>;
+using RowTile10 = RowTile<128, 128, 64, 64, 32, false, 3, true>;  // t7 + MFMA-phase priority
+using RowTile11 = RowTile<128, 128, 64, 64, 32, false, 1, true>;  // t4 + MFMA-phase priority
+using RowTile12 = RowTile<128, 64, 64, 32, 32, false, 1, true>;   // t1 + MFMA-phase priority
 #define ROWGEMM_TILES(X) \
     X(0, RowTile0) X(1, RowTile1) X(2, RowTile2) X(3, RowTile3) X(4, RowTile4) X(5, RowTile5) \
-    X(6, RowTile6) X(7, RowTile7) X(8, RowTile8) X(9, RowTile9)
+    X(6, RowTile6) X(7, RowTile7) X(8, RowTile8) X(9, RowTile9) X(10, RowTile10)            \
+    X(11, RowTile11) X(12, RowTile12)
 
 template <int AMODE, int AOP, int EMODE, class T, bool BF>
 static int rowgemm_go(const RowGemmArgs& a, hipStream_t s) {

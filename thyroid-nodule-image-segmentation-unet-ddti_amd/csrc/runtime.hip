@@ -336,13 +336,13 @@ struct WgradCfg {
 // wgrad_row3_kernel) when UNET_WGRAD_ROW3 selects them: 1 = every eligible layer,
 // 2 = only layers with a 64-channel operand (the 256x256 / 128x128 levels), 0 = never.
 WgradCfg wgrad_cfg(int CA, int tapsA, int CB, int tapsB, int64_t P, bool bf16, int row_w = 0) {
-    static int tw = -2, tn = -2, t16 = -2, r3 = -2, r3t = -2;
-    if (r3 == -2) {
-        const char* e = getenv("UNET_WGRAD_ROW3");
-        r3 = e ? atoi(e) : 0;
-        e = getenv("UNET_WGRAD_ROW3_TILE");
-        r3t = e ? atoi(e) : -1;
-    }
+    static int tw = -2, tn = -2, t16 = -2;
+    // read per call (the workspace plan and the backward of one step read it alike), so a
+    // test can compare both schedules in one process
+    const char* e3 = getenv("UNET_WGRAD_ROW3");
+    const int r3 = e3 ? atoi(e3) : 0;
+    e3 = getenv("UNET_WGRAD_ROW3_TILE");
+    const int r3t = e3 ? atoi(e3) : -1;
     if (tw == -2) {
         const char* e = getenv("UNET_WGRAD_TILE_W");
         tw = e ? atoi(e) : 0;

@@ -63,7 +63,7 @@ int main(int argc, char** argv) {
         float* dz = dalloc((size_t)M * sh.Cout, 8, 1.f);
         const double flop = 2.0 * M * sh.Cout * 9.0 * sh.Cin;
         // forward (CONV3 + affine + stats) per tile, dgrad (CONV3 store) per tile
-        const int NT = 10, NW = 17;
+        const int NT = 13, NW = 17;
         std::vector<std::vector<double>> best(2, std::vector<double>(NT, 0));
         std::vector<std::vector<double>> rerr(2, std::vector<double>(NT, 0));
         std::vector<float> rref[2];
