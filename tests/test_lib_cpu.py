@@ -185,7 +185,8 @@ def test_unsupported_configs_rejected():
     from unet_hip import _lib
     from unet_hip.runtime import UNetRuntime
     for args in [(1, 1, _lib.VARIANT_MOD, 32, 5), (1, 1, _lib.VARIANT_MODEL, 64, 5),
-                 (3, 1, _lib.VARIANT_MOD, 64, 4), (1, 1, 7, 64, 4)]:
+                 (3, 1, _lib.VARIANT_MOD, 64, 4), (1, 1, 7, 64, 4),
+                 (1, 1, _lib.VARIANT_MOD, 192, 4)]:
         with pytest.raises(_lib.HipError):
             UNetRuntime("cuda:0", *args)
 

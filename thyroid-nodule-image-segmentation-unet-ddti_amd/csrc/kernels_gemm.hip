@@ -410,23 +410,32 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_kernel(RowGemmArgs
             }
         }
     } else if constexpr (EMODE == E_CONVT) {
+        // one pixel decode per accumulator row (f32-reciprocal division), shared by the NT
+        // column groups: with K = Cin as short as 128 the epilogue is a large part of the
+        // block, and an integer-division decode per element cost more than its MFMAs
+        const float rH = 1.f / (float)H, rW = 1.f / (float)W;
+        int coff[NT], co_[NT];
+        float bb[NT];
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) {
             const int n = n0 + wn * WN + nt * 32 + li;
             const int ab = n / p.cout, co = n - ab * p.cout;
-            const int a = ab >> 1, b = ab & 1;
-            const float bb = p.bias[co];
-#pragma unroll
-            for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int m = m0 + wm * WM + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-                    if (m >= p.M) continue;
-                    const Pix q = decode(m, H, W);
-                    const size_t op = (size_t)(q.img * 2 * H + 2 * q.y + a) * (2 * W) + 2 * q.x + b;
-                    p.out[op * p.ldo + p.ooff + co] = acc[mt][nt][r] + bb;
-                }
+            coff[nt] = (ab >> 1) * (2 * W) + (ab & 1);  // (a, b) offset in the output grid
+            co_[nt] = co;
+            bb[nt] = p.bias[co];
         }
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = m0 + wm * WM + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                if (m >= p.M) continue;
+                const Pix q = decode_fast(m, H, W, rH, rW);
+                const size_t ob = (size_t)(q.img * 2 * H + 2 * q.y) * (2 * W) + 2 * q.x;
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt)
+                    p.out[(ob + coff[nt]) * p.ldo + p.ooff + co_[nt]] = acc[mt][nt][r] + bb[nt];
+            }
     } else if constexpr (EMODE == E_RESID || EMODE == E_ADD) {
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) {

@@ -325,10 +325,64 @@ __global__ void bn_finalize_eval_kernel(int C, const float* __restrict__ gamma,
 // -------------------------------------------------------------------------------------
 // relu: BN -> ReLU order (mod.py:46-47); the max of ReLU(v) is ReLU(max v) and the winner
 // only differs where every candidate is <= 0, where the ReLU blocks its gradient anyway.
-__global__ void maxpool_bn_kernel(const float* __restrict__ y, int ld, int off,
-                                  const float* __restrict__ scale,
-                                  const float* __restrict__ shift, int relu, int N, int H, int W,
-                                  int C, float* __restrict__ out, uint8_t* __restrict__ idx) {
+// One pooled pixel: BN affine of the four window values, torch's tie rule, optional ReLU.
+__device__ __forceinline__ void maxpool_px(const float* __restrict__ y, int ld, int off, f32x4 sc,
+                                           f32x4 sh, int relu, int H, int W, int img, int yo,
+                                           int xo, int c, float* __restrict__ out,
+                                           uint8_t* __restrict__ idx, int64_t o) {
+    f32x4 best;
+    uint32_t bi = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int64_t pin = ((int64_t)img * H + 2 * yo + (k >> 1)) * W + 2 * xo + (k & 1);
+        const f32x4 v = *(const f32x4*)(y + pin * ld + off + c) * sc + sh;
+        if (k == 0) {
+            best = v;
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (v[j] > best[j] || v[j] != v[j]) {
+                    best[j] = v[j];
+                    bi = (bi & ~(0xFFu << (8 * j))) | ((uint32_t)k << (8 * j));
+                }
+        }
+    }
+    if (relu)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) best[j] = fmaxf(best[j], 0.f);
+    *(f32x4*)(out + o) = best;
+    *(uint32_t*)(idx + o) = bi;
+}
+
+// Row form (C/4 divides 256 or is a multiple of it; N*H*W < 2^31): a thread keeps one
+// channel quad and its affine in registers and walks pooled pixels with 32-bit index math.
+__global__ __launch_bounds__(256) void maxpool_bn_kernel(const float* __restrict__ y, int ld,
+                                                         int off, const float* __restrict__ scale,
+                                                         const float* __restrict__ shift, int relu,
+                                                         int N, int H, int W, int C,
+                                                         float* __restrict__ out,
+                                                         uint8_t* __restrict__ idx) {
+    const int Ho = H / 2, Wo = W / 2, c4n = C / 4;
+    const int tpr = c4n < 256 ? c4n : 256, rpp = 256 / tpr;
+    const int PO = N * Ho * Wo;
+    for (int cb = 0; cb < c4n; cb += tpr) {
+        const int c = 4 * (cb + (int)threadIdx.x % tpr);
+        const f32x4 sc = scale ? *(const f32x4*)(scale + c) : f32x4{1.f, 1.f, 1.f, 1.f};
+        const f32x4 sh = shift ? *(const f32x4*)(shift + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int po = blockIdx.x * rpp + (int)threadIdx.x / tpr; po < PO; po += gridDim.x * rpp) {
+            const int t = po / Wo, xo = po - t * Wo;
+            const int img = t / Ho, yo = t - img * Ho;
+            maxpool_px(y, ld, off, sc, sh, relu, H, W, img, yo, xo, c, out, idx, (int64_t)po * C + c);
+        }
+    }
+}
+
+// Any C % 4 == 0: one thread per (pooled pixel, channel quad).
+__global__ void maxpool_bn_any_kernel(const float* __restrict__ y, int ld, int off,
+                                      const float* __restrict__ scale,
+                                      const float* __restrict__ shift, int relu, int N, int H,
+                                      int W, int C, float* __restrict__ out,
+                                      uint8_t* __restrict__ idx) {
     const int Ho = H / 2, Wo = W / 2, c4n = C / 4;
     const int64_t total = (int64_t)N * Ho * Wo * c4n;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
@@ -340,28 +394,7 @@ __global__ void maxpool_bn_kernel(const float* __restrict__ y, int ld, int off,
         const int yo = (int)(t % Ho), img = (int)(t / Ho);
         const f32x4 sc = scale ? *(const f32x4*)(scale + 4 * c4) : f32x4{1.f, 1.f, 1.f, 1.f};
         const f32x4 sh = shift ? *(const f32x4*)(shift + 4 * c4) : f32x4{0.f, 0.f, 0.f, 0.f};
-        f32x4 best;
-        uint32_t bi = 0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int64_t pin = ((int64_t)img * H + 2 * yo + (k >> 1)) * W + 2 * xo + (k & 1);
-            const f32x4 v = *(const f32x4*)(y + pin * ld + off + 4 * c4) * sc + sh;
-            if (k == 0) {
-                best = v;
-            } else {
-#pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    if (v[j] > best[j] || v[j] != v[j]) {
-                        best[j] = v[j];
-                        bi = (bi & ~(0xFFu << (8 * j))) | ((uint32_t)k << (8 * j));
-                    }
-            }
-        }
-        if (relu)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) best[j] = fmaxf(best[j], 0.f);
-        *(f32x4*)(out + po * C + 4 * c4) = best;
-        *(uint32_t*)(idx + po * C + 4 * c4) = bi;
+        maxpool_px(y, ld, off, sc, sh, relu, H, W, img, yo, xo, 4 * c4, out, idx, po * C + 4 * c4);
     }
 }
 
@@ -400,9 +433,9 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const float* __restric
         const int64_t per = (PO + gridDim.x - 1) / gridDim.x;
         const int64_t r0 = blockIdx.x * per, r1 = r0 + per < PO ? r0 + per : PO;
         for (int64_t po = r0 + g; po < r1; po += rpp) {
-            const int xo = (int)(po % Wo);
-            const int64_t t = po / Wo;
-            const int yo = (int)(t % Ho), img = (int)(t / Ho);
+            // 32-bit index math (the launcher guarantees N*H*W < 2^31)
+            const int t = (int)po / Wo, xo = (int)po - t * Wo;
+            const int img = t / Ho, yo = t - img * Ho;
             const f32x4 gp = *(const f32x4*)(dp + po * C + c);
             const uint32_t bi = *(const uint32_t*)(idx + po * C + c);
 #pragma unroll
@@ -456,6 +489,28 @@ __global__ void bn_bwd_finalize2_kernel(const float* __restrict__ part, int G, i
 }
 
 // dz = A do + B y + C in place, masked by [y > 0] when `mask` (ReLU before the BN).
+// Row form (C / 4 divides 256): each thread keeps one channel quad and its coefficients
+// in registers and walks pixel rows, so there is no per-element index division.
+__global__ __launch_bounds__(256) void bn_dz_rows_kernel(float* __restrict__ d,
+                                                         const float* __restrict__ y, int ld,
+                                                         int off, int64_t P, int C,
+                                                         const float* __restrict__ coef, int mask) {
+    const int tpr = C / 4, rpp = 256 / tpr;
+    const int c = (threadIdx.x % tpr) * 4;
+    const f32x4 ka = *(const f32x4*)(coef + c), kb = *(const f32x4*)(coef + C + c),
+                kc = *(const f32x4*)(coef + 2 * C + c);
+    for (int64_t m = (int64_t)blockIdx.x * rpp + threadIdx.x / tpr; m < P;
+         m += (int64_t)gridDim.x * rpp) {
+        f32x4* pd = (f32x4*)(d + m * C + c);
+        const f32x4 v = *(const f32x4*)(y + m * ld + off + c);
+        const f32x4 r = ka * (*pd) + kb * v + kc;
+        f32x4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = (!mask || v[j] > 0.f) ? r[j] : 0.f;
+        *pd = o;
+    }
+}
+
 __global__ void bn_dz_kernel(float* __restrict__ d, const float* __restrict__ y, int ld, int off,
                              int64_t P, int C, const float* __restrict__ coef, int mask) {
     const int c4n = C / 4;
@@ -974,13 +1029,20 @@ int k_bn_finalize_eval(int C, const float* gamma, const float* beta, const float
 int k_maxpool_bn(const float* y, int ld, int off, const float* scale, const float* shift, int relu,
                  int N, int H, int W, int C, float* out, uint8_t* idx, hipStream_t s) {
     const int64_t n = (int64_t)N * (H / 2) * (W / 2) * (C / 4);
-    hipLaunchKernelGGL(maxpool_bn_kernel, dim3(grid_for(n)), dim3(256), 0, s, y, ld, off, scale,
-                       shift, relu, N, H, W, C, out, idx);
+    const int c4n = C / 4;
+    if (C % 4 == 0 && (int64_t)N * H * W < (1ll << 31) &&
+        (c4n <= 256 ? 256 % c4n == 0 : c4n % 256 == 0))
+        hipLaunchKernelGGL(maxpool_bn_kernel, dim3(grid_for(n)), dim3(256), 0, s, y, ld, off, scale,
+                           shift, relu, N, H, W, C, out, idx);
+    else
+        hipLaunchKernelGGL(maxpool_bn_any_kernel, dim3(grid_for(n)), dim3(256), 0, s, y, ld, off,
+                           scale, shift, relu, N, H, W, C, out, idx);
     LAUNCH_CHECK();
 }
 int k_maxpool_bwd(const float* dp, const uint8_t* idx, const float* dskip, int ldskip, int offskip,
                   const float* y, int ldy, int offy, const float* mscale, const float* mshift,
                   int N, int H, int W, int C, float* dout, float* partial, int G, hipStream_t s) {
+    if ((int64_t)N * H * W >= (1ll << 31)) return -1;  // 32-bit pixel index math
     hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(G), dim3(256), 0, s, dp, idx, dskip, ldskip,
                        offskip, y, ldy, offy, mscale, mshift, N, H, W, C, dout, partial);
     LAUNCH_CHECK();
@@ -994,8 +1056,12 @@ int k_bn_bwd_finalize2(const float* part, int G, int C, double count, const floa
 }
 int k_bn_dz(float* d, const float* y, int ld, int off, int64_t P, int C, const float* coef, int mask,
             hipStream_t s) {
-    hipLaunchKernelGGL(bn_dz_kernel, dim3(grid_for(P * (C / 4))), dim3(256), 0, s, d, y, ld, off, P, C,
-                       coef, mask);
+    if (C % 4 == 0 && C <= 1024 && 256 % (C / 4) == 0)
+        hipLaunchKernelGGL(bn_dz_rows_kernel, dim3(grid_for(P * (C / 4))), dim3(256), 0, s, d, y, ld,
+                           off, P, C, coef, mask);
+    else
+        hipLaunchKernelGGL(bn_dz_kernel, dim3(grid_for(P * (C / 4))), dim3(256), 0, s, d, y, ld, off,
+                           P, C, coef, mask);
     LAUNCH_CHECK();
 }
 int k_bias_reduce(const float* slab, int S, int taps, int C, float* out, hipStream_t s) {

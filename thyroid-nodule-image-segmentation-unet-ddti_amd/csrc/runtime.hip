@@ -1391,11 +1391,13 @@ int unet_create(const unet_cfg* cfg, int device, unet_ctx** out) {
         }
     }
     // The first conv kernel is specialised for a single input channel (every BASELINE
-    // config); the GEMM tiles need 64-multiples of channels at every level; the head's
-    // fused BN-partials path handles up to 4 classes.
+    // config); the GEMM tiles need 64-multiples of channels at every level and the
+    // channel-quad row kernels (pool, head, BN backward) a power-of-two channel count, so
+    // base is 64, 128 or 256; the head's fused BN-partials path handles up to 4 classes.
     if ((c->variant != UNET_VARIANT_MODEL && c->variant != UNET_VARIANT_MOD &&
          c->variant != UNET_VARIANT_RES) || c->in_ch != 1 ||
-        c->out_ch < 1 || c->out_ch > 4 || c->base % 64 || c->base > 256 || c->depth < 1 ||
+        c->out_ch < 1 || c->out_ch > 4 || c->base % 64 || c->base > 256 ||
+        (c->base & (c->base - 1)) || c->depth < 1 ||
         c->depth > MAX_DEPTH || (c->base << c->depth) > 8192) {
         delete c;
         return UNET_ERR_UNSUPPORTED;
