@@ -4,7 +4,7 @@ set -u
 TAG=${1:-run}
 R=$GRAFT_REPO_ROOT
 cd $R
-timeout -k 10 700 python -m pytest tests -m gpu -q -p no:cacheprovider > gpurun_out/$TAG.pytest.log 2>&1
+timeout -k 10 700 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread -p no:cacheprovider > gpurun_out/$TAG.pytest.log 2>&1
 rc=$?
 echo "pytest rc=$rc"; tail -15 gpurun_out/$TAG.pytest.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
