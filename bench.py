@@ -87,7 +87,7 @@ def cpu_baseline(steps, size, config=2):
     opt = O.AdamWState(P, lr=1e-5)
     x = torch.from_numpy(Wt.make_input(21, nb, 1, side, side))
     t = torch.from_numpy(Wt.make_target(21, nb, side, side))
-    run(P, B, opt, x, t)  # warm-up
+    first = run(P, B, opt, x, t)  # warm-up; also the reference side of dice_vs_ref
     ts = []
     for _ in range(steps):
         t0 = time.perf_counter()
@@ -103,11 +103,45 @@ def cpu_baseline(steps, size, config=2):
                 break
     except OSError:
         pass
-    return {"value": round(nb * scale / med, 4), "unit": "images/sec", "cores": threads,
+    sample = (x, t, first) if config == 2 else None
+    return sample, {"value": round(nb * scale / med, 4), "unit": "images/sec", "cores": threads,
             "kind": "port",
             "sample": f"{what} (fwd+BCE+Dice+bwd+AdamW), bs={nb}, 1x{side}x{side}"
                       f"{' (scaled x0.25 to 512x512 images)' if scale != 1.0 else ''}, median of "
                       f"{steps} steps after 1 warm-up, torch CPU {threads} threads, {cpu_model}"}
+
+
+def dice_vs_ref(sample, dev):
+    """BASELINE metric's "Dice vs ref": the first training step of the HIP path on the CPU
+    baseline's sample (same counter-hash weights, fresh BN buffers, same 4 images), against
+    the oracle's step on the host.  Dice loss (models/loss.py:13-24) and the Dice score of
+    the sigmoid > 0.5 masks vs the targets (utils/utils.py:225-251 F1) from both paths."""
+    import torch
+    import unet_hip
+    from oracle import unet_ref_cpu as O
+    x, t, ref = sample
+    P = O.make_params(42)
+    m = unet_hip.UNet(1, 1)
+    m.load_state_dict({**P, **O.init_buffers()})
+    m = m.to(dev).train()
+    logits = m(x.to(dev))
+    losses = unet_hip.seg_losses(logits, t.to(dev))
+    torch.cuda.synchronize()
+    lg = logits.detach().cpu()
+
+    def mask_dice(lgt):
+        pm = (torch.sigmoid(lgt) > 0.5)
+        tm = t > 0
+        tp = (pm & tm).sum().item()
+        return 2.0 * tp / max(1, pm.sum().item() + tm.sum().item())
+    d_hip, d_ref = float(losses[1].item()), float(ref["dice"].item())
+    agree = float(((torch.sigmoid(lg) > 0.5) == (torch.sigmoid(ref["logits"]) > 0.5)).float().mean())
+    return {"sample": "first train step, bs=4 1x256x256 (the cpu_baseline sample), oracle weights seed 42",
+            "dice_loss": round(d_hip, 8), "dice_loss_ref": round(d_ref, 8),
+            "abs_diff": float(f"{abs(d_hip - d_ref):.3g}"),
+            "mask_dice": round(mask_dice(lg), 6), "mask_dice_ref": round(mask_dice(ref["logits"]), 6),
+            "mask_agreement": round(agree, 8),
+            "logits_max_rel": float(f"{float((lg - ref['logits']).abs().max() / ref['logits'].abs().max()):.3g}")}
 
 
 def load_pmc(kernel):
@@ -271,7 +305,9 @@ def main():
                       "image": [1, S, S], "parallelism": f"dp{world}"},
            "roofline": roofline}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(args.cpu_steps, S, args.config)
+        sample, out["cpu_baseline"] = cpu_baseline(args.cpu_steps, S, args.config)
+        if sample is not None:
+            out["dice_vs_ref"] = dice_vs_ref(sample, dev)
     elif rank == 0:
         out["cpu_baseline"] = None
     if rank == 0:

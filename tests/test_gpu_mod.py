@@ -156,8 +156,42 @@ def _to64(d):
     return {k: (v.double() if v.is_floating_point() else v.clone()) for k, v in d.items()}
 
 
-@pytest.mark.parametrize("base,depth", [(64, 3), (128, 5)])
-def test_mod_bf16_matches_bf16_oracle(base, depth):
+@pytest.mark.parametrize("tile", ["0", "1", "3"])
+def test_rg16_bit_identical_to_register_staged(tile, monkeypatch):
+    """The LDS-DMA bf16 GEMMs (kernels_gemm16.hip, fed by the k_to_bf16 operand images)
+    against the register-staged bf16 kernel (UNET_RG16=0) on a base-128 network, where
+    every GEMM but the Cin = 1 first conv takes the new path: the same bf16 roundings of
+    the same f32 values, the same K order and 128-row BN partials, so one training step
+    gives bit-identical logits, gradients and BN statistics for every 128-row tile."""
+    import unet_hip
+    x, t = inputs(23, 2, 128, 128)
+    P = MO.make_params(9, 128, 3)
+    outs = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("UNET_RG16", flag)
+        monkeypatch.setenv("UNET_RG16_TILE", tile)
+        m = unet_hip.ModUNet(1, 1, base_filters=128, depth=3, mfma_dtype="bf16")
+        sd = m.state_dict()
+        for k, v in P.items():
+            sd[k] = v.clone()
+        m.load_state_dict(sd)
+        m = m.to(DEV).train()
+        logits = m(x.to(DEV))
+        losses = unet_hip.seg_losses(logits, t.to(DEV))
+        (losses[0] + losses[1]).backward()
+        torch.cuda.synchronize()
+        outs.append((logits.detach().clone(),
+                     {k: p.grad.detach().clone() for k, p in m.named_parameters()},
+                     {k: b.detach().clone() for k, b in m.named_buffers()}))
+    assert torch.equal(outs[0][0], outs[1][0])
+    for k, g0 in outs[0][1].items():
+        assert torch.equal(g0, outs[1][1][k]), k
+    for k, b0 in outs[0][2].items():
+        assert torch.equal(b0, outs[1][2][k]), k
+
+
+@pytest.mark.parametrize("base,depth,tile", [(64, 3, "0"), (128, 5, "0"), (128, 5, "2")])
+def test_mod_bf16_matches_bf16_oracle(base, depth, tile, monkeypatch):
     """mfma_dtype="bf16": one step at B=2 64x64 vs the oracle that rounds exactly the GEMM
     operands the HIP bf16 kernels round (oracle/mod_ref_cpu.py, bf16=True).
 
@@ -165,8 +199,11 @@ def test_mod_bf16_matches_bf16_oracle(base, depth):
     rounding boundary with probability ~1e-5 per element, and the flips compound through
     BN.  The oracle itself shows it: evaluated in fp32 and in fp64 (same bf16 roundings of
     its own values) it differs by ~6e-3 in the logits and up to ~15 % on small BN-bias
-    gradients.  The bar is 2x that spread of the oracle against itself."""
+    gradients.  The bar is 2x that spread of the oracle against itself.  tile = the
+    LDS-DMA GEMM tile (UNET_RG16_TILE; "2" = 256 rows x 8 waves, whose BN partials group
+    256 rows, so its bf16 roundings differ from the 128-row tiles')."""
     import unet_hip
+    monkeypatch.setenv("UNET_RG16_TILE", tile)
     P = MO.make_params(42, base, depth)
     x, t = inputs(5, 2, 64, 64)
     ref = MO.train_step(P, MO.init_buffers(base, depth), None, x, t, depth=depth, bf16=True)

@@ -72,6 +72,8 @@ struct RowGemmArgs {
     const float* escale;  // E_STORE_BN, BN -> ReLU order: affine of that BN (ReLU mask)
     const float* eshift;
     int xcd;              // remap blocks so each XCD gets a contiguous range of tiles
+    const uint16_t* a16;  // rowgemm16: A as a dense bf16 image [pixels][lda] (prepared operand)
+    const void* zero16;   // rowgemm16: >= 16 zero bytes (padding taps / rows past M)
 };
 
 struct WgradArgs {
@@ -111,6 +113,8 @@ int rowgemm_tile_dbuf(int tile);
 // 2 = 128x64 two waves, 3 = 64x128 two waves, 4 = 64x64 four waves, 5 = 128x64 four waves
 // 20.. = one row of 3x3 taps per block (3 accumulator sets; BM = channels of ONE tap):
 // 20 = 64x64, 21 = 128x64, 22 = 64x128, 23 = 128x128, 24 = 64x64 with 64-pixel chunks
+int launch_rowgemm16(const RowGemmArgs& a, int tile, hipStream_t s);
+int rowgemm16_tile_dims(int tile, int* bm, int* bn);
 int launch_wgrad(const WgradArgs& a, int tile, hipStream_t s);
 int wgrad_tile_dims(int tile, int* bm, int* bn, int* bkp);
 int wgrad_tile_taps(int tile);  // taps of the M dimension one block covers (3 for 20..)

@@ -1,0 +1,250 @@
+// Shared device helpers of the row-GEMM kernels (kernels_gemm.hip: f32 and register-staged
+// bf16; kernels_gemm16.hip: LDS-DMA bf16): MFMA wrappers, pixel decode, the implicit-conv
+// row gather and the epilogues (bias / ReLU / BN statistics, ConvTranspose scatter, BN-backward
+// partials, residual close), so every kernel family stores identical results.
+#pragma once
+#include "common.h"
+
+namespace {
+
+__device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+// bf16 operands (BF kernels): 8 bf16 per lane, k = 8 * (lane >> 5) + j
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x16 mfma32_bf16(bf16x8 a, bf16x8 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// f32x4 -> 4 bf16 (round to nearest even; v_cvt_pk_bf16_f32)
+__device__ __forceinline__ bf16x4 to_bf16x4(f32x4 v) {
+    return bf16x4{(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+}
+
+struct Pix {
+    int img, y, x;
+};
+
+// Blocks are dispatched round-robin over the 8 XCDs (block b -> XCD b % 8), each with its
+// own L2.  Give XCD x the contiguous logical tiles [x*n/8, (x+1)*n/8) instead, so tiles
+// that share input rows (3x3 halos, the taps and channel slices of one pixel range) hit
+// the same L2.
+__device__ __forceinline__ int xcd_remap(int b, int n) {
+    const int q = n >> 3, r = n & 7, x = b & 7, i = b >> 3;
+    return x < r ? x * (q + 1) + i : r * (q + 1) + (x - r) * q + i;
+}
+
+__device__ __forceinline__ Pix decode(int m, int H, int W) {
+    Pix r;
+    int t = m / W;
+    r.x = m - t * W;
+    r.img = t / H;
+    r.y = t - r.img * H;
+    return r;
+}
+
+// Division by a per-launch constant through an f32 reciprocal plus one correction step:
+// exact while the quotient stays below 2^22 (P / W < 4M pixel rows here).
+__device__ __forceinline__ int fdiv(int n, int d, float rd) {
+    int q = (int)((float)n * rd);
+    const int r = n - q * d;
+    q += (r >= d) ? 1 : 0;
+    q -= (r < 0) ? 1 : 0;
+    return q;
+}
+
+__device__ __forceinline__ Pix decode_fast(int m, int H, int W, float rH, float rW) {
+    Pix r;
+    const int t = fdiv(m, W, rW);
+    r.x = m - t * W;
+    r.img = fdiv(t, H, rH);
+    r.y = t - r.img * H;
+    return r;
+}
+
+// Source pixel of row pixel `q` (on grid HxW) for `tap` in MODE; `valid` false for
+// zero-padding taps (the returned index is then the row pixel itself, always in range).
+template <int MODE>
+__device__ __forceinline__ int gather_src(int tap, int m, Pix q, int H, int W, bool& valid) {
+    if constexpr (MODE == G_CONV3) {
+        const int yy = q.y + tap / 3 - 1, xx = q.x + tap % 3 - 1;
+        valid = (yy >= 0) & (yy < H) & (xx >= 0) & (xx < W);
+        return valid ? (q.img * H + yy) * W + xx : m;
+    } else if constexpr (MODE == G_UP2) {
+        valid = true;
+        const int a = tap >> 1, b = tap & 1;
+        return (q.img * 2 * H + 2 * q.y + a) * (2 * W) + 2 * q.x + b;
+    } else {
+        valid = true;
+        return m;
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// Row-GEMM epilogue: accumulators acc[MT][NT] of wave (wm, wn) of the BM x BN block tile at
+// (m0, n0); tile_m indexes the per-block BN partial rows; smem (>= WAVES_M * 2 * BN doubles)
+// is free scratch (the caller has finished with its LDS images).
+// ------------------------------------------------------------------------------------
+template <int EMODE, int BM, int BN, int WM, int WN>
+__device__ __forceinline__ void row_epilogue(const RowGemmArgs& p, f32x16 (&acc)[WM / 32][WN / 32],
+                                             int m0, int n0, int tile_m, int wm, int wn,
+                                             int lane, int tid, float* smem) {
+    constexpr int MT = WM / 32, NT = WN / 32, WAVES_M = BM / WM;
+    const int li = lane & 31, lh = lane >> 5;
+    const int H = p.H, W = p.W;
+    if constexpr (EMODE == E_BIAS_RELU_STATS || EMODE == E_STATS) {
+        constexpr bool BR = EMODE == E_BIAS_RELU_STATS;
+        float s1[NT], s2[NT];
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+            const int n = n0 + wn * WN + nt * 32 + li;
+            const float b = BR ? p.bias[n] : 0.f;
+            s1[nt] = 0.f;
+            s2[nt] = 0.f;
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int m = m0 + wm * WM + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                    if (m < p.M) {
+                        const float v = BR ? fmaxf(acc[mt][nt][r] + b, 0.f) : acc[mt][nt][r];
+                        p.out[(size_t)m * p.ldo + p.ooff + n] = v;
+                        s1[nt] += v;
+                        s2[nt] += v * v;
+                    }
+                }
+            s1[nt] += __shfl_xor(s1[nt], 32);
+            s2[nt] += __shfl_xor(s2[nt], 32);
+        }
+        // combine the M-waves that share these columns (LDS is free after the loop)
+        __syncthreads();
+        float* red = smem;  // [WAVES_M][2][BN]
+        if (lh == 0) {
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) {
+                red[(wm * 2 + 0) * BN + wn * WN + nt * 32 + li] = s1[nt];
+                red[(wm * 2 + 1) * BN + wn * WN + nt * 32 + li] = s2[nt];
+            }
+        }
+        __syncthreads();
+        if (tid < BN) {
+            float a = 0.f, q = 0.f;
+#pragma unroll
+            for (int w = 0; w < WAVES_M; ++w) {
+                a += red[(w * 2 + 0) * BN + tid];
+                q += red[(w * 2 + 1) * BN + tid];
+            }
+            p.stats[(size_t)tile_m * 2 * p.N + n0 + tid] = a;
+            p.stats[(size_t)tile_m * 2 * p.N + p.N + n0 + tid] = q;
+        }
+    } else if constexpr (EMODE == E_STORE_BN) {
+        // BN-backward partials are differences of nearly equal sums downstream (sum do can be
+        // 1e-3 of sum |do|): accumulate in f64, round once per block.
+        const bool emask = p.escale != nullptr;
+        double q[NT][2];
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+            const int n = n0 + wn * WN + nt * 32 + li;
+            const float es = emask ? p.escale[n] : 0.f, eb = emask ? p.eshift[n] : 0.f;
+            q[nt][0] = q[nt][1] = 0.0;
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int m = m0 + wm * WM + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                    if (m < p.M) {
+                        float v = acc[mt][nt][r];
+                        const float y = p.ey[(size_t)m * p.ldey + p.offey + n];
+                        if (emask && !(es * y + eb > 0.f)) v = 0.f;
+                        p.out[(size_t)m * p.ldo + p.ooff + n] = v;
+                        q[nt][0] += v;
+                        q[nt][1] += (double)v * y;
+                    }
+                }
+#pragma unroll
+            for (int j = 0; j < 2; ++j) q[nt][j] += __shfl_xor(q[nt][j], 32);
+        }
+        __syncthreads();
+        double* red = (double*)smem;  // [WAVES_M][2][BN]
+        if (lh == 0) {
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) red[(wm * 2 + j) * BN + wn * WN + nt * 32 + li] = q[nt][j];
+        }
+        __syncthreads();
+        if (tid < BN) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                double a = 0.0;
+#pragma unroll
+                for (int w = 0; w < WAVES_M; ++w) a += red[(w * 2 + j) * BN + tid];
+                p.stats[((size_t)tile_m * 2 + j) * p.N + n0 + tid] = (float)a;
+            }
+        }
+    } else if constexpr (EMODE == E_CONVT) {
+        // one pixel decode per accumulator row (f32-reciprocal division), shared by the NT
+        // column groups: with K = Cin as short as 128 the epilogue is a large part of the
+        // block, and an integer-division decode per element cost more than its MFMAs
+        const float rH = 1.f / (float)H, rW = 1.f / (float)W;
+        int coff[NT], co_[NT];
+        float bb[NT];
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+            const int n = n0 + wn * WN + nt * 32 + li;
+            const int ab = n / p.cout, co = n - ab * p.cout;
+            coff[nt] = (ab >> 1) * (2 * W) + (ab & 1);  // (a, b) offset in the output grid
+            co_[nt] = co;
+            bb[nt] = p.bias[co];
+        }
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = m0 + wm * WM + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                if (m >= p.M) continue;
+                const Pix q = decode_fast(m, H, W, rH, rW);
+                const size_t ob = (size_t)(q.img * 2 * H + 2 * q.y) * (2 * W) + 2 * q.x;
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt)
+                    p.out[(ob + coff[nt]) * p.ldo + p.ooff + co_[nt]] = acc[mt][nt][r] + bb[nt];
+            }
+    } else if constexpr (EMODE == E_RESID || EMODE == E_ADD) {
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+            const int n = n0 + wn * WN + nt * 32 + li;
+            const float es = EMODE == E_RESID ? p.escale[n] : 0.f;
+            const float eb = EMODE == E_RESID ? p.eshift[n] : 0.f;
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int m = m0 + wm * WM + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                    if (m >= p.M) continue;
+                    float* o = p.out + (size_t)m * p.ldo + p.ooff + n;
+                    if constexpr (EMODE == E_RESID)
+                        *o = fmaxf(acc[mt][nt][r] + (es * p.ey[(size_t)m * p.ldey + p.offey + n] + eb),
+                                   0.f);
+                    else
+                        *o += acc[mt][nt][r];
+                }
+        }
+    } else {
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+            const int n = n0 + wn * WN + nt * 32 + li;
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int m = m0 + wm * WM + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                    if (m < p.M) p.out[(size_t)m * p.ldo + p.ooff + n] = acc[mt][nt][r];
+                }
+        }
+    }
+}
+
+}  // namespace

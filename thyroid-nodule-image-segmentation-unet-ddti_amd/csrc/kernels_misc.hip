@@ -530,6 +530,45 @@ __global__ void bn_dz_kernel(float* __restrict__ d, const float* __restrict__ y,
     }
 }
 
+// bf16 operand image for the LDS-DMA GEMMs (kernels_gemm16.hip): dst[m][c] (dense, ld C) =
+// bf16(op(src[m * ld + off + c])), op = scale * x + shift when scale is set, then ReLU on
+// channels c < relu (BN -> ReLU order, models/mod.py:46-47; a [skip, up] concat has it on
+// the skip half only).  Round to nearest even -- the rounding the register-staged bf16 GEMMs
+// apply when they stage the same values.  tpr threads per row, 8 channels each.
+__global__ __launch_bounds__(256) void to_bf16_kernel(const float* __restrict__ src, int ld, int off,
+                                                      int C, const float* __restrict__ scale,
+                                                      const float* __restrict__ shift, int relu,
+                                                      int64_t P, int tpr, __bf16* __restrict__ dst) {
+    typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+    const int rpp = 256 / tpr;
+    const int c_first = (threadIdx.x % tpr) * 8;
+    for (int64_t m = (int64_t)blockIdx.x * rpp + threadIdx.x / tpr; m < P;
+         m += (int64_t)gridDim.x * rpp) {
+        const float* row = src + m * ld + off;
+        for (int c = c_first; c < C; c += tpr * 8) {
+            f32x4 v0 = *(const f32x4*)(row + c), v1 = *(const f32x4*)(row + c + 4);
+            if (scale) {
+                v0 = v0 * *(const f32x4*)(scale + c) + *(const f32x4*)(shift + c);
+                v1 = v1 * *(const f32x4*)(scale + c + 4) + *(const f32x4*)(shift + c + 4);
+            }
+            if (c < relu) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    v0[j] = fmaxf(v0[j], 0.f);
+                    v1[j] = fmaxf(v1[j], 0.f);
+                }
+            }
+            bf16x8 o;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                o[j] = (__bf16)v0[j];
+                o[4 + j] = (__bf16)v1[j];
+            }
+            *(bf16x8*)(dst + m * C + c) = o;
+        }
+    }
+}
+
 // bias gradient from the wgrad kernels' column sums: out[co] = sum_s sum_tap slab[s][tap*C+co]
 __global__ void bias_reduce_kernel(const float* __restrict__ slab, int S, int taps, int C,
                                    float* __restrict__ out) {
@@ -1062,6 +1101,16 @@ int k_bn_dz(float* d, const float* y, int ld, int off, int64_t P, int C, const f
     else
         hipLaunchKernelGGL(bn_dz_kernel, dim3(grid_for(P * (C / 4))), dim3(256), 0, s, d, y, ld, off,
                            P, C, coef, mask);
+    LAUNCH_CHECK();
+}
+int k_to_bf16(const float* src, int ld, int off, int C, const float* scale, const float* shift,
+              int relu, int64_t P, uint16_t* dst, hipStream_t s) {
+    if (C % 8 || ld % 4 || off % 4 || (scale == nullptr) != (shift == nullptr)) return -1;
+    const int c8 = C / 8;
+    const int tpr = c8 >= 256 ? 256 : c8;
+    if (256 % tpr || (c8 > 256 && c8 % 256)) return -1;
+    hipLaunchKernelGGL(to_bf16_kernel, dim3(grid_for(P * tpr)), dim3(256), 0, s, src, ld, off, C,
+                       scale, shift, relu, P, tpr, (__bf16*)dst);
     LAUNCH_CHECK();
 }
 int k_bias_reduce(const float* slab, int S, int taps, int C, float* out, hipStream_t s) {

@@ -310,6 +310,9 @@ struct Plan {
     float* hpart;  // head / conv-first weight-gradient partials
     float* bslab;  // [splits][Nw] bias-gradient column sums from the wgrad kernels
     float* coef;
+    // bf16 LDS-DMA GEMMs: prepared operand image (dense [pixels][C] bf16) and a zero page
+    uint16_t* s16;
+    void* zero16;
     size_t bytes;
 };
 
@@ -452,6 +455,16 @@ void make_plan(unet_ctx* c, int N, int H, int W, bool training, char* base, Plan
     }
     p.stats = b.take<float>(srows);
     p.stats2 = b.take<float>((int64_t)STAT_G * 2 * c->cmax);
+    p.s16 = nullptr;
+    p.zero16 = nullptr;
+    if (c->bf16) {
+        int64_t n16 = 0;
+        for (const ConvL& L : c->conv) n16 = std::max(n16, p.P[L.level] * std::max(L.cin, L.cout));
+        for (const ConvTL& T : c->convt)
+            n16 = std::max(n16, std::max(p.P[T.in_level] * T.cin, p.P[T.in_level - 1] * T.cout));
+        p.s16 = b.take<uint16_t>(n16);
+        p.zero16 = b.take<char>(256);
+    }
     if (training) {
         int64_t gmax = p.P[0] * c->base;
         for (int i = 0; i < NC; ++i) {
@@ -673,6 +686,37 @@ void set_weights(const unet_ctx* c, RowGemmArgs& g, const float* img) {
         g.bt = img;
 }
 
+// bf16 math: conv / ConvT GEMMs whose K channels are a multiple of 64 and whose N is a
+// multiple of 128 run on the LDS-DMA kernel (kernels_gemm16.hip) from a prepared bf16
+// operand image; UNET_RG16=0 keeps the register-staged bf16 kernel (A/B runs),
+// UNET_RG16_TILE picks its tile (kernels_gemm16.hip ROWGEMM16_TILES).
+// (read per call, so a test can compare both kernels in one process)
+bool rg16_on(const unet_ctx* c, int C, int N) {
+    const char* e = getenv("UNET_RG16");
+    return c->bf16 && (e ? atoi(e) : 1) != 0 && C % 64 == 0 && N % 128 == 0;
+}
+int rg16_tile() {
+    const char* e = getenv("UNET_RG16_TILE");
+    return e ? atoi(e) : 0;
+}
+std::string tlabel16(const char* fam, int tile, int layer) {
+    int bm = 0, bn = 0;
+    rowgemm16_tile_dims(tile, &bm, &bn);
+    char b[112];
+    snprintf(b, sizeof b, "%s/rg16_%dx%d_t%d|%d", fam, bm, bn, tile, layer);
+    return b;
+}
+// point g's A operand at the prepared bf16 image (lda = C channels)
+void use_a16(const Plan& p, RowGemmArgs& g, int C) {
+    g.a16 = p.s16;
+    g.lda = C;
+    g.aoff = 0;
+    g.ascale = g.ashift = nullptr;
+    g.arelu = 0;
+    g.acoef = nullptr;
+    g.zero16 = p.zero16;
+}
+
 int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, const float* x,
                  float* logits, Plan& p, bool training, hipStream_t s) {
     Launcher L{c, s};
@@ -708,6 +752,7 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
         RUN("fill", 0, k_fill(p.cat_scale[l] + uo, C, 1.f, s));
         RUN("fill", 0, k_fill(p.cat_shift[l] + uo, C, 0.f, s));
     }
+    if (p.zero16) RUN("fill", 0, (int)hipMemsetAsync(p.zero16, 0, 256, s));
     // in_channels == 1: NCHW == NHWC; keep a private copy for the conv-0 wgrad
     RUN("copy_x", 0, (int)hipMemcpyAsync(p.x_nhwc, x, sizeof(float) * p.P[0] * c->in_ch,
                                          hipMemcpyDeviceToDevice, s));
@@ -746,6 +791,18 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
             g.bias = bias_ptr(prm, C.b);
             g.stats = p.stats;
             g.emode = c->bn_relu ? E_STATS : E_BIAS_RELU_STATS;
+            if (rg16_on(c, C.cin, C.cout)) {
+                RUN("prep16", 0, k_to_bf16(a.ptr, a.ld, a.off, C.cin, a.scale, a.shift, a.relu, M,
+                                           p.s16, s));
+                use_a16(p, g, C.cin);
+                const int tile = rg16_tile();
+                int bm, bn;
+                rowgemm16_tile_dims(tile, &bm, &bn);
+                R = (int)((M + bm - 1) / bm);
+                RUN(tlabel16("conv_fwd", tile, i), 2.0 * M * C.cout * 9 * C.cin,
+                    launch_rowgemm16(g, tile, s));
+                return stats_finalize(c, L, p, i, R, M, training, prm, bn_run, bn_cnt);
+            }
             const int tile = pick_tile(C.cout, false, c->bf16, M);
             int bm, bn, bk;
             rowgemm_tile_dims(tile, &bm, &bn, &bk);
@@ -785,6 +842,15 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
         g.bias = prm + T.b;
         g.cout = T.cout;
         g.emode = E_CONVT;
+        if (!c->res && rg16_on(c, T.cin, T.cout)) {
+            RUN("prep16", 0, k_to_bf16(g.a, g.lda, g.aoff, T.cin, g.ascale, g.ashift, g.arelu, g.M,
+                                       p.s16, s));
+            use_a16(p, g, T.cin);
+            const int tile = rg16_tile();
+            RUN(tlabel16("convT_fwd", tile, 100 + k), 2.0 * g.M * g.N * g.K,
+                launch_rowgemm16(g, tile, s));
+            return 0;
+        }
         const int tile = pick_tile(T.cout, false, c->bf16, 4 * (int64_t)g.M);  // grid N = 4 cout
         RUN(tlabel("convT_fwd", tile, 100 + k), 2.0 * g.M * g.N * g.K, launch_rowgemm(g, tile, s));
         return 0;
@@ -1052,6 +1118,17 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
                 }
                 g.stats = p.part;
             }
+            if (!dzc && rg16_on(c, C.cout, C.cin)) {
+                RUN("prep16", 0, k_to_bf16(dout, C.cout, 0, C.cout, nullptr, nullptr, 0, P, p.s16, s));
+                use_a16(p, g, C.cout);
+                const int tile = rg16_tile();
+                int bm, bn;
+                rowgemm16_tile_dims(tile, &bm, &bn);
+                if (rows) *rows = (int)((P + bm - 1) / bm);
+                RUN(tlabel16("conv_dgrad", tile, i), 2.0 * P * C.cout * 9 * C.cin,
+                    launch_rowgemm16(g, tile, s));
+                return 0;
+            }
             const int tile = pick_tile(C.cin, true, c->bf16, P);
             int bm, bn, bk;
             rowgemm_tile_dims(tile, &bm, &bn, &bk);
@@ -1136,6 +1213,18 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
                 g.eshift = p.shift[src];
             }
             g.stats = p.part;
+        }
+        if (!c->res && rg16_on(c, T.cout, T.cin)) {
+            RUN("prep16", 0, k_to_bf16(p.dcat[lo], ldo, uo, T.cout, nullptr, nullptr, 0, p.P[lo],
+                                       p.s16, s));
+            use_a16(p, g, T.cout);
+            const int tile = rg16_tile();
+            int bm, bn;
+            rowgemm16_tile_dims(tile, &bm, &bn);
+            *rows = (int)((Pin + bm - 1) / bm);
+            RUN(tlabel16("convT_dgrad", tile, 100 + k), 2.0 * Pin * T.cin * 4 * T.cout,
+                launch_rowgemm16(g, tile, s));
+            return 0;
         }
         const int tile = pick_tile(T.cin, true, c->bf16, Pin);
         int bm, bn, bk;
