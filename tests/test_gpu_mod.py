@@ -158,18 +158,21 @@ def _to64(d):
 
 @pytest.mark.parametrize("tile", ["0", "1", "3"])
 def test_rg16_bit_identical_to_register_staged(tile, monkeypatch):
-    """The LDS-DMA bf16 GEMMs (kernels_gemm16.hip, fed by the k_to_bf16 operand images)
-    against the register-staged bf16 kernel (UNET_RG16=0) on a base-128 network, where
-    every GEMM but the Cin = 1 first conv takes the new path: the same bf16 roundings of
-    the same f32 values, the same K order and 128-row BN partials, so one training step
-    gives bit-identical logits, gradients and BN statistics for every 128-row tile."""
+    """The LDS-DMA bf16 GEMMs (kernels_gemm16.hip, fed by the k_to_bf16 operand images:
+    row GEMMs and the transposed-read weight gradients) against the register-staged bf16
+    kernels (UNET_RG16=0, UNET_WG16=0) on a base-128 network, where every GEMM but the
+    Cin = 1 first conv takes the new path: the same bf16 roundings of the same f32 values,
+    the same K order, split-K partition and 128-row BN partials, so one training step gives
+    bit-identical logits, gradients and BN statistics for every 128-row tile."""
     import unet_hip
     x, t = inputs(23, 2, 128, 128)
     P = MO.make_params(9, 128, 3)
     outs = []
     for flag in ("0", "1"):
         monkeypatch.setenv("UNET_RG16", flag)
+        monkeypatch.setenv("UNET_WG16", flag)
         monkeypatch.setenv("UNET_RG16_TILE", tile)
+        monkeypatch.setenv("UNET_WG16_TILE", "1" if tile == "1" else "0")
         m = unet_hip.ModUNet(1, 1, base_filters=128, depth=3, mfma_dtype="bf16")
         sd = m.state_dict()
         for k, v in P.items():

@@ -95,6 +95,7 @@ struct WgradArgs {
     const float* bcoef;
     float* bias_slab;    // optional [splits][Nw]: column sums of B' (the bias gradient)
     int bf16;            // bf16 MFMA (operands rounded to bf16 in LDS, f32 accumulate)
+    const void* zero16;  // wgrad16: >= 16 zero bytes (padding taps / pixels past the split)
     int xcd;             // remap blocks so each XCD gets a contiguous range of tiles
 };
 
@@ -116,6 +117,7 @@ int rowgemm_tile_dbuf(int tile);
 int launch_rowgemm16(const RowGemmArgs& a, int tile, hipStream_t s);
 int rowgemm16_tile_dims(int tile, int* bm, int* bn);
 int launch_wgrad(const WgradArgs& a, int tile, hipStream_t s);
+int launch_wgrad16(const WgradArgs& a, int tile, hipStream_t s);
 int wgrad_tile_dims(int tile, int* bm, int* bn, int* bkp);
 int wgrad_tile_taps(int tile);  // taps of the M dimension one block covers (3 for 20..)
 // bf16 wgrad tile ids (a.bf16): 0 = 128x128/32 px, 1 = 128x128/64, 2 = 64x64/64,

@@ -22,6 +22,8 @@
 // in flight x loads per chunk), s_barrier (every wave's DMA for chunk k has landed), MFMAs
 // from stage k % S, s_barrier (stage free for reuse).  Raw s_barrier, not __syncthreads():
 // the latter's fence would drain the DMAs still in flight.
+#include <type_traits>
+
 #include "gemm_common.h"
 
 namespace {
@@ -210,6 +212,228 @@ static int rg16_tile(const RowGemmArgs& a, int tile, hipStream_t s) {
     return -1;
 }
 
+// ------------------------------------------------------------------------------------
+// Weight gradient on LDS-DMA bf16 operands: dW[m][n] = sum_p A'[p][m] * B'[p][n], the
+// reduction over pixels p split into `splits` slices of pps pixels, each block writing its
+// fp32 tile of slab[split] (k_slab_reduce sums the slices in fixed order).  A' = gather of
+// the conv input's bf16 image (tap = m / CA), B' = the bf16 image of dz (G_IDENT) or of the
+// ConvT output gradient (G_UP2, tap = n / CB).
+//
+// The MFMA wants 8 consecutive PIXELS of one channel per lane, while the images are
+// pixel-major (NHWC).  LDS holds [BKP pixels][128 channels] (256-B rows, filled by
+// global_load_lds: one wave-instruction = 4 pixel rows) and the operands are read with
+// ds_read_b64_tr_b16, which hands lane i of each 16-lane group column i of a 4-row x
+// 16-column block: two such reads give a lane channel c's pixels 8h .. 8h+7.  The 16-B
+// chunk ch of pixel row r sits in slot ch ^ ((r & 3) << 2), so the four rows a group reads
+// land in four different bank quarters (conflict-free per 32-lane half).
+// ------------------------------------------------------------------------------------
+typedef short short4v __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) short4v lds_short4;
+
+// ds_read_b64_tr_b16 as inline asm: through the builtin, hipcc cannot tell the read from
+// the LDS-DMA writes still in flight and drains them (s_waitcnt vmcnt(0)) before every
+// k-step.  An asm read is outside hipcc's wait bookkeeping, so the caller waits lgkmcnt
+// itself and fences the MFMAs behind it with sched_barrier (cdna_hip_programming.md rule 18).
+template <int OFF>
+__device__ __forceinline__ short4v ds_tr16(unsigned addr) {
+    short4v r;
+    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(OFF));
+    return r;
+}
+
+__device__ __forceinline__ unsigned lds_u32(const void* p) {
+    return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+
+template <int BM_, int BN_, int WM_, int WN_, int BKP_, int S_, int OCC_>
+struct WTile16 {
+    static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, BKP = BKP_, S = S_, OCC = OCC_;
+    static constexpr int WAVES = (BM / WM) * (BN / WN);
+    static constexpr int THREADS = 64 * WAVES;
+};
+
+template <int AMODE, int BMODE, class T>
+__global__ __launch_bounds__(T::THREADS, T::OCC) void wgrad16_kernel(WgradArgs p) {
+    constexpr int BM = T::BM, BN = T::BN, WM = T::WM, WN = T::WN, BKP = T::BKP, S = T::S;
+    constexpr int WAVES = T::WAVES, WAVES_N = BN / WN;
+    constexpr int MT = WM / 32, NT = WN / 32;
+    static_assert(BM == 128 && BN == 128, "256-B pixel rows");
+    constexpr int RB = 256;                                  // bytes per pixel row
+    constexpr int AI = BKP / (4 * WAVES), BI = BKP / (4 * WAVES);  // DMA instructions per chunk
+    static_assert(AI * 4 * WAVES == BKP, "loader shape");
+    constexpr int GPC = AI + BI;
+    constexpr int STAGE = 2 * BKP * RB;
+    __shared__ __attribute__((aligned(1024))) char smem[STAGE * S];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+    const int tiles_n = p.Nw / BN, tiles_m = p.Mw / BM;
+    int idx = p.xcd ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+    const int tn = idx % tiles_n;
+    idx /= tiles_n;
+    const int tm = idx % tiles_m;
+    const int split = idx / tiles_m;
+    const int tapA = (tm * BM) / p.CA, ca0 = tm * BM - tapA * p.CA;
+    const int tapB = (tn * BN) / p.CB, cb0 = tn * BN - tapB * p.CB;
+    const int H = p.H, W = p.W;
+    const float rH = 1.f / (float)H, rW = 1.f / (float)W;
+    const int pbeg = split * p.pps;
+    const int pend = min(pbeg + p.pps, p.P);
+    const int nk = (pend - pbeg + BKP - 1) / BKP;
+
+    // loader: instruction j of this wave fills pixel rows (j * WAVES + wave) * 4 .. + 3;
+    // lane l -> row l / 16, slot l % 16 holding global chunk slot ^ ((row & 3) << 2)
+    const int lr = lane >> 4;
+    const int gch = ((lane & 15) ^ (lr << 2)) * 8;
+    const uint16_t* a16 = (const uint16_t*)p.a;
+    const uint16_t* b16 = (const uint16_t*)p.b;
+    const uint16_t* zero = (const uint16_t*)p.zero16;
+
+    auto issue = [&](int kc, int st) {
+        const int pc = pbeg + kc * BKP;
+        char* base = smem + st * STAGE;
+#pragma unroll
+        for (int j = 0; j < AI; ++j) {
+            const int pix = pc + (j * WAVES + wave) * 4 + lr;
+            const bool in = pix < pend;
+            const int m = in ? pix : pend - 1;
+            bool valid;
+            const Pix q = AMODE == G_IDENT ? Pix{0, 0, 0} : decode_fast(m, H, W, rH, rW);
+            const int src = gather_src<AMODE>(tapA, m, q, H, W, valid);
+            const uint16_t* g = (valid && in) ? a16 + (size_t)src * p.lda + ca0 + gch : zero;
+            glds16(g, base + (j * WAVES + wave) * 1024);
+        }
+#pragma unroll
+        for (int j = 0; j < BI; ++j) {
+            const int pix = pc + (j * WAVES + wave) * 4 + lr;
+            const bool in = pix < pend;
+            const int m = in ? pix : pend - 1;
+            bool valid;
+            const Pix q = BMODE == G_IDENT ? Pix{0, 0, 0} : decode_fast(m, H, W, rH, rW);
+            const int src = gather_src<BMODE>(tapB, m, q, H, W, valid);
+            const uint16_t* g = (valid && in) ? b16 + (size_t)src * p.ldb + cb0 + gch : zero;
+            glds16(g, base + BKP * RB + (j * WAVES + wave) * 1024);
+        }
+    };
+
+    f32x16 acc[MT][NT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    // transposed-read addresses (bytes within a stage, k-step 0, read t = 0): lane l of
+    // group g = l / 16 supplies row 8 (g >> 1) + q, columns 16 (g & 1) + 4 p (l % 16 = 4q + p)
+    const int g = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
+    const int trow = 8 * (g >> 1) + qq;  // + 4 t + 16 kk: (row & 3) stays qq
+    int aoff[MT], boff[NT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+        const int col = wm * WM + mt * 32 + 16 * (g & 1) + 4 * pp;
+        aoff[mt] = trow * RB + (((col >> 3) ^ (qq << 2)) << 4) + ((col >> 2) & 1) * 8;
+    }
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+        const int col = wn * WN + nt * 32 + 16 * (g & 1) + 4 * pp;
+        boff[nt] = BKP * RB + trow * RB + (((col >> 3) ^ (qq << 2)) << 4) + ((col >> 2) & 1) * 8;
+    }
+
+#pragma unroll
+    for (int s = 0; s < S - 1; ++s)
+        if (s < nk) issue(s, s);
+    for (int kc = 0; kc < nk; ++kc) {
+        if (kc + S - 1 < nk) issue(kc + S - 1, (kc + S - 1) % S);
+        const int ahead = min(S - 1, nk - 1 - kc);
+        if constexpr (S >= 3) {
+            if (ahead >= 2) wait_vm<2 * GPC>();
+            else if (ahead == 1) wait_vm<GPC>();
+            else wait_vm<0>();
+        } else {
+            if (ahead >= 1) wait_vm<GPC>();
+            else wait_vm<0>();
+        }
+        block_barrier();
+        const unsigned sb = lds_u32(smem) + (kc % S) * STAGE;
+        // fragments of k-step kk (A then B; two transposed reads each), software-pipelined:
+        // the reads of kk + 1 are in flight while the MFMAs of kk run
+        short4v fa[2][MT][2], fb[2][NT][2];
+        auto load = [&](auto KK) {
+            constexpr int kk = decltype(KK)::value, set = kk & 1;
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt) {
+                fa[set][mt][0] = ds_tr16<kk * 16 * RB>(sb + aoff[mt]);
+                fa[set][mt][1] = ds_tr16<kk * 16 * RB + 4 * RB>(sb + aoff[mt]);
+            }
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) {
+                fb[set][nt][0] = ds_tr16<kk * 16 * RB>(sb + boff[nt]);
+                fb[set][nt][1] = ds_tr16<kk * 16 * RB + 4 * RB>(sb + boff[nt]);
+            }
+        };
+        auto mma = [&](auto KK) {
+            constexpr int set = decltype(KK)::value & 1;
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt)
+                    acc[mt][nt] = mfma32_bf16(*(const bf16x8*)fa[set][mt], *(const bf16x8*)fb[set][nt],
+                                              acc[mt][nt]);
+        };
+        static_assert(BKP == 64, "four k-steps per chunk");
+        constexpr int RD = 2 * (MT + NT);  // reads per k-step
+        load(std::integral_constant<int, 0>{});
+        load(std::integral_constant<int, 1>{});
+        asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(RD) : "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        mma(std::integral_constant<int, 0>{});
+        __builtin_amdgcn_sched_barrier(0);
+        load(std::integral_constant<int, 2>{});
+        asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(RD) : "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        mma(std::integral_constant<int, 1>{});
+        __builtin_amdgcn_sched_barrier(0);
+        load(std::integral_constant<int, 3>{});
+        asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(RD) : "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        mma(std::integral_constant<int, 2>{});
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        mma(std::integral_constant<int, 3>{});
+        block_barrier();
+    }
+
+    const int li = lane & 31, lh = lane >> 5;
+    float* slab = p.slab + (size_t)split * p.Mw * p.Nw;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = tm * BM + wm * WM + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                const int n = tn * BN + wn * WN + nt * 32 + li;
+                slab[(size_t)m * p.Nw + n] = acc[mt][nt][r];
+            }
+}
+
+// wgrad16 tiles: 0 = 128x128, 64 pixels per stage, 2 stages (64 KB, 2 blocks/CU);
+// 1 = the same with 3 stages (96 KB, 1 block/CU)
+using W16_0 = WTile16<128, 128, 64, 64, 64, 2, 2>;
+using W16_1 = WTile16<128, 128, 64, 64, 64, 3, 1>;
+#define WGRAD16G_TILES(X) X(0, W16_0) X(1, W16_1)
+
+template <int AMODE, int BMODE, class T>
+static int wg16_go(const WgradArgs& a, hipStream_t s) {
+    if (a.Mw % T::BM || a.Nw % T::BN || a.CA % T::BM || a.CB % T::BN || a.pps % T::BKP) return -1;
+    const dim3 grid((a.Mw / T::BM) * (a.Nw / T::BN) * a.splits);
+    hipLaunchKernelGGL((wgrad16_kernel<AMODE, BMODE, T>), grid, dim3(T::THREADS), 0, s, a);
+    return (int)hipGetLastError();
+}
+
 }  // namespace
 
 int rowgemm16_tile_dims(int tile, int* bm, int* bn) {
@@ -236,5 +460,22 @@ int launch_rowgemm16(const RowGemmArgs& a, int tile, hipStream_t s) {
     if (a.amode == G_CONV3 && a.emode == E_STORE_BN) return rg16_tile<G_CONV3, E_STORE_BN>(a, tile, s);
     if (a.amode == G_IDENT && a.emode == E_CONVT) return rg16_tile<G_IDENT, E_CONVT>(a, tile, s);
     if (a.amode == G_UP2 && a.emode == E_STORE_BN) return rg16_tile<G_UP2, E_STORE_BN>(a, tile, s);
+    return -1;
+}
+
+// Weight gradient from bf16 images: a / b point at uint16 images [pixels][lda] /
+// [pixels][ldb] (aoff / boff must be 0: the images are dense), zero16 at a zeroed page.
+// 3x3 conv (A' G_CONV3, B' G_IDENT) and ConvT (A' G_IDENT, B' G_UP2); no bias column sums.
+int launch_wgrad16(const WgradArgs& a, int tile, hipStream_t s) {
+    if (a.aoff || a.boff || a.ascale || a.bcoef || a.bias_slab || !a.zero16 || a.P < 1) return -1;
+#define WG16G(AM, BMD)                                   \
+    do {                                                 \
+        if (tile == 0) return wg16_go<AM, BMD, W16_0>(a, s); \
+        if (tile == 1) return wg16_go<AM, BMD, W16_1>(a, s); \
+        return -1;                                       \
+    } while (0)
+    if (a.amode == G_CONV3 && a.bmode == G_IDENT) WG16G(G_CONV3, G_IDENT);
+    if (a.amode == G_IDENT && a.bmode == G_UP2) WG16G(G_IDENT, G_UP2);
+#undef WG16G
     return -1;
 }

@@ -313,6 +313,7 @@ struct Plan {
     // bf16 LDS-DMA GEMMs: prepared operand image (dense [pixels][C] bf16) and a zero page
     uint16_t* s16;
     void* zero16;
+    std::vector<uint16_t*> x16;  // training, bf16: per-conv input images kept for the wgrad
     size_t bytes;
 };
 
@@ -385,6 +386,32 @@ WgradCfg wgrad_cfg(int CA, int tapsA, int CB, int tapsB, int64_t P, bool bf16, i
     w.pps = (int)pps;
     w.splits = (int)((P + pps - 1) / pps);
     return w;
+}
+
+// bf16 math: conv / ConvT GEMMs whose K channels are a multiple of 64 and whose N is a
+// multiple of 128 run on the LDS-DMA kernel (kernels_gemm16.hip) from a prepared bf16
+// operand image; UNET_RG16=0 keeps the register-staged bf16 kernel (A/B runs),
+// UNET_RG16_TILE picks its tile (kernels_gemm16.hip ROWGEMM16_TILES).
+// (read per call, so a test can compare both kernels in one process)
+bool rg16_on(const unet_ctx* c, int C, int N) {
+    const char* e = getenv("UNET_RG16");
+    return c->bf16 && (e ? atoi(e) : 1) != 0 && C % 64 == 0 && N % 128 == 0;
+}
+int rg16_tile() {
+    const char* e = getenv("UNET_RG16_TILE");
+    return e ? atoi(e) : 0;
+}
+// 3x3 weight gradients of layers with Cin, Cout multiples of 128 on the LDS-DMA
+// transposed-read kernel (kernels_gemm16.hip wgrad16_kernel) from the forward's bf16 input
+// image and the dz image; UNET_WG16=0 keeps the register-staged bf16 wgrad, UNET_WG16_TILE
+// picks the tile.
+bool wg16_on(const unet_ctx* c, int CA, int CB) {
+    const char* e = getenv("UNET_WG16");
+    return c->bf16 && (e ? atoi(e) : 1) != 0 && CA % 128 == 0 && CB % 128 == 0;
+}
+int wg16_tile() {
+    const char* e = getenv("UNET_WG16_TILE");
+    return e ? atoi(e) : 0;
 }
 
 void make_plan(unet_ctx* c, int N, int H, int W, bool training, char* base, Plan& p) {
@@ -465,6 +492,10 @@ void make_plan(unet_ctx* c, int N, int H, int W, bool training, char* base, Plan
         p.s16 = b.take<uint16_t>(n16);
         p.zero16 = b.take<char>(256);
     }
+    p.x16.assign(NC, nullptr);
+    for (int i = 0; i < NC && training; ++i)
+        if (wg16_on(c, c->conv[i].cin, c->conv[i].cout) && rg16_on(c, c->conv[i].cin, c->conv[i].cout))
+            p.x16[i] = b.take<uint16_t>(p.P[c->conv[i].level] * c->conv[i].cin);
     if (training) {
         int64_t gmax = p.P[0] * c->base;
         for (int i = 0; i < NC; ++i) {
@@ -686,19 +717,6 @@ void set_weights(const unet_ctx* c, RowGemmArgs& g, const float* img) {
         g.bt = img;
 }
 
-// bf16 math: conv / ConvT GEMMs whose K channels are a multiple of 64 and whose N is a
-// multiple of 128 run on the LDS-DMA kernel (kernels_gemm16.hip) from a prepared bf16
-// operand image; UNET_RG16=0 keeps the register-staged bf16 kernel (A/B runs),
-// UNET_RG16_TILE picks its tile (kernels_gemm16.hip ROWGEMM16_TILES).
-// (read per call, so a test can compare both kernels in one process)
-bool rg16_on(const unet_ctx* c, int C, int N) {
-    const char* e = getenv("UNET_RG16");
-    return c->bf16 && (e ? atoi(e) : 1) != 0 && C % 64 == 0 && N % 128 == 0;
-}
-int rg16_tile() {
-    const char* e = getenv("UNET_RG16_TILE");
-    return e ? atoi(e) : 0;
-}
 std::string tlabel16(const char* fam, int tile, int layer) {
     int bm = 0, bn = 0;
     rowgemm16_tile_dims(tile, &bm, &bn);
@@ -792,9 +810,11 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
             g.stats = p.stats;
             g.emode = c->bn_relu ? E_STATS : E_BIAS_RELU_STATS;
             if (rg16_on(c, C.cin, C.cout)) {
+                uint16_t* img = p.x16[i] ? p.x16[i] : p.s16;
                 RUN("prep16", 0, k_to_bf16(a.ptr, a.ld, a.off, C.cin, a.scale, a.shift, a.relu, M,
-                                           p.s16, s));
+                                           img, s));
                 use_a16(p, g, C.cin);
+                g.a16 = img;
                 const int tile = rg16_tile();
                 int bm, bn;
                 rowgemm16_tile_dims(tile, &bm, &bn);
@@ -1045,8 +1065,14 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
             RUN("bn_dz", 0, k_bn_dz(const_cast<float*>(dout), p.y[i], p.ldy[i], p.offy[i], P, C.cout,
                                     p.coef, dz_mask, s));
         }
-        side_after_main();
         const float* dzc = dz_in_loaders ? p.coef : nullptr;
+        // bf16 image of dz: A operand of the LDS-DMA dgrad, B' of the LDS-DMA wgrad
+        const bool dz16 = !dzc && (rg16_on(c, C.cout, C.cin) || p.x16[i]);
+        if (dz16) {
+            before_write(p.s16);
+            RUN("prep16", 0, k_to_bf16(dout, C.cout, 0, C.cout, nullptr, nullptr, 0, P, p.s16, s));
+        }
+        side_after_main();
         Operand a = conv_input(c, p, i);
         WgradCfg wc = wgrad_cfg(C.cin, 9, C.cout, 1, P, c->bf16, Wl);
         WgradArgs w{};
@@ -1078,8 +1104,25 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         w.splits = wc.splits;
         w.slab = p.slab;
         w.bf16 = c->bf16;
-        RUNW(wlabel("conv_wgrad", wc, i), 2.0 * P * C.cout * 9 * C.cin,
-             launch_wgrad(w, wc.tile, sw));
+        if (p.x16[i] && !dzc) {
+            w.a = (const float*)p.x16[i];
+            w.lda = C.cin;
+            w.aoff = 0;
+            w.ascale = w.ashift = nullptr;
+            w.arelu = 0;
+            w.b = (const float*)p.s16;
+            w.by = nullptr;
+            w.bcoef = nullptr;
+            w.zero16 = p.zero16;
+            const int t = wg16_tile();
+            char lb[96];
+            snprintf(lb, sizeof lb, "conv_wgrad/wg16_128x128_t%d|%d", t, i);
+            RUNW(lb, 2.0 * P * C.cout * 9 * C.cin, launch_wgrad16(w, t, sw));
+            side_read(p.s16);
+        } else {
+            RUNW(wlabel("conv_wgrad", wc, i), 2.0 * P * C.cout * 9 * C.cin,
+                 launch_wgrad(w, wc.tile, sw));
+        }
         side_read(dout);
         RUNW("wgrad_reduce", 0,
              k_slab_reduce(p.slab, wc.splits, w.Mw, w.Nw, 0, C.cin, C.cout, grads + C.w, sw));
@@ -1118,8 +1161,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
                 }
                 g.stats = p.part;
             }
-            if (!dzc && rg16_on(c, C.cout, C.cin)) {
-                RUN("prep16", 0, k_to_bf16(dout, C.cout, 0, C.cout, nullptr, nullptr, 0, P, p.s16, s));
+            if (dz16 && rg16_on(c, C.cout, C.cin)) {
                 use_a16(p, g, C.cout);
                 const int tile = rg16_tile();
                 int bm, bn;
