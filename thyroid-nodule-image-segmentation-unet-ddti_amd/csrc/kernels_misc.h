@@ -35,6 +35,9 @@ int k_bn_dz(float* d, const float* y, int ld, int off, int64_t P, int C, const f
 // dense bf16 image [P][C] of op(src) for the LDS-DMA GEMMs (affine if scale, ReLU on c < relu)
 int k_to_bf16(const float* src, int ld, int off, int C, const float* scale, const float* shift,
               int relu, int64_t P, uint16_t* dst, hipStream_t s);
+// bn_dz writing the dense bf16 image of dz (and the f32 dz in place when f32 != 0)
+int k_bn_dz16(float* d, const float* y, int ld, int off, int64_t P, int C, const float* coef,
+              int mask, uint16_t* dz16, int f32, hipStream_t s);
 int k_bias_reduce(const float* slab, int S, int taps, int C, float* out, hipStream_t s);
 int k_sum_partials(const float* part, int G, int ncols, float* out, hipStream_t s);
 int k_slab_reduce(const float* slab, int S, int Mw, int Nw, int kind, int cin, int cout,

@@ -511,6 +511,40 @@ __global__ __launch_bounds__(256) void bn_dz_rows_kernel(float* __restrict__ d,
     }
 }
 
+// bn_dz for the bf16 GEMMs: dz as the dense bf16 image the LDS-DMA dgrad / wgrad read
+// (round to nearest even, as k_to_bf16), and the f32 dz in place only when another consumer
+// still reads it (f32 != 0).  8 channels per thread.
+__global__ __launch_bounds__(256) void bn_dz16_kernel(float* __restrict__ d, const float* __restrict__ y,
+                                                      int ld, int off, int64_t P, int C,
+                                                      const float* __restrict__ coef, int mask,
+                                                      int tpr, __bf16* __restrict__ dz16, int f32) {
+    typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+    const int rpp = 256 / tpr;
+    const int c_first = (threadIdx.x % tpr) * 8;
+    for (int64_t m = (int64_t)blockIdx.x * rpp + threadIdx.x / tpr; m < P;
+         m += (int64_t)gridDim.x * rpp) {
+        for (int c = c_first; c < C; c += tpr * 8) {
+            bf16x8 o16;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int cc = c + 4 * h;
+                f32x4* pd = (f32x4*)(d + m * C + cc);
+                const f32x4 v = *(const f32x4*)(y + m * ld + off + cc);
+                const f32x4 r = *(const f32x4*)(coef + cc) * (*pd) + *(const f32x4*)(coef + C + cc) * v +
+                                *(const f32x4*)(coef + 2 * C + cc);
+                f32x4 o;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    o[j] = (!mask || v[j] > 0.f) ? r[j] : 0.f;
+                    o16[4 * h + j] = (__bf16)o[j];
+                }
+                if (f32) *pd = o;
+            }
+            *(bf16x8*)(dz16 + m * C + c) = o16;
+        }
+    }
+}
+
 __global__ void bn_dz_kernel(float* __restrict__ d, const float* __restrict__ y, int ld, int off,
                              int64_t P, int C, const float* __restrict__ coef, int mask) {
     const int c4n = C / 4;
@@ -636,6 +670,45 @@ __global__ void slab_reduce_kernel(const float* __restrict__ slab, int S, int Mw
             }
             grad[o] = s4[j];
         }
+    }
+}
+
+// 3x3 weight gradient, slab rows m = tap * cin + ci, columns n = co -> grad[co][ci][tap]
+// through an LDS tile of 32 co x 32 ci x 9 taps: reads stay coalesced along n, and each co
+// writes one contiguous run of 32 * 9 floats (the row-per-thread kernel above scatters every
+// float 9 * cin apart, which on the 4096-channel layers made this pass HBM-write-bound at a
+// small fraction of the bandwidth).  Per element the S slabs are summed in exactly the
+// association of slab_reduce_kernel, so both kernels give identical bits.
+__global__ __launch_bounds__(256) void slab_reduce_conv3_kernel(const float* __restrict__ slab, int S,
+                                                                int cin, int cout,
+                                                                float* __restrict__ grad) {
+    __shared__ float tile[32][32 * 9 + 1];
+    const int n0 = blockIdx.x * 32, c0 = blockIdx.y * 32;
+    const int Nw = cout;
+    const int64_t total = (int64_t)9 * cin * cout;
+    const int nl = threadIdx.x & 31, rr = threadIdx.x >> 5;
+    for (int row = rr; row < 9 * 32; row += 8) {
+        const int tap = row / 32, cl = row - tap * 32;
+        const int64_t e = (int64_t)(tap * cin + c0 + cl) * Nw + n0 + nl;
+        const float* sp = slab + e;
+        float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+        int k = 0;
+        for (; k + 8 <= S; k += 8) {
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = sp[(int64_t)(k + u) * total];
+            a0 += v[0] + v[4];
+            a1 += v[1] + v[5];
+            a2 += v[2] + v[6];
+            a3 += v[3] + v[7];
+        }
+        for (; k < S; ++k) a0 += sp[(int64_t)k * total];
+        tile[nl][cl * 9 + tap] = (a0 + a1) + (a2 + a3);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < 32 * 32 * 9; i += 256) {
+        const int n = i / (32 * 9), off = i - n * (32 * 9);
+        grad[((int64_t)(n0 + n) * cin + c0) * 9 + off] = tile[n][off];
     }
 }
 
@@ -1113,6 +1186,16 @@ int k_to_bf16(const float* src, int ld, int off, int C, const float* scale, cons
                        scale, shift, relu, P, tpr, (__bf16*)dst);
     LAUNCH_CHECK();
 }
+int k_bn_dz16(float* d, const float* y, int ld, int off, int64_t P, int C, const float* coef,
+              int mask, uint16_t* dz16, int f32, hipStream_t s) {
+    if (C % 8 || ld % 4 || off % 4) return -1;
+    const int c8 = C / 8;
+    const int tpr = c8 >= 256 ? 256 : c8;
+    if (256 % tpr || (c8 > 256 && c8 % 256)) return -1;
+    hipLaunchKernelGGL(bn_dz16_kernel, dim3(grid_for(P * tpr)), dim3(256), 0, s, d, y, ld, off, P, C,
+                       coef, mask, tpr, (__bf16*)dz16, f32);
+    LAUNCH_CHECK();
+}
 int k_bias_reduce(const float* slab, int S, int taps, int C, float* out, hipStream_t s) {
     hipLaunchKernelGGL(bias_reduce_kernel, dim3((C + 63) / 64), dim3(64, 16), 0, s, slab, S, taps, C,
                        out);
@@ -1125,6 +1208,11 @@ int k_sum_partials(const float* part, int G, int ncols, float* out, hipStream_t 
 }
 int k_slab_reduce(const float* slab, int S, int Mw, int Nw, int kind, int cin, int cout,
                   float* grad, hipStream_t s) {
+    if (kind == 0 && cin % 32 == 0 && cout % 32 == 0 && (cin / 32) * (cout / 32) >= 128) {
+        hipLaunchKernelGGL(slab_reduce_conv3_kernel, dim3(cout / 32, cin / 32), dim3(256), 0, s, slab, S,
+                           cin, cout, grad);
+        LAUNCH_CHECK();
+    }
     if (Nw % 4) return -1;
     hipLaunchKernelGGL(slab_reduce_kernel, dim3(grid_for((int64_t)Mw * Nw / 4)), dim3(256), 0, s,
                        slab, S, Mw, Nw, kind, cin, cout, grad);

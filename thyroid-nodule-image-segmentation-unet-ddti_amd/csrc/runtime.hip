@@ -1060,17 +1060,20 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
                                    C.b >= 0 ? grads + C.b : nullptr, s));
             return 0;
         }
-        if (!dz_in_loaders) {
+        const float* dzc = dz_in_loaders ? p.coef : nullptr;
+        // bf16 image of dz: A operand of the LDS-DMA dgrad, B' of the LDS-DMA wgrad; the f32
+        // dz is still written when the register-staged kernel of either consumes it
+        const bool dz16 = !dzc && (rg16_on(c, C.cout, C.cin) || p.x16[i]);
+        if (dz16) {
+            const bool f32 = !p.x16[i] || !(dx && rg16_on(c, C.cout, C.cin));
+            before_write(p.s16);
+            before_write(dout);
+            RUN("bn_dz", 0, k_bn_dz16(const_cast<float*>(dout), p.y[i], p.ldy[i], p.offy[i], P, C.cout,
+                                      p.coef, dz_mask, p.s16, f32 ? 1 : 0, s));
+        } else if (!dz_in_loaders) {
             before_write(dout);
             RUN("bn_dz", 0, k_bn_dz(const_cast<float*>(dout), p.y[i], p.ldy[i], p.offy[i], P, C.cout,
                                     p.coef, dz_mask, s));
-        }
-        const float* dzc = dz_in_loaders ? p.coef : nullptr;
-        // bf16 image of dz: A operand of the LDS-DMA dgrad, B' of the LDS-DMA wgrad
-        const bool dz16 = !dzc && (rg16_on(c, C.cout, C.cin) || p.x16[i]);
-        if (dz16) {
-            before_write(p.s16);
-            RUN("prep16", 0, k_to_bf16(dout, C.cout, 0, C.cout, nullptr, nullptr, 0, P, p.s16, s));
         }
         side_after_main();
         Operand a = conv_input(c, p, i);
