@@ -156,14 +156,15 @@ def _to64(d):
     return {k: (v.double() if v.is_floating_point() else v.clone()) for k, v in d.items()}
 
 
-@pytest.mark.parametrize("tile", ["0", "1", "3"])
-def test_rg16_bit_identical_to_register_staged(tile, monkeypatch):
+@pytest.mark.parametrize("tile,wtile", [("0", "0"), ("1", "1"), ("3", "0"), ("0", "2")])
+def test_rg16_bit_identical_to_register_staged(tile, wtile, monkeypatch):
     """The LDS-DMA bf16 GEMMs (kernels_gemm16.hip, fed by the k_to_bf16 operand images:
     row GEMMs and the transposed-read weight gradients) against the register-staged bf16
     kernels (UNET_RG16=0, UNET_WG16=0) on a base-128 network, where every GEMM but the
     Cin = 1 first conv takes the new path: the same bf16 roundings of the same f32 values,
     the same K order, split-K partition and 128-row BN partials, so one training step gives
-    bit-identical logits, gradients and BN statistics for every 128-row tile."""
+    bit-identical logits, gradients and BN statistics for every 128-row tile (and every
+    weight-gradient tile: those have no BN partials)."""
     import unet_hip
     x, t = inputs(23, 2, 128, 128)
     P = MO.make_params(9, 128, 3)
@@ -172,7 +173,7 @@ def test_rg16_bit_identical_to_register_staged(tile, monkeypatch):
         monkeypatch.setenv("UNET_RG16", flag)
         monkeypatch.setenv("UNET_WG16", flag)
         monkeypatch.setenv("UNET_RG16_TILE", tile)
-        monkeypatch.setenv("UNET_WG16_TILE", "1" if tile == "1" else "0")
+        monkeypatch.setenv("UNET_WG16_TILE", wtile)
         m = unet_hip.ModUNet(1, 1, base_filters=128, depth=3, mfma_dtype="bf16")
         sd = m.state_dict()
         for k, v in P.items():
@@ -193,7 +194,7 @@ def test_rg16_bit_identical_to_register_staged(tile, monkeypatch):
         assert torch.equal(b0, outs[1][2][k]), k
 
 
-@pytest.mark.parametrize("base,depth,tile", [(64, 3, "0"), (128, 5, "0"), (128, 5, "2")])
+@pytest.mark.parametrize("base,depth,tile", [(64, 3, "4"), (128, 5, "0"), (128, 5, "2"), (128, 5, "4")])
 def test_mod_bf16_matches_bf16_oracle(base, depth, tile, monkeypatch):
     """mfma_dtype="bf16": one step at B=2 64x64 vs the oracle that rounds exactly the GEMM
     operands the HIP bf16 kernels round (oracle/mod_ref_cpu.py, bf16=True).
@@ -203,10 +204,12 @@ def test_mod_bf16_matches_bf16_oracle(base, depth, tile, monkeypatch):
     BN.  The oracle itself shows it: evaluated in fp32 and in fp64 (same bf16 roundings of
     its own values) it differs by ~6e-3 in the logits and up to ~15 % on small BN-bias
     gradients.  The bar is 2x that spread of the oracle against itself.  tile = the
-    LDS-DMA GEMM tile (UNET_RG16_TILE; "2" = 256 rows x 8 waves, whose BN partials group
-    256 rows, so its bf16 roundings differ from the 128-row tiles')."""
+    LDS-DMA GEMM tile (UNET_RG16_TILE; "2" = 256 rows x 8 waves, "4" = 256 x 256, the
+    default: BN partials grouped by 256 rows, so the bf16 roundings differ from the
+    128-row tiles'), with the 256x256 weight-gradient tile on the 256-channel layers."""
     import unet_hip
     monkeypatch.setenv("UNET_RG16_TILE", tile)
+    monkeypatch.setenv("UNET_WG16_TILE", "2" if tile == "4" else "0")
     P = MO.make_params(42, base, depth)
     x, t = inputs(5, 2, 64, 64)
     ref = MO.train_step(P, MO.init_buffers(base, depth), None, x, t, depth=depth, bf16=True)

@@ -187,12 +187,15 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm16_kernel(RowGemmAr
 }
 
 // tiles: 0 = 128x128, 2 stages (64 KB LDS, 2 blocks/CU); 1 = 128x128, 3 stages (96 KB);
-// 2 = 256x128, 8 waves, 2 stages (96 KB); 3 = 128x128, 4 stages (128 KB)
+// 2 = 256x128, 8 waves, 2 stages (96 KB); 3 = 128x128, 4 stages (128 KB);
+// 4 = 256x256, 8 waves of 128x64, 2 stages (128 KB); 5 = 256x128, 8 waves, 3 stages (144 KB)
 using T16_0 = Tile16<128, 128, 64, 64, 2, 2>;
 using T16_1 = Tile16<128, 128, 64, 64, 3, 1>;
 using T16_2 = Tile16<256, 128, 64, 64, 2, 1>;
 using T16_3 = Tile16<128, 128, 64, 64, 4, 1>;
-#define ROWGEMM16_TILES(X) X(0, T16_0) X(1, T16_1) X(2, T16_2) X(3, T16_3)
+using T16_4 = Tile16<256, 256, 128, 64, 2, 1>;
+using T16_5 = Tile16<256, 128, 64, 64, 3, 1>;
+#define ROWGEMM16_TILES(X) X(0, T16_0) X(1, T16_1) X(2, T16_2) X(3, T16_3) X(4, T16_4) X(5, T16_5)
 
 template <int AMODE, int EMODE, class T>
 static int rg16_go(const RowGemmArgs& a, hipStream_t s) {
@@ -257,12 +260,14 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void wgrad16_kernel(WgradArgs p
     constexpr int BM = T::BM, BN = T::BN, WM = T::WM, WN = T::WN, BKP = T::BKP, S = T::S;
     constexpr int WAVES = T::WAVES, WAVES_N = BN / WN;
     constexpr int MT = WM / 32, NT = WN / 32;
-    static_assert(BM == 128 && BN == 128, "256-B pixel rows");
-    constexpr int RB = 256;                                  // bytes per pixel row
-    constexpr int AI = BKP / (4 * WAVES), BI = BKP / (4 * WAVES);  // DMA instructions per chunk
-    static_assert(AI * 4 * WAVES == BKP, "loader shape");
+    static_assert(BM % 128 == 0 && BN % 128 == 0 && BM <= 512 && BN <= 512, "pixel rows");
+    constexpr int RA = 2 * BM, RBB = 2 * BN;   // bytes per pixel row of the A' / B' images
+    constexpr int LA = RA / 16, LB = RBB / 16;  // lanes per pixel row in a DMA instruction
+    constexpr int PA = 64 / LA, PB = 64 / LB;   // pixel rows per DMA instruction
+    constexpr int AI = BKP / (PA * WAVES), BI = BKP / (PB * WAVES);  // DMA instructions per chunk
+    static_assert(AI * PA * WAVES == BKP && BI * PB * WAVES == BKP, "loader shape");
     constexpr int GPC = AI + BI;
-    constexpr int STAGE = 2 * BKP * RB;
+    constexpr int STAGE = BKP * (RA + RBB);
     __shared__ __attribute__((aligned(1024))) char smem[STAGE * S];
 
     const int tid = threadIdx.x, lane = tid & 63;
@@ -282,10 +287,9 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void wgrad16_kernel(WgradArgs p
     const int pend = min(pbeg + p.pps, p.P);
     const int nk = (pend - pbeg + BKP - 1) / BKP;
 
-    // loader: instruction j of this wave fills pixel rows (j * WAVES + wave) * 4 .. + 3;
-    // lane l -> row l / 16, slot l % 16 holding global chunk slot ^ ((row & 3) << 2)
-    const int lr = lane >> 4;
-    const int gch = ((lane & 15) ^ (lr << 2)) * 8;
+    // loader: instruction j of this wave fills pixel rows (j * WAVES + wave) * PA .. (A');
+    // lane l -> row l / LA, slot l % LA holding global chunk slot ^ ((row & 3) << 2)
+    const int lra = lane / LA, lrb = lane / LB;
     const uint16_t* a16 = (const uint16_t*)p.a;
     const uint16_t* b16 = (const uint16_t*)p.b;
     const uint16_t* zero = (const uint16_t*)p.zero16;
@@ -295,25 +299,29 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void wgrad16_kernel(WgradArgs p
         char* base = smem + st * STAGE;
 #pragma unroll
         for (int j = 0; j < AI; ++j) {
-            const int pix = pc + (j * WAVES + wave) * 4 + lr;
+            const int row = (j * WAVES + wave) * PA + lra;
+            const int gcha = ((lane % LA) ^ ((row & 3) << 2)) * 8;
+            const int pix = pc + row;
             const bool in = pix < pend;
             const int m = in ? pix : pend - 1;
             bool valid;
             const Pix q = AMODE == G_IDENT ? Pix{0, 0, 0} : decode_fast(m, H, W, rH, rW);
             const int src = gather_src<AMODE>(tapA, m, q, H, W, valid);
-            const uint16_t* g = (valid && in) ? a16 + (size_t)src * p.lda + ca0 + gch : zero;
+            const uint16_t* g = (valid && in) ? a16 + (size_t)src * p.lda + ca0 + gcha : zero;
             glds16(g, base + (j * WAVES + wave) * 1024);
         }
 #pragma unroll
         for (int j = 0; j < BI; ++j) {
-            const int pix = pc + (j * WAVES + wave) * 4 + lr;
+            const int row = (j * WAVES + wave) * PB + lrb;
+            const int gchb = ((lane % LB) ^ ((row & 3) << 2)) * 8;
+            const int pix = pc + row;
             const bool in = pix < pend;
             const int m = in ? pix : pend - 1;
             bool valid;
             const Pix q = BMODE == G_IDENT ? Pix{0, 0, 0} : decode_fast(m, H, W, rH, rW);
             const int src = gather_src<BMODE>(tapB, m, q, H, W, valid);
-            const uint16_t* g = (valid && in) ? b16 + (size_t)src * p.ldb + cb0 + gch : zero;
-            glds16(g, base + BKP * RB + (j * WAVES + wave) * 1024);
+            const uint16_t* g = (valid && in) ? b16 + (size_t)src * p.ldb + cb0 + gchb : zero;
+            glds16(g, base + BKP * RA + (j * WAVES + wave) * 1024);
         }
     };
 
@@ -333,12 +341,12 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void wgrad16_kernel(WgradArgs p
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
         const int col = wm * WM + mt * 32 + 16 * (g & 1) + 4 * pp;
-        aoff[mt] = trow * RB + (((col >> 3) ^ (qq << 2)) << 4) + ((col >> 2) & 1) * 8;
+        aoff[mt] = trow * RA + (((col >> 3) ^ (qq << 2)) << 4) + ((col >> 2) & 1) * 8;
     }
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
         const int col = wn * WN + nt * 32 + 16 * (g & 1) + 4 * pp;
-        boff[nt] = BKP * RB + trow * RB + (((col >> 3) ^ (qq << 2)) << 4) + ((col >> 2) & 1) * 8;
+        boff[nt] = BKP * RA + trow * RBB + (((col >> 3) ^ (qq << 2)) << 4) + ((col >> 2) & 1) * 8;
     }
 
 #pragma unroll
@@ -364,13 +372,13 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void wgrad16_kernel(WgradArgs p
             constexpr int kk = decltype(KK)::value, set = kk & 1;
 #pragma unroll
             for (int mt = 0; mt < MT; ++mt) {
-                fa[set][mt][0] = ds_tr16<kk * 16 * RB>(sb + aoff[mt]);
-                fa[set][mt][1] = ds_tr16<kk * 16 * RB + 4 * RB>(sb + aoff[mt]);
+                fa[set][mt][0] = ds_tr16<kk * 16 * RA>(sb + aoff[mt]);
+                fa[set][mt][1] = ds_tr16<kk * 16 * RA + 4 * RA>(sb + aoff[mt]);
             }
 #pragma unroll
             for (int nt = 0; nt < NT; ++nt) {
-                fb[set][nt][0] = ds_tr16<kk * 16 * RB>(sb + boff[nt]);
-                fb[set][nt][1] = ds_tr16<kk * 16 * RB + 4 * RB>(sb + boff[nt]);
+                fb[set][nt][0] = ds_tr16<kk * 16 * RBB>(sb + boff[nt]);
+                fb[set][nt][1] = ds_tr16<kk * 16 * RBB + 4 * RBB>(sb + boff[nt]);
             }
         };
         auto mma = [&](auto KK) {
@@ -421,10 +429,12 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void wgrad16_kernel(WgradArgs p
 }
 
 // wgrad16 tiles: 0 = 128x128, 64 pixels per stage, 2 stages (64 KB, 2 blocks/CU);
-// 1 = the same with 3 stages (96 KB, 1 block/CU)
+// 1 = the same with 3 stages (96 KB, 1 block/CU); 2 = 256x256, 8 waves of 128x64,
+// 2 stages (128 KB, 1 block/CU)
 using W16_0 = WTile16<128, 128, 64, 64, 64, 2, 2>;
 using W16_1 = WTile16<128, 128, 64, 64, 64, 3, 1>;
-#define WGRAD16G_TILES(X) X(0, W16_0) X(1, W16_1)
+using W16_2 = WTile16<256, 256, 128, 64, 64, 2, 1>;
+#define WGRAD16G_TILES(X) X(0, W16_0) X(1, W16_1) X(2, W16_2)
 
 template <int AMODE, int BMODE, class T>
 static int wg16_go(const WgradArgs& a, hipStream_t s) {
@@ -472,6 +482,7 @@ int launch_wgrad16(const WgradArgs& a, int tile, hipStream_t s) {
     do {                                                 \
         if (tile == 0) return wg16_go<AM, BMD, W16_0>(a, s); \
         if (tile == 1) return wg16_go<AM, BMD, W16_1>(a, s); \
+        if (tile == 2) return wg16_go<AM, BMD, W16_2>(a, s); \
         return -1;                                       \
     } while (0)
     if (a.amode == G_CONV3 && a.bmode == G_IDENT) WG16G(G_CONV3, G_IDENT);

@@ -397,9 +397,14 @@ bool rg16_on(const unet_ctx* c, int C, int N) {
     const char* e = getenv("UNET_RG16");
     return c->bf16 && (e ? atoi(e) : 1) != 0 && C % 64 == 0 && N % 128 == 0;
 }
-int rg16_tile() {
+// tile for an output width N (and ConvT cout): the requested one (default 256x256) when N
+// divides into it, else the 128x128 tile
+int rg16_tile(int N = 128, int cout = 0) {
     const char* e = getenv("UNET_RG16_TILE");
-    return e ? atoi(e) : 0;
+    const int t = e ? atoi(e) : 4;  // 256x256 (config 4 A/B: 104.2 vs 99.7 img/s for 128x128)
+    int bm = 0, bn = 0;
+    if (rowgemm16_tile_dims(t, &bm, &bn) != 0) return 0;
+    return (N % bn == 0 && (cout == 0 || cout % bn == 0)) ? t : 0;
 }
 // 3x3 weight gradients of layers with Cin, Cout multiples of 128 on the LDS-DMA
 // transposed-read kernel (kernels_gemm16.hip wgrad16_kernel) from the forward's bf16 input
@@ -415,9 +420,12 @@ int xcd16_on() {
     const char* e = getenv("UNET_XCD16");
     return (e ? atoi(e) : 1) != 0 ? 1 : 0;
 }
-int wg16_tile() {
+// tile: UNET_WG16_TILE, else 256x256 (tile 2) where both channel counts allow it
+int wg16_tile(int CA = 128, int CB = 128) {
     const char* e = getenv("UNET_WG16_TILE");
-    return e ? atoi(e) : 0;
+    const int t = e ? atoi(e) : 2;
+    if (t == 2 && (CA % 256 || CB % 256)) return 0;
+    return t;
 }
 
 void make_plan(unet_ctx* c, int N, int H, int W, bool training, char* base, Plan& p) {
@@ -822,7 +830,7 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
                                            img, s));
                 use_a16(p, g, C.cin);
                 g.a16 = img;
-                const int tile = rg16_tile();
+                const int tile = rg16_tile(C.cout);
                 int bm, bn;
                 rowgemm16_tile_dims(tile, &bm, &bn);
                 R = (int)((M + bm - 1) / bm);
@@ -873,7 +881,7 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
             RUN("prep16", 0, k_to_bf16(g.a, g.lda, g.aoff, T.cin, g.ascale, g.ashift, g.arelu, g.M,
                                        p.s16, s));
             use_a16(p, g, T.cin);
-            const int tile = rg16_tile();
+            const int tile = rg16_tile(g.N, T.cout);
             RUN(tlabel16("convT_fwd", tile, 100 + k), 2.0 * g.M * g.N * g.K,
                 launch_rowgemm16(g, tile, s));
             return 0;
@@ -1125,9 +1133,10 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
             w.bcoef = nullptr;
             w.zero16 = p.zero16;
             w.xcd = xcd16_on();
-            const int t = wg16_tile();
+            // (the split count, sized for >= 2048 128x128 tiles, gives >= 512 256x256 ones)
+            const int t = wg16_tile(C.cin, C.cout);
             char lb[96];
-            snprintf(lb, sizeof lb, "conv_wgrad/wg16_128x128_t%d|%d", t, i);
+            snprintf(lb, sizeof lb, "conv_wgrad/wg16_t%d|%d", t, i);
             RUNW(lb, 2.0 * P * C.cout * 9 * C.cin, launch_wgrad16(w, t, sw));
             side_read(p.s16);
         } else {
@@ -1174,7 +1183,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
             }
             if (dz16 && rg16_on(c, C.cout, C.cin)) {
                 use_a16(p, g, C.cout);
-                const int tile = rg16_tile();
+                const int tile = rg16_tile(C.cin);
                 int bm, bn;
                 rowgemm16_tile_dims(tile, &bm, &bn);
                 if (rows) *rows = (int)((P + bm - 1) / bm);
@@ -1271,7 +1280,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
             RUN("prep16", 0, k_to_bf16(p.dcat[lo], ldo, uo, T.cout, nullptr, nullptr, 0, p.P[lo],
                                        p.s16, s));
             use_a16(p, g, T.cout);
-            const int tile = rg16_tile();
+            const int tile = rg16_tile(T.cin);
             int bm, bn;
             rowgemm16_tile_dims(tile, &bm, &bn);
             *rows = (int)((Pin + bm - 1) / bm);
