@@ -88,7 +88,11 @@ __device__ __forceinline__ int gather_src(int tap, int m, Pix q, int H, int W, b
 // (m0, n0); tile_m indexes the per-block BN partial rows; smem (>= WAVES_M * 2 * BN doubles)
 // is free scratch (the caller has finished with its LDS images).
 // ------------------------------------------------------------------------------------
-template <int EMODE, int BM, int BN, int WM, int WN>
+// PRELOAD: the epilogues that read memory (E_STORE_BN, E_RESID, E_ADD) issue all 16 loads
+// of an accumulator first -- a load under `if (m < M)` makes hipcc wait for each one before
+// the next, which dominated the short-K bf16 GEMMs; the long-K f32 kernels keep the
+// per-element form (fewer live registers, measured 4 % faster on their dgrads).
+template <int EMODE, int BM, int BN, int WM, int WN, bool PRELOAD = false>
 __device__ __forceinline__ void row_epilogue(const RowGemmArgs& p, f32x16 (&acc)[WM / 32][WN / 32],
                                              int m0, int n0, int tile_m, int wm, int wn,
                                              int lane, int tid, float* smem) {
@@ -151,7 +155,7 @@ __device__ __forceinline__ void row_epilogue(const RowGemmArgs& p, f32x16 (&acc)
             const float es = emask ? p.escale[n] : 0.f, eb = emask ? p.eshift[n] : 0.f;
             q[nt][0] = q[nt][1] = 0.0;
 #pragma unroll
-            for (int mt = 0; mt < MT; ++mt)
+            for (int mt = 0; mt < MT && !PRELOAD; ++mt)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     const int m = m0 + wm * WM + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
@@ -164,6 +168,27 @@ __device__ __forceinline__ void row_epilogue(const RowGemmArgs& p, f32x16 (&acc)
                         q[nt][1] += (double)v * y;
                     }
                 }
+#pragma unroll
+            for (int mt = 0; mt < MT && PRELOAD; ++mt) {
+                // all 16 loads first (rows past M clamped, their products zeroed below)
+                float yv[16];
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int m = m0 + wm * WM + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                    yv[r] = p.ey[(size_t)(m < p.M ? m : p.M - 1) * p.ldey + p.offey + n];
+                }
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int m = m0 + wm * WM + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                    const float y = yv[r];
+                    float v = acc[mt][nt][r];
+                    if (emask && !(es * y + eb > 0.f)) v = 0.f;
+                    if (m < p.M) p.out[(size_t)m * p.ldo + p.ooff + n] = v;
+                    v = m < p.M ? v : 0.f;
+                    q[nt][0] += v;
+                    q[nt][1] += (double)v * y;
+                }
+            }
 #pragma unroll
             for (int j = 0; j < 2; ++j) q[nt][j] += __shfl_xor(q[nt][j], 32);
         }
@@ -219,7 +244,7 @@ __device__ __forceinline__ void row_epilogue(const RowGemmArgs& p, f32x16 (&acc)
             const float es = EMODE == E_RESID ? p.escale[n] : 0.f;
             const float eb = EMODE == E_RESID ? p.eshift[n] : 0.f;
 #pragma unroll
-            for (int mt = 0; mt < MT; ++mt)
+            for (int mt = 0; mt < MT && !PRELOAD; ++mt)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     const int m = m0 + wm * WM + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
@@ -231,6 +256,27 @@ __device__ __forceinline__ void row_epilogue(const RowGemmArgs& p, f32x16 (&acc)
                     else
                         *o += acc[mt][nt][r];
                 }
+#pragma unroll
+            for (int mt = 0; mt < MT && PRELOAD; ++mt) {
+                float xv[16];  // ey (E_RESID) or the current out (E_ADD), loaded up front
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    int m = m0 + wm * WM + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                    m = m < p.M ? m : p.M - 1;
+                    xv[r] = EMODE == E_RESID ? p.ey[(size_t)m * p.ldey + p.offey + n]
+                                             : p.out[(size_t)m * p.ldo + p.ooff + n];
+                }
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int m = m0 + wm * WM + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                    if (m >= p.M) continue;
+                    float* o = p.out + (size_t)m * p.ldo + p.ooff + n;
+                    if constexpr (EMODE == E_RESID)
+                        *o = fmaxf(acc[mt][nt][r] + (es * xv[r] + eb), 0.f);
+                    else
+                        *o = xv[r] + acc[mt][nt][r];
+                }
+            }
         }
     } else {
 #pragma unroll

@@ -183,7 +183,7 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm16_kernel(RowGemmAr
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         block_barrier();
     }
-    row_epilogue<EMODE, BM, BN, WM, WN>(p, acc, m0, n0, tile_m, wm, wn, lane, tid, (float*)smem);
+    row_epilogue<EMODE, BM, BN, WM, WN, true>(p, acc, m0, n0, tile_m, wm, wn, lane, tid, (float*)smem);
 }
 
 // tiles: 0 = 128x128, 2 stages (64 KB LDS, 2 blocks/CU); 1 = 128x128, 3 stages (96 KB);

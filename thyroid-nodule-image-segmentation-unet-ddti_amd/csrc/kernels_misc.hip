@@ -32,10 +32,27 @@ __global__ __launch_bounds__(256) void pack_conv3_tiled_kernel(const float* __re
     const int ci0 = blockIdx.x * T, co0 = blockIdx.y * T;
     const int nci = min(T, cin - ci0), nco = min(T, cout - co0);
     const int tid = threadIdx.x;
-    for (int e = tid; e < T * T * 9; e += 256) {  // e = co_l * 288 + (ci_l * 9 + tap)
-        const int co_l = e / (T * 9), r = e - co_l * (T * 9);
-        if (co_l < nco && r < nci * 9)
-            tile[co_l * RS + r] = w[((int64_t)(co0 + co_l) * cin + ci0) * 9 + r];
+    if (nci == T && nco == T) {
+        // full tile: 36 independent loads per thread in flight before the LDS stores
+        float v[T * T * 9 / 256];
+#pragma unroll
+        for (int k = 0; k < T * T * 9 / 256; ++k) {
+            const int e = tid + 256 * k;  // e = co_l * 288 + (ci_l * 9 + tap)
+            const int co_l = e / (T * 9), r = e - co_l * (T * 9);
+            v[k] = w[((int64_t)(co0 + co_l) * cin + ci0) * 9 + r];
+        }
+#pragma unroll
+        for (int k = 0; k < T * T * 9 / 256; ++k) {
+            const int e = tid + 256 * k;
+            const int co_l = e / (T * 9), r = e - co_l * (T * 9);
+            tile[co_l * RS + r] = v[k];
+        }
+    } else {
+        for (int e = tid; e < T * T * 9; e += 256) {  // e = co_l * 288 + (ci_l * 9 + tap)
+            const int co_l = e / (T * 9), r = e - co_l * (T * 9);
+            if (co_l < nco && r < nci * 9)
+                tile[co_l * RS + r] = w[((int64_t)(co0 + co_l) * cin + ci0) * 9 + r];
+        }
     }
     __syncthreads();
     const int l = tid & 31, g = tid >> 5;  // 8 groups of 32 lanes
@@ -687,7 +704,20 @@ __global__ __launch_bounds__(256) void slab_reduce_conv3_kernel(const float* __r
     const int Nw = cout;
     const int64_t total = (int64_t)9 * cin * cout;
     const int nl = threadIdx.x & 31, rr = threadIdx.x >> 5;
-    for (int row = rr; row < 9 * 32; row += 8) {
+    if (S == 1) {  // a transposing copy: all 36 loads of the thread in flight at once
+        float v[36];
+#pragma unroll
+        for (int it = 0; it < 36; ++it) {
+            const int row = rr + 8 * it, tap = row / 32, cl = row - tap * 32;
+            v[it] = slab[(int64_t)(tap * cin + c0 + cl) * Nw + n0 + nl];
+        }
+#pragma unroll
+        for (int it = 0; it < 36; ++it) {
+            const int row = rr + 8 * it, tap = row / 32, cl = row - tap * 32;
+            tile[nl][cl * 9 + tap] = v[it];
+        }
+    }
+    for (int row = S == 1 ? 9 * 32 : rr; row < 9 * 32; row += 8) {
         const int tap = row / 32, cl = row - tap * 32;
         const int64_t e = (int64_t)(tap * cin + c0 + cl) * Nw + n0 + nl;
         const float* sp = slab + e;
