@@ -144,9 +144,11 @@ def dice_vs_ref(sample, dev):
             "logits_max_rel": float(f"{float((lg - ref['logits']).abs().max() / ref['logits'].abs().max()):.3g}")}
 
 
-def load_pmc(kernel):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary, if any."""
-    path = os.path.join(REPO, "profiles", "pmc_summary.json")
+def load_pmc(kernel, config=2, mfma="fp32"):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of this
+    workload (profiles/pmc_summary.json: config 2; pmc_summary_c4_<mfma>.json), if any."""
+    name = "pmc_summary.json" if config == 2 else f"pmc_summary_c4_{mfma}.json"
+    path = os.path.join(REPO, "profiles", name)
     try:
         d = json.load(open(path))
         return d.get("kernels", {}).get(kernel, {}).get("hbm_bytes_per_launch")
@@ -269,7 +271,7 @@ def main():
     n_l, t_l, f_l = kern_t[dom]
     achieved = f_l / (t_l * 1e-3) / 1e12 if t_l > 0 else 0.0
     per_launch_flop = f_l / n_l
-    pmc = load_pmc(dom)
+    pmc = load_pmc(dom, args.config, args.mfma)
     conv_flop = (MO.train_flops_per_image(S, S, 128, 5) if c4 else O.train_flops_per_image(S, S)) * B
     bf16 = c4 and args.mfma == "bf16"
     peak = BF16_MFMA_PEAK_TFLOPS if bf16 else FP32_MFMA_PEAK_TFLOPS

@@ -446,12 +446,26 @@ static int wg16_go(const WgradArgs& a, hipStream_t s) {
 
 }  // namespace
 
-int rowgemm16_tile_dims(int tile, int* bm, int* bn) {
-#define RG16_DIMS(id, T) \
-    if (tile == id) {    \
-        *bm = T::BM;     \
-        *bn = T::BN;     \
-        return 0;        \
+int wgrad16g_tile_dims(int tile, int* bm, int* bn, int* stages) {
+#define WG16_DIMS(id, T)          \
+    if (tile == id) {             \
+        *bm = T::BM;              \
+        *bn = T::BN;              \
+        if (stages) *stages = T::S; \
+        return 0;                 \
+    }
+    WGRAD16G_TILES(WG16_DIMS)
+#undef WG16_DIMS
+    return -1;
+}
+
+int rowgemm16_tile_dims(int tile, int* bm, int* bn, int* stages) {
+#define RG16_DIMS(id, T)          \
+    if (tile == id) {             \
+        *bm = T::BM;              \
+        *bn = T::BN;              \
+        if (stages) *stages = T::S; \
+        return 0;                 \
     }
     ROWGEMM16_TILES(RG16_DIMS)
 #undef RG16_DIMS

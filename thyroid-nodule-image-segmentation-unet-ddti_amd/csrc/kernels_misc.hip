@@ -690,6 +690,60 @@ __global__ void slab_reduce_kernel(const float* __restrict__ slab, int S, int Mw
     }
 }
 
+// Many-slab reduce (S >= 32: the narrow layers, whose split-K runs hundreds of slices):
+// 16 lanes per 4-column quad walk the slabs k = lane, lane + 16, ... (8 loads in flight),
+// and the 16 partial sums are combined in lane order through LDS -- a fixed association, so
+// deterministic, with 16x more threads and 16x shorter chains than one thread per quad.
+__global__ __launch_bounds__(256) void slab_reduce_wide_kernel(const float* __restrict__ slab, int S,
+                                                               int Mw, int Nw, int kind, int cin,
+                                                               int cout, float* __restrict__ grad) {
+    __shared__ f32x4 red[16][17];
+    const int64_t total = (int64_t)Mw * Nw;
+    const int64_t nq = total / 4;
+    const int ql = threadIdx.x & 15, sl = threadIdx.x >> 4;
+    const int64_t iq = (int64_t)blockIdx.x * 16 + ql;
+    f32x4 a0 = {0, 0, 0, 0}, a1 = a0;
+    if (iq < nq) {
+        const f32x4* sp = (const f32x4*)slab + iq;
+        const int64_t stride = total / 4;
+        int k = sl;
+        for (; k + 16 * 7 < S; k += 16 * 8) {
+            f32x4 v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = sp[(int64_t)(k + 16 * u) * stride];
+#pragma unroll
+            for (int u = 0; u < 8; u += 2) {
+                a0 += v[u];
+                a1 += v[u + 1];
+            }
+        }
+        for (; k < S; k += 16) a0 += sp[(int64_t)k * stride];
+    }
+    red[sl][ql] = a0 + a1;
+    __syncthreads();
+    if (sl != 0 || iq >= nq) return;
+    f32x4 s4 = red[0][ql];
+#pragma unroll
+    for (int j = 1; j < 16; ++j) s4 += red[j][ql];
+    const int64_t i0 = iq * 4;
+    const int m = (int)(i0 / Nw), n0 = (int)(i0 % Nw);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int n = n0 + j;
+        int64_t o;
+        if (kind == 0) {
+            const int tap = m / cin, ci = m - tap * cin;
+            o = ((int64_t)n * cin + ci) * 9 + tap;
+        } else if (kind == 2) {
+            o = (int64_t)n * cin + m;
+        } else {
+            const int ab = n / cout, co = n - ab * cout;
+            o = ((int64_t)m * cout + co) * 4 + ab;
+        }
+        grad[o] = s4[j];
+    }
+}
+
 // 3x3 weight gradient, slab rows m = tap * cin + ci, columns n = co -> grad[co][ci][tap]
 // through an LDS tile of 32 co x 32 ci x 9 taps: reads stay coalesced along n, and each co
 // writes one contiguous run of 32 * 9 floats (the row-per-thread kernel above scatters every
@@ -1244,6 +1298,11 @@ int k_slab_reduce(const float* slab, int S, int Mw, int Nw, int kind, int cin, i
         LAUNCH_CHECK();
     }
     if (Nw % 4) return -1;
+    if (S >= 32) {
+        hipLaunchKernelGGL(slab_reduce_wide_kernel, dim3((int)(((int64_t)Mw * Nw / 4 + 15) / 16)),
+                           dim3(256), 0, s, slab, S, Mw, Nw, kind, cin, cout, grad);
+        LAUNCH_CHECK();
+    }
     hipLaunchKernelGGL(slab_reduce_kernel, dim3(grid_for((int64_t)Mw * Nw / 4)), dim3(256), 0, s,
                        slab, S, Mw, Nw, kind, cin, cout, grad);
     LAUNCH_CHECK();

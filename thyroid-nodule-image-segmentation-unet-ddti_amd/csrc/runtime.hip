@@ -732,10 +732,10 @@ void set_weights(const unet_ctx* c, RowGemmArgs& g, const float* img) {
 }
 
 std::string tlabel16(const char* fam, int tile, int layer) {
-    int bm = 0, bn = 0;
-    rowgemm16_tile_dims(tile, &bm, &bn);
+    int bm = 0, bn = 0, st = 0;
+    rowgemm16_tile_dims(tile, &bm, &bn, &st);
     char b[112];
-    snprintf(b, sizeof b, "%s/rg16_%dx%d_t%d|%d", fam, bm, bn, tile, layer);
+    snprintf(b, sizeof b, "%s/rg16_%dx%ds%d|%d", fam, bm, bn, st, layer);
     return b;
 }
 // point g's A operand at the prepared bf16 image (lda = C channels)
@@ -1135,8 +1135,10 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
             w.xcd = xcd16_on();
             // (the split count, sized for >= 2048 128x128 tiles, gives >= 512 256x256 ones)
             const int t = wg16_tile(C.cin, C.cout);
+            int wbm = 0, wbn = 0, wst = 0;
+            wgrad16g_tile_dims(t, &wbm, &wbn, &wst);
             char lb[96];
-            snprintf(lb, sizeof lb, "conv_wgrad/wg16_t%d|%d", t, i);
+            snprintf(lb, sizeof lb, "conv_wgrad/wg16_%dx%ds%d|%d", wbm, wbn, wst, i);
             RUNW(lb, 2.0 * P * C.cout * 9 * C.cin, launch_wgrad16(w, t, sw));
             side_read(p.s16);
         } else {

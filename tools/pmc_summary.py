@@ -29,6 +29,12 @@ def short(name):
     m = re.search(r"WgTile<(\d+), (\d+), \d+, \d+, (\d+)", name)
     if m:
         return f"wgrad_{m.group(1)}x{m.group(2)}x{m.group(3)}"
+    m = re.search(r"Tile16<(\d+), (\d+), \d+, \d+, (\d+), \d+>", name)
+    if m:
+        return f"rg16_{m.group(1)}x{m.group(2)}s{m.group(3)}"
+    m = re.search(r"WTile16<(\d+), (\d+), \d+, \d+, \d+, (\d+), \d+>", name)
+    if m:
+        return f"wg16_{m.group(1)}x{m.group(2)}s{m.group(3)}"
     m = re.search(r"::(\w+?)_kernel", name)
     return m.group(1) if m else name[:60]
 
