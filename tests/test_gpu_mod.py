@@ -156,7 +156,7 @@ def _to64(d):
     return {k: (v.double() if v.is_floating_point() else v.clone()) for k, v in d.items()}
 
 
-@pytest.mark.parametrize("tile,wtile", [("0", "0"), ("1", "1"), ("3", "0"), ("0", "2")])
+@pytest.mark.parametrize("tile,wtile", [("0", "0"), ("1", "1"), ("3", "0"), ("0", "2"), ("8", "0"), ("11", "0")])
 def test_rg16_bit_identical_to_register_staged(tile, wtile, monkeypatch):
     """The LDS-DMA bf16 GEMMs (kernels_gemm16.hip, fed by the k_to_bf16 operand images:
     row GEMMs and the transposed-read weight gradients) against the register-staged bf16
@@ -194,7 +194,9 @@ def test_rg16_bit_identical_to_register_staged(tile, wtile, monkeypatch):
         assert torch.equal(b0, outs[1][2][k]), k
 
 
-@pytest.mark.parametrize("base,depth,tile", [(64, 3, "4"), (128, 5, "0"), (128, 5, "2"), (128, 5, "4")])
+@pytest.mark.parametrize("base,depth,tile", [(64, 3, "4"), (128, 5, "0"), (128, 5, "2"), (128, 5, "4"),
+                                             (128, 5, "6"), (128, 5, "7"),
+                                             (128, 5, "9"), (128, 5, "10")])
 def test_mod_bf16_matches_bf16_oracle(base, depth, tile, monkeypatch):
     """mfma_dtype="bf16": one step at B=2 64x64 vs the oracle that rounds exactly the GEMM
     operands the HIP bf16 kernels round (oracle/mod_ref_cpu.py, bf16=True).
@@ -209,7 +211,7 @@ def test_mod_bf16_matches_bf16_oracle(base, depth, tile, monkeypatch):
     128-row tiles'), with the 256x256 weight-gradient tile on the 256-channel layers."""
     import unet_hip
     monkeypatch.setenv("UNET_RG16_TILE", tile)
-    monkeypatch.setenv("UNET_WG16_TILE", "2" if tile == "4" else "0")
+    monkeypatch.setenv("UNET_WG16_TILE", "2" if tile in ("4", "6", "7", "9", "10") else "0")
     P = MO.make_params(42, base, depth)
     x, t = inputs(5, 2, 64, 64)
     ref = MO.train_step(P, MO.init_buffers(base, depth), None, x, t, depth=depth, bf16=True)

@@ -48,24 +48,44 @@ __device__ __forceinline__ void wait_vm() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-// block tile BM x BN, wave tile WM x WN, S LDS stages of 64 K each
-template <int BM_, int BN_, int WM_, int WN_, int S_, int OCC_>
+// block tile BM x BN, wave tile WM x WN, S LDS stages of BK (64 or 32) K each.
+// ONEBAR: prefetch distance S-2 chunks and one barrier per chunk (the stage restaged at
+// iteration k was read at iteration k-2, and every wave has passed iteration k-1's barrier
+// since); otherwise distance S-1 with a second barrier after the MFMAs.
+// ILV: the DMA pieces of chunk k+DIST are issued between the MFMAs of chunk k (one share
+// per k-step, placed by sched_group_barrier) instead of all at the top of the iteration,
+// where every wave of the block issued them at once and left the matrix pipes idle.
+template <int BM_, int BN_, int WM_, int WN_, int S_, int OCC_, int BK_ = 64, bool ONEBAR_ = false,
+          bool ILV_ = false>
 struct Tile16 {
     static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, S = S_, OCC = OCC_;
-    static constexpr int BK = 64;
+    static constexpr int BK = BK_;
+    static constexpr bool ONEBAR = ONEBAR_, ILV = ILV_;
     static constexpr int WAVES = (BM / WM) * (BN / WN);
     static constexpr int THREADS = 64 * WAVES;
 };
 
 template <int AMODE, int EMODE, class T>
 __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm16_kernel(RowGemmArgs p) {
-    constexpr int BM = T::BM, BN = T::BN, WM = T::WM, WN = T::WN, S = T::S;
+    constexpr int BM = T::BM, BN = T::BN, WM = T::WM, WN = T::WN, S = T::S, BK = T::BK;
+    constexpr bool ONEBAR = T::ONEBAR, ILV = T::ILV;
     constexpr int WAVES = T::WAVES, WAVES_N = BN / WN;
     constexpr int MT = WM / 32, NT = WN / 32;
-    constexpr int AI = BM / (8 * WAVES), BI = BN / (8 * WAVES);  // DMA instructions per chunk
-    static_assert(AI * 8 * WAVES == BM && BI * 8 * WAVES == BN, "loader shape");
+    constexpr int RB = 2 * BK;             // bytes per LDS row
+    constexpr int LPR = RB / 16;           // 16-B chunks (DMA lanes) per row
+    constexpr int RPI = 64 / LPR;          // rows per DMA wave-instruction (1 KB)
+    constexpr int RPB = 256 / RB;          // rows per 256-B bank row
+    // slot of chunk c in row r: c ^ swz(r).  A 16-lane ds_read_b128 phase reads one chunk of
+    // 16 rows; with RPB rows per bank row and LPR slots per row, XORing by (r / RPB) mod LPR
+    // spreads them over all 16 slots of the 256-B bank row.
+    auto swz = [](int r) { return (r / RPB) & (LPR - 1); };
+    constexpr int AI = BM / (RPI * WAVES), BI = BN / (RPI * WAVES);  // DMA instructions per chunk
+    static_assert(AI * RPI * WAVES == BM && BI * RPI * WAVES == BN, "loader shape");
+    static_assert(BK == 64 || BK == 32, "chunk depth");
     constexpr int GPC = AI + BI;
-    constexpr int STAGE = (BM + BN) * 128;  // bytes
+    constexpr int DIST = ONEBAR ? S - 2 : S - 1;  // chunks in flight beyond the current one
+    static_assert(DIST >= 1, "stages");
+    constexpr int STAGE = (BM + BN) * RB;  // bytes
     constexpr int RED = 2 * (BM / WM) * BN * 8;  // epilogue scratch (f64 partials)
     constexpr int SMEM = STAGE * S > RED ? STAGE * S : RED;
     __shared__ __attribute__((aligned(1024))) char smem[SMEM];
@@ -79,43 +99,49 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm16_kernel(RowGemmAr
     const int m0 = tile_m * BM, n0 = tile_n * BN;
     const int H = p.H, W = p.W, C = p.C, K = p.K;
 
-    // loader rows: instruction j of this wave fills rows (j * WAVES + wave) * 8 .. + 7
-    const int lr = lane >> 3, slot = lane & 7;
+    // loader rows: instruction j of this wave fills rows (j * WAVES + wave) * RPI .. + RPI-1
+    const int lr = lane / LPR, slot = lane % LPR;
     Pix aq[AI];
     int am[AI], ach[AI];
     bool aok[AI];
 #pragma unroll
     for (int j = 0; j < AI; ++j) {
-        const int r = (j * WAVES + wave) * 8 + lr;
+        const int r = (j * WAVES + wave) * RPI + lr;
         const int m = m0 + r;
         aok[j] = m < p.M;
         am[j] = aok[j] ? m : p.M - 1;
         aq[j] = decode(am[j], H, W);
-        ach[j] = (slot ^ ((r >> 1) & 7)) * 8;
+        ach[j] = (slot ^ swz(r)) * 8;
     }
     const uint16_t* bsrc[BI];
 #pragma unroll
     for (int j = 0; j < BI; ++j) {
-        const int r = (j * WAVES + wave) * 8 + lr;
-        bsrc[j] = p.bt16 + (size_t)(n0 + r) * K + (slot ^ ((r >> 1) & 7)) * 8;
+        const int r = (j * WAVES + wave) * RPI + lr;
+        bsrc[j] = p.bt16 + (size_t)(n0 + r) * K + (slot ^ swz(r)) * 8;
     }
     const uint16_t* zero = (const uint16_t*)p.zero16;
 
-    auto issue = [&](int kc, int st) {
-        const int k0 = kc * 64;
+    // DMA pieces [j0, j1) of chunk kc into stage st (pieces 0..AI-1 = A rows, then B rows)
+    auto issue_range = [&](int kc, int st, int j0, int j1) {
+        const int k0 = kc * BK;
         const int tap = k0 / C;
         const int c0 = k0 - tap * C;
         char* base = smem + st * STAGE;
 #pragma unroll
         for (int j = 0; j < AI; ++j) {
+            if (j < j0 || j >= j1) continue;
             bool valid;
             const int src = gather_src<AMODE>(tap, am[j], aq[j], H, W, valid);
             const uint16_t* g = (valid && aok[j]) ? p.a16 + (size_t)src * p.lda + c0 + ach[j] : zero;
             glds16(g, base + (j * WAVES + wave) * 1024);
         }
 #pragma unroll
-        for (int j = 0; j < BI; ++j) glds16(bsrc[j] + k0, base + BM * 128 + (j * WAVES + wave) * 1024);
+        for (int j = 0; j < BI; ++j) {
+            if (AI + j < j0 || AI + j >= j1) continue;
+            glds16(bsrc[j] + k0, base + BM * RB + (j * WAVES + wave) * 1024);
+        }
     };
+    auto issue = [&](int kc, int st) { issue_range(kc, st, 0, GPC); };
 
     f32x16 acc[MT][NT];
 #pragma unroll
@@ -131,41 +157,48 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm16_kernel(RowGemmAr
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
         const int r = wm * WM + mt * 32 + li;
-        aro[mt] = r * 128;
-        afx[mt] = (r >> 1) & 7;
+        aro[mt] = r * RB;
+        afx[mt] = swz(r);
     }
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
-        const int r = BM + wn * WN + nt * 32 + li;
-        bro[nt] = r * 128;
-        bfx[nt] = ((r - BM) >> 1) & 7;
+        const int r = wn * WN + nt * 32 + li;
+        bro[nt] = (BM + r) * RB;
+        bfx[nt] = swz(r);
     }
 
-    const int nk = K / 64;
+    const int nk = K / BK;
 #pragma unroll
-    for (int s = 0; s < S - 1; ++s)
+    for (int s = 0; s < DIST; ++s)
         if (s < nk) issue(s, s);
+    constexpr int KS = BK / 16;                 // MFMA k-steps per chunk
+    static_assert(!ILV || GPC % KS == 0, "pieces per k-step");
+    constexpr int PPS = GPC / KS;               // ILV: DMA pieces per k-step
+    constexpr int INFL = ILV ? DIST - 1 : DIST; // chunks issued after kc before its wait
     for (int kc = 0; kc < nk; ++kc) {
-        if (kc + S - 1 < nk) issue(kc + S - 1, (kc + S - 1) % S);
+        if (!ILV && kc + DIST < nk) issue(kc + DIST, (kc + DIST) % S);
         // chunks issued after kc that may stay in flight
-        const int ahead = min(S - 1, nk - 1 - kc);
-        if constexpr (S >= 4) {
+        const int ahead = min(INFL, nk - 1 - kc);
+        if constexpr (INFL >= 3) {
             if (ahead >= 3) wait_vm<3 * GPC>();
             else if (ahead == 2) wait_vm<2 * GPC>();
             else if (ahead == 1) wait_vm<GPC>();
             else wait_vm<0>();
-        } else if constexpr (S == 3) {
+        } else if constexpr (INFL == 2) {
             if (ahead >= 2) wait_vm<2 * GPC>();
             else if (ahead == 1) wait_vm<GPC>();
             else wait_vm<0>();
-        } else {
+        } else if constexpr (INFL == 1) {
             if (ahead >= 1) wait_vm<GPC>();
             else wait_vm<0>();
+        } else {
+            wait_vm<0>();
         }
         block_barrier();
         const char* base = smem + (kc % S) * STAGE;
+        const bool more = kc + DIST < nk;
 #pragma unroll
-        for (int kk = 0; kk < 4; ++kk) {
+        for (int kk = 0; kk < BK / 16; ++kk) {
             const int c = kk * 2 + lh;
             bf16x8 af[MT], bfr[NT];
 #pragma unroll
@@ -178,8 +211,29 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm16_kernel(RowGemmAr
             for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
                 for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma32_bf16(af[mt], bfr[nt], acc[mt][nt]);
+            if constexpr (ILV) {
+                if (more) issue_range(kc + DIST, (kc + DIST) % S, kk * PPS, (kk + 1) * PPS);
+            }
         }
-        // this stage's ds_reads must have returned before any wave restages it
+        if constexpr (ILV) {
+            // per k-step: its LDS reads, then MFMAs with the DMA pieces spread between them
+#pragma unroll
+            for (int kk = 0; kk < KS; ++kk) {
+                __builtin_amdgcn_sched_group_barrier(0x100, MT + NT, 0);  // DS read
+#pragma unroll
+                for (int q = 0; q < PPS; ++q) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, MT * NT / PPS, 0);  // MFMA
+                    __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);              // VMEM read
+                }
+            }
+        }
+        if constexpr (!ONEBAR) {
+            // this stage's ds_reads must have returned before any wave restages it
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            block_barrier();
+        }
+    }
+    if constexpr (ONEBAR) {  // the epilogue's LDS scratch overlaps stages other waves may read
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         block_barrier();
     }
@@ -188,18 +242,30 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm16_kernel(RowGemmAr
 
 // tiles: 0 = 128x128, 2 stages (64 KB LDS, 2 blocks/CU); 1 = 128x128, 3 stages (96 KB);
 // 2 = 256x128, 8 waves, 2 stages (96 KB); 3 = 128x128, 4 stages (128 KB);
-// 4 = 256x256, 8 waves of 128x64, 2 stages (128 KB); 5 = 256x128, 8 waves, 3 stages (144 KB)
+// 4 = 256x256, 8 waves of 128x64, 2 stages (128 KB); 5 = 256x128, 8 waves, 3 stages (144 KB);
+// BK = 32 stages: 6 = 256x256, 4 stages (128 KB, 3 chunks = 96 K in flight); 7 = 256x256,
+// 5 stages, one barrier per chunk (160 KB, 3 chunks in flight); 8 = 128x128, 4 stages, one
+// barrier (64 KB, 2 blocks/CU)
 using T16_0 = Tile16<128, 128, 64, 64, 2, 2>;
 using T16_1 = Tile16<128, 128, 64, 64, 3, 1>;
 using T16_2 = Tile16<256, 128, 64, 64, 2, 1>;
 using T16_3 = Tile16<128, 128, 64, 64, 4, 1>;
 using T16_4 = Tile16<256, 256, 128, 64, 2, 1>;
 using T16_5 = Tile16<256, 128, 64, 64, 3, 1>;
-#define ROWGEMM16_TILES(X) X(0, T16_0) X(1, T16_1) X(2, T16_2) X(3, T16_3) X(4, T16_4) X(5, T16_5)
+using T16_6 = Tile16<256, 256, 128, 64, 4, 1, 32>;
+using T16_7 = Tile16<256, 256, 128, 64, 5, 1, 32, true>;
+using T16_8 = Tile16<128, 128, 64, 64, 4, 2, 32, true>;
+// interleaved DMA issue: 9 = tile 6, 10 = tile 7, 11 = 128x128 BK 64 3 stages 1 block/CU
+using T16_9 = Tile16<256, 256, 128, 64, 4, 1, 32, false, true>;
+using T16_10 = Tile16<256, 256, 128, 64, 5, 1, 32, true, true>;
+using T16_11 = Tile16<128, 128, 64, 64, 3, 1, 64, false, true>;
+#define ROWGEMM16_TILES(X)                                                                     \
+    X(0, T16_0) X(1, T16_1) X(2, T16_2) X(3, T16_3) X(4, T16_4) X(5, T16_5) X(6, T16_6) X(7, T16_7) \
+    X(8, T16_8) X(9, T16_9) X(10, T16_10) X(11, T16_11)
 
 template <int AMODE, int EMODE, class T>
 static int rg16_go(const RowGemmArgs& a, hipStream_t s) {
-    if (a.N % T::BN || a.C % 64 || a.K % 64) return -1;
+    if (a.N % T::BN || a.C % T::BK || a.K % T::BK) return -1;
     if (EMODE == E_CONVT && (a.cout % T::BN)) return -1;
     const dim3 grid(((a.M + T::BM - 1) / T::BM) * (a.N / T::BN));
     hipLaunchKernelGGL((rowgemm16_kernel<AMODE, EMODE, T>), grid, dim3(T::THREADS), 0, s, a);
