@@ -151,6 +151,40 @@ def test_mod_config4_full_size_smoke():
     assert norm_rel(bn.running_mean.cpu(), 0.1 * mean.cpu()) <= 1e-4
 
 
+def test_mod_config4_bf16_full_size_vs_f32():
+    """Config 4 at 512x512 (bs 2) with bf16 MFMA and the runtime's default per-GEMM tile
+    choice (256x256 and 128x128 row GEMMs both occur at this size): two bf16 runs are
+    bit-identical, and the logits and gradients stay within bf16 distance of the f32-MFMA
+    evaluation of the same step (a gross indexing or pipelining fault in a tile that only
+    large M reaches would show as O(1) errors here; the fine parity is the bf16 oracle test
+    below at 64x64)."""
+    import unet_hip
+    torch.manual_seed(0)
+    x = torch.rand(2, 1, 512, 512, device=DEV)
+    t = (torch.rand(2, 1, 512, 512, device=DEV) > 0.5).float()
+    sd0 = None
+    outs = []
+    for dt in ("fp32", "bf16", "bf16"):
+        m = unet_hip.ModUNet(1, 1, base_filters=128, depth=5, mfma_dtype=dt)
+        if sd0 is None:
+            sd0 = {k: v.clone() for k, v in m.state_dict().items()}
+        m.load_state_dict(sd0)
+        m = m.to(DEV).train()
+        logits = m(x)
+        losses = unet_hip.seg_losses(logits, t)
+        (losses[0] + losses[1]).backward()
+        torch.cuda.synchronize()
+        outs.append((logits.detach().clone(),
+                     torch.cat([p.grad.reshape(-1) for p in m.parameters()]).clone()))
+        del m
+    (l32, g32), (l16, g16), (l16b, g16b) = outs
+    assert torch.equal(l16, l16b) and torch.equal(g16, g16b)
+    el = norm_rel(l16.cpu(), l32.cpu())
+    eg = norm_rel(g16.cpu(), g32.cpu())
+    print(f"config 4 512x512 bf16 vs f32: logits {el:.2e}, all grads {eg:.2e}")
+    assert el <= 5e-2 and eg <= 0.15
+
+
 # ---------------------------------------------------------------- bf16 MFMA (config 4)
 def _to64(d):
     return {k: (v.double() if v.is_floating_point() else v.clone()) for k, v in d.items()}
@@ -196,7 +230,7 @@ def test_rg16_bit_identical_to_register_staged(tile, wtile, monkeypatch):
 
 @pytest.mark.parametrize("base,depth,tile", [(64, 3, "4"), (128, 5, "0"), (128, 5, "2"), (128, 5, "4"),
                                              (128, 5, "6"), (128, 5, "7"),
-                                             (128, 5, "9"), (128, 5, "10")])
+                                             (128, 5, "9"), (128, 5, "10"), (128, 5, "auto")])
 def test_mod_bf16_matches_bf16_oracle(base, depth, tile, monkeypatch):
     """mfma_dtype="bf16": one step at B=2 64x64 vs the oracle that rounds exactly the GEMM
     operands the HIP bf16 kernels round (oracle/mod_ref_cpu.py, bf16=True).
@@ -208,10 +242,15 @@ def test_mod_bf16_matches_bf16_oracle(base, depth, tile, monkeypatch):
     gradients.  The bar is 2x that spread of the oracle against itself.  tile = the
     LDS-DMA GEMM tile (UNET_RG16_TILE; "2" = 256 rows x 8 waves, "4" = 256 x 256, the
     default: BN partials grouped by 256 rows, so the bf16 roundings differ from the
-    128-row tiles'), with the 256x256 weight-gradient tile on the 256-channel layers."""
+    128-row tiles'), with the 256x256 weight-gradient tile on the 256-channel layers;
+    "auto" = the runtime's per-GEMM choice (rg16_tile, runtime.hip) and default wgrad tile."""
     import unet_hip
-    monkeypatch.setenv("UNET_RG16_TILE", tile)
-    monkeypatch.setenv("UNET_WG16_TILE", "2" if tile in ("4", "6", "7", "9", "10") else "0")
+    if tile == "auto":
+        monkeypatch.delenv("UNET_RG16_TILE", raising=False)
+        monkeypatch.delenv("UNET_WG16_TILE", raising=False)
+    else:
+        monkeypatch.setenv("UNET_RG16_TILE", tile)
+        monkeypatch.setenv("UNET_WG16_TILE", "2" if tile in ("4", "6", "7", "9", "10") else "0")
     P = MO.make_params(42, base, depth)
     x, t = inputs(5, 2, 64, 64)
     ref = MO.train_step(P, MO.init_buffers(base, depth), None, x, t, depth=depth, bf16=True)

@@ -39,6 +39,9 @@ int k_to_bf16(const float* src, int ld, int off, int C, const float* scale, cons
 int k_bn_dz16(float* d, const float* y, int ld, int off, int64_t P, int C, const float* coef,
               int mask, uint16_t* dz16, int f32, hipStream_t s);
 int k_bias_reduce(const float* slab, int S, int taps, int C, float* out, hipStream_t s);
+// ConvT bias partials [splits][4][C] from the up half of the concat gradient (LDS-DMA wgrad)
+int k_up2_bias_partials(const float* d, int ld, int off, int H, int W, int64_t P, int C, int pps,
+                        int splits, float* bslab, hipStream_t s);
 int k_sum_partials(const float* part, int G, int ncols, float* out, hipStream_t s);
 int k_slab_reduce(const float* slab, int S, int Mw, int Nw, int kind, int cin, int cout,
                   float* grad, hipStream_t s);

@@ -536,28 +536,50 @@ __global__ __launch_bounds__(256) void bn_dz16_kernel(float* __restrict__ d, con
                                                       const float* __restrict__ coef, int mask,
                                                       int tpr, __bf16* __restrict__ dz16, int f32) {
     typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+    constexpr int U = 4;  // rows per thread per trip: 16 independent 16-B loads in flight
     const int rpp = 256 / tpr;
     const int c_first = (threadIdx.x % tpr) * 8;
-    for (int64_t m = (int64_t)blockIdx.x * rpp + threadIdx.x / tpr; m < P;
-         m += (int64_t)gridDim.x * rpp) {
+    for (int64_t m0 = (int64_t)blockIdx.x * rpp * U + threadIdx.x / tpr; m0 < P;
+         m0 += (int64_t)gridDim.x * rpp * U) {
         for (int c = c_first; c < C; c += tpr * 8) {
-            bf16x8 o16;
+            f32x4 dv[U][2], yv[U][2];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t m = m0 + u * rpp;
+                if (m < P) {
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        dv[u][h] = *(const f32x4*)(d + m * C + c + 4 * h);
+                        yv[u][h] = *(const f32x4*)(y + m * ld + off + c + 4 * h);
+                    }
+                }
+            }
+            f32x4 ka[2], kb[2], kc[2];
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
-                const int cc = c + 4 * h;
-                f32x4* pd = (f32x4*)(d + m * C + cc);
-                const f32x4 v = *(const f32x4*)(y + m * ld + off + cc);
-                const f32x4 r = *(const f32x4*)(coef + cc) * (*pd) + *(const f32x4*)(coef + C + cc) * v +
-                                *(const f32x4*)(coef + 2 * C + cc);
-                f32x4 o;
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    o[j] = (!mask || v[j] > 0.f) ? r[j] : 0.f;
-                    o16[4 * h + j] = (__bf16)o[j];
-                }
-                if (f32) *pd = o;
+                ka[h] = *(const f32x4*)(coef + c + 4 * h);
+                kb[h] = *(const f32x4*)(coef + C + c + 4 * h);
+                kc[h] = *(const f32x4*)(coef + 2 * C + c + 4 * h);
             }
-            *(bf16x8*)(dz16 + m * C + c) = o16;
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t m = m0 + u * rpp;
+                if (m >= P) break;
+                bf16x8 o16;
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const f32x4 v = yv[u][h];
+                    const f32x4 r = ka[h] * dv[u][h] + kb[h] * v + kc[h];
+                    f32x4 o;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        o[j] = (!mask || v[j] > 0.f) ? r[j] : 0.f;
+                        o16[4 * h + j] = (__bf16)o[j];
+                    }
+                    if (f32) *(f32x4*)(d + m * C + c + 4 * h) = o;
+                }
+                *(bf16x8*)(dz16 + m * C + c) = o16;
+            }
         }
     }
 }
@@ -591,31 +613,53 @@ __global__ __launch_bounds__(256) void to_bf16_kernel(const float* __restrict__ 
                                                       const float* __restrict__ shift, int relu,
                                                       int64_t P, int tpr, __bf16* __restrict__ dst) {
     typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+    constexpr int U = 4;  // rows per thread per trip: 8 independent 16-B loads in flight
     const int rpp = 256 / tpr;
     const int c_first = (threadIdx.x % tpr) * 8;
-    for (int64_t m = (int64_t)blockIdx.x * rpp + threadIdx.x / tpr; m < P;
-         m += (int64_t)gridDim.x * rpp) {
-        const float* row = src + m * ld + off;
+    for (int64_t m0 = (int64_t)blockIdx.x * rpp * U + threadIdx.x / tpr; m0 < P;
+         m0 += (int64_t)gridDim.x * rpp * U) {
         for (int c = c_first; c < C; c += tpr * 8) {
-            f32x4 v0 = *(const f32x4*)(row + c), v1 = *(const f32x4*)(row + c + 4);
-            if (scale) {
-                v0 = v0 * *(const f32x4*)(scale + c) + *(const f32x4*)(shift + c);
-                v1 = v1 * *(const f32x4*)(scale + c + 4) + *(const f32x4*)(shift + c + 4);
-            }
-            if (c < relu) {
+            f32x4 v[U][2];
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    v0[j] = fmaxf(v0[j], 0.f);
-                    v1[j] = fmaxf(v1[j], 0.f);
+            for (int u = 0; u < U; ++u) {
+                const int64_t m = m0 + u * rpp;
+                if (m < P) {
+                    const float* row = src + m * ld + off + c;
+                    v[u][0] = *(const f32x4*)row;
+                    v[u][1] = *(const f32x4*)(row + 4);
                 }
             }
-            bf16x8 o;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                o[j] = (__bf16)v0[j];
-                o[4 + j] = (__bf16)v1[j];
+            f32x4 sc0 = {1.f, 1.f, 1.f, 1.f}, sc1 = sc0, sh0 = {0.f, 0.f, 0.f, 0.f}, sh1 = sh0;
+            if (scale) {
+                sc0 = *(const f32x4*)(scale + c);
+                sc1 = *(const f32x4*)(scale + c + 4);
+                sh0 = *(const f32x4*)(shift + c);
+                sh1 = *(const f32x4*)(shift + c + 4);
             }
-            *(bf16x8*)(dst + m * C + c) = o;
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t m = m0 + u * rpp;
+                if (m >= P) break;
+                f32x4 v0 = v[u][0], v1 = v[u][1];
+                if (scale) {
+                    v0 = v0 * sc0 + sh0;
+                    v1 = v1 * sc1 + sh1;
+                }
+                if (c < relu) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        v0[j] = fmaxf(v0[j], 0.f);
+                        v1[j] = fmaxf(v1[j], 0.f);
+                    }
+                }
+                bf16x8 o;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    o[j] = (__bf16)v0[j];
+                    o[4 + j] = (__bf16)v1[j];
+                }
+                *(bf16x8*)(dst + m * C + c) = o;
+            }
         }
     }
 }
@@ -632,6 +676,62 @@ __global__ void bias_reduce_kernel(const float* __restrict__ slab, int S, int ta
         __syncthreads();
     }
     if (threadIdx.y == 0 && c < C) out[c] = (float)t;
+}
+
+// ConvT bias gradient partials for the LDS-DMA weight gradient (which has no B' column
+// sums): bslab[s][ab*C + c] = sum over the coarse pixels m of split s (pps per split) of
+// d[fine(m, ab)][off + c], i.e. the column sums of the G_UP2-gathered B' operand the
+// register-staged kernel forms, accumulated in f64 and rounded once, as it does.
+// Block = (split, ab, 64 channels); thread (quad q = tid % 16, row group g = tid / 16).
+__global__ __launch_bounds__(256) void up2_bias_partials_kernel(const float* __restrict__ d, int ld,
+                                                                int off, int H, int W, int64_t P,
+                                                                int C, int pps,
+                                                                float* __restrict__ bslab) {
+    __shared__ double red[16][64];
+    const int split = blockIdx.x, ab = blockIdx.y, c0 = blockIdx.z * 64;
+    const int tid = threadIdx.x, q = tid & 15, g = tid >> 4;
+    const int a = ab >> 1, b = ab & 1;
+    const int64_t pbeg = (int64_t)split * pps, pend = min(pbeg + pps, P);
+    const int c = c0 + 4 * q;
+    const bool ok = c < C;
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+    const int HW = H * W;
+    constexpr int U = 8;  // 8 independent row loads in flight per thread
+    for (int64_t m0 = pbeg + g; m0 < pend && ok; m0 += 16 * U) {
+        f32x4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t m = m0 + 16 * u;
+            if (m < pend) {
+                // 32-bit index math (the launcher guarantees 4 P < 2^31)
+                const int mm = (int)m;
+                const int n = mm / HW;
+                const int r = mm - n * HW;
+                const int i = r / W, j = r - i * W;
+                const int64_t f = (int64_t)n * 4 * HW + (2 * i + a) * (2 * W) + (2 * j + b);
+                v[u] = *(const f32x4*)(d + f * ld + off + c);
+            } else {
+                v[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            s0 += v[u][0];
+            s1 += v[u][1];
+            s2 += v[u][2];
+            s3 += v[u][3];
+        }
+    }
+    red[g][4 * q] = s0;
+    red[g][4 * q + 1] = s1;
+    red[g][4 * q + 2] = s2;
+    red[g][4 * q + 3] = s3;
+    __syncthreads();
+    if (tid < 64 && c0 + tid < C) {
+        double t = 0.0;
+        for (int k = 0; k < 16; ++k) t += red[k][tid];
+        bslab[(int64_t)split * 4 * C + ab * C + c0 + tid] = (float)t;
+    }
 }
 
 // out[c] = sum over G partial rows (fixed order), optional scatter stride
@@ -750,29 +850,36 @@ __global__ __launch_bounds__(256) void slab_reduce_wide_kernel(const float* __re
 // float 9 * cin apart, which on the 4096-channel layers made this pass HBM-write-bound at a
 // small fraction of the bandwidth).  Per element the S slabs are summed in exactly the
 // association of slab_reduce_kernel, so both kernels give identical bits.
+// CI = input channels per tile: 32 for the transposing copy (S == 1: 36 loads per thread in
+// flight), 8 when slabs are summed (each thread walks S slabs per element with 8 loads in
+// flight; the 4x smaller tile gives 4x the blocks, which is what keeps enough loads in flight
+// on layers with only 256 32x32 tiles).
+template <int CI>
 __global__ __launch_bounds__(256) void slab_reduce_conv3_kernel(const float* __restrict__ slab, int S,
                                                                 int cin, int cout,
                                                                 float* __restrict__ grad) {
-    __shared__ float tile[32][32 * 9 + 1];
-    const int n0 = blockIdx.x * 32, c0 = blockIdx.y * 32;
+    constexpr int ROWS = 9 * CI;  // (tap, ci) rows of the tile
+    __shared__ float tile[32][ROWS + 1];
+    const int n0 = blockIdx.x * 32, c0 = blockIdx.y * CI;
     const int Nw = cout;
     const int64_t total = (int64_t)9 * cin * cout;
     const int nl = threadIdx.x & 31, rr = threadIdx.x >> 5;
-    if (S == 1) {  // a transposing copy: all 36 loads of the thread in flight at once
-        float v[36];
+    if (S == 1) {  // a transposing copy: all loads of the thread in flight at once
+        constexpr int NV = ROWS / 8;
+        float v[NV];
 #pragma unroll
-        for (int it = 0; it < 36; ++it) {
-            const int row = rr + 8 * it, tap = row / 32, cl = row - tap * 32;
+        for (int it = 0; it < NV; ++it) {
+            const int row = rr + 8 * it, tap = row / CI, cl = row - tap * CI;
             v[it] = slab[(int64_t)(tap * cin + c0 + cl) * Nw + n0 + nl];
         }
 #pragma unroll
-        for (int it = 0; it < 36; ++it) {
-            const int row = rr + 8 * it, tap = row / 32, cl = row - tap * 32;
+        for (int it = 0; it < NV; ++it) {
+            const int row = rr + 8 * it, tap = row / CI, cl = row - tap * CI;
             tile[nl][cl * 9 + tap] = v[it];
         }
     }
-    for (int row = S == 1 ? 9 * 32 : rr; row < 9 * 32; row += 8) {
-        const int tap = row / 32, cl = row - tap * 32;
+    for (int row = S == 1 ? ROWS : rr; row < ROWS; row += 8) {
+        const int tap = row / CI, cl = row - tap * CI;
         const int64_t e = (int64_t)(tap * cin + c0 + cl) * Nw + n0 + nl;
         const float* sp = slab + e;
         float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
@@ -790,8 +897,8 @@ __global__ __launch_bounds__(256) void slab_reduce_conv3_kernel(const float* __r
         tile[nl][cl * 9 + tap] = (a0 + a1) + (a2 + a3);
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < 32 * 32 * 9; i += 256) {
-        const int n = i / (32 * 9), off = i - n * (32 * 9);
+    for (int i = threadIdx.x; i < 32 * ROWS; i += 256) {
+        const int n = i / ROWS, off = i - n * ROWS;
         grad[((int64_t)(n0 + n) * cin + c0) * 9 + off] = tile[n][off];
     }
 }
@@ -1266,7 +1373,7 @@ int k_to_bf16(const float* src, int ld, int off, int C, const float* scale, cons
     const int c8 = C / 8;
     const int tpr = c8 >= 256 ? 256 : c8;
     if (256 % tpr || (c8 > 256 && c8 % 256)) return -1;
-    hipLaunchKernelGGL(to_bf16_kernel, dim3(grid_for(P * tpr)), dim3(256), 0, s, src, ld, off, C,
+    hipLaunchKernelGGL(to_bf16_kernel, dim3(grid_for((P + 3) / 4 * tpr)), dim3(256), 0, s, src, ld, off, C,
                        scale, shift, relu, P, tpr, (__bf16*)dst);
     LAUNCH_CHECK();
 }
@@ -1276,13 +1383,20 @@ int k_bn_dz16(float* d, const float* y, int ld, int off, int64_t P, int C, const
     const int c8 = C / 8;
     const int tpr = c8 >= 256 ? 256 : c8;
     if (256 % tpr || (c8 > 256 && c8 % 256)) return -1;
-    hipLaunchKernelGGL(bn_dz16_kernel, dim3(grid_for(P * tpr)), dim3(256), 0, s, d, y, ld, off, P, C,
+    hipLaunchKernelGGL(bn_dz16_kernel, dim3(grid_for((P + 3) / 4 * tpr)), dim3(256), 0, s, d, y, ld, off, P, C,
                        coef, mask, tpr, (__bf16*)dz16, f32);
     LAUNCH_CHECK();
 }
 int k_bias_reduce(const float* slab, int S, int taps, int C, float* out, hipStream_t s) {
     hipLaunchKernelGGL(bias_reduce_kernel, dim3((C + 63) / 64), dim3(64, 16), 0, s, slab, S, taps, C,
                        out);
+    LAUNCH_CHECK();
+}
+int k_up2_bias_partials(const float* d, int ld, int off, int H, int W, int64_t P, int C, int pps,
+                        int splits, float* bslab, hipStream_t s) {
+    if (C % 4 || ld % 4 || off % 4 || pps < 1 || splits < 1 || 4 * P >= (1ll << 31)) return -1;
+    hipLaunchKernelGGL(up2_bias_partials_kernel, dim3(splits, 4, (C + 63) / 64), dim3(256), 0, s, d,
+                       ld, off, H, W, P, C, pps, bslab);
     LAUNCH_CHECK();
 }
 int k_sum_partials(const float* part, int G, int ncols, float* out, hipStream_t s) {
@@ -1292,9 +1406,14 @@ int k_sum_partials(const float* part, int G, int ncols, float* out, hipStream_t 
 }
 int k_slab_reduce(const float* slab, int S, int Mw, int Nw, int kind, int cin, int cout,
                   float* grad, hipStream_t s) {
-    if (kind == 0 && cin % 32 == 0 && cout % 32 == 0 && (cin / 32) * (cout / 32) >= 128) {
-        hipLaunchKernelGGL(slab_reduce_conv3_kernel, dim3(cout / 32, cin / 32), dim3(256), 0, s, slab, S,
-                           cin, cout, grad);
+    if (kind == 0 && S == 1 && cin % 32 == 0 && cout % 32 == 0 && (cin / 32) * (cout / 32) >= 128) {
+        hipLaunchKernelGGL(slab_reduce_conv3_kernel<32>, dim3(cout / 32, cin / 32), dim3(256), 0, s, slab,
+                           S, cin, cout, grad);
+        LAUNCH_CHECK();
+    }
+    if (kind == 0 && S > 1 && S < 32 && cin % 8 == 0 && cout % 32 == 0 && (cin / 8) * (cout / 32) >= 256) {
+        hipLaunchKernelGGL(slab_reduce_conv3_kernel<8>, dim3(cout / 32, cin / 8), dim3(256), 0, s, slab,
+                           S, cin, cout, grad);
         LAUNCH_CHECK();
     }
     if (Nw % 4) return -1;

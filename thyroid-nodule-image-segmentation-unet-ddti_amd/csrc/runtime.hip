@@ -314,6 +314,7 @@ struct Plan {
     uint16_t* s16;
     void* zero16;
     std::vector<uint16_t*> x16;  // training, bf16: per-conv input images kept for the wgrad
+    std::vector<uint16_t*> t16;  // training, bf16: per-ConvT input images kept for the wgrad
     size_t bytes;
 };
 
@@ -397,14 +398,31 @@ bool rg16_on(const unet_ctx* c, int C, int N) {
     const char* e = getenv("UNET_RG16");
     return c->bf16 && (e ? atoi(e) : 1) != 0 && C % 64 == 0 && N % 128 == 0;
 }
-// tile for an output width N (and ConvT cout): the requested one (default 256x256) when N
-// divides into it, else the 128x128 tile
-int rg16_tile(int N = 128, int cout = 0) {
-    const char* e = getenv("UNET_RG16_TILE");
-    const int t = e ? atoi(e) : 4;  // 256x256 (config 4 A/B: 104.2 vs 99.7 img/s for 128x128)
-    int bm = 0, bn = 0;
-    if (rowgemm16_tile_dims(t, &bm, &bn) != 0) return 0;
-    return (N % bn == 0 && (cout == 0 || cout % bn == 0)) ? t : 0;
+// tile for one LDS-DMA row GEMM.  UNET_RG16_TILE forces a tile (128x128 where N does not
+// divide into it).  Default: the 256x256 tile (8 waves, one block per CU) unless
+//  * it would leave CUs idle: fewer than 256 blocks (the 16x16 / 32x32 levels of config 4:
+//    bottleneck fwd 0.48 -> 0.37 ms, its dgrad 0.90 -> 0.48 ms on the 128x128 tile), or
+//  * the epilogue is the BN-backward-partials one (E_STORE_BN: reads the BN input, writes
+//    f32 and reduces per-channel partials) over a short K < 8192: with one block per CU
+//    nothing hides that epilogue, while two co-resident 128x128 blocks overlap one's
+//    epilogue with the other's MFMAs (level-1 dgrad 1.15 -> 0.80 ms, level-0 ConvT dgrad
+//    0.77 -> 0.37 ms; per-layer sweep in profiles/r01_rg16_tile_sweep.txt).
+int rg16_tile(const RowGemmArgs& g) {
+    const int cout = g.emode == E_CONVT ? g.cout : 0;
+    auto fits = [&](int t) {
+        int bm = 0, bn = 0;
+        if (rowgemm16_tile_dims(t, &bm, &bn) != 0) return false;
+        return g.N % bn == 0 && (cout == 0 || cout % bn == 0);
+    };
+    if (const char* e = getenv("UNET_RG16_TILE")) {
+        const int t = atoi(e);
+        return fits(t) ? t : 0;
+    }
+    if (!fits(4)) return 0;
+    const int64_t blocks = (g.M + 255) / 256 * (g.N / 256);
+    if (blocks < 256) return 0;
+    if (g.emode == E_STORE_BN && g.K < 8192) return 0;
+    return 4;
 }
 // 3x3 weight gradients of layers with Cin, Cout multiples of 128 on the LDS-DMA
 // transposed-read kernel (kernels_gemm16.hip wgrad16_kernel) from the forward's bf16 input
@@ -426,6 +444,15 @@ int wg16_tile(int CA = 128, int CB = 128) {
     const int t = e ? atoi(e) : 2;
     if (t == 2 && (CA % 256 || CB % 256)) return 0;
     return t;
+}
+// ConvT weight gradient on the LDS-DMA transposed-read kernel (A' = the forward's bf16
+// ConvT input image, B' = the bf16 image of the concat gradient's up half, G_UP2-gathered);
+// the bias gradient then comes from k_up2_bias_partials.  UNET_WG16T=0 keeps the
+// register-staged kernel.
+bool convt_wg16_on(const unet_ctx* c, int cin, int cout) {
+    const char* e = getenv("UNET_WG16T");
+    return (e ? atoi(e) : 1) != 0 && wg16_on(c, cin, cout) && rg16_on(c, cin, 4 * cout) &&
+           rg16_on(c, cout, cin);
 }
 
 void make_plan(unet_ctx* c, int N, int H, int W, bool training, char* base, Plan& p) {
@@ -510,6 +537,12 @@ void make_plan(unet_ctx* c, int N, int H, int W, bool training, char* base, Plan
     for (int i = 0; i < NC && training; ++i)
         if (wg16_on(c, c->conv[i].cin, c->conv[i].cout) && rg16_on(c, c->conv[i].cin, c->conv[i].cout))
             p.x16[i] = b.take<uint16_t>(p.P[c->conv[i].level] * c->conv[i].cin);
+    p.t16.assign(c->convt.size(), nullptr);
+    for (size_t k = 0; k < c->convt.size() && training; ++k) {
+        const ConvTL& T = c->convt[k];
+        if (!c->res && convt_wg16_on(c, T.cin, T.cout))
+            p.t16[k] = b.take<uint16_t>(p.P[T.in_level] * T.cin);
+    }
     if (training) {
         int64_t gmax = p.P[0] * c->base;
         for (int i = 0; i < NC; ++i) {
@@ -830,7 +863,7 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
                                            img, s));
                 use_a16(p, g, C.cin);
                 g.a16 = img;
-                const int tile = rg16_tile(C.cout);
+                const int tile = rg16_tile(g);
                 int bm, bn;
                 rowgemm16_tile_dims(tile, &bm, &bn);
                 R = (int)((M + bm - 1) / bm);
@@ -878,10 +911,12 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
         g.cout = T.cout;
         g.emode = E_CONVT;
         if (!c->res && rg16_on(c, T.cin, T.cout)) {
+            uint16_t* img = p.t16[k] ? p.t16[k] : p.s16;
             RUN("prep16", 0, k_to_bf16(g.a, g.lda, g.aoff, T.cin, g.ascale, g.ashift, g.arelu, g.M,
-                                       p.s16, s));
+                                       img, s));
             use_a16(p, g, T.cin);
-            const int tile = rg16_tile(g.N, T.cout);
+            g.a16 = img;
+            const int tile = rg16_tile(g);
             RUN(tlabel16("convT_fwd", tile, 100 + k), 2.0 * g.M * g.N * g.K,
                 launch_rowgemm16(g, tile, s));
             return 0;
@@ -1185,7 +1220,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
             }
             if (dz16 && rg16_on(c, C.cout, C.cin)) {
                 use_a16(p, g, C.cout);
-                const int tile = rg16_tile(C.cin);
+                const int tile = rg16_tile(g);
                 int bm, bn;
                 rowgemm16_tile_dims(tile, &bm, &bn);
                 if (rows) *rows = (int)((P + bm - 1) / bm);
@@ -1242,9 +1277,38 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         w.splits = wc.splits;
         w.slab = p.slab;
         w.bf16 = c->bf16;
-        side_after_main();
-        RUNW(wlabel("convT_wgrad", wc, 100 + k), 2.0 * Pin * T.cin * 4 * T.cout,
-             launch_wgrad(w, wc.tile, sw));
+        const bool t16 = p.t16[k] != nullptr;
+        if (t16) {
+            // bf16 image of the up half of the concat gradient: B' here, A of the dgrad below
+            before_write(p.s16);
+            RUN("prep16", 0, k_to_bf16(p.dcat[lo], ldo, uo, T.cout, nullptr, nullptr, 0, p.P[lo],
+                                       p.s16, s));
+            side_after_main();
+            w.a = (const float*)p.t16[k];
+            w.lda = T.cin;
+            w.aoff = 0;
+            w.ascale = w.ashift = nullptr;
+            w.arelu = 0;
+            w.b = (const float*)p.s16;
+            w.ldb = T.cout;
+            w.boff = 0;
+            w.bias_slab = nullptr;
+            w.zero16 = p.zero16;
+            w.xcd = xcd16_on();
+            const int t = wg16_tile(T.cin, T.cout);
+            int wbm = 0, wbn = 0, wst = 0;
+            wgrad16g_tile_dims(t, &wbm, &wbn, &wst);
+            char lb[96];
+            snprintf(lb, sizeof lb, "convT_wgrad/wg16_%dx%ds%d|%d", wbm, wbn, wst, 100 + k);
+            RUNW(lb, 2.0 * Pin * T.cin * 4 * T.cout, launch_wgrad16(w, t, sw));
+            side_read(p.s16);
+            RUNW("bias_grad", 0, k_up2_bias_partials(p.dcat[lo], ldo, uo, Hi, Wi, Pin, T.cout, wc.pps,
+                                                     wc.splits, p.bslab, sw));
+        } else {
+            side_after_main();
+            RUNW(wlabel("convT_wgrad", wc, 100 + k), 2.0 * Pin * T.cin * 4 * T.cout,
+                 launch_wgrad(w, wc.tile, sw));
+        }
         side_read(p.dcat[lo]);
         RUNW("wgrad_reduce", 0,
              k_slab_reduce(p.slab, wc.splits, w.Mw, w.Nw, 1, T.cin, T.cout, grads + T.w, sw));
@@ -1279,10 +1343,13 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
             g.stats = p.part;
         }
         if (!c->res && rg16_on(c, T.cout, T.cin)) {
-            RUN("prep16", 0, k_to_bf16(p.dcat[lo], ldo, uo, T.cout, nullptr, nullptr, 0, p.P[lo],
-                                       p.s16, s));
+            if (!t16) {
+                before_write(p.s16);
+                RUN("prep16", 0, k_to_bf16(p.dcat[lo], ldo, uo, T.cout, nullptr, nullptr, 0, p.P[lo],
+                                           p.s16, s));
+            }
             use_a16(p, g, T.cout);
-            const int tile = rg16_tile(T.cin);
+            const int tile = rg16_tile(g);
             int bm, bn;
             rowgemm16_tile_dims(tile, &bm, &bn);
             *rows = (int)((Pin + bm - 1) / bm);
