@@ -72,18 +72,39 @@ __global__ __launch_bounds__(256) void pack_conv3_tiled_kernel(const float* __re
     }
 }
 
+// ConvT: one block per LDS tile of 32 ci x 32 co x 4 taps (ab).  The torch rows (co, ab
+// contiguous per ci) are read with unit stride; Tf rows (ab, co) are written as 32-element ci
+// runs and Td rows (ci) as 32-element co runs per ab (the element-wise form scattered every
+// Tf element cin apart).  Row stride 129 floats: both LDS read patterns are conflict-free.
 template <class OUT>
-__global__ void pack_convT_kernel(const float* __restrict__ w, OUT* __restrict__ tf,
-                                  OUT* __restrict__ td, int cin, int cout) {
-    const int64_t n = (int64_t)cin * cout * 4;
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
-         i += (int64_t)gridDim.x * blockDim.x) {
-        const int ab = (int)(i & 3);
-        const int64_t t = i >> 2;
-        const int co = (int)(t % cout), ci = (int)(t / cout);
-        const OUT v = (OUT)w[i];
-        tf[((int64_t)ab * cout + co) * cin + ci] = v;
-        if (td) td[(int64_t)ci * 4 * cout + ab * cout + co] = v;
+__global__ __launch_bounds__(256) void pack_convT_tiled_kernel(const float* __restrict__ w,
+                                                               OUT* __restrict__ tf,
+                                                               OUT* __restrict__ td, int cin,
+                                                               int cout) {
+    constexpr int T = 32, RS = T * 4 + 1;
+    __shared__ float tile[T * RS];  // [ci_l][co_l * 4 + ab]
+    const int co0 = blockIdx.x * T, ci0 = blockIdx.y * T;
+    const int nci = min(T, cin - ci0), nco = min(T, cout - co0);
+    const int tid = threadIdx.x;
+    for (int e = tid; e < T * T * 4; e += 256) {  // e = ci_l * 128 + (co_l * 4 + ab)
+        const int ci_l = e / (T * 4), r = e - ci_l * (T * 4);
+        if (ci_l < nci && r < nco * 4)
+            tile[ci_l * RS + r] = w[((int64_t)(ci0 + ci_l) * cout + co0) * 4 + r];
+    }
+    __syncthreads();
+    const int l = tid & 31, g = tid >> 5;  // 8 groups of 32 lanes
+    // Tf[(ab * cout + co)][ci]: rows (ab, co_l), lanes over ci
+    for (int row = g; row < 4 * T; row += 8) {
+        const int ab = row / T, co_l = row - ab * T;
+        if (co_l < nco && l < nci)
+            tf[((int64_t)ab * cout + co0 + co_l) * cin + ci0 + l] = (OUT)tile[l * RS + co_l * 4 + ab];
+    }
+    if (!td) return;
+    // Td[ci][ab * cout + co]: rows (ci_l, ab), lanes over co
+    for (int row = g; row < 4 * T; row += 8) {
+        const int ci_l = row >> 2, ab = row & 3;
+        if (ci_l < nci && l < nco)
+            td[(int64_t)(ci0 + ci_l) * 4 * cout + ab * cout + co0 + l] = (OUT)tile[ci_l * RS + l * 4 + ab];
     }
 }
 
@@ -1280,15 +1301,13 @@ int k_pack_conv3_bf16(const float* w, uint16_t* wf, uint16_t* wd, int cin, int c
     LAUNCH_CHECK();
 }
 int k_pack_convT(const float* w, float* tf, float* td, int cin, int cout, hipStream_t s) {
-    const int64_t n = (int64_t)cin * cout * 4;
-    hipLaunchKernelGGL(pack_convT_kernel<float>, dim3(grid_for(n)), dim3(256), 0, s, w, tf, td, cin,
-                       cout);
+    hipLaunchKernelGGL(pack_convT_tiled_kernel<float>, dim3((cout + 31) / 32, (cin + 31) / 32),
+                       dim3(256), 0, s, w, tf, td, cin, cout);
     LAUNCH_CHECK();
 }
 int k_pack_convT_bf16(const float* w, uint16_t* tf, uint16_t* td, int cin, int cout, hipStream_t s) {
-    const int64_t n = (int64_t)cin * cout * 4;
-    hipLaunchKernelGGL(pack_convT_kernel<__bf16>, dim3(grid_for(n)), dim3(256), 0, s, w,
-                       (__bf16*)tf, (__bf16*)td, cin, cout);
+    hipLaunchKernelGGL(pack_convT_tiled_kernel<__bf16>, dim3((cout + 31) / 32, (cin + 31) / 32),
+                       dim3(256), 0, s, w, (__bf16*)tf, (__bf16*)td, cin, cout);
     LAUNCH_CHECK();
 }
 int k_conv_first_fwd(const float* x, const float* w, const float* b, float* y, int P, int H, int W,

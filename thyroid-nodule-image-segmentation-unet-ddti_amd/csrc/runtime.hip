@@ -34,6 +34,10 @@ namespace {
 constexpr float BN_EPS = 1e-5f;       // nn.BatchNorm2d default (models/model.py:38,41)
 constexpr float BN_MOMENTUM = 0.1f;   // nn.BatchNorm2d default
 constexpr int RED_G = 512;            // first-level blocks of the channel reductions
+constexpr int WIDE_G = 2048;          // ... of the level-0 bandwidth passes (more loads in flight)
+// blocks of a channel-reduction pass over P pixels: RED_G, up to WIDE_G on large levels (the
+// partial buffers hold P/64 + 1 rows: p.stats / p.part per conv of the level, p.hpart WIDE_G)
+inline int wide_g(int64_t P) { return (int)std::min<int64_t>(WIDE_G, std::max<int64_t>(RED_G, P / 64)); }
 constexpr int STAT_G = 256;           // second level of the BN-stat reduction
 constexpr int MAX_DEPTH = 6;
 
@@ -576,7 +580,7 @@ void make_plan(unet_ctx* c, int N, int H, int W, bool training, char* base, Plan
             pmax = std::max(pmax, (p.P[c->conv[i].level] / 64 + 1) * 2 * c->conv[i].cout);
         p.part = b.take<float>(pmax);
         p.part2 = b.take<float>((int64_t)STAT_G * 2 * c->cmax);
-        p.hpart = b.take<float>((int64_t)RED_G *
+        p.hpart = b.take<float>((int64_t)WIDE_G *
                                 std::max<int64_t>(10 * c->base, (int64_t)c->out_ch * (c->base + 1)));
         p.bslab = b.take<float>(std::max<int64_t>(bmax, 1));
         p.coef = b.take<float>(3 * (int64_t)c->cmax);
@@ -830,7 +834,7 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
         const int64_t M = p.P[C.level];
         int R;
         if (i == 0 && C.pf < 0) {
-            R = RED_G;
+            R = wide_g(M);
             RUN("conv_first_fwd", 2.0 * M * 9 * C.cout,
                 k_conv_first_fwd(xin, prm + C.w, bias_ptr(prm, C.b), p.y[0], (int)M, Hl, Wl, C.cout,
                                  c->bn_relu ? 0 : 1, p.stats, R, s));
@@ -1106,7 +1110,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         if (i == 0 && C.pf < 0) {
             RUN("conv_first_wgrad", 2.0 * P * 9 * C.cout,
                 k_conv_first_wgrad(p.x_nhwc, dout, p.y[0], p.coef, (int)P, Hl, Wl, C.cout, dz_mask,
-                                   p.hpart, RED_G, grads + C.w,
+                                   p.hpart, wide_g(P), grads + C.w,
                                    C.b >= 0 ? grads + C.b : nullptr, s));
             return 0;
         }
@@ -1446,8 +1450,8 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         };
         RUN("head_bwd", 2.0 * p.P[0] * c->base * c->out_ch * 2,
             k_head_bwd(p.out[2 * D], c->base, nullptr, nullptr, 0, prm + c->head_w, c->out_ch,
-                       (int)p.P[0], H * W, dlogits, G0, p.hpart, nullptr, RED_G, s));
-        RUN("head_grad", 0, k_sum_partials(p.hpart, RED_G, c->out_ch * c->base + c->out_ch,
+                       (int)p.P[0], H * W, dlogits, G0, p.hpart, nullptr, wide_g(p.P[0]), s));
+        RUN("head_grad", 0, k_sum_partials(p.hpart, wide_g(p.P[0]), c->out_ch * c->base + c->out_ch,
                                            grads + c->head_w, s));
         if ((rc = block_bwd(2 * D, p.dcat[0], 2 * c->base))) return rc;
         stage_done(0);
@@ -1478,10 +1482,10 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
     RUN("head_bwd", 2.0 * p.P[0] * c->base * c->out_ch * 2,
         k_head_bwd(p.y[last], c->base, p.scale[last], p.shift[last], c->bn_relu ? 1 : 0,
                    prm + c->head_w, c->out_ch, (int)p.P[0], H * W, dlogits, G0, p.hpart, p.part,
-                   RED_G, s));
-    RUN("head_grad", 0, k_sum_partials(p.hpart, RED_G, c->out_ch * c->base + c->out_ch,
+                   wide_g(p.P[0]), s));
+    RUN("head_grad", 0, k_sum_partials(p.hpart, wide_g(p.P[0]), c->out_ch * c->base + c->out_ch,
                                        grads + c->head_w, s));
-    if ((rc = bn_finalize(last, RED_G))) return rc;
+    if ((rc = bn_finalize(last, wide_g(p.P[0])))) return rc;
     if ((rc = conv_bwd(last, G0, G1, c->base, true, &R))) return rc;
     if ((rc = bn_finalize(last - 1, R))) return rc;
     if ((rc = conv_bwd(last - 1, G1, p.dcat[0], 2 * c->base, false, nullptr))) return rc;
@@ -1510,14 +1514,17 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         const int i1 = 2 * b + 1, i0 = 2 * b;
         float* nxt = cur == G0 ? G1 : G0;
         before_write(nxt);
+        // up to 2048 blocks on the large levels (512 left the pass at ~4.7 TB/s); the partial
+        // rows fit: p.part holds P/64 + 1 rows of 2C for every conv of the level
+        const int Gmp = wide_g(p.P[b]);
         RUN("maxpool_bwd", 0,
             k_maxpool_bwd(cur, p.idx[b], p.dcat[b], 2 * C, c->skip_off(b), p.y[i1], p.ldy[i1],
                           p.offy[i1], c->bn_relu ? p.scale[i1] : nullptr,
                           c->bn_relu ? p.shift[i1] : nullptr, p.N, H >> b, W >> b, C, nxt, p.part,
-                          RED_G, s));
+                          Gmp, s));
         cur = nxt;
         nxt = cur == G0 ? G1 : G0;
-        if ((rc = bn_finalize(i1, RED_G))) return rc;
+        if ((rc = bn_finalize(i1, Gmp))) return rc;
         if ((rc = conv_bwd(i1, cur, nxt, C, true, &R))) return rc;
         cur = nxt;
         nxt = cur == G0 ? G1 : G0;
