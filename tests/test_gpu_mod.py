@@ -190,7 +190,8 @@ def _to64(d):
     return {k: (v.double() if v.is_floating_point() else v.clone()) for k, v in d.items()}
 
 
-@pytest.mark.parametrize("tile,wtile", [("0", "0"), ("1", "1"), ("3", "0"), ("0", "2"), ("8", "0"), ("11", "0")])
+@pytest.mark.parametrize("tile,wtile", [("0", "0"), ("1", "1"), ("3", "0"), ("0", "2"), ("8", "0"), ("11", "0"),
+                                       ("0", "3"), ("0", "4")])
 def test_rg16_bit_identical_to_register_staged(tile, wtile, monkeypatch):
     """The LDS-DMA bf16 GEMMs (kernels_gemm16.hip, fed by the k_to_bf16 operand images:
     row GEMMs and the transposed-read weight gradients) against the register-staged bf16

@@ -500,7 +500,10 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void wgrad16_kernel(WgradArgs p
 using W16_0 = WTile16<128, 128, 64, 64, 64, 2, 2>;
 using W16_1 = WTile16<128, 128, 64, 64, 64, 3, 1>;
 using W16_2 = WTile16<256, 256, 128, 64, 64, 2, 1>;
-#define WGRAD16G_TILES(X) X(0, W16_0) X(1, W16_1) X(2, W16_2)
+// 3 = 256x128, 4 = 128x256: 8 waves of 64x64, 3 stages (144 KB, two chunks in flight)
+using W16_3 = WTile16<256, 128, 64, 64, 64, 3, 1>;
+using W16_4 = WTile16<128, 256, 64, 64, 64, 3, 1>;
+#define WGRAD16G_TILES(X) X(0, W16_0) X(1, W16_1) X(2, W16_2) X(3, W16_3) X(4, W16_4)
 
 template <int AMODE, int BMODE, class T>
 static int wg16_go(const WgradArgs& a, hipStream_t s) {
@@ -563,6 +566,8 @@ int launch_wgrad16(const WgradArgs& a, int tile, hipStream_t s) {
         if (tile == 0) return wg16_go<AM, BMD, W16_0>(a, s); \
         if (tile == 1) return wg16_go<AM, BMD, W16_1>(a, s); \
         if (tile == 2) return wg16_go<AM, BMD, W16_2>(a, s); \
+        if (tile == 3) return wg16_go<AM, BMD, W16_3>(a, s); \
+        if (tile == 4) return wg16_go<AM, BMD, W16_4>(a, s); \
         return -1;                                       \
     } while (0)
     if (a.amode == G_CONV3 && a.bmode == G_IDENT) WG16G(G_CONV3, G_IDENT);

@@ -446,7 +446,8 @@ int xcd16_on() {
 int wg16_tile(int CA = 128, int CB = 128) {
     const char* e = getenv("UNET_WG16_TILE");
     const int t = e ? atoi(e) : 2;
-    if (t == 2 && (CA % 256 || CB % 256)) return 0;
+    int bm = 0, bn = 0;
+    if (wgrad16g_tile_dims(t, &bm, &bn) != 0 || CA % bm || CB % bn) return 0;
     return t;
 }
 // ConvT weight gradient on the LDS-DMA transposed-read kernel (A' = the forward's bf16

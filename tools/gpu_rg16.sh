@@ -8,7 +8,7 @@ rc=$?
 echo "pytest rc=$rc"; grep -E "PASS|FAIL|Error|assert|bf16 base" gpurun_out/$TAG.pytest.log | head -30
 if [ $rc -ne 0 ]; then tail -30 gpurun_out/$TAG.pytest.log; exit $rc; fi
 for T in ${TILES:-}; do
-  if [ "$T" = auto ]; then E=""; else E="UNET_RG16_TILE=$T"; fi
+  if [ "$T" = auto ]; then E=""; else E="${TVAR:-UNET_RG16_TILE}=$T"; fi
   env $E timeout -k 10 300 python bench.py --config 4 --mfma bf16 --steps 4 --warmup 2 --verbose --no-cpu-baseline > gpurun_out/$TAG.t$T.json 2> gpurun_out/$TAG.t$T.err
   rc=$?
   echo "tile $T rc=$rc"; python3 -c "import json;d=json.load(open('gpurun_out/$TAG.t$T.json'));print(d['value'], d['ms_per_step'], d['roofline']['kernel'], d['roofline']['achieved'])"
