@@ -29,7 +29,7 @@ def short(name):
     m = re.search(r"WgTile<(\d+), (\d+), \d+, \d+, (\d+)", name)
     if m:
         return f"wgrad_{m.group(1)}x{m.group(2)}x{m.group(3)}"
-    m = re.search(r"Tile16<(\d+), (\d+), \d+, \d+, (\d+), \d+>", name)
+    m = re.search(r"(?<!W)Tile16<(\d+), (\d+), \d+, \d+, (\d+), \d+[,>]", name)
     if m:
         return f"rg16_{m.group(1)}x{m.group(2)}s{m.group(3)}"
     m = re.search(r"WTile16<(\d+), (\d+), \d+, \d+, \d+, (\d+), \d+>", name)
