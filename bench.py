@@ -16,8 +16,10 @@ time = max over ranks).  ``roofline`` is for the dominant kernel (most GPU time 
 profiling step), from per-launch HIP events recorded on the launch stream inside the
 library around that kernel's launches in the timed region: achieved = algorithmic FLOP
 of its launches / their summed duration.
-``cpu_baseline`` times the CPU oracle (oracle/unet_ref_cpu.py, a torch-CPU restatement
-of the reference's step) on a bounded sample (bs=4) on rank 0 only.
+``step_ms_median`` / ``step_ms_p90`` are per-step device times (HIP events at the step
+boundaries on the launch stream).  ``cpu_baseline`` times the CPU oracle
+(oracle/unet_ref_cpu.py, a torch-CPU restatement of the reference's step) on a bounded
+sample (bs=4, median of 3 steps) on rank 0 only -- the only use of oracle/ here.
 """
 import argparse
 import json
@@ -49,8 +51,11 @@ def parse():
     ap.add_argument("--batch", type=int, default=0, help="images per GPU (default 32 / 8)")
     ap.add_argument("--size", type=int, default=0, help="image side (default 256 / 512)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--cpu-steps", type=int, default=3)
     ap.add_argument("--verbose", action="store_true")
+    ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
+                    help="kernel-schedule option of the native context (unet_set_option; "
+                         "A/B runs), repeatable")
     ap.add_argument("--timing", default="dominant", choices=("dominant", "all"),
                     help="per-launch events in the timed region: around the dominant kernel "
                          "only (default) or around every launch")
@@ -181,8 +186,7 @@ def main():
 
     import unet_hip
     from unet_hip.dist import DistributedUNet
-    from oracle import mod_ref_cpu as MO  # analytic FLOP counts only
-    from oracle import unet_ref_cpu as O
+    from unet_hip.flops import train_flops_per_image
 
     c4 = args.config == 4
     args.batch = args.batch or (8 if c4 else 32)
@@ -195,6 +199,9 @@ def main():
         model = unet_hip.UNet(1, 1).to(dev).train()
     opt = unet_hip.HipAdamW(model.parameters(), lr=1e-5)
     ddp = DistributedUNet(model, opt) if world > 1 else None
+    for kv in args.opt:
+        name, _, val = kv.partition("=")
+        model.flatten_().rt.set_option(name, int(val))
 
     g = torch.Generator(device="cpu").manual_seed(1000 + rank)
     B, S = args.batch, args.size
@@ -204,7 +211,8 @@ def main():
     def step():
         opt.zero_grad(set_to_none=True)
         logits = model(x)
-        losses = unet_hip.seg_losses(logits, t)
+        # DP: the gathered batch's losses (nn.DataParallel semantics), gradients summed
+        losses = ddp.losses(logits, t) if ddp is not None else unet_hip.seg_losses(logits, t)
         loss = losses[0] + losses[1]
         loss.backward()
         if ddp is not None:
@@ -247,9 +255,14 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    # step boundaries as HIP events on the launch stream (the library enqueues on torch's
+    # current stream): per-step device times for the median / p90
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    evs[0].record()
+    for i in range(args.steps):
         loss = step()
+        evs[i + 1].record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -266,13 +279,16 @@ def main():
     images = B * world * args.steps
     value = images / elapsed
     ms = 1000 * elapsed / args.steps
+    step_ms = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps))
+    step_med = step_ms[len(step_ms) // 2]
+    step_p90 = step_ms[min(len(step_ms) - 1, int(0.9 * len(step_ms)))]
     _, kern_t, _ = aggregate(recs)
     prof_steps = 1
     n_l, t_l, f_l = kern_t[dom]
     achieved = f_l / (t_l * 1e-3) / 1e12 if t_l > 0 else 0.0
     per_launch_flop = f_l / n_l
     pmc = load_pmc(dom, args.config, args.mfma)
-    conv_flop = (MO.train_flops_per_image(S, S, 128, 5) if c4 else O.train_flops_per_image(S, S)) * B
+    conv_flop = (train_flops_per_image(S, S, 128, 5) if c4 else train_flops_per_image(S, S)) * B
     bf16 = c4 and args.mfma == "bf16"
     peak = BF16_MFMA_PEAK_TFLOPS if bf16 else FP32_MFMA_PEAK_TFLOPS
     roofline = {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 3),
@@ -300,7 +316,9 @@ def main():
         mname = "UNet(in=1,out=1) 31,042,369 params"
     out = {"metric": metric,
            "value": round(value, 3), "unit": "images/sec", "n_gpus": world, "steps": args.steps,
-           "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
+           "warmup": args.warmup, "ms_per_step": round(ms, 3),
+           "step_ms_median": round(step_med, 3), "step_ms_p90": round(step_p90, 3),
+           "higher_is_better": True,
            "scaling": "weak", "vs_baseline": None, "dtype": "bf16" if bf16 else "fp32",
            "data": "synthetic",
            "config": {"workload": workload, "model": mname, "global_batch": B * world,

@@ -17,9 +17,10 @@
  *                                                           running-stat BN), called from
  *                                                           utils/trainer.py:84,139,216
  *   unet_backward                   utils/trainer.py:91    loss.backward() through the UNet
- *   unet_loss_fwd                   utils/trainer.py:85-87 BCEWithLogitsLoss, models/loss.py:13-24
- *                                                           DiceLoss, models/loss.py:34-46
- *                                                           FocalTverskyLoss
+ *   unet_loss_stats / _finalize /   utils/trainer.py:85-87 BCEWithLogitsLoss, models/loss.py:13-24
+ *   unet_loss_fwd                                           DiceLoss, models/loss.py:34-46
+ *                                                           FocalTverskyLoss (two phases so DP
+ *                                                           can all-reduce the batch sums)
  *   unet_loss_bwd                   utils/trainer.py:90-91 d(weighted loss)/d(logits)
  *   unet_adamw                      utils/trainer.py:41,92 AdamW.step (torch optim/adam.py
  *                                                           _single_tensor_adam, decoupled wd)
@@ -63,7 +64,9 @@ typedef enum {
     UNET_ERR_SHAPE = -2,       /* H or W not divisible by 16, N < 1, ... */
     UNET_ERR_HIP = -3,         /* a HIP runtime call failed */
     UNET_ERR_WORKSPACE = -4,   /* workspace too small */
-    UNET_ERR_UNSUPPORTED = -5  /* configuration not implemented */
+    UNET_ERR_UNSUPPORTED = -5, /* configuration not implemented */
+    UNET_ERR_NOMEM = -6,       /* host allocation failed */
+    UNET_ERR_INTERNAL = -7     /* unexpected internal failure (caught C++ exception) */
 } unet_status;
 
 /* Which reference network the context runs. */
@@ -125,23 +128,39 @@ int unet_forward(unet_ctx* ctx, const float* params, float* bn_running, int64_t*
 int unet_backward(unet_ctx* ctx, const float* params, const float* dlogits, float* grads,
                   void* workspace, size_t ws_bytes, int N, int H, int W, unet_stream_t stream);
 
-/* Losses over logits/targets (N, C, H, W) (targets may be soft, e.g. mixup).
- * stats: device fp32[4*N + 8] scratch the caller keeps for unet_loss_bwd.
- * losses: device fp32[3] <- {bce_mean, dice_loss, focal_tversky_loss}.
+/* Losses over logits/targets (N, C, H, W) (targets may be soft, e.g. mixup), in two
+ * phases so that data parallelism can insert one collective between them:
+ *   unet_loss_stats     per-sample partials stats (device fp32[4*N]) and the batch sums
+ *                       sums (device fp64[8]) = {sum bce_elem, sum_n dice_n, TP, sum p,
+ *                       sum t, samples, elements, 0}
+ *   [DP: all-reduce(SUM) sums across ranks -- the loss of the gathered batch, exactly
+ *        what nn.DataParallel evaluates (utils/trainer.py:28-30,85-90); FocalTversky's
+ *        TP/FP/FN are batch-global (models/loss.py:41-45)]
+ *   unet_loss_finalize  losses (device fp32[3]) <- {bce_mean, dice_loss, focal_tversky}
+ * unet_loss_fwd = unet_loss_stats + unet_loss_finalize (single process).
  * focal uses (alpha, beta, gamma) of utils/trainer.py:38 / models/loss.py:27 defaults. */
+int unet_loss_stats(unet_ctx* ctx, const float* logits, const float* targets, int N, int C, int H,
+                    int W, float* stats, double* sums, unet_stream_t stream);
+int unet_loss_finalize(unet_ctx* ctx, const double* sums, float* losses, float focal_alpha,
+                       float focal_beta, float focal_gamma, unet_stream_t stream);
 int unet_loss_fwd(unet_ctx* ctx, const float* logits, const float* targets, int N, int C, int H,
-                  int W, float* stats, float* losses, float focal_alpha, float focal_beta,
-                  float focal_gamma, unet_stream_t stream);
-/* dlogits = w[0]*dBCE + w[1]*dDice + w[2]*dFocal, w a device fp32[3]. */
-int unet_loss_bwd(unet_ctx* ctx, const float* logits, const float* targets, int N, int C, int H,
-                  int W, const float* stats, const float* w, float* dlogits, float focal_alpha,
+                  int W, float* stats, double* sums, float* losses, float focal_alpha,
                   float focal_beta, float focal_gamma, unet_stream_t stream);
+/* dlogits = w[0]*dBCE + w[1]*dDice + w[2]*dFocal of the batch described by `sums`
+ * (w a device fp32[3]).  With all-reduced sums each rank writes its slice of the
+ * gathered batch's dlogits, so the ranks' gradients SUM to the reference's. */
+int unet_loss_bwd(unet_ctx* ctx, const float* logits, const float* targets, int N, int C, int H,
+                  int W, const float* stats, const double* sums, const float* w, float* dlogits,
+                  float focal_alpha, float focal_beta, float focal_gamma, unet_stream_t stream);
 
-/* AdamW over flat arenas of n floats (one launch for all 82 tensors).
- * grads are multiplied by grad_scale first (1/world_size after an RCCL sum). */
+/* AdamW over flat arenas of n floats (one launch for all parameter tensors).
+ * Hyper-parameters are the optimizer's Python floats (double); the library forms
+ * 1 - lr*wd, 1 - beta1, 1 - beta2, -lr/(1 - beta1^step) and (1 - beta2^step)**0.5 in
+ * double and rounds each to float once, as torch does (optim/adam.py _single_tensor_adam).
+ * grads are multiplied by grad_scale first when it is not 1. */
 int unet_adamw(unet_ctx* ctx, float* params, const float* grads, float* exp_avg,
-               float* exp_avg_sq, int64_t n, int step, float lr, float beta1, float beta2,
-               float eps, float weight_decay, float grad_scale, unet_stream_t stream);
+               float* exp_avg_sq, int64_t n, int step, double lr, double beta1, double beta2,
+               double eps, double weight_decay, double grad_scale, unet_stream_t stream);
 
 /* Mask readout + confusion counts, utils/trainer.py:101-107,217-242, utils/utils.py:225-251.
  * counts (device int64[6]) += {TP, FP, FN, TN} of (sigmoid(logits) > 0.5) vs targets cast to
@@ -171,6 +190,18 @@ int unet_resize_plan(int in_size, int out_size, int32_t* coeffs, int32_t* bounds
 int unet_resize_u8(unet_ctx* ctx, const uint8_t* src, int h, int w, float* dst, int oh, int ow,
                    const int32_t* kh, const int32_t* bh, int ksh, const int32_t* kv,
                    const int32_t* bv, int ksv, float divisor, unet_stream_t stream);
+
+/* Kernel-schedule options of a context (new; no reference counterpart).  The defaults are
+ * the measured-best schedules; the named alternatives (tiles, LDS-DMA vs register-staged
+ * bf16 kernels, XCD block order, a weight-gradient stream, ...) exist for A/B runs and
+ * tests.  The library never reads the environment: an option changes only when set here.
+ * Names: wgrad_row3, wgrad_row3_tile, wgrad_tile_w, wgrad_tile_n, wgrad16_tile, tile_n128,
+ * tile_n128_dgrad, tile_n64, tile16_n128, tile16_n128_dgrad, tile16_n64, rg16, rg16_tile,
+ * wg16, wg16_tile, wg16t, xcd16, xcd_remap, wgrad_stream, dz_in_loaders
+ * (runtime.hip: struct Options).  Set them between steps, not between a forward and its
+ * backward (the workspace plan depends on some of them). */
+int unet_set_option(unet_ctx* ctx, const char* name, int64_t value);
+int unet_get_option(const unet_ctx* ctx, const char* name, int64_t* value);
 
 /* Per-kernel timing: when enabled, unet_forward/unet_backward bracket every launch with
  * HIP events; unet_timing_read synchronises and returns, per kernel family, the launch

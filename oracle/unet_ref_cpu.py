@@ -9,8 +9,9 @@ Follows, op for op and in the same order:
   conv (``:28-31``).
 * ``nn.BatchNorm2d`` train semantics (eps 1e-5, momentum 0.1, biased batch var for
   normalisation, unbiased for running_var, ``num_batches_tracked += 1``).
-* ``utils/trainer.py:37,85`` ``nn.BCEWithLogitsLoss()`` (mean) and
-  ``models/loss.py:7-24`` ``DiceLoss`` (per-sample soft dice, smooth 1).
+* ``utils/trainer.py:37,85`` ``nn.BCEWithLogitsLoss()`` (mean),
+  ``models/loss.py:7-24`` ``DiceLoss`` (per-sample soft dice, smooth 1) and
+  ``models/loss.py:26-46`` ``FocalTverskyLoss`` (batch-global TP/FP/FN).
 * ``utils/trainer.py:90`` weighted loss sum; ``:81-93`` zero_grad/backward/step.
 * ``utils/trainer.py:41`` ``AdamW(lr)`` with torch defaults betas (0.9, 0.999),
   eps 1e-8, weight_decay 1e-2, restated as torch's ``_single_tensor_adam``.
@@ -171,6 +172,19 @@ def dice_loss(logits, targets, smooth=1.0):
     return 1 - dice.mean()
 
 
+def focal_tversky(logits, targets, alpha=0.4, beta=0.6, gamma=2.0, smooth=1e-6):
+    # models/loss.py:26-46 FocalTverskyLoss (defaults as utils/trainer.py:38): TP/FP/FN over
+    # the WHOLE batch (flattened), ti = (TP+s)/(TP + a FP + b FN + s), loss = (1-ti)^gamma
+    probs = torch.sigmoid(logits)
+    probs_flat = probs.view(-1)
+    targets_flat = targets.view(-1)
+    TP = (probs_flat * targets_flat).sum()
+    FP = ((probs_flat) * (1 - targets_flat)).sum()
+    FN = ((1 - probs_flat) * targets_flat).sum()
+    ti = (TP + smooth) / (TP + alpha * FP + beta * FN + smooth)
+    return (1 - ti) ** gamma
+
+
 def mask_readout(logits):
     # utils/trainer.py:101,217
     return (torch.sigmoid(logits) > 0.5).to(torch.uint8)
@@ -203,13 +217,16 @@ class AdamWState:
                 p.addcdiv_(self.m[k], denom, value=-step_size)
 
 
-def train_step(P, B, opt, x, t, w_bce=1.0, w_dice=1.0, shards=1, forward_fn=None):
+def train_step(P, B, opt, x, t, w_bce=1.0, w_dice=1.0, shards=1, forward_fn=None, w_focal=0.0,
+               focal_abg=(0.4, 0.6, 2.0)):
     """utils/trainer.py:81-93 for one batch.  ``shards`` > 1 emulates nn.DataParallel
-    (utils/trainer.py:28-30): the batch is split on dim 0, every shard runs its own
+    (utils/trainer.py:28-30): the batch is split on dim 0 with torch.chunk (DataParallel's
+    scatter; B=3 over 2 replicas gives shards of 2 and 1), every shard runs its own
     train-mode BN, logits are gathered and the loss is taken on the full batch.
     (Only shard 0's running stats are kept, as DP keeps replica 0's.)
-    ``forward_fn`` replaces models/model.py's graph (e.g. mod_ref_cpu.make_forward).
-    Returns dict(logits, loss, bce, dice, grads)."""
+    Loss = w_bce*BCE + w_dice*Dice + w_focal*FocalTversky (utils/trainer.py:90; the CLI
+    defaults main.py:43-46 are 1/0/1/0).  ``forward_fn`` replaces models/model.py's graph
+    (e.g. mod_ref_cpu.make_forward).  Returns dict(logits, loss, bce, dice, focal, grads)."""
     fwd = forward if forward_fn is None else forward_fn
     Pg = {k: v.detach().clone().requires_grad_(True) for k, v in P.items()}
     if shards == 1:
@@ -222,13 +239,16 @@ def train_step(P, B, opt, x, t, w_bce=1.0, w_dice=1.0, shards=1, forward_fn=None
         logits = torch.cat(outs, 0)
     bce = bce_with_logits(logits, t)
     dice = dice_loss(logits, t)
+    focal = focal_tversky(logits, t, *focal_abg)
     loss = w_bce * bce + w_dice * dice
+    if w_focal != 0:
+        loss = loss + w_focal * focal
     loss.backward()
     grads = {k: v.grad.detach().clone() for k, v in Pg.items()}
     if opt is not None:
         opt.step(P, grads)
     return dict(logits=logits.detach(), loss=loss.detach(), bce=bce.detach(),
-                dice=dice.detach(), grads=grads)
+                dice=dice.detach(), focal=focal.detach(), grads=grads)
 
 
 # ---- analytic FLOP count -------------------------------------------------

@@ -61,3 +61,58 @@ def hip_mod_model(P, dev, base, depth, buffers=None):
         sd[k] = v.clone()
     m.load_state_dict(sd)
     return m.to(dev).train()
+
+
+def check_eval(m, forward_fn, x, t, tol=1e-4):
+    """Resync the oracle from m's parameters AND running buffers and compare eval-mode
+    (running-stat BN) logits at the north-star bar, the test masks (utils/trainer.py:217
+    sigmoid > 0.5, bit-exact outside the forward error band) and the confusion counts of
+    unet_mask_counts vs the reference's counting (utils/trainer.py:219-242: targets
+    astype(uint8), TP/FP/FN/TN over every pixel).  Returns the near-boundary mask flips."""
+    dev = next(m.parameters()).device
+    Pc = {k: v.detach().cpu().clone() for k, v in m.named_parameters()}
+    Bc = {k: v.detach().cpu().clone() for k, v in m.named_buffers()}
+    m.eval()
+    with torch.no_grad():
+        lg = m(x.to(dev))
+        ref = forward_fn(x, Pc, Bc, False)
+    m.train()
+    rl = ref.numpy()
+    e = rel_max(lg.cpu().numpy(), rl)
+    assert e <= tol, f"eval logits {e:.2e}"
+    rt = m.flatten_().rt
+    counts = torch.zeros(6, dtype=torch.int64, device=dev)
+    mask = torch.empty(lg.shape, dtype=torch.uint8, device=dev)
+    rt.mask_counts(lg, t.to(dev), counts, mask)
+    ref_mask = O.mask_readout(ref).numpy()
+    ok, nd = masks_agree(mask.cpu().numpy(), ref_mask, rl, 10 * tol * np.abs(rl).max())
+    assert ok, f"{nd} eval mask bits differ away from the decision boundary"
+    tg = t.numpy().astype(np.uint8)
+    pr = mask.cpu().numpy().astype(bool)
+    want = [int((pr & (tg == 1)).sum()), int((pr & (tg == 0)).sum()),
+            int((~pr & (tg == 1)).sum()), int((~pr & (tg == 0)).sum())]
+    assert counts.cpu().tolist()[:4] == want
+    rp = ref_mask.astype(bool)  # vs the oracle's masks: only near-boundary pixels move
+    ref_counts = [int((rp & (tg == 1)).sum()), int((rp & (tg == 0)).sum()),
+                  int((~rp & (tg == 1)).sum()), int((~rp & (tg == 0)).sum())]
+    assert sum(abs(a - b) for a, b in zip(want, ref_counts)) <= 2 * nd
+    return nd
+
+
+class options:
+    """Set native kernel-schedule options (unet_set_option) for a block, restoring the
+    previous values after it: runtimes are cached per device and network configuration."""
+
+    def __init__(self, rt, **kv):
+        self.rt, self.kv, self.old = rt, kv, {}
+
+    def __enter__(self):
+        for k, v in self.kv.items():
+            self.old[k] = self.rt.get_option(k)
+            self.rt.set_option(k, v)
+        return self.rt
+
+    def __exit__(self, *exc):
+        for k, v in self.old.items():
+            self.rt.set_option(k, v)
+        return False

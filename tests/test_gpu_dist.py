@@ -1,10 +1,13 @@
 """The data-parallel product path on a real GPU: two ranks (gloo, both on cuda:0 -- the
 pool's boxes have one GPU, and RCCL refuses two ranks on one device) run the HIP UNet
 through ``unet_hip.dist.DistributedUNet``: parameters broadcast from rank 0, per-rank
-train-mode BN on its shard, the native per-bucket events gating the side-stream
-all-reduce, the 1/world mean folded into HipAdamW.  The averaged gradients must match the
-reference's own nn.DataParallel fixture (tests/golden/unet_dp2_64.npz), and both ranks
-must hold identical parameters after the AdamW step."""
+train-mode BN on its shard (DataParallel's torch.chunk scatter), the loss of the GATHERED
+batch (``DistributedUNet.losses``: native loss statistics -> all-reduce of the 8 batch
+sums -> native finalize), the native per-bucket events gating the side-stream all-reduce
+that SUMS the gradients.  Loss values and summed gradients must match the reference's own
+nn.DataParallel fixtures -- BCE + Dice (tests/golden/unet_dp2_64.npz) and the default
+FocalTversky mix on equal and unequal shards (tests/golden/unet_dpf_64.npz) -- and both
+ranks must hold identical parameters after the AdamW step."""
 import os
 import socket
 
@@ -28,7 +31,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, seed, B, ratios, average):
     import sys
     for p in (REPO, PKG, os.path.join(REPO, "tests")):
         sys.path.insert(0, p)
@@ -45,20 +48,26 @@ def _worker(rank, world, port, q):
         # rank 1 starts from different weights: the broadcast must replace them
         m = hip_model(O.make_params(42 if rank == 0 else 7), dev)
         opt = unet_hip.HipAdamW(m.parameters(), lr=1e-5)
-        ddp = DistributedUNet(m, opt)
-        x = torch.from_numpy(Wt.make_input(3, 4, 1, 64, 64))
-        t = torch.from_numpy(Wt.make_target(3, 4, 64, 64))
+        ddp = DistributedUNet(m, opt, average=average)
+        x = torch.from_numpy(Wt.make_input(seed, B, 1, 64, 64))
+        t = torch.from_numpy(Wt.make_target(seed, B, 64, 64))
         xs, ts = torch.chunk(x, world)[rank].to(dev), torch.chunk(t, world)[rank].to(dev)
         opt.zero_grad(set_to_none=True)
         logits = ddp(xs)
-        losses = unet_hip.seg_losses(logits, ts)
-        (losses[0] + losses[1]).backward()
+        if average:  # per-rank local losses, averaged gradients
+            losses = unet_hip.seg_losses(logits, ts)
+        else:        # the gathered batch's losses, summed gradients
+            losses = ddp.losses(logits, ts)
+        loss = ratios[0] * losses[0] + ratios[1] * losses[1] + ratios[2] * losses[2]
+        loss.backward()
         scale = ddp.reduce_gradients()
         grads = m._state.grad_arena.detach().clone() * scale
         opt.step()
         params = m._state.param_arena.detach().clone()
-        loss = (losses[0] + losses[1]).detach().reshape(1).cpu()
-        dist.all_reduce(loss)
+        vals = torch.cat([losses.detach().double(), loss.detach().double().reshape(1)]).cpu()
+        if average:
+            dist.all_reduce(vals)
+            vals /= world
         pd = params.cpu()
         dist.broadcast(pd, src=0)
         same = bool(torch.equal(pd, params.cpu()))
@@ -66,20 +75,19 @@ def _worker(rank, world, port, q):
             rt = m._state.rt
             norms = [float(grads[off:off + int(np.prod(shape))].double().norm())
                      for name, shape, off in rt.params]
-            q.put((float(loss) / world, norms, scale, same))
+            q.put((vals.tolist(), norms, scale, same))
         else:
-            q.put(("rank1", same))
+            q.put(("rank1", vals.tolist(), same))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.timeout(600)
-def test_dp2_on_gpu_matches_dataparallel_golden(golden_dir):
-    f = np.load(os.path.join(golden_dir, "unet_dp2_64.npz"), allow_pickle=False)
+def _run(seed, B, ratios, average):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, seed, B, ratios, average))
+             for r in range(2)]
     for p in procs:
         p.start()
     res = [q.get(timeout=500), q.get(timeout=500)]
@@ -88,8 +96,35 @@ def test_dp2_on_gpu_matches_dataparallel_golden(golden_dir):
         assert p.exitcode == 0
     r0 = [r for r in res if r[0] != "rank1"][0]
     r1 = [r for r in res if r[0] == "rank1"][0]
-    loss, norms, scale, same0 = r0
-    assert scale == 0.5
-    assert same0 and r1[1], "ranks diverged after the AdamW step"
-    assert abs(loss - float(f["loss"])) < 1e-5
-    np.testing.assert_allclose(norms, f["grad_norm"], rtol=1e-2)
+    return r0, r1
+
+
+@pytest.mark.timeout(600)
+def test_dp2_on_gpu_matches_dataparallel_golden(golden_dir):
+    """BCE + Dice, equal shards, both DP modes: the gathered-batch loss with summed
+    gradients (default) and per-rank local losses with averaged gradients."""
+    f = np.load(os.path.join(golden_dir, "unet_dp2_64.npz"), allow_pickle=False)
+    for average in (False, True):
+        (vals, norms, scale, same0), r1 = _run(3, 4, (1.0, 1.0, 0.0), average)
+        assert scale == (0.5 if average else 1.0)
+        assert same0 and r1[2], "ranks diverged after the AdamW step"
+        assert abs(vals[3] - float(f["loss"])) < 1e-5, (average, vals[3], float(f["loss"]))
+        if not average:
+            assert vals == r1[1], "ranks disagree on the gathered-batch loss"
+        np.testing.assert_allclose(norms, f["grad_norm"], rtol=1e-2)
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("tag,B,seed", [("eq_", 4, 22), ("uneq_", 3, 23)])
+def test_dp2_focal_on_gpu_matches_dataparallel_golden(golden_dir, tag, B, seed):
+    """FocalTversky in the DP loss (global TP/FP/FN of the gathered batch): the CLI default
+    ratios on equal shards, 1/1/1 on DataParallel's unequal scatter (3 -> 2 + 1)."""
+    f = np.load(os.path.join(golden_dir, "unet_dpf_64.npz"), allow_pickle=False)
+    ratios = tuple(float(v) for v in f[tag + "ratios"])
+    (vals, norms, scale, same0), r1 = _run(seed, B, ratios, False)
+    assert scale == 1.0
+    assert same0 and r1[2], "ranks diverged after the AdamW step"
+    assert vals == r1[1], "ranks disagree on the gathered-batch loss"
+    for v, k in zip(vals, ("bce", "dice", "focal", "loss")):
+        assert abs(v - float(f[tag + k])) < 1e-5, (k, v, float(f[tag + k]))
+    np.testing.assert_allclose(norms, f[tag + "grad_norm"], rtol=1e-2)

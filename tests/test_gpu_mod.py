@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 import torch
 
-from _helpers import grad_errors, hip_mod_model, inputs, masks_agree, norm_rel, rel_max
+from _helpers import check_eval, options, grad_errors, hip_mod_model, inputs, masks_agree, norm_rel, rel_max
 from oracle import mod_ref_cpu as MO
 from oracle import weights as Wt
 
@@ -90,10 +90,9 @@ def test_mod_train_steps_match_golden(golden_dir, tag, seed, lo, hi):
         rm = torch.cat([sd[f"{n}.running_mean"].cpu() for n in names]).numpy()
         btol = 1e-4 if s == 0 else 1e-3
         np.testing.assert_allclose(rm, f[p + "running_mean"], rtol=btol, atol=btol)
-    m.eval()
-    with torch.no_grad():
-        ev = m(x).cpu().numpy()
-    assert rel_max(ev, f[tag + "eval_logits"]) <= 2e-3
+    # eval mode (Trainer.validate / test, utils/trainer.py:130,206-250): the oracle resynced
+    # from this path's parameters and running statistics, at the north-star bar
+    check_eval(m, MO.make_forward(3), x.cpu(), t.cpu())
 
 
 def test_mod_full_grads_vs_oracle():
@@ -190,49 +189,77 @@ def _to64(d):
     return {k: (v.double() if v.is_floating_point() else v.clone()) for k, v in d.items()}
 
 
-@pytest.mark.parametrize("tile,wtile", [("0", "0"), ("1", "1"), ("3", "0"), ("0", "2"), ("8", "0"), ("11", "0"),
-                                       ("0", "3"), ("0", "4")])
-def test_rg16_bit_identical_to_register_staged(tile, wtile, monkeypatch):
+def _bf16_model(P, base, depth):
+    import unet_hip
+    m = unet_hip.ModUNet(1, 1, base_filters=base, depth=depth, mfma_dtype="bf16")
+    sd = m.state_dict()
+    for k, v in P.items():
+        sd[k] = v.clone()
+    m.load_state_dict(sd)
+    return m.to(DEV).train()
+
+
+def _bf16_step(m, x, t):
+    import unet_hip
+    logits = m(x.to(DEV))
+    losses = unet_hip.seg_losses(logits, t.to(DEV))
+    (losses[0] + losses[1]).backward()
+    torch.cuda.synchronize()
+    return (logits.detach().clone(),
+            {k: p.grad.detach().clone() for k, p in m.named_parameters()},
+            {k: b.detach().clone() for k, b in m.named_buffers()})
+
+
+def _assert_same(a, b, what):
+    assert torch.equal(a[0], b[0]), f"{what}: logits"
+    for k, g0 in a[1].items():
+        assert torch.equal(g0, b[1][k]), f"{what}: grad {k}"
+    for k, b0 in a[2].items():
+        assert torch.equal(b0, b[2][k]), f"{what}: buffer {k}"
+
+
+@pytest.mark.parametrize("tile,wtile", [(0, 0), (1, 1), (3, 0), (0, 2), (8, 0), (11, 0),
+                                        (0, 3), (0, 4), (2, 2), (4, 2)])
+def test_rg16_bit_identical_to_register_staged(tile, wtile):
     """The LDS-DMA bf16 GEMMs (kernels_gemm16.hip, fed by the k_to_bf16 operand images:
     row GEMMs and the transposed-read weight gradients) against the register-staged bf16
-    kernels (UNET_RG16=0, UNET_WG16=0) on a base-128 network, where every GEMM but the
+    kernels (options rg16 = wg16 = 0) on a base-128 network, where every GEMM but the
     Cin = 1 first conv takes the new path: the same bf16 roundings of the same f32 values,
-    the same K order, split-K partition and 128-row BN partials, so one training step gives
-    bit-identical logits, gradients and BN statistics for every 128-row tile (and every
-    weight-gradient tile: those have no BN partials)."""
-    import unet_hip
+    the same K order, split-K partition and 128-row BN partial groups, so one training step
+    gives bit-identical logits, gradients and BN statistics for every row tile (256-row
+    tiles included) and every weight-gradient tile."""
     x, t = inputs(23, 2, 128, 128)
     P = MO.make_params(9, 128, 3)
     outs = []
-    for flag in ("0", "1"):
-        monkeypatch.setenv("UNET_RG16", flag)
-        monkeypatch.setenv("UNET_WG16", flag)
-        monkeypatch.setenv("UNET_RG16_TILE", tile)
-        monkeypatch.setenv("UNET_WG16_TILE", wtile)
-        m = unet_hip.ModUNet(1, 1, base_filters=128, depth=3, mfma_dtype="bf16")
-        sd = m.state_dict()
-        for k, v in P.items():
-            sd[k] = v.clone()
-        m.load_state_dict(sd)
-        m = m.to(DEV).train()
-        logits = m(x.to(DEV))
-        losses = unet_hip.seg_losses(logits, t.to(DEV))
-        (losses[0] + losses[1]).backward()
-        torch.cuda.synchronize()
-        outs.append((logits.detach().clone(),
-                     {k: p.grad.detach().clone() for k, p in m.named_parameters()},
-                     {k: b.detach().clone() for k, b in m.named_buffers()}))
-    assert torch.equal(outs[0][0], outs[1][0])
-    for k, g0 in outs[0][1].items():
-        assert torch.equal(g0, outs[1][1][k]), k
-    for k, b0 in outs[0][2].items():
-        assert torch.equal(b0, outs[1][2][k]), k
+    for flag in (0, 1):
+        m = _bf16_model(P, 128, 3)
+        with options(m.flatten_().rt, rg16=flag, wg16=flag, rg16_tile=tile, wg16_tile=wtile):
+            outs.append(_bf16_step(m, x, t))
+    _assert_same(outs[0], outs[1], f"tile {tile}/{wtile}")
+
+
+@pytest.mark.parametrize("side", [128, 512])
+def test_rg16_tile_choice_is_numerically_invisible(side):
+    """BASELINE config 4's network (mod.py UNet(128, 5), bf16 MFMA), bs 2: the row-GEMM tile
+    (0 = 128x128, 2 = 256x128, 4 = 256x256, auto = the runtime's per-GEMM choice) changes
+    speed only -- one training step is bit-identical across all of them (BN partials in
+    fixed 128-row groups, gemm_common.h row_epilogue)."""
+    x, t = inputs(29, 2, side, side)
+    P = MO.make_params(31, 128, 5)
+    outs = {}
+    for tile in (0, 2, 4, -1):
+        m = _bf16_model(P, 128, 5)
+        with options(m.flatten_().rt, rg16_tile=tile):
+            outs[tile] = _bf16_step(m, x, t)
+        del m
+    for tile in (2, 4, -1):
+        _assert_same(outs[0], outs[tile], f"{side}^2 tile {tile} vs 0")
 
 
 @pytest.mark.parametrize("base,depth,tile", [(64, 3, "4"), (128, 5, "0"), (128, 5, "2"), (128, 5, "4"),
                                              (128, 5, "6"), (128, 5, "7"),
                                              (128, 5, "9"), (128, 5, "10"), (128, 5, "auto")])
-def test_mod_bf16_matches_bf16_oracle(base, depth, tile, monkeypatch):
+def test_mod_bf16_matches_bf16_oracle(base, depth, tile):
     """mfma_dtype="bf16": one step at B=2 64x64 vs the oracle that rounds exactly the GEMM
     operands the HIP bf16 kernels round (oracle/mod_ref_cpu.py, bf16=True).
 
@@ -241,17 +268,12 @@ def test_mod_bf16_matches_bf16_oracle(base, depth, tile, monkeypatch):
     BN.  The oracle itself shows it: evaluated in fp32 and in fp64 (same bf16 roundings of
     its own values) it differs by ~6e-3 in the logits and up to ~15 % on small BN-bias
     gradients.  The bar is 2x that spread of the oracle against itself.  tile = the
-    LDS-DMA GEMM tile (UNET_RG16_TILE; "2" = 256 rows x 8 waves, "4" = 256 x 256, the
-    default: BN partials grouped by 256 rows, so the bf16 roundings differ from the
-    128-row tiles'), with the 256x256 weight-gradient tile on the 256-channel layers;
-    "auto" = the runtime's per-GEMM choice (rg16_tile, runtime.hip) and default wgrad tile."""
+    LDS-DMA GEMM tile (option rg16_tile; "2" = 256 rows x 8 waves, "4" = 256 x 256), with
+    the 256x256 weight-gradient tile on the 256-channel layers; "auto" = the runtime's
+    per-GEMM choice (rg16_tile, runtime.hip) and default wgrad tile."""
     import unet_hip
-    if tile == "auto":
-        monkeypatch.delenv("UNET_RG16_TILE", raising=False)
-        monkeypatch.delenv("UNET_WG16_TILE", raising=False)
-    else:
-        monkeypatch.setenv("UNET_RG16_TILE", tile)
-        monkeypatch.setenv("UNET_WG16_TILE", "2" if tile in ("4", "6", "7", "9", "10") else "0")
+    opts = {} if tile == "auto" else dict(
+        rg16_tile=int(tile), wg16_tile=2 if tile in ("4", "6", "7", "9", "10") else 0)
     P = MO.make_params(42, base, depth)
     x, t = inputs(5, 2, 64, 64)
     ref = MO.train_step(P, MO.init_buffers(base, depth), None, x, t, depth=depth, bf16=True)
@@ -264,9 +286,11 @@ def test_mod_bf16_matches_bf16_oracle(base, depth, tile, monkeypatch):
         sd[k] = v.clone()
     m.load_state_dict(sd)
     m = m.to(DEV).train()
-    logits = m(x.to(DEV))
-    losses = unet_hip.seg_losses(logits, t.to(DEV))
-    (losses[0] + losses[1]).backward()
+    with options(m.flatten_().rt, **opts):
+        logits = m(x.to(DEV))
+        losses = unet_hip.seg_losses(logits, t.to(DEV))
+        (losses[0] + losses[1]).backward()
+        torch.cuda.synchronize()
     lg = logits.detach().cpu().numpy()
     spread_l = rel_max(ref["logits"].numpy(), r64["logits"].numpy())
     e_l = rel_max(lg, ref["logits"].numpy())

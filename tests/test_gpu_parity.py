@@ -16,7 +16,7 @@ import numpy as np
 import pytest
 import torch
 
-from _helpers import grad_errors, hip_model, inputs, masks_agree, norm_rel, rel_max
+from _helpers import check_eval, grad_errors, hip_model, inputs, masks_agree, norm_rel, rel_max
 from oracle import unet_ref_cpu as O
 from oracle import weights as Wt
 
@@ -125,10 +125,9 @@ def test_train_steps_match_golden(golden_dir):
         np.testing.assert_allclose(rv, f[f"s{s}_running_var"], rtol=btol, atol=btol)
         nbt = [int(m.state_dict()[f"{n}.num_batches_tracked"]) for n in O.BN_LAYERS]
         assert nbt == list(f[f"s{s}_nbt"])
-    m.eval()
-    with torch.no_grad():
-        ev = m(x).cpu().numpy()
-    assert rel_max(ev, f["eval_logits"]) <= 2e-3
+    # eval mode (Trainer.validate / test): the oracle resynced from this path's parameters
+    # and running statistics, at the north-star bar
+    check_eval(m, O.forward, x.cpu(), t.cpu())
 
 
 def _to64(d):
@@ -273,6 +272,151 @@ def test_adamw_vs_torch():
     assert torch.max(torch.abs(pa - pb)).item() <= 1e-6
 
 
+class _IeeeSqrtAdamW(O.AdamWState):
+    """The oracle's AdamW (torch's CPU ops, op for op) with a correctly rounded sqrt: this
+    host's vectorised torch.sqrt is 1 ulp low on ~0.7 % of fp32 inputs (measured against
+    IEEE sqrt; a host-library property, not part of the algorithm)."""
+
+    def step(self, params, grads):
+        import math
+        self.step_count += 1
+        b1, b2 = self.betas
+        bc1 = 1 - b1 ** self.step_count
+        bc2 = 1 - b2 ** self.step_count
+        step_size = self.lr / bc1
+        bc2_sqrt = math.sqrt(bc2)
+        with torch.no_grad():
+            for k, p in params.items():
+                g = grads[k]
+                p.mul_(1 - self.lr * self.wd)
+                self.m[k].lerp_(g, 1 - b1)
+                self.v[k].mul_(b2).addcmul_(g, g, value=1 - b2)
+                sq = torch.from_numpy(np.sqrt(self.v[k].numpy()))
+                denom = (sq / bc2_sqrt).add_(self.eps)
+                p.addcdiv_(self.m[k], denom, value=-step_size)
+
+
+@pytest.mark.parametrize("lr,wd,betas", [(1e-5, 1e-2, (0.9, 0.999)), (1e-3, 1e-2, (0.9, 0.999)),
+                                         (3e-4, 0.1, (0.8, 0.99)), (1e-3, 0.0, (0.3, 0.9))])
+def test_adamw_bitwise_vs_oracle(lr, wd, betas):
+    """The native AdamW vs the oracle's (torch's _single_tensor_adam CPU ops, utils/
+    trainer.py:41,92) from IDENTICAL p, g, m, v at every one of 4 steps, over a flat arena
+    of 2^20 + 3 floats (16-B-vectorised kernel on the aligned body).
+
+    * exp_avg and exp_avg_sq: bit-identical on every element;
+    * params: bit-identical to the oracle's op sequence with a correctly rounded sqrt
+      (_IeeeSqrtAdamW) on every element, and within 1 ulp of the pure-torch oracle, whose
+      only differences are the elements where the host's sqrt is not correctly rounded."""
+    import unet_hip
+    n = (1 << 20) + 3
+    gen = torch.Generator().manual_seed(int(lr * 1e6) + int(wd * 100))
+    p = (torch.randn(n, generator=gen) * 0.05).float()
+    ref = O.AdamWState({"a": p.clone()}, lr=lr, betas=betas, weight_decay=wd)
+    ieee = _IeeeSqrtAdamW({"a": p.clone()}, lr=lr, betas=betas, weight_decay=wd)
+    pd = torch.nn.Parameter(p.clone().to(DEV))
+    opt = unet_hip.HipAdamW([pd], lr=lr, betas=betas, weight_decay=wd)
+    for s in range(4):
+        scale = 10.0 ** torch.empty(n).uniform_(-7, -1, generator=gen)
+        g = torch.randn(n, generator=gen) * scale
+        # identical state going in: the device copy of the oracle's p, m, v
+        P_ref, P_ieee = {"a": p.clone()}, {"a": p.clone()}
+        ref.m["a"], ref.v["a"] = ieee.m["a"].clone(), ieee.v["a"].clone()
+        ref.step_count = ieee.step_count
+        m_in, v_in = ieee.m["a"].clone(), ieee.v["a"].clone()
+        with torch.no_grad():
+            pd.copy_(p.to(DEV))
+        if s:
+            opt.state[pd]["exp_avg"].copy_(m_in.to(DEV))
+            opt.state[pd]["exp_avg_sq"].copy_(v_in.to(DEV))
+        pd.grad = g.to(DEV)
+        ref.step(P_ref, {"a": g})
+        ieee.step(P_ieee, {"a": g})
+        opt.step()
+        torch.cuda.synchronize()
+        got_p = pd.detach().cpu()
+        got_m = opt.state[pd]["exp_avg"].cpu()
+        got_v = opt.state[pd]["exp_avg_sq"].cpu()
+        assert torch.equal(got_m, ref.m["a"]), f"step {s}: exp_avg differs"
+        assert torch.equal(got_v, ref.v["a"]), f"step {s}: exp_avg_sq differs"
+        assert torch.equal(got_p, P_ieee["a"]), \
+            f"step {s}: {(got_p != P_ieee['a']).sum().item()} params differ from the IEEE-sqrt oracle"
+        diff = got_p != P_ref["a"]
+        ulp = (got_p.view(torch.int32).long() - P_ref["a"].view(torch.int32).long()).abs()
+        assert int(ulp.max()) <= 1, f"step {s}: {int(ulp.max())} ulp"
+        v = ref.v["a"]
+        host_sqrt_off = torch.sqrt(v) != torch.from_numpy(np.sqrt(v.numpy()))
+        assert bool(torch.all(host_sqrt_off[diff])), "a difference not explained by the host sqrt"
+        print(f"step {s}: {int(diff.sum())} of {n} params 1 ulp off the torch-CPU oracle "
+              f"(host sqrt inexact on {int(host_sqrt_off.sum())})")
+        p = P_ieee["a"]
+
+
+def _focal_step(m, opt, x, t):
+    import unet_hip
+    opt.zero_grad()
+    logits = m(x)
+    losses = unet_hip.seg_losses(logits, t)
+    loss = 1.0 * losses[0] + 0.0 * losses[1] + 1.0 * losses[2]  # main.py:43-46 defaults
+    loss.backward()
+    opt.step()
+    return logits.detach(), losses.detach(), loss.detach()
+
+
+def test_focal_default_mix_matches_golden(golden_dir):
+    """The reference CLI's default loss (BCE 1 / Dice 0 / FocalTversky 1, main.py:43-46)
+    over three training steps vs tests/golden/unet_focal_64.npz (the real
+    FocalTverskyLoss of models/loss.py:26-46).  Step 0 at the strict bars; steps 1-2 at
+    the trajectory-drift bars of test_train_steps_match_golden."""
+    import unet_hip
+    f = _golden(golden_dir, "unet_focal_64.npz")
+    m = hip_model(O.make_params(42), DEV)
+    opt = unet_hip.HipAdamW(m.parameters(), lr=1e-5)
+    x, t = torch.from_numpy(f["x"]).to(DEV), torch.from_numpy(f["t"]).to(DEV)
+    for s in range(3):
+        p = f"s{s}_"
+        logits, losses, loss = _focal_step(m, opt, x, t)
+        tol = LOGIT_TOL if s == 0 else 2e-3
+        assert rel_max(logits.cpu().numpy(), f[p + "logits"]) <= tol, f"step {s} logits"
+        ltol = 1e-5 if s == 0 else 1e-4
+        for i, k in enumerate(("bce", "dice", "focal")):
+            assert abs(losses[i].item() - float(f[p + k])) <= ltol, (s, k)
+        assert abs(loss.item() - float(f[p + "loss"])) <= ltol
+        gtol = GRAD_TOL if s == 0 else 10 * GRAD_TOL
+        norms = f[p + "grad_norm"]
+        for ti, (name, prm) in enumerate(m.named_parameters()):
+            n = prm.grad.detach().double().norm().item()
+            assert abs(n - norms[ti]) <= gtol * norms[ti], (s, name)
+
+
+def test_focal_full_grads_vs_oracle():
+    """Every gradient element with FocalTversky in the loss (weights 1/1/1) vs the oracle."""
+    P = O.make_params(42)
+    x, t = inputs(21, 2, 64, 64)
+    ref = O.train_step(P, O.init_buffers(), None, x, t, w_bce=1.0, w_dice=1.0, w_focal=1.0)
+    m = hip_model(P, DEV)
+    import unet_hip
+    logits = m(x.to(DEV))
+    losses = unet_hip.seg_losses(logits, t.to(DEV))
+    (losses[0] + losses[1] + losses[2]).backward()
+    assert abs(losses[2].item() - ref["focal"].item()) <= 1e-5
+    errs = grad_errors(m, ref["grads"])
+    worst = max(errs, key=errs.get)
+    assert errs[worst] <= GRAD_TOL, f"{worst}: {errs[worst]:.3e}"
+
+
+def test_eval_mode_parity_after_training():
+    """Trainer.test / validate path (utils/trainer.py:130,206-250): eval-mode BN from the
+    running statistics of three training steps, at 1e-4, masks and counts."""
+    import unet_hip
+    x, t = inputs(7, 4, 128, 96)
+    m = hip_model(O.make_params(42), DEV)
+    opt = unet_hip.HipAdamW(m.parameters(), lr=1e-4)
+    for _ in range(3):
+        _step(m, opt, x.to(DEV), t.to(DEV))
+    nd = check_eval(m, O.forward, x, t)
+    print(f"eval masks: {nd} near-boundary bits differ")
+
+
 def test_mask_counts():
     import unet_hip
     g = torch.Generator().manual_seed(9)
@@ -328,8 +472,8 @@ def test_determinism_full_size():
 
 
 @pytest.mark.parametrize("variant", ["model", "mod"])
-def test_wgrad_stream_bit_identical(variant, monkeypatch):
-    """UNET_WGRAD_STREAM=1 moves the weight gradients to a second stream (runtime.hip
+def test_wgrad_stream_bit_identical(variant):
+    """Option wgrad_stream=1 moves the weight gradients to a second stream (runtime.hip
     backward_impl); every kernel still sees the same inputs, so logits and the whole grad
     arena must be bit-identical to the single-stream schedule, also for the bucket-event
     path a DP run waits on."""
@@ -337,17 +481,21 @@ def test_wgrad_stream_bit_identical(variant, monkeypatch):
     from _helpers import hip_mod_model
     x, t = inputs(13, 8, 256, 256)
     outs = []
-    for flag in ("0", "1"):
-        monkeypatch.setenv("UNET_WGRAD_STREAM", flag)
+    for flag in (0, 1):
         if variant == "model":
             m = hip_model(O.make_params(42), DEV)
         else:
             from oracle import mod_ref_cpu as MO
             m = hip_mod_model(MO.make_params(5, base=64, depth=4), DEV, 64, 4)
-        logits = m(x.to(DEV))
-        l = unet_hip.seg_losses(logits, t.to(DEV))
-        (l[0] + l[1]).backward()
-        torch.cuda.synchronize()
+        rt = m.flatten_().rt
+        rt.set_option("wgrad_stream", flag)
+        try:
+            logits = m(x.to(DEV))
+            l = unet_hip.seg_losses(logits, t.to(DEV))
+            (l[0] + l[1]).backward()
+            torch.cuda.synchronize()
+        finally:
+            rt.set_option("wgrad_stream", 0)
         outs.append((logits.detach().clone(), m._state.grad_arena.clone()))
     assert torch.equal(outs[0][0], outs[1][0])
     assert torch.equal(outs[0][1], outs[1][1])
@@ -389,8 +537,8 @@ def test_shapes_and_classes_vs_oracle(out_ch, B, H, W):
 
 
 @pytest.mark.parametrize("variant", ["model", "mod"])
-def test_wgrad_row3_matches_one_tap_tiles(variant, monkeypatch):
-    """UNET_WGRAD_ROW3=1 computes every eligible 3x3 weight gradient with the
+def test_wgrad_row3_matches_one_tap_tiles(variant):
+    """Option wgrad_row3=1 computes every eligible 3x3 weight gradient with the
     one-row-of-taps kernel (kernels_gemm.hip wgrad_row3_kernel: three taps per block from
     a halo-staged input row, a different split-K partition).  Same products, different
     summation grouping: every weight / bias gradient within 1e-5 norm-relative of the
@@ -399,17 +547,21 @@ def test_wgrad_row3_matches_one_tap_tiles(variant, monkeypatch):
     from _helpers import hip_mod_model
     x, t = inputs(17, 8, 256, 256)
     outs = []
-    for flag in ("0", "1"):
-        monkeypatch.setenv("UNET_WGRAD_ROW3", flag)
+    for flag in (0, 1):
         if variant == "model":
             m = hip_model(O.make_params(42), DEV)
         else:
             from oracle import mod_ref_cpu as MO
             m = hip_mod_model(MO.make_params(5, base=64, depth=4), DEV, 64, 4)
-        logits = m(x.to(DEV))
-        l = unet_hip.seg_losses(logits, t.to(DEV))
-        (l[0] + l[1]).backward()
-        torch.cuda.synchronize()
+        rt = m.flatten_().rt
+        rt.set_option("wgrad_row3", flag)
+        try:
+            logits = m(x.to(DEV))
+            l = unet_hip.seg_losses(logits, t.to(DEV))
+            (l[0] + l[1]).backward()
+            torch.cuda.synchronize()
+        finally:
+            rt.set_option("wgrad_row3", 0)
         outs.append((logits.detach().clone(),
                      {k: p.grad.detach().clone() for k, p in m.named_parameters()}))
     assert torch.equal(outs[0][0], outs[1][0])

@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 import torch
 
-from _helpers import grad_errors, inputs, masks_agree, norm_rel, rel_max
+from _helpers import check_eval, grad_errors, inputs, masks_agree, norm_rel, rel_max
 from oracle import mod_ref_cpu as MO
 from oracle import weights as Wt
 
@@ -74,10 +74,9 @@ def test_res_train_steps_match_golden(golden_dir):
         rm = torch.cat([sd[f"{n}.running_mean"].cpu() for n in names]).numpy()
         btol = 1e-4 if s == 0 else 1e-3
         np.testing.assert_allclose(rm, f[p + "running_mean"], rtol=btol, atol=btol)
-    m.eval()
-    with torch.no_grad():
-        ev = m(x).cpu().numpy()
-    assert rel_max(ev, f["eval_logits"]) <= 2e-3
+    # eval mode (Trainer.validate / test, utils/trainer.py:130,206-250): the oracle resynced
+    # from this path's parameters and running statistics, at the north-star bar
+    check_eval(m, MO.make_res_forward(3), x.cpu(), t.cpu())
 
 
 def _to64(d):

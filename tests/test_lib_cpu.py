@@ -259,3 +259,37 @@ def test_res_tables_and_rng_like_reference():
     b = unet_hip.ResUNet(1, 1, base_filters=64, depth=3)
     for (na, pa), (nb, pb) in zip(a.state_dict().items(), b.state_dict().items()):
         assert na == nb and torch.equal(pa, pb), na
+
+
+def test_schedule_options_are_explicit(rt, monkeypatch):
+    """Kernel-schedule options live in the context (unet_set_option), never in the
+    environment: a stray UNET_* variable must not change the defaults."""
+    from unet_hip._lib import HipError
+    from unet_hip.runtime import UNetRuntime
+    monkeypatch.setenv("UNET_RG16_TILE", "3")
+    monkeypatch.setenv("UNET_WGRAD_STREAM", "1")
+    fresh = UNetRuntime("cuda:0")
+    assert fresh.get_option("rg16_tile") == -1
+    assert fresh.get_option("wgrad_stream") == 0
+    fresh.set_option("wgrad_stream", 1)
+    assert fresh.get_option("wgrad_stream") == 1
+    assert rt.get_option("wgrad_stream") == 0  # per context
+    with pytest.raises(HipError):
+        fresh.set_option("no_such_option", 1)
+    import subprocess
+    out = subprocess.run(["nm", "-D", "--undefined-only", _lib_path()], capture_output=True, text=True)
+    assert out.returncode == 0 and " getenv" not in out.stdout, "the library reads the environment"
+
+
+def _lib_path():
+    from unet_hip import _lib
+    return _lib.LIB_PATH
+
+
+def test_flop_counts_agree_with_oracle():
+    from oracle import mod_ref_cpu as MO
+    from unet_hip.flops import train_flops_per_image
+    assert train_flops_per_image(256, 256) == O.train_flops_per_image(256, 256) == 288_475_840_512
+    assert train_flops_per_image(512, 512, 128, 5) == MO.train_flops_per_image(512, 512, 128, 5)
+    for H, W, base, depth in ((64, 96, 32, 4), (128, 128, 16, 6), (96, 64, 48, 3)):
+        assert train_flops_per_image(H, W, base, depth) == MO.train_flops_per_image(H, W, base, depth)

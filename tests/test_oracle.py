@@ -196,3 +196,45 @@ def test_oracle_res_d3_two_steps(golden_dir):
     with torch.no_grad():
         ev = MO.make_res_forward(3)(x, P, B, training=False).numpy()
     assert np.max(np.abs(ev - f["eval_logits"])) <= 1e-5 * np.max(np.abs(f["eval_logits"]))
+
+
+def test_oracle_focal_default_mix_three_steps(golden_dir):
+    """The reference CLI's default loss mix (main.py:43-46: BCE 1, Dice 0, FocalTversky 1)
+    over three AdamW steps (tests/golden/unet_focal_64.npz, real FocalTverskyLoss)."""
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    f = _load(golden_dir, "unet_focal_64.npz")
+    P = O.make_params(42)
+    B = O.init_buffers()
+    opt = O.AdamWState(P, lr=1e-5)
+    x, t = torch.from_numpy(f["x"]), torch.from_numpy(f["t"])
+    np.testing.assert_array_equal(f["x"], W.make_input(21, 2, 1, 64, 64))
+    spec = O.param_spec()
+    for s in range(3):
+        p = f"s{s}_"
+        r = O.train_step(P, B, opt, x, t, w_bce=1.0, w_dice=0.0, w_focal=1.0)
+        ref = f[p + "logits"]
+        assert np.max(np.abs(r["logits"].numpy() - ref)) <= 1e-5 * np.max(np.abs(ref))
+        for k in ("bce", "dice", "focal", "loss"):
+            assert abs(r[k].item() - float(f[p + k])) < 1e-6, k
+        _check_grads(_grad_stats(r["grads"], spec), f[p + "grad_norm"], f[p + "grad_sum"],
+                     f[p + "grad_samp"], rtol=1e-4)
+        psamp = np.stack([P[it[0]].reshape(-1)[torch.from_numpy(
+            np.floor(W.uniform(7, 3000 + ti, 64) * P[it[0]].numel()).astype(np.int64))].numpy()
+            for ti, it in enumerate(spec)])
+        np.testing.assert_allclose(psamp, f[p + "params_samp"], rtol=0, atol=1e-7)
+
+
+@pytest.mark.parametrize("tag,B,seed", [("eq_", 4, 22), ("uneq_", 3, 23)])
+def test_oracle_dataparallel_focal(golden_dir, tag, B, seed):
+    """nn.DataParallel with FocalTversky: loss of the gathered logits (global TP/FP/FN),
+    equal shards and DataParallel's unequal chunked scatter (3 -> 2 + 1)."""
+    f = _load(golden_dir, "unet_dpf_64.npz")
+    wb, wd, wf = (float(v) for v in f[tag + "ratios"])
+    P = O.make_params(42)
+    x = torch.from_numpy(W.make_input(seed, B, 1, 64, 64))
+    t = torch.from_numpy(W.make_target(seed, B, 64, 64))
+    r = O.train_step(P, O.init_buffers(), None, x, t, w_bce=wb, w_dice=wd, w_focal=wf, shards=2)
+    for k in ("bce", "dice", "focal", "loss"):
+        assert abs(r[k].item() - float(f[tag + k])) < 1e-6, k
+    _check_grads(_grad_stats(r["grads"], O.param_spec()), f[tag + "grad_norm"],
+                 f[tag + "grad_sum"], f[tag + "grad_samp"], rtol=1e-4)

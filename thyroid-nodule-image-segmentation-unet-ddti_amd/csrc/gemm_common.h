@@ -85,8 +85,15 @@ __device__ __forceinline__ int gather_src(int tap, int m, Pix q, int H, int W, b
 
 // ------------------------------------------------------------------------------------
 // Row-GEMM epilogue: accumulators acc[MT][NT] of wave (wm, wn) of the BM x BN block tile at
-// (m0, n0); tile_m indexes the per-block BN partial rows; smem (>= WAVES_M * 2 * BN doubles)
-// is free scratch (the caller has finished with its LDS images).
+// (m0, n0); tile_m indexes the block row; smem (>= (BM / 64) * 2 * BN doubles) is free
+// scratch (the caller has finished with its LDS images).
+//
+// BN partials (E_BIAS_RELU_STATS / E_STATS / E_STORE_BN) are emitted per 128-ROW GROUP
+// whatever the tile: partial row tile_m * (BM / 128) + g.  Inside a group the sum runs in a
+// fixed order -- per lane over each 64-row unit's 32 rows in (mt, r) order, the two lane
+// halves combined, then unit 0 + unit 1 -- so a 128x128 tile (two 64-row waves), a 256x128
+// tile (four) and a 256x256 tile (two 128-row waves, two units each) produce bit-identical
+// partial rows, and the tile choice changes speed only (tests/test_gpu_mod.py).
 // ------------------------------------------------------------------------------------
 // PRELOAD: the epilogues that read memory (E_STORE_BN, E_RESID, E_ADD) issue all 16 loads
 // of an accumulator first -- a load under `if (m < M)` makes hipcc wait for each one before
@@ -97,17 +104,21 @@ __device__ __forceinline__ void row_epilogue(const RowGemmArgs& p, f32x16 (&acc)
                                              int m0, int n0, int tile_m, int wm, int wn,
                                              int lane, int tid, float* smem) {
     constexpr int MT = WM / 32, NT = WN / 32, WAVES_M = BM / WM;
+    constexpr int U = WM / 64;           // 64-row units per wave
+    constexpr int GB = BM / 128;         // 128-row BN groups per block
+    constexpr int THREADS = 64 * WAVES_M * (BN / WN);
+    static_assert(WM % 64 == 0 && BM % 128 == 0, "BN partial groups need 64-row units");
     const int li = lane & 31, lh = lane >> 5;
     const int H = p.H, W = p.W;
     if constexpr (EMODE == E_BIAS_RELU_STATS || EMODE == E_STATS) {
         constexpr bool BR = EMODE == E_BIAS_RELU_STATS;
-        float s1[NT], s2[NT];
+        float s1[U][NT], s2[U][NT];
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) {
             const int n = n0 + wn * WN + nt * 32 + li;
             const float b = BR ? p.bias[n] : 0.f;
-            s1[nt] = 0.f;
-            s2[nt] = 0.f;
+#pragma unroll
+            for (int u = 0; u < U; ++u) s1[u][nt] = s2[u][nt] = 0.f;
 #pragma unroll
             for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
@@ -116,44 +127,55 @@ __device__ __forceinline__ void row_epilogue(const RowGemmArgs& p, f32x16 (&acc)
                     if (m < p.M) {
                         const float v = BR ? fmaxf(acc[mt][nt][r] + b, 0.f) : acc[mt][nt][r];
                         p.out[(size_t)m * p.ldo + p.ooff + n] = v;
-                        s1[nt] += v;
-                        s2[nt] += v * v;
+                        s1[mt / 2][nt] += v;
+                        s2[mt / 2][nt] += v * v;
                     }
                 }
-            s1[nt] += __shfl_xor(s1[nt], 32);
-            s2[nt] += __shfl_xor(s2[nt], 32);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                s1[u][nt] += __shfl_xor(s1[u][nt], 32);
+                s2[u][nt] += __shfl_xor(s2[u][nt], 32);
+            }
         }
-        // combine the M-waves that share these columns (LDS is free after the loop)
+        // combine the 64-row units of each 128-row group (LDS is free after the loop)
         __syncthreads();
-        float* red = smem;  // [WAVES_M][2][BN]
+        float* red = smem;  // [BM / 64][2][BN]
         if (lh == 0) {
 #pragma unroll
-            for (int nt = 0; nt < NT; ++nt) {
-                red[(wm * 2 + 0) * BN + wn * WN + nt * 32 + li] = s1[nt];
-                red[(wm * 2 + 1) * BN + wn * WN + nt * 32 + li] = s2[nt];
-            }
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt) {
+                    const int ub = wm * U + u;
+                    red[(ub * 2 + 0) * BN + wn * WN + nt * 32 + li] = s1[u][nt];
+                    red[(ub * 2 + 1) * BN + wn * WN + nt * 32 + li] = s2[u][nt];
+                }
         }
         __syncthreads();
-        if (tid < BN) {
+        for (int i = tid; i < GB * BN; i += THREADS) {
+            const int g = i / BN, col = i - g * BN;
             float a = 0.f, q = 0.f;
 #pragma unroll
-            for (int w = 0; w < WAVES_M; ++w) {
-                a += red[(w * 2 + 0) * BN + tid];
-                q += red[(w * 2 + 1) * BN + tid];
+            for (int w = 2 * g; w < 2 * g + 2; ++w) {
+                a += red[(w * 2 + 0) * BN + col];
+                q += red[(w * 2 + 1) * BN + col];
             }
-            p.stats[(size_t)tile_m * 2 * p.N + n0 + tid] = a;
-            p.stats[(size_t)tile_m * 2 * p.N + p.N + n0 + tid] = q;
+            if (m0 + g * 128 < p.M) {
+                const size_t row = (size_t)tile_m * GB + g;
+                p.stats[row * 2 * p.N + n0 + col] = a;
+                p.stats[row * 2 * p.N + p.N + n0 + col] = q;
+            }
         }
     } else if constexpr (EMODE == E_STORE_BN) {
         // BN-backward partials are differences of nearly equal sums downstream (sum do can be
-        // 1e-3 of sum |do|): accumulate in f64, round once per block.
+        // 1e-3 of sum |do|): accumulate in f64, round once per 128-row group.
         const bool emask = p.escale != nullptr;
-        double q[NT][2];
+        double q[U][NT][2];
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) {
             const int n = n0 + wn * WN + nt * 32 + li;
             const float es = emask ? p.escale[n] : 0.f, eb = emask ? p.eshift[n] : 0.f;
-            q[nt][0] = q[nt][1] = 0.0;
+#pragma unroll
+            for (int u = 0; u < U; ++u) q[u][nt][0] = q[u][nt][1] = 0.0;
 #pragma unroll
             for (int mt = 0; mt < MT && !PRELOAD; ++mt)
 #pragma unroll
@@ -164,8 +186,8 @@ __device__ __forceinline__ void row_epilogue(const RowGemmArgs& p, f32x16 (&acc)
                         const float y = p.ey[(size_t)m * p.ldey + p.offey + n];
                         if (emask && !(es * y + eb > 0.f)) v = 0.f;
                         p.out[(size_t)m * p.ldo + p.ooff + n] = v;
-                        q[nt][0] += v;
-                        q[nt][1] += (double)v * y;
+                        q[mt / 2][nt][0] += v;
+                        q[mt / 2][nt][1] += (double)v * y;
                     }
                 }
 #pragma unroll
@@ -185,29 +207,37 @@ __device__ __forceinline__ void row_epilogue(const RowGemmArgs& p, f32x16 (&acc)
                     if (emask && !(es * y + eb > 0.f)) v = 0.f;
                     if (m < p.M) p.out[(size_t)m * p.ldo + p.ooff + n] = v;
                     v = m < p.M ? v : 0.f;
-                    q[nt][0] += v;
-                    q[nt][1] += (double)v * y;
+                    q[mt / 2][nt][0] += v;
+                    q[mt / 2][nt][1] += (double)v * y;
                 }
             }
 #pragma unroll
-            for (int j = 0; j < 2; ++j) q[nt][j] += __shfl_xor(q[nt][j], 32);
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) q[u][nt][j] += __shfl_xor(q[u][nt][j], 32);
         }
         __syncthreads();
-        double* red = (double*)smem;  // [WAVES_M][2][BN]
+        double* red = (double*)smem;  // [BM / 64][2][BN]
         if (lh == 0) {
 #pragma unroll
-            for (int nt = 0; nt < NT; ++nt)
+            for (int u = 0; u < U; ++u)
 #pragma unroll
-                for (int j = 0; j < 2; ++j) red[(wm * 2 + j) * BN + wn * WN + nt * 32 + li] = q[nt][j];
+                for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j)
+                        red[((wm * U + u) * 2 + j) * BN + wn * WN + nt * 32 + li] = q[u][nt][j];
         }
         __syncthreads();
-        if (tid < BN) {
+        for (int i = tid; i < GB * BN; i += THREADS) {
+            const int g = i / BN, col = i - g * BN;
+            if (m0 + g * 128 >= p.M) continue;
+            const size_t row = (size_t)tile_m * GB + g;
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
                 double a = 0.0;
 #pragma unroll
-                for (int w = 0; w < WAVES_M; ++w) a += red[(w * 2 + j) * BN + tid];
-                p.stats[((size_t)tile_m * 2 + j) * p.N + n0 + tid] = (float)a;
+                for (int w = 2 * g; w < 2 * g + 2; ++w) a += red[(w * 2 + j) * BN + col];
+                p.stats[(row * 2 + j) * p.N + n0 + col] = (float)a;
             }
         }
     } else if constexpr (EMODE == E_CONVT) {

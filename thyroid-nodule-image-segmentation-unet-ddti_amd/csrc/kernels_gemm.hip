@@ -76,6 +76,7 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_kernel(RowGemmArgs
     constexpr int IMG = (BM + BN) * LDK;  // elements per LDS image
     constexpr int SMEM_F = BF ? (NBUF * IMG + 1) / 2 : NBUF * IMG;
     __shared__ __attribute__((aligned(16))) float smem[SMEM_F];
+    static_assert(SMEM_F * 4 >= (BM / 64) * 2 * BN * 8, "epilogue scratch (row_epilogue)");
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave / WAVES_N, wn = wave % WAVES_N;

@@ -86,7 +86,7 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm16_kernel(RowGemmAr
     constexpr int DIST = ONEBAR ? S - 2 : S - 1;  // chunks in flight beyond the current one
     static_assert(DIST >= 1, "stages");
     constexpr int STAGE = (BM + BN) * RB;  // bytes
-    constexpr int RED = 2 * (BM / WM) * BN * 8;  // epilogue scratch (f64 partials)
+    constexpr int RED = 2 * (BM / 64) * BN * 8;  // epilogue scratch (f64 partials per 64-row unit)
     constexpr int SMEM = STAGE * S > RED ? STAGE * S : RED;
     __shared__ __attribute__((aligned(1024))) char smem[SMEM];
 

@@ -63,12 +63,28 @@ int k_res_first_wgrad(const float* x, const float* du, int P, int C, float* part
 int k_resize_u8(const uint8_t* src, int H, int W, float* dst, int OH, int OW, const int* kh,
                 const int* bh, int ksh, const int* kv, const int* bv, int ksv, int need_h,
                 int need_v, float divisor, hipStream_t s);
-int k_loss_fwd(const float* x, const float* t, int N, int64_t per, float* stats, float* losses,
-               float alpha, float beta, float gamma, hipStream_t s);
+// Losses: per-sample stats fp32[4N] + batch sums fp64[8] (see kernels_misc.hip)
+int k_loss_stats(const float* x, const float* t, int N, int64_t per, float* stats, double* sums,
+                 hipStream_t s);
+int k_loss_finalize(const double* sums, float alpha, float beta, float gamma, float* losses,
+                    hipStream_t s);
 int k_loss_bwd(const float* x, const float* t, int N, int64_t per, const float* stats,
-               const float* w, float alpha, float beta, float gamma, float* dx, hipStream_t s);
-int k_adamw(float* p, const float* g, float* m, float* v, int64_t n, float lr, float b1, float b2,
-            float eps, float wd, float step_size, float bc2_sqrt, float gscale, hipStream_t s);
+               const double* sums, const float* w, float alpha, float beta, float gamma, float* dx,
+               hipStream_t s);
+// AdamW scalars, each formed in double and rounded to float once (torch Scalar -> float)
+struct AdamwScalars {
+    float decay;     // 1 - lr * weight_decay
+    float w1;        // 1 - beta1 (lerp weight)
+    float b2;        // beta2
+    float w2;        // 1 - beta2
+    float neg_step;  // -lr / (1 - beta1^step)
+    float bc2_sqrt;  // (1 - beta2^step) ** 0.5
+    float eps;
+    float gscale;    // gradient pre-scale (1 = none)
+    int lerp_small;  // |w1| < 0.5 (ATen lerp branch)
+};
+int k_adamw(float* p, const float* g, float* m, float* v, int64_t n, const AdamwScalars& a,
+            hipStream_t s);
 int k_mask_counts(const float* x, const float* t, int64_t n, uint8_t* mask, int64_t* counts,
                   hipStream_t s);
 int k_nchw_to_nhwc(const float* x, int N, int C, int HW, float* y, hipStream_t s);

@@ -1155,42 +1155,65 @@ __global__ __launch_bounds__(1024) void loss_stats_kernel(const float* __restric
     }
 }
 
-// stats[4N + 0..] = {TP, Sp, St} globals; losses = {bce_mean, dice_loss, focal}
-__global__ void loss_finalize_kernel(float* __restrict__ stats, int N, double total, float alpha,
-                                     float beta, float gamma, float* __restrict__ losses) {
+// Batch sums of the per-sample statistics (double, fixed sample order):
+//   sums = {Σ bce_elem, Σ_n dice_n, TP = Σ I, Σ p, Σ t, samples, elements, 0}
+// These are the only cross-sample quantities of the three losses, so under data
+// parallelism an all-reduce (SUM) of `sums` turns every rank's local batch into the
+// reference's gathered batch (nn.DataParallel computes the loss on the gathered logits,
+// utils/trainer.py:28-30,85-90; FocalTversky's TP/FP/FN are global, models/loss.py:41-45).
+__global__ void loss_sums_kernel(const float* __restrict__ stats, int N, int64_t per,
+                                 double* __restrict__ sums) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     double bce = 0, dice = 0, tp = 0, sp = 0, st = 0;
     for (int n = 0; n < N; ++n) {
         const double I = stats[4 * n], P = stats[4 * n + 1], T = stats[4 * n + 2];
         bce += stats[4 * n + 3];
-        dice += (2.0 * I + 1.0) / (P + T + 1.0);
+        dice += (2.0 * I + 1.0) / (P + T + 1.0);  // models/loss.py:23, smooth = 1
         tp += I;
         sp += P;
         st += T;
     }
-    const double fp = sp - tp, fn = st - tp, sm = 1e-6;
-    const double ti = (tp + sm) / (tp + alpha * fp + beta * fn + sm);
-    stats[4 * N + 0] = (float)tp;
-    stats[4 * N + 1] = (float)sp;
-    stats[4 * N + 2] = (float)st;
-    losses[0] = (float)(bce / total);
-    losses[1] = (float)(1.0 - dice / N);
-    losses[2] = (float)pow(1.0 - ti, (double)gamma);
+    sums[0] = bce;
+    sums[1] = dice;
+    sums[2] = tp;
+    sums[3] = sp;
+    sums[4] = st;
+    sums[5] = (double)N;
+    sums[6] = (double)per * N;
+    sums[7] = 0.0;
 }
 
+// losses = {bce_mean, dice_loss, focal} of the (possibly all-reduced) batch sums
+__global__ void loss_finalize_kernel(const double* __restrict__ sums, float alpha, float beta,
+                                     float gamma, float* __restrict__ losses) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    const double tp = sums[2], fp = sums[3] - tp, fn = sums[4] - tp, sm = 1e-6;  // loss.py:41-43
+    const double ti = (tp + sm) / (tp + alpha * fp + beta * fn + sm);              // loss.py:44
+    losses[0] = (float)(sums[0] / sums[6]);
+    losses[1] = (float)(1.0 - sums[1] / sums[5]);
+    losses[2] = (float)pow(1.0 - ti, (double)gamma);                               // loss.py:45
+}
+
+// dlogits of w[0]*bce + w[1]*dice + w[2]*focal for this rank's samples; the batch
+// normalisers (elements, samples) and the focal TP/FP/FN come from `sums`, so with
+// all-reduced sums every rank writes its slice of the gathered batch's gradient and the
+// ranks' weight gradients SUM to the reference's (DataParallel's reduce-add).
 __global__ void loss_bwd_kernel(const float* __restrict__ x, const float* __restrict__ t,
                                 int64_t per, int N, const float* __restrict__ stats,
-                                const float* __restrict__ w, float alpha, float beta,
-                                float gamma, float* __restrict__ dx) {
+                                const double* __restrict__ sums, const float* __restrict__ w,
+                                float alpha, float beta, float gamma, float* __restrict__ dx) {
     const int64_t total = per * N;
     const float wb = w[0], wd = w[1], wf = w[2];
-    const float inv_total = (float)(1.0 / (double)total);
-    // focal-tversky scalars
-    const float tp = stats[4 * N], sp = stats[4 * N + 1], st = stats[4 * N + 2];
-    const float fp = sp - tp, fn = st - tp, sm = 1e-6f;
-    const float A = tp + sm, Bd = tp + alpha * fp + beta * fn + sm;
-    const float ti = A / Bd;
-    const float dLdti = (wf != 0.f) ? -gamma * powf(fmaxf(1.f - ti, 0.f), gamma - 1.f) : 0.f;
+    const float inv_total = (float)(1.0 / sums[6]);
+    const float inv_n = (float)(1.0 / sums[5]);
+    // focal-tversky scalars (models/loss.py:41-45), formed once in double
+    const double tpd = sums[2], smd = 1e-6;
+    const double Ad = tpd + smd;
+    const double Bdd = tpd + alpha * (sums[3] - tpd) + beta * (sums[4] - tpd) + smd;
+    const double tid = Ad / Bdd;
+    const float A = (float)Ad, Bd = (float)Bdd;
+    const float dLdti = (wf != 0.f) ? (float)(-gamma * pow(fmax(1.0 - tid, 0.0), gamma - 1.0)) : 0.f;
+    const float inv_B2 = (float)(1.0 / (Bdd * Bdd));
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
          i += (int64_t)gridDim.x * blockDim.x) {
         const int n = (int)(i / per);
@@ -1199,9 +1222,9 @@ __global__ void loss_bwd_kernel(const float* __restrict__ x, const float* __rest
         float g = wb * (pv - tv) * inv_total;  // d bce_mean / dx
         const float I = stats[4 * n], U = stats[4 * n + 1] + stats[4 * n + 2];
         const float dd = (2.f * tv * (U + 1.f) - (2.f * I + 1.f)) / ((U + 1.f) * (U + 1.f));
-        float gp = -wd * dd / (float)N;  // d dice_loss / dp
+        float gp = -wd * dd * inv_n;  // d dice_loss / dp
         if (wf != 0.f) {
-            const float dti = (tv * Bd - A * (tv + alpha * (1.f - tv) - beta * tv)) / (Bd * Bd);
+            const float dti = (tv * Bd - A * (tv + alpha * (1.f - tv) - beta * tv)) * inv_B2;
             gp += wf * dLdti * dti;
         }
         g += gp * pv * (1.f - pv);
@@ -1210,24 +1233,61 @@ __global__ void loss_bwd_kernel(const float* __restrict__ x, const float* __rest
 }
 
 // -------------------------------------------------------------------------------------
-// AdamW (utils/trainer.py:41,92; torch optim/adam.py _single_tensor_adam, decoupled wd).
-// Same op order as the CPU reference; __f*_rn keeps the compiler from contracting.
+// AdamW (utils/trainer.py:41,92; torch optim/adam.py _single_tensor_adam with decoupled
+// weight decay).  The element update is torch's CPU op sequence with each op rounded
+// where ATen rounds it; the scalars were formed in double on the host and rounded to
+// float once, as ATen casts a Python-float Scalar (runtime.hip: unet_adamw):
+//   param.mul_(1 - lr*wd)                      p * decay
+//   exp_avg.lerp_(grad, 1 - beta1)             ATen lerp_vec: fma(w, g - m, m) for |w| < 0.5,
+//                                              else fma(w - 1, g - m, g)
+//   exp_avg_sq.mul_(beta2)                     v * b2
+//     .addcmul_(grad, grad, value=1 - beta2)   fma(w2 * g, g, v)  (ATen's vectorised
+//                                              self + s*t1*t2, contracted by the compiler)
+//   denom = (exp_avg_sq.sqrt() / bc2_sqrt).add_(eps)
+//   param.addcdiv_(exp_avg, denom, value=-step_size)   p + (-step * m) / denom
+// Contraction is switched off so the compiler cannot fuse any other pair; sqrt and the
+// divisions are IEEE correctly rounded (HIP's default).  This matches the oracle's AdamW
+// bit for bit except where the host's vectorised sqrtf is not correctly rounded
+// (tests/test_gpu_parity.py::test_adamw_bitwise_vs_oracle).
 // -------------------------------------------------------------------------------------
+__device__ __forceinline__ void adamw_elem(float& p, float g, float& m, float& v,
+                                           const AdamwScalars& a) {
+#pragma clang fp contract(off)
+    if (a.gscale != 1.f) g = g * a.gscale;
+    p = p * a.decay;
+    const float d = g - m;
+    m = a.lerp_small ? __builtin_fmaf(a.w1, d, m) : __builtin_fmaf(a.w1 - 1.f, d, g);
+    v = v * a.b2;
+    v = __builtin_fmaf(a.w2 * g, g, v);
+    const float den = __builtin_sqrtf(v) / a.bc2_sqrt + a.eps;
+    p = p + (a.neg_step * m) / den;
+}
+
 __global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
-                             float* __restrict__ m, float* __restrict__ v, int64_t n, float lr,
-                             float b1, float b2, float eps, float wd, float step_size,
-                             float bc2_sqrt, float gscale) {
-    const float decay = 1.f - lr * wd;
-    const float w1 = 1.f - b1, w2 = 1.f - b2;
+                             float* __restrict__ m, float* __restrict__ v, int64_t n,
+                             AdamwScalars a) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * blockDim.x) {
-        const float gi = __fmul_rn(g[i], gscale);
-        float pi = __fmul_rn(p[i], decay);
-        float mi = m[i];
-        mi = __fadd_rn(mi, __fmul_rn(w1, __fsub_rn(gi, mi)));  // lerp, weight < 0.5 branch
-        float vi = __fadd_rn(__fmul_rn(v[i], b2), __fmul_rn(__fmul_rn(w2, gi), gi));
-        const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(vi), bc2_sqrt), eps);
-        pi = __fadd_rn(pi, __fmul_rn(-step_size, __fdiv_rn(mi, denom)));
+        float pi = p[i], mi = m[i], vi = v[i];
+        adamw_elem(pi, g[i], mi, vi, a);
+        p[i] = pi;
+        m[i] = mi;
+        v[i] = vi;
+    }
+}
+
+// 16-B vectorised form (same per-element code): 28 B/parameter in 7 dwordx4 accesses
+__global__ void adamw4_kernel(float4* __restrict__ p, const float4* __restrict__ g,
+                              float4* __restrict__ m, float4* __restrict__ v, int64_t n4,
+                              AdamwScalars a) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        float4 pi = p[i], mi = m[i], vi = v[i];
+        const float4 gi = g[i];
+        adamw_elem(pi.x, gi.x, mi.x, vi.x, a);
+        adamw_elem(pi.y, gi.y, mi.y, vi.y, a);
+        adamw_elem(pi.z, gi.z, mi.z, vi.z, a);
+        adamw_elem(pi.w, gi.w, mi.w, vi.w, a);
         p[i] = pi;
         m[i] = mi;
         v[i] = vi;
@@ -1489,24 +1549,34 @@ int k_head_bwd(const float* y, int C, const float* scale, const float* shift, in
                        HW, dlog, dout, partial, bnpart);
     LAUNCH_CHECK();
 }
-int k_loss_fwd(const float* x, const float* t, int N, int64_t per, float* stats, float* losses,
-               float alpha, float beta, float gamma, hipStream_t s) {
+int k_loss_stats(const float* x, const float* t, int N, int64_t per, float* stats, double* sums,
+                 hipStream_t s) {
     hipLaunchKernelGGL(loss_stats_kernel, dim3(N), dim3(1024), 0, s, x, t, per, stats);
     HIP_OK(hipGetLastError());
-    hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(64), 0, s, stats, N,
-                       (double)per * N, alpha, beta, gamma, losses);
+    hipLaunchKernelGGL(loss_sums_kernel, dim3(1), dim3(64), 0, s, stats, N, per, sums);
+    LAUNCH_CHECK();
+}
+int k_loss_finalize(const double* sums, float alpha, float beta, float gamma, float* losses,
+                    hipStream_t s) {
+    hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(64), 0, s, sums, alpha, beta, gamma,
+                       losses);
     LAUNCH_CHECK();
 }
 int k_loss_bwd(const float* x, const float* t, int N, int64_t per, const float* stats,
-               const float* w, float alpha, float beta, float gamma, float* dx, hipStream_t s) {
+               const double* sums, const float* w, float alpha, float beta, float gamma, float* dx,
+               hipStream_t s) {
     hipLaunchKernelGGL(loss_bwd_kernel, dim3(grid_for(per * N)), dim3(256), 0, s, x, t, per, N,
-                       stats, w, alpha, beta, gamma, dx);
+                       stats, sums, w, alpha, beta, gamma, dx);
     LAUNCH_CHECK();
 }
-int k_adamw(float* p, const float* g, float* m, float* v, int64_t n, float lr, float b1, float b2,
-            float eps, float wd, float step_size, float bc2_sqrt, float gscale, hipStream_t s) {
-    hipLaunchKernelGGL(adamw_kernel, dim3(grid_for(n, 256, 16384)), dim3(256), 0, s, p, g, m, v, n,
-                       lr, b1, b2, eps, wd, step_size, bc2_sqrt, gscale);
+int k_adamw(float* p, const float* g, float* m, float* v, int64_t n, const AdamwScalars& a,
+            hipStream_t s) {
+    if ((n & 3) == 0 && ((((uintptr_t)p) | ((uintptr_t)g) | ((uintptr_t)m) | ((uintptr_t)v)) & 15) == 0)
+        hipLaunchKernelGGL(adamw4_kernel, dim3(grid_for(n / 4, 256, 16384)), dim3(256), 0, s,
+                           (float4*)p, (const float4*)g, (float4*)m, (float4*)v, n / 4, a);
+    else
+        hipLaunchKernelGGL(adamw_kernel, dim3(grid_for(n, 256, 16384)), dim3(256), 0, s, p, g, m, v,
+                           n, a);
     LAUNCH_CHECK();
 }
 int k_mask_counts(const float* x, const float* t, int64_t n, uint8_t* mask, int64_t* counts,

@@ -23,6 +23,9 @@
 #include <string.h>
 
 #include <algorithm>
+#include <memory>
+#include <new>
+#include <stdexcept>
 #include <string>
 #include <vector>
 
@@ -72,6 +75,50 @@ struct TimeRec {
     double flop;
 };
 
+// Kernel-schedule options of one context (unet_set_option).  The defaults are the
+// measured-best schedules; the alternatives exist for A/B runs and tests and are chosen
+// explicitly through the ABI (never from the environment).  None of them changes the
+// numerics except where noted as bit-identical alternatives in DESIGN.md.
+struct Options {
+    int wgrad_row3 = 0;        // f32 3x3 wgrad on the one-row-of-taps kernel: 0 never,
+                               // 1 every eligible layer, 2 layers with a 64-channel operand
+    int wgrad_row3_tile = -1;  // its tile (>= 20), -1 = by channel counts
+    int wgrad_tile_w = 0;      // f32 wgrad tile, both channel counts multiples of 128
+    int wgrad_tile_n = 7;      // ... 64-channel layers (64x64, 3 waves/SIMD)
+    int wgrad16_tile = 0;      // register-staged bf16 wgrad tile (128-multiples)
+    int tile_n128 = -1;        // f32 row-GEMM tile, N % 128 == 0 (-1 = by grid size)
+    int tile_n128_dgrad = -1;  // ... dgrad-type
+    int tile_n64 = 1;          // ... N = 64 outputs
+    int tile16_n128 = 6;       // register-staged bf16 row-GEMM tiles
+    int tile16_n128_dgrad = 6;
+    int tile16_n64 = 1;
+    int rg16 = 1;              // bf16 row GEMMs on the LDS-DMA kernel (0: register-staged)
+    int rg16_tile = -1;        // its tile (-1 = per GEMM, rg16_tile())
+    int wg16 = 1;              // bf16 3x3 wgrad on the LDS-DMA transposed-read kernel
+    int wg16_tile = 2;         // its tile (2 = 256x256)
+    int wg16t = 1;             // bf16 ConvT wgrad on the same kernel
+    int xcd16 = 1;             // XCD-contiguous block order, LDS-DMA kernels
+    int xcd_remap = 0;         // ... f32 GEMMs: 0 none, 1 both, 2 row GEMMs, 3 wgrad
+    int wgrad_stream = 0;      // weight gradients on a second stream (bit-identical)
+    int dz_in_loaders = 0;     // BN-backward dz inside the GEMM loaders (model.py order)
+};
+struct OptionDesc {
+    const char* name;
+    int Options::*field;
+};
+const OptionDesc OPTION_TABLE[] = {
+    {"wgrad_row3", &Options::wgrad_row3},       {"wgrad_row3_tile", &Options::wgrad_row3_tile},
+    {"wgrad_tile_w", &Options::wgrad_tile_w},   {"wgrad_tile_n", &Options::wgrad_tile_n},
+    {"wgrad16_tile", &Options::wgrad16_tile},   {"tile_n128", &Options::tile_n128},
+    {"tile_n128_dgrad", &Options::tile_n128_dgrad}, {"tile_n64", &Options::tile_n64},
+    {"tile16_n128", &Options::tile16_n128},     {"tile16_n128_dgrad", &Options::tile16_n128_dgrad},
+    {"tile16_n64", &Options::tile16_n64},       {"rg16", &Options::rg16},
+    {"rg16_tile", &Options::rg16_tile},         {"wg16", &Options::wg16},
+    {"wg16_tile", &Options::wg16_tile},         {"wg16t", &Options::wg16t},
+    {"xcd16", &Options::xcd16},                 {"xcd_remap", &Options::xcd_remap},
+    {"wgrad_stream", &Options::wgrad_stream},   {"dz_in_loaders", &Options::dz_in_loaders},
+};
+
 }  // namespace
 
 struct unet_ctx {
@@ -108,6 +155,7 @@ struct unet_ctx {
     hipStream_t side = nullptr;
     std::vector<hipEvent_t> sync_pool;
     size_t sync_used = 0;
+    Options opt;
 
     int nconv() const { return (int)conv.size(); }
     int ch(int level) const { return base << level; }
@@ -123,9 +171,30 @@ int fail(unet_ctx* c, int code, const char* fmt, ...) {
     va_start(ap, fmt);
     vsnprintf(buf, sizeof buf, fmt, ap);
     va_end(ap);
-    if (c) c->err = buf;
+    if (c) {
+        try {
+            c->err = buf;
+        } catch (...) {  // out of memory for the message itself: keep the code
+        }
+    }
     return code;
 }
+
+// Every extern "C" entry runs its body inside ABI_TRY / ABI_CATCH(ctx): no C++ exception
+// (std::bad_alloc from the graph / plan / timing containers, ...) unwinds into the caller.
+#define ABI_TRY try {
+#define ABI_CATCH(ctx)                                                                      \
+    }                                                                                       \
+    catch (const std::bad_alloc&) {                                                         \
+        return fail(const_cast<unet_ctx*>(ctx), UNET_ERR_NOMEM, "out of host memory");       \
+    }                                                                                       \
+    catch (const std::exception& e_) {                                                      \
+        return fail(const_cast<unet_ctx*>(ctx), UNET_ERR_INTERNAL, "internal error: %s",     \
+                    e_.what());                                                             \
+    }                                                                                       \
+    catch (...) {                                                                           \
+        return fail(const_cast<unet_ctx*>(ctx), UNET_ERR_INTERNAL, "internal error");        \
+    }
 
 // Parameter table in the reference's named_parameters() order, layer tables, packing
 // offsets and gradient buckets.
@@ -339,27 +408,18 @@ struct WgradCfg {
 };
 
 // wgrad tile (kernels_gemm.hip WGRAD_TILES) + split-K over pixels so that every layer
-// launches >= 2048 blocks; UNET_WGRAD_TILE_{W,N} override (tuning runs).
+// launches >= 2048 blocks; options wgrad_tile_{w,n} override (tuning runs).
 // row_w: row width of a 3x3 conv's pixel grid (0 otherwise).  3x3 weight gradients on
 // rows that are a multiple of 32 pixels take the one-row-of-taps tiles (ids 20..,
-// wgrad_row3_kernel) when UNET_WGRAD_ROW3 selects them: 1 = every eligible layer,
+// wgrad_row3_kernel) when option wgrad_row3 selects them: 1 = every eligible layer,
 // 2 = only layers with a 64-channel operand (the 256x256 / 128x128 levels), 0 = never.
-WgradCfg wgrad_cfg(int CA, int tapsA, int CB, int tapsB, int64_t P, bool bf16, int row_w = 0) {
-    static int tw = -2, tn = -2, t16 = -2;
-    // read per call (the workspace plan and the backward of one step read it alike), so a
-    // test can compare both schedules in one process
-    const char* e3 = getenv("UNET_WGRAD_ROW3");
-    const int r3 = e3 ? atoi(e3) : 0;
-    e3 = getenv("UNET_WGRAD_ROW3_TILE");
-    const int r3t = e3 ? atoi(e3) : -1;
-    if (tw == -2) {
-        const char* e = getenv("UNET_WGRAD_TILE_W");
-        tw = e ? atoi(e) : 0;
-        e = getenv("UNET_WGRAD_TILE_N");
-        tn = e ? atoi(e) : 7;  // 64x64, 3 waves/SIMD (tools/gemm_tune: +1 % over w4)
-        e = getenv("UNET_WGRAD16_TILE");
-        t16 = e ? atoi(e) : 0;
-    }
+// The split-K partition follows from the (default) tile dims; the bf16 LDS-DMA weight
+// gradient (wg16_tile) reuses the register-staged tile's partition, so its tile choice
+// never changes the summation order.
+WgradCfg wgrad_cfg(const unet_ctx* c, int CA, int tapsA, int CB, int tapsB, int64_t P, bool bf16,
+                   int row_w = 0) {
+    const int r3 = c->opt.wgrad_row3, r3t = c->opt.wgrad_row3_tile;
+    const int tw = c->opt.wgrad_tile_w, tn = c->opt.wgrad_tile_n, t16 = c->opt.wgrad16_tile;
     WgradCfg w;
     if (bf16) {  // kernels_gemm.hip WGRAD16_TILES
         w.tile = (CA % 128 == 0 && CB % 128 == 0) ? t16 : CA % 128 == 0 ? 3 : CB % 128 == 0 ? 4 : 2;
@@ -395,15 +455,14 @@ WgradCfg wgrad_cfg(int CA, int tapsA, int CB, int tapsB, int64_t P, bool bf16, i
 
 // bf16 math: conv / ConvT GEMMs whose K channels are a multiple of 64 and whose N is a
 // multiple of 128 run on the LDS-DMA kernel (kernels_gemm16.hip) from a prepared bf16
-// operand image; UNET_RG16=0 keeps the register-staged bf16 kernel (A/B runs),
-// UNET_RG16_TILE picks its tile (kernels_gemm16.hip ROWGEMM16_TILES).
-// (read per call, so a test can compare both kernels in one process)
+// operand image; option rg16 = 0 keeps the register-staged bf16 kernel (A/B runs),
+// rg16_tile picks its tile (kernels_gemm16.hip ROWGEMM16_TILES).
 bool rg16_on(const unet_ctx* c, int C, int N) {
-    const char* e = getenv("UNET_RG16");
-    return c->bf16 && (e ? atoi(e) : 1) != 0 && C % 64 == 0 && N % 128 == 0;
+    return c->bf16 && c->opt.rg16 != 0 && C % 64 == 0 && N % 128 == 0;
 }
-// tile for one LDS-DMA row GEMM.  UNET_RG16_TILE forces a tile (128x128 where N does not
-// divide into it).  Default: the 256x256 tile (8 waves, one block per CU) unless
+// tile for one LDS-DMA row GEMM.  Option rg16_tile forces a tile (128x128 where N does not
+// divide into it).  Every tile emits BN partials in 128-row groups, so the choice changes
+// speed only.  Default: the 256x256 tile (8 waves, one block per CU) unless
 //  * it would leave CUs idle: fewer than 256 blocks (the 16x16 / 32x32 levels of config 4:
 //    bottleneck fwd 0.48 -> 0.37 ms, its dgrad 0.90 -> 0.48 ms on the 128x128 tile), or
 //  * the epilogue is the BN-backward-partials one (E_STORE_BN: reads the BN input, writes
@@ -411,17 +470,14 @@ bool rg16_on(const unet_ctx* c, int C, int N) {
 //    nothing hides that epilogue, while two co-resident 128x128 blocks overlap one's
 //    epilogue with the other's MFMAs (level-1 dgrad 1.15 -> 0.80 ms, level-0 ConvT dgrad
 //    0.77 -> 0.37 ms; per-layer sweep in profiles/r01_rg16_tile_sweep.txt).
-int rg16_tile(const RowGemmArgs& g) {
+int rg16_tile(const unet_ctx* c, const RowGemmArgs& g) {
     const int cout = g.emode == E_CONVT ? g.cout : 0;
     auto fits = [&](int t) {
         int bm = 0, bn = 0;
         if (rowgemm16_tile_dims(t, &bm, &bn) != 0) return false;
         return g.N % bn == 0 && (cout == 0 || cout % bn == 0);
     };
-    if (const char* e = getenv("UNET_RG16_TILE")) {
-        const int t = atoi(e);
-        return fits(t) ? t : 0;
-    }
+    if (c->opt.rg16_tile >= 0) return fits(c->opt.rg16_tile) ? c->opt.rg16_tile : 0;
     if (!fits(4)) return 0;
     const int64_t blocks = (g.M + 255) / 256 * (g.N / 256);
     if (blocks < 256) return 0;
@@ -430,33 +486,27 @@ int rg16_tile(const RowGemmArgs& g) {
 }
 // 3x3 weight gradients of layers with Cin, Cout multiples of 128 on the LDS-DMA
 // transposed-read kernel (kernels_gemm16.hip wgrad16_kernel) from the forward's bf16 input
-// image and the dz image; UNET_WG16=0 keeps the register-staged bf16 wgrad, UNET_WG16_TILE
+// image and the dz image; option wg16 = 0 keeps the register-staged bf16 wgrad, wg16_tile
 // picks the tile.
 bool wg16_on(const unet_ctx* c, int CA, int CB) {
-    const char* e = getenv("UNET_WG16");
-    return c->bf16 && (e ? atoi(e) : 1) != 0 && CA % 128 == 0 && CB % 128 == 0;
+    return c->bf16 && c->opt.wg16 != 0 && CA % 128 == 0 && CB % 128 == 0;
 }
 // XCD-contiguous block order for the LDS-DMA bf16 kernels: on by default (config 4 A/B:
-// wgrad 718 -> 766 TF/s, forward 854 -> 871, dgrad -2 %, step +2 %); UNET_XCD16=0 turns it off
-int xcd16_on() {
-    const char* e = getenv("UNET_XCD16");
-    return (e ? atoi(e) : 1) != 0 ? 1 : 0;
-}
-// tile: UNET_WG16_TILE, else 256x256 (tile 2) where both channel counts allow it
-int wg16_tile(int CA = 128, int CB = 128) {
-    const char* e = getenv("UNET_WG16_TILE");
-    const int t = e ? atoi(e) : 2;
+// wgrad 718 -> 766 TF/s, forward 854 -> 871, dgrad -2 %, step +2 %); option xcd16 = 0 off
+int xcd16_on(const unet_ctx* c) { return c->opt.xcd16 != 0 ? 1 : 0; }
+// tile: option wg16_tile (default 256x256, tile 2) where both channel counts allow it
+int wg16_tile(const unet_ctx* c, int CA = 128, int CB = 128) {
+    const int t = c->opt.wg16_tile;
     int bm = 0, bn = 0;
     if (wgrad16g_tile_dims(t, &bm, &bn) != 0 || CA % bm || CB % bn) return 0;
     return t;
 }
 // ConvT weight gradient on the LDS-DMA transposed-read kernel (A' = the forward's bf16
 // ConvT input image, B' = the bf16 image of the concat gradient's up half, G_UP2-gathered);
-// the bias gradient then comes from k_up2_bias_partials.  UNET_WG16T=0 keeps the
+// the bias gradient then comes from k_up2_bias_partials.  Option wg16t = 0 keeps the
 // register-staged kernel.
 bool convt_wg16_on(const unet_ctx* c, int cin, int cout) {
-    const char* e = getenv("UNET_WG16T");
-    return (e ? atoi(e) : 1) != 0 && wg16_on(c, cin, cout) && rg16_on(c, cin, 4 * cout) &&
+    return c->opt.wg16t != 0 && wg16_on(c, cin, cout) && rg16_on(c, cin, 4 * cout) &&
            rg16_on(c, cout, cin);
 }
 
@@ -561,17 +611,17 @@ void make_plan(unet_ctx* c, int N, int H, int W, bool training, char* base, Plan
         int64_t smax = 0, bmax = 0;
         for (int i = 1; i < NC; ++i) {
             const ConvL& L = c->conv[i];
-            WgradCfg w = wgrad_cfg(L.cin, 9, L.cout, 1, p.P[L.level], c->bf16, W >> L.level);
+            WgradCfg w = wgrad_cfg(c, L.cin, 9, L.cout, 1, p.P[L.level], c->bf16, W >> L.level);
             smax = std::max(smax, (int64_t)w.splits * 9 * L.cin * L.cout);
             bmax = std::max(bmax, (int64_t)w.splits * L.cout);
         }
         for (int blk = 1; blk <= 2 * D && c->res; ++blk) {
             const ConvL& L = c->conv[2 * blk];
-            WgradCfg w = wgrad_cfg(L.cin, 1, L.cout, 1, p.P[L.level], c->bf16);
+            WgradCfg w = wgrad_cfg(c, L.cin, 1, L.cout, 1, p.P[L.level], c->bf16);
             smax = std::max(smax, (int64_t)w.splits * L.cin * L.cout);
         }
         for (const ConvTL& T : c->convt) {
-            WgradCfg w = wgrad_cfg(T.cin, 1, T.cout, 4, p.P[T.in_level], c->bf16);
+            WgradCfg w = wgrad_cfg(c, T.cin, 1, T.cout, 4, p.P[T.in_level], c->bf16);
             smax = std::max(smax, (int64_t)w.splits * T.cin * 4 * T.cout);
             bmax = std::max(bmax, (int64_t)w.splits * 4 * T.cout);
         }
@@ -627,9 +677,6 @@ struct Launcher {
 };
 
 // Row-GEMM tile choice for an output width N (tile ids: kernels_gemm.hip ROWGEMM_TILES).
-// UNET_TILE_N128 / UNET_TILE_N64 override the choice (tuning runs).
-// Defaults from tools/gemm_tune (r01): forward-type ops 128x128/BK32 single LDS image
-// (4 waves/SIMD), dgrad-type 128x128 double-buffered, N = 64 outputs 128x64.
 // Defaults from tools/gemm_tune (r01, 15 rounds, profiles/r01_gemm_tune.txt):
 //  * forward-type, N % 128 == 0: 128x128/BK32 single LDS image; at >= 2048 blocks the
 //    3-waves/SIMD variant (t7) is 2-4 % faster, below that its partial last round of
@@ -637,27 +684,15 @@ struct Launcher {
 //  * dgrad-type, N % 128 == 0: double-buffered 128x128 (t0) except on the big grids
 //    (>= 4096 blocks) where the single-image t4 is 2-4 % faster;
 //  * N = 64 outputs: 128x64 (t1).
-// bf16 MFMA (UNET_TILE16_*): a chunk of 64 K per barrier (4 MFMA k-steps) by default.
-// UNET_TILE_* environment variables override (tuning runs; -1 = automatic).
-int pick_tile(int N, bool dgrad, bool bf16, int64_t M = 0) {
-    static int t128 = -2, t128d = -2, t64 = -2, b128 = -2, b128d = -2, b64 = -2;
-    if (t128 == -2) {
-        auto env = [](const char* n, int d) {
-            const char* e = getenv(n);
-            return e ? atoi(e) : d;
-        };
-        t128 = env("UNET_TILE_N128", -1);
-        t128d = env("UNET_TILE_N128_DGRAD", -1);
-        t64 = env("UNET_TILE_N64", 1);
-        b128 = env("UNET_TILE16_N128", 6);
-        b128d = env("UNET_TILE16_N128_DGRAD", 6);
-        b64 = env("UNET_TILE16_N64", 1);
-    }
-    if (bf16) return N % 128 == 0 ? (dgrad ? b128d : b128) : b64;
-    if (N % 128) return t64;
+// bf16 MFMA (register-staged): a chunk of 64 K per barrier (4 MFMA k-steps) by default.
+// Options tile_* override (tuning runs; -1 = automatic).
+int pick_tile(const unet_ctx* c, int N, bool dgrad, bool bf16, int64_t M = 0) {
+    const Options& o = c->opt;
+    if (bf16) return N % 128 == 0 ? (dgrad ? o.tile16_n128_dgrad : o.tile16_n128) : o.tile16_n64;
+    if (N % 128) return o.tile_n64;
     const int64_t blocks = (M + 127) / 128 * (N / 128);
-    if (dgrad) return t128d >= 0 ? t128d : (blocks >= 4096 ? 4 : 0);
-    return t128 >= 0 ? t128 : (blocks >= 2048 ? 7 : 4);
+    if (dgrad) return o.tile_n128_dgrad >= 0 ? o.tile_n128_dgrad : (blocks >= 4096 ? 4 : 0);
+    return o.tile_n128 >= 0 ? o.tile_n128 : (blocks >= 2048 ? 7 : 4);
 }
 
 std::string tlabel(const char* fam, int tile, int layer) {
@@ -736,33 +771,24 @@ Operand conv_input(unet_ctx* c, Plan& p, int i) {
     return {nullptr, 0, 0, nullptr, nullptr, 0};  // conv 0: x
 }
 
+// BN partial rows a row GEMM emits: one per 128-row group, whatever its tile (gemm_common.h
+// row_epilogue), so the BN statistics do not depend on the tile choice
+int bn_groups(int64_t M) { return (int)((M + 127) / 128); }
+
 const float* bias_ptr(const float* prm, int64_t off) { return off >= 0 ? prm + off : nullptr; }
 
-// XCD-aware block order for the GEMMs (UNET_XCD_REMAP: 0 none, 1 both, 2 row GEMMs only,
-// 3 wgrad only; A/B runs)
-int xcd_mode() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("UNET_XCD_REMAP");
-        v = e ? atoi(e) : 0;
-    }
-    return v;
-}
-int xcd_remap_on() { return xcd_mode() == 1 || xcd_mode() == 2; }
-int xcd_remap_wgrad() { return xcd_mode() == 1 || xcd_mode() == 3; }
+// XCD-aware block order for the f32 GEMMs (option xcd_remap: 0 none, 1 both, 2 row GEMMs
+// only, 3 wgrad only; A/B runs)
+int xcd_remap_on(const unet_ctx* c) { return c->opt.xcd_remap == 1 || c->opt.xcd_remap == 2; }
+int xcd_remap_wgrad(const unet_ctx* c) { return c->opt.xcd_remap == 1 || c->opt.xcd_remap == 3; }
 
-// UNET_WGRAD_STREAM=1: weight gradients on a second stream.  Off by default: measured
+// option wgrad_stream = 1: weight gradients on a second stream.  Off by default: measured
 // 1 % slower at bs = 32 (370 vs 374 img/s, r01 A/B) -- the GEMMs fill the chip on their
 // own, so the overlap only wins the tails back, and the ~50 cross-stream waits cost more.
-// (read per backward call, so a test can compare both schedules in one process)
-bool wgrad_stream_env() {
-    const char* e = getenv("UNET_WGRAD_STREAM");
-    return e && atoi(e) != 0;
-}
 
 // weight image of a row GEMM: f32, or bf16 packed into the same slot (half its size)
 void set_weights(const unet_ctx* c, RowGemmArgs& g, const float* img) {
-    g.xcd = xcd_remap_on();
+    g.xcd = xcd_remap_on(c);
     if (c->bf16)
         g.bt16 = (const uint16_t*)img;
     else
@@ -777,7 +803,7 @@ std::string tlabel16(const char* fam, int tile, int layer) {
     return b;
 }
 // point g's A operand at the prepared bf16 image (lda = C channels)
-void use_a16(const Plan& p, RowGemmArgs& g, int C) {
+void use_a16(const unet_ctx* c, const Plan& p, RowGemmArgs& g, int C) {
     g.a16 = p.s16;
     g.lda = C;
     g.aoff = 0;
@@ -785,7 +811,7 @@ void use_a16(const Plan& p, RowGemmArgs& g, int C) {
     g.arelu = 0;
     g.acoef = nullptr;
     g.zero16 = p.zero16;
-    g.xcd = xcd16_on();
+    g.xcd = xcd16_on(c);
 }
 
 int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, const float* x,
@@ -866,20 +892,16 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
                 uint16_t* img = p.x16[i] ? p.x16[i] : p.s16;
                 RUN("prep16", 0, k_to_bf16(a.ptr, a.ld, a.off, C.cin, a.scale, a.shift, a.relu, M,
                                            img, s));
-                use_a16(p, g, C.cin);
+                use_a16(c, p, g, C.cin);
                 g.a16 = img;
-                const int tile = rg16_tile(g);
-                int bm, bn;
-                rowgemm16_tile_dims(tile, &bm, &bn);
-                R = (int)((M + bm - 1) / bm);
+                const int tile = rg16_tile(c, g);
+                R = bn_groups(M);
                 RUN(tlabel16("conv_fwd", tile, i), 2.0 * M * C.cout * 9 * C.cin,
                     launch_rowgemm16(g, tile, s));
                 return stats_finalize(c, L, p, i, R, M, training, prm, bn_run, bn_cnt);
             }
-            const int tile = pick_tile(C.cout, false, c->bf16, M);
-            int bm, bn, bk;
-            rowgemm_tile_dims(tile, &bm, &bn, &bk);
-            R = (int)((M + bm - 1) / bm);
+            const int tile = pick_tile(c, C.cout, false, c->bf16, M);
+            R = bn_groups(M);
             RUN(tlabel("conv_fwd", tile, i), 2.0 * M * C.cout * 9 * C.cin, launch_rowgemm(g, tile, s));
         }
         return stats_finalize(c, L, p, i, R, M, training, prm, bn_run, bn_cnt);
@@ -919,14 +941,14 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
             uint16_t* img = p.t16[k] ? p.t16[k] : p.s16;
             RUN("prep16", 0, k_to_bf16(g.a, g.lda, g.aoff, T.cin, g.ascale, g.ashift, g.arelu, g.M,
                                        img, s));
-            use_a16(p, g, T.cin);
+            use_a16(c, p, g, T.cin);
             g.a16 = img;
-            const int tile = rg16_tile(g);
+            const int tile = rg16_tile(c, g);
             RUN(tlabel16("convT_fwd", tile, 100 + k), 2.0 * g.M * g.N * g.K,
                 launch_rowgemm16(g, tile, s));
             return 0;
         }
-        const int tile = pick_tile(T.cout, false, c->bf16, 4 * (int64_t)g.M);  // grid N = 4 cout
+        const int tile = pick_tile(c, T.cout, false, c->bf16, 4 * (int64_t)g.M);  // grid N = 4 cout
         RUN(tlabel("convT_fwd", tile, 100 + k), 2.0 * g.M * g.N * g.K, launch_rowgemm(g, tile, s));
         return 0;
     };
@@ -955,7 +977,7 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
         g.C = CL.cin;
         g.amode = G_IDENT;
         g.bt = prm + c->skip_w[b];  // torch layout [co][ci] is already Bt[n][k]
-        g.xcd = xcd_remap_on();
+        g.xcd = xcd_remap_on(c);
         g.out = p.out[b];
         g.ldo = p.ldout[b];
         g.ooff = p.offout[b];
@@ -965,7 +987,7 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
         g.offey = p.offy[i2];
         g.escale = p.scale[i2];
         g.eshift = p.shift[i2];
-        const int tile = pick_tile(CL.cout, false, false, M);
+        const int tile = pick_tile(c, CL.cout, false, false, M);
         RUN(tlabel("skip_fwd", tile, b), 2.0 * M * CL.cout * CL.cin, launch_rowgemm(g, tile, s));
         return 0;
     };
@@ -1011,12 +1033,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
     Launcher L{c, s};
     const int H = p.H, W = p.W, D = c->depth, NC = c->nconv();
     int rc;
-    static int dz_env = -1;
-    if (dz_env < 0) {
-        const char* e = getenv("UNET_DZ_IN_LOADERS");
-        dz_env = e ? atoi(e) : 0;
-    }
-    const bool dz_in_loaders = dz_env && !c->bn_relu;
+    const bool dz_in_loaders = c->opt.dz_in_loaders && !c->bn_relu;
 
     // Weight gradients (wgrad GEMM + slab reduce + bias sums) go to a second stream: they
     // only read the layer input (forward buffers, never written in backward) and dz, and
@@ -1031,7 +1048,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
     // Off for the residual network (its skip wgrad shares the slabs on the main stream), for
     // the loader-fused dz (the coefficients are rewritten per layer on the main stream) and
     // when every launch is timed (a clean per-kernel breakdown needs serial launches).
-    const bool async_w = wgrad_stream_env() && !c->res && !dz_in_loaders &&
+    const bool async_w = c->opt.wgrad_stream && !c->res && !dz_in_loaders &&
                          !(c->timing && c->tfilter.empty());
     if (async_w && !c->side &&
         hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess)
@@ -1132,9 +1149,9 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         }
         side_after_main();
         Operand a = conv_input(c, p, i);
-        WgradCfg wc = wgrad_cfg(C.cin, 9, C.cout, 1, P, c->bf16, Wl);
+        WgradCfg wc = wgrad_cfg(c, C.cin, 9, C.cout, 1, P, c->bf16, Wl);
         WgradArgs w{};
-        w.xcd = xcd_remap_wgrad();
+        w.xcd = xcd_remap_wgrad(c);
         w.H = Hl;
         w.W = Wl;
         w.P = (int)P;
@@ -1172,9 +1189,9 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
             w.by = nullptr;
             w.bcoef = nullptr;
             w.zero16 = p.zero16;
-            w.xcd = xcd16_on();
+            w.xcd = xcd16_on(c);
             // (the split count, sized for >= 2048 128x128 tiles, gives >= 512 256x256 ones)
-            const int t = wg16_tile(C.cin, C.cout);
+            const int t = wg16_tile(c, C.cin, C.cout);
             int wbm = 0, wbn = 0, wst = 0;
             wgrad16g_tile_dims(t, &wbm, &wbn, &wst);
             char lb[96];
@@ -1224,19 +1241,15 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
                 g.stats = p.part;
             }
             if (dz16 && rg16_on(c, C.cout, C.cin)) {
-                use_a16(p, g, C.cout);
-                const int tile = rg16_tile(g);
-                int bm, bn;
-                rowgemm16_tile_dims(tile, &bm, &bn);
-                if (rows) *rows = (int)((P + bm - 1) / bm);
+                use_a16(c, p, g, C.cout);
+                const int tile = rg16_tile(c, g);
+                if (rows) *rows = bn_groups(P);
                 RUN(tlabel16("conv_dgrad", tile, i), 2.0 * P * C.cout * 9 * C.cin,
                     launch_rowgemm16(g, tile, s));
                 return 0;
             }
-            const int tile = pick_tile(C.cin, true, c->bf16, P);
-            int bm, bn, bk;
-            rowgemm_tile_dims(tile, &bm, &bn, &bk);
-            if (rows) *rows = (int)((P + bm - 1) / bm);
+            const int tile = pick_tile(c, C.cin, true, c->bf16, P);
+            if (rows) *rows = bn_groups(P);
             RUN(tlabel("conv_dgrad", tile, i), 2.0 * P * C.cout * 9 * C.cin, launch_rowgemm(g, tile, s));
         }
         return 0;
@@ -1250,9 +1263,9 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         const int ldo = 2 * c->ch(lo), uo = c->up_off(lo);
         const int Hi = H >> T.in_level, Wi = W >> T.in_level;
         const int64_t Pin = p.P[T.in_level];
-        WgradCfg wc = wgrad_cfg(T.cin, 1, T.cout, 4, Pin, c->bf16);
+        WgradCfg wc = wgrad_cfg(c, T.cin, 1, T.cout, 4, Pin, c->bf16);
         WgradArgs w{};
-        w.xcd = xcd_remap_wgrad();
+        w.xcd = xcd_remap_wgrad(c);
         w.H = Hi;
         w.W = Wi;
         w.P = (int)Pin;
@@ -1299,8 +1312,8 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
             w.boff = 0;
             w.bias_slab = nullptr;
             w.zero16 = p.zero16;
-            w.xcd = xcd16_on();
-            const int t = wg16_tile(T.cin, T.cout);
+            w.xcd = xcd16_on(c);
+            const int t = wg16_tile(c, T.cin, T.cout);
             int wbm = 0, wbn = 0, wst = 0;
             wgrad16g_tile_dims(t, &wbm, &wbn, &wst);
             char lb[96];
@@ -1353,19 +1366,15 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
                 RUN("prep16", 0, k_to_bf16(p.dcat[lo], ldo, uo, T.cout, nullptr, nullptr, 0, p.P[lo],
                                            p.s16, s));
             }
-            use_a16(p, g, T.cout);
-            const int tile = rg16_tile(g);
-            int bm, bn;
-            rowgemm16_tile_dims(tile, &bm, &bn);
-            *rows = (int)((Pin + bm - 1) / bm);
+            use_a16(c, p, g, T.cout);
+            const int tile = rg16_tile(c, g);
+            *rows = bn_groups(Pin);
             RUN(tlabel16("convT_dgrad", tile, 100 + k), 2.0 * Pin * T.cin * 4 * T.cout,
                 launch_rowgemm16(g, tile, s));
             return 0;
         }
-        const int tile = pick_tile(T.cin, true, c->bf16, Pin);
-        int bm, bn, bk;
-        rowgemm_tile_dims(tile, &bm, &bn, &bk);
-        *rows = (int)((Pin + bm - 1) / bm);
+        const int tile = pick_tile(c, T.cin, true, c->bf16, Pin);
+        *rows = bn_groups(Pin);
         RUN(tlabel("convT_dgrad", tile, 100 + k), 2.0 * Pin * T.cin * 4 * T.cout, launch_rowgemm(g, tile, s));
         return 0;
     };
@@ -1403,9 +1412,9 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
                                       grads + c->skip_w[b], s));
             } else {
                 Operand a = conv_input(c, p, i1);
-                WgradCfg wc = wgrad_cfg(CL.cin, 1, CL.cout, 1, P, false);
+                WgradCfg wc = wgrad_cfg(c, CL.cin, 1, CL.cout, 1, P, false);
                 WgradArgs w{};
-                w.xcd = xcd_remap_wgrad();
+                w.xcd = xcd_remap_wgrad(c);
                 w.H = H >> CL.level;
                 w.W = W >> CL.level;
                 w.P = (int)P;
@@ -1437,11 +1446,11 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
                 g.C = CL.cout;
                 g.amode = G_IDENT;
                 g.bt = p.pack + c->skip_pd[b];
-                g.xcd = xcd_remap_on();
+                g.xcd = xcd_remap_on(c);
                 g.out = dx;
                 g.ldo = ldx;
                 g.emode = E_STORE;
-                const int tile = pick_tile(CL.cin, true, false, P);
+                const int tile = pick_tile(c, CL.cin, true, false, P);
                 RUN(tlabel("skip_dgrad", tile, b), 2.0 * P * CL.cin * CL.cout, launch_rowgemm(g, tile, s));
             }
             if ((rc = bn_finalize(i2, RED_G))) return rc;
@@ -1597,52 +1606,51 @@ extern "C" {
 int unet_create(const unet_cfg* cfg, int device, unet_ctx** out) {
     if (!out) return UNET_ERR_INVALID;
     *out = nullptr;
-    unet_ctx* c = new unet_ctx();
-    c->device = device;
-    if (cfg) {
-        c->in_ch = cfg->in_channels;
-        c->out_ch = cfg->out_channels;
-        c->variant = cfg->variant;
-        c->bf16 = cfg->math == UNET_MATH_BF16;
-        if (cfg->math != UNET_MATH_F32 && cfg->math != UNET_MATH_BF16) {
-            delete c;
-            return UNET_ERR_UNSUPPORTED;
+    try {
+        std::unique_ptr<unet_ctx> c(new unet_ctx());
+        c->device = device;
+        if (cfg) {
+            c->in_ch = cfg->in_channels;
+            c->out_ch = cfg->out_channels;
+            c->variant = cfg->variant;
+            c->bf16 = cfg->math == UNET_MATH_BF16;
+            if (cfg->math != UNET_MATH_F32 && cfg->math != UNET_MATH_BF16) return UNET_ERR_UNSUPPORTED;
+            if (c->variant == UNET_VARIANT_MOD || c->variant == UNET_VARIANT_RES) {
+                // mod.py:13-14 / :91-92 defaults base 64, depth 5
+                c->base = cfg->base_filters > 0 ? cfg->base_filters : 64;
+                c->depth = cfg->depth > 0 ? cfg->depth : 5;
+            } else if ((cfg->base_filters > 0 && cfg->base_filters != 64) ||
+                       (cfg->depth > 0 && cfg->depth != 4)) {
+                return UNET_ERR_UNSUPPORTED;  // models/model.py:UNet has a fixed topology
+            }
         }
-        if (c->variant == UNET_VARIANT_MOD || c->variant == UNET_VARIANT_RES) {
-            // mod.py:13-14 / :91-92 defaults base 64, depth 5
-            c->base = cfg->base_filters > 0 ? cfg->base_filters : 64;
-            c->depth = cfg->depth > 0 ? cfg->depth : 5;
-        } else if ((cfg->base_filters > 0 && cfg->base_filters != 64) ||
-                   (cfg->depth > 0 && cfg->depth != 4)) {
-            delete c;  // models/model.py:UNet has a fixed topology
+        // The first conv kernel is specialised for a single input channel (every BASELINE
+        // config); the GEMM tiles need 64-multiples of channels at every level and the
+        // channel-quad row kernels (pool, head, BN backward) a power-of-two channel count, so
+        // base is 64, 128 or 256; the head's fused BN-partials path handles up to 4 classes.
+        if ((c->variant != UNET_VARIANT_MODEL && c->variant != UNET_VARIANT_MOD &&
+             c->variant != UNET_VARIANT_RES) || c->in_ch != 1 ||
+            c->out_ch < 1 || c->out_ch > 4 || c->base % 64 || c->base > 256 ||
+            (c->base & (c->base - 1)) || c->depth < 1 ||
+            c->depth > MAX_DEPTH || (c->base << c->depth) > 8192)
             return UNET_ERR_UNSUPPORTED;
-        }
+        c->res = c->variant == UNET_VARIANT_RES;
+        c->bn_relu = c->variant != UNET_VARIANT_MODEL;
+        c->skip_first = c->bn_relu;
+        if (c->bf16 && c->variant != UNET_VARIANT_MOD)  // bf16 GEMMs: mod.py UNet (config 4) only
+            return UNET_ERR_UNSUPPORTED;
+        build_graph(c.get());
+        *out = c.release();
+        return UNET_OK;
+    } catch (const std::bad_alloc&) {
+        return UNET_ERR_NOMEM;
+    } catch (...) {
+        return UNET_ERR_INTERNAL;
     }
-    // The first conv kernel is specialised for a single input channel (every BASELINE
-    // config); the GEMM tiles need 64-multiples of channels at every level and the
-    // channel-quad row kernels (pool, head, BN backward) a power-of-two channel count, so
-    // base is 64, 128 or 256; the head's fused BN-partials path handles up to 4 classes.
-    if ((c->variant != UNET_VARIANT_MODEL && c->variant != UNET_VARIANT_MOD &&
-         c->variant != UNET_VARIANT_RES) || c->in_ch != 1 ||
-        c->out_ch < 1 || c->out_ch > 4 || c->base % 64 || c->base > 256 ||
-        (c->base & (c->base - 1)) || c->depth < 1 ||
-        c->depth > MAX_DEPTH || (c->base << c->depth) > 8192) {
-        delete c;
-        return UNET_ERR_UNSUPPORTED;
-    }
-    c->res = c->variant == UNET_VARIANT_RES;
-    c->bn_relu = c->variant != UNET_VARIANT_MODEL;
-    c->skip_first = c->bn_relu;
-    if (c->bf16 && c->variant != UNET_VARIANT_MOD) {  // bf16 GEMMs: mod.py UNet (config 4) only
-        delete c;
-        return UNET_ERR_UNSUPPORTED;
-    }
-    build_graph(c);
-    *out = c;
-    return UNET_OK;
 }
 
 int unet_destroy(unet_ctx* c) {
+    ABI_TRY
     if (!c) return UNET_ERR_INVALID;
     for (auto e : c->bucket_ev) (void)hipEventDestroy(e);
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
@@ -1650,6 +1658,7 @@ int unet_destroy(unet_ctx* c) {
     if (c->side) (void)hipStreamDestroy(c->side);
     delete c;
     return UNET_OK;
+    ABI_CATCH(c)
 }
 
 const char* unet_last_error(const unet_ctx* c) { return c ? c->err.c_str() : "null context"; }
@@ -1663,6 +1672,7 @@ int unet_num_params(const unet_ctx* c, int* n, int64_t* nf) {
 
 int unet_param_info(const unet_ctx* c, int i, const char** name, int* ndim, int64_t shape[4],
                     int64_t* offset) {
+    ABI_TRY
     if (!c || i < 0 || i >= (int)c->params.size()) return UNET_ERR_INVALID;
     const ParamT& p = c->params[i];
     if (name) *name = p.name.c_str();
@@ -1671,35 +1681,43 @@ int unet_param_info(const unet_ctx* c, int i, const char** name, int* ndim, int6
         for (int k = 0; k < 4; ++k) shape[k] = p.shape[k];
     if (offset) *offset = p.off;
     return UNET_OK;
+    ABI_CATCH(c)
 }
 
 int unet_num_bn(const unet_ctx* c, int* n, int64_t* nf) {
+    ABI_TRY
     if (!c) return UNET_ERR_INVALID;
     if (n) *n = c->nconv();
     if (nf) *nf = c->n_bn_floats;
     return UNET_OK;
+    ABI_CATCH(c)
 }
 
 int unet_bn_info(const unet_ctx* c, int i, const char** name, int* ch, int64_t* off) {
+    ABI_TRY
     if (!c || i < 0 || i >= c->nconv()) return UNET_ERR_INVALID;
     if (name) *name = c->bn[i].name.c_str();
     if (ch) *ch = c->bn[i].C;
     if (off) *off = c->bn[i].run;
     return UNET_OK;
+    ABI_CATCH(c)
 }
 
 int unet_workspace_size(unet_ctx* c, int N, int H, int W, int training, size_t* bytes) {
+    ABI_TRY
     if (!c || !bytes) return UNET_ERR_INVALID;
     if (!shape_ok(c, N, H, W)) return fail(c, UNET_ERR_SHAPE, "bad shape N=%d H=%d W=%d", N, H, W);
     Plan p;
     make_plan(c, N, H, W, training != 0, nullptr, p);
     *bytes = p.bytes;
     return UNET_OK;
+    ABI_CATCH(c)
 }
 
 int unet_forward(unet_ctx* c, const float* params, float* bn_running, int64_t* bn_count,
                  const float* x, float* logits, void* ws, size_t ws_bytes, int N, int H, int W,
                  int training, unet_stream_t stream) {
+    ABI_TRY
     if (!c || !params || !x || !logits || !ws) return c ? fail(c, UNET_ERR_INVALID, "null pointer") : UNET_ERR_INVALID;
     if (!shape_ok(c, N, H, W)) return fail(c, UNET_ERR_SHAPE, "bad shape N=%d H=%d W=%d", N, H, W);
     if (!training && !bn_running)
@@ -1712,10 +1730,12 @@ int unet_forward(unet_ctx* c, const float* params, float* bn_running, int64_t* b
     if (!c->timing) c->ev_used = 0;
     return forward_impl(c, params, bn_running, bn_count, x, logits, p, training != 0,
                         (hipStream_t)stream);
+    ABI_CATCH(c)
 }
 
 int unet_backward(unet_ctx* c, const float* params, const float* dlogits, float* grads, void* ws,
                   size_t ws_bytes, int N, int H, int W, unet_stream_t stream) {
+    ABI_TRY
     if (!c || !params || !dlogits || !grads || !ws) return c ? fail(c, UNET_ERR_INVALID, "null pointer") : UNET_ERR_INVALID;
     if (!shape_ok(c, N, H, W)) return fail(c, UNET_ERR_SHAPE, "bad shape N=%d H=%d W=%d", N, H, W);
     Plan p;
@@ -1728,97 +1748,166 @@ int unet_backward(unet_ctx* c, const float* params, const float* dlogits, float*
         for (auto& e : c->bucket_ev) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
     }
     return backward_impl(c, params, dlogits, grads, p, (hipStream_t)stream);
+    ABI_CATCH(c)
+}
+
+int unet_loss_stats(unet_ctx* c, const float* logits, const float* targets, int N, int C, int H,
+                    int W, float* stats, double* sums, unet_stream_t stream) {
+    ABI_TRY
+    if (!c || !logits || !targets || !stats || !sums) return UNET_ERR_INVALID;
+    if (N < 1 || C < 1 || H < 1 || W < 1) return fail(c, UNET_ERR_SHAPE, "bad loss shape");
+    int r = k_loss_stats(logits, targets, N, (int64_t)C * H * W, stats, sums, (hipStream_t)stream);
+    return r ? fail(c, UNET_ERR_HIP, "loss_stats launch %d", r) : UNET_OK;
+    ABI_CATCH(c)
+}
+
+int unet_loss_finalize(unet_ctx* c, const double* sums, float* losses, float fa, float fb,
+                       float fg, unet_stream_t stream) {
+    ABI_TRY
+    if (!c || !sums || !losses) return UNET_ERR_INVALID;
+    int r = k_loss_finalize(sums, fa, fb, fg, losses, (hipStream_t)stream);
+    return r ? fail(c, UNET_ERR_HIP, "loss_finalize launch %d", r) : UNET_OK;
+    ABI_CATCH(c)
 }
 
 int unet_loss_fwd(unet_ctx* c, const float* logits, const float* targets, int N, int C, int H,
-                  int W, float* stats, float* losses, float fa, float fb, float fg,
+                  int W, float* stats, double* sums, float* losses, float fa, float fb, float fg,
                   unet_stream_t stream) {
-    if (!c || !logits || !targets || !stats || !losses) return UNET_ERR_INVALID;
-    if (N < 1 || C < 1 || H < 1 || W < 1) return fail(c, UNET_ERR_SHAPE, "bad loss shape");
-    int r = k_loss_fwd(logits, targets, N, (int64_t)C * H * W, stats, losses, fa, fb, fg,
-                       (hipStream_t)stream);
-    return r ? fail(c, UNET_ERR_HIP, "loss_fwd launch %d", r) : UNET_OK;
+    const int r = unet_loss_stats(c, logits, targets, N, C, H, W, stats, sums, stream);
+    return r ? r : unet_loss_finalize(c, sums, losses, fa, fb, fg, stream);
 }
 
 int unet_loss_bwd(unet_ctx* c, const float* logits, const float* targets, int N, int C, int H,
-                  int W, const float* stats, const float* w, float* dlogits, float fa, float fb,
-                  float fg, unet_stream_t stream) {
-    if (!c || !logits || !targets || !stats || !w || !dlogits) return UNET_ERR_INVALID;
+                  int W, const float* stats, const double* sums, const float* w, float* dlogits,
+                  float fa, float fb, float fg, unet_stream_t stream) {
+    ABI_TRY
+    if (!c || !logits || !targets || !stats || !sums || !w || !dlogits) return UNET_ERR_INVALID;
     if (N < 1 || C < 1 || H < 1 || W < 1) return fail(c, UNET_ERR_SHAPE, "bad loss shape");
-    int r = k_loss_bwd(logits, targets, N, (int64_t)C * H * W, stats, w, fa, fb, fg, dlogits,
+    int r = k_loss_bwd(logits, targets, N, (int64_t)C * H * W, stats, sums, w, fa, fb, fg, dlogits,
                        (hipStream_t)stream);
     return r ? fail(c, UNET_ERR_HIP, "loss_bwd launch %d", r) : UNET_OK;
+    ABI_CATCH(c)
 }
 
 int unet_adamw(unet_ctx* c, float* params, const float* grads, float* m, float* v, int64_t n,
-               int step, float lr, float b1, float b2, float eps, float wd, float gscale,
+               int step, double lr, double b1, double b2, double eps, double wd, double gscale,
                unet_stream_t stream) {
+    ABI_TRY
     if (!c || !params || !grads || !m || !v || n < 0 || step < 1) return UNET_ERR_INVALID;
-    // torch optim/adam.py: bias corrections computed on the host in double then used as
-    // python floats (double) -> step_size and bias_correction2_sqrt
-    const double bc1 = 1.0 - pow((double)b1, step);
-    const double bc2 = 1.0 - pow((double)b2, step);
-    const double step_size = (double)lr / bc1;
-    const double bc2_sqrt = sqrt(bc2);
-    int r = k_adamw(params, grads, m, v, n, lr, b1, b2, eps, wd, (float)step_size, (float)bc2_sqrt,
-                    gscale, (hipStream_t)stream);
+    // torch optim/adam.py _single_tensor_adam: every scalar is a Python float (double)
+    // that ATen rounds to float once when it meets the fp32 tensor
+    AdamwScalars a;
+    a.decay = (float)(1.0 - lr * wd);                 // param.mul_(1 - lr * weight_decay)
+    a.w1 = (float)(1.0 - b1);                         // exp_avg.lerp_(grad, 1 - beta1)
+    a.lerp_small = fabs(1.0 - b1) < 0.5 ? 1 : 0;
+    a.b2 = (float)b2;                                 // exp_avg_sq.mul_(beta2)
+    a.w2 = (float)(1.0 - b2);                         // .addcmul_(grad, grad, value=1 - beta2)
+    const double bc1 = 1.0 - pow(b1, (double)step);   // beta1 ** step (Python float pow)
+    const double bc2 = 1.0 - pow(b2, (double)step);
+    a.neg_step = (float)(-(lr / bc1));                // addcdiv_(..., value=-step_size)
+    a.bc2_sqrt = (float)pow(bc2, 0.5);                // bias_correction2 ** 0.5
+    a.eps = (float)eps;                               // .add_(eps)
+    a.gscale = (float)gscale;
+    int r = k_adamw(params, grads, m, v, n, a, (hipStream_t)stream);
     return r ? fail(c, UNET_ERR_HIP, "adamw launch %d", r) : UNET_OK;
+    ABI_CATCH(c)
+}
+
+int unet_set_option(unet_ctx* c, const char* name, int64_t value) {
+    ABI_TRY
+    if (!c || !name) return UNET_ERR_INVALID;
+    for (const OptionDesc& d : OPTION_TABLE)
+        if (strcmp(d.name, name) == 0) {
+            c->opt.*d.field = (int)value;
+            return UNET_OK;
+        }
+    return fail(c, UNET_ERR_INVALID, "unknown option '%s'", name);
+    ABI_CATCH(c)
+}
+
+int unet_get_option(const unet_ctx* c, const char* name, int64_t* value) {
+    ABI_TRY
+    if (!c || !name || !value) return UNET_ERR_INVALID;
+    for (const OptionDesc& d : OPTION_TABLE)
+        if (strcmp(d.name, name) == 0) {
+            *value = c->opt.*d.field;
+            return UNET_OK;
+        }
+    return UNET_ERR_INVALID;
+    ABI_CATCH(c)
 }
 
 int unet_mask_counts(unet_ctx* c, const float* logits, const float* targets, int64_t n,
                      uint8_t* mask, int64_t* counts, unet_stream_t stream) {
+    ABI_TRY
     if (!c || !logits || !targets || !counts || n < 0) return UNET_ERR_INVALID;
     int r = k_mask_counts(logits, targets, n, mask, counts, (hipStream_t)stream);
     return r ? fail(c, UNET_ERR_HIP, "mask_counts launch %d", r) : UNET_OK;
+    ABI_CATCH(c)
 }
 
 int unet_num_buckets(const unet_ctx* c, int* n) {
+    ABI_TRY
     if (!c || !n) return UNET_ERR_INVALID;
     *n = (int)c->bucket_off.size();
     return UNET_OK;
+    ABI_CATCH(c)
 }
 
 int unet_bucket_range(const unet_ctx* c, int b, int64_t* off, int64_t* len) {
+    ABI_TRY
     if (!c || b < 0 || b >= (int)c->bucket_off.size()) return UNET_ERR_INVALID;
     if (off) *off = c->bucket_off[b];
     if (len) *len = c->bucket_len[b];
     return UNET_OK;
+    ABI_CATCH(c)
 }
 
 int unet_stream_wait_bucket(unet_ctx* c, int b, unet_stream_t stream) {
+    ABI_TRY
     if (!c || b < 0 || b >= (int)c->bucket_ev.size()) return UNET_ERR_INVALID;
     if (hipStreamWaitEvent((hipStream_t)stream, c->bucket_ev[b], 0) != hipSuccess)
         return fail(c, UNET_ERR_HIP, "hipStreamWaitEvent");
     return UNET_OK;
+    ABI_CATCH(c)
 }
 
 int unet_timing_enable(unet_ctx* c, int en) {
+    ABI_TRY
     if (!c) return UNET_ERR_INVALID;
     c->timing = en != 0;
     return UNET_OK;
+    ABI_CATCH(c)
 }
 
 int unet_timing_filter(unet_ctx* c, const char* substring) {
+    ABI_TRY
     if (!c) return UNET_ERR_INVALID;
     c->tfilter = substring ? substring : "";
     return UNET_OK;
+    ABI_CATCH(c)
 }
 
 int unet_timing_reset(unet_ctx* c) {
+    ABI_TRY
     if (!c) return UNET_ERR_INVALID;
     c->trec.clear();
     c->ev_used = 0;
     return UNET_OK;
+    ABI_CATCH(c)
 }
 
 int unet_timing_count(unet_ctx* c, int* n) {
+    ABI_TRY
     if (!c || !n) return UNET_ERR_INVALID;
     *n = (int)c->trec.size();
     return UNET_OK;
+    ABI_CATCH(c)
 }
 
 int unet_timing_read(unet_ctx* c, int i, const char** family, int64_t* launches, double* total_ms,
                      double* flop) {
+    ABI_TRY
     if (!c || i < 0 || i >= (int)c->trec.size()) return UNET_ERR_INVALID;
     TimeRec& t = c->trec[i];
     if (hipEventSynchronize(t.b) != hipSuccess) return fail(c, UNET_ERR_HIP, "event sync");
@@ -1829,17 +1918,21 @@ int unet_timing_read(unet_ctx* c, int i, const char** family, int64_t* launches,
     if (total_ms) *total_ms = ms;
     if (flop) *flop = t.flop;
     return UNET_OK;
+    ABI_CATCH(c)
 }
 
 int unet_resize_plan(int in_size, int out_size, int32_t* coeffs, int32_t* bounds, int* ksize) {
+    ABI_TRY
     if (in_size < 1 || out_size < 1 || !ksize) return UNET_ERR_INVALID;
     *ksize = pil_resample_plan(in_size, out_size, coeffs, bounds);
     return UNET_OK;
+    ABI_CATCH((unet_ctx*)nullptr)
 }
 
 int unet_resize_u8(unet_ctx* c, const uint8_t* src, int h, int w, float* dst, int oh, int ow,
                    const int32_t* kh, const int32_t* bh, int ksh, const int32_t* kv,
                    const int32_t* bv, int ksv, float divisor, unet_stream_t stream) {
+    ABI_TRY
     if (!c || !src || !dst || h < 1 || w < 1 || oh < 1 || ow < 1 || !(divisor > 0.f))
         return UNET_ERR_INVALID;
     const int need_h = ow != w, need_v = oh != h;
@@ -1848,10 +1941,12 @@ int unet_resize_u8(unet_ctx* c, const uint8_t* src, int h, int w, float* dst, in
     int r = k_resize_u8(src, h, w, dst, oh, ow, kh, bh, ksh, kv, bv, ksv, need_h, need_v, divisor,
                         (hipStream_t)stream);
     return r ? fail(c, UNET_ERR_HIP, "resize launch %d", r) : UNET_OK;
+    ABI_CATCH(c)
 }
 
 int unet_debug_view(unet_ctx* c, int N, int H, int W, int training, int kind, int index,
                     int64_t* byte_offset, int64_t* count, int* ld, int* off) {
+    ABI_TRY
     if (!c || !byte_offset || !count) return UNET_ERR_INVALID;
     if (!shape_ok(c, N, H, W)) return fail(c, UNET_ERR_SHAPE, "bad shape");
     Plan p;
@@ -1898,6 +1993,7 @@ int unet_debug_view(unet_ctx* c, int N, int H, int W, int training, int kind, in
     if (ld) *ld = l;
     if (off) *off = o;
     return UNET_OK;
+    ABI_CATCH(c)
 }
 
 }  // extern "C"

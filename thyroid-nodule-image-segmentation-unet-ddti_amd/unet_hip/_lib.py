@@ -28,7 +28,8 @@ class HipError(RuntimeError):
 
 
 STATUS = {0: "UNET_OK", -1: "UNET_ERR_INVALID", -2: "UNET_ERR_SHAPE", -3: "UNET_ERR_HIP",
-          -4: "UNET_ERR_WORKSPACE", -5: "UNET_ERR_UNSUPPORTED"}
+          -4: "UNET_ERR_WORKSPACE", -5: "UNET_ERR_UNSUPPORTED", -6: "UNET_ERR_NOMEM",
+          -7: "UNET_ERR_INTERNAL"}
 
 c_int, c_int64, c_float, c_double, c_size_t = (ctypes.c_int, ctypes.c_int64, ctypes.c_float,
                                                 ctypes.c_double, ctypes.c_size_t)
@@ -62,12 +63,18 @@ SIGNATURES = {
                              c_size_t, c_int, c_int, c_int, c_int, c_void_p]),
     "unet_backward": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_int,
                               c_int, c_int, c_void_p]),
+    "unet_loss_stats": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                                c_void_p, c_void_p, c_void_p]),
+    "unet_loss_finalize": (c_int, [c_void_p, c_void_p, c_void_p, c_float, c_float, c_float,
+                                   c_void_p]),
     "unet_loss_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
-                              c_void_p, c_float, c_float, c_float, c_void_p]),
-    "unet_loss_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
                               c_void_p, c_void_p, c_float, c_float, c_float, c_void_p]),
+    "unet_loss_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
+                              c_void_p, c_void_p, c_void_p, c_float, c_float, c_float, c_void_p]),
     "unet_adamw": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int,
-                           c_float, c_float, c_float, c_float, c_float, c_float, c_void_p]),
+                           c_double, c_double, c_double, c_double, c_double, c_double, c_void_p]),
+    "unet_set_option": (c_int, [c_void_p, c_char_p, c_int64]),
+    "unet_get_option": (c_int, [c_void_p, c_char_p, P(c_int64)]),
     "unet_mask_counts": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p,
                                  c_void_p]),
     "unet_num_buckets": (c_int, [c_void_p, P(c_int)]),

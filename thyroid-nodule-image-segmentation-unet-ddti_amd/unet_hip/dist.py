@@ -1,14 +1,24 @@
 """Data-parallel training: one process per GPU, RCCL all-reduce of the flat gradient arena.
 
 Replaces the reference's single-process ``nn.DataParallel`` (utils/trainer.py:28-30), which
-re-broadcasts all 124 MB of parameters every forward and reduces gradients to GPU 0.
-Here every rank holds a full replica, parameters are broadcast ONCE from rank 0, each
-rank runs its shard of the batch with its own train-mode BatchNorm statistics (exactly
-DataParallel's per-replica BN), and after backward the gradient arena is summed with
-``torch.distributed.all_reduce`` (backend "nccl" == RCCL on ROCm, over xGMI).  The sum
-is turned into the mean (= the gradient of the full-batch loss with equal shards, since
-BCE-mean and the per-sample Dice mean are averages over the shards) inside the AdamW
-pass via ``grad_scale = 1 / world_size``.
+re-broadcasts all 124 MB of parameters every forward, gathers the logits on GPU 0, takes the
+loss of the gathered batch there and reduce-adds the replicas' gradients.  Here every rank
+holds a full replica, parameters are broadcast ONCE from rank 0, each rank runs its shard of
+the batch with its own train-mode BatchNorm statistics (exactly DataParallel's per-replica
+BN), and the two exchanges DataParallel implies are made explicit:
+
+* the loss: ``DistributedUNet.losses`` all-reduces the 8 batch sums of the fused loss
+  statistics (Σbce, Σdice_n, TP, Σp, Σt, samples, elements) before the finalize, so every
+  rank evaluates the loss of the gathered batch -- including FocalTversky, whose TP/FP/FN
+  are global (models/loss.py:41-45) -- and its dlogits are its slice of the gathered
+  batch's dlogits (any shard sizes);
+* the gradients: the ranks' gradient arenas are SUMMED with ``torch.distributed``
+  all-reduce (backend "nccl" == RCCL on ROCm, over xGMI), DataParallel's reduce-add.
+
+A caller that takes a per-rank LOCAL loss instead (plain ``seg_losses`` without a group)
+passes ``average=True``: the sum is then scaled by 1/world inside the AdamW pass
+(``grad_scale``), which equals the gathered-batch gradient for equal shards and
+shard-decomposable losses (BCE-mean, per-sample Dice), not for FocalTversky.
 
 Overlap: the native backward records one event per gradient bucket (decoder first,
 unet_bucket_range); ``reduce_gradients`` enqueues, on a side stream, "wait for bucket b"
@@ -36,9 +46,10 @@ class BucketReducer:
         self.stream = None
 
     def reduce(self, arena):
+        """Sum `arena` over the ranks in place; returns the world size."""
         ws = dist.get_world_size(self.group)
         if ws == 1:
-            return 1.0
+            return 1
         works = []
         if arena.is_cuda:
             if self.stream is None:
@@ -60,7 +71,7 @@ class BucketReducer:
                 works.append(dist.all_reduce(arena[off:off + n], group=self.group, async_op=True))
             for w in works:
                 w.wait()
-        return 1.0 / ws
+        return ws
 
 
 def broadcast_module(module, src=0, group=None):
@@ -71,11 +82,16 @@ def broadcast_module(module, src=0, group=None):
 
 
 class DistributedUNet:
-    """Wraps the HIP ``UNet`` for one-process-per-GPU data parallelism."""
+    """Wraps the HIP ``UNet`` for one-process-per-GPU data parallelism.
 
-    def __init__(self, model, optimizer=None, group=None):
+    ``losses(logits, targets)`` -> the [bce, dice, focal] of the GATHERED batch (same value
+    on every rank); after ``backward``, ``reduce_gradients()`` sums the gradient arenas.
+    ``average=True`` is for per-rank local losses (see the module docstring)."""
+
+    def __init__(self, model, optimizer=None, group=None, average=False):
         self.model = model
         self.group = group
+        self.average = average
         st = model.flatten_()
         broadcast_module(model, 0, group)
         rt = st.rt
@@ -85,14 +101,22 @@ class DistributedUNet:
     def __call__(self, x):
         return self.model(x)
 
+    def losses(self, logits, targets, alpha=0.4, beta=0.6, gamma=2.0):
+        from .functional import seg_losses
+        grp = self.group if self.group is not None else dist.group.WORLD
+        return seg_losses(logits, targets, alpha, beta, gamma, group=grp)
+
     def reduce_gradients(self):
+        """Sum (or, with average=True, average) the flat gradient arena over the ranks.
+        Returns the scale the optimizer applies to the summed gradients."""
         st = self.model._state
         p0 = st.params[0][0]
         arena = st.grad_arena
         if p0.grad is None or p0.grad.data_ptr() != arena.data_ptr():
             raise RuntimeError("gradients are not in the flat grad arena (accumulated grads are "
                                "not supported by the bucketed reducer)")
-        scale = self.reducer.reduce(arena)
+        ws = self.reducer.reduce(arena)
+        scale = 1.0 / ws if self.average else 1.0
         if self.optimizer is not None and hasattr(self.optimizer, "grad_scale"):
             self.optimizer.grad_scale = scale
         elif scale != 1.0:

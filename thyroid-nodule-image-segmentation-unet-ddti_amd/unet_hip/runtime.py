@@ -97,30 +97,54 @@ class UNetRuntime:
     def out_channels(self):
         return self.params[-1][1][0]
 
-    def loss_fwd(self, logits, targets, alpha=0.4, beta=0.6, gamma=2.0):
+    def loss_stats(self, logits, targets):
+        """Per-sample partials fp32[4N] and the batch sums fp64[8] (unet_loss_stats)."""
         N, C, H, W = logits.shape
-        stats = torch.empty(4 * N + 8, dtype=torch.float32, device=logits.device)
-        losses = torch.empty(3, dtype=torch.float32, device=logits.device)
-        rc = self.lib.unet_loss_fwd(self.ctx, _lib.ptr(logits), _lib.ptr(targets), N, C, H, W,
-                                    _lib.ptr(stats), _lib.ptr(losses), alpha, beta, gamma,
-                                    _lib.stream_ptr(logits.device))
-        _lib.check(rc, self.ctx, "unet_loss_fwd")
-        return losses, stats
+        stats = torch.empty(4 * N, dtype=torch.float32, device=logits.device)
+        sums = torch.empty(8, dtype=torch.float64, device=logits.device)
+        rc = self.lib.unet_loss_stats(self.ctx, _lib.ptr(logits), _lib.ptr(targets), N, C, H, W,
+                                      _lib.ptr(stats), _lib.ptr(sums), _lib.stream_ptr(logits.device))
+        _lib.check(rc, self.ctx, "unet_loss_stats")
+        return stats, sums
 
-    def loss_bwd(self, logits, targets, stats, w, alpha=0.4, beta=0.6, gamma=2.0):
+    def loss_finalize(self, sums, alpha=0.4, beta=0.6, gamma=2.0):
+        losses = torch.empty(3, dtype=torch.float32, device=sums.device)
+        rc = self.lib.unet_loss_finalize(self.ctx, _lib.ptr(sums), _lib.ptr(losses), alpha, beta,
+                                         gamma, _lib.stream_ptr(sums.device))
+        _lib.check(rc, self.ctx, "unet_loss_finalize")
+        return losses
+
+    def loss_fwd(self, logits, targets, alpha=0.4, beta=0.6, gamma=2.0):
+        stats, sums = self.loss_stats(logits, targets)
+        return self.loss_finalize(sums, alpha, beta, gamma), stats, sums
+
+    def loss_bwd(self, logits, targets, stats, sums, w, alpha=0.4, beta=0.6, gamma=2.0):
         N, C, H, W = logits.shape
         d = torch.empty_like(logits)
         rc = self.lib.unet_loss_bwd(self.ctx, _lib.ptr(logits), _lib.ptr(targets), N, C, H, W,
-                                    _lib.ptr(stats), _lib.ptr(w), _lib.ptr(d), alpha, beta, gamma,
-                                    _lib.stream_ptr(logits.device))
+                                    _lib.ptr(stats), _lib.ptr(sums), _lib.ptr(w), _lib.ptr(d), alpha,
+                                    beta, gamma, _lib.stream_ptr(logits.device))
         _lib.check(rc, self.ctx, "unet_loss_bwd")
         return d
 
     def adamw(self, params, grads, m, v, step, lr, beta1, beta2, eps, wd, grad_scale=1.0):
         rc = self.lib.unet_adamw(self.ctx, _lib.ptr(params), _lib.ptr(grads), _lib.ptr(m), _lib.ptr(v),
-                                 params.numel(), step, lr, beta1, beta2, eps, wd, grad_scale,
+                                 params.numel(), step, float(lr), float(beta1), float(beta2),
+                                 float(eps), float(wd), float(grad_scale),
                                  _lib.stream_ptr(params.device))
         _lib.check(rc, self.ctx, "unet_adamw")
+
+    # ------------------------------------------------------------------ schedule options
+    def set_option(self, name, value):
+        """Kernel-schedule option (include/unet_hip.h unet_set_option); A/B runs and tests."""
+        _lib.check(self.lib.unet_set_option(self.ctx, name.encode(), int(value)), self.ctx,
+                   f"unet_set_option({name})")
+
+    def get_option(self, name):
+        v = ctypes.c_int64()
+        _lib.check(self.lib.unet_get_option(self.ctx, name.encode(), ctypes.byref(v)), self.ctx,
+                   f"unet_get_option({name})")
+        return v.value
 
     def mask_counts(self, logits, targets, counts, mask=None):
         rc = self.lib.unet_mask_counts(self.ctx, _lib.ptr(logits), _lib.ptr(targets), logits.numel(),

@@ -87,20 +87,35 @@ class Trainer:
     # -------------------------------------------------------------- helpers
     def _losses(self, logits, masks):
         c = self.config
-        l = unet_hip.seg_losses(logits, masks, *self.focal_abg)
+        if self.ddp is not None:  # the gathered batch's losses (nn.DataParallel semantics)
+            l = self.ddp.losses(logits, masks, *self.focal_abg)
+        else:
+            l = unet_hip.seg_losses(logits, masks, *self.focal_abg)
         w = torch.tensor([c.bce_ratio, c.dice_ratio, c.focal_ratio], device=logits.device)
         loss = (w * l).sum()
         lb = torch.zeros((), device=logits.device)
         if c.boundary_ratio != 0:
-            lb = self.criterion_boundary(logits, masks)
-            loss = loss + c.boundary_ratio * lb
+            lb = self.criterion_boundary(logits, masks)  # mean over this rank's samples
+            if self.ddp is not None:
+                # gathered-batch mean (models/loss.py:66 divides by the full batch): weight
+                # the local mean by n_local / n_global; gradients are summed over ranks
+                n = torch.tensor([float(logits.shape[0])], device=logits.device)
+                dist.all_reduce(n)
+                lb = lb * (logits.shape[0] / float(n.item()))
+                loss = loss + c.boundary_ratio * lb
+                lb = lb.detach().clone()
+                dist.all_reduce(lb)
+            else:
+                loss = loss + c.boundary_ratio * lb
         return loss, l, lb
 
-    def _reduce_scalars(self, v):
+    def _reduce_scalars(self, sums, n_seen):
+        """Epoch means weighted like the reference's AverageMeter.update(loss, batch size)
+        over the gathered batches: sum Σ(l·b) and Σb over the ranks, then divide."""
+        v = torch.cat([sums, torch.tensor([float(n_seen)], dtype=sums.dtype, device=sums.device)])
         if _distributed():
             dist.all_reduce(v)
-            v /= dist.get_world_size()
-        return v
+        return v[:-1] / max(float(v[-1]), 1.0)
 
     def _reduce_counts(self, c):
         if _distributed():
@@ -152,7 +167,7 @@ class Trainer:
             sums += torch.stack([l[0], l[1], l[2], lb, loss]).detach().double() * bs
             n_seen += bs
             self.rt.mask_counts(logits.detach(), masks, counts)
-        totals = self._reduce_scalars(sums / max(n_seen, 1)).tolist()
+        totals = self._reduce_scalars(sums, n_seen).tolist()
         for m, v in zip(meters, totals):
             m.update(v, n_seen)
         return meters, self._reduce_counts(counts)

@@ -32,6 +32,14 @@ Fixtures (all float64 statistics computed from fp32 results):
   mod_c4_64.npz     models/mod.py UNet(base 128, depth 5) -- the config-4 architecture,
                     497,438,849 params -- at B=2 1x64x64, one step: full logits, losses,
                     grad norm/sum/samples.
+  unet_focal_64.npz the reference CLI's default loss mix (main.py:43-46: bce 1, dice 0,
+                    focal 1, boundary 0) with the real FocalTverskyLoss() (trainer.py:38),
+                    B=2 1x64x64, 3 AdamW steps (utils/trainer.py:81-93): full logits, the
+                    three loss terms, grad norm/sum/samples, param samples.
+  unet_dpf_64.npz   nn.DataParallel with FocalTversky in the loss (the loss of the gathered
+                    logits, global TP/FP/FN): eq_* B=4 in 2 shards of 2, ratios 1/0/1/0;
+                    uneq_* B=3 in shards of 2 and 1 (DataParallel's chunked scatter), ratios
+                    1/1/1/0.  Losses and grad norm/sum/samples.
 """
 import os
 import sys
@@ -46,6 +54,7 @@ sys.path.insert(0, REF)
 
 from models.model import UNet as RefUNet  # noqa: E402  (reference)
 from models.loss import DiceLoss as RefDice  # noqa: E402  (reference)
+from models.loss import FocalTverskyLoss as RefFocal  # noqa: E402  (reference, models/loss.py:26-46)
 from models.mod import UNet as RefModUNet  # noqa: E402  (reference, models/mod.py:9-66)
 from models.mod import ResUNet as RefResUNet  # noqa: E402  (reference, models/mod.py:88-131)
 
@@ -177,6 +186,76 @@ def case_dp2_64():
     np.savez_compressed(os.path.join(OUT, "unet_dp2_64.npz"), **out)
 
 
+def step_ratios(m, opt, x, t, w_bce, w_dice, w_focal):
+    """utils/trainer.py:81-93 with the reference's loss objects and weights (:85-90)."""
+    bce, dice, focal = torch.nn.BCEWithLogitsLoss(), RefDice(), RefFocal()
+    if opt is not None:
+        opt.zero_grad()
+    logits = m(x)
+    lb, ld, lf = bce(logits, t), dice(logits, t), focal(logits, t)
+    loss = w_bce * lb + w_dice * ld + w_focal * lf
+    loss.backward()
+    if opt is not None:
+        opt.step()
+    return logits.detach(), lb.item(), ld.item(), lf.item(), loss.item()
+
+
+def case_focal_64():
+    m = build()
+    m.train()
+    x = torch.from_numpy(W.make_input(21, 2, 1, 64, 64))
+    t = torch.from_numpy(W.make_target(21, 2, 64, 64))
+    opt = torch.optim.AdamW(m.parameters(), lr=1e-5)
+    out = dict(x=x.numpy(), t=t.numpy())
+    for s in range(3):
+        logits, lb, ld, lf, loss = step_ratios(m, opt, x, t, 1.0, 0.0, 1.0)
+        p = f"s{s}_"
+        out[p + "logits"] = logits.numpy()
+        out[p + "bce"], out[p + "dice"], out[p + "focal"], out[p + "loss"] = lb, ld, lf, loss
+        grad_stats(m, p, out)
+        out[p + "params_samp"] = param_samples(m)
+    np.savez_compressed(os.path.join(OUT, "unet_focal_64.npz"), **out)
+
+
+def dp_forward(m, x, shards):
+    """nn.DataParallel forward (utils/trainer.py:28-30): torch.chunk scatter, per-replica BN
+    (replica 0 keeps its running stats), logits gathered on dim 0."""
+    bns = [mod for mod in m.modules() if isinstance(mod, torch.nn.BatchNorm2d)]
+    bufs0 = [(b.running_mean.clone(), b.running_var.clone(), b.num_batches_tracked.clone()) for b in bns]
+    outs = []
+    for s, xs in enumerate(torch.chunk(x, shards, 0)):
+        if s > 0:
+            keep = [(b.running_mean, b.running_var, b.num_batches_tracked) for b in bns]
+            for b, (rm, rv, nb) in zip(bns, bufs0):
+                b.running_mean, b.running_var, b.num_batches_tracked = rm.clone(), rv.clone(), nb.clone()
+        outs.append(m(xs))
+        if s > 0:
+            for b, (rm, rv, nb) in zip(bns, keep):
+                b.running_mean, b.running_var, b.num_batches_tracked = rm, rv, nb
+    return torch.cat(outs, 0)
+
+
+def case_dp_focal_64():
+    out = {}
+    for tag, B, ratios, seed in (("eq_", 4, (1.0, 0.0, 1.0), 22), ("uneq_", 3, (1.0, 1.0, 1.0), 23)):
+        m = build()
+        m.train()
+        x = torch.from_numpy(W.make_input(seed, B, 1, 64, 64))
+        t = torch.from_numpy(W.make_target(seed, B, 64, 64))
+        logits = dp_forward(m, x, 2)
+        lb = torch.nn.BCEWithLogitsLoss()(logits, t)
+        ld = RefDice()(logits, t)
+        lf = RefFocal()(logits, t)
+        loss = ratios[0] * lb + ratios[1] * ld + ratios[2] * lf
+        loss.backward()
+        out[tag + "ratios"] = np.array(ratios)
+        out[tag + "bce"], out[tag + "dice"], out[tag + "focal"], out[tag + "loss"] = (
+            lb.item(), ld.item(), lf.item(), loss.item())
+        out[tag + "logits"] = logits.detach().numpy()
+        grad_stats(m, tag, out)
+    np.savez_compressed(os.path.join(OUT, "unet_dpf_64.npz"), **out)
+
+
 def case_neg_32():
     m = build(seed=5, gamma_lo=-1.0, gamma_hi=1.0)
     m.train()
@@ -282,6 +361,11 @@ def case_mod_c4_64():
 if __name__ == "__main__":
     torch.set_num_threads(8)
     os.makedirs(OUT, exist_ok=True)
+    only = sys.argv[1:]  # optional subset of case names, e.g. focal_64 dp_focal_64
+    if only:
+        for name in only:
+            globals()["case_" + name]()
+        sys.exit(0)
     case_b2_64()
     case_b2_256()
     case_dp2_64()
@@ -289,5 +373,7 @@ if __name__ == "__main__":
     case_mod_d3_64()
     case_res_d3_64()
     case_mod_c4_64()
+    case_focal_64()
+    case_dp_focal_64()
     for f in sorted(os.listdir(OUT)):
         print(f, os.path.getsize(os.path.join(OUT, f)))
