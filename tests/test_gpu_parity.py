@@ -305,8 +305,9 @@ def test_adamw_bitwise_vs_oracle(lr, wd, betas):
 
     * exp_avg and exp_avg_sq: bit-identical on every element;
     * params: bit-identical to the oracle's op sequence with a correctly rounded sqrt
-      (_IeeeSqrtAdamW) on every element, and within 1 ulp of the pure-torch oracle, whose
-      only differences are the elements where the host's sqrt is not correctly rounded."""
+      (_IeeeSqrtAdamW) on every element, and within 1 ulp (of the larger addend) of the
+      pure-torch oracle, whose only differences are the elements where the host's sqrt is
+      not correctly rounded."""
     import unet_hip
     n = (1 << 20) + 3
     gen = torch.Generator().manual_seed(int(lr * 1e6) + int(wd * 100))
@@ -341,13 +342,21 @@ def test_adamw_bitwise_vs_oracle(lr, wd, betas):
         assert torch.equal(got_p, P_ieee["a"]), \
             f"step {s}: {(got_p != P_ieee['a']).sum().item()} params differ from the IEEE-sqrt oracle"
         diff = got_p != P_ref["a"]
-        ulp = (got_p.view(torch.int32).long() - P_ref["a"].view(torch.int32).long()).abs()
-        assert int(ulp.max()) <= 1, f"step {s}: {int(ulp.max())} ulp"
         v = ref.v["a"]
-        host_sqrt_off = torch.sqrt(v) != torch.from_numpy(np.sqrt(v.numpy()))
+        hs, ies = torch.sqrt(v), torch.from_numpy(np.sqrt(v.numpy()))
+        host_sqrt_off = hs != ies
         assert bool(torch.all(host_sqrt_off[diff])), "a difference not explained by the host sqrt"
-        print(f"step {s}: {int(diff.sum())} of {n} params 1 ulp off the torch-CPU oracle "
-              f"(host sqrt inexact on {int(host_sqrt_off.sum())})")
+        # a k-ulp error of the host's sqrt is a relative error of k * 2^-23 in the denominator,
+        # so at most a few k * 2^-23 of the update u = p_new - p * decay (plus the final
+        # rounding of p_new): bound it at 8 k * 2^-23 |u| + 1 ulp of p_new
+        k = int((hs.view(torch.int32).long() - ies.view(torch.int32).long()).abs().max())
+        u = P_ieee["a"].double() - p.double() * (1 - lr * wd)
+        dp = (got_p.double() - P_ref["a"].double()).abs()
+        bound = 8 * k * 2.0 ** -23 * u.abs() + torch.from_numpy(np.spacing(P_ref["a"].abs().numpy())).double()
+        assert bool(torch.all(dp <= bound)), \
+            f"step {s}: {float((dp / bound).max()):.2f} x the bound, host sqrt up to {k} ulp"
+        print(f"step {s}: {int(diff.sum())} of {n} params differ from the torch-CPU oracle "
+              f"(host sqrt inexact on {int(host_sqrt_off.sum())}, by up to {k} ulp)")
         p = P_ieee["a"]
 
 

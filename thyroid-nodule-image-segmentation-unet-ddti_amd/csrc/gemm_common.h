@@ -93,7 +93,10 @@ __device__ __forceinline__ int gather_src(int tap, int m, Pix q, int H, int W, b
 // fixed order -- per lane over each 64-row unit's 32 rows in (mt, r) order, the two lane
 // halves combined, then unit 0 + unit 1 -- so a 128x128 tile (two 64-row waves), a 256x128
 // tile (four) and a 256x256 tile (two 128-row waves, two units each) produce bit-identical
-// partial rows, and the tile choice changes speed only (tests/test_gpu_mod.py).
+// partial rows, and the tile choice changes speed only (tests/test_gpu_mod.py).  The
+// squared terms are explicit fmas: left to -ffp-contract, hipcc fused them in some tile
+// instantiations and not in others (a 1-ulp invstd difference between 128- and 256-row
+// tiles, tools/diag_tile.py).
 // ------------------------------------------------------------------------------------
 // PRELOAD: the epilogues that read memory (E_STORE_BN, E_RESID, E_ADD) issue all 16 loads
 // of an accumulator first -- a load under `if (m < M)` makes hipcc wait for each one before
@@ -128,7 +131,7 @@ __device__ __forceinline__ void row_epilogue(const RowGemmArgs& p, f32x16 (&acc)
                         const float v = BR ? fmaxf(acc[mt][nt][r] + b, 0.f) : acc[mt][nt][r];
                         p.out[(size_t)m * p.ldo + p.ooff + n] = v;
                         s1[mt / 2][nt] += v;
-                        s2[mt / 2][nt] += v * v;
+                        s2[mt / 2][nt] = __builtin_fmaf(v, v, s2[mt / 2][nt]);
                     }
                 }
 #pragma unroll
@@ -187,7 +190,7 @@ __device__ __forceinline__ void row_epilogue(const RowGemmArgs& p, f32x16 (&acc)
                         if (emask && !(es * y + eb > 0.f)) v = 0.f;
                         p.out[(size_t)m * p.ldo + p.ooff + n] = v;
                         q[mt / 2][nt][0] += v;
-                        q[mt / 2][nt][1] += (double)v * y;
+                        q[mt / 2][nt][1] = __builtin_fma((double)v, (double)y, q[mt / 2][nt][1]);
                     }
                 }
 #pragma unroll
@@ -208,7 +211,7 @@ __device__ __forceinline__ void row_epilogue(const RowGemmArgs& p, f32x16 (&acc)
                     if (m < p.M) p.out[(size_t)m * p.ldo + p.ooff + n] = v;
                     v = m < p.M ? v : 0.f;
                     q[mt / 2][nt][0] += v;
-                    q[mt / 2][nt][1] += (double)v * y;
+                    q[mt / 2][nt][1] = __builtin_fma((double)v, (double)y, q[mt / 2][nt][1]);
                 }
             }
 #pragma unroll
