@@ -74,3 +74,24 @@ def test_boundary_loss_matches_reference_formula():
         d = torch.from_numpy(nd.distance_transform_edt(1 - t[b, 0].numpy().astype(np.uint8))).float()
         ref += torch.mean(torch.abs(torch.sigmoid(x[b, 0]) - t[b, 0]) * d)
     assert float(BoundaryLoss()(x, t)) == pytest.approx(float(ref / 2), rel=1e-6)
+
+
+def test_to_tensor_keeps_the_image_mode():
+    """utils/transforms.py ToTensor = TF.to_tensor per image: bands kept, u8 / 255."""
+    from PIL import Image
+    from data.data_loader import DecodeU8
+    from utils.transforms import ToTensor
+    rng = np.random.default_rng(4)
+    rgb = rng.integers(0, 256, (20, 30, 3), dtype=np.uint8)
+    gray = rng.integers(0, 256, (20, 30), dtype=np.uint8)
+    a, m = ToTensor()(Image.fromarray(rgb, "RGB"), Image.fromarray(gray, "L"))
+    assert a.shape == (3, 20, 30) and m.shape == (1, 20, 30)
+    assert torch.equal(a, torch.from_numpy(rgb).permute(2, 0, 1).float().div(255))
+    assert torch.equal(m[0], torch.from_numpy(gray).float().div(255))
+    bil = Image.fromarray(gray > 128).convert("1")
+    _, b = ToTensor()(bil, bil)
+    assert torch.equal(b[0], torch.from_numpy((gray > 128).astype(np.float32)))
+    u8 = DecodeU8()
+    assert np.array_equal(u8(bil, Image.fromarray(gray, "L"))[0], (gray > 128).astype(np.uint8) * 255)
+    with pytest.raises(ValueError):
+        u8(Image.fromarray(rgb, "RGB"), Image.fromarray(gray, "L"))

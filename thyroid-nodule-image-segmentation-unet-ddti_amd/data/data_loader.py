@@ -66,11 +66,24 @@ def create_dataloader(dataset, config, shuffle):
 
 
 class DecodeU8:
-    """Transform that only decodes: (PIL image, PIL mask) -> two (H, W) uint8 arrays."""
+    """Transform that only decodes: (PIL image, PIL mask) -> two (H, W) uint8 arrays.
+
+    The device pipeline is single-band: an 8-bit grayscale ("L") or bilevel ("1") file
+    gives the same tensor as the reference's TF.to_tensor; any other mode (e.g. RGB) would
+    give a multi-band tensor there, which the 1-channel networks reject, so it is refused
+    here too rather than silently converted."""
+
+    @staticmethod
+    def _plane(pic):
+        if pic.mode == "L":
+            return np.asarray(pic, dtype=np.uint8)
+        if pic.mode == "1":  # TF.to_tensor: {0, 1}; == "L" conversion (0/255) then / 255
+            return np.asarray(pic.convert("L"), dtype=np.uint8)
+        raise ValueError(f"image mode {pic.mode!r}: the device pipeline takes single-band 8-bit "
+                         f"images (TF.to_tensor would give a {len(pic.getbands())}-band tensor)")
 
     def __call__(self, img, mask):
-        return (np.asarray(img.convert("L"), dtype=np.uint8),
-                np.asarray(mask.convert("L"), dtype=np.uint8))
+        return self._plane(img), self._plane(mask)
 
 
 def u8_collate(batch):

@@ -32,13 +32,27 @@ class Resize:
         return img.resize((w, h), Image.BILINEAR), mask.resize((w, h), Image.BILINEAR)
 
 
+def _to_tensor(pic):
+    """torchvision TF.to_tensor for a PIL image (utils/transforms.py:152-156 calls it on
+    both the image and the mask): the image's OWN mode is kept -- (C, H, W) with C = the
+    mode's bands ("L" 1, "RGB" 3, ...); 8-bit data is divided by 255 (torch division),
+    mode "1" becomes {0, 1}; 16/32-bit integer and float modes are returned unscaled."""
+    nptype = {"I": np.int32, "I;16": np.int16, "F": np.float32}.get(pic.mode, np.uint8)
+    a = np.array(pic, dtype=nptype, copy=True)
+    if pic.mode == "1":
+        a = 255 * a.astype(np.uint8)
+    t = torch.from_numpy(a)
+    t = t.view(pic.size[1], pic.size[0], -1).permute(2, 0, 1).contiguous()
+    if t.dtype == torch.uint8:
+        return t.to(torch.float32).div(255)
+    return t
+
+
 class ToTensor:
-    """PIL -> float tensors in [0, 1]: image (C, H, W) grayscale, mask (1, H, W)."""
+    """PIL -> tensors exactly as the reference's ToTensor (TF.to_tensor of each)."""
 
     def __call__(self, img, mask):
-        a = np.asarray(img.convert("L"), dtype=np.float32) / 255.0
-        m = np.asarray(mask.convert("L"), dtype=np.float32) / 255.0
-        return torch.from_numpy(a[None].copy()), torch.from_numpy(m[None].copy())
+        return _to_tensor(img), _to_tensor(mask)
 
 
 def _unavailable(name):

@@ -12,11 +12,6 @@ timeout -k 10 300 python bench.py --steps 10 --warmup 3 --verbose > gpurun_out/$
 rc=$?
 echo "bench rc=$rc"; cat gpurun_out/$TAG.bench.json; grep -v amdgpu.ids gpurun_out/$TAG.bench.err | head -40
 if [ $rc -ne 0 ]; then exit $rc; fi
-if [ -n "${AB_ENV:-}" ]; then
-  # A/B: same bench with an alternative environment setting (e.g. AB_ENV=UNET_ROWGEMM_DBUF=0)
-  env $AB_ENV timeout -k 10 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --verbose > gpurun_out/$TAG.benchB.json 2> gpurun_out/$TAG.benchB.err
-  echo "bench B ($AB_ENV) rc=$?"; cat gpurun_out/$TAG.benchB.json
-fi
 if [ "${2:-}" = "prof" ] || [ "${3:-}" = "prof" ]; then
   cd /tmp && export TMPDIR=/tmp
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/$TAG.prof -o run --output-format csv -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $R/gpurun_out/$TAG.prof.log 2>&1
