@@ -547,7 +547,7 @@ def test_shapes_and_classes_vs_oracle(out_ch, B, H, W):
 
 @pytest.mark.parametrize("variant", ["model", "mod"])
 def test_wgrad_row3_matches_one_tap_tiles(variant):
-    """Option wgrad_row3=1 computes every eligible 3x3 weight gradient with the
+    """Option wgrad_row3=1 (the default) computes every eligible 3x3 weight gradient with the
     one-row-of-taps kernel (kernels_gemm.hip wgrad_row3_kernel: three taps per block from
     a halo-staged input row, a different split-K partition).  Same products, different
     summation grouping: every weight / bias gradient within 1e-5 norm-relative of the
@@ -570,7 +570,7 @@ def test_wgrad_row3_matches_one_tap_tiles(variant):
             (l[0] + l[1]).backward()
             torch.cuda.synchronize()
         finally:
-            rt.set_option("wgrad_row3", 0)
+            rt.set_option("wgrad_row3", 1)  # the default
         outs.append((logits.detach().clone(),
                      {k: p.grad.detach().clone() for k, p in m.named_parameters()}))
     assert torch.equal(outs[0][0], outs[1][0])

@@ -80,9 +80,12 @@ struct TimeRec {
 // explicitly through the ABI (never from the environment).  None of them changes the
 // numerics except where noted as bit-identical alternatives in DESIGN.md.
 struct Options {
-    int wgrad_row3 = 0;        // f32 3x3 wgrad on the one-row-of-taps kernel: 0 never,
-                               // 1 every eligible layer, 2 layers with a 64-channel operand
+    int wgrad_row3 = 1;        // f32 3x3 wgrad on the one-row-of-taps kernel: 0 never,
+                               // 1 every eligible layer (default: r02 A/B, conv wgrad
+                               // 27.1 -> 24.4 ms/step), 2 layers with a 64-channel operand
     int wgrad_row3_tile = -1;  // its tile (>= 20), -1 = by channel counts
+    int wgrad_row3_blocks = 1536;  // split-K target (blocks) of the row3 weight gradients
+                                   // (r02 sweep 512..2048: 1536 best, 391 vs 386 img/s)
     int wgrad_tile_w = 0;      // f32 wgrad tile, both channel counts multiples of 128
     int wgrad_tile_n = 7;      // ... 64-channel layers (64x64, 3 waves/SIMD)
     int wgrad16_tile = 0;      // register-staged bf16 wgrad tile (128-multiples)
@@ -108,6 +111,7 @@ struct OptionDesc {
 };
 const OptionDesc OPTION_TABLE[] = {
     {"wgrad_row3", &Options::wgrad_row3},       {"wgrad_row3_tile", &Options::wgrad_row3_tile},
+    {"wgrad_row3_blocks", &Options::wgrad_row3_blocks},
     {"wgrad_tile_w", &Options::wgrad_tile_w},   {"wgrad_tile_n", &Options::wgrad_tile_n},
     {"wgrad16_tile", &Options::wgrad16_tile},   {"tile_n128", &Options::tile_n128},
     {"tile_n128_dgrad", &Options::tile_n128_dgrad}, {"tile_n64", &Options::tile_n64},
@@ -441,7 +445,10 @@ WgradCfg wgrad_cfg(const unet_ctx* c, int CA, int tapsA, int CB, int tapsB, int6
     }
     const int64_t tiles =
         (int64_t)(tapsA * CA / (w.bm * wgrad_tile_taps(w.tile))) * (tapsB * CB / w.bn);
-    int64_t s = (2048 + tiles - 1) / tiles;
+    // blocks to launch: 2048 one-tap blocks; a row3 block does the work of three, and every
+    // extra split adds a full Mw x Nw slab to write and reduce
+    const int64_t target = w.tile >= 20 ? c->opt.wgrad_row3_blocks : 2048;
+    int64_t s = (target + tiles - 1) / tiles;
     const int64_t maxs = P / (8 * w.bkp) > 0 ? P / (8 * w.bkp) : 1;  // >= 8 chunks per split
     // (P need not be a multiple of the pixel chunk: the kernel zero-fills the tail)
     if (s > maxs) s = maxs;
