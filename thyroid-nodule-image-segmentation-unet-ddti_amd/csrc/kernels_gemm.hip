@@ -886,6 +886,8 @@ using RowTile9 = RowTile<128, 128, 64, 64, 16, true, 3>;
 using RowTile10 = RowTile<128, 128, 64, 64, 32, false, 3, true>;  // t7 + MFMA-phase priority
 using RowTile11 = RowTile<128, 128, 64, 64, 32, false, 1, true>;  // t4 + MFMA-phase priority
 using RowTile12 = RowTile<128, 64, 64, 32, 32, false, 1, true>;   // t1 + MFMA-phase priority
+// (r02: 256x128 with 4 waves of 128x64, 128x128 with 2 waves of 128x64 and 128x64 with 2
+// waves of 64x64 measured 3-17 % slower than these defaults; not kept)
 #define ROWGEMM_TILES(X) \
     X(0, RowTile0) X(1, RowTile1) X(2, RowTile2) X(3, RowTile3) X(4, RowTile4) X(5, RowTile5) \
     X(6, RowTile6) X(7, RowTile7) X(8, RowTile8) X(9, RowTile9) X(10, RowTile10)            \
