@@ -91,7 +91,9 @@ typedef struct {
     int in_channels;   /* models/model.py:6 / mod.py:11 in_channels (default 1; must be 1) */
     int out_channels;  /* models/model.py:6 / mod.py:12 out_channels (default 1; 1..4)   */
     int variant;       /* unet_variant (0 = models/model.py)                               */
-    int base_filters;  /* mod.py:13 (0 = default 64); a multiple of 64, <= 256             */
+    int base_filters;  /* mod.py:13 (0 = default 64); a multiple of 8, <= 256.  64 / 128 /
+                          256 run natively; other widths (the reference grid's 16 / 24 /
+                          32 / 48) run zero-padded to the next power of two >= 64 */
     int depth;         /* mod.py:14 (0 = default 5 for mod, 4 for model); 1..6             */
     int math;          /* unet_math of the conv GEMMs (0 = f32)                            */
 } unet_cfg;

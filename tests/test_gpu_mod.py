@@ -307,3 +307,81 @@ def test_mod_bf16_matches_bf16_oracle(base, depth, tile):
     assert errs[worst] <= env, f"{worst}: {errs[worst]:.3e}"
     # and bf16 stays a bf16-sized perturbation of the fp32 network
     assert e_l32 <= 5e-2
+
+
+# ---------------------------------------------------------------- narrow widths (padded)
+def test_mod_narrow_b32_matches_golden(golden_dir):
+    """The reference grid's narrow widths (config/config.yaml: base_filters 16 / 24 / 32 /
+    48): mod.py UNet(base 32, depth 4) runs with every level zero-padded to 64 / 128 / ...
+    inside the library.  Two AdamW steps vs the reference's own outputs
+    (tests/golden/mod_narrow_64.npz) at the usual bars, the running statistics, and the
+    eval-mode path from the resynced state."""
+    import unet_hip
+    f = _golden(golden_dir, "mod_narrow_64.npz")
+    m = hip_mod_model(MO.make_params(42, 32, 4), DEV, 32, 4)
+    opt = unet_hip.HipAdamW(m.parameters(), lr=1e-4)
+    x = torch.from_numpy(Wt.make_input(31, 2, 1, 64, 64)).to(DEV)
+    t = torch.from_numpy(Wt.make_target(31, 2, 64, 64)).to(DEV)
+    spec = MO.param_spec(1, 1, 32, 4)
+    names = [n for n, _ in MO.bn_layers(32, 4)]
+    for s in range(2):
+        p = f"b32_s{s}_"
+        tol = LOGIT_TOL if s == 0 else 2e-3
+        logits, losses = _step(m, opt, x, t)
+        assert rel_max(logits.cpu().numpy(), f[p + "logits"]) <= tol, f"{p} logits"
+        assert abs((losses[0] + losses[1]).item() - float(f[p + "loss"])) <= (1e-5 if s == 0 else 1e-4)
+        _check_grad_stats(m, spec, f[p + "grad_norm"], f[p + "grad_samp"],
+                          GRAD_TOL if s == 0 else 10 * GRAD_TOL, p)
+        sd = m.state_dict()
+        rm = torch.cat([sd[f"{n}.running_mean"].cpu() for n in names]).numpy()
+        rv = torch.cat([sd[f"{n}.running_var"].cpu() for n in names]).numpy()
+        btol = 1e-4 if s == 0 else 1e-3
+        np.testing.assert_allclose(rm, f[p + "running_mean"], rtol=btol, atol=btol)
+        np.testing.assert_allclose(rv, f[p + "running_var"], rtol=btol, atol=btol)
+    check_eval(m, MO.make_forward(4), x.cpu(), t.cpu())
+
+
+@pytest.mark.parametrize("tag,base", [("u24_", 24), ("u48_", 48)])
+def test_mod_narrow_one_step_matches_golden(golden_dir, tag, base):
+    import unet_hip
+    f = _golden(golden_dir, "mod_narrow_64.npz")
+    m = hip_mod_model(MO.make_params(42, base, 3), DEV, base, 3)
+    x = torch.from_numpy(Wt.make_input(31, 2, 1, 64, 64)).to(DEV)
+    t = torch.from_numpy(Wt.make_target(31, 2, 64, 64)).to(DEV)
+    logits = m(x)
+    losses = unet_hip.seg_losses(logits, t)
+    (losses[0] + losses[1]).backward()
+    assert rel_max(logits.detach().cpu().numpy(), f[tag + "logits"]) <= LOGIT_TOL
+    assert abs((losses[0] + losses[1]).item() - float(f[tag + "loss"])) <= 1e-5
+    _check_grad_stats(m, MO.param_spec(1, 1, base, 3), f[tag + "grad_norm"], f[tag + "grad_samp"],
+                      GRAD_TOL, tag)
+
+
+@pytest.mark.parametrize("base,depth,H,W", [(16, 5, 64, 96), (24, 4, 128, 64), (48, 6, 128, 128)])
+def test_mod_narrow_full_grads_vs_fp64(base, depth, H, W):
+    """Every gradient element of narrow networks (padded inside the library) against the
+    fp64 oracle, within 2x the fp32 oracle's own error (floor 1e-2), and the padding is
+    invisible in the caller's arenas (torch-layout gradients, running stats)."""
+    import unet_hip
+    P = MO.make_params(7, base, depth)
+    x, t = inputs(33, 2, H, W)
+    ref = MO.train_step(P, MO.init_buffers(base, depth), None, x, t, depth=depth)
+    r64 = MO.train_step({k: v.double() for k, v in P.items()},
+                        {k: (v.double() if v.is_floating_point() else v.clone())
+                         for k, v in MO.init_buffers(base, depth).items()},
+                        None, x.double(), t.double(), depth=depth)
+    m = hip_mod_model(P, DEV, base, depth)
+    logits = m(x.to(DEV))
+    losses = unet_hip.seg_losses(logits, t.to(DEV))
+    (losses[0] + losses[1]).backward()
+    assert rel_max(logits.detach().cpu().numpy(), ref["logits"].numpy()) <= LOGIT_TOL
+    e32 = {k: norm_rel(g, r64["grads"][k]) for k, g in ref["grads"].items()}
+    env = max(2 * max(e32.values()), GRAD_TOL)
+    errs = grad_errors(m, r64["grads"])
+    worst = max(errs, key=errs.get)
+    assert errs[worst] <= env, f"{worst}: {errs[worst]:.3e} (fp32 oracle {e32[worst]:.3e})"
+    Bref = MO.init_buffers(base, depth)
+    MO.make_forward(depth)(x, P, Bref, True)
+    for k, v in m.named_buffers():
+        if v.is_floating_point():
+            np.testing.assert_allclose(v.cpu().numpy(), Bref[k].numpy(), rtol=1e-4, atol=1e-5, err_msg=k)

@@ -114,3 +114,22 @@ def test_res_full_grads_vs_oracle(base, depth, size):
     errs = grad_errors(m, r64["grads"])
     worst = max(errs, key=errs.get)
     assert errs[worst] <= env, f"{worst}: {errs[worst]:.3e} (fp32 oracle {e32[worst]:.3e})"
+
+
+def test_res_narrow_b16_matches_golden(golden_dir):
+    """ResUNet(base 16, depth 3) -- the smallest width of the reference grid -- one step vs
+    tests/golden/mod_narrow_64.npz (channels zero-padded to 64 inside the library)."""
+    import unet_hip
+    f = np.load(os.path.join(golden_dir, "mod_narrow_64.npz"), allow_pickle=False)
+    m = _model(MO.res_make_params(42, 16, 3), 16, 3)
+    x = torch.from_numpy(Wt.make_input(31, 2, 1, 64, 64)).to(DEV)
+    t = torch.from_numpy(Wt.make_target(31, 2, 64, 64)).to(DEV)
+    logits = m(x)
+    losses = unet_hip.seg_losses(logits, t)
+    (losses[0] + losses[1]).backward()
+    assert rel_max(logits.detach().cpu().numpy(), f["r16_logits"]) <= LOGIT_TOL
+    assert abs((losses[0] + losses[1]).item() - float(f["r16_loss"])) <= 1e-5
+    for ti, (name, p) in enumerate(m.named_parameters()):
+        n = p.grad.detach().double().norm().item()
+        assert abs(n - f["r16_grad_norm"][ti]) <= GRAD_TOL * f["r16_grad_norm"][ti], name
+    check_eval(m, MO.make_res_forward(3), x.cpu(), t.cpu())

@@ -137,7 +137,10 @@ def test_init_consumes_rng_like_reference():
 
 
 # ---------------------------------------------------------------- models/mod.py:UNet
-MOD_CFGS = [(64, 3), (64, 5), (128, 5)]
+# 64 / 128 run natively; 16 / 24 / 32 / 48 are the reference grid's narrow widths
+# (config/config.yaml), run zero-padded inside the library with torch-layout tables
+MOD_CFGS = [(64, 3), (64, 5), (128, 5), (16, 3), (16, 5), (24, 4), (24, 6), (32, 3), (32, 5),
+            (48, 4), (48, 6)]
 
 
 def _mod_rt(base, depth):
@@ -184,9 +187,11 @@ def test_mod_config4_workspace():
 def test_unsupported_configs_rejected():
     from unet_hip import _lib
     from unet_hip.runtime import UNetRuntime
-    for args in [(1, 1, _lib.VARIANT_MOD, 32, 5), (1, 1, _lib.VARIANT_MODEL, 64, 5),
+    for args in [(1, 1, _lib.VARIANT_MOD, 20, 4), (1, 1, _lib.VARIANT_MODEL, 64, 5),
                  (3, 1, _lib.VARIANT_MOD, 64, 4), (1, 1, 7, 64, 4),
-                 (1, 1, _lib.VARIANT_MOD, 192, 4)]:
+                 (1, 1, _lib.VARIANT_MOD, 512, 4), (1, 1, _lib.VARIANT_MOD, 48, 7),
+                 (1, 1, _lib.VARIANT_MODEL, 32, 4),
+                 (1, 1, _lib.VARIANT_MOD, 48, 4, _lib.MATH_BF16)]:
         with pytest.raises(_lib.HipError):
             UNetRuntime("cuda:0", *args)
 
@@ -224,6 +229,19 @@ def test_bf16_math_only_for_mod_variant():
     a = UNetRuntime("cuda:0", 1, 1, _lib.VARIANT_MOD, 128, 5, _lib.MATH_BF16)
     b = _mod_rt(128, 5)
     assert a.params == b.params and a.bn == b.bn and a.buckets == b.buckets
+
+
+@pytest.mark.parametrize("base,depth", [(16, 4), (24, 3), (48, 5)])
+def test_res_narrow_tables(base, depth):
+    from unet_hip import _lib
+    from unet_hip.runtime import UNetRuntime
+    from oracle import mod_ref_cpu as MO
+    rt = UNetRuntime.get("cuda:0", 1, 1, _lib.VARIANT_RES, base, depth)
+    spec = MO.res_param_spec(1, 1, base, depth)
+    assert [(p[0], tuple(p[1])) for p in rt.params] == [(s[0], tuple(s[1])) for s in spec]
+    assert [(b[0], b[1]) for b in rt.bn] == MO.res_bn_layers(base, depth)
+    assert rt.n_param_floats == sum(int(np.prod(s[1])) for s in spec)
+    assert rt.workspace_bytes(2, 64, 64, True) > 0
 
 
 def test_res_tables_and_rng_like_reference():

@@ -238,3 +238,41 @@ def test_oracle_dataparallel_focal(golden_dir, tag, B, seed):
         assert abs(r[k].item() - float(f[tag + k])) < 1e-6, k
     _check_grads(_grad_stats(r["grads"], O.param_spec()), f[tag + "grad_norm"],
                  f[tag + "grad_sum"], f[tag + "grad_samp"], rtol=1e-4)
+
+
+def test_oracle_mod_narrow_widths(golden_dir):
+    """The reference grid's narrow widths (config/config.yaml): mod.py UNet(32, 4) over two
+    AdamW steps, UNet(24, 3), UNet(48, 3) and ResUNet(16, 3) one step each."""
+    from oracle import mod_ref_cpu as MO
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    f = _load(golden_dir, "mod_narrow_64.npz")
+    x = torch.from_numpy(W.make_input(31, 2, 1, 64, 64))
+    t = torch.from_numpy(W.make_target(31, 2, 64, 64))
+    P = MO.make_params(42, 32, 4)
+    B = MO.init_buffers(32, 4)
+    opt = O.AdamWState(P, lr=1e-4)
+    names = [n for n, _ in MO.bn_layers(32, 4)]
+    for s in range(2):
+        p = f"b32_s{s}_"
+        r = MO.train_step(P, B, opt, x, t, depth=4)
+        ref = f[p + "logits"]
+        assert np.max(np.abs(r["logits"].numpy() - ref)) <= 1e-5 * np.max(np.abs(ref))
+        assert abs(r["loss"].item() - float(f[p + "loss"])) < 1e-6
+        _check_grads(_grad_stats(r["grads"], MO.param_spec(1, 1, 32, 4)), f[p + "grad_norm"],
+                     f[p + "grad_sum"], f[p + "grad_samp"], rtol=1e-4)
+        rm = np.concatenate([B[f"{n}.running_mean"].numpy() for n in names])
+        np.testing.assert_allclose(rm, f[p + "running_mean"], rtol=1e-5, atol=1e-6)
+    with torch.no_grad():
+        ev = MO.make_forward(4)(x, P, B, training=False).numpy()
+    assert np.max(np.abs(ev - f["b32_eval_logits"])) <= 1e-5 * np.max(np.abs(f["b32_eval_logits"]))
+    for tag, base in (("u24_", 24), ("u48_", 48)):
+        r = MO.train_step(MO.make_params(42, base, 3), MO.init_buffers(base, 3), None, x, t, depth=3)
+        assert np.max(np.abs(r["logits"].numpy() - f[tag + "logits"])) <= 1e-5 * np.max(np.abs(f[tag + "logits"]))
+        assert abs(r["loss"].item() - float(f[tag + "loss"])) < 1e-6
+        _check_grads(_grad_stats(r["grads"], MO.param_spec(1, 1, base, 3)), f[tag + "grad_norm"],
+                     f[tag + "grad_sum"], f[tag + "grad_samp"], rtol=1e-4)
+    r = MO.res_train_step(MO.res_make_params(42, 16, 3), MO.res_init_buffers(16, 3), None, x, t, depth=3)
+    assert np.max(np.abs(r["logits"].numpy() - f["r16_logits"])) <= 1e-5 * np.max(np.abs(f["r16_logits"]))
+    assert abs(r["loss"].item() - float(f["r16_loss"])) < 1e-6
+    _check_grads(_grad_stats(r["grads"], MO.res_param_spec(1, 1, 16, 3)), f["r16_grad_norm"],
+                 f["r16_grad_sum"], f["r16_grad_samp"], rtol=1e-4)

@@ -63,6 +63,17 @@ int k_res_first_wgrad(const float* x, const float* du, int P, int C, float* part
 int k_resize_u8(const uint8_t* src, int H, int W, float* dst, int OH, int OW, const int* kh,
                 const int* bh, int ksh, const int* kv, const int* bv, int ksv, int need_h,
                 int need_v, float divisor, hipStream_t s);
+// Channel padding (runtime.hip, unet_ctx::padded): one tensor of the caller's torch-layout
+// arena (roff) and of the padded arena (poff).  Dim k holds nseg[k] segments of seg[k] real
+// entries, each padded to pseg[k] entries (unused dims: 1, 1, 1).
+struct PadDesc {
+    int64_t roff, poff, rnumel, pnumel;
+    int32_t seg[4], pseg[4], nseg[4];
+};
+// expand = 1: dst (padded) <- src (torch layout), zeros in the padding;
+// expand = 0: dst (torch layout) <- src (padded).  table: device copy of n descriptors.
+int k_pad_copy(const PadDesc* table, int n, int64_t max_numel, const float* src, float* dst,
+               int expand, hipStream_t s);
 // Losses: per-sample stats fp32[4N] + batch sums fp64[8] (see kernels_misc.hip)
 int k_loss_stats(const float* x, const float* t, int N, int64_t per, float* stats, double* sums,
                  hipStream_t s);

@@ -1592,12 +1592,64 @@ int k_nchw_to_nhwc(const float* x, int N, int C, int HW, float* y, hipStream_t s
 }
 
 namespace {
+// one tensor per blockIdx.y; grid-stride over its padded (expand) or real (compact) elements
+__global__ __launch_bounds__(256) void pad_copy_kernel(const PadDesc* __restrict__ table,
+                                                       const float* __restrict__ src,
+                                                       float* __restrict__ dst, int expand) {
+    const PadDesc d = table[blockIdx.y];
+    int64_t rd[4], pd[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        rd[k] = (int64_t)d.seg[k] * d.nseg[k];
+        pd[k] = (int64_t)d.pseg[k] * d.nseg[k];
+    }
+    const int64_t n = expand ? d.pnumel : d.rnumel;
+    for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < n;
+         j += (int64_t)gridDim.x * blockDim.x) {
+        // decode j over the (padded or real) dims, innermost last
+        int64_t rem = j, ridx = 0, pidx = 0, rstride = 1, pstride = 1;
+        bool valid = true;
+#pragma unroll
+        for (int k = 3; k >= 0; --k) {
+            const int64_t ext = expand ? pd[k] : rd[k];
+            const int64_t i = rem % ext;
+            rem /= ext;
+            int64_t sg, w;
+            if (expand) {
+                sg = i / d.pseg[k];
+                w = i - sg * d.pseg[k];
+                valid = valid && w < d.seg[k];
+            } else {
+                sg = i / d.seg[k];
+                w = i - sg * d.seg[k];
+            }
+            ridx += (sg * d.seg[k] + w) * rstride;
+            pidx += (sg * d.pseg[k] + w) * pstride;
+            rstride *= rd[k];
+            pstride *= pd[k];
+        }
+        if (expand)
+            dst[d.poff + j] = valid ? src[d.roff + ridx] : 0.f;
+        else
+            dst[d.roff + j] = src[d.poff + pidx];
+    }
+}
+
 __global__ void fill_kernel(float* __restrict__ p, int64_t n, float v) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * blockDim.x)
         p[i] = v;
 }
 }  // namespace
+int k_pad_copy(const PadDesc* table, int n, int64_t max_numel, const float* src, float* dst,
+               int expand, hipStream_t s) {
+    if (n <= 0) return 0;
+    const int64_t nb = (max_numel + 255) / 256;
+    const unsigned bx = (unsigned)(nb < 1024 ? nb : 1024);
+    hipLaunchKernelGGL(pad_copy_kernel, dim3(bx > 0 ? bx : 1, n), dim3(256), 0, s, table, src, dst,
+                       expand);
+    LAUNCH_CHECK();
+}
 int k_fill(float* p, int64_t n, float v, hipStream_t s) {
     hipLaunchKernelGGL(fill_kernel, dim3(grid_for(n)), dim3(256), 0, s, p, n, v);
     LAUNCH_CHECK();

@@ -44,12 +44,19 @@ inline int wide_g(int64_t P) { return (int)std::min<int64_t>(WIDE_G, std::max<in
 constexpr int STAT_G = 256;           // second level of the BN-stat reduction
 constexpr int MAX_DEPTH = 6;
 
+// A parameter tensor.  shape / off / numel describe the torch tensor in the caller's flat
+// arena (what unet_param_info reports); poff / pshape the same tensor in the context's
+// channel-padded arena (== the torch layout unless the network is padded, see
+// unet_ctx::padded).  Padded dims are segmented: dim k holds nseg[k] segments of seg[k]
+// real entries, each padded to pseg[k] (2 segments for a concat input [skip | up]).
 struct ParamT {
     std::string name;
     int ndim;
     int64_t shape[4];
     int64_t off, numel;
     int stage;           // backward stage after which its gradient is final
+    int64_t poff, pnumel;
+    int64_t seg[4], pseg[4], nseg[4];
 };
 
 struct ConvL {
@@ -58,9 +65,11 @@ struct ConvL {
     int64_t pf, pd;      // packed weight offsets (floats) inside the pack region
 };
 struct BnL {
-    int C;
-    int64_t g, b;        // gamma / beta param offsets
-    int64_t run;         // running_mean offset in the bn arena (var at run + C)
+    int C;               // channels the kernels see (padded)
+    int rC;              // channels of the torch module (running stats, gamma, beta)
+    int64_t g, b;        // gamma / beta offsets in the (padded) parameter arena
+    int64_t run;         // running_mean offset in the (padded) bn arena (var at run + C)
+    int64_t rrun;        // ... in the caller's bn arena (var at rrun + rC)
     std::string name;
 };
 struct ConvTL {
@@ -129,20 +138,33 @@ struct unet_ctx {
     int device = 0;
     int in_ch = 1, out_ch = 1;
     int variant = UNET_VARIANT_MODEL;
-    int base = 64, depth = 4;
+    int base = 64, depth = 4;  // base: channels of level 0 as the kernels see them (padded)
+    int rbase = 64;            // base_filters of the reference module (models/mod.py:13)
+    // Narrow networks (base_filters 16 / 24 / 32 / 48 of the reference's model grid,
+    // config/config.yaml) run with every level's channels zero-padded to the next power of
+    // two >= 64, the widths the GEMM tiles and channel-quad kernels are built for.  The
+    // caller's arenas keep the torch layouts; unet_forward / unet_backward expand them
+    // into padded arenas in the workspace (zeros in the padding: zero weights, gamma,
+    // beta, so padded channels stay exactly 0 through BN / ReLU / pooling / ConvT / the
+    // head and add +0 to every real sum) and compact the running stats and gradients back.
+    bool padded = false;
     bool bn_relu = false;    // BN -> ReLU (mod.py) instead of ReLU -> BN (model.py)
     bool skip_first = false; // concat [skip, up] (mod.py) instead of [up, skip] (model.py)
     bool bf16 = false;       // conv GEMMs on bf16 MFMA (f32 accumulate), BASELINE config 4
     bool res = false;        // residual blocks (mod.py:ResUNet): block outputs materialised
     std::vector<ParamT> params;
-    int64_t n_param_floats = 0;
+    int64_t n_param_floats = 0;   // caller's (torch-layout) arena
+    int64_t n_pparam_floats = 0;  // padded arena (== n_param_floats unless padded)
     std::vector<ConvL> conv;
     std::vector<BnL> bn;
     std::vector<ConvTL> convt;
     std::vector<int64_t> skip_w, skip_pd;  // per block: 1x1 skip weight, its dgrad image
     int64_t head_w = 0, head_b = 0;
-    int64_t n_bn_floats = 0;
+    int64_t n_bn_floats = 0;      // caller's running-stat arena
+    int64_t n_pbn_floats = 0;     // padded
     int64_t pack_floats = 0;
+    std::vector<PadDesc> pad_params, pad_bn;  // expand / compact tables (padded only)
+    int64_t pad_max_numel = 0, pad_bn_max = 0;
     int cmax = 0;
     std::string err;
     // buckets (DP overlap): contiguous grad ranges, ready after backward stage bucket_stage
@@ -162,7 +184,8 @@ struct unet_ctx {
     Options opt;
 
     int nconv() const { return (int)conv.size(); }
-    int ch(int level) const { return base << level; }
+    int ch(int level) const { return base << level; }     // kernel (padded) channels
+    int rch(int level) const { return rbase << level; }   // torch module channels
     int up_off(int l) const { return skip_first ? ch(l) : 0; }    // CAT_l channel offsets
     int skip_off(int l) const { return skip_first ? 0 : ch(l); }
 };
@@ -202,36 +225,62 @@ int fail(unet_ctx* c, int code, const char* fmt, ...) {
 
 // Parameter table in the reference's named_parameters() order, layer tables, packing
 // offsets and gradient buckets.
+// One dimension of a parameter tensor: nseg segments of seg real entries, each padded to
+// pseg entries (nseg = 2 for the [skip | up] concat input of a decoder block).
+struct Dim {
+    int64_t seg, pseg, nseg;
+};
+
 void build_graph(unet_ctx* c) {
     const int D = c->depth;
     const int nb = 2 * D + 1;
     c->conv.assign(2 * nb, ConvL{});
     c->bn.assign(2 * nb, BnL{});
     c->convt.assign(D, ConvTL{});
-    int64_t off = 0;
-    auto add = [&](const std::string& name, std::initializer_list<int64_t> shape, int stage) {
+    c->params.clear();
+    int64_t off = 0, poff = 0;
+    // returns the tensor's offset in the padded arena (what the kernels index)
+    auto add = [&](const std::string& name, std::initializer_list<Dim> dims, int stage) {
         ParamT p;
         p.name = name;
-        p.ndim = (int)shape.size();
+        p.ndim = (int)dims.size();
         p.numel = 1;
+        p.pnumel = 1;
         int i = 0;
-        for (int64_t s : shape) {
-            p.shape[i++] = s;
-            p.numel *= s;
+        for (const Dim& d : dims) {
+            p.shape[i] = d.seg * d.nseg;
+            p.seg[i] = d.seg;
+            p.pseg[i] = d.pseg;
+            p.nseg[i] = d.nseg;
+            p.numel *= d.seg * d.nseg;
+            p.pnumel *= d.pseg * d.nseg;
+            ++i;
         }
-        for (; i < 4; ++i) p.shape[i] = 0;
+        for (; i < 4; ++i) {
+            p.shape[i] = 0;
+            p.seg[i] = p.pseg[i] = p.nseg[i] = 1;
+        }
         p.off = off;
+        p.poff = poff;
         p.stage = stage;
         off += p.numel;
+        poff += p.pnumel;
         c->params.push_back(p);
-        return p.off;
+        return p.poff;
     };
     auto level_of = [&](int b) { return b <= D ? b : 2 * D - b; };
-    auto block_cin = [&](int b) {
+    auto lvl = [&](int l) { return Dim{c->rch(l), c->ch(l), 1}; };  // one level's channels
+    auto block_cin = [&](int b) {  // kernel (padded) input channels of block b
         if (b == 0) return c->in_ch;
         if (b <= D) return c->ch(b - 1);
         return 2 * c->ch(level_of(b));
     };
+    auto block_in_dim = [&](int b) {  // the same as a torch dimension
+        if (b == 0) return Dim{c->in_ch, c->in_ch, 1};
+        if (b <= D) return lvl(b - 1);
+        return Dim{c->rch(level_of(b)), c->ch(level_of(b)), 2};  // concat of two halves
+    };
+    const Dim k3{3, 3, 1}, k2{2, 2, 1}, k1{1, 1, 1};
     // backward stage after which a block's gradients are final: 0 = head + last decoder,
     // then ConvT k together with block D+k (k = D-1 .. 0), then the encoders
     auto stage_of_block = [&](int b) { return 2 * D - b; };
@@ -246,18 +295,20 @@ void build_graph(unet_ctx* c) {
         L.which = which;
         BnL& B = c->bn[i];
         B.C = L.cout;
+        B.rC = c->rch(L.level);
+        const Dim dout = lvl(L.level), din = which == 0 ? block_in_dim(b) : dout;
         const int st = stage_of_block(b);
         const std::string cp = c->res ? pfx + ".conv" : pfx;  // ResidualBlock.conv (mod.py:75)
-        L.w = add(cp + (which ? ".3.weight" : ".0.weight"), {L.cout, L.cin, 3, 3}, st);
+        L.w = add(cp + (which ? ".3.weight" : ".0.weight"), {dout, din, k3, k3}, st);
         if (c->variant == UNET_VARIANT_MODEL) {  // model.py:33-43: 0 conv, 2 BN, 3 conv, 5 BN
-            L.b = add(pfx + (which ? ".3.bias" : ".0.bias"), {L.cout}, st);
+            L.b = add(pfx + (which ? ".3.bias" : ".0.bias"), {dout}, st);
             B.name = pfx + (which ? ".5" : ".2");
         } else {  // mod.py:43-51 / :75-81: 0 conv (no bias), 1 BN, 3 conv, 4 BN
             L.b = -1;
             B.name = cp + (which ? ".4" : ".1");
         }
-        B.g = add(B.name + ".weight", {L.cout}, st);
-        B.b = add(B.name + ".bias", {L.cout}, st);
+        B.g = add(B.name + ".weight", {dout}, st);
+        B.b = add(B.name + ".bias", {dout}, st);
     };
     c->skip_w.assign(nb, -1);
     c->skip_pd.assign(nb, -1);
@@ -265,7 +316,7 @@ void build_graph(unet_ctx* c) {
         conv_pair(b, 0, pfx);
         conv_pair(b, 1, pfx);
         if (c->res)  // ResidualBlock.skip, Conv2d(in, out, 1, bias=False) (mod.py:83)
-            c->skip_w[b] = add(pfx + ".skip.weight", {c->conv[2 * b].cout, c->conv[2 * b].cin, 1, 1},
+            c->skip_w[b] = add(pfx + ".skip.weight", {lvl(level_of(b)), block_in_dim(b), k1, k1},
                                stage_of_block(b));
     };
     auto convT = [&](int k, const std::string& name) {
@@ -274,9 +325,10 @@ void build_graph(unet_ctx* c) {
         T.cin = c->ch(D - k);
         T.cout = c->ch(D - k - 1);
         const int st = stage_of_block(D + k);
-        T.w = add(name + ".weight", {T.cin, T.cout, 2, 2}, st);
-        T.b = add(name + ".bias", {T.cout}, st);
+        T.w = add(name + ".weight", {lvl(D - k), lvl(D - k - 1), k2, k2}, st);
+        T.b = add(name + ".bias", {lvl(D - k - 1)}, st);
     };
+    const Dim dout_head{c->out_ch, c->out_ch, 1};
     if (c->variant == UNET_VARIANT_MODEL) {
         // models/model.py:6-31 registration order (D = 4, base 64)
         const char* bname[9] = {"encoder1", "encoder2", "encoder3", "encoder4", "middle.1",
@@ -287,24 +339,51 @@ void build_graph(unet_ctx* c) {
             convT(k, tname[k]);
             block(D + 1 + k, bname[D + 1 + k]);
         }
-        c->head_w = add("final.1.weight", {c->out_ch, c->base, 1, 1}, 0);
-        c->head_b = add("final.1.bias", {c->out_ch}, 0);
+        c->head_w = add("final.1.weight", {dout_head, lvl(0), k1, k1}, 0);
+        c->head_b = add("final.1.bias", {dout_head}, 0);
     } else {
         // models/mod.py:21-41: encoders, (pools), bottleneck, upconvs, decoders, final_conv
         for (int l = 0; l < D; ++l) block(l, "encoders." + std::to_string(l));
         block(D, "bottleneck");
         for (int k = 0; k < D; ++k) convT(k, "upconvs." + std::to_string(k));
         for (int k = 0; k < D; ++k) block(D + 1 + k, "decoders." + std::to_string(k));
-        c->head_w = add("final_conv.weight", {c->out_ch, c->base, 1, 1}, 0);
-        c->head_b = add("final_conv.bias", {c->out_ch}, 0);
+        c->head_w = add("final_conv.weight", {dout_head, lvl(0), k1, k1}, 0);
+        c->head_b = add("final_conv.bias", {dout_head}, 0);
     }
     c->n_param_floats = off;
-    int64_t run = 0;
+    c->n_pparam_floats = poff;
+    int64_t run = 0, rrun = 0;
     for (auto& B : c->bn) {  // named_buffers() order == conv order in both variants
         B.run = run;
+        B.rrun = rrun;
         run += 2 * B.C;
+        rrun += 2 * B.rC;
     }
-    c->n_bn_floats = run;
+    c->n_bn_floats = rrun;
+    c->n_pbn_floats = run;
+    // expand / compact tables (the bn arena: mean and var vectors of each layer)
+    c->pad_params.clear();
+    c->pad_bn.clear();
+    c->pad_max_numel = c->pad_bn_max = 0;
+    if (c->padded) {
+        for (const ParamT& p : c->params) {
+            PadDesc d{p.off, p.poff, p.numel, p.pnumel, {1, 1, 1, 1}, {1, 1, 1, 1}, {1, 1, 1, 1}};
+            for (int k = 0; k < 4; ++k) {
+                d.seg[k] = (int32_t)p.seg[k];
+                d.pseg[k] = (int32_t)p.pseg[k];
+                d.nseg[k] = (int32_t)p.nseg[k];
+            }
+            c->pad_params.push_back(d);
+            c->pad_max_numel = std::max(c->pad_max_numel, p.pnumel);
+        }
+        for (const BnL& B : c->bn)
+            for (int v = 0; v < 2; ++v) {
+                PadDesc d{B.rrun + v * B.rC, B.run + v * B.C, B.rC, B.C,
+                          {B.rC, 1, 1, 1}, {B.C, 1, 1, 1}, {1, 1, 1, 1}};
+                c->pad_bn.push_back(d);
+                c->pad_bn_max = std::max<int64_t>(c->pad_bn_max, B.C);
+            }
+    }
     c->cmax = 0;
     for (auto& L : c->conv) c->cmax = std::max(c->cmax, std::max(L.cin, L.cout));
     // packed weights (forward + dgrad images); conv 0 (Cin = in_channels) has its own kernel
@@ -392,6 +471,13 @@ struct Plan {
     void* zero16;
     std::vector<uint16_t*> x16;  // training, bf16: per-conv input images kept for the wgrad
     std::vector<uint16_t*> t16;  // training, bf16: per-ConvT input images kept for the wgrad
+    // channel-padded networks: padded parameter / running-stat / gradient arenas and the
+    // device copies of the expand / compact tables
+    float* pprm;
+    float* pbn;
+    float* pgrad;
+    PadDesc* ptab;
+    PadDesc* btab;
     size_t bytes;
 };
 
@@ -532,6 +618,15 @@ void make_plan(unet_ctx* c, int N, int H, int W, bool training, char* base, Plan
     p.mean.assign(NC, nullptr);
     p.invstd.assign(NC, nullptr);
     p.pack = b.take<float>(c->pack_floats);
+    p.pprm = p.pbn = p.pgrad = nullptr;
+    p.ptab = p.btab = nullptr;
+    if (c->padded) {
+        p.pprm = b.take<float>(c->n_pparam_floats);
+        p.pbn = b.take<float>(c->n_pbn_floats);
+        p.pgrad = training ? b.take<float>(c->n_pparam_floats) : nullptr;
+        p.ptab = b.take<PadDesc>((int64_t)c->pad_params.size());
+        p.btab = b.take<PadDesc>((int64_t)c->pad_bn.size());
+    }
     p.x_nhwc = b.take<float>(p.P[0] * c->in_ch);  // NHWC copy of x (conv-0 wgrad input)
     for (int l = 0; l < D; ++l) {
         const int C = c->ch(l);
@@ -819,6 +914,17 @@ void use_a16(const unet_ctx* c, const Plan& p, RowGemmArgs& g, int C) {
     g.acoef = nullptr;
     g.zero16 = p.zero16;
     g.xcd = xcd16_on(c);
+}
+
+// device copies of the expand / compact tables (the host tables live in the context, so
+// the asynchronous copy's source outlives it)
+int upload_pad_tables(unet_ctx* c, Plan& p, hipStream_t s) {
+    hipError_t e = hipMemcpyAsync(p.ptab, c->pad_params.data(), sizeof(PadDesc) * c->pad_params.size(),
+                                  hipMemcpyHostToDevice, s);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(p.btab, c->pad_bn.data(), sizeof(PadDesc) * c->pad_bn.size(),
+                           hipMemcpyHostToDevice, s);
+    return (int)e;
 }
 
 int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, const float* x,
@@ -1386,6 +1492,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         return 0;
     };
     auto stage_done = [&](int st) {
+        if (c->padded) return;  // unet_backward records every bucket after the compaction
         bool any = false;
         for (size_t b = 0; b < c->bucket_stage.size(); ++b) any |= c->bucket_stage[b] == st;
         if (!any) return;
@@ -1633,13 +1740,25 @@ int unet_create(const unet_cfg* cfg, int device, unet_ctx** out) {
         }
         // The first conv kernel is specialised for a single input channel (every BASELINE
         // config); the GEMM tiles need 64-multiples of channels at every level and the
-        // channel-quad row kernels (pool, head, BN backward) a power-of-two channel count, so
-        // base is 64, 128 or 256; the head's fused BN-partials path handles up to 4 classes.
+        // channel-quad row kernels (pool, head, BN backward) a power-of-two channel count,
+        // so the kernels run base 64, 128 or 256.  Other base_filters (the reference grid's
+        // 16 / 24 / 32 / 48, config/config.yaml; any multiple of 8 up to 256) run padded
+        // to the next power of two >= 64 (unet_ctx::padded); the head's fused BN-partials
+        // path handles up to 4 classes.
+        c->rbase = c->base;
+        if (c->base >= 8 && c->base <= 256 && c->base % 8 == 0) {
+            int pb = 64;
+            while (pb < c->base) pb <<= 1;
+            c->padded = pb != c->base;
+            c->base = pb;
+        }
         if ((c->variant != UNET_VARIANT_MODEL && c->variant != UNET_VARIANT_MOD &&
              c->variant != UNET_VARIANT_RES) || c->in_ch != 1 ||
             c->out_ch < 1 || c->out_ch > 4 || c->base % 64 || c->base > 256 ||
             (c->base & (c->base - 1)) || c->depth < 1 ||
             c->depth > MAX_DEPTH || (c->base << c->depth) > 8192)
+            return UNET_ERR_UNSUPPORTED;
+        if (c->padded && c->bf16)  // the bf16 kernels need 128-multiples of real channels
             return UNET_ERR_UNSUPPORTED;
         c->res = c->variant == UNET_VARIANT_RES;
         c->bn_relu = c->variant != UNET_VARIANT_MODEL;
@@ -1704,8 +1823,8 @@ int unet_bn_info(const unet_ctx* c, int i, const char** name, int* ch, int64_t* 
     ABI_TRY
     if (!c || i < 0 || i >= c->nconv()) return UNET_ERR_INVALID;
     if (name) *name = c->bn[i].name.c_str();
-    if (ch) *ch = c->bn[i].C;
-    if (off) *off = c->bn[i].run;
+    if (ch) *ch = c->bn[i].rC;
+    if (off) *off = c->bn[i].rrun;
     return UNET_OK;
     ABI_CATCH(c)
 }
@@ -1735,8 +1854,22 @@ int unet_forward(unet_ctx* c, const float* params, float* bn_running, int64_t* b
     make_plan(c, N, H, W, training != 0, (char*)ws, p);
     if (hipSetDevice(c->device) != hipSuccess) return fail(c, UNET_ERR_HIP, "hipSetDevice");
     if (!c->timing) c->ev_used = 0;
-    return forward_impl(c, params, bn_running, bn_count, x, logits, p, training != 0,
-                        (hipStream_t)stream);
+    const hipStream_t s = (hipStream_t)stream;
+    if (!c->padded)
+        return forward_impl(c, params, bn_running, bn_count, x, logits, p, training != 0, s);
+    // narrow network: torch-layout arenas -> padded arenas, forward, running stats back
+    int r = upload_pad_tables(c, p, s);
+    if (!r) r = k_pad_copy(p.ptab, (int)c->pad_params.size(), c->pad_max_numel, params, p.pprm, 1, s);
+    if (!r && bn_running)
+        r = k_pad_copy(p.btab, (int)c->pad_bn.size(), c->pad_bn_max, bn_running, p.pbn, 1, s);
+    if (r) return fail(c, UNET_ERR_HIP, "channel-padding expand: %d", r);
+    r = forward_impl(c, p.pprm, bn_running ? p.pbn : nullptr, bn_count, x, logits, p,
+                     training != 0, s);
+    if (r) return r;
+    if (training && bn_running &&
+        k_pad_copy(p.btab, (int)c->pad_bn.size(), c->pad_bn_max, p.pbn, bn_running, 0, s))
+        return fail(c, UNET_ERR_HIP, "channel-padding compact (running stats)");
+    return UNET_OK;
     ABI_CATCH(c)
 }
 
@@ -1754,7 +1887,16 @@ int unet_backward(unet_ctx* c, const float* params, const float* dlogits, float*
         c->bucket_ev.resize(c->bucket_off.size());
         for (auto& e : c->bucket_ev) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
     }
-    return backward_impl(c, params, dlogits, grads, p, (hipStream_t)stream);
+    const hipStream_t s = (hipStream_t)stream;
+    if (!c->padded) return backward_impl(c, params, dlogits, grads, p, s);
+    // narrow network: the padded parameters expanded by the forward are still in the
+    // workspace; gradients are compacted into the caller's arena, then every bucket is ready
+    int r = backward_impl(c, p.pprm, dlogits, p.pgrad, p, s);
+    if (r) return r;
+    if (k_pad_copy(p.ptab, (int)c->pad_params.size(), c->pad_max_numel, p.pgrad, grads, 0, s))
+        return fail(c, UNET_ERR_HIP, "channel-padding compact (gradients)");
+    for (auto e : c->bucket_ev) (void)hipEventRecord(e, s);
+    return UNET_OK;
     ABI_CATCH(c)
 }
 

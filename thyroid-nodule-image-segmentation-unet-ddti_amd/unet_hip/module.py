@@ -199,8 +199,9 @@ def _mod_block(cin, cout):
 class ModUNet(_HipUNet):
     """models/mod.py:9-66 ``UNet(in_channels, out_channels, base_filters, depth)``.
 
-    Supported here: in_channels 1, out_channels 1..4, base_filters a multiple of 64
-    (<= 256), depth 1..6 (the native GEMM tiles work on 64-channel multiples).
+    Supported here: in_channels 1, out_channels 1..4, base_filters a multiple of 8 up to
+    256 (64 / 128 / 256 natively; narrower widths such as the reference grid's 16 / 24 /
+    32 / 48 run zero-padded to the next power of two >= 64 inside the library), depth 1..6.
 
     ``mfma_dtype``: "fp32" (default; exact f32 products like the reference) or "bf16"
     (BASELINE config 4: conv GEMM operands rounded to bf16, f32 accumulate; parameters,
@@ -256,7 +257,7 @@ class _ResidualBlock(nn.Module):
 class ResUNet(_HipUNet):
     """models/mod.py:88-131 ``ResUNet(in_channels, out_channels, base_filters, depth)``:
     every block is ReLU(conv(x) + skip(x)) with conv = Conv-BN-ReLU-Conv-BN and a bias-free
-    1x1 skip.  Same support limits as ``ModUNet`` (f32 GEMMs)."""
+    1x1 skip.  Same widths as ``ModUNet`` (f32 GEMMs)."""
 
     _name = "models.mod.ResUNet"
 

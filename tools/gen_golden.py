@@ -36,6 +36,11 @@ Fixtures (all float64 statistics computed from fp32 results):
                     focal 1, boundary 0) with the real FocalTverskyLoss() (trainer.py:38),
                     B=2 1x64x64, 3 AdamW steps (utils/trainer.py:81-93): full logits, the
                     three loss terms, grad norm/sum/samples, param samples.
+  mod_narrow_64.npz the reference grid's narrow widths (config/config.yaml): models/mod.py
+                    UNet(base 32, depth 4) two AdamW steps (lr 1e-4) with full logits,
+                    losses, grad norm/sum/samples, param samples, running stats, eval
+                    logits (prefix b32_); one step of UNet(base 24, depth 3) (u24_),
+                    UNet(base 48, depth 3) (u48_) and ResUNet(base 16, depth 3) (r16_).
   unet_dpf_64.npz   nn.DataParallel with FocalTversky in the loss (the loss of the gathered
                     logits, global TP/FP/FN): eq_* B=4 in 2 shards of 2, ratios 1/0/1/0;
                     uneq_* B=3 in shards of 2 and 1 (DataParallel's chunked scatter), ratios
@@ -343,6 +348,52 @@ def case_res_d3_64():
     np.savez_compressed(os.path.join(OUT, "res_d3_64.npz"), **out)
 
 
+def case_mod_narrow_64():
+    out = {}
+    m = build_mod(32, 4)
+    m.train()
+    x = torch.from_numpy(W.make_input(31, 2, 1, 64, 64))
+    t = torch.from_numpy(W.make_target(31, 2, 64, 64))
+    opt = torch.optim.AdamW(m.parameters(), lr=1e-4)
+    names = [n for n, _ in MO.bn_layers(32, 4)]
+    for s in range(2):
+        logits, lb, ld, loss = step(m, opt, x, t, RefDice())
+        p = f"b32_s{s}_"
+        out[p + "logits"] = logits.numpy()
+        out[p + "bce"], out[p + "dice"], out[p + "loss"] = lb, ld, loss
+        grad_stats(m, p, out)
+        out[p + "params_samp"] = param_samples(m)
+        bufs = dict(m.named_buffers())
+        out[p + "running_mean"] = np.concatenate([bufs[f"{n}.running_mean"].numpy() for n in names])
+        out[p + "running_var"] = np.concatenate([bufs[f"{n}.running_var"].numpy() for n in names])
+    m.eval()
+    with torch.no_grad():
+        out["b32_eval_logits"] = m(x).numpy()
+    for tag, base in (("u24_", 24), ("u48_", 48)):
+        m = build_mod(base, 3)
+        m.train()
+        logits = m(x)
+        lb, ld = torch.nn.BCEWithLogitsLoss()(logits, t), RefDice()(logits, t)
+        (lb + ld).backward()
+        out[tag + "logits"] = logits.detach().numpy()
+        out[tag + "loss"] = (lb + ld).item()
+        grad_stats(m, tag, out)
+    torch.manual_seed(0)
+    m = RefResUNet(1, 1, base_filters=16, depth=3)
+    sd = m.state_dict()
+    for k, v in MO.res_make_params(42, 16, 3).items():
+        sd[k] = v.clone()
+    m.load_state_dict(sd)
+    m.train()
+    logits = m(x)
+    lb, ld = torch.nn.BCEWithLogitsLoss()(logits, t), RefDice()(logits, t)
+    (lb + ld).backward()
+    out["r16_logits"] = logits.detach().numpy()
+    out["r16_loss"] = (lb + ld).item()
+    grad_stats(m, "r16_", out)
+    np.savez_compressed(os.path.join(OUT, "mod_narrow_64.npz"), **out)
+
+
 def case_mod_c4_64():
     m = build_mod(128, 5)
     m.train()
@@ -375,5 +426,6 @@ if __name__ == "__main__":
     case_mod_c4_64()
     case_focal_64()
     case_dp_focal_64()
+    case_mod_narrow_64()
     for f in sorted(os.listdir(OUT)):
         print(f, os.path.getsize(os.path.join(OUT, f)))
