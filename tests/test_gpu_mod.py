@@ -357,15 +357,19 @@ def test_mod_narrow_one_step_matches_golden(golden_dir, tag, base):
                       GRAD_TOL, tag)
 
 
-@pytest.mark.parametrize("base,depth,H,W", [(16, 5, 64, 96), (24, 4, 128, 64), (48, 6, 128, 128)])
+@pytest.mark.parametrize("base,depth,H,W", [(16, 5, 64, 96), (24, 4, 128, 64), (48, 6, 128, 256)])
 def test_mod_narrow_full_grads_vs_fp64(base, depth, H, W):
     """Every gradient element of narrow networks (padded inside the library) against the
-    fp64 oracle, within 2x the fp32 oracle's own error (floor 1e-2), and the padding is
-    invisible in the caller's arenas (torch-layout gradients, running stats)."""
+    fp64 oracle, and the padding is invisible in the caller's arenas (torch-layout
+    gradients, running stats).  At depth 6 the bottleneck BN sees 16 values per channel,
+    where a near-zero ReLU input flips under any fp32 rounding change: the envelope is 2x
+    the fp32 oracle's own error over x and x * (1 + 1e-7) (as tests/test_gpu_res.py),
+    floor 1e-2."""
     import unet_hip
     P = MO.make_params(7, base, depth)
     x, t = inputs(33, 2, H, W)
     ref = MO.train_step(P, MO.init_buffers(base, depth), None, x, t, depth=depth)
+    refp = MO.train_step(P, MO.init_buffers(base, depth), None, x * (1 + 1e-7), t, depth=depth)
     r64 = MO.train_step({k: v.double() for k, v in P.items()},
                         {k: (v.double() if v.is_floating_point() else v.clone())
                          for k, v in MO.init_buffers(base, depth).items()},
@@ -375,7 +379,8 @@ def test_mod_narrow_full_grads_vs_fp64(base, depth, H, W):
     losses = unet_hip.seg_losses(logits, t.to(DEV))
     (losses[0] + losses[1]).backward()
     assert rel_max(logits.detach().cpu().numpy(), ref["logits"].numpy()) <= LOGIT_TOL
-    e32 = {k: norm_rel(g, r64["grads"][k]) for k, g in ref["grads"].items()}
+    e32 = {k: max(norm_rel(g, r64["grads"][k]), norm_rel(refp["grads"][k], r64["grads"][k]))
+           for k, g in ref["grads"].items()}
     env = max(2 * max(e32.values()), GRAD_TOL)
     errs = grad_errors(m, r64["grads"])
     worst = max(errs, key=errs.get)
