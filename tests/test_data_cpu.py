@@ -26,3 +26,27 @@ def test_library_plan_matches_restatement(n_in, n_out):
     rk, rb = RR.plan(n_in, n_out)
     np.testing.assert_array_equal(k, rk)
     np.testing.assert_array_equal(b, rb)
+
+
+@pytest.mark.parametrize("n,bs,world", [(10, 4, 2), (37, 8, 3), (5, 4, 4), (16, 16, 8), (3, 2, 4)])
+@pytest.mark.parametrize("shuffle", [False, True])
+def test_dataparallel_shard_sampler(n, bs, world, shuffle):
+    """Every rank's shards concatenate to the reference loader's global batch
+    (data/data_loader.py:29-33, drop_last=False) split with torch.chunk exactly as
+    nn.DataParallel scatters it (utils/trainer.py:28-30); every sample once per epoch."""
+    import torch
+    from data.data_loader import DataParallelShardSampler
+    samplers = [DataParallelShardSampler(n, bs, shuffle, r, world, seed=3) for r in range(world)]
+    for ep in (0, 1):
+        for s in samplers:
+            s.set_epoch(ep)
+        per_rank = [list(s) for s in samplers]
+        assert all(len(p) == len(samplers[0]) == (n + bs - 1) // bs for p in per_rank)
+        seen = []
+        for b, glob in enumerate(samplers[0].global_batches()):
+            chunks = torch.chunk(glob, world)
+            for r in range(world):
+                want = chunks[r].tolist() if r < len(chunks) else []
+                assert per_rank[r][b] == want
+            seen += glob.tolist()
+        assert sorted(seen) == list(range(n))

@@ -128,3 +128,96 @@ def test_dp2_focal_on_gpu_matches_dataparallel_golden(golden_dir, tag, B, seed):
     for v, k in zip(vals, ("bce", "dice", "focal", "loss")):
         assert abs(v - float(f[tag + k])) < 1e-5, (k, v, float(f[tag + k]))
     np.testing.assert_allclose(norms, f[tag + "grad_norm"], rtol=1e-2)
+
+
+def _trainer_worker(rank, world, port, q, tmp):
+    import sys
+    for p in (REPO, PKG, os.path.join(REPO, "tests")):
+        sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import argparse
+        from data.data_loader import DataParallelShardSampler, SyntheticSegmentation, dp_collate
+        from models.model import UNet
+        from oracle import unet_ref_cpu as O
+        from utils.trainer import Trainer
+        from utils.utils import Config, create_logger
+        torch.cuda.set_device(0)
+        ns = argparse.Namespace(model_type="UNet", lr=1e-4, bce_ratio=1.0, dice_ratio=0.0,
+                                focal_ratio=1.0, boundary_ratio=0.0, use_mixup=False,
+                                mixup_prob=0.0, mixup_alpha=0.2, epochs=1, early_stop_patience=5,
+                                batch_size=4, num_workers=0)
+        cfg = Config(ns, base_dir=os.path.join(tmp, f"r{rank}"))
+        cfg.device = torch.device("cuda:0")
+        ds = SyntheticSegmentation(5, 64, seed=4)
+        loaders = tuple(torch.utils.data.DataLoader(
+            ds, batch_sampler=DataParallelShardSampler(5, 4, False, rank, world), collate_fn=dp_collate())
+            for _ in range(3))
+        P = O.make_params(42)
+        m = UNet()
+        m.load_state_dict({**P, **O.init_buffers()})
+        tr = Trainer(cfg, loaders, create_logger(os.path.join(cfg.log_dir, "t.log")), m)
+        avg = tr.train_one_epoch(0)
+        params = tr.model._state.param_arena.detach().cpu().clone()
+        pd = params.clone()
+        dist.broadcast(pd, src=0)
+        same = bool(torch.equal(pd, params))
+        q.put((rank, avg, same, params.numpy() if rank == 0 else None))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+def test_trainer_dp2_ragged_last_batch_matches_dataparallel(tmp_path):
+    """utils.trainer.Trainer over two ranks, one epoch of 5 samples at batch_size 4 (the
+    reference loader's drop_last=False): batch 1 splits 2 + 2, the last batch of one sample
+    goes to rank 0 and leaves rank 1's shard empty (it joins the collectives with zeros).
+    Loss = the CLI defaults BCE + FocalTversky on the gathered batch.  The epoch loss and
+    the parameters after both AdamW steps must match the oracle's nn.DataParallel
+    emulation; both ranks must hold identical parameters."""
+    from data.data_loader import SyntheticSegmentation
+    from oracle import unet_ref_cpu as O
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_trainer_worker, args=(r, 2, port, q, str(tmp_path))) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=500), q.get(timeout=500)], key=lambda r: r[0])
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    assert res[0][2] and res[1][2], "ranks diverged"
+    ds = SyntheticSegmentation(5, 64, seed=4)
+    xs = torch.stack([ds[i][0] for i in range(5)])
+    ts = torch.stack([ds[i][1] for i in range(5)])
+
+    def dp_epoch(dtype, xscale=1.0):
+        P = {k: v.to(dtype) for k, v in O.make_params(42).items()}
+        B = {k: (v.to(dtype) if v.is_floating_point() else v) for k, v in O.init_buffers().items()}
+        opt = O.AdamWState(P, lr=1e-4)
+        losses = []
+        for sl in (slice(0, 4), slice(4, 5)):  # global batches; DataParallel scatters each
+            r = O.train_step(P, B, opt, xs[sl].to(dtype) * xscale, ts[sl].to(dtype), w_bce=1.0,
+                             w_dice=0.0, w_focal=1.0, shards=2)
+            losses.append(float(r["loss"]))
+        flat = torch.cat([P[n].reshape(-1) for n, *_ in O.param_spec()]).double().numpy()
+        return losses, flat
+
+    losses, ref32 = dp_epoch(torch.float32)
+    _, ref32p = dp_epoch(torch.float32, 1 + 1e-7)  # a second fp32 noise realisation
+    _, ref64 = dp_epoch(torch.float64)
+    want = (4 * losses[0] + 1 * losses[1]) / 5  # AverageMeter over the global batches
+    assert abs(res[0][1] - want) < 1e-4, (res[0][1], want)
+    # two Adam steps from fp32 gradients: elements whose gradient is rounding noise move by
+    # up to lr per step in any fp32 evaluation, so the HIP trajectory is judged against the
+    # fp64 one within 2x the fp32 oracle's own deviation from it (the larger of two fp32
+    # realisations: x and x * (1 + 1e-7))
+    d_hip = np.abs(res[0][3].astype(np.float64) - ref64)
+    d_32 = max(np.abs(ref32 - ref64).mean(), np.abs(ref32p - ref64).mean())
+    print(f"vs fp64: hip mean {d_hip.mean():.3e} max {d_hip.max():.3e}; "
+          f"fp32 oracle mean {np.abs(ref32 - ref64).mean():.3e} / {np.abs(ref32p - ref64).mean():.3e}")
+    assert d_hip.max() <= 4 * 1e-4 * 1.01
+    assert d_hip.mean() <= 2 * d_32 + 1e-8

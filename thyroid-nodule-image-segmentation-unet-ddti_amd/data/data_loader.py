@@ -65,6 +65,53 @@ def create_dataloader(dataset, config, shuffle):
                       num_workers=config.num_workers)
 
 
+class DataParallelShardSampler(torch.utils.data.Sampler):
+    """Batch sampler giving one rank of a one-process-per-GPU run exactly its
+    nn.DataParallel share of the reference loader's batches.
+
+    The reference loads GLOBAL batches of ``batch_size`` (data/data_loader.py:29-33:
+    shuffle, drop_last=False, so the last batch may be short) and DataParallel scatters each
+    one with torch.chunk over the replicas (utils/trainer.py:28-30).  Here every rank draws
+    the same batch order (shared seed, re-drawn per epoch by ``set_epoch``) and yields its
+    torch.chunk slice of every batch.  The slice is empty for a last batch with fewer
+    samples than ranks; ``dp_collate`` turns that into ``None`` and the Trainer then joins
+    the step's collectives with zero contributions (``DistributedUNet.empty_step``)."""
+
+    def __init__(self, n, batch_size, shuffle, rank, world, seed=0):
+        self.n, self.batch_size, self.shuffle = int(n), int(batch_size), bool(shuffle)
+        self.rank, self.world, self.seed, self.epoch = int(rank), int(world), int(seed), 0
+
+    def set_epoch(self, epoch):
+        self.epoch = int(epoch)
+
+    def global_batches(self):
+        if self.shuffle:
+            g = torch.Generator()
+            g.manual_seed(self.seed + self.epoch)
+            order = torch.randperm(self.n, generator=g)
+        else:
+            order = torch.arange(self.n)
+        return [order[b:b + self.batch_size] for b in range(0, self.n, self.batch_size)]
+
+    def __iter__(self):
+        for batch in self.global_batches():
+            chunks = torch.chunk(batch, self.world)
+            yield chunks[self.rank].tolist() if self.rank < len(chunks) else []
+
+    def __len__(self):
+        return (self.n + self.batch_size - 1) // self.batch_size
+
+
+def dp_collate(collate=None):
+    """Collate for DataParallelShardSampler: an empty shard becomes None."""
+    from torch.utils.data import default_collate
+    inner = collate or default_collate
+
+    def fn(batch):
+        return None if len(batch) == 0 else inner(batch)
+    return fn
+
+
 class DecodeU8:
     """Transform that only decodes: (PIL image, PIL mask) -> two (H, W) uint8 arrays.
 
@@ -103,6 +150,10 @@ class DeviceResizeLoader:
     def __len__(self):
         return len(self.loader)
 
+    @property
+    def batch_sampler(self):
+        return self.loader.batch_sampler
+
     def __iter__(self):
-        for imgs, masks in self.loader:
-            yield self.pipe(imgs, masks)
+        for batch in self.loader:
+            yield None if batch is None else self.pipe(*batch)

@@ -23,8 +23,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 if HERE not in sys.path:
     sys.path.insert(0, HERE)
 
-from data.data_loader import (DecodeU8, DeviceResizeLoader, MedicalDataset,  # noqa: E402
-                              SyntheticSegmentation, create_dataloader, u8_collate)
+from data.data_loader import (DataParallelShardSampler, DecodeU8, DeviceResizeLoader,  # noqa: E402
+                              MedicalDataset, SyntheticSegmentation, create_dataloader,
+                              dp_collate, u8_collate)
 from models.mod import ResUNet  # noqa: E402
 from models.mod import UNet as ModUNet  # noqa: E402
 from models.model import UNet  # noqa: E402
@@ -106,8 +107,12 @@ def main(args):
         if gpu_tf:
             kw["collate_fn"] = u8_collate
         if world > 1:
-            kw["sampler"] = torch.utils.data.distributed.DistributedSampler(ds, shuffle=(i != 1))
-            dl = torch.utils.data.DataLoader(ds, **kw)
+            # nn.DataParallel's split of every global batch (utils/trainer.py:28-30):
+            # --batch_size stays the GLOBAL batch, as in the reference
+            rank = torch.distributed.get_rank()
+            bs = DataParallelShardSampler(len(ds), config.batch_size, i != 1, rank, world, seed=42)
+            dl = torch.utils.data.DataLoader(ds, batch_sampler=bs, num_workers=config.num_workers,
+                                             collate_fn=dp_collate(u8_collate if gpu_tf else None))
         elif gpu_tf:
             dl = torch.utils.data.DataLoader(ds, shuffle=(i != 1), **kw)
         else:

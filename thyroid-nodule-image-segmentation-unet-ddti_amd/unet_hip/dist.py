@@ -45,8 +45,9 @@ class BucketReducer:
         self.wait_fn = wait_fn
         self.stream = None
 
-    def reduce(self, arena):
-        """Sum `arena` over the ranks in place; returns the world size."""
+    def reduce(self, arena, wait_native=True):
+        """Sum `arena` over the ranks in place; returns the world size.  wait_native=False:
+        the arena was not written by a native backward this step (an empty shard)."""
         ws = dist.get_world_size(self.group)
         if ws == 1:
             return 1
@@ -57,7 +58,7 @@ class BucketReducer:
             main = torch.cuda.current_stream(arena.device)
             with torch.cuda.stream(self.stream):
                 for b, (off, n) in enumerate(self.buckets):
-                    if self.wait_fn is not None:
+                    if self.wait_fn is not None and wait_native:
                         self.wait_fn(b, self.stream)
                     else:
                         self.stream.wait_stream(main)
@@ -106,7 +107,37 @@ class DistributedUNet:
         grp = self.group if self.group is not None else dist.group.WORLD
         return seg_losses(logits, targets, alpha, beta, gamma, group=grp)
 
-    def reduce_gradients(self):
+    def empty_step(self, extra_scalar_reduces=0):
+        """This rank's shard of the batch is empty (a last batch with fewer samples than
+        ranks, data.data_loader.DataParallelShardSampler): join the step's collectives -- the
+        loss sums, `extra_scalar_reduces` single-value all-reduces (the trainer's boundary
+        loss), the gradient buckets -- with zero contributions, so that every rank then
+        applies the same summed gradients."""
+        st = self.model.flatten_()
+        dev = st.param_arena.device
+        sums = torch.zeros(8, dtype=torch.float64, device=dev)
+        dist.all_reduce(sums, group=self.group)  # SegLossFunction.forward's collective
+        for _ in range(extra_scalar_reduces):
+            z = torch.zeros(1, device=dev)
+            dist.all_reduce(z, group=self.group)
+        if st.grad_arena is None:
+            st.grad_arena = torch.zeros_like(st.param_arena)
+        else:
+            st.grad_arena.zero_()
+        for (p, _, _), g in zip(st.params, st.grad_views(st.grad_arena)):
+            p.grad = g
+        return self.reduce_gradients(wait_native=False)
+
+    def empty_losses(self, extra_scalar_reduces=0):
+        """Eval-mode counterpart of empty_step: only the loss collectives."""
+        dev = self.model.flatten_().param_arena.device
+        sums = torch.zeros(8, dtype=torch.float64, device=dev)
+        dist.all_reduce(sums, group=self.group)
+        for _ in range(extra_scalar_reduces):
+            z = torch.zeros(1, device=dev)
+            dist.all_reduce(z, group=self.group)
+
+    def reduce_gradients(self, wait_native=True):
         """Sum (or, with average=True, average) the flat gradient arena over the ranks.
         Returns the scale the optimizer applies to the summed gradients."""
         st = self.model._state
@@ -115,7 +146,7 @@ class DistributedUNet:
         if p0.grad is None or p0.grad.data_ptr() != arena.data_ptr():
             raise RuntimeError("gradients are not in the flat grad arena (accumulated grads are "
                                "not supported by the bucketed reducer)")
-        ws = self.reducer.reduce(arena)
+        ws = self.reducer.reduce(arena, wait_native)
         scale = 1.0 / ws if self.average else 1.0
         if self.optimizer is not None and hasattr(self.optimizer, "grad_scale"):
             self.optimizer.grad_scale = scale

@@ -17,8 +17,11 @@ What runs where (MI355X-first):
   epoch metrics are sums of those counts, so the numbers are the same);
 * multi-GPU: one process per GPU (``torch.distributed`` with the "nccl" = RCCL backend
   initialised by the launcher) with bucketed gradient all-reduce overlapped with the
-  backward, replacing ``nn.DataParallel`` (:28-30).  Per-rank BatchNorm statistics, as
-  DataParallel's per-replica BN; losses and metrics are averaged / summed over ranks.
+  backward, replacing ``nn.DataParallel`` (:28-30).  Every rank takes its torch.chunk share
+  of each global batch (data.data_loader.DataParallelShardSampler, ``--batch_size`` stays
+  global), runs per-rank BatchNorm as DataParallel's replicas do, gets the gathered batch's
+  losses (incl. FocalTversky's global TP/FP/FN) and the summed gradients; epoch meters and
+  confusion counts are summed over ranks.
 * BoundaryLoss keeps the reference's host EDT and is only evaluated when its ratio != 0
   (the reference evaluates it every step even at ratio 0; 0 * finite == 0, so skipping it
   changes no number).
@@ -143,11 +146,29 @@ class Trainer:
         sums = torch.zeros(5, dtype=torch.float64, device=self.device)  # device-side meters
         n_seen = 0
         desc = f"{'Training' if train else 'Validating'} Epoch {epoch + 1}"
-        for images, masks in tqdm(loader, desc=desc, leave=True):
+        bsamp = getattr(loader, "batch_sampler", None)
+        if hasattr(bsamp, "set_epoch"):  # DataParallelShardSampler: same batches on every rank
+            bsamp.set_epoch(epoch)
+        nb_extra = 2 if self.config.boundary_ratio != 0 else 0
+        for batch in tqdm(loader, desc=desc, leave=True):
+            # utils/trainer.py:62-64: the mixup draws come first, on every rank alike (ranks
+            # share the python / numpy seeds, set_seed(42)), so they stay in step even when a
+            # rank's shard is empty.  Under data parallelism a shard mixes with itself, where
+            # the reference's DataParallel mixes the whole batch before scattering it.
+            mix = train and random.random() < self.config.mixup_prob and self.config.use_mixup
+            lam = np.random.beta(self.config.mixup_alpha, self.config.mixup_alpha) if mix else None
+            if batch is None:  # empty DataParallel shard: join the step's collectives only
+                if train:
+                    self.optimizer.zero_grad(set_to_none=True)
+                    self.ddp.empty_step(nb_extra)
+                    self.optimizer.step()
+                else:
+                    self.ddp.empty_losses(nb_extra)
+                continue
+            images, masks = batch
             images = images.to(self.device, non_blocking=True).float()
             masks = masks.to(self.device, non_blocking=True).float()
-            if train and random.random() < self.config.mixup_prob and self.config.use_mixup:
-                lam = np.random.beta(self.config.mixup_alpha, self.config.mixup_alpha)
+            if mix:
                 perm = torch.randperm(images.size(0), device=self.device)
                 images = lam * images + (1.0 - lam) * images[perm]
                 masks = lam * masks + (1.0 - lam) * masks[perm]
