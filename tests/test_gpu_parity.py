@@ -580,3 +580,61 @@ def test_wgrad_row3_matches_one_tap_tiles(variant):
         worst = max(worst, d)
         assert d <= 1e-5, (k, d)
     print(f"row3 vs one-tap worst grad norm-rel {worst:.2e}")
+
+
+@pytest.mark.parametrize("variant,B,H,W", [("model", 2, 64, 64), ("model", 2, 256, 128),
+                                           ("model", 1, 48, 80), ("mod", 2, 128, 64),
+                                           ("res", 2, 64, 64)])
+def test_row3_gemm_matches_oracle(variant, B, H, W):
+    """Option row3_gemm: 3x3 forward / dgrad GEMMs on the tap-row kernel
+    (kernels_gemm.hip rowgemm_row3_kernel; W = 80 exercises the fallback to the one-tap
+    kernel on grids it cannot tile).  Logits at the north-star bar; every gradient against
+    fp64 within 2x the fp32 oracle's own error (over x and x * (1 + 1e-7)), floor 1e-2, or
+    within 1.25x the default (one-tap) kernel's error on the same case -- both GEMM
+    schedules see the same discrete ReLU-boundary flips (test_train_steps_strict_resync),
+    which move small BN-bias gradients by ~1e-2 on some inputs."""
+    import unet_hip
+    from _helpers import hip_mod_model, options
+    from oracle import mod_ref_cpu as MO
+    x, t = inputs(41, B, H, W)
+    if variant == "model":
+        P, Bf = O.make_params(42), O.init_buffers()
+        make = lambda: hip_model(P, DEV)  # noqa: E731
+        step = lambda P, B, x, t: O.train_step(P, B, None, x, t)  # noqa: E731
+    elif variant == "mod":
+        P, Bf = MO.make_params(5, 64, 3), MO.init_buffers(64, 3)
+        make = lambda: hip_mod_model(P, DEV, 64, 3)  # noqa: E731
+        step = lambda P, B, x, t: MO.train_step(P, B, None, x, t, depth=3)  # noqa: E731
+    else:
+        P, Bf = MO.res_make_params(42, 64, 3), MO.res_init_buffers(64, 3)
+
+        def make():
+            m = unet_hip.ResUNet(1, 1, base_filters=64, depth=3)
+            sd = m.state_dict()
+            sd.update({k: v.clone() for k, v in P.items()})
+            sd.update({k: v.clone() for k, v in Bf.items()})
+            m.load_state_dict(sd)
+            return m.to(DEV).train()
+        step = lambda P, B, x, t: MO.res_train_step(P, B, None, x, t, depth=3)  # noqa: E731
+    ref = step(P, {k: v.clone() for k, v in Bf.items()}, x, t)
+    refp = step(P, {k: v.clone() for k, v in Bf.items()}, x * (1 + 1e-7), t)
+    r64 = step(_to64(P), _to64(Bf), x.double(), t.double())
+    e32 = {k: max(norm_rel(g, r64["grads"][k]), norm_rel(refp["grads"][k], r64["grads"][k]))
+           for k, g in ref["grads"].items()}
+    env = max(2 * max(e32.values()), GRAD_TOL)
+    worst = {}
+    for flag in (0, 1):
+        m = make()
+        with options(m.flatten_().rt, row3_gemm=flag):
+            logits = m(x.to(DEV))
+            losses = unet_hip.seg_losses(logits, t.to(DEV))
+            (losses[0] + losses[1]).backward()
+            torch.cuda.synchronize()
+        assert rel_max(logits.detach().cpu().numpy(), ref["logits"].numpy()) <= LOGIT_TOL
+        errs = grad_errors(m, r64["grads"])
+        k = max(errs, key=errs.get)
+        worst[flag] = (k, errs[k])
+        print(f"{variant} {B}x{H}x{W} row3_gemm={flag}: worst {k} {errs[k]:.3e} "
+              f"(fp32 oracle {e32[k]:.3e}, envelope {env:.3e})")
+    k, e = worst[1]
+    assert e <= max(env, 1.25 * worst[0][1]), f"{k}: {e:.3e} (default kernel {worst[0][1]:.3e})"

@@ -44,8 +44,9 @@ enum EpiMode {
 //   OP_AFFINE: per-channel BN affine scale*x + shift (forward consumers of a BN output)
 //   OP_AFFINE_RELU: the same followed by ReLU on channels [0, arelu) (BN -> ReLU order,
 //              models/mod.py:46-47; a concat [skip, up] has ReLU on the skip half only)
-//   OP_DZ    : BN+ReLU backward on the fly, dz = [y > 0] (A*do + B*y + C) per channel,
-//              from do (the operand pointer), y (its BN input) and coef = [A | B | C]
+//   OP_DZ    : BN+ReLU backward on the fly, dz = [y > 0] (A*do + B*(y - mean) + C) per
+//              channel, from do (the operand pointer), y (its BN input) and
+//              coef = [A | B | C | mean]
 enum LoadOp { OP_PLAIN = 0, OP_AFFINE = 1, OP_DZ = 2, OP_AFFINE_RELU = 3 };
 
 struct RowGemmArgs {
@@ -66,7 +67,7 @@ struct RowGemmArgs {
     int emode;
     const float* ay;     // OP_DZ: BN input y of the A operand (ld, off)
     int lday, offay;
-    const float* acoef;  // OP_DZ: [3][C] coefficients
+    const float* acoef;  // OP_DZ: [4][C] coefficients (A, B, Cc, mean: A do + B (y - mean) + Cc)
     const float* ey;     // E_STORE_BN: BN input y at the output position (ld, off)
     int ldey, offey;
     const float* escale;  // E_STORE_BN, BN -> ReLU order: affine of that BN (ReLU mask)
@@ -90,7 +91,7 @@ struct WgradArgs {
     int pps;         // pixels per split (multiple of the pixel chunk)
     int splits;
     float* slab;     // [splits][Mw][Nw]
-    const float* by;     // OP_DZ on B': BN input y (ld, off) and coef [3][CB]
+    const float* by;     // OP_DZ on B': BN input y (ld, off) and coef [4][CB]
     int ldby, offby;
     const float* bcoef;
     float* bias_slab;    // optional [splits][Nw]: column sums of B' (the bias gradient)
@@ -108,6 +109,10 @@ struct WgradArgs {
 // host launchers (kernels_gemm.hip)
 // tile ids: 0 = 128x128 (DBUF), 1 = 128x64, 2 = 256x64, 3 = 128x128 BK64 (kernels_gemm.hip)
 int launch_rowgemm(const RowGemmArgs& a, int tile, hipStream_t s);
+// 3x3 conv forward / dgrad with one row of taps per K-step (kernels_gemm.hip
+// rowgemm_row3_kernel); rowgemm_row3_ok: the launch's shape and operands are supported
+int launch_rowgemm_row3(const RowGemmArgs& a, hipStream_t s);
+int rowgemm_row3_ok(const RowGemmArgs& a);
 int rowgemm_tile_dims(int tile, int* bm, int* bn, int* bk);
 int rowgemm_tile_dbuf(int tile);
 // wgrad tile ids (kernels_gemm.hip WGRAD_TILES): 0 = 128x128, 1 = 64x64 one wave,

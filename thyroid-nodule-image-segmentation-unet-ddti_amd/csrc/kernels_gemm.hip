@@ -98,7 +98,7 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_kernel(RowGemmArgs
         rq[i] = decode(rm[i], H, W);
     }
 
-    f32x4 ra[AP], rb[BP], rsc, rsh, rcc;
+    f32x4 ra[AP], rb[BP], rsc, rsh, rcc, rmu;
     uint4 rb8[BP8];
     f32x4 ry[ADZ ? AP : 1];
     unsigned vmask = 0;
@@ -118,6 +118,7 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_kernel(RowGemmArgs
             rsc = *(const f32x4*)(p.acoef + c);
             rsh = *(const f32x4*)(p.acoef + p.C + c);
             rcc = *(const f32x4*)(p.acoef + 2 * p.C + c);
+            rmu = *(const f32x4*)(p.acoef + 3 * p.C + c);
         }
         vmask = 0;
 #pragma unroll
@@ -153,7 +154,7 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_kernel(RowGemmArgs
                     for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
             }
             if constexpr (ADZ) {
-                const f32x4 d = rsc * v + rsh * ry[i] + rcc;
+                const f32x4 d = rsc * v + rsh * (ry[i] - rmu) + rcc;
 #pragma unroll
                 for (int j = 0; j < 4; ++j) v[j] = ry[i][j] > 0.f ? d[j] : 0.f;
             }
@@ -247,6 +248,161 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_kernel(RowGemmArgs
 }
 
 // ------------------------------------------------------------------------------------
+// 3x3 conv row GEMM, one ROW of taps per K-step (dy fixed, dx = 0..2): the forward / dgrad
+// counterpart of wgrad_row3_kernel.  A block's BM output pixels are SEG consecutive pixels
+// of ROWS image rows (SEG = min(W, BM), ROWS = BM / SEG; W a multiple or a divisor of BM),
+// so for a fixed dy the three dx taps read the same input row segments shifted by one
+// pixel.  Per K-step (dy, 32-channel slice) the block stages those segments ONCE with a
+// one-pixel halo (ROWS * (SEG + 2) LDS rows, zero outside the image, BN affine applied as
+// in rowgemm_kernel) plus the three taps' weight slices, then runs 3 x 16 MFMA k-steps per
+// wave: A of tap dx for local pixel (r, x) is LDS row r * (SEG + 2) + x + dx.  A third of
+// the A staging of the one-tap kernel and one commit phase per three taps.  K order: dy,
+// channel slice, dx, k (a reordering of the one-tap kernel's sum); same epilogues.
+// ------------------------------------------------------------------------------------
+template <int AOP, int EMODE, class T>
+__global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_row3_kernel(RowGemmArgs p) {
+    constexpr bool AFFINE = AOP == OP_AFFINE || AOP == OP_AFFINE_RELU;
+    constexpr bool ARELU = AOP == OP_AFFINE_RELU;
+    constexpr int BM = T::BM, BN = T::BN, WM = T::WM, WN = T::WN, BK = T::BK;
+    constexpr int NTH = T::THREADS;
+    constexpr int WAVES_N = BN / WN;
+    constexpr int LDK = BK + 4;
+    constexpr int MT = WM / 32, NT = WN / 32;
+    constexpr int F4R = BK / 4;
+    constexpr int RPP = NTH / F4R;
+    constexpr int AMAX = BM + 2 * (BM / 16);     // halo rows for the narrowest grid (W = 16)
+    constexpr int AP = (AMAX + RPP - 1) / RPP, BP = BN / RPP;
+    static_assert(BP * RPP == BN, "loader shape");
+    __shared__ __attribute__((aligned(16))) float As[AMAX * LDK];
+    __shared__ __attribute__((aligned(16))) float Bs[3 * BN * LDK];
+    static_assert(AMAX * LDK * 4 >= (BM / 64) * 2 * BN * 8, "epilogue scratch (row_epilogue)");
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+    const int ntn = p.N / BN;
+    const int bid = p.xcd ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+    const int tile_m = bid / ntn, tile_n = bid - tile_m * ntn;
+    const int m0 = tile_m * BM, n0 = tile_n * BN;
+    const int H = p.H, W = p.W, C = p.C;
+    const int SEG = W < BM ? W : BM;          // pixels per image row in this block
+    const int arows = (BM / SEG) * (SEG + 2);
+    const Pix q0 = decode(m0, H, W);          // block start: rows q0.y .. q0.y + BM/SEG - 1
+
+    const int lrow = tid / F4R, lc4 = tid % F4R;
+    // halo rows this thread stages: (local output row, pixel) -> source pixel of row dy
+    int hy[AP], hx[AP];
+    bool hok[AP];
+#pragma unroll
+    for (int i = 0; i < AP; ++i) {
+        const int hr = lrow + i * RPP;
+        const int r = hr / (SEG + 2), xl = hr - r * (SEG + 2) - 1;
+        hok[i] = hr < arows;
+        hy[i] = q0.y + r;
+        hx[i] = q0.x + xl;
+    }
+
+    f32x4 ra[AP], rb[3][BP], rsc, rsh;
+    unsigned vmask = 0;
+    bool rrelu = false;
+    const int nc = C / BK;
+
+    auto issue = [&](int t) {
+        const int dy = t / nc, c = (t - dy * nc) * BK + lc4 * 4;
+        if constexpr (AFFINE) {
+            rsc = *(const f32x4*)(p.ascale + c);
+            rsh = *(const f32x4*)(p.ashift + c);
+            if constexpr (ARELU) rrelu = c < p.arelu;
+        }
+        vmask = 0;
+#pragma unroll
+        for (int i = 0; i < AP; ++i) {
+            const int yy = hy[i] + dy - 1, xx = hx[i];
+            const bool valid = hok[i] & (yy >= 0) & (yy < H) & (xx >= 0) & (xx < W);
+            vmask |= valid ? (1u << i) : 0u;
+            const int src = valid ? (q0.img * H + yy) * W + xx : m0;
+            ra[i] = *(const f32x4*)(p.a + (size_t)src * p.lda + p.aoff + c);
+        }
+#pragma unroll
+        for (int d = 0; d < 3; ++d)
+#pragma unroll
+            for (int i = 0; i < BP; ++i)
+                rb[d][i] = *(const f32x4*)(p.bt + (size_t)(n0 + lrow + i * RPP) * p.K +
+                                           (dy * 3 + d) * C + c);
+    };
+    auto commit = [&]() {
+#pragma unroll
+        for (int i = 0; i < AP; ++i) {
+            if (AP * RPP > AMAX && lrow + i * RPP >= AMAX) break;
+            f32x4 v = ra[i];
+            if constexpr (AFFINE) {
+                v = v * rsc + rsh;
+                if (ARELU && rrelu)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
+            }
+            if (!((vmask >> i) & 1u)) v = f32x4{0.f, 0.f, 0.f, 0.f};
+            *(f32x4*)&As[(lrow + i * RPP) * LDK + lc4 * 4] = v;
+        }
+#pragma unroll
+        for (int d = 0; d < 3; ++d)
+#pragma unroll
+            for (int i = 0; i < BP; ++i)
+                *(f32x4*)&Bs[(d * BN + lrow + i * RPP) * LDK + lc4 * 4] = rb[d][i];
+    };
+
+    f32x16 acc[MT][NT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    const int li = lane & 31, lh = lane >> 5;
+    int arow[MT];  // LDS halo row of this lane's output pixel for dx = 0
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+        const int ml = wm * WM + mt * 32 + li;
+        const int r = ml / SEG;
+        arow[mt] = r * (SEG + 2) + (ml - r * SEG);
+    }
+    const int nt_steps = 3 * nc;
+    issue(0);
+    commit();
+    __syncthreads();
+    for (int t = 0; t < nt_steps; ++t) {
+        if (t + 1 < nt_steps) issue(t + 1);
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            const float* bs = Bs + d * BN * LDK;
+#pragma unroll
+            for (int kk = 0; kk < BK / 8; ++kk) {
+                f32x4 af[MT], bf[NT];
+#pragma unroll
+                for (int mt = 0; mt < MT; ++mt)
+                    af[mt] = *(const f32x4*)&As[(arow[mt] + d) * LDK + kk * 8 + lh * 4];
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt)
+                    bf[nt] = *(const f32x4*)&bs[(wn * WN + nt * 32 + li) * LDK + kk * 8 + lh * 4];
+#pragma unroll
+                for (int s = 0; s < 4; ++s)
+#pragma unroll
+                    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                        for (int nt = 0; nt < NT; ++nt)
+                            acc[mt][nt] = mfma32(af[mt][s], bf[nt][s], acc[mt][nt]);
+            }
+        }
+        __syncthreads();
+        if (t + 1 < nt_steps) {
+            commit();
+            __syncthreads();
+        }
+    }
+    row_epilogue<EMODE, BM, BN, WM, WN>(p, acc, m0, n0, tile_m, wm, wn, lane, tid, As);
+}
+
+// ------------------------------------------------------------------------------------
 // Weight-gradient GEMM (reduction over pixels), same issue / compute / commit pipeline.
 // ------------------------------------------------------------------------------------
 // wgrad tile: block BM x BN, wave tile WM x WN, pixels per chunk BKP.
@@ -296,11 +452,12 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void wgrad_kernel(WgradArgs p) 
         if constexpr (ARELU) arl = ca0 + ac4 * 4 < p.arelu;
     }
 
-    f32x4 ca = {0, 0, 0, 0}, cb = ca, cc = ca;  // OP_DZ coefficients of this thread's columns
+    f32x4 ca = {0, 0, 0, 0}, cb = ca, cc = ca, cm = ca;  // OP_DZ coefficients of this thread's columns
     if constexpr (BDZ) {
         ca = *(const f32x4*)(p.bcoef + cb0 + bc4 * 4);
         cb = *(const f32x4*)(p.bcoef + p.CB + cb0 + bc4 * 4);
         cc = *(const f32x4*)(p.bcoef + 2 * p.CB + cb0 + bc4 * 4);
+        cm = *(const f32x4*)(p.bcoef + 3 * p.CB + cb0 + bc4 * 4);
     }
     const bool bsum = p.bias_slab != nullptr && tm == 0;
     double bacc[4] = {0.0, 0.0, 0.0, 0.0};  // f64: the bias gradient is a small sum of +/- terms
@@ -357,7 +514,7 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void wgrad_kernel(WgradArgs p) 
         for (int i = 0; i < BP; ++i) {
             f32x4 v = rb[i];
             if constexpr (BDZ) {
-                const f32x4 d = ca * v + cb * ryb[i] + cc;
+                const f32x4 d = ca * v + cb * (ryb[i] - cm) + cc;
 #pragma unroll
                 for (int j = 0; j < 4; ++j) v[j] = ryb[i][j] > 0.f ? d[j] : 0.f;
             }
@@ -487,11 +644,12 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void wgrad_row3_kernel(WgradArg
         sh = *(const f32x4*)(p.ashift + ca0 + ac4 * 4);
         if constexpr (ARELU) arl = ca0 + ac4 * 4 < p.arelu;
     }
-    f32x4 ca = {0, 0, 0, 0}, cb = ca, cc = ca;
+    f32x4 ca = {0, 0, 0, 0}, cb = ca, cc = ca, cm = ca;
     if constexpr (BDZ) {
         ca = *(const f32x4*)(p.bcoef + cb0 + bc4 * 4);
         cb = *(const f32x4*)(p.bcoef + p.CB + cb0 + bc4 * 4);
         cc = *(const f32x4*)(p.bcoef + 2 * p.CB + cb0 + bc4 * 4);
+        cm = *(const f32x4*)(p.bcoef + 3 * p.CB + cb0 + bc4 * 4);
     }
     const bool bsum = p.bias_slab != nullptr && tm == 0;
     double bacc[4] = {0.0, 0.0, 0.0, 0.0};
@@ -549,7 +707,7 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void wgrad_row3_kernel(WgradArg
         for (int i = 0; i < BP; ++i) {
             f32x4 v = rb[i];
             if constexpr (BDZ) {
-                const f32x4 d = ca * v + cb * ryb[i] + cc;
+                const f32x4 d = ca * v + cb * (ryb[i] - cm) + cc;
 #pragma unroll
                 for (int j = 0; j < 4; ++j) v[j] = ryb[i][j] > 0.f ? d[j] : 0.f;
             }
@@ -974,6 +1132,50 @@ static int rowgemm_dispatch(const RowGemmArgs& a, int tile, hipStream_t s) {
             return rowgemm_tile<G_IDENT, OP_AFFINE, E_CONVT, false>(a, tile, s);
     }
     return -1;  // combination not instantiated
+}
+
+// tap-row kernel tiles: 128 x 128 (4 waves of 64x64, 76 KB LDS, 2 blocks / CU) and
+// 128 x 64 (4 waves of 64x32, 48 KB, 3 blocks / CU) for N = 64 outputs
+using Row3Tile0 = RowTile<128, 128, 64, 64, 32, false, 2>;
+using Row3Tile1 = RowTile<128, 64, 64, 32, 32, false, 3>;
+
+template <int AOP, int EMODE, class T>
+static int row3_go(const RowGemmArgs& a, hipStream_t s) {
+    const dim3 grid((a.M / T::BM) * (a.N / T::BN));
+    hipLaunchKernelGGL((rowgemm_row3_kernel<AOP, EMODE, T>), grid, dim3(T::THREADS), 0, s, a);
+    return (int)hipGetLastError();
+}
+
+template <class T>
+static int row3_dispatch(const RowGemmArgs& a, hipStream_t s) {
+    const bool aff = a.ascale != nullptr;
+    if (a.emode == E_BIAS_RELU_STATS)
+        return aff ? row3_go<OP_AFFINE, E_BIAS_RELU_STATS, T>(a, s)
+                   : row3_go<OP_PLAIN, E_BIAS_RELU_STATS, T>(a, s);
+    if (a.emode == E_STATS)
+        return a.arelu ? row3_go<OP_AFFINE_RELU, E_STATS, T>(a, s)
+                       : (aff ? -1 : row3_go<OP_PLAIN, E_STATS, T>(a, s));
+    if (aff) return -1;
+    if (a.emode == E_STORE) return row3_go<OP_PLAIN, E_STORE, T>(a, s);
+    if (a.emode == E_STORE_BN) return row3_go<OP_PLAIN, E_STORE_BN, T>(a, s);
+    if (a.emode == E_ADD) return row3_go<OP_PLAIN, E_ADD, T>(a, s);
+    return -1;
+}
+
+int rowgemm_row3_ok(const RowGemmArgs& a) {
+    const int bm = 128, bn = a.N % 128 == 0 ? 128 : 64;
+    return a.amode == G_CONV3 && a.acoef == nullptr && a.bt != nullptr && a.bt16 == nullptr &&
+           a.K == 9 * a.C && a.C % 32 == 0 && a.N % bn == 0 && a.W >= 16 &&
+           (a.W % bm == 0 || bm % a.W == 0) && a.M % bm == 0 && a.H % (bm / (a.W < bm ? a.W : bm)) == 0 &&
+           (a.emode == E_BIAS_RELU_STATS || a.emode == E_STATS || a.emode == E_STORE ||
+            a.emode == E_STORE_BN || a.emode == E_ADD);
+}
+
+int launch_rowgemm_row3(const RowGemmArgs& a, hipStream_t s) {
+    if (!rowgemm_row3_ok(a)) return -1;
+    if ((a.emode == E_STORE_BN || a.emode == E_RESID) != (a.ey != nullptr)) return -1;
+    if ((a.escale != nullptr) != (a.eshift != nullptr) || (a.arelu && !a.ascale)) return -1;
+    return a.N % 128 == 0 ? row3_dispatch<Row3Tile0>(a, s) : row3_dispatch<Row3Tile1>(a, s);
 }
 
 int launch_rowgemm(const RowGemmArgs& a, int tile, hipStream_t s) {

@@ -232,10 +232,11 @@ __global__ __launch_bounds__(256) void conv_first_wgrad_kernel(const float* __re
     const int r1 = min(P, r0 + per);
     for (int m = r0 + g; m < r1; m += rpp) {
         const int xx = m % W, t = m / W, yy = t % H, img = t / H;
-        // dz = [y > 0] (A do + B y + C) (or unmasked, BN -> ReLU order): BN backward fused
+        // dz = [y > 0] (A do + B (y - mean) + C) (or unmasked, BN -> ReLU order): BN backward fused
         const f32x4 dv = *(const f32x4*)(dout + (int64_t)m * C + 4 * q);
         const f32x4 yv = *(const f32x4*)(y + (int64_t)m * C + 4 * q);
-        const f32x4 dd = *(const f32x4*)(coef + 4 * q) * dv + *(const f32x4*)(coef + C + 4 * q) * yv +
+        const f32x4 dd = *(const f32x4*)(coef + 4 * q) * dv +
+                         *(const f32x4*)(coef + C + 4 * q) * (yv - *(const f32x4*)(coef + 3 * C + 4 * q)) +
                          *(const f32x4*)(coef + 2 * C + 4 * q);
         f32x4 d;
 #pragma unroll
@@ -503,7 +504,7 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const float* __restric
 // BatchNorm backward (train mode).  The producer of the BN-output gradient leaves column
 // partials [G][2][C] = {S1 = sum do, S2 = sum do*y} (y = BN input; with BN -> ReLU order
 // do is already masked by the ReLU).  From them: dgamma = invstd (S2 - mean S1),
-// dbeta = S1 and the coefficients of dz = A do + B y + Cc (model.py order additionally
+// dbeta = S1 and the coefficients of dz = A do + B (y - mean) + Cc, coef[4][C] (model.py order additionally
 // masks dz by [y > 0], the ReLU in front of the BN: model.py:37-38,40-41).
 // -------------------------------------------------------------------------------------
 __global__ void bn_bwd_finalize2_kernel(const float* __restrict__ part, int G, int C, double count,
@@ -519,14 +520,17 @@ __global__ void bn_bwd_finalize2_kernel(const float* __restrict__ part, int G, i
     const double is = invstd[c], mu = mean[c];
     const double sdxh = is * (s2 - mu * s1);
     const double k = (double)gamma[c] * is;
+    // centred form dz = A do + B (y - mean) + Cc: B (y - mean) is formed from the small
+    // centred value, not as B y + (large constant), which cancelled to a few ulp of B * mean
     coef[c] = (float)k;
     coef[C + c] = (float)(-k * is * sdxh / count);
-    coef[2 * C + c] = (float)(-k * s1 / count + k * is * mu * sdxh / count);
+    coef[2 * C + c] = (float)(-k * s1 / count);
+    coef[3 * C + c] = (float)mu;
     dgamma[c] = (float)sdxh;
     dbeta[c] = (float)s1;
 }
 
-// dz = A do + B y + C in place, masked by [y > 0] when `mask` (ReLU before the BN).
+// dz = A do + B (y - mean) + C in place, masked by [y > 0] when `mask` (ReLU before the BN).
 // Row form (C / 4 divides 256): each thread keeps one channel quad and its coefficients
 // in registers and walks pixel rows, so there is no per-element index division.
 __global__ __launch_bounds__(256) void bn_dz_rows_kernel(float* __restrict__ d,
@@ -536,12 +540,12 @@ __global__ __launch_bounds__(256) void bn_dz_rows_kernel(float* __restrict__ d,
     const int tpr = C / 4, rpp = 256 / tpr;
     const int c = (threadIdx.x % tpr) * 4;
     const f32x4 ka = *(const f32x4*)(coef + c), kb = *(const f32x4*)(coef + C + c),
-                kc = *(const f32x4*)(coef + 2 * C + c);
+                kc = *(const f32x4*)(coef + 2 * C + c), km = *(const f32x4*)(coef + 3 * C + c);
     for (int64_t m = (int64_t)blockIdx.x * rpp + threadIdx.x / tpr; m < P;
          m += (int64_t)gridDim.x * rpp) {
         f32x4* pd = (f32x4*)(d + m * C + c);
         const f32x4 v = *(const f32x4*)(y + m * ld + off + c);
-        const f32x4 r = ka * (*pd) + kb * v + kc;
+        const f32x4 r = ka * (*pd) + kb * (v - km) + kc;
         f32x4 o;
 #pragma unroll
         for (int j = 0; j < 4; ++j) o[j] = (!mask || v[j] > 0.f) ? r[j] : 0.f;
@@ -575,12 +579,13 @@ __global__ __launch_bounds__(256) void bn_dz16_kernel(float* __restrict__ d, con
                     }
                 }
             }
-            f32x4 ka[2], kb[2], kc[2];
+            f32x4 ka[2], kb[2], kc[2], km[2];
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 ka[h] = *(const f32x4*)(coef + c + 4 * h);
                 kb[h] = *(const f32x4*)(coef + C + c + 4 * h);
                 kc[h] = *(const f32x4*)(coef + 2 * C + c + 4 * h);
+                km[h] = *(const f32x4*)(coef + 3 * C + c + 4 * h);
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) {
@@ -590,7 +595,7 @@ __global__ __launch_bounds__(256) void bn_dz16_kernel(float* __restrict__ d, con
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
                     const f32x4 v = yv[u][h];
-                    const f32x4 r = ka[h] * dv[u][h] + kb[h] * v + kc[h];
+                    const f32x4 r = ka[h] * dv[u][h] + kb[h] * (v - km[h]) + kc[h];
                     f32x4 o;
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
@@ -615,7 +620,8 @@ __global__ void bn_dz_kernel(float* __restrict__ d, const float* __restrict__ y,
         const int64_t m = i / c4n;
         f32x4* pd = (f32x4*)(d + m * C + c);
         const f32x4 v = *(const f32x4*)(y + m * ld + off + c);
-        const f32x4 r = *(const f32x4*)(coef + c) * (*pd) + *(const f32x4*)(coef + C + c) * v +
+        const f32x4 r = *(const f32x4*)(coef + c) * (*pd) +
+                        *(const f32x4*)(coef + C + c) * (v - *(const f32x4*)(coef + 3 * C + c)) +
                         *(const f32x4*)(coef + 2 * C + c);
         f32x4 o;
 #pragma unroll

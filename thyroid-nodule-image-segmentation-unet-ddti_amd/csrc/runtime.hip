@@ -113,6 +113,8 @@ struct Options {
     int xcd_remap = 0;         // ... f32 GEMMs: 0 none, 1 both, 2 row GEMMs, 3 wgrad
     int wgrad_stream = 0;      // weight gradients on a second stream (bit-identical)
     int dz_in_loaders = 0;     // BN-backward dz inside the GEMM loaders (model.py order)
+    int row3_gemm = 0;         // f32 3x3 forward / dgrad on the tap-row kernel
+                               // (rowgemm_row3_kernel) where its shapes allow
 };
 struct OptionDesc {
     const char* name;
@@ -130,6 +132,7 @@ const OptionDesc OPTION_TABLE[] = {
     {"wg16_tile", &Options::wg16_tile},         {"wg16t", &Options::wg16t},
     {"xcd16", &Options::xcd16},                 {"xcd_remap", &Options::xcd_remap},
     {"wgrad_stream", &Options::wgrad_stream},   {"dz_in_loaders", &Options::dz_in_loaders},
+    {"row3_gemm", &Options::row3_gemm},
 };
 
 }  // namespace
@@ -736,7 +739,7 @@ void make_plan(unet_ctx* c, int N, int H, int W, bool training, char* base, Plan
         p.hpart = b.take<float>((int64_t)WIDE_G *
                                 std::max<int64_t>(10 * c->base, (int64_t)c->out_ch * (c->base + 1)));
         p.bslab = b.take<float>(std::max<int64_t>(bmax, 1));
-        p.coef = b.take<float>(3 * (int64_t)c->cmax);
+        p.coef = b.take<float>(4 * (int64_t)c->cmax);  // BN-backward dz coefficients [4][C]
     } else {
         p.g[0] = p.g[1] = p.g[2] = p.slab = p.part = p.part2 = p.hpart = p.bslab = p.coef = nullptr;
         for (int l = 0; l < D; ++l) p.dcat[l] = nullptr;
@@ -803,6 +806,16 @@ std::string tlabel(const char* fam, int tile, int layer) {
     char b[112];
     snprintf(b, sizeof b, "%s/rowgemm_%dx%dx%d%s|%d", fam, bm, bn, bk,
              rowgemm_tile_dbuf(tile) ? "d" : "", layer);
+    return b;
+}
+
+// f32 3x3 forward / dgrad on the tap-row kernel (option row3_gemm)
+bool use_row3(const unet_ctx* c, const RowGemmArgs& g) {
+    return c->opt.row3_gemm && !c->bf16 && rowgemm_row3_ok(g);
+}
+std::string r3label(const char* fam, const RowGemmArgs& g, int layer) {
+    char b[112];
+    snprintf(b, sizeof b, "%s/rowgemm3_128x%d|%d", fam, g.N % 128 == 0 ? 128 : 64, layer);
     return b;
 }
 
@@ -1013,8 +1026,12 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
                     launch_rowgemm16(g, tile, s));
                 return stats_finalize(c, L, p, i, R, M, training, prm, bn_run, bn_cnt);
             }
-            const int tile = pick_tile(c, C.cout, false, c->bf16, M);
             R = bn_groups(M);
+            if (use_row3(c, g)) {
+                RUN(r3label("conv_fwd", g, i), 2.0 * M * C.cout * 9 * C.cin, launch_rowgemm_row3(g, s));
+                return stats_finalize(c, L, p, i, R, M, training, prm, bn_run, bn_cnt);
+            }
+            const int tile = pick_tile(c, C.cout, false, c->bf16, M);
             RUN(tlabel("conv_fwd", tile, i), 2.0 * M * C.cout * 9 * C.cin, launch_rowgemm(g, tile, s));
         }
         return stats_finalize(c, L, p, i, R, M, training, prm, bn_run, bn_cnt);
@@ -1209,7 +1226,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
     // BatchNorm backward is fused: the producer of `do` (head_bwd, a dgrad epilogue,
     // maxpool_bwd) leaves {sum do, sum do*y} column partials in p.part (do already masked by
     // the following ReLU in BN -> ReLU order); this finalize turns them into dgamma, dbeta
-    // and the per-channel coefficients of dz = A do + B y + C (masked by [y > 0] in
+    // and the per-channel coefficients of dz = A do + B (y - mean) + C (masked by [y > 0] in
     // ReLU -> BN order).
     auto bn_finalize = [&](int i, int R) -> int {
         const ConvL& C = c->conv[i];
@@ -1226,7 +1243,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
                                p.invstd[i], p.coef, grads + B.g, grads + B.b, s));
         return 0;
     };
-    // dz = A do + B y + C either as one elementwise pass over do (default) or inside the
+    // dz = A do + B (y - mean) + C either as one elementwise pass over do (default) or inside the
     // wgrad / dgrad loaders (UNET_DZ_IN_LOADERS=1, ReLU -> BN order only: fewer passes, but
     // every 3x3 tap re-gathers both do and y -- measured slower on MI355X, kept for A/B runs)
     const int dz_mask = c->bn_relu ? 0 : 1;
@@ -1361,8 +1378,13 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
                     launch_rowgemm16(g, tile, s));
                 return 0;
             }
-            const int tile = pick_tile(c, C.cin, true, c->bf16, P);
             if (rows) *rows = bn_groups(P);
+            if (use_row3(c, g)) {
+                RUN(r3label("conv_dgrad", g, i), 2.0 * P * C.cout * 9 * C.cin,
+                    launch_rowgemm_row3(g, s));
+                return 0;
+            }
+            const int tile = pick_tile(c, C.cin, true, c->bf16, P);
             RUN(tlabel("conv_dgrad", tile, i), 2.0 * P * C.cout * 9 * C.cin, launch_rowgemm(g, tile, s));
         }
         return 0;
