@@ -638,3 +638,45 @@ def test_row3_gemm_matches_oracle(variant, B, H, W):
               f"(fp32 oracle {e32[k]:.3e}, envelope {env:.3e})")
     k, e = worst[1]
     assert e <= max(env, 1.25 * worst[0][1]), f"{k}: {e:.3e} (default kernel {worst[0][1]:.3e})"
+
+
+@pytest.mark.parametrize("variant,B,H,W", [("model", 2, 64, 64), ("model", 8, 256, 256),
+                                           ("model", 1, 48, 80), ("mod", 2, 128, 64),
+                                           ("res", 2, 64, 64)])
+def test_pipe_gemm_bit_identical(variant, B, H, W):
+    """Row-GEMM tiles 16..19 (kernels_gemm_pipe.hip: the software-pipelined schedule of the
+    128x128 / 128x64 f32 tiles, global loads one or two chunks ahead; 18 / 16 are the
+    defaults) walk K in the same order with the same fused prologue and the same epilogues
+    as the register-staged rowgemm_kernel tiles (4, 0, 1), so a training step -- logits and
+    the whole gradient arena -- is bit-identical across the three schedules.  48x80 has M
+    tiles that end past M (rows masked in the gather and the guarded epilogue path); the
+    ResUNet covers the 1x1 skip GEMMs (E_RESID) and E_ADD, the ConvTranspose GEMMs run in
+    every variant."""
+    import unet_hip
+    from _helpers import hip_mod_model, options
+    from oracle import mod_ref_cpu as MO
+    x, t = inputs(43, B, H, W)
+    outs = []
+    for tiles in ((4, 0, 1), (16, 16, 17), (18, 18, 19)):
+        if variant == "model":
+            m = hip_model(O.make_params(42), DEV)
+        elif variant == "mod":
+            m = hip_mod_model(MO.make_params(5, 64, 3), DEV, 64, 3)
+        else:
+            m = unet_hip.ResUNet(1, 1, base_filters=64, depth=3)
+            sd = m.state_dict()
+            sd.update({k: v.clone() for k, v in MO.res_make_params(42, 64, 3).items()})
+            m.load_state_dict(sd)
+            m = m.to(DEV).train()
+        with options(m.flatten_().rt, tile_n128=tiles[0], tile_n128_dgrad=tiles[1],
+                     tile_n64=tiles[2]):
+            logits = m(x.to(DEV))
+            l = unet_hip.seg_losses(logits, t.to(DEV))
+            (l[0] + l[1]).backward()
+            torch.cuda.synchronize()
+        outs.append((logits.detach().clone(), m._state.grad_arena.clone()))
+        del m
+    for i in (1, 2):
+        assert torch.equal(outs[0][0], outs[i][0]), i
+        d = (outs[0][1] - outs[i][1]).abs().max().item()
+        assert torch.equal(outs[0][1], outs[i][1]), (i, d)

@@ -115,6 +115,10 @@ int launch_rowgemm_row3(const RowGemmArgs& a, hipStream_t s);
 int rowgemm_row3_ok(const RowGemmArgs& a);
 int rowgemm_tile_dims(int tile, int* bm, int* bn, int* bk);
 int rowgemm_tile_dbuf(int tile);
+// software-pipelined f32 row GEMM (kernels_gemm_pipe.hip); tile 0 = 128x128, 1 = 128x64.
+// launch_rowgemm routes tile ids 16 / 17 here.
+int rowgemm_pipe_ok(const RowGemmArgs& a);
+int launch_rowgemm_pipe(const RowGemmArgs& a, int tile, hipStream_t s);
 // wgrad tile ids (kernels_gemm.hip WGRAD_TILES): 0 = 128x128, 1 = 64x64 one wave,
 // 2 = 128x64 two waves, 3 = 64x128 two waves, 4 = 64x64 four waves, 5 = 128x64 four waves
 // 20.. = one row of 3x3 taps per block (3 accumulator sets; BM = channels of ONE tap):

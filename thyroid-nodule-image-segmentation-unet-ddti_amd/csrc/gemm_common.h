@@ -113,6 +113,15 @@ __device__ __forceinline__ void row_epilogue(const RowGemmArgs& p, f32x16 (&acc)
     static_assert(WM % 64 == 0 && BM % 128 == 0, "BN partial groups need 64-row units");
     const int li = lane & 31, lh = lane >> 5;
     const int H = p.H, W = p.W;
+    // FULL: the block tile lies inside M, so no row needs a guard.  Row (mt, r) of the wave
+    // then has a wave-uniform base address (SGPRs) and each lane a fixed 32-bit byte offset
+    // (4 lh rows + its column): one store per element, no per-element branch or 64-bit
+    // address arithmetic.  Same values, same order as the guarded path.
+    const bool full = m0 + BM <= p.M;
+    const int wrow = __builtin_amdgcn_readfirstlane(m0 + wm * WM);
+    auto urow = [&](const float* base, int ld, int off, int mt, int r) {
+        return (const char*)(base + (size_t)(wrow + mt * 32 + (r & 3) + 8 * (r >> 2)) * ld + off);
+    };
     if constexpr (EMODE == E_BIAS_RELU_STATS || EMODE == E_STATS) {
         constexpr bool BR = EMODE == E_BIAS_RELU_STATS;
         float s1[U][NT], s2[U][NT];
@@ -122,18 +131,31 @@ __device__ __forceinline__ void row_epilogue(const RowGemmArgs& p, f32x16 (&acc)
             const float b = BR ? p.bias[n] : 0.f;
 #pragma unroll
             for (int u = 0; u < U; ++u) s1[u][nt] = s2[u][nt] = 0.f;
+            if (full) {
+                const unsigned lo = (unsigned)(4 * lh * p.ldo + n) * 4u;
 #pragma unroll
-            for (int mt = 0; mt < MT; ++mt)
+                for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int m = m0 + wm * WM + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-                    if (m < p.M) {
+                    for (int r = 0; r < 16; ++r) {
                         const float v = BR ? fmaxf(acc[mt][nt][r] + b, 0.f) : acc[mt][nt][r];
-                        p.out[(size_t)m * p.ldo + p.ooff + n] = v;
+                        *(float*)(urow(p.out, p.ldo, p.ooff, mt, r) + lo) = v;
                         s1[mt / 2][nt] += v;
                         s2[mt / 2][nt] = __builtin_fmaf(v, v, s2[mt / 2][nt]);
                     }
-                }
+            } else {
+#pragma unroll
+                for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int m = m0 + wm * WM + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                        if (m < p.M) {
+                            const float v = BR ? fmaxf(acc[mt][nt][r] + b, 0.f) : acc[mt][nt][r];
+                            p.out[(size_t)m * p.ldo + p.ooff + n] = v;
+                            s1[mt / 2][nt] += v;
+                            s2[mt / 2][nt] = __builtin_fmaf(v, v, s2[mt / 2][nt]);
+                        }
+                    }
+            }
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 s1[u][nt] += __shfl_xor(s1[u][nt], 32);
@@ -179,8 +201,21 @@ __device__ __forceinline__ void row_epilogue(const RowGemmArgs& p, f32x16 (&acc)
             const float es = emask ? p.escale[n] : 0.f, eb = emask ? p.eshift[n] : 0.f;
 #pragma unroll
             for (int u = 0; u < U; ++u) q[u][nt][0] = q[u][nt][1] = 0.0;
+            const unsigned lo = (unsigned)(4 * lh * p.ldo + n) * 4u;
+            const unsigned ly = (unsigned)(4 * lh * p.ldey + n) * 4u;
 #pragma unroll
-            for (int mt = 0; mt < MT && !PRELOAD; ++mt)
+            for (int mt = 0; mt < MT && !PRELOAD && full; ++mt)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    float v = acc[mt][nt][r];
+                    const float y = *(const float*)(urow(p.ey, p.ldey, p.offey, mt, r) + ly);
+                    if (emask && !(es * y + eb > 0.f)) v = 0.f;
+                    *(float*)(urow(p.out, p.ldo, p.ooff, mt, r) + lo) = v;
+                    q[mt / 2][nt][0] += v;
+                    q[mt / 2][nt][1] = __builtin_fma((double)v, (double)y, q[mt / 2][nt][1]);
+                }
+#pragma unroll
+            for (int mt = 0; mt < MT && !PRELOAD && !full; ++mt)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     const int m = m0 + wm * WM + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
@@ -315,13 +350,22 @@ __device__ __forceinline__ void row_epilogue(const RowGemmArgs& p, f32x16 (&acc)
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) {
             const int n = n0 + wn * WN + nt * 32 + li;
+            const unsigned lo = (unsigned)(4 * lh * p.ldo + n) * 4u;
+            if (full) {
 #pragma unroll
-            for (int mt = 0; mt < MT; ++mt)
+                for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int m = m0 + wm * WM + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-                    if (m < p.M) p.out[(size_t)m * p.ldo + p.ooff + n] = acc[mt][nt][r];
-                }
+                    for (int r = 0; r < 16; ++r)
+                        *(float*)(urow(p.out, p.ldo, p.ooff, mt, r) + lo) = acc[mt][nt][r];
+            } else {
+#pragma unroll
+                for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int m = m0 + wm * WM + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                        if (m < p.M) p.out[(size_t)m * p.ldo + p.ooff + n] = acc[mt][nt][r];
+                    }
+            }
         }
     }
 }

@@ -1070,6 +1070,12 @@ static int rowgemm_tile(const RowGemmArgs& a, int tile, hipStream_t s) {
 }
 
 int rowgemm_tile_dims(int tile, int* bm, int* bn, int* bk) {
+    if (tile >= 16 && tile <= 19) {  // rowgemm_pipe_kernel (18, 19: loads two chunks ahead)
+        *bm = 128;
+        *bn = tile % 2 == 0 ? 128 : 64;
+        *bk = 32;
+        return 0;
+    }
 #define RG_DIMS(id, T)   \
     if (tile == id) {    \
         *bm = T::BM;     \
@@ -1083,6 +1089,7 @@ int rowgemm_tile_dims(int tile, int* bm, int* bn, int* bk) {
 }
 
 int rowgemm_tile_dbuf(int tile) {
+    if (tile >= 16 && tile <= 19) return 2;  // pipelined
 #define RG_DB(id, T) \
     if (tile == id) return T::DBUF ? 1 : 0;
     ROWGEMM_TILES(RG_DB)
@@ -1186,6 +1193,13 @@ int launch_rowgemm(const RowGemmArgs& a, int tile, hipStream_t s) {
     if ((a.escale != nullptr) != (a.eshift != nullptr) || (a.arelu && !aff)) return -1;
     if (a.emode == E_RESID && !a.escale) return -1;
     if ((a.bt != nullptr) == (a.bt16 != nullptr)) return -1;  // exactly one weight image
+    // ids 16..19: the software-pipelined f32 kernel (128x128 / 128x64, loads one or two
+    // chunks ahead); operands it does not take (bf16 weights, dz in the loader, > 2 GB
+    // offsets) run the same tile shape here
+    if (tile >= 16 && tile <= 19) {
+        if (rowgemm_pipe_ok(a)) return launch_rowgemm_pipe(a, tile - 16, s);
+        tile = tile % 2 == 0 ? 4 : 1;
+    }
     return a.bt16 ? rowgemm_dispatch<true>(a, tile, s) : rowgemm_dispatch<false>(a, tile, s);
 }
 

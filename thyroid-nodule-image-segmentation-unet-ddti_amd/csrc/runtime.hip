@@ -98,7 +98,7 @@ struct Options {
     int wgrad_tile_w = 0;      // f32 wgrad tile, both channel counts multiples of 128
     int wgrad_tile_n = 7;      // ... 64-channel layers (64x64, 3 waves/SIMD)
     int wgrad16_tile = 0;      // register-staged bf16 wgrad tile (128-multiples)
-    int tile_n128 = -1;        // f32 row-GEMM tile, N % 128 == 0 (-1 = by grid size)
+    int tile_n128 = -1;        // f32 row-GEMM tile, N % 128 == 0 (-1 = pick_tile's default)
     int tile_n128_dgrad = -1;  // ... dgrad-type
     int tile_n64 = 1;          // ... N = 64 outputs
     int tile16_n128 = 6;       // register-staged bf16 row-GEMM tiles
@@ -781,31 +781,32 @@ struct Launcher {
     }
 };
 
-// Row-GEMM tile choice for an output width N (tile ids: kernels_gemm.hip ROWGEMM_TILES).
-// Defaults from tools/gemm_tune (r01, 15 rounds, profiles/r01_gemm_tune.txt):
-//  * forward-type, N % 128 == 0: 128x128/BK32 single LDS image; at >= 2048 blocks the
-//    3-waves/SIMD variant (t7) is 2-4 % faster, below that its partial last round of
-//    blocks costs more than it gains (L3: 103 vs 125 TF/s), so t4;
-//  * dgrad-type, N % 128 == 0: double-buffered 128x128 (t0) except on the big grids
-//    (>= 4096 blocks) where the single-image t4 is 2-4 % faster;
-//  * N = 64 outputs: 128x64 (t1).
+// Row-GEMM tile choice for an output width N (tile ids: kernels_gemm.hip ROWGEMM_TILES,
+// 16..19 = kernels_gemm_pipe.hip).
+//  * f32, N % 128 == 0: the software-pipelined 128x128 kernel, forward with its global loads
+//    two chunks ahead (18), dgrad one chunk ahead (16).  r02 A/B (tools/gpu_ab.sh, config 2):
+//    401 img/s against 390 for the register-staged tiles (t7 / t4 / t0 by grid size), the
+//    dominant kernel 128.9 vs 122.2 TF/s; the two schedules store identical bits
+//    (tests/test_gpu_parity.py::test_pipe_gemm_bit_identical);
+//  * f32, N = 64 outputs: 128x64 (t1) -- the pipelined 128x64 (19) wins on the forward
+//    GEMMs and loses on the dgrads and the level-0 ConvT, net neutral.
 // bf16 MFMA (register-staged): a chunk of 64 K per barrier (4 MFMA k-steps) by default.
 // Options tile_* override (tuning runs; -1 = automatic).
-int pick_tile(const unet_ctx* c, int N, bool dgrad, bool bf16, int64_t M = 0) {
+int pick_tile(const unet_ctx* c, int N, bool dgrad, bool bf16) {
     const Options& o = c->opt;
     if (bf16) return N % 128 == 0 ? (dgrad ? o.tile16_n128_dgrad : o.tile16_n128) : o.tile16_n64;
     if (N % 128) return o.tile_n64;
-    const int64_t blocks = (M + 127) / 128 * (N / 128);
-    if (dgrad) return o.tile_n128_dgrad >= 0 ? o.tile_n128_dgrad : (blocks >= 4096 ? 4 : 0);
-    return o.tile_n128 >= 0 ? o.tile_n128 : (blocks >= 2048 ? 7 : 4);
+    if (dgrad) return o.tile_n128_dgrad >= 0 ? o.tile_n128_dgrad : 16;
+    return o.tile_n128 >= 0 ? o.tile_n128 : 18;
 }
 
 std::string tlabel(const char* fam, int tile, int layer) {
     int bm = 0, bn = 0, bk = 0;
     rowgemm_tile_dims(tile, &bm, &bn, &bk);
     char b[112];
+    const int db = rowgemm_tile_dbuf(tile);  // 1 = two LDS images, 2 = software-pipelined
     snprintf(b, sizeof b, "%s/rowgemm_%dx%dx%d%s|%d", fam, bm, bn, bk,
-             rowgemm_tile_dbuf(tile) ? "d" : "", layer);
+             db == 2 ? "p" : (db ? "d" : ""), layer);
     return b;
 }
 
@@ -1031,7 +1032,7 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
                 RUN(r3label("conv_fwd", g, i), 2.0 * M * C.cout * 9 * C.cin, launch_rowgemm_row3(g, s));
                 return stats_finalize(c, L, p, i, R, M, training, prm, bn_run, bn_cnt);
             }
-            const int tile = pick_tile(c, C.cout, false, c->bf16, M);
+            const int tile = pick_tile(c, C.cout, false, c->bf16);
             RUN(tlabel("conv_fwd", tile, i), 2.0 * M * C.cout * 9 * C.cin, launch_rowgemm(g, tile, s));
         }
         return stats_finalize(c, L, p, i, R, M, training, prm, bn_run, bn_cnt);
@@ -1078,7 +1079,7 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
                 launch_rowgemm16(g, tile, s));
             return 0;
         }
-        const int tile = pick_tile(c, T.cout, false, c->bf16, 4 * (int64_t)g.M);  // grid N = 4 cout
+        const int tile = pick_tile(c, T.cout, false, c->bf16);  // grid N = 4 cout
         RUN(tlabel("convT_fwd", tile, 100 + k), 2.0 * g.M * g.N * g.K, launch_rowgemm(g, tile, s));
         return 0;
     };
@@ -1117,7 +1118,7 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
         g.offey = p.offy[i2];
         g.escale = p.scale[i2];
         g.eshift = p.shift[i2];
-        const int tile = pick_tile(c, CL.cout, false, false, M);
+        const int tile = pick_tile(c, CL.cout, false, false);
         RUN(tlabel("skip_fwd", tile, b), 2.0 * M * CL.cout * CL.cin, launch_rowgemm(g, tile, s));
         return 0;
     };
@@ -1384,7 +1385,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
                     launch_rowgemm_row3(g, s));
                 return 0;
             }
-            const int tile = pick_tile(c, C.cin, true, c->bf16, P);
+            const int tile = pick_tile(c, C.cin, true, c->bf16);
             RUN(tlabel("conv_dgrad", tile, i), 2.0 * P * C.cout * 9 * C.cin, launch_rowgemm(g, tile, s));
         }
         return 0;
@@ -1508,7 +1509,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
                 launch_rowgemm16(g, tile, s));
             return 0;
         }
-        const int tile = pick_tile(c, T.cin, true, c->bf16, Pin);
+        const int tile = pick_tile(c, T.cin, true, c->bf16);
         *rows = bn_groups(Pin);
         RUN(tlabel("convT_dgrad", tile, 100 + k), 2.0 * Pin * T.cin * 4 * T.cout, launch_rowgemm(g, tile, s));
         return 0;
@@ -1586,7 +1587,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
                 g.out = dx;
                 g.ldo = ldx;
                 g.emode = E_STORE;
-                const int tile = pick_tile(c, CL.cin, true, false, P);
+                const int tile = pick_tile(c, CL.cin, true, false);
                 RUN(tlabel("skip_dgrad", tile, b), 2.0 * P * CL.cin * CL.cout, launch_rowgemm(g, tile, s));
             }
             if ((rc = bn_finalize(i2, RED_G))) return rc;
