@@ -680,3 +680,39 @@ def test_pipe_gemm_bit_identical(variant, B, H, W):
         assert torch.equal(outs[0][0], outs[i][0]), i
         d = (outs[0][1] - outs[i][1]).abs().max().item()
         assert torch.equal(outs[0][1], outs[i][1]), (i, d)
+
+
+@pytest.mark.parametrize("variant,B,H,W,dzl", [("model", 2, 64, 64, 0), ("model", 4, 128, 128, 0),
+                                               ("model", 2, 64, 64, 1), ("mod", 2, 128, 64, 0),
+                                               ("res", 2, 64, 64, 0)])
+def test_wgrad_row3_pipe_bit_identical(variant, B, H, W, dzl):
+    """Option wgrad_row3_pipe (kernels_wgrad_pipe.hip: the software-pipelined schedule of the
+    row3 weight-gradient tiles) keeps wgrad_row3_kernel's pixel order, loaders, split-K slabs
+    and bias column sums, so a training step is bit-identical with and without it;
+    dz_in_loaders = 1 covers the OP_DZ operand (BN backward folded into the B' loader)."""
+    import unet_hip
+    from _helpers import hip_mod_model, options
+    from oracle import mod_ref_cpu as MO
+    x, t = inputs(47, B, H, W)
+    outs = []
+    for pipe in (0, 1):
+        if variant == "model":
+            m = hip_model(O.make_params(42), DEV)
+        elif variant == "mod":
+            m = hip_mod_model(MO.make_params(5, 64, 3), DEV, 64, 3)
+        else:
+            m = unet_hip.ResUNet(1, 1, base_filters=64, depth=3)
+            sd = m.state_dict()
+            sd.update({k: v.clone() for k, v in MO.res_make_params(42, 64, 3).items()})
+            m.load_state_dict(sd)
+            m = m.to(DEV).train()
+        with options(m.flatten_().rt, wgrad_row3_pipe=pipe, dz_in_loaders=dzl):
+            logits = m(x.to(DEV))
+            l = unet_hip.seg_losses(logits, t.to(DEV))
+            (l[0] + l[1]).backward()
+            torch.cuda.synchronize()
+        outs.append((logits.detach().clone(), m._state.grad_arena.clone()))
+        del m
+    assert torch.equal(outs[0][0], outs[1][0])
+    d = (outs[0][1] - outs[1][1]).abs().max().item()
+    assert torch.equal(outs[0][1], outs[1][1]), d

@@ -7,6 +7,18 @@
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
+// BN(+ReLU) backward value dz = A do + B (y - mean) + C in one explicit rounding order,
+// shared by every kernel that forms it (the bn_dz passes, the OP_DZ GEMM loaders,
+// conv_first_wgrad): left to -ffp-contract, hipcc contracted the same source expression
+// differently per kernel, and the fused-loader and materialised paths disagreed in the last
+// bit.
+__device__ __forceinline__ f32x4 bn_dz4(f32x4 a, f32x4 d, f32x4 b, f32x4 y, f32x4 mu, f32x4 c) {
+    f32x4 r;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) r[j] = __builtin_fmaf(a[j], d[j], __builtin_fmaf(b[j], y[j] - mu[j], c[j]));
+    return r;
+}
+
 // How the rows of a GEMM operand are gathered from an NHWC activation.
 //   G_CONV3: 3x3 / pad 1 taps on the row grid (tap t -> dy = t/3-1, dx = t%3-1),
 //            out-of-image taps read as zero (post-BN zero padding, models/model.py:36).
@@ -119,6 +131,9 @@ int rowgemm_tile_dbuf(int tile);
 // launch_rowgemm routes tile ids 16 / 17 here.
 int rowgemm_pipe_ok(const RowGemmArgs& a);
 int launch_rowgemm_pipe(const RowGemmArgs& a, int tile, hipStream_t s);
+// software-pipelined row3 weight gradient (kernels_wgrad_pipe.hip), tiles 0..3 = the shapes of
+// row3 tiles 20..23; launch_wgrad routes ids 30..33 here.
+int launch_wgrad_row3_pipe(const WgradArgs& a, int tile, hipStream_t s);
 // wgrad tile ids (kernels_gemm.hip WGRAD_TILES): 0 = 128x128, 1 = 64x64 one wave,
 // 2 = 128x64 two waves, 3 = 64x128 two waves, 4 = 64x64 four waves, 5 = 128x64 four waves
 // 20.. = one row of 3x3 taps per block (3 accumulator sets; BM = channels of ONE tap):

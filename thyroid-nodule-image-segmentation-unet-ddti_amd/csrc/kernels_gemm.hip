@@ -154,7 +154,7 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_kernel(RowGemmArgs
                     for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
             }
             if constexpr (ADZ) {
-                const f32x4 d = rsc * v + rsh * (ry[i] - rmu) + rcc;
+                const f32x4 d = bn_dz4(rsc, v, rsh, ry[i], rmu, rcc);
 #pragma unroll
                 for (int j = 0; j < 4; ++j) v[j] = ry[i][j] > 0.f ? d[j] : 0.f;
             }
@@ -514,7 +514,7 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void wgrad_kernel(WgradArgs p) 
         for (int i = 0; i < BP; ++i) {
             f32x4 v = rb[i];
             if constexpr (BDZ) {
-                const f32x4 d = ca * v + cb * (ryb[i] - cm) + cc;
+                const f32x4 d = bn_dz4(ca, v, cb, ryb[i], cm, cc);
 #pragma unroll
                 for (int j = 0; j < 4; ++j) v[j] = ryb[i][j] > 0.f ? d[j] : 0.f;
             }
@@ -707,7 +707,7 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void wgrad_row3_kernel(WgradArg
         for (int i = 0; i < BP; ++i) {
             f32x4 v = rb[i];
             if constexpr (BDZ) {
-                const f32x4 d = ca * v + cb * (ryb[i] - cm) + cc;
+                const f32x4 d = bn_dz4(ca, v, cb, ryb[i], cm, cc);
 #pragma unroll
                 for (int j = 0; j < 4; ++j) v[j] = ryb[i][j] > 0.f ? d[j] : 0.f;
             }
@@ -1236,6 +1236,7 @@ using Wr3Tile4 = WgTile<64, 64, 32, 32, 64>;    // 64-pixel chunks
 int wgrad_tile_taps(int tile) { return tile >= 20 ? 3 : 1; }
 
 int wgrad_tile_dims(int tile, int* bm, int* bn, int* bkp) {
+    if (tile >= 30 && tile <= 33) tile -= 10;  // pipelined row3 (kernels_wgrad_pipe.hip)
     if (tile == 10 || tile == 15) return wgrad16_tile_dims(tile - 10, bm, bn, bkp);
     WGRAD_ROW3_TILES(WG_DIMS_R3)
 #define WG_DIMS(id, T) \
@@ -1349,6 +1350,8 @@ int launch_wgrad(const WgradArgs& a, int tile, hipStream_t s) {
     const bool aff = a.ascale != nullptr, dz = a.bcoef != nullptr;
     if (a.arelu && !aff) return -1;
     if (a.arelu && dz) return -1;  // OP_DZ loaders are the ReLU -> BN order only
+    if (tile >= 30 && tile <= 33)  // row3, software-pipelined (kernels_wgrad_pipe.hip)
+        return launch_wgrad_row3_pipe(a, tile - 30, s);
     if (tile >= 20) {  // one row of 3x3 taps per block (wgrad_row3_kernel)
         if (a.amode != G_CONV3 || a.bmode != G_IDENT) return -1;
         if (dz) return aff ? wgrad_row3_tile<OP_AFFINE, true>(a, tile, s)

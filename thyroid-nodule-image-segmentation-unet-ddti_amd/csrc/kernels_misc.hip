@@ -235,9 +235,8 @@ __global__ __launch_bounds__(256) void conv_first_wgrad_kernel(const float* __re
         // dz = [y > 0] (A do + B (y - mean) + C) (or unmasked, BN -> ReLU order): BN backward fused
         const f32x4 dv = *(const f32x4*)(dout + (int64_t)m * C + 4 * q);
         const f32x4 yv = *(const f32x4*)(y + (int64_t)m * C + 4 * q);
-        const f32x4 dd = *(const f32x4*)(coef + 4 * q) * dv +
-                         *(const f32x4*)(coef + C + 4 * q) * (yv - *(const f32x4*)(coef + 3 * C + 4 * q)) +
-                         *(const f32x4*)(coef + 2 * C + 4 * q);
+        const f32x4 dd = bn_dz4(*(const f32x4*)(coef + 4 * q), dv, *(const f32x4*)(coef + C + 4 * q), yv,
+                                *(const f32x4*)(coef + 3 * C + 4 * q), *(const f32x4*)(coef + 2 * C + 4 * q));
         f32x4 d;
 #pragma unroll
         for (int j = 0; j < 4; ++j) d[j] = (!mask || yv[j] > 0.f) ? dd[j] : 0.f;
@@ -545,7 +544,7 @@ __global__ __launch_bounds__(256) void bn_dz_rows_kernel(float* __restrict__ d,
          m += (int64_t)gridDim.x * rpp) {
         f32x4* pd = (f32x4*)(d + m * C + c);
         const f32x4 v = *(const f32x4*)(y + m * ld + off + c);
-        const f32x4 r = ka * (*pd) + kb * (v - km) + kc;
+        const f32x4 r = bn_dz4(ka, *pd, kb, v, km, kc);
         f32x4 o;
 #pragma unroll
         for (int j = 0; j < 4; ++j) o[j] = (!mask || v[j] > 0.f) ? r[j] : 0.f;
@@ -595,7 +594,7 @@ __global__ __launch_bounds__(256) void bn_dz16_kernel(float* __restrict__ d, con
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
                     const f32x4 v = yv[u][h];
-                    const f32x4 r = ka[h] * dv[u][h] + kb[h] * (v - km[h]) + kc[h];
+                    const f32x4 r = bn_dz4(ka[h], dv[u][h], kb[h], v, km[h], kc[h]);
                     f32x4 o;
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {

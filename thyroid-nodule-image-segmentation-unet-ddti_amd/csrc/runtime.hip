@@ -93,6 +93,7 @@ struct Options {
                                // 1 every eligible layer (default: r02 A/B, conv wgrad
                                // 27.1 -> 24.4 ms/step), 2 layers with a 64-channel operand
     int wgrad_row3_tile = -1;  // its tile (>= 20), -1 = by channel counts
+    int wgrad_row3_pipe = 0;       // row3 weight gradients on the pipelined kernel (ids 30..33)
     int wgrad_row3_blocks = 1536;  // split-K target (blocks) of the row3 weight gradients
                                    // (r02 sweep 512..2048: 1536 best, 391 vs 386 img/s)
     int wgrad_tile_w = 0;      // f32 wgrad tile, both channel counts multiples of 128
@@ -122,7 +123,7 @@ struct OptionDesc {
 };
 const OptionDesc OPTION_TABLE[] = {
     {"wgrad_row3", &Options::wgrad_row3},       {"wgrad_row3_tile", &Options::wgrad_row3_tile},
-    {"wgrad_row3_blocks", &Options::wgrad_row3_blocks},
+    {"wgrad_row3_blocks", &Options::wgrad_row3_blocks}, {"wgrad_row3_pipe", &Options::wgrad_row3_pipe},
     {"wgrad_tile_w", &Options::wgrad_tile_w},   {"wgrad_tile_n", &Options::wgrad_tile_n},
     {"wgrad16_tile", &Options::wgrad16_tile},   {"tile_n128", &Options::tile_n128},
     {"tile_n128_dgrad", &Options::tile_n128_dgrad}, {"tile_n64", &Options::tile_n64},
@@ -529,7 +530,8 @@ WgradCfg wgrad_cfg(const unet_ctx* c, int CA, int tapsA, int CB, int tapsB, int6
                           (r3 == 1 || (r3 == 2 && (CA == 64 || CB == 64)));
         if (row3)
             w.tile = r3t >= 20 ? r3t
-                               : (CA % 128 == 0 ? (CB % 128 == 0 ? 23 : 21) : (CB % 128 == 0 ? 22 : 20));
+                               : (CA % 128 == 0 ? (CB % 128 == 0 ? 23 : 21) : (CB % 128 == 0 ? 22 : 20)) +
+                                     (c->opt.wgrad_row3_pipe ? 10 : 0);
         wgrad_tile_dims(w.tile, &w.bm, &w.bn, &w.bkp);
     }
     const int64_t tiles =
@@ -822,8 +824,8 @@ std::string r3label(const char* fam, const RowGemmArgs& g, int layer) {
 
 std::string wlabel(const char* fam, const WgradCfg& w, int layer) {
     char b[112];
-    snprintf(b, sizeof b, "%s/wgrad%s_%dx%dx%d|%d", fam, w.tile >= 20 ? "3" : "", w.bm, w.bn,
-             w.bkp, layer);
+    snprintf(b, sizeof b, "%s/wgrad%s_%dx%dx%d|%d", fam,
+             w.tile >= 30 ? "3p" : (w.tile >= 20 ? "3" : ""), w.bm, w.bn, w.bkp, layer);
     return b;
 }
 

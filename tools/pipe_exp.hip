@@ -49,6 +49,24 @@ static void go_dgrad(const RowGemmArgs& g) {
     hipLaunchKernelGGL((rowgemm_pipe_kernel<G_CONV3, OP_PLAIN, E_STORE, T, V % 100>), grid, dim3(256), 0, 0, g);
 }
 
+
+// N = 64 tiles (experiment): 128x64 / 4 waves of 64x32 (library tile 1 / 3), 256x64 / 4 waves
+// of 64x64 (one block per CU), 128x64 / 2 waves of 64x64
+using N64a = PipeTile1;
+using N64b = PipeTile<256, 64, 64, 64, 1, 1>;
+using N64c = PipeTile<256, 64, 64, 64, 1, 2>;
+using N64d = PipeTile<128, 64, 64, 64, 2, 1>;
+using N64e = PipeTile3;
+template <class T, bool FWD>
+static void go64(const RowGemmArgs& g) {
+    const dim3 grid(((g.M + T::BM - 1) / T::BM) * (g.N / T::BN));
+    if (FWD)
+        hipLaunchKernelGGL((rowgemm_pipe_kernel<G_CONV3, OP_AFFINE, E_BIAS_RELU_STATS, T>), grid,
+                           dim3(T::THREADS), 0, 0, g);
+    else
+        hipLaunchKernelGGL((rowgemm_pipe_kernel<G_CONV3, OP_PLAIN, E_STORE, T>), grid, dim3(T::THREADS), 0, 0, g);
+}
+
 struct Shape { const char* name; int N, H, W, Cin, Cout; };
 
 int main(int argc, char** argv) {
@@ -114,6 +132,62 @@ int main(int argc, char** argv) {
         fflush(stdout);
         CK(hipFree(x)); CK(hipFree(w)); CK(hipFree(sc)); CK(hipFree(shf)); CK(hipFree(bias));
         CK(hipFree(y)); CK(hipFree(st)); CK(hipFree(dz)); CK(hipFree(xo));
+    }
+    {  // N = 64 outputs: forward 64->64 and 128->64 at 256^2 (N = Cout = 64), dgrad of 64->64
+        constexpr int NV64 = 5;
+        typedef void (*Fn)(const RowGemmArgs&);
+        const Fn f64[NV64] = {go64<N64a, true>, go64<N64b, true>, go64<N64c, true>, go64<N64d, true>, go64<N64e, true>};
+        const Fn d64[NV64] = {go64<N64a, false>, go64<N64b, false>, go64<N64c, false>, go64<N64d, false>, go64<N64e, false>};
+        const char* nm[NV64] = {"128x64/w64x32", "256x64/w64x64", "256x64/w64x64/d2", "128x64/w64x64x2", "128x64/w64x32/d2"};
+        Shape s64[] = {{"L0 64->64 @256", 32, 256, 256, 64, 64}, {"L0 128->64 @256", 32, 256, 256, 128, 64}};
+        for (const Shape& sh : s64) {
+            const int M = sh.N * sh.H * sh.W;
+            float* x = dalloc((size_t)M * sh.Cin, 1, 2.f);
+            float* w = dalloc((size_t)sh.Cout * 9 * sh.Cin, 2, 0.1f);
+            float* sc = dalloc(sh.Cin, 3, 1.f);
+            float* shf = dalloc(sh.Cin, 4, 1.f);
+            float* bias = dalloc(sh.Cout, 5, 1.f);
+            float* y = dalloc((size_t)M * sh.Cout, 6, 0.f);
+            float* st = dalloc((size_t)(M / 64 + 1) * 2 * sh.Cout, 7, 0.f);
+            float* dz = dalloc((size_t)M * sh.Cin, 8, 1.f);
+            float* xo = dalloc((size_t)M * sh.Cin, 9, 0.f);
+            const double flop = 2.0 * M * sh.Cout * 9.0 * sh.Cin;
+            double best[2][NV64] = {};
+            for (int r = 0; r < rounds; ++r)
+                for (int v = 0; v < NV64; ++v)
+                    for (int op = 0; op < 2; ++op) {
+                        if (op == 1 && sh.Cin != 64) continue;
+                        RowGemmArgs g{};
+                        g.H = sh.H; g.W = sh.W; g.M = M; g.amode = G_CONV3; g.bt = w;
+                        if (op == 0) {
+                            g.N = sh.Cout; g.K = 9 * sh.Cin; g.a = x; g.lda = sh.Cin; g.C = sh.Cin;
+                            g.ascale = sc; g.ashift = shf; g.emode = E_BIAS_RELU_STATS; g.bias = bias;
+                            g.stats = st; g.out = y; g.ldo = sh.Cout;
+                        } else {  // dgrad of a Cin -> 64 conv: N = Cin = 64, K = 9 * 64
+                            g.N = sh.Cin; g.K = 9 * sh.Cout; g.a = dz; g.lda = sh.Cout; g.C = sh.Cout;
+                            g.emode = E_STORE; g.out = xo; g.ldo = sh.Cin;
+                        }
+                        const Fn f = op ? d64[v] : f64[v];
+                        f(g);
+                        CK(hipGetLastError());
+                        CK(hipEventRecord(e0, 0));
+                        for (int it = 0; it < iters; ++it) f(g);
+                        CK(hipEventRecord(e1, 0));
+                        CK(hipEventSynchronize(e1));
+                        float ms;
+                        CK(hipEventElapsedTime(&ms, e0, e1));
+                        const double tf = flop * iters / (ms * 1e-3) / 1e12;
+                        if (tf > best[op][v]) best[op][v] = tf;
+                    }
+            for (int op = 0; op < 2; ++op) {
+                printf("%-18s %-5s", sh.name, op ? "dgrad" : "fwd");
+                for (int v = 0; v < NV64; ++v) printf("  %s %6.1f", nm[v], best[op][v]);
+                printf("\n");
+            }
+            fflush(stdout);
+            CK(hipFree(x)); CK(hipFree(w)); CK(hipFree(sc)); CK(hipFree(shf)); CK(hipFree(bias));
+            CK(hipFree(y)); CK(hipFree(st)); CK(hipFree(dz)); CK(hipFree(xo));
+        }
     }
     return 0;
 }
