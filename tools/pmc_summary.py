@@ -23,6 +23,16 @@ from collections import defaultdict
 
 def short(name):
     """rocprofv3 kernel name -> bench.py label (rowgemm_BMxBNxBK / wgrad_BMxBNxBKP)."""
+    m = re.search(r"Wr3PipeTile<(\d+), (\d+), \d+, \d+, (\d+)", name)
+    if m:
+        return f"wgrad3p_{m.group(1)}x{m.group(2)}x{m.group(3)}"
+    m = re.search(r"PipeTile<(\d+), (\d+), \d+, \d+, \d+", name)
+    if m:
+        return f"rowgemm_{m.group(1)}x{m.group(2)}x32p"
+    m = re.search(r"row3_kernel.*?(?:Row|Wg)Tile<(\d+), (\d+), \d+, \d+, (\d+)", name)
+    if m:
+        fam = "wgrad3" if "wgrad_row3" in name else "rowgemm3"
+        return f"{fam}_{m.group(1)}x{m.group(2)}x{m.group(3)}"
     m = re.search(r"RowTile<(\d+), (\d+), \d+, \d+, (\d+), (true|false)", name)
     if m:
         return f"rowgemm_{m.group(1)}x{m.group(2)}x{m.group(3)}{'d' if m.group(4) == 'true' else ''}"
