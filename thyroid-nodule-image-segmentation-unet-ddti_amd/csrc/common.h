@@ -134,6 +134,10 @@ int launch_rowgemm_pipe(const RowGemmArgs& a, int tile, hipStream_t s);
 // software-pipelined row3 weight gradient (kernels_wgrad_pipe.hip), tiles 0..3 = the shapes of
 // row3 tiles 20..23; launch_wgrad routes ids 30..33 here.
 int launch_wgrad_row3_pipe(const WgradArgs& a, int tile, hipStream_t s);
+// f32 row GEMM with LDS-DMA operands (kernels_gemm_dma.hip): tile 0 = 128x128 (2 stages),
+// 1 = 128x64, 2 = 128x128 (3 stages); launch_rowgemm routes ids 20..22 here.  Needs zero16.
+int rowgemm_dma_ok(const RowGemmArgs& a);
+int launch_rowgemm_dma(const RowGemmArgs& a, int tile, hipStream_t s);
 // wgrad tile ids (kernels_gemm.hip WGRAD_TILES): 0 = 128x128, 1 = 64x64 one wave,
 // 2 = 128x64 two waves, 3 = 64x128 two waves, 4 = 64x64 four waves, 5 = 128x64 four waves
 // 20.. = one row of 3x3 taps per block (3 accumulator sets; BM = channels of ONE tap):

@@ -1070,6 +1070,12 @@ static int rowgemm_tile(const RowGemmArgs& a, int tile, hipStream_t s) {
 }
 
 int rowgemm_tile_dims(int tile, int* bm, int* bn, int* bk) {
+    if (tile >= 20 && tile <= 22) {  // rowgemm_dma_kernel (LDS-DMA operands)
+        *bm = 128;
+        *bn = tile == 21 ? 64 : 128;
+        *bk = 32;
+        return 0;
+    }
     if (tile >= 16 && tile <= 19) {  // rowgemm_pipe_kernel (18, 19: loads two chunks ahead)
         *bm = 128;
         *bn = tile % 2 == 0 ? 128 : 64;
@@ -1090,6 +1096,7 @@ int rowgemm_tile_dims(int tile, int* bm, int* bn, int* bk) {
 
 int rowgemm_tile_dbuf(int tile) {
     if (tile >= 16 && tile <= 19) return 2;  // pipelined
+    if (tile >= 20 && tile <= 22) return 3;  // LDS-DMA
 #define RG_DB(id, T) \
     if (tile == id) return T::DBUF ? 1 : 0;
     ROWGEMM_TILES(RG_DB)
@@ -1196,6 +1203,11 @@ int launch_rowgemm(const RowGemmArgs& a, int tile, hipStream_t s) {
     // ids 16..19: the software-pipelined f32 kernel (128x128 / 128x64, loads one or two
     // chunks ahead); operands it does not take (bf16 weights, dz in the loader, > 2 GB
     // offsets) run the same tile shape here
+    // ids 20..22: both operands by LDS-DMA (kernels_gemm_dma.hip); else the pipelined tile
+    if (tile >= 20 && tile <= 22) {
+        if (rowgemm_dma_ok(a)) return launch_rowgemm_dma(a, tile - 20, s);
+        tile = tile == 21 ? 17 : 16;
+    }
     if (tile >= 16 && tile <= 19) {
         if (rowgemm_pipe_ok(a)) return launch_rowgemm_pipe(a, tile - 16, s);
         tile = tile % 2 == 0 ? 4 : 1;

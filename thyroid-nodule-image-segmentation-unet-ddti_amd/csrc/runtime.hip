@@ -686,14 +686,13 @@ void make_plan(unet_ctx* c, int N, int H, int W, bool training, char* base, Plan
     p.stats = b.take<float>(srows);
     p.stats2 = b.take<float>((int64_t)STAT_G * 2 * c->cmax);
     p.s16 = nullptr;
-    p.zero16 = nullptr;
+    p.zero16 = b.take<char>(256);  // zeroed 16-B page: padding taps of the LDS-DMA GEMMs
     if (c->bf16) {
         int64_t n16 = 0;
         for (const ConvL& L : c->conv) n16 = std::max(n16, p.P[L.level] * std::max(L.cin, L.cout));
         for (const ConvTL& T : c->convt)
             n16 = std::max(n16, std::max(p.P[T.in_level] * T.cin, p.P[T.in_level - 1] * T.cout));
         p.s16 = b.take<uint16_t>(n16);
-        p.zero16 = b.take<char>(256);
     }
     p.x16.assign(NC, nullptr);
     for (int i = 0; i < NC && training; ++i)
@@ -806,9 +805,9 @@ std::string tlabel(const char* fam, int tile, int layer) {
     int bm = 0, bn = 0, bk = 0;
     rowgemm_tile_dims(tile, &bm, &bn, &bk);
     char b[112];
-    const int db = rowgemm_tile_dbuf(tile);  // 1 = two LDS images, 2 = software-pipelined
+    const int db = rowgemm_tile_dbuf(tile);  // 1 = two LDS images, 2 = pipelined, 3 = LDS-DMA
     snprintf(b, sizeof b, "%s/rowgemm_%dx%dx%d%s|%d", fam, bm, bn, bk,
-             db == 2 ? "p" : (db ? "d" : ""), layer);
+             db == 3 ? "m" : (db == 2 ? "p" : (db ? "d" : "")), layer);
     return b;
 }
 
@@ -997,6 +996,7 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
         } else {
             Operand a = conv_input(c, p, i);
             RowGemmArgs g{};
+            g.zero16 = p.zero16;
             g.H = Hl;
             g.W = Wl;
             g.M = (int)M;
@@ -1044,6 +1044,7 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
         const int src = 2 * (D + k) + 1;  // second conv of the bottleneck / decoder block
         const int lo = T.in_level - 1;
         RowGemmArgs g{};
+        g.zero16 = p.zero16;
         g.H = H >> T.in_level;
         g.W = W >> T.in_level;
         g.M = (int)p.P[T.in_level];
@@ -1099,6 +1100,7 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
         }
         Operand a = conv_input(c, p, 2 * b);
         RowGemmArgs g{};
+        g.zero16 = p.zero16;
         g.H = H >> CL.level;
         g.W = W >> CL.level;
         g.M = (int)M;
@@ -1343,6 +1345,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         if (dx) {
             before_write(dx);
             RowGemmArgs g{};
+            g.zero16 = p.zero16;
             g.H = Hl;
             g.W = Wl;
             g.M = (int)P;
@@ -1471,6 +1474,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         RUNW("bias_grad", 0, k_bias_reduce(p.bslab, wc.splits, 4, T.cout, grads + T.b, sw));
         before_write(dx);
         RowGemmArgs g{};
+        g.zero16 = p.zero16;
         g.H = Hi;
         g.W = Wi;
         g.M = (int)Pin;
@@ -1575,6 +1579,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
                 RUN("wgrad_reduce", 0, k_slab_reduce(p.slab, wc.splits, w.Mw, w.Nw, 2, CL.cin, CL.cout,
                                                      grads + c->skip_w[b], s));
                 RowGemmArgs g{};
+                g.zero16 = p.zero16;
                 g.H = H >> CL.level;
                 g.W = W >> CL.level;
                 g.M = (int)P;
