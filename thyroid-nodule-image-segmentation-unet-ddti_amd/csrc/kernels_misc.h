@@ -2,11 +2,21 @@
 #pragma once
 #include "common.h"
 
-int k_pack_conv3(const float* w, float* wf, float* wd, int cin, int cout, hipStream_t s);
-int k_pack_convT(const float* w, float* tf, float* td, int cin, int cout, hipStream_t s);
-// bf16 weight images (round to nearest even) for the bf16-MFMA GEMMs
-int k_pack_conv3_bf16(const float* w, uint16_t* wf, uint16_t* wd, int cin, int cout, hipStream_t s);
-int k_pack_convT_bf16(const float* w, uint16_t* tf, uint16_t* td, int cin, int cout, hipStream_t s);
+// Weight images of the row GEMMs, every 3x3 conv (kind 0) and ConvTranspose (kind 1) of the
+// network in one launch.  Offsets w (params), f / d (forward / dgrad images; d < 0: none)
+// count floats; bf16 images (round to nearest even) are addressed at the same float offsets.
+// A job covers tx x ty 32x32 tiles (conv3: x over cin, y over cout; ConvT: x over cout, y
+// over cin) starting at block block0.
+struct PackJob {
+    int64_t w, f, d;
+    int cin, cout, kind, tx, ty, block0;
+};
+constexpr int MAX_PACK_JOBS = 48;
+struct PackJobs {
+    int n;
+    PackJob j[MAX_PACK_JOBS];
+};
+int k_pack_all(const PackJobs& jobs, const float* prm, float* pack, int bf16, hipStream_t s);
 // conv_first: relu = ReLU after (+bias) (model.py order); b may be null (mod.py, bias-free).
 // wgrad: mask = dz masked by [y > 0] (ReLU before the BN, model.py order); gb may be null.
 int k_conv_first_fwd(const float* x, const float* w, const float* b, float* y, int P, int H, int W,

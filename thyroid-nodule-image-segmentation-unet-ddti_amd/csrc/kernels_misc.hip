@@ -23,13 +23,10 @@ namespace {
 // (ci runs of Wf, co runs of Wd) rather than an element-wise stride-9 / stride-9*Cout
 // scatter.  Row stride 289 floats: both LDS read patterns are conflict-free.
 template <class OUT>
-__global__ __launch_bounds__(256) void pack_conv3_tiled_kernel(const float* __restrict__ w,
-                                                               OUT* __restrict__ wf,
-                                                               OUT* __restrict__ wd, int cin,
-                                                               int cout) {
+__device__ void pack_conv3_tile(const float* __restrict__ w, OUT* __restrict__ wf,
+                                OUT* __restrict__ wd, int cin, int cout, int ci0, int co0,
+                                float* tile) {
     constexpr int T = 32, RS = T * 9 + 1;
-    __shared__ float tile[T * RS];
-    const int ci0 = blockIdx.x * T, co0 = blockIdx.y * T;
     const int nci = min(T, cin - ci0), nco = min(T, cout - co0);
     const int tid = threadIdx.x;
     if (nci == T && nco == T) {
@@ -77,13 +74,10 @@ __global__ __launch_bounds__(256) void pack_conv3_tiled_kernel(const float* __re
 // runs and Td rows (ci) as 32-element co runs per ab (the element-wise form scattered every
 // Tf element cin apart).  Row stride 129 floats: both LDS read patterns are conflict-free.
 template <class OUT>
-__global__ __launch_bounds__(256) void pack_convT_tiled_kernel(const float* __restrict__ w,
-                                                               OUT* __restrict__ tf,
-                                                               OUT* __restrict__ td, int cin,
-                                                               int cout) {
-    constexpr int T = 32, RS = T * 4 + 1;
-    __shared__ float tile[T * RS];  // [ci_l][co_l * 4 + ab]
-    const int co0 = blockIdx.x * T, ci0 = blockIdx.y * T;
+__device__ void pack_convT_tile(const float* __restrict__ w, OUT* __restrict__ tf,
+                                OUT* __restrict__ td, int cin, int cout, int co0, int ci0,
+                                float* tile) {
+    constexpr int T = 32, RS = T * 4 + 1;  // tile: [ci_l][co_l * 4 + ab]
     const int nci = min(T, cin - ci0), nco = min(T, cout - co0);
     const int tid = threadIdx.x;
     for (int e = tid; e < T * T * 4; e += 256) {  // e = ci_l * 128 + (co_l * 4 + ab)
@@ -106,6 +100,27 @@ __global__ __launch_bounds__(256) void pack_convT_tiled_kernel(const float* __re
         if (ci_l < nci && l < nco)
             td[(int64_t)(ci0 + ci_l) * 4 * cout + ab * cout + co0 + l] = (OUT)tile[ci_l * RS + l * 4 + ab];
     }
+}
+
+// Every 3x3 / ConvT weight image of the network in ONE launch (the per-layer launches were
+// 21 small grids per step, most of them too small to fill the chip): block b runs tile
+// b - block0 of the last job with block0 <= b; the job table travels as a kernel argument.
+template <class OUT>
+__global__ __launch_bounds__(256) void pack_all_kernel(PackJobs jobs, const float* __restrict__ prm,
+                                                       float* __restrict__ pack) {
+    __shared__ float tile[32 * (32 * 9 + 1)];
+    const int b = blockIdx.x;
+    int j = 0;
+    for (int k = 1; k < jobs.n; ++k)
+        if (jobs.j[k].block0 <= b) j = k;
+    const PackJob& J = jobs.j[j];
+    const int local = b - J.block0, ix = local % J.tx, iy = local / J.tx;
+    OUT* f = (OUT*)(pack + J.f);
+    OUT* d = J.d >= 0 ? (OUT*)(pack + J.d) : nullptr;
+    if (J.kind == 0)
+        pack_conv3_tile<OUT>(prm + J.w, f, d, J.cin, J.cout, ix * 32, iy * 32, tile);
+    else
+        pack_convT_tile<OUT>(prm + J.w, f, d, J.cin, J.cout, ix * 32, iy * 32, tile);
 }
 
 // 1x1 conv weight W[co][ci] -> its dgrad image Wt[ci][co] (models/mod.py:83 skip)
@@ -313,17 +328,11 @@ __device__ void colsum16(const float* __restrict__ part, int G, int stride, int 
 // biased var for normalisation, running stats r = (1-m) r + m * stat with unbiased var.
 // Emits the fused affine (scale, shift) consumers apply in their load path, and keeps
 // mean / invstd for the backward.
-__global__ void bn_finalize_train_kernel(const float* __restrict__ part, int G, int C,
-                                         double count, const float* __restrict__ gamma,
-                                         const float* __restrict__ beta, float* rmean,
-                                         float* rvar, int64_t* nbt, float momentum, float eps,
-                                         float* __restrict__ scale, float* __restrict__ shift,
-                                         float* __restrict__ mean_out,
-                                         float* __restrict__ invstd_out) {
-    const int c = blockIdx.x * 64 + threadIdx.x;
-    double sq[2];
-    colsum16<2>(part, G, 2 * C, C, c, c < C, sq);
-    if (threadIdx.y != 0) return;
+__device__ void bn_train_final(int c, int C, const double (&sq)[2], double count,
+                               const float* __restrict__ gamma, const float* __restrict__ beta,
+                               float* rmean, float* rvar, int64_t* nbt, float momentum, float eps,
+                               float* __restrict__ scale, float* __restrict__ shift,
+                               float* __restrict__ mean_out, float* __restrict__ invstd_out) {
     if (c == 0 && nbt) *nbt += 1;
     if (c >= C) return;
     const double s = sq[0], q = sq[1];
@@ -341,6 +350,21 @@ __global__ void bn_finalize_train_kernel(const float* __restrict__ part, int G, 
         rmean[c] = (1.f - momentum) * rmean[c] + momentum * (float)mean;
         rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)unb;
     }
+}
+
+__global__ void bn_finalize_train_kernel(const float* __restrict__ part, int G, int C,
+                                         double count, const float* __restrict__ gamma,
+                                         const float* __restrict__ beta, float* rmean,
+                                         float* rvar, int64_t* nbt, float momentum, float eps,
+                                         float* __restrict__ scale, float* __restrict__ shift,
+                                         float* __restrict__ mean_out,
+                                         float* __restrict__ invstd_out) {
+    const int c = blockIdx.x * 64 + threadIdx.x;
+    double sq[2];
+    colsum16<2>(part, G, 2 * C, C, c, c < C, sq);
+    if (threadIdx.y != 0) return;
+    bn_train_final(c, C, sq, count, gamma, beta, rmean, rvar, nbt, momentum, eps, scale, shift,
+                   mean_out, invstd_out);
 }
 
 __global__ void bn_finalize_eval_kernel(int C, const float* __restrict__ gamma,
@@ -506,15 +530,11 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const float* __restric
 // dbeta = S1 and the coefficients of dz = A do + B (y - mean) + Cc, coef[4][C] (model.py order additionally
 // masks dz by [y > 0], the ReLU in front of the BN: model.py:37-38,40-41).
 // -------------------------------------------------------------------------------------
-__global__ void bn_bwd_finalize2_kernel(const float* __restrict__ part, int G, int C, double count,
-                                        const float* __restrict__ gamma,
-                                        const float* __restrict__ mean,
-                                        const float* __restrict__ invstd, float* __restrict__ coef,
-                                        float* __restrict__ dgamma, float* __restrict__ dbeta) {
-    const int c = blockIdx.x * 64 + threadIdx.x;
-    double ss[2];
-    colsum16<2>(part, G, 2 * C, C, c, c < C, ss);
-    if (threadIdx.y != 0 || c >= C) return;
+__device__ void bn_bwd_final(int c, int C, const double (&ss)[2], double count,
+                             const float* __restrict__ gamma, const float* __restrict__ mean,
+                             const float* __restrict__ invstd, float* __restrict__ coef,
+                             float* __restrict__ dgamma, float* __restrict__ dbeta) {
+    if (c >= C) return;
     const double s1 = ss[0], s2 = ss[1];
     const double is = invstd[c], mu = mean[c];
     const double sdxh = is * (s2 - mu * s1);
@@ -528,6 +548,19 @@ __global__ void bn_bwd_finalize2_kernel(const float* __restrict__ part, int G, i
     dgamma[c] = (float)sdxh;
     dbeta[c] = (float)s1;
 }
+
+__global__ void bn_bwd_finalize2_kernel(const float* __restrict__ part, int G, int C, double count,
+                                        const float* __restrict__ gamma,
+                                        const float* __restrict__ mean,
+                                        const float* __restrict__ invstd, float* __restrict__ coef,
+                                        float* __restrict__ dgamma, float* __restrict__ dbeta) {
+    const int c = blockIdx.x * 64 + threadIdx.x;
+    double ss[2];
+    colsum16<2>(part, G, 2 * C, C, c, c < C, ss);
+    if (threadIdx.y != 0) return;
+    bn_bwd_final(c, C, ss, count, gamma, mean, invstd, coef, dgamma, dbeta);
+}
+
 
 // dz = A do + B (y - mean) + C in place, masked by [y > 0] when `mask` (ReLU before the BN).
 // Row form (C / 4 divides 256): each thread keeps one channel quad and its coefficients
@@ -1354,25 +1387,14 @@ inline int grid_for(int64_t n, int block = 256, int cap = 8192) {
 // ============================ host launchers ============================
 #define LAUNCH_CHECK() return (int)hipGetLastError()
 
-int k_pack_conv3(const float* w, float* wf, float* wd, int cin, int cout, hipStream_t s) {
-    const dim3 grid((cin + 31) / 32, (cout + 31) / 32);
-    hipLaunchKernelGGL(pack_conv3_tiled_kernel<float>, grid, dim3(256), 0, s, w, wf, wd, cin, cout);
-    LAUNCH_CHECK();
-}
-int k_pack_conv3_bf16(const float* w, uint16_t* wf, uint16_t* wd, int cin, int cout, hipStream_t s) {
-    const dim3 grid((cin + 31) / 32, (cout + 31) / 32);
-    hipLaunchKernelGGL(pack_conv3_tiled_kernel<__bf16>, grid, dim3(256), 0, s, w, (__bf16*)wf,
-                       (__bf16*)wd, cin, cout);
-    LAUNCH_CHECK();
-}
-int k_pack_convT(const float* w, float* tf, float* td, int cin, int cout, hipStream_t s) {
-    hipLaunchKernelGGL(pack_convT_tiled_kernel<float>, dim3((cout + 31) / 32, (cin + 31) / 32),
-                       dim3(256), 0, s, w, tf, td, cin, cout);
-    LAUNCH_CHECK();
-}
-int k_pack_convT_bf16(const float* w, uint16_t* tf, uint16_t* td, int cin, int cout, hipStream_t s) {
-    hipLaunchKernelGGL(pack_convT_tiled_kernel<__bf16>, dim3((cout + 31) / 32, (cin + 31) / 32),
-                       dim3(256), 0, s, w, (__bf16*)tf, (__bf16*)td, cin, cout);
+int k_pack_all(const PackJobs& jobs, const float* prm, float* pack, int bf16, hipStream_t s) {
+    if (jobs.n < 1 || jobs.n > MAX_PACK_JOBS) return -1;
+    const PackJob& last = jobs.j[jobs.n - 1];
+    const int blocks = last.block0 + last.tx * last.ty;
+    if (bf16)
+        hipLaunchKernelGGL(pack_all_kernel<__bf16>, dim3(blocks), dim3(256), 0, s, jobs, prm, pack);
+    else
+        hipLaunchKernelGGL(pack_all_kernel<float>, dim3(blocks), dim3(256), 0, s, jobs, prm, pack);
     LAUNCH_CHECK();
 }
 int k_conv_first_fwd(const float* x, const float* w, const float* b, float* y, int P, int H, int W,

@@ -948,25 +948,30 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
     const int H = p.H, W = p.W, D = c->depth, NC = c->nconv();
     // 1. weight images for the row GEMMs (re-packed every call: params may have changed
     //    through the optimizer or load_state_dict; ~0.1 ms of HBM traffic per step)
-    for (int i = 0; i < NC; ++i) {
-        const ConvL& C = c->conv[i];
-        if (C.pf < 0) continue;
-        if (c->bf16)
-            RUN("pack", 0, k_pack_conv3_bf16(prm + C.w, (uint16_t*)(p.pack + C.pf),
-                                             training ? (uint16_t*)(p.pack + C.pd) : nullptr, C.cin,
-                                             C.cout, s));
-        else
-            RUN("pack", 0, k_pack_conv3(prm + C.w, p.pack + C.pf, training ? p.pack + C.pd : nullptr,
-                                        C.cin, C.cout, s));
-    }
-    for (const ConvTL& T : c->convt) {
-        if (c->bf16)
-            RUN("pack", 0, k_pack_convT_bf16(prm + T.w, (uint16_t*)(p.pack + T.pf),
-                                             training ? (uint16_t*)(p.pack + T.pd) : nullptr, T.cin,
-                                             T.cout, s));
-        else
-            RUN("pack", 0, k_pack_convT(prm + T.w, p.pack + T.pf, training ? p.pack + T.pd : nullptr,
-                                        T.cin, T.cout, s));
+    {
+        PackJobs jobs{};
+        int blocks = 0;
+        auto add = [&](int64_t w, int64_t f, int64_t d, int cin, int cout, int kind) {
+            PackJob& J = jobs.j[jobs.n++];
+            J.w = w;
+            J.f = f;
+            J.d = training ? d : -1;
+            J.cin = cin;
+            J.cout = cout;
+            J.kind = kind;
+            J.tx = ((kind == 0 ? cin : cout) + 31) / 32;
+            J.ty = ((kind == 0 ? cout : cin) + 31) / 32;
+            J.block0 = blocks;
+            blocks += J.tx * J.ty;
+        };
+        for (int i = 0; i < NC; ++i) {
+            const ConvL& C = c->conv[i];
+            if (C.pf >= 0 && jobs.n < MAX_PACK_JOBS) add(C.w, C.pf, C.pd, C.cin, C.cout, 0);
+        }
+        for (const ConvTL& T : c->convt)
+            if (jobs.n < MAX_PACK_JOBS) add(T.w, T.pf, T.pd, T.cin, T.cout, 1);
+        if (jobs.n >= MAX_PACK_JOBS) return fail(c, UNET_ERR_INTERNAL, "pack job table full");
+        if (jobs.n) RUN("pack", 0, k_pack_all(jobs, prm, p.pack, c->bf16, s));
     }
     for (int b = 1; b <= 2 * D && c->res && training; ++b)
         RUN("pack", 0, k_pack_1x1_t(prm + c->skip_w[b], p.pack + c->skip_pd[b], c->conv[2 * b].cin,
