@@ -670,7 +670,7 @@ def test_pipe_gemm_bit_identical(variant, B, H, W):
             m.load_state_dict(sd)
             m = m.to(DEV).train()
         with options(m.flatten_().rt, tile_n128=tiles[0], tile_n128_dgrad=tiles[1],
-                     tile_n64=tiles[2]):
+                     tile_n64=tiles[2], tile_n64_dgrad=tiles[2], tile_convt64=tiles[2]):
             logits = m(x.to(DEV))
             l = unet_hip.seg_losses(logits, t.to(DEV))
             (l[0] + l[1]).backward()

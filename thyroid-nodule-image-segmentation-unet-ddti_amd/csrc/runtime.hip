@@ -101,7 +101,9 @@ struct Options {
     int wgrad16_tile = 0;      // register-staged bf16 wgrad tile (128-multiples)
     int tile_n128 = -1;        // f32 row-GEMM tile, N % 128 == 0 (-1 = pick_tile's default)
     int tile_n128_dgrad = -1;  // ... dgrad-type
-    int tile_n64 = 1;          // ... N = 64 outputs
+    int tile_n64 = 19;         // ... N = 64 outputs (forward-type)
+    int tile_n64_dgrad = 1;    // ... N = 64, dgrad-type
+    int tile_convt64 = 1;      // ConvT forward with 64 output channels (grid N = 256)
     int tile16_n128 = 6;       // register-staged bf16 row-GEMM tiles
     int tile16_n128_dgrad = 6;
     int tile16_n64 = 1;
@@ -127,6 +129,7 @@ const OptionDesc OPTION_TABLE[] = {
     {"wgrad_tile_w", &Options::wgrad_tile_w},   {"wgrad_tile_n", &Options::wgrad_tile_n},
     {"wgrad16_tile", &Options::wgrad16_tile},   {"tile_n128", &Options::tile_n128},
     {"tile_n128_dgrad", &Options::tile_n128_dgrad}, {"tile_n64", &Options::tile_n64},
+    {"tile_n64_dgrad", &Options::tile_n64_dgrad}, {"tile_convt64", &Options::tile_convt64},
     {"tile16_n128", &Options::tile16_n128},     {"tile16_n128_dgrad", &Options::tile16_n128_dgrad},
     {"tile16_n64", &Options::tile16_n64},       {"rg16", &Options::rg16},
     {"rg16_tile", &Options::rg16_tile},         {"wg16", &Options::wg16},
@@ -789,14 +792,16 @@ struct Launcher {
 //    401 img/s against 390 for the register-staged tiles (t7 / t4 / t0 by grid size), the
 //    dominant kernel 128.9 vs 122.2 TF/s; the two schedules store identical bits
 //    (tests/test_gpu_parity.py::test_pipe_gemm_bit_identical);
-//  * f32, N = 64 outputs: 128x64 (t1) -- the pipelined 128x64 (19) wins on the forward
-//    GEMMs and loses on the dgrads and the level-0 ConvT, net neutral.
+//  * f32, N = 64 outputs: the pipelined 128x64 with loads two chunks ahead (19) on the
+//    forward GEMMs (level-0 128 -> 64 conv 112 -> 117 TF/s), the register-staged 128x64
+//    (t1) on the dgrads and the level-0 ConvT forward, where 17 / 19 measured slower
+//    (options tile_n64 / tile_n64_dgrad / tile_convt64; profiles/r02_pipe_exp.txt).
 // bf16 MFMA (register-staged): a chunk of 64 K per barrier (4 MFMA k-steps) by default.
 // Options tile_* override (tuning runs; -1 = automatic).
-int pick_tile(const unet_ctx* c, int N, bool dgrad, bool bf16) {
+int pick_tile(const unet_ctx* c, int N, bool dgrad, bool bf16, bool convt = false) {
     const Options& o = c->opt;
     if (bf16) return N % 128 == 0 ? (dgrad ? o.tile16_n128_dgrad : o.tile16_n128) : o.tile16_n64;
-    if (N % 128) return o.tile_n64;
+    if (N % 128) return convt && !dgrad ? o.tile_convt64 : (dgrad ? o.tile_n64_dgrad : o.tile_n64);
     if (dgrad) return o.tile_n128_dgrad >= 0 ? o.tile_n128_dgrad : 16;
     return o.tile_n128 >= 0 ? o.tile_n128 : 18;
 }
@@ -1087,7 +1092,7 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
                 launch_rowgemm16(g, tile, s));
             return 0;
         }
-        const int tile = pick_tile(c, T.cout, false, c->bf16);  // grid N = 4 cout
+        const int tile = pick_tile(c, T.cout, false, c->bf16, true);  // grid N = 4 cout
         RUN(tlabel("convT_fwd", tile, 100 + k), 2.0 * g.M * g.N * g.K, launch_rowgemm(g, tile, s));
         return 0;
     };
