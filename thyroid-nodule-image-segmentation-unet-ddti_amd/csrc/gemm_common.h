@@ -229,7 +229,22 @@ __device__ __forceinline__ void row_epilogue(const RowGemmArgs& p, f32x16 (&acc)
                     }
                 }
 #pragma unroll
-            for (int mt = 0; mt < MT && PRELOAD; ++mt) {
+            for (int mt = 0; mt < MT && PRELOAD && full; ++mt) {
+                float yv[16];  // all 16 loads first, then the stores (no guards: full tile)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) yv[r] = *(const float*)(urow(p.ey, p.ldey, p.offey, mt, r) + ly);
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const float y = yv[r];
+                    float v = acc[mt][nt][r];
+                    if (emask && !(es * y + eb > 0.f)) v = 0.f;
+                    *(float*)(urow(p.out, p.ldo, p.ooff, mt, r) + lo) = v;
+                    q[mt / 2][nt][0] += v;
+                    q[mt / 2][nt][1] = __builtin_fma((double)v, (double)y, q[mt / 2][nt][1]);
+                }
+            }
+#pragma unroll
+            for (int mt = 0; mt < MT && PRELOAD && !full; ++mt) {
                 // all 16 loads first (rows past M clamped, their products zeroed below)
                 float yv[16];
 #pragma unroll
