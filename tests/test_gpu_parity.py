@@ -658,7 +658,7 @@ def test_pipe_gemm_bit_identical(variant, B, H, W):
     from oracle import mod_ref_cpu as MO
     x, t = inputs(43, B, H, W)
     outs = []
-    for tiles in ((4, 0, 1), (16, 16, 17), (18, 18, 19), (20, 20, 21), (22, 22, 21)):
+    for tiles in ((4, 0, 1), (16, 16, 17), (18, 18, 19), (20, 20, 21)):
         if variant == "model":
             m = hip_model(O.make_params(42), DEV)
         elif variant == "mod":

@@ -16,6 +16,8 @@
 // the ReLU on the channels below arelu and the padding select, from a per-block LDS copy
 // of scale / shift and a per-row 9-bit tap mask -- the values rowgemm_kernel's commit
 // writes, so the products are the same.
+#include <type_traits>
+
 #include "gemm_common.h"
 
 namespace {
@@ -37,6 +39,26 @@ __device__ __forceinline__ void block_barrier() {
 template <int N>
 __device__ __forceinline__ void wait_vm() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// ds_read_b128 as inline asm: a compiler-visible LDS read makes hipcc drain every LDS-DMA in
+// flight first (s_waitcnt vmcnt(0): it cannot tell which stage a DMA writes), which
+// serialised the prefetch.  An asm read is outside hipcc's wait bookkeeping, so the caller
+// counts lgkmcnt itself and fences the consumers with sched_barrier.
+template <int OFF>
+__device__ __forceinline__ f32x4 ds_read16(unsigned addr) {
+    f32x4 r;
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(OFF));
+    return r;
+}
+
+template <int N>
+__device__ __forceinline__ void wait_lgkm() {
+    asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+    return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
 }
 
 template <int BM_, int BN_, int WM_, int WN_, int S_, int OCC_>
@@ -64,12 +86,16 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_dma_kernel(RowGemm
     constexpr int AI = BM / (RPI * WAVES), BI = BN / (RPI * WAVES);
     static_assert(AI * RPI * WAVES == BM && BI * RPI * WAVES == BN, "loader shape");
     constexpr int GPC = AI + BI;  // DMA instructions per chunk per wave
-    constexpr int DIST = S - 1;
-    static_assert(DIST >= 1 && DIST <= 3, "stages");
+    static_assert(S == 2, "two LDS stages");
     constexpr int STAGE = (BM + BN) * RB;
-    constexpr int RED = 2 * (BM / 64) * BN * 8;
-    constexpr int SMEM = STAGE * S > RED ? STAGE * S : RED;
-    __shared__ __attribute__((aligned(1024))) char smem[SMEM];
+    static_assert(STAGE >= 2 * (BM / 64) * BN * 8, "epilogue scratch");
+    // The two stages are separate LDS objects and the chunk loop is unrolled by two, so
+    // every ds_read and every DMA names its stage statically: hipcc's wait insertion can then
+    // tell a read of one stage from the DMA still in flight into the other and waits only
+    // for the former (with one array it drained every DMA before each read, the prefetch
+    // included).
+    __shared__ __attribute__((aligned(1024))) char st0[STAGE];
+    __shared__ __attribute__((aligned(1024))) char st1[STAGE];
     __shared__ __attribute__((aligned(16))) float sct[AFFINE ? 2 * DMA_MAXC : 4];
 
     const int tid = threadIdx.x, lane = tid & 63;
@@ -112,11 +138,10 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_dma_kernel(RowGemm
     const float* zero = (const float*)p.zero16;
     const float* abase = p.a + p.aoff;
 
-    auto issue = [&](int kc, int st) {
+    auto issue = [&](int kc, char* base) {
         const int k0 = kc * BK;
         const int tap = k0 / C;
         const int c0 = k0 - tap * C;
-        char* base = smem + st * STAGE;
 #pragma unroll
         for (int j = 0; j < AI; ++j) {
             bool valid;
@@ -168,49 +193,48 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_dma_kernel(RowGemm
     }
 
     const int nk = K / BK;
+    // per-lane LDS byte offsets of the MFMA fragments of k-group kg (slot (2 kg + lh) ^ swizzle)
+    unsigned aofs[KG][MT], bofs[KG][NT];
 #pragma unroll
-    for (int s = 0; s < DIST; ++s)
-        if (s < nk) issue(s, s);
-    for (int kc = 0; kc < nk; ++kc) {
-        if (kc + DIST < nk) issue(kc + DIST, (kc + DIST) % S);
-        const int ahead = min(DIST, nk - 1 - kc);  // chunks issued after kc, may stay in flight
-        if constexpr (DIST >= 3) {
-            if (ahead >= 3) wait_vm<3 * GPC>();
-            else if (ahead == 2) wait_vm<2 * GPC>();
-            else if (ahead == 1) wait_vm<GPC>();
-            else wait_vm<0>();
-        } else if constexpr (DIST == 2) {
-            if (ahead >= 2) wait_vm<2 * GPC>();
-            else if (ahead == 1) wait_vm<GPC>();
-            else wait_vm<0>();
-        } else {
-            if (ahead >= 1) wait_vm<GPC>();
-            else wait_vm<0>();
-        }
-        block_barrier();
-        const char* base = smem + (kc % S) * STAGE;
+    for (int kg = 0; kg < KG; ++kg) {
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) aofs[kg][mt] = aro[mt] + (((kg * 2 + lh) ^ afx[mt]) << 4);
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) bofs[kg][nt] = bro[nt] + (((kg * 2 + lh) ^ bfx[nt]) << 4);
+    }
+    const unsigned sct_lane = lds_addr(sct) + lh * 16;
+    constexpr int RD = MT + NT + (AFFINE ? 2 : 0);  // asm reads per k-group
+    auto compute = [&](int kc, const char* base) {
         const int k0 = kc * BK;
         const int tap = k0 / C, c0 = k0 - tap * C;
+        const unsigned sb = lds_addr(base);
+        const unsigned sa = sct_lane + c0 * 4;
+        f32x4 af[2][MT], bf[2][NT], sc[2], sh[2];
+        // fragments of k-group kg into register set kg & 1 (in flight until the counted wait)
+        auto load = [&](auto KG_) {
+            constexpr int kg = decltype(KG_)::value, set = kg & 1;
 #pragma unroll
-        for (int kg = 0; kg < KG; ++kg) {
-            const int c = kg * 2 + lh;
-            f32x4 af[MT], bf[NT];
+            for (int mt = 0; mt < MT; ++mt) af[set][mt] = ds_read16<0>(sb + aofs[kg][mt]);
 #pragma unroll
-            for (int mt = 0; mt < MT; ++mt) af[mt] = *(const f32x4*)(base + aro[mt] + ((c ^ afx[mt]) << 4));
-#pragma unroll
-            for (int nt = 0; nt < NT; ++nt) bf[nt] = *(const f32x4*)(base + bro[nt] + ((c ^ bfx[nt]) << 4));
+            for (int nt = 0; nt < NT; ++nt) bf[set][nt] = ds_read16<0>(sb + bofs[kg][nt]);
             if constexpr (AFFINE) {
+                sc[set] = ds_read16<kg * 32>(sa);
+                sh[set] = ds_read16<DMA_MAXC * 4 + kg * 32>(sa);
+            }
+        };
+        auto mma = [&](auto KG_) {
+            constexpr int kg = decltype(KG_)::value, set = kg & 1;
+            if constexpr (AFFINE) {  // rowgemm_kernel's commit arithmetic, on the fragment
                 const int ch = c0 + kg * 8 + lh * 4;  // the fragment's 4 channels
-                const f32x4 sc = *(const f32x4*)&sct[ch], sh = *(const f32x4*)&sct[DMA_MAXC + ch];
                 const bool rl = ARELU && ch < p.arelu;
 #pragma unroll
                 for (int mt = 0; mt < MT; ++mt) {
                     const bool keep = (tmask[mt] >> tap) & 1u;
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
-                        const float t = __builtin_fmaf(af[mt][j], sc[j], sh[j]);
+                        const float t = __builtin_fmaf(af[set][mt][j], sc[set][j], sh[set][j]);
                         const float u = rl ? fmaxf(t, 0.f) : t;
-                        af[mt][j] = keep ? u : 0.f;
+                        af[set][mt][j] = keep ? u : 0.f;
                     }
                 }
             }
@@ -220,18 +244,57 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_dma_kernel(RowGemm
                 for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
                     for (int nt = 0; nt < NT; ++nt)
-                        acc[mt][nt] = mfma32(af[mt][s], bf[nt][s], acc[mt][nt]);
-        }
-        // this stage's ds_reads must have returned before any wave restages it
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                        acc[mt][nt] = mfma32(af[set][mt][s], bf[set][nt][s], acc[mt][nt]);
+        };
+        static_assert(KG == 4, "four k-groups per chunk");
+        load(std::integral_constant<int, 0>{});
+        load(std::integral_constant<int, 1>{});
+        wait_lgkm<RD>();
+        __builtin_amdgcn_sched_barrier(0);
+        mma(std::integral_constant<int, 0>{});
+        __builtin_amdgcn_sched_barrier(0);
+        load(std::integral_constant<int, 2>{});
+        wait_lgkm<RD>();
+        __builtin_amdgcn_sched_barrier(0);
+        mma(std::integral_constant<int, 1>{});
+        __builtin_amdgcn_sched_barrier(0);
+        load(std::integral_constant<int, 3>{});
+        wait_lgkm<RD>();
+        __builtin_amdgcn_sched_barrier(0);
+        mma(std::integral_constant<int, 2>{});
+        __builtin_amdgcn_sched_barrier(0);
+        wait_lgkm<0>();
+        __builtin_amdgcn_sched_barrier(0);
+        mma(std::integral_constant<int, 3>{});
+        // every wave's reads of this stage have returned (waited above) before any restages it
         block_barrier();
+    };
+    // even chunks in st0, odd chunks in st1; chunk kc+1's DMA flies during chunk kc's MFMAs
+    issue(0, st0);
+    for (int kc = 0; kc < nk; kc += 2) {
+        if (kc + 1 < nk) {
+            issue(kc + 1, st1);
+            wait_vm<GPC>();
+        } else {
+            wait_vm<0>();
+        }
+        block_barrier();
+        compute(kc, st0);
+        if (kc + 1 >= nk) break;
+        if (kc + 2 < nk) {
+            issue(kc + 2, st0);
+            wait_vm<GPC>();
+        } else {
+            wait_vm<0>();
+        }
+        block_barrier();
+        compute(kc + 1, st1);
     }
-    row_epilogue<EMODE, BM, BN, WM, WN>(p, acc, m0, n0, tile_m, wm, wn, lane, tid, (float*)smem);
+    row_epilogue<EMODE, BM, BN, WM, WN>(p, acc, m0, n0, tile_m, wm, wn, lane, tid, (float*)st0);
 }
 
 using DmaTile0 = DmaTile<128, 128, 64, 64, 2, 2>;  // 2 stages, 64 KB (+8 KB affine table)
 using DmaTile1 = DmaTile<128, 64, 64, 32, 2, 2>;
-using DmaTile2 = DmaTile<128, 128, 64, 64, 3, 1>;  // 3 stages, one block per CU
 
 template <int AMODE, int AOP, int EMODE, class T>
 static int dma_go(const RowGemmArgs& a, hipStream_t s) {
@@ -246,7 +309,6 @@ template <int AMODE, int AOP, int EMODE>
 static int dma_tile(const RowGemmArgs& a, int tile, hipStream_t s) {
     if (tile == 0) return dma_go<AMODE, AOP, EMODE, DmaTile0>(a, s);
     if (tile == 1) return dma_go<AMODE, AOP, EMODE, DmaTile1>(a, s);
-    if (tile == 2) return dma_go<AMODE, AOP, EMODE, DmaTile2>(a, s);
     return -1;
 }
 
@@ -259,7 +321,7 @@ int rowgemm_dma_ok(const RowGemmArgs& a) {
     return 1;
 }
 
-// tile: 0 = 128x128 (2 stages), 1 = 128x64, 2 = 128x128 (3 stages, one block per CU)
+// tile: 0 = 128x128, 1 = 128x64 (two LDS stages each)
 int launch_rowgemm_dma(const RowGemmArgs& a, int tile, hipStream_t s) {
     if (!rowgemm_dma_ok(a) || a.M < 1 || a.K != gather_taps(a.amode) * a.C) return -1;
     const bool aff = a.ascale != nullptr;
