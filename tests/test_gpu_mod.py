@@ -247,12 +247,12 @@ def test_rg16_tile_choice_is_numerically_invisible(side):
     x, t = inputs(29, 2, side, side)
     P = MO.make_params(31, 128, 5)
     outs = {}
-    for tile in (0, 2, 4, -1):
+    for tile in (0, 2, 4, 12, 13, -1):  # 12 / 13: tiles 4 / 0 with read-ahead fragments
         m = _bf16_model(P, 128, 5)
         with options(m.flatten_().rt, rg16_tile=tile):
             outs[tile] = _bf16_step(m, x, t)
         del m
-    for tile in (2, 4, -1):
+    for tile in (2, 4, 12, 13, -1):
         _assert_same(outs[0], outs[tile], f"{side}^2 tile {tile} vs 0")
 
 

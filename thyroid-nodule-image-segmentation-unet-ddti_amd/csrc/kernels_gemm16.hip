@@ -55,12 +55,16 @@ __device__ __forceinline__ void wait_vm() {
 // ILV: the DMA pieces of chunk k+DIST are issued between the MFMAs of chunk k (one share
 // per k-step, placed by sched_group_barrier) instead of all at the top of the iteration,
 // where every wave of the block issued them at once and left the matrix pipes idle.
+// RA: read ahead -- the LDS fragments of k-step kk + 1 are issued before the MFMAs of k-step
+// kk (two register sets, sched_barrier fences), so each k-step waits only for reads issued
+// one k-step earlier instead of for its own (the compiler's schedule waited lgkmcnt(0) in
+// front of every k-step's MFMAs).
 template <int BM_, int BN_, int WM_, int WN_, int S_, int OCC_, int BK_ = 64, bool ONEBAR_ = false,
-          bool ILV_ = false>
+          bool ILV_ = false, bool RA_ = false>
 struct Tile16 {
     static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, S = S_, OCC = OCC_;
     static constexpr int BK = BK_;
-    static constexpr bool ONEBAR = ONEBAR_, ILV = ILV_;
+    static constexpr bool ONEBAR = ONEBAR_, ILV = ILV_, RA = RA_;
     static constexpr int WAVES = (BM / WM) * (BN / WN);
     static constexpr int THREADS = 64 * WAVES;
 };
@@ -197,6 +201,30 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm16_kernel(RowGemmAr
         block_barrier();
         const char* base = smem + (kc % S) * STAGE;
         const bool more = kc + DIST < nk;
+        if constexpr (T::RA && !ILV) {
+            bf16x8 af[2][MT], bfr[2][NT];
+            auto rd = [&](int kk, int set) {
+                const int c = kk * 2 + lh;
+#pragma unroll
+                for (int mt = 0; mt < MT; ++mt)
+                    af[set][mt] = *(const bf16x8*)(base + aro[mt] + ((c ^ afx[mt]) << 4));
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt)
+                    bfr[set][nt] = *(const bf16x8*)(base + bro[nt] + ((c ^ bfx[nt]) << 4));
+            };
+            rd(0, 0);
+#pragma unroll
+            for (int kk = 0; kk < BK / 16; ++kk) {
+                if (kk + 1 < BK / 16) rd(kk + 1, (kk + 1) & 1);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                    for (int nt = 0; nt < NT; ++nt)
+                        acc[mt][nt] = mfma32_bf16(af[kk & 1][mt], bfr[kk & 1][nt], acc[mt][nt]);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        } else
 #pragma unroll
         for (int kk = 0; kk < BK / 16; ++kk) {
             const int c = kk * 2 + lh;
@@ -259,9 +287,12 @@ using T16_8 = Tile16<128, 128, 64, 64, 4, 2, 32, true>;
 using T16_9 = Tile16<256, 256, 128, 64, 4, 1, 32, false, true>;
 using T16_10 = Tile16<256, 256, 128, 64, 5, 1, 32, true, true>;
 using T16_11 = Tile16<128, 128, 64, 64, 3, 1, 64, false, true>;
+// read-ahead LDS fragments: 12 = tile 4 (256x256), 13 = tile 0 (128x128, 2 blocks per CU)
+using T16_12 = Tile16<256, 256, 128, 64, 2, 1, 64, false, false, true>;
+using T16_13 = Tile16<128, 128, 64, 64, 2, 2, 64, false, false, true>;
 #define ROWGEMM16_TILES(X)                                                                     \
     X(0, T16_0) X(1, T16_1) X(2, T16_2) X(3, T16_3) X(4, T16_4) X(5, T16_5) X(6, T16_6) X(7, T16_7) \
-    X(8, T16_8) X(9, T16_9) X(10, T16_10) X(11, T16_11)
+    X(8, T16_8) X(9, T16_9) X(10, T16_10) X(11, T16_11) X(12, T16_12) X(13, T16_13)
 
 template <int AMODE, int EMODE, class T>
 static int rg16_go(const RowGemmArgs& a, hipStream_t s) {

@@ -109,6 +109,7 @@ struct Options {
     int tile16_n64 = 1;
     int rg16 = 1;              // bf16 row GEMMs on the LDS-DMA kernel (0: register-staged)
     int rg16_tile = -1;        // its tile (-1 = per GEMM, rg16_tile())
+    int rg16_ra = 0;           // per-GEMM choice on the read-ahead tiles 12 / 13
     int wg16 = 1;              // bf16 3x3 wgrad on the LDS-DMA transposed-read kernel
     int wg16_tile = 2;         // its tile (2 = 256x256)
     int wg16t = 1;             // bf16 ConvT wgrad on the same kernel
@@ -132,7 +133,7 @@ const OptionDesc OPTION_TABLE[] = {
     {"tile_n64_dgrad", &Options::tile_n64_dgrad}, {"tile_convt64", &Options::tile_convt64},
     {"tile16_n128", &Options::tile16_n128},     {"tile16_n128_dgrad", &Options::tile16_n128_dgrad},
     {"tile16_n64", &Options::tile16_n64},       {"rg16", &Options::rg16},
-    {"rg16_tile", &Options::rg16_tile},         {"wg16", &Options::wg16},
+    {"rg16_tile", &Options::rg16_tile},         {"rg16_ra", &Options::rg16_ra},         {"wg16", &Options::wg16},
     {"wg16_tile", &Options::wg16_tile},         {"wg16t", &Options::wg16t},
     {"xcd16", &Options::xcd16},                 {"xcd_remap", &Options::xcd_remap},
     {"wgrad_stream", &Options::wgrad_stream},   {"dz_in_loaders", &Options::dz_in_loaders},
@@ -579,11 +580,13 @@ int rg16_tile(const unet_ctx* c, const RowGemmArgs& g) {
         return g.N % bn == 0 && (cout == 0 || cout % bn == 0);
     };
     if (c->opt.rg16_tile >= 0) return fits(c->opt.rg16_tile) ? c->opt.rg16_tile : 0;
-    if (!fits(4)) return 0;
+    // option rg16_ra: the same shapes with read-ahead LDS fragments (tiles 12 / 13)
+    const int t0 = c->opt.rg16_ra ? 13 : 0, t4 = c->opt.rg16_ra ? 12 : 4;
+    if (!fits(4)) return t0;
     const int64_t blocks = (g.M + 255) / 256 * (g.N / 256);
-    if (blocks < 256) return 0;
-    if (g.emode == E_STORE_BN && g.K < 8192) return 0;
-    return 4;
+    if (blocks < 256) return t0;
+    if (g.emode == E_STORE_BN && g.K < 8192) return t0;
+    return t4;
 }
 // 3x3 weight gradients of layers with Cin, Cout multiples of 128 on the LDS-DMA
 // transposed-read kernel (kernels_gemm16.hip wgrad16_kernel) from the forward's bf16 input
