@@ -1248,6 +1248,7 @@ using Wr3Tile4 = WgTile<64, 64, 32, 32, 64>;    // 64-pixel chunks
 int wgrad_tile_taps(int tile) { return tile >= 20 ? 3 : 1; }
 
 int wgrad_tile_dims(int tile, int* bm, int* bn, int* bkp) {
+    if (tile == 34) tile = 21;                 // pipelined row3, 128x64 at 2 waves / SIMD
     if (tile >= 30 && tile <= 33) tile -= 10;  // pipelined row3 (kernels_wgrad_pipe.hip)
     if (tile == 10 || tile == 15) return wgrad16_tile_dims(tile - 10, bm, bn, bkp);
     WGRAD_ROW3_TILES(WG_DIMS_R3)
@@ -1362,7 +1363,7 @@ int launch_wgrad(const WgradArgs& a, int tile, hipStream_t s) {
     const bool aff = a.ascale != nullptr, dz = a.bcoef != nullptr;
     if (a.arelu && !aff) return -1;
     if (a.arelu && dz) return -1;  // OP_DZ loaders are the ReLU -> BN order only
-    if (tile >= 30 && tile <= 33)  // row3, software-pipelined (kernels_wgrad_pipe.hip)
+    if (tile >= 30 && tile <= 34)  // row3, software-pipelined (kernels_wgrad_pipe.hip)
         return launch_wgrad_row3_pipe(a, tile - 30, s);
     if (tile >= 20) {  // one row of 3x3 taps per block (wgrad_row3_kernel)
         if (a.amode != G_CONV3 || a.bmode != G_IDENT) return -1;

@@ -250,6 +250,7 @@ using Wr3P0 = Wr3PipeTile<64, 64, 32, 32, 32>;
 using Wr3P1 = Wr3PipeTile<128, 64, 64, 32, 32>;
 using Wr3P2 = Wr3PipeTile<64, 128, 32, 64, 32>;
 using Wr3P3 = Wr3PipeTile<128, 128, 64, 64, 32>;
+using Wr3P4 = Wr3PipeTile<128, 64, 64, 32, 32, 2>;  // Wr3P1 at two waves per SIMD
 
 template <int AOP, bool BDZ, class T>
 static int wr3p_go(const WgradArgs& a, hipStream_t s) {
@@ -268,13 +269,14 @@ static int wr3p_tile(const WgradArgs& a, int tile, hipStream_t s) {
         case 1: return wr3p_go<AOP, BDZ, Wr3P1>(a, s);
         case 2: return wr3p_go<AOP, BDZ, Wr3P2>(a, s);
         case 3: return wr3p_go<AOP, BDZ, Wr3P3>(a, s);
+        case 4: return wr3p_go<AOP, BDZ, Wr3P4>(a, s);
     }
     return -1;
 }
 
 }  // namespace
 
-// tile 0..3: the shapes of kernels_gemm.hip's row3 tiles 20..23
+// tile 0..3: the shapes of kernels_gemm.hip's row3 tiles 20..23; 4 = tile 1 at two waves per SIMD
 int launch_wgrad_row3_pipe(const WgradArgs& a, int tile, hipStream_t s) {
     if (a.P < 1 || a.bf16 || a.amode != G_CONV3 || a.bmode != G_IDENT) return -1;
     const bool aff = a.ascale != nullptr, dz = a.bcoef != nullptr;

@@ -94,6 +94,7 @@ struct Options {
                                // 27.1 -> 24.4 ms/step), 2 layers with a 64-channel operand
     int wgrad_row3_tile = -1;  // its tile (>= 20), -1 = by channel counts
     int wgrad_row3_pipe = 0;       // row3 weight gradients on the pipelined kernel (ids 30..33)
+    int wgrad_row3_big = 21;       // row3 tile where Cin, Cout % 128 == 0 (-1 = 23 / 33)
     int wgrad_row3_blocks = 1536;  // split-K target (blocks) of the row3 weight gradients
                                    // (r02 sweep 512..2048: 1536 best, 391 vs 386 img/s)
     int wgrad_tile_w = 0;      // f32 wgrad tile, both channel counts multiples of 128
@@ -127,6 +128,7 @@ struct OptionDesc {
 const OptionDesc OPTION_TABLE[] = {
     {"wgrad_row3", &Options::wgrad_row3},       {"wgrad_row3_tile", &Options::wgrad_row3_tile},
     {"wgrad_row3_blocks", &Options::wgrad_row3_blocks}, {"wgrad_row3_pipe", &Options::wgrad_row3_pipe},
+    {"wgrad_row3_big", &Options::wgrad_row3_big},
     {"wgrad_tile_w", &Options::wgrad_tile_w},   {"wgrad_tile_n", &Options::wgrad_tile_n},
     {"wgrad16_tile", &Options::wgrad16_tile},   {"tile_n128", &Options::tile_n128},
     {"tile_n128_dgrad", &Options::tile_n128_dgrad}, {"tile_n64", &Options::tile_n64},
@@ -532,10 +534,18 @@ WgradCfg wgrad_cfg(const unet_ctx* c, int CA, int tapsA, int CB, int tapsB, int6
         const bool row3 = tapsA == 9 && tapsB == 1 && row_w > 0 && row_w % 32 == 0 &&
                           CA % 64 == 0 && CB % 64 == 0 &&
                           (r3 == 1 || (r3 == 2 && (CA == 64 || CB == 64)));
-        if (row3)
+        if (row3) {
             w.tile = r3t >= 20 ? r3t
                                : (CA % 128 == 0 ? (CB % 128 == 0 ? 23 : 21) : (CB % 128 == 0 ? 22 : 20)) +
                                      (c->opt.wgrad_row3_pipe ? 10 : 0);
+            // option wgrad_row3_big: the tile of the layers whose channel counts both divide
+            // 128.  Default 128x64 (21) rather than 128x128 (23): the same GEMM time (126 TF/s)
+            // but twice the tiles, so the 1536-block target needs half the split-K slices and
+            // the slab reduction halves (r02 A/B: wgrad_reduce 1.09 -> 0.64 ms, 404 -> 408 img/s)
+            if (r3t < 20 && c->opt.wgrad_row3_big >= 20 && !c->opt.wgrad_row3_pipe &&
+                CA % 128 == 0 && CB % 128 == 0)
+                w.tile = c->opt.wgrad_row3_big;
+        }
         wgrad_tile_dims(w.tile, &w.bm, &w.bn, &w.bkp);
     }
     const int64_t tiles =
@@ -832,7 +842,7 @@ std::string r3label(const char* fam, const RowGemmArgs& g, int layer) {
 std::string wlabel(const char* fam, const WgradCfg& w, int layer) {
     char b[112];
     snprintf(b, sizeof b, "%s/wgrad%s_%dx%dx%d|%d", fam,
-             w.tile >= 30 ? "3p" : (w.tile >= 20 ? "3" : ""), w.bm, w.bn, w.bkp, layer);
+             w.tile >= 30 ? (w.tile == 34 ? "3p2" : "3p") : (w.tile >= 20 ? "3" : ""), w.bm, w.bn, w.bkp, layer);
     return b;
 }
 
