@@ -94,6 +94,8 @@ struct Options {
                                // 27.1 -> 24.4 ms/step), 2 layers with a 64-channel operand
     int wgrad_row3_tile = -1;  // its tile (>= 20), -1 = by channel counts
     int wgrad_row3_pipe = 0;       // row3 weight gradients on the pipelined kernel (ids 30..33)
+    int wgrad_blocks = 2048;       // split-K target (blocks) of the one-tap f32 weight gradients
+    int rg16_bn_k = 8192;          // rg16: E_STORE_BN GEMMs with K below this take the 128x128 tile
     int wgrad16_blocks = 1536;     // split-K target (blocks) of the bf16 weight gradients
                                    // (config 4 A/B: 1536 +1.4 % over 2048, 1024 -4.7 %)
     int wgrad_row3_big = 21;       // row3 tile where Cin, Cout % 128 == 0 (-1 = 23 / 33)
@@ -131,6 +133,7 @@ const OptionDesc OPTION_TABLE[] = {
     {"wgrad_row3", &Options::wgrad_row3},       {"wgrad_row3_tile", &Options::wgrad_row3_tile},
     {"wgrad_row3_blocks", &Options::wgrad_row3_blocks}, {"wgrad_row3_pipe", &Options::wgrad_row3_pipe},
     {"wgrad_row3_big", &Options::wgrad_row3_big}, {"wgrad16_blocks", &Options::wgrad16_blocks},
+    {"wgrad_blocks", &Options::wgrad_blocks},   {"rg16_bn_k", &Options::rg16_bn_k},
     {"wgrad_tile_w", &Options::wgrad_tile_w},   {"wgrad_tile_n", &Options::wgrad_tile_n},
     {"wgrad16_tile", &Options::wgrad16_tile},   {"tile_n128", &Options::tile_n128},
     {"tile_n128_dgrad", &Options::tile_n128_dgrad}, {"tile_n64", &Options::tile_n64},
@@ -554,7 +557,8 @@ WgradCfg wgrad_cfg(const unet_ctx* c, int CA, int tapsA, int CB, int tapsB, int6
         (int64_t)(tapsA * CA / (w.bm * wgrad_tile_taps(w.tile))) * (tapsB * CB / w.bn);
     // blocks to launch: 2048 one-tap blocks; a row3 block does the work of three, and every
     // extra split adds a full Mw x Nw slab to write and reduce
-    const int64_t target = bf16 ? c->opt.wgrad16_blocks : (w.tile >= 20 ? c->opt.wgrad_row3_blocks : 2048);
+    const int64_t target = bf16 ? c->opt.wgrad16_blocks
+                                : (w.tile >= 20 ? c->opt.wgrad_row3_blocks : c->opt.wgrad_blocks);
     int64_t s = (target + tiles - 1) / tiles;
     const int64_t maxs = P / (8 * w.bkp) > 0 ? P / (8 * w.bkp) : 1;  // >= 8 chunks per split
     // (P need not be a multiple of the pixel chunk: the kernel zero-fills the tail)
@@ -597,7 +601,7 @@ int rg16_tile(const unet_ctx* c, const RowGemmArgs& g) {
     if (!fits(4)) return t0;
     const int64_t blocks = (g.M + 255) / 256 * (g.N / 256);
     if (blocks < 256) return t0;
-    if (g.emode == E_STORE_BN && g.K < 8192) return t0;
+    if (g.emode == E_STORE_BN && g.K < c->opt.rg16_bn_k) return t0;
     return t4;
 }
 // 3x3 weight gradients of layers with Cin, Cout multiples of 128 on the LDS-DMA
