@@ -311,8 +311,15 @@ def main():
         mname = "mod.UNet(in=1,out=1,base_filters=128,depth=5) 497,438,849 params"
     else:
         metric = "images/sec fwd+bwd, UNet 256x256x1 bs=32/GPU (Dice+BCE, AdamW)"
+        if world == 1:
+            tag = "BASELINE config 2"
+        elif backend == "nccl" and ndev >= world:
+            tag = "BASELINE config 3" if (world, B) == (8, 32) else f"config-3 shape on {world} GPUs"
+        else:  # several ranks sharing devices over gloo: exercises the DP code path only
+            tag = (f"DP rehearsal: {world} ranks on {max(ndev, 1)} GPU(s) over {backend}, "
+                   f"not BASELINE config 3")
         workload = (f"models/model.py UNet depth-4 base-64, 1x{S}x{S}, bs={B}/GPU, "
-                    f"fwd+BCE+Dice+bwd+AdamW (BASELINE config {'2' if world == 1 else '3'})")
+                    f"fwd+BCE+Dice+bwd+AdamW ({tag})")
         mname = "UNet(in=1,out=1) 31,042,369 params"
     out = {"metric": metric,
            "value": round(value, 3), "unit": "images/sec", "n_gpus": world, "steps": args.steps,

@@ -66,6 +66,24 @@ def resize_u8(img, oh, ow):
     return np.ascontiguousarray(a)
 
 
+def nearest_index(in_size, out_size):
+    """Pillow's NEAREST scale (Image.resize forces it for "P" and "1" images; libImaging
+    Geometry.c ImagingScaleAffine): the source coordinate starts at s/2, s = in/out, and
+    is advanced by += s in double per output pixel; index = int(coordinate)."""
+    s = float(in_size) / out_size
+    xo = s * 0.5
+    idx = np.empty(out_size, np.int64)
+    for x in range(out_size):
+        idx[x] = int(xo)
+        xo += s
+    return idx
+
+
+def resize_nearest_u8(img, oh, ow):
+    a = np.asarray(img, np.uint8)
+    return np.ascontiguousarray(a[nearest_index(a.shape[0], oh)][:, nearest_index(a.shape[1], ow)])
+
+
 def to_tensor(img_u8):
     """TF.to_tensor of an 'L' image: float32(u8) / 255."""
     return np.asarray(img_u8, np.float32) / np.float32(255.0)

@@ -28,7 +28,8 @@ def test_library_plan_matches_restatement(n_in, n_out):
     np.testing.assert_array_equal(b, rb)
 
 
-@pytest.mark.parametrize("n,bs,world", [(10, 4, 2), (37, 8, 3), (5, 4, 4), (16, 16, 8), (3, 2, 4)])
+@pytest.mark.parametrize("n,bs,world", [(10, 4, 2), (37, 8, 3), (5, 4, 4), (16, 16, 8), (3, 2, 4),
+                                         (2 * 256 + 3, 256, 8), (256 + 5, 256, 4)])
 @pytest.mark.parametrize("shuffle", [False, True])
 def test_dataparallel_shard_sampler(n, bs, world, shuffle):
     """Every rank's shards concatenate to the reference loader's global batch
@@ -50,3 +51,48 @@ def test_dataparallel_shard_sampler(n, bs, world, shuffle):
                 assert per_rank[r][b] == want
             seen += glob.tolist()
         assert sorted(seen) == list(range(n))
+
+
+@pytest.mark.parametrize("h,w,oh,ow", [(580, 360, 512, 512), (37, 100, 64, 64), (2999, 17, 256, 1000),
+                                       (64, 64, 64, 64), (7, 3, 513, 1)])
+def test_nearest_restatement_matches_pillow(h, w, oh, ow):
+    """Pillow resizes palette ("P") and bilevel ("1") images with NEAREST whatever filter
+    TF.resize asks for (Image.resize); the restatement and the library's one-tap plan
+    reproduce it."""
+    from PIL import Image
+    from unet_hip.data import nearest_plan
+    rng = np.random.default_rng(h * 31 + w)
+    idx = rng.integers(0, 256, (h, w), dtype=np.uint8)
+    pal = Image.fromarray(idx, "P")
+    ref = np.asarray(pal.resize((ow, oh), Image.BILINEAR))
+    np.testing.assert_array_equal(RR.resize_nearest_u8(idx, oh, ow), ref)
+    bits = Image.fromarray((idx > 127).astype(np.uint8) * 255, "L").convert("1", dither=Image.Dither.NONE)
+    rb = np.asarray(bits.resize((ow, oh), Image.BILINEAR).convert("L"))
+    np.testing.assert_array_equal(RR.resize_nearest_u8(np.asarray(bits.convert("L")), oh, ow), rb)
+    for n_in, n_out in ((w, ow), (h, oh)):
+        k, b = nearest_plan(n_in, n_out)
+        assert (k == 1 << 22).all() and (b[:, 1] == 1).all()
+        np.testing.assert_array_equal(b[:, 0], RR.nearest_index(n_in, n_out))
+
+
+def test_decode_u8_modes_match_to_tensor():
+    """DecodeU8 planes / 255 == the host ToTensor (TF.to_tensor) for "L", "P" and "1";
+    "P" / "1" planes are tagged for NEAREST and keep the tag through pickling (workers);
+    multi-band images are refused."""
+    import pickle
+    import torch
+    from PIL import Image
+    from data.data_loader import DecodeU8
+    from utils.transforms import ToTensor
+    rng = np.random.default_rng(5)
+    a = rng.integers(0, 256, (40, 30), dtype=np.uint8)
+    for mode, img in (("L", Image.fromarray(a, "L")), ("P", Image.fromarray(a, "P")),
+                      ("1", Image.fromarray(a, "L").convert("1"))):
+        pl, _ = DecodeU8()(img, img)
+        assert pl.resample == ("bilinear" if mode == "L" else "nearest")
+        assert pickle.loads(pickle.dumps(pl)).resample == pl.resample
+        want, _ = ToTensor()(img, img)
+        got = torch.from_numpy(np.asarray(pl, np.float32) / np.float32(255.0))[None]
+        assert torch.equal(got, want), mode
+    with pytest.raises(ValueError):
+        DecodeU8()(Image.fromarray(np.zeros((4, 4, 3), np.uint8), "RGB"), None)

@@ -204,3 +204,108 @@ def test_gathered_batch_loss_matches_dataparallel_focal(golden_dir, tag, B, seed
     # reference's fp32 error (~4e-3 norm-relative is the reference's own
     # fp32 vs fp64 spread; the loss here is evaluated in fp64)
     np.testing.assert_allclose(norms, f[tag + "grad_norm"], rtol=2e-3)
+
+
+def _config3_worker(rank, world, port, q, n, bs):
+    """One rank of config 3's data-parallel step arithmetic: its DataParallelShardSampler
+    shard of every global batch, a per-rank 'gradient' arena built from its samples, the
+    product's BucketReducer over the real 31M-float bucket table of models/model.py."""
+    import sys
+    for p in (REPO, PKG):
+        sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(1)
+    try:
+        from data.data_loader import DataParallelShardSampler
+        from unet_hip.dist import BucketReducer
+        from unet_hip.runtime import UNetRuntime
+        rt = UNetRuntime("cuda:0")  # host-side tables only (no device work)
+        base = (torch.arange(rt.n_param_floats) % 13).float()
+        samp = DataParallelShardSampler(n, bs, True, rank, world, seed=7)
+        out = []
+        for shard in samp:
+            # every per-sample contribution is an exact small integer multiple of `base`,
+            # so the summed arena is exact whatever the reduction order
+            w = float(sum(i + 1 for i in shard))
+            arena = base * w
+            ws = BucketReducer(rt.buckets).reduce(arena)
+            ok = torch.equal(arena[:1000], base[:1000] * arena[1] / max(base[1].item(), 1.0))
+            out.append((len(shard), float(arena[1]), float(arena[-1]), ok, ws,
+                        bool(torch.equal(arena, base * float(arena[1])))))
+        if rank == 0:
+            q.put(out)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("world,n,bs", [(4, 256 + 5, 256), (8, 2 * 256 + 3, 256)])
+def test_config3_shards_and_bucket_sum(world, n, bs):
+    """Config 3 (bs 256 = 8 x 32 over 8 ranks; 4 x 64 over 4) with a ragged last batch
+    smaller than the rank count (some shards empty): every rank's BucketReducer result
+    equals the single-process sum over the GLOBAL batch, for every bucket of the real
+    models/model.py gradient table."""
+    from data.data_loader import DataParallelShardSampler
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_config3_worker, args=(r, world, port, q, n, bs)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = q.get(timeout=500)
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    glob = DataParallelShardSampler(n, bs, True, 0, world, seed=7).global_batches()
+    assert len(out) == len(glob)
+    for (n0, v1, vlast, ok, ws, whole), gb in zip(out, glob):
+        want = float(sum(int(i) + 1 for i in gb))
+        assert ws == world and ok and whole
+        assert v1 == want * 1.0, (v1, want)   # base[1] == 1
+        assert n0 == len(torch.chunk(gb, world)[0])
+    assert out[0][0] == bs // world                 # 32 per GPU at 8 ranks
+    assert len(torch.chunk(glob[-1], world)) < world  # the ragged batch left shards empty
+
+
+def _gather_worker(rank, world, port, q, sizes):
+    import sys
+    from types import SimpleNamespace
+    sys.path.insert(0, PKG)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from unet_hip.dist import DistributedUNet
+        off = sum(sizes[:rank])
+        n = sizes[rank]
+        full = torch.arange(sum(sizes) * 2 * 3 * 3, dtype=torch.float32).view(-1, 2, 3, 3)
+        mfull = -full[:, :1]
+        imgs = full[off:off + n] if n else None
+        msks = mfull[off:off + n] if n else None
+        gi, gm, o, c = DistributedUNet.gather_batch(SimpleNamespace(group=None), imgs, msks, "cpu")
+        q.put((rank, torch.equal(gi, full), torch.equal(gm, mfull), o, c))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("sizes", [(2, 2, 1), (1, 0, 0), (3, 3, 2)])
+def test_gather_batch_rebuilds_the_global_batch(sizes):
+    """DistributedUNet.gather_batch (the trainer's DataParallel mixup: the reference mixes
+    the whole batch before the scatter, utils/trainer.py:62-78) rebuilds the gathered batch
+    on every rank from ragged and empty shards, with each rank's offset and count."""
+    world = len(sizes)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_worker, args=(r, world, port, q, list(sizes))) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)])
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    for r, ok_i, ok_m, o, c in res:
+        assert ok_i and ok_m
+        assert (o, c) == (sum(sizes[:r]), sizes[r])

@@ -69,3 +69,23 @@ def test_main_cli_gpu_transforms(tmp_path, monkeypatch):
                             "--dice_ratio", "1", "--gpu_transforms"])
     main.main(args)
     assert len(os.listdir(tmp_path / "experiments")) == 1
+
+
+@pytest.mark.parametrize("mode", ["P", "1"])
+@pytest.mark.parametrize("h,w,s", [(580, 360, 512), (100, 37, 64), (64, 64, 64)])
+def test_palette_and_bilevel_resize_bit_exact(mode, h, w, s):
+    """Palette and bilevel files: Pillow's Image.resize (TF.resize) uses NEAREST for those
+    modes; DecodeU8 tags the planes and the device path matches Resize + ToTensor."""
+    from PIL import Image
+    import unet_hip
+    from data.data_loader import DecodeU8
+    from utils.transforms import Resize, ToTensor
+    rng = np.random.default_rng(h * 3 + w)
+    a = rng.integers(0, 256, (h, w), dtype=np.uint8)
+    img = Image.fromarray(a, "P") if mode == "P" else Image.fromarray(a, "L").convert("1")
+    pi, pm = DecodeU8()(img, img)
+    pipe = unet_hip.GpuResizeToTensor((s, s), device="cuda:0")
+    x, t = pipe([pi], [pm])
+    torch.cuda.synchronize()
+    hx, ht = ToTensor()(*Resize((s, s))(img, img))
+    assert torch.equal(x[0].cpu(), hx) and torch.equal(t[0].cpu(), ht)

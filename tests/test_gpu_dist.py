@@ -221,3 +221,131 @@ def test_trainer_dp2_ragged_last_batch_matches_dataparallel(tmp_path):
           f"fp32 oracle mean {np.abs(ref32 - ref64).mean():.3e} / {np.abs(ref32p - ref64).mean():.3e}")
     assert d_hip.max() <= 4 * 1e-4 * 1.01
     assert d_hip.mean() <= 2 * d_32 + 1e-8
+
+
+def _eval_worker(rank, world, port, q, tmp, tag, lr):
+    import sys
+    for p in (REPO, PKG, os.path.join(REPO, "tests")):
+        sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import argparse
+        from _helpers import check_eval
+        from data.data_loader import DataParallelShardSampler, SyntheticSegmentation, dp_collate
+        from models.model import UNet
+        from oracle import unet_ref_cpu as O
+        from utils.trainer import Trainer
+        from utils.utils import Config, create_logger
+        torch.cuda.set_device(0)
+        f = np.load(os.path.join(REPO, "tests", "golden", "unet_dpe_64.npz"), allow_pickle=False)
+        ns = argparse.Namespace(model_type="UNet", lr=lr, bce_ratio=1.0, dice_ratio=0.0,
+                                focal_ratio=1.0, boundary_ratio=0.0, use_mixup=False,
+                                mixup_prob=0.0, mixup_alpha=0.2, epochs=1, early_stop_patience=5,
+                                batch_size=4, num_workers=0)
+        cfg = Config(ns, base_dir=os.path.join(tmp, f"r{rank}"))
+        cfg.device = torch.device("cuda:0")
+
+        def loader(seed, bs):
+            return torch.utils.data.DataLoader(
+                SyntheticSegmentation(5, 64, seed=seed),
+                batch_sampler=DataParallelShardSampler(5, bs, False, rank, world), collate_fn=dp_collate())
+        # val: global batches [0..3] -> 2 + 2 and [4] -> 1 + empty; test at batch 2: 1 + 1,
+        # 1 + 1 and 1 + empty (Trainer.test must join the count reduction on an empty shard)
+        loaders = (loader(4, 4), loader(5, 4), loader(6, 2))
+        bufs = O.init_buffers()
+        off = 0
+        for name in O.BN_LAYERS:
+            c = bufs[f"{name}.running_mean"].numel()
+            bufs[f"{name}.running_mean"] = torch.from_numpy(f[tag + "init_running_mean"][off:off + c].copy())
+            bufs[f"{name}.running_var"] = torch.from_numpy(f[tag + "init_running_var"][off:off + c].copy())
+            bufs[f"{name}.num_batches_tracked"] = torch.tensor(30)
+            off += c
+        m = UNet()
+        m.load_state_dict({**O.make_params(42), **bufs})
+        tr = Trainer(cfg, loaders, create_logger(os.path.join(cfg.log_dir, "t.log")), m)
+        tr.train_one_epoch(0)
+        st = tr.model._state
+        own = st.bn_arena.detach().clone()
+        r0 = own.clone()
+        dist.broadcast(r0, src=0)
+        drifted = not torch.equal(own, r0)  # rank 1 trained on other shards: its EMA differs
+        val_loss, val_iou = tr.validate(0)
+        after = st.bn_arena.detach().clone()
+        synced = torch.equal(after, r0) and torch.equal(st.nbt_arena.cpu(), torch.full((18,), 32))
+        metrics = tr.test()
+        # this rank's shards of the val set in eval mode, and the semantic check: the eval
+        # forward equals the oracle's resynced from this rank's (now rank 0's) params + buffers
+        ds = SyntheticSegmentation(5, 64, seed=5)
+        mine = [i for b in loaders[1].batch_sampler for i in b]
+        x = torch.stack([ds[i][0] for i in mine])
+        t = torch.stack([ds[i][1] for i in mine])
+        tr.model.eval()
+        with torch.no_grad():
+            lg = tr.model(x.to("cuda:0")).cpu().numpy()
+        check_eval(tr.model, O.forward, x, t)
+        q.put((rank, drifted, synced, val_loss, val_iou, metrics, mine, lg,
+               after.cpu().numpy() if rank == 0 else None,
+               st.param_arena.detach().cpu().numpy() if rank == 0 else None))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("tag,lr", [("lr0_", 0.0), ("lr4_", 1e-4)])
+def test_trainer_dp2_eval_uses_replica0_buffers(tmp_path, golden_dir, tag, lr):
+    """Trainer.validate / Trainer.test over two ranks after a DP training epoch evaluate
+    every shard with rank 0's BN running statistics, as nn.DataParallel does (it
+    re-replicates module 0, buffers included, for every forward: utils/trainer.py:28-30,
+    139, 216), pinned by the reference-generated tests/golden/unet_dpe_64.npz.
+
+    * rank 1's running statistics drift from rank 0's during training (the test is
+      sensitive) and equal rank 0's bit for bit after validate();
+    * lr = 0 (only the buffers move): eval logits of both ranks' shards vs the fixture at
+      1e-4, validation loss at 1e-5, test confusion counts equal the fixture's up to
+      pixels inside the forward error band;
+    * lr = 1e-4: each rank's eval logits equal the oracle resynced from rank 0's params and
+      buffers at 1e-4 (check_eval), the fixture within the two-step trajectory bar."""
+    from _helpers import masks_agree, rel_max
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_eval_worker, args=(r, 2, port, q, str(tmp_path), tag, lr))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=500), q.get(timeout=500)], key=lambda r: r[0])
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    f = np.load(os.path.join(golden_dir, "unet_dpe_64.npz"), allow_pickle=False)
+    assert res[1][1], "rank 1's running statistics did not drift: the test would not see a bug"
+    assert res[0][2] and res[1][2], "validate() did not give every rank rank 0's BN buffers"
+    assert res[0][3] == res[1][3] and res[0][4] == res[1][4], "ranks disagree on val metrics"
+    assert res[0][5] == res[1][5], "ranks disagree on test metrics"
+    ref_vl = f[tag + "val_logits"]
+    got = np.zeros_like(ref_vl)
+    for r in res:
+        got[r[6]] = r[7]
+    rm = np.concatenate([f[tag + "running_mean"], f[tag + "running_var"]])
+    n = rm.size // 2
+    own = res[0][8]
+    print(f"{tag}: val logits vs fixture {rel_max(got, ref_vl):.2e}; running stats "
+          f"{np.abs(own - rm).max() / np.abs(rm).max():.2e}")
+    lossw = f[tag + "val_losses"]
+    want_loss = float((lossw[:, 3] * lossw[:, 4]).sum() / lossw[:, 4].sum())
+    if lr == 0.0:
+        assert rel_max(got, ref_vl) <= 1e-4
+        np.testing.assert_allclose(own, rm, rtol=1e-4, atol=1e-5 * np.abs(rm).max())
+        assert abs(res[0][3] - want_loss) < 1e-5, (res[0][3], want_loss)
+        tol = 10 * 1e-4 * np.abs(f[tag + "test_logits"]).max()
+        near = int((np.abs(f[tag + "test_logits"]) <= tol).sum())
+        cm = res[0][5]
+        got_c = [cm["TP"], cm["FP"], cm["FN"], cm["TN"]]
+        assert sum(abs(int(a) - int(b)) for a, b in zip(got_c, f[tag + "test_counts"])) <= 2 * near, \
+            (got_c, f[tag + "test_counts"].tolist(), near)
+    else:
+        assert rel_max(got, ref_vl) <= 2e-3
+        assert abs(res[0][3] - want_loss) < 1e-3, (res[0][3], want_loss)
+    assert n == 5888

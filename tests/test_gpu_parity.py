@@ -717,3 +717,62 @@ def test_wgrad_row3_pipe_bit_identical(variant, B, H, W, dzl):
     assert torch.equal(outs[0][0], outs[1][0])
     d = (outs[0][1] - outs[1][1]).abs().max().item()
     assert torch.equal(outs[0][1], outs[1][1]), d
+
+
+def test_adamw_resume_from_state_dict_matches_uninterrupted():
+    """HipAdamW honours optimizer.load_state_dict on its flat path: two steps, save the
+    state dict, a fresh optimizer over fresh parameters loads it (and the parameters), then
+    two more steps -- bit-identical params, exp_avg, exp_avg_sq to the uninterrupted run,
+    which itself keeps m / v bit-identical to the oracle (torch's _single_tensor_adam)."""
+    import unet_hip
+    sizes = [(64, 3, 3, 3), (64,), (1000, 7)]
+    n = sum(int(np.prod(s)) for s in sizes)
+    gen = torch.Generator().manual_seed(3)
+    p0 = torch.randn(n, generator=gen) * 0.05
+    grads = [torch.randn(n, generator=gen) * 10.0 ** torch.empty(n).uniform_(-6, -1, generator=gen)
+             for _ in range(4)]
+
+    def make(flat_init):
+        flat = flat_init.clone().to(DEV)
+        gflat = torch.zeros_like(flat)
+        ps, off = [], 0
+        for s in sizes:
+            k = int(np.prod(s))
+            ps.append(torch.nn.Parameter(flat[off:off + k].view(s)))
+            off += k
+        return flat, gflat, ps
+
+    def run(opt, flat, gflat, ps, gs):
+        for g in gs:
+            gflat.copy_(g.to(DEV))
+            off = 0
+            for p in ps:
+                p.grad = gflat[off:off + p.numel()].view(p.shape)
+                off += p.numel()
+            opt.step()
+
+    fa, ga, pa = make(p0)
+    oa = unet_hip.HipAdamW(pa, lr=1e-3)
+    ref = O.AdamWState({"a": p0.clone()}, lr=1e-3)
+    run(oa, fa, ga, pa, grads[:2])
+    sd = {k: v for k, v in oa.state_dict().items()}
+    sd = torch.utils._pytree.tree_map(lambda v: v.detach().cpu().clone() if torch.is_tensor(v) else v, sd)
+    mid = fa.detach().cpu().clone()
+    run(oa, fa, ga, pa, grads[2:])
+    fb, gb, pb = make(mid)
+    ob = unet_hip.HipAdamW(pb, lr=1e-3)
+    ob.load_state_dict(sd)
+    run(ob, fb, gb, pb, grads[2:])
+    torch.cuda.synchronize()
+    assert torch.equal(fa.cpu(), fb.cpu()), "resumed params differ from the uninterrupted run"
+    for p, q in zip(pa, pb):
+        for k in ("exp_avg", "exp_avg_sq"):
+            assert torch.equal(oa.state[p][k].cpu(), ob.state[q][k].cpu()), k
+        assert float(ob.state[q]["step"]) == 4.0
+    # the moments of the uninterrupted run vs the oracle's op sequence
+    P = {"a": p0.clone()}
+    for g in grads:
+        ref.step(P, {"a": g})
+    m = torch.cat([oa.state[p]["exp_avg"].reshape(-1).cpu() for p in pa])
+    v = torch.cat([oa.state[p]["exp_avg_sq"].reshape(-1).cpu() for p in pa])
+    assert torch.equal(m, ref.m["a"]) and torch.equal(v, ref.v["a"])

@@ -95,3 +95,26 @@ def test_to_tensor_keeps_the_image_mode():
     assert np.array_equal(u8(bil, Image.fromarray(gray, "L"))[0], (gray > 128).astype(np.uint8) * 255)
     with pytest.raises(ValueError):
         u8(Image.fromarray(rgb, "RGB"), Image.fromarray(gray, "L"))
+
+
+def test_hip_adamw_rebuilds_flat_moments_from_loaded_state():
+    """HipAdamW keeps self.state as the source of truth: after load_state_dict the flat
+    moment arenas are rebuilt from the loaded exp_avg / exp_avg_sq (host-side logic; the
+    device update itself is covered by the GPU tests)."""
+    import unet_hip
+    flat = torch.arange(10, dtype=torch.float32)
+    ps = [torch.nn.Parameter(flat[0:4].view(2, 2)), torch.nn.Parameter(flat[4:10])]
+    opt = unet_hip.HipAdamW(ps, lr=1e-3)
+    sd = {"state": {0: {"step": torch.tensor(3.0), "exp_avg": torch.full((2, 2), 0.5),
+                        "exp_avg_sq": torch.full((2, 2), 0.25)},
+                    1: {"step": torch.tensor(3.0), "exp_avg": torch.arange(6.0),
+                        "exp_avg_sq": torch.arange(6.0) * 2}},
+          "param_groups": opt.state_dict()["param_groups"]}
+    opt.load_state_dict(sd)
+    m, v = opt._rebuild_flat(ps, flat)
+    assert torch.equal(m, torch.cat([torch.full((4,), 0.5), torch.arange(6.0)]))
+    assert torch.equal(v, torch.cat([torch.full((4,), 0.25), torch.arange(6.0) * 2]))
+    assert opt._views_of(ps, m, v)
+    assert opt.state[ps[1]]["exp_avg"].data_ptr() == m.data_ptr() + 4 * 4
+    opt.load_state_dict(sd)  # fresh tensors again: no longer views of the arenas
+    assert not opt._views_of(ps, m, v)

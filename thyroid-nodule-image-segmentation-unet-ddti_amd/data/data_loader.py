@@ -112,22 +112,52 @@ def dp_collate(collate=None):
     return fn
 
 
-class DecodeU8:
-    """Transform that only decodes: (PIL image, PIL mask) -> two (H, W) uint8 arrays.
+class U8Plane(np.ndarray):
+    """A decoded (H, W) uint8 plane that remembers which filter Pillow's resize would use
+    for its source image: ``"nearest"`` for palette ("P") and bilevel ("1") images, for
+    which Image.resize replaces BILINEAR by NEAREST, else ``"bilinear"``."""
 
-    The device pipeline is single-band: an 8-bit grayscale ("L") or bilevel ("1") file
-    gives the same tensor as the reference's TF.to_tensor; any other mode (e.g. RGB) would
-    give a multi-band tensor there, which the 1-channel networks reject, so it is refused
-    here too rather than silently converted."""
+    resample = "bilinear"
+
+    def __array_finalize__(self, obj):
+        self.resample = getattr(obj, "resample", "bilinear")
+
+    def __reduce__(self):  # DataLoader workers pickle samples: keep the tag
+        fn, args, state = super().__reduce__()
+        return fn, args, (state, self.resample)
+
+    def __setstate__(self, st):
+        state, self.resample = st
+        super().__setstate__(state)
+
+    @staticmethod
+    def of(a, resample):
+        p = np.ascontiguousarray(a, dtype=np.uint8).view(U8Plane)
+        p.resample = resample
+        return p
+
+
+class DecodeU8:
+    """Transform that only decodes: (PIL image, PIL mask) -> two (H, W) uint8 planes.
+
+    The device pipeline is single-band 8-bit, as TF.to_tensor sees it: "L" gives the
+    pixel values; "P" (palette) the raw palette indices (to_tensor divides the indices by
+    255); "1" 0 / 255 (to_tensor's {0, 1} after its x255 and /255).  For "P" and "1" the
+    planes are tagged ``resample="nearest"``: Pillow's Image.resize (which TF.resize calls)
+    resizes those modes with NEAREST whatever filter is asked for.  Multi-band or
+    non-8-bit modes (RGB, I;16, F, ...) would give a different tensor there and are
+    refused rather than silently converted."""
 
     @staticmethod
     def _plane(pic):
         if pic.mode == "L":
-            return np.asarray(pic, dtype=np.uint8)
-        if pic.mode == "1":  # TF.to_tensor: {0, 1}; == "L" conversion (0/255) then / 255
-            return np.asarray(pic.convert("L"), dtype=np.uint8)
+            return U8Plane.of(np.asarray(pic), "bilinear")
+        if pic.mode == "P":
+            return U8Plane.of(np.asarray(pic), "nearest")
+        if pic.mode == "1":
+            return U8Plane.of(np.asarray(pic.convert("L")), "nearest")
         raise ValueError(f"image mode {pic.mode!r}: the device pipeline takes single-band 8-bit "
-                         f"images (TF.to_tensor would give a {len(pic.getbands())}-band tensor)")
+                         f"images ('L', 'P' or '1'; this one has bands {pic.getbands()})")
 
     def __call__(self, img, mask):
         return self._plane(img), self._plane(mask)

@@ -10,6 +10,12 @@ fp32 batch directly, bit-identical to Pillow (tests/test_gpu_data.py).
     pipe = GpuResizeToTensor((512, 512), device="cuda")
     x, t = pipe(images, masks)           # lists of HxW uint8 arrays / tensors (any sizes)
                                          # -> (N, 1, 512, 512) fp32 each, on the device
+
+Palette ("P") and bilevel ("1") images: Pillow's Image.resize switches to NEAREST for
+those modes whatever filter is asked for.  Planes tagged ``resample="nearest"``
+(data.data_loader.DecodeU8 does that) run the same kernel with a one-tap plan: source
+index = int(x0), x0 = s/2 then += s per output pixel (s = in/out, Pillow's accumulated
+double coordinate of ImagingScaleAffine), coefficient 1.0 in 22-bit fixed point.
 """
 import ctypes
 
@@ -33,6 +39,19 @@ def resize_plan(in_size, out_size):
     return k, b
 
 
+def nearest_plan(in_size, out_size):
+    """One-tap plan reproducing Pillow's NEAREST scale (coefficient 1 << 22 at the nearest
+    source index)."""
+    k = np.full((out_size, 1), 1 << 22, np.int32)
+    b = np.ones((out_size, 2), np.int32)
+    step = float(in_size) / out_size
+    xo = step * 0.5
+    for x in range(out_size):
+        b[x, 0] = min(int(xo), in_size - 1)
+        xo += step
+    return k, b
+
+
 class GpuResizeToTensor:
     """Batched Resize((H, W)) + ToTensor of (image, mask) pairs on the device."""
 
@@ -42,16 +61,17 @@ class GpuResizeToTensor:
         self.rt = UNetRuntime.get(self.device)
         self._plans = {}
 
-    def _plan(self, n_in, n_out):
-        key = (n_in, n_out)
+    def _plan(self, n_in, n_out, nearest=False):
+        key = (n_in, n_out, nearest)
         if key not in self._plans:
-            k, b = resize_plan(n_in, n_out)
+            k, b = nearest_plan(n_in, n_out) if nearest else resize_plan(n_in, n_out)
             self._plans[key] = (torch.from_numpy(k).to(self.device),
                                 torch.from_numpy(b).to(self.device), k.shape[1])
         return self._plans[key]
 
     def resize(self, img, out=None):
         """One HxW uint8 image -> (oh, ow) fp32 in [0, 1] on the device."""
+        nearest = getattr(img, "resample", "bilinear") == "nearest"
         if isinstance(img, np.ndarray):  # PIL-backed arrays are read-only views
             img = np.require(img, requirements=["C", "W"])
         t = torch.as_tensor(img)
@@ -61,8 +81,8 @@ class GpuResizeToTensor:
         h, w = t.shape
         if out is None:
             out = torch.empty((self.oh, self.ow), dtype=torch.float32, device=self.device)
-        kh, bh, ksh = self._plan(w, self.ow)
-        kv, bv, ksv = self._plan(h, self.oh)
+        kh, bh, ksh = self._plan(w, self.ow, nearest)
+        kv, bv, ksv = self._plan(h, self.oh, nearest)
         _lib.check(self.rt.lib.unet_resize_u8(
             self.rt.ctx, _lib.ptr(t), h, w, _lib.ptr(out), self.oh, self.ow, _lib.ptr(kh),
             _lib.ptr(bh), ksh, _lib.ptr(kv), _lib.ptr(bv), ksv, 255.0,

@@ -18,7 +18,18 @@ BN), and the two exchanges DataParallel implies are made explicit:
 A caller that takes a per-rank LOCAL loss instead (plain ``seg_losses`` without a group)
 passes ``average=True``: the sum is then scaled by 1/world inside the AdamW pass
 (``grad_scale``), which equals the gathered-batch gradient for equal shards and
-shard-decomposable losses (BCE-mean, per-sample Dice), not for FocalTversky.
+shard-decomposable losses (BCE-mean, per-sample Dice), not for FocalTversky.  With
+``average=False`` (the default) ``reduce_gradients`` refuses a step whose loss did not
+come from ``losses`` (or ``empty_step``): summing gradients of per-rank local losses would
+silently train with world-times-larger gradients.
+
+BatchNorm buffers: DataParallel re-broadcasts replica 0's parameters AND buffers before
+every forward (torch nn/parallel/replicate.py), so every shard is evaluated with GPU 0's
+running statistics and only replica 0's running-stat updates survive a training step.
+Train-mode forwards never read the running statistics, so here they may drift per rank
+during training; ``sync_buffers`` broadcasts rank 0's running-stat and counter arenas
+(2 x 5,888 floats + 18 int64 for models/model.py) and the Trainer calls it before every
+validate / test pass (utils/trainer.py:130,210 -> eval forwards at :139,216).
 
 Overlap: the native backward records one event per gradient bucket (decoder first,
 unet_bucket_range); ``reduce_gradients`` enqueues, on a side stream, "wait for bucket b"
@@ -98,6 +109,47 @@ class DistributedUNet:
         rt = st.rt
         self.reducer = BucketReducer(rt.buckets, group, wait_fn=rt.stream_wait_bucket)
         self.optimizer = optimizer
+        self._gathered_loss = False  # set by losses() / empty_step(), consumed by reduce_gradients
+
+    def _src(self):
+        return 0 if self.group is None else dist.get_global_rank(self.group, 0)
+
+    def sync_buffers(self):
+        """Every rank takes rank 0's BN running statistics and num_batches_tracked (the
+        buffers nn.DataParallel evaluates every shard with).  One broadcast per arena."""
+        st = self.model.flatten_()
+        dist.broadcast(st.bn_arena, src=self._src(), group=self.group)
+        dist.broadcast(st.nbt_arena, src=self._src(), group=self.group)
+
+    def gather_batch(self, images, masks, device):
+        """The gathered global batch (DataParallel's input before its scatter) on every
+        rank, plus this rank's (offset, count) in it.  images / masks: this rank's shard or
+        None for an empty shard.  Used by mixup, which the reference applies to the whole
+        batch before DataParallel scatters it (utils/trainer.py:62-78)."""
+        ws = dist.get_world_size(self.group)
+        n = 0 if images is None else int(images.shape[0])
+        shape = [0, 0, 0, 0] if images is None else list(images.shape)
+        mshape = [0, 0, 0, 0] if masks is None else list(masks.shape)
+        meta = torch.tensor([n] + shape[1:] + mshape[1:], dtype=torch.int64, device=device)
+        metas = [torch.zeros_like(meta) for _ in range(ws)]
+        dist.all_gather(metas, meta, group=self.group)
+        metas = [m.tolist() for m in metas]
+        counts = [m[0] for m in metas]
+        full = next((m for m in metas if m[0] > 0), None)
+        if full is None:
+            return None, None, 0, 0
+        ishape, mshp = full[1:4], full[4:7]
+        cap = max(counts)
+        out = []
+        for t, shp in ((images, ishape), (masks, mshp)):
+            pad = torch.zeros([cap] + shp, dtype=torch.float32, device=device)
+            if n:
+                pad[:n].copy_(t)
+            parts = [torch.empty_like(pad) for _ in range(ws)]
+            dist.all_gather(parts, pad, group=self.group)
+            out.append(torch.cat([p[:c] for p, c in zip(parts, counts)]))
+        rank = dist.get_rank(self.group)
+        return out[0], out[1], sum(counts[:rank]), n
 
     def __call__(self, x):
         return self.model(x)
@@ -105,6 +157,7 @@ class DistributedUNet:
     def losses(self, logits, targets, alpha=0.4, beta=0.6, gamma=2.0):
         from .functional import seg_losses
         grp = self.group if self.group is not None else dist.group.WORLD
+        self._gathered_loss = True
         return seg_losses(logits, targets, alpha, beta, gamma, group=grp)
 
     def empty_step(self, extra_scalar_reduces=0):
@@ -126,6 +179,7 @@ class DistributedUNet:
             st.grad_arena.zero_()
         for (p, _, _), g in zip(st.params, st.grad_views(st.grad_arena)):
             p.grad = g
+        self._gathered_loss = True
         return self.reduce_gradients(wait_native=False)
 
     def empty_losses(self, extra_scalar_reduces=0):
@@ -140,6 +194,12 @@ class DistributedUNet:
     def reduce_gradients(self, wait_native=True):
         """Sum (or, with average=True, average) the flat gradient arena over the ranks.
         Returns the scale the optimizer applies to the summed gradients."""
+        if not self.average and not self._gathered_loss:
+            raise RuntimeError("reduce_gradients() SUMS the ranks' gradients, which is the "
+                               "gathered-batch gradient only when the loss came from "
+                               "DistributedUNet.losses() this step; for per-rank local losses "
+                               "construct DistributedUNet(..., average=True)")
+        self._gathered_loss = False
         st = self.model._state
         p0 = st.params[0][0]
         arena = st.grad_arena

@@ -7,6 +7,12 @@ decoupled weight decay.  When every parameter is a view into one flat arena (the
 laid out the same way, the whole step is ONE kernel over 31M floats; otherwise it runs
 one native launch per parameter tensor.  ``grad_scale`` (e.g. 1/world_size after an
 RCCL sum) is folded into the same pass.
+
+``self.state[p]["exp_avg"] / ["exp_avg_sq"]`` stay the source of truth, as in any
+``torch.optim.Optimizer``: on the flat path they are views of the two moment arenas, and
+when they are not (``load_state_dict`` replaced them, or a parameter had no state yet) the
+arenas are rebuilt from them before the step, so a resumed optimizer continues from the
+loaded moments.
 """
 import torch
 
@@ -41,6 +47,35 @@ class HipAdamW(torch.optim.Optimizer):
         self.grad_scale = 1.0
         self._flat = {}
 
+    def _views_of(self, params, m, v):
+        """True if every param's exp_avg / exp_avg_sq is the slice of arenas m / v."""
+        off = 0
+        for p in params:
+            s = self.state.get(p, {})
+            ea, eq = s.get("exp_avg"), s.get("exp_avg_sq")
+            if ea is None or eq is None or ea.data_ptr() != m.data_ptr() + 4 * off \
+                    or eq.data_ptr() != v.data_ptr() + 4 * off:
+                return False
+            off += p.numel()
+        return True
+
+    def _rebuild_flat(self, params, fp):
+        """Fresh moment arenas holding each param's current state (zeros where none), with
+        the state re-pointed at their slices."""
+        m = torch.zeros_like(fp)
+        v = torch.zeros_like(fp)
+        off = 0
+        for p in params:
+            s = self.state[p]
+            n = p.numel()
+            for k, arena in (("exp_avg", m), ("exp_avg_sq", v)):
+                view = arena[off:off + n].view_as(p)
+                if k in s:
+                    view.copy_(s[k].reshape(p.shape))
+                s[k] = view
+            off += n
+        return m, v
+
     @torch.no_grad()
     def step(self, closure=None):
         loss = None
@@ -63,18 +98,10 @@ class HipAdamW(torch.optim.Optimizer):
             fg = _flat_base([p.grad for p in params]) if fp is not None else None
             if fp is not None and fg is not None:
                 key = (gi, fp.data_ptr(), fp.numel())
-                if key not in self._flat:
-                    m = torch.zeros_like(fp)
-                    v = torch.zeros_like(fp)
+                m, v = self._flat.get(key, (None, None))
+                if m is None or not self._views_of(params, m, v):
+                    m, v = self._rebuild_flat(params, fp)
                     self._flat = {key: (m, v)}
-                    off = 0
-                    for p in params:
-                        s = self.state[p]
-                        n = p.numel()
-                        s["exp_avg"] = m[off:off + n].view_as(p)
-                        s["exp_avg_sq"] = v[off:off + n].view_as(p)
-                        off += n
-                m, v = self._flat[key]
                 rt.adamw(fp, fg, m, v, step, lr, b1, b2, eps, wd, self.grad_scale)
             else:
                 for p in params:

@@ -89,6 +89,10 @@ class Trainer:
 
     # -------------------------------------------------------------- helpers
     def _losses(self, logits, masks):
+        """-> (loss to differentiate, [bce, dice, focal], boundary, reported total).  Under
+        data parallelism the first is this rank's share of the gathered batch's loss (its
+        gradient summed over the ranks is DataParallel's), the others are the gathered
+        batch's values (same on every rank)."""
         c = self.config
         if self.ddp is not None:  # the gathered batch's losses (nn.DataParallel semantics)
             l = self.ddp.losses(logits, masks, *self.focal_abg)
@@ -97,6 +101,7 @@ class Trainer:
         w = torch.tensor([c.bce_ratio, c.dice_ratio, c.focal_ratio], device=logits.device)
         loss = (w * l).sum()
         lb = torch.zeros((), device=logits.device)
+        total = loss
         if c.boundary_ratio != 0:
             lb = self.criterion_boundary(logits, masks)  # mean over this rank's samples
             if self.ddp is not None:
@@ -108,9 +113,11 @@ class Trainer:
                 loss = loss + c.boundary_ratio * lb
                 lb = lb.detach().clone()
                 dist.all_reduce(lb)
+                total = total.detach() + c.boundary_ratio * lb
             else:
                 loss = loss + c.boundary_ratio * lb
-        return loss, l, lb
+                total = loss
+        return loss, l, lb, total
 
     def _reduce_scalars(self, sums, n_seen):
         """Epoch means weighted like the reference's AverageMeter.update(loss, batch size)
@@ -151,12 +158,29 @@ class Trainer:
             bsamp.set_epoch(epoch)
         nb_extra = 2 if self.config.boundary_ratio != 0 else 0
         for batch in tqdm(loader, desc=desc, leave=True):
-            # utils/trainer.py:62-64: the mixup draws come first, on every rank alike (ranks
-            # share the python / numpy seeds, set_seed(42)), so they stay in step even when a
-            # rank's shard is empty.  Under data parallelism a shard mixes with itself, where
-            # the reference's DataParallel mixes the whole batch before scattering it.
+            # utils/trainer.py:62-78: the mixup draws (random, numpy beta, then a CPU
+            # torch.randperm of the batch size) come first and are consumed alike on every
+            # rank (ranks share the seeds, set_seed(42)), even when a rank's shard is empty.
+            # Under data parallelism the GATHERED batch is mixed, as the reference mixes the
+            # whole batch before DataParallel scatters it, and each rank keeps its slice.
             mix = train and random.random() < self.config.mixup_prob and self.config.use_mixup
             lam = np.random.beta(self.config.mixup_alpha, self.config.mixup_alpha) if mix else None
+            if batch is not None:
+                images, masks = batch
+                images = images.to(self.device, non_blocking=True).float()
+                masks = masks.to(self.device, non_blocking=True).float()
+            if mix and self.ddp is not None:
+                gi, gm, off, n = self.ddp.gather_batch(None if batch is None else images,
+                                                       None if batch is None else masks, self.device)
+                perm = torch.randperm(gi.size(0)).to(self.device)
+                if batch is not None:
+                    sl = slice(off, off + n)
+                    images = lam * gi[sl] + (1.0 - lam) * gi[perm[sl]]
+                    masks = lam * gm[sl] + (1.0 - lam) * gm[perm[sl]]
+            elif mix:
+                perm = torch.randperm(images.size(0)).to(self.device)
+                images = lam * images + (1.0 - lam) * images[perm]
+                masks = lam * masks + (1.0 - lam) * masks[perm]
             if batch is None:  # empty DataParallel shard: join the step's collectives only
                 if train:
                     self.optimizer.zero_grad(set_to_none=True)
@@ -165,17 +189,10 @@ class Trainer:
                 else:
                     self.ddp.empty_losses(nb_extra)
                 continue
-            images, masks = batch
-            images = images.to(self.device, non_blocking=True).float()
-            masks = masks.to(self.device, non_blocking=True).float()
-            if mix:
-                perm = torch.randperm(images.size(0), device=self.device)
-                images = lam * images + (1.0 - lam) * images[perm]
-                masks = lam * masks + (1.0 - lam) * masks[perm]
             if train:
                 self.optimizer.zero_grad(set_to_none=True)
                 logits = self.model(images)
-                loss, l, lb = self._losses(logits, masks)
+                loss, l, lb, total = self._losses(logits, masks)
                 loss.backward()
                 if self.ddp is not None:
                     self.ddp.reduce_gradients()
@@ -183,9 +200,9 @@ class Trainer:
             else:
                 with torch.no_grad():
                     logits = self.model(images)
-                    loss, l, lb = self._losses(logits, masks)
+                    loss, l, lb, total = self._losses(logits, masks)
             bs = masks.size(0)
-            sums += torch.stack([l[0], l[1], l[2], lb, loss]).detach().double() * bs
+            sums += torch.stack([l[0], l[1], l[2], lb, total]).detach().double() * bs
             n_seen += bs
             self.rt.mask_counts(logits.detach(), masks, counts)
         totals = self._reduce_scalars(sums, n_seen).tolist()
@@ -203,6 +220,8 @@ class Trainer:
     @torch.no_grad()
     def validate(self, epoch):
         self.model.eval()
+        if self.ddp is not None:  # every shard evaluated with replica 0's BN buffers (DataParallel)
+            self.ddp.sync_buffers()
         meters, counts = self._run_epoch(self.val_loader, epoch, False)
         iou = self._log_epoch("Validate", epoch, meters, counts)
         return meters[4].avg, iou
@@ -236,10 +255,15 @@ class Trainer:
         matplotlib and scikit-image are importable."""
         self.logger.info("------------------Starting Testing Model------------------")
         self.model.eval()
+        if self.ddp is not None:  # every shard evaluated with replica 0's BN buffers (DataParallel)
+            self.ddp.sync_buffers()
         counts = torch.zeros(6, dtype=torch.int64, device=self.device)
         total = 0
         keep = []
-        for images, masks in tqdm(self.test_loader, desc="Testing Model", leave=True):
+        for batch in tqdm(self.test_loader, desc="Testing Model", leave=True):
+            if batch is None:  # empty DataParallel shard: nothing to count on this rank
+                continue
+            images, masks = batch
             images = images.to(self.device).float()
             masks = masks.to(self.device).float()
             logits = self.model(images)
@@ -247,6 +271,10 @@ class Trainer:
             self.rt.mask_counts(logits, masks, counts, mask)
             total += images.size(0)
             keep.append((images.cpu(), masks.cpu(), mask.cpu()))
+        if _distributed():
+            nt = torch.tensor([total], dtype=torch.int64, device=self.device)
+            dist.all_reduce(nt)
+            total = int(nt.item())
         m = global_metrics_from_counts(self._reduce_counts(counts).tolist())
         msg = (f"Test Metrics  —  Total Images: {total}\n"
                f"  TP={m['TP']}, FP={m['FP']}, FN={m['FN']}, TN={m['TN']}\n"
@@ -254,7 +282,8 @@ class Trainer:
                f"Recall={m['Recall']:.4f}, F1={m['F1']:.4f}, IoU={m['IoU']:.4f}")
         print(msg)
         self.logger.info(msg)
-        self._plot_contours(keep)
+        if keep:
+            self._plot_contours(keep)
         return m
 
     def _plot_contours(self, keep):

@@ -45,6 +45,15 @@ Fixtures (all float64 statistics computed from fp32 results):
                     logits, global TP/FP/FN): eq_* B=4 in 2 shards of 2, ratios 1/0/1/0;
                     uneq_* B=3 in shards of 2 and 1 (DataParallel's chunked scatter), ratios
                     1/1/1/0.  Losses and grad norm/sum/samples.
+  unet_dpe_64.npz   nn.DataParallel training THEN evaluation (utils/trainer.py:28-30, 47-119,
+                    121-172, 206-250): Trainer.train_one_epoch over SyntheticSegmentation(5, 64,
+                    seed=4) at global batch 4 (shards 2+2, then 1 sample on replica 0 only),
+                    the CLI default loss mix 1/0/1/0 (starting from running statistics warmed by 30
+                    train-mode passes, stored as init_*), then validate (seed 5) and test (seed 6)
+                    in eval mode, where DataParallel re-replicates module 0 so every shard
+                    uses replica 0's running statistics.  lr0_: lr = 0 (parameters fixed, only
+                    the BN buffers move: a strict pin of the buffer semantics); lr4_: lr =
+                    1e-4.  Running stats, val / test logits, per-batch val losses, counts.
 """
 import os
 import sys
@@ -261,6 +270,61 @@ def case_dp_focal_64():
     np.savez_compressed(os.path.join(OUT, "unet_dpf_64.npz"), **out)
 
 
+def _synthetic(n, seed):
+    sys.path.insert(0, os.path.join(REPO, "thyroid-nodule-image-segmentation-unet-ddti_amd"))
+    from data.data_loader import SyntheticSegmentation
+    ds = SyntheticSegmentation(n, 64, seed=seed)
+    return (torch.stack([ds[i][0] for i in range(n)]), torch.stack([ds[i][1] for i in range(n)]))
+
+
+def case_dp_eval_64():
+    out = {}
+    xtr, ttr = _synthetic(5, 4)
+    xva, tva = _synthetic(5, 5)
+    xte, tte = _synthetic(5, 6)
+    bce, dice, focal = torch.nn.BCEWithLogitsLoss(), RefDice(), RefFocal()
+    for tag, lr in (("lr0_", 0.0), ("lr4_", 1e-4)):
+        m = build()
+        m.train()
+        with torch.no_grad():  # warm the running statistics (fresh ones give constant eval
+            for _ in range(30):  # logits); the test loads these as the starting buffers
+                m(xtr)
+        bufs = dict(m.named_buffers())
+        out[tag + "init_running_mean"] = np.concatenate([bufs[f"{n}.running_mean"].numpy() for n in O.BN_LAYERS])
+        out[tag + "init_running_var"] = np.concatenate([bufs[f"{n}.running_var"].numpy() for n in O.BN_LAYERS])
+        out[tag + "init_nbt"] = np.array([bufs[f"{n}.num_batches_tracked"].item() for n in O.BN_LAYERS])
+        opt = torch.optim.AdamW(m.parameters(), lr=lr)
+        for sl in (slice(0, 4), slice(4, 5)):  # Trainer.train_one_epoch, DataParallel step
+            opt.zero_grad()
+            logits = dp_forward(m, xtr[sl], 2)
+            loss = 1.0 * bce(logits, ttr[sl]) + 0.0 * dice(logits, ttr[sl]) + 1.0 * focal(logits, ttr[sl])
+            loss.backward()
+            opt.step()
+        bufs = dict(m.named_buffers())
+        out[tag + "running_mean"] = np.concatenate([bufs[f"{n}.running_mean"].numpy() for n in O.BN_LAYERS])
+        out[tag + "running_var"] = np.concatenate([bufs[f"{n}.running_var"].numpy() for n in O.BN_LAYERS])
+        out[tag + "params_samp"] = param_samples(m)
+        m.eval()
+        with torch.no_grad():
+            vl = m(xva)  # == the gathered per-shard eval forwards (eval BN is per sample)
+            tl = m(xte)
+            vloss = []
+            for sl in (slice(0, 4), slice(4, 5)):  # Trainer.validate's per-batch losses
+                lb, ld, lf = bce(vl[sl], tva[sl]), dice(vl[sl], tva[sl]), focal(vl[sl], tva[sl])
+                vloss.append([lb.item(), ld.item(), lf.item(), (lb + 0.0 * ld + lf).item(), sl.stop - sl.start])
+        out[tag + "val_logits"] = vl.numpy()
+        out[tag + "val_losses"] = np.array(vloss)
+        out[tag + "test_logits"] = tl.numpy()
+        for k, lg, tg in (("val_", vl, tva), ("test_", tl, tte)):
+            pr = (torch.sigmoid(lg) > 0.5).numpy().reshape(-1)
+            # validate: targets cast to int (utils/utils.py:240-251); test: astype(uint8)
+            # (utils/trainer.py:220,236-242); both {0, 1} here
+            tgi = tg.numpy().astype(np.uint8).reshape(-1)
+            out[tag + k + "counts"] = np.array([(pr & (tgi == 1)).sum(), (pr & (tgi == 0)).sum(),
+                                                (~pr & (tgi == 1)).sum(), (~pr & (tgi == 0)).sum()])
+    np.savez_compressed(os.path.join(OUT, "unet_dpe_64.npz"), **out)
+
+
 def case_neg_32():
     m = build(seed=5, gamma_lo=-1.0, gamma_hi=1.0)
     m.train()
@@ -427,5 +491,6 @@ if __name__ == "__main__":
     case_focal_64()
     case_dp_focal_64()
     case_mod_narrow_64()
+    case_dp_eval_64()
     for f in sorted(os.listdir(OUT)):
         print(f, os.path.getsize(os.path.join(OUT, f)))
