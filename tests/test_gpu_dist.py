@@ -285,8 +285,11 @@ def _eval_worker(rank, world, port, q, tmp, tag, lr):
         with torch.no_grad():
             lg = tr.model(x.to("cuda:0")).cpu().numpy()
         check_eval(tr.model, O.forward, x, t)
+        nb = dict(tr.model.named_buffers())
+        rs = np.concatenate([nb[f"{n}.running_mean"].cpu().numpy() for n in O.BN_LAYERS] +
+                            [nb[f"{n}.running_var"].cpu().numpy() for n in O.BN_LAYERS])
         q.put((rank, drifted, synced, val_loss, val_iou, metrics, mine, lg,
-               after.cpu().numpy() if rank == 0 else None,
+               rs if rank == 0 else None,
                st.param_arena.detach().cpu().numpy() if rank == 0 else None))
     finally:
         dist.destroy_process_group()
@@ -346,6 +349,32 @@ def test_trainer_dp2_eval_uses_replica0_buffers(tmp_path, golden_dir, tag, lr):
         assert sum(abs(int(a) - int(b)) for a, b in zip(got_c, f[tag + "test_counts"])) <= 2 * near, \
             (got_c, f[tag + "test_counts"].tolist(), near)
     else:
-        assert rel_max(got, ref_vl) <= 2e-3
+        # two Adam steps move rounding-noise gradients' elements by up to lr each, in any
+        # fp32 evaluation: the bar is 2x the fp32 oracle's own spread from the fixture over
+        # two noise realisations (x and x * (1 + 1e-7)) of the same DataParallel epoch
+        from data.data_loader import SyntheticSegmentation
+        from oracle import unet_ref_cpu as O
+
+        def stack(seed):
+            ds = SyntheticSegmentation(5, 64, seed=seed)
+            return (torch.stack([ds[i][0] for i in range(5)]), torch.stack([ds[i][1] for i in range(5)]))
+        (xtr, ttr), (xva, _) = stack(4), stack(5)
+        spread = 0.0
+        for xs in (1.0, 1 + 1e-7):
+            P = O.make_params(42)
+            B = O.init_buffers()
+            off = 0
+            for name in O.BN_LAYERS:
+                c = B[f"{name}.running_mean"].numel()
+                B[f"{name}.running_mean"] = torch.from_numpy(f[tag + "init_running_mean"][off:off + c].copy())
+                B[f"{name}.running_var"] = torch.from_numpy(f[tag + "init_running_var"][off:off + c].copy())
+                off += c
+            opt = O.AdamWState(P, lr=lr)
+            for sl in (slice(0, 4), slice(4, 5)):
+                O.train_step(P, B, opt, xtr[sl] * xs, ttr[sl], w_bce=1.0, w_dice=0.0, w_focal=1.0, shards=2)
+            with torch.no_grad():
+                spread = max(spread, rel_max(O.forward(xva, P, B, False).numpy(), ref_vl))
+        print(f"lr4_: fp32 oracle spread {spread:.2e}")
+        assert rel_max(got, ref_vl) <= max(2 * spread, 1e-4)
         assert abs(res[0][3] - want_loss) < 1e-3, (res[0][3], want_loss)
     assert n == 5888

@@ -276,3 +276,35 @@ def test_oracle_mod_narrow_widths(golden_dir):
     assert abs(r["loss"].item() - float(f["r16_loss"])) < 1e-6
     _check_grads(_grad_stats(r["grads"], MO.res_param_spec(1, 1, 16, 3)), f["r16_grad_norm"],
                  f["r16_grad_sum"], f["r16_grad_samp"], rtol=1e-4)
+
+
+@pytest.mark.parametrize("tag,lr", [("lr0_", 0.0), ("lr4_", 1e-4)])
+def test_oracle_dataparallel_train_then_eval(golden_dir, tag, lr):
+    """The oracle's nn.DataParallel epoch (two steps: shards 2 + 2, then replica 0 alone;
+    only replica 0's running statistics kept) and its eval forward reproduce the
+    reference-generated unet_dpe_64.npz: running statistics and val / test logits."""
+    from data.data_loader import SyntheticSegmentation
+    f = np.load(os.path.join(golden_dir, "unet_dpe_64.npz"), allow_pickle=False)
+
+    def stack(seed):
+        ds = SyntheticSegmentation(5, 64, seed=seed)
+        return (torch.stack([ds[i][0] for i in range(5)]), torch.stack([ds[i][1] for i in range(5)]))
+    (xtr, ttr), (xva, _), (xte, _) = stack(4), stack(5), stack(6)
+    P = O.make_params(42)
+    B = O.init_buffers()
+    off = 0
+    for name in O.BN_LAYERS:
+        c = B[f"{name}.running_mean"].numel()
+        B[f"{name}.running_mean"] = torch.from_numpy(f[tag + "init_running_mean"][off:off + c].copy())
+        B[f"{name}.running_var"] = torch.from_numpy(f[tag + "init_running_var"][off:off + c].copy())
+        off += c
+    opt = O.AdamWState(P, lr=lr)
+    for sl in (slice(0, 4), slice(4, 5)):
+        O.train_step(P, B, opt, xtr[sl], ttr[sl], w_bce=1.0, w_dice=0.0, w_focal=1.0, shards=2)
+    rm = np.concatenate([B[f"{n}.running_mean"].numpy() for n in O.BN_LAYERS])
+    rv = np.concatenate([B[f"{n}.running_var"].numpy() for n in O.BN_LAYERS])
+    np.testing.assert_array_equal(rm, f[tag + "running_mean"])
+    np.testing.assert_array_equal(rv, f[tag + "running_var"])
+    with torch.no_grad():
+        np.testing.assert_array_equal(O.forward(xva, P, B, False).numpy(), f[tag + "val_logits"])
+        np.testing.assert_array_equal(O.forward(xte, P, B, False).numpy(), f[tag + "test_logits"])

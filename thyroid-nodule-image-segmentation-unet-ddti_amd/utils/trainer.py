@@ -125,7 +125,8 @@ class Trainer:
         v = torch.cat([sums, torch.tensor([float(n_seen)], dtype=sums.dtype, device=sums.device)])
         if _distributed():
             dist.all_reduce(v)
-        return v[:-1] / max(float(v[-1]), 1.0)
+        n = max(float(v[-1]), 1.0)
+        return v[:-1] / n, n
 
     def _reduce_counts(self, c):
         if _distributed():
@@ -205,9 +206,9 @@ class Trainer:
             sums += torch.stack([l[0], l[1], l[2], lb, total]).detach().double() * bs
             n_seen += bs
             self.rt.mask_counts(logits.detach(), masks, counts)
-        totals = self._reduce_scalars(sums, n_seen).tolist()
-        for m, v in zip(meters, totals):
-            m.update(v, n_seen)
+        totals, n_glob = self._reduce_scalars(sums, n_seen)
+        for m, v in zip(meters, totals.tolist()):
+            m.update(v, n_glob)  # the global count: identical meters on every rank
         return meters, self._reduce_counts(counts)
 
     # -------------------------------------------------------------- reference API
