@@ -115,6 +115,8 @@ struct Options {
     int rg16 = 1;              // bf16 row GEMMs on the LDS-DMA kernel (0: register-staged)
     int rg16_tile = -1;        // its tile (-1 = per GEMM, rg16_tile())
     int rg16_ra = 0;           // per-GEMM choice on the read-ahead tiles 12 / 13
+    int rg16_m16 = 0;          // per-GEMM choice on the 16x16x32-MFMA tiles: 1 = 14 / 15,
+                               // 2 = with s_setprio around the MFMAs (16 / 17)
     int wg16 = 1;              // bf16 3x3 wgrad on the LDS-DMA transposed-read kernel
     int wg16_tile = 2;         // its tile (2 = 256x256)
     int wg16t = 1;             // bf16 ConvT wgrad on the same kernel
@@ -141,6 +143,7 @@ const OptionDesc OPTION_TABLE[] = {
     {"tile16_n128", &Options::tile16_n128},     {"tile16_n128_dgrad", &Options::tile16_n128_dgrad},
     {"tile16_n64", &Options::tile16_n64},       {"rg16", &Options::rg16},
     {"rg16_tile", &Options::rg16_tile},         {"rg16_ra", &Options::rg16_ra},         {"wg16", &Options::wg16},
+    {"rg16_m16", &Options::rg16_m16},
     {"wg16_tile", &Options::wg16_tile},         {"wg16t", &Options::wg16t},
     {"xcd16", &Options::xcd16},                 {"xcd_remap", &Options::xcd_remap},
     {"wgrad_stream", &Options::wgrad_stream},   {"dz_in_loaders", &Options::dz_in_loaders},
@@ -597,7 +600,11 @@ int rg16_tile(const unet_ctx* c, const RowGemmArgs& g) {
     };
     if (c->opt.rg16_tile >= 0) return fits(c->opt.rg16_tile) ? c->opt.rg16_tile : 0;
     // option rg16_ra: the same shapes with read-ahead LDS fragments (tiles 12 / 13)
-    const int t0 = c->opt.rg16_ra ? 13 : 0, t4 = c->opt.rg16_ra ? 12 : 4;
+    int t0 = c->opt.rg16_ra ? 13 : 0, t4 = c->opt.rg16_ra ? 12 : 4;
+    if (c->opt.rg16_m16) {  // option rg16_m16: the 16x16x32-MFMA tiles of the same shapes
+        t0 = c->opt.rg16_m16 == 2 ? 17 : 15;
+        t4 = c->opt.rg16_m16 == 2 ? 16 : 14;
+    }
     if (!fits(4)) return t0;
     const int64_t blocks = (g.M + 255) / 256 * (g.N / 256);
     if (blocks < 256) return t0;
@@ -940,7 +947,7 @@ std::string tlabel16(const char* fam, int tile, int layer) {
     int bm = 0, bn = 0, st = 0;
     rowgemm16_tile_dims(tile, &bm, &bn, &st);
     char b[112];
-    snprintf(b, sizeof b, "%s/rg16_%dx%ds%d|%d", fam, bm, bn, st, layer);
+    snprintf(b, sizeof b, "%s/rg16%s_%dx%ds%d|%d", fam, tile >= 14 ? "m" : "", bm, bn, st, layer);
     return b;
 }
 // point g's A operand at the prepared bf16 image (lda = C channels)
