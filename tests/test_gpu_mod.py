@@ -219,7 +219,7 @@ def _assert_same(a, b, what):
 
 
 @pytest.mark.parametrize("tile,wtile", [(0, 0), (1, 1), (3, 0), (0, 2), (8, 0), (11, 0),
-                                        (0, 3), (0, 4), (2, 2), (4, 2)])
+                                        (0, 3), (0, 4), (2, 2), (4, 2), (18, 2)])
 def test_rg16_bit_identical_to_register_staged(tile, wtile):
     """The LDS-DMA bf16 GEMMs (kernels_gemm16.hip, fed by the k_to_bf16 operand images:
     row GEMMs and the transposed-read weight gradients) against the register-staged bf16
@@ -247,18 +247,20 @@ def test_rg16_tile_choice_is_numerically_invisible(side):
     x, t = inputs(29, 2, side, side)
     P = MO.make_params(31, 128, 5)
     outs = {}
-    for tile in (0, 2, 4, 12, 13, -1):  # 12 / 13: tiles 4 / 0 with read-ahead fragments
+    # 12 / 13: tiles 4 / 0 with read-ahead fragments; 18: the ping-pong 256x256 kernel
+    for tile in (0, 2, 4, 12, 13, 18, -1):
         m = _bf16_model(P, 128, 5)
         with options(m.flatten_().rt, rg16_tile=tile):
             outs[tile] = _bf16_step(m, x, t)
         del m
-    for tile in (2, 4, 12, 13, -1):
+    for tile in (2, 4, 12, 13, 18, -1):
         _assert_same(outs[0], outs[tile], f"{side}^2 tile {tile} vs 0")
 
 
 @pytest.mark.parametrize("base,depth,tile", [(64, 3, "4"), (128, 5, "0"), (128, 5, "2"), (128, 5, "4"),
                                              (128, 5, "6"), (128, 5, "7"),
-                                             (128, 5, "9"), (128, 5, "10"), (128, 5, "auto")])
+                                             (128, 5, "9"), (128, 5, "10"), (128, 5, "14"),
+                                             (128, 5, "15"), (128, 5, "18"), (128, 5, "auto")])
 def test_mod_bf16_matches_bf16_oracle(base, depth, tile):
     """mfma_dtype="bf16": one step at B=2 64x64 vs the oracle that rounds exactly the GEMM
     operands the HIP bf16 kernels round (oracle/mod_ref_cpu.py, bf16=True).
@@ -273,7 +275,7 @@ def test_mod_bf16_matches_bf16_oracle(base, depth, tile):
     per-GEMM choice (rg16_tile, runtime.hip) and default wgrad tile."""
     import unet_hip
     opts = {} if tile == "auto" else dict(
-        rg16_tile=int(tile), wg16_tile=2 if tile in ("4", "6", "7", "9", "10") else 0)
+        rg16_tile=int(tile), wg16_tile=2 if tile in ("4", "6", "7", "9", "10", "14", "18") else 0)
     P = MO.make_params(42, base, depth)
     x, t = inputs(5, 2, 64, 64)
     ref = MO.train_step(P, MO.init_buffers(base, depth), None, x, t, depth=depth, bf16=True)

@@ -143,6 +143,8 @@ int launch_rowgemm_dma(const RowGemmArgs& a, int tile, hipStream_t s);
 // 20.. = one row of 3x3 taps per block (3 accumulator sets; BM = channels of ONE tap):
 // 20 = 64x64, 21 = 128x64, 22 = 64x128, 23 = 128x128, 24 = 64x64 with 64-pixel chunks
 int launch_rowgemm16(const RowGemmArgs& a, int tile, hipStream_t s);
+// speed-of-light ablations of the forward rg16 GEMM (tile 4): -2 when not applicable
+int launch_rowgemm16_xp(const RowGemmArgs& a, int xp, hipStream_t s);
 int rowgemm16_tile_dims(int tile, int* bm, int* bn, int* stages = nullptr);
 int wgrad16g_tile_dims(int tile, int* bm, int* bn, int* stages = nullptr);
 int launch_wgrad(const WgradArgs& a, int tile, hipStream_t s);

@@ -43,6 +43,16 @@ __device__ __forceinline__ void block_barrier() {
     asm volatile("" ::: "memory");
 }
 
+// block barrier that the scheduler may not move any instruction across (MFMAs included: the
+// ping-pong kernel's phases are defined by which barrier interval an MFMA lands in)
+__device__ __forceinline__ void pp_barrier() {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+}
+
 template <int N>
 __device__ __forceinline__ void wait_vm() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -75,7 +85,10 @@ struct Tile16 {
     static constexpr int THREADS = 64 * WAVES;
 };
 
-template <int AMODE, int EMODE, class T>
+// XP: speed-of-light ablations (option rg16_xp, forward GEMMs on tile 4 only; results are
+// garbage): bit 0 drops the A DMA, 1 the B DMA, 2 the LDS fragment reads, 3 the loop's
+// waits and barriers.  The library's normal path instantiates XP = 0.
+template <int AMODE, int EMODE, class T, int XP = 0>
 __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm16_kernel(RowGemmArgs p) {
     constexpr int BM = T::BM, BN = T::BN, WM = T::WM, WN = T::WN, S = T::S, BK = T::BK;
     constexpr bool ONEBAR = T::ONEBAR, ILV = T::ILV;
@@ -139,7 +152,7 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm16_kernel(RowGemmAr
         char* base = smem + st * STAGE;
 #pragma unroll
         for (int j = 0; j < AI; ++j) {
-            if (j < j0 || j >= j1) continue;
+            if (j < j0 || j >= j1 || (XP & 1)) continue;
             bool valid;
             const int src = gather_src<AMODE>(tap, am[j], aq[j], H, W, valid);
             const uint16_t* g = (valid && aok[j]) ? p.a16 + (size_t)src * p.lda + c0 + ach[j] : zero;
@@ -147,7 +160,7 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm16_kernel(RowGemmAr
         }
 #pragma unroll
         for (int j = 0; j < BI; ++j) {
-            if (AI + j < j0 || AI + j >= j1) continue;
+            if (AI + j < j0 || AI + j >= j1 || (XP & 2)) continue;
             glds16(bsrc[j] + k0, base + BM * RB + (j * WAVES + wave) * 1024);
         }
     };
@@ -194,6 +207,9 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm16_kernel(RowGemmAr
     }
 
     const int nk = K / BK;
+    bf16x8 xa;  // XP & 4: a register operand
+#pragma unroll
+    for (int j = 0; j < 8; ++j) xa[j] = (__bf16)(float)(lane + j);
 #pragma unroll
     for (int s = 0; s < DIST; ++s)
         if (s < nk) issue(s, s);
@@ -205,7 +221,8 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm16_kernel(RowGemmAr
         if (!ILV && kc + DIST < nk) issue(kc + DIST, (kc + DIST) % S);
         // chunks issued after kc that may stay in flight
         const int ahead = min(INFL, nk - 1 - kc);
-        if constexpr (INFL >= 3) {
+        if constexpr (XP & 8) {
+        } else if constexpr (INFL >= 3) {
             if (ahead >= 3) wait_vm<3 * GPC>();
             else if (ahead == 2) wait_vm<2 * GPC>();
             else if (ahead == 1) wait_vm<GPC>();
@@ -220,7 +237,7 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm16_kernel(RowGemmAr
         } else {
             wait_vm<0>();
         }
-        block_barrier();
+        if constexpr (!(XP & 8)) block_barrier();
         const char* base = smem + (kc % S) * STAGE;
         const bool more = kc + DIST < nk;
         if constexpr (M16) {
@@ -270,12 +287,19 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm16_kernel(RowGemmAr
         for (int kk = 0; kk < BK / 16; ++kk) {
             const int c = kk * 2 + lh;
             bf16x8 af[MT], bfr[NT];
+            if constexpr (XP & 4) {  // operands from registers only (no LDS traffic)
+#pragma unroll
+                for (int mt = 0; mt < MT; ++mt) af[mt] = xa;
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt) bfr[nt] = xa;
+            } else {
 #pragma unroll
             for (int mt = 0; mt < MT; ++mt)
                 af[mt] = *(const bf16x8*)(base + aro[mt] + ((c ^ afx[mt]) << 4));
 #pragma unroll
             for (int nt = 0; nt < NT; ++nt)
                 bfr[nt] = *(const bf16x8*)(base + bro[nt] + ((c ^ bfx[nt]) << 4));
+            }
 #pragma unroll
             for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
@@ -296,7 +320,7 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm16_kernel(RowGemmAr
                 }
             }
         }
-        if constexpr (!ONEBAR) {
+        if constexpr (!ONEBAR && !(XP & 8)) {
             // this stage's ds_reads must have returned before any wave restages it
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             block_barrier();
@@ -336,6 +360,156 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm16_kernel(RowGemmAr
     }
 }
 
+// ------------------------------------------------------------------------------------
+// Ping-pong schedule of the same GEMM (256x256 tile, 8 waves of 128x64, two 64-K stages):
+// the two waves that share a SIMD (wave w and w + 4) belong to different groups, G0 = waves
+// 0-3 and G1 = waves 4-7, and G1 runs one barrier behind G0, so in every barrier interval one
+// group runs its chunk's MFMAs while the other issues the next chunk's LDS-DMA pieces.  The
+// one-schedule kernel above issues and waits in every wave at once, which left the matrix pipes
+// idle for the DMA issue (speed-of-light ablation, profiles/r03_xp.txt: dropping the DMA
+// raised the forward GEMM from 1079 to 1432 TF/s).  Events (hardware barrier counts): G0's
+// barriers A_k (2k) and B_k (2k+1), G1's X (0), A_k (2k+1), B_k (2k+2).
+//   G0: [issue k+1 -> stage (k+1)%2, vmcnt(0)] A_k [MFMAs of k] B_k    ... one extra barrier
+//   G1: X [issue k+1] A_k [MFMAs of k, lgkmcnt(0), vmcnt(0)] B_k
+// RAW: G0 reads chunk k after event 2k; its own pieces were waited before A_k, G1's before
+// G1's B_{k-1} (event 2k).  G1 reads chunk k after event 2k+1.  WAR: stage (k+1)%2 held chunk
+// k-1; G1 writes it after event 2k (G0 finished k-1 at 2k-1, G1 itself at 2k), G0 after event
+// 2k+1.  Same K order, per-chunk MFMA order and epilogue as rowgemm16_kernel: bit-identical.
+// ------------------------------------------------------------------------------------
+template <int AMODE, int EMODE>
+__global__ __launch_bounds__(512, 1) void rowgemm16_pp_kernel(RowGemmArgs p) {
+    constexpr int BM = 256, BN = 256, WM = 128, WN = 64, BK = 64, WAVES = 8, WAVES_N = 4;
+    constexpr int MT = WM / 32, NT = WN / 32;
+    constexpr int RB = 2 * BK, LPR = RB / 16, RPI = 64 / LPR, RPB = 256 / RB;
+    auto swz = [](int r) { return (r / RPB) & (LPR - 1); };
+    constexpr int AI = BM / (RPI * WAVES), BI = BN / (RPI * WAVES);
+    constexpr int STAGE = (BM + BN) * RB;
+    constexpr int SMEM = 2 * STAGE;
+    static_assert(SMEM >= 2 * (BM / 64) * BN * 8, "epilogue scratch");
+    __shared__ __attribute__((aligned(1024))) char smem[SMEM];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int grp = wave >> 2;  // wave w and w + 4 share a SIMD
+    const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+    const int ntn = p.N / BN;
+    const int bid = p.xcd ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+    const int tile_m = bid / ntn, tile_n = bid - tile_m * ntn;
+    const int m0 = tile_m * BM, n0 = tile_n * BN;
+    const int H = p.H, W = p.W, C = p.C, K = p.K;
+
+    const int lr = lane / LPR, slot = lane % LPR;
+    Pix aq[AI];
+    int am[AI], ach[AI];
+    bool aok[AI];
+#pragma unroll
+    for (int j = 0; j < AI; ++j) {
+        const int r = (j * WAVES + wave) * RPI + lr;
+        const int m = m0 + r;
+        aok[j] = m < p.M;
+        am[j] = aok[j] ? m : p.M - 1;
+        aq[j] = decode(am[j], H, W);
+        ach[j] = (slot ^ swz(r)) * 8;
+    }
+    const uint16_t* bsrc[BI];
+#pragma unroll
+    for (int j = 0; j < BI; ++j) {
+        const int r = (j * WAVES + wave) * RPI + lr;
+        bsrc[j] = p.bt16 + (size_t)(n0 + r) * K + (slot ^ swz(r)) * 8;
+    }
+    const uint16_t* zero = (const uint16_t*)p.zero16;
+    auto issue = [&](int kc) {
+        const int k0 = kc * BK;
+        const int tap = k0 / C;
+        const int c0 = k0 - tap * C;
+        char* base = smem + (kc & 1) * STAGE;
+#pragma unroll
+        for (int j = 0; j < AI; ++j) {
+            bool valid;
+            const int src = gather_src<AMODE>(tap, am[j], aq[j], H, W, valid);
+            const uint16_t* g = (valid && aok[j]) ? p.a16 + (size_t)src * p.lda + c0 + ach[j] : zero;
+            glds16(g, base + (j * WAVES + wave) * 1024);
+        }
+#pragma unroll
+        for (int j = 0; j < BI; ++j) glds16(bsrc[j] + k0, base + BM * RB + (j * WAVES + wave) * 1024);
+    };
+
+    f32x16 acc[MT][NT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    const int lh = lane >> 5, li = lane & 31;
+    int aro[MT], afx[MT], bro[NT], bfx[NT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+        const int r = wm * WM + mt * 32 + li;
+        aro[mt] = r * RB;
+        afx[mt] = swz(r);
+    }
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+        const int r = wn * WN + nt * 32 + li;
+        bro[nt] = (BM + r) * RB;
+        bfx[nt] = swz(r);
+    }
+    // the chunk's MFMAs from stage kc & 1 (same order as rowgemm16_kernel's plain path)
+    auto compute = [&](int kc) {
+        const char* base = smem + (kc & 1) * STAGE;
+#pragma unroll
+        for (int kk = 0; kk < BK / 16; ++kk) {
+            const int c = kk * 2 + lh;
+            bf16x8 af[MT], bfr[NT];
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt) af[mt] = *(const bf16x8*)(base + aro[mt] + ((c ^ afx[mt]) << 4));
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) bfr[nt] = *(const bf16x8*)(base + bro[nt] + ((c ^ bfx[nt]) << 4));
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma32_bf16(af[mt], bfr[nt], acc[mt][nt]);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    };
+
+    const int nk = K / BK;
+    issue(0);
+    wait_vm<0>();
+    if (grp == 0) {
+        for (int kc = 0; kc < nk; ++kc) {
+            pp_barrier();  // A_k
+            compute(kc);
+            pp_barrier();  // B_k
+            if (kc + 1 < nk) {
+                issue(kc + 1);
+                wait_vm<0>();
+            }
+        }
+        pp_barrier();  // pairs with G1's B_{nk-1}
+    } else {
+        pp_barrier();  // X
+        for (int kc = 0; kc < nk; ++kc) {
+            if (kc + 1 < nk) issue(kc + 1);
+            pp_barrier();  // A_k
+            compute(kc);
+            wait_vm<0>();
+            pp_barrier();  // B_k
+        }
+    }
+    row_epilogue<EMODE, BM, BN, WM, WN, true>(p, acc, m0, n0, tile_m, wm, wn, lane, tid, (float*)smem);
+}
+
+template <int AMODE, int EMODE>
+static int rg16pp_go(const RowGemmArgs& a, hipStream_t s) {
+    if (a.N % 256 || a.C % 64 || a.K % 64) return -1;
+    if (EMODE == E_CONVT && (a.cout % 256)) return -1;
+    const dim3 grid(((a.M + 255) / 256) * (a.N / 256));
+    hipLaunchKernelGGL((rowgemm16_pp_kernel<AMODE, EMODE>), grid, dim3(512), 0, s, a);
+    return (int)hipGetLastError();
+}
+
 // tiles: 0 = 128x128, 2 stages (64 KB LDS, 2 blocks/CU); 1 = 128x128, 3 stages (96 KB);
 // 2 = 256x128, 8 waves, 2 stages (96 KB); 3 = 128x128, 4 stages (128 KB);
 // 4 = 256x256, 8 waves of 128x64, 2 stages (128 KB); 5 = 256x128, 8 waves, 3 stages (144 KB);
@@ -368,17 +542,18 @@ using T16_17 = Tile16<128, 128, 64, 64, 2, 2, 64, false, false, false, true, tru
     X(8, T16_8) X(9, T16_9) X(10, T16_10) X(11, T16_11) X(12, T16_12) X(13, T16_13)            \
     X(14, T16_14) X(15, T16_15) X(16, T16_16) X(17, T16_17)
 
-template <int AMODE, int EMODE, class T>
+template <int AMODE, int EMODE, class T, int XP = 0>
 static int rg16_go(const RowGemmArgs& a, hipStream_t s) {
     if (a.N % T::BN || a.C % T::BK || a.K % T::BK) return -1;
     if (EMODE == E_CONVT && (a.cout % T::BN)) return -1;
     const dim3 grid(((a.M + T::BM - 1) / T::BM) * (a.N / T::BN));
-    hipLaunchKernelGGL((rowgemm16_kernel<AMODE, EMODE, T>), grid, dim3(T::THREADS), 0, s, a);
+    hipLaunchKernelGGL((rowgemm16_kernel<AMODE, EMODE, T, XP>), grid, dim3(T::THREADS), 0, s, a);
     return (int)hipGetLastError();
 }
 
 template <int AMODE, int EMODE>
 static int rg16_tile(const RowGemmArgs& a, int tile, hipStream_t s) {
+    if (tile == 18) return rg16pp_go<AMODE, EMODE>(a, s);
 #define RG16_CASE(id, T) \
     if (tile == id) return rg16_go<AMODE, EMODE, T>(a, s);
     ROWGEMM16_TILES(RG16_CASE)
@@ -634,6 +809,11 @@ int wgrad16g_tile_dims(int tile, int* bm, int* bn, int* stages) {
 }
 
 int rowgemm16_tile_dims(int tile, int* bm, int* bn, int* stages) {
+    if (tile == 18) {  // ping-pong 256x256 (rowgemm16_pp_kernel)
+        *bm = *bn = 256;
+        if (stages) *stages = 2;
+        return 0;
+    }
 #define RG16_DIMS(id, T)          \
     if (tile == id) {             \
         *bm = T::BM;              \
@@ -648,6 +828,15 @@ int rowgemm16_tile_dims(int tile, int* bm, int* bn, int* stages) {
 
 // The combinations of the BN -> ReLU network (models/mod.py): conv forward (E_STATS),
 // conv dgrad (E_STORE / E_STORE_BN), ConvT forward (E_CONVT), ConvT dgrad (G_UP2, E_STORE_BN).
+int launch_rowgemm16_xp(const RowGemmArgs& a, int xp, hipStream_t s) {
+    if (a.amode != G_CONV3 || a.emode != E_STATS) return -2;
+#define XPC(v) \
+    if (xp == v) return rg16_go<G_CONV3, E_STATS, T16_4, v>(a, s);
+    XPC(1) XPC(2) XPC(3) XPC(4) XPC(7) XPC(8) XPC(12) XPC(15)
+#undef XPC
+    return -2;
+}
+
 int launch_rowgemm16(const RowGemmArgs& a, int tile, hipStream_t s) {
     if (a.M < 1 || a.K != gather_taps(a.amode) * a.C || !a.a16 || !a.bt16 || !a.zero16) return -1;
     if (a.ascale || a.acoef || a.arelu) return -1;  // operands arrive prepared (k_to_bf16)

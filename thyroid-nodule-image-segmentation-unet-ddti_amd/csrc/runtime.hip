@@ -115,6 +115,9 @@ struct Options {
     int rg16 = 1;              // bf16 row GEMMs on the LDS-DMA kernel (0: register-staged)
     int rg16_tile = -1;        // its tile (-1 = per GEMM, rg16_tile())
     int rg16_ra = 0;           // per-GEMM choice on the read-ahead tiles 12 / 13
+    int rg16_xp = 0;           // speed-of-light ablation of the forward rg16 GEMMs (garbage
+                               // results; A/B timing only, kernels_gemm16.hip XP)
+    int rg16_pp = 0;           // 256x256 GEMMs on the ping-pong kernel (tile 18)
     int rg16_m16 = 0;          // per-GEMM choice on the 16x16x32-MFMA tiles: 1 = 14 / 15,
                                // 2 = with s_setprio around the MFMAs (16 / 17)
     int wg16 = 1;              // bf16 3x3 wgrad on the LDS-DMA transposed-read kernel
@@ -143,7 +146,8 @@ const OptionDesc OPTION_TABLE[] = {
     {"tile16_n128", &Options::tile16_n128},     {"tile16_n128_dgrad", &Options::tile16_n128_dgrad},
     {"tile16_n64", &Options::tile16_n64},       {"rg16", &Options::rg16},
     {"rg16_tile", &Options::rg16_tile},         {"rg16_ra", &Options::rg16_ra},         {"wg16", &Options::wg16},
-    {"rg16_m16", &Options::rg16_m16},
+    {"rg16_m16", &Options::rg16_m16},         {"rg16_xp", &Options::rg16_xp},
+    {"rg16_pp", &Options::rg16_pp},
     {"wg16_tile", &Options::wg16_tile},         {"wg16t", &Options::wg16t},
     {"xcd16", &Options::xcd16},                 {"xcd_remap", &Options::xcd_remap},
     {"wgrad_stream", &Options::wgrad_stream},   {"dz_in_loaders", &Options::dz_in_loaders},
@@ -605,6 +609,7 @@ int rg16_tile(const unet_ctx* c, const RowGemmArgs& g) {
         t0 = c->opt.rg16_m16 == 2 ? 17 : 15;
         t4 = c->opt.rg16_m16 == 2 ? 16 : 14;
     }
+    if (c->opt.rg16_pp) t4 = 18;  // option rg16_pp: the ping-pong 256x256 kernel
     if (!fits(4)) return t0;
     const int64_t blocks = (g.M + 255) / 256 * (g.N / 256);
     if (blocks < 256) return t0;
@@ -947,7 +952,8 @@ std::string tlabel16(const char* fam, int tile, int layer) {
     int bm = 0, bn = 0, st = 0;
     rowgemm16_tile_dims(tile, &bm, &bn, &st);
     char b[112];
-    snprintf(b, sizeof b, "%s/rg16%s_%dx%ds%d|%d", fam, tile >= 14 ? "m" : "", bm, bn, st, layer);
+    snprintf(b, sizeof b, "%s/rg16%s_%dx%ds%d|%d", fam, tile == 18 ? "pp" : tile >= 14 ? "m" : "",
+             bm, bn, st, layer);
     return b;
 }
 // point g's A operand at the prepared bf16 image (lda = C channels)
@@ -1061,8 +1067,9 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
                 g.a16 = img;
                 const int tile = rg16_tile(c, g);
                 R = bn_groups(M);
+                const bool xp = c->opt.rg16_xp && tile == 4;
                 RUN(tlabel16("conv_fwd", tile, i), 2.0 * M * C.cout * 9 * C.cin,
-                    launch_rowgemm16(g, tile, s));
+                    xp ? launch_rowgemm16_xp(g, c->opt.rg16_xp, s) : launch_rowgemm16(g, tile, s));
                 return stats_finalize(c, L, p, i, R, M, training, prm, bn_run, bn_cnt);
             }
             R = bn_groups(M);
