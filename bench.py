@@ -43,9 +43,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", type=int, default=2, choices=(2, 4),
+    ap.add_argument("--config", default="2", choices=("2", "4", "res"),
                     help="BASELINE config: 2 = models/model.py UNet (3 = 2 on N ranks), "
-                         "4 = models/mod.py UNet(base 128, depth 5) at 512x512")
+                         "4 = models/mod.py UNet(base 128, depth 5) at 512x512; res = "
+                         "models/mod.py ResUNet(64, 5) at 512x512, bs 16 (what the reference "
+                         "main.py:122 trains; not a BASELINE config)")
     ap.add_argument("--mfma", default="fp32", choices=("fp32", "bf16"),
                     help="config 4 only: conv GEMM arithmetic (BASELINE config 4 is bf16)")
     ap.add_argument("--batch", type=int, default=0, help="images per GPU (default 32 / 8)")
@@ -152,7 +154,8 @@ def dice_vs_ref(sample, dev):
 def load_pmc(kernel, config=2, mfma="fp32"):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of this
     workload (profiles/pmc_summary.json: config 2; pmc_summary_c4_<mfma>.json), if any."""
-    name = "pmc_summary.json" if config == 2 else f"pmc_summary_c4_{mfma}.json"
+    name = ("pmc_summary.json" if str(config) == "2" else
+            f"pmc_summary_c4_{mfma}.json" if str(config) == "4" else f"pmc_summary_{config}.json")
     path = os.path.join(REPO, "profiles", name)
     try:
         d = json.load(open(path))
@@ -186,13 +189,16 @@ def main():
 
     import unet_hip
     from unet_hip.dist import DistributedUNet
-    from unet_hip.flops import train_flops_per_image
+    from unet_hip.flops import res_train_flops_per_image, train_flops_per_image
 
-    c4 = args.config == 4
-    args.batch = args.batch or (8 if c4 else 32)
-    args.size = args.size or (512 if c4 else 256)
+    c4 = args.config == "4"
+    cres = args.config == "res"
+    args.batch = args.batch or (8 if c4 else 16 if cres else 32)
+    args.size = args.size or (512 if c4 or cres else 256)
     torch.manual_seed(42)
-    if c4:
+    if cres:
+        model = unet_hip.ResUNet(1, 1, base_filters=64, depth=5).to(dev).train()
+    elif c4:
         model = unet_hip.ModUNet(1, 1, base_filters=128, depth=5,
                                  mfma_dtype=args.mfma).to(dev).train()
     else:
@@ -288,7 +294,8 @@ def main():
     achieved = f_l / (t_l * 1e-3) / 1e12 if t_l > 0 else 0.0
     per_launch_flop = f_l / n_l
     pmc = load_pmc(dom, args.config, args.mfma)
-    conv_flop = (train_flops_per_image(S, S, 128, 5) if c4 else train_flops_per_image(S, S)) * B
+    conv_flop = (train_flops_per_image(S, S, 128, 5) if c4 else
+                 res_train_flops_per_image(S, S, 64, 5) if cres else train_flops_per_image(S, S)) * B
     bf16 = c4 and args.mfma == "bf16"
     peak = BF16_MFMA_PEAK_TFLOPS if bf16 else FP32_MFMA_PEAK_TFLOPS
     roofline = {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 3),
@@ -300,7 +307,12 @@ def main():
                 "step_conv_tflops": round(conv_flop / (ms * 1e-3) / 1e12, 3),
                 "step_conv_frac": round(conv_flop / (ms * 1e-3) / 1e12 / peak, 4)}
 
-    if c4:
+    if cres:
+        metric = f"images/sec fwd+bwd, mod.ResUNet(base 64, depth 5) {S}x{S}x1 bs={B}/GPU"
+        workload = (f"models/mod.py ResUNet base-64 depth-5 (reference main.py:122), 1x{S}x{S}, "
+                    f"bs={B}/GPU, fwd+BCE+Dice+bwd+AdamW, f32 MFMA (not a BASELINE config)")
+        mname = "mod.ResUNet(in=1,out=1,base_filters=64,depth=5)"
+    elif c4:
         metric = f"images/sec fwd+bwd, mod.UNet(base 128, depth 5) {S}x{S}x1 bs={B}/GPU"
         if bf16:
             workload_note = " (conv GEMMs bf16 MFMA, f32 accumulate)"
@@ -331,8 +343,8 @@ def main():
            "config": {"workload": workload, "model": mname, "global_batch": B * world,
                       "image": [1, S, S], "parallelism": f"dp{world}"},
            "roofline": roofline}
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        sample, out["cpu_baseline"] = cpu_baseline(args.cpu_steps, S, args.config)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not cres:
+        sample, out["cpu_baseline"] = cpu_baseline(args.cpu_steps, S, int(args.config))
         if sample is not None:
             out["dice_vs_ref"] = dice_vs_ref(sample, dev)
     elif rank == 0:

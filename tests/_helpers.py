@@ -116,3 +116,61 @@ class options:
         for k, v in self.old.items():
             self.rt.set_option(k, v)
         return False
+
+
+def _to64(d):
+    return {k: (v.double() if v.is_floating_point() else v.clone()) for k, v in d.items()}
+
+
+def _copy(d):
+    return {k: v.clone() for k, v in d.items()}
+
+
+def strict_resync_steps(m, train_step_fn, x, t, steps=3, lr=1e-4, floor0=5e-3, floor=1e-2):
+    """Per-step parity with the oracle restarted from THIS path's state before every step
+    (tests/test_gpu_parity.py::test_train_steps_strict_resync, generalised to any network
+    through train_step_fn(P, B, opt, x, t) -> dict(logits, loss, grads)).
+
+    Each step: the oracle takes this path's parameters, BN running statistics and Adam
+    moments; logits must match it at the north-star bar (1e-4 of max|ref|), the loss at
+    1e-5; every gradient is judged against the fp64 evaluation of the same graph, within 2x
+    the larger fp32 oracle deviation from fp64 over two fp32 noise realisations (x and
+    x * (1 + 1e-7)) and never above `floor0` (step 0) / `floor` (later steps, where ReLU
+    boundary flips compound).  Returns the per-step worst gradient errors."""
+    import unet_hip
+    from oracle import unet_ref_cpu as O
+    dev = next(m.parameters()).device
+    opt = unet_hip.HipAdamW(m.parameters(), lr=lr)
+    xd, td = x.to(dev), t.to(dev)
+    worst = []
+    for s in range(steps):
+        Pc = {k: v.detach().cpu().clone() for k, v in m.named_parameters()}
+        Bc = {k: v.detach().cpu().clone() for k, v in m.named_buffers()}
+        r64 = train_step_fn(_to64(Pc), _to64(Bc), None, x.double(), t.double())
+        r32p = train_step_fn(_copy(Pc), _copy(Bc), None, x * (1 + 1e-7), t)
+        ref_opt = O.AdamWState(_copy(Pc), lr=lr)
+        if s:
+            for k, p in m.named_parameters():
+                ref_opt.m[k] = opt.state[p]["exp_avg"].detach().cpu().clone()
+                ref_opt.v[k] = opt.state[p]["exp_avg_sq"].detach().cpu().clone()
+        ref_opt.step_count = s
+        ref = train_step_fn(_copy(Pc), _copy(Bc), ref_opt, x, t)
+        opt.zero_grad()
+        logits = m(xd)
+        losses = unet_hip.seg_losses(logits, td)
+        loss = losses[0] + losses[1]
+        loss.backward()
+        e_l = rel_max(logits.detach().cpu().numpy(), ref["logits"].numpy())
+        assert e_l <= 1e-4, f"step {s}: logits {e_l:.2e}"
+        assert abs(loss.item() - ref["loss"].item()) <= 1e-5, f"step {s}: loss"
+        e_hip = grad_errors(m, r64["grads"])
+        e32 = max(norm_rel(g, r64["grads"][k]) for k, g in ref["grads"].items())
+        e32p = max(norm_rel(g, r64["grads"][k]) for k, g in r32p["grads"].items())
+        env = max(2 * max(e32, e32p), floor0 if s == 0 else floor)
+        k_w = max(e_hip, key=e_hip.get)
+        assert e_hip[k_w] <= env, f"step {s} {k_w}: hip {e_hip[k_w]:.2e}, envelope {env:.2e}"
+        print(f"step {s}: logits {e_l:.2e}; worst grad {k_w} {e_hip[k_w]:.2e} (fp32 oracle "
+              f"{e32:.2e} / {e32p:.2e}, envelope {env:.2e})")
+        worst.append(e_hip[k_w])
+        opt.step()
+    return worst

@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 import torch
 
-from _helpers import check_eval, grad_errors, inputs, masks_agree, norm_rel, rel_max
+from _helpers import check_eval, grad_errors, inputs, masks_agree, norm_rel, rel_max, strict_resync_steps
 from oracle import mod_ref_cpu as MO
 from oracle import weights as Wt
 
@@ -77,6 +77,16 @@ def test_res_train_steps_match_golden(golden_dir):
     # eval mode (Trainer.validate / test, utils/trainer.py:130,206-250): the oracle resynced
     # from this path's parameters and running statistics, at the north-star bar
     check_eval(m, MO.make_res_forward(3), x.cpu(), t.cpu())
+
+
+def test_res_train_steps_strict_resync():
+    """Three AdamW steps (lr 1e-4) of ResUNet(base 64, depth 3) -- the block structure of
+    the network the reference main.py:122 trains -- with the oracle restarted from this
+    path's parameters, running statistics and Adam moments at every step: logits at 1e-4
+    and gradients within the fp64 envelope at every step."""
+    x, t = inputs(13, 2, 64, 64)
+    m = _model(MO.res_make_params(42, 64, 3), 64, 3)
+    strict_resync_steps(m, lambda P_, B_, o, x_, t_: MO.res_train_step(P_, B_, o, x_, t_, depth=3), x, t)
 
 
 def _to64(d):

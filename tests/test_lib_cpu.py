@@ -326,3 +326,19 @@ def test_flop_counts_agree_with_oracle():
     assert train_flops_per_image(512, 512, 128, 5) == MO.train_flops_per_image(512, 512, 128, 5)
     for H, W, base, depth in ((64, 96, 32, 4), (128, 128, 16, 6), (96, 64, 48, 3)):
         assert train_flops_per_image(H, W, base, depth) == MO.train_flops_per_image(H, W, base, depth)
+
+
+def test_res_flop_count_matches_torch_counter():
+    """bench.py --config res prices ResUNet's step with unet_hip.flops (3x3 / ConvT / head
+    + the 1x1 skips): its forward part equals torch's own FLOP counter over the oracle's
+    ResUNet forward (models/mod.py:86-131)."""
+    import torch
+    from torch.utils.flop_counter import FlopCounterMode
+    from oracle import mod_ref_cpu as MO
+    from unet_hip.flops import res_skip_macs, unet_level_macs
+    for base, depth, side in ((16, 3, 64), (8, 5, 64)):
+        P, B = MO.res_make_params(1, base, depth), MO.res_init_buffers(base, depth)
+        with FlopCounterMode(display=False) as fc:
+            MO.make_res_forward(depth)(torch.rand(1, 1, side, side), P, B, True)
+        want = 2 * (unet_level_macs(side, side, 1, 1, base, depth) + res_skip_macs(side, side, 1, base, depth))
+        assert fc.get_total_flops() == want

@@ -7,6 +7,8 @@ no input gradient.  BN, ReLU, pooling, losses and AdamW are not counted (bandwid
 
     models/model.py UNet, 256x256:       288,475,840,512 FLOP / image
     models/mod.py UNet(128, 5), 512x512: 5,709,420,822,528 FLOP / image
+    models/mod.py ResUNet(64, 5), 512x512 (what the reference main.py:122 trains):
+        res_train_flops_per_image -- the same 3x3 / ConvT work plus every block's 1x1 skip
 
 (The oracle's own counters, oracle/*_ref_cpu.py, are pinned to the same numbers by
 tests/test_host_cpu.py.)
@@ -38,3 +40,26 @@ def train_flops_per_image(H, W, base=64, depth=4, in_channels=1, out_channels=1)
     """fwd + dgrad + wgrad = 6 x forward MACs, minus the first conv's unneeded dgrad."""
     macs = unet_level_macs(H, W, in_channels, out_channels, base, depth)
     return 6 * macs - 2 * (H * W * 9 * base * in_channels)
+
+
+def res_skip_macs(H, W, in_channels, base, depth):
+    """Forward MACs of ResUNet's 1x1 skip convs (models/mod.py:83): one per block, Cin ->
+    Cout at the block's resolution (the decoders' Cin is the 2c-channel concat)."""
+    macs = 0
+    prev = in_channels
+    for i in range(depth + 1):
+        c = base << i
+        macs += (H >> i) * (W >> i) * prev * c
+        prev = c
+    for lv in range(depth - 1, -1, -1):
+        c = base << lv
+        macs += (H >> lv) * (W >> lv) * 2 * c * c
+    return macs
+
+
+def res_train_flops_per_image(H, W, base=64, depth=5, in_channels=1, out_channels=1):
+    """ResUNet: fwd + dgrad + wgrad of the UNet topology plus the skips, minus the first
+    block's unneeded input gradients (its 3x3 conv and its skip)."""
+    macs = unet_level_macs(H, W, in_channels, out_channels, base, depth) + \
+        res_skip_macs(H, W, in_channels, base, depth)
+    return 6 * macs - 2 * (H * W * 9 * base * in_channels) - 2 * (H * W * base * in_channels)
