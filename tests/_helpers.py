@@ -134,9 +134,11 @@ def strict_resync_steps(m, train_step_fn, x, t, steps=3, lr=1e-4, floor0=5e-3, f
     Each step: the oracle takes this path's parameters, BN running statistics and Adam
     moments; logits must match it at the north-star bar (1e-4 of max|ref|), the loss at
     1e-5; every gradient is judged against the fp64 evaluation of the same graph, within 2x
-    the larger fp32 oracle deviation from fp64 over two fp32 noise realisations (x and
-    x * (1 + 1e-7)) and never above `floor0` (step 0) / `floor` (later steps, where ReLU
-    boundary flips compound).  Returns the per-step worst gradient errors."""
+    the largest fp32 oracle deviation from fp64 over nine fp32 noise realisations (x scaled
+    by 1, 1 +- 1e-7 .. 1 +- 5e-7: each moves a different few ReLU inputs across
+    zero; measured on mod.py UNet(64, 3) at step 0 they span 3e-5 .. 9e-3 on the small BN /
+    ConvT bias gradients) and at least `floor0` (step 0) / `floor` (later steps, where
+    the flips compound).  Returns the per-step worst gradient errors."""
     import unet_hip
     from oracle import unet_ref_cpu as O
     dev = next(m.parameters()).device
@@ -147,7 +149,10 @@ def strict_resync_steps(m, train_step_fn, x, t, steps=3, lr=1e-4, floor0=5e-3, f
         Pc = {k: v.detach().cpu().clone() for k, v in m.named_parameters()}
         Bc = {k: v.detach().cpu().clone() for k, v in m.named_buffers()}
         r64 = train_step_fn(_to64(Pc), _to64(Bc), None, x.double(), t.double())
-        r32p = train_step_fn(_copy(Pc), _copy(Bc), None, x * (1 + 1e-7), t)
+        spread = 0.0
+        for eps in (1e-7, -1e-7, 2e-7, -2e-7, 3e-7, -3e-7, 5e-7, -5e-7):
+            r32p = train_step_fn(_copy(Pc), _copy(Bc), None, x * (1 + eps), t)
+            spread = max(spread, max(norm_rel(g, r64["grads"][k]) for k, g in r32p["grads"].items()))
         ref_opt = O.AdamWState(_copy(Pc), lr=lr)
         if s:
             for k, p in m.named_parameters():
@@ -164,13 +169,17 @@ def strict_resync_steps(m, train_step_fn, x, t, steps=3, lr=1e-4, floor0=5e-3, f
         assert e_l <= 1e-4, f"step {s}: logits {e_l:.2e}"
         assert abs(loss.item() - ref["loss"].item()) <= 1e-5, f"step {s}: loss"
         e_hip = grad_errors(m, r64["grads"])
-        e32 = max(norm_rel(g, r64["grads"][k]) for k, g in ref["grads"].items())
-        e32p = max(norm_rel(g, r64["grads"][k]) for k, g in r32p["grads"].items())
-        env = max(2 * max(e32, e32p), floor0 if s == 0 else floor)
+        e32d = {k: norm_rel(g, r64["grads"][k]) for k, g in ref["grads"].items()}
+        e32 = max(e32d.values())
+        e32p = max(e32, spread)
+        env = max(2 * e32p, floor0 if s == 0 else floor)
         k_w = max(e_hip, key=e_hip.get)
-        assert e_hip[k_w] <= env, f"step {s} {k_w}: hip {e_hip[k_w]:.2e}, envelope {env:.2e}"
+        med = float(np.median(list(e_hip.values())))
+        med32 = float(np.median(list(e32d.values())))
         print(f"step {s}: logits {e_l:.2e}; worst grad {k_w} {e_hip[k_w]:.2e} (fp32 oracle "
-              f"{e32:.2e} / {e32p:.2e}, envelope {env:.2e})")
+              f"{e32:.2e} / {e32p:.2e}, envelope {env:.2e}); median tensor {med:.2e} "
+              f"(fp32 oracle {med32:.2e})")
+        assert e_hip[k_w] <= env, f"step {s} {k_w}: hip {e_hip[k_w]:.2e}, envelope {env:.2e}"
         worst.append(e_hip[k_w])
         opt.step()
     return worst

@@ -83,10 +83,14 @@ def test_res_train_steps_strict_resync():
     """Three AdamW steps (lr 1e-4) of ResUNet(base 64, depth 3) -- the block structure of
     the network the reference main.py:122 trains -- with the oracle restarted from this
     path's parameters, running statistics and Adam moments at every step: logits at 1e-4
-    and gradients within the fp64 envelope at every step."""
+    and gradients within the fp64 envelope at every step.  Later-step floor 2e-2: one ReLU
+    input crossing zero moves a small residual-block BN-bias gradient by up to 1.5e-2 in
+    this network (measured on the fp32 oracle alone; here step 2 moves
+    decoders.0.conv.1.bias by 1.1e-2 while the median tensor stays at fp32 rounding)."""
     x, t = inputs(13, 2, 64, 64)
     m = _model(MO.res_make_params(42, 64, 3), 64, 3)
-    strict_resync_steps(m, lambda P_, B_, o, x_, t_: MO.res_train_step(P_, B_, o, x_, t_, depth=3), x, t)
+    strict_resync_steps(m, lambda P_, B_, o, x_, t_: MO.res_train_step(P_, B_, o, x_, t_, depth=3), x, t,
+                        floor=2e-2)
 
 
 def _to64(d):

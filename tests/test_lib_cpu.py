@@ -302,14 +302,16 @@ def test_schedule_options_are_explicit(rt, monkeypatch):
 def test_schedule_option_defaults():
     """The measured defaults documented in INTEGRATION.md §3: the pipelined
     row GEMMs (-1 = pick_tile: 18 forward / 16 dgrad), the row3 weight gradients with the
-    128x64 tile on the wide layers, the bf16 LDS-DMA kernels; A/B alternatives off."""
+    128x64 tile on the wide layers, the bf16 LDS-DMA kernels, XCD-contiguous tiles for the
+    f32 GEMMs; A/B alternatives off."""
     from unet_hip.runtime import UNetRuntime
     fresh = UNetRuntime("cuda:0")
     want = {"tile_n128": -1, "tile_n128_dgrad": -1, "tile_n64": 19, "tile_n64_dgrad": 1,
             "tile_convt64": 1, "wgrad_row3": 1, "wgrad_row3_big": 21, "wgrad_row3_blocks": 1536,
             "wgrad_row3_pipe": 0, "wgrad_blocks": 2048, "rg16": 1, "rg16_tile": -1, "rg16_ra": 0,
             "rg16_bn_k": 8192, "wg16": 1, "wg16_tile": 2, "wgrad16_blocks": 1536,
-            "wgrad_stream": 0, "dz_in_loaders": 0, "row3_gemm": 0, "xcd_remap": 0}
+            "wgrad_stream": 0, "dz_in_loaders": 0, "row3_gemm": 0, "xcd_remap": 1,
+            "tile_convt": -1, "tile_convt_dgrad": -1, "rg16_m16": 0, "rg16_pp": 0, "rg16_xp": 0}
     got = {k: fresh.get_option(k) for k in want}
     assert got == want
 

@@ -1082,6 +1082,12 @@ int rowgemm_tile_dims(int tile, int* bm, int* bn, int* bk) {
         *bk = 32;
         return 0;
     }
+    if (tile == 23 || tile == 24) {  // rowgemm_pipe_kernel, 8 waves: 128x256 / 256x128
+        *bm = tile == 23 ? 128 : 256;
+        *bn = tile == 23 ? 256 : 128;
+        *bk = 32;
+        return 0;
+    }
 #define RG_DIMS(id, T)   \
     if (tile == id) {    \
         *bm = T::BM;     \
@@ -1095,7 +1101,7 @@ int rowgemm_tile_dims(int tile, int* bm, int* bn, int* bk) {
 }
 
 int rowgemm_tile_dbuf(int tile) {
-    if (tile >= 16 && tile <= 19) return 2;  // pipelined
+    if ((tile >= 16 && tile <= 19) || tile == 23 || tile == 24) return 2;  // pipelined
     if (tile >= 20 && tile <= 22) return 3;  // LDS-DMA
 #define RG_DB(id, T) \
     if (tile == id) return T::DBUF ? 1 : 0;
@@ -1211,6 +1217,10 @@ int launch_rowgemm(const RowGemmArgs& a, int tile, hipStream_t s) {
     if (tile >= 16 && tile <= 19) {
         if (rowgemm_pipe_ok(a)) return launch_rowgemm_pipe(a, tile - 16, s);
         tile = tile % 2 == 0 ? 4 : 1;
+    }
+    if (tile == 23 || tile == 24) {  // wide pipelined tiles (short-K GEMMs: ConvT)
+        if (rowgemm_pipe_ok(a)) return launch_rowgemm_pipe(a, tile - 19, s);
+        tile = 4;
     }
     return a.bt16 ? rowgemm_dispatch<true>(a, tile, s) : rowgemm_dispatch<false>(a, tile, s);
 }

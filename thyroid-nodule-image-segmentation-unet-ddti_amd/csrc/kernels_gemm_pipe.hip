@@ -274,11 +274,18 @@ using PipeTile0 = PipeTile<128, 128, 64, 64, 2>;  // 4 waves of 64x64, 74 KB LDS
 using PipeTile1 = PipeTile<128, 64, 64, 32, 2>;   // 4 waves of 64x32 (N = 64 outputs)
 using PipeTile2 = PipeTile<128, 128, 64, 64, 2, 2>;  // tile 0, loads two chunks ahead
 using PipeTile3 = PipeTile<128, 64, 64, 32, 2, 2>;
+// 8 waves of 64x64, one block per CU (110 KB LDS): the short-K ConvT GEMMs (K = 128..256),
+// where a 128x64 block re-gathered its A rows for every one of the four (a, b) column tiles
+// and paid its prologue / epilogue per 4-8 chunks of MFMAs
+using PipeTile4 = PipeTile<128, 256, 64, 64, 1>;
+using PipeTile5 = PipeTile<256, 128, 64, 64, 1>;
 
 template <int AMODE, int AOP, int EMODE, class T>
 static int pipe_go(const RowGemmArgs& a, hipStream_t s) {
+    // (E_CONVT: the epilogue maps every column to its (a, b, co) on its own, so a tile may
+    // span several taps -- the 128x256 tile covers all four of a 64-channel ConvT)
     if (a.N % T::BN || a.K % T::BK || a.C % T::BK) return -1;
-    if (EMODE == E_CONVT && (a.cout % T::BN)) return -1;
+    if (EMODE == E_CONVT && (a.cout % T::BN) && (T::BN % a.cout)) return -1;
     const dim3 grid(((a.M + T::BM - 1) / T::BM) * (a.N / T::BN));
     hipLaunchKernelGGL((rowgemm_pipe_kernel<AMODE, AOP, EMODE, T>), grid, dim3(T::THREADS), 0, s, a);
     return (int)hipGetLastError();
@@ -290,6 +297,8 @@ static int pipe_tile(const RowGemmArgs& a, int tile, hipStream_t s) {
     if (tile == 1) return pipe_go<AMODE, AOP, EMODE, PipeTile1>(a, s);
     if (tile == 2) return pipe_go<AMODE, AOP, EMODE, PipeTile2>(a, s);
     if (tile == 3) return pipe_go<AMODE, AOP, EMODE, PipeTile3>(a, s);
+    if (tile == 4) return pipe_go<AMODE, AOP, EMODE, PipeTile4>(a, s);
+    if (tile == 5) return pipe_go<AMODE, AOP, EMODE, PipeTile5>(a, s);
     return -1;
 }
 
@@ -305,7 +314,8 @@ int rowgemm_pipe_ok(const RowGemmArgs& a) {
     return 1;
 }
 
-// tile: 0 = 128x128, 1 = 128x64
+// tile: 0 = 128x128, 1 = 128x64, 2 / 3 = those loading two chunks ahead, 4 = 128x256,
+// 5 = 256x128 (8 waves)
 int launch_rowgemm_pipe(const RowGemmArgs& a, int tile, hipStream_t s) {
     if (!rowgemm_pipe_ok(a) || a.M < 1 || a.K != gather_taps(a.amode) * a.C) return -1;
     const bool aff = a.ascale != nullptr;

@@ -156,17 +156,21 @@ __device__ void block_combine(const f32x4 (&acc)[NV], int tpr, int C, float* out
     }
 }
 
-// f64 variant (BN-backward partials, where downstream differences of the sums cancel)
+// f64 variant (BN-backward partials, where downstream differences of the sums cancel).
+// smem holds component (v, j) of every thread contiguously ([v][j][thread]): consecutive
+// lanes touch consecutive doubles, conflict-free (the [thread][v][j] order put lanes 32 B
+// apart, an 8-way bank conflict on every store and load: 499,712 extra LDS cycles per
+// max-pool backward launch in r02).  Same summation order as before: bit-identical.
 template <int NV>
 __device__ void block_combine_d(const double (&acc)[NV][4], int tpr, int C, float* out,
                                 double* smem) {
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, nt = blockDim.x;
     const int g = tid / tpr, q = tid % tpr;
-    const int groups = blockDim.x / tpr;
+    const int groups = nt / tpr;
 #pragma unroll
     for (int v = 0; v < NV; ++v)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) smem[(v * blockDim.x + tid) * 4 + j] = acc[v][j];
+        for (int j = 0; j < 4; ++j) smem[(v * 4 + j) * nt + tid] = acc[v][j];
     __syncthreads();
     if (g == 0) {
 #pragma unroll
@@ -174,7 +178,7 @@ __device__ void block_combine_d(const double (&acc)[NV][4], int tpr, int C, floa
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 double a = 0.0;
-                for (int k = 0; k < groups; ++k) a += smem[(v * blockDim.x + k * tpr + q) * 4 + j];
+                for (int k = 0; k < groups; ++k) a += smem[(v * 4 + j) * nt + k * tpr + q];
                 out[v * C + 4 * q + j] = (float)a;
             }
     }

@@ -109,6 +109,8 @@ struct Options {
     int tile_n64 = 19;         // ... N = 64 outputs (forward-type)
     int tile_n64_dgrad = 1;    // ... N = 64, dgrad-type
     int tile_convt64 = 1;      // ConvT forward with 64 output channels (grid N = 256)
+    int tile_convt = -1;       // ConvT forward, >= 128 output channels (-1 = tile_n128's)
+    int tile_convt_dgrad = -1; // ConvT input gradient (-1 = tile_n128_dgrad's)
     int tile16_n128 = 6;       // register-staged bf16 row-GEMM tiles
     int tile16_n128_dgrad = 6;
     int tile16_n64 = 1;
@@ -124,7 +126,9 @@ struct Options {
     int wg16_tile = 2;         // its tile (2 = 256x256)
     int wg16t = 1;             // bf16 ConvT wgrad on the same kernel
     int xcd16 = 1;             // XCD-contiguous block order, LDS-DMA kernels
-    int xcd_remap = 0;         // ... f32 GEMMs: 0 none, 1 both, 2 row GEMMs, 3 wgrad
+    int xcd_remap = 1;         // ... f32 GEMMs: 0 none, 1 both (default: r03 PMC, HBM bytes
+                               // per launch rowgemm 128x128 2.21 -> 1.00 GB, row3 wgrad
+                               // 2.02 -> 0.97 GB at equal time), 2 row GEMMs, 3 wgrad
     int wgrad_stream = 0;      // weight gradients on a second stream (bit-identical)
     int dz_in_loaders = 0;     // BN-backward dz inside the GEMM loaders (model.py order)
     int row3_gemm = 0;         // f32 3x3 forward / dgrad on the tap-row kernel
@@ -143,6 +147,7 @@ const OptionDesc OPTION_TABLE[] = {
     {"wgrad16_tile", &Options::wgrad16_tile},   {"tile_n128", &Options::tile_n128},
     {"tile_n128_dgrad", &Options::tile_n128_dgrad}, {"tile_n64", &Options::tile_n64},
     {"tile_n64_dgrad", &Options::tile_n64_dgrad}, {"tile_convt64", &Options::tile_convt64},
+    {"tile_convt", &Options::tile_convt},       {"tile_convt_dgrad", &Options::tile_convt_dgrad},
     {"tile16_n128", &Options::tile16_n128},     {"tile16_n128_dgrad", &Options::tile16_n128_dgrad},
     {"tile16_n64", &Options::tile16_n64},       {"rg16", &Options::rg16},
     {"rg16_tile", &Options::rg16_tile},         {"rg16_ra", &Options::rg16_ra},         {"wg16", &Options::wg16},
@@ -833,6 +838,8 @@ int pick_tile(const unet_ctx* c, int N, bool dgrad, bool bf16, bool convt = fals
     const Options& o = c->opt;
     if (bf16) return N % 128 == 0 ? (dgrad ? o.tile16_n128_dgrad : o.tile16_n128) : o.tile16_n64;
     if (N % 128) return convt && !dgrad ? o.tile_convt64 : (dgrad ? o.tile_n64_dgrad : o.tile_n64);
+    if (convt && !dgrad && o.tile_convt >= 0) return o.tile_convt;
+    if (convt && dgrad && o.tile_convt_dgrad >= 0) return o.tile_convt_dgrad;
     if (dgrad) return o.tile_n128_dgrad >= 0 ? o.tile_n128_dgrad : 16;
     return o.tile_n128 >= 0 ? o.tile_n128 : 18;
 }
@@ -1558,7 +1565,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
                 launch_rowgemm16(g, tile, s));
             return 0;
         }
-        const int tile = pick_tile(c, T.cin, true, c->bf16);
+        const int tile = pick_tile(c, T.cin, true, c->bf16, true);
         *rows = bn_groups(Pin);
         RUN(tlabel("convT_dgrad", tile, 100 + k), 2.0 * Pin * T.cin * 4 * T.cout, launch_rowgemm(g, tile, s));
         return 0;
