@@ -51,6 +51,9 @@ def parse():
     ap.add_argument("--mfma", default="fp32", choices=("fp32", "bf16"),
                     help="config 4 only: conv GEMM arithmetic (BASELINE config 4 is bf16)")
     ap.add_argument("--batch", type=int, default=0, help="images per GPU (default 32 / 8)")
+    ap.add_argument("--base", type=int, default=64, help="config res: base_filters (e.g. 32, the "
+                    "reference grid's narrow ResUNet; default 64 = main.py's ResUNet())")
+    ap.add_argument("--depth", type=int, default=5, help="config res: depth")
     ap.add_argument("--size", type=int, default=0, help="image side (default 256 / 512)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=3)
@@ -197,7 +200,7 @@ def main():
     args.size = args.size or (512 if c4 or cres else 256)
     torch.manual_seed(42)
     if cres:
-        model = unet_hip.ResUNet(1, 1, base_filters=64, depth=5).to(dev).train()
+        model = unet_hip.ResUNet(1, 1, base_filters=args.base, depth=args.depth).to(dev).train()
     elif c4:
         model = unet_hip.ModUNet(1, 1, base_filters=128, depth=5,
                                  mfma_dtype=args.mfma).to(dev).train()
@@ -295,7 +298,8 @@ def main():
     per_launch_flop = f_l / n_l
     pmc = load_pmc(dom, args.config, args.mfma)
     conv_flop = (train_flops_per_image(S, S, 128, 5) if c4 else
-                 res_train_flops_per_image(S, S, 64, 5) if cres else train_flops_per_image(S, S)) * B
+                 res_train_flops_per_image(S, S, args.base, args.depth) if cres else
+                 train_flops_per_image(S, S)) * B
     bf16 = c4 and args.mfma == "bf16"
     peak = BF16_MFMA_PEAK_TFLOPS if bf16 else FP32_MFMA_PEAK_TFLOPS
     roofline = {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 3),
@@ -308,10 +312,13 @@ def main():
                 "step_conv_frac": round(conv_flop / (ms * 1e-3) / 1e12 / peak, 4)}
 
     if cres:
-        metric = f"images/sec fwd+bwd, mod.ResUNet(base 64, depth 5) {S}x{S}x1 bs={B}/GPU"
-        workload = (f"models/mod.py ResUNet base-64 depth-5 (reference main.py:122), 1x{S}x{S}, "
-                    f"bs={B}/GPU, fwd+BCE+Dice+bwd+AdamW, f32 MFMA (not a BASELINE config)")
-        mname = "mod.ResUNet(in=1,out=1,base_filters=64,depth=5)"
+        metric = f"images/sec fwd+bwd, mod.ResUNet(base {args.base}, depth {args.depth}) {S}x{S}x1 bs={B}/GPU"
+        which = ("reference main.py:122" if (args.base, args.depth) == (64, 5)
+                 else "reference config/config.yaml grid")
+        workload = (f"models/mod.py ResUNet base-{args.base} depth-{args.depth} ({which}), 1x{S}x{S}, "
+                    f"bs={B}/GPU, fwd+BCE+Dice+bwd+AdamW, f32 MFMA (not a BASELINE config; "
+                    f"step_conv_* over the unpadded FLOPs)")
+        mname = f"mod.ResUNet(in=1,out=1,base_filters={args.base},depth={args.depth})"
     elif c4:
         metric = f"images/sec fwd+bwd, mod.UNet(base 128, depth 5) {S}x{S}x1 bs={B}/GPU"
         if bf16:

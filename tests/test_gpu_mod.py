@@ -372,9 +372,11 @@ def test_mod_narrow_one_step_matches_golden(golden_dir, tag, base):
                       GRAD_TOL, tag)
 
 
-@pytest.mark.parametrize("base,depth,H,W", [(16, 5, 64, 96), (24, 4, 128, 64), (48, 6, 128, 256)])
+@pytest.mark.parametrize("base,depth,H,W", [(16, 5, 64, 96), (24, 4, 128, 64), (48, 6, 128, 256),
+                                            (32, 4, 64, 64)])
 def test_mod_narrow_full_grads_vs_fp64(base, depth, H, W):
-    """Every gradient element of narrow networks (padded inside the library) against the
+    """Every gradient element of narrow networks (base 32 native on the 32-channel tiles;
+    16 / 24 padded to 32 and 48 to 64 inside the library) against the
     fp64 oracle, and the padding is invisible in the caller's arenas (torch-layout
     gradients, running stats).  At depth 6 the bottleneck BN sees 16 values per channel,
     where a near-zero ReLU input flips under any fp32 rounding change: the envelope is 2x

@@ -97,7 +97,7 @@ def _to64(d):
     return {k: (v.double() if v.is_floating_point() else v.clone()) for k, v in d.items()}
 
 
-@pytest.mark.parametrize("base,depth,size", [(64, 3, 64), (64, 5, 128)])
+@pytest.mark.parametrize("base,depth,size", [(64, 3, 64), (64, 5, 128), (32, 4, 64)])
 def test_res_full_grads_vs_oracle(base, depth, size):
     """Every element of every gradient vs the oracle (depth 5 = the reference default).
 

@@ -1046,18 +1046,27 @@ using RowTile11 = RowTile<128, 128, 64, 64, 32, false, 1, true>;  // t4 + MFMA-p
 using RowTile12 = RowTile<128, 64, 64, 32, 32, false, 1, true>;   // t1 + MFMA-phase priority
 // (r02: 256x128 with 4 waves of 128x64, 128x128 with 2 waves of 128x64 and 128x64 with 2
 // waves of 64x64 measured 3-17 % slower than these defaults; not kept)
+// 32-output tiles (the 32-channel level 0 of the reference grid's narrow networks,
+// config/config.yaml base_filters 16 / 24 / 32, padded to 32): 128 x 32 (2 waves) and
+// 256 x 32 (4 waves), two LDS images
+using RowTile13 = RowTile<128, 32, 64, 32, 32, true, 2>;
+using RowTile14 = RowTile<256, 32, 64, 32, 32, true>;
 #define ROWGEMM_TILES(X) \
     X(0, RowTile0) X(1, RowTile1) X(2, RowTile2) X(3, RowTile3) X(4, RowTile4) X(5, RowTile5) \
     X(6, RowTile6) X(7, RowTile7) X(8, RowTile8) X(9, RowTile9) X(10, RowTile10)            \
-    X(11, RowTile11) X(12, RowTile12)
+    X(11, RowTile11) X(12, RowTile12) X(13, RowTile13) X(14, RowTile14)
 
 template <int AMODE, int AOP, int EMODE, class T, bool BF>
 static int rowgemm_go(const RowGemmArgs& a, hipStream_t s) {
-    if (a.N % T::BN || a.K % T::BK || a.C % T::BK) return -1;
-    if (EMODE == E_CONVT && (a.cout % T::BN)) return -1;
-    const dim3 grid(((a.M + T::BM - 1) / T::BM) * (a.N / T::BN));
-    hipLaunchKernelGGL((rowgemm_kernel<AMODE, AOP, EMODE, T, BF>), grid, dim3(T::THREADS), 0, s, a);
-    return (int)hipGetLastError();
+    if constexpr (BF && T::BN < 64) {  // the bf16 B loader needs 64-column tiles
+        return -1;
+    } else {
+        if (a.N % T::BN || a.K % T::BK || a.C % T::BK) return -1;
+        if (EMODE == E_CONVT && (a.cout % T::BN) && (T::BN % a.cout)) return -1;  // per-column map
+        const dim3 grid(((a.M + T::BM - 1) / T::BM) * (a.N / T::BN));
+        hipLaunchKernelGGL((rowgemm_kernel<AMODE, AOP, EMODE, T, BF>), grid, dim3(T::THREADS), 0, s, a);
+        return (int)hipGetLastError();
+    }
 }
 
 template <int AMODE, int AOP, int EMODE, bool BF>
@@ -1235,9 +1244,13 @@ using WgTile4 = WgTile<64, 64, 32, 32, 32>;    // 4 waves, 32x32 per wave
 using WgTile5 = WgTile<128, 64, 64, 32, 32>;   // 4 waves
 using WgTile6 = WgTile<128, 128, 64, 64, 32, 3>;  // 3 waves / SIMD
 using WgTile7 = WgTile<64, 64, 32, 32, 32, 3>;
+// 32-channel operands (narrow level 0): 64 x 32 (2 waves), 32 x 32 (1 wave); ids 10.. are
+// the channel-major wgradT tiles
+using WgTile8 = WgTile<64, 32, 32, 32, 32>;
+using WgTile9 = WgTile<32, 32, 32, 32, 32>;
 #define WGRAD_TILES(X) \
     X(0, WgTile0) X(1, WgTile1) X(2, WgTile2) X(3, WgTile3) X(4, WgTile4) X(5, WgTile5) \
-    X(6, WgTile6) X(7, WgTile7)
+    X(6, WgTile6) X(7, WgTile7) X(8, WgTile8) X(9, WgTile9)
 
 #define WG_DIMS_R3(id, T) \
     if (tile == id) {     \

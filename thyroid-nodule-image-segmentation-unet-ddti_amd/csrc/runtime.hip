@@ -109,6 +109,7 @@ struct Options {
     int tile_n64 = 19;         // ... N = 64 outputs (forward-type)
     int tile_n64_dgrad = 1;    // ... N = 64, dgrad-type
     int tile_convt64 = 1;      // ConvT forward with 64 output channels (grid N = 256)
+    int tile_n32 = 14;         // f32 row GEMMs with 32 outputs (256 x 32, 4 waves)
     int tile_convt = -1;       // ConvT forward, >= 128 output channels (-1 = tile_n128's)
     int tile_convt_dgrad = -1; // ConvT input gradient (-1 = tile_n128_dgrad's)
     int tile16_n128 = 6;       // register-staged bf16 row-GEMM tiles
@@ -147,7 +148,7 @@ const OptionDesc OPTION_TABLE[] = {
     {"wgrad16_tile", &Options::wgrad16_tile},   {"tile_n128", &Options::tile_n128},
     {"tile_n128_dgrad", &Options::tile_n128_dgrad}, {"tile_n64", &Options::tile_n64},
     {"tile_n64_dgrad", &Options::tile_n64_dgrad}, {"tile_convt64", &Options::tile_convt64},
-    {"tile_convt", &Options::tile_convt},       {"tile_convt_dgrad", &Options::tile_convt_dgrad},
+    {"tile_convt", &Options::tile_convt},       {"tile_n32", &Options::tile_n32},       {"tile_convt_dgrad", &Options::tile_convt_dgrad},
     {"tile16_n128", &Options::tile16_n128},     {"tile16_n128_dgrad", &Options::tile16_n128_dgrad},
     {"tile16_n64", &Options::tile16_n64},       {"rg16", &Options::rg16},
     {"rg16_tile", &Options::rg16_tile},         {"rg16_ra", &Options::rg16_ra},         {"wg16", &Options::wg16},
@@ -546,6 +547,10 @@ WgradCfg wgrad_cfg(const unet_ctx* c, int CA, int tapsA, int CB, int tapsB, int6
             w.tile = tw;
         else if (CA % 64 == 0 && CB % 64 == 0 && (CA % 128 || CB % 128) && tn >= 0)
             w.tile = (CA % 128 == 0) ? 5 : (CB % 128 == 0 ? 3 : tn);
+        else if (CA % 64)  // 32-channel operands (narrow networks' level 0)
+            w.tile = 9;
+        else if (CB % 64)
+            w.tile = 8;
         else
             w.tile = 7;
         const bool row3 = tapsA == 9 && tapsB == 1 && row_w > 0 && row_w % 32 == 0 &&
@@ -837,6 +842,7 @@ struct Launcher {
 int pick_tile(const unet_ctx* c, int N, bool dgrad, bool bf16, bool convt = false) {
     const Options& o = c->opt;
     if (bf16) return N % 128 == 0 ? (dgrad ? o.tile16_n128_dgrad : o.tile16_n128) : o.tile16_n64;
+    if (N % 64) return o.tile_n32;  // 32 outputs (narrow networks' level 0)
     if (N % 128) return convt && !dgrad ? o.tile_convt64 : (dgrad ? o.tile_n64_dgrad : o.tile_n64);
     if (convt && !dgrad && o.tile_convt >= 0) return o.tile_convt;
     if (convt && dgrad && o.tile_convt_dgrad >= 0) return o.tile_convt_dgrad;
@@ -1819,26 +1825,27 @@ int unet_create(const unet_cfg* cfg, int device, unet_ctx** out) {
             }
         }
         // The first conv kernel is specialised for a single input channel (every BASELINE
-        // config); the GEMM tiles need 64-multiples of channels at every level and the
+        // config); the GEMM tiles need 32-multiples of channels at every level (32-output
+        // row tiles 13 / 14 and 32-channel wgrad tiles 8..10 for a 32-channel level 0) and the
         // channel-quad row kernels (pool, head, BN backward) a power-of-two channel count,
-        // so the kernels run base 64, 128 or 256.  Other base_filters (the reference grid's
-        // 16 / 24 / 32 / 48, config/config.yaml; any multiple of 8 up to 256) run padded
-        // to the next power of two >= 64 (unet_ctx::padded); the head's fused BN-partials
-        // path handles up to 4 classes.
+        // so the kernels run base 32, 64, 128 or 256.  Other base_filters (the reference
+        // grid's 16 / 24 / 48, config/config.yaml; any multiple of 8 up to 256) run padded to
+        // the next power of two >= 32 (unet_ctx::padded); the head's fused BN-partials path
+        // handles up to 4 classes.
         c->rbase = c->base;
         if (c->base >= 8 && c->base <= 256 && c->base % 8 == 0) {
-            int pb = 64;
+            int pb = 32;
             while (pb < c->base) pb <<= 1;
             c->padded = pb != c->base;
             c->base = pb;
         }
         if ((c->variant != UNET_VARIANT_MODEL && c->variant != UNET_VARIANT_MOD &&
              c->variant != UNET_VARIANT_RES) || c->in_ch != 1 ||
-            c->out_ch < 1 || c->out_ch > 4 || c->base % 64 || c->base > 256 ||
+            c->out_ch < 1 || c->out_ch > 4 || c->base % 32 || c->base > 256 ||
             (c->base & (c->base - 1)) || c->depth < 1 ||
             c->depth > MAX_DEPTH || (c->base << c->depth) > 8192)
             return UNET_ERR_UNSUPPORTED;
-        if (c->padded && c->bf16)  // the bf16 kernels need 128-multiples of real channels
+        if ((c->padded || c->base < 64) && c->bf16)  // the bf16 kernels: 128-multiples of real channels
             return UNET_ERR_UNSUPPORTED;
         c->res = c->variant == UNET_VARIANT_RES;
         c->bn_relu = c->variant != UNET_VARIANT_MODEL;

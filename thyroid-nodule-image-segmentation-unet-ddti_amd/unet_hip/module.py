@@ -200,8 +200,8 @@ class ModUNet(_HipUNet):
     """models/mod.py:9-66 ``UNet(in_channels, out_channels, base_filters, depth)``.
 
     Supported here: in_channels 1, out_channels 1..4, base_filters a multiple of 8 up to
-    256 (64 / 128 / 256 natively; narrower widths such as the reference grid's 16 / 24 /
-    32 / 48 run zero-padded to the next power of two >= 64 inside the library), depth 1..6.
+    256 (32 / 64 / 128 / 256 natively; the reference grid's 16 / 24 / 48 run zero-padded to
+    the next power of two >= 32 inside the library), depth 1..6.
 
     ``mfma_dtype``: "fp32" (default; exact f32 products like the reference) or "bf16"
     (BASELINE config 4: conv GEMM operands rounded to bf16, f32 accumulate; parameters,
