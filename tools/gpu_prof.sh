@@ -4,7 +4,7 @@ set -u
 R=$GRAFT_REPO_ROOT
 TAG=${1:-prof}
 cd /tmp && export TMPDIR=/tmp
-for C in c2 c4; do
+for C in ${CONFIGS:-c2 c4}; do
   if [ $C = c2 ]; then ARGS="--steps 3 --warmup 1 --no-cpu-baseline"; else ARGS="--config 4 --mfma bf16 --steps 2 --warmup 1 --no-cpu-baseline"; fi
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/$TAG.$C.prof -o run --output-format csv -- python3 $R/bench.py $ARGS > $R/gpurun_out/$TAG.$C.prof.log 2>&1
   rc=$?
