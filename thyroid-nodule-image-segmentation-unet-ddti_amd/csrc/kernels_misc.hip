@@ -72,18 +72,21 @@ __device__ void pack_conv3_tile(const float* __restrict__ w, OUT* __restrict__ w
 // ConvT: one block per LDS tile of 32 ci x 32 co x 4 taps (ab).  The torch rows (co, ab
 // contiguous per ci) are read with unit stride; Tf rows (ab, co) are written as 32-element ci
 // runs and Td rows (ci) as 32-element co runs per ab (the element-wise form scattered every
-// Tf element cin apart).  Row stride 129 floats: both LDS read patterns are conflict-free.
+// Tf element cin apart).  LDS tile [ci_l][ab][co_l], ab stride 40, row stride 161 floats:
+// the fill (lanes over (co_l, ab)), the Tf read (lanes over ci) and the Td read (lanes over
+// co) are all conflict-free (the r02 [ci_l][co_l * 4 + ab] image read Td at a 4-float lane
+// stride: 4-way conflicts, 4.19 M extra LDS cycles per config-4 repack).
 template <class OUT>
 __device__ void pack_convT_tile(const float* __restrict__ w, OUT* __restrict__ tf,
                                 OUT* __restrict__ td, int cin, int cout, int co0, int ci0,
                                 float* tile) {
-    constexpr int T = 32, RS = T * 4 + 1;  // tile: [ci_l][co_l * 4 + ab]
+    constexpr int T = 32, AS = 40, RS = 4 * AS + 1;  // tile: [ci_l][ab][co_l]
     const int nci = min(T, cin - ci0), nco = min(T, cout - co0);
     const int tid = threadIdx.x;
     for (int e = tid; e < T * T * 4; e += 256) {  // e = ci_l * 128 + (co_l * 4 + ab)
         const int ci_l = e / (T * 4), r = e - ci_l * (T * 4);
         if (ci_l < nci && r < nco * 4)
-            tile[ci_l * RS + r] = w[((int64_t)(ci0 + ci_l) * cout + co0) * 4 + r];
+            tile[ci_l * RS + (r & 3) * AS + (r >> 2)] = w[((int64_t)(ci0 + ci_l) * cout + co0) * 4 + r];
     }
     __syncthreads();
     const int l = tid & 31, g = tid >> 5;  // 8 groups of 32 lanes
@@ -91,14 +94,14 @@ __device__ void pack_convT_tile(const float* __restrict__ w, OUT* __restrict__ t
     for (int row = g; row < 4 * T; row += 8) {
         const int ab = row / T, co_l = row - ab * T;
         if (co_l < nco && l < nci)
-            tf[((int64_t)ab * cout + co0 + co_l) * cin + ci0 + l] = (OUT)tile[l * RS + co_l * 4 + ab];
+            tf[((int64_t)ab * cout + co0 + co_l) * cin + ci0 + l] = (OUT)tile[l * RS + ab * AS + co_l];
     }
     if (!td) return;
     // Td[ci][ab * cout + co]: rows (ci_l, ab), lanes over co
     for (int row = g; row < 4 * T; row += 8) {
         const int ci_l = row >> 2, ab = row & 3;
         if (ci_l < nci && l < nco)
-            td[(int64_t)(ci0 + ci_l) * 4 * cout + ab * cout + co0 + l] = (OUT)tile[ci_l * RS + l * 4 + ab];
+            td[(int64_t)(ci0 + ci_l) * 4 * cout + ab * cout + co0 + l] = (OUT)tile[ci_l * RS + ab * AS + l];
     }
 }
 
