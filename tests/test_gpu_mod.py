@@ -270,10 +270,48 @@ def test_rg16_tile_choice_is_numerically_invisible(side):
         _assert_same(outs[0], outs[tile], f"{side}^2 tile {tile} vs 0")
 
 
+def test_rg16_halo_tile_within_bf16_error():
+    """Tile 19 (the tap-row halo kernel, kernels_gemm16.hip rowgemm16_row3_kernel) sums K in
+    the order (tap row, channel slice, tap column) instead of the one-tap kernel's (tap,
+    channel), so it is not bit-identical to tile 4.  BASELINE config 4's network at 256^2
+    (halo levels W = 256 .. 16; the 8x8 bottleneck falls back to the one-tap tile), one
+    training step: its distance from tile 4 must stay below the distance of tile 4 itself
+    from the fp32-MFMA network (the bf16 rounding error the path already carries), for the
+    logits and for every gradient (floor 1e-3 for near-zero BN-bias gradients)."""
+    x, t = inputs(37, 1, 256, 256)
+    P = MO.make_params(41, 128, 5)
+    outs = {}
+    for tile in (4, 19):
+        m = _bf16_model(P, 128, 5)
+        with options(m.flatten_().rt, rg16_tile=tile):
+            outs[tile] = _bf16_step(m, x, t)
+        del m
+    import unet_hip
+    m = unet_hip.ModUNet(1, 1, base_filters=128, depth=5)
+    sd = m.state_dict()
+    for k, v in P.items():
+        sd[k] = v.clone()
+    m.load_state_dict(sd)
+    f32 = _bf16_step(m.to(DEV).train(), x, t)
+    e_l = rel_max(outs[19][0].cpu(), outs[4][0].cpu())
+    b_l = rel_max(outs[4][0].cpu(), f32[0].cpu())
+    print(f"logits: halo vs one-tap {e_l:.3e}, bf16 vs fp32 {b_l:.3e}")
+    assert e_l <= b_l, (e_l, b_l)
+    worst = []
+    for k, g4 in outs[4][1].items():
+        e = norm_rel(outs[19][1][k].cpu(), g4.cpu())
+        b = norm_rel(g4.cpu(), f32[1][k].cpu())
+        worst.append((e / max(b, 1e-3), k, e, b))
+    worst.sort(reverse=True)
+    print("worst grads (ratio, name, halo-vs-one-tap, bf16-vs-fp32):", worst[:4])
+    assert worst[0][0] <= 1.0, worst[:4]
+
+
 @pytest.mark.parametrize("base,depth,tile", [(64, 3, "4"), (128, 5, "0"), (128, 5, "2"), (128, 5, "4"),
                                              (128, 5, "6"), (128, 5, "7"),
                                              (128, 5, "9"), (128, 5, "10"), (128, 5, "14"),
-                                             (128, 5, "15"), (128, 5, "18"), (128, 5, "auto")])
+                                             (128, 5, "15"), (128, 5, "18"), (128, 5, "19"),
+                                             (128, 5, "auto")])
 def test_mod_bf16_matches_bf16_oracle(base, depth, tile):
     """mfma_dtype="bf16": one step at B=2 64x64 vs the oracle that rounds exactly the GEMM
     operands the HIP bf16 kernels round (oracle/mod_ref_cpu.py, bf16=True).
@@ -288,7 +326,7 @@ def test_mod_bf16_matches_bf16_oracle(base, depth, tile):
     per-GEMM choice (rg16_tile, runtime.hip) and default wgrad tile."""
     import unet_hip
     opts = {} if tile == "auto" else dict(
-        rg16_tile=int(tile), wg16_tile=2 if tile in ("4", "6", "7", "9", "10", "14", "18") else 0)
+        rg16_tile=int(tile), wg16_tile=2 if tile in ("4", "6", "7", "9", "10", "14", "18", "19") else 0)
     P = MO.make_params(42, base, depth)
     x, t = inputs(5, 2, 64, 64)
     ref = MO.train_step(P, MO.init_buffers(base, depth), None, x, t, depth=depth, bf16=True)

@@ -683,6 +683,29 @@ def test_pipe_gemm_bit_identical(variant, B, H, W):
         assert torch.equal(outs[0][1], outs[i][1]), (i, d)
 
 
+@pytest.mark.parametrize("B,H,W", [(2, 64, 64), (8, 256, 256), (1, 48, 80)])
+def test_dz_in_wgrad_bit_identical(B, H, W):
+    """Option dz_in_wgrad: the weight gradient's B' loader forms the BN-backward dz from do
+    and y (the same bn_dz4 helper as the bn_dz pass) and its first A'-tile blocks store it
+    for the dgrad, so the bn_dz pass disappears.  The stored dz, the bias column sums and
+    every gradient are the same bits as with the separate pass (models/model.py order)."""
+    import unet_hip
+    from _helpers import options
+    x, t = inputs(47, B, H, W)
+    outs = []
+    for flag in (0, 1):
+        m = hip_model(O.make_params(42), DEV)
+        with options(m.flatten_().rt, dz_in_wgrad=flag):
+            logits = m(x.to(DEV))
+            l = unet_hip.seg_losses(logits, t.to(DEV))
+            (l[0] + l[1]).backward()
+            torch.cuda.synchronize()
+        outs.append((logits.detach().clone(), m._state.grad_arena.clone()))
+        del m
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1]), (outs[0][1] - outs[1][1]).abs().max().item()
+
+
 @pytest.mark.parametrize("variant,B,H,W,dzl", [("model", 2, 64, 64, 0), ("model", 4, 128, 128, 0),
                                                ("model", 2, 64, 64, 1), ("mod", 2, 128, 64, 0),
                                                ("res", 2, 64, 64, 0)])

@@ -110,6 +110,8 @@ struct WgradArgs {
     int bf16;            // bf16 MFMA (operands rounded to bf16 in LDS, f32 accumulate)
     const void* zero16;  // wgrad16: >= 16 zero bytes (padding taps / pixels past the split)
     int xcd;             // remap blocks so each XCD gets a contiguous range of tiles
+    float* dzout;        // OP_DZ on B': the blocks of the first A' tile also store the dz
+    int lddz;            // they formed ([P][lddz], channels cb0..), for the dgrad to read
 };
 
 #define HIP_OK(x)                                   \

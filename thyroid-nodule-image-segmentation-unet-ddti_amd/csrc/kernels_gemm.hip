@@ -468,6 +468,8 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void wgrad_kernel(WgradArgs p) 
     const int nchunks = (pend - pbeg + BKP - 1) / BKP;
 
     f32x4 ryb[BDZ ? BP : 1];
+    int bm_row[BDZ ? BP : 1];
+    const bool dzw = BDZ && p.dzout != nullptr && tm == 0 && BMODE == G_IDENT;
     f32x4 ra[AP], rb[BP];
     unsigned amask = 0, bmask = 0;
     auto issue = [&](int pc) {
@@ -493,8 +495,10 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void wgrad_kernel(WgradArgs p) 
             const int src = gather_src<BMODE>(tapB, m, q, H, W, valid);
             bmask |= (valid && in) ? (1u << i) : 0u;
             rb[i] = *(const f32x4*)(p.b + (size_t)src * p.ldb + p.boff + cb0 + bc4 * 4);
-            if constexpr (BDZ)
+            if constexpr (BDZ) {
                 ryb[i] = *(const f32x4*)(p.by + (size_t)src * p.ldby + p.offby + cb0 + bc4 * 4);
+                bm_row[i] = src;
+            }
         }
     };
     auto commit = [&]() {
@@ -517,6 +521,9 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void wgrad_kernel(WgradArgs p) 
                 const f32x4 d = bn_dz4(ca, v, cb, ryb[i], cm, cc);
 #pragma unroll
                 for (int j = 0; j < 4; ++j) v[j] = ryb[i][j] > 0.f ? d[j] : 0.f;
+                // the first A' tile's blocks (tap 0, channels 0..BM) hand dz to the dgrad
+                if (dzw && ((bmask >> i) & 1u))
+                    *(f32x4*)(p.dzout + (size_t)bm_row[i] * p.lddz + cb0 + bc4 * 4) = v;
             }
             if (!((bmask >> i) & 1u)) v = f32x4{0.f, 0.f, 0.f, 0.f};
             if (bsum)
@@ -660,6 +667,8 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void wgrad_row3_kernel(WgradArg
     const int nchunks = (pend - pbeg + BKP - 1) / BKP;
 
     f32x4 ryb[BDZ ? BP : 1];
+    int bm_row[BDZ ? BP : 1];
+    const bool dzw = BDZ && p.dzout != nullptr && tm == 0;
     f32x4 ra[AP], rb[BP];
     unsigned amask = 0, bmask = 0;
     auto issue = [&](int pc) {
@@ -684,8 +693,10 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void wgrad_row3_kernel(WgradArg
             m = in ? m : pend - 1;
             bmask |= in ? (1u << i) : 0u;
             rb[i] = *(const f32x4*)(p.b + (size_t)m * p.ldb + p.boff + cb0 + bc4 * 4);
-            if constexpr (BDZ)
+            if constexpr (BDZ) {
                 ryb[i] = *(const f32x4*)(p.by + (size_t)m * p.ldby + p.offby + cb0 + bc4 * 4);
+                bm_row[i] = m;
+            }
         }
     };
     auto commit = [&]() {
@@ -710,6 +721,9 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void wgrad_row3_kernel(WgradArg
                 const f32x4 d = bn_dz4(ca, v, cb, ryb[i], cm, cc);
 #pragma unroll
                 for (int j = 0; j < 4; ++j) v[j] = ryb[i][j] > 0.f ? d[j] : 0.f;
+                // the first A' tile's blocks (tap row 0, channels 0..BM) hand dz to the dgrad
+                if (dzw && ((bmask >> i) & 1u))
+                    *(f32x4*)(p.dzout + (size_t)bm_row[i] * p.lddz + cb0 + bc4 * 4) = v;
             }
             if (!((bmask >> i) & 1u)) v = f32x4{0.f, 0.f, 0.f, 0.f};
             if (bsum)

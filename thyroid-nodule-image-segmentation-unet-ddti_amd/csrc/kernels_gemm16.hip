@@ -501,6 +501,162 @@ __global__ __launch_bounds__(512, 1) void rowgemm16_pp_kernel(RowGemmArgs p) {
     row_epilogue<EMODE, BM, BN, WM, WN, true>(p, acc, m0, n0, tile_m, wm, wn, lane, tid, (float*)smem);
 }
 
+// ------------------------------------------------------------------------------------
+// Tap-row halo variant of the 3x3 conv GEMM (tile 19, G_CONV3 only, W >= 16).  The
+// one-tap kernel restages the block's 256 A rows for each of the 9 taps; here a stage holds
+// the HALO of one tap row dy -- the block's image rows shifted by dy - 1, one extra pixel
+// either side (ROWS x (SEG + 2) rows, <= 288) -- with the B rows of the three taps (dy, 0..2),
+// and the three dx taps read A rows h + dx from the same halo.  Per 32-channel stage: 17-18
+// A + 48 B DMA pieces of 1 KB feed 48 MFMAs per wave (one-tap kernel: 32 + 32 pieces per 32
+// MFMAs), i.e. 25 % fewer LDS-DMA bytes per MFMA and 1.5x the MFMAs between barriers.
+//   geometry: SEG = min(W, 256) output pixels per image row of the tile, ROWS = 256 / SEG
+//   (W a power of two: a tile is ROWS whole rows, or half a 512-pixel row); halo row
+//   h = r (SEG + 2) + xl + 1 holds pixel (row r shifted by dy - 1, column x0 + xl),
+//   xl = -1 .. SEG; output pixel (r, xo) reads halo row r (SEG + 2) + xo + dx for tap dx.
+//   LDS rows are 64 B (32 bf16); chunk c of row r sits in slot c ^ ((r >> 2) & 3), which
+//   keeps the shifted, row-jumping A reads at most 2-way conflicted (W = 16; none otherwise).
+//   K order: dy, 32-channel slice, dx, k -- a reordering of the one-tap kernel's sum, so
+//   results agree with the other tiles to fp32 rounding, not bitwise.
+// ------------------------------------------------------------------------------------
+template <int EMODE>
+__global__ __launch_bounds__(512, 1) void rowgemm16_row3_kernel(RowGemmArgs p) {
+    constexpr int BM = 256, BN = 256, WM = 128, WN = 64, BK = 32, WAVES = 8, WAVES_N = 4;
+    constexpr int MT = WM / 32, NT = WN / 32;
+    constexpr int RB = 2 * BK, LPR = RB / 16, RPI = 64 / LPR;  // 64-B rows, 16 rows / piece
+    auto swz = [](int r) { return (r >> 2) & 3; };
+    constexpr int AR = 288;                   // halo rows held (W = 16: 16 x 18)
+    constexpr int AI = 3;                     // A pieces per wave (pieces w, w + 8, w + 16)
+    constexpr int BR = 3 * BN;                // B rows: taps dx = 0..2 x 256 outputs
+    constexpr int BI = BR / (RPI * WAVES);    // 6
+    static_assert(BI * RPI * WAVES == BR && (AR / RPI) <= AI * WAVES, "loader shape");
+    constexpr int STAGE = (AR + BR) * RB;     // 66 KB
+    constexpr int SMEM = 2 * STAGE;
+    static_assert(SMEM >= 2 * (BM / 64) * BN * 8, "epilogue scratch");
+    __shared__ __attribute__((aligned(1024))) char smem[SMEM];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+    const int ntn = p.N / BN;
+    const int bid = p.xcd ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+    const int tile_m = bid / ntn, tile_n = bid - tile_m * ntn;
+    const int m0 = tile_m * BM, n0 = tile_n * BN;
+    const int H = p.H, W = p.W, C = p.C, K = p.K;
+    const int SEG = W < BM ? W : BM, HW = SEG + 2;
+    const int AROWS = (BM / SEG) * HW;
+    const int NA = (AROWS + RPI - 1) / RPI;           // A pieces per stage (17 or 18)
+    const bool a3 = 2 * WAVES + wave < NA;            // this wave issues a third A piece
+
+    const int lr = lane / LPR, slot = lane % LPR;
+    int acen[AI], ayr[AI], ach[AI];  // pixel at dy = 1 (-1: padding), its image row, chunk
+#pragma unroll
+    for (int j = 0; j < AI; ++j) {
+        const int h = (j * WAVES + wave) * RPI + lr;
+        const int r = h / HW, xl = h - r * HW - 1;
+        const int mrow = m0 + r * SEG;  // first output pixel of the tile's image row r
+        bool ok = h < AROWS && mrow < p.M;
+        const Pix q = decode(ok ? mrow : 0, H, W);
+        ok = ok && q.x + xl >= 0 && q.x + xl < W;
+        acen[j] = ok ? mrow + xl : -1;
+        ayr[j] = q.y;
+        ach[j] = (slot ^ swz(h)) * 8;
+    }
+    const uint16_t* bsrc[BI];
+#pragma unroll
+    for (int j = 0; j < BI; ++j) {
+        const int rb = (j * WAVES + wave) * RPI + lr;
+        const int dx = rb / BN, nl = rb - dx * BN;
+        bsrc[j] = p.bt16 + (size_t)(n0 + nl) * K + dx * C + (slot ^ swz(rb)) * 8;
+    }
+    const uint16_t* zero = (const uint16_t*)p.zero16;
+    const int CC = C / BK;  // channel slices per tap row
+    auto issue = [&](int s) {
+        const int dy = s / CC, c0 = (s - dy * CC) * BK;
+        char* base = smem + (s & 1) * STAGE;
+#pragma unroll
+        for (int j = 0; j < AI; ++j) {
+            if (j == AI - 1 && !a3) continue;
+            const int yy = ayr[j] + dy - 1;
+            const bool valid = acen[j] >= 0 && yy >= 0 && yy < H;
+            const uint16_t* g =
+                valid ? p.a16 + (size_t)(acen[j] + (dy - 1) * W) * p.lda + c0 + ach[j] : zero;
+            glds16(g, base + (j * WAVES + wave) * 1024);
+        }
+        const int kb = dy * 3 * C + c0;
+#pragma unroll
+        for (int j = 0; j < BI; ++j) glds16(bsrc[j] + kb, base + AR * RB + (j * WAVES + wave) * 1024);
+    };
+
+    f32x16 acc[MT][NT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    const int lh = lane >> 5, li = lane & 31;
+    int ahb[MT], bro[NT], bfx[NT];  // halo row of output pixel at dx = 0; B row offsets
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+        const int mo = wm * WM + mt * 32 + li;
+        const int r = mo / SEG;
+        ahb[mt] = r * HW + (mo - r * SEG);
+    }
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+        const int r = wn * WN + nt * 32 + li;
+        bro[nt] = (AR + r) * RB;
+        bfx[nt] = swz(r);  // rows dx * 256 + r share it
+    }
+
+    const int ns = 3 * CC;
+    issue(0);
+    for (int s = 0; s < ns; ++s) {
+        if (s + 1 < ns) {
+            issue(s + 1);
+            if (a3) wait_vm<AI + BI>();
+            else wait_vm<AI - 1 + BI>();
+        } else {
+            wait_vm<0>();
+        }
+        block_barrier();
+        const char* base = smem + (s & 1) * STAGE;
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+            for (int kk = 0; kk < BK / 16; ++kk) {
+                const int c = kk * 2 + lh;
+                bf16x8 af[MT], bfr[NT];
+#pragma unroll
+                for (int mt = 0; mt < MT; ++mt) {
+                    const int h = ahb[mt] + dx;
+                    af[mt] = *(const bf16x8*)(base + h * RB + ((c ^ swz(h)) << 4));
+                }
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt)
+                    bfr[nt] = *(const bf16x8*)(base + bro[nt] + dx * BN * RB + ((c ^ bfx[nt]) << 4));
+#pragma unroll
+                for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                    for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma32_bf16(af[mt], bfr[nt], acc[mt][nt]);
+            }
+        // this stage's ds_reads must have returned before any wave restages it
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        block_barrier();
+    }
+    row_epilogue<EMODE, BM, BN, WM, WN, true>(p, acc, m0, n0, tile_m, wm, wn, lane, tid, (float*)smem);
+}
+
+template <int EMODE>
+static int rg16r3_go(const RowGemmArgs& a, hipStream_t s) {
+    // 256 % W == 0 or W % 256 == 0 keeps a tile on whole rows / half rows; W >= 16 bounds the halo
+    if (a.amode != G_CONV3 || a.N % 256 || a.C % 32 || a.K != 9 * a.C) return -1;
+    if (a.W < 16 || (256 % a.W && a.W % 256)) return -1;
+    const dim3 grid(((a.M + 255) / 256) * (a.N / 256));
+    hipLaunchKernelGGL((rowgemm16_row3_kernel<EMODE>), grid, dim3(512), 0, s, a);
+    return (int)hipGetLastError();
+}
+
 template <int AMODE, int EMODE>
 static int rg16pp_go(const RowGemmArgs& a, hipStream_t s) {
     if (a.N % 256 || a.C % 64 || a.K % 64) return -1;
@@ -554,6 +710,10 @@ static int rg16_go(const RowGemmArgs& a, hipStream_t s) {
 template <int AMODE, int EMODE>
 static int rg16_tile(const RowGemmArgs& a, int tile, hipStream_t s) {
     if (tile == 18) return rg16pp_go<AMODE, EMODE>(a, s);
+    if (tile == 19) {
+        if constexpr (AMODE == G_CONV3) return rg16r3_go<EMODE>(a, s);
+        return -1;
+    }
 #define RG16_CASE(id, T) \
     if (tile == id) return rg16_go<AMODE, EMODE, T>(a, s);
     ROWGEMM16_TILES(RG16_CASE)
@@ -809,7 +969,7 @@ int wgrad16g_tile_dims(int tile, int* bm, int* bn, int* stages) {
 }
 
 int rowgemm16_tile_dims(int tile, int* bm, int* bn, int* stages) {
-    if (tile == 18) {  // ping-pong 256x256 (rowgemm16_pp_kernel)
+    if (tile == 18 || tile == 19) {  // ping-pong / tap-row halo 256x256
         *bm = *bn = 256;
         if (stages) *stages = 2;
         return 0;

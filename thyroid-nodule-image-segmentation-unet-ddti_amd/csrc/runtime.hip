@@ -121,6 +121,7 @@ struct Options {
     int rg16_xp = 0;           // speed-of-light ablation of the forward rg16 GEMMs (garbage
                                // results; A/B timing only, kernels_gemm16.hip XP)
     int rg16_pp = 0;           // 256x256 GEMMs on the ping-pong kernel (tile 18)
+    int rg16_r3 = 0;           // 256x256 3x3-conv GEMMs (W >= 16) on the tap-row halo kernel (tile 19)
     int rg16_m16 = 0;          // per-GEMM choice on the 16x16x32-MFMA tiles: 1 = 14 / 15,
                                // 2 = with s_setprio around the MFMAs (16 / 17)
     int wg16 = 1;              // bf16 3x3 wgrad on the LDS-DMA transposed-read kernel
@@ -132,6 +133,8 @@ struct Options {
                                // 2.02 -> 0.97 GB at equal time), 2 row GEMMs, 3 wgrad
     int wgrad_stream = 0;      // weight gradients on a second stream (bit-identical)
     int dz_in_loaders = 0;     // BN-backward dz inside the GEMM loaders (model.py order)
+    int dz_in_wgrad = 0;       // BN-backward dz formed by the weight gradient's B' loader, which
+                               // also stores it for the dgrad (no bn_dz pass; model.py order)
     int row3_gemm = 0;         // f32 3x3 forward / dgrad on the tap-row kernel
                                // (rowgemm_row3_kernel) where its shapes allow
 };
@@ -153,10 +156,11 @@ const OptionDesc OPTION_TABLE[] = {
     {"tile16_n64", &Options::tile16_n64},       {"rg16", &Options::rg16},
     {"rg16_tile", &Options::rg16_tile},         {"rg16_ra", &Options::rg16_ra},         {"wg16", &Options::wg16},
     {"rg16_m16", &Options::rg16_m16},         {"rg16_xp", &Options::rg16_xp},
-    {"rg16_pp", &Options::rg16_pp},
+    {"rg16_pp", &Options::rg16_pp},           {"rg16_r3", &Options::rg16_r3},
     {"wg16_tile", &Options::wg16_tile},         {"wg16t", &Options::wg16t},
     {"xcd16", &Options::xcd16},                 {"xcd_remap", &Options::xcd_remap},
     {"wgrad_stream", &Options::wgrad_stream},   {"dz_in_loaders", &Options::dz_in_loaders},
+    {"dz_in_wgrad", &Options::dz_in_wgrad},
     {"row3_gemm", &Options::row3_gemm},
 };
 
@@ -494,6 +498,7 @@ struct Plan {
     float* hpart;  // head / conv-first weight-gradient partials
     float* bslab;  // [splits][Nw] bias-gradient column sums from the wgrad kernels
     float* coef;
+    float* gdz;    // option dz_in_wgrad: the dz the weight gradient stores for the dgrad
     // bf16 LDS-DMA GEMMs: prepared operand image (dense [pixels][C] bf16) and a zero page
     uint16_t* s16;
     void* zero16;
@@ -610,6 +615,7 @@ int rg16_tile(const unet_ctx* c, const RowGemmArgs& g) {
     auto fits = [&](int t) {
         int bm = 0, bn = 0;
         if (rowgemm16_tile_dims(t, &bm, &bn) != 0) return false;
+        if (t == 19 && (g.amode != G_CONV3 || g.W < 16 || (256 % g.W && g.W % 256))) return false;
         return g.N % bn == 0 && (cout == 0 || cout % bn == 0);
     };
     if (c->opt.rg16_tile >= 0) return fits(c->opt.rg16_tile) ? c->opt.rg16_tile : 0;
@@ -620,6 +626,7 @@ int rg16_tile(const unet_ctx* c, const RowGemmArgs& g) {
         t4 = c->opt.rg16_m16 == 2 ? 16 : 14;
     }
     if (c->opt.rg16_pp) t4 = 18;  // option rg16_pp: the ping-pong 256x256 kernel
+    if (c->opt.rg16_r3 && fits(19)) t4 = 19;  // option rg16_r3: the tap-row halo kernel
     if (!fits(4)) return t0;
     const int64_t blocks = (g.M + 255) / 256 * (g.N / 256);
     if (blocks < 256) return t0;
@@ -785,7 +792,9 @@ void make_plan(unet_ctx* c, int N, int H, int W, bool training, char* base, Plan
                                 std::max<int64_t>(10 * c->base, (int64_t)c->out_ch * (c->base + 1)));
         p.bslab = b.take<float>(std::max<int64_t>(bmax, 1));
         p.coef = b.take<float>(4 * (int64_t)c->cmax);  // BN-backward dz coefficients [4][C]
+        p.gdz = (c->opt.dz_in_wgrad && !c->bn_relu && !c->bf16) ? b.take<float>(gmax) : nullptr;
     } else {
+        p.gdz = nullptr;
         p.g[0] = p.g[1] = p.g[2] = p.slab = p.part = p.part2 = p.hpart = p.bslab = p.coef = nullptr;
         for (int l = 0; l < D; ++l) p.dcat[l] = nullptr;
     }
@@ -1327,7 +1336,15 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         // bf16 image of dz: A operand of the LDS-DMA dgrad, B' of the LDS-DMA wgrad; the f32
         // dz is still written when the register-staged kernel of either consumes it
         const bool dz16 = !dzc && (rg16_on(c, C.cout, C.cin) || p.x16[i]);
-        if (dz16) {
+        Operand a = conv_input(c, p, i);
+        WgradCfg wc = wgrad_cfg(c, C.cin, 9, C.cout, 1, P, c->bf16, Wl);
+        // option dz_in_wgrad: the weight gradient's B' loader forms dz from do and y (the
+        // bn_dz pass disappears) and its first A'-tile blocks store it for the dgrad; f32
+        // register-staged weight-gradient tiles only, model.py order, with a dgrad to feed
+        const bool dzw = p.gdz && !dz16 && !dzc && dx && !async_w &&
+                         (wc.tile < 10 || (wc.tile >= 20 && wc.tile < 30));
+        if (dzw) {
+        } else if (dz16) {
             const bool f32 = !p.x16[i] || !(dx && rg16_on(c, C.cout, C.cin));
             before_write(p.s16);
             before_write(dout);
@@ -1339,8 +1356,6 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
                                     p.coef, dz_mask, s));
         }
         side_after_main();
-        Operand a = conv_input(c, p, i);
-        WgradCfg wc = wgrad_cfg(c, C.cin, 9, C.cout, 1, P, c->bf16, Wl);
         WgradArgs w{};
         w.xcd = xcd_remap_wgrad(c);
         w.H = Hl;
@@ -1362,7 +1377,9 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         w.by = p.y[i];
         w.ldby = p.ldy[i];
         w.offby = p.offy[i];
-        w.bcoef = dzc;
+        w.bcoef = dzw ? p.coef : dzc;
+        w.dzout = dzw ? p.gdz : nullptr;
+        w.lddz = C.cout;
         w.bias_slab = C.b >= 0 ? p.bslab : nullptr;
         w.Mw = 9 * C.cin;
         w.Nw = C.cout;
@@ -1407,7 +1424,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
             g.M = (int)P;
             g.N = C.cin;
             g.K = 9 * C.cout;
-            g.a = dout;
+            g.a = dzw ? p.gdz : dout;
             g.lda = C.cout;
             g.aoff = 0;
             g.C = C.cout;
