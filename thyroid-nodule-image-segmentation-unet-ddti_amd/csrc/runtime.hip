@@ -133,8 +133,9 @@ struct Options {
                                // 2.02 -> 0.97 GB at equal time), 2 row GEMMs, 3 wgrad
     int wgrad_stream = 0;      // weight gradients on a second stream (bit-identical)
     int dz_in_loaders = 0;     // BN-backward dz inside the GEMM loaders (model.py order)
-    int dz_in_wgrad = 0;       // BN-backward dz formed by the weight gradient's B' loader, which
-                               // also stores it for the dgrad (no bn_dz pass; model.py order)
+    int dz_in_wgrad = 1;       // BN-backward dz formed by the weight gradient's B' loader, which
+                               // also stores it for the dgrad (no bn_dz pass; model.py order;
+                               // config 2: 77.96 -> 77.53 ms/step, gpurun_out n64 A/B)
     int row3_gemm = 0;         // f32 3x3 forward / dgrad on the tap-row kernel
                                // (rowgemm_row3_kernel) where its shapes allow
 };
@@ -974,7 +975,7 @@ std::string tlabel16(const char* fam, int tile, int layer) {
     int bm = 0, bn = 0, st = 0;
     rowgemm16_tile_dims(tile, &bm, &bn, &st);
     char b[112];
-    snprintf(b, sizeof b, "%s/rg16%s_%dx%ds%d|%d", fam, tile == 18 ? "pp" : tile >= 14 ? "m" : "",
+    snprintf(b, sizeof b, "%s/rg16%s_%dx%ds%d|%d", fam, tile == 19 ? "r3" : tile == 18 ? "pp" : tile >= 14 ? "m" : "",
              bm, bn, st, layer);
     return b;
 }
