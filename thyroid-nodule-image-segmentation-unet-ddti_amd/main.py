@@ -30,7 +30,7 @@ from models.mod import ResUNet  # noqa: E402
 from models.mod import UNet as ModUNet  # noqa: E402
 from models.model import UNet  # noqa: E402
 from utils.trainer import Trainer  # noqa: E402
-from utils.transforms import Compose, Resize, ToTensor  # noqa: E402
+from utils.transforms import Compose, Resize, ToTensor, build_train_transform  # noqa: E402
 from utils.utils import Config, create_logger, set_seed  # noqa: E402
 
 
@@ -89,17 +89,18 @@ def main(args):
     if args.model_type not in ("UNet", "ModUNet", "ResUNet"):
         raise SystemExit(f"model_type {args.model_type!r}: the HIP path has UNet (models/model.py), "
                          "ModUNet and ResUNet (models/mod.py)")
-    if args.use_elastic or args.use_speckle or args.use_tgc or args.use_clahe:
-        raise SystemExit("ultrasound augmentations need OpenCV/torchvision (not in this image)")
 
     S = args.image_size
     gpu_tf = args.gpu_transforms and not args.synthetic
     if args.synthetic:
         splits = [SyntheticSegmentation(args.synthetic, S, seed=s) for s in range(3)]
     else:
+        # main.py:99-100: augmentations on the training split only
         tf = DecodeU8() if gpu_tf else Compose([Resize((S, S)), ToTensor()])
+        train_tf = build_train_transform(config, (S, S), tail=[DecodeU8()] if gpu_tf else None)
         root = config.dataset_path
-        splits = [MedicalDataset(os.path.join(root, d), os.path.join(root, d + "_mask"), tf)
+        splits = [MedicalDataset(os.path.join(root, d), os.path.join(root, d + "_mask"),
+                                 train_tf if d == "train" else tf)
                   for d in ("train", "val", "test")]
     loaders = []
     for i, ds in enumerate(splits):
