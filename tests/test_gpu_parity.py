@@ -693,7 +693,7 @@ def test_dz_in_wgrad_bit_identical(B, H, W):
     from _helpers import options
     x, t = inputs(47, B, H, W)
     outs = []
-    for flag in (0, 1):
+    for flag in (0, 1 << 20):  # off / every layer (default: Cin <= 256)
         m = hip_model(O.make_params(42), DEV)
         with options(m.flatten_().rt, dz_in_wgrad=flag):
             logits = m(x.to(DEV))

@@ -133,9 +133,12 @@ struct Options {
                                // 2.02 -> 0.97 GB at equal time), 2 row GEMMs, 3 wgrad
     int wgrad_stream = 0;      // weight gradients on a second stream (bit-identical)
     int dz_in_loaders = 0;     // BN-backward dz inside the GEMM loaders (model.py order)
-    int dz_in_wgrad = 1;       // BN-backward dz formed by the weight gradient's B' loader, which
-                               // also stores it for the dgrad (no bn_dz pass; model.py order;
-                               // config 2: 77.96 -> 77.53 ms/step, gpurun_out n64 A/B)
+    int dz_in_wgrad = 256;     // layers with Cin <= this form the BN-backward dz in the weight
+                               // gradient's B' loader, which also stores it for the dgrad (no
+                               // bn_dz pass; model.py order; 0 = off).  Every A'-tile row of
+                               // blocks re-reads do and y instead of dz, so the fusion pays
+                               // where few A' tiles share a pixel slice (profiles/
+                               // r03_tile_experiments.txt: Cin 64..256 gain, 512..1024 lose)
     int row3_gemm = 0;         // f32 3x3 forward / dgrad on the tap-row kernel
                                // (rowgemm_row3_kernel) where its shapes allow
 };
@@ -1342,7 +1345,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         // option dz_in_wgrad: the weight gradient's B' loader forms dz from do and y (the
         // bn_dz pass disappears) and its first A'-tile blocks store it for the dgrad; f32
         // register-staged weight-gradient tiles only, model.py order, with a dgrad to feed
-        const bool dzw = p.gdz && !dz16 && !dzc && dx && !async_w &&
+        const bool dzw = p.gdz && C.cin <= c->opt.dz_in_wgrad && !dz16 && !dzc && dx && !async_w &&
                          (wc.tile < 10 || (wc.tile >= 20 && wc.tile < 30));
         if (dzw) {
         } else if (dz16) {
