@@ -306,7 +306,7 @@ def test_schedule_option_defaults():
     f32 GEMMs; A/B alternatives off."""
     from unet_hip.runtime import UNetRuntime
     fresh = UNetRuntime("cuda:0")
-    want = {"tile_n128": -1, "tile_n128_dgrad": -1, "tile_n64": 19, "tile_n64_dgrad": 1,
+    want = {"tile_n128": -1, "tile_n128_dgrad": -1, "tile_n64": 19, "tile_n64_dgrad": 25,
             "tile_convt64": 1, "wgrad_row3": 1, "wgrad_row3_big": 21, "wgrad_row3_blocks": 1536,
             "wgrad_row3_pipe": 0, "wgrad_blocks": 2048, "rg16": 1, "rg16_tile": -1, "rg16_ra": 0,
             "rg16_bn_k": 8192, "wg16": 1, "wg16_tile": 2, "wgrad16_blocks": 1536,

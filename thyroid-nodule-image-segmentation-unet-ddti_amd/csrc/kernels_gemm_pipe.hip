@@ -26,11 +26,13 @@
 namespace {
 
 // DEPTH: chunks whose global loads are in flight in registers (2 = issued two chunks before
-// their commit; costs one more stage of registers).
-template <int BM_, int BN_, int WM_, int WN_, int OCC_, int DEPTH_ = 1>
+// their commit; costs one more stage of registers).  SWZ: unpadded, XOR-swizzled LDS rows
+// (see the kernel), 8/9 of the padded images' space.
+template <int BM_, int BN_, int WM_, int WN_, int OCC_, int DEPTH_ = 1, bool SWZ_ = false>
 struct PipeTile {
     static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, BK = 32, OCC = OCC_;
     static constexpr int DEPTH = DEPTH_;
+    static constexpr bool SWZ = SWZ_;
     static constexpr int WAVES = (BM / WM) * (BN / WN);
     static constexpr int THREADS = 64 * WAVES;
 };
@@ -45,7 +47,15 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_pipe_kernel(RowGem
     constexpr bool ARELU = AOP == OP_AFFINE_RELU;
     constexpr int BM = T::BM, BN = T::BN, WM = T::WM, WN = T::WN, BK = T::BK;
     constexpr int NTH = T::THREADS, WAVES_N = BN / WN;
-    constexpr int LDK = BK + 4;  // f32 row stride of the LDS images
+    // LDS images: rows of BK + 4 f32 (the padding makes the 16-lane groups of ds_read_b128
+    // conflict-free), or, SWZ, unpadded 128-B rows with 16-B chunk c of row r in slot
+    // c ^ ((r >> 1) & 7): the groups (rows r0 + {0-3, 12-15, 20-27} or {4-11, 16-19, 28-31},
+    // one chunk) again hit 16 distinct slots, in 8/9 of the space (the 128x64 tile then fits
+    // three blocks per CU).  The XOR costs the 128x128 tile ~0.8 % (A/B on one box), so only
+    // the three-block tiles use it.
+    constexpr bool SWZ = T::SWZ;
+    constexpr int LDK = SWZ ? BK : BK + 4;
+    auto swz = [](int r) { return SWZ ? (r >> 1) & 7 : 0; };
     constexpr int MT = WM / 32, NT = WN / 32, KG = BK / 8;
     constexpr int F4R = BK / 4, RPP = NTH / F4R;
     constexpr int AP = BM / RPP, BP = BN / RPP;
@@ -149,13 +159,19 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_pipe_kernel(RowGem
             const bool keep = (st.vbits >> i) & 1u;
 #pragma unroll
             for (int j = 0; j < 4; ++j) v[j] = keep ? v[j] : 0.f;
-            *(f32x4*)&as[(lrow + i * RPP) * LDK + lc4 * 4] = v;
+            const int r = lrow + i * RPP;
+            *(f32x4*)&as[r * LDK + ((lc4 ^ swz(r)) << 2)] = v;
         }
 #pragma unroll
-        for (int i = 0; i < BP; ++i) *(f32x4*)&bs[(lrow + i * RPP) * LDK + lc4 * 4] = st.rb[i];
+        for (int i = 0; i < BP; ++i) {
+            const int r = lrow + i * RPP;
+            *(f32x4*)&bs[r * LDK + ((lc4 ^ swz(r)) << 2)] = st.rb[i];
+        }
     };
 
     const int li = lane & 31, lh = lane >> 5;
+    const int sl = swz(li);  // = swz(row) of every operand row (row bases are multiples of 32)
+    static_assert(WM % 32 == 0 && WN % 32 == 0, "operand row bases");
     f32x4 af[KG][MT], bf[KG][NT];
     // MFMA operands of k-group kg (8 k) of the chunk in image buf
     auto read_kg = [&](int buf, int kg) {
@@ -163,10 +179,10 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_pipe_kernel(RowGem
         const float* bs = as + BM * LDK;
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt)
-            af[kg][mt] = *(const f32x4*)&as[(wm * WM + mt * 32 + li) * LDK + kg * 8 + lh * 4];
+            af[kg][mt] = *(const f32x4*)&as[(wm * WM + mt * 32 + li) * LDK + (((2 * kg + lh) ^ sl) << 2)];
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt)
-            bf[kg][nt] = *(const f32x4*)&bs[(wn * WN + nt * 32 + li) * LDK + kg * 8 + lh * 4];
+            bf[kg][nt] = *(const f32x4*)&bs[(wn * WN + nt * 32 + li) * LDK + (((2 * kg + lh) ^ sl) << 2)];
     };
 
     f32x16 acc[MT][NT];
@@ -279,6 +295,10 @@ using PipeTile3 = PipeTile<128, 64, 64, 32, 2, 2>;
 // and paid its prologue / epilogue per 4-8 chunks of MFMAs
 using PipeTile4 = PipeTile<128, 256, 64, 64, 1>;
 using PipeTile5 = PipeTile<256, 128, 64, 64, 1>;
+// N = 64 at three blocks per CU (48 KB of LDS each): a third resident block to overlap the
+// epilogues of the short-K (576) level-0 GEMMs; 7 loads two chunks ahead
+using PipeTile6 = PipeTile<128, 64, 64, 32, 3, 1, true>;
+using PipeTile7 = PipeTile<128, 64, 64, 32, 3, 2, true>;
 
 template <int AMODE, int AOP, int EMODE, class T>
 static int pipe_go(const RowGemmArgs& a, hipStream_t s) {
@@ -299,6 +319,8 @@ static int pipe_tile(const RowGemmArgs& a, int tile, hipStream_t s) {
     if (tile == 3) return pipe_go<AMODE, AOP, EMODE, PipeTile3>(a, s);
     if (tile == 4) return pipe_go<AMODE, AOP, EMODE, PipeTile4>(a, s);
     if (tile == 5) return pipe_go<AMODE, AOP, EMODE, PipeTile5>(a, s);
+    if (tile == 6) return pipe_go<AMODE, AOP, EMODE, PipeTile6>(a, s);
+    if (tile == 7) return pipe_go<AMODE, AOP, EMODE, PipeTile7>(a, s);
     return -1;
 }
 
@@ -315,7 +337,7 @@ int rowgemm_pipe_ok(const RowGemmArgs& a) {
 }
 
 // tile: 0 = 128x128, 1 = 128x64, 2 / 3 = those loading two chunks ahead, 4 = 128x256,
-// 5 = 256x128 (8 waves)
+// 5 = 256x128 (8 waves), 6 / 7 = 128x64 at three blocks per CU
 int launch_rowgemm_pipe(const RowGemmArgs& a, int tile, hipStream_t s) {
     if (!rowgemm_pipe_ok(a) || a.M < 1 || a.K != gather_taps(a.amode) * a.C) return -1;
     const bool aff = a.ascale != nullptr;

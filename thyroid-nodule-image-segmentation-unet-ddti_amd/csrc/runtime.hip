@@ -107,7 +107,8 @@ struct Options {
     int tile_n128 = -1;        // f32 row-GEMM tile, N % 128 == 0 (-1 = pick_tile's default)
     int tile_n128_dgrad = -1;  // ... dgrad-type
     int tile_n64 = 19;         // ... N = 64 outputs (forward-type)
-    int tile_n64_dgrad = 1;    // ... N = 64, dgrad-type
+    int tile_n64_dgrad = 25;   // ... N = 64, dgrad-type (pipelined 128x64 at three blocks per
+                               // CU: level-0 dgrads 1.50-1.55 -> 1.40-1.45 ms, r03)
     int tile_convt64 = 1;      // ConvT forward with 64 output channels (grid N = 256)
     int tile_n32 = 14;         // f32 row GEMMs with 32 outputs (256 x 32, 4 waves)
     int tile_convt = -1;       // ConvT forward, >= 128 output channels (-1 = tile_n128's)
