@@ -658,7 +658,8 @@ def test_pipe_gemm_bit_identical(variant, B, H, W):
     from oracle import mod_ref_cpu as MO
     x, t = inputs(43, B, H, W)
     outs = []
-    for tiles in ((4, 0, 1), (16, 16, 17), (18, 18, 19), (20, 20, 21), (16, 18, 25), (18, 16, 26)):
+    for tiles in ((4, 0, 1, 0), (16, 16, 17, 16), (18, 18, 19, 18), (20, 20, 21, 20),
+                  (16, 18, 25, 26), (18, 16, 26, 25)):
         if variant == "model":
             m = hip_model(O.make_params(42), DEV)
         elif variant == "mod":
@@ -670,7 +671,8 @@ def test_pipe_gemm_bit_identical(variant, B, H, W):
             m.load_state_dict(sd)
             m = m.to(DEV).train()
         with options(m.flatten_().rt, tile_n128=tiles[0], tile_n128_dgrad=tiles[1],
-                     tile_n64=tiles[2], tile_n64_dgrad=tiles[2], tile_convt64=tiles[2]):
+                     tile_n64=tiles[2], tile_n64_dgrad=tiles[2], tile_convt64=tiles[2],
+                     tile_convt_dgrad=tiles[3]):
             logits = m(x.to(DEV))
             l = unet_hip.seg_losses(logits, t.to(DEV))
             (l[0] + l[1]).backward()
