@@ -214,8 +214,15 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_pipe_kernel(RowGem
     Stage S[D];
     issue(S[0], 0);
     commit(S[0], 0);
+    // the prologue's chunks are issued in order, each behind a scheduling fence: loads of
+    // chunk 2 hoisted between chunk 1's would make the loop's first commit wait for (almost)
+    // every load in flight -- the wait counts are merged over the loop entry and back edge
 #pragma unroll
-    for (int d = 0; d < D; ++d) issue(S[(1 + d) % D], clampk(1 + d));
+    for (int d = 0; d < D; ++d) {
+        __builtin_amdgcn_sched_barrier(0);
+        issue(S[(1 + d) % D], clampk(1 + d));
+    }
+    __builtin_amdgcn_sched_barrier(0);
     __syncthreads();
 #pragma unroll
     for (int kg = 0; kg < KG; ++kg) read_kg(0, kg);
