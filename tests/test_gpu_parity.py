@@ -801,3 +801,36 @@ def test_adamw_resume_from_state_dict_matches_uninterrupted():
     m = torch.cat([oa.state[p]["exp_avg"].reshape(-1).cpu() for p in pa])
     v = torch.cat([oa.state[p]["exp_avg_sq"].reshape(-1).cpu() for p in pa])
     assert torch.equal(m, ref.m["a"]) and torch.equal(v, ref.v["a"])
+
+
+@pytest.mark.parametrize("variant,B,H,W", [("model", 2, 64, 64), ("model", 8, 256, 256),
+                                           ("mod", 2, 128, 128)])
+def test_reduce_stream_bit_identical(variant, B, H, W):
+    """Option reduce_stream: the split-K slab reductions and bias sums run on a second stream
+    beside the dgrad GEMMs (the next weight gradient waits for them before it rewrites the
+    slabs; bucket events are recorded on that stream).  Same kernels, same order of
+    summation: the gradient arena is bit-identical to the one-stream schedule, over two
+    steps so that the ordering of the next step's writers is exercised too."""
+    import unet_hip
+    from _helpers import hip_mod_model, options
+    from oracle import mod_ref_cpu as MO
+    x, t = inputs(53, B, H, W)
+    outs = []
+    for flag in (0, 1):
+        if variant == "model":
+            m = hip_model(O.make_params(42), DEV)
+        else:
+            m = hip_mod_model(MO.make_params(5, 64, 3), DEV, 64, 3)
+        grads = []
+        with options(m.flatten_().rt, reduce_stream=flag):
+            for _ in range(2):
+                m.zero_grad(set_to_none=False)
+                logits = m(x.to(DEV))
+                l = unet_hip.seg_losses(logits, t.to(DEV))
+                (l[0] + l[1]).backward()
+                torch.cuda.synchronize()
+                grads.append(m._state.grad_arena.clone())
+        outs.append(grads)
+        del m
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b), (a - b).abs().max().item()

@@ -135,6 +135,8 @@ struct Options {
                                // per launch rowgemm 128x128 2.21 -> 1.00 GB, row3 wgrad
                                // 2.02 -> 0.97 GB at equal time), 2 row GEMMs, 3 wgrad
     int wgrad_stream = 0;      // weight gradients on a second stream (bit-identical)
+    int reduce_stream = 0;     // only the split-K slab reductions + bias sums on it (bit-identical;
+                               // 1 % slower: they slow the concurrent dgrad GEMM, r03)
     int dz_in_loaders = 0;     // BN-backward dz inside the GEMM loaders (model.py order)
     int dz_in_wgrad = 256;     // layers with Cin <= this form the BN-backward dz in the weight
                                // gradient's B' loader, which also stores it for the dgrad (no
@@ -167,7 +169,7 @@ const OptionDesc OPTION_TABLE[] = {
     {"wg16_tile", &Options::wg16_tile},         {"wg16t", &Options::wg16t},
     {"xcd16", &Options::xcd16},                 {"xcd_remap", &Options::xcd_remap},
     {"wgrad_stream", &Options::wgrad_stream},   {"dz_in_loaders", &Options::dz_in_loaders},
-    {"dz_in_wgrad", &Options::dz_in_wgrad},
+    {"dz_in_wgrad", &Options::dz_in_wgrad},     {"reduce_stream", &Options::reduce_stream},
     {"row3_gemm", &Options::row3_gemm},
 };
 
@@ -1264,6 +1266,17 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         return fail(c, UNET_ERR_HIP, "cannot create the weight-gradient stream");
     hipStream_t sw = async_w ? c->side : s;
     Launcher LW{c, sw};
+    // Option reduce_stream: only the split-K slab reductions and bias sums (small,
+    // latency-bound launches) go to the second stream, where they overlap the layer's dgrad
+    // GEMM; the next weight gradient (the next writer of the slabs) waits for them.  Bucket
+    // events are then recorded on that stream.
+    const bool async_r = !async_w && c->opt.reduce_stream && !c->res &&
+                         !(c->timing && c->tfilter.empty());
+    if (async_r && !c->side &&
+        hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess)
+        return fail(c, UNET_ERR_HIP, "cannot create the reduction stream");
+    hipStream_t sr = async_r ? c->side : sw;
+    Launcher LR{c, sr};
     c->sync_used = 0;
     auto sev = [&]() {
         if (c->sync_used == c->sync_pool.size()) {
@@ -1301,6 +1314,27 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         int rc_ = LW.run(label, flop, [&]() { return (expr); });   \
         if (rc_) return rc_;                                       \
     } while (0)
+#define RUNR(label, flop, expr)                                    \
+    do {                                                           \
+        int rc_ = LR.run(label, flop, [&]() { return (expr); });   \
+        if (rc_) return rc_;                                       \
+    } while (0)
+    hipEvent_t red_pending = nullptr;  // async_r: the last reduction's completion on sr
+    auto before_slab_write = [&]() {   // main-stream writers of p.slab / p.bslab
+        if (red_pending) (void)hipStreamWaitEvent(s, red_pending, 0);
+        red_pending = nullptr;
+    };
+    auto reduce_after_main = [&]() {   // sr waits for the weight gradient just enqueued on s
+        if (!async_r) return;
+        hipEvent_t e = sev();
+        (void)hipEventRecord(e, s);
+        (void)hipStreamWaitEvent(sr, e, 0);
+    };
+    auto reduce_enqueued = [&]() {
+        if (!async_r) return;
+        red_pending = sev();
+        (void)hipEventRecord(red_pending, sr);
+    };
 
     // BatchNorm backward is fused: the producer of `do` (head_bwd, a dgrad epilogue,
     // maxpool_bwd) leaves {sum do, sum do*y} column partials in p.part (do already masked by
@@ -1396,6 +1430,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         w.splits = wc.splits;
         w.slab = p.slab;
         w.bf16 = c->bf16;
+        before_slab_write();
         if (p.x16[i] && !dzc) {
             w.a = (const float*)p.x16[i];
             w.lda = C.cin;
@@ -1420,10 +1455,12 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
                  launch_wgrad(w, wc.tile, sw));
         }
         side_read(dout);
-        RUNW("wgrad_reduce", 0,
-             k_slab_reduce(p.slab, wc.splits, w.Mw, w.Nw, 0, C.cin, C.cout, grads + C.w, sw));
+        reduce_after_main();
+        RUNR("wgrad_reduce", 0,
+             k_slab_reduce(p.slab, wc.splits, w.Mw, w.Nw, 0, C.cin, C.cout, grads + C.w, sr));
         if (C.b >= 0)
-            RUNW("bias_grad", 0, k_bias_reduce(p.bslab, wc.splits, 1, C.cout, grads + C.b, sw));
+            RUNR("bias_grad", 0, k_bias_reduce(p.bslab, wc.splits, 1, C.cout, grads + C.b, sr));
+        reduce_enqueued();
         if (dx) {
             before_write(dx);
             RowGemmArgs g{};
@@ -1519,6 +1556,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         w.slab = p.slab;
         w.bf16 = c->bf16;
         const bool t16 = p.t16[k] != nullptr;
+        before_slab_write();
         if (t16) {
             // bf16 image of the up half of the concat gradient: B' here, A of the dgrad below
             before_write(p.s16);
@@ -1551,9 +1589,11 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
                  launch_wgrad(w, wc.tile, sw));
         }
         side_read(p.dcat[lo]);
-        RUNW("wgrad_reduce", 0,
-             k_slab_reduce(p.slab, wc.splits, w.Mw, w.Nw, 1, T.cin, T.cout, grads + T.w, sw));
-        RUNW("bias_grad", 0, k_bias_reduce(p.bslab, wc.splits, 4, T.cout, grads + T.b, sw));
+        reduce_after_main();
+        RUNR("wgrad_reduce", 0,
+             k_slab_reduce(p.slab, wc.splits, w.Mw, w.Nw, 1, T.cin, T.cout, grads + T.w, sr));
+        RUNR("bias_grad", 0, k_bias_reduce(p.bslab, wc.splits, 4, T.cout, grads + T.b, sr));
+        reduce_enqueued();
         before_write(dx);
         RowGemmArgs g{};
         g.zero16 = p.zero16;
@@ -1607,11 +1647,25 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         bool any = false;
         for (size_t b = 0; b < c->bucket_stage.size(); ++b) any |= c->bucket_stage[b] == st;
         if (!any) return;
+        if (async_r) {  // the stage's reductions are on sr; BN / head grads on s
+            hipEvent_t e = sev();
+            (void)hipEventRecord(e, s);
+            (void)hipStreamWaitEvent(sr, e, 0);
+            for (size_t b = 0; b < c->bucket_stage.size(); ++b)
+                if (c->bucket_stage[b] == st) (void)hipEventRecord(c->bucket_ev[b], sr);
+            return;
+        }
         side_after_main();  // BN / head grads of the stage come from the main stream
         for (size_t b = 0; b < c->bucket_stage.size(); ++b)
             if (c->bucket_stage[b] == st) (void)hipEventRecord(c->bucket_ev[b], sw);
     };
     auto join = [&]() {
+        if (async_r) {
+            hipEvent_t e = sev();
+            (void)hipEventRecord(e, sr);
+            (void)hipStreamWaitEvent(s, e, 0);
+            return;
+        }
         if (!async_w) return;
         hipEvent_t e = sev();
         (void)hipEventRecord(e, sw);
@@ -1776,6 +1830,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
     join();
     return 0;
 #undef RUNW
+#undef RUNR
 }
 
 // Pillow's precompute_coeffs + normalize_coeffs_8bpc (libImaging/Resample.c) for the
