@@ -46,6 +46,18 @@ __device__ __forceinline__ Pix decode(int m, int H, int W) {
     return r;
 }
 
+// q += d pixels (row-major over H x W images), without dividing
+__device__ __forceinline__ void pix_advance(Pix& q, int d, int H, int W) {
+    q.x += d;
+    while (q.x >= W) {
+        q.x -= W;
+        if (++q.y == H) {
+            q.y = 0;
+            ++q.img;
+        }
+    }
+}
+
 // Division by a per-launch constant through an f32 reciprocal plus one correction step:
 // exact while the quotient stays below 2^22 (P / W < 4M pixel rows here).
 __device__ __forceinline__ int fdiv(int n, int d, float rd) {

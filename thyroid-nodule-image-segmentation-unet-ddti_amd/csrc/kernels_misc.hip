@@ -6,6 +6,7 @@
 // reductions (no float atomics), so two runs of the same inputs are bit-identical.
 // Layout everywhere: NHWC, channel stride `ld`, channel offset `off` (concat slices).
 #include "kernels_misc.h"
+#include "gemm_common.h"  // Pix, decode, pix_advance
 
 namespace {
 
@@ -211,8 +212,11 @@ __global__ __launch_bounds__(256) void conv_first_fwd_kernel(const float* __rest
     const int per = (P + gridDim.x - 1) / gridDim.x;
     const int r0 = blockIdx.x * per;
     const int r1 = min(P, r0 + per);
+    // pixel coordinates walked incrementally (m advances by rpp): no integer division per pixel
+    Pix at = decode(min(r0 + g, P - 1), H, W);
     for (int m = r0 + g; m < r1; m += rpp) {
-        const int xx = m % W, t = m / W, yy = t % H, img = t / H;
+        const int xx = at.x, yy = at.y, img = at.img;
+        pix_advance(at, rpp, H, W);
         float xv[9];
 #pragma unroll
         for (int tap = 0; tap < 9; ++tap) {
@@ -252,8 +256,10 @@ __global__ __launch_bounds__(256) void conv_first_wgrad_kernel(const float* __re
     const int per = (P + gridDim.x - 1) / gridDim.x;
     const int r0 = blockIdx.x * per;
     const int r1 = min(P, r0 + per);
+    Pix at = decode(min(r0 + g, P - 1), H, W);
     for (int m = r0 + g; m < r1; m += rpp) {
-        const int xx = m % W, t = m / W, yy = t % H, img = t / H;
+        const int xx = at.x, yy = at.y, img = at.img;
+        pix_advance(at, rpp, H, W);
         // dz = [y > 0] (A do + B (y - mean) + C) (or unmasked, BN -> ReLU order): BN backward fused
         const f32x4 dv = *(const f32x4*)(dout + (int64_t)m * C + 4 * q);
         const f32x4 yv = *(const f32x4*)(y + (int64_t)m * C + 4 * q);
@@ -994,13 +1000,14 @@ __global__ void head_fwd_kernel(const float* __restrict__ y, int C, const float*
                                 const float* __restrict__ b, int O, int P, int HW,
                                 float* __restrict__ logits) {
     const int lpp = C / 4;  // lanes per pixel (C == 64 -> 16)
-    const int64_t gt = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    const int64_t pix = gt / lpp;
-    const int q = (int)(gt % lpp);
+    // 32-bit index math (P * lpp < 2^31: the launcher's thread count)
+    const int gt = blockIdx.x * blockDim.x + threadIdx.x;
+    const int pix = gt / lpp;
+    const int q = gt - pix * lpp;
     const bool ok = pix < P;
     f32x4 v = {0, 0, 0, 0};
     if (ok) {
-        v = *(const f32x4*)(y + pix * C + 4 * q);
+        v = *(const f32x4*)(y + (int64_t)pix * C + 4 * q);
         if (scale) v = v * *(const f32x4*)(scale + 4 * q) + *(const f32x4*)(shift + 4 * q);
     }
     if (relu)
@@ -1011,8 +1018,8 @@ __global__ void head_fwd_kernel(const float* __restrict__ y, int C, const float*
         float s = v[0] * wv[0] + v[1] * wv[1] + v[2] * wv[2] + v[3] * wv[3];
         for (int d = lpp / 2; d >= 1; d >>= 1) s += __shfl_xor(s, d);
         if (ok && q == 0) {
-            const int64_t img = pix / HW, hw = pix % HW;
-            logits[(img * O + o) * HW + hw] = s + b[o];
+            const int img = pix / HW, hw = pix - img * HW;
+            logits[((int64_t)img * O + o) * HW + hw] = s + b[o];
         }
     }
 }
@@ -1571,6 +1578,7 @@ int k_head_fwd(const float* y, int C, const float* scale, const float* shift, in
                const float* w, const float* b, int O, int P, int HW, float* logits, hipStream_t s) {
     if (C % 4 || C / 4 > 64 || (C / 4 & (C / 4 - 1))) return -1;  // lanes per pixel: pow2 <= 64
     const int64_t threads = (int64_t)P * (C / 4);
+    if (threads + 255 >= (1ll << 31)) return -1;  // the kernel's 32-bit thread index
     hipLaunchKernelGGL(head_fwd_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, y,
                        C, scale, shift, relu, w, b, O, P, HW, logits);
     LAUNCH_CHECK();
