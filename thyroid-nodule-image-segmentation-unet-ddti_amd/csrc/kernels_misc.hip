@@ -444,10 +444,16 @@ __global__ __launch_bounds__(256) void maxpool_bn_kernel(const float* __restrict
         const int c = 4 * (cb + (int)threadIdx.x % tpr);
         const f32x4 sc = scale ? *(const f32x4*)(scale + c) : f32x4{1.f, 1.f, 1.f, 1.f};
         const f32x4 sh = shift ? *(const f32x4*)(shift + c) : f32x4{0.f, 0.f, 0.f, 0.f};
-        for (int po = blockIdx.x * rpp + (int)threadIdx.x / tpr; po < PO; po += gridDim.x * rpp) {
-            const int t = po / Wo, xo = po - t * Wo;
-            const int img = t / Ho, yo = t - img * Ho;
-            maxpool_px(y, ld, off, sc, sh, relu, H, W, img, yo, xo, c, out, idx, (int64_t)po * C + c);
+        // each block walks one contiguous range of pooled pixels, the coordinates advanced
+        // incrementally (no integer division per pixel)
+        const int per = (PO + gridDim.x - 1) / gridDim.x;
+        const int r0 = blockIdx.x * per, r1 = min(PO, r0 + per);
+        const int g = (int)threadIdx.x / tpr;
+        Pix at = decode(min(r0 + g, PO - 1), Ho, Wo);
+        for (int po = r0 + g; po < r1; po += rpp) {
+            maxpool_px(y, ld, off, sc, sh, relu, H, W, at.img, at.y, at.x, c, out, idx,
+                       (int64_t)po * C + c);
+            pix_advance(at, rpp, Ho, Wo);
         }
     }
 }
@@ -507,10 +513,10 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const float* __restric
             for (int j = 0; j < 4; ++j) acc[v][j] = 0.0;
         const int64_t per = (PO + gridDim.x - 1) / gridDim.x;
         const int64_t r0 = blockIdx.x * per, r1 = r0 + per < PO ? r0 + per : PO;
+        Pix at = decode((int)min(r0 + g, PO - 1), Ho, Wo);  // N*H*W < 2^31 (launcher)
         for (int64_t po = r0 + g; po < r1; po += rpp) {
-            // 32-bit index math (the launcher guarantees N*H*W < 2^31)
-            const int t = (int)po / Wo, xo = (int)po - t * Wo;
-            const int img = t / Ho, yo = t - img * Ho;
+            const int xo = at.x, yo = at.y, img = at.img;
+            pix_advance(at, rpp, Ho, Wo);
             const f32x4 gp = *(const f32x4*)(dp + po * C + c);
             const uint32_t bi = *(const uint32_t*)(idx + po * C + c);
 #pragma unroll
