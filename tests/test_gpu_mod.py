@@ -263,7 +263,9 @@ def test_rg16_tile_choice_is_numerically_invisible(side):
     # 12 / 13: tiles 4 / 0 with read-ahead fragments; 18: the ping-pong 256x256 kernel
     for tile in (0, 2, 4, 12, 13, 18, -1):
         m = _bf16_model(P, 128, 5)
-        with options(m.flatten_().rt, rg16_tile=tile):
+        # the tap-row halo tile (19, the auto choice's 256x256 forward / dgrad since r03) sums
+        # K in another order: held to the bf16 envelope by test_rg16_halo_tile_within_bf16_error
+        with options(m.flatten_().rt, rg16_tile=tile, rg16_r3=0):
             outs[tile] = _bf16_step(m, x, t)
         del m
     for tile in (2, 4, 12, 13, 18, -1):

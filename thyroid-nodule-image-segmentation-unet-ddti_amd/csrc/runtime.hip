@@ -124,7 +124,8 @@ struct Options {
     int rg16_xp = 0;           // speed-of-light ablation of the forward rg16 GEMMs (garbage
                                // results; A/B timing only, kernels_gemm16.hip XP)
     int rg16_pp = 0;           // 256x256 GEMMs on the ping-pong kernel (tile 18)
-    int rg16_r3 = 0;           // 256x256 3x3-conv GEMMs (W >= 16) on the tap-row halo kernel (tile 19)
+    int rg16_r3 = 1;           // 256x256 3x3-conv GEMMs (W >= 16) on the tap-row halo kernel (tile 19;
+                               // config 4: +0.9..1.2 % over three A/B pairs, r03)
     int rg16_m16 = 0;          // per-GEMM choice on the 16x16x32-MFMA tiles: 1 = 14 / 15,
                                // 2 = with s_setprio around the MFMAs (16 / 17)
     int wg16 = 1;              // bf16 3x3 wgrad on the LDS-DMA transposed-read kernel
