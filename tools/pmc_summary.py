@@ -39,6 +39,10 @@ def short(name):
     m = re.search(r"WgTile<(\d+), (\d+), \d+, \d+, (\d+)", name)
     if m:
         return f"wgrad_{m.group(1)}x{m.group(2)}x{m.group(3)}"
+    if "rowgemm16_row3_kernel" in name:  # tap-row halo bf16 GEMM (tile 19)
+        return "rg16r3_256x256s2"
+    if "rowgemm16_pp_kernel" in name:    # ping-pong bf16 GEMM (tile 18)
+        return "rg16pp_256x256s2"
     m = re.search(r"(?<!W)Tile16<(\d+), (\d+), \d+, \d+, (\d+), \d+[,>]", name)
     if m:
         return f"rg16_{m.group(1)}x{m.group(2)}s{m.group(3)}"
