@@ -1289,8 +1289,9 @@ using Wr3Tile1 = WgTile<128, 64, 64, 32, 32>;   // 4 waves, 3 x 64x32
 using Wr3Tile2 = WgTile<64, 128, 32, 64, 32>;   // 4 waves, 3 x 32x64
 using Wr3Tile3 = WgTile<128, 128, 64, 64, 32>;  // 4 waves, 3 x 64x64 (192 accumulators)
 using Wr3Tile4 = WgTile<64, 64, 32, 32, 64>;    // 64-pixel chunks
+using Wr3Tile5 = WgTile<128, 64, 64, 32, 16>;   // tile 21 on 16-pixel chunks (16-wide rows)
 #define WGRAD_ROW3_TILES(X) \
-    X(20, Wr3Tile0) X(21, Wr3Tile1) X(22, Wr3Tile2) X(23, Wr3Tile3) X(24, Wr3Tile4)
+    X(20, Wr3Tile0) X(21, Wr3Tile1) X(22, Wr3Tile2) X(23, Wr3Tile3) X(24, Wr3Tile4) X(25, Wr3Tile5)
 
 int wgrad_tile_taps(int tile) { return tile >= 20 ? 3 : 1; }
 

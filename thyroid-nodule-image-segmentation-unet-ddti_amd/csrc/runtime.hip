@@ -136,6 +136,7 @@ struct Options {
                                // per launch rowgemm 128x128 2.21 -> 1.00 GB, row3 wgrad
                                // 2.02 -> 0.97 GB at equal time), 2 row GEMMs, 3 wgrad
     int wgrad_stream = 0;      // weight gradients on a second stream (bit-identical)
+    int wgrad_row3_16 = 0;     // row3 weight gradients on 16-pixel rows (tile 25)
     int reduce_stream = 0;     // only the split-K slab reductions + bias sums on it (bit-identical;
                                // 1 % slower: they slow the concurrent dgrad GEMM, r03)
     int dz_in_loaders = 0;     // BN-backward dz inside the GEMM loaders (model.py order)
@@ -171,6 +172,7 @@ const OptionDesc OPTION_TABLE[] = {
     {"xcd16", &Options::xcd16},                 {"xcd_remap", &Options::xcd_remap},
     {"wgrad_stream", &Options::wgrad_stream},   {"dz_in_loaders", &Options::dz_in_loaders},
     {"dz_in_wgrad", &Options::dz_in_wgrad},     {"reduce_stream", &Options::reduce_stream},
+    {"wgrad_row3_16", &Options::wgrad_row3_16},
     {"row3_gemm", &Options::row3_gemm},
 };
 
@@ -571,6 +573,12 @@ WgradCfg wgrad_cfg(const unet_ctx* c, int CA, int tapsA, int CB, int tapsB, int6
         const bool row3 = tapsA == 9 && tapsB == 1 && row_w > 0 && row_w % 32 == 0 &&
                           CA % 64 == 0 && CB % 64 == 0 &&
                           (r3 == 1 || (r3 == 2 && (CA == 64 || CB == 64)));
+        // 16-pixel image rows (the 16x16 bottleneck of a 256^2 input): the 128x64 row tile
+        // on 16-pixel chunks (tile 25) instead of the one-tap kernel (102 TF/s there, r03)
+        const bool row3_16 = tapsA == 9 && tapsB == 1 && r3 == 1 && c->opt.wgrad_row3_16 &&
+                             row_w == 16 && CA % 128 == 0 && CB % 64 == 0 &&
+                             !c->opt.wgrad_row3_pipe && r3t < 20;
+        if (row3_16) w.tile = 25;
         if (row3) {
             w.tile = r3t >= 20 ? r3t
                                : (CA % 128 == 0 ? (CB % 128 == 0 ? 23 : 21) : (CB % 128 == 0 ? 22 : 20)) +
