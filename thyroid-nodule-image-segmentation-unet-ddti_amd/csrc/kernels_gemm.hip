@@ -1111,6 +1111,12 @@ int rowgemm_tile_dims(int tile, int* bm, int* bn, int* bk) {
         *bk = 32;
         return 0;
     }
+    if (tile == 27 || tile == 28) {  // rowgemm_pipe_kernel 256x64, 64x64 wave tiles
+        *bm = 256;
+        *bn = 64;
+        *bk = 32;
+        return 0;
+    }
     if (tile == 25 || tile == 26) {  // rowgemm_pipe_kernel 128x64, three blocks per CU
         *bm = 128;
         *bn = 64;
@@ -1130,7 +1136,7 @@ int rowgemm_tile_dims(int tile, int* bm, int* bn, int* bk) {
 }
 
 int rowgemm_tile_dbuf(int tile) {
-    if ((tile >= 16 && tile <= 19) || (tile >= 23 && tile <= 26)) return 2;  // pipelined
+    if ((tile >= 16 && tile <= 19) || (tile >= 23 && tile <= 28)) return 2;  // pipelined
     if (tile >= 20 && tile <= 22) return 3;  // LDS-DMA
 #define RG_DB(id, T) \
     if (tile == id) return T::DBUF ? 1 : 0;
@@ -1251,7 +1257,7 @@ int launch_rowgemm(const RowGemmArgs& a, int tile, hipStream_t s) {
         if (rowgemm_pipe_ok(a)) return launch_rowgemm_pipe(a, tile - 19, s);
         tile = 4;
     }
-    if (tile == 25 || tile == 26) {  // 128x64 at three blocks per CU (N = 64)
+    if (tile >= 25 && tile <= 28) {  // 128x64 at three blocks per CU / 256x64 (N = 64)
         if (rowgemm_pipe_ok(a)) return launch_rowgemm_pipe(a, tile - 19, s);
         tile = 1;
     }

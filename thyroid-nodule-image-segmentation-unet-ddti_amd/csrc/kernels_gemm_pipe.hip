@@ -306,6 +306,10 @@ using PipeTile5 = PipeTile<256, 128, 64, 64, 1>;
 // epilogues of the short-K (576) level-0 GEMMs; 7 loads two chunks ahead
 using PipeTile6 = PipeTile<128, 64, 64, 32, 3, 1, true>;
 using PipeTile7 = PipeTile<128, 64, 64, 32, 3, 2, true>;
+// N = 64 on 64x64 wave tiles (the dominant tile's MFMA : load : ds_read ratios): 4 waves
+// stacked along M, unpadded swizzled images of 80 KB, so two blocks fill the 160 KB of a CU
+using PipeTile8 = PipeTile<256, 64, 64, 64, 2, 1, true>;
+using PipeTile9 = PipeTile<256, 64, 64, 64, 2, 2, true>;
 
 template <int AMODE, int AOP, int EMODE, class T>
 static int pipe_go(const RowGemmArgs& a, hipStream_t s) {
@@ -328,6 +332,8 @@ static int pipe_tile(const RowGemmArgs& a, int tile, hipStream_t s) {
     if (tile == 5) return pipe_go<AMODE, AOP, EMODE, PipeTile5>(a, s);
     if (tile == 6) return pipe_go<AMODE, AOP, EMODE, PipeTile6>(a, s);
     if (tile == 7) return pipe_go<AMODE, AOP, EMODE, PipeTile7>(a, s);
+    if (tile == 8) return pipe_go<AMODE, AOP, EMODE, PipeTile8>(a, s);
+    if (tile == 9) return pipe_go<AMODE, AOP, EMODE, PipeTile9>(a, s);
     return -1;
 }
 
@@ -344,7 +350,8 @@ int rowgemm_pipe_ok(const RowGemmArgs& a) {
 }
 
 // tile: 0 = 128x128, 1 = 128x64, 2 / 3 = those loading two chunks ahead, 4 = 128x256,
-// 5 = 256x128 (8 waves), 6 / 7 = 128x64 at three blocks per CU
+// 5 = 256x128 (8 waves), 6 / 7 = 128x64 at three blocks per CU, 8 / 9 = 256x64 on 64x64
+// wave tiles at two blocks per CU
 int launch_rowgemm_pipe(const RowGemmArgs& a, int tile, hipStream_t s) {
     if (!rowgemm_pipe_ok(a) || a.M < 1 || a.K != gather_taps(a.amode) * a.C) return -1;
     const bool aff = a.ascale != nullptr;

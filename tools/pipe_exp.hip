@@ -57,14 +57,14 @@ using N64b = PipeTile<256, 64, 64, 64, 1, 1>;
 using N64c = PipeTile<256, 64, 64, 64, 1, 2>;
 using N64d = PipeTile<128, 64, 64, 64, 2, 1>;
 using N64e = PipeTile3;
-template <class T, bool FWD>
+template <class T, bool FWD, int XP = 0>
 static void go64(const RowGemmArgs& g) {
     const dim3 grid(((g.M + T::BM - 1) / T::BM) * (g.N / T::BN));
     if (FWD)
-        hipLaunchKernelGGL((rowgemm_pipe_kernel<G_CONV3, OP_AFFINE, E_BIAS_RELU_STATS, T>), grid,
+        hipLaunchKernelGGL((rowgemm_pipe_kernel<G_CONV3, OP_AFFINE, E_BIAS_RELU_STATS, T, XP>), grid,
                            dim3(T::THREADS), 0, 0, g);
     else
-        hipLaunchKernelGGL((rowgemm_pipe_kernel<G_CONV3, OP_PLAIN, E_STORE, T>), grid, dim3(T::THREADS), 0, 0, g);
+        hipLaunchKernelGGL((rowgemm_pipe_kernel<G_CONV3, OP_PLAIN, E_STORE, T, XP>), grid, dim3(T::THREADS), 0, 0, g);
 }
 
 struct Shape { const char* name; int N, H, W, Cin, Cout; };
@@ -134,11 +134,17 @@ int main(int argc, char** argv) {
         CK(hipFree(y)); CK(hipFree(st)); CK(hipFree(dz)); CK(hipFree(xo));
     }
     {  // N = 64 outputs: forward 64->64 and 128->64 at 256^2 (N = Cout = 64), dgrad of 64->64
-        constexpr int NV64 = 5;
+        // r04: ablations of the library's N = 64 tiles (19 = PipeTile3 forward, 25 = PipeTile6
+        // dgrad): xp16 no epilogue, xp2 no loop global loads, xp31 MFMAs only
+        constexpr int NV64 = 8;
         typedef void (*Fn)(const RowGemmArgs&);
-        const Fn f64[NV64] = {go64<N64a, true>, go64<N64b, true>, go64<N64c, true>, go64<N64d, true>, go64<N64e, true>};
-        const Fn d64[NV64] = {go64<N64a, false>, go64<N64b, false>, go64<N64c, false>, go64<N64d, false>, go64<N64e, false>};
-        const char* nm[NV64] = {"128x64/w64x32", "256x64/w64x64", "256x64/w64x64/d2", "128x64/w64x64x2", "128x64/w64x32/d2"};
+        const Fn f64[NV64] = {go64<PipeTile3, true>, go64<PipeTile3, true, 16>, go64<PipeTile3, true, 2>,
+                              go64<PipeTile3, true, 31>, go64<PipeTile6, true>, go64<PipeTile6, true, 16>,
+                              go64<PipeTile6, true, 2>, go64<PipeTile6, true, 31>};
+        const Fn d64[NV64] = {go64<PipeTile3, false>, go64<PipeTile3, false, 16>, go64<PipeTile3, false, 2>,
+                              go64<PipeTile3, false, 31>, go64<PipeTile6, false>, go64<PipeTile6, false, 16>,
+                              go64<PipeTile6, false, 2>, go64<PipeTile6, false, 31>};
+        const char* nm[NV64] = {"t19", "t19/xp16", "t19/xp2", "t19/xp31", "t25", "t25/xp16", "t25/xp2", "t25/xp31"};
         Shape s64[] = {{"L0 64->64 @256", 32, 256, 256, 64, 64}, {"L0 128->64 @256", 32, 256, 256, 128, 64}};
         for (const Shape& sh : s64) {
             const int M = sh.N * sh.H * sh.W;
