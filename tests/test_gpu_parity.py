@@ -744,6 +744,44 @@ def test_wgrad_row3_pipe_bit_identical(variant, B, H, W, dzl):
     assert torch.equal(outs[0][1], outs[1][1]), d
 
 
+@pytest.mark.parametrize("variant,B,H,W,dzw", [("model", 2, 64, 64, 256), ("model", 4, 128, 128, 256),
+                                               ("model", 2, 64, 64, 0), ("model", 1, 96, 64, 256),
+                                               ("mod", 2, 128, 64, 256), ("res", 2, 64, 64, 256)])
+def test_wgrad_row9_bit_identical(variant, B, H, W, dzw):
+    """Option wgrad_row9 (wgrad_row3_kernel with NDY = 3: one block holds all three tap rows of
+    a 64x64 channel tile and reads x and dz -- or do and y with the BN-backward dz formed in
+    its loader, dz_in_wgrad -- once instead of once per tap row) keeps tile 20's split-K
+    partition, per-tap pixel order, bias column sums and dz hand-off, so a training step is
+    bit-identical with and without it.  dz_in_wgrad = 0 covers the plain dz operand, the
+    mod.py variant the BN -> ReLU loader, 96 x 64 an image taller than wide."""
+    import unet_hip
+    from _helpers import hip_mod_model, options
+    from oracle import mod_ref_cpu as MO
+    x, t = inputs(49, B, H, W)
+    outs = []
+    for row9 in (0, 1):
+        if variant == "model":
+            m = hip_model(O.make_params(42), DEV)
+        elif variant == "mod":
+            m = hip_mod_model(MO.make_params(5, 64, 3), DEV, 64, 3)
+        else:
+            m = unet_hip.ResUNet(1, 1, base_filters=64, depth=3)
+            sd = m.state_dict()
+            sd.update({k: v.clone() for k, v in MO.res_make_params(42, 64, 3).items()})
+            m.load_state_dict(sd)
+            m = m.to(DEV).train()
+        with options(m.flatten_().rt, wgrad_row9=row9, dz_in_wgrad=dzw):
+            logits = m(x.to(DEV))
+            l = unet_hip.seg_losses(logits, t.to(DEV))
+            (l[0] + l[1]).backward()
+            torch.cuda.synchronize()
+        outs.append((logits.detach().clone(), m._state.grad_arena.clone()))
+        del m
+    assert torch.equal(outs[0][0], outs[1][0])
+    d = (outs[0][1] - outs[1][1]).abs().max().item()
+    assert torch.equal(outs[0][1], outs[1][1]), d
+
+
 def test_adamw_resume_from_state_dict_matches_uninterrupted():
     """HipAdamW honours optimizer.load_state_dict on its flat path: two steps, save the
     state dict, a fresh optimizer over fresh parameters loads it (and the parameters), then

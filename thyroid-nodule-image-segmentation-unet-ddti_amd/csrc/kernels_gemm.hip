@@ -611,9 +611,14 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void wgrad_kernel(WgradArgs p) 
 // instead of 9x per layer and does a third of the staging per MFMA.  Same K order,
 // split-K slabs, bias column sums and loaders (OP_AFFINE / OP_AFFINE_RELU on x, OP_DZ on
 // dz) as wgrad_kernel; slab rows m = (3*dy + dx)*CA + ci, the one-tap layout.
+// NDY = 3 (row9, r03): one block covers all three tap rows -- it stages the chunk's three
+// input rows (3 (BKP + 2) LDS rows) and feeds nine accumulator sets, so x and the dz chunk
+// (or, BDZ, do and y) are read once per layer instead of once per tap row.  Same split-K
+// partition, same per-tap K order: the slabs are the row3 kernel's bits.
 // ------------------------------------------------------------------------------------
-template <int AOP, bool BDZ, class T>
+template <int AOP, bool BDZ, class T, int NDY = 1>
 __global__ __launch_bounds__(T::THREADS, T::OCC) void wgrad_row3_kernel(WgradArgs p) {
+    static_assert(NDY == 1 || NDY == 3, "tap rows per block");
     constexpr bool AFFINE = AOP == OP_AFFINE || AOP == OP_AFFINE_RELU;
     constexpr bool ARELU = AOP == OP_AFFINE_RELU;
     constexpr int BM = T::BM, BN = T::BN, BKP = T::BKP, WM = T::WM, WN = T::WN;
@@ -623,7 +628,8 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void wgrad_row3_kernel(WgradArg
     constexpr int MT = WM / 32, NT = WN / 32;
     constexpr int AF = BM / 4, BF = BN / 4;          // float4 per pixel row
     constexpr int ARPP = NTH / AF, BRPP = NTH / BF;  // rows per pass
-    constexpr int AROWS = BKP + 2;                   // chunk + halo
+    constexpr int HROWS = BKP + 2;                   // chunk + halo
+    constexpr int AROWS = NDY * HROWS;               // (row9: three image rows)
     constexpr int AP = (AROWS + ARPP - 1) / ARPP, BP = BKP / BRPP;
     static_assert(ARPP * AF == NTH && BP * BRPP == BKP, "loader shape");
     __shared__ __attribute__((aligned(16))) float As[AROWS * LDA];
@@ -632,13 +638,13 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void wgrad_row3_kernel(WgradArg
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave / WAVES_N, wn = wave % WAVES_N;
     const int ctm = p.CA / BM;                       // channel tiles per tap row
-    const int tiles_n = p.Nw / BN, tiles_m = 3 * ctm;
+    const int tiles_n = p.Nw / BN, tiles_m = (NDY == 3 ? 1 : 3) * ctm;
     int idx = p.xcd ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
     const int tn = idx % tiles_n;
     idx /= tiles_n;
     const int tm = idx % tiles_m;
     const int split = idx / tiles_m;
-    const int dy = tm / ctm, ca0 = (tm - dy * ctm) * BM;
+    const int dy = NDY == 3 ? 0 : tm / ctm, ca0 = (tm - dy * ctm) * BM;  // (first) tap row
     const int tapB = (tn * BN) / p.CB, cb0 = tn * BN - tapB * p.CB;
     const int H = p.H, W = p.W;
 
@@ -674,14 +680,15 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void wgrad_row3_kernel(WgradArg
     auto issue = [&](int pc) {
         amask = bmask = 0;
         const Pix q = decode(pc, H, W);  // chunk start; the chunk stays on this row
-        const int yy = q.y + dy - 1;
-        const bool rowok = (yy >= 0) & (yy < H);
-        const int rbase = (q.img * H + (rowok ? yy : q.y)) * W;
 #pragma unroll
         for (int i = 0; i < AP; ++i) {
-            const int r = arow + i * ARPP;
+            const int r0 = arow + i * ARPP;
+            const int dyi = NDY == 3 ? r0 / HROWS : 0, r = r0 - dyi * HROWS;
+            const int yy = q.y + dy + dyi - 1;
+            const bool rowok = (yy >= 0) & (yy < H);
+            const int rbase = (q.img * H + (rowok ? yy : q.y)) * W;
             const int xx = q.x + r - 1;
-            const bool valid = rowok & (r < AROWS) & (xx >= 0) & (xx < W);
+            const bool valid = rowok & (r0 < AROWS) & (xx >= 0) & (xx < W);
             amask |= valid ? (1u << i) : 0u;
             const int src = valid ? rbase + xx : pc;
             ra[i] = *(const f32x4*)(p.a + (size_t)src * p.lda + p.aoff + ca0 + ac4 * 4);
@@ -733,9 +740,10 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void wgrad_row3_kernel(WgradArg
         }
     };
 
-    f32x16 acc[3][MT][NT];
+    constexpr int NTAP = 3 * NDY;
+    f32x16 acc[NTAP][MT][NT];
 #pragma unroll
-    for (int d = 0; d < 3; ++d)
+    for (int d = 0; d < NTAP; ++d)
 #pragma unroll
         for (int i = 0; i < MT; ++i)
 #pragma unroll
@@ -760,10 +768,12 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void wgrad_row3_kernel(WgradArg
 #pragma unroll
                 for (int nt = 0; nt < NT; ++nt) bf[nt] = Bs[pr * LDB + wn * WN + nt * 32 + li];
 #pragma unroll
-                for (int d = 0; d < 3; ++d) {
+                for (int d = 0; d < NTAP; ++d) {
+                    // tap d = 3 dyi + dx reads halo row pr + dx of image row dyi
+                    const int ar = (d / 3) * HROWS + pr + d % 3;
                     float af[MT];
 #pragma unroll
-                    for (int mt = 0; mt < MT; ++mt) af[mt] = As[(pr + d) * LDA + wm * WM + mt * 32 + li];
+                    for (int mt = 0; mt < MT; ++mt) af[mt] = As[ar * LDA + wm * WM + mt * 32 + li];
 #pragma unroll
                     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
@@ -797,7 +807,7 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void wgrad_row3_kernel(WgradArg
 
     float* slab = p.slab + (size_t)split * p.Mw * p.Nw;
 #pragma unroll
-    for (int d = 0; d < 3; ++d)
+    for (int d = 0; d < NTAP; ++d)
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
@@ -1299,9 +1309,12 @@ using Wr3Tile5 = WgTile<128, 64, 64, 32, 16>;   // tile 21 on 16-pixel chunks (1
 #define WGRAD_ROW3_TILES(X) \
     X(20, Wr3Tile0) X(21, Wr3Tile1) X(22, Wr3Tile2) X(23, Wr3Tile3) X(24, Wr3Tile4) X(25, Wr3Tile5)
 
+// tile 26 (row9): all three tap rows of a 64x64 channel tile per block (wgrad_row3_kernel
+// NDY = 3); it counts 3 taps here so that its split-K partition is tile 20's
 int wgrad_tile_taps(int tile) { return tile >= 20 ? 3 : 1; }
 
 int wgrad_tile_dims(int tile, int* bm, int* bn, int* bkp) {
+    if (tile == 26) tile = 20;                 // row9 (64x64, three tap rows per block)
     if (tile == 34) tile = 21;                 // pipelined row3, 128x64 at 2 waves / SIMD
     if (tile >= 30 && tile <= 33) tile -= 10;  // pipelined row3 (kernels_wgrad_pipe.hip)
     if (tile == 10 || tile == 15) return wgrad16_tile_dims(tile - 10, bm, bn, bkp);
@@ -1331,6 +1344,15 @@ static int wgrad_row3_tile(const WgradArgs& a, int tile, hipStream_t s) {
     }
     WGRAD_ROW3_TILES(WR3_CASE)
 #undef WR3_CASE
+    if (tile == 26) {  // row9 on tile 20's shape, two waves per SIMD (144 accumulators)
+        using T = WgTile<64, 64, 32, 32, 32, 2>;
+        if (a.Mw != 9 * a.CA || a.CA % T::BM || a.Nw % T::BN || a.CB % T::BN || a.pps % T::BKP ||
+            a.W % T::BKP)
+            return -1;
+        const dim3 grid((a.CA / T::BM) * (a.Nw / T::BN) * a.splits);
+        hipLaunchKernelGGL((wgrad_row3_kernel<AOP, BDZ, T, 3>), grid, dim3(T::THREADS), 0, s, a);
+        return (int)hipGetLastError();
+    }
     return -1;
 }
 

@@ -137,6 +137,8 @@ struct Options {
                                // 2.02 -> 0.97 GB at equal time), 2 row GEMMs, 3 wgrad
     int wgrad_stream = 0;      // weight gradients on a second stream (bit-identical)
     int wgrad_row3_16 = 0;     // row3 weight gradients on 16-pixel rows (tile 25)
+    int wgrad_row9 = 0;        // 64x64-channel row3 weight gradients with all three tap rows
+                               // per block (tile 26: x and dz / do, y read once, not 3x)
     int reduce_stream = 0;     // only the split-K slab reductions + bias sums on it (bit-identical;
                                // 1 % slower: they slow the concurrent dgrad GEMM, r03)
     int dz_in_loaders = 0;     // BN-backward dz inside the GEMM loaders (model.py order)
@@ -172,7 +174,7 @@ const OptionDesc OPTION_TABLE[] = {
     {"xcd16", &Options::xcd16},                 {"xcd_remap", &Options::xcd_remap},
     {"wgrad_stream", &Options::wgrad_stream},   {"dz_in_loaders", &Options::dz_in_loaders},
     {"dz_in_wgrad", &Options::dz_in_wgrad},     {"reduce_stream", &Options::reduce_stream},
-    {"wgrad_row3_16", &Options::wgrad_row3_16},
+    {"wgrad_row3_16", &Options::wgrad_row3_16}, {"wgrad_row9", &Options::wgrad_row9},
     {"row3_gemm", &Options::row3_gemm},
 };
 
@@ -590,6 +592,7 @@ WgradCfg wgrad_cfg(const unet_ctx* c, int CA, int tapsA, int CB, int tapsB, int6
             if (r3t < 20 && c->opt.wgrad_row3_big >= 20 && !c->opt.wgrad_row3_pipe &&
                 CA % 128 == 0 && CB % 128 == 0)
                 w.tile = c->opt.wgrad_row3_big;
+            if (w.tile == 20 && c->opt.wgrad_row9) w.tile = 26;  // same split-K partition
         }
         wgrad_tile_dims(w.tile, &w.bm, &w.bn, &w.bkp);
     }
@@ -902,7 +905,8 @@ std::string r3label(const char* fam, const RowGemmArgs& g, int layer) {
 std::string wlabel(const char* fam, const WgradCfg& w, int layer) {
     char b[112];
     snprintf(b, sizeof b, "%s/wgrad%s_%dx%dx%d|%d", fam,
-             w.tile >= 30 ? (w.tile == 34 ? "3p2" : "3p") : (w.tile >= 20 ? "3" : ""), w.bm, w.bn, w.bkp, layer);
+             w.tile >= 30 ? (w.tile == 34 ? "3p2" : "3p") : (w.tile == 26 ? "9" : (w.tile >= 20 ? "3" : "")),
+             w.bm, w.bn, w.bkp, layer);
     return b;
 }
 
