@@ -1121,6 +1121,12 @@ int rowgemm_tile_dims(int tile, int* bm, int* bn, int* bk) {
         *bk = 32;
         return 0;
     }
+    if (tile >= 29 && tile <= 32) {  // persistent pipelined 128x64 (29, 30) / 128x128 (31, 32)
+        *bm = 128;
+        *bn = tile <= 30 ? 64 : 128;
+        *bk = 32;
+        return 0;
+    }
     if (tile == 27 || tile == 28) {  // rowgemm_pipe_kernel 256x64, 64x64 wave tiles
         *bm = 256;
         *bn = 64;
@@ -1146,7 +1152,7 @@ int rowgemm_tile_dims(int tile, int* bm, int* bn, int* bk) {
 }
 
 int rowgemm_tile_dbuf(int tile) {
-    if ((tile >= 16 && tile <= 19) || (tile >= 23 && tile <= 28)) return 2;  // pipelined
+    if ((tile >= 16 && tile <= 19) || (tile >= 23 && tile <= 32)) return 2;  // pipelined
     if (tile >= 20 && tile <= 22) return 3;  // LDS-DMA
 #define RG_DB(id, T) \
     if (tile == id) return T::DBUF ? 1 : 0;
@@ -1270,6 +1276,10 @@ int launch_rowgemm(const RowGemmArgs& a, int tile, hipStream_t s) {
     if (tile >= 25 && tile <= 28) {  // 128x64 at three blocks per CU / 256x64 (N = 64)
         if (rowgemm_pipe_ok(a)) return launch_rowgemm_pipe(a, tile - 19, s);
         tile = 1;
+    }
+    if (tile >= 29 && tile <= 32) {  // persistent: tiles 25 / 26 / 16 / 18 walking their tiles
+        if (rowgemm_pipe_ok(a)) return launch_rowgemm_pipe(a, tile - 19, s);
+        tile = tile <= 30 ? 1 : 4;
     }
     return a.bt16 ? rowgemm_dispatch<true>(a, tile, s) : rowgemm_dispatch<false>(a, tile, s);
 }

@@ -888,7 +888,7 @@ std::string tlabel(const char* fam, int tile, int layer) {
     char b[112];
     const int db = rowgemm_tile_dbuf(tile);  // 1 = two LDS images, 2 = pipelined, 3 = LDS-DMA
     snprintf(b, sizeof b, "%s/rowgemm_%dx%dx%d%s|%d", fam, bm, bn, bk,
-             db == 3 ? "m" : (db == 2 ? "p" : (db ? "d" : "")), layer);
+             db == 3 ? "m" : (db == 2 ? (tile >= 29 && tile <= 32 ? "q" : "p") : (db ? "d" : "")), layer);
     return b;
 }
 
