@@ -647,7 +647,8 @@ def test_pipe_gemm_bit_identical(variant, B, H, W):
     """Row-GEMM tiles 16..19 (kernels_gemm_pipe.hip: the software-pipelined schedule of the
     128x128 / 128x64 f32 tiles, global loads one or two chunks ahead; 18 / 16 are the
     defaults; 25 / 26: 128x64 at three blocks per CU; 27 / 28: 256x64 on 64x64 wave tiles;
-    29..32: persistent blocks walking several tiles of 25 / 26 / 16 / 18) and 20..22 (kernels_gemm_dma.hip: LDS-DMA operands, the BN prologue applied
+    29..32: persistent blocks walking several tiles of 25 / 26 / 16 / 18; 22: LDS-DMA 128x64 at
+    three stages) and 20..22 (kernels_gemm_dma.hip: LDS-DMA operands, the BN prologue applied
     after the LDS read) walk K in the same order with the same prologue arithmetic and the
     same epilogues as the register-staged rowgemm_kernel tiles (4, 0, 1), so a training
     step -- logits and the whole gradient arena -- is bit-identical across the schedules.  48x80 has M
@@ -661,7 +662,7 @@ def test_pipe_gemm_bit_identical(variant, B, H, W):
     outs = []
     for tiles in ((4, 0, 1, 0), (16, 16, 17, 16), (18, 18, 19, 18), (20, 20, 21, 20),
                   (16, 18, 25, 26), (18, 16, 26, 25), (18, 18, 27, 27), (16, 16, 28, 28),
-                  (32, 31, 29, 30), (31, 32, 30, 29)):
+                  (32, 31, 29, 30), (31, 32, 30, 29), (18, 16, 22, 22)):
         if variant == "model":
             m = hip_model(O.make_params(42), DEV)
         elif variant == "mod":

@@ -1105,7 +1105,7 @@ static int rowgemm_tile(const RowGemmArgs& a, int tile, hipStream_t s) {
 int rowgemm_tile_dims(int tile, int* bm, int* bn, int* bk) {
     if (tile >= 20 && tile <= 22) {  // rowgemm_dma_kernel (LDS-DMA operands)
         *bm = 128;
-        *bn = tile == 21 ? 64 : 128;
+        *bn = tile == 20 ? 128 : 64;  // 22: 128x64, three stages
         *bk = 32;
         return 0;
     }
@@ -1263,7 +1263,7 @@ int launch_rowgemm(const RowGemmArgs& a, int tile, hipStream_t s) {
     // ids 20..22: both operands by LDS-DMA (kernels_gemm_dma.hip); else the pipelined tile
     if (tile >= 20 && tile <= 22) {
         if (rowgemm_dma_ok(a)) return launch_rowgemm_dma(a, tile - 20, s);
-        tile = tile == 21 ? 17 : 16;
+        tile = tile == 20 ? 16 : 17;
     }
     if (tile >= 16 && tile <= 19) {
         if (rowgemm_pipe_ok(a)) return launch_rowgemm_pipe(a, tile - 16, s);

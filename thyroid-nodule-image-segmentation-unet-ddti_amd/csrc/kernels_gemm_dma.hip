@@ -86,7 +86,7 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_dma_kernel(RowGemm
     constexpr int AI = BM / (RPI * WAVES), BI = BN / (RPI * WAVES);
     static_assert(AI * RPI * WAVES == BM && BI * RPI * WAVES == BN, "loader shape");
     constexpr int GPC = AI + BI;  // DMA instructions per chunk per wave
-    static_assert(S == 2, "two LDS stages");
+    static_assert(S == 2 || S == 3, "two or three LDS stages");
     constexpr int STAGE = (BM + BN) * RB;
     static_assert(STAGE >= 2 * (BM / 64) * BN * 8, "epilogue scratch");
     // The two stages are separate LDS objects and the chunk loop is unrolled by two, so
@@ -96,6 +96,7 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_dma_kernel(RowGemm
     // included).
     __shared__ __attribute__((aligned(1024))) char st0[STAGE];
     __shared__ __attribute__((aligned(1024))) char st1[STAGE];
+    __shared__ __attribute__((aligned(1024))) char st2[S == 3 ? STAGE : 16];
     __shared__ __attribute__((aligned(16))) float sct[AFFINE ? 2 * DMA_MAXC : 4];
 
     const int tid = threadIdx.x, lane = tid & 63;
@@ -269,6 +270,33 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_dma_kernel(RowGemm
         // every wave's reads of this stage have returned (waited above) before any restages it
         block_barrier();
     };
+    if constexpr (S == 3) {
+        // chunk c in stage c % 3; chunks kc + 1 and kc + 2 fly during chunk kc's MFMAs (kc + 2
+        // restages the image chunk kc - 1 left, free since compute's closing barrier)
+        issue(0, st0);
+        if (nk > 1) issue(1, st1);
+        auto stage = [&](int kc, const char* cur, char* nxt2) {
+            if (kc + 2 < nk) {
+                issue(kc + 2, nxt2);
+                wait_vm<2 * GPC>();
+            } else if (kc + 1 < nk) {
+                wait_vm<GPC>();
+            } else {
+                wait_vm<0>();
+            }
+            block_barrier();
+            compute(kc, cur);
+        };
+        for (int kc = 0; kc < nk; kc += 3) {
+            stage(kc, st0, st2);
+            if (kc + 1 >= nk) break;
+            stage(kc + 1, st1, st0);
+            if (kc + 2 >= nk) break;
+            stage(kc + 2, st2, st1);
+        }
+        row_epilogue<EMODE, BM, BN, WM, WN>(p, acc, m0, n0, tile_m, wm, wn, lane, tid, (float*)st0);
+        return;
+    }
     // even chunks in st0, odd chunks in st1; chunk kc+1's DMA flies during chunk kc's MFMAs
     issue(0, st0);
     for (int kc = 0; kc < nk; kc += 2) {
@@ -295,6 +323,8 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_dma_kernel(RowGemm
 
 using DmaTile0 = DmaTile<128, 128, 64, 64, 2, 2>;  // 2 stages, 64 KB (+8 KB affine table)
 using DmaTile1 = DmaTile<128, 64, 64, 32, 2, 2>;
+// N = 64 with two chunks in flight: 3 stages of 24 KB, two blocks per CU
+using DmaTile2 = DmaTile<128, 64, 64, 32, 3, 2>;
 
 template <int AMODE, int AOP, int EMODE, class T>
 static int dma_go(const RowGemmArgs& a, hipStream_t s) {
@@ -309,6 +339,7 @@ template <int AMODE, int AOP, int EMODE>
 static int dma_tile(const RowGemmArgs& a, int tile, hipStream_t s) {
     if (tile == 0) return dma_go<AMODE, AOP, EMODE, DmaTile0>(a, s);
     if (tile == 1) return dma_go<AMODE, AOP, EMODE, DmaTile1>(a, s);
+    if (tile == 2) return dma_go<AMODE, AOP, EMODE, DmaTile2>(a, s);
     return -1;
 }
 
