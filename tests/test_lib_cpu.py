@@ -312,7 +312,8 @@ def test_schedule_option_defaults():
             "rg16_bn_k": 8192, "wg16": 1, "wg16_tile": 2, "wgrad16_blocks": 1536,
             "wgrad_stream": 0, "dz_in_loaders": 0, "row3_gemm": 0, "xcd_remap": 1,
             "tile_convt": -1, "tile_convt_dgrad": 26, "rg16_m16": 0, "rg16_pp": 0, "rg16_xp": 0,
-            "dz_in_wgrad": 256, "rg16_r3": 1, "reduce_stream": 0}
+            "dz_in_wgrad": 256, "rg16_r3": 1, "reduce_stream": 0, "wgrad_row9": 0,
+            "wgrad_row3_16": 0}
     got = {k: fresh.get_option(k) for k in want}
     assert got == want
 
