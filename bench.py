@@ -7,7 +7,10 @@ synthetic bs=32 x 1x256x256 batch per GPU (BASELINE config 2; config 3 = 8 ranks
 inputs resident in HBM before the timed region.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
-    torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU, RCCL)
+        N > 1 without a launcher: this process starts N rank processes of itself (one per
+        GPU, RCCL over xGMI; rank env + 127.0.0.1 rendezvous) and exits with their status
+    torchrun --nproc-per-node N bench.py --gpus N ...   (same ranks, started by torchrun)
+    BENCH_DIST_BACKEND=gloo python bench.py --gpus 2    (DP rehearsal on one GPU)
     python bench.py --config 4      models/mod.py UNet(base 128, depth 5), 512x512, bs 8
                                     (BASELINE config 4; not the headline metric)
 
@@ -64,7 +67,74 @@ def parse():
     ap.add_argument("--timing", default="dominant", choices=("dominant", "all"),
                     help="per-launch events in the timed region: around the dominant kernel "
                          "only (default) or around every launch")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher plumbing check: every rank prints its rank environment as "
+                         "one JSON line and exits (no torch, no GPU)")
     return ap.parse_args()
+
+
+_RANK_ENV = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")
+
+
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def rank_envs(n, port, base=None):
+    """Environment of each of the n rank processes `launch` starts (one process per GPU,
+    as torch.distributed.run would set it up on one node; rendezvous on 127.0.0.1)."""
+    base = dict(os.environ if base is None else base)
+    envs = []
+    for r in range(n):
+        e = dict(base)
+        e.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                 LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        envs.append(e)
+    return envs
+
+
+def launch(n, argv):
+    """`python bench.py --gpus N` without a launcher: start N fresh child processes of this
+    script, one per GPU (the reference drives every GPU from one command through
+    nn.DataParallel, utils/trainer.py:28-30).  Nothing here touches torch or the GPU, and
+    the children are started with Popen (no exec of the parent).  Rank 0's stdout is the
+    children's shared stdout, so its one JSON line is the command's output.  If any rank
+    fails the others are stopped (they would wait in a collective) and the exit status is
+    non-zero."""
+    import signal
+    import subprocess
+    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=e,
+                              start_new_session=True)
+             for e in rank_envs(n, _free_port())]
+    status = 0
+    try:
+        while procs:
+            for p in list(procs):
+                rc = p.poll()
+                if rc is None:
+                    continue
+                procs.remove(p)
+                if rc != 0 and status == 0:
+                    status = rc if rc > 0 else 128 - rc
+                    print(f"bench.py: rank process {p.pid} exited with {rc}; stopping the "
+                          f"other ranks", file=sys.stderr, flush=True)
+                    for q in procs:
+                        try:
+                            os.killpg(q.pid, signal.SIGTERM)
+                        except ProcessLookupError:
+                            pass
+            time.sleep(0.05)
+    except KeyboardInterrupt:
+        for q in procs:
+            try:
+                os.killpg(q.pid, signal.SIGTERM)
+            except ProcessLookupError:
+                pass
+        raise
+    return status
 
 
 def cpu_baseline(steps, size, config=2):
@@ -169,16 +239,36 @@ def load_pmc(kernel, config=2, mfma="fp32"):
 
 def main():
     args = parse()
-    import torch
-    import torch.distributed as dist
-
+    if args.gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # no launcher: this process only starts the ranks (before any torch / HIP call)
+        sys.exit(launch(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started {world} "
+                         f"ranks (WORLD_SIZE); n_gpus must equal the rank count")
+    if args.dry_run:
+        print(json.dumps({"dry_run": True, "argv": sys.argv[1:],
+                          **{k: os.environ.get(k) for k in _RANK_ENV}}), flush=True)
+        fail = os.environ.get("BENCH_DRY_RUN_FAIL_RANK")  # launcher test: one rank fails,
+        if fail is not None:                              # the others wait as if in a collective
+            if str(rank) == fail:
+                sys.exit(3)
+            time.sleep(60)
+        return
+    import torch
+    import torch.distributed as dist
+
     # BENCH_DIST_BACKEND=gloo: rehearsal of the N>1 path with several ranks on one GPU
     # (RCCL refuses two ranks per device); the real runs use "nccl" (= RCCL over xGMI)
     backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")
     ndev = torch.cuda.device_count()
+    if backend == "nccl" and world > ndev:
+        raise SystemExit(f"bench.py: {world} ranks but only {ndev} visible GPU(s); one rank "
+                         f"per GPU over RCCL (BENCH_DIST_BACKEND=gloo rehearses on fewer)")
     local = local % ndev if backend != "nccl" and ndev else local
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -349,7 +439,10 @@ def main():
            "data": "synthetic",
            "config": {"workload": workload, "model": mname, "global_batch": B * world,
                       "image": [1, S, S], "parallelism": f"dp{world}"},
+           "ranks": dist.get_world_size() if world > 1 else 1,
+           "backend": (("rccl" if backend == "nccl" else backend) if world > 1 else None),
            "roofline": roofline}
+    assert out["n_gpus"] == out["ranks"], (out["n_gpus"], out["ranks"])
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not cres:
         sample, out["cpu_baseline"] = cpu_baseline(args.cpu_steps, S, int(args.config))
         if sample is not None:

@@ -378,3 +378,94 @@ def test_trainer_dp2_eval_uses_replica0_buffers(tmp_path, golden_dir, tag, lr):
         assert rel_max(got, ref_vl) <= max(2 * spread, 1e-4)
         assert abs(res[0][3] - want_loss) < 1e-3, (res[0][3], want_loss)
     assert n == 5888
+
+
+def _hygiene_worker(rank, world, port, q, tmp):
+    import sys
+    for p in (REPO, PKG, os.path.join(REPO, "tests")):
+        sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import argparse
+        import random
+        import unet_hip
+        from data.data_loader import DataParallelShardSampler, SyntheticSegmentation, dp_collate
+        from models.model import UNet
+        from oracle import unet_ref_cpu as O
+        from utils.trainer import Trainer
+        from utils.utils import Config, create_logger
+        torch.cuda.set_device(0)
+        # per-rank host RNG streams (main.py seeds augmentations per rank): the mixup
+        # decision, lam and permutation must still be rank 0's on every rank
+        random.seed(100 + rank)
+        np.random.seed(100 + rank)
+        ns = argparse.Namespace(model_type="UNet", lr=1e-4, bce_ratio=1.0, dice_ratio=1.0,
+                                focal_ratio=0.0, boundary_ratio=0.0, use_mixup=True,
+                                mixup_prob=0.5, mixup_alpha=0.2, epochs=1, early_stop_patience=5,
+                                batch_size=4, num_workers=0)
+        cfg = Config(ns, base_dir=os.path.join(tmp, "exp"), stamp="shared")
+        cfg.device = torch.device("cuda:0")
+
+        def loader(n, bs, seed):
+            return torch.utils.data.DataLoader(
+                SyntheticSegmentation(n, 64, seed=seed),
+                batch_sampler=DataParallelShardSampler(n, bs, True, rank, world, seed=3),
+                collate_fn=dp_collate())
+        # 7 samples at global batch 3: shards 2 + 1 (ragged) and a last batch 1 + empty
+        loaders = (loader(7, 3, 4), loader(3, 2, 5), loader(3, 2, 6))
+        m = UNet()
+        m.load_state_dict({**O.make_params(42), **O.init_buffers()})
+        log = os.path.join(tmp, "shared.log")  # the same file for both ranks, as in main.py
+        tr = Trainer(cfg, loaders, create_logger(log), m)
+        for ep in range(2):
+            tr.train_one_epoch(ep)
+        tr.validate(0)
+        tr.test()
+        params = tr.model._state.param_arena.detach().cpu().clone()
+        pd = params.clone()
+        dist.broadcast(pd, src=0)
+        same = bool(torch.equal(pd, params))
+        # validate() ran gathered eval losses: they must not license summing the gradients
+        # of a per-rank LOCAL loss (DistributedUNet(average=False) refuses it)
+        ds = SyntheticSegmentation(2, 64, seed=9)
+        x = torch.stack([ds[i][0] for i in range(2)]).to("cuda:0")
+        t = torch.stack([ds[i][1] for i in range(2)]).to("cuda:0")
+        tr.model.train()
+        tr.optimizer.zero_grad(set_to_none=True)
+        unet_hip.seg_losses(tr.model(x), t)[0].backward()
+        refused = False
+        try:
+            tr.ddp.reduce_gradients()
+        except RuntimeError:
+            refused = True
+        dist.barrier()
+        q.put((rank, same, refused))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+def test_trainer_dp2_mixup_logging_hygiene(tmp_path):
+    """Two ranks with different host RNG streams, mixup on (prob 0.5), ragged and empty
+    shards (7 samples at global batch 3), two epochs + validate + test: no collective
+    mismatch (rank 0's mixup draws are broadcast), identical parameters on both ranks,
+    each log line written once to the shared log file (rank 0 only), and a local-loss
+    gradient sum after validate() is still refused."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_hygiene_worker, args=(r, 2, port, q, str(tmp_path)))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=500), q.get(timeout=500)], key=lambda r: r[0])
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    assert res[0][1] and res[1][1], "ranks diverged"
+    assert res[0][2] and res[1][2], "local-loss gradient sum was not refused after validate()"
+    text = open(os.path.join(str(tmp_path), "shared.log")).read()
+    assert text.count("Train Epoch: 1,") == 1 and text.count("Train Epoch: 2,") == 1, text
+    assert text.count("Test Metrics") == 1, text

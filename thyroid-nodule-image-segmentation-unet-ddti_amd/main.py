@@ -14,9 +14,12 @@ Multi-GPU: launch one process per GPU, e.g.
 (RCCL backend; replaces nn.DataParallel of utils/trainer.py:28-30).
 """
 import argparse
+import logging
 import os
+import random
 import sys
 
+import numpy as np
 import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -82,10 +85,27 @@ def main(args):
         torch.cuda.set_device(local)
         torch.distributed.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
     set_seed(seed=42)
-    config = Config(args)
+    rank = torch.distributed.get_rank() if world > 1 else 0
+    if rank:
+        # per-rank host augmentation streams (utils/transforms.py draws from random / numpy
+        # in the main process when num_workers == 0): otherwise every shard would get rank 0's
+        # Flip / Rotate / ... sequence.  torch's stream stays shared (identical model init;
+        # parameters are broadcast from rank 0 anyway) and the mixup draws come from rank 0.
+        random.seed(42 + rank)
+        np.random.seed(42 + rank)
+    stamp = [None]
+    if world > 1:  # one experiments/<model>_<stamp>/ tree for the job: rank 0's
+        stamp = [Config.make_stamp()] if rank == 0 else [None]
+        torch.distributed.broadcast_object_list(stamp, src=0)
+    config = Config(args, stamp=stamp[0])
     if torch.cuda.is_available():
         config.device = torch.device("cuda", torch.cuda.current_device())
-    logger = create_logger(os.path.join(config.log_dir, "train_log.log"))
+    if rank == 0:
+        logger = create_logger(os.path.join(config.log_dir, "train_log.log"))
+    else:  # one writer of the shared log file (the Trainer also logs from rank 0 only)
+        logger = logging.getLogger(f"unet_hip.rank{rank}")
+        logger.addHandler(logging.NullHandler())
+        logger.propagate = False
     if args.model_type not in ("UNet", "ModUNet", "ResUNet"):
         raise SystemExit(f"model_type {args.model_type!r}: the HIP path has UNet (models/model.py), "
                          "ModUNet and ResUNet (models/mod.py)")
@@ -110,10 +130,12 @@ def main(args):
         if world > 1:
             # nn.DataParallel's split of every global batch (utils/trainer.py:28-30):
             # --batch_size stays the GLOBAL batch, as in the reference
-            rank = torch.distributed.get_rank()
             bs = DataParallelShardSampler(len(ds), config.batch_size, i != 1, rank, world, seed=42)
+            # per-rank worker seeds (the sampler's shared order seed is separate): DataLoader
+            # derives each worker's random / numpy / torch seeds from this generator
             dl = torch.utils.data.DataLoader(ds, batch_sampler=bs, num_workers=config.num_workers,
-                                             collate_fn=dp_collate(u8_collate if gpu_tf else None))
+                                             collate_fn=dp_collate(u8_collate if gpu_tf else None),
+                                             generator=torch.Generator().manual_seed(42 + rank))
         elif gpu_tf:
             dl = torch.utils.data.DataLoader(ds, shuffle=(i != 1), **kw)
         else:
@@ -130,7 +152,8 @@ def main(args):
         model.load_state_dict(torch.load(config.checkpoint_path, weights_only=True))
     n = sum(p.numel() for p in model.parameters() if p.requires_grad)
     logger.info(f"Model: {config.model_type} | Trainable params: {n / 1e6:.2f}M ({n:,})")
-    print(f"[PARAMS] {config.model_type},{n}")
+    if rank == 0:
+        print(f"[PARAMS] {config.model_type},{n}")
 
     trainer = Trainer(config, tuple(loaders), logger, model)
     if args.mode in ("train", "both"):

@@ -157,7 +157,10 @@ class DistributedUNet:
     def losses(self, logits, targets, alpha=0.4, beta=0.6, gamma=2.0):
         from .functional import seg_losses
         grp = self.group if self.group is not None else dist.group.WORLD
-        self._gathered_loss = True
+        if torch.is_grad_enabled() and logits.requires_grad:
+            # only a differentiable (training) loss licenses the next gradient sum; an
+            # eval / no_grad pass in between (validate) must not
+            self._gathered_loss = True
         return seg_losses(logits, targets, alpha, beta, gamma, group=grp)
 
     def empty_step(self, extra_scalar_reduces=0):

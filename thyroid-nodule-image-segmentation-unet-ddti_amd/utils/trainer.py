@@ -52,6 +52,14 @@ except Exception:  # tensorboard is not installed in every image: logging only
         def close(self):
             pass
 
+class _NullWriter:
+    def add_scalar(self, *a, **k):
+        pass
+
+    def close(self):
+        pass
+
+
 try:
     from tqdm import tqdm
 except Exception:
@@ -63,10 +71,31 @@ def _distributed():
     return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
 
 
+def _is_rank0():
+    return not _distributed() or dist.get_rank() == 0
+
+
+class _Rank0Logger:
+    """Under data parallelism every rank runs the Trainer, but the reference's single process
+    writes each log line once: only rank 0 forwards to the shared logger (whose file handler
+    all ranks would otherwise append to)."""
+
+    def __init__(self, logger, enabled):
+        self._logger, self._enabled = logger, enabled
+
+    def __getattr__(self, name):
+        attr = getattr(self._logger, name)
+        if name in ("debug", "info", "warning", "error", "critical", "exception", "log") \
+                and not self._enabled:
+            return lambda *a, **k: None
+        return attr
+
+
 class Trainer:
     def __init__(self, config, data_loader, logger, model):
         self.config = config
-        self.logger = logger
+        self.rank0 = _is_rank0()
+        self.logger = _Rank0Logger(logger, self.rank0)
         dev = getattr(config, "device", torch.device("cuda"))
         if _distributed():
             dev = torch.device("cuda", torch.cuda.current_device())
@@ -84,7 +113,8 @@ class Trainer:
         self.criterion_boundary = BoundaryLoss()
         self.early_stopping = EarlyStopping(logger=self.logger,
                                             patience=getattr(config, "early_stop_patience", 50), delta=0)
-        self.writer = SummaryWriter(log_dir=getattr(config, "result_dir", None))
+        self.writer = (SummaryWriter(log_dir=getattr(config, "result_dir", None)) if self.rank0
+                       else _NullWriter())
         self.rt = self.model._state.rt
 
     # -------------------------------------------------------------- helpers
@@ -118,6 +148,13 @@ class Trainer:
                 loss = loss + c.boundary_ratio * lb
                 total = loss
         return loss, l, lb, total
+
+    def _rank0_mixup(self, mix, lam):
+        d = torch.tensor([1.0 if mix else 0.0, lam if mix else 0.0], dtype=torch.float64,
+                         device=self.device)
+        dist.broadcast(d, src=self.ddp._src(), group=self.ddp.group)
+        mix = bool(d[0].item() != 0.0)
+        return mix, (float(d[1].item()) if mix else None)
 
     def _reduce_scalars(self, sums, n_seen):
         """Epoch means weighted like the reference's AverageMeter.update(loss, batch size)
@@ -166,6 +203,10 @@ class Trainer:
             # whole batch before DataParallel scatters it, and each rank keeps its slice.
             mix = train and random.random() < self.config.mixup_prob and self.config.use_mixup
             lam = np.random.beta(self.config.mixup_alpha, self.config.mixup_alpha) if mix else None
+            if train and self.config.use_mixup and self.ddp is not None:
+                # the host RNG streams differ per rank (per-rank augmentation seeds, shards of
+                # unequal size), but gather_batch is a collective: rank 0's draws decide
+                mix, lam = self._rank0_mixup(mix, lam)
             if batch is not None:
                 images, masks = batch
                 images = images.to(self.device, non_blocking=True).float()
@@ -174,6 +215,7 @@ class Trainer:
                 gi, gm, off, n = self.ddp.gather_batch(None if batch is None else images,
                                                        None if batch is None else masks, self.device)
                 perm = torch.randperm(gi.size(0)).to(self.device)
+                dist.broadcast(perm, src=self.ddp._src(), group=self.ddp.group)
                 if batch is not None:
                     sl = slice(off, off + n)
                     images = lam * gi[sl] + (1.0 - lam) * gi[perm[sl]]
@@ -263,6 +305,7 @@ class Trainer:
         keep = []
         for batch in tqdm(self.test_loader, desc="Testing Model", leave=True):
             if batch is None:  # empty DataParallel shard: nothing to count on this rank
+                keep.append(None)
                 continue
             images, masks = batch
             images = images.to(self.device).float()
@@ -281,11 +324,29 @@ class Trainer:
                f"  TP={m['TP']}, FP={m['FP']}, FN={m['FN']}, TN={m['TN']}\n"
                f"  ACC={m['ACC']:.4f}, Precision={m['Precision']:.4f}, "
                f"Recall={m['Recall']:.4f}, F1={m['F1']:.4f}, IoU={m['IoU']:.4f}")
-        print(msg)
+        if self.rank0:
+            print(msg)
         self.logger.info(msg)
-        if keep:
+        if _distributed() and self._can_plot():
+            # one set of PNGs over the whole test set, in the reference's sample order: batch
+            # by batch, each batch's shards in rank order (DataParallel's gather order)
+            parts = [None] * dist.get_world_size()
+            dist.all_gather_object(parts, keep)
+            keep = ([p[b] for b in range(len(parts[0])) for p in parts if b < len(p)]
+                    if self.rank0 else [])
+        keep = [k for k in keep if k is not None]
+        if keep and self.rank0:
             self._plot_contours(keep)
         return m
+
+    @staticmethod
+    def _can_plot():
+        try:
+            import matplotlib  # noqa: F401
+            from skimage import measure  # noqa: F401
+        except Exception:
+            return False
+        return True
 
     def _plot_contours(self, keep):
         try:

@@ -20,11 +20,11 @@ import yaml
 class Config:
     """argparse namespace -> attributes + experiments/<model>_<UTC+8 stamp>/ tree + YAML dump."""
 
-    def __init__(self, args, base_dir="experiments"):
+    def __init__(self, args, base_dir="experiments", stamp=None):
         for k, v in vars(args).items():
             setattr(self, k, v)
         self.device = torch.device("cuda" if torch.cuda.is_available() else "cpu")
-        stamp = (datetime.now(timezone.utc) + timedelta(hours=8)).strftime("%Y%m%d_%H%M%S")
+        stamp = stamp or self.make_stamp()
         self.base_dir = base_dir
         self.cfg_dir = os.path.join(base_dir, f"{self.model_type}_{stamp}")
         self.model_dir = os.path.join(self.cfg_dir, "models")
@@ -32,6 +32,15 @@ class Config:
         self.result_dir = os.path.join(self.cfg_dir, "result")
         for d in (self.cfg_dir, self.model_dir, self.log_dir, self.result_dir):
             os.makedirs(d, exist_ok=True)
+        if not (torch.distributed.is_available() and torch.distributed.is_initialized()) \
+                or torch.distributed.get_rank() == 0:
+            self._dump()
+
+    @staticmethod
+    def make_stamp():
+        return (datetime.now(timezone.utc) + timedelta(hours=8)).strftime("%Y%m%d_%H%M%S")
+
+    def _dump(self):
         with open(os.path.join(self.cfg_dir, "config.yaml"), "w") as f:
             yaml.safe_dump({k: (str(v) if isinstance(v, torch.device) else v)
                             for k, v in self.__dict__.items() if not k.startswith("_")}, f)
