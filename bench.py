@@ -347,7 +347,9 @@ def main():
     torch.cuda.synchronize()
     fam, kern, layer = aggregate(rt.timing_records())
     rt.timing(False)
-    dom = max(kern, key=lambda k: kern[k][1])
+    # the dominant MFMA kernel: most GPU time among the kernel instances with algorithmic
+    # FLOPs (GEMMs; bandwidth passes carry none and have no MFMA roofline)
+    dom = max((k for k in kern if kern[k][2] > 0), key=lambda k: kern[k][1])
     # 2. the timed region: events only around the dominant kernel's launches (so the
     #    per-launch markers of ~400 other launches do not inflate the step time)
     rt.timing(True, only=None if args.timing == "all" else f"/{dom}|")

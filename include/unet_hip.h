@@ -91,9 +91,10 @@ typedef struct {
     int in_channels;   /* models/model.py:6 / mod.py:11 in_channels (default 1; must be 1) */
     int out_channels;  /* models/model.py:6 / mod.py:12 out_channels (default 1; 1..4)   */
     int variant;       /* unet_variant (0 = models/model.py)                               */
-    int base_filters;  /* mod.py:13 (0 = default 64); a multiple of 8, <= 256.  64 / 128 /
-                          256 run natively; other widths (the reference grid's 16 / 24 /
-                          32 / 48) run zero-padded to the next power of two >= 64 */
+    int base_filters;  /* mod.py:13 (0 = default 64); a multiple of 8, <= 256.  32 / 64 /
+                          128 / 256 run natively; other widths (the reference grid's 16 /
+                          24 / 48) run zero-padded to the next power of two >= 32 inside
+                          the library (the caller's arenas keep the torch layouts) */
     int depth;         /* mod.py:14 (0 = default 5 for mod, 4 for model); 1..6             */
     int math;          /* unet_math of the conv GEMMs (0 = f32)                            */
 } unet_cfg;
@@ -178,6 +179,12 @@ int unet_num_buckets(const unet_ctx* ctx, int* n);
 int unet_bucket_range(const unet_ctx* ctx, int b, int64_t* offset, int64_t* len);
 /* Make `stream` wait (device-side) until bucket b of the last backward is complete. */
 int unet_stream_wait_bucket(unet_ctx* ctx, int b, unet_stream_t stream);
+/* The hipEvent_t (returned as void*) that each unet_backward records on its stream when
+ * bucket b is complete -- for a caller that drives RCCL (ncclAllReduce on its own
+ * hipStream_t) without torch: hipStreamWaitEvent(comm_stream, ev, 0), then reduce
+ * grads[offset, offset+len).  Owned by the context (valid until unet_destroy; created by
+ * the first unet_backward, UNET_ERR_INVALID before it). */
+int unet_bucket_event(unet_ctx* ctx, int b, void** hip_event);
 
 /* Input pipeline (data/data_loader.py:20-27 + utils/transforms.py:143-156): the reference
  * resizes every PIL image and mask with TF.resize (= Pillow Image.resize(size, BILINEAR))
@@ -195,15 +202,20 @@ int unet_resize_u8(unet_ctx* ctx, const uint8_t* src, int h, int w, float* dst, 
 
 /* Kernel-schedule options of a context (new; no reference counterpart).  The defaults are
  * the measured-best schedules; the named alternatives (tiles, LDS-DMA vs register-staged
- * bf16 kernels, XCD block order, a weight-gradient stream, ...) exist for A/B runs and
- * tests.  The library never reads the environment: an option changes only when set here.
- * Names: wgrad_row3, wgrad_row3_tile, wgrad_tile_w, wgrad_tile_n, wgrad16_tile, tile_n128,
- * tile_n128_dgrad, tile_n64, tile16_n128, tile16_n128_dgrad, tile16_n64, rg16, rg16_tile,
- * wg16, wg16_tile, wg16t, xcd16, xcd_remap, wgrad_stream, dz_in_loaders
- * (runtime.hip: struct Options).  Set them between steps, not between a forward and its
- * backward (the workspace plan depends on some of them). */
+ * bf16 kernels, XCD block order, ...) exist for A/B runs and the bit-identity tests.  The
+ * library never reads the environment: an option changes only when set here.
+ * Names (runtime.hip OPTION_TABLE, in this order; unet_option_name enumerates them):
+ *   wgrad_row3 wgrad_row3_tile wgrad_row3_big wgrad_row3_blocks wgrad_blocks
+ *   wgrad16_blocks wgrad_tile_w wgrad_tile_n wgrad16_tile tile_n128 tile_n128_dgrad
+ *   tile_n64 tile_n64_dgrad tile_n32 tile_convt64 tile_convt tile_convt_dgrad tile16_n128
+ *   tile16_n128_dgrad tile16_n64 rg16 rg16_tile rg16_bn_k rg16_r3 rg16_xp wg16 wg16_tile
+ *   wg16t xcd16 xcd_remap dz_in_wgrad
+ * Set them between steps, not between a forward and its backward (the workspace plan
+ * depends on some of them). */
 int unet_set_option(unet_ctx* ctx, const char* name, int64_t value);
 int unet_get_option(const unet_ctx* ctx, const char* name, int64_t* value);
+/* i-th option name (0 ..), UNET_ERR_INVALID past the last one; *name is static. */
+int unet_option_name(int i, const char** name);
 
 /* Per-kernel timing: when enabled, unet_forward/unet_backward bracket every launch with
  * HIP events; unet_timing_read synchronises and returns, per kernel family, the launch

@@ -469,3 +469,101 @@ def test_trainer_dp2_mixup_logging_hygiene(tmp_path):
     text = open(os.path.join(str(tmp_path), "shared.log")).read()
     assert text.count("Train Epoch: 1,") == 1 and text.count("Train Epoch: 2,") == 1, text
     assert text.count("Test Metrics") == 1, text
+
+
+def _modres_worker(rank, world, port, q, tag):
+    import sys
+    for p in (REPO, PKG, os.path.join(REPO, "tests")):
+        sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import unet_hip
+        from oracle import mod_ref_cpu as MO
+        from oracle import weights as Wt
+        from unet_hip.dist import DistributedUNet
+        dev = torch.device("cuda:0")
+        torch.cuda.set_device(0)
+        if tag == "res_":
+            m = unet_hip.ResUNet(1, 1, base_filters=64, depth=3)
+            P, B = MO.res_make_params(42 if rank == 0 else 7, 64, 3), MO.res_init_buffers(64, 3)
+        else:
+            m = unet_hip.ModUNet(1, 1, base_filters=64, depth=3)
+            P, B = MO.make_params(42 if rank == 0 else 7, 64, 3), MO.init_buffers(64, 3)
+        sd = m.state_dict()
+        sd.update({k: v.clone() for k, v in P.items()})
+        sd.update({k: v.clone() for k, v in B.items()})
+        m.load_state_dict(sd)
+        m = m.to(dev).train()
+        opt = unet_hip.HipAdamW(m.parameters(), lr=1e-4)
+        ddp = DistributedUNet(m, opt)  # rank 1's different weights are replaced by rank 0's
+        x = torch.from_numpy(Wt.make_input(17, 3, 1, 64, 64))
+        t = torch.from_numpy(Wt.make_target(17, 3, 64, 64))
+        xs, ts = torch.chunk(x, world)[rank].to(dev), torch.chunk(t, world)[rank].to(dev)
+        res = []
+        for s in range(2):
+            opt.zero_grad(set_to_none=True)
+            logits = ddp(xs)
+            losses = ddp.losses(logits, ts)
+            loss = losses[0] + losses[1]
+            loss.backward()
+            ddp.reduce_gradients()
+            norms = [float(p.grad.detach().double().norm()) for _, p in m.named_parameters()]
+            opt.step()
+            parts = [torch.zeros(2, 1, 64, 64, device=dev) for _ in range(world)]
+            pad = torch.zeros(2, 1, 64, 64, device=dev)
+            pad[:logits.shape[0]].copy_(logits.detach())
+            dist.all_gather(parts, pad)
+            gl = torch.cat([p[:c] for p, c in zip(parts, [2, 1])]).cpu().numpy()
+            res.append((gl, [float(v) for v in losses.detach().cpu()], float(loss.item()), norms))
+        params = m._state.param_arena.detach().cpu().clone()
+        pd = params.clone()
+        dist.broadcast(pd, src=0)
+        same = bool(torch.equal(pd, params))
+        ddp.sync_buffers()
+        m.eval()
+        with torch.no_grad():
+            ev = m(x.to(dev)).cpu().numpy()
+        q.put((rank, res, same, ev))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("tag", ["res_", "mod_"])
+def test_dp2_modres_match_dataparallel_golden(golden_dir, tag):
+    """Data parallelism of the networks the reference CLI trains (main.py:122 ResUNet;
+    models/mod.py UNet) over two ranks on one GPU (gloo): B = 3 scattered 2 + 1, two AdamW
+    steps, against the reference's nn.DataParallel fixture tests/golden/modres_dp_64.npz.
+    The gradients are summed bucket by bucket on a side stream that waits on the native
+    bucket events; for ResUNet a bucket that fired before conv1's input gradient was ADDED
+    into the skip's (E_ADD) would sum an incomplete gradient, so step 0's gradient norms at
+    1e-2 pin bucket readiness.  Step 1 (after one Adam step, where rounding-noise gradient
+    elements move by up to lr) at the trajectory bars of the single-GPU golden tests."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_modres_worker, args=(r, 2, port, q, tag)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=500), q.get(timeout=500)], key=lambda r: r[0])
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    from _helpers import rel_max
+    f = np.load(os.path.join(golden_dir, "modres_dp_64.npz"), allow_pickle=False)
+    assert res[0][2] and res[1][2], "ranks diverged"
+    for s in range(2):
+        p = f"{tag}s{s}_"
+        gl, l3, loss, norms = res[0][1][s]
+        tol = 1e-4 if s == 0 else 2e-3
+        assert rel_max(gl, f[p + "logits"]) <= tol, (s, rel_max(gl, f[p + "logits"]))
+        assert abs(loss - float(f[p + "loss"])) <= (1e-5 if s == 0 else 1e-4), (s, loss)
+        assert res[1][1][s][2] == loss, "ranks disagree on the gathered loss"
+        gtol = 1e-2 if s == 0 else 1e-1
+        np.testing.assert_allclose(norms, f[p + "grad_norm"], rtol=gtol)
+        np.testing.assert_allclose(res[1][1][s][3], norms, rtol=0, atol=0)  # summed on both
+    ev = res[0][3]
+    assert rel_max(ev, f[tag + "eval_logits"]) <= 2e-3
+    np.testing.assert_array_equal(res[0][3], res[1][3])  # replica 0's buffers on every rank

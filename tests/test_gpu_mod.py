@@ -231,8 +231,7 @@ def _assert_same(a, b, what):
         assert torch.equal(b0, b[2][k]), f"{what}: buffer {k}"
 
 
-@pytest.mark.parametrize("tile,wtile", [(0, 0), (1, 1), (3, 0), (0, 2), (8, 0), (11, 0),
-                                        (0, 3), (0, 4), (2, 2), (4, 2), (18, 2)])
+@pytest.mark.parametrize("tile,wtile", [(0, 0), (0, 2), (2, 2), (4, 2)])
 def test_rg16_bit_identical_to_register_staged(tile, wtile):
     """The LDS-DMA bf16 GEMMs (kernels_gemm16.hip, fed by the k_to_bf16 operand images:
     row GEMMs and the transposed-read weight gradients) against the register-staged bf16
@@ -260,15 +259,14 @@ def test_rg16_tile_choice_is_numerically_invisible(side):
     x, t = inputs(29, 2, side, side)
     P = MO.make_params(31, 128, 5)
     outs = {}
-    # 12 / 13: tiles 4 / 0 with read-ahead fragments; 18: the ping-pong 256x256 kernel
-    for tile in (0, 2, 4, 12, 13, 18, -1):
+    for tile in (0, 2, 4, -1):
         m = _bf16_model(P, 128, 5)
         # the tap-row halo tile (19, the auto choice's 256x256 forward / dgrad since r03) sums
         # K in another order: held to the bf16 envelope by test_rg16_halo_tile_within_bf16_error
         with options(m.flatten_().rt, rg16_tile=tile, rg16_r3=0):
             outs[tile] = _bf16_step(m, x, t)
         del m
-    for tile in (2, 4, 12, 13, 18, -1):
+    for tile in (2, 4, -1):
         _assert_same(outs[0], outs[tile], f"{side}^2 tile {tile} vs 0")
 
 
@@ -309,11 +307,27 @@ def test_rg16_halo_tile_within_bf16_error():
     assert worst[0][0] <= 1.0, worst[:4]
 
 
+_BF16_ORACLES = {}
+
+
+def _bf16_oracles(base, depth):
+    """The three oracle evaluations test_mod_bf16_matches_bf16_oracle compares against
+    (bf16-operand fp32, bf16-operand fp64, plain fp32), computed once per network: they do
+    not depend on the HIP tile under test."""
+    key = (base, depth)
+    if key not in _BF16_ORACLES:
+        P = MO.make_params(42, base, depth)
+        x, t = inputs(5, 2, 64, 64)
+        _BF16_ORACLES[key] = (
+            MO.train_step(P, MO.init_buffers(base, depth), None, x, t, depth=depth, bf16=True),
+            MO.train_step(_to64(P), _to64(MO.init_buffers(base, depth)), None, x.double(),
+                          t.double(), depth=depth, bf16=True),
+            MO.train_step(P, MO.init_buffers(base, depth), None, x, t, depth=depth))
+    return _BF16_ORACLES[key]
+
+
 @pytest.mark.parametrize("base,depth,tile", [(64, 3, "4"), (128, 5, "0"), (128, 5, "2"), (128, 5, "4"),
-                                             (128, 5, "6"), (128, 5, "7"),
-                                             (128, 5, "9"), (128, 5, "10"), (128, 5, "14"),
-                                             (128, 5, "15"), (128, 5, "18"), (128, 5, "19"),
-                                             (128, 5, "auto")])
+                                             (128, 5, "19"), (128, 5, "auto")])
 def test_mod_bf16_matches_bf16_oracle(base, depth, tile):
     """mfma_dtype="bf16": one step at B=2 64x64 vs the oracle that rounds exactly the GEMM
     operands the HIP bf16 kernels round (oracle/mod_ref_cpu.py, bf16=True).
@@ -328,13 +342,10 @@ def test_mod_bf16_matches_bf16_oracle(base, depth, tile):
     per-GEMM choice (rg16_tile, runtime.hip) and default wgrad tile."""
     import unet_hip
     opts = {} if tile == "auto" else dict(
-        rg16_tile=int(tile), wg16_tile=2 if tile in ("4", "6", "7", "9", "10", "14", "18", "19") else 0)
+        rg16_tile=int(tile), wg16_tile=2 if tile in ("4", "19") else 0)
     P = MO.make_params(42, base, depth)
     x, t = inputs(5, 2, 64, 64)
-    ref = MO.train_step(P, MO.init_buffers(base, depth), None, x, t, depth=depth, bf16=True)
-    r64 = MO.train_step(_to64(P), _to64(MO.init_buffers(base, depth)), None, x.double(),
-                        t.double(), depth=depth, bf16=True)
-    ref32 = MO.train_step(P, MO.init_buffers(base, depth), None, x, t, depth=depth)
+    ref, r64, ref32 = _bf16_oracles(base, depth)
     m = unet_hip.ModUNet(1, 1, base_filters=base, depth=depth, mfma_dtype="bf16")
     sd = m.state_dict()
     for k, v in P.items():

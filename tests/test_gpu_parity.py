@@ -445,14 +445,13 @@ def test_mask_counts():
 
 
 def test_full_size_vs_torch_gpu_reference():
-    """bs=32, 1x256x256 (BASELINE config 2): forward and gradients vs the oracle's functional
-    graph evaluated by torch fp32 on the same GPU (the CPU oracle would take ~20 s/step)."""
+    """bs=32, 1x256x256 (BASELINE config 2): forward and gradients vs the CPU oracle's step on
+    the box's host threads (~15 s; the same functional graph on the GPU through torch/MIOpen
+    spent ~110 s compiling its kernels on every fresh box)."""
     import unet_hip
     P = O.make_params(42)
     x, t = inputs(11, 32, 256, 256)
-    Pd = {k: v.to(DEV) for k, v in P.items()}
-    Bd = {k: v.to(DEV) for k, v in O.init_buffers().items()}
-    ref = O.train_step(Pd, Bd, None, x.to(DEV), t.to(DEV))
+    ref = O.train_step(P, O.init_buffers(), None, x, t)
     m = hip_model(P, DEV)
     logits = m(x.to(DEV))
     losses = unet_hip.seg_losses(logits, t.to(DEV))
@@ -476,36 +475,6 @@ def test_determinism_full_size():
         (l[0] + l[1]).backward()
         outs.append((logits.detach().clone(), m.flat_params.grad if False else
                      m._state.grad_arena.clone()))
-    assert torch.equal(outs[0][0], outs[1][0])
-    assert torch.equal(outs[0][1], outs[1][1])
-
-
-@pytest.mark.parametrize("variant", ["model", "mod"])
-def test_wgrad_stream_bit_identical(variant):
-    """Option wgrad_stream=1 moves the weight gradients to a second stream (runtime.hip
-    backward_impl); every kernel still sees the same inputs, so logits and the whole grad
-    arena must be bit-identical to the single-stream schedule, also for the bucket-event
-    path a DP run waits on."""
-    import unet_hip
-    from _helpers import hip_mod_model
-    x, t = inputs(13, 8, 256, 256)
-    outs = []
-    for flag in (0, 1):
-        if variant == "model":
-            m = hip_model(O.make_params(42), DEV)
-        else:
-            from oracle import mod_ref_cpu as MO
-            m = hip_mod_model(MO.make_params(5, base=64, depth=4), DEV, 64, 4)
-        rt = m.flatten_().rt
-        rt.set_option("wgrad_stream", flag)
-        try:
-            logits = m(x.to(DEV))
-            l = unet_hip.seg_losses(logits, t.to(DEV))
-            (l[0] + l[1]).backward()
-            torch.cuda.synchronize()
-        finally:
-            rt.set_option("wgrad_stream", 0)
-        outs.append((logits.detach().clone(), m._state.grad_arena.clone()))
     assert torch.equal(outs[0][0], outs[1][0])
     assert torch.equal(outs[0][1], outs[1][1])
 
@@ -582,76 +551,16 @@ def test_wgrad_row3_matches_one_tap_tiles(variant):
     print(f"row3 vs one-tap worst grad norm-rel {worst:.2e}")
 
 
-@pytest.mark.parametrize("variant,B,H,W", [("model", 2, 64, 64), ("model", 2, 256, 128),
-                                           ("model", 1, 48, 80), ("mod", 2, 128, 64),
-                                           ("res", 2, 64, 64)])
-def test_row3_gemm_matches_oracle(variant, B, H, W):
-    """Option row3_gemm: 3x3 forward / dgrad GEMMs on the tap-row kernel
-    (kernels_gemm.hip rowgemm_row3_kernel; W = 80 exercises the fallback to the one-tap
-    kernel on grids it cannot tile).  Logits at the north-star bar; every gradient against
-    fp64 within 2x the fp32 oracle's own error (over x and x * (1 + 1e-7)), floor 1e-2, or
-    within 1.25x the default (one-tap) kernel's error on the same case -- both GEMM
-    schedules see the same discrete ReLU-boundary flips (test_train_steps_strict_resync),
-    which move small BN-bias gradients by ~1e-2 on some inputs."""
-    import unet_hip
-    from _helpers import hip_mod_model, options
-    from oracle import mod_ref_cpu as MO
-    x, t = inputs(41, B, H, W)
-    if variant == "model":
-        P, Bf = O.make_params(42), O.init_buffers()
-        make = lambda: hip_model(P, DEV)  # noqa: E731
-        step = lambda P, B, x, t: O.train_step(P, B, None, x, t)  # noqa: E731
-    elif variant == "mod":
-        P, Bf = MO.make_params(5, 64, 3), MO.init_buffers(64, 3)
-        make = lambda: hip_mod_model(P, DEV, 64, 3)  # noqa: E731
-        step = lambda P, B, x, t: MO.train_step(P, B, None, x, t, depth=3)  # noqa: E731
-    else:
-        P, Bf = MO.res_make_params(42, 64, 3), MO.res_init_buffers(64, 3)
-
-        def make():
-            m = unet_hip.ResUNet(1, 1, base_filters=64, depth=3)
-            sd = m.state_dict()
-            sd.update({k: v.clone() for k, v in P.items()})
-            sd.update({k: v.clone() for k, v in Bf.items()})
-            m.load_state_dict(sd)
-            return m.to(DEV).train()
-        step = lambda P, B, x, t: MO.res_train_step(P, B, None, x, t, depth=3)  # noqa: E731
-    ref = step(P, {k: v.clone() for k, v in Bf.items()}, x, t)
-    refp = step(P, {k: v.clone() for k, v in Bf.items()}, x * (1 + 1e-7), t)
-    r64 = step(_to64(P), _to64(Bf), x.double(), t.double())
-    e32 = {k: max(norm_rel(g, r64["grads"][k]), norm_rel(refp["grads"][k], r64["grads"][k]))
-           for k, g in ref["grads"].items()}
-    env = max(2 * max(e32.values()), GRAD_TOL)
-    worst = {}
-    for flag in (0, 1):
-        m = make()
-        with options(m.flatten_().rt, row3_gemm=flag):
-            logits = m(x.to(DEV))
-            losses = unet_hip.seg_losses(logits, t.to(DEV))
-            (losses[0] + losses[1]).backward()
-            torch.cuda.synchronize()
-        assert rel_max(logits.detach().cpu().numpy(), ref["logits"].numpy()) <= LOGIT_TOL
-        errs = grad_errors(m, r64["grads"])
-        k = max(errs, key=errs.get)
-        worst[flag] = (k, errs[k])
-        print(f"{variant} {B}x{H}x{W} row3_gemm={flag}: worst {k} {errs[k]:.3e} "
-              f"(fp32 oracle {e32[k]:.3e}, envelope {env:.3e})")
-    k, e = worst[1]
-    assert e <= max(env, 1.25 * worst[0][1]), f"{k}: {e:.3e} (default kernel {worst[0][1]:.3e})"
-
-
 @pytest.mark.parametrize("variant,B,H,W", [("model", 2, 64, 64), ("model", 8, 256, 256),
                                            ("model", 1, 48, 80), ("mod", 2, 128, 64),
                                            ("res", 2, 64, 64)])
 def test_pipe_gemm_bit_identical(variant, B, H, W):
-    """Row-GEMM tiles 16..19 (kernels_gemm_pipe.hip: the software-pipelined schedule of the
-    128x128 / 128x64 f32 tiles, global loads one or two chunks ahead; 18 / 16 are the
-    defaults; 25 / 26: 128x64 at three blocks per CU; 27 / 28: 256x64 on 64x64 wave tiles;
-    29..32: persistent blocks walking several tiles of 25 / 26 / 16 / 18; 22: LDS-DMA 128x64 at
-    three stages) and 20..22 (kernels_gemm_dma.hip: LDS-DMA operands, the BN prologue applied
-    after the LDS read) walk K in the same order with the same prologue arithmetic and the
-    same epilogues as the register-staged rowgemm_kernel tiles (4, 0, 1), so a training
-    step -- logits and the whole gradient arena -- is bit-identical across the schedules.  48x80 has M
+    """Row-GEMM tiles 16..19, 25, 26 (kernels_gemm_pipe.hip: the software-pipelined schedule
+    of the 128x128 / 128x64 f32 tiles, global loads one or two chunks ahead, 18 the default;
+    25 / 26: 128x64 at three blocks per CU, the N = 64 dgrad / ConvT-dgrad defaults) walk K in
+    the same order with the same prologue arithmetic and the same epilogues as the
+    register-staged rowgemm_kernel tiles (4, 0, 1), so a training step -- logits and the
+    whole gradient arena -- is bit-identical across the schedules.  48x80 has M
     tiles that end past M (rows masked in the gather and the guarded epilogue path); the
     ResUNet covers the 1x1 skip GEMMs (E_RESID) and E_ADD, the ConvTranspose GEMMs run in
     every variant."""
@@ -660,9 +569,8 @@ def test_pipe_gemm_bit_identical(variant, B, H, W):
     from oracle import mod_ref_cpu as MO
     x, t = inputs(43, B, H, W)
     outs = []
-    for tiles in ((4, 0, 1, 0), (16, 16, 17, 16), (18, 18, 19, 18), (20, 20, 21, 20),
-                  (16, 18, 25, 26), (18, 16, 26, 25), (18, 18, 27, 27), (16, 16, 28, 28),
-                  (32, 31, 29, 30), (31, 32, 30, 29), (18, 16, 22, 22)):
+    for tiles in ((4, 0, 1, 0), (16, 16, 17, 16), (18, 18, 19, 18), (16, 18, 25, 26),
+                  (18, 16, 26, 25)):
         if variant == "model":
             m = hip_model(O.make_params(42), DEV)
         elif variant == "mod":
@@ -709,80 +617,6 @@ def test_dz_in_wgrad_bit_identical(B, H, W):
         del m
     assert torch.equal(outs[0][0], outs[1][0])
     assert torch.equal(outs[0][1], outs[1][1]), (outs[0][1] - outs[1][1]).abs().max().item()
-
-
-@pytest.mark.parametrize("variant,B,H,W,dzl", [("model", 2, 64, 64, 0), ("model", 4, 128, 128, 0),
-                                               ("model", 2, 64, 64, 1), ("mod", 2, 128, 64, 0),
-                                               ("res", 2, 64, 64, 0)])
-def test_wgrad_row3_pipe_bit_identical(variant, B, H, W, dzl):
-    """Option wgrad_row3_pipe (kernels_wgrad_pipe.hip: the software-pipelined schedule of the
-    row3 weight-gradient tiles) keeps wgrad_row3_kernel's pixel order, loaders, split-K slabs
-    and bias column sums, so a training step is bit-identical with and without it;
-    dz_in_loaders = 1 covers the OP_DZ operand (BN backward folded into the B' loader)."""
-    import unet_hip
-    from _helpers import hip_mod_model, options
-    from oracle import mod_ref_cpu as MO
-    x, t = inputs(47, B, H, W)
-    outs = []
-    for pipe in (0, 1):
-        if variant == "model":
-            m = hip_model(O.make_params(42), DEV)
-        elif variant == "mod":
-            m = hip_mod_model(MO.make_params(5, 64, 3), DEV, 64, 3)
-        else:
-            m = unet_hip.ResUNet(1, 1, base_filters=64, depth=3)
-            sd = m.state_dict()
-            sd.update({k: v.clone() for k, v in MO.res_make_params(42, 64, 3).items()})
-            m.load_state_dict(sd)
-            m = m.to(DEV).train()
-        with options(m.flatten_().rt, wgrad_row3_pipe=pipe, dz_in_loaders=dzl):
-            logits = m(x.to(DEV))
-            l = unet_hip.seg_losses(logits, t.to(DEV))
-            (l[0] + l[1]).backward()
-            torch.cuda.synchronize()
-        outs.append((logits.detach().clone(), m._state.grad_arena.clone()))
-        del m
-    assert torch.equal(outs[0][0], outs[1][0])
-    d = (outs[0][1] - outs[1][1]).abs().max().item()
-    assert torch.equal(outs[0][1], outs[1][1]), d
-
-
-@pytest.mark.parametrize("variant,B,H,W,dzw", [("model", 2, 64, 64, 256), ("model", 4, 128, 128, 256),
-                                               ("model", 2, 64, 64, 0), ("model", 1, 96, 64, 256),
-                                               ("mod", 2, 128, 64, 256), ("res", 2, 64, 64, 256)])
-def test_wgrad_row9_bit_identical(variant, B, H, W, dzw):
-    """Option wgrad_row9 (wgrad_row3_kernel with NDY = 3: one block holds all three tap rows of
-    a 64x64 channel tile and reads x and dz -- or do and y with the BN-backward dz formed in
-    its loader, dz_in_wgrad -- once instead of once per tap row) keeps tile 20's split-K
-    partition, per-tap pixel order, bias column sums and dz hand-off, so a training step is
-    bit-identical with and without it.  dz_in_wgrad = 0 covers the plain dz operand, the
-    mod.py variant the BN -> ReLU loader, 96 x 64 an image taller than wide."""
-    import unet_hip
-    from _helpers import hip_mod_model, options
-    from oracle import mod_ref_cpu as MO
-    x, t = inputs(49, B, H, W)
-    outs = []
-    for row9 in (0, 1):
-        if variant == "model":
-            m = hip_model(O.make_params(42), DEV)
-        elif variant == "mod":
-            m = hip_mod_model(MO.make_params(5, 64, 3), DEV, 64, 3)
-        else:
-            m = unet_hip.ResUNet(1, 1, base_filters=64, depth=3)
-            sd = m.state_dict()
-            sd.update({k: v.clone() for k, v in MO.res_make_params(42, 64, 3).items()})
-            m.load_state_dict(sd)
-            m = m.to(DEV).train()
-        with options(m.flatten_().rt, wgrad_row9=row9, dz_in_wgrad=dzw):
-            logits = m(x.to(DEV))
-            l = unet_hip.seg_losses(logits, t.to(DEV))
-            (l[0] + l[1]).backward()
-            torch.cuda.synchronize()
-        outs.append((logits.detach().clone(), m._state.grad_arena.clone()))
-        del m
-    assert torch.equal(outs[0][0], outs[1][0])
-    d = (outs[0][1] - outs[1][1]).abs().max().item()
-    assert torch.equal(outs[0][1], outs[1][1]), d
 
 
 def test_adamw_resume_from_state_dict_matches_uninterrupted():
@@ -844,34 +678,30 @@ def test_adamw_resume_from_state_dict_matches_uninterrupted():
     assert torch.equal(m, ref.m["a"]) and torch.equal(v, ref.v["a"])
 
 
-@pytest.mark.parametrize("variant,B,H,W", [("model", 2, 64, 64), ("model", 8, 256, 256),
-                                           ("mod", 2, 128, 128)])
-def test_reduce_stream_bit_identical(variant, B, H, W):
-    """Option reduce_stream: the split-K slab reductions and bias sums run on a second stream
-    beside the dgrad GEMMs (the next weight gradient waits for them before it rewrites the
-    slabs; bucket events are recorded on that stream).  Same kernels, same order of
-    summation: the gradient arena is bit-identical to the one-stream schedule, over two
-    steps so that the ordering of the next step's writers is exercised too."""
+def test_bucket_event_exported_for_non_torch_callers():
+    """unet_bucket_event (include/unet_hip.h): the raw hipEvent_t per gradient bucket that a
+    caller driving RCCL on its own streams waits on.  Each bucket's slice, copied on a
+    fresh stream that only waited (hipStreamWaitEvent through the HIP runtime itself, no
+    torch stream sync) on that bucket's event, equals the final gradient arena."""
+    import ctypes
     import unet_hip
-    from _helpers import hip_mod_model, options
-    from oracle import mod_ref_cpu as MO
-    x, t = inputs(53, B, H, W)
-    outs = []
-    for flag in (0, 1):
-        if variant == "model":
-            m = hip_model(O.make_params(42), DEV)
-        else:
-            m = hip_mod_model(MO.make_params(5, 64, 3), DEV, 64, 3)
-        grads = []
-        with options(m.flatten_().rt, reduce_stream=flag):
-            for _ in range(2):
-                m.zero_grad(set_to_none=False)
-                logits = m(x.to(DEV))
-                l = unet_hip.seg_losses(logits, t.to(DEV))
-                (l[0] + l[1]).backward()
-                torch.cuda.synchronize()
-                grads.append(m._state.grad_arena.clone())
-        outs.append(grads)
-        del m
-    for a, b in zip(outs[0], outs[1]):
-        assert torch.equal(a, b), (a - b).abs().max().item()
+    hip = ctypes.CDLL("libamdhip64.so")  # the process's one HIP runtime (torch's)
+    hip.hipStreamWaitEvent.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint]
+    x, t = inputs(61, 4, 128, 128)
+    m = hip_model(O.make_params(42), DEV)
+    rt = m.flatten_().rt
+    logits = m(x.to(DEV))
+    l = unet_hip.seg_losses(logits, t.to(DEV))
+    (l[0] + l[1]).backward()  # enqueued; no host sync before the waits below
+    arena = m._state.grad_arena
+    copies = []
+    for b, (off, n) in enumerate(rt.buckets):
+        s = torch.cuda.Stream(device=DEV)
+        ev = rt.bucket_event(b)
+        assert ev, "null event"
+        assert hip.hipStreamWaitEvent(ctypes.c_void_p(s.cuda_stream), ctypes.c_void_p(ev), 0) == 0
+        with torch.cuda.stream(s):
+            copies.append(arena[off:off + n].clone())
+    torch.cuda.synchronize()
+    for (off, n), c in zip(rt.buckets, copies):
+        assert torch.equal(c, arena[off:off + n])

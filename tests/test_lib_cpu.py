@@ -285,13 +285,13 @@ def test_schedule_options_are_explicit(rt, monkeypatch):
     from unet_hip._lib import HipError
     from unet_hip.runtime import UNetRuntime
     monkeypatch.setenv("UNET_RG16_TILE", "3")
-    monkeypatch.setenv("UNET_WGRAD_STREAM", "1")
+    monkeypatch.setenv("UNET_DZ_IN_WGRAD", "0")
     fresh = UNetRuntime("cuda:0")
     assert fresh.get_option("rg16_tile") == -1
-    assert fresh.get_option("wgrad_stream") == 0
-    fresh.set_option("wgrad_stream", 1)
-    assert fresh.get_option("wgrad_stream") == 1
-    assert rt.get_option("wgrad_stream") == 0  # per context
+    assert fresh.get_option("dz_in_wgrad") == 256
+    fresh.set_option("dz_in_wgrad", 0)
+    assert fresh.get_option("dz_in_wgrad") == 0
+    assert rt.get_option("dz_in_wgrad") == 256  # per context
     with pytest.raises(HipError):
         fresh.set_option("no_such_option", 1)
     import subprocess
@@ -301,21 +301,44 @@ def test_schedule_options_are_explicit(rt, monkeypatch):
 
 def test_schedule_option_defaults():
     """The measured defaults documented in INTEGRATION.md §3: the pipelined
-    row GEMMs (-1 = pick_tile: 18 forward / 16 dgrad), the row3 weight gradients with the
-    128x64 tile on the wide layers, the bf16 LDS-DMA kernels, XCD-contiguous tiles for the
-    f32 GEMMs; A/B alternatives off."""
+    row GEMMs (-1 = pick_tile: 18), the three-block 128x64 tiles for the N = 64 / ConvT
+    dgrads, the row3 weight gradients with the 128x64 tile on the wide layers, the bf16
+    LDS-DMA kernels with the tap-row halo tile, XCD-contiguous tiles."""
     from unet_hip.runtime import UNetRuntime
     fresh = UNetRuntime("cuda:0")
     want = {"tile_n128": -1, "tile_n128_dgrad": -1, "tile_n64": 19, "tile_n64_dgrad": 25,
-            "tile_convt64": 1, "wgrad_row3": 1, "wgrad_row3_big": 21, "wgrad_row3_blocks": 1536,
-            "wgrad_row3_pipe": 0, "wgrad_blocks": 2048, "rg16": 1, "rg16_tile": -1, "rg16_ra": 0,
+            "tile_n32": 14, "tile_convt64": 1, "wgrad_row3": 1, "wgrad_row3_big": 21,
+            "wgrad_row3_blocks": 1536, "wgrad_blocks": 2048, "rg16": 1, "rg16_tile": -1,
             "rg16_bn_k": 8192, "wg16": 1, "wg16_tile": 2, "wgrad16_blocks": 1536,
-            "wgrad_stream": 0, "dz_in_loaders": 0, "row3_gemm": 0, "xcd_remap": 1,
-            "tile_convt": -1, "tile_convt_dgrad": 26, "rg16_m16": 0, "rg16_pp": 0, "rg16_xp": 0,
-            "dz_in_wgrad": 256, "rg16_r3": 1, "reduce_stream": 0, "wgrad_row9": 0,
-            "wgrad_row3_16": 0}
+            "xcd_remap": 1, "xcd16": 1, "tile_convt": -1, "tile_convt_dgrad": 26, "rg16_xp": 0,
+            "dz_in_wgrad": 256, "rg16_r3": 1}
     got = {k: fresh.get_option(k) for k in want}
     assert got == want
+
+
+def test_header_option_list_matches_library():
+    """include/unet_hip.h names every option the library accepts, in OPTION_TABLE order
+    (the header list had drifted), and each one round-trips through
+    unet_get_option."""
+    import re
+    from unet_hip import _lib
+    from unet_hip.runtime import UNetRuntime
+    text = open(_lib.HEADER).read()
+    block = text[text.index("Names (runtime.hip OPTION_TABLE"):text.index("Set them between steps")]
+    block = block.split("\n", 1)[1]
+    header = re.findall(r"[a-z][a-z0-9_]+", block.replace("*", " "))
+    lib_names = _lib.option_names()
+    assert header == lib_names, (set(header) ^ set(lib_names))
+    fresh = UNetRuntime("cuda:0")
+    for n in lib_names:
+        fresh.get_option(n)
+
+
+def test_abi_exports_bucket_event():
+    """SURVEY §8b's per-bucket readiness event for non-torch RCCL callers is exported."""
+    import subprocess
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib_path()], capture_output=True, text=True)
+    assert " unet_bucket_event" in out.stdout and " unet_option_name" in out.stdout
 
 
 def _lib_path():

@@ -308,3 +308,39 @@ def test_oracle_dataparallel_train_then_eval(golden_dir, tag, lr):
     with torch.no_grad():
         np.testing.assert_array_equal(O.forward(xva, P, B, False).numpy(), f[tag + "val_logits"])
         np.testing.assert_array_equal(O.forward(xte, P, B, False).numpy(), f[tag + "test_logits"])
+
+
+@pytest.mark.parametrize("tag", ["res_", "mod_"])
+def test_oracle_dataparallel_modres(golden_dir, tag):
+    """nn.DataParallel emulation (shards 2 + 1, per-replica BN, gathered loss, summed
+    gradients, replica 0's buffers) of ResUNet(64, 3) and mod.py UNet(64, 3), two AdamW
+    steps then eval, against tests/golden/modres_dp_64.npz from the reference modules."""
+    from oracle import mod_ref_cpu as MO
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    f = _load(golden_dir, "modres_dp_64.npz")
+    if tag == "res_":
+        P, B = MO.res_make_params(42, 64, 3), MO.res_init_buffers(64, 3)
+        spec, names = MO.res_param_spec(1, 1, 64, 3), [n for n, _ in MO.res_bn_layers(64, 3)]
+        step = lambda o, x_, t_: MO.res_train_step(P, B, o, x_, t_, depth=3, shards=2)  # noqa: E731
+        fwd = MO.make_res_forward(3)
+    else:
+        P, B = MO.make_params(42, 64, 3), MO.init_buffers(64, 3)
+        spec, names = MO.param_spec(1, 1, 64, 3), [n for n, _ in MO.bn_layers(64, 3)]
+        step = lambda o, x_, t_: MO.train_step(P, B, o, x_, t_, depth=3, shards=2)  # noqa: E731
+        fwd = MO.make_forward(3)
+    opt = O.AdamWState(P, lr=1e-4)
+    x = torch.from_numpy(W.make_input(17, 3, 1, 64, 64))
+    t = torch.from_numpy(W.make_target(17, 3, 64, 64))
+    for s in range(2):
+        p = f"{tag}s{s}_"
+        r = step(opt, x, t)
+        ref = f[p + "logits"]
+        assert np.max(np.abs(r["logits"].numpy() - ref)) <= 1e-5 * np.max(np.abs(ref))
+        assert abs(r["loss"].item() - float(f[p + "loss"])) < 1e-6
+        _check_grads(_grad_stats(r["grads"], spec), f[p + "grad_norm"], f[p + "grad_sum"],
+                     f[p + "grad_samp"], rtol=1e-4)
+        rm = np.concatenate([B[f"{n}.running_mean"].numpy() for n in names])
+        np.testing.assert_allclose(rm, f[p + "running_mean"], rtol=1e-5, atol=1e-6)
+    with torch.no_grad():
+        ev = fwd(x, P, B, training=False).numpy()
+    assert np.max(np.abs(ev - f[tag + "eval_logits"])) <= 1e-5 * np.max(np.abs(f[tag + "eval_logits"]))

@@ -121,29 +121,21 @@ struct WgradArgs {
     } while (0)
 
 // host launchers (kernels_gemm.hip)
-// tile ids: 0 = 128x128 (DBUF), 1 = 128x64, 2 = 256x64, 3 = 128x128 BK64 (kernels_gemm.hip)
+// row-GEMM tile ids: register-staged 0 = 128x128 (two LDS images), 1 = 128x64, 4 = 128x128,
+// 6 = 128x128 64-K chunks (bf16), 13 = 128x32, 14 = 256x32; software-pipelined (kernels_gemm_pipe.hip)
+// 16 = 128x128, 17 = 128x64, 18 / 19 = the same loading two chunks ahead, 25 / 26 = 128x64 at
+// three blocks per CU (one / two chunks ahead)
 int launch_rowgemm(const RowGemmArgs& a, int tile, hipStream_t s);
-// 3x3 conv forward / dgrad with one row of taps per K-step (kernels_gemm.hip
-// rowgemm_row3_kernel); rowgemm_row3_ok: the launch's shape and operands are supported
-int launch_rowgemm_row3(const RowGemmArgs& a, hipStream_t s);
-int rowgemm_row3_ok(const RowGemmArgs& a);
 int rowgemm_tile_dims(int tile, int* bm, int* bn, int* bk);
 int rowgemm_tile_dbuf(int tile);
-// software-pipelined f32 row GEMM (kernels_gemm_pipe.hip); tile 0 = 128x128, 1 = 128x64.
-// launch_rowgemm routes tile ids 16 / 17 here.
+// software-pipelined f32 row GEMM (kernels_gemm_pipe.hip); tile 0 = 128x128, 1 = 128x64,
+// 2 / 3 = two chunks ahead, 4 / 5 = 128x64 at three blocks per CU
 int rowgemm_pipe_ok(const RowGemmArgs& a);
 int launch_rowgemm_pipe(const RowGemmArgs& a, int tile, hipStream_t s);
-// software-pipelined row3 weight gradient (kernels_wgrad_pipe.hip), tiles 0..3 = the shapes of
-// row3 tiles 20..23; launch_wgrad routes ids 30..33 here.
-int launch_wgrad_row3_pipe(const WgradArgs& a, int tile, hipStream_t s);
-// f32 row GEMM with LDS-DMA operands (kernels_gemm_dma.hip): tile 0 = 128x128 (2 stages),
-// 1 = 128x64, 2 = 128x128 (3 stages); launch_rowgemm routes ids 20..22 here.  Needs zero16.
-int rowgemm_dma_ok(const RowGemmArgs& a);
-int launch_rowgemm_dma(const RowGemmArgs& a, int tile, hipStream_t s);
-// wgrad tile ids (kernels_gemm.hip WGRAD_TILES): 0 = 128x128, 1 = 64x64 one wave,
-// 2 = 128x64 two waves, 3 = 64x128 two waves, 4 = 64x64 four waves, 5 = 128x64 four waves
+// wgrad tile ids (kernels_gemm.hip WGRAD_TILES): 0 = 128x128, 3 = 64x128 two waves,
+// 5 = 128x64 four waves, 7 = 64x64 three waves / SIMD, 8 = 64x32, 9 = 32x32;
 // 20.. = one row of 3x3 taps per block (3 accumulator sets; BM = channels of ONE tap):
-// 20 = 64x64, 21 = 128x64, 22 = 64x128, 23 = 128x128, 24 = 64x64 with 64-pixel chunks
+// 20 = 64x64, 21 = 128x64, 22 = 64x128, 23 = 128x128
 int launch_rowgemm16(const RowGemmArgs& a, int tile, hipStream_t s);
 // speed-of-light ablations of the forward rg16 GEMM (tile 4): -2 when not applicable
 int launch_rowgemm16_xp(const RowGemmArgs& a, int xp, hipStream_t s);
@@ -153,6 +145,6 @@ int launch_wgrad(const WgradArgs& a, int tile, hipStream_t s);
 int launch_wgrad16(const WgradArgs& a, int tile, hipStream_t s);
 int wgrad_tile_dims(int tile, int* bm, int* bn, int* bkp);
 int wgrad_tile_taps(int tile);  // taps of the M dimension one block covers (3 for 20..)
-// bf16 wgrad tile ids (a.bf16): 0 = 128x128/32 px, 1 = 128x128/64, 2 = 64x64/64,
+// register-staged bf16 wgrad tile ids (a.bf16): 0 = 128x128/32 px, 2 = 64x64/64,
 // 3 = 128x64/64, 4 = 64x128/64
 int wgrad16_tile_dims(int tile, int* bm, int* bn, int* bkp);

@@ -248,161 +248,6 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_kernel(RowGemmArgs
 }
 
 // ------------------------------------------------------------------------------------
-// 3x3 conv row GEMM, one ROW of taps per K-step (dy fixed, dx = 0..2): the forward / dgrad
-// counterpart of wgrad_row3_kernel.  A block's BM output pixels are SEG consecutive pixels
-// of ROWS image rows (SEG = min(W, BM), ROWS = BM / SEG; W a multiple or a divisor of BM),
-// so for a fixed dy the three dx taps read the same input row segments shifted by one
-// pixel.  Per K-step (dy, 32-channel slice) the block stages those segments ONCE with a
-// one-pixel halo (ROWS * (SEG + 2) LDS rows, zero outside the image, BN affine applied as
-// in rowgemm_kernel) plus the three taps' weight slices, then runs 3 x 16 MFMA k-steps per
-// wave: A of tap dx for local pixel (r, x) is LDS row r * (SEG + 2) + x + dx.  A third of
-// the A staging of the one-tap kernel and one commit phase per three taps.  K order: dy,
-// channel slice, dx, k (a reordering of the one-tap kernel's sum); same epilogues.
-// ------------------------------------------------------------------------------------
-template <int AOP, int EMODE, class T>
-__global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_row3_kernel(RowGemmArgs p) {
-    constexpr bool AFFINE = AOP == OP_AFFINE || AOP == OP_AFFINE_RELU;
-    constexpr bool ARELU = AOP == OP_AFFINE_RELU;
-    constexpr int BM = T::BM, BN = T::BN, WM = T::WM, WN = T::WN, BK = T::BK;
-    constexpr int NTH = T::THREADS;
-    constexpr int WAVES_N = BN / WN;
-    constexpr int LDK = BK + 4;
-    constexpr int MT = WM / 32, NT = WN / 32;
-    constexpr int F4R = BK / 4;
-    constexpr int RPP = NTH / F4R;
-    constexpr int AMAX = BM + 2 * (BM / 16);     // halo rows for the narrowest grid (W = 16)
-    constexpr int AP = (AMAX + RPP - 1) / RPP, BP = BN / RPP;
-    static_assert(BP * RPP == BN, "loader shape");
-    __shared__ __attribute__((aligned(16))) float As[AMAX * LDK];
-    __shared__ __attribute__((aligned(16))) float Bs[3 * BN * LDK];
-    static_assert(AMAX * LDK * 4 >= (BM / 64) * 2 * BN * 8, "epilogue scratch (row_epilogue)");
-
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wm = wave / WAVES_N, wn = wave % WAVES_N;
-    const int ntn = p.N / BN;
-    const int bid = p.xcd ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
-    const int tile_m = bid / ntn, tile_n = bid - tile_m * ntn;
-    const int m0 = tile_m * BM, n0 = tile_n * BN;
-    const int H = p.H, W = p.W, C = p.C;
-    const int SEG = W < BM ? W : BM;          // pixels per image row in this block
-    const int arows = (BM / SEG) * (SEG + 2);
-    const Pix q0 = decode(m0, H, W);          // block start: rows q0.y .. q0.y + BM/SEG - 1
-
-    const int lrow = tid / F4R, lc4 = tid % F4R;
-    // halo rows this thread stages: (local output row, pixel) -> source pixel of row dy
-    int hy[AP], hx[AP];
-    bool hok[AP];
-#pragma unroll
-    for (int i = 0; i < AP; ++i) {
-        const int hr = lrow + i * RPP;
-        const int r = hr / (SEG + 2), xl = hr - r * (SEG + 2) - 1;
-        hok[i] = hr < arows;
-        hy[i] = q0.y + r;
-        hx[i] = q0.x + xl;
-    }
-
-    f32x4 ra[AP], rb[3][BP], rsc, rsh;
-    unsigned vmask = 0;
-    bool rrelu = false;
-    const int nc = C / BK;
-
-    auto issue = [&](int t) {
-        const int dy = t / nc, c = (t - dy * nc) * BK + lc4 * 4;
-        if constexpr (AFFINE) {
-            rsc = *(const f32x4*)(p.ascale + c);
-            rsh = *(const f32x4*)(p.ashift + c);
-            if constexpr (ARELU) rrelu = c < p.arelu;
-        }
-        vmask = 0;
-#pragma unroll
-        for (int i = 0; i < AP; ++i) {
-            const int yy = hy[i] + dy - 1, xx = hx[i];
-            const bool valid = hok[i] & (yy >= 0) & (yy < H) & (xx >= 0) & (xx < W);
-            vmask |= valid ? (1u << i) : 0u;
-            const int src = valid ? (q0.img * H + yy) * W + xx : m0;
-            ra[i] = *(const f32x4*)(p.a + (size_t)src * p.lda + p.aoff + c);
-        }
-#pragma unroll
-        for (int d = 0; d < 3; ++d)
-#pragma unroll
-            for (int i = 0; i < BP; ++i)
-                rb[d][i] = *(const f32x4*)(p.bt + (size_t)(n0 + lrow + i * RPP) * p.K +
-                                           (dy * 3 + d) * C + c);
-    };
-    auto commit = [&]() {
-#pragma unroll
-        for (int i = 0; i < AP; ++i) {
-            if (AP * RPP > AMAX && lrow + i * RPP >= AMAX) break;
-            f32x4 v = ra[i];
-            if constexpr (AFFINE) {
-                v = v * rsc + rsh;
-                if (ARELU && rrelu)
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
-            }
-            if (!((vmask >> i) & 1u)) v = f32x4{0.f, 0.f, 0.f, 0.f};
-            *(f32x4*)&As[(lrow + i * RPP) * LDK + lc4 * 4] = v;
-        }
-#pragma unroll
-        for (int d = 0; d < 3; ++d)
-#pragma unroll
-            for (int i = 0; i < BP; ++i)
-                *(f32x4*)&Bs[(d * BN + lrow + i * RPP) * LDK + lc4 * 4] = rb[d][i];
-    };
-
-    f32x16 acc[MT][NT];
-#pragma unroll
-    for (int i = 0; i < MT; ++i)
-#pragma unroll
-        for (int j = 0; j < NT; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-    const int li = lane & 31, lh = lane >> 5;
-    int arow[MT];  // LDS halo row of this lane's output pixel for dx = 0
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-        const int ml = wm * WM + mt * 32 + li;
-        const int r = ml / SEG;
-        arow[mt] = r * (SEG + 2) + (ml - r * SEG);
-    }
-    const int nt_steps = 3 * nc;
-    issue(0);
-    commit();
-    __syncthreads();
-    for (int t = 0; t < nt_steps; ++t) {
-        if (t + 1 < nt_steps) issue(t + 1);
-#pragma unroll
-        for (int d = 0; d < 3; ++d) {
-            const float* bs = Bs + d * BN * LDK;
-#pragma unroll
-            for (int kk = 0; kk < BK / 8; ++kk) {
-                f32x4 af[MT], bf[NT];
-#pragma unroll
-                for (int mt = 0; mt < MT; ++mt)
-                    af[mt] = *(const f32x4*)&As[(arow[mt] + d) * LDK + kk * 8 + lh * 4];
-#pragma unroll
-                for (int nt = 0; nt < NT; ++nt)
-                    bf[nt] = *(const f32x4*)&bs[(wn * WN + nt * 32 + li) * LDK + kk * 8 + lh * 4];
-#pragma unroll
-                for (int s = 0; s < 4; ++s)
-#pragma unroll
-                    for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-                        for (int nt = 0; nt < NT; ++nt)
-                            acc[mt][nt] = mfma32(af[mt][s], bf[nt][s], acc[mt][nt]);
-            }
-        }
-        __syncthreads();
-        if (t + 1 < nt_steps) {
-            commit();
-            __syncthreads();
-        }
-    }
-    row_epilogue<EMODE, BM, BN, WM, WN>(p, acc, m0, n0, tile_m, wm, wn, lane, tid, As);
-}
-
-// ------------------------------------------------------------------------------------
 // Weight-gradient GEMM (reduction over pixels), same issue / compute / commit pipeline.
 // ------------------------------------------------------------------------------------
 // wgrad tile: block BM x BN, wave tile WM x WN, pixels per chunk BKP.
@@ -611,14 +456,9 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void wgrad_kernel(WgradArgs p) 
 // instead of 9x per layer and does a third of the staging per MFMA.  Same K order,
 // split-K slabs, bias column sums and loaders (OP_AFFINE / OP_AFFINE_RELU on x, OP_DZ on
 // dz) as wgrad_kernel; slab rows m = (3*dy + dx)*CA + ci, the one-tap layout.
-// NDY = 3 (row9, r03): one block covers all three tap rows -- it stages the chunk's three
-// input rows (3 (BKP + 2) LDS rows) and feeds nine accumulator sets, so x and the dz chunk
-// (or, BDZ, do and y) are read once per layer instead of once per tap row.  Same split-K
-// partition, same per-tap K order: the slabs are the row3 kernel's bits.
 // ------------------------------------------------------------------------------------
-template <int AOP, bool BDZ, class T, int NDY = 1>
+template <int AOP, bool BDZ, class T>
 __global__ __launch_bounds__(T::THREADS, T::OCC) void wgrad_row3_kernel(WgradArgs p) {
-    static_assert(NDY == 1 || NDY == 3, "tap rows per block");
     constexpr bool AFFINE = AOP == OP_AFFINE || AOP == OP_AFFINE_RELU;
     constexpr bool ARELU = AOP == OP_AFFINE_RELU;
     constexpr int BM = T::BM, BN = T::BN, BKP = T::BKP, WM = T::WM, WN = T::WN;
@@ -629,7 +469,7 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void wgrad_row3_kernel(WgradArg
     constexpr int AF = BM / 4, BF = BN / 4;          // float4 per pixel row
     constexpr int ARPP = NTH / AF, BRPP = NTH / BF;  // rows per pass
     constexpr int HROWS = BKP + 2;                   // chunk + halo
-    constexpr int AROWS = NDY * HROWS;               // (row9: three image rows)
+    constexpr int AROWS = HROWS;
     constexpr int AP = (AROWS + ARPP - 1) / ARPP, BP = BKP / BRPP;
     static_assert(ARPP * AF == NTH && BP * BRPP == BKP, "loader shape");
     __shared__ __attribute__((aligned(16))) float As[AROWS * LDA];
@@ -638,13 +478,13 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void wgrad_row3_kernel(WgradArg
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave / WAVES_N, wn = wave % WAVES_N;
     const int ctm = p.CA / BM;                       // channel tiles per tap row
-    const int tiles_n = p.Nw / BN, tiles_m = (NDY == 3 ? 1 : 3) * ctm;
+    const int tiles_n = p.Nw / BN, tiles_m = 3 * ctm;
     int idx = p.xcd ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
     const int tn = idx % tiles_n;
     idx /= tiles_n;
     const int tm = idx % tiles_m;
     const int split = idx / tiles_m;
-    const int dy = NDY == 3 ? 0 : tm / ctm, ca0 = (tm - dy * ctm) * BM;  // (first) tap row
+    const int dy = tm / ctm, ca0 = (tm - dy * ctm) * BM;  // tap row
     const int tapB = (tn * BN) / p.CB, cb0 = tn * BN - tapB * p.CB;
     const int H = p.H, W = p.W;
 
@@ -682,9 +522,8 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void wgrad_row3_kernel(WgradArg
         const Pix q = decode(pc, H, W);  // chunk start; the chunk stays on this row
 #pragma unroll
         for (int i = 0; i < AP; ++i) {
-            const int r0 = arow + i * ARPP;
-            const int dyi = NDY == 3 ? r0 / HROWS : 0, r = r0 - dyi * HROWS;
-            const int yy = q.y + dy + dyi - 1;
+            const int r0 = arow + i * ARPP, r = r0;
+            const int yy = q.y + dy - 1;
             const bool rowok = (yy >= 0) & (yy < H);
             const int rbase = (q.img * H + (rowok ? yy : q.y)) * W;
             const int xx = q.x + r - 1;
@@ -740,7 +579,7 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void wgrad_row3_kernel(WgradArg
         }
     };
 
-    constexpr int NTAP = 3 * NDY;
+    constexpr int NTAP = 3;
     f32x16 acc[NTAP][MT][NT];
 #pragma unroll
     for (int d = 0; d < NTAP; ++d)
@@ -769,8 +608,8 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void wgrad_row3_kernel(WgradArg
                 for (int nt = 0; nt < NT; ++nt) bf[nt] = Bs[pr * LDB + wn * WN + nt * 32 + li];
 #pragma unroll
                 for (int d = 0; d < NTAP; ++d) {
-                    // tap d = 3 dyi + dx reads halo row pr + dx of image row dyi
-                    const int ar = (d / 3) * HROWS + pr + d % 3;
+                    // tap dx = d reads halo row pr + dx
+                    const int ar = pr + d;
                     float af[MT];
 #pragma unroll
                     for (int mt = 0; mt < MT; ++mt) af[mt] = As[ar * LDA + wm * WM + mt * 32 + li];
@@ -1057,17 +896,8 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void wgradT_kernel(WgradArgs p)
 // layer; ROWGEMM_TILES lists what is instantiated.
 using RowTile0 = RowTile<128, 128, 64, 64, 32, true>;
 using RowTile1 = RowTile<128, 64, 64, 32, 32, false>;
-using RowTile2 = RowTile<256, 64, 64, 64, 32, false>;
-using RowTile3 = RowTile<128, 128, 64, 64, 64, false>;
 using RowTile4 = RowTile<128, 128, 64, 64, 32, false>;
-using RowTile5 = RowTile<256, 128, 64, 64, 32, false>;
 using RowTile6 = RowTile<128, 128, 64, 64, 64, true>;  // bf16: 4 MFMA k-steps per barrier
-using RowTile7 = RowTile<128, 128, 64, 64, 32, false, 3>;  // 3 waves / SIMD
-using RowTile8 = RowTile<128, 64, 64, 32, 32, false, 3>;
-using RowTile9 = RowTile<128, 128, 64, 64, 16, true, 3>;
-using RowTile10 = RowTile<128, 128, 64, 64, 32, false, 3, true>;  // t7 + MFMA-phase priority
-using RowTile11 = RowTile<128, 128, 64, 64, 32, false, 1, true>;  // t4 + MFMA-phase priority
-using RowTile12 = RowTile<128, 64, 64, 32, 32, false, 1, true>;   // t1 + MFMA-phase priority
 // (r02: 256x128 with 4 waves of 128x64, 128x128 with 2 waves of 128x64 and 128x64 with 2
 // waves of 64x64 measured 3-17 % slower than these defaults; not kept)
 // 32-output tiles (the 32-channel level 0 of the reference grid's narrow networks,
@@ -1075,10 +905,10 @@ using RowTile12 = RowTile<128, 64, 64, 32, 32, false, 1, true>;   // t1 + MFMA-p
 // 256 x 32 (4 waves), two LDS images
 using RowTile13 = RowTile<128, 32, 64, 32, 32, true, 2>;
 using RowTile14 = RowTile<256, 32, 64, 32, 32, true>;
+// (r01-r03: 256x64, 128x128 with 64-K chunks, 256x128, three waves per SIMD and
+// MFMA-phase s_setprio variants measured at or below these; not kept)
 #define ROWGEMM_TILES(X) \
-    X(0, RowTile0) X(1, RowTile1) X(2, RowTile2) X(3, RowTile3) X(4, RowTile4) X(5, RowTile5) \
-    X(6, RowTile6) X(7, RowTile7) X(8, RowTile8) X(9, RowTile9) X(10, RowTile10)            \
-    X(11, RowTile11) X(12, RowTile12) X(13, RowTile13) X(14, RowTile14)
+    X(0, RowTile0) X(1, RowTile1) X(4, RowTile4) X(6, RowTile6) X(13, RowTile13) X(14, RowTile14)
 
 template <int AMODE, int AOP, int EMODE, class T, bool BF>
 static int rowgemm_go(const RowGemmArgs& a, hipStream_t s) {
@@ -1103,33 +933,9 @@ static int rowgemm_tile(const RowGemmArgs& a, int tile, hipStream_t s) {
 }
 
 int rowgemm_tile_dims(int tile, int* bm, int* bn, int* bk) {
-    if (tile >= 20 && tile <= 22) {  // rowgemm_dma_kernel (LDS-DMA operands)
-        *bm = 128;
-        *bn = tile == 20 ? 128 : 64;  // 22: 128x64, three stages
-        *bk = 32;
-        return 0;
-    }
     if (tile >= 16 && tile <= 19) {  // rowgemm_pipe_kernel (18, 19: loads two chunks ahead)
         *bm = 128;
         *bn = tile % 2 == 0 ? 128 : 64;
-        *bk = 32;
-        return 0;
-    }
-    if (tile == 23 || tile == 24) {  // rowgemm_pipe_kernel, 8 waves: 128x256 / 256x128
-        *bm = tile == 23 ? 128 : 256;
-        *bn = tile == 23 ? 256 : 128;
-        *bk = 32;
-        return 0;
-    }
-    if (tile >= 29 && tile <= 32) {  // persistent pipelined 128x64 (29, 30) / 128x128 (31, 32)
-        *bm = 128;
-        *bn = tile <= 30 ? 64 : 128;
-        *bk = 32;
-        return 0;
-    }
-    if (tile == 27 || tile == 28) {  // rowgemm_pipe_kernel 256x64, 64x64 wave tiles
-        *bm = 256;
-        *bn = 64;
         *bk = 32;
         return 0;
     }
@@ -1152,8 +958,7 @@ int rowgemm_tile_dims(int tile, int* bm, int* bn, int* bk) {
 }
 
 int rowgemm_tile_dbuf(int tile) {
-    if ((tile >= 16 && tile <= 19) || (tile >= 23 && tile <= 32)) return 2;  // pipelined
-    if (tile >= 20 && tile <= 22) return 3;  // LDS-DMA
+    if ((tile >= 16 && tile <= 19) || tile == 25 || tile == 26) return 2;  // pipelined
 #define RG_DB(id, T) \
     if (tile == id) return T::DBUF ? 1 : 0;
     ROWGEMM_TILES(RG_DB)
@@ -1195,58 +1000,10 @@ static int rowgemm_dispatch(const RowGemmArgs& a, int tile, hipStream_t s) {
         if (a.amode == G_CONV3 && a.emode == E_BIAS_RELU_STATS)
             return aff ? rowgemm_tile<G_CONV3, OP_AFFINE, E_BIAS_RELU_STATS, false>(a, tile, s)
                        : rowgemm_tile<G_CONV3, OP_PLAIN, E_BIAS_RELU_STATS, false>(a, tile, s);
-        if (a.amode == G_CONV3 && a.emode == E_STORE && dz)
-            return rowgemm_tile<G_CONV3, OP_DZ, E_STORE, false>(a, tile, s);
-        if (a.amode == G_CONV3 && a.emode == E_STORE_BN && dz)
-            return rowgemm_tile<G_CONV3, OP_DZ, E_STORE_BN, false>(a, tile, s);
         if (a.amode == G_IDENT && a.emode == E_CONVT && aff && !a.arelu)
             return rowgemm_tile<G_IDENT, OP_AFFINE, E_CONVT, false>(a, tile, s);
     }
     return -1;  // combination not instantiated
-}
-
-// tap-row kernel tiles: 128 x 128 (4 waves of 64x64, 76 KB LDS, 2 blocks / CU) and
-// 128 x 64 (4 waves of 64x32, 48 KB, 3 blocks / CU) for N = 64 outputs
-using Row3Tile0 = RowTile<128, 128, 64, 64, 32, false, 2>;
-using Row3Tile1 = RowTile<128, 64, 64, 32, 32, false, 3>;
-
-template <int AOP, int EMODE, class T>
-static int row3_go(const RowGemmArgs& a, hipStream_t s) {
-    const dim3 grid((a.M / T::BM) * (a.N / T::BN));
-    hipLaunchKernelGGL((rowgemm_row3_kernel<AOP, EMODE, T>), grid, dim3(T::THREADS), 0, s, a);
-    return (int)hipGetLastError();
-}
-
-template <class T>
-static int row3_dispatch(const RowGemmArgs& a, hipStream_t s) {
-    const bool aff = a.ascale != nullptr;
-    if (a.emode == E_BIAS_RELU_STATS)
-        return aff ? row3_go<OP_AFFINE, E_BIAS_RELU_STATS, T>(a, s)
-                   : row3_go<OP_PLAIN, E_BIAS_RELU_STATS, T>(a, s);
-    if (a.emode == E_STATS)
-        return a.arelu ? row3_go<OP_AFFINE_RELU, E_STATS, T>(a, s)
-                       : (aff ? -1 : row3_go<OP_PLAIN, E_STATS, T>(a, s));
-    if (aff) return -1;
-    if (a.emode == E_STORE) return row3_go<OP_PLAIN, E_STORE, T>(a, s);
-    if (a.emode == E_STORE_BN) return row3_go<OP_PLAIN, E_STORE_BN, T>(a, s);
-    if (a.emode == E_ADD) return row3_go<OP_PLAIN, E_ADD, T>(a, s);
-    return -1;
-}
-
-int rowgemm_row3_ok(const RowGemmArgs& a) {
-    const int bm = 128, bn = a.N % 128 == 0 ? 128 : 64;
-    return a.amode == G_CONV3 && a.acoef == nullptr && a.bt != nullptr && a.bt16 == nullptr &&
-           a.K == 9 * a.C && a.C % 32 == 0 && a.N % bn == 0 && a.W >= 16 &&
-           (a.W % bm == 0 || bm % a.W == 0) && a.M % bm == 0 && a.H % (bm / (a.W < bm ? a.W : bm)) == 0 &&
-           (a.emode == E_BIAS_RELU_STATS || a.emode == E_STATS || a.emode == E_STORE ||
-            a.emode == E_STORE_BN || a.emode == E_ADD);
-}
-
-int launch_rowgemm_row3(const RowGemmArgs& a, hipStream_t s) {
-    if (!rowgemm_row3_ok(a)) return -1;
-    if ((a.emode == E_STORE_BN || a.emode == E_RESID) != (a.ey != nullptr)) return -1;
-    if ((a.escale != nullptr) != (a.eshift != nullptr) || (a.arelu && !a.ascale)) return -1;
-    return a.N % 128 == 0 ? row3_dispatch<Row3Tile0>(a, s) : row3_dispatch<Row3Tile1>(a, s);
 }
 
 int launch_rowgemm(const RowGemmArgs& a, int tile, hipStream_t s) {
@@ -1257,29 +1014,12 @@ int launch_rowgemm(const RowGemmArgs& a, int tile, hipStream_t s) {
     if ((a.escale != nullptr) != (a.eshift != nullptr) || (a.arelu && !aff)) return -1;
     if (a.emode == E_RESID && !a.escale) return -1;
     if ((a.bt != nullptr) == (a.bt16 != nullptr)) return -1;  // exactly one weight image
-    // ids 16..19: the software-pipelined f32 kernel (128x128 / 128x64, loads one or two
-    // chunks ahead); operands it does not take (bf16 weights, dz in the loader, > 2 GB
-    // offsets) run the same tile shape here
-    // ids 20..22: both operands by LDS-DMA (kernels_gemm_dma.hip); else the pipelined tile
-    if (tile >= 20 && tile <= 22) {
-        if (rowgemm_dma_ok(a)) return launch_rowgemm_dma(a, tile - 20, s);
-        tile = tile == 20 ? 16 : 17;
-    }
-    if (tile >= 16 && tile <= 19) {
-        if (rowgemm_pipe_ok(a)) return launch_rowgemm_pipe(a, tile - 16, s);
-        tile = tile % 2 == 0 ? 4 : 1;
-    }
-    if (tile == 23 || tile == 24) {  // wide pipelined tiles (short-K GEMMs: ConvT)
-        if (rowgemm_pipe_ok(a)) return launch_rowgemm_pipe(a, tile - 19, s);
-        tile = 4;
-    }
-    if (tile >= 25 && tile <= 28) {  // 128x64 at three blocks per CU / 256x64 (N = 64)
-        if (rowgemm_pipe_ok(a)) return launch_rowgemm_pipe(a, tile - 19, s);
-        tile = 1;
-    }
-    if (tile >= 29 && tile <= 32) {  // persistent: tiles 25 / 26 / 16 / 18 walking their tiles
-        if (rowgemm_pipe_ok(a)) return launch_rowgemm_pipe(a, tile - 19, s);
-        tile = tile <= 30 ? 1 : 4;
+    // ids 16..19, 25, 26: the software-pipelined f32 kernel (128x128 / 128x64, loads one or
+    // two chunks ahead; 25 / 26: 128x64 at three blocks per CU); operands it does not take
+    // (bf16 weights, > 2 GB offsets) run the same tile shape on the register-staged kernel
+    if ((tile >= 16 && tile <= 19) || tile == 25 || tile == 26) {
+        if (rowgemm_pipe_ok(a)) return launch_rowgemm_pipe(a, tile <= 19 ? tile - 16 : tile - 21, s);
+        tile = (tile <= 19 && tile % 2 == 0) ? 4 : 1;
     }
     return a.bt16 ? rowgemm_dispatch<true>(a, tile, s) : rowgemm_dispatch<false>(a, tile, s);
 }
@@ -1287,20 +1027,14 @@ int launch_rowgemm(const RowGemmArgs& a, int tile, hipStream_t s) {
 // wgrad tiles: (BM, BN, pixels per chunk).  Narrow tiles take deeper pixel chunks so the
 // per-chunk staging cost is spread over as many MFMAs as the 128x128 tile's.
 using WgTile0 = WgTile<128, 128, 64, 64, 32>;  // 4 waves
-using WgTile1 = WgTile<64, 64, 64, 64, 16>;    // 1 wave, 64x64 per wave
-using WgTile2 = WgTile<128, 64, 64, 64, 32>;   // 2 waves
 using WgTile3 = WgTile<64, 128, 64, 64, 32>;   // 2 waves
-using WgTile4 = WgTile<64, 64, 32, 32, 32>;    // 4 waves, 32x32 per wave
 using WgTile5 = WgTile<128, 64, 64, 32, 32>;   // 4 waves
-using WgTile6 = WgTile<128, 128, 64, 64, 32, 3>;  // 3 waves / SIMD
 using WgTile7 = WgTile<64, 64, 32, 32, 32, 3>;
-// 32-channel operands (narrow level 0): 64 x 32 (2 waves), 32 x 32 (1 wave); ids 10.. are
-// the channel-major wgradT tiles
+// 32-channel operands (narrow level 0): 64 x 32 (2 waves), 32 x 32 (1 wave)
 using WgTile8 = WgTile<64, 32, 32, 32, 32>;
 using WgTile9 = WgTile<32, 32, 32, 32, 32>;
 #define WGRAD_TILES(X) \
-    X(0, WgTile0) X(1, WgTile1) X(2, WgTile2) X(3, WgTile3) X(4, WgTile4) X(5, WgTile5) \
-    X(6, WgTile6) X(7, WgTile7) X(8, WgTile8) X(9, WgTile9)
+    X(0, WgTile0) X(3, WgTile3) X(5, WgTile5) X(7, WgTile7) X(8, WgTile8) X(9, WgTile9)
 
 #define WG_DIMS_R3(id, T) \
     if (tile == id) {     \
@@ -1314,20 +1048,14 @@ using Wr3Tile0 = WgTile<64, 64, 32, 32, 32>;    // 4 waves, 3 x 32x32 per wave
 using Wr3Tile1 = WgTile<128, 64, 64, 32, 32>;   // 4 waves, 3 x 64x32
 using Wr3Tile2 = WgTile<64, 128, 32, 64, 32>;   // 4 waves, 3 x 32x64
 using Wr3Tile3 = WgTile<128, 128, 64, 64, 32>;  // 4 waves, 3 x 64x64 (192 accumulators)
-using Wr3Tile4 = WgTile<64, 64, 32, 32, 64>;    // 64-pixel chunks
-using Wr3Tile5 = WgTile<128, 64, 64, 32, 16>;   // tile 21 on 16-pixel chunks (16-wide rows)
-#define WGRAD_ROW3_TILES(X) \
-    X(20, Wr3Tile0) X(21, Wr3Tile1) X(22, Wr3Tile2) X(23, Wr3Tile3) X(24, Wr3Tile4) X(25, Wr3Tile5)
+// (r03: 64-pixel chunks, 16-pixel rows, all three tap rows per block and a software-
+// pipelined schedule of these tiles measured at or below them; not kept)
+#define WGRAD_ROW3_TILES(X) X(20, Wr3Tile0) X(21, Wr3Tile1) X(22, Wr3Tile2) X(23, Wr3Tile3)
 
-// tile 26 (row9): all three tap rows of a 64x64 channel tile per block (wgrad_row3_kernel
-// NDY = 3); it counts 3 taps here so that its split-K partition is tile 20's
+// a row3 block covers three taps (its split-K partition counts them)
 int wgrad_tile_taps(int tile) { return tile >= 20 ? 3 : 1; }
 
 int wgrad_tile_dims(int tile, int* bm, int* bn, int* bkp) {
-    if (tile == 26) tile = 20;                 // row9 (64x64, three tap rows per block)
-    if (tile == 34) tile = 21;                 // pipelined row3, 128x64 at 2 waves / SIMD
-    if (tile >= 30 && tile <= 33) tile -= 10;  // pipelined row3 (kernels_wgrad_pipe.hip)
-    if (tile == 10 || tile == 15) return wgrad16_tile_dims(tile - 10, bm, bn, bkp);
     WGRAD_ROW3_TILES(WG_DIMS_R3)
 #define WG_DIMS(id, T) \
     if (tile == id) {  \
@@ -1354,15 +1082,6 @@ static int wgrad_row3_tile(const WgradArgs& a, int tile, hipStream_t s) {
     }
     WGRAD_ROW3_TILES(WR3_CASE)
 #undef WR3_CASE
-    if (tile == 26) {  // row9 on tile 20's shape, two waves per SIMD (144 accumulators)
-        using T = WgTile<64, 64, 32, 32, 32, 2>;
-        if (a.Mw != 9 * a.CA || a.CA % T::BM || a.Nw % T::BN || a.CB % T::BN || a.pps % T::BKP ||
-            a.W % T::BKP)
-            return -1;
-        const dim3 grid((a.CA / T::BM) * (a.Nw / T::BN) * a.splits);
-        hipLaunchKernelGGL((wgrad_row3_kernel<AOP, BDZ, T, 3>), grid, dim3(T::THREADS), 0, s, a);
-        return (int)hipGetLastError();
-    }
     return -1;
 }
 
@@ -1381,18 +1100,13 @@ static int wgrad_tile(const WgradArgs& a, int tile, hipStream_t s) {
     return -1;
 }
 
-// channel-major wgrad tiles (wgradT_kernel; bf16 ids 0.., f32 ids 10..): 4-pixel x
+// channel-major wgrad tiles of the register-staged bf16 path (wgradT_kernel): 4-pixel x
 // 4-channel loader units
 using Wg16Tile0 = WgTile<128, 128, 64, 64, 32>;
-using Wg16Tile1 = WgTile<128, 128, 64, 64, 64>;
 using Wg16Tile2 = WgTile<64, 64, 32, 32, 64>;
 using Wg16Tile3 = WgTile<128, 64, 64, 32, 64>;
 using Wg16Tile4 = WgTile<64, 128, 32, 64, 64>;
-using Wg16Tile5 = WgTile<128, 128, 64, 64, 32, 2>;
-using Wg16Tile6 = WgTile<64, 64, 32, 32, 64, 3>;
-#define WGRAD16_TILES(X) \
-    X(0, Wg16Tile0) X(1, Wg16Tile1) X(2, Wg16Tile2) X(3, Wg16Tile3) X(4, Wg16Tile4) \
-    X(5, Wg16Tile5) X(6, Wg16Tile6)
+#define WGRAD16_TILES(X) X(0, Wg16Tile0) X(2, Wg16Tile2) X(3, Wg16Tile3) X(4, Wg16Tile4)
 
 int wgrad16_tile_dims(int tile, int* bm, int* bn, int* bkp) {
 #define WG16_DIMS(id, T) \
@@ -1407,32 +1121,21 @@ int wgrad16_tile_dims(int tile, int* bm, int* bn, int* bkp) {
     return -1;
 }
 
-#define WGT_CASE(id, T, BF)                                                                   \
+#define WG16_CASE(id, T)                                                                      \
     if (tile == id) {                                                                         \
         if (a.Mw % T::BM || a.Nw % T::BN || a.CA % T::BM || a.CB % T::BN || a.pps % T::BKP) \
             return -1;                                                                        \
         const dim3 grid((a.Mw / T::BM) * (a.Nw / T::BN) * a.splits);                          \
-        hipLaunchKernelGGL((wgradT_kernel<AMODE, AOP, BMODE, T, BF>), grid, dim3(T::THREADS), 0, s, a); \
+        hipLaunchKernelGGL((wgradT_kernel<AMODE, AOP, BMODE, T, true>), grid, dim3(T::THREADS), 0, s, a); \
         return (int)hipGetLastError();                                                        \
     }
-#define WG16_CASE(id, T) WGT_CASE(id, T, true)
-#define WG32_CASE(id, T) WGT_CASE(id, T, false)
-// f32 channel-major tiles: measured ~3% below the pixel-major wgrad_kernel on every
-// layer shape (tools/gemm_tune), kept as a tuner/env alternative (ids 10 + t)
-#define WGRADT32_TILES(X) X(0, Wg16Tile0) X(5, Wg16Tile5)
 
-template <int AMODE, int AOP, int BMODE, bool BF>
+template <int AMODE, int AOP, int BMODE>
 static int wgradT_tile(const WgradArgs& a, int tile, hipStream_t s) {
-    if constexpr (BF) {
-        WGRAD16_TILES(WG16_CASE)
-    } else {
-        WGRADT32_TILES(WG32_CASE)
-    }
+    WGRAD16_TILES(WG16_CASE)
     return -1;
 }
 #undef WG16_CASE
-#undef WG32_CASE
-#undef WGT_CASE
 
 int launch_wgrad(const WgradArgs& a, int tile, hipStream_t s) {
     if (a.P < 1) return -1;
@@ -1440,17 +1143,15 @@ int launch_wgrad(const WgradArgs& a, int tile, hipStream_t s) {
         const bool aff = a.ascale != nullptr;
         if (a.bcoef || (a.arelu && !aff) || (aff && !a.arelu)) return -1;
         if (a.amode == G_CONV3 && a.bmode == G_IDENT)
-            return aff ? wgradT_tile<G_CONV3, OP_AFFINE_RELU, G_IDENT, true>(a, tile, s)
-                       : wgradT_tile<G_CONV3, OP_PLAIN, G_IDENT, true>(a, tile, s);
+            return aff ? wgradT_tile<G_CONV3, OP_AFFINE_RELU, G_IDENT>(a, tile, s)
+                       : wgradT_tile<G_CONV3, OP_PLAIN, G_IDENT>(a, tile, s);
         if (a.amode == G_IDENT && a.bmode == G_UP2 && aff)
-            return wgradT_tile<G_IDENT, OP_AFFINE_RELU, G_UP2, true>(a, tile, s);
+            return wgradT_tile<G_IDENT, OP_AFFINE_RELU, G_UP2>(a, tile, s);
         return -1;
     }
     const bool aff = a.ascale != nullptr, dz = a.bcoef != nullptr;
     if (a.arelu && !aff) return -1;
     if (a.arelu && dz) return -1;  // OP_DZ loaders are the ReLU -> BN order only
-    if (tile >= 30 && tile <= 34)  // row3, software-pipelined (kernels_wgrad_pipe.hip)
-        return launch_wgrad_row3_pipe(a, tile - 30, s);
     if (tile >= 20) {  // one row of 3x3 taps per block (wgrad_row3_kernel)
         if (a.amode != G_CONV3 || a.bmode != G_IDENT) return -1;
         if (dz) return aff ? wgrad_row3_tile<OP_AFFINE, true>(a, tile, s)
@@ -1458,22 +1159,6 @@ int launch_wgrad(const WgradArgs& a, int tile, hipStream_t s) {
         if (a.arelu) return wgrad_row3_tile<OP_AFFINE_RELU, false>(a, tile, s);
         return aff ? wgrad_row3_tile<OP_AFFINE, false>(a, tile, s)
                    : wgrad_row3_tile<OP_PLAIN, false>(a, tile, s);
-    }
-    if (tile >= 10 && !dz) {  // f32, channel-major LDS image (wgradT_kernel)
-        const int t = tile - 10;
-        if (a.amode == G_CONV3 && a.bmode == G_IDENT) {
-            if (a.arelu) return wgradT_tile<G_CONV3, OP_AFFINE_RELU, G_IDENT, false>(a, t, s);
-            return aff ? wgradT_tile<G_CONV3, OP_AFFINE, G_IDENT, false>(a, t, s)
-                       : wgradT_tile<G_CONV3, OP_PLAIN, G_IDENT, false>(a, t, s);
-        }
-        if (a.amode == G_IDENT && a.bmode == G_UP2) {
-            if (a.arelu) return wgradT_tile<G_IDENT, OP_AFFINE_RELU, G_UP2, false>(a, t, s);
-            return aff ? wgradT_tile<G_IDENT, OP_AFFINE, G_UP2, false>(a, t, s)
-                       : wgradT_tile<G_IDENT, OP_PLAIN, G_UP2, false>(a, t, s);
-        }
-        if (a.amode == G_IDENT && a.bmode == G_IDENT && !aff)
-            return wgradT_tile<G_IDENT, OP_PLAIN, G_IDENT, false>(a, t, s);
-        return -1;
     }
     if (a.amode == G_CONV3 && a.bmode == G_IDENT && dz)
         return aff ? wgrad_tile<G_CONV3, OP_AFFINE, G_IDENT, true>(a, tile, s)

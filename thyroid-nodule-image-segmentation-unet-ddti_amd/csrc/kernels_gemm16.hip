@@ -43,44 +43,21 @@ __device__ __forceinline__ void block_barrier() {
     asm volatile("" ::: "memory");
 }
 
-// block barrier that the scheduler may not move any instruction across (MFMAs included: the
-// ping-pong kernel's phases are defined by which barrier interval an MFMA lands in)
-__device__ __forceinline__ void pp_barrier() {
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-}
-
 template <int N>
 __device__ __forceinline__ void wait_vm() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-// block tile BM x BN, wave tile WM x WN, S LDS stages of BK (64 or 32) K each.
-// ONEBAR: prefetch distance S-2 chunks and one barrier per chunk (the stage restaged at
-// iteration k was read at iteration k-2, and every wave has passed iteration k-1's barrier
-// since); otherwise distance S-1 with a second barrier after the MFMAs.
-// ILV: the DMA pieces of chunk k+DIST are issued between the MFMAs of chunk k (one share
-// per k-step, placed by sched_group_barrier) instead of all at the top of the iteration,
-// where every wave of the block issued them at once and left the matrix pipes idle.
-// RA: read ahead -- the LDS fragments of k-step kk + 1 are issued before the MFMAs of k-step
-// kk (two register sets, sched_barrier fences), so each k-step waits only for reads issued
-// one k-step earlier instead of for its own (the compiler's schedule waited lgkmcnt(0) in
-// front of every k-step's MFMAs).
-// M16: v_mfma_f32_16x16x32_bf16 instead of 32x32x16 (the same FLOP per cycle; the chip holds
-// a higher clock under the 16x16 shape on random data, MI355X_MICROARCH.md "DVFS give-back"
-// item 7).  Lane l reads A row l & 15, 16-B chunk 4 ks + (l >> 4) of k-step ks; the
-// accumulators are re-laid out to the 32x32 map through LDS before the shared epilogue.
-// PRIO: s_setprio(1) around each k-step's MFMA cluster (keeps hipcc from moving MFMAs across
-// the barriers, cdna_hip_programming.md T5).
-template <int BM_, int BN_, int WM_, int WN_, int S_, int OCC_, int BK_ = 64, bool ONEBAR_ = false,
-          bool ILV_ = false, bool RA_ = false, bool M16_ = false, bool PRIO_ = false>
+// block tile BM x BN, wave tile WM x WN, S LDS stages of BK = 64 K each; prefetch distance
+// S-1 chunks, a second barrier after each chunk's MFMAs frees its stage.
+// (r01-r03 variants measured at or below this schedule and not kept: 32-K chunks with 4-5
+// stages and one barrier per chunk, DMA issue interleaved between the MFMAs, LDS fragments
+// read one k-step ahead, 16x16x32 MFMAs with / without s_setprio, a ping-pong schedule of two
+// wave groups one barrier apart)
+template <int BM_, int BN_, int WM_, int WN_, int S_, int OCC_>
 struct Tile16 {
     static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, S = S_, OCC = OCC_;
-    static constexpr int BK = BK_;
-    static constexpr bool ONEBAR = ONEBAR_, ILV = ILV_, RA = RA_, M16 = M16_, PRIO = PRIO_;
+    static constexpr int BK = 64;
     static constexpr int WAVES = (BM / WM) * (BN / WN);
     static constexpr int THREADS = 64 * WAVES;
 };
@@ -91,7 +68,6 @@ struct Tile16 {
 template <int AMODE, int EMODE, class T, int XP = 0>
 __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm16_kernel(RowGemmArgs p) {
     constexpr int BM = T::BM, BN = T::BN, WM = T::WM, WN = T::WN, S = T::S, BK = T::BK;
-    constexpr bool ONEBAR = T::ONEBAR, ILV = T::ILV;
     constexpr int WAVES = T::WAVES, WAVES_N = BN / WN;
     constexpr int MT = WM / 32, NT = WN / 32;
     constexpr int RB = 2 * BK;             // bytes per LDS row
@@ -104,9 +80,8 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm16_kernel(RowGemmAr
     auto swz = [](int r) { return (r / RPB) & (LPR - 1); };
     constexpr int AI = BM / (RPI * WAVES), BI = BN / (RPI * WAVES);  // DMA instructions per chunk
     static_assert(AI * RPI * WAVES == BM && BI * RPI * WAVES == BN, "loader shape");
-    static_assert(BK == 64 || BK == 32, "chunk depth");
     constexpr int GPC = AI + BI;
-    constexpr int DIST = ONEBAR ? S - 2 : S - 1;  // chunks in flight beyond the current one
+    constexpr int DIST = S - 1;  // chunks in flight beyond the current one
     static_assert(DIST >= 1, "stages");
     constexpr int STAGE = (BM + BN) * RB;  // bytes
     constexpr int RED = 2 * (BM / 64) * BN * 8;  // epilogue scratch (f64 partials per 64-row unit)
@@ -145,14 +120,14 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm16_kernel(RowGemmAr
     const uint16_t* zero = (const uint16_t*)p.zero16;
 
     // DMA pieces [j0, j1) of chunk kc into stage st (pieces 0..AI-1 = A rows, then B rows)
-    auto issue_range = [&](int kc, int st, int j0, int j1) {
+    auto issue = [&](int kc, int st) {
         const int k0 = kc * BK;
         const int tap = k0 / C;
         const int c0 = k0 - tap * C;
         char* base = smem + st * STAGE;
 #pragma unroll
         for (int j = 0; j < AI; ++j) {
-            if (j < j0 || j >= j1 || (XP & 1)) continue;
+            if (XP & 1) continue;
             bool valid;
             const int src = gather_src<AMODE>(tap, am[j], aq[j], H, W, valid);
             const uint16_t* g = (valid && aok[j]) ? p.a16 + (size_t)src * p.lda + c0 + ach[j] : zero;
@@ -160,35 +135,18 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm16_kernel(RowGemmAr
         }
 #pragma unroll
         for (int j = 0; j < BI; ++j) {
-            if (AI + j < j0 || AI + j >= j1 || (XP & 2)) continue;
+            if (XP & 2) continue;
             glds16(bsrc[j] + k0, base + BM * RB + (j * WAVES + wave) * 1024);
         }
     };
-    auto issue = [&](int kc, int st) { issue_range(kc, st, 0, GPC); };
 
-    constexpr bool M16 = T::M16;
-    constexpr int MI = WM / 16, NJ = WN / 16;  // M16: 16x16 accumulator tiles per wave
-    // exactly one of the two accumulator sets is live (the other is sized 1x1 and unused)
-    f32x16 acc[M16 ? 1 : MT][M16 ? 1 : NT];
-    f32x4 acc4[M16 ? MI : 1][M16 ? NJ : 1];
-    if constexpr (M16) {
+    f32x16 acc[MT][NT];
 #pragma unroll
-        for (int i = 0; i < MI; ++i)
+    for (int i = 0; i < MT; ++i)
 #pragma unroll
-            for (int j = 0; j < NJ; ++j) acc4[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    } else {
+        for (int j = 0; j < NT; ++j)
 #pragma unroll
-        for (int i = 0; i < MT; ++i)
-#pragma unroll
-            for (int j = 0; j < NT; ++j)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-    }
-    // M16 fragment rows: row = wave base + 16 i + (lane & 15); the row XOR (r / RPB) & (LPR - 1)
-    // is the same for every i (16 i / RPB is a multiple of LPR), so one per lane
-    const int r16 = lane & 15, q16 = lane >> 4;
-    const int sa16 = swz(wm * WM + r16), sb16 = swz(wn * WN + r16);
-    const int a16o = (wm * WM + r16) * RB, b16o = (BM + wn * WN + r16) * RB;
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
     const int li = lane & 31, lh = lane >> 5;
     // LDS read offsets (bytes) of this lane's rows; the chunk XOR depends on the row only
@@ -213,12 +171,9 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm16_kernel(RowGemmAr
 #pragma unroll
     for (int s = 0; s < DIST; ++s)
         if (s < nk) issue(s, s);
-    constexpr int KS = BK / 16;                 // MFMA k-steps per chunk
-    static_assert(!ILV || GPC % KS == 0, "pieces per k-step");
-    constexpr int PPS = GPC / KS;               // ILV: DMA pieces per k-step
-    constexpr int INFL = ILV ? DIST - 1 : DIST; // chunks issued after kc before its wait
+    constexpr int INFL = DIST;  // chunks issued after kc before its wait
     for (int kc = 0; kc < nk; ++kc) {
-        if (!ILV && kc + DIST < nk) issue(kc + DIST, (kc + DIST) % S);
+        if (kc + DIST < nk) issue(kc + DIST, (kc + DIST) % S);
         // chunks issued after kc that may stay in flight
         const int ahead = min(INFL, nk - 1 - kc);
         if constexpr (XP & 8) {
@@ -239,50 +194,6 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm16_kernel(RowGemmAr
         }
         if constexpr (!(XP & 8)) block_barrier();
         const char* base = smem + (kc % S) * STAGE;
-        const bool more = kc + DIST < nk;
-        if constexpr (M16) {
-#pragma unroll
-            for (int ks = 0; ks < BK / 32; ++ks) {
-                const int c = ks * 4 + q16;
-                bf16x8 af[MI], bfr[NJ];
-#pragma unroll
-                for (int i = 0; i < MI; ++i)
-                    af[i] = *(const bf16x8*)(base + a16o + i * 16 * RB + ((c ^ sa16) << 4));
-#pragma unroll
-                for (int j = 0; j < NJ; ++j)
-                    bfr[j] = *(const bf16x8*)(base + b16o + j * 16 * RB + ((c ^ sb16) << 4));
-                if constexpr (T::PRIO) __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-                for (int i = 0; i < MI; ++i)
-#pragma unroll
-                    for (int j = 0; j < NJ; ++j)
-                        acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc4[i][j], 0, 0, 0);
-                if constexpr (T::PRIO) __builtin_amdgcn_s_setprio(0);
-            }
-        } else if constexpr (T::RA && !ILV) {
-            bf16x8 af[2][MT], bfr[2][NT];
-            auto rd = [&](int kk, int set) {
-                const int c = kk * 2 + lh;
-#pragma unroll
-                for (int mt = 0; mt < MT; ++mt)
-                    af[set][mt] = *(const bf16x8*)(base + aro[mt] + ((c ^ afx[mt]) << 4));
-#pragma unroll
-                for (int nt = 0; nt < NT; ++nt)
-                    bfr[set][nt] = *(const bf16x8*)(base + bro[nt] + ((c ^ bfx[nt]) << 4));
-            };
-            rd(0, 0);
-#pragma unroll
-            for (int kk = 0; kk < BK / 16; ++kk) {
-                if (kk + 1 < BK / 16) rd(kk + 1, (kk + 1) & 1);
-                __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-                    for (int nt = 0; nt < NT; ++nt)
-                        acc[mt][nt] = mfma32_bf16(af[kk & 1][mt], bfr[kk & 1][nt], acc[mt][nt]);
-                __builtin_amdgcn_sched_barrier(0);
-            }
-        } else
 #pragma unroll
         for (int kk = 0; kk < BK / 16; ++kk) {
             const int c = kk * 2 + lh;
@@ -294,208 +205,21 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm16_kernel(RowGemmAr
                 for (int nt = 0; nt < NT; ++nt) bfr[nt] = xa;
             } else {
 #pragma unroll
-            for (int mt = 0; mt < MT; ++mt)
-                af[mt] = *(const bf16x8*)(base + aro[mt] + ((c ^ afx[mt]) << 4));
+                for (int mt = 0; mt < MT; ++mt)
+                    af[mt] = *(const bf16x8*)(base + aro[mt] + ((c ^ afx[mt]) << 4));
 #pragma unroll
-            for (int nt = 0; nt < NT; ++nt)
-                bfr[nt] = *(const bf16x8*)(base + bro[nt] + ((c ^ bfx[nt]) << 4));
+                for (int nt = 0; nt < NT; ++nt)
+                    bfr[nt] = *(const bf16x8*)(base + bro[nt] + ((c ^ bfx[nt]) << 4));
             }
 #pragma unroll
             for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
                 for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma32_bf16(af[mt], bfr[nt], acc[mt][nt]);
-            if constexpr (ILV) {
-                if (more) issue_range(kc + DIST, (kc + DIST) % S, kk * PPS, (kk + 1) * PPS);
-            }
         }
-        if constexpr (ILV) {
-            // per k-step: its LDS reads, then MFMAs with the DMA pieces spread between them
-#pragma unroll
-            for (int kk = 0; kk < KS; ++kk) {
-                __builtin_amdgcn_sched_group_barrier(0x100, MT + NT, 0);  // DS read
-#pragma unroll
-                for (int q = 0; q < PPS; ++q) {
-                    __builtin_amdgcn_sched_group_barrier(0x008, MT * NT / PPS, 0);  // MFMA
-                    __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);              // VMEM read
-                }
-            }
-        }
-        if constexpr (!ONEBAR && !(XP & 8)) {
+        if constexpr (!(XP & 8)) {
             // this stage's ds_reads must have returned before any wave restages it
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             block_barrier();
-        }
-    }
-    if constexpr (ONEBAR) {  // the epilogue's LDS scratch overlaps stages other waves may read
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        block_barrier();
-    }
-    if constexpr (M16) {
-        // 16x16 map (row 4 (l >> 4) + r, col l & 15) -> 32x32 map (row (r & 3) + 8 (r >> 2) +
-        // 4 (l >> 5), col l & 31), one 32x32 tile at a time through a per-wave LDS scratch
-        // [32][33] (the stages are free: every wave is past the loop's last barrier)
-        static_assert(WAVES * 32 * 33 * 4 <= SMEM, "M16 re-layout scratch");
-        f32x16 acc32[MT][NT];
-        float* scr = (float*)smem + wave * 32 * 33;
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-            for (int nt = 0; nt < NT; ++nt) {
-#pragma unroll
-                for (int a = 0; a < 2; ++a)
-#pragma unroll
-                    for (int b = 0; b < 2; ++b)
-#pragma unroll
-                        for (int r = 0; r < 4; ++r)
-                            scr[(16 * a + 4 * q16 + r) * 33 + 16 * b + r16] = acc4[2 * mt + a][2 * nt + b][r];
-                __builtin_amdgcn_wave_barrier();  // a wave's LDS accesses complete in order
-#pragma unroll
-                for (int r = 0; r < 16; ++r)
-                    acc32[mt][nt][r] = scr[((r & 3) + 8 * (r >> 2) + 4 * lh) * 33 + li];
-                __builtin_amdgcn_wave_barrier();
-            }
-        row_epilogue<EMODE, BM, BN, WM, WN, true>(p, acc32, m0, n0, tile_m, wm, wn, lane, tid, (float*)smem);
-    } else {
-        row_epilogue<EMODE, BM, BN, WM, WN, true>(p, acc, m0, n0, tile_m, wm, wn, lane, tid, (float*)smem);
-    }
-}
-
-// ------------------------------------------------------------------------------------
-// Ping-pong schedule of the same GEMM (256x256 tile, 8 waves of 128x64, two 64-K stages):
-// the two waves that share a SIMD (wave w and w + 4) belong to different groups, G0 = waves
-// 0-3 and G1 = waves 4-7, and G1 runs one barrier behind G0, so in every barrier interval one
-// group runs its chunk's MFMAs while the other issues the next chunk's LDS-DMA pieces.  The
-// one-schedule kernel above issues and waits in every wave at once, which left the matrix pipes
-// idle for the DMA issue (speed-of-light ablation, profiles/r03_xp.txt: dropping the DMA
-// raised the forward GEMM from 1079 to 1432 TF/s).  Events (hardware barrier counts): G0's
-// barriers A_k (2k) and B_k (2k+1), G1's X (0), A_k (2k+1), B_k (2k+2).
-//   G0: [issue k+1 -> stage (k+1)%2, vmcnt(0)] A_k [MFMAs of k] B_k    ... one extra barrier
-//   G1: X [issue k+1] A_k [MFMAs of k, lgkmcnt(0), vmcnt(0)] B_k
-// RAW: G0 reads chunk k after event 2k; its own pieces were waited before A_k, G1's before
-// G1's B_{k-1} (event 2k).  G1 reads chunk k after event 2k+1.  WAR: stage (k+1)%2 held chunk
-// k-1; G1 writes it after event 2k (G0 finished k-1 at 2k-1, G1 itself at 2k), G0 after event
-// 2k+1.  Same K order, per-chunk MFMA order and epilogue as rowgemm16_kernel: bit-identical.
-// ------------------------------------------------------------------------------------
-template <int AMODE, int EMODE>
-__global__ __launch_bounds__(512, 1) void rowgemm16_pp_kernel(RowGemmArgs p) {
-    constexpr int BM = 256, BN = 256, WM = 128, WN = 64, BK = 64, WAVES = 8, WAVES_N = 4;
-    constexpr int MT = WM / 32, NT = WN / 32;
-    constexpr int RB = 2 * BK, LPR = RB / 16, RPI = 64 / LPR, RPB = 256 / RB;
-    auto swz = [](int r) { return (r / RPB) & (LPR - 1); };
-    constexpr int AI = BM / (RPI * WAVES), BI = BN / (RPI * WAVES);
-    constexpr int STAGE = (BM + BN) * RB;
-    constexpr int SMEM = 2 * STAGE;
-    static_assert(SMEM >= 2 * (BM / 64) * BN * 8, "epilogue scratch");
-    __shared__ __attribute__((aligned(1024))) char smem[SMEM];
-
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int grp = wave >> 2;  // wave w and w + 4 share a SIMD
-    const int wm = wave / WAVES_N, wn = wave % WAVES_N;
-    const int ntn = p.N / BN;
-    const int bid = p.xcd ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
-    const int tile_m = bid / ntn, tile_n = bid - tile_m * ntn;
-    const int m0 = tile_m * BM, n0 = tile_n * BN;
-    const int H = p.H, W = p.W, C = p.C, K = p.K;
-
-    const int lr = lane / LPR, slot = lane % LPR;
-    Pix aq[AI];
-    int am[AI], ach[AI];
-    bool aok[AI];
-#pragma unroll
-    for (int j = 0; j < AI; ++j) {
-        const int r = (j * WAVES + wave) * RPI + lr;
-        const int m = m0 + r;
-        aok[j] = m < p.M;
-        am[j] = aok[j] ? m : p.M - 1;
-        aq[j] = decode(am[j], H, W);
-        ach[j] = (slot ^ swz(r)) * 8;
-    }
-    const uint16_t* bsrc[BI];
-#pragma unroll
-    for (int j = 0; j < BI; ++j) {
-        const int r = (j * WAVES + wave) * RPI + lr;
-        bsrc[j] = p.bt16 + (size_t)(n0 + r) * K + (slot ^ swz(r)) * 8;
-    }
-    const uint16_t* zero = (const uint16_t*)p.zero16;
-    auto issue = [&](int kc) {
-        const int k0 = kc * BK;
-        const int tap = k0 / C;
-        const int c0 = k0 - tap * C;
-        char* base = smem + (kc & 1) * STAGE;
-#pragma unroll
-        for (int j = 0; j < AI; ++j) {
-            bool valid;
-            const int src = gather_src<AMODE>(tap, am[j], aq[j], H, W, valid);
-            const uint16_t* g = (valid && aok[j]) ? p.a16 + (size_t)src * p.lda + c0 + ach[j] : zero;
-            glds16(g, base + (j * WAVES + wave) * 1024);
-        }
-#pragma unroll
-        for (int j = 0; j < BI; ++j) glds16(bsrc[j] + k0, base + BM * RB + (j * WAVES + wave) * 1024);
-    };
-
-    f32x16 acc[MT][NT];
-#pragma unroll
-    for (int i = 0; i < MT; ++i)
-#pragma unroll
-        for (int j = 0; j < NT; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-    const int lh = lane >> 5, li = lane & 31;
-    int aro[MT], afx[MT], bro[NT], bfx[NT];
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-        const int r = wm * WM + mt * 32 + li;
-        aro[mt] = r * RB;
-        afx[mt] = swz(r);
-    }
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-        const int r = wn * WN + nt * 32 + li;
-        bro[nt] = (BM + r) * RB;
-        bfx[nt] = swz(r);
-    }
-    // the chunk's MFMAs from stage kc & 1 (same order as rowgemm16_kernel's plain path)
-    auto compute = [&](int kc) {
-        const char* base = smem + (kc & 1) * STAGE;
-#pragma unroll
-        for (int kk = 0; kk < BK / 16; ++kk) {
-            const int c = kk * 2 + lh;
-            bf16x8 af[MT], bfr[NT];
-#pragma unroll
-            for (int mt = 0; mt < MT; ++mt) af[mt] = *(const bf16x8*)(base + aro[mt] + ((c ^ afx[mt]) << 4));
-#pragma unroll
-            for (int nt = 0; nt < NT; ++nt) bfr[nt] = *(const bf16x8*)(base + bro[nt] + ((c ^ bfx[nt]) << 4));
-#pragma unroll
-            for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-                for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma32_bf16(af[mt], bfr[nt], acc[mt][nt]);
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    };
-
-    const int nk = K / BK;
-    issue(0);
-    wait_vm<0>();
-    if (grp == 0) {
-        for (int kc = 0; kc < nk; ++kc) {
-            pp_barrier();  // A_k
-            compute(kc);
-            pp_barrier();  // B_k
-            if (kc + 1 < nk) {
-                issue(kc + 1);
-                wait_vm<0>();
-            }
-        }
-        pp_barrier();  // pairs with G1's B_{nk-1}
-    } else {
-        pp_barrier();  // X
-        for (int kc = 0; kc < nk; ++kc) {
-            if (kc + 1 < nk) issue(kc + 1);
-            pp_barrier();  // A_k
-            compute(kc);
-            wait_vm<0>();
-            pp_barrier();  // B_k
         }
     }
     row_epilogue<EMODE, BM, BN, WM, WN, true>(p, acc, m0, n0, tile_m, wm, wn, lane, tid, (float*)smem);
@@ -657,46 +381,12 @@ static int rg16r3_go(const RowGemmArgs& a, hipStream_t s) {
     return (int)hipGetLastError();
 }
 
-template <int AMODE, int EMODE>
-static int rg16pp_go(const RowGemmArgs& a, hipStream_t s) {
-    if (a.N % 256 || a.C % 64 || a.K % 64) return -1;
-    if (EMODE == E_CONVT && (a.cout % 256)) return -1;
-    const dim3 grid(((a.M + 255) / 256) * (a.N / 256));
-    hipLaunchKernelGGL((rowgemm16_pp_kernel<AMODE, EMODE>), grid, dim3(512), 0, s, a);
-    return (int)hipGetLastError();
-}
-
-// tiles: 0 = 128x128, 2 stages (64 KB LDS, 2 blocks/CU); 1 = 128x128, 3 stages (96 KB);
-// 2 = 256x128, 8 waves, 2 stages (96 KB); 3 = 128x128, 4 stages (128 KB);
-// 4 = 256x256, 8 waves of 128x64, 2 stages (128 KB); 5 = 256x128, 8 waves, 3 stages (144 KB);
-// BK = 32 stages: 6 = 256x256, 4 stages (128 KB, 3 chunks = 96 K in flight); 7 = 256x256,
-// 5 stages, one barrier per chunk (160 KB, 3 chunks in flight); 8 = 128x128, 4 stages, one
-// barrier (64 KB, 2 blocks/CU)
+// tiles: 0 = 128x128, 2 stages (64 KB LDS, 2 blocks/CU); 2 = 256x128, 8 waves, 2 stages
+// (96 KB); 4 = 256x256, 8 waves of 128x64, 2 stages (128 KB); 19 = the tap-row halo kernel
 using T16_0 = Tile16<128, 128, 64, 64, 2, 2>;
-using T16_1 = Tile16<128, 128, 64, 64, 3, 1>;
 using T16_2 = Tile16<256, 128, 64, 64, 2, 1>;
-using T16_3 = Tile16<128, 128, 64, 64, 4, 1>;
 using T16_4 = Tile16<256, 256, 128, 64, 2, 1>;
-using T16_5 = Tile16<256, 128, 64, 64, 3, 1>;
-using T16_6 = Tile16<256, 256, 128, 64, 4, 1, 32>;
-using T16_7 = Tile16<256, 256, 128, 64, 5, 1, 32, true>;
-using T16_8 = Tile16<128, 128, 64, 64, 4, 2, 32, true>;
-// interleaved DMA issue: 9 = tile 6, 10 = tile 7, 11 = 128x128 BK 64 3 stages 1 block/CU
-using T16_9 = Tile16<256, 256, 128, 64, 4, 1, 32, false, true>;
-using T16_10 = Tile16<256, 256, 128, 64, 5, 1, 32, true, true>;
-using T16_11 = Tile16<128, 128, 64, 64, 3, 1, 64, false, true>;
-// read-ahead LDS fragments: 12 = tile 4 (256x256), 13 = tile 0 (128x128, 2 blocks per CU)
-using T16_12 = Tile16<256, 256, 128, 64, 2, 1, 64, false, false, true>;
-using T16_13 = Tile16<128, 128, 64, 64, 2, 2, 64, false, false, true>;
-// 16x16x32 MFMAs (M16): 14 = tile 4, 15 = tile 0; with s_setprio around the MFMAs: 16, 17
-using T16_14 = Tile16<256, 256, 128, 64, 2, 1, 64, false, false, false, true>;
-using T16_15 = Tile16<128, 128, 64, 64, 2, 2, 64, false, false, false, true>;
-using T16_16 = Tile16<256, 256, 128, 64, 2, 1, 64, false, false, false, true, true>;
-using T16_17 = Tile16<128, 128, 64, 64, 2, 2, 64, false, false, false, true, true>;
-#define ROWGEMM16_TILES(X)                                                                     \
-    X(0, T16_0) X(1, T16_1) X(2, T16_2) X(3, T16_3) X(4, T16_4) X(5, T16_5) X(6, T16_6) X(7, T16_7) \
-    X(8, T16_8) X(9, T16_9) X(10, T16_10) X(11, T16_11) X(12, T16_12) X(13, T16_13)            \
-    X(14, T16_14) X(15, T16_15) X(16, T16_16) X(17, T16_17)
+#define ROWGEMM16_TILES(X) X(0, T16_0) X(2, T16_2) X(4, T16_4)
 
 template <int AMODE, int EMODE, class T, int XP = 0>
 static int rg16_go(const RowGemmArgs& a, hipStream_t s) {
@@ -709,7 +399,6 @@ static int rg16_go(const RowGemmArgs& a, hipStream_t s) {
 
 template <int AMODE, int EMODE>
 static int rg16_tile(const RowGemmArgs& a, int tile, hipStream_t s) {
-    if (tile == 18) return rg16pp_go<AMODE, EMODE>(a, s);
     if (tile == 19) {
         if constexpr (AMODE == G_CONV3) return rg16r3_go<EMODE>(a, s);
         return -1;
@@ -935,15 +624,11 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void wgrad16_kernel(WgradArgs p
 }
 
 // wgrad16 tiles: 0 = 128x128, 64 pixels per stage, 2 stages (64 KB, 2 blocks/CU);
-// 1 = the same with 3 stages (96 KB, 1 block/CU); 2 = 256x256, 8 waves of 128x64,
-// 2 stages (128 KB, 1 block/CU)
+// 2 = 256x256, 8 waves of 128x64, 2 stages (128 KB, 1 block/CU)
+// (r01-r02, not kept: 3-stage 128x128, 256x128 / 128x256 at 3 stages)
 using W16_0 = WTile16<128, 128, 64, 64, 64, 2, 2>;
-using W16_1 = WTile16<128, 128, 64, 64, 64, 3, 1>;
 using W16_2 = WTile16<256, 256, 128, 64, 64, 2, 1>;
-// 3 = 256x128, 4 = 128x256: 8 waves of 64x64, 3 stages (144 KB, two chunks in flight)
-using W16_3 = WTile16<256, 128, 64, 64, 64, 3, 1>;
-using W16_4 = WTile16<128, 256, 64, 64, 64, 3, 1>;
-#define WGRAD16G_TILES(X) X(0, W16_0) X(1, W16_1) X(2, W16_2) X(3, W16_3) X(4, W16_4)
+#define WGRAD16G_TILES(X) X(0, W16_0) X(2, W16_2)
 
 template <int AMODE, int BMODE, class T>
 static int wg16_go(const WgradArgs& a, hipStream_t s) {
@@ -969,7 +654,7 @@ int wgrad16g_tile_dims(int tile, int* bm, int* bn, int* stages) {
 }
 
 int rowgemm16_tile_dims(int tile, int* bm, int* bn, int* stages) {
-    if (tile == 18 || tile == 19) {  // ping-pong / tap-row halo 256x256
+    if (tile == 19) {  // tap-row halo 256x256
         *bm = *bn = 256;
         if (stages) *stages = 2;
         return 0;
@@ -1018,10 +703,7 @@ int launch_wgrad16(const WgradArgs& a, int tile, hipStream_t s) {
 #define WG16G(AM, BMD)                                   \
     do {                                                 \
         if (tile == 0) return wg16_go<AM, BMD, W16_0>(a, s); \
-        if (tile == 1) return wg16_go<AM, BMD, W16_1>(a, s); \
         if (tile == 2) return wg16_go<AM, BMD, W16_2>(a, s); \
-        if (tile == 3) return wg16_go<AM, BMD, W16_3>(a, s); \
-        if (tile == 4) return wg16_go<AM, BMD, W16_4>(a, s); \
         return -1;                                       \
     } while (0)
     if (a.amode == G_CONV3 && a.bmode == G_IDENT) WG16G(G_CONV3, G_IDENT);

@@ -28,16 +28,11 @@ namespace {
 // DEPTH: chunks whose global loads are in flight in registers (2 = issued two chunks before
 // their commit; costs one more stage of registers).  SWZ: unpadded, XOR-swizzled LDS rows
 // (see the kernel), 8/9 of the padded images' space.
-// PERS: persistent blocks (OCC per CU, launch_rowgemm_pipe sizes the grid) walk the tiles
-// v = blockIdx.x, + gridDim.x, ...; the next tile's first chunk is loaded under the current
-// tile's epilogue (the short-K GEMMs pay their prologue latency once per block, not per tile).
-template <int BM_, int BN_, int WM_, int WN_, int OCC_, int DEPTH_ = 1, bool SWZ_ = false,
-          bool PERS_ = false>
+template <int BM_, int BN_, int WM_, int WN_, int OCC_, int DEPTH_ = 1, bool SWZ_ = false>
 struct PipeTile {
     static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, BK = 32, OCC = OCC_;
     static constexpr int DEPTH = DEPTH_;
     static constexpr bool SWZ = SWZ_;
-    static constexpr bool PERS = PERS_;
     static constexpr int WAVES = (BM / WM) * (BN / WN);
     static constexpr int THREADS = 64 * WAVES;
 };
@@ -72,7 +67,7 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_pipe_kernel(RowGem
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave / WAVES_N, wn = wave % WAVES_N;
     const int ntn = p.N / BN;
-    const int ntiles = ((p.M + BM - 1) / BM) * ntn;  // = gridDim.x unless PERS
+    const int ntiles = ((p.M + BM - 1) / BM) * ntn;  // = gridDim.x
     const int H = p.H, W = p.W, C = p.C;
 
     // loader rows: lrow + i * RPP, 16 B (4 channels) per lane, F4R lanes per 128-B row
@@ -81,8 +76,7 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_pipe_kernel(RowGem
     unsigned aoff[AP];  // byte offset of the row's tap-0 source (+ the lane's 4 channels)
     unsigned tmask[AP]; // bit t: tap t reads inside the image (and the row is inside M)
     unsigned boff[BP];
-    // tile of virtual block v (XCD x = v % 8 keeps its contiguous tile range: gridDim.x is a
-    // multiple of 8 when PERS) and its gather offsets / tap masks
+    // tile of block v and its gather offsets / tap masks
     auto setup = [&](int v) {
         const int bid = p.xcd ? xcd_remap(v, ntiles) : v;
         tile_m = bid / ntn;
@@ -115,8 +109,7 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_pipe_kernel(RowGem
 #pragma unroll
         for (int i = 0; i < BP; ++i) boff[i] = (unsigned)((n0 + lrow + i * RPP) * p.K + lc4 * 4) * 4u;
     };
-    int vt = blockIdx.x;
-    setup(vt);
+    setup(blockIdx.x);
     const char* abytes = (const char*)(p.a + p.aoff);
 
     // one chunk's global loads, held in registers until its commit
@@ -222,7 +215,6 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_pipe_kernel(RowGem
     constexpr int D = T::DEPTH;  // chunks in flight in registers (1 or 2)
     Stage S[D];
     issue(S[0], 0);
-    for (;;) {  // tiles of this block (one unless PERS)
 #pragma unroll
     for (int i = 0; i < MT; ++i)
 #pragma unroll
@@ -295,16 +287,6 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_pipe_kernel(RowGem
         if (kc < nk) body(kc, S[1]);
     }
 
-    // PERS: the next tile's first chunk goes out before this tile's epilogue
-    const int em0 = m0, en0 = n0, etm = tile_m;
-    const int vn = vt + (int)gridDim.x;
-    const bool more = T::PERS && vn < ntiles;
-    if (more) {
-        __builtin_amdgcn_sched_barrier(0);
-        setup(vn);
-        issue(S[0], 0);
-        __builtin_amdgcn_sched_barrier(0);
-    }
     if constexpr (XP & 16) {  // keep the accumulators live: one store per lane
         float v = 0.f;
 #pragma unroll
@@ -315,11 +297,7 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_pipe_kernel(RowGem
                 for (int r = 0; r < 16; ++r) v += acc[i][j][r];
         p.out[(size_t)blockIdx.x * NTH + tid] = v;
     } else {
-        row_epilogue<EMODE, BM, BN, WM, WN>(p, acc, em0, en0, etm, wm, wn, lane, tid, smem);
-    }
-    if (!more) break;
-    vt = vn;
-    __syncthreads();  // the epilogue's LDS scratch and the last fragment reads are done
+        row_epilogue<EMODE, BM, BN, WM, WN>(p, acc, m0, n0, tile_m, wm, wn, lane, tid, smem);
     }
 }
 
@@ -327,38 +305,13 @@ using PipeTile0 = PipeTile<128, 128, 64, 64, 2>;  // 4 waves of 64x64, 74 KB LDS
 using PipeTile1 = PipeTile<128, 64, 64, 32, 2>;   // 4 waves of 64x32 (N = 64 outputs)
 using PipeTile2 = PipeTile<128, 128, 64, 64, 2, 2>;  // tile 0, loads two chunks ahead
 using PipeTile3 = PipeTile<128, 64, 64, 32, 2, 2>;
-// 8 waves of 64x64, one block per CU (110 KB LDS): the short-K ConvT GEMMs (K = 128..256),
-// where a 128x64 block re-gathered its A rows for every one of the four (a, b) column tiles
-// and paid its prologue / epilogue per 4-8 chunks of MFMAs
-using PipeTile4 = PipeTile<128, 256, 64, 64, 1>;
-using PipeTile5 = PipeTile<256, 128, 64, 64, 1>;
 // N = 64 at three blocks per CU (48 KB of LDS each): a third resident block to overlap the
-// epilogues of the short-K (576) level-0 GEMMs; 7 loads two chunks ahead
-using PipeTile6 = PipeTile<128, 64, 64, 32, 3, 1, true>;
-using PipeTile7 = PipeTile<128, 64, 64, 32, 3, 2, true>;
-// N = 64 on 64x64 wave tiles (the dominant tile's MFMA : load : ds_read ratios): 4 waves
-// stacked along M, unpadded swizzled images of 80 KB, so two blocks fill the 160 KB of a CU
-using PipeTile8 = PipeTile<256, 64, 64, 64, 2, 1, true>;
-using PipeTile9 = PipeTile<256, 64, 64, 64, 2, 2, true>;
-// persistent versions (PERS): the three-block 128x64 tiles 25 / 26 and the 128x128 tiles 16 / 18
-using PipeTile10 = PipeTile<128, 64, 64, 32, 3, 1, true, true>;
-using PipeTile11 = PipeTile<128, 64, 64, 32, 3, 2, true, true>;
-using PipeTile12 = PipeTile<128, 128, 64, 64, 2, 1, false, true>;
-using PipeTile13 = PipeTile<128, 128, 64, 64, 2, 2, false, true>;
-
-// compute units of the current device (persistent grids)
-static int device_cus() {
-    static int cus[64] = {};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-    if (!cus[dev]) {
-        int n = 0;
-        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n < 8)
-            n = 256;
-        cus[dev] = n;
-    }
-    return cus[dev];
-}
+// epilogues of the short-K (576) level-0 GEMMs; 5 loads two chunks ahead
+using PipeTile4 = PipeTile<128, 64, 64, 32, 3, 1, true>;
+using PipeTile5 = PipeTile<128, 64, 64, 32, 3, 2, true>;
+// (r02-r03, not kept: 128x256 / 256x128 eight-wave tiles for the short-K ConvT GEMMs, 256x64
+// on 64x64 wave tiles, persistent blocks walking several tiles -- 0-12 % slower or neutral,
+// DESIGN.md §3)
 
 template <int AMODE, int AOP, int EMODE, class T>
 static int pipe_go(const RowGemmArgs& a, hipStream_t s) {
@@ -366,13 +319,7 @@ static int pipe_go(const RowGemmArgs& a, hipStream_t s) {
     // span several taps -- the 128x256 tile covers all four of a 64-channel ConvT)
     if (a.N % T::BN || a.K % T::BK || a.C % T::BK) return -1;
     if (EMODE == E_CONVT && (a.cout % T::BN) && (T::BN % a.cout)) return -1;
-    const int ntiles = ((a.M + T::BM - 1) / T::BM) * (a.N / T::BN);
-    int nb = ntiles;
-    if (T::PERS) {  // OCC resident blocks per CU, a multiple of 8 (one per XCD) in all
-        const int res = (T::OCC * device_cus()) / 8 * 8;
-        if (res >= 8 && ntiles > res) nb = res;
-    }
-    const dim3 grid(nb);
+    const dim3 grid(((a.M + T::BM - 1) / T::BM) * (a.N / T::BN));
     hipLaunchKernelGGL((rowgemm_pipe_kernel<AMODE, AOP, EMODE, T>), grid, dim3(T::THREADS), 0, s, a);
     return (int)hipGetLastError();
 }
@@ -385,14 +332,6 @@ static int pipe_tile(const RowGemmArgs& a, int tile, hipStream_t s) {
     if (tile == 3) return pipe_go<AMODE, AOP, EMODE, PipeTile3>(a, s);
     if (tile == 4) return pipe_go<AMODE, AOP, EMODE, PipeTile4>(a, s);
     if (tile == 5) return pipe_go<AMODE, AOP, EMODE, PipeTile5>(a, s);
-    if (tile == 6) return pipe_go<AMODE, AOP, EMODE, PipeTile6>(a, s);
-    if (tile == 7) return pipe_go<AMODE, AOP, EMODE, PipeTile7>(a, s);
-    if (tile == 8) return pipe_go<AMODE, AOP, EMODE, PipeTile8>(a, s);
-    if (tile == 9) return pipe_go<AMODE, AOP, EMODE, PipeTile9>(a, s);
-    if (tile == 10) return pipe_go<AMODE, AOP, EMODE, PipeTile10>(a, s);
-    if (tile == 11) return pipe_go<AMODE, AOP, EMODE, PipeTile11>(a, s);
-    if (tile == 12) return pipe_go<AMODE, AOP, EMODE, PipeTile12>(a, s);
-    if (tile == 13) return pipe_go<AMODE, AOP, EMODE, PipeTile13>(a, s);
     return -1;
 }
 
@@ -408,9 +347,8 @@ int rowgemm_pipe_ok(const RowGemmArgs& a) {
     return 1;
 }
 
-// tile: 0 = 128x128, 1 = 128x64, 2 / 3 = those loading two chunks ahead, 4 = 128x256,
-// 5 = 256x128 (8 waves), 6 / 7 = 128x64 at three blocks per CU, 8 / 9 = 256x64 on 64x64
-// wave tiles at two blocks per CU, 10..13 = persistent 6 / 7 / 0 / 2
+// tile: 0 = 128x128, 1 = 128x64, 2 / 3 = those loading two chunks ahead, 4 / 5 = 128x64 at
+// three blocks per CU
 int launch_rowgemm_pipe(const RowGemmArgs& a, int tile, hipStream_t s) {
     if (!rowgemm_pipe_ok(a) || a.M < 1 || a.K != gather_taps(a.amode) * a.C) return -1;
     const bool aff = a.ascale != nullptr;

@@ -93,12 +93,11 @@ struct Options {
                                // 1 every eligible layer (default: r02 A/B, conv wgrad
                                // 27.1 -> 24.4 ms/step), 2 layers with a 64-channel operand
     int wgrad_row3_tile = -1;  // its tile (>= 20), -1 = by channel counts
-    int wgrad_row3_pipe = 0;       // row3 weight gradients on the pipelined kernel (ids 30..33)
     int wgrad_blocks = 2048;       // split-K target (blocks) of the one-tap f32 weight gradients
     int rg16_bn_k = 8192;          // rg16: E_STORE_BN GEMMs with K below this take the 128x128 tile
     int wgrad16_blocks = 1536;     // split-K target (blocks) of the bf16 weight gradients
                                    // (config 4 A/B: 1536 +1.4 % over 2048, 1024 -4.7 %)
-    int wgrad_row3_big = 21;       // row3 tile where Cin, Cout % 128 == 0 (-1 = 23 / 33)
+    int wgrad_row3_big = 21;       // row3 tile where Cin, Cout % 128 == 0 (-1 = 23)
     int wgrad_row3_blocks = 1536;  // split-K target (blocks) of the row3 weight gradients
                                    // (r02 sweep 512..2048: 1536 best, 391 vs 386 img/s)
     int wgrad_tile_w = 0;      // f32 wgrad tile, both channel counts multiples of 128
@@ -120,14 +119,10 @@ struct Options {
     int tile16_n64 = 1;
     int rg16 = 1;              // bf16 row GEMMs on the LDS-DMA kernel (0: register-staged)
     int rg16_tile = -1;        // its tile (-1 = per GEMM, rg16_tile())
-    int rg16_ra = 0;           // per-GEMM choice on the read-ahead tiles 12 / 13
     int rg16_xp = 0;           // speed-of-light ablation of the forward rg16 GEMMs (garbage
                                // results; A/B timing only, kernels_gemm16.hip XP)
-    int rg16_pp = 0;           // 256x256 GEMMs on the ping-pong kernel (tile 18)
     int rg16_r3 = 1;           // 256x256 3x3-conv GEMMs (W >= 16) on the tap-row halo kernel (tile 19;
                                // config 4: +0.9..1.2 % over three A/B pairs, r03)
-    int rg16_m16 = 0;          // per-GEMM choice on the 16x16x32-MFMA tiles: 1 = 14 / 15,
-                               // 2 = with s_setprio around the MFMAs (16 / 17)
     int wg16 = 1;              // bf16 3x3 wgrad on the LDS-DMA transposed-read kernel
     int wg16_tile = 2;         // its tile (2 = 256x256)
     int wg16t = 1;             // bf16 ConvT wgrad on the same kernel
@@ -135,47 +130,50 @@ struct Options {
     int xcd_remap = 1;         // ... f32 GEMMs: 0 none, 1 both (default: r03 PMC, HBM bytes
                                // per launch rowgemm 128x128 2.21 -> 1.00 GB, row3 wgrad
                                // 2.02 -> 0.97 GB at equal time), 2 row GEMMs, 3 wgrad
-    int wgrad_stream = 0;      // weight gradients on a second stream (bit-identical)
-    int wgrad_row3_16 = 0;     // row3 weight gradients on 16-pixel rows (tile 25)
-    int wgrad_row9 = 0;        // 64x64-channel row3 weight gradients with all three tap rows
-                               // per block (tile 26: x and dz / do, y read once, not 3x)
-    int reduce_stream = 0;     // only the split-K slab reductions + bias sums on it (bit-identical;
-                               // 1 % slower: they slow the concurrent dgrad GEMM, r03)
-    int dz_in_loaders = 0;     // BN-backward dz inside the GEMM loaders (model.py order)
     int dz_in_wgrad = 256;     // layers with Cin <= this form the BN-backward dz in the weight
                                // gradient's B' loader, which also stores it for the dgrad (no
                                // bn_dz pass; model.py order; 0 = off).  Every A'-tile row of
                                // blocks re-reads do and y instead of dz, so the fusion pays
                                // where few A' tiles share a pixel slice (profiles/
                                // r03_tile_experiments.txt: Cin 64..256 gain, 512..1024 lose)
-    int row3_gemm = 0;         // f32 3x3 forward / dgrad on the tap-row kernel
-                               // (rowgemm_row3_kernel) where its shapes allow
 };
 struct OptionDesc {
     const char* name;
     int Options::*field;
 };
+// (include/unet_hip.h lists these names; tests/test_lib_cpu.py checks the two agree)
 const OptionDesc OPTION_TABLE[] = {
-    {"wgrad_row3", &Options::wgrad_row3},       {"wgrad_row3_tile", &Options::wgrad_row3_tile},
-    {"wgrad_row3_blocks", &Options::wgrad_row3_blocks}, {"wgrad_row3_pipe", &Options::wgrad_row3_pipe},
-    {"wgrad_row3_big", &Options::wgrad_row3_big}, {"wgrad16_blocks", &Options::wgrad16_blocks},
-    {"wgrad_blocks", &Options::wgrad_blocks},   {"rg16_bn_k", &Options::rg16_bn_k},
-    {"wgrad_tile_w", &Options::wgrad_tile_w},   {"wgrad_tile_n", &Options::wgrad_tile_n},
-    {"wgrad16_tile", &Options::wgrad16_tile},   {"tile_n128", &Options::tile_n128},
-    {"tile_n128_dgrad", &Options::tile_n128_dgrad}, {"tile_n64", &Options::tile_n64},
-    {"tile_n64_dgrad", &Options::tile_n64_dgrad}, {"tile_convt64", &Options::tile_convt64},
-    {"tile_convt", &Options::tile_convt},       {"tile_n32", &Options::tile_n32},       {"tile_convt_dgrad", &Options::tile_convt_dgrad},
-    {"tile16_n128", &Options::tile16_n128},     {"tile16_n128_dgrad", &Options::tile16_n128_dgrad},
-    {"tile16_n64", &Options::tile16_n64},       {"rg16", &Options::rg16},
-    {"rg16_tile", &Options::rg16_tile},         {"rg16_ra", &Options::rg16_ra},         {"wg16", &Options::wg16},
-    {"rg16_m16", &Options::rg16_m16},         {"rg16_xp", &Options::rg16_xp},
-    {"rg16_pp", &Options::rg16_pp},           {"rg16_r3", &Options::rg16_r3},
-    {"wg16_tile", &Options::wg16_tile},         {"wg16t", &Options::wg16t},
-    {"xcd16", &Options::xcd16},                 {"xcd_remap", &Options::xcd_remap},
-    {"wgrad_stream", &Options::wgrad_stream},   {"dz_in_loaders", &Options::dz_in_loaders},
-    {"dz_in_wgrad", &Options::dz_in_wgrad},     {"reduce_stream", &Options::reduce_stream},
-    {"wgrad_row3_16", &Options::wgrad_row3_16}, {"wgrad_row9", &Options::wgrad_row9},
-    {"row3_gemm", &Options::row3_gemm},
+    {"wgrad_row3", &Options::wgrad_row3},
+    {"wgrad_row3_tile", &Options::wgrad_row3_tile},
+    {"wgrad_row3_big", &Options::wgrad_row3_big},
+    {"wgrad_row3_blocks", &Options::wgrad_row3_blocks},
+    {"wgrad_blocks", &Options::wgrad_blocks},
+    {"wgrad16_blocks", &Options::wgrad16_blocks},
+    {"wgrad_tile_w", &Options::wgrad_tile_w},
+    {"wgrad_tile_n", &Options::wgrad_tile_n},
+    {"wgrad16_tile", &Options::wgrad16_tile},
+    {"tile_n128", &Options::tile_n128},
+    {"tile_n128_dgrad", &Options::tile_n128_dgrad},
+    {"tile_n64", &Options::tile_n64},
+    {"tile_n64_dgrad", &Options::tile_n64_dgrad},
+    {"tile_n32", &Options::tile_n32},
+    {"tile_convt64", &Options::tile_convt64},
+    {"tile_convt", &Options::tile_convt},
+    {"tile_convt_dgrad", &Options::tile_convt_dgrad},
+    {"tile16_n128", &Options::tile16_n128},
+    {"tile16_n128_dgrad", &Options::tile16_n128_dgrad},
+    {"tile16_n64", &Options::tile16_n64},
+    {"rg16", &Options::rg16},
+    {"rg16_tile", &Options::rg16_tile},
+    {"rg16_bn_k", &Options::rg16_bn_k},
+    {"rg16_r3", &Options::rg16_r3},
+    {"rg16_xp", &Options::rg16_xp},
+    {"wg16", &Options::wg16},
+    {"wg16_tile", &Options::wg16_tile},
+    {"wg16t", &Options::wg16t},
+    {"xcd16", &Options::xcd16},
+    {"xcd_remap", &Options::xcd_remap},
+    {"dz_in_wgrad", &Options::dz_in_wgrad},
 };
 
 }  // namespace
@@ -216,6 +214,8 @@ struct unet_ctx {
     // buckets (DP overlap): contiguous grad ranges, ready after backward stage bucket_stage
     std::vector<int64_t> bucket_off, bucket_len;
     std::vector<int> bucket_stage;
+    std::vector<int> bucket_p0, bucket_p1;     // parameter tensors [p0, p1) of each bucket
+    std::vector<int64_t> bucket_pmax;          // ... their largest padded numel
     std::vector<hipEvent_t> bucket_ev;
     // timing
     bool timing = false;
@@ -223,10 +223,6 @@ struct unet_ctx {
     std::vector<TimeRec> trec;
     std::vector<hipEvent_t> ev_pool;
     size_t ev_used = 0;
-    // backward: weight-gradient stream (wgrad + slab reduce run beside the dgrad chain)
-    hipStream_t side = nullptr;
-    std::vector<hipEvent_t> sync_pool;
-    size_t sync_used = 0;
     Options opt;
 
     int nconv() const { return (int)conv.size(); }
@@ -480,6 +476,24 @@ void build_graph(unet_ctx* c) {
     c->bucket_off.push_back(0);
     c->bucket_len.push_back(end);
     c->bucket_stage.push_back(cur);
+    // the parameter tensors of each bucket (contiguous in arena order): a channel-padded
+    // network compacts exactly these into the caller's arena before the bucket's event
+    c->bucket_p0.assign(c->bucket_off.size(), 0);
+    c->bucket_p1.assign(c->bucket_off.size(), 0);
+    c->bucket_pmax.assign(c->bucket_off.size(), 0);
+    for (size_t b = 0; b < c->bucket_off.size(); ++b) {
+        int p0 = -1, p1 = -1;
+        for (int t = 0; t < (int)c->params.size(); ++t) {
+            const ParamT& q = c->params[t];
+            if (q.off >= c->bucket_off[b] && q.off + q.numel <= c->bucket_off[b] + c->bucket_len[b]) {
+                if (p0 < 0) p0 = t;
+                p1 = t + 1;
+                c->bucket_pmax[b] = std::max(c->bucket_pmax[b], q.pnumel);
+            }
+        }
+        c->bucket_p0[b] = p0 < 0 ? 0 : p0;
+        c->bucket_p1[b] = p1 < 0 ? 0 : p1;
+    }
 }
 
 // ------------------------------------------------------------------------------------
@@ -523,6 +537,7 @@ struct Plan {
     float* pprm;
     float* pbn;
     float* pgrad;
+    float* ugrad;  // padded network: the caller's (torch-layout) gradient arena
     PadDesc* ptab;
     PadDesc* btab;
     size_t bytes;
@@ -575,24 +590,15 @@ WgradCfg wgrad_cfg(const unet_ctx* c, int CA, int tapsA, int CB, int tapsB, int6
         const bool row3 = tapsA == 9 && tapsB == 1 && row_w > 0 && row_w % 32 == 0 &&
                           CA % 64 == 0 && CB % 64 == 0 &&
                           (r3 == 1 || (r3 == 2 && (CA == 64 || CB == 64)));
-        // 16-pixel image rows (the 16x16 bottleneck of a 256^2 input): the 128x64 row tile
-        // on 16-pixel chunks (tile 25) instead of the one-tap kernel (102 TF/s there, r03)
-        const bool row3_16 = tapsA == 9 && tapsB == 1 && r3 == 1 && c->opt.wgrad_row3_16 &&
-                             row_w == 16 && CA % 128 == 0 && CB % 64 == 0 &&
-                             !c->opt.wgrad_row3_pipe && r3t < 20;
-        if (row3_16) w.tile = 25;
         if (row3) {
             w.tile = r3t >= 20 ? r3t
-                               : (CA % 128 == 0 ? (CB % 128 == 0 ? 23 : 21) : (CB % 128 == 0 ? 22 : 20)) +
-                                     (c->opt.wgrad_row3_pipe ? 10 : 0);
+                               : (CA % 128 == 0 ? (CB % 128 == 0 ? 23 : 21) : (CB % 128 == 0 ? 22 : 20));
             // option wgrad_row3_big: the tile of the layers whose channel counts both divide
             // 128.  Default 128x64 (21) rather than 128x128 (23): the same GEMM time (126 TF/s)
             // but twice the tiles, so the 1536-block target needs half the split-K slices and
             // the slab reduction halves (r02 A/B: wgrad_reduce 1.09 -> 0.64 ms, 404 -> 408 img/s)
-            if (r3t < 20 && c->opt.wgrad_row3_big >= 20 && !c->opt.wgrad_row3_pipe &&
-                CA % 128 == 0 && CB % 128 == 0)
+            if (r3t < 20 && c->opt.wgrad_row3_big >= 20 && CA % 128 == 0 && CB % 128 == 0)
                 w.tile = c->opt.wgrad_row3_big;
-            if (w.tile == 20 && c->opt.wgrad_row9) w.tile = 26;  // same split-K partition
         }
         wgrad_tile_dims(w.tile, &w.bm, &w.bn, &w.bkp);
     }
@@ -640,13 +646,8 @@ int rg16_tile(const unet_ctx* c, const RowGemmArgs& g) {
         return g.N % bn == 0 && (cout == 0 || cout % bn == 0);
     };
     if (c->opt.rg16_tile >= 0) return fits(c->opt.rg16_tile) ? c->opt.rg16_tile : 0;
-    // option rg16_ra: the same shapes with read-ahead LDS fragments (tiles 12 / 13)
-    int t0 = c->opt.rg16_ra ? 13 : 0, t4 = c->opt.rg16_ra ? 12 : 4;
-    if (c->opt.rg16_m16) {  // option rg16_m16: the 16x16x32-MFMA tiles of the same shapes
-        t0 = c->opt.rg16_m16 == 2 ? 17 : 15;
-        t4 = c->opt.rg16_m16 == 2 ? 16 : 14;
-    }
-    if (c->opt.rg16_pp) t4 = 18;  // option rg16_pp: the ping-pong 256x256 kernel
+    const int t0 = 0;
+    int t4 = 4;
     if (c->opt.rg16_r3 && fits(19)) t4 = 19;  // option rg16_r3: the tap-row halo kernel
     if (!fits(4)) return t0;
     const int64_t blocks = (g.M + 255) / 256 * (g.N / 256);
@@ -695,7 +696,7 @@ void make_plan(unet_ctx* c, int N, int H, int W, bool training, char* base, Plan
     p.mean.assign(NC, nullptr);
     p.invstd.assign(NC, nullptr);
     p.pack = b.take<float>(c->pack_floats);
-    p.pprm = p.pbn = p.pgrad = nullptr;
+    p.pprm = p.pbn = p.pgrad = p.ugrad = nullptr;
     p.ptab = p.btab = nullptr;
     if (c->padded) {
         p.pprm = b.take<float>(c->n_pparam_floats);
@@ -886,27 +887,16 @@ std::string tlabel(const char* fam, int tile, int layer) {
     int bm = 0, bn = 0, bk = 0;
     rowgemm_tile_dims(tile, &bm, &bn, &bk);
     char b[112];
-    const int db = rowgemm_tile_dbuf(tile);  // 1 = two LDS images, 2 = pipelined, 3 = LDS-DMA
+    const int db = rowgemm_tile_dbuf(tile);  // 1 = two LDS images, 2 = pipelined
     snprintf(b, sizeof b, "%s/rowgemm_%dx%dx%d%s|%d", fam, bm, bn, bk,
-             db == 3 ? "m" : (db == 2 ? (tile >= 29 && tile <= 32 ? "q" : "p") : (db ? "d" : "")), layer);
-    return b;
-}
-
-// f32 3x3 forward / dgrad on the tap-row kernel (option row3_gemm)
-bool use_row3(const unet_ctx* c, const RowGemmArgs& g) {
-    return c->opt.row3_gemm && !c->bf16 && rowgemm_row3_ok(g);
-}
-std::string r3label(const char* fam, const RowGemmArgs& g, int layer) {
-    char b[112];
-    snprintf(b, sizeof b, "%s/rowgemm3_128x%d|%d", fam, g.N % 128 == 0 ? 128 : 64, layer);
+             db == 2 ? "p" : (db ? "d" : ""), layer);
     return b;
 }
 
 std::string wlabel(const char* fam, const WgradCfg& w, int layer) {
     char b[112];
-    snprintf(b, sizeof b, "%s/wgrad%s_%dx%dx%d|%d", fam,
-             w.tile >= 30 ? (w.tile == 34 ? "3p2" : "3p") : (w.tile == 26 ? "9" : (w.tile >= 20 ? "3" : "")),
-             w.bm, w.bn, w.bkp, layer);
+    snprintf(b, sizeof b, "%s/wgrad%s_%dx%dx%d|%d", fam, w.tile >= 20 ? "3" : "", w.bm, w.bn, w.bkp,
+             layer);
     return b;
 }
 
@@ -981,10 +971,6 @@ const float* bias_ptr(const float* prm, int64_t off) { return off >= 0 ? prm + o
 int xcd_remap_on(const unet_ctx* c) { return c->opt.xcd_remap == 1 || c->opt.xcd_remap == 2; }
 int xcd_remap_wgrad(const unet_ctx* c) { return c->opt.xcd_remap == 1 || c->opt.xcd_remap == 3; }
 
-// option wgrad_stream = 1: weight gradients on a second stream.  Off by default: measured
-// 1 % slower at bs = 32 (370 vs 374 img/s, r01 A/B) -- the GEMMs fill the chip on their
-// own, so the overlap only wins the tails back, and the ~50 cross-stream waits cost more.
-
 // weight image of a row GEMM: f32, or bf16 packed into the same slot (half its size)
 void set_weights(const unet_ctx* c, RowGemmArgs& g, const float* img) {
     g.xcd = xcd_remap_on(c);
@@ -998,7 +984,7 @@ std::string tlabel16(const char* fam, int tile, int layer) {
     int bm = 0, bn = 0, st = 0;
     rowgemm16_tile_dims(tile, &bm, &bn, &st);
     char b[112];
-    snprintf(b, sizeof b, "%s/rg16%s_%dx%ds%d|%d", fam, tile == 19 ? "r3" : tile == 18 ? "pp" : tile >= 14 ? "m" : "",
+    snprintf(b, sizeof b, "%s/rg16%s_%dx%ds%d|%d", fam, tile == 19 ? "r3" : "",
              bm, bn, st, layer);
     return b;
 }
@@ -1119,10 +1105,6 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
                 return stats_finalize(c, L, p, i, R, M, training, prm, bn_run, bn_cnt);
             }
             R = bn_groups(M);
-            if (use_row3(c, g)) {
-                RUN(r3label("conv_fwd", g, i), 2.0 * M * C.cout * 9 * C.cin, launch_rowgemm_row3(g, s));
-                return stats_finalize(c, L, p, i, R, M, training, prm, bn_run, bn_cnt);
-            }
             const int tile = pick_tile(c, C.cout, false, c->bf16);
             RUN(tlabel("conv_fwd", tile, i), 2.0 * M * C.cout * 9 * C.cin, launch_rowgemm(g, tile, s));
         }
@@ -1257,98 +1239,8 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
     Launcher L{c, s};
     const int H = p.H, W = p.W, D = c->depth, NC = c->nconv();
     int rc;
-    const bool dz_in_loaders = c->opt.dz_in_loaders && !c->bn_relu;
-
-    // Weight gradients (wgrad GEMM + slab reduce + bias sums) go to a second stream: they
-    // only read the layer input (forward buffers, never written in backward) and dz, and
-    // only write their own grads + the slabs (side-stream only), so they can run beside the
-    // dgrad chain, which fills the MFMA gaps of its bandwidth kernels (bn_dz, pool, BN
-    // finalize) and of the GEMM tails.  Ordering:
-    //  * side waits for the event after bn_dz (conv) / after the dgrad that wrote dcat (ConvT);
-    //  * a main-stream kernel that overwrites a gradient buffer first waits for the side
-    //    wgrad that read it (before_write);
-    //  * bucket events are recorded on the side stream after it joined the main stream;
-    //  * the main stream joins the side stream before returning.
-    // Off for the residual network (its skip wgrad shares the slabs on the main stream), for
-    // the loader-fused dz (the coefficients are rewritten per layer on the main stream) and
-    // when every launch is timed (a clean per-kernel breakdown needs serial launches).
-    const bool async_w = c->opt.wgrad_stream && !c->res && !dz_in_loaders &&
-                         !(c->timing && c->tfilter.empty());
-    if (async_w && !c->side &&
-        hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess)
-        return fail(c, UNET_ERR_HIP, "cannot create the weight-gradient stream");
-    hipStream_t sw = async_w ? c->side : s;
-    Launcher LW{c, sw};
-    // Option reduce_stream: only the split-K slab reductions and bias sums (small,
-    // latency-bound launches) go to the second stream, where they overlap the layer's dgrad
-    // GEMM; the next weight gradient (the next writer of the slabs) waits for them.  Bucket
-    // events are then recorded on that stream.
-    const bool async_r = !async_w && c->opt.reduce_stream && !c->res &&
-                         !(c->timing && c->tfilter.empty());
-    if (async_r && !c->side &&
-        hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess)
-        return fail(c, UNET_ERR_HIP, "cannot create the reduction stream");
-    hipStream_t sr = async_r ? c->side : sw;
-    Launcher LR{c, sr};
-    c->sync_used = 0;
-    auto sev = [&]() {
-        if (c->sync_used == c->sync_pool.size()) {
-            hipEvent_t e;
-            (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
-            c->sync_pool.push_back(e);
-        }
-        return c->sync_pool[c->sync_used++];
-    };
-    std::vector<std::pair<const void*, hipEvent_t>> readers;  // side-stream reads pending
-    auto side_after_main = [&]() {  // side waits for everything enqueued on s so far
-        if (!async_w) return;
-        hipEvent_t e = sev();
-        (void)hipEventRecord(e, s);
-        (void)hipStreamWaitEvent(sw, e, 0);
-    };
-    auto side_read = [&](const void* buf) {  // the side stream's last enqueued op reads buf
-        if (!async_w) return;
-        hipEvent_t e = sev();
-        (void)hipEventRecord(e, sw);
-        readers.emplace_back(buf, e);
-    };
-    auto before_write = [&](const void* buf) {
-        for (size_t k = 0; k < readers.size();) {
-            if (readers[k].first == buf) {
-                (void)hipStreamWaitEvent(s, readers[k].second, 0);
-                readers.erase(readers.begin() + k);
-            } else {
-                ++k;
-            }
-        }
-    };
-#define RUNW(label, flop, expr)                                    \
-    do {                                                           \
-        int rc_ = LW.run(label, flop, [&]() { return (expr); });   \
-        if (rc_) return rc_;                                       \
-    } while (0)
-#define RUNR(label, flop, expr)                                    \
-    do {                                                           \
-        int rc_ = LR.run(label, flop, [&]() { return (expr); });   \
-        if (rc_) return rc_;                                       \
-    } while (0)
-    hipEvent_t red_pending = nullptr;  // async_r: the last reduction's completion on sr
-    auto before_slab_write = [&]() {   // main-stream writers of p.slab / p.bslab
-        if (red_pending) (void)hipStreamWaitEvent(s, red_pending, 0);
-        red_pending = nullptr;
-    };
-    auto reduce_after_main = [&]() {   // sr waits for the weight gradient just enqueued on s
-        if (!async_r) return;
-        hipEvent_t e = sev();
-        (void)hipEventRecord(e, s);
-        (void)hipStreamWaitEvent(sr, e, 0);
-    };
-    auto reduce_enqueued = [&]() {
-        if (!async_r) return;
-        red_pending = sev();
-        (void)hipEventRecord(red_pending, sr);
-    };
-
+    // (weight gradients run on the same stream as the dgrad chain: a second stream measured
+    // 1 % slower, every GEMM fills the chip on its own)
     // BatchNorm backward is fused: the producer of `do` (head_bwd, a dgrad epilogue,
     // maxpool_bwd) leaves {sum do, sum do*y} column partials in p.part (do already masked by
     // the following ReLU in BN -> ReLU order); this finalize turns them into dgamma, dbeta
@@ -1369,9 +1261,8 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
                                p.invstd[i], p.coef, grads + B.g, grads + B.b, s));
         return 0;
     };
-    // dz = A do + B (y - mean) + C either as one elementwise pass over do (default) or inside the
-    // wgrad / dgrad loaders (UNET_DZ_IN_LOADERS=1, ReLU -> BN order only: fewer passes, but
-    // every 3x3 tap re-gathers both do and y -- measured slower on MI355X, kept for A/B runs)
+    // dz = A do + B (y - mean) + C as one elementwise pass over do, or (option dz_in_wgrad)
+    // inside the weight gradient's B' loader, which also stores it for the dgrad
     const int dz_mask = c->bn_relu ? 0 : 1;
     // conv i backward from do_i (dense [P][cout]).
     // dgrad -> dx (ld ldx).  bn_next: dx is the `do` of BN layer i-1 (second conv of a
@@ -1388,30 +1279,25 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
                                    C.b >= 0 ? grads + C.b : nullptr, s));
             return 0;
         }
-        const float* dzc = dz_in_loaders ? p.coef : nullptr;
         // bf16 image of dz: A operand of the LDS-DMA dgrad, B' of the LDS-DMA wgrad; the f32
         // dz is still written when the register-staged kernel of either consumes it
-        const bool dz16 = !dzc && (rg16_on(c, C.cout, C.cin) || p.x16[i]);
+        const bool dz16 = rg16_on(c, C.cout, C.cin) || p.x16[i];
         Operand a = conv_input(c, p, i);
         WgradCfg wc = wgrad_cfg(c, C.cin, 9, C.cout, 1, P, c->bf16, Wl);
         // option dz_in_wgrad: the weight gradient's B' loader forms dz from do and y (the
         // bn_dz pass disappears) and its first A'-tile blocks store it for the dgrad; f32
         // register-staged weight-gradient tiles only, model.py order, with a dgrad to feed
-        const bool dzw = p.gdz && C.cin <= c->opt.dz_in_wgrad && !dz16 && !dzc && dx && !async_w &&
-                         (wc.tile < 10 || (wc.tile >= 20 && wc.tile < 30));
+        const bool dzw = p.gdz && C.cin <= c->opt.dz_in_wgrad && !dz16 && dx &&
+                         (wc.tile < 10 || wc.tile >= 20);
         if (dzw) {
         } else if (dz16) {
             const bool f32 = !p.x16[i] || !(dx && rg16_on(c, C.cout, C.cin));
-            before_write(p.s16);
-            before_write(dout);
             RUN("bn_dz", 0, k_bn_dz16(const_cast<float*>(dout), p.y[i], p.ldy[i], p.offy[i], P, C.cout,
                                       p.coef, dz_mask, p.s16, f32 ? 1 : 0, s));
-        } else if (!dz_in_loaders) {
-            before_write(dout);
+        } else {
             RUN("bn_dz", 0, k_bn_dz(const_cast<float*>(dout), p.y[i], p.ldy[i], p.offy[i], P, C.cout,
                                     p.coef, dz_mask, s));
         }
-        side_after_main();
         WgradArgs w{};
         w.xcd = xcd_remap_wgrad(c);
         w.H = Hl;
@@ -1433,7 +1319,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         w.by = p.y[i];
         w.ldby = p.ldy[i];
         w.offby = p.offy[i];
-        w.bcoef = dzw ? p.coef : dzc;
+        w.bcoef = dzw ? p.coef : nullptr;
         w.dzout = dzw ? p.gdz : nullptr;
         w.lddz = C.cout;
         w.bias_slab = C.b >= 0 ? p.bslab : nullptr;
@@ -1443,8 +1329,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         w.splits = wc.splits;
         w.slab = p.slab;
         w.bf16 = c->bf16;
-        before_slab_write();
-        if (p.x16[i] && !dzc) {
+        if (p.x16[i]) {
             w.a = (const float*)p.x16[i];
             w.lda = C.cin;
             w.aoff = 0;
@@ -1461,21 +1346,14 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
             wgrad16g_tile_dims(t, &wbm, &wbn, &wst);
             char lb[96];
             snprintf(lb, sizeof lb, "conv_wgrad/wg16_%dx%ds%d|%d", wbm, wbn, wst, i);
-            RUNW(lb, 2.0 * P * C.cout * 9 * C.cin, launch_wgrad16(w, t, sw));
-            side_read(p.s16);
+            RUN(lb, 2.0 * P * C.cout * 9 * C.cin, launch_wgrad16(w, t, s));
         } else {
-            RUNW(wlabel("conv_wgrad", wc, i), 2.0 * P * C.cout * 9 * C.cin,
-                 launch_wgrad(w, wc.tile, sw));
+            RUN(wlabel("conv_wgrad", wc, i), 2.0 * P * C.cout * 9 * C.cin, launch_wgrad(w, wc.tile, s));
         }
-        side_read(dout);
-        reduce_after_main();
-        RUNR("wgrad_reduce", 0,
-             k_slab_reduce(p.slab, wc.splits, w.Mw, w.Nw, 0, C.cin, C.cout, grads + C.w, sr));
-        if (C.b >= 0)
-            RUNR("bias_grad", 0, k_bias_reduce(p.bslab, wc.splits, 1, C.cout, grads + C.b, sr));
-        reduce_enqueued();
+        RUN("wgrad_reduce", 0,
+            k_slab_reduce(p.slab, wc.splits, w.Mw, w.Nw, 0, C.cin, C.cout, grads + C.w, s));
+        if (C.b >= 0) RUN("bias_grad", 0, k_bias_reduce(p.bslab, wc.splits, 1, C.cout, grads + C.b, s));
         if (dx) {
-            before_write(dx);
             RowGemmArgs g{};
             g.zero16 = p.zero16;
             g.H = Hl;
@@ -1491,7 +1369,6 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
             g.ay = p.y[i];
             g.lday = p.ldy[i];
             g.offay = p.offy[i];
-            g.acoef = dzc;
             set_weights(c, g, p.pack + C.pd);
             g.out = dx;
             g.ldo = ldx;
@@ -1517,11 +1394,6 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
                 return 0;
             }
             if (rows) *rows = bn_groups(P);
-            if (use_row3(c, g)) {
-                RUN(r3label("conv_dgrad", g, i), 2.0 * P * C.cout * 9 * C.cin,
-                    launch_rowgemm_row3(g, s));
-                return 0;
-            }
             const int tile = pick_tile(c, C.cin, true, c->bf16);
             RUN(tlabel("conv_dgrad", tile, i), 2.0 * P * C.cout * 9 * C.cin, launch_rowgemm(g, tile, s));
         }
@@ -1569,13 +1441,10 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         w.slab = p.slab;
         w.bf16 = c->bf16;
         const bool t16 = p.t16[k] != nullptr;
-        before_slab_write();
         if (t16) {
             // bf16 image of the up half of the concat gradient: B' here, A of the dgrad below
-            before_write(p.s16);
             RUN("prep16", 0, k_to_bf16(p.dcat[lo], ldo, uo, T.cout, nullptr, nullptr, 0, p.P[lo],
                                        p.s16, s));
-            side_after_main();
             w.a = (const float*)p.t16[k];
             w.lda = T.cin;
             w.aoff = 0;
@@ -1592,22 +1461,16 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
             wgrad16g_tile_dims(t, &wbm, &wbn, &wst);
             char lb[96];
             snprintf(lb, sizeof lb, "convT_wgrad/wg16_%dx%ds%d|%d", wbm, wbn, wst, 100 + k);
-            RUNW(lb, 2.0 * Pin * T.cin * 4 * T.cout, launch_wgrad16(w, t, sw));
-            side_read(p.s16);
-            RUNW("bias_grad", 0, k_up2_bias_partials(p.dcat[lo], ldo, uo, Hi, Wi, Pin, T.cout, wc.pps,
-                                                     wc.splits, p.bslab, sw));
+            RUN(lb, 2.0 * Pin * T.cin * 4 * T.cout, launch_wgrad16(w, t, s));
+            RUN("bias_grad", 0, k_up2_bias_partials(p.dcat[lo], ldo, uo, Hi, Wi, Pin, T.cout, wc.pps,
+                                                    wc.splits, p.bslab, s));
         } else {
-            side_after_main();
-            RUNW(wlabel("convT_wgrad", wc, 100 + k), 2.0 * Pin * T.cin * 4 * T.cout,
-                 launch_wgrad(w, wc.tile, sw));
+            RUN(wlabel("convT_wgrad", wc, 100 + k), 2.0 * Pin * T.cin * 4 * T.cout,
+                launch_wgrad(w, wc.tile, s));
         }
-        side_read(p.dcat[lo]);
-        reduce_after_main();
-        RUNR("wgrad_reduce", 0,
-             k_slab_reduce(p.slab, wc.splits, w.Mw, w.Nw, 1, T.cin, T.cout, grads + T.w, sr));
-        RUNR("bias_grad", 0, k_bias_reduce(p.bslab, wc.splits, 4, T.cout, grads + T.b, sr));
-        reduce_enqueued();
-        before_write(dx);
+        RUN("wgrad_reduce", 0,
+            k_slab_reduce(p.slab, wc.splits, w.Mw, w.Nw, 1, T.cin, T.cout, grads + T.w, s));
+        RUN("bias_grad", 0, k_bias_reduce(p.bslab, wc.splits, 4, T.cout, grads + T.b, s));
         RowGemmArgs g{};
         g.zero16 = p.zero16;
         g.H = Hi;
@@ -1639,7 +1502,6 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         }
         if (!c->res && rg16_on(c, T.cout, T.cin)) {
             if (!t16) {
-                before_write(p.s16);
                 RUN("prep16", 0, k_to_bf16(p.dcat[lo], ldo, uo, T.cout, nullptr, nullptr, 0, p.P[lo],
                                            p.s16, s));
             }
@@ -1655,34 +1517,19 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         RUN(tlabel("convT_dgrad", tile, 100 + k), 2.0 * Pin * T.cin * 4 * T.cout, launch_rowgemm(g, tile, s));
         return 0;
     };
-    auto stage_done = [&](int st) {
-        if (c->padded) return;  // unet_backward records every bucket after the compaction
-        bool any = false;
-        for (size_t b = 0; b < c->bucket_stage.size(); ++b) any |= c->bucket_stage[b] == st;
-        if (!any) return;
-        if (async_r) {  // the stage's reductions are on sr; BN / head grads on s
-            hipEvent_t e = sev();
-            (void)hipEventRecord(e, s);
-            (void)hipStreamWaitEvent(sr, e, 0);
-            for (size_t b = 0; b < c->bucket_stage.size(); ++b)
-                if (c->bucket_stage[b] == st) (void)hipEventRecord(c->bucket_ev[b], sr);
-            return;
+    // gradient bucket b is final once stage bucket_stage[b] is done: record its event (a
+    // channel-padded network first compacts the bucket's tensors into the caller's arena,
+    // so its all-reduce can overlap the rest of the backward as well)
+    auto stage_done = [&](int st) -> int {
+        for (size_t b = 0; b < c->bucket_stage.size(); ++b) {
+            if (c->bucket_stage[b] != st) continue;
+            if (c->padded && c->bucket_p1[b] > c->bucket_p0[b])
+                RUN("pad_compact", 0,
+                    k_pad_copy(p.ptab + c->bucket_p0[b], c->bucket_p1[b] - c->bucket_p0[b],
+                               c->bucket_pmax[b], p.pgrad, p.ugrad, 0, s));
+            (void)hipEventRecord(c->bucket_ev[b], s);
         }
-        side_after_main();  // BN / head grads of the stage come from the main stream
-        for (size_t b = 0; b < c->bucket_stage.size(); ++b)
-            if (c->bucket_stage[b] == st) (void)hipEventRecord(c->bucket_ev[b], sw);
-    };
-    auto join = [&]() {
-        if (async_r) {
-            hipEvent_t e = sev();
-            (void)hipEventRecord(e, sr);
-            (void)hipStreamWaitEvent(s, e, 0);
-            return;
-        }
-        if (!async_w) return;
-        hipEvent_t e = sev();
-        (void)hipEventRecord(e, sw);
-        (void)hipStreamWaitEvent(s, e, 0);
+        return 0;
     };
 
     float* G0 = p.g[0];
@@ -1757,7 +1604,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         RUN("head_grad", 0, k_sum_partials(p.hpart, wide_g(p.P[0]), c->out_ch * c->base + c->out_ch,
                                            grads + c->head_w, s));
         if ((rc = block_bwd(2 * D, p.dcat[0], 2 * c->base))) return rc;
-        stage_done(0);
+        if ((rc = stage_done(0))) return rc;
         for (int k = D - 1; k >= 0; --k) {
             const int b = D + k;
             if ((rc = convT_bwd(k, G0, &R))) return rc;
@@ -1767,7 +1614,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
             } else if ((rc = block_bwd(b, p.g[2], c->conv[2 * b].cin))) {
                 return rc;
             }
-            stage_done(D - k);
+            if ((rc = stage_done(D - k))) return rc;
         }
         for (int b = D - 1; b >= 0; --b) {
             const int C = c->ch(b);
@@ -1776,7 +1623,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
                               nullptr, nullptr, p.N, H >> b, W >> b, C, G0, nullptr, RED_G, s));
             if ((rc = block_bwd(b, b > 0 ? p.g[2] : nullptr, b > 0 ? c->conv[2 * b].cin : 0)))
                 return rc;
-            stage_done(2 * D - b);
+            if ((rc = stage_done(2 * D - b))) return rc;
         }
         return 0;
     }
@@ -1792,7 +1639,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
     if ((rc = conv_bwd(last, G0, G1, c->base, true, &R))) return rc;
     if ((rc = bn_finalize(last - 1, R))) return rc;
     if ((rc = conv_bwd(last - 1, G1, p.dcat[0], 2 * c->base, false, nullptr))) return rc;
-    stage_done(0);
+    if ((rc = stage_done(0))) return rc;
     // ---- ConvT k, then block D+k (the block whose output it up-samples) ----
     for (int k = D - 1; k >= 0; --k) {
         const int b = D + k;
@@ -1808,7 +1655,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
             // bottleneck: its input is pool[D-1]; G0 <- d pool[D-1]
             if ((rc = conv_bwd(i0, G1, G0, c->conv[i0].cin, false, nullptr))) return rc;
         }
-        stage_done(D - k);
+        if ((rc = stage_done(D - k))) return rc;
     }
     // ---- encoders ----
     float* cur = G0;
@@ -1816,7 +1663,6 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         const int C = c->ch(b);
         const int i1 = 2 * b + 1, i0 = 2 * b;
         float* nxt = cur == G0 ? G1 : G0;
-        before_write(nxt);
         // up to 2048 blocks on the large levels (512 left the pass at ~4.7 TB/s); the partial
         // rows fit: p.part holds P/64 + 1 rows of 2C for every conv of the level
         const int Gmp = wide_g(p.P[b]);
@@ -1838,12 +1684,9 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         } else {
             if ((rc = conv_bwd(0, cur, nullptr, 0, false, nullptr))) return rc;
         }
-        stage_done(2 * D - b);
+        if ((rc = stage_done(2 * D - b))) return rc;
     }
-    join();
     return 0;
-#undef RUNW
-#undef RUNR
 }
 
 // Pillow's precompute_coeffs + normalize_coeffs_8bpc (libImaging/Resample.c) for the
@@ -1961,8 +1804,6 @@ int unet_destroy(unet_ctx* c) {
     if (!c) return UNET_ERR_INVALID;
     for (auto e : c->bucket_ev) (void)hipEventDestroy(e);
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
-    for (auto e : c->sync_pool) (void)hipEventDestroy(e);
-    if (c->side) (void)hipStreamDestroy(c->side);
     delete c;
     return UNET_OK;
     ABI_CATCH(c)
@@ -2071,13 +1912,10 @@ int unet_backward(unet_ctx* c, const float* params, const float* dlogits, float*
     const hipStream_t s = (hipStream_t)stream;
     if (!c->padded) return backward_impl(c, params, dlogits, grads, p, s);
     // narrow network: the padded parameters expanded by the forward are still in the
-    // workspace; gradients are compacted into the caller's arena, then every bucket is ready
-    int r = backward_impl(c, p.pprm, dlogits, p.pgrad, p, s);
-    if (r) return r;
-    if (k_pad_copy(p.ptab, (int)c->pad_params.size(), c->pad_max_numel, p.pgrad, grads, 0, s))
-        return fail(c, UNET_ERR_HIP, "channel-padding compact (gradients)");
-    for (auto e : c->bucket_ev) (void)hipEventRecord(e, s);
-    return UNET_OK;
+    // workspace; each bucket's gradients are compacted into the caller's arena as soon as
+    // they are final (backward_impl stage_done), then its event is recorded
+    p.ugrad = grads;
+    return backward_impl(c, p.pprm, dlogits, p.pgrad, p, s);
     ABI_CATCH(c)
 }
 
@@ -2200,6 +2038,21 @@ int unet_stream_wait_bucket(unet_ctx* c, int b, unet_stream_t stream) {
         return fail(c, UNET_ERR_HIP, "hipStreamWaitEvent");
     return UNET_OK;
     ABI_CATCH(c)
+}
+
+int unet_bucket_event(unet_ctx* c, int b, void** hip_event) {
+    ABI_TRY
+    if (!c || !hip_event || b < 0 || b >= (int)c->bucket_ev.size()) return UNET_ERR_INVALID;
+    *hip_event = (void*)c->bucket_ev[b];
+    return UNET_OK;
+    ABI_CATCH(c)
+}
+
+int unet_option_name(int i, const char** name) {
+    if (!name || i < 0 || i >= (int)(sizeof OPTION_TABLE / sizeof OPTION_TABLE[0]))
+        return UNET_ERR_INVALID;
+    *name = OPTION_TABLE[i].name;
+    return UNET_OK;
 }
 
 int unet_timing_enable(unet_ctx* c, int en) {

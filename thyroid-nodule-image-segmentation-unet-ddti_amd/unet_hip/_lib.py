@@ -80,6 +80,8 @@ SIGNATURES = {
     "unet_num_buckets": (c_int, [c_void_p, P(c_int)]),
     "unet_bucket_range": (c_int, [c_void_p, c_int, P(c_int64), P(c_int64)]),
     "unet_stream_wait_bucket": (c_int, [c_void_p, c_int, c_void_p]),
+    "unet_bucket_event": (c_int, [c_void_p, c_int, P(c_void_p)]),
+    "unet_option_name": (c_int, [c_int, P(c_char_p)]),
     "unet_debug_view": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, P(c_int64),
                                 P(c_int64), P(c_int), P(c_int)]),
     "unet_resize_plan": (c_int, [c_int, c_int, c_void_p, c_void_p, P(c_int)]),
@@ -119,6 +121,18 @@ def load():
         f.argtypes = args
     _lib = lib
     return lib
+
+
+def option_names():
+    """Every kernel-schedule option name the library accepts (unet_option_name)."""
+    lib = load()
+    out, i = [], 0
+    while True:
+        n = c_char_p()
+        if lib.unet_option_name(i, ctypes.byref(n)) != 0:
+            return out
+        out.append(n.value.decode())
+        i += 1
 
 
 def check(rc, ctx=None, what=""):

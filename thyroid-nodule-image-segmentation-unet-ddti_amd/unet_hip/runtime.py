@@ -155,6 +155,14 @@ class UNetRuntime:
         rc = self.lib.unet_stream_wait_bucket(self.ctx, b, ctypes.c_void_p(stream.cuda_stream))
         _lib.check(rc, self.ctx, "unet_stream_wait_bucket")
 
+    def bucket_event(self, b):
+        """The hipEvent_t (as an int handle) the last backward recorded for bucket b -- what a
+        caller driving RCCL without torch streams waits on (hipStreamWaitEvent)."""
+        e = ctypes.c_void_p()
+        _lib.check(self.lib.unet_bucket_event(self.ctx, b, ctypes.byref(e)), self.ctx,
+                   "unet_bucket_event")
+        return e.value
+
     # ------------------------------------------------------------------ timing
     def timing(self, enable, only=None):
         """Per-launch HIP-event timing; `only`: time just the labels containing it."""

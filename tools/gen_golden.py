@@ -54,6 +54,11 @@ Fixtures (all float64 statistics computed from fp32 results):
                     uses replica 0's running statistics.  lr0_: lr = 0 (parameters fixed, only
                     the BN buffers move: a strict pin of the buffer semantics); lr4_: lr =
                     1e-4.  Running stats, val / test logits, per-batch val losses, counts.
+  modres_dp_64.npz  nn.DataParallel training of the networks the reference CLI builds:
+                    ResUNet(64, 3) (res_, main.py:122) and mod.py UNet(64, 3) (mod_), B = 3
+                    over two replicas (shards 2 + 1), BCE + Dice of the gathered logits, two
+                    AdamW steps (lr 1e-4): logits, losses, grad norm/sum/samples, param
+                    samples, running stats per step; eval logits with replica 0's buffers.
 """
 import os
 import sys
@@ -458,6 +463,50 @@ def case_mod_narrow_64():
     np.savez_compressed(os.path.join(OUT, "mod_narrow_64.npz"), **out)
 
 
+def _build_res(base, depth, seed=42):
+    torch.manual_seed(0)
+    m = RefResUNet(1, 1, base_filters=base, depth=depth)
+    sd = m.state_dict()
+    for k, v in MO.res_make_params(seed, base, depth).items():
+        sd[k] = v.clone()
+    m.load_state_dict(sd)
+    return m
+
+
+def case_dp_modres_64():
+    """nn.DataParallel training of the two networks the reference CLI builds (main.py:122
+    ResUNet; models/mod.py:9-66 UNet), base 64, depth 3, B = 3 over two replicas (torch.chunk:
+    shards of 2 and 1), BCE + Dice on the gathered logits, gradients summed, two AdamW steps
+    (lr 1e-4), then eval with replica 0's buffers (utils/trainer.py:28-30, 81-93, 130)."""
+    out = {}
+    x = torch.from_numpy(W.make_input(17, 3, 1, 64, 64))
+    t = torch.from_numpy(W.make_target(17, 3, 64, 64))
+    for tag, m, names in (("res_", _build_res(64, 3), [n for n, _ in MO.res_bn_layers(64, 3)]),
+                          ("mod_", build_mod(64, 3), [n for n, _ in MO.bn_layers(64, 3)])):
+        m.train()
+        opt = torch.optim.AdamW(m.parameters(), lr=1e-4)
+        for s in range(2):
+            p = f"{tag}s{s}_"
+            opt.zero_grad()
+            logits = dp_forward(m, x, 2)
+            lb = torch.nn.BCEWithLogitsLoss()(logits, t)
+            ld = RefDice()(logits, t)
+            loss = lb + ld
+            loss.backward()
+            out[p + "logits"] = logits.detach().numpy()
+            out[p + "bce"], out[p + "dice"], out[p + "loss"] = lb.item(), ld.item(), loss.item()
+            grad_stats(m, p, out)
+            opt.step()
+            out[p + "params_samp"] = param_samples(m)
+            bufs = dict(m.named_buffers())
+            out[p + "running_mean"] = np.concatenate([bufs[f"{n}.running_mean"].numpy() for n in names])
+            out[p + "running_var"] = np.concatenate([bufs[f"{n}.running_var"].numpy() for n in names])
+        m.eval()
+        with torch.no_grad():
+            out[tag + "eval_logits"] = m(x).numpy()
+    np.savez_compressed(os.path.join(OUT, "modres_dp_64.npz"), **out)
+
+
 def case_mod_c4_64():
     m = build_mod(128, 5)
     m.train()
@@ -492,5 +541,6 @@ if __name__ == "__main__":
     case_dp_focal_64()
     case_mod_narrow_64()
     case_dp_eval_64()
+    case_dp_modres_64()
     for f in sorted(os.listdir(OUT)):
         print(f, os.path.getsize(os.path.join(OUT, f)))
