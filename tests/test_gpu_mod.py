@@ -253,25 +253,27 @@ def test_rg16_bit_identical_to_register_staged(tile, wtile):
 @pytest.mark.parametrize("side", [128, 512])
 def test_rg16_tile_choice_is_numerically_invisible(side):
     """BASELINE config 4's network (mod.py UNet(128, 5), bf16 MFMA), bs 2: the row-GEMM tile
-    (0 = 128x128, 2 = 256x128, 4 = 256x256, auto = the runtime's per-GEMM choice) changes
-    speed only -- one training step is bit-identical across all of them (BN partials in
-    fixed 128-row groups, gemm_common.h row_epilogue)."""
+    (0 = 128x128, 2 = 256x128, 4 = 256x256, 6 = 512x128, auto = the runtime's per-GEMM
+    choice) changes speed only -- one training step is bit-identical across all of them (BN
+    partials in fixed 128-row groups, gemm_common.h row_epilogue)."""
     x, t = inputs(29, 2, side, side)
     P = MO.make_params(31, 128, 5)
     outs = {}
-    for tile in (0, 2, 4, -1):
+    for tile in (0, 2, 4, 6, -1):
         m = _bf16_model(P, 128, 5)
         # the tap-row halo tile (19, the auto choice's 256x256 forward / dgrad since r03) sums
         # K in another order: held to the bf16 envelope by test_rg16_halo_tile_within_bf16_error
         with options(m.flatten_().rt, rg16_tile=tile, rg16_r3=0):
             outs[tile] = _bf16_step(m, x, t)
         del m
-    for tile in (2, 4, -1):
+    for tile in (2, 4, 6, -1):
         _assert_same(outs[0], outs[tile], f"{side}^2 tile {tile} vs 0")
 
 
-def test_rg16_halo_tile_within_bf16_error():
-    """Tile 19 (the tap-row halo kernel, kernels_gemm16.hip rowgemm16_row3_kernel) sums K in
+@pytest.mark.parametrize("halo", [19, 20])
+def test_rg16_halo_tile_within_bf16_error(halo):
+    """Tiles 19 / 20 (the tap-row halo kernel at 256x256 / 512x128, kernels_gemm16.hip
+    rowgemm16_row3_kernel) sum K in
     the order (tap row, channel slice, tap column) instead of the one-tap kernel's (tap,
     channel), so it is not bit-identical to tile 4.  BASELINE config 4's network at 256^2
     (halo levels W = 256 .. 16; the 8x8 bottleneck falls back to the one-tap tile), one
@@ -281,7 +283,7 @@ def test_rg16_halo_tile_within_bf16_error():
     x, t = inputs(37, 1, 256, 256)
     P = MO.make_params(41, 128, 5)
     outs = {}
-    for tile in (4, 19):
+    for tile in (4, halo):
         m = _bf16_model(P, 128, 5)
         with options(m.flatten_().rt, rg16_tile=tile):
             outs[tile] = _bf16_step(m, x, t)
@@ -293,13 +295,13 @@ def test_rg16_halo_tile_within_bf16_error():
         sd[k] = v.clone()
     m.load_state_dict(sd)
     f32 = _bf16_step(m.to(DEV).train(), x, t)
-    e_l = rel_max(outs[19][0].cpu(), outs[4][0].cpu())
+    e_l = rel_max(outs[halo][0].cpu(), outs[4][0].cpu())
     b_l = rel_max(outs[4][0].cpu(), f32[0].cpu())
     print(f"logits: halo vs one-tap {e_l:.3e}, bf16 vs fp32 {b_l:.3e}")
     assert e_l <= b_l, (e_l, b_l)
     worst = []
     for k, g4 in outs[4][1].items():
-        e = norm_rel(outs[19][1][k].cpu(), g4.cpu())
+        e = norm_rel(outs[halo][1][k].cpu(), g4.cpu())
         b = norm_rel(g4.cpu(), f32[1][k].cpu())
         worst.append((e / max(b, 1e-3), k, e, b))
     worst.sort(reverse=True)
@@ -327,7 +329,7 @@ def _bf16_oracles(base, depth):
 
 
 @pytest.mark.parametrize("base,depth,tile", [(64, 3, "4"), (128, 5, "0"), (128, 5, "2"), (128, 5, "4"),
-                                             (128, 5, "19"), (128, 5, "auto")])
+                                             (128, 5, "19"), (128, 5, "20"), (128, 5, "auto")])
 def test_mod_bf16_matches_bf16_oracle(base, depth, tile):
     """mfma_dtype="bf16": one step at B=2 64x64 vs the oracle that rounds exactly the GEMM
     operands the HIP bf16 kernels round (oracle/mod_ref_cpu.py, bf16=True).
@@ -342,7 +344,7 @@ def test_mod_bf16_matches_bf16_oracle(base, depth, tile):
     per-GEMM choice (rg16_tile, runtime.hip) and default wgrad tile."""
     import unet_hip
     opts = {} if tile == "auto" else dict(
-        rg16_tile=int(tile), wg16_tile=2 if tile in ("4", "19") else 0)
+        rg16_tile=int(tile), wg16_tile=2 if tile in ("4", "19", "20") else 0)
     P = MO.make_params(42, base, depth)
     x, t = inputs(5, 2, 64, 64)
     ref, r64, ref32 = _bf16_oracles(base, depth)

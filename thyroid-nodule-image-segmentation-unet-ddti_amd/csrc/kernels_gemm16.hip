@@ -242,18 +242,22 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm16_kernel(RowGemmAr
 //   K order: dy, 32-channel slice, dx, k -- a reordering of the one-tap kernel's sum, so
 //   results agree with the other tiles to fp32 rounding, not bitwise.
 // ------------------------------------------------------------------------------------
-template <int EMODE>
+// BM x BN block tiles: 256 x 256 (tile 19) and 512 x 128 (tile 20, the 128-output layers of
+// config 4's level 0: 8 waves of 128 x 64 either way).
+template <int EMODE, int BM, int BN>
 __global__ __launch_bounds__(512, 1) void rowgemm16_row3_kernel(RowGemmArgs p) {
-    constexpr int BM = 256, BN = 256, WM = 128, WN = 64, BK = 32, WAVES = 8, WAVES_N = 4;
+    constexpr int WM = 128, WN = 64, BK = 32, WAVES_N = BN / WN;
+    constexpr int WAVES = (BM / WM) * WAVES_N;
+    static_assert(WAVES == 8, "512 threads");
     constexpr int MT = WM / 32, NT = WN / 32;
     constexpr int RB = 2 * BK, LPR = RB / 16, RPI = 64 / LPR;  // 64-B rows, 16 rows / piece
     auto swz = [](int r) { return (r >> 2) & 3; };
-    constexpr int AR = 288;                   // halo rows held (W = 16: 16 x 18)
-    constexpr int AI = 3;                     // A pieces per wave (pieces w, w + 8, w + 16)
-    constexpr int BR = 3 * BN;                // B rows: taps dx = 0..2 x 256 outputs
-    constexpr int BI = BR / (RPI * WAVES);    // 6
+    constexpr int AR = (BM / 16) * 18;        // halo rows held (W = 16: BM / 16 rows x 18)
+    constexpr int AI = (AR / RPI + WAVES - 1) / WAVES;  // A pieces per wave (w, w + 8, ...)
+    constexpr int BR = 3 * BN;                // B rows: taps dx = 0..2 x BN outputs
+    constexpr int BI = BR / (RPI * WAVES);    // 6 / 3
     static_assert(BI * RPI * WAVES == BR && (AR / RPI) <= AI * WAVES, "loader shape");
-    constexpr int STAGE = (AR + BR) * RB;     // 66 KB
+    constexpr int STAGE = (AR + BR) * RB;     // 66 KB / 60 KB
     constexpr int SMEM = 2 * STAGE;
     static_assert(SMEM >= 2 * (BM / 64) * BN * 8, "epilogue scratch");
     __shared__ __attribute__((aligned(1024))) char smem[SMEM];
@@ -269,7 +273,7 @@ __global__ __launch_bounds__(512, 1) void rowgemm16_row3_kernel(RowGemmArgs p) {
     const int SEG = W < BM ? W : BM, HW = SEG + 2;
     const int AROWS = (BM / SEG) * HW;
     const int NA = (AROWS + RPI - 1) / RPI;           // A pieces per stage (17 or 18)
-    const bool a3 = 2 * WAVES + wave < NA;            // this wave issues a third A piece
+    const bool a3 = (AI - 1) * WAVES + wave < NA;     // this wave issues its last A piece
 
     const int lr = lane / LPR, slot = lane % LPR;
     int acen[AI], ayr[AI], ach[AI];  // pixel at dy = 1 (-1: padding), its image row, chunk
@@ -371,22 +375,24 @@ __global__ __launch_bounds__(512, 1) void rowgemm16_row3_kernel(RowGemmArgs p) {
     row_epilogue<EMODE, BM, BN, WM, WN, true>(p, acc, m0, n0, tile_m, wm, wn, lane, tid, (float*)smem);
 }
 
-template <int EMODE>
+template <int EMODE, int BM, int BN>
 static int rg16r3_go(const RowGemmArgs& a, hipStream_t s) {
-    // 256 % W == 0 or W % 256 == 0 keeps a tile on whole rows / half rows; W >= 16 bounds the halo
-    if (a.amode != G_CONV3 || a.N % 256 || a.C % 32 || a.K != 9 * a.C) return -1;
-    if (a.W < 16 || (256 % a.W && a.W % 256)) return -1;
-    const dim3 grid(((a.M + 255) / 256) * (a.N / 256));
-    hipLaunchKernelGGL((rowgemm16_row3_kernel<EMODE>), grid, dim3(512), 0, s, a);
+    // BM % W == 0 or W % BM == 0 keeps a tile on whole rows / row segments; W >= 16 bounds the halo
+    if (a.amode != G_CONV3 || a.N % BN || a.C % 32 || a.K != 9 * a.C) return -1;
+    if (a.W < 16 || (BM % a.W && a.W % BM)) return -1;
+    const dim3 grid(((a.M + BM - 1) / BM) * (a.N / BN));
+    hipLaunchKernelGGL((rowgemm16_row3_kernel<EMODE, BM, BN>), grid, dim3(512), 0, s, a);
     return (int)hipGetLastError();
 }
 
 // tiles: 0 = 128x128, 2 stages (64 KB LDS, 2 blocks/CU); 2 = 256x128, 8 waves, 2 stages
-// (96 KB); 4 = 256x256, 8 waves of 128x64, 2 stages (128 KB); 19 = the tap-row halo kernel
+// (96 KB); 4 = 256x256, 8 waves of 128x64, 2 stages (128 KB); 6 = 512x128, 8 waves of 128x64,
+// 2 stages (160 KB); 19 / 20 = the tap-row halo kernel at 256x256 / 512x128
 using T16_0 = Tile16<128, 128, 64, 64, 2, 2>;
 using T16_2 = Tile16<256, 128, 64, 64, 2, 1>;
 using T16_4 = Tile16<256, 256, 128, 64, 2, 1>;
-#define ROWGEMM16_TILES(X) X(0, T16_0) X(2, T16_2) X(4, T16_4)
+using T16_6 = Tile16<512, 128, 128, 64, 2, 1>;
+#define ROWGEMM16_TILES(X) X(0, T16_0) X(2, T16_2) X(4, T16_4) X(6, T16_6)
 
 template <int AMODE, int EMODE, class T, int XP = 0>
 static int rg16_go(const RowGemmArgs& a, hipStream_t s) {
@@ -399,8 +405,9 @@ static int rg16_go(const RowGemmArgs& a, hipStream_t s) {
 
 template <int AMODE, int EMODE>
 static int rg16_tile(const RowGemmArgs& a, int tile, hipStream_t s) {
-    if (tile == 19) {
-        if constexpr (AMODE == G_CONV3) return rg16r3_go<EMODE>(a, s);
+    if (tile == 19 || tile == 20) {
+        if constexpr (AMODE == G_CONV3)
+            return tile == 19 ? rg16r3_go<EMODE, 256, 256>(a, s) : rg16r3_go<EMODE, 512, 128>(a, s);
         return -1;
     }
 #define RG16_CASE(id, T) \
@@ -654,8 +661,9 @@ int wgrad16g_tile_dims(int tile, int* bm, int* bn, int* stages) {
 }
 
 int rowgemm16_tile_dims(int tile, int* bm, int* bn, int* stages) {
-    if (tile == 19) {  // tap-row halo 256x256
-        *bm = *bn = 256;
+    if (tile == 19 || tile == 20) {  // tap-row halo 256x256 / 512x128
+        *bm = tile == 19 ? 256 : 512;
+        *bn = tile == 19 ? 256 : 128;
         if (stages) *stages = 2;
         return 0;
     }

@@ -165,9 +165,11 @@ __device__ void block_combine(const f32x4 (&acc)[NV], int tpr, int C, float* out
 // lanes touch consecutive doubles, conflict-free (the [thread][v][j] order put lanes 32 B
 // apart, an 8-way bank conflict on every store and load: 499,712 extra LDS cycles per
 // max-pool backward launch in r02).  Same summation order as before: bit-identical.
+// Row groups: the nt / tpr complete ones (threads past them hold zeros and are not read);
+// only the first nq channel quads are written (a last pass over C / 4 > 256 quads).
 template <int NV>
 __device__ void block_combine_d(const double (&acc)[NV][4], int tpr, int C, float* out,
-                                double* smem) {
+                                double* smem, int nq = 1 << 30) {
     const int tid = threadIdx.x, nt = blockDim.x;
     const int g = tid / tpr, q = tid % tpr;
     const int groups = nt / tpr;
@@ -176,7 +178,7 @@ __device__ void block_combine_d(const double (&acc)[NV][4], int tpr, int C, floa
 #pragma unroll
         for (int j = 0; j < 4; ++j) smem[(v * 4 + j) * nt + tid] = acc[v][j];
     __syncthreads();
-    if (g == 0) {
+    if (g == 0 && q < nq) {
 #pragma unroll
         for (int v = 0; v < NV; ++v)
 #pragma unroll
@@ -429,8 +431,9 @@ __device__ __forceinline__ void maxpool_px(const float* __restrict__ y, int ld, 
     *(uint32_t*)(idx + o) = bi;
 }
 
-// Row form (C/4 divides 256 or is a multiple of it; N*H*W < 2^31): a thread keeps one
-// channel quad and its affine in registers and walks pooled pixels with 32-bit index math.
+// Row form (N*H*W < 2^31): a thread keeps one channel quad and its affine in registers and
+// walks pooled pixels with 32-bit index math (threads past the last complete row group of
+// tpr = min(C / 4, 256) idle, and so do the quads past C / 4 in a last pass).
 __global__ __launch_bounds__(256) void maxpool_bn_kernel(const float* __restrict__ y, int ld,
                                                          int off, const float* __restrict__ scale,
                                                          const float* __restrict__ shift, int relu,
@@ -442,13 +445,15 @@ __global__ __launch_bounds__(256) void maxpool_bn_kernel(const float* __restrict
     const int PO = N * Ho * Wo;
     for (int cb = 0; cb < c4n; cb += tpr) {
         const int c = 4 * (cb + (int)threadIdx.x % tpr);
-        const f32x4 sc = scale ? *(const f32x4*)(scale + c) : f32x4{1.f, 1.f, 1.f, 1.f};
-        const f32x4 sh = shift ? *(const f32x4*)(shift + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+        const bool cin = c < C;
+        const f32x4 sc = scale && cin ? *(const f32x4*)(scale + c) : f32x4{1.f, 1.f, 1.f, 1.f};
+        const f32x4 sh = shift && cin ? *(const f32x4*)(shift + c) : f32x4{0.f, 0.f, 0.f, 0.f};
         // each block walks one contiguous range of pooled pixels, the coordinates advanced
         // incrementally (no integer division per pixel)
         const int per = (PO + gridDim.x - 1) / gridDim.x;
         const int r0 = blockIdx.x * per, r1 = min(PO, r0 + per);
         const int g = (int)threadIdx.x / tpr;
+        if (g >= rpp || c >= C) continue;  // partial row group (tpr does not divide 256) / pass
         Pix at = decode(min(r0 + g, PO - 1), Ho, Wo);
         for (int po = r0 + g; po < r1; po += rpp) {
             maxpool_px(y, ld, off, sc, sh, relu, H, W, at.img, at.y, at.x, c, out, idx,
@@ -496,14 +501,17 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const float* __restric
                                                          float* __restrict__ dout, float* partial) {
     __shared__ double smem[256 * 2 * 4];
     const int Ho = H / 2, Wo = W / 2;
+    // tpr need not divide 256 (C = 96, 192, ...: the threads past the last complete row
+    // group idle) nor C / 4 (the last pass over C / 4 > 256 quads idles its upper quads)
     const int tpr = C / 4 < 256 ? C / 4 : 256, rpp = 256 / tpr;
     const int64_t PO = (int64_t)N * Ho * Wo;
     double acc[2][4];
     for (int c0 = 0; c0 < C; c0 += 4 * tpr) {
         const int q = threadIdx.x % tpr, g = threadIdx.x / tpr;
         const int c = c0 + 4 * q;
+        const bool live = g < rpp && c < C;
         f32x4 ms = {0, 0, 0, 0}, mb = ms;
-        if (mscale) {
+        if (mscale && live) {
             ms = *(const f32x4*)(mscale + c);
             mb = *(const f32x4*)(mshift + c);
         }
@@ -514,7 +522,7 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const float* __restric
         const int64_t per = (PO + gridDim.x - 1) / gridDim.x;
         const int64_t r0 = blockIdx.x * per, r1 = r0 + per < PO ? r0 + per : PO;
         Pix at = decode((int)min(r0 + g, PO - 1), Ho, Wo);  // N*H*W < 2^31 (launcher)
-        for (int64_t po = r0 + g; po < r1; po += rpp) {
+        for (int64_t po = r0 + g; live && po < r1; po += rpp) {
             const int xo = at.x, yo = at.y, img = at.img;
             pix_advance(at, rpp, Ho, Wo);
             const f32x4 gp = *(const f32x4*)(dp + po * C + c);
@@ -537,7 +545,9 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const float* __restric
                 }
             }
         }
-        if (partial) block_combine_d<2>(acc, tpr, C, partial + (int64_t)blockIdx.x * 2 * C + c0, smem);
+        if (partial)
+            block_combine_d<2>(acc, tpr, C, partial + (int64_t)blockIdx.x * 2 * C + c0, smem,
+                               (C - c0) / 4);
         __syncthreads();
     }
 }
@@ -582,13 +592,14 @@ __global__ void bn_bwd_finalize2_kernel(const float* __restrict__ part, int G, i
 
 
 // dz = A do + B (y - mean) + C in place, masked by [y > 0] when `mask` (ReLU before the BN).
-// Row form (C / 4 divides 256): each thread keeps one channel quad and its coefficients
-// in registers and walks pixel rows, so there is no per-element index division.
+// Row form (C / 4 <= 256): each thread keeps one channel quad and its coefficients in
+// registers and walks pixel rows, so there is no per-element index division.
 __global__ __launch_bounds__(256) void bn_dz_rows_kernel(float* __restrict__ d,
                                                          const float* __restrict__ y, int ld,
                                                          int off, int64_t P, int C,
                                                          const float* __restrict__ coef, int mask) {
     const int tpr = C / 4, rpp = 256 / tpr;
+    if ((int)threadIdx.x >= rpp * tpr) return;  // partial row group (tpr does not divide 256)
     const int c = (threadIdx.x % tpr) * 4;
     const f32x4 ka = *(const f32x4*)(coef + c), kb = *(const f32x4*)(coef + C + c),
                 kc = *(const f32x4*)(coef + 2 * C + c), km = *(const f32x4*)(coef + 3 * C + c);
@@ -1137,13 +1148,14 @@ __global__ __launch_bounds__(256) void res_bwd_prep_kernel(float* __restrict__ d
     for (int c0 = 0; c0 < C; c0 += 4 * tpr) {
         const int q = threadIdx.x % tpr, g = threadIdx.x / tpr;
         const int c = c0 + 4 * q;
+        const bool live = g < rpp && c < C;  // (maxpool_bwd_kernel: partial groups / passes)
 #pragma unroll
         for (int v = 0; v < 2; ++v)
 #pragma unroll
             for (int j = 0; j < 4; ++j) acc[v][j] = 0.0;
         const int64_t per = (P + gridDim.x - 1) / gridDim.x;
         const int64_t r0 = blockIdx.x * per, r1 = r0 + per < P ? r0 + per : P;
-        for (int64_t m = r0 + g; m < r1; m += rpp) {
+        for (int64_t m = r0 + g; live && m < r1; m += rpp) {
             f32x4* pd = (f32x4*)(d + m * C + c);
             f32x4 v = *pd;
             const f32x4 ov = *(const f32x4*)(out + m * ldo + offo + c);
@@ -1156,7 +1168,8 @@ __global__ __launch_bounds__(256) void res_bwd_prep_kernel(float* __restrict__ d
             }
             *pd = v;
         }
-        block_combine_d<2>(acc, tpr, C, partial + (int64_t)blockIdx.x * 2 * C + c0, smem);
+        block_combine_d<2>(acc, tpr, C, partial + (int64_t)blockIdx.x * 2 * C + c0, smem,
+                           (C - c0) / 4);
         __syncthreads();
     }
 }
@@ -1459,8 +1472,7 @@ int k_maxpool_bn(const float* y, int ld, int off, const float* scale, const floa
                  int N, int H, int W, int C, float* out, uint8_t* idx, hipStream_t s) {
     const int64_t n = (int64_t)N * (H / 2) * (W / 2) * (C / 4);
     const int c4n = C / 4;
-    if (C % 4 == 0 && (int64_t)N * H * W < (1ll << 31) &&
-        (c4n <= 256 ? 256 % c4n == 0 : c4n % 256 == 0))
+    if (C % 4 == 0 && c4n >= 1 && (int64_t)N * H * W < (1ll << 31))
         hipLaunchKernelGGL(maxpool_bn_kernel, dim3(grid_for(n)), dim3(256), 0, s, y, ld, off, scale,
                            shift, relu, N, H, W, C, out, idx);
     else
@@ -1485,7 +1497,7 @@ int k_bn_bwd_finalize2(const float* part, int G, int C, double count, const floa
 }
 int k_bn_dz(float* d, const float* y, int ld, int off, int64_t P, int C, const float* coef, int mask,
             hipStream_t s) {
-    if (C % 4 == 0 && C <= 1024 && 256 % (C / 4) == 0)
+    if (C % 4 == 0 && C >= 4 && C <= 1024)
         hipLaunchKernelGGL(bn_dz_rows_kernel, dim3(grid_for(P * (C / 4))), dim3(256), 0, s, d, y, ld,
                            off, P, C, coef, mask);
     else

@@ -121,6 +121,10 @@ struct Options {
     int rg16_tile = -1;        // its tile (-1 = per GEMM, rg16_tile())
     int rg16_xp = 0;           // speed-of-light ablation of the forward rg16 GEMMs (garbage
                                // results; A/B timing only, kernels_gemm16.hip XP)
+    int rg16_n128 = -1;        // rg16 tile of the GEMMs whose N is not a multiple of 256 (the
+                               // 128-output layers; -1 = 128x128, 6 = 512x128, 20 = 512x128 tap-row
+                               // halo for 3x3 convs, 6 elsewhere)
+    int rg16_n128_bn = 0;      // ... also for the short-K E_STORE_BN GEMMs (else 128x128)
     int rg16_r3 = 1;           // 256x256 3x3-conv GEMMs (W >= 16) on the tap-row halo kernel (tile 19;
                                // config 4: +0.9..1.2 % over three A/B pairs, r03)
     int wg16 = 1;              // bf16 3x3 wgrad on the LDS-DMA transposed-read kernel
@@ -167,6 +171,8 @@ const OptionDesc OPTION_TABLE[] = {
     {"rg16_tile", &Options::rg16_tile},
     {"rg16_bn_k", &Options::rg16_bn_k},
     {"rg16_r3", &Options::rg16_r3},
+    {"rg16_n128", &Options::rg16_n128},
+    {"rg16_n128_bn", &Options::rg16_n128_bn},
     {"rg16_xp", &Options::rg16_xp},
     {"wg16", &Options::wg16},
     {"wg16_tile", &Options::wg16_tile},
@@ -226,7 +232,8 @@ struct unet_ctx {
     Options opt;
 
     int nconv() const { return (int)conv.size(); }
-    int ch(int level) const { return base << level; }     // kernel (padded) channels
+    int chl[MAX_DEPTH + 1] = {};                           // kernel (padded) channels per level
+    int ch(int level) const { return chl[level]; }         // kernel (padded) channels
     int rch(int level) const { return rbase << level; }   // torch module channels
     int up_off(int l) const { return skip_first ? ch(l) : 0; }    // CAT_l channel offsets
     int skip_off(int l) const { return skip_first ? 0 : ch(l); }
@@ -642,14 +649,23 @@ int rg16_tile(const unet_ctx* c, const RowGemmArgs& g) {
     auto fits = [&](int t) {
         int bm = 0, bn = 0;
         if (rowgemm16_tile_dims(t, &bm, &bn) != 0) return false;
-        if (t == 19 && (g.amode != G_CONV3 || g.W < 16 || (256 % g.W && g.W % 256))) return false;
+        if ((t == 19 || t == 20) && (g.amode != G_CONV3 || g.W < 16 || (bm % g.W && g.W % bm)))
+            return false;
         return g.N % bn == 0 && (cout == 0 || cout % bn == 0);
     };
     if (c->opt.rg16_tile >= 0) return fits(c->opt.rg16_tile) ? c->opt.rg16_tile : 0;
     const int t0 = 0;
     int t4 = 4;
     if (c->opt.rg16_r3 && fits(19)) t4 = 19;  // option rg16_r3: the tap-row halo kernel
-    if (!fits(4)) return t0;
+    if (!fits(4)) {
+        // option rg16_n128: a 512-row tile for the 128-output GEMMs (halo kernel for 3x3 convs)
+        int tn = c->opt.rg16_n128;
+        if (tn == 20 && !fits(20)) tn = 6;
+        if (tn < 0 || !fits(tn)) return t0;
+        if ((g.M + 511) / 512 * (g.N / 128) < 256) return t0;
+        if (g.emode == E_STORE_BN && g.K < c->opt.rg16_bn_k && !c->opt.rg16_n128_bn) return t0;
+        return tn;
+    }
     const int64_t blocks = (g.M + 255) / 256 * (g.N / 256);
     if (blocks < 256) return t0;
     if (g.emode == E_STORE_BN && g.K < c->opt.rg16_bn_k) return t0;
@@ -984,7 +1000,7 @@ std::string tlabel16(const char* fam, int tile, int layer) {
     int bm = 0, bn = 0, st = 0;
     rowgemm16_tile_dims(tile, &bm, &bn, &st);
     char b[112];
-    snprintf(b, sizeof b, "%s/rg16%s_%dx%ds%d|%d", fam, tile == 19 ? "r3" : "",
+    snprintf(b, sizeof b, "%s/rg16%s_%dx%ds%d|%d", fam, (tile == 19 || tile == 20) ? "r3" : "",
              bm, bn, st, layer);
     return b;
 }
@@ -1769,18 +1785,29 @@ int unet_create(const unet_cfg* cfg, int device, unet_ctx** out) {
         // grid's 16 / 24 / 48, config/config.yaml; any multiple of 8 up to 256) run padded to
         // the next power of two >= 32 (unet_ctx::padded); the head's fused BN-partials path
         // handles up to 4 classes.
+        // Per level: level 0 runs the next power of two >= 32 channels (the head and
+        // first-conv kernels want a power-of-two channel-quad count), every deeper level the
+        // next multiple of 32 of base_filters << l (a K-chunk is 32 channels of one tap; the
+        // 32-column row tiles and 32-channel wgrad tiles cover 96, 192, ... natively), so
+        // base 16 pads level 0 only (16 -> 32, then 32, 64, ...: r03 padded every level 2x),
+        // base 48 level 0 only (48 -> 64, then 96, 192, ...), base 24 levels 0 and 1.
         c->rbase = c->base;
-        if (c->base >= 8 && c->base <= 256 && c->base % 8 == 0) {
-            int pb = 32;
-            while (pb < c->base) pb <<= 1;
-            c->padded = pb != c->base;
-            c->base = pb;
+        if (c->base < 8 || c->base > 256 || c->base % 8 || c->depth < 1 || c->depth > MAX_DEPTH)
+            return UNET_ERR_UNSUPPORTED;
+        c->padded = false;
+        for (int l = 0; l <= c->depth; ++l) {
+            int pc = 32;
+            if (l == 0)
+                while (pc < c->rbase) pc <<= 1;
+            else
+                pc = ((c->rbase << l) + 31) / 32 * 32;
+            c->chl[l] = pc;
+            c->padded = c->padded || pc != (c->rbase << l);
         }
+        c->base = c->chl[0];
         if ((c->variant != UNET_VARIANT_MODEL && c->variant != UNET_VARIANT_MOD &&
              c->variant != UNET_VARIANT_RES) || c->in_ch != 1 ||
-            c->out_ch < 1 || c->out_ch > 4 || c->base % 32 || c->base > 256 ||
-            (c->base & (c->base - 1)) || c->depth < 1 ||
-            c->depth > MAX_DEPTH || (c->base << c->depth) > 8192)
+            c->out_ch < 1 || c->out_ch > 4 || c->ch(c->depth) > 8192)
             return UNET_ERR_UNSUPPORTED;
         if ((c->padded || c->base < 64) && c->bf16)  // the bf16 kernels: 128-multiples of real channels
             return UNET_ERR_UNSUPPORTED;
