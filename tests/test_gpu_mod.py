@@ -270,6 +270,24 @@ def test_rg16_tile_choice_is_numerically_invisible(side):
         _assert_same(outs[0], outs[tile], f"{side}^2 tile {tile} vs 0")
 
 
+def test_wg16_tap_row_bit_identical():
+    """The tap-row bf16 weight gradient (kernels_gemm16.hip wgrad16_row3_kernel, option wg16_r3
+    = 3 / 4 LDS stages: the three dx taps of one tap row from one halo of 66 pixel rows) runs
+    the same MFMA sequence per weight element as the one-tap kernel (same operands, pixel
+    chunks, k-steps and split partition), so one training step of BASELINE config 4's network
+    at 256^2 (tap-row levels W = 256, 128, 64; the rest fall back) is bit-identical."""
+    x, t = inputs(43, 2, 256, 256)
+    P = MO.make_params(47, 128, 5)
+    outs = {}
+    for r3 in (0, 3, 4):
+        m = _bf16_model(P, 128, 5)
+        with options(m.flatten_().rt, wg16_r3=r3):
+            outs[r3] = _bf16_step(m, x, t)
+        del m
+    for r3 in (3, 4):
+        _assert_same(outs[0], outs[r3], f"wg16_r3={r3} vs one-tap")
+
+
 @pytest.mark.parametrize("halo", [19, 20])
 def test_rg16_halo_tile_within_bf16_error(halo):
     """Tiles 19 / 20 (the tap-row halo kernel at 256x256 / 512x128, kernels_gemm16.hip

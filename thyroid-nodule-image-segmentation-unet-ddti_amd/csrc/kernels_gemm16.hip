@@ -630,6 +630,194 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void wgrad16_kernel(WgradArgs p
             }
 }
 
+// ------------------------------------------------------------------------------------
+// Tap-row weight gradient (3x3 convs, W % 64 == 0): one block computes the three dx taps of
+// one tap row dy for a 128-channel (ci) x 128-channel (co) tile over its split's pixels.  A
+// 64-pixel chunk never crosses an image row (pps and W are multiples of 64), so the A'
+// operands of the three taps are the SAME 66 halo pixel rows of source row y + dy - 1
+// (columns x0 - 1 .. x0 + 64, zero outside the image), read at row offsets dx = 0, 1, 2;
+// the one-tap kernel streams a shifted copy of them per tap.  LDS stage: [68 halo rows][128
+// ci] + [64 pixel rows][128 co] bf16 (33 KB; 3 stages, one block of 8 waves per CU).  Wave
+// tile 32 (ci) x 64 (co) per tap: 6 accumulators, 10 transposed reads per 6 MFMAs.
+// Same operands, pixel chunks, k-steps and split partition as wgrad16_kernel, so every
+// element's sum is the same sequence of MFMAs: bit-identical to the one-tap tiles.
+// ------------------------------------------------------------------------------------
+template <int S>
+__global__ __launch_bounds__(512, 1) void wgrad16_row3_kernel(WgradArgs p) {
+    constexpr int BM = 128, BN = 128, WM = 32, WN = 64, BKP = 64;
+    constexpr int WAVES = 8, WAVES_N = BN / WN;  // 4 x 2 waves
+    constexpr int NT = WN / 32;
+    constexpr int RA = 2 * BM, RBB = 2 * BN;    // 256-B pixel rows
+    constexpr int LA = RA / 16, LB = RBB / 16;  // 16 lanes per row in a DMA instruction
+    constexpr int PA = 64 / LA, PB = 64 / LB;   // 4 rows per DMA instruction
+    constexpr int AROWS = BKP + 2;              // halo rows
+    constexpr int NA = (AROWS + PA - 1) / PA;   // 17 A' pieces
+    constexpr int AI = (NA + WAVES - 1) / WAVES;  // 3 (the third: wave 0 only)
+    constexpr int BI = BKP / (PB * WAVES);      // 2
+    static_assert(BI * PB * WAVES == BKP && (AI - 1) * WAVES < NA, "loader shape");
+    constexpr int AST = NA * PA * RA;           // A' bytes per stage (68 rows)
+    constexpr int STAGE = AST + BKP * RBB;
+    __shared__ __attribute__((aligned(1024))) char smem[STAGE * S];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+    const int tiles_n = p.Nw / BN, tiles_m = p.CA / BM;
+    int idx = p.xcd ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+    const int tn = idx % tiles_n;
+    idx /= tiles_n;
+    const int tm = idx % tiles_m;
+    idx /= tiles_m;
+    const int dy = idx % 3;
+    const int split = idx / 3;
+    const int ca0 = tm * BM, cb0 = tn * BN;
+    const int H = p.H, W = p.W;
+    const float rH = 1.f / (float)H, rW = 1.f / (float)W;
+    const int pbeg = split * p.pps;
+    const int pend = min(pbeg + p.pps, p.P);
+    const int nk = (pend - pbeg + BKP - 1) / BKP;
+    const bool a3 = (AI - 1) * WAVES + wave < NA;  // this wave issues a third A' piece
+
+    const int lra = lane / LA, lrb = lane / LB;
+    const uint16_t* a16 = (const uint16_t*)p.a;
+    const uint16_t* b16 = (const uint16_t*)p.b;
+    const uint16_t* zero = (const uint16_t*)p.zero16;
+
+    auto issue = [&](int kc, int st) {
+        const int pc = pbeg + kc * BKP;  // first output pixel of the chunk (one image row)
+        const Pix q = decode_fast(pc, H, W, rH, rW);
+        const int yy = q.y + dy - 1;
+        const bool rowok = yy >= 0 && yy < H;
+        const int srow = (q.img * H + yy) * W;  // source row's first pixel (when rowok)
+        char* base = smem + st * STAGE;
+#pragma unroll
+        for (int j = 0; j < AI; ++j) {
+            if (j == AI - 1 && !a3) continue;
+            const int row = (j * WAVES + wave) * PA + lra;  // halo row: column x0 - 1 + row
+            const int gcha = ((lane % LA) ^ ((row & 3) << 2)) * 8;
+            const int xx = q.x - 1 + row;
+            const bool ok = rowok && row < AROWS && xx >= 0 && xx < W;
+            const uint16_t* g = ok ? a16 + (size_t)(srow + xx) * p.lda + ca0 + gcha : zero;
+            glds16(g, base + (j * WAVES + wave) * 1024);
+        }
+#pragma unroll
+        for (int j = 0; j < BI; ++j) {
+            const int row = (j * WAVES + wave) * PB + lrb;
+            const int gchb = ((lane % LB) ^ ((row & 3) << 2)) * 8;
+            const int pix = pc + row;
+            const uint16_t* g = pix < pend ? b16 + (size_t)pix * p.ldb + cb0 + gchb : zero;
+            glds16(g, base + AST + (j * WAVES + wave) * 1024);
+        }
+    };
+
+    f32x16 acc[3][NT];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    // transposed reads (wgrad16_kernel's addressing): lane l of group g = l / 16 supplies row
+    // 8 (g >> 1) + qq (+ 4 t + 16 kk, + dx for tap dx), columns 16 (g & 1) + 4 pp
+    const int g = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
+    int aoff[3], boff[NT];
+#pragma unroll
+    for (int dx = 0; dx < 3; ++dx) {
+        const int row = 8 * (g >> 1) + qq + dx;  // (row & 3) == ((qq + dx) & 3) for every kk, t
+        const int col = wm * WM + 16 * (g & 1) + 4 * pp;
+        aoff[dx] = row * RA + (((col >> 3) ^ ((row & 3) << 2)) << 4) + ((col >> 2) & 1) * 8;
+    }
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+        const int row = 8 * (g >> 1) + qq;
+        const int col = wn * WN + nt * 32 + 16 * (g & 1) + 4 * pp;
+        boff[nt] = AST + row * RBB + (((col >> 3) ^ (qq << 2)) << 4) + ((col >> 2) & 1) * 8;
+    }
+
+#pragma unroll
+    for (int s = 0; s < S - 1; ++s)
+        if (s < nk) issue(s, s);
+    for (int kc = 0; kc < nk; ++kc) {
+        if (kc + S - 1 < nk) issue(kc + S - 1, (kc + S - 1) % S);
+        const int ahead = min(S - 1, nk - 1 - kc);
+        // this wave's pieces per chunk: AI + BI (a3) or AI - 1 + BI
+        if (a3) {
+            constexpr int G = AI + BI;
+            if (ahead >= 3) wait_vm<3 * G>();
+            else if (ahead == 2) wait_vm<2 * G>();
+            else if (ahead == 1) wait_vm<G>();
+            else wait_vm<0>();
+        } else {
+            constexpr int G = AI - 1 + BI;
+            if (ahead >= 3) wait_vm<3 * G>();
+            else if (ahead == 2) wait_vm<2 * G>();
+            else if (ahead == 1) wait_vm<G>();
+            else wait_vm<0>();
+        }
+        block_barrier();
+        const unsigned sb = lds_u32(smem) + (kc % S) * STAGE;
+        short4v fa[2][3][2], fb[2][NT][2];
+        auto load = [&](auto KK) {
+            constexpr int kk = decltype(KK)::value, set = kk & 1;
+#pragma unroll
+            for (int dx = 0; dx < 3; ++dx) {
+                fa[set][dx][0] = ds_tr16<kk * 16 * RA>(sb + aoff[dx]);
+                fa[set][dx][1] = ds_tr16<kk * 16 * RA + 4 * RA>(sb + aoff[dx]);
+            }
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) {
+                fb[set][nt][0] = ds_tr16<kk * 16 * RBB>(sb + boff[nt]);
+                fb[set][nt][1] = ds_tr16<kk * 16 * RBB + 4 * RBB>(sb + boff[nt]);
+            }
+        };
+        auto mma = [&](auto KK) {
+            constexpr int set = decltype(KK)::value & 1;
+#pragma unroll
+            for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt)
+                    acc[dx][nt] = mfma32_bf16(*(const bf16x8*)fa[set][dx], *(const bf16x8*)fb[set][nt],
+                                              acc[dx][nt]);
+        };
+        static_assert(BKP == 64, "four k-steps per chunk");
+        constexpr int RD = 2 * (3 + NT);  // reads per k-step
+        load(std::integral_constant<int, 0>{});
+        load(std::integral_constant<int, 1>{});
+        asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(RD) : "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        mma(std::integral_constant<int, 0>{});
+        __builtin_amdgcn_sched_barrier(0);
+        load(std::integral_constant<int, 2>{});
+        asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(RD) : "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        mma(std::integral_constant<int, 1>{});
+        __builtin_amdgcn_sched_barrier(0);
+        load(std::integral_constant<int, 3>{});
+        asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(RD) : "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        mma(std::integral_constant<int, 2>{});
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        mma(std::integral_constant<int, 3>{});
+        block_barrier();
+    }
+
+    const int li = lane & 31, lh = lane >> 5;
+    float* slab = p.slab + (size_t)split * p.Mw * p.Nw;
+#pragma unroll
+    for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = (3 * dy + dx) * p.CA + ca0 + wm * WM + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                const int n = cb0 + wn * WN + nt * 32 + li;
+                slab[(size_t)m * p.Nw + n] = acc[dx][nt][r];
+            }
+}
+
 // wgrad16 tiles: 0 = 128x128, 64 pixels per stage, 2 stages (64 KB, 2 blocks/CU);
 // 2 = 256x256, 8 waves of 128x64, 2 stages (128 KB, 1 block/CU)
 // (r01-r02, not kept: 3-stage 128x128, 256x128 / 128x256 at 3 stages)
@@ -648,6 +836,11 @@ static int wg16_go(const WgradArgs& a, hipStream_t s) {
 }  // namespace
 
 int wgrad16g_tile_dims(int tile, int* bm, int* bn, int* stages) {
+    if (tile == 3 || tile == 4) {  // tap-row: 128 x 128 per tap, three taps per block
+        *bm = *bn = 128;
+        if (stages) *stages = tile;
+        return 0;
+    }
 #define WG16_DIMS(id, T)          \
     if (tile == id) {             \
         *bm = T::BM;              \
@@ -708,6 +901,17 @@ int launch_rowgemm16(const RowGemmArgs& a, int tile, hipStream_t s) {
 // 3x3 conv (A' G_CONV3, B' G_IDENT) and ConvT (A' G_IDENT, B' G_UP2); no bias column sums.
 int launch_wgrad16(const WgradArgs& a, int tile, hipStream_t s) {
     if (a.aoff || a.boff || a.ascale || a.bcoef || a.bias_slab || !a.zero16 || a.P < 1) return -1;
+    if (tile == 3 || tile == 4) {  // tap-row kernel (3 / 4 LDS stages): 3x3 conv layers, W % 64 == 0
+        if (a.amode != G_CONV3 || a.bmode != G_IDENT || a.Mw != 9 * a.CA || a.Nw != a.CB ||
+            a.CA % 128 || a.CB % 128 || a.W % 64 || a.pps % 64)
+            return -1;
+        const dim3 grid((a.CA / 128) * 3 * (a.Nw / 128) * a.splits);
+        if (tile == 3)
+            hipLaunchKernelGGL((wgrad16_row3_kernel<3>), grid, dim3(512), 0, s, a);
+        else
+            hipLaunchKernelGGL((wgrad16_row3_kernel<4>), grid, dim3(512), 0, s, a);
+        return (int)hipGetLastError();
+    }
 #define WG16G(AM, BMD)                                   \
     do {                                                 \
         if (tile == 0) return wg16_go<AM, BMD, W16_0>(a, s); \

@@ -214,29 +214,43 @@ __global__ __launch_bounds__(256) void conv_first_fwd_kernel(const float* __rest
     const int per = (P + gridDim.x - 1) / gridDim.x;
     const int r0 = blockIdx.x * per;
     const int r1 = min(P, r0 + per);
-    // pixel coordinates walked incrementally (m advances by rpp): no integer division per pixel
-    Pix at = decode(min(r0 + g, P - 1), H, W);
-    for (int m = r0 + g; m < r1; m += rpp) {
-        const int xx = at.x, yy = at.y, img = at.img;
-        pix_advance(at, rpp, H, W);
-        float xv[9];
+    // U pixels per trip (m, m + rpp, ..., their 9 U image loads issued together), pixel
+    // coordinates walked incrementally: no integer division per pixel.  Each thread still sums
+    // its pixels in increasing m, so the partials are those of one pixel per trip.
+    constexpr int U = 4;
+    Pix at[U];
 #pragma unroll
-        for (int tap = 0; tap < 9; ++tap) {
-            const int sy = yy + tap / 3 - 1, sx = xx + tap % 3 - 1;
-            const bool ok = sy >= 0 && sy < H && sx >= 0 && sx < W;
-            xv[tap] = ok ? x[((int64_t)img * H + sy) * W + sx] : 0.f;
+    for (int u = 0; u < U; ++u) {
+        at[u] = decode(min(r0 + g, P - 1), H, W);
+        pix_advance(at[u], u * rpp, H, W);
+    }
+    for (int m0 = r0 + g; m0 < r1; m0 += U * rpp) {
+        float xv[U][9];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int tap = 0; tap < 9; ++tap) {
+                const int sy = at[u].y + tap / 3 - 1, sx = at[u].x + tap % 3 - 1;
+                const bool ok = sy >= 0 && sy < H && sx >= 0 && sx < W && m0 + u * rpp < r1;
+                xv[u][tap] = ok ? x[((int64_t)at[u].img * H + sy) * W + sx] : 0.f;
+            }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int m = m0 + u * rpp;
+            pix_advance(at[u], U * rpp, H, W);
+            if (m >= r1) continue;
+            f32x4 o;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                float s = 0.f;
+#pragma unroll
+                for (int tap = 0; tap < 9; ++tap) s = fmaf(xv[u][tap], wr[j][tap], s);
+                o[j] = relu ? fmaxf(s + b[j], 0.f) : s + b[j];
+            }
+            __builtin_nontemporal_store(o, (f32x4*)(y + (int64_t)m * C + 4 * q));
+            acc[0] += o;
+            acc[1] += o * o;
         }
-        f32x4 o;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            float s = 0.f;
-#pragma unroll
-            for (int tap = 0; tap < 9; ++tap) s = fmaf(xv[tap], wr[j][tap], s);
-            o[j] = relu ? fmaxf(s + b[j], 0.f) : s + b[j];
-        }
-        *(f32x4*)(y + (int64_t)m * C + 4 * q) = o;
-        acc[0] += o;
-        acc[1] += o * o;
     }
     block_combine<2>(acc, tpr, C, partial + (int64_t)blockIdx.x * 2 * C, smem);
 }
@@ -1017,26 +1031,41 @@ __global__ void head_fwd_kernel(const float* __restrict__ y, int C, const float*
                                 const float* __restrict__ b, int O, int P, int HW,
                                 float* __restrict__ logits) {
     const int lpp = C / 4;  // lanes per pixel (C == 64 -> 16)
-    // 32-bit index math (P * lpp < 2^31: the launcher's thread count)
+    // U pixels per thread, strided by the grid's pixel count (their loads issued together:
+    // a one-pixel thread left too few bytes in flight, 3.8 TB/s); 32-bit index math
+    // (P * lpp < 2^31: the launcher's thread count)
+    constexpr int U = 4;
     const int gt = blockIdx.x * blockDim.x + threadIdx.x;
-    const int pix = gt / lpp;
-    const int q = gt - pix * lpp;
-    const bool ok = pix < P;
-    f32x4 v = {0, 0, 0, 0};
-    if (ok) {
-        v = *(const f32x4*)(y + (int64_t)pix * C + 4 * q);
-        if (scale) v = v * *(const f32x4*)(scale + 4 * q) + *(const f32x4*)(shift + 4 * q);
-    }
-    if (relu)
+    const int pix0 = gt / lpp;
+    const int q = gt - pix0 * lpp;
+    const int stride = gridDim.x * (blockDim.x / lpp);  // pixels per grid sweep
+    const f32x4 sc = scale ? *(const f32x4*)(scale + 4 * q) : f32x4{1.f, 1.f, 1.f, 1.f};
+    const f32x4 sh = scale ? *(const f32x4*)(shift + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int pb = pix0; pb < P; pb += U * stride) {
+        f32x4 v[U];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
-    for (int o = 0; o < O; ++o) {
-        const f32x4 wv = *(const f32x4*)(w + o * C + 4 * q);
-        float s = v[0] * wv[0] + v[1] * wv[1] + v[2] * wv[2] + v[3] * wv[3];
-        for (int d = lpp / 2; d >= 1; d >>= 1) s += __shfl_xor(s, d);
-        if (ok && q == 0) {
-            const int img = pix / HW, hw = pix - img * HW;
-            logits[((int64_t)img * O + o) * HW + hw] = s + b[o];
+        for (int u = 0; u < U; ++u) {
+            const int pix = pb + u * stride;
+            v[u] = pix < P ? __builtin_nontemporal_load((const f32x4*)(y + (int64_t)pix * C + 4 * q))
+                           : f32x4{0, 0, 0, 0};
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int pix = pb + u * stride;
+            f32x4 a = v[u];
+            if (scale) a = a * sc + sh;
+            if (relu)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) a[j] = fmaxf(a[j], 0.f);
+            for (int o = 0; o < O; ++o) {
+                const f32x4 wv = *(const f32x4*)(w + o * C + 4 * q);
+                float s = a[0] * wv[0] + a[1] * wv[1] + a[2] * wv[2] + a[3] * wv[3];
+                for (int d = lpp / 2; d >= 1; d >>= 1) s += __shfl_xor(s, d);
+                if (pix < P && q == 0) {
+                    const int img = pix / HW, hw = pix - img * HW;
+                    logits[((int64_t)img * O + o) * HW + hw] = s + b[o];
+                }
+            }
         }
     }
 }
@@ -1597,7 +1626,8 @@ int k_head_fwd(const float* y, int C, const float* scale, const float* shift, in
     if (C % 4 || C / 4 > 64 || (C / 4 & (C / 4 - 1))) return -1;  // lanes per pixel: pow2 <= 64
     const int64_t threads = (int64_t)P * (C / 4);
     if (threads + 255 >= (1ll << 31)) return -1;  // the kernel's 32-bit thread index
-    hipLaunchKernelGGL(head_fwd_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, y,
+    // 4 pixels per thread (head_fwd_kernel U), at most 8192 blocks (a grid-stride remainder)
+    hipLaunchKernelGGL(head_fwd_kernel, dim3(grid_for((threads + 3) / 4)), dim3(256), 0, s, y,
                        C, scale, shift, relu, w, b, O, P, HW, logits);
     LAUNCH_CHECK();
 }

@@ -129,6 +129,8 @@ struct Options {
                                // config 4: +0.9..1.2 % over three A/B pairs, r03)
     int wg16 = 1;              // bf16 3x3 wgrad on the LDS-DMA transposed-read kernel
     int wg16_tile = 2;         // its tile (2 = 256x256)
+    int wg16_r3 = 0;           // 3x3 layers with W % 64 == 0 on the tap-row bf16 weight gradient
+                               // (tile 3 / 4 = three / four LDS stages; 0 = off)
     int wg16t = 1;             // bf16 ConvT wgrad on the same kernel
     int xcd16 = 1;             // XCD-contiguous block order, LDS-DMA kernels
     int xcd_remap = 1;         // ... f32 GEMMs: 0 none, 1 both (default: r03 PMC, HBM bytes
@@ -176,6 +178,7 @@ const OptionDesc OPTION_TABLE[] = {
     {"rg16_xp", &Options::rg16_xp},
     {"wg16", &Options::wg16},
     {"wg16_tile", &Options::wg16_tile},
+    {"wg16_r3", &Options::wg16_r3},
     {"wg16t", &Options::wg16t},
     {"xcd16", &Options::xcd16},
     {"xcd_remap", &Options::xcd_remap},
@@ -1357,11 +1360,17 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
             w.zero16 = p.zero16;
             w.xcd = xcd16_on(c);
             // (the split count, sized for >= 2048 128x128 tiles, gives >= 512 256x256 ones)
-            const int t = wg16_tile(c, C.cin, C.cout);
+            int t = wg16_tile(c, C.cin, C.cout);
+            // option wg16_r3: the tap-row kernel (three taps per block from one halo row)
+            const int r3 = c->opt.wg16_r3;
+            if ((r3 == 3 || r3 == 4) && Wl % 64 == 0 && C.cin % 128 == 0 && C.cout % 128 == 0 &&
+                wc.pps % 64 == 0)
+                t = r3;
             int wbm = 0, wbn = 0, wst = 0;
             wgrad16g_tile_dims(t, &wbm, &wbn, &wst);
             char lb[96];
-            snprintf(lb, sizeof lb, "conv_wgrad/wg16_%dx%ds%d|%d", wbm, wbn, wst, i);
+            snprintf(lb, sizeof lb, "conv_wgrad/wg16%s_%dx%ds%d|%d", t == 3 || t == 4 ? "r3" : "", wbm,
+                     wbn, wst, i);
             RUN(lb, 2.0 * P * C.cout * 9 * C.cin, launch_wgrad16(w, t, s));
         } else {
             RUN(wlabel("conv_wgrad", wc, i), 2.0 * P * C.cout * 9 * C.cin, launch_wgrad(w, wc.tile, s));
