@@ -270,6 +270,22 @@ def test_rg16_tile_choice_is_numerically_invisible(side):
         _assert_same(outs[0], outs[tile], f"{side}^2 tile {tile} vs 0")
 
 
+def test_convt16_bit_identical():
+    """Option convt16 (default on): in a bf16 training step the ConvT forward stores bf16 of
+    its output straight into the decoder conv's kept operand image (the same RNE rounding of
+    the same f32 value k_to_bf16 applies) and that conv's prep pass converts the skip half
+    only.  BASELINE config 4's network, one step at 128^2: bit-identical to convt16 = 0."""
+    x, t = inputs(53, 2, 128, 128)
+    P = MO.make_params(59, 128, 5)
+    outs = {}
+    for flag in (0, 1):
+        m = _bf16_model(P, 128, 5)
+        with options(m.flatten_().rt, convt16=flag):
+            outs[flag] = _bf16_step(m, x, t)
+        del m
+    _assert_same(outs[0], outs[1], "convt16")
+
+
 def test_wg16_tap_row_bit_identical():
     """The tap-row bf16 weight gradient (kernels_gemm16.hip wgrad16_row3_kernel, option wg16_r3
     = 3 / 4 LDS stages: the three dx taps of one tap row from one halo of 66 pixel rows) runs

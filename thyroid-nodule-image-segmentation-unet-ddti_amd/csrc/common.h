@@ -87,6 +87,8 @@ struct RowGemmArgs {
     int xcd;              // remap blocks so each XCD gets a contiguous range of tiles
     const uint16_t* a16;  // rowgemm16: A as a dense bf16 image [pixels][lda] (prepared operand)
     const void* zero16;   // rowgemm16: >= 16 zero bytes (padding taps / rows past M)
+    uint16_t* out16;      // E_CONVT: store bf16(result) into this image (ld ldo, offset ooff)
+                          // instead of f32 into out (the bf16 consumer's operand image)
 };
 
 struct WgradArgs {

@@ -328,9 +328,16 @@ __device__ __forceinline__ void row_epilogue(const RowGemmArgs& p, f32x16 (&acc)
                 if (m >= p.M) continue;
                 const Pix q = decode_fast(m, H, W, rH, rW);
                 const size_t ob = (size_t)(q.img * 2 * H + 2 * q.y) * (2 * W) + 2 * q.x;
+                if (p.out16) {  // bf16 straight into the consumer's operand image (RNE, as k_to_bf16)
 #pragma unroll
-                for (int nt = 0; nt < NT; ++nt)
-                    p.out[(ob + coff[nt]) * p.ldo + p.ooff + co_[nt]] = acc[mt][nt][r] + bb[nt];
+                    for (int nt = 0; nt < NT; ++nt)
+                        ((__bf16*)p.out16)[(ob + coff[nt]) * p.ldo + p.ooff + co_[nt]] =
+                            (__bf16)(acc[mt][nt][r] + bb[nt]);
+                } else {
+#pragma unroll
+                    for (int nt = 0; nt < NT; ++nt)
+                        p.out[(ob + coff[nt]) * p.ldo + p.ooff + co_[nt]] = acc[mt][nt][r] + bb[nt];
+                }
             }
     } else if constexpr (EMODE == E_RESID || EMODE == E_ADD) {
 #pragma unroll

@@ -42,9 +42,10 @@ int k_bn_bwd_finalize2(const float* part, int G, int C, double count, const floa
                        float* dbeta, hipStream_t s);
 int k_bn_dz(float* d, const float* y, int ld, int off, int64_t P, int C, const float* coef, int mask,
             hipStream_t s);
-// dense bf16 image [P][C] of op(src) for the LDS-DMA GEMMs (affine if scale, ReLU on c < relu)
+// bf16 image [P][dld] (dld 0 = C: dense) of op(src), channels [0, C), for the LDS-DMA GEMMs
+// (affine if scale, ReLU on c < relu)
 int k_to_bf16(const float* src, int ld, int off, int C, const float* scale, const float* shift,
-              int relu, int64_t P, uint16_t* dst, hipStream_t s);
+              int relu, int64_t P, uint16_t* dst, hipStream_t s, int dld = 0);
 // bn_dz writing the dense bf16 image of dz (and the f32 dz in place when f32 != 0)
 int k_bn_dz16(float* d, const float* y, int ld, int off, int64_t P, int C, const float* coef,
               int mask, uint16_t* dz16, int f32, hipStream_t s);

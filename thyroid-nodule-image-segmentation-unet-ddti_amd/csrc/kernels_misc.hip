@@ -714,7 +714,8 @@ __global__ void bn_dz_kernel(float* __restrict__ d, const float* __restrict__ y,
 __global__ __launch_bounds__(256) void to_bf16_kernel(const float* __restrict__ src, int ld, int off,
                                                       int C, const float* __restrict__ scale,
                                                       const float* __restrict__ shift, int relu,
-                                                      int64_t P, int tpr, __bf16* __restrict__ dst) {
+                                                      int64_t P, int tpr, __bf16* __restrict__ dst,
+                                                      int dld) {
     typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
     constexpr int U = 4;  // rows per thread per trip: 8 independent 16-B loads in flight
     const int rpp = 256 / tpr;
@@ -761,7 +762,7 @@ __global__ __launch_bounds__(256) void to_bf16_kernel(const float* __restrict__ 
                     o[j] = (__bf16)v0[j];
                     o[4 + j] = (__bf16)v1[j];
                 }
-                *(bf16x8*)(dst + m * C + c) = o;
+                *(bf16x8*)(dst + m * dld + c) = o;
             }
         }
     }
@@ -1535,13 +1536,15 @@ int k_bn_dz(float* d, const float* y, int ld, int off, int64_t P, int C, const f
     LAUNCH_CHECK();
 }
 int k_to_bf16(const float* src, int ld, int off, int C, const float* scale, const float* shift,
-              int relu, int64_t P, uint16_t* dst, hipStream_t s) {
-    if (C % 8 || ld % 4 || off % 4 || (scale == nullptr) != (shift == nullptr)) return -1;
+              int relu, int64_t P, uint16_t* dst, hipStream_t s, int dld) {
+    if (dld == 0) dld = C;
+    if (C % 8 || ld % 4 || off % 4 || dld % 8 || dld < C || (scale == nullptr) != (shift == nullptr))
+        return -1;
     const int c8 = C / 8;
     const int tpr = c8 >= 256 ? 256 : c8;
     if (256 % tpr || (c8 > 256 && c8 % 256)) return -1;
     hipLaunchKernelGGL(to_bf16_kernel, dim3(grid_for((P + 3) / 4 * tpr)), dim3(256), 0, s, src, ld, off, C,
-                       scale, shift, relu, P, tpr, (__bf16*)dst);
+                       scale, shift, relu, P, tpr, (__bf16*)dst, dld);
     LAUNCH_CHECK();
 }
 int k_bn_dz16(float* d, const float* y, int ld, int off, int64_t P, int C, const float* coef,

@@ -129,6 +129,9 @@ struct Options {
                                // config 4: +0.9..1.2 % over three A/B pairs, r03)
     int wg16 = 1;              // bf16 3x3 wgrad on the LDS-DMA transposed-read kernel
     int wg16_tile = 2;         // its tile (2 = 256x256)
+    int convt16 = 1;           // bf16 training: the ConvT forward stores the up half of the
+                               // decoder's concat straight into that conv's bf16 operand image
+                               // (no f32 up half; its prep pass converts the skip half only)
     int wg16_r3 = 0;           // 3x3 layers with W % 64 == 0 on the tap-row bf16 weight gradient
                                // (tile 3 / 4 = three / four LDS stages; 0 = off)
     int wg16t = 1;             // bf16 ConvT wgrad on the same kernel
@@ -179,6 +182,7 @@ const OptionDesc OPTION_TABLE[] = {
     {"wg16", &Options::wg16},
     {"wg16_tile", &Options::wg16_tile},
     {"wg16_r3", &Options::wg16_r3},
+    {"convt16", &Options::convt16},
     {"wg16t", &Options::wg16t},
     {"xcd16", &Options::xcd16},
     {"xcd_remap", &Options::xcd_remap},
@@ -1075,6 +1079,8 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
     RUN("copy_x", 0, (int)hipMemcpyAsync(p.x_nhwc, x, sizeof(float) * p.P[0] * c->in_ch,
                                          hipMemcpyDeviceToDevice, s));
     const float* xin = p.x_nhwc;
+    // decoder convs whose operand image already holds the ConvT's up half (option convt16)
+    std::vector<char> up16(NC, 0);
 
     auto conv = [&](int i) -> int {
         const ConvL& C = c->conv[i];
@@ -1112,8 +1118,14 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
             g.emode = c->bn_relu ? E_STATS : E_BIAS_RELU_STATS;
             if (rg16_on(c, C.cin, C.cout)) {
                 uint16_t* img = p.x16[i] ? p.x16[i] : p.s16;
-                RUN("prep16", 0, k_to_bf16(a.ptr, a.ld, a.off, C.cin, a.scale, a.shift, a.relu, M,
-                                           img, s));
+                if (up16[i]) {  // the ConvT stored the up half already: convert the skip half
+                    const int l = C.level, so = c->skip_off(l);
+                    RUN("prep16", 0, k_to_bf16(a.ptr, a.ld, a.off + so, c->ch(l), a.scale + so,
+                                               a.shift + so, a.relu, M, img + so, s, C.cin));
+                } else {
+                    RUN("prep16", 0, k_to_bf16(a.ptr, a.ld, a.off, C.cin, a.scale, a.shift, a.relu, M,
+                                               img, s));
+                }
                 use_a16(c, p, g, C.cin);
                 g.a16 = img;
                 const int tile = rg16_tile(c, g);
@@ -1167,6 +1179,14 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
                                        img, s));
             use_a16(c, p, g, T.cin);
             g.a16 = img;
+            // option convt16: the up half goes to the decoder conv's kept bf16 image (the only
+            // reader of that half in a bf16 training step; skip-first concat, identity affine)
+            const int idec = 2 * (D + 1 + k);
+            const ConvL& Cd = c->conv[idec];
+            if (c->opt.convt16 && c->skip_first && p.x16[idec] && rg16_on(c, Cd.cin, Cd.cout)) {
+                g.out16 = p.x16[idec];
+                up16[idec] = true;
+            }
             const int tile = rg16_tile(c, g);
             RUN(tlabel16("convT_fwd", tile, 100 + k), 2.0 * g.M * g.N * g.K,
                 launch_rowgemm16(g, tile, s));
