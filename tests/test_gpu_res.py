@@ -147,3 +147,40 @@ def test_res_narrow_b16_matches_golden(golden_dir):
         n = p.grad.detach().double().norm().item()
         assert abs(n - f["r16_grad_norm"][ti]) <= GRAD_TOL * f["r16_grad_norm"][ti], name
     check_eval(m, MO.make_res_forward(3), x.cpu(), t.cpu())
+
+
+def _f32_step(m, x, t):
+    import unet_hip
+    logits = m(x.to(DEV))
+    losses = unet_hip.seg_losses(logits, t.to(DEV))
+    (losses[0] + losses[1]).backward()
+    torch.cuda.synchronize()
+    return (logits.detach().clone(),
+            {k: p.grad.detach().clone() for k, p in m.named_parameters()},
+            {k: b.detach().clone() for k, b in m.named_buffers()})
+
+
+@pytest.mark.parametrize("net", ["res", "mod"])
+def test_n32_direct_tile_bit_identical(net):
+    """The 32-output row GEMMs of a base-32 level 0 (forward, dgrad incl. the BN-partials and
+    residual-add epilogues, 1x1 skip, ConvT with 32 outputs per tap) on tile 15
+    (kernels_gemm.hip rowgemm_n32_kernel: operands straight from global memory into the MFMA
+    registers) against the LDS-staged tile 14: same K order and MFMA sequence per element,
+    same epilogue, so one training step is bit-identical (ResUNet and mod.py UNet, base 32)."""
+    from _helpers import hip_mod_model, options
+    x, t = inputs(61, 2, 128, 128)
+    outs = {}
+    for tile in (14, 15):
+        if net == "res":
+            m = _model(MO.res_make_params(67, 32, 3), 32, 3)
+        else:
+            m = hip_mod_model(MO.make_params(67, 32, 3), DEV, 32, 3)
+        with options(m.flatten_().rt, tile_n32=tile):
+            outs[tile] = _f32_step(m, x, t)
+        del m
+    a, b = outs[14], outs[15]
+    assert torch.equal(a[0], b[0]), "logits"
+    for k, g in a[1].items():
+        assert torch.equal(g, b[1][k]), f"grad {k}"
+    for k, v in a[2].items():
+        assert torch.equal(v, b[2][k]), f"buffer {k}"

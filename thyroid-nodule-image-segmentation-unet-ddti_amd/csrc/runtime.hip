@@ -912,7 +912,7 @@ std::string tlabel(const char* fam, int tile, int layer) {
     char b[112];
     const int db = rowgemm_tile_dbuf(tile);  // 1 = two LDS images, 2 = pipelined
     snprintf(b, sizeof b, "%s/rowgemm_%dx%dx%d%s|%d", fam, bm, bn, bk,
-             db == 2 ? "p" : (db ? "d" : ""), layer);
+             db == 3 ? "g" : db == 2 ? "p" : (db ? "d" : ""), layer);
     return b;
 }
 

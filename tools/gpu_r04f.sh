@@ -4,7 +4,7 @@ set -u
 cd $GRAFT_REPO_ROOT
 TAG=${1:-r04f}
 timeout -k 10 700 python -u -m pytest -x -v --timeout 300 --timeout-method thread -p no:cacheprovider \
-  tests/test_gpu_res.py "tests/test_gpu_mod.py" -k "narrow or res or rg16_tile_choice or halo or bf16_oracle or tap_row or convt16 or register_staged" \
+  tests/test_gpu_res.py "tests/test_gpu_mod.py" -k "narrow or res or rg16_tile_choice or halo or bf16_oracle or tap_row or convt16 or register_staged or n32" \
   > gpurun_out/$TAG.pytest.log 2>&1
 rc=$?
 echo "pytest rc=$rc"; grep -E "passed|failed" gpurun_out/$TAG.pytest.log | tail -3
@@ -23,4 +23,5 @@ run c4base --config 4 --mfma bf16 && run c4r3 --config 4 --mfma bf16 --opt wg16_
   run c4n20 --config 4 --mfma bf16 --opt rg16_n128=20 && \
   run c4n20bn --config 4 --mfma bf16 --opt rg16_n128=20 --opt rg16_n128_bn=1 && \
   run res16 --config res --base 16 --depth 4 && run res32 --config res --base 32 --depth 4 && \
-  run res48 --config res --base 48 --depth 4 && run c2 --steps 10
+  run res48 --config res --base 48 --depth 4 && run res32t15 --config res --base 32 --depth 4 --opt tile_n32=15 && \
+  run res32t13 --config res --base 32 --depth 4 --opt tile_n32=13 && run res16t15 --config res --base 16 --depth 4 --opt tile_n32=15 && run c2 --steps 10
