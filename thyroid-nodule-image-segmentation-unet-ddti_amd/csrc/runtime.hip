@@ -109,7 +109,9 @@ struct Options {
     int tile_n64_dgrad = 25;   // ... N = 64, dgrad-type (pipelined 128x64 at three blocks per
                                // CU: level-0 dgrads 1.50-1.55 -> 1.40-1.45 ms, r03)
     int tile_convt64 = 1;      // ConvT forward with 64 output channels (grid N = 256)
-    int tile_n32 = 14;         // f32 row GEMMs with 32 outputs (256 x 32, 4 waves)
+    int tile_n32 = 15;         // f32 row GEMMs with 32 outputs: 15 = 256 x 32 with operands
+                               // straight from global memory (r04, ResUNet(32, 4) 263 -> 282
+                               // img/s, (16, 4) 419 -> 478), 14 = the LDS-staged 256 x 32
     int tile_convt = -1;       // ConvT forward, >= 128 output channels (-1 = tile_n128's)
     int tile_convt_dgrad = 26; // ConvT input gradient (-1 = tile_n128_dgrad's; 26 = pipelined
                                // 128x64 at three blocks per CU: the K = 4 Cout short-K GEMMs
@@ -121,9 +123,10 @@ struct Options {
     int rg16_tile = -1;        // its tile (-1 = per GEMM, rg16_tile())
     int rg16_xp = 0;           // speed-of-light ablation of the forward rg16 GEMMs (garbage
                                // results; A/B timing only, kernels_gemm16.hip XP)
-    int rg16_n128 = -1;        // rg16 tile of the GEMMs whose N is not a multiple of 256 (the
+    int rg16_n128 = 20;        // rg16 tile of the GEMMs whose N is not a multiple of 256 (the
                                // 128-output layers; -1 = 128x128, 6 = 512x128, 20 = 512x128 tap-row
-                               // halo for 3x3 convs, 6 elsewhere)
+                               // halo for 3x3 convs, 6 elsewhere; r04 config 4: 122.7 -> 124.8
+                               // img/s with 20, 121.9 with 6)
     int rg16_n128_bn = 0;      // ... also for the short-K E_STORE_BN GEMMs (else 128x128)
     int rg16_r3 = 1;           // 256x256 3x3-conv GEMMs (W >= 16) on the tap-row halo kernel (tile 19;
                                // config 4: +0.9..1.2 % over three A/B pairs, r03)
@@ -132,8 +135,9 @@ struct Options {
     int convt16 = 1;           // bf16 training: the ConvT forward stores the up half of the
                                // decoder's concat straight into that conv's bf16 operand image
                                // (no f32 up half; its prep pass converts the skip half only)
-    int wg16_r3 = 0;           // 3x3 layers with W % 64 == 0 on the tap-row bf16 weight gradient
-                               // (tile 3 / 4 = three / four LDS stages; 0 = off)
+    int wg16_r3 = 4;           // 3x3 layers with W % 64 == 0 on the tap-row bf16 weight gradient
+                               // (tile 3 / 4 = three / four LDS stages; 0 = off; r04 config 4:
+                               // 122.7 -> 124.5 / 125.2 img/s)
     int wg16t = 1;             // bf16 ConvT wgrad on the same kernel
     int xcd16 = 1;             // XCD-contiguous block order, LDS-DMA kernels
     int xcd_remap = 1;         // ... f32 GEMMs: 0 none, 1 both (default: r03 PMC, HBM bytes
