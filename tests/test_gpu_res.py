@@ -160,25 +160,33 @@ def _f32_step(m, x, t):
             {k: b.detach().clone() for k, b in m.named_buffers()})
 
 
-@pytest.mark.parametrize("net", ["res", "mod"])
-def test_n32_direct_tile_bit_identical(net):
-    """The 32-output row GEMMs of a base-32 level 0 (forward, dgrad incl. the BN-partials and
-    residual-add epilogues, 1x1 skip, ConvT with 32 outputs per tap) on tile 15
-    (kernels_gemm.hip rowgemm_n32_kernel: operands straight from global memory into the MFMA
-    registers) against the LDS-staged tile 14: same K order and MFMA sequence per element,
-    same epilogue, so one training step is bit-identical (ResUNet and mod.py UNet, base 32)."""
+@pytest.mark.parametrize("net,base,ref,alt", [
+    ("res", 32, dict(tile_n32=14), dict(tile_n32=15)),
+    ("mod", 32, dict(tile_n32=14), dict(tile_n32=15)),
+    ("res", 32, dict(tile_n32=14), dict(tile_n32=29)),
+    ("mod", 32, dict(tile_n64=19, tile_n64_dgrad=25), dict(tile_n64=27, tile_n64_dgrad=27)),
+    ("res", 48, dict(tile_n96=-1, tile_n32=14), dict(tile_n96=28)),
+    ("mod", 48, dict(tile_n96=-1, tile_n32=14), dict(tile_n96=28)),
+])
+def test_direct_tiles_bit_identical(net, base, ref, alt):
+    """Row GEMMs on the direct-from-global tiles (kernels_gemm.hip rowgemm_direct_kernel:
+    15 / 29 = 32 outputs, 27 = 64, 28 = 96; MFMA operands straight from global memory into
+    registers) against the LDS-staged tiles (14 = 256 x 32, 19 / 25 = the pipelined 128 x 64,
+    three 32-column tiles for 96 outputs): same K order and MFMA sequence per element, same
+    epilogues (forward BN statistics, dgrad BN partials, residual add, 1x1 skip, ConvT), so
+    one training step of a ResUNet / mod.py UNet at that width is bit-identical."""
     from _helpers import hip_mod_model, options
     x, t = inputs(61, 2, 128, 128)
-    outs = {}
-    for tile in (14, 15):
+    outs = []
+    for opts in (ref, alt):
         if net == "res":
-            m = _model(MO.res_make_params(67, 32, 3), 32, 3)
+            m = _model(MO.res_make_params(67, base, 3), base, 3)
         else:
-            m = hip_mod_model(MO.make_params(67, 32, 3), DEV, 32, 3)
-        with options(m.flatten_().rt, tile_n32=tile):
-            outs[tile] = _f32_step(m, x, t)
+            m = hip_mod_model(MO.make_params(67, base, 3), DEV, base, 3)
+        with options(m.flatten_().rt, **opts):
+            outs.append(_f32_step(m, x, t))
         del m
-    a, b = outs[14], outs[15]
+    a, b = outs
     assert torch.equal(a[0], b[0]), "logits"
     for k, g in a[1].items():
         assert torch.equal(g, b[1][k]), f"grad {k}"

@@ -248,22 +248,24 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_kernel(RowGemmArgs
 }
 
 // ------------------------------------------------------------------------------------
-// Skinny row GEMM (N = 32 outputs: the narrow networks' level 0; tile 15).  With a 32-column
-// block tile every A row feeds exactly one wave, so staging A through LDS (tile 14) bought no
-// reuse and held the CU to one 83-KB block of four waves.  Here every MFMA operand comes from
-// global memory straight into registers, in the layout tile 14 reads from LDS (lane half h
+// Skinny row GEMMs (N = 32 / 64 / 96 outputs: the narrow networks' level 0 and the 96-channel
+// levels of base 24 / 48; tiles 15, 27, 28).  With one wave per 64-row band holding the whole
+// N, every A row feeds exactly one wave, so staging A through LDS (tile 14) bought no reuse
+// and held the CU to one 83-KB block of four waves.  Here every MFMA operand comes from
+// global memory straight into registers, in the layout the LDS-staged tiles read (lane half h
 // owns k = 4h..4h+3 of each 8-k group: one dwordx4 of A per accumulator row band and one of
-// Bt, which every wave of the CU shares through L1), one 32-k chunk loaded ahead of the
-// MFMAs.  No LDS in the main loop and no barriers: the four waves of a block run
-// independently, several blocks per CU.  Same K order, same MFMA sequence per element and
-// the same epilogue as tile 14: bit-identical results.
+// Bt per 32 columns, which every wave of the CU shares through L1), one chunk of GK 8-k
+// groups loaded ahead of the MFMAs.  No LDS in the main loop and no barriers: the four waves
+// of a block run independently, several blocks per CU.  Same K order, same MFMA sequence per
+// element and the same epilogue as the LDS-staged tiles: bit-identical results.
 // ------------------------------------------------------------------------------------
-template <int AMODE, int AOP, int EMODE>
-__global__ __launch_bounds__(256, 2) void rowgemm_n32_kernel(RowGemmArgs p) {
+template <int AMODE, int AOP, int EMODE, int NT, int GK, int OCC>
+__global__ __launch_bounds__(256, OCC) void rowgemm_direct_kernel(RowGemmArgs p) {
     constexpr bool AFFINE = AOP == OP_AFFINE || AOP == OP_AFFINE_RELU;
     constexpr bool ARELU = AOP == OP_AFFINE_RELU;
     static_assert(AOP != OP_DZ, "plain / affine A operands only");
-    constexpr int BM = 256, BN = 32, WM = 64, WN = 32, MT = 2, GK = 4;  // GK 8-k groups / chunk
+    static_assert(GK == 1 || GK == 2 || GK == 4, "a chunk is 8, 16 or 32 k of one tap");
+    constexpr int BM = 256, BN = 32 * NT, WM = 64, WN = BN, MT = 2, KC = 8 * GK;
     constexpr int CMAX = 256;  // affine operands: per-channel scale / shift staged in LDS
     __shared__ __attribute__((aligned(16))) float smem[(BM / 64) * 2 * BN * 2];  // epilogue
     __shared__ __attribute__((aligned(16))) float aff[AFFINE ? 2 * CMAX : 4];
@@ -294,15 +296,15 @@ __global__ __launch_bounds__(256, 2) void rowgemm_n32_kernel(RowGemmArgs p) {
     }
     const float* brow = p.bt + (size_t)(n0 + li) * p.K + 4 * lh;
 
-    // chunk kc = one tap x 32 channels: A[mt][g], Bt[g] for its four 8-k groups
+    // chunk kc = KC k of one tap: A[mt][g], Bt[nt][g] for its GK 8-k groups
     struct Chunk {
-        f32x4 a[MT][GK], b[GK];
+        f32x4 a[MT][GK], b[NT][GK];
         int c0;  // the lane's first channel (affine lookup)
         unsigned vmask;
         bool relu;
     };
     auto load = [&](int kc, Chunk& ch) {
-        const int k0 = kc * 32;
+        const int k0 = kc * KC;
         const int tap = k0 / C;
         const int c0 = k0 - tap * C + 4 * lh;
         ch.vmask = 0;
@@ -316,16 +318,22 @@ __global__ __launch_bounds__(256, 2) void rowgemm_n32_kernel(RowGemmArgs p) {
             for (int g = 0; g < GK; ++g) ch.a[mt][g] = *(const f32x4*)(ar + 8 * g);
         }
 #pragma unroll
-        for (int g = 0; g < GK; ++g) ch.b[g] = *(const f32x4*)(brow + k0 + 8 * g);
+        for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+            for (int g = 0; g < GK; ++g)
+                ch.b[nt][g] = *(const f32x4*)(brow + (size_t)nt * 32 * p.K + k0 + 8 * g);
         ch.c0 = c0;
-        if constexpr (ARELU) ch.relu = c0 - 4 * lh < p.arelu;  // a chunk lies in one half
+        // (the ReLU span is a multiple of 32 channels: a chunk lies in one half of a concat)
+        if constexpr (ARELU) ch.relu = c0 - 4 * lh < p.arelu;
     };
 
-    f32x16 acc[MT][1];
+    f32x16 acc[MT][NT];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc[mt][0][r] = 0.f;
+        for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[mt][nt][r] = 0.f;
 
     auto compute = [&](const Chunk& ch) {
 #pragma unroll
@@ -347,14 +355,18 @@ __global__ __launch_bounds__(256, 2) void rowgemm_n32_kernel(RowGemmArgs p) {
                 if (!((ch.vmask >> mt) & 1u)) v = f32x4{0.f, 0.f, 0.f, 0.f};
                 av[mt] = v;
             }
+            // the LDS-staged tiles' order per accumulator: k-steps st = 0..3 of each group
 #pragma unroll
             for (int st = 0; st < 4; ++st)
 #pragma unroll
-                for (int mt = 0; mt < MT; ++mt) acc[mt][0] = mfma32(av[mt][st], ch.b[g][st], acc[mt][0]);
+                for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                    for (int nt = 0; nt < NT; ++nt)
+                        acc[mt][nt] = mfma32(av[mt][st], ch.b[nt][g][st], acc[mt][nt]);
         }
     };
     // two register sets, one chunk ahead (unrolled by two: no set copies)
-    const int nk = p.K / 32;
+    const int nk = p.K / KC;
     Chunk c0, c1;
     load(0, c0);
     for (int kc = 0; kc < nk; kc += 2) {
@@ -367,6 +379,204 @@ __global__ __launch_bounds__(256, 2) void rowgemm_n32_kernel(RowGemmArgs p) {
     row_epilogue<EMODE, BM, BN, WM, WN>(p, acc, m0, n0, tile_m, wave, 0, lane, tid, smem);
 }
 
+
+// ------------------------------------------------------------------------------------
+// Weight-gradient GEMM (reduction over pixels), same issue / compute / commit pipeline.
+// ------------------------------------------------------------------------------------
+// wgrad tile: block BM x BN, wave tile WM x WN, pixels per chunk BKP.
+template <int BM_, int BN_, int WM_, int WN_, int BKP_, int OCC_ = 1>
+struct WgTile {
+    static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, BKP = BKP_;
+    static constexpr int THREADS = 64 * (BM / WM) * (BN / WN);
+    static constexpr int OCC = OCC_;
+};
+
+template <int AMODE, int AOP, int BMODE, bool BDZ, class T>
+__global__ __launch_bounds__(T::THREADS, T::OCC) void wgrad_kernel(WgradArgs p) {
+    constexpr bool AFFINE = AOP == OP_AFFINE || AOP == OP_AFFINE_RELU;
+    constexpr bool ARELU = AOP == OP_AFFINE_RELU;
+    constexpr int BM = T::BM, BN = T::BN, BKP = T::BKP, WM = T::WM, WN = T::WN;
+    constexpr int NTH = T::THREADS;
+    constexpr int WAVES_N = BN / WN;
+    constexpr int LDA = BM + 4, LDB = BN + 4;
+    constexpr int MT = WM / 32, NT = WN / 32;
+    constexpr int AF = BM / 4, BF = BN / 4;          // float4 per pixel row
+    constexpr int ARPP = NTH / AF, BRPP = NTH / BF;  // rows per pass
+    constexpr int AP = BKP / ARPP, BP = BKP / BRPP;
+    static_assert(AP * ARPP == BKP && BP * BRPP == BKP, "loader shape");
+    __shared__ __attribute__((aligned(16))) float As[BKP * LDA];
+    __shared__ __attribute__((aligned(16))) float Bs[BKP * LDB];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+    const int tiles_n = p.Nw / BN, tiles_m = p.Mw / BM;
+    int idx = p.xcd ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+    const int tn = idx % tiles_n;
+    idx /= tiles_n;
+    const int tm = idx % tiles_m;
+    const int split = idx / tiles_m;
+    const int tapA = (tm * BM) / p.CA, ca0 = tm * BM - tapA * p.CA;
+    const int tapB = (tn * BN) / p.CB, cb0 = tn * BN - tapB * p.CB;
+    const int H = p.H, W = p.W;
+    const float rH = 1.f / (float)H, rW = 1.f / (float)W;
+
+    const int ac4 = tid % AF, arow = tid / AF;
+    const int bc4 = tid % BF, brow = tid / BF;
+    f32x4 sc = {1.f, 1.f, 1.f, 1.f}, sh = {0.f, 0.f, 0.f, 0.f};
+    bool arl = false;
+    if constexpr (AFFINE) {
+        sc = *(const f32x4*)(p.ascale + ca0 + ac4 * 4);
+        sh = *(const f32x4*)(p.ashift + ca0 + ac4 * 4);
+        if constexpr (ARELU) arl = ca0 + ac4 * 4 < p.arelu;
+    }
+
+    f32x4 ca = {0, 0, 0, 0}, cb = ca, cc = ca, cm = ca;  // OP_DZ coefficients of this thread's columns
+    if constexpr (BDZ) {
+        ca = *(const f32x4*)(p.bcoef + cb0 + bc4 * 4);
+        cb = *(const f32x4*)(p.bcoef + p.CB + cb0 + bc4 * 4);
+        cc = *(const f32x4*)(p.bcoef + 2 * p.CB + cb0 + bc4 * 4);
+        cm = *(const f32x4*)(p.bcoef + 3 * p.CB + cb0 + bc4 * 4);
+    }
+    const bool bsum = p.bias_slab != nullptr && tm == 0;
+    double bacc[4] = {0.0, 0.0, 0.0, 0.0};  // f64: the bias gradient is a small sum of +/- terms
+
+    const int pbeg = split * p.pps;
+    int pend = pbeg + p.pps;
+    if (pend > p.P) pend = p.P;
+    const int nchunks = (pend - pbeg + BKP - 1) / BKP;
+
+    f32x4 ryb[BDZ ? BP : 1];
+    int bm_row[BDZ ? BP : 1];
+    const bool dzw = BDZ && p.dzout != nullptr && tm == 0 && BMODE == G_IDENT;
+    f32x4 ra[AP], rb[BP];
+    unsigned amask = 0, bmask = 0;
+    auto issue = [&](int pc) {
+        amask = bmask = 0;
+#pragma unroll
+        for (int i = 0; i < AP; ++i) {
+            int m = pc + arow + i * ARPP;
+            const bool in = m < pend;
+            m = in ? m : pend - 1;
+            bool valid;
+            const Pix q = AMODE == G_IDENT ? Pix{0, 0, 0} : decode_fast(m, H, W, rH, rW);
+            const int src = gather_src<AMODE>(tapA, m, q, H, W, valid);
+            amask |= (valid && in) ? (1u << i) : 0u;
+            ra[i] = *(const f32x4*)(p.a + (size_t)src * p.lda + p.aoff + ca0 + ac4 * 4);
+        }
+#pragma unroll
+        for (int i = 0; i < BP; ++i) {
+            int m = pc + brow + i * BRPP;
+            const bool in = m < pend;
+            m = in ? m : pend - 1;
+            bool valid;
+            const Pix q = BMODE == G_IDENT ? Pix{0, 0, 0} : decode_fast(m, H, W, rH, rW);
+            const int src = gather_src<BMODE>(tapB, m, q, H, W, valid);
+            bmask |= (valid && in) ? (1u << i) : 0u;
+            rb[i] = *(const f32x4*)(p.b + (size_t)src * p.ldb + p.boff + cb0 + bc4 * 4);
+            if constexpr (BDZ) {
+                ryb[i] = *(const f32x4*)(p.by + (size_t)src * p.ldby + p.offby + cb0 + bc4 * 4);
+                bm_row[i] = src;
+            }
+        }
+    };
+    auto commit = [&]() {
+#pragma unroll
+        for (int i = 0; i < AP; ++i) {
+            f32x4 v = ra[i];
+            if constexpr (AFFINE) {
+                v = v * sc + sh;
+                if (ARELU && arl)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
+            }
+            if (!((amask >> i) & 1u)) v = f32x4{0.f, 0.f, 0.f, 0.f};
+            *(f32x4*)&As[(arow + i * ARPP) * LDA + ac4 * 4] = v;
+        }
+#pragma unroll
+        for (int i = 0; i < BP; ++i) {
+            f32x4 v = rb[i];
+            if constexpr (BDZ) {
+                const f32x4 d = bn_dz4(ca, v, cb, ryb[i], cm, cc);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) v[j] = ryb[i][j] > 0.f ? d[j] : 0.f;
+                // the first A' tile's blocks (tap 0, channels 0..BM) hand dz to the dgrad
+                if (dzw && ((bmask >> i) & 1u))
+                    *(f32x4*)(p.dzout + (size_t)bm_row[i] * p.lddz + cb0 + bc4 * 4) = v;
+            }
+            if (!((bmask >> i) & 1u)) v = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (bsum)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) bacc[j] += v[j];
+            *(f32x4*)&Bs[(brow + i * BRPP) * LDB + bc4 * 4] = v;
+        }
+    };
+
+    f32x16 acc[MT][NT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    const int li = lane & 31, lh = lane >> 5;
+    if (nchunks > 0) {
+        issue(pbeg);
+        commit();
+        __syncthreads();
+    }
+    for (int c = 0; c < nchunks; ++c) {
+        if (c + 1 < nchunks) issue(pbeg + (c + 1) * BKP);
+#pragma unroll
+        for (int kk = 0; kk < BKP / 8; ++kk)
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const int pr = kk * 8 + lh * 4 + s;
+                float af[MT], bf[NT];
+#pragma unroll
+                for (int mt = 0; mt < MT; ++mt) af[mt] = As[pr * LDA + wm * WM + mt * 32 + li];
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt) bf[nt] = Bs[pr * LDB + wn * WN + nt * 32 + li];
+#pragma unroll
+                for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                    for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma32(af[mt], bf[nt], acc[mt][nt]);
+            }
+        __syncthreads();
+        if (c + 1 < nchunks) {
+            commit();
+            __syncthreads();
+        }
+    }
+
+    if (bsum) {  // column sums of B' for the bias gradient: combine the row groups in order
+        __syncthreads();
+        double* red = (double*)As;  // [NTH][4]; As holds >= BKP*LDA floats >= 8*NTH
+#pragma unroll
+        for (int j = 0; j < 4; ++j) red[tid * 4 + j] = bacc[j];
+        __syncthreads();
+        if (tid < BF) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                double t = 0.0;
+                for (int g = 0; g < BRPP; ++g) t += red[(g * BF + tid) * 4 + j];
+                p.bias_slab[(size_t)split * p.Nw + tn * BN + tid * 4 + j] = (float)t;
+            }
+        }
+    }
+
+    float* slab = p.slab + (size_t)split * p.Mw * p.Nw;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = tm * BM + wm * WM + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                const int n = tn * BN + wn * WN + nt * 32 + li;
+                slab[(size_t)m * p.Nw + n] = acc[mt][nt][r];
+            }
+}
 
 // ------------------------------------------------------------------------------------
 // Weight gradient of a 3x3 conv, one ROW of taps per block (dy fixed, dx = 0..2).
@@ -846,223 +1056,34 @@ static int rowgemm_go(const RowGemmArgs& a, hipStream_t s) {
     }
 }
 
-template <int AMODE, int AOP, int EMODE>
-static int rowgemm_n32_go(const RowGemmArgs& a, hipStream_t s) {
+// tiles 15 = 256x32 (32-k chunks, two waves per SIMD), 29 = 256x32 (16-k chunks, four waves
+// per SIMD), 27 = 256x64 (16-k chunks), 28 = 256x96 (8-k chunks)
+template <int AMODE, int AOP, int EMODE, int NT, int GK, int OCC>
+static int rowgemm_direct_go(const RowGemmArgs& a, hipStream_t s) {
     if constexpr (AOP == OP_DZ) {
         return -1;
     } else {
-        if (a.N % 32 || a.K % 32 || a.C % 32 || !a.bt || a.bt16) return -1;
-        if (EMODE == E_CONVT && (a.cout % 32) && (32 % a.cout)) return -1;
+        constexpr int BN = 32 * NT;
+        if (a.N % BN || a.K % 32 || a.C % 32 || !a.bt || a.bt16) return -1;
+        if (EMODE == E_CONVT && (a.cout % BN) && (BN % a.cout)) return -1;
         // affine operands stage at most 256 channels of scale / shift: the LDS-staged tile
-        if (AOP != OP_PLAIN && a.C > 256) return rowgemm_go<AMODE, AOP, EMODE, RowTile14, false>(a, s);
-        const dim3 grid(((a.M + 255) / 256) * (a.N / 32));
-        hipLaunchKernelGGL((rowgemm_n32_kernel<AMODE, AOP, EMODE>), grid, dim3(256), 0, s, a);
+        if (AOP != OP_PLAIN && a.C > 256) {
+            if constexpr (NT == 1) return rowgemm_go<AMODE, AOP, EMODE, RowTile14, false>(a, s);
+            return -1;
+        }
+        const dim3 grid(((a.M + 255) / 256) * (a.N / BN));
+        hipLaunchKernelGGL((rowgemm_direct_kernel<AMODE, AOP, EMODE, NT, GK, OCC>), grid, dim3(256), 0, s, a);
         return (int)hipGetLastError();
     }
-}
-
-// ------------------------------------------------------------------------------------
-// Weight-gradient GEMM (reduction over pixels), same issue / compute / commit pipeline.
-// ------------------------------------------------------------------------------------
-// wgrad tile: block BM x BN, wave tile WM x WN, pixels per chunk BKP.
-template <int BM_, int BN_, int WM_, int WN_, int BKP_, int OCC_ = 1>
-struct WgTile {
-    static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, BKP = BKP_;
-    static constexpr int THREADS = 64 * (BM / WM) * (BN / WN);
-    static constexpr int OCC = OCC_;
-};
-
-template <int AMODE, int AOP, int BMODE, bool BDZ, class T>
-__global__ __launch_bounds__(T::THREADS, T::OCC) void wgrad_kernel(WgradArgs p) {
-    constexpr bool AFFINE = AOP == OP_AFFINE || AOP == OP_AFFINE_RELU;
-    constexpr bool ARELU = AOP == OP_AFFINE_RELU;
-    constexpr int BM = T::BM, BN = T::BN, BKP = T::BKP, WM = T::WM, WN = T::WN;
-    constexpr int NTH = T::THREADS;
-    constexpr int WAVES_N = BN / WN;
-    constexpr int LDA = BM + 4, LDB = BN + 4;
-    constexpr int MT = WM / 32, NT = WN / 32;
-    constexpr int AF = BM / 4, BF = BN / 4;          // float4 per pixel row
-    constexpr int ARPP = NTH / AF, BRPP = NTH / BF;  // rows per pass
-    constexpr int AP = BKP / ARPP, BP = BKP / BRPP;
-    static_assert(AP * ARPP == BKP && BP * BRPP == BKP, "loader shape");
-    __shared__ __attribute__((aligned(16))) float As[BKP * LDA];
-    __shared__ __attribute__((aligned(16))) float Bs[BKP * LDB];
-
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wm = wave / WAVES_N, wn = wave % WAVES_N;
-    const int tiles_n = p.Nw / BN, tiles_m = p.Mw / BM;
-    int idx = p.xcd ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
-    const int tn = idx % tiles_n;
-    idx /= tiles_n;
-    const int tm = idx % tiles_m;
-    const int split = idx / tiles_m;
-    const int tapA = (tm * BM) / p.CA, ca0 = tm * BM - tapA * p.CA;
-    const int tapB = (tn * BN) / p.CB, cb0 = tn * BN - tapB * p.CB;
-    const int H = p.H, W = p.W;
-    const float rH = 1.f / (float)H, rW = 1.f / (float)W;
-
-    const int ac4 = tid % AF, arow = tid / AF;
-    const int bc4 = tid % BF, brow = tid / BF;
-    f32x4 sc = {1.f, 1.f, 1.f, 1.f}, sh = {0.f, 0.f, 0.f, 0.f};
-    bool arl = false;
-    if constexpr (AFFINE) {
-        sc = *(const f32x4*)(p.ascale + ca0 + ac4 * 4);
-        sh = *(const f32x4*)(p.ashift + ca0 + ac4 * 4);
-        if constexpr (ARELU) arl = ca0 + ac4 * 4 < p.arelu;
-    }
-
-    f32x4 ca = {0, 0, 0, 0}, cb = ca, cc = ca, cm = ca;  // OP_DZ coefficients of this thread's columns
-    if constexpr (BDZ) {
-        ca = *(const f32x4*)(p.bcoef + cb0 + bc4 * 4);
-        cb = *(const f32x4*)(p.bcoef + p.CB + cb0 + bc4 * 4);
-        cc = *(const f32x4*)(p.bcoef + 2 * p.CB + cb0 + bc4 * 4);
-        cm = *(const f32x4*)(p.bcoef + 3 * p.CB + cb0 + bc4 * 4);
-    }
-    const bool bsum = p.bias_slab != nullptr && tm == 0;
-    double bacc[4] = {0.0, 0.0, 0.0, 0.0};  // f64: the bias gradient is a small sum of +/- terms
-
-    const int pbeg = split * p.pps;
-    int pend = pbeg + p.pps;
-    if (pend > p.P) pend = p.P;
-    const int nchunks = (pend - pbeg + BKP - 1) / BKP;
-
-    f32x4 ryb[BDZ ? BP : 1];
-    int bm_row[BDZ ? BP : 1];
-    const bool dzw = BDZ && p.dzout != nullptr && tm == 0 && BMODE == G_IDENT;
-    f32x4 ra[AP], rb[BP];
-    unsigned amask = 0, bmask = 0;
-    auto issue = [&](int pc) {
-        amask = bmask = 0;
-#pragma unroll
-        for (int i = 0; i < AP; ++i) {
-            int m = pc + arow + i * ARPP;
-            const bool in = m < pend;
-            m = in ? m : pend - 1;
-            bool valid;
-            const Pix q = AMODE == G_IDENT ? Pix{0, 0, 0} : decode_fast(m, H, W, rH, rW);
-            const int src = gather_src<AMODE>(tapA, m, q, H, W, valid);
-            amask |= (valid && in) ? (1u << i) : 0u;
-            ra[i] = *(const f32x4*)(p.a + (size_t)src * p.lda + p.aoff + ca0 + ac4 * 4);
-        }
-#pragma unroll
-        for (int i = 0; i < BP; ++i) {
-            int m = pc + brow + i * BRPP;
-            const bool in = m < pend;
-            m = in ? m : pend - 1;
-            bool valid;
-            const Pix q = BMODE == G_IDENT ? Pix{0, 0, 0} : decode_fast(m, H, W, rH, rW);
-            const int src = gather_src<BMODE>(tapB, m, q, H, W, valid);
-            bmask |= (valid && in) ? (1u << i) : 0u;
-            rb[i] = *(const f32x4*)(p.b + (size_t)src * p.ldb + p.boff + cb0 + bc4 * 4);
-            if constexpr (BDZ) {
-                ryb[i] = *(const f32x4*)(p.by + (size_t)src * p.ldby + p.offby + cb0 + bc4 * 4);
-                bm_row[i] = src;
-            }
-        }
-    };
-    auto commit = [&]() {
-#pragma unroll
-        for (int i = 0; i < AP; ++i) {
-            f32x4 v = ra[i];
-            if constexpr (AFFINE) {
-                v = v * sc + sh;
-                if (ARELU && arl)
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
-            }
-            if (!((amask >> i) & 1u)) v = f32x4{0.f, 0.f, 0.f, 0.f};
-            *(f32x4*)&As[(arow + i * ARPP) * LDA + ac4 * 4] = v;
-        }
-#pragma unroll
-        for (int i = 0; i < BP; ++i) {
-            f32x4 v = rb[i];
-            if constexpr (BDZ) {
-                const f32x4 d = bn_dz4(ca, v, cb, ryb[i], cm, cc);
-#pragma unroll
-                for (int j = 0; j < 4; ++j) v[j] = ryb[i][j] > 0.f ? d[j] : 0.f;
-                // the first A' tile's blocks (tap 0, channels 0..BM) hand dz to the dgrad
-                if (dzw && ((bmask >> i) & 1u))
-                    *(f32x4*)(p.dzout + (size_t)bm_row[i] * p.lddz + cb0 + bc4 * 4) = v;
-            }
-            if (!((bmask >> i) & 1u)) v = f32x4{0.f, 0.f, 0.f, 0.f};
-            if (bsum)
-#pragma unroll
-                for (int j = 0; j < 4; ++j) bacc[j] += v[j];
-            *(f32x4*)&Bs[(brow + i * BRPP) * LDB + bc4 * 4] = v;
-        }
-    };
-
-    f32x16 acc[MT][NT];
-#pragma unroll
-    for (int i = 0; i < MT; ++i)
-#pragma unroll
-        for (int j = 0; j < NT; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-    const int li = lane & 31, lh = lane >> 5;
-    if (nchunks > 0) {
-        issue(pbeg);
-        commit();
-        __syncthreads();
-    }
-    for (int c = 0; c < nchunks; ++c) {
-        if (c + 1 < nchunks) issue(pbeg + (c + 1) * BKP);
-#pragma unroll
-        for (int kk = 0; kk < BKP / 8; ++kk)
-#pragma unroll
-            for (int s = 0; s < 4; ++s) {
-                const int pr = kk * 8 + lh * 4 + s;
-                float af[MT], bf[NT];
-#pragma unroll
-                for (int mt = 0; mt < MT; ++mt) af[mt] = As[pr * LDA + wm * WM + mt * 32 + li];
-#pragma unroll
-                for (int nt = 0; nt < NT; ++nt) bf[nt] = Bs[pr * LDB + wn * WN + nt * 32 + li];
-#pragma unroll
-                for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-                    for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma32(af[mt], bf[nt], acc[mt][nt]);
-            }
-        __syncthreads();
-        if (c + 1 < nchunks) {
-            commit();
-            __syncthreads();
-        }
-    }
-
-    if (bsum) {  // column sums of B' for the bias gradient: combine the row groups in order
-        __syncthreads();
-        double* red = (double*)As;  // [NTH][4]; As holds >= BKP*LDA floats >= 8*NTH
-#pragma unroll
-        for (int j = 0; j < 4; ++j) red[tid * 4 + j] = bacc[j];
-        __syncthreads();
-        if (tid < BF) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                double t = 0.0;
-                for (int g = 0; g < BRPP; ++g) t += red[(g * BF + tid) * 4 + j];
-                p.bias_slab[(size_t)split * p.Nw + tn * BN + tid * 4 + j] = (float)t;
-            }
-        }
-    }
-
-    float* slab = p.slab + (size_t)split * p.Mw * p.Nw;
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int m = tm * BM + wm * WM + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-                const int n = tn * BN + wn * WN + nt * 32 + li;
-                slab[(size_t)m * p.Nw + n] = acc[mt][nt][r];
-            }
 }
 
 template <int AMODE, int AOP, int EMODE, bool BF>
 static int rowgemm_tile(const RowGemmArgs& a, int tile, hipStream_t s) {
     if constexpr (!BF) {
-        if (tile == 15) return rowgemm_n32_go<AMODE, AOP, EMODE>(a, s);
+        if (tile == 15) return rowgemm_direct_go<AMODE, AOP, EMODE, 1, 4, 2>(a, s);
+        if (tile == 29) return rowgemm_direct_go<AMODE, AOP, EMODE, 1, 2, 4>(a, s);
+        if (tile == 27) return rowgemm_direct_go<AMODE, AOP, EMODE, 2, 2, 2>(a, s);
+        if (tile == 28) return rowgemm_direct_go<AMODE, AOP, EMODE, 3, 1, 2>(a, s);
     }
 #define RG_CASE(id, T) \
     if (tile == id) return rowgemm_go<AMODE, AOP, EMODE, T, BF>(a, s);
@@ -1072,10 +1093,10 @@ static int rowgemm_tile(const RowGemmArgs& a, int tile, hipStream_t s) {
 }
 
 int rowgemm_tile_dims(int tile, int* bm, int* bn, int* bk) {
-    if (tile == 15) {  // rowgemm_n32_kernel (operands straight from global memory)
+    if (tile == 15 || tile == 27 || tile == 28 || tile == 29) {  // rowgemm_direct_kernel
         *bm = 256;
-        *bn = 32;
-        *bk = 32;
+        *bn = tile == 27 ? 64 : tile == 28 ? 96 : 32;
+        *bk = tile == 15 ? 32 : tile == 28 ? 8 : 16;
         return 0;
     }
     if (tile >= 16 && tile <= 19) {  // rowgemm_pipe_kernel (18, 19: loads two chunks ahead)
@@ -1103,7 +1124,7 @@ int rowgemm_tile_dims(int tile, int* bm, int* bn, int* bk) {
 }
 
 int rowgemm_tile_dbuf(int tile) {
-    if (tile == 15) return 3;  // operands straight from global memory
+    if (tile == 15 || tile == 27 || tile == 28 || tile == 29) return 3;  // operands from global memory
     if ((tile >= 16 && tile <= 19) || tile == 25 || tile == 26) return 2;  // pipelined
 #define RG_DB(id, T) \
     if (tile == id) return T::DBUF ? 1 : 0;

@@ -4,7 +4,7 @@ set -u
 cd $GRAFT_REPO_ROOT
 TAG=${1:-r04f}
 timeout -k 10 700 python -u -m pytest -x -v --timeout 300 --timeout-method thread -p no:cacheprovider \
-  tests/test_gpu_res.py "tests/test_gpu_mod.py" -k "narrow or res or rg16_tile_choice or halo or bf16_oracle or tap_row or convt16 or register_staged or n32" \
+  tests/test_gpu_res.py "tests/test_gpu_mod.py" -k "narrow or res or rg16_tile_choice or halo or bf16_oracle or tap_row or convt16 or register_staged or direct_tiles" \
   > gpurun_out/$TAG.pytest.log 2>&1
 rc=$?
 echo "pytest rc=$rc"; grep -E "passed|failed" gpurun_out/$TAG.pytest.log | tail -3
