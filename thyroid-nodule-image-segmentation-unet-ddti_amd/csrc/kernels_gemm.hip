@@ -1215,9 +1215,15 @@ using Wr3Tile0 = WgTile<64, 64, 32, 32, 32>;    // 4 waves, 3 x 32x32 per wave
 using Wr3Tile1 = WgTile<128, 64, 64, 32, 32>;   // 4 waves, 3 x 64x32
 using Wr3Tile2 = WgTile<64, 128, 32, 64, 32>;   // 4 waves, 3 x 32x64
 using Wr3Tile3 = WgTile<128, 128, 64, 64, 32>;  // 4 waves, 3 x 64x64 (192 accumulators)
+// 32-channel operands (the narrow networks' level 0, r04): one / two waves of 3 x 32x32
+using Wr3Tile4 = WgTile<32, 32, 32, 32, 32>;    // Cin = Cout = 32
+using Wr3Tile5 = WgTile<64, 32, 32, 32, 32>;    // Cin 64 (a [skip | up] concat), Cout 32
+using Wr3Tile6 = WgTile<32, 64, 32, 32, 32>;    // Cin 32, Cout 64
 // (r03: 64-pixel chunks, 16-pixel rows, all three tap rows per block and a software-
 // pipelined schedule of these tiles measured at or below them; not kept)
-#define WGRAD_ROW3_TILES(X) X(20, Wr3Tile0) X(21, Wr3Tile1) X(22, Wr3Tile2) X(23, Wr3Tile3)
+#define WGRAD_ROW3_TILES(X) \
+    X(20, Wr3Tile0) X(21, Wr3Tile1) X(22, Wr3Tile2) X(23, Wr3Tile3) X(24, Wr3Tile4) X(25, Wr3Tile5) \
+    X(26, Wr3Tile6)
 
 // a row3 block covers three taps (its split-K partition counts them)
 int wgrad_tile_taps(int tile) { return tile >= 20 ? 3 : 1; }

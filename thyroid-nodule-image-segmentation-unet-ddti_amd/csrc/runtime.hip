@@ -98,6 +98,8 @@ struct Options {
     int wgrad16_blocks = 1536;     // split-K target (blocks) of the bf16 weight gradients
                                    // (config 4 A/B: 1536 +1.4 % over 2048, 1024 -4.7 %)
     int wgrad_row3_big = 21;       // row3 tile where Cin, Cout % 128 == 0 (-1 = 23)
+    int wgrad_row3_n32 = 1;        // row3 weight gradients for 32-channel operands too (tiles 24..26,
+                                   // one / two waves: the split-K target counts four-wave blocks)
     int wgrad_row3_blocks = 1536;  // split-K target (blocks) of the row3 weight gradients
                                    // (r02 sweep 512..2048: 1536 best, 391 vs 386 img/s)
     int wgrad_tile_w = 0;      // f32 wgrad tile, both channel counts multiples of 128
@@ -162,6 +164,7 @@ const OptionDesc OPTION_TABLE[] = {
     {"wgrad_row3_tile", &Options::wgrad_row3_tile},
     {"wgrad_row3_big", &Options::wgrad_row3_big},
     {"wgrad_row3_blocks", &Options::wgrad_row3_blocks},
+    {"wgrad_row3_n32", &Options::wgrad_row3_n32},
     {"wgrad_blocks", &Options::wgrad_blocks},
     {"wgrad16_blocks", &Options::wgrad16_blocks},
     {"wgrad_tile_w", &Options::wgrad_tile_w},
@@ -609,9 +612,12 @@ WgradCfg wgrad_cfg(const unet_ctx* c, int CA, int tapsA, int CB, int tapsB, int6
         else
             w.tile = 7;
         const bool row3 = tapsA == 9 && tapsB == 1 && row_w > 0 && row_w % 32 == 0 &&
-                          CA % 64 == 0 && CB % 64 == 0 &&
+                          CA % 32 == 0 && CB % 32 == 0 &&
                           (r3 == 1 || (r3 == 2 && (CA == 64 || CB == 64)));
-        if (row3) {
+        const bool r3n = CA % 64 || CB % 64;  // a 32-channel operand (r04 tiles 24..26)
+        if (row3 && r3n && c->opt.wgrad_row3_n32) {
+            w.tile = CA % 64 ? (CB % 64 ? 24 : 26) : 25;
+        } else if (row3 && !r3n) {
             w.tile = r3t >= 20 ? r3t
                                : (CA % 128 == 0 ? (CB % 128 == 0 ? 23 : 21) : (CB % 128 == 0 ? 22 : 20));
             // option wgrad_row3_big: the tile of the layers whose channel counts both divide
@@ -628,7 +634,8 @@ WgradCfg wgrad_cfg(const unet_ctx* c, int CA, int tapsA, int CB, int tapsB, int6
     // blocks to launch: 2048 one-tap blocks; a row3 block does the work of three, and every
     // extra split adds a full Mw x Nw slab to write and reduce
     const int64_t target = bf16 ? c->opt.wgrad16_blocks
-                                : (w.tile >= 20 ? c->opt.wgrad_row3_blocks : c->opt.wgrad_blocks);
+                                : (w.tile >= 20 ? c->opt.wgrad_row3_blocks : c->opt.wgrad_blocks) *
+                                      (w.tile == 24 ? 4 : (w.tile == 25 || w.tile == 26) ? 2 : 1);
     int64_t s = (target + tiles - 1) / tiles;
     const int64_t maxs = P / (8 * w.bkp) > 0 ? P / (8 * w.bkp) : 1;  // >= 8 chunks per split
     // (P need not be a multiple of the pixel chunk: the kernel zero-fills the tail)
