@@ -163,18 +163,15 @@ def _f32_step(m, x, t):
 @pytest.mark.parametrize("net,base,ref,alt", [
     ("res", 32, dict(tile_n32=14), dict(tile_n32=15)),
     ("mod", 32, dict(tile_n32=14), dict(tile_n32=15)),
-    ("res", 32, dict(tile_n32=14), dict(tile_n32=29)),
-    ("mod", 32, dict(tile_n64=19, tile_n64_dgrad=25), dict(tile_n64=27, tile_n64_dgrad=27)),
-    ("res", 48, dict(tile_n96=-1, tile_n32=14), dict(tile_n96=28)),
-    ("mod", 48, dict(tile_n96=-1, tile_n32=14), dict(tile_n96=28)),
+    ("res", 48, dict(tile_n32=14), dict(tile_n32=15)),  # 96-channel level: three column tiles
 ])
 def test_direct_tiles_bit_identical(net, base, ref, alt):
-    """Row GEMMs on the direct-from-global tiles (kernels_gemm.hip rowgemm_direct_kernel:
-    15 / 29 = 32 outputs, 27 = 64, 28 = 96; MFMA operands straight from global memory into
-    registers) against the LDS-staged tiles (14 = 256 x 32, 19 / 25 = the pipelined 128 x 64,
-    three 32-column tiles for 96 outputs): same K order and MFMA sequence per element, same
-    epilogues (forward BN statistics, dgrad BN partials, residual add, 1x1 skip, ConvT), so
-    one training step of a ResUNet / mod.py UNet at that width is bit-identical."""
+    """Row GEMMs on the direct-from-global tile (kernels_gemm.hip rowgemm_direct_kernel, tile
+    15: MFMA operands straight from global memory into registers) against the LDS-staged tile
+    14 (256 x 32): same K order and MFMA sequence per element, same epilogues (forward BN
+    statistics, dgrad BN partials, residual add, 1x1 skip, ConvT), so one training step of a
+    ResUNet / mod.py UNet at that width is bit-identical (base 48: the 96-channel level runs
+    three 32-column tiles)."""
     from _helpers import hip_mod_model, options
     x, t = inputs(61, 2, 128, 128)
     outs = []

@@ -248,8 +248,7 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_kernel(RowGemmArgs
 }
 
 // ------------------------------------------------------------------------------------
-// Skinny row GEMMs (N = 32 / 64 / 96 outputs: the narrow networks' level 0 and the 96-channel
-// levels of base 24 / 48; tiles 15, 27, 28).  With one wave per 64-row band holding the whole
+// Skinny row GEMM (N = 32 outputs: the narrow networks' level 0; tile 15).  With one wave per 64-row band holding the whole
 // N, every A row feeds exactly one wave, so staging A through LDS (tile 14) bought no reuse
 // and held the CU to one 83-KB block of four waves.  Here every MFMA operand comes from
 // global memory straight into registers, in the layout the LDS-staged tiles read (lane half h
@@ -1056,8 +1055,7 @@ static int rowgemm_go(const RowGemmArgs& a, hipStream_t s) {
     }
 }
 
-// tiles 15 = 256x32 (32-k chunks, two waves per SIMD), 29 = 256x32 (16-k chunks, four waves
-// per SIMD), 27 = 256x64 (16-k chunks), 28 = 256x96 (8-k chunks)
+// tile 15 = 256x32 (32-k chunks, two waves per SIMD)
 template <int AMODE, int AOP, int EMODE, int NT, int GK, int OCC>
 static int rowgemm_direct_go(const RowGemmArgs& a, hipStream_t s) {
     if constexpr (AOP == OP_DZ) {
@@ -1080,10 +1078,9 @@ static int rowgemm_direct_go(const RowGemmArgs& a, hipStream_t s) {
 template <int AMODE, int AOP, int EMODE, bool BF>
 static int rowgemm_tile(const RowGemmArgs& a, int tile, hipStream_t s) {
     if constexpr (!BF) {
+        // (r04 A/B, not kept: 16-k chunks at four waves per SIMD for 32 outputs, and the
+        // same kernel for 64 / 96 outputs -- slower / neutral against tiles 19/25 and 15)
         if (tile == 15) return rowgemm_direct_go<AMODE, AOP, EMODE, 1, 4, 2>(a, s);
-        if (tile == 29) return rowgemm_direct_go<AMODE, AOP, EMODE, 1, 2, 4>(a, s);
-        if (tile == 27) return rowgemm_direct_go<AMODE, AOP, EMODE, 2, 2, 2>(a, s);
-        if (tile == 28) return rowgemm_direct_go<AMODE, AOP, EMODE, 3, 1, 2>(a, s);
     }
 #define RG_CASE(id, T) \
     if (tile == id) return rowgemm_go<AMODE, AOP, EMODE, T, BF>(a, s);
@@ -1093,10 +1090,10 @@ static int rowgemm_tile(const RowGemmArgs& a, int tile, hipStream_t s) {
 }
 
 int rowgemm_tile_dims(int tile, int* bm, int* bn, int* bk) {
-    if (tile == 15 || tile == 27 || tile == 28 || tile == 29) {  // rowgemm_direct_kernel
+    if (tile == 15) {  // rowgemm_direct_kernel (operands straight from global memory)
         *bm = 256;
-        *bn = tile == 27 ? 64 : tile == 28 ? 96 : 32;
-        *bk = tile == 15 ? 32 : tile == 28 ? 8 : 16;
+        *bn = 32;
+        *bk = 32;
         return 0;
     }
     if (tile >= 16 && tile <= 19) {  // rowgemm_pipe_kernel (18, 19: loads two chunks ahead)
@@ -1124,7 +1121,7 @@ int rowgemm_tile_dims(int tile, int* bm, int* bn, int* bk) {
 }
 
 int rowgemm_tile_dbuf(int tile) {
-    if (tile == 15 || tile == 27 || tile == 28 || tile == 29) return 3;  // operands from global memory
+    if (tile == 15) return 3;  // operands straight from global memory
     if ((tile >= 16 && tile <= 19) || tile == 25 || tile == 26) return 2;  // pipelined
 #define RG_DB(id, T) \
     if (tile == id) return T::DBUF ? 1 : 0;

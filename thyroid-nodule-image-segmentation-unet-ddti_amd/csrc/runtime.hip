@@ -110,8 +110,6 @@ struct Options {
     int tile_n64 = 19;         // ... N = 64 outputs (forward-type)
     int tile_n64_dgrad = 25;   // ... N = 64, dgrad-type (pipelined 128x64 at three blocks per
                                // CU: level-0 dgrads 1.50-1.55 -> 1.40-1.45 ms, r03)
-    int tile_n96 = 28;         // f32 row GEMMs with 96 outputs (base 24 / 48 levels): 28 = one
-                               // 256 x 96 tile from global memory (-1 = three 32-column tiles)
     int tile_convt64 = 1;      // ConvT forward with 64 output channels (grid N = 256)
     int tile_n32 = 15;         // f32 row GEMMs with 32 outputs: 15 = 256 x 32 with operands
                                // straight from global memory (r04, ResUNet(32, 4) 263 -> 282
@@ -175,7 +173,6 @@ const OptionDesc OPTION_TABLE[] = {
     {"tile_n64", &Options::tile_n64},
     {"tile_n64_dgrad", &Options::tile_n64_dgrad},
     {"tile_n32", &Options::tile_n32},
-    {"tile_n96", &Options::tile_n96},
     {"tile_convt64", &Options::tile_convt64},
     {"tile_convt", &Options::tile_convt},
     {"tile_convt_dgrad", &Options::tile_convt_dgrad},
@@ -910,7 +907,6 @@ struct Launcher {
 int pick_tile(const unet_ctx* c, int N, bool dgrad, bool bf16, bool convt = false) {
     const Options& o = c->opt;
     if (bf16) return N % 128 == 0 ? (dgrad ? o.tile16_n128_dgrad : o.tile16_n128) : o.tile16_n64;
-    if (N % 64 && N % 96 == 0 && o.tile_n96 >= 0) return o.tile_n96;  // 96 (base 24 / 48 levels)
     if (N % 64) return o.tile_n32;  // 32 outputs (narrow networks' level 0)
     if (N % 128) return convt && !dgrad ? o.tile_convt64 : (dgrad ? o.tile_n64_dgrad : o.tile_n64);
     if (convt && !dgrad && o.tile_convt >= 0) return o.tile_convt;

@@ -4,7 +4,7 @@ set -u
 cd $GRAFT_REPO_ROOT
 TAG=${1:-r04i}
 timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -p no:cacheprovider \
-  tests/test_gpu_res.py "tests/test_gpu_mod.py" -k "narrow or res_" > gpurun_out/$TAG.pytest.log 2>&1
+  tests/test_gpu_res.py "tests/test_gpu_mod.py" -k "narrow or res_ or direct_tiles" > gpurun_out/$TAG.pytest.log 2>&1
 rc=$?
 echo "pytest rc=$rc"; grep -E "passed|failed" gpurun_out/$TAG.pytest.log | tail -3
 [ $rc -ne 0 ] && { grep -E "FAILED|Error|assert" gpurun_out/$TAG.pytest.log | head -30; exit $rc; }
