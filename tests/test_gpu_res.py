@@ -189,3 +189,27 @@ def test_direct_tiles_bit_identical(net, base, ref, alt):
         assert torch.equal(g, b[1][k]), f"grad {k}"
     for k, v in a[2].items():
         assert torch.equal(v, b[2][k]), f"buffer {k}"
+
+
+@pytest.mark.parametrize("net,base", [("res", 32), ("mod", 32), ("mod", 64)])
+def test_dz_in_wgrad_bn_relu_bit_identical(net, base):
+    """Option dz_in_wgrad on the BN -> ReLU networks (r04; models/mod.py UNet and ResUNet,
+    f32): the weight gradient's B' loader forms dz = A do + B (z - mean) + C unmasked (the
+    producer of do already applied the ReLU mask), its first A'-tile blocks store it for the
+    dgrad, and the bn_dz pass disappears -- the same bn_dz4 arithmetic, so one training step
+    is bit-identical to the separate pass."""
+    from _helpers import hip_mod_model, options
+    x, t = inputs(71, 2, 128, 128)
+    outs = []
+    for flag in (0, 1 << 20):  # off / every layer (default: Cin <= 256)
+        if net == "res":
+            m = _model(MO.res_make_params(73, base, 3), base, 3)
+        else:
+            m = hip_mod_model(MO.make_params(73, base, 3), DEV, base, 3)
+        with options(m.flatten_().rt, dz_in_wgrad=flag):
+            outs.append(_f32_step(m, x, t))
+        del m
+    a, b = outs
+    assert torch.equal(a[0], b[0]), "logits"
+    for k, g in a[1].items():
+        assert torch.equal(g, b[1][k]), f"grad {k}: {(g - b[1][k]).abs().max().item()}"

@@ -114,6 +114,8 @@ struct WgradArgs {
     int xcd;             // remap blocks so each XCD gets a contiguous range of tiles
     float* dzout;        // OP_DZ on B': the blocks of the first A' tile also store the dz
     int lddz;            // they formed ([P][lddz], channels cb0..), for the dgrad to read
+    int bdznomask;       // OP_DZ on B', BN -> ReLU order (models/mod.py): dz is not masked by
+                         // [y > 0] (the producer of do already applied the ReLU mask)
 };
 
 #define HIP_OK(x)                                   \

@@ -375,7 +375,9 @@ __global__ __launch_bounds__(256, OCC) void rowgemm_direct_kernel(RowGemmArgs p)
         if (kc + 2 < nk) load(kc + 2, c0);
         compute(c1);
     }
-    row_epilogue<EMODE, BM, BN, WM, WN>(p, acc, m0, n0, tile_m, wave, 0, lane, tid, smem);
+    // PRELOAD: the short-K (64 .. 576) GEMMs of this tile are epilogue-heavy; the reading
+    // epilogues (BN partials, residual close / add) issue each accumulator's 16 loads first
+    row_epilogue<EMODE, BM, BN, WM, WN, true>(p, acc, m0, n0, tile_m, wave, 0, lane, tid, smem);
 }
 
 
@@ -497,7 +499,7 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void wgrad_kernel(WgradArgs p) 
             if constexpr (BDZ) {
                 const f32x4 d = bn_dz4(ca, v, cb, ryb[i], cm, cc);
 #pragma unroll
-                for (int j = 0; j < 4; ++j) v[j] = ryb[i][j] > 0.f ? d[j] : 0.f;
+                for (int j = 0; j < 4; ++j) v[j] = (p.bdznomask || ryb[i][j] > 0.f) ? d[j] : 0.f;
                 // the first A' tile's blocks (tap 0, channels 0..BM) hand dz to the dgrad
                 if (dzw && ((bmask >> i) & 1u))
                     *(f32x4*)(p.dzout + (size_t)bm_row[i] * p.lddz + cb0 + bc4 * 4) = v;
@@ -698,7 +700,7 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void wgrad_row3_kernel(WgradArg
             if constexpr (BDZ) {
                 const f32x4 d = bn_dz4(ca, v, cb, ryb[i], cm, cc);
 #pragma unroll
-                for (int j = 0; j < 4; ++j) v[j] = ryb[i][j] > 0.f ? d[j] : 0.f;
+                for (int j = 0; j < 4; ++j) v[j] = (p.bdznomask || ryb[i][j] > 0.f) ? d[j] : 0.f;
                 // the first A' tile's blocks (tap row 0, channels 0..BM) hand dz to the dgrad
                 if (dzw && ((bmask >> i) & 1u))
                     *(f32x4*)(p.dzout + (size_t)bm_row[i] * p.lddz + cb0 + bc4 * 4) = v;
@@ -1321,18 +1323,21 @@ int launch_wgrad(const WgradArgs& a, int tile, hipStream_t s) {
     }
     const bool aff = a.ascale != nullptr, dz = a.bcoef != nullptr;
     if (a.arelu && !aff) return -1;
-    if (a.arelu && dz) return -1;  // OP_DZ loaders are the ReLU -> BN order only
+    if (a.arelu && dz && !a.bdznomask) return -1;  // BN -> ReLU A' operands come with an unmasked dz
     if (tile >= 20) {  // one row of 3x3 taps per block (wgrad_row3_kernel)
         if (a.amode != G_CONV3 || a.bmode != G_IDENT) return -1;
+        if (dz && a.arelu) return wgrad_row3_tile<OP_AFFINE_RELU, true>(a, tile, s);
         if (dz) return aff ? wgrad_row3_tile<OP_AFFINE, true>(a, tile, s)
                            : wgrad_row3_tile<OP_PLAIN, true>(a, tile, s);
         if (a.arelu) return wgrad_row3_tile<OP_AFFINE_RELU, false>(a, tile, s);
         return aff ? wgrad_row3_tile<OP_AFFINE, false>(a, tile, s)
                    : wgrad_row3_tile<OP_PLAIN, false>(a, tile, s);
     }
-    if (a.amode == G_CONV3 && a.bmode == G_IDENT && dz)
+    if (a.amode == G_CONV3 && a.bmode == G_IDENT && dz) {
+        if (a.arelu) return wgrad_tile<G_CONV3, OP_AFFINE_RELU, G_IDENT, true>(a, tile, s);
         return aff ? wgrad_tile<G_CONV3, OP_AFFINE, G_IDENT, true>(a, tile, s)
                    : wgrad_tile<G_CONV3, OP_PLAIN, G_IDENT, true>(a, tile, s);
+    }
     if (a.amode == G_CONV3 && a.bmode == G_IDENT && !dz) {
         if (a.arelu) return wgrad_tile<G_CONV3, OP_AFFINE_RELU, G_IDENT, false>(a, tile, s);
         return aff ? wgrad_tile<G_CONV3, OP_AFFINE, G_IDENT, false>(a, tile, s)

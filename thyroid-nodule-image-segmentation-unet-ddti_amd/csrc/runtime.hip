@@ -147,7 +147,7 @@ struct Options {
                                // 2.02 -> 0.97 GB at equal time), 2 row GEMMs, 3 wgrad
     int dz_in_wgrad = 256;     // layers with Cin <= this form the BN-backward dz in the weight
                                // gradient's B' loader, which also stores it for the dgrad (no
-                               // bn_dz pass; model.py order; 0 = off).  Every A'-tile row of
+                               // bn_dz pass; f32, both BN orders since r04; 0 = off).  Every A'-tile row of
                                // blocks re-reads do and y instead of dz, so the fusion pays
                                // where few A' tiles share a pixel slice (profiles/
                                // r03_tile_experiments.txt: Cin 64..256 gain, 512..1024 lose)
@@ -848,7 +848,7 @@ void make_plan(unet_ctx* c, int N, int H, int W, bool training, char* base, Plan
                                 std::max<int64_t>(10 * c->base, (int64_t)c->out_ch * (c->base + 1)));
         p.bslab = b.take<float>(std::max<int64_t>(bmax, 1));
         p.coef = b.take<float>(4 * (int64_t)c->cmax);  // BN-backward dz coefficients [4][C]
-        p.gdz = (c->opt.dz_in_wgrad && !c->bn_relu && !c->bf16) ? b.take<float>(gmax) : nullptr;
+        p.gdz = (c->opt.dz_in_wgrad && !c->bf16) ? b.take<float>(gmax) : nullptr;
     } else {
         p.gdz = nullptr;
         p.g[0] = p.g[1] = p.g[2] = p.slab = p.part = p.part2 = p.hpart = p.bslab = p.coef = nullptr;
@@ -1336,7 +1336,8 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         WgradCfg wc = wgrad_cfg(c, C.cin, 9, C.cout, 1, P, c->bf16, Wl);
         // option dz_in_wgrad: the weight gradient's B' loader forms dz from do and y (the
         // bn_dz pass disappears) and its first A'-tile blocks store it for the dgrad; f32
-        // register-staged weight-gradient tiles only, model.py order, with a dgrad to feed
+        // register-staged weight-gradient tiles only, with a dgrad to feed (r04: both BN orders;
+        // BN -> ReLU forms dz unmasked, do already carries the ReLU mask)
         const bool dzw = p.gdz && C.cin <= c->opt.dz_in_wgrad && !dz16 && dx &&
                          (wc.tile < 10 || wc.tile >= 20);
         if (dzw) {
@@ -1371,6 +1372,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         w.offby = p.offy[i];
         w.bcoef = dzw ? p.coef : nullptr;
         w.dzout = dzw ? p.gdz : nullptr;
+        w.bdznomask = dz_mask ? 0 : 1;
         w.lddz = C.cout;
         w.bias_slab = C.b >= 0 ? p.bslab : nullptr;
         w.Mw = 9 * C.cin;
