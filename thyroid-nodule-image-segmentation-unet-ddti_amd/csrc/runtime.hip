@@ -677,8 +677,9 @@ int rg16_tile(const unet_ctx* c, const RowGemmArgs& g) {
     if (c->opt.rg16_r3 && fits(19)) t4 = 19;  // option rg16_r3: the tap-row halo kernel
     if (!fits(4)) {
         // option rg16_n128: a 512-row tile for the 128-output GEMMs (halo kernel for 3x3 convs)
+        // (rg16_r3 = 0 turns the halo kernel off here too: the one-tap 512x128 tile instead)
         int tn = c->opt.rg16_n128;
-        if (tn == 20 && !fits(20)) tn = 6;
+        if (tn == 20 && (!c->opt.rg16_r3 || !fits(20))) tn = 6;
         if (tn < 0 || !fits(tn)) return t0;
         if ((g.M + 511) / 512 * (g.N / 128) < 256) return t0;
         if (g.emode == E_STORE_BN && g.K < c->opt.rg16_bn_k && !c->opt.rg16_n128_bn) return t0;
