@@ -38,6 +38,9 @@ for _p in (REPO, PKG):
 
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md chip table, dense fp32 matrix
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # dense bf16 matrix (no 2:1 sparsity)
+# f32 GEMMs on the bf16 matrix cores through exact three-way operand splits (option x3,
+# kernels_gemm_x3.hip): six bf16 MFMA products per f32 product
+X3_MFMA_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 6
 HBM_PEAK_GBS = 8000.0
 
 
@@ -393,7 +396,8 @@ def main():
                  res_train_flops_per_image(S, S, args.base, args.depth) if cres else
                  train_flops_per_image(S, S)) * B
     bf16 = c4 and args.mfma == "bf16"
-    peak = BF16_MFMA_PEAK_TFLOPS if bf16 else FP32_MFMA_PEAK_TFLOPS
+    x3 = dom.startswith("x3_") or dom.startswith("wx3_")
+    peak = BF16_MFMA_PEAK_TFLOPS if bf16 else X3_MFMA_PEAK_TFLOPS if x3 else FP32_MFMA_PEAK_TFLOPS
     roofline = {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 3),
                 "peak": peak, "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4),
@@ -402,6 +406,12 @@ def main():
                 "kernel_share_of_gpu_time": round(kern[dom][1] / max(1e-9, sum(v[1] for v in kern.values())), 4),
                 "step_conv_tflops": round(conv_flop / (ms * 1e-3) / 1e12, 3),
                 "step_conv_frac": round(conv_flop / (ms * 1e-3) / 1e12 / peak, 4)}
+    if x3:
+        roofline["peak_note"] = ("f32 GEMM on bf16 MFMA through exact 3-way operand splits: 6 bf16 "
+                                 "products per f32 product, so the peak is the bf16 dense peak / 6")
+        roofline["fp32_mfma_peak_frac"] = round(achieved / FP32_MFMA_PEAK_TFLOPS, 4)
+        roofline["step_conv_fp32_mfma_frac"] = round(conv_flop / (ms * 1e-3) / 1e12 /
+                                                     FP32_MFMA_PEAK_TFLOPS, 4)
 
     if cres:
         metric = f"images/sec fwd+bwd, mod.ResUNet(base {args.base}, depth {args.depth}) {S}x{S}x1 bs={B}/GPU"
@@ -429,8 +439,10 @@ def main():
         else:  # several ranks sharing devices over gloo: exercises the DP code path only
             tag = (f"DP rehearsal: {world} ranks on {max(ndev, 1)} GPU(s) over {backend}, "
                    f"not BASELINE config 3")
+        gemms = ("f32 GEMMs on bf16 MFMA via exact 3-way operand splits, split f32 accumulators"
+                 if model.flatten_().rt.get_option("x3") else "f32 MFMA")
         workload = (f"models/model.py UNet depth-4 base-64, 1x{S}x{S}, bs={B}/GPU, "
-                    f"fwd+BCE+Dice+bwd+AdamW ({tag})")
+                    f"fwd+BCE+Dice+bwd+AdamW ({tag}; {gemms})")
         mname = "UNet(in=1,out=1) 31,042,369 params"
     out = {"metric": metric,
            "value": round(value, 3), "unit": "images/sec", "n_gpus": world, "steps": args.steps,

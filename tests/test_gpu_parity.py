@@ -532,6 +532,7 @@ def test_wgrad_row3_matches_one_tap_tiles(variant):
             from oracle import mod_ref_cpu as MO
             m = hip_mod_model(MO.make_params(5, base=64, depth=4), DEV, 64, 4)
         rt = m.flatten_().rt
+        rt.set_option("x3", 0)  # the f32 MFMA weight gradients are the subject
         rt.set_option("wgrad_row3", flag)
         try:
             logits = m(x.to(DEV))
@@ -581,7 +582,7 @@ def test_pipe_gemm_bit_identical(variant, B, H, W):
             sd.update({k: v.clone() for k, v in MO.res_make_params(42, 64, 3).items()})
             m.load_state_dict(sd)
             m = m.to(DEV).train()
-        with options(m.flatten_().rt, tile_n128=tiles[0], tile_n128_dgrad=tiles[1],
+        with options(m.flatten_().rt, x3=0, tile_n128=tiles[0], tile_n128_dgrad=tiles[1],
                      tile_n64=tiles[2], tile_n64_dgrad=tiles[2], tile_convt64=tiles[2],
                      tile_convt_dgrad=tiles[3]):
             logits = m(x.to(DEV))
@@ -608,7 +609,7 @@ def test_dz_in_wgrad_bit_identical(B, H, W):
     outs = []
     for flag in (0, 1 << 20):  # off / every layer (default: Cin <= 256)
         m = hip_model(O.make_params(42), DEV)
-        with options(m.flatten_().rt, dz_in_wgrad=flag):
+        with options(m.flatten_().rt, x3=0, dz_in_wgrad=flag):
             logits = m(x.to(DEV))
             l = unet_hip.seg_losses(logits, t.to(DEV))
             (l[0] + l[1]).backward()

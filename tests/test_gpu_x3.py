@@ -1,0 +1,120 @@
+"""f32 GEMMs on the bf16 matrix cores through exact three-way operand splits (option x3,
+csrc/kernels_gemm_x3.hip) against the f32-MFMA kernels (option x3 = 0), both measured
+against the oracle evaluated in fp64.
+
+Every f32 operand splits exactly into three bf16 pieces; the kernels form six of the nine
+piece products (the three dropped ones are below 2^-25 |a b| together) and keep the five
+small products in a separate f32 accumulator, so the large accumulator takes one rounding
+per 16 products against the f32 MFMA's one per 2.  The bar here is therefore "no worse than
+the f32 MFMA path", per layer and on the logits; the 1e-4 north-star bars are the other GPU
+tests' (they run the default, x3 on).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from _helpers import hip_model, inputs, norm_rel
+from oracle import unet_ref_cpu as O
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda:0")
+
+
+@pytest.fixture(autouse=True, scope="module")
+def _threads():
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+
+
+def _to64(d):
+    return {k: (v.double() if v.is_floating_point() else v.clone()) for k, v in d.items()}
+
+
+def test_x3_forward_no_less_accurate_than_f32_mfma():
+    """B=2 at 128x128 (every conv but the Cin = 1 first one and every ConvT on x3 kernels):
+    each layer's output and the logits, relative to the fp64 oracle, with x3 on and off.
+    The x3 error must not exceed the f32 MFMA kernels' by more than 25 % at any layer (in
+    practice it is ~3x smaller, profiles/r04_x3_probe_*.txt)."""
+    P = O.make_params(7)
+    x, _ = inputs(3, 2, 128, 128)
+    rec = []
+    ref = O.forward(x.double(), _to64(P), _to64(O.init_buffers()), True, record=rec)
+    errs = {}
+    for x3 in (1, 0):
+        m = hip_model(P, DEV)
+        st = m.flatten_()
+        st.rt.set_option("x3", x3)
+        with torch.no_grad():
+            logits, ws = st.rt.forward(st.param_arena, st.bn_arena, st.nbt_arena, x.to(DEV),
+                                       training=True)
+        torch.cuda.synchronize()
+        e = []
+        for i in range(18):
+            v, off = st.rt.debug_view(ws, 2, 128, 128, True, 0, i)
+            C = rec[i].shape[1]
+            got = v[:, off:off + C].cpu().double()
+            want = rec[i].permute(0, 2, 3, 1).reshape(-1, C)
+            e.append(norm_rel(got, want))
+        e.append(norm_rel(logits.cpu().double(), ref))
+        errs[x3] = np.array(e)
+        del m, st, ws
+    print("per-layer norm-rel error vs fp64, x3:", np.array2string(errs[1], precision=2))
+    print("per-layer norm-rel error vs fp64, f32:", np.array2string(errs[0], precision=2))
+    assert np.all(errs[1] <= 1.25 * errs[0] + 1e-8), (errs[1], errs[0])
+    assert errs[1][-1] <= 1e-5
+
+
+def test_x3_train_step_matches_f32_mfma():
+    """One training step (fwd, BCE+Dice, bwd) at B=2 128x128 against the fp64 oracle: logits
+    at least as accurate as the f32-MFMA path's (measured 1.2e-6 vs 3.1e-6), gradients within
+    the spread the f32 path itself shows (a ReLU input within ~1e-6 of zero flips in one
+    evaluation or the other and moves upstream gradients by ~1e-2: measured worst tensor 9.3e-3
+    for x3, 1.5e-2 for f32)."""
+    import unet_hip
+    P = O.make_params(11)
+    x, t = inputs(5, 2, 128, 128)
+    ref = O.train_step(_to64(P), _to64(O.init_buffers()), None, x.double(), t.double())
+    res = {}
+    for x3 in (1, 0):
+        m = hip_model(P, DEV)
+        m.flatten_().rt.set_option("x3", x3)
+        logits = m(x.to(DEV))
+        losses = unet_hip.seg_losses(logits, t.to(DEV))
+        (losses[0] + losses[1]).backward()
+        torch.cuda.synchronize()
+        res[x3] = (logits.detach().cpu().double(),
+                   {k: p.grad.detach().cpu().double() for k, p in m.named_parameters()})
+        del m
+    el = {k: norm_rel(res[k][0], ref["logits"]) for k in res}
+    assert el[1] <= 1e-5 and el[1] <= 1.25 * el[0] + 1e-8, el
+    worst = {k: max(norm_rel(res[k][1][n], g) for n, g in ref["grads"].items()) for k in res}
+    print(f"logits vs fp64: x3 {el[1]:.2e} f32 {el[0]:.2e}; worst grad: x3 {worst[1]:.2e} "
+          f"f32 {worst[0]:.2e}")
+    assert worst[1] <= 1.25 * max(worst[0], 1e-2), worst
+
+
+@pytest.mark.parametrize("B,H,W", [(2, 128, 128), (1, 48, 80)])
+def test_x3_row_tile_choice_bit_identical(B, H, W):
+    """Every x3 row-GEMM tile (0 = 256x128, 1 = 128x128, 2 = 128x64; -1 = the per-GEMM
+    choice) walks K in the same chunk order with the same six-product MFMA sequence per
+    element and emits BN partials in the same 128-row groups, so one training step -- logits
+    and the whole gradient arena -- is bit-identical across them (48x80: tiles ending past
+    M, the guarded epilogue)."""
+    import unet_hip
+    from _helpers import options
+    x, t = inputs(13, B, H, W)
+    outs = []
+    for tile in (-1, 0, 1, 2):
+        m = hip_model(O.make_params(42), DEV)
+        with options(m.flatten_().rt, x3_tile=tile):
+            logits = m(x.to(DEV))
+            l = unet_hip.seg_losses(logits, t.to(DEV))
+            (l[0] + l[1]).backward()
+            torch.cuda.synchronize()
+        outs.append((logits.detach().clone(), m._state.grad_arena.clone()))
+        del m
+    for i in range(1, len(outs)):
+        assert torch.equal(outs[0][0], outs[i][0]), i
+        assert torch.equal(outs[0][1], outs[i][1]), (i, (outs[0][1] - outs[i][1]).abs().max().item())

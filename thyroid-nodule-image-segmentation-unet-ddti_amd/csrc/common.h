@@ -149,6 +149,23 @@ int launch_wgrad(const WgradArgs& a, int tile, hipStream_t s);
 int launch_wgrad16(const WgradArgs& a, int tile, hipStream_t s);
 int wgrad_tile_dims(int tile, int* bm, int* bn, int* bkp);
 int wgrad_tile_taps(int tile);  // taps of the M dimension one block covers (3 for 20..)
+// f32 GEMMs on bf16 MFMAs through exact three-way operand splits (kernels_gemm_x3.hip):
+// x3 images bf16 [rows][C / 32][3][32] (hi, mid, lo planes per 32-channel group).  Row GEMM:
+// a16 / bt16 are x3 images (lda channels per A row, aoff a channel offset); tiles 0 =
+// 256x128, 1 = 128x128, 2 = 128x64.  Weight gradient: a / b are x3 images; tiles 0 = 128x128,
+// 1 = 64x64.
+int launch_rowgemm_x3(const RowGemmArgs& a, int tile, hipStream_t s);
+int rowgemm_x3_tile_dims(int tile, int* bm, int* bn);
+int launch_wgrad_x3(const WgradArgs& a, int tile, hipStream_t s);
+int wgrad_x3_tile_dims(int tile, int* bm, int* bn);
+// x3 image of op(src) (BN affine if scale, ReLU on channels < relu) into dst [P][dld] at
+// channel offset doff
+int k_to_x3(const float* src, int ld, int off, int C, const float* scale, const float* shift,
+            int relu, int64_t P, uint16_t* dst, int dld, int doff, hipStream_t s);
+// BN-backward dz (bn_dz4) as an x3 image; bpart (optional): [x3_dz_blocks(P)][C] column sums
+int k_bn_dz_x3(const float* d, const float* y, int ld, int off, int64_t P, int C, const float* coef,
+               int mask, uint16_t* dz3, float* bpart, hipStream_t s);
+int x3_dz_blocks(int64_t P);
 // register-staged bf16 wgrad tile ids (a.bf16): 0 = 128x128/32 px, 2 = 64x64/64,
 // 3 = 128x64/64, 4 = 64x128/64
 int wgrad16_tile_dims(int tile, int* bm, int* bn, int* bkp);

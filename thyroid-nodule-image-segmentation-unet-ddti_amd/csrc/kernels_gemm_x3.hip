@@ -62,9 +62,21 @@ __device__ __forceinline__ f32x16 mfma_x3(const bf16x8 (&a)[3], const bf16x8 (&b
     return mfma32_bf16(a[0], b[0], c);
 }
 
-template <int BM_, int BN_, int WM_, int WN_, int S_, int OCC_>
+// the same with the five small products in their own accumulator (split accumulation: the
+// large one then takes one rounding per 16 products)
+__device__ __forceinline__ void mfma_x3s(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f32x16& hi,
+                                         f32x16& lo) {
+    lo = mfma32_bf16(a[2], b[0], lo);
+    lo = mfma32_bf16(a[1], b[1], lo);
+    lo = mfma32_bf16(a[0], b[2], lo);
+    lo = mfma32_bf16(a[1], b[0], lo);
+    lo = mfma32_bf16(a[0], b[1], lo);
+    hi = mfma32_bf16(a[0], b[0], hi);
+}
+
+template <int BM_, int BN_, int WM_, int WN_, int S_, int OCC_, int SA_ = 0>
 struct TileX3 {
-    static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, S = S_, OCC = OCC_;
+    static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, S = S_, OCC = OCC_, SA = SA_;
     static constexpr int BK = 32;  // K per chunk (one tap, 32 channels), per plane
     static constexpr int WAVES = (BM / WM) * (BN / WN);
     static constexpr int THREADS = 64 * WAVES;
@@ -140,13 +152,17 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_x3_kernel(RowGemmA
             x3_dma16(bsrc[j] + k0 * 3, base + BM * RB + (j * WAVES + wave) * 1024);
     };
 
-    f32x16 acc[MT][NT];
+    constexpr int SA = T::SA;
+    f32x16 acc[MT][NT], acl[SA ? MT : 1][SA ? NT : 1];
 #pragma unroll
     for (int i = 0; i < MT; ++i)
 #pragma unroll
         for (int j = 0; j < NT; ++j)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+            for (int r = 0; r < 16; ++r) {
+                acc[i][j][r] = 0.f;
+                if constexpr (SA) acl[i][j][r] = 0.f;
+            }
 
     const int li = lane & 31, lh = lane >> 5;
     int aro[MT], afx[MT], bro[NT], bfx[NT];
@@ -202,23 +218,30 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_x3_kernel(RowGemmA
 #pragma unroll
             for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-                for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma_x3(af[mt], bfr[nt], acc[mt][nt]);
+                for (int nt = 0; nt < NT; ++nt) {
+                    if constexpr (SA) mfma_x3s(af[mt], bfr[nt], acc[mt][nt], acl[mt][nt]);
+                    else acc[mt][nt] = mfma_x3(af[mt], bfr[nt], acc[mt][nt]);
+                }
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         x3_barrier();
     }
+    if constexpr (SA) {
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) acc[mt][nt] += acl[mt][nt];
+    }
     row_epilogue<EMODE, BM, BN, WM, WN, true>(p, acc, m0, n0, tile_m, wm, wn, lane, tid, (float*)smem);
 }
 
-// tiles: 0 = 256x128 (8 waves of 64x64, 2 stages, 144 KB), 1 = 128x128 (4 waves of 64x64,
-// 3 stages), 2 = 256x64 (4 waves of 64x64, 2 stages), 3 = 256x128 (4 waves of 128x64),
-// 4 = 128x128 (4 waves, 2 stages: 96 KB)
-using TX0 = TileX3<256, 128, 64, 64, 2, 1>;
-using TX1 = TileX3<128, 128, 64, 64, 3, 1>;
-using TX2 = TileX3<256, 64, 64, 64, 2, 1>;
-using TX3 = TileX3<256, 128, 128, 64, 2, 1>;
-using TX4 = TileX3<128, 128, 64, 64, 2, 1>;
-#define ROWGEMM_X3_TILES(X) X(0, TX0) X(1, TX1) X(2, TX2) X(3, TX3) X(4, TX4)
+// tiles (split accumulators; probe: profiles/r04_x3_probe_*.txt): 0 = 256x128 (8 waves of
+// 64x64, 2 stages, 144 KB, one block per CU), 1 = 128x128 (4 waves, 2 stages: grids below 256
+// blocks of tile 0), 2 = 128x64 (4 waves of 64x32, two blocks per CU: the 64-output layers)
+using TX0 = TileX3<256, 128, 64, 64, 2, 1, 1>;
+using TX1 = TileX3<128, 128, 64, 64, 2, 1, 1>;
+using TX2 = TileX3<128, 64, 64, 32, 2, 2, 1>;
+#define ROWGEMM_X3_TILES(X) X(0, TX0) X(1, TX1) X(2, TX2)
 
 template <int AMODE, int EMODE, class T>
 static int x3_go(const RowGemmArgs& a, hipStream_t s) {
@@ -236,6 +259,255 @@ static int x3_tile(const RowGemmArgs& a, int tile, hipStream_t s) {
     ROWGEMM_X3_TILES(X3_CASE)
 #undef X3_CASE
     return -1;
+}
+
+// ------------------------------------------------------------------------------------
+// Weight gradient on x3 images: dW[m][n] = sum_p A'[p][m] * B'[p][n] over the pixels p of
+// one split (slab[split], reduced in fixed order by k_slab_reduce).  A' = gather of the
+// conv input's x3 image (tap = m / CA), B' = the x3 image of dz (G_IDENT) or of the ConvT
+// output gradient (G_UP2, tap = n / CB).  The MFMA wants 8 consecutive PIXELS of one channel
+// per lane: LDS holds [BKP pixel rows][BM / 32 groups][3 planes][32] (the x3 row as it lies in
+// HBM, RA = 6 BM bytes) and the fragments come from ds_read_b64_tr_b16 (lane i of a 16-lane
+// group receives column i of a 4-row x 16-column block), as wgrad16_kernel, the 16-B slots
+// of each pixel row permuted by x3_tswz.
+// ------------------------------------------------------------------------------------
+typedef short x3_short4 __attribute__((ext_vector_type(4)));
+
+// LDS slot of global 16-B slot sl in pixel row `row` of an RB-byte stage row (an involution,
+// used by the loader and the reader alike): the four rows a 32-lane half reads (rows r0..r0+3,
+// 64 B of one plane each) must fall into four different 64-B bank quarters.  RB % 256 == 0:
+// XOR the quarter by row & 3; RB % 256 == 128 (BM = 64): rows r, r + 1 already differ by half
+// a bank row, XOR by bit 1 of the row; RB = 192 (BM = 32): the rows are spread already.
+template <int RB>
+__device__ __forceinline__ int x3_tswz(int sl, int row) {
+    if constexpr (RB % 256 == 0) return sl ^ ((row & 3) << 2);
+    else if constexpr (RB % 256 == 128) return sl ^ (((row >> 1) & 1) << 2);
+    else return sl;
+}
+
+template <int OFF>
+__device__ __forceinline__ x3_short4 x3_tr16(unsigned addr) {
+    x3_short4 r;
+    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(OFF));
+    return r;
+}
+
+__device__ __forceinline__ unsigned x3_lds_u32(const void* p) {
+    return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+
+template <int BM_, int BN_, int WM_, int WN_, int S_, int SA_ = 0>
+struct WTileX3 {
+    static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, S = S_, SA = SA_;
+    static constexpr int BKP = 32;  // pixels per chunk (two 16-pixel k-steps)
+    static constexpr int WAVES = (BM / WM) * (BN / WN);
+    static constexpr int THREADS = 64 * WAVES;
+};
+
+template <int AMODE, int BMODE, class T>
+__global__ __launch_bounds__(T::THREADS, 1) void wgrad_x3_kernel(WgradArgs p) {
+    constexpr int BM = T::BM, BN = T::BN, WM = T::WM, WN = T::WN, BKP = T::BKP, S = T::S;
+    constexpr int WAVES = T::WAVES, WAVES_N = BN / WN;
+    constexpr int MT = WM / 32, NT = WN / 32;
+    constexpr int RA = 6 * BM, RBB = 6 * BN;  // bytes per pixel row of the A' / B' stage images
+    static_assert((BKP * RA) % (1024 * WAVES) == 0 && (BKP * RBB) % (1024 * WAVES) == 0, "loader");
+    constexpr int AI = BKP * RA / (1024 * WAVES), BI = BKP * RBB / (1024 * WAVES);
+    constexpr int GPC = AI + BI;
+    static_assert(S >= 2 && S <= 3, "stages");
+    constexpr int STAGE = BKP * (RA + RBB);
+    __shared__ __attribute__((aligned(1024))) char smem[STAGE * S];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+    const int tiles_n = p.Nw / BN, tiles_m = p.Mw / BM;
+    int idx = p.xcd ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+    const int tn = idx % tiles_n;
+    idx /= tiles_n;
+    const int tm = idx % tiles_m;
+    const int split = idx / tiles_m;
+    const int tapA = (tm * BM) / p.CA, ca0 = tm * BM - tapA * p.CA;
+    const int tapB = (tn * BN) / p.CB, cb0 = tn * BN - tapB * p.CB;
+    const int H = p.H, W = p.W;
+    const float rH = 1.f / (float)H, rW = 1.f / (float)W;
+    const int pbeg = split * p.pps;
+    const int pend = min(pbeg + p.pps, p.P);
+    const int nk = (pend - pbeg + BKP - 1) / BKP;
+
+    // loader: lane of instruction j fills stage byte o = (j WAVES + wave) KB + 16 lane: pixel
+    // row o / RA, 16-B slot s = (o % RA) / 16, sourcing global slot x3_tswz(s, row) of the
+    // row's x3 segment
+    int arow[AI], aele[AI], brow[BI], bele[BI];
+#pragma unroll
+    for (int j = 0; j < AI; ++j) {
+        const int o = ((j * WAVES + wave) * 64 + lane) * 16;
+        const int r = o / RA, sl = (o - r * RA) >> 4;
+        arow[j] = r;
+        aele[j] = x3_tswz<RA>(sl, r) * 8;
+    }
+#pragma unroll
+    for (int j = 0; j < BI; ++j) {
+        const int o = ((j * WAVES + wave) * 64 + lane) * 16;
+        const int r = o / RBB, sl = (o - r * RBB) >> 4;
+        brow[j] = r;
+        bele[j] = x3_tswz<RBB>(sl, r) * 8;
+    }
+    const uint16_t* a16 = (const uint16_t*)p.a + (size_t)(p.aoff + ca0) * 3;
+    const uint16_t* b16 = (const uint16_t*)p.b + (size_t)(p.boff + cb0) * 3;
+    const size_t rowa = 3 * (size_t)p.lda, rowb = 3 * (size_t)p.ldb;
+    const uint16_t* zero = (const uint16_t*)p.zero16;
+
+    auto issue = [&](int kc, int st) {
+        const int pc = pbeg + kc * BKP;
+        char* base = smem + st * STAGE;
+#pragma unroll
+        for (int j = 0; j < AI; ++j) {
+            const int pix = pc + arow[j];
+            const bool in = pix < pend;
+            const int m = in ? pix : pend - 1;
+            bool valid;
+            const Pix q = AMODE == G_IDENT ? Pix{0, 0, 0} : decode_fast(m, H, W, rH, rW);
+            const int src = gather_src<AMODE>(tapA, m, q, H, W, valid);
+            const uint16_t* g = (valid && in) ? a16 + (size_t)src * rowa + aele[j] : zero;
+            x3_dma16(g, base + (j * WAVES + wave) * 1024);
+        }
+#pragma unroll
+        for (int j = 0; j < BI; ++j) {
+            const int pix = pc + brow[j];
+            const bool in = pix < pend;
+            const int m = in ? pix : pend - 1;
+            bool valid;
+            const Pix q = BMODE == G_IDENT ? Pix{0, 0, 0} : decode_fast(m, H, W, rH, rW);
+            const int src = gather_src<BMODE>(tapB, m, q, H, W, valid);
+            const uint16_t* g = (valid && in) ? b16 + (size_t)src * rowb + bele[j] : zero;
+            x3_dma16(g, base + BKP * RA + (j * WAVES + wave) * 1024);
+        }
+    };
+
+    constexpr int SA = T::SA;
+    f32x16 acc[MT][NT], acl[SA ? MT : 1][SA ? NT : 1];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                acc[i][j][r] = 0.f;
+                if constexpr (SA) acl[i][j][r] = 0.f;
+            }
+
+    // transposed-read addresses (bytes within a stage, k-step 0): lane l of group g = l / 16
+    // supplies row 8 (g >> 1) + qq, columns 16 (g & 1) + 4 pp (l % 16 = 4 qq + pp) of plane q
+    const int g = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
+    const int trow = 8 * (g >> 1) + qq;  // + 4 t + 16 kk: (row & 3) stays qq
+    auto slot = [](int col, int q) { return (col >> 5) * 12 + q * 4 + ((col & 31) >> 3); };
+    int aoff[MT][3], boff[NT][3];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            const int col = wm * WM + mt * 32 + 16 * (g & 1) + 4 * pp;
+            aoff[mt][q] = trow * RA + (x3_tswz<RA>(slot(col, q), trow) << 4) + ((col >> 2) & 1) * 8;
+        }
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            const int col = wn * WN + nt * 32 + 16 * (g & 1) + 4 * pp;
+            boff[nt][q] = BKP * RA + trow * RBB + (x3_tswz<RBB>(slot(col, q), trow) << 4) + ((col >> 2) & 1) * 8;
+        }
+
+#pragma unroll
+    for (int s = 0; s < S - 1; ++s)
+        if (s < nk) issue(s, s);
+    for (int kc = 0; kc < nk; ++kc) {
+        if (kc + S - 1 < nk) issue(kc + S - 1, (kc + S - 1) % S);
+        const int ahead = min(S - 1, nk - 1 - kc);
+        if constexpr (S >= 3) {
+            if (ahead >= 2) x3_wait_vm<2 * GPC>();
+            else if (ahead == 1) x3_wait_vm<GPC>();
+            else x3_wait_vm<0>();
+        } else {
+            if (ahead >= 1) x3_wait_vm<GPC>();
+            else x3_wait_vm<0>();
+        }
+        x3_barrier();
+        const unsigned sb = x3_lds_u32(smem) + (kc % S) * STAGE;
+        x3_short4 fa[2][MT][3][2], fb[2][NT][3][2];
+        auto load = [&](auto KK) {
+            constexpr int kk = decltype(KK)::value;
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                for (int q = 0; q < 3; ++q) {
+                    fa[kk][mt][q][0] = x3_tr16<kk * 16 * RA>(sb + aoff[mt][q]);
+                    fa[kk][mt][q][1] = x3_tr16<kk * 16 * RA + 4 * RA>(sb + aoff[mt][q]);
+                }
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+                for (int q = 0; q < 3; ++q) {
+                    fb[kk][nt][q][0] = x3_tr16<kk * 16 * RBB>(sb + boff[nt][q]);
+                    fb[kk][nt][q][1] = x3_tr16<kk * 16 * RBB + 4 * RBB>(sb + boff[nt][q]);
+                }
+        };
+        auto mma = [&](auto KK) {
+            constexpr int kk = decltype(KK)::value;
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt) {
+                    bf16x8 a3[3], b3[3];
+#pragma unroll
+                    for (int q = 0; q < 3; ++q) {
+                        a3[q] = *(const bf16x8*)fa[kk][mt][q];
+                        b3[q] = *(const bf16x8*)fb[kk][nt][q];
+                    }
+                    if constexpr (SA) mfma_x3s(a3, b3, acc[mt][nt], acl[mt][nt]);
+                    else acc[mt][nt] = mfma_x3(a3, b3, acc[mt][nt]);
+                }
+        };
+        static_assert(BKP == 32, "two k-steps per chunk");
+        load(std::integral_constant<int, 0>{});
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        load(std::integral_constant<int, 1>{});
+        __builtin_amdgcn_sched_barrier(0);
+        mma(std::integral_constant<int, 0>{});
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        mma(std::integral_constant<int, 1>{});
+        x3_barrier();
+    }
+
+    const int li = lane & 31, lh = lane >> 5;
+    float* slab = p.slab + (size_t)split * p.Mw * p.Nw;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = tm * BM + wm * WM + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                const int n = tn * BN + wn * WN + nt * 32 + li;
+                slab[(size_t)m * p.Nw + n] = SA ? acc[mt][nt][r] + acl[SA ? mt : 0][SA ? nt : 0][r]
+                                                : acc[mt][nt][r];
+            }
+}
+
+// tiles (split accumulators): 0 = 128x128 (8 waves of 64x32), 1 = 64x64 (4 waves of 32x32);
+// three LDS stages of 32 pixels
+using WX0 = WTileX3<128, 128, 64, 32, 3, 1>;
+using WX1 = WTileX3<64, 64, 32, 32, 3, 1>;
+#define WGRAD_X3_TILES(X) X(0, WX0) X(1, WX1)
+
+template <int AMODE, int BMODE, class T>
+static int wx3_go(const WgradArgs& a, hipStream_t s) {
+    if (a.Mw % T::BM || a.Nw % T::BN || a.CA % T::BM || a.CB % T::BN || a.pps % T::BKP) return -1;
+    const dim3 grid((a.Mw / T::BM) * (a.Nw / T::BN) * a.splits);
+    hipLaunchKernelGGL((wgrad_x3_kernel<AMODE, BMODE, T>), grid, dim3(T::THREADS), 0, s, a);
+    return (int)hipGetLastError();
 }
 
 // x3 image of op(src) (f32 [P][ld] at channel offset off, C channels; scale / shift: the
@@ -277,6 +549,71 @@ __global__ void to_x3_kernel(const float* __restrict__ src, int ld, int off, int
         *(bf16x8*)d = h;
         *(bf16x8*)(d + 32) = m;
         *(bf16x8*)(d + 64) = l;
+    }
+}
+
+// dz = [!mask || y > 0] (A do + B (y - mean) + C) per channel (bn_dz4, the f32 path's
+// rounding order) as the x3 image dz3 [P][C / 32][3][32]; with bpart, also the per-block
+// column sums of dz (the conv bias gradient; k_sum_partials adds the G rows in f64).  A
+// block covers RPB rows; thread t handles channel octet t % (C / 8) of rows t / (C / 8) +
+// k 256 / (C / 8).
+constexpr int X3_DZ_RPB = 256;
+__global__ __launch_bounds__(256) void bn_dz_x3_kernel(const float* __restrict__ d, const float* __restrict__ y,
+                                                       int ld, int off, int64_t P, int C,
+                                                       const float* __restrict__ coef, int mask,
+                                                       uint16_t* __restrict__ dz3, float* __restrict__ bpart) {
+    __shared__ float red[256 * 8];
+    const int g8 = C / 8;
+    const int oct = threadIdx.x % g8, r0 = threadIdx.x / g8, rstep = 256 / g8;
+    const int c = oct * 8;
+    const bool active = r0 < rstep;  // threads past the last complete row group idle
+    f32x4 ka[2], kb[2], kc[2], km[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        ka[h] = *(const f32x4*)(coef + c + 4 * h);
+        kb[h] = *(const f32x4*)(coef + C + c + 4 * h);
+        kc[h] = *(const f32x4*)(coef + 2 * C + c + 4 * h);
+        km[h] = *(const f32x4*)(coef + 3 * C + c + 4 * h);
+    }
+    float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const int64_t mb = (int64_t)blockIdx.x * X3_DZ_RPB;
+    const int64_t me = min(mb + X3_DZ_RPB, P);
+    for (int64_t m = mb + r0; active && m < me; m += rstep) {
+        float v[8];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const f32x4 dv = *(const f32x4*)(d + m * C + c + 4 * h);
+            const f32x4 yv = *(const f32x4*)(y + m * ld + off + c + 4 * h);
+            const f32x4 r = bn_dz4(ka[h], dv, kb[h], yv, km[h], kc[h]);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[4 * h + j] = (!mask || yv[j] > 0.f) ? r[j] : 0.f;
+        }
+        bf16x8 hi, mi, lo;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const __bf16 hj = (__bf16)v[j];
+            const float r1 = v[j] - (float)hj;
+            const __bf16 mj = (__bf16)r1;
+            hi[j] = hj;
+            mi[j] = mj;
+            lo[j] = (__bf16)(r1 - (float)mj);
+            cs[j] += v[j];
+        }
+        uint16_t* o = dz3 + m * 3 * (int64_t)C + (c >> 5) * 96 + (c & 31);
+        *(bf16x8*)o = hi;
+        *(bf16x8*)(o + 32) = mi;
+        *(bf16x8*)(o + 64) = lo;
+    }
+    if (!bpart) return;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[threadIdx.x * 8 + j] = active ? cs[j] : 0.f;
+    __syncthreads();
+    // column c + j: the rstep row groups' sums in fixed order
+    for (int i = threadIdx.x; i < C; i += 256) {
+        const int o8 = i >> 3, j = i & 7;
+        float a = 0.f;
+        for (int r = 0; r < rstep; ++r) a += red[(r * g8 + o8) * 8 + j];
+        bpart[(size_t)blockIdx.x * C + i] = a;
     }
 }
 
@@ -322,5 +659,45 @@ int k_to_x3(const float* src, int ld, int off, int C, const float* scale, const 
     const int blocks = (int)std::min<int64_t>((n + 255) / 256, 8192);
     hipLaunchKernelGGL(to_x3_kernel, dim3(blocks), dim3(256), 0, s, src, ld, off, C, scale, shift,
                        relu, P, dst, dld, doff);
+    return (int)hipGetLastError();
+}
+
+int wgrad_x3_tile_dims(int tile, int* bm, int* bn) {
+#define WX3_DIMS(id, T) \
+    if (tile == id) {   \
+        *bm = T::BM;    \
+        *bn = T::BN;    \
+        return 0;       \
+    }
+    WGRAD_X3_TILES(WX3_DIMS)
+#undef WX3_DIMS
+    return -1;
+}
+
+// Weight gradient from x3 images: a / b point at uint16 x3 images (lda / ldb channels per
+// row, channel offsets aoff / boff multiples of 32), zero16 at a zeroed page.  3x3 conv (A'
+// G_CONV3, B' G_IDENT) and ConvT (A' G_IDENT, B' G_UP2); no bias column sums.
+int launch_wgrad_x3(const WgradArgs& a, int tile, hipStream_t s) {
+    if (a.ascale || a.bcoef || a.bias_slab || !a.zero16 || a.P < 1) return -1;
+    if (a.aoff % 32 || a.boff % 32 || a.lda % 32 || a.ldb % 32) return -1;
+#define WX3G(AM, BMD)                                      \
+    do {                                                   \
+        if (tile == 0) return wx3_go<AM, BMD, WX0>(a, s);  \
+        if (tile == 1) return wx3_go<AM, BMD, WX1>(a, s);  \
+        return -1;                                         \
+    } while (0)
+    if (a.amode == G_CONV3 && a.bmode == G_IDENT) WX3G(G_CONV3, G_IDENT);
+    if (a.amode == G_IDENT && a.bmode == G_UP2) WX3G(G_IDENT, G_UP2);
+#undef WX3G
+    return -1;
+}
+
+int x3_dz_blocks(int64_t P) { return (int)((P + X3_DZ_RPB - 1) / X3_DZ_RPB); }
+
+int k_bn_dz_x3(const float* d, const float* y, int ld, int off, int64_t P, int C, const float* coef,
+               int mask, uint16_t* dz3, float* bpart, hipStream_t s) {
+    if (C % 32 || C > 2048 || ld % 4 || off % 4 || P < 1) return -1;
+    hipLaunchKernelGGL(bn_dz_x3_kernel, dim3(x3_dz_blocks(P)), dim3(256), 0, s, d, y, ld, off, P, C, coef,
+                       mask, dz3, bpart);
     return (int)hipGetLastError();
 }

@@ -151,6 +151,13 @@ struct Options {
                                // blocks re-reads do and y instead of dz, so the fusion pays
                                // where few A' tiles share a pixel slice (profiles/
                                // r03_tile_experiments.txt: Cin 64..256 gain, 512..1024 lose)
+    int x3 = 1;                // f32 math: conv / ConvT GEMMs whose channel counts are multiples
+                               // of 64 on the bf16 matrix cores through exact three-way operand
+                               // splits (kernels_gemm_x3.hip; fp64 error below the f32 MFMA
+                               // kernels'); 0 = the f32 MFMA kernels everywhere
+    int x3_tile = -1;          // its row-GEMM tile (-1 = x3_tile())
+    int x3_wtile = -1;         // its weight-gradient tile (-1 = by channel counts)
+    int x3_wblocks = 1536;     // split-K target (blocks) of its 128x128 weight gradients
 };
 struct OptionDesc {
     const char* name;
@@ -194,6 +201,10 @@ const OptionDesc OPTION_TABLE[] = {
     {"xcd16", &Options::xcd16},
     {"xcd_remap", &Options::xcd_remap},
     {"dz_in_wgrad", &Options::dz_in_wgrad},
+    {"x3", &Options::x3},
+    {"x3_tile", &Options::x3_tile},
+    {"x3_wtile", &Options::x3_wtile},
+    {"x3_wblocks", &Options::x3_wblocks},
 };
 
 }  // namespace
@@ -458,21 +469,23 @@ void build_graph(unet_ctx* c) {
             L.pf = L.pd = -1;
             continue;
         }
+        // (every image starts at a multiple of 32 floats: the x3 copy of the whole region,
+        // converted as rows of 32, then holds each image's x3 image at 3x its offset)
         L.pf = pk;
-        pk += n;
+        pk += (n + 31) / 32 * 32;
         L.pd = pk;
-        pk += n;
+        pk += (n + 31) / 32 * 32;
     }
     for (auto& T : c->convt) {
         const int64_t n = (int64_t)T.cin * T.cout * 4;
         T.pf = pk;
-        pk += n;
+        pk += (n + 31) / 32 * 32;
         T.pd = pk;
-        pk += n;
+        pk += (n + 31) / 32 * 32;
     }
     for (int b = 1; b < nb && c->res; ++b) {  // transposed skip images for the dgrad
         c->skip_pd[b] = pk;
-        pk += (int64_t)c->conv[2 * b].cin * c->conv[2 * b].cout;
+        pk += ((int64_t)c->conv[2 * b].cin * c->conv[2 * b].cout + 31) / 32 * 32;
     }
     c->pack_floats = pk;
     // gradient buckets: walk the arena from its end (what backward finishes first), open a
@@ -553,6 +566,12 @@ struct Plan {
     void* zero16;
     std::vector<uint16_t*> x16;  // training, bf16: per-conv input images kept for the wgrad
     std::vector<uint16_t*> t16;  // training, bf16: per-ConvT input images kept for the wgrad
+    // f32 GEMMs on split bf16 operands (option x3): x3 copy of the weight images, per-conv /
+    // per-ConvT input images kept for the weight gradients, one scratch image
+    uint16_t* pack3;
+    uint16_t* s3;
+    std::vector<uint16_t*> x3;
+    std::vector<uint16_t*> t3;
     // channel-padded networks: padded parameter / running-stat / gradient arenas and the
     // device copies of the expand / compact tables
     float* pprm;
@@ -716,6 +735,84 @@ bool convt_wg16_on(const unet_ctx* c, int cin, int cout) {
            rg16_on(c, cout, cin);
 }
 
+// f32 math on the bf16 matrix cores (option x3, kernels_gemm_x3.hip): a 3x3 conv / ConvT
+// whose in- and output channels are multiples of 64 runs its forward, input-gradient and
+// weight-gradient GEMMs on x3 images (exact three-way bf16 splits of the f32 operands, six
+// MFMA products, split f32 accumulators: fp64 error ~3x below the f32 MFMA kernels',
+// profiles/r04_x3_probe_*.txt).  The residual network keeps the f32 kernels.
+bool x3_conv_on(const unet_ctx* c, int cin, int cout) {
+    return c->opt.x3 && !c->bf16 && !c->res && cin % 64 == 0 && cout % 64 == 0;
+}
+bool x3_convt_on(const unet_ctx* c, int cin, int cout) { return x3_conv_on(c, cin, cout); }
+
+// row-GEMM tile: 256x128 (one block of 8 waves per CU) unless that grid leaves CUs idle
+// (128x128), 128x64 for the 64-output GEMMs
+int x3_tile(const unet_ctx* c, const RowGemmArgs& g) {
+    auto fits = [&](int t) {
+        int bm = 0, bn = 0;
+        if (rowgemm_x3_tile_dims(t, &bm, &bn) != 0 || g.N % bn) return false;
+        return g.emode != E_CONVT || g.cout % bn == 0 || bn % g.cout == 0;
+    };
+    if (c->opt.x3_tile >= 0 && fits(c->opt.x3_tile)) return c->opt.x3_tile;
+    if (g.N % 128 == 0 && fits(0)) {
+        const int64_t blocks = (int64_t)(g.M + 255) / 256 * (g.N / 128);
+        return blocks >= 256 ? 0 : 1;
+    }
+    return 2;
+}
+
+// weight gradient: 128x128 tile where both channel counts allow it, else 64x64; split-K over
+// pixels so the grid has >= x3_wblocks 128x128 blocks (4x that of 64x64 ones); pixels per
+// split a multiple of 256
+WgradCfg x3_wgrad_cfg(const unet_ctx* c, int CA, int tapsA, int CB, int tapsB, int64_t P) {
+    WgradCfg w{};
+    w.tile = (CA % 128 == 0 && CB % 128 == 0) ? 0 : 1;
+    if (c->opt.x3_wtile >= 0) {
+        int bm = 0, bn = 0;
+        if (wgrad_x3_tile_dims(c->opt.x3_wtile, &bm, &bn) == 0 && CA % bm == 0 && CB % bn == 0)
+            w.tile = c->opt.x3_wtile;
+    }
+    wgrad_x3_tile_dims(w.tile, &w.bm, &w.bn);
+    w.bkp = 32;
+    const int64_t tiles = (int64_t)(tapsA * CA / w.bm) * (tapsB * CB / w.bn);
+    const int64_t target = (int64_t)c->opt.x3_wblocks * (w.tile == 0 ? 1 : 4);
+    int64_t splits = std::max<int64_t>(1, (target + tiles - 1) / tiles);
+    int64_t pps = (P + splits - 1) / splits;
+    pps = (pps + 255) / 256 * 256;
+    w.pps = (int)pps;
+    w.splits = (int)((P + pps - 1) / pps);
+    return w;
+}
+
+// point g at x3 operands: A image `img` (lda = C channels), weights w3
+void use_x3(const Plan& p, RowGemmArgs& g, const uint16_t* img, int C, const uint16_t* w3) {
+    g.a = nullptr;
+    g.a16 = img;
+    g.lda = C;
+    g.aoff = 0;
+    g.ascale = g.ashift = nullptr;
+    g.arelu = 0;
+    g.acoef = nullptr;
+    g.bt = nullptr;
+    g.bt16 = w3;
+    g.zero16 = p.zero16;
+    g.xcd = 1;
+}
+
+std::string x3wlabel(const char* fam, const WgradCfg& w, int layer) {
+    char b[112];
+    snprintf(b, sizeof b, "%s/wx3_%dx%d|%d", fam, w.bm, w.bn, layer);
+    return b;
+}
+
+std::string xlabel(const char* fam, int tile, int layer) {
+    int bm = 0, bn = 0;
+    rowgemm_x3_tile_dims(tile, &bm, &bn);
+    char b[112];
+    snprintf(b, sizeof b, "%s/x3_%dx%d|%d", fam, bm, bn, layer);
+    return b;
+}
+
 void make_plan(unet_ctx* c, int N, int H, int W, bool training, char* base, Plan& p) {
     Bump b{base};
     const int D = c->depth, NC = c->nconv();
@@ -812,6 +909,30 @@ void make_plan(unet_ctx* c, int N, int H, int W, bool training, char* base, Plan
         if (!c->res && convt_wg16_on(c, T.cin, T.cout))
             p.t16[k] = b.take<uint16_t>(p.P[T.in_level] * T.cin);
     }
+    // option x3: weight images, kept input images, one scratch image (dz, the concat
+    // gradient's up half, and every input image of an inference pass)
+    p.pack3 = p.s3 = nullptr;
+    p.x3.assign(NC, nullptr);
+    p.t3.assign(c->convt.size(), nullptr);
+    {
+        int64_t n3 = 0;
+        for (int i = 0; i < NC; ++i) {
+            const ConvL& L = c->conv[i];
+            if (L.pf < 0 || !x3_conv_on(c, L.cin, L.cout)) continue;
+            n3 = std::max(n3, p.P[L.level] * std::max(L.cin, L.cout));
+            if (training) p.x3[i] = b.take<uint16_t>(3 * p.P[L.level] * L.cin);
+        }
+        for (size_t k = 0; k < c->convt.size(); ++k) {
+            const ConvTL& T = c->convt[k];
+            if (!x3_convt_on(c, T.cin, T.cout)) continue;
+            n3 = std::max(n3, std::max(p.P[T.in_level] * T.cin, p.P[T.in_level - 1] * T.cout));
+            if (training) p.t3[k] = b.take<uint16_t>(3 * p.P[T.in_level] * T.cin);
+        }
+        if (n3) {
+            p.pack3 = b.take<uint16_t>(3 * c->pack_floats);
+            p.s3 = b.take<uint16_t>(3 * n3);
+        }
+    }
     if (training) {
         int64_t gmax = p.P[0] * c->base;
         for (int i = 0; i < NC; ++i) {
@@ -825,7 +946,9 @@ void make_plan(unet_ctx* c, int N, int H, int W, bool training, char* base, Plan
         int64_t smax = 0, bmax = 0;
         for (int i = 1; i < NC; ++i) {
             const ConvL& L = c->conv[i];
-            WgradCfg w = wgrad_cfg(c, L.cin, 9, L.cout, 1, p.P[L.level], c->bf16, W >> L.level);
+            WgradCfg w = x3_conv_on(c, L.cin, L.cout)
+                             ? x3_wgrad_cfg(c, L.cin, 9, L.cout, 1, p.P[L.level])
+                             : wgrad_cfg(c, L.cin, 9, L.cout, 1, p.P[L.level], c->bf16, W >> L.level);
             smax = std::max(smax, (int64_t)w.splits * 9 * L.cin * L.cout);
             bmax = std::max(bmax, (int64_t)w.splits * L.cout);
         }
@@ -835,7 +958,9 @@ void make_plan(unet_ctx* c, int N, int H, int W, bool training, char* base, Plan
             smax = std::max(smax, (int64_t)w.splits * L.cin * L.cout);
         }
         for (const ConvTL& T : c->convt) {
-            WgradCfg w = wgrad_cfg(c, T.cin, 1, T.cout, 4, p.P[T.in_level], c->bf16);
+            WgradCfg w = x3_convt_on(c, T.cin, T.cout) && !c->res
+                             ? x3_wgrad_cfg(c, T.cin, 1, T.cout, 4, p.P[T.in_level])
+                             : wgrad_cfg(c, T.cin, 1, T.cout, 4, p.P[T.in_level], c->bf16);
             smax = std::max(smax, (int64_t)w.splits * T.cin * 4 * T.cout);
             bmax = std::max(bmax, (int64_t)w.splits * 4 * T.cout);
         }
@@ -1076,6 +1201,10 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
             if (jobs.n < MAX_PACK_JOBS) add(T.w, T.pf, T.pd, T.cin, T.cout, 1);
         if (jobs.n >= MAX_PACK_JOBS) return fail(c, UNET_ERR_INTERNAL, "pack job table full");
         if (jobs.n) RUN("pack", 0, k_pack_all(jobs, prm, p.pack, c->bf16, s));
+        // option x3: the whole region as rows of 32 floats (every image 32-aligned)
+        if (p.pack3)
+            RUN("pack", 0, k_to_x3(p.pack, 32, 0, 32, nullptr, nullptr, 0, c->pack_floats / 32, p.pack3,
+                                   32, 0, s));
     }
     for (int b = 1; b <= 2 * D && c->res && training; ++b)
         RUN("pack", 0, k_pack_1x1_t(prm + c->skip_w[b], p.pack + c->skip_pd[b], c->conv[2 * b].cin,
@@ -1128,6 +1257,16 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
             g.bias = bias_ptr(prm, C.b);
             g.stats = p.stats;
             g.emode = c->bn_relu ? E_STATS : E_BIAS_RELU_STATS;
+            if (p.pack3 && x3_conv_on(c, C.cin, C.cout)) {
+                uint16_t* img = p.x3[i] ? p.x3[i] : p.s3;
+                RUN("prep_x3", 0, k_to_x3(a.ptr, a.ld, a.off, C.cin, a.scale, a.shift, a.relu, M, img,
+                                          C.cin, 0, s));
+                use_x3(p, g, img, C.cin, p.pack3 + 3 * C.pf);
+                const int tile = x3_tile(c, g);
+                R = bn_groups(M);
+                RUN(xlabel("conv_fwd", tile, i), 2.0 * M * C.cout * 9 * C.cin, launch_rowgemm_x3(g, tile, s));
+                return stats_finalize(c, L, p, i, R, M, training, prm, bn_run, bn_cnt);
+            }
             if (rg16_on(c, C.cin, C.cout)) {
                 uint16_t* img = p.x16[i] ? p.x16[i] : p.s16;
                 if (up16[i]) {  // the ConvT stored the up half already: convert the skip half
@@ -1185,6 +1324,15 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
         g.bias = prm + T.b;
         g.cout = T.cout;
         g.emode = E_CONVT;
+        if (!c->res && p.pack3 && x3_convt_on(c, T.cin, T.cout)) {
+            uint16_t* img = p.t3[k] ? p.t3[k] : p.s3;
+            RUN("prep_x3", 0, k_to_x3(g.a, g.lda, g.aoff, T.cin, g.ascale, g.ashift, g.arelu, g.M, img,
+                                      T.cin, 0, s));
+            use_x3(p, g, img, T.cin, p.pack3 + 3 * T.pf);
+            const int tile = x3_tile(c, g);
+            RUN(xlabel("convT_fwd", tile, 100 + k), 2.0 * g.M * g.N * g.K, launch_rowgemm_x3(g, tile, s));
+            return 0;
+        }
         if (!c->res && rg16_on(c, T.cin, T.cout)) {
             uint16_t* img = p.t16[k] ? p.t16[k] : p.s16;
             RUN("prep16", 0, k_to_bf16(g.a, g.lda, g.aoff, T.cin, g.ascale, g.ashift, g.arelu, g.M,
@@ -1330,6 +1478,66 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
                                    C.b >= 0 ? grads + C.b : nullptr, s));
             return 0;
         }
+        if (p.pack3 && x3_conv_on(c, C.cin, C.cout)) {
+            // option x3: dz as an x3 image (and the conv bias's column partials), the weight
+            // gradient from the forward's kept input image and dz, the input gradient from dz
+            float* bp = C.b >= 0 ? p.part : nullptr;
+            RUN("bn_dz", 0, k_bn_dz_x3(dout, p.y[i], p.ldy[i], p.offy[i], P, C.cout, p.coef, dz_mask,
+                                      p.s3, bp, s));
+            if (bp) RUN("bias_grad", 0, k_sum_partials(p.part, x3_dz_blocks(P), C.cout, grads + C.b, s));
+            const WgradCfg wc = x3_wgrad_cfg(c, C.cin, 9, C.cout, 1, P);
+            WgradArgs w{};
+            w.xcd = 1;
+            w.H = Hl;
+            w.W = Wl;
+            w.P = (int)P;
+            w.a = (const float*)p.x3[i];
+            w.lda = C.cin;
+            w.CA = C.cin;
+            w.amode = G_CONV3;
+            w.b = (const float*)p.s3;
+            w.ldb = C.cout;
+            w.CB = C.cout;
+            w.bmode = G_IDENT;
+            w.Mw = 9 * C.cin;
+            w.Nw = C.cout;
+            w.pps = wc.pps;
+            w.splits = wc.splits;
+            w.slab = p.slab;
+            w.zero16 = p.zero16;
+            RUN(x3wlabel("conv_wgrad", wc, i), 2.0 * P * C.cout * 9 * C.cin, launch_wgrad_x3(w, wc.tile, s));
+            RUN("wgrad_reduce", 0,
+                k_slab_reduce(p.slab, wc.splits, w.Mw, w.Nw, 0, C.cin, C.cout, grads + C.w, s));
+            if (!dx) return 0;
+            RowGemmArgs g{};
+            g.H = Hl;
+            g.W = Wl;
+            g.M = (int)P;
+            g.N = C.cin;
+            g.K = 9 * C.cout;
+            g.C = C.cout;
+            g.amode = G_CONV3;
+            use_x3(p, g, p.s3, C.cout, p.pack3 + 3 * C.pd);
+            g.out = dx;
+            g.ldo = ldx;
+            g.ooff = 0;
+            g.emode = accumulate ? E_ADD : E_STORE;
+            if (bn_next) {
+                g.emode = E_STORE_BN;
+                g.ey = p.y[i - 1];
+                g.ldey = p.ldy[i - 1];
+                g.offey = p.offy[i - 1];
+                if (c->bn_relu) {
+                    g.escale = p.scale[i - 1];
+                    g.eshift = p.shift[i - 1];
+                }
+                g.stats = p.part;
+            }
+            const int tile = x3_tile(c, g);
+            if (rows) *rows = bn_groups(P);
+            RUN(xlabel("conv_dgrad", tile, i), 2.0 * P * C.cout * 9 * C.cin, launch_rowgemm_x3(g, tile, s));
+            return 0;
+        }
         // bf16 image of dz: A operand of the LDS-DMA dgrad, B' of the LDS-DMA wgrad; the f32
         // dz is still written when the register-staged kernel of either consumes it
         const bool dz16 = rg16_on(c, C.cout, C.cin) || p.x16[i];
@@ -1467,6 +1675,65 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         const int ldo = 2 * c->ch(lo), uo = c->up_off(lo);
         const int Hi = H >> T.in_level, Wi = W >> T.in_level;
         const int64_t Pin = p.P[T.in_level];
+        if (!c->res && p.pack3 && x3_convt_on(c, T.cin, T.cout)) {
+            // option x3: the up half of the concat gradient as an x3 image feeds the weight
+            // gradient (B', gathered 2x2) and the input gradient (A)
+            RUN("prep_x3", 0, k_to_x3(p.dcat[lo], ldo, uo, T.cout, nullptr, nullptr, 0, p.P[lo], p.s3,
+                                      T.cout, 0, s));
+            const WgradCfg wc = x3_wgrad_cfg(c, T.cin, 1, T.cout, 4, Pin);
+            WgradArgs w{};
+            w.xcd = 1;
+            w.H = Hi;
+            w.W = Wi;
+            w.P = (int)Pin;
+            w.a = (const float*)p.t3[k];
+            w.lda = T.cin;
+            w.CA = T.cin;
+            w.amode = G_IDENT;
+            w.b = (const float*)p.s3;
+            w.ldb = T.cout;
+            w.CB = T.cout;
+            w.bmode = G_UP2;
+            w.Mw = T.cin;
+            w.Nw = 4 * T.cout;
+            w.pps = wc.pps;
+            w.splits = wc.splits;
+            w.slab = p.slab;
+            w.zero16 = p.zero16;
+            RUN(x3wlabel("convT_wgrad", wc, 100 + k), 2.0 * Pin * T.cin * 4 * T.cout,
+                launch_wgrad_x3(w, wc.tile, s));
+            RUN("bias_grad", 0, k_up2_bias_partials(p.dcat[lo], ldo, uo, Hi, Wi, Pin, T.cout, wc.pps,
+                                                    wc.splits, p.bslab, s));
+            RUN("wgrad_reduce", 0,
+                k_slab_reduce(p.slab, wc.splits, w.Mw, w.Nw, 1, T.cin, T.cout, grads + T.w, s));
+            RUN("bias_grad", 0, k_bias_reduce(p.bslab, wc.splits, 4, T.cout, grads + T.b, s));
+            RowGemmArgs g{};
+            g.H = Hi;
+            g.W = Wi;
+            g.M = (int)Pin;
+            g.N = T.cin;
+            g.K = 4 * T.cout;
+            g.C = T.cout;
+            g.amode = G_UP2;
+            use_x3(p, g, p.s3, T.cout, p.pack3 + 3 * T.pd);
+            g.out = dx;
+            g.ldo = T.cin;
+            g.ooff = 0;
+            g.emode = E_STORE_BN;
+            g.ey = p.y[src];
+            g.ldey = p.ldy[src];
+            g.offey = p.offy[src];
+            if (c->bn_relu) {
+                g.escale = p.scale[src];
+                g.eshift = p.shift[src];
+            }
+            g.stats = p.part;
+            const int tile = x3_tile(c, g);
+            *rows = bn_groups(Pin);
+            RUN(xlabel("convT_dgrad", tile, 100 + k), 2.0 * Pin * T.cin * 4 * T.cout,
+                launch_rowgemm_x3(g, tile, s));
+            return 0;
+        }
         WgradCfg wc = wgrad_cfg(c, T.cin, 1, T.cout, 4, Pin, c->bf16);
         WgradArgs w{};
         w.xcd = xcd_remap_wgrad(c);

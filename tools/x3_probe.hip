@@ -2,7 +2,10 @@
 // pipelined kernel (csrc/kernels_gemm_pipe.hip) on the 3x3 conv GEMMs of BASELINE config 2
 // (bs 32, 256^2, models/model.py UNet): time per launch of each, max |difference| between
 // them, and both kernels' errors against an fp64 dot product on sampled outputs.
-//   build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/x3_probe.hip -o /tmp/x3_probe
+// Second part: the x3 weight gradient against the f32 library kernels (launch_wgrad, linked
+// from lib/libunet_hip.so), slabs summed on the host.
+//   build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/x3_probe.hip -o /tmp/x3_probe \
+//          -L thyroid-nodule-image-segmentation-unet-ddti_amd/lib -lunet_hip
 #include <stdio.h>
 #include <stdlib.h>
 #include <algorithm>
@@ -37,8 +40,11 @@ struct Shape {
     int N, H, W, Cin, Cout;
 };
 
+static void probe_wgrad(int iters, void* zero);
+
 int main(int argc, char** argv) {
     const int iters = argc > 1 ? atoi(argv[1]) : 5;
+    const int what = argc > 2 ? atoi(argv[2]) : 3;  // bit 0 row GEMMs, bit 1 weight gradients
     Shape shapes[] = {
         {"L0 64->64 @256", 32, 256, 256, 64, 64},     {"L0 128->64 @256", 32, 256, 256, 128, 64},
         {"L0 64->128 @256 (dgrad)", 32, 256, 256, 64, 128},
@@ -52,7 +58,9 @@ int main(int argc, char** argv) {
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
+    if (what & 2) probe_wgrad(iters, zero);
     for (const Shape& sh : shapes) {
+        if (!(what & 1)) break;
         const int M = sh.N * sh.H * sh.W, N = sh.Cout, C = sh.Cin, K = 9 * C;
         float *x, *w, *y32, *yx3;
         uint16_t *x3, *w3;
@@ -111,7 +119,7 @@ int main(int argc, char** argv) {
         CK(hipMemcpy(r32.data(), y32, r32.size() * 4, hipMemcpyDeviceToHost));
         std::vector<float> hx, hw;
         bool host_loaded = false;
-        for (int tile = 0; tile <= 4; ++tile) {
+        for (int tile = 0; tile <= 6; ++tile) {
             int bm, bn;
             rowgemm_x3_tile_dims(tile, &bm, &bn);
             if (N % bn) continue;
@@ -169,4 +177,143 @@ int main(int argc, char** argv) {
         CK(hipFree(w3));
     }
     return 0;
+}
+
+static void probe_wgrad(int iters, void* zero) {
+    Shape shapes[] = {
+        {"L0 64x64 @256", 32, 256, 256, 64, 64},      {"L0 128x64 @256", 32, 256, 256, 128, 64},
+        {"L1 128x128 @128", 32, 128, 128, 128, 128},  {"L1 256x128 @128", 32, 128, 128, 256, 128},
+        {"L2 256x256 @64", 32, 64, 64, 256, 256},     {"L3 512x512 @32", 32, 32, 32, 512, 512},
+        {"L4 1024x1024 @16", 32, 16, 16, 1024, 1024},
+    };
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    for (const Shape& sh : shapes) {
+        const int P = sh.N * sh.H * sh.W, CA = sh.Cin, CB = sh.Cout, Mw = 9 * CA, Nw = CB;
+        // split-K over pixels: >= 1536 blocks of 128x128
+        int splits = std::max(1, 1536 / std::max(1, (Mw / 128) * std::max(1, Nw / 128)));
+        int pps = (P + splits - 1) / splits;
+        pps = (pps + 255) / 256 * 256;
+        splits = (P + pps - 1) / pps;
+        float *x, *dz, *slab;
+        uint16_t *x3, *dz3;
+        CK(hipMalloc(&x, (size_t)P * CA * 4));
+        CK(hipMalloc(&dz, (size_t)P * CB * 4));
+        CK(hipMalloc(&x3, (size_t)P * CA * 6));
+        CK(hipMalloc(&dz3, (size_t)P * CB * 6));
+        CK(hipMalloc(&slab, (size_t)splits * Mw * Nw * 4));
+        hipLaunchKernelGGL(fill_rand, dim3(4096), dim3(256), 0, 0, x, (size_t)P * CA, 23u, 4.f, 1);
+        hipLaunchKernelGGL(fill_rand, dim3(4096), dim3(256), 0, 0, dz, (size_t)P * CB, 29u, 1e-3f, 0);
+        CK((hipError_t)k_to_x3(x, CA, 0, CA, nullptr, nullptr, 0, P, x3, CA, 0, 0));
+        CK((hipError_t)k_to_x3(dz, CB, 0, CB, nullptr, nullptr, 0, P, dz3, CB, 0, 0));
+        WgradArgs w{};
+        w.H = sh.H;
+        w.W = sh.W;
+        w.P = P;
+        w.a = x;
+        w.lda = CA;
+        w.CA = CA;
+        w.amode = G_CONV3;
+        w.b = dz;
+        w.ldb = CB;
+        w.CB = CB;
+        w.bmode = G_IDENT;
+        w.Mw = Mw;
+        w.Nw = Nw;
+        w.pps = pps;
+        w.splits = splits;
+        w.slab = slab;
+        w.xcd = 1;
+        WgradArgs v = w;
+        v.a = (const float*)x3;
+        v.b = (const float*)dz3;
+        v.zero16 = zero;
+        const double fl = 2.0 * P * Mw * Nw;
+        auto timeit = [&](auto fn) {
+            CK((hipError_t)fn());
+            CK(hipDeviceSynchronize());
+            CK(hipEventRecord(e0, 0));
+            for (int i = 0; i < iters; ++i) fn();
+            CK(hipEventRecord(e1, 0));
+            CK(hipEventSynchronize(e1));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            return ms / iters;
+        };
+        auto reduce = [&]() {
+            std::vector<float> hs((size_t)splits * Mw * Nw);
+            CK(hipMemcpy(hs.data(), slab, hs.size() * 4, hipMemcpyDeviceToHost));
+            std::vector<double> r((size_t)Mw * Nw, 0.0);
+            for (int sp = 0; sp < splits; ++sp)
+                for (size_t i = 0; i < r.size(); ++i) r[i] += hs[(size_t)sp * Mw * Nw + i];
+            return r;
+        };
+        // f32 library tiles: row3 128x128 (23) / 64x64 (20) where they fit, one-tap 128x128 (0)
+        const int f32tiles[] = {23, 21, 22, 20, 0, 7};
+        float tbest = 1e30f;
+        int fbest = -1;
+        std::vector<double> r32;
+        for (int t : f32tiles) {
+            int bm, bn, bkp;
+            if (wgrad_tile_dims(t, &bm, &bn, &bkp)) continue;
+            if (CA % bm || Nw % bn || pps % bkp) continue;
+            CK(hipMemset(slab, 0, (size_t)splits * Mw * Nw * 4));
+            if (launch_wgrad(w, t, 0) != 0) continue;
+            const float tt = timeit([&] { return launch_wgrad(w, t, 0); });
+            if (tt < tbest) {
+                tbest = tt;
+                fbest = t;
+                r32 = reduce();
+            }
+        }
+        printf("%-20s P=%d Mw=%d Nw=%d splits=%d  f32 wgrad tile %d: %.3f ms %.1f TF/s\n", sh.name, P, Mw,
+               Nw, splits, fbest, tbest, fl / tbest / 1e9);
+        std::vector<float> hx((size_t)P * CA), hd((size_t)P * CB);
+        CK(hipMemcpy(hx.data(), x, hx.size() * 4, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(hd.data(), dz, hd.size() * 4, hipMemcpyDeviceToHost));
+        for (int tile = 0; tile <= 6; ++tile) {
+            int bm, bn;
+            wgrad_x3_tile_dims(tile, &bm, &bn);
+            if (CA % bm || Nw % bn) continue;
+            CK(hipMemset(slab, 0, (size_t)splits * Mw * Nw * 4));
+            const float tx = timeit([&] { return launch_wgrad_x3(v, tile, 0); });
+            std::vector<double> rx = reduce();
+            double md = 0, mref = 0;
+            for (size_t i = 0; i < rx.size(); ++i) {
+                md = std::max(md, fabs(rx[i] - r32[i]));
+                mref = std::max(mref, fabs(r32[i]));
+            }
+            // fp64 reference on sampled weights: dW[(t, ci)][co] = sum_p x[p + tap][ci] dz[p][co]
+            double e32 = 0, ex3 = 0, s2 = 0;
+            unsigned st = 777;
+            for (int smp = 0; smp < 64; ++smp) {
+                st = st * 1664525u + 1013904223u;
+                const int m = (int)(st % (unsigned)Mw);
+                st = st * 1664525u + 1013904223u;
+                const int n = (int)(st % (unsigned)Nw);
+                const int t = m / CA, ci = m % CA;
+                double acc = 0;
+                for (int pix = 0; pix < P; ++pix) {
+                    const int img = pix / (sh.H * sh.W), yy = (pix / sh.W) % sh.H, xx = pix % sh.W;
+                    const int sy = yy + t / 3 - 1, sx = xx + t % 3 - 1;
+                    if (sy < 0 || sy >= sh.H || sx < 0 || sx >= sh.W) continue;
+                    acc += (double)hx[((size_t)(img * sh.H + sy) * sh.W + sx) * CA + ci] * hd[(size_t)pix * CB + n];
+                }
+                const double d32 = r32[(size_t)m * Nw + n] - acc, dx3 = rx[(size_t)m * Nw + n] - acc;
+                e32 += d32 * d32;
+                ex3 += dx3 * dx3;
+                s2 += acc * acc;
+            }
+            printf("    x3 wgrad tile %d (%dx%d): %.3f ms %.1f TF/s (x%.2f)  max|x3-f32|/max|f32| %.2e  "
+                   "rms err vs fp64: f32 %.2e x3 %.2e\n",
+                   tile, bm, bn, tx, fl / tx / 1e9, tbest / tx, md / mref, sqrt(e32 / s2), sqrt(ex3 / s2));
+            fflush(stdout);
+        }
+        CK(hipFree(x));
+        CK(hipFree(dz));
+        CK(hipFree(x3));
+        CK(hipFree(dz3));
+        CK(hipFree(slab));
+    }
 }
