@@ -118,3 +118,29 @@ def test_x3_row_tile_choice_bit_identical(B, H, W):
     for i in range(1, len(outs)):
         assert torch.equal(outs[0][0], outs[i][0]), i
         assert torch.equal(outs[0][1], outs[i][1]), (i, (outs[0][1] - outs[i][1]).abs().max().item())
+
+
+def test_x3_tap_row_wgrad_matches_one_tap():
+    """The tap-row x3 weight gradient (wgrad_x3_row3_kernel: three dx taps from one 34-pixel
+    halo, default on rows of 32k pixels) against the one-tap x3 kernel (option x3_wtile = 1
+    everywhere): the same products summed over other split partitions, so every weight and
+    bias gradient agrees to f32 summation noise (<= 1e-5 norm-relative); the forward is
+    unchanged (logits bit-identical).  B=2 at 128x128: W = 128, 64, 32 on the tap-row kernel,
+    16 and 8 on the one-tap kernel either way."""
+    import unet_hip
+    from _helpers import options
+    x, t = inputs(19, 2, 128, 128)
+    outs = []
+    for wt in (-1, 1):
+        m = hip_model(O.make_params(42), DEV)
+        with options(m.flatten_().rt, x3_wtile=wt):
+            logits = m(x.to(DEV))
+            l = unet_hip.seg_losses(logits, t.to(DEV))
+            (l[0] + l[1]).backward()
+            torch.cuda.synchronize()
+        outs.append((logits.detach().clone(), {k: p.grad.detach().clone() for k, p in m.named_parameters()}))
+        del m
+    assert torch.equal(outs[0][0], outs[1][0])
+    worst = max(norm_rel(outs[0][1][k].cpu(), g.cpu()) for k, g in outs[1][1].items())
+    print(f"tap-row vs one-tap x3 weight gradients: worst norm-rel {worst:.2e}")
+    assert worst <= 1e-5

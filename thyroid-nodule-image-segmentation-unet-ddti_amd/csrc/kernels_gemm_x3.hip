@@ -496,6 +496,180 @@ __global__ __launch_bounds__(T::THREADS, 1) void wgrad_x3_kernel(WgradArgs p) {
             }
 }
 
+// ------------------------------------------------------------------------------------
+// Tap-row weight gradient on x3 images (3x3 convs, W % 32 == 0): one block computes the three
+// dx taps of one tap row dy for a BM (ci) x BN (co) tile over its split's pixels.  A 32-pixel
+// chunk never crosses an image row, so the A' operands of the three taps are the same 34
+// halo pixels of source row y + dy - 1 (columns x0 - 1 .. x0 + 32, zero outside the image),
+// read at row offsets dx = 0, 1, 2: a third of the one-tap kernel's A' staging per MFMA.
+// 8 waves, each 32 ci x 32 co x 3 taps (3 accumulator pairs); per k-step 18 + 6 transposed
+// reads feed 18 MFMAs.  Stage: [AR halo rows][6 BM B] + [32 pixel rows][6 BN B]; the loader
+// gives every wave the same instruction count (rows past the halo / chunk read zeros).
+// ------------------------------------------------------------------------------------
+template <int BM, int BN>
+__global__ __launch_bounds__(512, 1) void wgrad_x3_row3_kernel(WgradArgs p) {
+    constexpr int WAVES = 8, BKP = 32, S = 3;
+    constexpr int WAVES_N = BN / 32;
+    static_assert((BM / 32) * WAVES_N == WAVES, "8 waves of 32 x 32");
+    constexpr int RA = 6 * BM, RBB = 6 * BN;
+    constexpr int HALO = BKP + 2;
+    constexpr int AI = (HALO * RA + 1024 * WAVES - 1) / (1024 * WAVES);  // per wave
+    constexpr int BI = (BKP * RBB + 1024 * WAVES - 1) / (1024 * WAVES);
+    constexpr int GPC = AI + BI;
+    constexpr int AREG = AI * WAVES * 1024, BREG = BI * WAVES * 1024;  // bytes per stage
+    constexpr int STAGE = AREG + BREG;
+    __shared__ __attribute__((aligned(1024))) char smem[STAGE * S];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+    const int tiles_n = p.CB / BN, tiles_m = p.CA / BM;
+    int idx = p.xcd ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+    const int tn = idx % tiles_n;
+    idx /= tiles_n;
+    const int dy = idx % 3;
+    idx /= 3;
+    const int tm = idx % tiles_m;
+    const int split = idx / tiles_m;
+    const int ca0 = tm * BM, cb0 = tn * BN;
+    const int H = p.H, W = p.W;
+    const int pbeg = split * p.pps;
+    const int pend = min(pbeg + p.pps, p.P);
+    const int nk = (pend - pbeg) / BKP;  // pps, P multiples of 32
+
+    int arow[AI], aele[AI], brow[BI], bele[BI];
+#pragma unroll
+    for (int j = 0; j < AI; ++j) {
+        const int o = ((j * WAVES + wave) * 64 + lane) * 16;
+        const int r = o / RA, sl = (o - r * RA) >> 4;
+        arow[j] = r;
+        aele[j] = x3_tswz<RA>(sl, r) * 8;
+    }
+#pragma unroll
+    for (int j = 0; j < BI; ++j) {
+        const int o = ((j * WAVES + wave) * 64 + lane) * 16;
+        const int r = o / RBB, sl = (o - r * RBB) >> 4;
+        brow[j] = r;
+        bele[j] = x3_tswz<RBB>(sl, r) * 8;
+    }
+    const uint16_t* a16 = (const uint16_t*)p.a + (size_t)(p.aoff + ca0) * 3;
+    const uint16_t* b16 = (const uint16_t*)p.b + (size_t)(p.boff + cb0) * 3;
+    const size_t rowa = 3 * (size_t)p.lda, rowb = 3 * (size_t)p.ldb;
+    const uint16_t* zero = (const uint16_t*)p.zero16;
+
+    auto issue = [&](int kc, int st) {
+        const int pc = pbeg + kc * BKP;  // wave-uniform: the chunk's image row and first column
+        const int t = pc / W, x0 = pc - t * W;
+        const int img = t / H, y = t - img * H;
+        const int yy = y + dy - 1;
+        const bool rowok = yy >= 0 && yy < H;
+        const int rowbase = (img * H + yy) * W;
+        char* base = smem + st * STAGE;
+#pragma unroll
+        for (int j = 0; j < AI; ++j) {
+            const int xx = x0 - 1 + arow[j];
+            const bool ok = rowok && arow[j] < HALO && xx >= 0 && xx < W;
+            const uint16_t* g = ok ? a16 + (size_t)(rowbase + xx) * rowa + aele[j] : zero;
+            x3_dma16(g, base + (j * WAVES + wave) * 1024);
+        }
+#pragma unroll
+        for (int j = 0; j < BI; ++j) {
+            const bool ok = brow[j] < BKP;
+            const uint16_t* g = ok ? b16 + (size_t)(pc + brow[j]) * rowb + bele[j] : zero;
+            x3_dma16(g, base + AREG + (j * WAVES + wave) * 1024);
+        }
+    };
+
+    f32x16 acc[3], acl[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][r] = acl[i][r] = 0.f;
+
+    // transposed-read addresses (k-step 0): lane l of group g = l / 16 supplies row
+    // 8 (g >> 1) + qq (+ dx for A'), columns 16 (g & 1) + 4 pp of plane q
+    const int g = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
+    const int trow = 8 * (g >> 1) + qq;
+    auto slot = [](int col, int q) { return (col >> 5) * 12 + q * 4 + ((col & 31) >> 3); };
+    int aoff[3][3], boff[3];
+    {
+        const int col = wm * 32 + 16 * (g & 1) + 4 * pp;
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+            for (int q = 0; q < 3; ++q)
+                aoff[dx][q] = (trow + dx) * RA + (x3_tswz<RA>(slot(col, q), trow + dx) << 4) + ((col >> 2) & 1) * 8;
+        const int colb = wn * 32 + 16 * (g & 1) + 4 * pp;
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+            boff[q] = AREG + trow * RBB + (x3_tswz<RBB>(slot(colb, q), trow) << 4) + ((colb >> 2) & 1) * 8;
+    }
+
+#pragma unroll
+    for (int s = 0; s < S - 1; ++s)
+        if (s < nk) issue(s, s);
+    for (int kc = 0; kc < nk; ++kc) {
+        if (kc + S - 1 < nk) issue(kc + S - 1, (kc + S - 1) % S);
+        const int ahead = min(S - 1, nk - 1 - kc);
+        if (ahead >= 2) x3_wait_vm<2 * GPC>();
+        else if (ahead == 1) x3_wait_vm<GPC>();
+        else x3_wait_vm<0>();
+        x3_barrier();
+        const unsigned sb = x3_lds_u32(smem) + (kc % S) * STAGE;
+        x3_short4 fa[2][3][3][2], fb[2][3][2];
+        auto load = [&](auto KK) {
+            constexpr int kk = decltype(KK)::value;
+#pragma unroll
+            for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+                for (int q = 0; q < 3; ++q) {
+                    fa[kk][dx][q][0] = x3_tr16<kk * 16 * RA>(sb + aoff[dx][q]);
+                    fa[kk][dx][q][1] = x3_tr16<kk * 16 * RA + 4 * RA>(sb + aoff[dx][q]);
+                }
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                fb[kk][q][0] = x3_tr16<kk * 16 * RBB>(sb + boff[q]);
+                fb[kk][q][1] = x3_tr16<kk * 16 * RBB + 4 * RBB>(sb + boff[q]);
+            }
+        };
+        auto mma = [&](auto KK) {
+            constexpr int kk = decltype(KK)::value;
+            bf16x8 b3[3];
+#pragma unroll
+            for (int q = 0; q < 3; ++q) b3[q] = *(const bf16x8*)fb[kk][q];
+#pragma unroll
+            for (int dx = 0; dx < 3; ++dx) {
+                bf16x8 a3[3];
+#pragma unroll
+                for (int q = 0; q < 3; ++q) a3[q] = *(const bf16x8*)fa[kk][dx][q];
+                mfma_x3s(a3, b3, acc[dx], acl[dx]);
+            }
+        };
+        load(std::integral_constant<int, 0>{});
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        load(std::integral_constant<int, 1>{});
+        __builtin_amdgcn_sched_barrier(0);
+        mma(std::integral_constant<int, 0>{});
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        mma(std::integral_constant<int, 1>{});
+        x3_barrier();
+    }
+
+    const int li = lane & 31, lh = lane >> 5;
+    float* slab = p.slab + (size_t)split * p.Mw * p.Nw;
+#pragma unroll
+    for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int m = (dy * 3 + dx) * p.CA + ca0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+            const int n = cb0 + wn * 32 + li;
+            slab[(size_t)m * p.Nw + n] = acc[dx][r] + acl[dx][r];
+        }
+}
+
 // tiles (split accumulators): 0 = 128x128 (8 waves of 64x32), 1 = 64x64 (4 waves of 32x32);
 // three LDS stages of 32 pixels
 using WX0 = WTileX3<128, 128, 64, 32, 3, 1>;
@@ -510,45 +684,77 @@ static int wx3_go(const WgradArgs& a, hipStream_t s) {
     return (int)hipGetLastError();
 }
 
+// exact three-way split of 8 f32 values into their hi / mid / lo bf16 pieces, stored at d,
+// d + 32, d + 64 (one 32-channel group of an x3 row)
+__device__ __forceinline__ void x3_store8(const float (&v)[8], uint16_t* d) {
+    bf16x8 h, m, l;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const __bf16 hj = (__bf16)v[j];
+        const float r1 = v[j] - (float)hj;
+        const __bf16 mj = (__bf16)r1;
+        h[j] = hj;
+        m[j] = mj;
+        l[j] = (__bf16)(r1 - (float)mj);
+    }
+    *(bf16x8*)d = h;
+    *(bf16x8*)(d + 32) = m;
+    *(bf16x8*)(d + 64) = l;
+}
+
 // x3 image of op(src) (f32 [P][ld] at channel offset off, C channels; scale / shift: the
 // BN affine, ReLU on channels < relu) into dst [P][dld / 32][3][32] at channel offset doff.
-// One thread per 8 channels of a row.
-__global__ void to_x3_kernel(const float* __restrict__ src, int ld, int off, int C,
-                             const float* __restrict__ scale, const float* __restrict__ shift,
-                             int relu, int64_t P, uint16_t* __restrict__ dst, int dld, int doff) {
+// A block covers X3_PREP_RPB rows; thread t handles channel octet t % (C / 8) of rows
+// t / (C / 8) + k 256 / (C / 8), two rows in flight; the affine is loaded once per thread.
+constexpr int X3_PREP_RPB = 256;
+__global__ __launch_bounds__(256) void to_x3_kernel(const float* __restrict__ src, int ld, int off, int C,
+                                                    const float* __restrict__ scale,
+                                                    const float* __restrict__ shift, int relu, int64_t P,
+                                                    uint16_t* __restrict__ dst, int dld, int doff) {
     const int g8 = C / 8;
-    const int64_t n = P * g8;
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
-         i += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t r = i / g8;
-        const int c = (int)(i - r * g8) * 8;
-        const float* s = src + r * ld + off + c;
-        const f32x4 v0 = *(const f32x4*)s, v1 = *(const f32x4*)(s + 4);
-        float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+    const int oct = threadIdx.x % g8, r0 = threadIdx.x / g8, rstep = 256 / g8;
+    if (r0 >= rstep) return;
+    const int c = oct * 8;
+    float sc[8], sh[8];
+    if (scale) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const f32x4 a = *(const f32x4*)(scale + c + 4 * h), b = *(const f32x4*)(shift + c + 4 * h);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                sc[4 * h + j] = a[j];
+                sh[4 * h + j] = b[j];
+            }
+        }
+    }
+    const int cc = doff + c;
+    uint16_t* dcol = dst + (cc >> 5) * 96 + (cc & 31);
+    const int64_t mb = (int64_t)blockIdx.x * X3_PREP_RPB;
+    const int64_t me = min(mb + X3_PREP_RPB, P);
+    auto load = [&](int64_t m, float (&v)[8]) {
+        const float* sp = src + m * ld + off + c;
+        const f32x4 v0 = *(const f32x4*)sp, v1 = *(const f32x4*)(sp + 4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            v[j] = v0[j];
+            v[4 + j] = v1[j];
+        }
         if (scale) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                float t = __builtin_fmaf(scale[c + j], v[j], shift[c + j]);
+                float t = __builtin_fmaf(sc[j], v[j], sh[j]);
                 if (c + j < relu) t = fmaxf(t, 0.f);
                 v[j] = t;
             }
         }
-        bf16x8 h, m, l;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const __bf16 hj = (__bf16)v[j];
-            const float r1 = v[j] - (float)hj;
-            const __bf16 mj = (__bf16)r1;
-            const float r2 = r1 - (float)mj;
-            h[j] = hj;
-            m[j] = mj;
-            l[j] = (__bf16)r2;
-        }
-        const int cc = doff + c;
-        uint16_t* d = dst + r * 3 * (int64_t)dld + (cc >> 5) * 96 + (cc & 31);
-        *(bf16x8*)d = h;
-        *(bf16x8*)(d + 32) = m;
-        *(bf16x8*)(d + 64) = l;
+    };
+    for (int64_t m = mb + r0; m < me; m += 2 * rstep) {
+        const int64_t m2 = m + rstep;
+        float v[8], w[8];
+        load(m, v);
+        if (m2 < me) load(m2, w);
+        x3_store8(v, dcol + m * 3 * (int64_t)dld);
+        if (m2 < me) x3_store8(w, dcol + m2 * 3 * (int64_t)dld);
     }
 }
 
@@ -588,21 +794,9 @@ __global__ __launch_bounds__(256) void bn_dz_x3_kernel(const float* __restrict__
 #pragma unroll
             for (int j = 0; j < 4; ++j) v[4 * h + j] = (!mask || yv[j] > 0.f) ? r[j] : 0.f;
         }
-        bf16x8 hi, mi, lo;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const __bf16 hj = (__bf16)v[j];
-            const float r1 = v[j] - (float)hj;
-            const __bf16 mj = (__bf16)r1;
-            hi[j] = hj;
-            mi[j] = mj;
-            lo[j] = (__bf16)(r1 - (float)mj);
-            cs[j] += v[j];
-        }
-        uint16_t* o = dz3 + m * 3 * (int64_t)C + (c >> 5) * 96 + (c & 31);
-        *(bf16x8*)o = hi;
-        *(bf16x8*)(o + 32) = mi;
-        *(bf16x8*)(o + 64) = lo;
+        for (int j = 0; j < 8; ++j) cs[j] += v[j];
+        x3_store8(v, dz3 + m * 3 * (int64_t)C + (c >> 5) * 96 + (c & 31));
     }
     if (!bpart) return;
 #pragma unroll
@@ -655,14 +849,19 @@ int launch_rowgemm_x3(const RowGemmArgs& a, int tile, hipStream_t s) {
 int k_to_x3(const float* src, int ld, int off, int C, const float* scale, const float* shift,
             int relu, int64_t P, uint16_t* dst, int dld, int doff, hipStream_t s) {
     if (C % 32 || dld % 32 || doff % 32 || ld % 4 || off % 4) return -1;
-    const int64_t n = P * (C / 8);
-    const int blocks = (int)std::min<int64_t>((n + 255) / 256, 8192);
+    if (C > 2048 || P < 1) return -1;
+    const int blocks = (int)((P + X3_PREP_RPB - 1) / X3_PREP_RPB);
     hipLaunchKernelGGL(to_x3_kernel, dim3(blocks), dim3(256), 0, s, src, ld, off, C, scale, shift,
                        relu, P, dst, dld, doff);
     return (int)hipGetLastError();
 }
 
 int wgrad_x3_tile_dims(int tile, int* bm, int* bn) {
+    if (tile == 2 || tile == 3) {  // tap-row: BM x BN per tap, three taps per block
+        *bm = tile == 2 ? 64 : 128;
+        *bn = tile == 2 ? 128 : 64;
+        return 0;
+    }
 #define WX3_DIMS(id, T) \
     if (tile == id) {   \
         *bm = T::BM;    \
@@ -680,6 +879,18 @@ int wgrad_x3_tile_dims(int tile, int* bm, int* bn) {
 int launch_wgrad_x3(const WgradArgs& a, int tile, hipStream_t s) {
     if (a.ascale || a.bcoef || a.bias_slab || !a.zero16 || a.P < 1) return -1;
     if (a.aoff % 32 || a.boff % 32 || a.lda % 32 || a.ldb % 32) return -1;
+    if (tile == 2 || tile == 3) {  // tap-row kernel: 3x3 convs, W % 32 == 0
+        const int bm = tile == 2 ? 64 : 128, bn = tile == 2 ? 128 : 64;
+        if (a.amode != G_CONV3 || a.bmode != G_IDENT || a.Mw != 9 * a.CA || a.Nw != a.CB ||
+            a.CA % bm || a.CB % bn || a.W % 32 || a.pps % 32 || a.P % 32)
+            return -1;
+        const dim3 grid((a.CA / bm) * 3 * (a.CB / bn) * a.splits);
+        if (tile == 2)
+            hipLaunchKernelGGL((wgrad_x3_row3_kernel<64, 128>), grid, dim3(512), 0, s, a);
+        else
+            hipLaunchKernelGGL((wgrad_x3_row3_kernel<128, 64>), grid, dim3(512), 0, s, a);
+        return (int)hipGetLastError();
+    }
 #define WX3G(AM, BMD)                                      \
     do {                                                   \
         if (tile == 0) return wx3_go<AM, BMD, WX0>(a, s);  \

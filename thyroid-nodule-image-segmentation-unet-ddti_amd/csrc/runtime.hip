@@ -764,18 +764,26 @@ int x3_tile(const unet_ctx* c, const RowGemmArgs& g) {
 // weight gradient: 128x128 tile where both channel counts allow it, else 64x64; split-K over
 // pixels so the grid has >= x3_wblocks 128x128 blocks (4x that of 64x64 ones); pixels per
 // split a multiple of 256
-WgradCfg x3_wgrad_cfg(const unet_ctx* c, int CA, int tapsA, int CB, int tapsB, int64_t P) {
+// 3x3 convs on rows of a multiple of 32 pixels (row_w): the tap-row kernel (tiles 2 = 64x128,
+// 3 = 128x64 per tap, three taps per block)
+WgradCfg x3_wgrad_cfg(const unet_ctx* c, int CA, int tapsA, int CB, int tapsB, int64_t P,
+                      int row_w = 0) {
     WgradCfg w{};
     w.tile = (CA % 128 == 0 && CB % 128 == 0) ? 0 : 1;
+    const bool r3 = tapsA == 9 && tapsB == 1 && row_w % 32 == 0 && row_w > 0;
+    if (r3 && CA % 64 == 0 && CB % 128 == 0) w.tile = 2;
+    else if (r3 && CA % 128 == 0 && CB % 64 == 0) w.tile = 3;
     if (c->opt.x3_wtile >= 0) {
         int bm = 0, bn = 0;
-        if (wgrad_x3_tile_dims(c->opt.x3_wtile, &bm, &bn) == 0 && CA % bm == 0 && CB % bn == 0)
-            w.tile = c->opt.x3_wtile;
+        const int t = c->opt.x3_wtile;
+        if (wgrad_x3_tile_dims(t, &bm, &bn) == 0 && CA % bm == 0 && CB % bn == 0 && (t < 2 || r3))
+            w.tile = t;
     }
     wgrad_x3_tile_dims(w.tile, &w.bm, &w.bn);
     w.bkp = 32;
-    const int64_t tiles = (int64_t)(tapsA * CA / w.bm) * (tapsB * CB / w.bn);
-    const int64_t target = (int64_t)c->opt.x3_wblocks * (w.tile == 0 ? 1 : 4);
+    const int64_t tiles = w.tile >= 2 ? (int64_t)(CA / w.bm) * 3 * (CB / w.bn)
+                                      : (int64_t)(tapsA * CA / w.bm) * (tapsB * CB / w.bn);
+    const int64_t target = (int64_t)c->opt.x3_wblocks * (w.tile == 1 ? 4 : 1);
     int64_t splits = std::max<int64_t>(1, (target + tiles - 1) / tiles);
     int64_t pps = (P + splits - 1) / splits;
     pps = (pps + 255) / 256 * 256;
@@ -801,7 +809,7 @@ void use_x3(const Plan& p, RowGemmArgs& g, const uint16_t* img, int C, const uin
 
 std::string x3wlabel(const char* fam, const WgradCfg& w, int layer) {
     char b[112];
-    snprintf(b, sizeof b, "%s/wx3_%dx%d|%d", fam, w.bm, w.bn, layer);
+    snprintf(b, sizeof b, "%s/wx3%s_%dx%d|%d", fam, w.tile >= 2 ? "r3" : "", w.bm, w.bn, layer);
     return b;
 }
 
@@ -947,7 +955,7 @@ void make_plan(unet_ctx* c, int N, int H, int W, bool training, char* base, Plan
         for (int i = 1; i < NC; ++i) {
             const ConvL& L = c->conv[i];
             WgradCfg w = x3_conv_on(c, L.cin, L.cout)
-                             ? x3_wgrad_cfg(c, L.cin, 9, L.cout, 1, p.P[L.level])
+                             ? x3_wgrad_cfg(c, L.cin, 9, L.cout, 1, p.P[L.level], W >> L.level)
                              : wgrad_cfg(c, L.cin, 9, L.cout, 1, p.P[L.level], c->bf16, W >> L.level);
             smax = std::max(smax, (int64_t)w.splits * 9 * L.cin * L.cout);
             bmax = std::max(bmax, (int64_t)w.splits * L.cout);
@@ -1485,7 +1493,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
             RUN("bn_dz", 0, k_bn_dz_x3(dout, p.y[i], p.ldy[i], p.offy[i], P, C.cout, p.coef, dz_mask,
                                       p.s3, bp, s));
             if (bp) RUN("bias_grad", 0, k_sum_partials(p.part, x3_dz_blocks(P), C.cout, grads + C.b, s));
-            const WgradCfg wc = x3_wgrad_cfg(c, C.cin, 9, C.cout, 1, P);
+            const WgradCfg wc = x3_wgrad_cfg(c, C.cin, 9, C.cout, 1, P, Wl);
             WgradArgs w{};
             w.xcd = 1;
             w.H = Hl;
