@@ -76,8 +76,10 @@ def test_train_steps_match_golden(golden_dir):
     Step 0 is held to the strict bars.  Adam's first updates are ~lr*sign(g), so elements
     whose reference gradient is at fp32 noise level can move by 2*lr in either
     implementation; the trajectories then differ at ~1e-4 relative and steps 1-2 are
-    compared to the golden trajectory at 2e-3 (logits) -- and, strictly, to the oracle
-    re-started from this path's own parameters (test_train_steps_strict_resync)."""
+    compared to the golden trajectory at 2e-3 (logits) and their gradients at 10 % or twice
+    the spread of the fp32 oracle's own trajectory under 1e-7-level input noise, whichever
+    is larger -- and, strictly, to the oracle re-started from this path's own parameters
+    (test_train_steps_strict_resync)."""
     import unet_hip
     f = _golden(golden_dir, "unet_b2_64.npz")
     m = hip_model(O.make_params(42), DEV)
@@ -85,6 +87,24 @@ def test_train_steps_match_golden(golden_dir):
     x, t = torch.from_numpy(f["x"]).to(DEV), torch.from_numpy(f["t"]).to(DEV)
     spec = O.param_spec()
     tiny = None
+    # steps 1-2: the fp32 reference trajectory itself moves under fp32 noise (inputs scaled
+    # by 1 +- 1e-7 .. 1 +- 5e-7): Adam's sign-noise updates send a few small gradients away
+    # (encoder4.0.bias at step 2: up to 18.7 % for x * (1 + 2e-7)).  The step >= 1 gradient
+    # bars are max(10 %, 2x that spread).
+    spread_n = np.zeros((3, len(spec)))
+    spread_s = np.zeros((3, len(spec)))
+    for eps in (1e-7, -1e-7, 2e-7, -2e-7, 3e-7, -3e-7, 5e-7, -5e-7):
+        Pr, Br = O.make_params(42), O.init_buffers()
+        opt_r = O.AdamWState(Pr, lr=1e-5)
+        xr, tr = torch.from_numpy(f["x"]) * (1 + eps), torch.from_numpy(f["t"])
+        for s in range(3):
+            r = O.train_step(Pr, Br, opt_r, xr, tr)
+            for ti, item in enumerate(spec):
+                g = r["grads"][item[0]].double().reshape(-1)
+                idx = np.floor(Wt.uniform(7, 3000 + ti, 64) * g.numel()).astype(np.int64)
+                spread_n[s, ti] = max(spread_n[s, ti], abs(g.norm().item() - f[f"s{s}_grad_norm"][ti]))
+                spread_s[s, ti] = max(spread_s[s, ti],
+                                      float(np.max(np.abs(g[idx].numpy() - f[f"s{s}_grad_samp"][ti]))))
     for s in range(3):
         tol = LOGIT_TOL if s == 0 else 2e-3
         logits, losses, loss = _step(m, opt, x, t)
@@ -103,8 +123,10 @@ def test_train_steps_match_golden(golden_dir):
         for ti, item in enumerate(spec):
             g = dict(m.named_parameters())[item[0]].grad.detach().double().cpu().reshape(-1)
             idx = np.floor(Wt.uniform(7, 3000 + ti, 64) * g.numel()).astype(np.int64)
-            assert abs(g.norm().item() - norms[ti]) <= gtol * norms[ti], item[0]
-            assert np.max(np.abs(g[idx].numpy() - samp[ti])) <= gtol * norms[ti], item[0]
+            bn = max(gtol * norms[ti], 2 * spread_n[s, ti]) if s else gtol * norms[ti]
+            bs = max(gtol * norms[ti], 2 * spread_s[s, ti]) if s else gtol * norms[ti]
+            assert abs(g.norm().item() - norms[ti]) <= bn, item[0]
+            assert np.max(np.abs(g[idx].numpy() - samp[ti])) <= bs, item[0]
         # post-AdamW parameters: 2 ulp, except sign-noise elements (|g_ref| < 1% of rms)
         pnow = dict(m.named_parameters())
         ps = np.stack([pnow[it[0]].detach().cpu().reshape(-1)[torch.from_numpy(

@@ -97,8 +97,8 @@ def test_x3_train_step_matches_f32_mfma():
 
 @pytest.mark.parametrize("B,H,W", [(2, 128, 128), (1, 48, 80)])
 def test_x3_row_tile_choice_bit_identical(B, H, W):
-    """Every x3 row-GEMM tile (0 = 256x128, 1 = 128x128, 2 = 128x64; -1 = the per-GEMM
-    choice) walks K in the same chunk order with the same six-product MFMA sequence per
+    """Every x3 row-GEMM tile (0 = 256x128, 1 = 128x128, 2 = 128x64, 3 = 256x64 for the
+    64-output GEMMs; -1 = the per-GEMM choice) walks K in the same chunk order with the same six-product MFMA sequence per
     element and emits BN partials in the same 128-row groups, so one training step -- logits
     and the whole gradient arena -- is bit-identical across them (48x80: tiles ending past
     M, the guarded epilogue)."""
@@ -106,9 +106,9 @@ def test_x3_row_tile_choice_bit_identical(B, H, W):
     from _helpers import options
     x, t = inputs(13, B, H, W)
     outs = []
-    for tile in (-1, 0, 1, 2):
+    for tile, n64 in ((-1, 2), (0, 2), (1, 2), (2, 2), (-1, 3)):
         m = hip_model(O.make_params(42), DEV)
-        with options(m.flatten_().rt, x3_tile=tile):
+        with options(m.flatten_().rt, x3_tile=tile, x3_n64=n64):
             logits = m(x.to(DEV))
             l = unet_hip.seg_losses(logits, t.to(DEV))
             (l[0] + l[1]).backward()

@@ -21,7 +21,8 @@
 // covers 5 1/3 such rows: the gathered activation rows cost 2 cache lines per chunk instead
 // of 3 for separate planes.
 //
-// LDS image per stage: [BM + BN rows][192 B]; 16-B slot s of plane q of row r holds global
+// LDS image per stage: [BM rows][192 B] (A) then [BN rows][192 B] (B, at the A region's
+// whole-KB end); 16-B slot s of plane q of row r (counted within its region) holds global
 // chunk s ^ ((r >> 2) & 3) (the XOR on the DMA source address, the destination stays
 // lane-linear).  The 16 lanes of a ds_read_b128 phase read one (plane, chunk) of 16
 // consecutive rows: 16-B units r * 12 + 4 q + (c ^ ((r >> 2) & 3)) mod 16 are all distinct,
@@ -88,12 +89,15 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_x3_kernel(RowGemmA
     constexpr int WAVES = T::WAVES, WAVES_N = BN / WN;
     constexpr int MT = WM / 32, NT = WN / 32;
     constexpr int RB = 192;  // bytes per LDS row: 3 planes x 32 bf16
-    static_assert((BM * RB) % (1024 * WAVES) == 0 && (BN * RB) % (1024 * WAVES) == 0, "loader");
-    constexpr int AI = BM * RB / (1024 * WAVES), BI = BN * RB / (1024 * WAVES);
+    // DMA instructions per wave and chunk: every wave issues the same count; rows past BM /
+    // BN (when a region is not a whole number of instructions per wave) read the zero page
+    constexpr int AI = (BM * RB + 1024 * WAVES - 1) / (1024 * WAVES);
+    constexpr int BI = (BN * RB + 1024 * WAVES - 1) / (1024 * WAVES);
+    constexpr int AREG = AI * WAVES * 1024;  // bytes of the A region of a stage
     constexpr int GPC = AI + BI;
     constexpr int DIST = S - 1;
     static_assert(DIST >= 1 && DIST <= 3, "stages");
-    constexpr int STAGE = (BM + BN) * RB;
+    constexpr int STAGE = AREG + BI * WAVES * 1024;
     constexpr int RED = 2 * (BM / 64) * BN * 8;
     constexpr int SMEM = STAGE * S > RED ? STAGE * S : RED;
     __shared__ __attribute__((aligned(1024))) char smem[SMEM];
@@ -120,17 +124,20 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_x3_kernel(RowGemmA
         const int o = ((j * WAVES + wave) * 64 + lane) * 16;
         const int r = o / RB, w = o - r * RB;
         const int m = m0 + r;
-        aok[j] = m < p.M;
-        am[j] = aok[j] ? m : p.M - 1;
+        aok[j] = m < p.M && r < BM;
+        am[j] = m < p.M ? m : p.M - 1;
         aq[j] = decode(am[j], H, W);
         ace[j] = (w >> 6) * 32 + ((((w >> 4) & 3) ^ swz(r)) << 3);
     }
     const uint16_t* bsrc[BI];
+    bool bok[BI];
 #pragma unroll
     for (int j = 0; j < BI; ++j) {
         const int o = ((j * WAVES + wave) * 64 + lane) * 16;
         const int r = o / RB, w = o - r * RB;
-        bsrc[j] = p.bt16 + (size_t)(n0 + r) * rowb + (w >> 6) * 32 + ((((w >> 4) & 3) ^ swz(BM + r)) << 3);
+        bok[j] = r < BN;
+        bsrc[j] = p.bt16 + (size_t)(n0 + (bok[j] ? r : 0)) * rowb + (w >> 6) * 32 +
+                  ((((w >> 4) & 3) ^ swz(r)) << 3);
     }
     const uint16_t* zero = (const uint16_t*)p.zero16;
     const uint16_t* a16 = p.a16 + (size_t)p.aoff * 3;
@@ -149,7 +156,7 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_x3_kernel(RowGemmA
         }
 #pragma unroll
         for (int j = 0; j < BI; ++j)
-            x3_dma16(bsrc[j] + k0 * 3, base + BM * RB + (j * WAVES + wave) * 1024);
+            x3_dma16(bok[j] ? bsrc[j] + k0 * 3 : zero, base + AREG + (j * WAVES + wave) * 1024);
     };
 
     constexpr int SA = T::SA;
@@ -174,8 +181,8 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_x3_kernel(RowGemmA
     }
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
-        const int r = BM + wn * WN + nt * 32 + li;
-        bro[nt] = r * RB;
+        const int r = wn * WN + nt * 32 + li;
+        bro[nt] = AREG + r * RB;
         bfx[nt] = swz(r);
     }
 
@@ -237,11 +244,13 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_x3_kernel(RowGemmA
 
 // tiles (split accumulators; probe: profiles/r04_x3_probe_*.txt): 0 = 256x128 (8 waves of
 // 64x64, 2 stages, 144 KB, one block per CU), 1 = 128x128 (4 waves, 2 stages: grids below 256
-// blocks of tile 0), 2 = 128x64 (4 waves of 64x32, two blocks per CU: the 64-output layers)
+// blocks of tile 0), 2 = 128x64 (4 waves of 64x32, two blocks per CU: the 64-output layers),
+// 3 = 256x64 (8 waves of 64x32, B region padded to 16 KB)
 using TX0 = TileX3<256, 128, 64, 64, 2, 1, 1>;
 using TX1 = TileX3<128, 128, 64, 64, 2, 1, 1>;
 using TX2 = TileX3<128, 64, 64, 32, 2, 2, 1>;
-#define ROWGEMM_X3_TILES(X) X(0, TX0) X(1, TX1) X(2, TX2)
+using TX3 = TileX3<256, 64, 64, 32, 2, 1, 1>;
+#define ROWGEMM_X3_TILES(X) X(0, TX0) X(1, TX1) X(2, TX2) X(3, TX3)
 
 template <int AMODE, int EMODE, class T>
 static int x3_go(const RowGemmArgs& a, hipStream_t s) {
@@ -506,11 +515,11 @@ __global__ __launch_bounds__(T::THREADS, 1) void wgrad_x3_kernel(WgradArgs p) {
 // reads feed 18 MFMAs.  Stage: [AR halo rows][6 BM B] + [32 pixel rows][6 BN B]; the loader
 // gives every wave the same instruction count (rows past the halo / chunk read zeros).
 // ------------------------------------------------------------------------------------
-template <int BM, int BN>
-__global__ __launch_bounds__(512, 1) void wgrad_x3_row3_kernel(WgradArgs p) {
-    constexpr int WAVES = 8, BKP = 32, S = 3;
+template <int BM, int BN, int S = 3, int OCC = 1>
+__global__ __launch_bounds__((BM / 32) * (BN / 32) * 64, OCC) void wgrad_x3_row3_kernel(WgradArgs p) {
+    constexpr int WAVES = (BM / 32) * (BN / 32), BKP = 32;
     constexpr int WAVES_N = BN / 32;
-    static_assert((BM / 32) * WAVES_N == WAVES, "8 waves of 32 x 32");
+    static_assert(S >= 2 && S <= 3, "stages");
     constexpr int RA = 6 * BM, RBB = 6 * BN;
     constexpr int HALO = BKP + 2;
     constexpr int AI = (HALO * RA + 1024 * WAVES - 1) / (1024 * WAVES);  // per wave
@@ -611,8 +620,8 @@ __global__ __launch_bounds__(512, 1) void wgrad_x3_row3_kernel(WgradArgs p) {
     for (int kc = 0; kc < nk; ++kc) {
         if (kc + S - 1 < nk) issue(kc + S - 1, (kc + S - 1) % S);
         const int ahead = min(S - 1, nk - 1 - kc);
-        if (ahead >= 2) x3_wait_vm<2 * GPC>();
-        else if (ahead == 1) x3_wait_vm<GPC>();
+        if (S >= 3 && ahead >= 2) x3_wait_vm<(S >= 3 ? 2 : 1) * GPC>();
+        else if (ahead >= 1) x3_wait_vm<GPC>();
         else x3_wait_vm<0>();
         x3_barrier();
         const unsigned sb = x3_lds_u32(smem) + (kc % S) * STAGE;
@@ -711,50 +720,52 @@ __global__ __launch_bounds__(256) void to_x3_kernel(const float* __restrict__ sr
                                                     const float* __restrict__ scale,
                                                     const float* __restrict__ shift, int relu, int64_t P,
                                                     uint16_t* __restrict__ dst, int dld, int doff) {
-    const int g8 = C / 8;
-    const int oct = threadIdx.x % g8, r0 = threadIdx.x / g8, rstep = 256 / g8;
+    const int g8 = C / 8, G = min(g8, 256);  // octets per pass (C > 2048: several passes)
+    const int r0 = threadIdx.x / G, rstep = 256 / G;
     if (r0 >= rstep) return;
-    const int c = oct * 8;
-    float sc[8], sh[8];
-    if (scale) {
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const f32x4 a = *(const f32x4*)(scale + c + 4 * h), b = *(const f32x4*)(shift + c + 4 * h);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                sc[4 * h + j] = a[j];
-                sh[4 * h + j] = b[j];
-            }
-        }
-    }
-    const int cc = doff + c;
-    uint16_t* dcol = dst + (cc >> 5) * 96 + (cc & 31);
     const int64_t mb = (int64_t)blockIdx.x * X3_PREP_RPB;
     const int64_t me = min(mb + X3_PREP_RPB, P);
-    auto load = [&](int64_t m, float (&v)[8]) {
-        const float* sp = src + m * ld + off + c;
-        const f32x4 v0 = *(const f32x4*)sp, v1 = *(const f32x4*)(sp + 4);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            v[j] = v0[j];
-            v[4 + j] = v1[j];
-        }
+    for (int oct = threadIdx.x % G; oct < g8; oct += G) {
+        const int c = oct * 8;
+        float sc[8], sh[8];
         if (scale) {
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                float t = __builtin_fmaf(sc[j], v[j], sh[j]);
-                if (c + j < relu) t = fmaxf(t, 0.f);
-                v[j] = t;
+            for (int h = 0; h < 2; ++h) {
+                const f32x4 a = *(const f32x4*)(scale + c + 4 * h), b = *(const f32x4*)(shift + c + 4 * h);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    sc[4 * h + j] = a[j];
+                    sh[4 * h + j] = b[j];
+                }
             }
         }
-    };
-    for (int64_t m = mb + r0; m < me; m += 2 * rstep) {
-        const int64_t m2 = m + rstep;
-        float v[8], w[8];
-        load(m, v);
-        if (m2 < me) load(m2, w);
-        x3_store8(v, dcol + m * 3 * (int64_t)dld);
-        if (m2 < me) x3_store8(w, dcol + m2 * 3 * (int64_t)dld);
+        const int cc = doff + c;
+        uint16_t* dcol = dst + (cc >> 5) * 96 + (cc & 31);
+        auto load = [&](int64_t m, float (&v)[8]) {
+            const float* sp = src + m * ld + off + c;
+            const f32x4 v0 = *(const f32x4*)sp, v1 = *(const f32x4*)(sp + 4);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                v[j] = v0[j];
+                v[4 + j] = v1[j];
+            }
+            if (scale) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    float t = __builtin_fmaf(sc[j], v[j], sh[j]);
+                    if (c + j < relu) t = fmaxf(t, 0.f);
+                    v[j] = t;
+                }
+            }
+        };
+        for (int64_t m = mb + r0; m < me; m += 2 * rstep) {
+            const int64_t m2 = m + rstep;
+            float v[8], w[8];
+            load(m, v);
+            if (m2 < me) load(m2, w);
+            x3_store8(v, dcol + m * 3 * (int64_t)dld);
+            if (m2 < me) x3_store8(w, dcol + m2 * 3 * (int64_t)dld);
+        }
     }
 }
 
@@ -769,36 +780,38 @@ __global__ __launch_bounds__(256) void bn_dz_x3_kernel(const float* __restrict__
                                                        const float* __restrict__ coef, int mask,
                                                        uint16_t* __restrict__ dz3, float* __restrict__ bpart) {
     __shared__ float red[256 * 8];
-    const int g8 = C / 8;
-    const int oct = threadIdx.x % g8, r0 = threadIdx.x / g8, rstep = 256 / g8;
-    const int c = oct * 8;
+    const int g8 = C / 8, G = min(g8, 256);  // octets per pass (bias sums: C <= 2048, one pass)
+    const int r0 = threadIdx.x / G, rstep = 256 / G;
     const bool active = r0 < rstep;  // threads past the last complete row group idle
-    f32x4 ka[2], kb[2], kc[2], km[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        ka[h] = *(const f32x4*)(coef + c + 4 * h);
-        kb[h] = *(const f32x4*)(coef + C + c + 4 * h);
-        kc[h] = *(const f32x4*)(coef + 2 * C + c + 4 * h);
-        km[h] = *(const f32x4*)(coef + 3 * C + c + 4 * h);
-    }
-    float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     const int64_t mb = (int64_t)blockIdx.x * X3_DZ_RPB;
     const int64_t me = min(mb + X3_DZ_RPB, P);
-    for (int64_t m = mb + r0; active && m < me; m += rstep) {
-        float v[8];
+    float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int oct = threadIdx.x % G; active && oct < g8; oct += G) {
+        const int c = oct * 8;
+        f32x4 ka[2], kb[2], kc[2], km[2];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-            const f32x4 dv = *(const f32x4*)(d + m * C + c + 4 * h);
-            const f32x4 yv = *(const f32x4*)(y + m * ld + off + c + 4 * h);
-            const f32x4 r = bn_dz4(ka[h], dv, kb[h], yv, km[h], kc[h]);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) v[4 * h + j] = (!mask || yv[j] > 0.f) ? r[j] : 0.f;
+            ka[h] = *(const f32x4*)(coef + c + 4 * h);
+            kb[h] = *(const f32x4*)(coef + C + c + 4 * h);
+            kc[h] = *(const f32x4*)(coef + 2 * C + c + 4 * h);
+            km[h] = *(const f32x4*)(coef + 3 * C + c + 4 * h);
         }
+        for (int64_t m = mb + r0; m < me; m += rstep) {
+            float v[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) cs[j] += v[j];
-        x3_store8(v, dz3 + m * 3 * (int64_t)C + (c >> 5) * 96 + (c & 31));
+            for (int h = 0; h < 2; ++h) {
+                const f32x4 dv = *(const f32x4*)(d + m * C + c + 4 * h);
+                const f32x4 yv = *(const f32x4*)(y + m * ld + off + c + 4 * h);
+                const f32x4 r = bn_dz4(ka[h], dv, kb[h], yv, km[h], kc[h]);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) v[4 * h + j] = (!mask || yv[j] > 0.f) ? r[j] : 0.f;
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) cs[j] += v[j];
+            x3_store8(v, dz3 + m * 3 * (int64_t)C + (c >> 5) * 96 + (c & 31));
+        }
     }
-    if (!bpart) return;
+    if (!bpart) return;  // (the launcher allows bias sums for C <= 2048 only)
 #pragma unroll
     for (int j = 0; j < 8; ++j) red[threadIdx.x * 8 + j] = active ? cs[j] : 0.f;
     __syncthreads();
@@ -849,7 +862,7 @@ int launch_rowgemm_x3(const RowGemmArgs& a, int tile, hipStream_t s) {
 int k_to_x3(const float* src, int ld, int off, int C, const float* scale, const float* shift,
             int relu, int64_t P, uint16_t* dst, int dld, int doff, hipStream_t s) {
     if (C % 32 || dld % 32 || doff % 32 || ld % 4 || off % 4) return -1;
-    if (C > 2048 || P < 1) return -1;
+    if (P < 1) return -1;
     const int blocks = (int)((P + X3_PREP_RPB - 1) / X3_PREP_RPB);
     hipLaunchKernelGGL(to_x3_kernel, dim3(blocks), dim3(256), 0, s, src, ld, off, C, scale, shift,
                        relu, P, dst, dld, doff);
@@ -857,8 +870,8 @@ int k_to_x3(const float* src, int ld, int off, int C, const float* scale, const 
 }
 
 int wgrad_x3_tile_dims(int tile, int* bm, int* bn) {
-    if (tile == 2 || tile == 3) {  // tap-row: BM x BN per tap, three taps per block
-        *bm = tile == 2 ? 64 : 128;
+    if (tile >= 2 && tile <= 4) {  // tap-row: BM x BN per tap, three taps per block
+        *bm = tile == 3 ? 128 : 64;
         *bn = tile == 2 ? 128 : 64;
         return 0;
     }
@@ -879,16 +892,19 @@ int wgrad_x3_tile_dims(int tile, int* bm, int* bn) {
 int launch_wgrad_x3(const WgradArgs& a, int tile, hipStream_t s) {
     if (a.ascale || a.bcoef || a.bias_slab || !a.zero16 || a.P < 1) return -1;
     if (a.aoff % 32 || a.boff % 32 || a.lda % 32 || a.ldb % 32) return -1;
-    if (tile == 2 || tile == 3) {  // tap-row kernel: 3x3 convs, W % 32 == 0
-        const int bm = tile == 2 ? 64 : 128, bn = tile == 2 ? 128 : 64;
+    if (tile >= 2 && tile <= 4) {  // tap-row kernel: 3x3 convs, W % 32 == 0
+        int bm = 0, bn = 0;
+        wgrad_x3_tile_dims(tile, &bm, &bn);
         if (a.amode != G_CONV3 || a.bmode != G_IDENT || a.Mw != 9 * a.CA || a.Nw != a.CB ||
             a.CA % bm || a.CB % bn || a.W % 32 || a.pps % 32 || a.P % 32)
             return -1;
         const dim3 grid((a.CA / bm) * 3 * (a.CB / bn) * a.splits);
         if (tile == 2)
             hipLaunchKernelGGL((wgrad_x3_row3_kernel<64, 128>), grid, dim3(512), 0, s, a);
-        else
+        else if (tile == 3)
             hipLaunchKernelGGL((wgrad_x3_row3_kernel<128, 64>), grid, dim3(512), 0, s, a);
+        else  // 64 x 64: four waves, two LDS stages, two blocks per CU
+            hipLaunchKernelGGL((wgrad_x3_row3_kernel<64, 64, 2, 2>), grid, dim3(256), 0, s, a);
         return (int)hipGetLastError();
     }
 #define WX3G(AM, BMD)                                      \
@@ -907,7 +923,7 @@ int x3_dz_blocks(int64_t P) { return (int)((P + X3_DZ_RPB - 1) / X3_DZ_RPB); }
 
 int k_bn_dz_x3(const float* d, const float* y, int ld, int off, int64_t P, int C, const float* coef,
                int mask, uint16_t* dz3, float* bpart, hipStream_t s) {
-    if (C % 32 || C > 2048 || ld % 4 || off % 4 || P < 1) return -1;
+    if (C % 32 || (bpart && C > 2048) || ld % 4 || off % 4 || P < 1) return -1;
     hipLaunchKernelGGL(bn_dz_x3_kernel, dim3(x3_dz_blocks(P)), dim3(256), 0, s, d, y, ld, off, P, C, coef,
                        mask, dz3, bpart);
     return (int)hipGetLastError();

@@ -158,6 +158,7 @@ struct Options {
     int x3_tile = -1;          // its row-GEMM tile (-1 = x3_tile())
     int x3_wtile = -1;         // its weight-gradient tile (-1 = by channel counts)
     int x3_wblocks = 1536;     // split-K target (blocks) of its 128x128 weight gradients
+    int x3_n64 = 2;            // its row-GEMM tile for 64 outputs (2 = 128x64, 3 = 256x64)
 };
 struct OptionDesc {
     const char* name;
@@ -205,6 +206,7 @@ const OptionDesc OPTION_TABLE[] = {
     {"x3_tile", &Options::x3_tile},
     {"x3_wtile", &Options::x3_wtile},
     {"x3_wblocks", &Options::x3_wblocks},
+    {"x3_n64", &Options::x3_n64},
 };
 
 }  // namespace
@@ -758,7 +760,7 @@ int x3_tile(const unet_ctx* c, const RowGemmArgs& g) {
         const int64_t blocks = (int64_t)(g.M + 255) / 256 * (g.N / 128);
         return blocks >= 256 ? 0 : 1;
     }
-    return 2;
+    return c->opt.x3_n64;
 }
 
 // weight gradient: 128x128 tile where both channel counts allow it, else 64x64; split-K over
@@ -773,6 +775,7 @@ WgradCfg x3_wgrad_cfg(const unet_ctx* c, int CA, int tapsA, int CB, int tapsB, i
     const bool r3 = tapsA == 9 && tapsB == 1 && row_w % 32 == 0 && row_w > 0;
     if (r3 && CA % 64 == 0 && CB % 128 == 0) w.tile = 2;
     else if (r3 && CA % 128 == 0 && CB % 64 == 0) w.tile = 3;
+    else if (r3 && CA % 64 == 0 && CB % 64 == 0) w.tile = 4;
     if (c->opt.x3_wtile >= 0) {
         int bm = 0, bn = 0;
         const int t = c->opt.x3_wtile;
@@ -783,7 +786,7 @@ WgradCfg x3_wgrad_cfg(const unet_ctx* c, int CA, int tapsA, int CB, int tapsB, i
     w.bkp = 32;
     const int64_t tiles = w.tile >= 2 ? (int64_t)(CA / w.bm) * 3 * (CB / w.bn)
                                       : (int64_t)(tapsA * CA / w.bm) * (tapsB * CB / w.bn);
-    const int64_t target = (int64_t)c->opt.x3_wblocks * (w.tile == 1 ? 4 : 1);
+    const int64_t target = (int64_t)c->opt.x3_wblocks * (w.tile == 1 ? 4 : w.tile == 4 ? 2 : 1);
     int64_t splits = std::max<int64_t>(1, (target + tiles - 1) / tiles);
     int64_t pps = (P + splits - 1) / splits;
     pps = (pps + 255) / 256 * 256;
