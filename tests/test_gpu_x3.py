@@ -144,3 +144,25 @@ def test_x3_tap_row_wgrad_matches_one_tap():
     worst = max(norm_rel(outs[0][1][k].cpu(), g.cpu()) for k, g in outs[1][1].items())
     print(f"tap-row vs one-tap x3 weight gradients: worst norm-rel {worst:.2e}")
     assert worst <= 1e-5
+
+
+def test_x3_convt_into_decoder_image_bit_identical():
+    """Option convt16 on the x3 path: the ConvT forward's epilogue writes the x3 split of its
+    output straight into the decoder conv's kept x3 image (the same RNE splits of the same
+    f32 values the prep pass forms) and that conv's prep converts the skip half only.  One
+    training step at B=2 128x128 is bit-identical to convt16 = 0."""
+    import unet_hip
+    from _helpers import options
+    x, t = inputs(23, 2, 128, 128)
+    outs = []
+    for flag in (0, 1):
+        m = hip_model(O.make_params(42), DEV)
+        with options(m.flatten_().rt, convt16=flag):
+            logits = m(x.to(DEV))
+            l = unet_hip.seg_losses(logits, t.to(DEV))
+            (l[0] + l[1]).backward()
+            torch.cuda.synchronize()
+        outs.append((logits.detach().clone(), m._state.grad_arena.clone()))
+        del m
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])

@@ -89,6 +89,8 @@ struct RowGemmArgs {
     const void* zero16;   // rowgemm16: >= 16 zero bytes (padding taps / rows past M)
     uint16_t* out16;      // E_CONVT: store bf16(result) into this image (ld ldo, offset ooff)
                           // instead of f32 into out (the bf16 consumer's operand image)
+    uint16_t* out3;       // E_CONVT: store the x3 split of the result into this x3 image (ldo
+                          // channels per row, channel offset ooff) instead of f32 into out
 };
 
 struct WgradArgs {

@@ -328,7 +328,20 @@ __device__ __forceinline__ void row_epilogue(const RowGemmArgs& p, f32x16 (&acc)
                 if (m >= p.M) continue;
                 const Pix q = decode_fast(m, H, W, rH, rW);
                 const size_t ob = (size_t)(q.img * 2 * H + 2 * q.y) * (2 * W) + 2 * q.x;
-                if (p.out16) {  // bf16 straight into the consumer's operand image (RNE, as k_to_bf16)
+                if (p.out3) {  // x3 split straight into the consumer's operand image (as k_to_x3)
+#pragma unroll
+                    for (int nt = 0; nt < NT; ++nt) {
+                        const float v = acc[mt][nt][r] + bb[nt];
+                        const __bf16 h = (__bf16)v;
+                        const float r1 = v - (float)h;
+                        const __bf16 mm = (__bf16)r1;
+                        const int ch = p.ooff + co_[nt];
+                        __bf16* d = (__bf16*)p.out3 + (ob + coff[nt]) * 3 * (size_t)p.ldo + (ch >> 5) * 96 + (ch & 31);
+                        d[0] = h;
+                        d[32] = mm;
+                        d[64] = (__bf16)(r1 - (float)mm);
+                    }
+                } else if (p.out16) {  // bf16 straight into the consumer's operand image (RNE, as k_to_bf16)
 #pragma unroll
                     for (int nt = 0; nt < NT; ++nt)
                         ((__bf16*)p.out16)[(ob + coff[nt]) * p.ldo + p.ooff + co_[nt]] =

@@ -1270,8 +1270,15 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
             g.emode = c->bn_relu ? E_STATS : E_BIAS_RELU_STATS;
             if (p.pack3 && x3_conv_on(c, C.cin, C.cout)) {
                 uint16_t* img = p.x3[i] ? p.x3[i] : p.s3;
-                RUN("prep_x3", 0, k_to_x3(a.ptr, a.ld, a.off, C.cin, a.scale, a.shift, a.relu, M, img,
-                                          C.cin, 0, s));
+                if (up16[i]) {  // the ConvT stored the up half's x3 split: convert the skip half
+                    const int l = C.level, so = c->skip_off(l), ch = c->ch(l);
+                    const int rl = std::min(std::max(a.relu - so, 0), ch);
+                    RUN("prep_x3", 0, k_to_x3(a.ptr, a.ld, a.off + so, ch, a.scale + so, a.shift + so, rl,
+                                              M, img, C.cin, so, s));
+                } else {
+                    RUN("prep_x3", 0, k_to_x3(a.ptr, a.ld, a.off, C.cin, a.scale, a.shift, a.relu, M, img,
+                                              C.cin, 0, s));
+                }
                 use_x3(p, g, img, C.cin, p.pack3 + 3 * C.pf);
                 const int tile = x3_tile(c, g);
                 R = bn_groups(M);
@@ -1340,6 +1347,15 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
             RUN("prep_x3", 0, k_to_x3(g.a, g.lda, g.aoff, T.cin, g.ascale, g.ashift, g.arelu, g.M, img,
                                       T.cin, 0, s));
             use_x3(p, g, img, T.cin, p.pack3 + 3 * T.pf);
+            // option convt16 (x3 training): the up half of the decoder's concat goes straight
+            // into that conv's kept x3 image, its only reader; the conv's prep pass then
+            // converts the skip half only
+            const int idec = 2 * (D + 1 + k);
+            const ConvL& Cd = c->conv[idec];
+            if (c->opt.convt16 && p.x3[idec] && x3_conv_on(c, Cd.cin, Cd.cout)) {
+                g.out3 = p.x3[idec];
+                up16[idec] = true;
+            }
             const int tile = x3_tile(c, g);
             RUN(xlabel("convT_fwd", tile, 100 + k), 2.0 * g.M * g.N * g.K, launch_rowgemm_x3(g, tile, s));
             return 0;

@@ -23,6 +23,15 @@ from collections import defaultdict
 
 def short(name):
     """rocprofv3 kernel name -> bench.py label (rowgemm_BMxBNxBK / wgrad_BMxBNxBKP)."""
+    m = re.search(r"wgrad_x3_row3_kernel<(\d+), (\d+)", name)
+    if m:  # split-bf16 f32 GEMMs (kernels_gemm_x3.hip)
+        return f"wx3r3_{m.group(1)}x{m.group(2)}"
+    m = re.search(r"WTileX3<(\d+), (\d+),", name)
+    if m:
+        return f"wx3_{m.group(1)}x{m.group(2)}"
+    m = re.search(r"TileX3<(\d+), (\d+),", name)
+    if m:
+        return f"x3_{m.group(1)}x{m.group(2)}"
     m = re.search(r"Wr3PipeTile<(\d+), (\d+), \d+, \d+, (\d+)", name)
     if m:
         return f"wgrad3p_{m.group(1)}x{m.group(2)}x{m.group(3)}"
