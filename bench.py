@@ -396,7 +396,7 @@ def main():
                  res_train_flops_per_image(S, S, args.base, args.depth) if cres else
                  train_flops_per_image(S, S)) * B
     bf16 = c4 and args.mfma == "bf16"
-    x3 = dom.startswith("x3_") or dom.startswith("wx3")
+    x3 = dom.startswith("x3") or dom.startswith("wx3")
     peak = BF16_MFMA_PEAK_TFLOPS if bf16 else X3_MFMA_PEAK_TFLOPS if x3 else FP32_MFMA_PEAK_TFLOPS
     roofline = {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 3),
                 "peak": peak, "unit": "TFLOP/s",

@@ -108,7 +108,8 @@ def test_x3_row_tile_choice_bit_identical(B, H, W):
     outs = []
     for tile, n64 in ((-1, 2), (0, 2), (1, 2), (2, 2), (-1, 3)):
         m = hip_model(O.make_params(42), DEV)
-        with options(m.flatten_().rt, x3_tile=tile, x3_n64=n64):
+        # (the tap-row halo tile sums K in another order: test_x3_halo_tile_matches_one_tap)
+        with options(m.flatten_().rt, x3_tile=tile, x3_n64=n64, x3_r3=0):
             logits = m(x.to(DEV))
             l = unet_hip.seg_losses(logits, t.to(DEV))
             (l[0] + l[1]).backward()
@@ -166,3 +167,30 @@ def test_x3_convt_into_decoder_image_bit_identical():
         del m
     assert torch.equal(outs[0][0], outs[1][0])
     assert torch.equal(outs[0][1], outs[1][1])
+
+
+def test_x3_halo_tile_matches_one_tap():
+    """The tap-row halo x3 GEMM (rowgemm_x3_row3_kernel, tile 4: one 32-channel group of one
+    tap row's halo feeds the three dx taps; default on the 256x128 3x3 GEMMs) against the
+    one-tap tile (option x3_r3 = 0): the same products summed in (dy, group, dx) instead of
+    (dy, dx, group) order, so logits and gradients agree to f32 summation noise.  B=2 at
+    256x256 (W = 256 .. 16 on the halo kernel) and 1 x 48 x 80 (off: W not a power of two)."""
+    import unet_hip
+    from _helpers import options
+    for (B, H, W) in ((2, 256, 256), (1, 48, 80)):
+        x, t = inputs(29, B, H, W)
+        outs = []
+        for r3 in (1, 0):
+            m = hip_model(O.make_params(42), DEV)
+            with options(m.flatten_().rt, x3_r3=r3):
+                logits = m(x.to(DEV))
+                l = unet_hip.seg_losses(logits, t.to(DEV))
+                (l[0] + l[1]).backward()
+                torch.cuda.synchronize()
+            outs.append((logits.detach().cpu().double(),
+                         {k: p.grad.detach().cpu().double() for k, p in m.named_parameters()}))
+            del m
+        el = norm_rel(outs[0][0], outs[1][0])
+        worst = max(norm_rel(outs[0][1][k], g) for k, g in outs[1][1].items())
+        print(f"{B}x{H}x{W}: halo vs one-tap logits {el:.2e}, worst grad {worst:.2e}")
+        assert el <= 1e-6 and worst <= 1e-4, (el, worst)

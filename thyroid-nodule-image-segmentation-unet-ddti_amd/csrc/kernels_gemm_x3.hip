@@ -83,7 +83,10 @@ struct TileX3 {
     static constexpr int THREADS = 64 * WAVES;
 };
 
-template <int AMODE, int EMODE, class T>
+// XP: speed-of-light ablations for tools/x3_probe.hip only (results are garbage): bit 0 drops
+// the A DMA, 1 the B DMA, 2 the LDS fragment reads, 3 the loop's waits and barriers; the
+// library instantiates XP = 0.
+template <int AMODE, int EMODE, class T, int XP = 0>
 __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_x3_kernel(RowGemmArgs p) {
     constexpr int BM = T::BM, BN = T::BN, WM = T::WM, WN = T::WN, S = T::S, BK = T::BK;
     constexpr int WAVES = T::WAVES, WAVES_N = BN / WN;
@@ -149,15 +152,19 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_x3_kernel(RowGemmA
         char* base = smem + st * STAGE;
 #pragma unroll
         for (int j = 0; j < AI; ++j) {
+            if (XP & 1) continue;
             bool valid;
             const int src = gather_src<AMODE>(tap, am[j], aq[j], H, W, valid);
             const uint16_t* g = (valid && aok[j]) ? a16 + (size_t)src * rowa + c0 * 3 + ace[j] : zero;
             x3_dma16(g, base + (j * WAVES + wave) * 1024);
         }
 #pragma unroll
-        for (int j = 0; j < BI; ++j)
+        for (int j = 0; j < BI; ++j) {
+            if (XP & 2) continue;
             x3_dma16(bok[j] ? bsrc[j] + k0 * 3 : zero, base + AREG + (j * WAVES + wave) * 1024);
+        }
     };
+    constexpr int GPCX = ((XP & 1) ? 0 : AI) + ((XP & 2) ? 0 : BI);  // DMA pieces actually issued
 
     constexpr int SA = T::SA;
     f32x16 acc[MT][NT], acl[SA ? MT : 1][SA ? NT : 1];
@@ -187,41 +194,56 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_x3_kernel(RowGemmA
     }
 
     const int nk = K / BK;
+    bf16x8 xa;  // XP & 4: a register operand
+#pragma unroll
+    for (int j = 0; j < 8; ++j) xa[j] = (__bf16)(float)(lane + j);
 #pragma unroll
     for (int s = 0; s < DIST; ++s)
         if (s < nk) issue(s, s);
     for (int kc = 0; kc < nk; ++kc) {
         if (kc + DIST < nk) issue(kc + DIST, (kc + DIST) % S);
         const int ahead = min(DIST, nk - 1 - kc);
-        if constexpr (DIST >= 3) {
-            if (ahead >= 3) x3_wait_vm<3 * GPC>();
-            else if (ahead == 2) x3_wait_vm<2 * GPC>();
-            else if (ahead == 1) x3_wait_vm<GPC>();
+        if constexpr (XP & 8) {
+        } else if constexpr (DIST >= 3) {
+            if (ahead >= 3) x3_wait_vm<3 * GPCX>();
+            else if (ahead == 2) x3_wait_vm<2 * GPCX>();
+            else if (ahead == 1) x3_wait_vm<GPCX>();
             else x3_wait_vm<0>();
         } else if constexpr (DIST == 2) {
-            if (ahead >= 2) x3_wait_vm<2 * GPC>();
-            else if (ahead == 1) x3_wait_vm<GPC>();
+            if (ahead >= 2) x3_wait_vm<2 * GPCX>();
+            else if (ahead == 1) x3_wait_vm<GPCX>();
             else x3_wait_vm<0>();
         } else {
-            if (ahead >= 1) x3_wait_vm<GPC>();
+            if (ahead >= 1) x3_wait_vm<GPCX>();
             else x3_wait_vm<0>();
         }
-        x3_barrier();
+        if constexpr (!(XP & 8)) x3_barrier();
         const char* base = smem + (kc % S) * STAGE;
 #pragma unroll
         for (int kk = 0; kk < BK / 16; ++kk) {
             const int c = kk * 2 + lh;
             bf16x8 af[MT][3], bfr[NT][3];
+            if constexpr (XP & 4) {  // operands from registers only (no LDS traffic)
 #pragma unroll
-            for (int mt = 0; mt < MT; ++mt)
+                for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-                for (int q = 0; q < 3; ++q)
-                    af[mt][q] = *(const bf16x8*)(base + aro[mt] + q * 64 + ((c ^ afx[mt]) << 4));
+                    for (int q = 0; q < 3; ++q) af[mt][q] = xa;
 #pragma unroll
-            for (int nt = 0; nt < NT; ++nt)
+                for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
-                for (int q = 0; q < 3; ++q)
-                    bfr[nt][q] = *(const bf16x8*)(base + bro[nt] + q * 64 + ((c ^ bfx[nt]) << 4));
+                    for (int q = 0; q < 3; ++q) bfr[nt][q] = xa;
+            } else {
+#pragma unroll
+                for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                    for (int q = 0; q < 3; ++q)
+                        af[mt][q] = *(const bf16x8*)(base + aro[mt] + q * 64 + ((c ^ afx[mt]) << 4));
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+                    for (int q = 0; q < 3; ++q)
+                        bfr[nt][q] = *(const bf16x8*)(base + bro[nt] + q * 64 + ((c ^ bfx[nt]) << 4));
+            }
 #pragma unroll
             for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
@@ -230,9 +252,12 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_x3_kernel(RowGemmA
                     else acc[mt][nt] = mfma_x3(af[mt], bfr[nt], acc[mt][nt]);
                 }
         }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        x3_barrier();
+        if constexpr (!(XP & 8)) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            x3_barrier();
+        }
     }
+    if constexpr (XP & 8) x3_wait_vm<0>();
     if constexpr (SA) {
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt)
@@ -240,6 +265,184 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_x3_kernel(RowGemmA
             for (int nt = 0; nt < NT; ++nt) acc[mt][nt] += acl[mt][nt];
     }
     row_epilogue<EMODE, BM, BN, WM, WN, true>(p, acc, m0, n0, tile_m, wm, wn, lane, tid, (float*)smem);
+}
+
+// ------------------------------------------------------------------------------------
+// Tap-row halo variant of the x3 3x3-conv GEMM (tile 4: 256 x 128, 8 waves of 64 x 64,
+// W >= 16 a power of two).  The one-tap kernel restages the block's 256 A rows for each of the
+// 9 taps, and its A gather is what holds it at ~0.55 of its MFMA-only speed (profiles/
+// r04_x3_ablation.txt).  Here one stage holds the HALO of one tap row dy for one 32-channel
+// group -- the block's image rows shifted by dy - 1, one extra pixel either side (ROWS x
+// (SEG + 2) <= 288 x3 rows) -- and the three dx taps read A rows h + dx from it: a third of
+// the A staging.  The x3 rows are 192 B, so the halo and the B rows of three taps (3 x 24 KB)
+// cannot be double-buffered together; B streams per sub-step (dy, group, dx) through its own
+// two-slot ring instead (2 x 56 KB halo + 2 x 24 KB B = 160 KB).  Per sub-step: issue B of the
+// next sub-step (and, on dx = 0, the next group's halo), wait, barrier, 2 k-steps x 4 x 6
+// MFMAs per wave, barrier.
+//   geometry (as rowgemm16_row3_kernel): SEG = min(W, 256) output pixels per image row of the
+//   tile, ROWS = 256 / SEG; halo row h = r (SEG + 2) + xl + 1 holds pixel (row r shifted by
+//   dy - 1, column x0 + xl), xl = -1 .. SEG; output pixel (r, xo) reads halo row
+//   r (SEG + 2) + xo + dx for tap dx.  16 consecutive output pixels stay in one image row
+//   (SEG >= 16), so a ds_read_b128 phase reads 16 consecutive halo rows: conflict-free.
+//   K order: dy, channel group, dx, k -- a reordering of the one-tap kernel's sum, so results
+//   agree with the other tiles to f32 rounding, not bitwise.
+// ------------------------------------------------------------------------------------
+template <int EMODE>
+__global__ __launch_bounds__(512, 1) void rowgemm_x3_row3_kernel(RowGemmArgs p) {
+    constexpr int BM = 256, BN = 128, WM = 64, WN = 64, BK = 32, WAVES = 8, WAVES_N = BN / WN;
+    constexpr int MT = WM / 32, NT = WN / 32;
+    constexpr int RB = 192;
+    constexpr int AR = 288;                                   // halo rows (W = 16: 16 x 18)
+    constexpr int AI = (AR * RB + 1024 * WAVES - 1) / (1024 * WAVES);  // 7 A pieces per wave
+    constexpr int BI = BN * RB / (1024 * WAVES);              // 3 B pieces per wave
+    static_assert(BI * 1024 * WAVES == BN * RB, "B loader");
+    constexpr int AREG = AI * WAVES * 1024, BREG = BI * WAVES * 1024;  // 56 KB, 24 KB
+    constexpr int SMEM = 2 * AREG + 2 * BREG;                 // 160 KB
+    static_assert(SMEM >= 2 * (BM / 64) * BN * 8, "epilogue scratch");
+    __shared__ __attribute__((aligned(1024))) char smem[SMEM];
+    auto swz = [](int r) { return (r >> 2) & 3; };
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+    const int ntn = p.N / BN;
+    const int bid = p.xcd ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+    const int tile_m = bid / ntn, tile_n = bid - tile_m * ntn;
+    const int m0 = tile_m * BM, n0 = tile_n * BN;
+    const int H = p.H, W = p.W, C = p.C, K = p.K;
+    const int SEG = W < BM ? W : BM, HW = SEG + 2;
+    const int AROWS = (BM / SEG) * HW;
+    const size_t rowa = 3 * (size_t)p.lda, rowb = 3 * (size_t)K;
+
+    // A loader: lane of piece j fills halo bytes (j WAVES + wave) KB + 16 lane: halo row h,
+    // 16-B slot w / 16 of its 192 B; pixel of h at dy = 1 (-1: padding column / past the halo)
+    int acen[AI], ayr[AI], ace[AI];
+#pragma unroll
+    for (int j = 0; j < AI; ++j) {
+        const int o = ((j * WAVES + wave) * 64 + lane) * 16;
+        const int h = o / RB, w = o - h * RB;
+        const int r = h / HW, xl = h - r * HW - 1;
+        const int mrow = m0 + r * SEG;
+        bool ok = h < AROWS && mrow < p.M;
+        const Pix q = decode(ok ? mrow : 0, H, W);
+        ok = ok && q.x + xl >= 0 && q.x + xl < W;
+        acen[j] = ok ? mrow + xl : -1;
+        ayr[j] = q.y;
+        ace[j] = (w >> 6) * 32 + ((((w >> 4) & 3) ^ swz(h)) << 3);
+    }
+    const uint16_t* bsrc[BI];
+#pragma unroll
+    for (int j = 0; j < BI; ++j) {
+        const int o = ((j * WAVES + wave) * 64 + lane) * 16;
+        const int r = o / RB, w = o - r * RB;
+        bsrc[j] = p.bt16 + (size_t)(n0 + r) * rowb + (w >> 6) * 32 + ((((w >> 4) & 3) ^ swz(r)) << 3);
+    }
+    const uint16_t* zero = (const uint16_t*)p.zero16;
+    const uint16_t* a16 = p.a16 + (size_t)p.aoff * 3;
+    const int CC = C / BK;  // channel groups per tap
+    // sub-step s = (dy, group, dx): halo of group g = s / 3 (dy = g / CC), B of tap dy * 3 + dx
+    auto issue_a = [&](int g) {
+        const int dy = g / CC, c0 = (g - dy * CC) * BK;
+        char* base = smem + (g & 1) * AREG;
+#pragma unroll
+        for (int j = 0; j < AI; ++j) {
+            const int yy = ayr[j] + dy - 1;
+            const bool valid = acen[j] >= 0 && yy >= 0 && yy < H;
+            const uint16_t* src =
+                valid ? a16 + (size_t)(acen[j] + (dy - 1) * W) * rowa + c0 * 3 + ace[j] : zero;
+            x3_dma16(src, base + (j * WAVES + wave) * 1024);
+        }
+    };
+    auto issue_b = [&](int s) {
+        const int g = s / 3, dx = s - g * 3;
+        const int dy = g / CC, c0 = (g - dy * CC) * BK;
+        const int k0 = (dy * 3 + dx) * C + c0;
+        char* base = smem + 2 * AREG + (s & 1) * BREG;
+#pragma unroll
+        for (int j = 0; j < BI; ++j) x3_dma16(bsrc[j] + k0 * 3, base + (j * WAVES + wave) * 1024);
+    };
+
+    f32x16 acc[MT][NT], acl[MT][NT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = acl[i][j][r] = 0.f;
+    const int lh = lane >> 5, li = lane & 31;
+    int ahb[MT], bro[NT], bfx[NT];  // halo row of output pixel at dx = 0; B row offsets
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+        const int mo = wm * WM + mt * 32 + li;
+        const int r = mo / SEG;
+        ahb[mt] = r * HW + (mo - r * SEG);
+    }
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+        const int r = wn * WN + nt * 32 + li;
+        bro[nt] = r * RB;
+        bfx[nt] = swz(r);
+    }
+
+    const int ns = 9 * CC;  // sub-steps
+    issue_a(0);
+    issue_b(0);
+    for (int s = 0; s < ns; ++s) {
+        const int g = s / 3, dx = s - g * 3;
+        // next B (and, entering a group, the next group's halo) while this sub-step computes;
+        // then wait for this sub-step's B (and everything issued before it, its group's halo
+        // included).  Issue order: B(s), [A(g + 1) when s - 1 entered group g], B(s + 1),
+        // [A(g + 1) when s enters group g]: the pieces allowed in flight are those after B(s).
+        const bool nb = s + 1 < ns, na = dx == 0 && g + 1 < 3 * CC;
+        const bool pa = dx == 1 && g + 1 < 3 * CC;  // s - 1 issued the next halo after B(s)
+        if (nb) issue_b(s + 1);
+        if (na) issue_a(g + 1);
+        if (nb && (na || pa)) x3_wait_vm<AI + BI>();
+        else if (nb) x3_wait_vm<BI>();
+        else if (na || pa) x3_wait_vm<AI>();
+        else x3_wait_vm<0>();
+        x3_barrier();
+        const char* abase = smem + (g & 1) * AREG;
+        const char* bbase = smem + 2 * AREG + (s & 1) * BREG;
+#pragma unroll
+        for (int kk = 0; kk < BK / 16; ++kk) {
+            const int c = kk * 2 + lh;
+            bf16x8 af[MT][3], bfr[NT][3];
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt) {
+                const int h = ahb[mt] + dx;
+#pragma unroll
+                for (int q = 0; q < 3; ++q)
+                    af[mt][q] = *(const bf16x8*)(abase + h * RB + q * 64 + ((c ^ swz(h)) << 4));
+            }
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+                for (int q = 0; q < 3; ++q)
+                    bfr[nt][q] = *(const bf16x8*)(bbase + bro[nt] + q * 64 + ((c ^ bfx[nt]) << 4));
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt) mfma_x3s(af[mt], bfr[nt], acc[mt][nt], acl[mt][nt]);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        x3_barrier();
+    }
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) acc[mt][nt] += acl[mt][nt];
+    row_epilogue<EMODE, BM, BN, WM, WN, true>(p, acc, m0, n0, tile_m, wm, wn, lane, tid, (float*)smem);
+}
+
+template <int EMODE>
+static int x3r3_go(const RowGemmArgs& a, hipStream_t s) {
+    // BM % W == 0 or W % BM == 0 keeps a tile on whole rows / row segments; W >= 16 bounds the halo
+    if (a.amode != G_CONV3 || a.N % 128 || a.C % 32 || a.K != 9 * a.C) return -1;
+    if (a.W < 16 || (256 % a.W && a.W % 256)) return -1;
+    const dim3 grid(((a.M + 255) / 256) * (a.N / 128));
+    hipLaunchKernelGGL((rowgemm_x3_row3_kernel<EMODE>), grid, dim3(512), 0, s, a);
+    return (int)hipGetLastError();
 }
 
 // tiles (split accumulators; probe: profiles/r04_x3_probe_*.txt): 0 = 256x128 (8 waves of
@@ -252,17 +455,21 @@ using TX2 = TileX3<128, 64, 64, 32, 2, 2, 1>;
 using TX3 = TileX3<256, 64, 64, 32, 2, 1, 1>;
 #define ROWGEMM_X3_TILES(X) X(0, TX0) X(1, TX1) X(2, TX2) X(3, TX3)
 
-template <int AMODE, int EMODE, class T>
+template <int AMODE, int EMODE, class T, int XP = 0>
 static int x3_go(const RowGemmArgs& a, hipStream_t s) {
     if (a.N % T::BN || a.C % 32 || a.K % 32) return -1;
     if (EMODE == E_CONVT && (a.cout % T::BN) && (T::BN % a.cout)) return -1;
     const dim3 grid(((a.M + T::BM - 1) / T::BM) * (a.N / T::BN));
-    hipLaunchKernelGGL((rowgemm_x3_kernel<AMODE, EMODE, T>), grid, dim3(T::THREADS), 0, s, a);
+    hipLaunchKernelGGL((rowgemm_x3_kernel<AMODE, EMODE, T, XP>), grid, dim3(T::THREADS), 0, s, a);
     return (int)hipGetLastError();
 }
 
 template <int AMODE, int EMODE>
 static int x3_tile(const RowGemmArgs& a, int tile, hipStream_t s) {
+    if (tile == 4) {  // tap-row halo kernel (3x3 convs)
+        if constexpr (AMODE == G_CONV3) return x3r3_go<EMODE>(a, s);
+        return -1;
+    }
 #define X3_CASE(id, T) \
     if (tile == id) return x3_go<AMODE, EMODE, T>(a, s);
     ROWGEMM_X3_TILES(X3_CASE)
@@ -827,6 +1034,11 @@ __global__ __launch_bounds__(256) void bn_dz_x3_kernel(const float* __restrict__
 }  // namespace
 
 int rowgemm_x3_tile_dims(int tile, int* bm, int* bn) {
+    if (tile == 4) {  // tap-row halo 256 x 128
+        *bm = 256;
+        *bn = 128;
+        return 0;
+    }
 #define X3_DIMS(id, T)  \
     if (tile == id) {   \
         *bm = T::BM;    \
@@ -927,4 +1139,15 @@ int k_bn_dz_x3(const float* d, const float* y, int ld, int off, int64_t P, int C
     hipLaunchKernelGGL(bn_dz_x3_kernel, dim3(x3_dz_blocks(P)), dim3(256), 0, s, d, y, ld, off, P, C, coef,
                        mask, dz3, bpart);
     return (int)hipGetLastError();
+}
+
+// speed-of-light ablations of tile 0 on the E_STORE 3x3 GEMM (tools/x3_probe.hip): -2 when
+// not applicable
+int launch_rowgemm_x3_xp(const RowGemmArgs& a, int xp, hipStream_t s) {
+    if (a.amode != G_CONV3 || a.emode != E_STORE) return -2;
+#define XPX(v) \
+    if (xp == v) return x3_go<G_CONV3, E_STORE, TX0, v>(a, s);
+    XPX(1) XPX(2) XPX(3) XPX(4) XPX(8) XPX(12) XPX(15) XPX(7)
+#undef XPX
+    return -2;
 }

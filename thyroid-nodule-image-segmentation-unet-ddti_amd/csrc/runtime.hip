@@ -159,6 +159,7 @@ struct Options {
     int x3_wtile = -1;         // its weight-gradient tile (-1 = by channel counts)
     int x3_wblocks = 1536;     // split-K target (blocks) of its 128x128 weight gradients
     int x3_n64 = 2;            // its row-GEMM tile for 64 outputs (2 = 128x64, 3 = 256x64)
+    int x3_r3 = 1;             // its 256x128 3x3 GEMMs on the tap-row halo kernel (tile 4)
 };
 struct OptionDesc {
     const char* name;
@@ -207,6 +208,7 @@ const OptionDesc OPTION_TABLE[] = {
     {"x3_wtile", &Options::x3_wtile},
     {"x3_wblocks", &Options::x3_wblocks},
     {"x3_n64", &Options::x3_n64},
+    {"x3_r3", &Options::x3_r3},
 };
 
 }  // namespace
@@ -755,10 +757,14 @@ int x3_tile(const unet_ctx* c, const RowGemmArgs& g) {
         if (rowgemm_x3_tile_dims(t, &bm, &bn) != 0 || g.N % bn) return false;
         return g.emode != E_CONVT || g.cout % bn == 0 || bn % g.cout == 0;
     };
-    if (c->opt.x3_tile >= 0 && fits(c->opt.x3_tile)) return c->opt.x3_tile;
+    // tile 4: the tap-row halo kernel (3x3 convs on rows of 16 .. 256k pixels, option x3_r3)
+    const bool r3ok = g.amode == G_CONV3 && g.W >= 16 && (256 % g.W == 0 || g.W % 256 == 0);
+    if (c->opt.x3_tile >= 0 && fits(c->opt.x3_tile) && (c->opt.x3_tile != 4 || r3ok))
+        return c->opt.x3_tile;
     if (g.N % 128 == 0 && fits(0)) {
         const int64_t blocks = (int64_t)(g.M + 255) / 256 * (g.N / 128);
-        return blocks >= 256 ? 0 : 1;
+        if (blocks < 256) return 1;
+        return c->opt.x3_r3 && r3ok ? 4 : 0;
     }
     return c->opt.x3_n64;
 }
@@ -820,7 +826,7 @@ std::string xlabel(const char* fam, int tile, int layer) {
     int bm = 0, bn = 0;
     rowgemm_x3_tile_dims(tile, &bm, &bn);
     char b[112];
-    snprintf(b, sizeof b, "%s/x3_%dx%d|%d", fam, bm, bn, layer);
+    snprintf(b, sizeof b, "%s/x3%s_%dx%d|%d", fam, tile == 4 ? "r3" : "", bm, bn, layer);
     return b;
 }
 

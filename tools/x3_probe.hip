@@ -44,7 +44,8 @@ static void probe_wgrad(int iters, void* zero);
 
 int main(int argc, char** argv) {
     const int iters = argc > 1 ? atoi(argv[1]) : 5;
-    const int what = argc > 2 ? atoi(argv[2]) : 3;  // bit 0 row GEMMs, bit 1 weight gradients
+    const int what = argc > 2 ? atoi(argv[2]) : 3;  // bit 0 row GEMMs, bit 1 weight gradients,
+                                                     // bit 2 speed-of-light ablations of tile 0
     Shape shapes[] = {
         {"L0 64->64 @256", 32, 256, 256, 64, 64},     {"L0 128->64 @256", 32, 256, 256, 128, 64},
         {"L0 64->128 @256 (dgrad)", 32, 256, 256, 64, 128},
@@ -60,7 +61,7 @@ int main(int argc, char** argv) {
     CK(hipEventCreate(&e1));
     if (what & 2) probe_wgrad(iters, zero);
     for (const Shape& sh : shapes) {
-        if (!(what & 1)) break;
+        if (!(what & 5)) break;
         const int M = sh.N * sh.H * sh.W, N = sh.Cout, C = sh.Cin, K = 9 * C;
         float *x, *w, *y32, *yx3;
         uint16_t *x3, *w3;
@@ -110,6 +111,18 @@ int main(int argc, char** argv) {
             CK(hipEventElapsedTime(&ms, e0, e1));
             return ms / iters;
         };
+        if (what & 4) {  // ablations: 1 no A DMA, 2 no B DMA, 4 no LDS reads, 8 no waits / barriers
+            if (N % 128) continue;
+            const float t0 = timeit([&] { return launch_rowgemm_x3(h, 0, 0); });
+            printf("%-26s M=%d N=%d K=%d  x3 tile 0: %.3f ms %.1f TF/s\n", sh.name, M, N, K, t0, fl / t0 / 1e9);
+            for (int xp : {1, 2, 3, 4, 8, 12, 7, 15}) {
+                const float tx = timeit([&] { return launch_rowgemm_x3_xp(h, xp, 0); });
+                printf("    xp %2d: %.3f ms %.1f TF/s\n", xp, tx, fl / tx / 1e9);
+            }
+            fflush(stdout);
+            CK(hipFree(x)); CK(hipFree(w)); CK(hipFree(y32)); CK(hipFree(yx3)); CK(hipFree(x3)); CK(hipFree(w3));
+            continue;
+        }
         const float t32 = timeit([&] { return launch_rowgemm_pipe(g, ptile, 0); });
         // the split pass of the activation (per layer in a real step; weights are per step)
         const float tsp = timeit([&] { return k_to_x3(x, C, 0, C, nullptr, nullptr, 0, M, x3, C, 0, 0); });
@@ -120,9 +133,8 @@ int main(int argc, char** argv) {
         std::vector<float> hx, hw;
         bool host_loaded = false;
         for (int tile = 0; tile <= 6; ++tile) {
-            int bm, bn;
-            rowgemm_x3_tile_dims(tile, &bm, &bn);
-            if (N % bn) continue;
+            int bm = 0, bn = 0;
+            if (rowgemm_x3_tile_dims(tile, &bm, &bn) != 0 || N % bn) continue;
             CK(hipMemset(yx3, 0, (size_t)M * N * 4));
             const float tx = timeit([&] { return launch_rowgemm_x3(h, tile, 0); });
             std::vector<float> rx((size_t)M * N);
@@ -273,9 +285,8 @@ static void probe_wgrad(int iters, void* zero) {
         CK(hipMemcpy(hx.data(), x, hx.size() * 4, hipMemcpyDeviceToHost));
         CK(hipMemcpy(hd.data(), dz, hd.size() * 4, hipMemcpyDeviceToHost));
         for (int tile = 0; tile <= 6; ++tile) {
-            int bm, bn;
-            wgrad_x3_tile_dims(tile, &bm, &bn);
-            if (CA % bm || Nw % bn) continue;
+            int bm = 0, bn = 0;
+            if (wgrad_x3_tile_dims(tile, &bm, &bn) != 0 || CA % bm || Nw % bn) continue;
             CK(hipMemset(slab, 0, (size_t)splits * Mw * Nw * 4));
             const float tx = timeit([&] { return launch_wgrad_x3(v, tile, 0); });
             std::vector<double> rx = reduce();
