@@ -287,16 +287,16 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_x3_kernel(RowGemmA
 //   K order: dy, channel group, dx, k -- a reordering of the one-tap kernel's sum, so results
 //   agree with the other tiles to f32 rounding, not bitwise.
 // ------------------------------------------------------------------------------------
-template <int EMODE>
+// BN = 128 (8 waves of 64 x 64) or 64 (8 waves of 64 x 32, B pieces padded to 2 per wave)
+template <int EMODE, int BN = 128>
 __global__ __launch_bounds__(512, 1) void rowgemm_x3_row3_kernel(RowGemmArgs p) {
-    constexpr int BM = 256, BN = 128, WM = 64, WN = 64, BK = 32, WAVES = 8, WAVES_N = BN / WN;
+    constexpr int BM = 256, WM = 64, WN = BN / 2, BK = 32, WAVES = 8, WAVES_N = 2;
     constexpr int MT = WM / 32, NT = WN / 32;
     constexpr int RB = 192;
     constexpr int AR = 288;                                   // halo rows (W = 16: 16 x 18)
     constexpr int AI = (AR * RB + 1024 * WAVES - 1) / (1024 * WAVES);  // 7 A pieces per wave
-    constexpr int BI = BN * RB / (1024 * WAVES);              // 3 B pieces per wave
-    static_assert(BI * 1024 * WAVES == BN * RB, "B loader");
-    constexpr int AREG = AI * WAVES * 1024, BREG = BI * WAVES * 1024;  // 56 KB, 24 KB
+    constexpr int BI = (BN * RB + 1024 * WAVES - 1) / (1024 * WAVES);  // 3 / 2 B pieces per wave
+    constexpr int AREG = AI * WAVES * 1024, BREG = BI * WAVES * 1024;  // 56 KB, 24 / 16 KB
     constexpr int SMEM = 2 * AREG + 2 * BREG;                 // 160 KB
     static_assert(SMEM >= 2 * (BM / 64) * BN * 8, "epilogue scratch");
     __shared__ __attribute__((aligned(1024))) char smem[SMEM];
@@ -331,11 +331,14 @@ __global__ __launch_bounds__(512, 1) void rowgemm_x3_row3_kernel(RowGemmArgs p) 
         ace[j] = (w >> 6) * 32 + ((((w >> 4) & 3) ^ swz(h)) << 3);
     }
     const uint16_t* bsrc[BI];
+    bool bok[BI];
 #pragma unroll
     for (int j = 0; j < BI; ++j) {
         const int o = ((j * WAVES + wave) * 64 + lane) * 16;
         const int r = o / RB, w = o - r * RB;
-        bsrc[j] = p.bt16 + (size_t)(n0 + r) * rowb + (w >> 6) * 32 + ((((w >> 4) & 3) ^ swz(r)) << 3);
+        bok[j] = r < BN;
+        bsrc[j] = p.bt16 + (size_t)(n0 + (bok[j] ? r : 0)) * rowb + (w >> 6) * 32 +
+                  ((((w >> 4) & 3) ^ swz(r)) << 3);
     }
     const uint16_t* zero = (const uint16_t*)p.zero16;
     const uint16_t* a16 = p.a16 + (size_t)p.aoff * 3;
@@ -359,7 +362,8 @@ __global__ __launch_bounds__(512, 1) void rowgemm_x3_row3_kernel(RowGemmArgs p) 
         const int k0 = (dy * 3 + dx) * C + c0;
         char* base = smem + 2 * AREG + (s & 1) * BREG;
 #pragma unroll
-        for (int j = 0; j < BI; ++j) x3_dma16(bsrc[j] + k0 * 3, base + (j * WAVES + wave) * 1024);
+        for (int j = 0; j < BI; ++j)
+            x3_dma16(bok[j] ? bsrc[j] + k0 * 3 : zero, base + (j * WAVES + wave) * 1024);
     };
 
     f32x16 acc[MT][NT], acl[MT][NT];
@@ -435,13 +439,13 @@ __global__ __launch_bounds__(512, 1) void rowgemm_x3_row3_kernel(RowGemmArgs p) 
     row_epilogue<EMODE, BM, BN, WM, WN, true>(p, acc, m0, n0, tile_m, wm, wn, lane, tid, (float*)smem);
 }
 
-template <int EMODE>
+template <int EMODE, int BN>
 static int x3r3_go(const RowGemmArgs& a, hipStream_t s) {
     // BM % W == 0 or W % BM == 0 keeps a tile on whole rows / row segments; W >= 16 bounds the halo
-    if (a.amode != G_CONV3 || a.N % 128 || a.C % 32 || a.K != 9 * a.C) return -1;
+    if (a.amode != G_CONV3 || a.N % BN || a.C % 32 || a.K != 9 * a.C) return -1;
     if (a.W < 16 || (256 % a.W && a.W % 256)) return -1;
-    const dim3 grid(((a.M + 255) / 256) * (a.N / 128));
-    hipLaunchKernelGGL((rowgemm_x3_row3_kernel<EMODE>), grid, dim3(512), 0, s, a);
+    const dim3 grid(((a.M + 255) / 256) * (a.N / BN));
+    hipLaunchKernelGGL((rowgemm_x3_row3_kernel<EMODE, BN>), grid, dim3(512), 0, s, a);
     return (int)hipGetLastError();
 }
 
@@ -466,8 +470,9 @@ static int x3_go(const RowGemmArgs& a, hipStream_t s) {
 
 template <int AMODE, int EMODE>
 static int x3_tile(const RowGemmArgs& a, int tile, hipStream_t s) {
-    if (tile == 4) {  // tap-row halo kernel (3x3 convs)
-        if constexpr (AMODE == G_CONV3) return x3r3_go<EMODE>(a, s);
+    if (tile == 4 || tile == 5) {  // tap-row halo kernel (3x3 convs), 256 x 128 / 256 x 64
+        if constexpr (AMODE == G_CONV3)
+            return tile == 4 ? x3r3_go<EMODE, 128>(a, s) : x3r3_go<EMODE, 64>(a, s);
         return -1;
     }
 #define X3_CASE(id, T) \
@@ -1034,9 +1039,9 @@ __global__ __launch_bounds__(256) void bn_dz_x3_kernel(const float* __restrict__
 }  // namespace
 
 int rowgemm_x3_tile_dims(int tile, int* bm, int* bn) {
-    if (tile == 4) {  // tap-row halo 256 x 128
+    if (tile == 4 || tile == 5) {  // tap-row halo 256 x 128 / 256 x 64
         *bm = 256;
-        *bn = 128;
+        *bn = tile == 4 ? 128 : 64;
         return 0;
     }
 #define X3_DIMS(id, T)  \

@@ -759,13 +759,15 @@ int x3_tile(const unet_ctx* c, const RowGemmArgs& g) {
     };
     // tile 4: the tap-row halo kernel (3x3 convs on rows of 16 .. 256k pixels, option x3_r3)
     const bool r3ok = g.amode == G_CONV3 && g.W >= 16 && (256 % g.W == 0 || g.W % 256 == 0);
-    if (c->opt.x3_tile >= 0 && fits(c->opt.x3_tile) && (c->opt.x3_tile != 4 || r3ok))
+    if (c->opt.x3_tile >= 0 && fits(c->opt.x3_tile) && (c->opt.x3_tile < 4 || r3ok))
         return c->opt.x3_tile;
     if (g.N % 128 == 0 && fits(0)) {
         const int64_t blocks = (int64_t)(g.M + 255) / 256 * (g.N / 128);
         if (blocks < 256) return 1;
         return c->opt.x3_r3 && r3ok ? 4 : 0;
     }
+    // 64 outputs: the 256 x 64 halo tile (5) where its grid fills the chip
+    if (c->opt.x3_r3 && r3ok && (int64_t)(g.M + 255) / 256 >= 512) return 5;
     return c->opt.x3_n64;
 }
 
@@ -826,7 +828,7 @@ std::string xlabel(const char* fam, int tile, int layer) {
     int bm = 0, bn = 0;
     rowgemm_x3_tile_dims(tile, &bm, &bn);
     char b[112];
-    snprintf(b, sizeof b, "%s/x3%s_%dx%d|%d", fam, tile == 4 ? "r3" : "", bm, bn, layer);
+    snprintf(b, sizeof b, "%s/x3%s_%dx%d|%d", fam, tile >= 4 ? "r3" : "", bm, bn, layer);
     return b;
 }
 

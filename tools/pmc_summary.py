@@ -23,8 +23,9 @@ from collections import defaultdict
 
 def short(name):
     """rocprofv3 kernel name -> bench.py label (rowgemm_BMxBNxBK / wgrad_BMxBNxBKP)."""
-    if "rowgemm_x3_row3_kernel" in name:  # tap-row halo x3 GEMM (tile 4)
-        return "x3r3_256x128"
+    m = re.search(r"rowgemm_x3_row3_kernel<\d+, (\d+)>", name)
+    if m:  # tap-row halo x3 GEMM (tiles 4 / 5)
+        return f"x3r3_256x{m.group(1)}"
     m = re.search(r"wgrad_x3_row3_kernel<(\d+), (\d+)", name)
     if m:  # split-bf16 f32 GEMMs (kernels_gemm_x3.hip)
         return f"wx3r3_{m.group(1)}x{m.group(2)}"
