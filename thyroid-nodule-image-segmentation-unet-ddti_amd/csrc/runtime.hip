@@ -743,9 +743,9 @@ bool convt_wg16_on(const unet_ctx* c, int cin, int cout) {
 // whose in- and output channels are multiples of 64 runs its forward, input-gradient and
 // weight-gradient GEMMs on x3 images (exact three-way bf16 splits of the f32 operands, six
 // MFMA products, split f32 accumulators: fp64 error ~3x below the f32 MFMA kernels',
-// profiles/r04_x3_probe_*.txt).  The residual network keeps the f32 kernels.
+// profiles/r04_x3_probe_*.txt).  The residual network's 1x1 skip GEMMs keep the f32 kernels.
 bool x3_conv_on(const unet_ctx* c, int cin, int cout) {
-    return c->opt.x3 && !c->bf16 && !c->res && cin % 64 == 0 && cout % 64 == 0;
+    return c->opt.x3 && !c->bf16 && cin % 64 == 0 && cout % 64 == 0;
 }
 bool x3_convt_on(const unet_ctx* c, int cin, int cout) { return x3_conv_on(c, cin, cout); }
 
@@ -977,7 +977,7 @@ void make_plan(unet_ctx* c, int N, int H, int W, bool training, char* base, Plan
             smax = std::max(smax, (int64_t)w.splits * L.cin * L.cout);
         }
         for (const ConvTL& T : c->convt) {
-            WgradCfg w = x3_convt_on(c, T.cin, T.cout) && !c->res
+            WgradCfg w = x3_convt_on(c, T.cin, T.cout)
                              ? x3_wgrad_cfg(c, T.cin, 1, T.cout, 4, p.P[T.in_level])
                              : wgrad_cfg(c, T.cin, 1, T.cout, 4, p.P[T.in_level], c->bf16);
             smax = std::max(smax, (int64_t)w.splits * T.cin * 4 * T.cout);
@@ -1281,8 +1281,8 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
                 if (up16[i]) {  // the ConvT stored the up half's x3 split: convert the skip half
                     const int l = C.level, so = c->skip_off(l), ch = c->ch(l);
                     const int rl = std::min(std::max(a.relu - so, 0), ch);
-                    RUN("prep_x3", 0, k_to_x3(a.ptr, a.ld, a.off + so, ch, a.scale + so, a.shift + so, rl,
-                                              M, img, C.cin, so, s));
+                    RUN("prep_x3", 0, k_to_x3(a.ptr, a.ld, a.off + so, ch, a.scale ? a.scale + so : nullptr,
+                                              a.shift ? a.shift + so : nullptr, rl, M, img, C.cin, so, s));
                 } else {
                     RUN("prep_x3", 0, k_to_x3(a.ptr, a.ld, a.off, C.cin, a.scale, a.shift, a.relu, M, img,
                                               C.cin, 0, s));
@@ -1350,7 +1350,7 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
         g.bias = prm + T.b;
         g.cout = T.cout;
         g.emode = E_CONVT;
-        if (!c->res && p.pack3 && x3_convt_on(c, T.cin, T.cout)) {
+        if (p.pack3 && x3_convt_on(c, T.cin, T.cout)) {
             uint16_t* img = p.t3[k] ? p.t3[k] : p.s3;
             RUN("prep_x3", 0, k_to_x3(g.a, g.lda, g.aoff, T.cin, g.ascale, g.ashift, g.arelu, g.M, img,
                                       T.cin, 0, s));
@@ -1360,7 +1360,8 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
             // converts the skip half only
             const int idec = 2 * (D + 1 + k);
             const ConvL& Cd = c->conv[idec];
-            if (c->opt.convt16 && p.x3[idec] && x3_conv_on(c, Cd.cin, Cd.cout)) {
+            // (not in the residual network: its 1x1 skip GEMM reads the f32 concat as well)
+            if (c->opt.convt16 && !c->res && p.x3[idec] && x3_conv_on(c, Cd.cin, Cd.cout)) {
                 g.out3 = p.x3[idec];
                 up16[idec] = true;
             }
@@ -1710,7 +1711,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         const int ldo = 2 * c->ch(lo), uo = c->up_off(lo);
         const int Hi = H >> T.in_level, Wi = W >> T.in_level;
         const int64_t Pin = p.P[T.in_level];
-        if (!c->res && p.pack3 && x3_convt_on(c, T.cin, T.cout)) {
+        if (p.pack3 && x3_convt_on(c, T.cin, T.cout)) {
             // option x3: the up half of the concat gradient as an x3 image feeds the weight
             // gradient (B', gathered 2x2) and the input gradient (A)
             RUN("prep_x3", 0, k_to_x3(p.dcat[lo], ldo, uo, T.cout, nullptr, nullptr, 0, p.P[lo], p.s3,
@@ -1754,15 +1755,19 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
             g.out = dx;
             g.ldo = T.cin;
             g.ooff = 0;
-            g.emode = E_STORE_BN;
-            g.ey = p.y[src];
-            g.ldey = p.ldy[src];
-            g.offey = p.offy[src];
-            if (c->bn_relu) {
-                g.escale = p.scale[src];
-                g.eshift = p.shift[src];
+            if (c->res) {  // d(block output); the block's own backward entry masks it
+                g.emode = E_STORE;
+            } else {
+                g.emode = E_STORE_BN;
+                g.ey = p.y[src];
+                g.ldey = p.ldy[src];
+                g.offey = p.offy[src];
+                if (c->bn_relu) {
+                    g.escale = p.scale[src];
+                    g.eshift = p.shift[src];
+                }
+                g.stats = p.part;
             }
-            g.stats = p.part;
             const int tile = x3_tile(c, g);
             *rows = bn_groups(Pin);
             RUN(xlabel("convT_dgrad", tile, 100 + k), 2.0 * Pin * T.cin * 4 * T.cout,
