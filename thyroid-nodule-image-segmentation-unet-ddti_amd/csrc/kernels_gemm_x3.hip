@@ -1008,19 +1008,40 @@ __global__ __launch_bounds__(256) void bn_dz_x3_kernel(const float* __restrict__
             kc[h] = *(const f32x4*)(coef + 2 * C + c + 4 * h);
             km[h] = *(const f32x4*)(coef + 3 * C + c + 4 * h);
         }
-        for (int64_t m = mb + r0; m < me; m += rstep) {
-            float v[8];
+        // two rows in flight (loads of both before either's arithmetic); the column sums add
+        // the rows in ascending order either way
+        auto dz8 = [&](const f32x4 (&dv)[2], const f32x4 (&yv)[2], float (&v)[8]) {
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
-                const f32x4 dv = *(const f32x4*)(d + m * C + c + 4 * h);
-                const f32x4 yv = *(const f32x4*)(y + m * ld + off + c + 4 * h);
-                const f32x4 r = bn_dz4(ka[h], dv, kb[h], yv, km[h], kc[h]);
+                const f32x4 r = bn_dz4(ka[h], dv[h], kb[h], yv[h], km[h], kc[h]);
 #pragma unroll
-                for (int j = 0; j < 4; ++j) v[4 * h + j] = (!mask || yv[j] > 0.f) ? r[j] : 0.f;
+                for (int j = 0; j < 4; ++j) v[4 * h + j] = (!mask || yv[h][j] > 0.f) ? r[j] : 0.f;
             }
+        };
+        for (int64_t m = mb + r0; m < me; m += 2 * rstep) {
+            const int64_t m2 = m + rstep;
+            const bool two = m2 < me;
+            f32x4 dv[2], yv[2], dw[2], yw[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                dv[h] = *(const f32x4*)(d + m * C + c + 4 * h);
+                yv[h] = *(const f32x4*)(y + m * ld + off + c + 4 * h);
+                if (two) {
+                    dw[h] = *(const f32x4*)(d + m2 * C + c + 4 * h);
+                    yw[h] = *(const f32x4*)(y + m2 * ld + off + c + 4 * h);
+                }
+            }
+            float v[8];
+            dz8(dv, yv, v);
 #pragma unroll
             for (int j = 0; j < 8; ++j) cs[j] += v[j];
             x3_store8(v, dz3 + m * 3 * (int64_t)C + (c >> 5) * 96 + (c & 31));
+            if (two) {
+                dz8(dw, yw, v);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) cs[j] += v[j];
+                x3_store8(v, dz3 + m2 * 3 * (int64_t)C + (c >> 5) * 96 + (c & 31));
+            }
         }
     }
     if (!bpart) return;  // (the launcher allows bias sums for C <= 2048 only)

@@ -1520,7 +1520,15 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
             float* bp = C.b >= 0 ? p.part : nullptr;
             RUN("bn_dz", 0, k_bn_dz_x3(dout, p.y[i], p.ldy[i], p.offy[i], P, C.cout, p.coef, dz_mask,
                                       p.s3, bp, s));
-            if (bp) RUN("bias_grad", 0, k_sum_partials(p.part, x3_dz_blocks(P), C.cout, grads + C.b, s));
+            if (bp) {  // many 256-row partials: one two-level reduction (as the BN statistics)
+                const int G = x3_dz_blocks(P);
+                if (G > STAT_G) {
+                    RUN("bias_grad", 0, k_reduce_rows(p.part, G, C.cout, p.part2, STAT_G, s));
+                    RUN("bias_grad", 0, k_sum_partials(p.part2, STAT_G, C.cout, grads + C.b, s));
+                } else {
+                    RUN("bias_grad", 0, k_sum_partials(p.part, G, C.cout, grads + C.b, s));
+                }
+            }
             const WgradCfg wc = x3_wgrad_cfg(c, C.cin, 9, C.cout, 1, P, Wl);
             WgradArgs w{};
             w.xcd = 1;
