@@ -82,7 +82,11 @@ typedef enum {
 
 /* Arithmetic of the convolution GEMMs. */
 typedef enum {
-    UNET_MATH_F32 = 0,  /* v_mfma_f32_32x32x2_f32: exact f32 products (the reference's fp32) */
+    UNET_MATH_F32 = 0,  /* f32 products (the reference's fp32): by default (option x3) the GEMMs
+                           with 64-multiple channel counts run on v_mfma_f32_32x32x16_bf16 through
+                           exact three-way bf16 splits of the f32 operands (six piece products,
+                           split f32 accumulators: below the f32 MFMA's error against fp64), the
+                           rest on v_mfma_f32_32x32x2_f32 */
     UNET_MATH_BF16 = 1  /* v_mfma_f32_32x32x16_bf16: operands rounded to bf16, f32 accumulate
                            (BASELINE config 4; models/mod.py variant only) */
 } unet_math;

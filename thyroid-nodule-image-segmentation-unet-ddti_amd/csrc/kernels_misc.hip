@@ -202,6 +202,7 @@ __global__ __launch_bounds__(256) void conv_first_fwd_kernel(const float* __rest
                                                             int W, int C, int relu,
                                                             float* partial) {
     __shared__ __attribute__((aligned(16))) float smem[256 * 2 * 4];
+    extern __shared__ float xs[];  // x[r0 - W - 1, r1 + W + 1): every tap of the block's pixels
     const int tpr = C / 4, rpp = 256 / tpr;
     const int q = threadIdx.x % tpr, g = threadIdx.x / tpr;
     float wr[4][9];
@@ -214,6 +215,15 @@ __global__ __launch_bounds__(256) void conv_first_fwd_kernel(const float* __rest
     const int per = (P + gridDim.x - 1) / gridDim.x;
     const int r0 = blockIdx.x * per;
     const int r1 = min(P, r0 + per);
+    // in_channels = 1: the image is one float per pixel, so the taps of the block's pixel range
+    // are one contiguous slice of x (the 16 lanes of a pixel then read it from LDS instead of
+    // issuing 9 global loads each)
+    const int xb = r0 - W - 1, xn = per + 2 * W + 2;
+    for (int i = threadIdx.x; i < xn; i += blockDim.x) {
+        const int gi = xb + i;
+        xs[i] = (gi >= 0 && gi < P) ? x[gi] : 0.f;
+    }
+    __syncthreads();
     // U pixels per trip (m, m + rpp, ..., their 9 U image loads issued together), pixel
     // coordinates walked incrementally: no integer division per pixel.  Each thread still sums
     // its pixels in increasing m, so the partials are those of one pixel per trip.
@@ -232,7 +242,7 @@ __global__ __launch_bounds__(256) void conv_first_fwd_kernel(const float* __rest
             for (int tap = 0; tap < 9; ++tap) {
                 const int sy = at[u].y + tap / 3 - 1, sx = at[u].x + tap % 3 - 1;
                 const bool ok = sy >= 0 && sy < H && sx >= 0 && sx < W && m0 + u * rpp < r1;
-                xv[u][tap] = ok ? x[((int64_t)at[u].img * H + sy) * W + sx] : 0.f;
+                xv[u][tap] = ok ? xs[m0 + u * rpp + (tap / 3 - 1) * W + tap % 3 - 1 - xb] : 0.f;
             }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -264,6 +274,7 @@ __global__ __launch_bounds__(256) void conv_first_wgrad_kernel(const float* __re
                                                               int P, int H, int W, int C,
                                                               int mask, float* partial) {
     __shared__ __attribute__((aligned(16))) float smem[256 * 10 * 4];
+    extern __shared__ float xs[];  // x[r0 - W - 1, r1 + W + 1), as conv_first_fwd_kernel
     const int tpr = C / 4, rpp = 256 / tpr;
     const int q = threadIdx.x % tpr, g = threadIdx.x / tpr;
     f32x4 acc[10];
@@ -272,26 +283,46 @@ __global__ __launch_bounds__(256) void conv_first_wgrad_kernel(const float* __re
     const int per = (P + gridDim.x - 1) / gridDim.x;
     const int r0 = blockIdx.x * per;
     const int r1 = min(P, r0 + per);
+    const int xb = r0 - W - 1, xn = per + 2 * W + 2;
+    for (int i = threadIdx.x; i < xn; i += blockDim.x) {
+        const int gi = xb + i;
+        xs[i] = (gi >= 0 && gi < P) ? x[gi] : 0.f;
+    }
+    __syncthreads();
+    const f32x4 ka = *(const f32x4*)(coef + 4 * q), kb = *(const f32x4*)(coef + C + 4 * q);
+    const f32x4 kc = *(const f32x4*)(coef + 2 * C + 4 * q), km = *(const f32x4*)(coef + 3 * C + 4 * q);
     Pix at = decode(min(r0 + g, P - 1), H, W);
-    for (int m = r0 + g; m < r1; m += rpp) {
-        const int xx = at.x, yy = at.y, img = at.img;
-        pix_advance(at, rpp, H, W);
-        // dz = [y > 0] (A do + B (y - mean) + C) (or unmasked, BN -> ReLU order): BN backward fused
-        const f32x4 dv = *(const f32x4*)(dout + (int64_t)m * C + 4 * q);
-        const f32x4 yv = *(const f32x4*)(y + (int64_t)m * C + 4 * q);
-        const f32x4 dd = bn_dz4(*(const f32x4*)(coef + 4 * q), dv, *(const f32x4*)(coef + C + 4 * q), yv,
-                                *(const f32x4*)(coef + 3 * C + 4 * q), *(const f32x4*)(coef + 2 * C + 4 * q));
+    // two pixels per trip (both pixels' loads issued first); each thread still adds its pixels
+    // in increasing m, so the partials are bit-identical to one pixel per trip
+    auto accum = [&](int m, const Pix& pq, const f32x4& dv, const f32x4& yv) {
+        const f32x4 dd = bn_dz4(ka, dv, kb, yv, km, kc);
         f32x4 d;
 #pragma unroll
         for (int j = 0; j < 4; ++j) d[j] = (!mask || yv[j] > 0.f) ? dd[j] : 0.f;
 #pragma unroll
         for (int tap = 0; tap < 9; ++tap) {
-            const int sy = yy + tap / 3 - 1, sx = xx + tap % 3 - 1;
+            const int sy = pq.y + tap / 3 - 1, sx = pq.x + tap % 3 - 1;
             const bool ok = sy >= 0 && sy < H && sx >= 0 && sx < W;
-            const float xv = ok ? x[((int64_t)img * H + sy) * W + sx] : 0.f;
+            const float xv = ok ? xs[m + (tap / 3 - 1) * W + tap % 3 - 1 - xb] : 0.f;
             acc[tap] += xv * d;
         }
         acc[9] += d;
+    };
+    for (int m = r0 + g; m < r1; m += 2 * rpp) {
+        const int m2 = m + rpp;
+        const Pix p1 = at;
+        pix_advance(at, rpp, H, W);
+        const Pix p2 = at;
+        pix_advance(at, rpp, H, W);
+        const f32x4 dv = *(const f32x4*)(dout + (int64_t)m * C + 4 * q);
+        const f32x4 yv = *(const f32x4*)(y + (int64_t)m * C + 4 * q);
+        f32x4 dw{0, 0, 0, 0}, yw{0, 0, 0, 0};
+        if (m2 < r1) {
+            dw = *(const f32x4*)(dout + (int64_t)m2 * C + 4 * q);
+            yw = *(const f32x4*)(y + (int64_t)m2 * C + 4 * q);
+        }
+        accum(m, p1, dv, yv);
+        if (m2 < r1) accum(m2, p2, dw, yw);
     }
     block_combine<10>(acc, tpr, C, partial + (int64_t)blockIdx.x * 10 * C, smem);
 }
@@ -1093,19 +1124,18 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__
     float ab[4] = {0, 0, 0, 0};
     const int per = (P + gridDim.x - 1) / gridDim.x;
     const int r0 = blockIdx.x * per, r1 = min(P, r0 + per);
-    for (int m = r0 + g; m < r1; m += rpp) {
-        const f32x4 yr = *(const f32x4*)(y + (int64_t)m * C + 4 * q);
+    // two pixels per trip, both pixels' loads issued first (P < 2^31: 32-bit pixel math);
+    // each thread still accumulates its pixels in increasing m (same partials)
+    auto one = [&](int m, const f32x4& yr, const float (&dl)[4]) {
         f32x4 v = yr * sc + sh;
         if (relu)
 #pragma unroll
             for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
-        const int64_t img = m / HW, hw = m % HW;
         f32x4 d = {0, 0, 0, 0};
         for (int o = 0; o < O; ++o) {
-            const float dl = dlog[(img * O + o) * HW + hw];
-            d += dl * *(const f32x4*)(w + o * C + 4 * q);
-            aw[o] += dl * v;
-            ab[o] += dl;
+            d += dl[o] * *(const f32x4*)(w + o * C + 4 * q);
+            aw[o] += dl[o] * v;
+            ab[o] += dl[o];
         }
         if (relu)
 #pragma unroll
@@ -1116,6 +1146,23 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__
             bq[0][j] += d[j];
             bq[1][j] += (double)d[j] * yr[j];
         }
+    };
+    for (int m = r0 + g; m < r1; m += 2 * rpp) {
+        const int m2 = m + rpp;
+        const bool two = m2 < r1;
+        const f32x4 y1 = *(const f32x4*)(y + (int64_t)m * C + 4 * q);
+        const f32x4 y2 = two ? *(const f32x4*)(y + (int64_t)m2 * C + 4 * q) : f32x4{0, 0, 0, 0};
+        float d1[4] = {0, 0, 0, 0}, d2[4] = {0, 0, 0, 0};
+        {
+            const int img = m / HW, hw = m - img * HW;
+            for (int o = 0; o < O; ++o) d1[o] = dlog[((int64_t)img * O + o) * HW + hw];
+        }
+        if (two) {
+            const int img = m2 / HW, hw = m2 - img * HW;
+            for (int o = 0; o < O; ++o) d2[o] = dlog[((int64_t)img * O + o) * HW + hw];
+        }
+        one(m, y1, d1);
+        if (two) one(m2, y2, d2);
     }
     if (bnpart) block_combine_d<2>(bq, lpp, C, bnpart + (int64_t)blockIdx.x * 2 * C, smem4);
     __syncthreads();
@@ -1463,7 +1510,9 @@ int k_pack_all(const PackJobs& jobs, const float* prm, float* pack, int bf16, hi
 int k_conv_first_fwd(const float* x, const float* w, const float* b, float* y, int P, int H, int W,
                      int C, int relu, float* partial, int G, hipStream_t s) {
     if (C % 4 || C > 1024) return -1;
-    hipLaunchKernelGGL(conv_first_fwd_kernel, dim3(G), dim3(256), 0, s, x, w, b, y, P, H, W, C,
+    const size_t xs = sizeof(float) * ((P + G - 1) / G + 2 * (size_t)W + 2);  // staged x slice
+    if (xs > 56 * 1024) return -1;
+    hipLaunchKernelGGL(conv_first_fwd_kernel, dim3(G), dim3(256), xs, s, x, w, b, y, P, H, W, C,
                        relu, partial);
     LAUNCH_CHECK();
 }
@@ -1471,7 +1520,9 @@ int k_conv_first_wgrad(const float* x, const float* dout, const float* y, const 
                        int H, int W, int C, int mask, float* partial, int G, float* gw, float* gb,
                        hipStream_t s) {
     if (C % 4 || C > 1024) return -1;
-    hipLaunchKernelGGL(conv_first_wgrad_kernel, dim3(G), dim3(256), 0, s, x, dout, y, coef, P, H, W,
+    const size_t xs = sizeof(float) * ((P + G - 1) / G + 2 * (size_t)W + 2);  // staged x slice
+    if (xs > 56 * 1024) return -1;
+    hipLaunchKernelGGL(conv_first_wgrad_kernel, dim3(G), dim3(256), xs, s, x, dout, y, coef, P, H, W,
                        C, mask, partial);
     HIP_OK(hipGetLastError());
     hipLaunchKernelGGL(conv_first_wgrad_finalize_kernel, dim3((10 * C + 63) / 64), dim3(64, 16), 0,
