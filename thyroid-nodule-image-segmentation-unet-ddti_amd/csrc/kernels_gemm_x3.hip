@@ -287,10 +287,12 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_x3_kernel(RowGemmA
 //   K order: dy, channel group, dx, k -- a reordering of the one-tap kernel's sum, so results
 //   agree with the other tiles to f32 rounding, not bitwise.
 // ------------------------------------------------------------------------------------
-// BN = 128 (8 waves of 64 x 64) or 64 (8 waves of 64 x 32, B pieces padded to 2 per wave)
-template <int EMODE, int BN = 128>
-__global__ __launch_bounds__(512, 1) void rowgemm_x3_row3_kernel(RowGemmArgs p) {
-    constexpr int BM = 256, WM = 64, WN = BN / 2, BK = 32, WAVES = 8, WAVES_N = 2;
+// BN = 128 (8 waves of 64 x 64) or 64 (8 waves of 64 x 32, B pieces padded to 2 per wave);
+// WM / WN: other wave tiles (4 waves of 128 x 64 / 64 x 128 per 256 x 128 block: one wave per
+// SIMD with twice the MFMAs per fragment read; A/B options)
+template <int EMODE, int BN = 128, int WM = 64, int WN = BN / 2>
+__global__ __launch_bounds__((256 / WM) * (BN / WN) * 64, 1) void rowgemm_x3_row3_kernel(RowGemmArgs p) {
+    constexpr int BM = 256, BK = 32, WAVES_N = BN / WN, WAVES = (BM / WM) * WAVES_N;
     constexpr int MT = WM / 32, NT = WN / 32;
     constexpr int RB = 192;
     constexpr int AR = 288;                                   // halo rows (W = 16: 16 x 18)
@@ -439,13 +441,14 @@ __global__ __launch_bounds__(512, 1) void rowgemm_x3_row3_kernel(RowGemmArgs p) 
     row_epilogue<EMODE, BM, BN, WM, WN, true>(p, acc, m0, n0, tile_m, wm, wn, lane, tid, (float*)smem);
 }
 
-template <int EMODE, int BN>
+template <int EMODE, int BN, int WM = 64, int WN = BN / 2>
 static int x3r3_go(const RowGemmArgs& a, hipStream_t s) {
     // BM % W == 0 or W % BM == 0 keeps a tile on whole rows / row segments; W >= 16 bounds the halo
     if (a.amode != G_CONV3 || a.N % BN || a.C % 32 || a.K != 9 * a.C) return -1;
     if (a.W < 16 || (256 % a.W && a.W % 256)) return -1;
     const dim3 grid(((a.M + 255) / 256) * (a.N / BN));
-    hipLaunchKernelGGL((rowgemm_x3_row3_kernel<EMODE, BN>), grid, dim3(512), 0, s, a);
+    constexpr int threads = (256 / WM) * (BN / WN) * 64;
+    hipLaunchKernelGGL((rowgemm_x3_row3_kernel<EMODE, BN, WM, WN>), grid, dim3(threads), 0, s, a);
     return (int)hipGetLastError();
 }
 
@@ -470,7 +473,8 @@ static int x3_go(const RowGemmArgs& a, hipStream_t s) {
 
 template <int AMODE, int EMODE>
 static int x3_tile(const RowGemmArgs& a, int tile, hipStream_t s) {
-    if (tile == 4 || tile == 5) {  // tap-row halo kernel (3x3 convs), 256 x 128 / 256 x 64
+    if (tile == 4 || tile == 5) {  // tap-row halo kernel (3x3 convs): 256 x 128 / 256 x 64
+        // (4-wave 128x64 / 64x128 wave tiles measured within noise of 8 waves, r04: not kept)
         if constexpr (AMODE == G_CONV3)
             return tile == 4 ? x3r3_go<EMODE, 128>(a, s) : x3r3_go<EMODE, 64>(a, s);
         return -1;
@@ -1062,7 +1066,7 @@ __global__ __launch_bounds__(256) void bn_dz_x3_kernel(const float* __restrict__
 int rowgemm_x3_tile_dims(int tile, int* bm, int* bn) {
     if (tile == 4 || tile == 5) {  // tap-row halo 256 x 128 / 256 x 64
         *bm = 256;
-        *bn = tile == 4 ? 128 : 64;
+        *bn = tile == 5 ? 64 : 128;
         return 0;
     }
 #define X3_DIMS(id, T)  \

@@ -132,7 +132,7 @@ int main(int argc, char** argv) {
         CK(hipMemcpy(r32.data(), y32, r32.size() * 4, hipMemcpyDeviceToHost));
         std::vector<float> hx, hw;
         bool host_loaded = false;
-        for (int tile = 0; tile <= 6; ++tile) {
+        for (int tile = 0; tile <= 7; ++tile) {
             int bm = 0, bn = 0;
             if (rowgemm_x3_tile_dims(tile, &bm, &bn) != 0 || N % bn) continue;
             CK(hipMemset(yx3, 0, (size_t)M * N * 4));
