@@ -194,3 +194,4 @@ def test_x3_halo_tile_matches_one_tap():
         worst = max(norm_rel(outs[0][1][k], g) for k, g in outs[1][1].items())
         print(f"{B}x{H}x{W}: halo vs one-tap logits {el:.2e}, worst grad {worst:.2e}")
         assert el <= 1e-6 and worst <= 1e-4, (el, worst)
+
