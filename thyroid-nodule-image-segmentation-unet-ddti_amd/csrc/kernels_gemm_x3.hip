@@ -441,156 +441,6 @@ __global__ __launch_bounds__((256 / WM) * (BN / WN) * 64, 1) void rowgemm_x3_row
     row_epilogue<EMODE, BM, BN, WM, WN, true>(p, acc, m0, n0, tile_m, wm, wn, lane, tid, (float*)smem);
 }
 
-// Variant of the halo kernel with B straight from global memory (tile 6, A/B option): the
-// weight fragments go from L2 into registers one k-step ahead (each wave loads its own 16 B per
-// lane; the four waves sharing a column block hit L1), so LDS holds only the double-buffered
-// halo and a halo stage needs one barrier instead of the B ring's two per sub-step.  The halo
-// of the next group is issued two k-steps before the group ends: VMEM loads retire in order,
-// so it must be complete by the time the k-step after it waits for its B.
-template <int EMODE>
-__global__ __launch_bounds__(512, 1) void rowgemm_x3_row3d_kernel(RowGemmArgs p) {
-    constexpr int BM = 256, BN = 128, WM = 64, WN = 64, BK = 32, WAVES = 8, WAVES_N = 2;
-    constexpr int MT = WM / 32, NT = WN / 32;
-    constexpr int RB = 192;
-    constexpr int AR = 288;
-    constexpr int AI = (AR * RB + 1024 * WAVES - 1) / (1024 * WAVES);  // 7
-    constexpr int AREG = AI * WAVES * 1024;
-    constexpr int SMEM = 2 * AREG;  // 112 KB
-    constexpr int BL = NT * 3;      // B loads per wave and k-step
-    static_assert(SMEM >= 2 * (BM / 64) * BN * 8, "epilogue scratch");
-    __shared__ __attribute__((aligned(1024))) char smem[SMEM];
-    auto swz = [](int r) { return (r >> 2) & 3; };
-
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = wave / WAVES_N, wn = wave % WAVES_N;
-    const int ntn = p.N / BN;
-    const int bid = p.xcd ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
-    const int tile_m = bid / ntn, tile_n = bid - tile_m * ntn;
-    const int m0 = tile_m * BM, n0 = tile_n * BN;
-    const int H = p.H, W = p.W, C = p.C, K = p.K;
-    const int SEG = W < BM ? W : BM, HW = SEG + 2;
-    const int AROWS = (BM / SEG) * HW;
-    const size_t rowa = 3 * (size_t)p.lda, rowb = 3 * (size_t)K;
-
-    int acen[AI], ayr[AI], ace[AI];
-#pragma unroll
-    for (int j = 0; j < AI; ++j) {
-        const int o = ((j * WAVES + wave) * 64 + lane) * 16;
-        const int h = o / RB, w = o - h * RB;
-        const int r = h / HW, xl = h - r * HW - 1;
-        const int mrow = m0 + r * SEG;
-        bool ok = h < AROWS && mrow < p.M;
-        const Pix q = decode(ok ? mrow : 0, H, W);
-        ok = ok && q.x + xl >= 0 && q.x + xl < W;
-        acen[j] = ok ? mrow + xl : -1;
-        ayr[j] = q.y;
-        ace[j] = (w >> 6) * 32 + ((((w >> 4) & 3) ^ swz(h)) << 3);
-    }
-    const uint16_t* zero = (const uint16_t*)p.zero16;
-    const uint16_t* a16 = p.a16 + (size_t)p.aoff * 3;
-    const int CC = C / BK;
-    const int NG = 3 * CC;  // halo groups (dy, channel group)
-    auto issue_a = [&](int g) {
-        const int dy = g / CC, c0 = (g - dy * CC) * BK;
-        char* base = smem + (g & 1) * AREG;
-#pragma unroll
-        for (int j = 0; j < AI; ++j) {
-            const int yy = ayr[j] + dy - 1;
-            const bool valid = acen[j] >= 0 && yy >= 0 && yy < H;
-            const uint16_t* src =
-                valid ? a16 + (size_t)(acen[j] + (dy - 1) * W) * rowa + c0 * 3 + ace[j] : zero;
-            x3_dma16(src, base + (j * WAVES + wave) * 1024);
-        }
-    };
-    const int lh = lane >> 5, li = lane & 31;
-    // B fragment of (nt, plane q) for k-step t = (g, dx, kk): row n0 + wn WN + nt 32 + li,
-    // element ((dy 3 + dx) C + c0) 3 + q 32 + (kk 2 + lh) 8
-    const uint16_t* brow[NT];
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) brow[nt] = p.bt16 + (size_t)(n0 + wn * WN + nt * 32 + li) * rowb + lh * 8;
-    auto load_b = [&](int t, bf16x8 (&bf)[NT][3]) {
-        const int g = t / 6, u = t - g * 6, dx = u >> 1, kk = u & 1;
-        const int dy = g / CC, c0 = (g - dy * CC) * BK;
-        const int e = ((dy * 3 + dx) * C + c0) * 3 + kk * 16;
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-            for (int q = 0; q < 3; ++q) bf[nt][q] = *(const bf16x8*)(brow[nt] + e + q * 32);
-    };
-
-    f32x16 acc[MT][NT], acl[MT][NT];
-#pragma unroll
-    for (int i = 0; i < MT; ++i)
-#pragma unroll
-        for (int j = 0; j < NT; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = acl[i][j][r] = 0.f;
-    int ahb[MT];
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-        const int mo = wm * WM + mt * 32 + li;
-        const int r = mo / SEG;
-        ahb[mt] = r * HW + (mo - r * SEG);
-    }
-
-    const int nt_steps = 6 * NG;  // k-steps: (group, dx, kk)
-    bf16x8 bb[2][NT][3];
-    issue_a(0);
-    load_b(0, bb[0]);
-    x3_wait_vm<0>();
-    x3_barrier();
-    for (int g = 0; g < NG; ++g) {
-        const char* abase = smem + (g & 1) * AREG;
-#pragma unroll
-        for (int u = 0; u < 6; ++u) {
-            const int t = g * 6 + u;
-            const int dx = u >> 1, kk = u & 1;
-            const bool more = t + 1 < nt_steps, na = u == 3 && g + 1 < NG;
-            // next k-step's B (after the next halo when u == 3: issue order B(t + 1), A(g + 1))
-            if (more) load_b(t + 1, bb[(u + 1) & 1]);
-            if (na) issue_a(g + 1);
-            // wait for this k-step's B; the loads issued after it may stay in flight: B(t + 1),
-            // and A(g + 1) at u = 3 (issued after B(t + 1)) and u = 4 (issued after B(t))
-            const bool ahead = (u == 3 || u == 4) && g + 1 < NG;
-            if (!more) x3_wait_vm<0>();
-            else if (ahead) x3_wait_vm<AI + BL>();
-            else x3_wait_vm<BL>();
-            if (u == 0 && g > 0) x3_barrier();  // the halo of g landed for every wave
-            const int c = kk * 2 + lh;
-            bf16x8 af[MT][3];
-#pragma unroll
-            for (int mt = 0; mt < MT; ++mt) {
-                const int h = ahb[mt] + dx;
-#pragma unroll
-                for (int q = 0; q < 3; ++q)
-                    af[mt][q] = *(const bf16x8*)(abase + h * RB + q * 64 + ((c ^ swz(h)) << 4));
-            }
-#pragma unroll
-            for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-                for (int nt = 0; nt < NT; ++nt) mfma_x3s(af[mt], bb[u & 1][nt], acc[mt][nt], acl[mt][nt]);
-        }
-        // this wave's reads of the halo buffer have returned before the next group's barrier,
-        // after which the halo of g + 2 (issued in group g + 1) overwrites it
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    }
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt) acc[mt][nt] += acl[mt][nt];
-    row_epilogue<EMODE, BM, BN, WM, WN, true>(p, acc, m0, n0, tile_m, wm, wn, lane, tid, (float*)smem);
-}
-
-template <int EMODE>
-static int x3r3d_go(const RowGemmArgs& a, hipStream_t s) {
-    if (a.amode != G_CONV3 || a.N % 128 || a.C % 32 || a.K != 9 * a.C) return -1;
-    if (a.W < 16 || (256 % a.W && a.W % 256)) return -1;
-    const dim3 grid(((a.M + 255) / 256) * (a.N / 128));
-    hipLaunchKernelGGL((rowgemm_x3_row3d_kernel<EMODE>), grid, dim3(512), 0, s, a);
-    return (int)hipGetLastError();
-}
-
 template <int EMODE, int BN, int WM = 64, int WN = BN / 2>
 static int x3r3_go(const RowGemmArgs& a, hipStream_t s) {
     // BM % W == 0 or W % BM == 0 keeps a tile on whole rows / row segments; W >= 16 bounds the halo
@@ -623,13 +473,13 @@ static int x3_go(const RowGemmArgs& a, hipStream_t s) {
 
 template <int AMODE, int EMODE>
 static int x3_tile(const RowGemmArgs& a, int tile, hipStream_t s) {
-    if (tile >= 4 && tile <= 6) {  // tap-row halo kernel (3x3 convs): 256 x 128 / 256 x 64;
-        // 6 = 256 x 128 with B straight from global memory.  (4-wave 128x64 / 64x128 wave
-        // tiles measured within noise of 8 waves, r04: not kept)
-        if constexpr (AMODE == G_CONV3) {
-            if (tile == 6) return x3r3d_go<EMODE>(a, s);
+    if (tile == 4 || tile == 5) {  // tap-row halo kernel (3x3 convs): 256 x 128 / 256 x 64
+        // (r04, not kept: 4-wave 128x64 / 64x128 wave tiles, within noise of 8 waves; B
+        // straight from global memory into registers instead of the LDS ring, one barrier per
+        // halo group, bit-identical but 222 -> 161 TF/s: the per-wave B loads cost more than
+        // the ring's barriers)
+        if constexpr (AMODE == G_CONV3)
             return tile == 4 ? x3r3_go<EMODE, 128>(a, s) : x3r3_go<EMODE, 64>(a, s);
-        }
         return -1;
     }
 #define X3_CASE(id, T) \
@@ -1217,7 +1067,7 @@ __global__ __launch_bounds__(256) void bn_dz_x3_kernel(const float* __restrict__
 }  // namespace
 
 int rowgemm_x3_tile_dims(int tile, int* bm, int* bn) {
-    if (tile >= 4 && tile <= 6) {  // tap-row halo 256 x 128 / 256 x 64 / 256 x 128 direct B
+    if (tile == 4 || tile == 5) {  // tap-row halo 256 x 128 / 256 x 64
         *bm = 256;
         *bn = tile == 5 ? 64 : 128;
         return 0;
