@@ -197,24 +197,17 @@ def test_x3_halo_tile_matches_one_tap():
 
 
 
-@pytest.mark.parametrize("opt,alt", [("x3_wbkp64", 1), ("x3_r3n64", 6)])
-def test_x3_schedule_variants_bit_identical(opt, alt):
-    """Schedule variants that leave every element's MFMA sequence unchanged, so one training
-    step (logits and the whole gradient arena) is bit-identical to the default:
-    * x3_wbkp64: the tap-row x3 weight gradient on 64-pixel chunks (tiles 5 / 6, rows of 64k
-      pixels) walks each split's pixels in the same 16-pixel k-steps as the 32-pixel tiles
-      2 / 3 over the same split partition;
-    * x3_r3n64 = 6: the 256 x 64 halo row GEMM with 4 waves of 64 x 64 instead of 8 of
-      64 x 32 (the same (dy, group, dx, k) order per element; 256x256 input: the level-0
-      64-output GEMMs take it)."""
+def test_x3_tap_row_wgrad_64_pixel_chunks_bit_identical():
+    """Option x3_wbkp64: the tap-row x3 weight gradient on 64-pixel chunks (tiles 5 / 6, rows
+    of 64k pixels) walks each split's pixels in the same 16-pixel k-steps as the 32-pixel
+    tiles 2 / 3 over the same split partition, so one training step is bit-identical."""
     import unet_hip
     from _helpers import options
-    x, t = inputs(31, 2, 256, 256)
+    x, t = inputs(31, 2, 128, 128)
     outs = []
-    for flag in (None, alt):
+    for flag in (0, 1):
         m = hip_model(O.make_params(42), DEV)
-        kw = {} if flag is None else {opt: flag}
-        with options(m.flatten_().rt, **kw):
+        with options(m.flatten_().rt, x3_wbkp64=flag):
             logits = m(x.to(DEV))
             l = unet_hip.seg_losses(logits, t.to(DEV))
             (l[0] + l[1]).backward()

@@ -313,7 +313,7 @@ def test_schedule_option_defaults():
             "xcd_remap": 1, "xcd16": 1, "tile_convt": -1, "tile_convt_dgrad": 26, "rg16_xp": 0,
             "dz_in_wgrad": 256, "rg16_r3": 1, "rg16_n128": 20, "rg16_n128_bn": 0, "wg16_r3": 4,
             "convt16": 1, "x3": 1, "x3_tile": -1, "x3_wtile": -1, "x3_wblocks": 1536, "x3_n64": 2, "x3_r3": 1,
-            "x3_wbkp64": 0, "x3_r3n64": 5}
+            "x3_wbkp64": 0}
     got = {k: fresh.get_option(k) for k in want}
     assert got == want
 

@@ -473,15 +473,13 @@ static int x3_go(const RowGemmArgs& a, hipStream_t s) {
 
 template <int AMODE, int EMODE>
 static int x3_tile(const RowGemmArgs& a, int tile, hipStream_t s) {
-    if (tile >= 4 && tile <= 6) {  // tap-row halo kernel (3x3 convs): 256 x 128 / 256 x 64
+    if (tile == 4 || tile == 5) {  // tap-row halo kernel (3x3 convs): 256 x 128 / 256 x 64
         // (r04, not kept: 4-wave 128x64 / 64x128 wave tiles, within noise of 8 waves; B
         // straight from global memory into registers instead of the LDS ring, one barrier per
         // halo group, bit-identical but 222 -> 161 TF/s: the per-wave B loads cost more than
         // the ring's barriers)
         if constexpr (AMODE == G_CONV3)
-            return tile == 4 ? x3r3_go<EMODE, 128>(a, s)
-                 : tile == 5 ? x3r3_go<EMODE, 64>(a, s)
-                             : x3r3_go<EMODE, 64, 64, 64>(a, s);  // 6: 4 waves of 64 x 64
+            return tile == 4 ? x3r3_go<EMODE, 128>(a, s) : x3r3_go<EMODE, 64>(a, s);
         return -1;
     }
 #define X3_CASE(id, T) \
@@ -1081,9 +1079,9 @@ __global__ __launch_bounds__(256) void bn_dz_x3_kernel(const float* __restrict__
 }  // namespace
 
 int rowgemm_x3_tile_dims(int tile, int* bm, int* bn) {
-    if (tile >= 4 && tile <= 6) {  // tap-row halo 256 x 128 / 256 x 64 (8 / 4 waves)
+    if (tile == 4 || tile == 5) {  // tap-row halo 256 x 128 / 256 x 64
         *bm = 256;
-        *bn = tile == 4 ? 128 : 64;
+        *bn = tile == 5 ? 64 : 128;
         return 0;
     }
 #define X3_DIMS(id, T)  \

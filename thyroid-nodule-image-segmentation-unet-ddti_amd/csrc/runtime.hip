@@ -161,7 +161,6 @@ struct Options {
     int x3_n64 = 2;            // its row-GEMM tile for 64 outputs (2 = 128x64, 3 = 256x64)
     int x3_r3 = 1;             // its 256x128 3x3 GEMMs on the tap-row halo kernel (tile 4)
     int x3_wbkp64 = 0;         // its tap-row weight gradients on 64-pixel chunks (W % 64 == 0)
-    int x3_r3n64 = 5;          // its halo tile for 64 outputs (5 = 8 waves, 6 = 4 waves)
 };
 struct OptionDesc {
     const char* name;
@@ -212,7 +211,6 @@ const OptionDesc OPTION_TABLE[] = {
     {"x3_n64", &Options::x3_n64},
     {"x3_r3", &Options::x3_r3},
     {"x3_wbkp64", &Options::x3_wbkp64},
-    {"x3_r3n64", &Options::x3_r3n64},
 };
 
 }  // namespace
@@ -770,10 +768,8 @@ int x3_tile(const unet_ctx* c, const RowGemmArgs& g) {
         if (blocks < 256) return 1;
         return c->opt.x3_r3 && r3ok ? 4 : 0;
     }
-    // 64 outputs: the 256 x 64 halo tile (option x3_r3n64: 5 = 8 waves of 64 x 32, 6 = 4 waves
-    // of 64 x 64) where its grid fills the chip
-    if (c->opt.x3_r3 && r3ok && (int64_t)(g.M + 255) / 256 >= 512)
-        return c->opt.x3_r3n64 == 6 ? 6 : 5;
+    // 64 outputs: the 256 x 64 halo tile (5) where its grid fills the chip
+    if (c->opt.x3_r3 && r3ok && (int64_t)(g.M + 255) / 256 >= 512) return 5;
     return c->opt.x3_n64;
 }
 
