@@ -195,24 +195,3 @@ def test_x3_halo_tile_matches_one_tap():
         print(f"{B}x{H}x{W}: halo vs one-tap logits {el:.2e}, worst grad {worst:.2e}")
         assert el <= 1e-6 and worst <= 1e-4, (el, worst)
 
-
-
-def test_x3_tap_row_wgrad_64_pixel_chunks_bit_identical():
-    """Option x3_wbkp64: the tap-row x3 weight gradient on 64-pixel chunks (tiles 5 / 6, rows
-    of 64k pixels) walks each split's pixels in the same 16-pixel k-steps as the 32-pixel
-    tiles 2 / 3 over the same split partition, so one training step is bit-identical."""
-    import unet_hip
-    from _helpers import options
-    x, t = inputs(31, 2, 128, 128)
-    outs = []
-    for flag in (0, 1):
-        m = hip_model(O.make_params(42), DEV)
-        with options(m.flatten_().rt, x3_wbkp64=flag):
-            logits = m(x.to(DEV))
-            l = unet_hip.seg_losses(logits, t.to(DEV))
-            (l[0] + l[1]).backward()
-            torch.cuda.synchronize()
-        outs.append((logits.detach().clone(), m._state.grad_arena.clone()))
-        del m
-    assert torch.equal(outs[0][0], outs[1][0])
-    assert torch.equal(outs[0][1], outs[1][1]), (outs[0][1] - outs[1][1]).abs().max().item()

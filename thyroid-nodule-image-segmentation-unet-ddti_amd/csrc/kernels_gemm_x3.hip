@@ -734,12 +734,11 @@ __global__ __launch_bounds__(T::THREADS, 1) void wgrad_x3_kernel(WgradArgs p) {
 // reads feed 18 MFMAs.  Stage: [AR halo rows][6 BM B] + [32 pixel rows][6 BN B]; the loader
 // gives every wave the same instruction count (rows past the halo / chunk read zeros).
 // ------------------------------------------------------------------------------------
-template <int BM, int BN, int S = 3, int OCC = 1, int BKP_ = 32>
+template <int BM, int BN, int S = 3, int OCC = 1>
 __global__ __launch_bounds__((BM / 32) * (BN / 32) * 64, OCC) void wgrad_x3_row3_kernel(WgradArgs p) {
-    constexpr int WAVES = (BM / 32) * (BN / 32), BKP = BKP_;  // pixels per chunk (32 / 64)
+    constexpr int WAVES = (BM / 32) * (BN / 32), BKP = 32;
     constexpr int WAVES_N = BN / 32;
     static_assert(S >= 2 && S <= 3, "stages");
-    static_assert(BKP == 32 || BKP == 64, "two or four 16-pixel k-steps per chunk");
     constexpr int RA = 6 * BM, RBB = 6 * BN;
     constexpr int HALO = BKP + 2;
     constexpr int AI = (HALO * RA + 1024 * WAVES - 1) / (1024 * WAVES);  // per wave
@@ -845,56 +844,45 @@ __global__ __launch_bounds__((BM / 32) * (BN / 32) * 64, OCC) void wgrad_x3_row3
         else x3_wait_vm<0>();
         x3_barrier();
         const unsigned sb = x3_lds_u32(smem) + (kc % S) * STAGE;
-        x3_short4 fa[2][3][3][2], fb[2][3][2];  // fragments of k-steps kk (set kk & 1)
+        x3_short4 fa[2][3][3][2], fb[2][3][2];
         auto load = [&](auto KK) {
-            constexpr int kk = decltype(KK)::value, st = kk & 1;
+            constexpr int kk = decltype(KK)::value;
 #pragma unroll
             for (int dx = 0; dx < 3; ++dx)
 #pragma unroll
                 for (int q = 0; q < 3; ++q) {
-                    fa[st][dx][q][0] = x3_tr16<kk * 16 * RA>(sb + aoff[dx][q]);
-                    fa[st][dx][q][1] = x3_tr16<kk * 16 * RA + 4 * RA>(sb + aoff[dx][q]);
+                    fa[kk][dx][q][0] = x3_tr16<kk * 16 * RA>(sb + aoff[dx][q]);
+                    fa[kk][dx][q][1] = x3_tr16<kk * 16 * RA + 4 * RA>(sb + aoff[dx][q]);
                 }
 #pragma unroll
             for (int q = 0; q < 3; ++q) {
-                fb[st][q][0] = x3_tr16<kk * 16 * RBB>(sb + boff[q]);
-                fb[st][q][1] = x3_tr16<kk * 16 * RBB + 4 * RBB>(sb + boff[q]);
+                fb[kk][q][0] = x3_tr16<kk * 16 * RBB>(sb + boff[q]);
+                fb[kk][q][1] = x3_tr16<kk * 16 * RBB + 4 * RBB>(sb + boff[q]);
             }
         };
         auto mma = [&](auto KK) {
-            constexpr int st = decltype(KK)::value & 1;
+            constexpr int kk = decltype(KK)::value;
             bf16x8 b3[3];
 #pragma unroll
-            for (int q = 0; q < 3; ++q) b3[q] = *(const bf16x8*)fb[st][q];
+            for (int q = 0; q < 3; ++q) b3[q] = *(const bf16x8*)fb[kk][q];
 #pragma unroll
             for (int dx = 0; dx < 3; ++dx) {
                 bf16x8 a3[3];
 #pragma unroll
-                for (int q = 0; q < 3; ++q) a3[q] = *(const bf16x8*)fa[st][dx][q];
+                for (int q = 0; q < 3; ++q) a3[q] = *(const bf16x8*)fa[kk][dx][q];
                 mfma_x3s(a3, b3, acc[dx], acl[dx]);
-            }
-        };
-        // k-step kk + 1's transposed reads are in flight while kk's MFMAs run
-        auto step = [&](auto KK) {
-            constexpr int kk = decltype(KK)::value;
-            if constexpr (kk + 1 < BKP / 16) load(std::integral_constant<int, kk + 1>{});
-            __builtin_amdgcn_sched_barrier(0);
-            mma(KK);
-            __builtin_amdgcn_sched_barrier(0);
-            if constexpr (kk + 1 < BKP / 16) {
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                __builtin_amdgcn_sched_barrier(0);
             }
         };
         load(std::integral_constant<int, 0>{});
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
-        step(std::integral_constant<int, 0>{});
-        step(std::integral_constant<int, 1>{});
-        if constexpr (BKP == 64) {
-            step(std::integral_constant<int, 2>{});
-            step(std::integral_constant<int, 3>{});
-        }
+        load(std::integral_constant<int, 1>{});
+        __builtin_amdgcn_sched_barrier(0);
+        mma(std::integral_constant<int, 0>{});
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        mma(std::integral_constant<int, 1>{});
         x3_barrier();
     }
 
@@ -1127,10 +1115,9 @@ int k_to_x3(const float* src, int ld, int off, int C, const float* scale, const 
 }
 
 int wgrad_x3_tile_dims(int tile, int* bm, int* bn) {
-    if (tile >= 2 && tile <= 6) {  // tap-row: BM x BN per tap, three taps per block
-        const int t = tile >= 5 ? tile - 3 : tile;  // 5, 6: tiles 2, 3 on 64-pixel chunks
-        *bm = t == 3 ? 128 : 64;
-        *bn = t == 2 ? 128 : 64;
+    if (tile >= 2 && tile <= 4) {  // tap-row: BM x BN per tap, three taps per block
+        *bm = tile == 3 ? 128 : 64;
+        *bn = tile == 2 ? 128 : 64;
         return 0;
     }
 #define WX3_DIMS(id, T) \
@@ -1150,25 +1137,19 @@ int wgrad_x3_tile_dims(int tile, int* bm, int* bn) {
 int launch_wgrad_x3(const WgradArgs& a, int tile, hipStream_t s) {
     if (a.ascale || a.bcoef || a.bias_slab || !a.zero16 || a.P < 1) return -1;
     if (a.aoff % 32 || a.boff % 32 || a.lda % 32 || a.ldb % 32) return -1;
-    if (tile >= 2 && tile <= 6) {  // tap-row kernel: 3x3 convs, W % 32 (5, 6: % 64) == 0
+    if (tile >= 2 && tile <= 4) {  // tap-row kernel: 3x3 convs, W % 32 == 0
         int bm = 0, bn = 0;
         wgrad_x3_tile_dims(tile, &bm, &bn);
-        const int bkp = tile >= 5 ? 64 : 32;
         if (a.amode != G_CONV3 || a.bmode != G_IDENT || a.Mw != 9 * a.CA || a.Nw != a.CB ||
-            a.CA % bm || a.CB % bn || a.W % bkp || a.pps % bkp || a.P % bkp)
+            a.CA % bm || a.CB % bn || a.W % 32 || a.pps % 32 || a.P % 32)
             return -1;
         const dim3 grid((a.CA / bm) * 3 * (a.CB / bn) * a.splits);
         if (tile == 2)
             hipLaunchKernelGGL((wgrad_x3_row3_kernel<64, 128>), grid, dim3(512), 0, s, a);
         else if (tile == 3)
             hipLaunchKernelGGL((wgrad_x3_row3_kernel<128, 64>), grid, dim3(512), 0, s, a);
-        else if (tile == 4)  // 64 x 64: four waves, two LDS stages, two blocks per CU
+        else  // 64 x 64: four waves, two LDS stages, two blocks per CU
             hipLaunchKernelGGL((wgrad_x3_row3_kernel<64, 64, 2, 2>), grid, dim3(256), 0, s, a);
-        // 64-pixel chunks: half the barriers per MFMA, two stages of 80 KB
-        else if (tile == 5)
-            hipLaunchKernelGGL((wgrad_x3_row3_kernel<64, 128, 2, 1, 64>), grid, dim3(512), 0, s, a);
-        else
-            hipLaunchKernelGGL((wgrad_x3_row3_kernel<128, 64, 2, 1, 64>), grid, dim3(512), 0, s, a);
         return (int)hipGetLastError();
     }
 #define WX3G(AM, BMD)                                      \

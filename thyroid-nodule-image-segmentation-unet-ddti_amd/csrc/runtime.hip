@@ -160,7 +160,6 @@ struct Options {
     int x3_wblocks = 1536;     // split-K target (blocks) of its 128x128 weight gradients
     int x3_n64 = 2;            // its row-GEMM tile for 64 outputs (2 = 128x64, 3 = 256x64)
     int x3_r3 = 1;             // its 256x128 3x3 GEMMs on the tap-row halo kernel (tile 4)
-    int x3_wbkp64 = 0;         // its tap-row weight gradients on 64-pixel chunks (W % 64 == 0)
 };
 struct OptionDesc {
     const char* name;
@@ -210,7 +209,6 @@ const OptionDesc OPTION_TABLE[] = {
     {"x3_wblocks", &Options::x3_wblocks},
     {"x3_n64", &Options::x3_n64},
     {"x3_r3", &Options::x3_r3},
-    {"x3_wbkp64", &Options::x3_wbkp64},
 };
 
 }  // namespace
@@ -786,20 +784,17 @@ WgradCfg x3_wgrad_cfg(const unet_ctx* c, int CA, int tapsA, int CB, int tapsB, i
     if (r3 && CA % 64 == 0 && CB % 128 == 0) w.tile = 2;
     else if (r3 && CA % 128 == 0 && CB % 64 == 0) w.tile = 3;
     else if (r3 && CA % 64 == 0 && CB % 64 == 0) w.tile = 4;
-    // option x3_wbkp64: tiles 2 / 3 on 64-pixel chunks (5 / 6) where the rows allow
-    if ((w.tile == 2 || w.tile == 3) && c->opt.x3_wbkp64 && row_w % 64 == 0) w.tile += 3;
     if (c->opt.x3_wtile >= 0) {
         int bm = 0, bn = 0;
         const int t = c->opt.x3_wtile;
-        if (wgrad_x3_tile_dims(t, &bm, &bn) == 0 && CA % bm == 0 && CB % bn == 0 && (t < 2 || r3) &&
-            (t < 5 || row_w % 64 == 0))
+        if (wgrad_x3_tile_dims(t, &bm, &bn) == 0 && CA % bm == 0 && CB % bn == 0 && (t < 2 || r3))
             w.tile = t;
     }
     wgrad_x3_tile_dims(w.tile, &w.bm, &w.bn);
+    w.bkp = 32;
     const int64_t tiles = w.tile >= 2 ? (int64_t)(CA / w.bm) * 3 * (CB / w.bn)
                                       : (int64_t)(tapsA * CA / w.bm) * (tapsB * CB / w.bn);
     const int64_t target = (int64_t)c->opt.x3_wblocks * (w.tile == 1 ? 4 : w.tile == 4 ? 2 : 1);
-    w.bkp = w.tile >= 5 ? 64 : 32;
     int64_t splits = std::max<int64_t>(1, (target + tiles - 1) / tiles);
     int64_t pps = (P + splits - 1) / splits;
     pps = (pps + 255) / 256 * 256;
