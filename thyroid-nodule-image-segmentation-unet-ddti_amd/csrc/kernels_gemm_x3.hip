@@ -477,7 +477,7 @@ static int x3_tile(const RowGemmArgs& a, int tile, hipStream_t s) {
         // (r04, not kept: 4-wave 128x64 / 64x128 wave tiles, within noise of 8 waves; B
         // straight from global memory into registers instead of the LDS ring, one barrier per
         // halo group, bit-identical but 222 -> 161 TF/s: the per-wave B loads cost more than
-        // the ring's barriers)
+        // the ring's barriers; 256 x 64 as 4 waves of 64 x 64, bit-identical, 589 -> 584 img/s)
         if constexpr (AMODE == G_CONV3)
             return tile == 4 ? x3r3_go<EMODE, 128>(a, s) : x3r3_go<EMODE, 64>(a, s);
         return -1;
@@ -1134,6 +1134,8 @@ int wgrad_x3_tile_dims(int tile, int* bm, int* bn) {
 // Weight gradient from x3 images: a / b point at uint16 x3 images (lda / ldb channels per
 // row, channel offsets aoff / boff multiples of 32), zero16 at a zeroed page.  3x3 conv (A'
 // G_CONV3, B' G_IDENT) and ConvT (A' G_IDENT, B' G_UP2); no bias column sums.
+// (r04, not kept: the tap-row tiles on 64-pixel chunks, four k-steps per barrier pair:
+// bit-identical, config 2 within noise, profiles/r04_x3_halo_ab.txt)
 int launch_wgrad_x3(const WgradArgs& a, int tile, hipStream_t s) {
     if (a.ascale || a.bcoef || a.bias_slab || !a.zero16 || a.P < 1) return -1;
     if (a.aoff % 32 || a.boff % 32 || a.lda % 32 || a.ldb % 32) return -1;
