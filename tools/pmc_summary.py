@@ -23,7 +23,7 @@ from collections import defaultdict
 
 def short(name):
     """rocprofv3 kernel name -> bench.py label (rowgemm_BMxBNxBK / wgrad_BMxBNxBKP)."""
-    m = re.search(r"rowgemm_x3_row3_kernel<\d+, (\d+)>", name)
+    m = re.search(r"rowgemm_x3_row3_kernel<\d+, (\d+)[,>]", name)
     if m:  # tap-row halo x3 GEMM (tiles 4 / 5)
         return f"x3r3_256x{m.group(1)}"
     m = re.search(r"wgrad_x3_row3_kernel<(\d+), (\d+)", name)
