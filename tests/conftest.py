@@ -19,3 +19,15 @@ def pytest_configure(config):
 @pytest.fixture(scope="session")
 def golden_dir():
     return GOLDEN
+
+
+@pytest.fixture(autouse=True)
+def _reset_schedule_options():
+    """Runtimes are cached per device and network configuration (unet_hip.runtime), so a
+    schedule option a test sets would otherwise leak into every later test of that
+    configuration: restore every cached runtime's options after each test."""
+    yield
+    rtmod = sys.modules.get("unet_hip.runtime")
+    if rtmod is not None:
+        for rt in list(rtmod._RUNTIMES.values()):
+            rt.reset_options()

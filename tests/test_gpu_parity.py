@@ -544,7 +544,7 @@ def test_wgrad_row3_matches_one_tap_tiles(variant):
     summation grouping: every weight / bias gradient within 1e-5 norm-relative of the
     one-tap schedule, logits bit-identical (the forward does not change)."""
     import unet_hip
-    from _helpers import hip_mod_model
+    from _helpers import hip_mod_model, options
     x, t = inputs(17, 8, 256, 256)
     outs = []
     for flag in (0, 1):
@@ -553,16 +553,12 @@ def test_wgrad_row3_matches_one_tap_tiles(variant):
         else:
             from oracle import mod_ref_cpu as MO
             m = hip_mod_model(MO.make_params(5, base=64, depth=4), DEV, 64, 4)
-        rt = m.flatten_().rt
-        rt.set_option("x3", 0)  # the f32 MFMA weight gradients are the subject
-        rt.set_option("wgrad_row3", flag)
-        try:
+        # (x3 = 0: the f32 MFMA weight gradients are the subject)
+        with options(m.flatten_().rt, x3=0, wgrad_row3=flag):
             logits = m(x.to(DEV))
             l = unet_hip.seg_losses(logits, t.to(DEV))
             (l[0] + l[1]).backward()
             torch.cuda.synchronize()
-        finally:
-            rt.set_option("wgrad_row3", 1)  # the default
         outs.append((logits.detach().clone(),
                      {k: p.grad.detach().clone() for k, p in m.named_parameters()}))
     assert torch.equal(outs[0][0], outs[1][0])

@@ -42,14 +42,14 @@ def test_x3_forward_no_less_accurate_than_f32_mfma():
     rec = []
     ref = O.forward(x.double(), _to64(P), _to64(O.init_buffers()), True, record=rec)
     errs = {}
+    from _helpers import options
     for x3 in (1, 0):
         m = hip_model(P, DEV)
         st = m.flatten_()
-        st.rt.set_option("x3", x3)
-        with torch.no_grad():
+        with options(st.rt, x3=x3), torch.no_grad():
             logits, ws = st.rt.forward(st.param_arena, st.bn_arena, st.nbt_arena, x.to(DEV),
                                        training=True)
-        torch.cuda.synchronize()
+            torch.cuda.synchronize()
         e = []
         for i in range(18):
             v, off = st.rt.debug_view(ws, 2, 128, 128, True, 0, i)
@@ -77,13 +77,14 @@ def test_x3_train_step_matches_f32_mfma():
     x, t = inputs(5, 2, 128, 128)
     ref = O.train_step(_to64(P), _to64(O.init_buffers()), None, x.double(), t.double())
     res = {}
+    from _helpers import options
     for x3 in (1, 0):
         m = hip_model(P, DEV)
-        m.flatten_().rt.set_option("x3", x3)
-        logits = m(x.to(DEV))
-        losses = unet_hip.seg_losses(logits, t.to(DEV))
-        (losses[0] + losses[1]).backward()
-        torch.cuda.synchronize()
+        with options(m.flatten_().rt, x3=x3):
+            logits = m(x.to(DEV))
+            losses = unet_hip.seg_losses(logits, t.to(DEV))
+            (losses[0] + losses[1]).backward()
+            torch.cuda.synchronize()
         res[x3] = (logits.detach().cpu().double(),
                    {k: p.grad.detach().cpu().double() for k, p in m.named_parameters()})
         del m
@@ -169,29 +170,39 @@ def test_x3_convt_into_decoder_image_bit_identical():
     assert torch.equal(outs[0][1], outs[1][1])
 
 
-def test_x3_halo_tile_matches_one_tap():
-    """The tap-row halo x3 GEMM (rowgemm_x3_row3_kernel, tile 4: one 32-channel group of one
-    tap row's halo feeds the three dx taps; default on the 256x128 3x3 GEMMs) against the
-    one-tap tile (option x3_r3 = 0): the same products summed in (dy, group, dx) instead of
-    (dy, dx, group) order, so logits and gradients agree to f32 summation noise.  B=2 at
-    256x256 (W = 256 .. 16 on the halo kernel) and 1 x 48 x 80 (off: W not a power of two)."""
+def test_x3_halo_tile_no_less_accurate_than_one_tap():
+    """The tap-row halo x3 GEMM (rowgemm_x3_row3_kernel, tiles 4 / 5: one 32-channel group of
+    one tap row's halo feeds the three dx taps; default on the 3x3 GEMMs of power-of-two
+    rows) sums K in (dy, group, dx) instead of the one-tap tiles' (dy, dx, group) order
+    (option x3_r3 = 0), so the two agree to f32 rounding, not bitwise -- and the conv biases
+    of this network (conv -> bias -> ReLU -> BN, models/model.py:36-38) get gradients that
+    largely cancel, whose relative rounding noise reaches ~6e-3 between the two orders.  So
+    both are judged against the fp64 oracle, as test_x3_train_step_matches_f32_mfma does:
+    B=2 at 256x256 (W = 256 .. 16 on the halo kernel, the 256x64 tile on level 0).  At
+    1 x 48 x 80 (W not a power of two) no GEMM takes the halo kernel: bit-identical."""
     import unet_hip
     from _helpers import options
-    for (B, H, W) in ((2, 256, 256), (1, 48, 80)):
-        x, t = inputs(29, B, H, W)
-        outs = []
-        for r3 in (1, 0):
-            m = hip_model(O.make_params(42), DEV)
-            with options(m.flatten_().rt, x3_r3=r3):
-                logits = m(x.to(DEV))
-                l = unet_hip.seg_losses(logits, t.to(DEV))
-                (l[0] + l[1]).backward()
-                torch.cuda.synchronize()
-            outs.append((logits.detach().cpu().double(),
-                         {k: p.grad.detach().cpu().double() for k, p in m.named_parameters()}))
-            del m
-        el = norm_rel(outs[0][0], outs[1][0])
-        worst = max(norm_rel(outs[0][1][k], g) for k, g in outs[1][1].items())
-        print(f"{B}x{H}x{W}: halo vs one-tap logits {el:.2e}, worst grad {worst:.2e}")
-        assert el <= 1e-6 and worst <= 1e-4, (el, worst)
+    P = O.make_params(42)
 
+    def step(x, t, r3):
+        m = hip_model(P, DEV)
+        with options(m.flatten_().rt, x3_r3=r3):
+            logits = m(x.to(DEV))
+            l = unet_hip.seg_losses(logits, t.to(DEV))
+            (l[0] + l[1]).backward()
+            torch.cuda.synchronize()
+        return (logits.detach().cpu().double(),
+                {k: p.grad.detach().cpu().double() for k, p in m.named_parameters()})
+
+    x, t = inputs(29, 2, 256, 256)
+    ref = O.train_step(_to64(P), _to64(O.init_buffers()), None, x.double(), t.double())
+    res = {r3: step(x, t, r3) for r3 in (1, 0)}
+    el = {k: norm_rel(res[k][0], ref["logits"]) for k in res}
+    worst = {k: max(norm_rel(res[k][1][n], g) for n, g in ref["grads"].items()) for k in res}
+    print(f"vs fp64: logits halo {el[1]:.2e} one-tap {el[0]:.2e}; worst grad halo {worst[1]:.2e} "
+          f"one-tap {worst[0]:.2e}")
+    assert el[1] <= 1e-5 and el[1] <= 1.25 * el[0] + 1e-8, el
+    assert worst[1] <= 1.25 * max(worst[0], 1e-2), worst
+    x, t = inputs(29, 1, 48, 80)
+    a, b = step(x, t, 1), step(x, t, 0)
+    assert torch.equal(a[0], b[0]) and all(torch.equal(a[1][k], b[1][k]) for k in a[1])

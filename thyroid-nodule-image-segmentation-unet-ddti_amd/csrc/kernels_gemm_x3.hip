@@ -276,9 +276,9 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_x3_kernel(RowGemmA
 // (SEG + 2) <= 288 x3 rows) -- and the three dx taps read A rows h + dx from it: a third of
 // the A staging.  The x3 rows are 192 B, so the halo and the B rows of three taps (3 x 24 KB)
 // cannot be double-buffered together; B streams per sub-step (dy, group, dx) through its own
-// two-slot ring instead (2 x 56 KB halo + 2 x 24 KB B = 160 KB).  Per sub-step: issue B of the
-// next sub-step (and, on dx = 0, the next group's halo), wait, barrier, 2 k-steps x 4 x 6
-// MFMAs per wave, barrier.
+// two-slot ring instead (2 x 56 KB halo + 2 x 24 KB B = 160 KB).  Per sub-step: wait for its
+// B, barrier, issue B of the next sub-step (and, on dx = 0, the next group's halo) into the
+// slot the previous sub-step read, 2 k-steps x 4 x 6 MFMAs per wave.
 //   geometry (as rowgemm16_row3_kernel): SEG = min(W, 256) output pixels per image row of the
 //   tile, ROWS = 256 / SEG; halo row h = r (SEG + 2) + xl + 1 holds pixel (row r shifted by
 //   dy - 1, column x0 + xl), xl = -1 .. SEG; output pixel (r, xo) reads halo row
@@ -395,19 +395,19 @@ __global__ __launch_bounds__((256 / WM) * (BN / WN) * 64, 1) void rowgemm_x3_row
     issue_b(0);
     for (int s = 0; s < ns; ++s) {
         const int g = s / 3, dx = s - g * 3;
-        // next B (and, entering a group, the next group's halo) while this sub-step computes;
-        // then wait for this sub-step's B (and everything issued before it, its group's halo
-        // included).  Issue order: B(s), [A(g + 1) when s - 1 entered group g], B(s + 1),
-        // [A(g + 1) when s enters group g]: the pieces allowed in flight are those after B(s).
         const bool nb = s + 1 < ns, na = dx == 0 && g + 1 < 3 * CC;
         const bool pa = dx == 1 && g + 1 < 3 * CC;  // s - 1 issued the next halo after B(s)
-        if (nb) issue_b(s + 1);
-        if (na) issue_a(g + 1);
-        if (nb && (na || pa)) x3_wait_vm<AI + BI>();
-        else if (nb) x3_wait_vm<BI>();
-        else if (na || pa) x3_wait_vm<AI>();
+        // one barrier per sub-step: wait for B(s) (in flight after it: the next halo when
+        // s - 1 issued it), barrier -- every wave's DMA has landed and every wave has finished
+        // reading sub-step s - 1 -- then issue B(s + 1) into s - 1's slot and, entering a
+        // group, the next halo into the previous group's buffer.  (r04: issuing before the
+        // wait and closing each sub-step with a second barrier gave the same bits at 2-3 %
+        // lower TF/s, profiles/r04_x3_halo_ab.txt.)
+        if (pa) x3_wait_vm<AI>();
         else x3_wait_vm<0>();
         x3_barrier();
+        if (nb) issue_b(s + 1);
+        if (na) issue_a(g + 1);
         const char* abase = smem + (g & 1) * AREG;
         const char* bbase = smem + 2 * AREG + (s & 1) * BREG;
 #pragma unroll
@@ -432,8 +432,8 @@ __global__ __launch_bounds__((256 / WM) * (BN / WN) * 64, 1) void rowgemm_x3_row
                 for (int nt = 0; nt < NT; ++nt) mfma_x3s(af[mt], bfr[nt], acc[mt][nt], acl[mt][nt]);
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        x3_barrier();
     }
+    x3_barrier();  // the epilogue reuses the stage memory
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll

@@ -49,6 +49,8 @@ class UNetRuntime:
             o, l = ctypes.c_int64(), ctypes.c_int64()
             lib.unet_bucket_range(h, b, ctypes.byref(o), ctypes.byref(l))
             self.buckets.append((o.value, l.value))
+        # the context's schedule options as created (reset_options restores them)
+        self._default_options = {k: self.get_option(k) for k in _lib.option_names()}
 
     def __del__(self):
         try:
@@ -139,6 +141,13 @@ class UNetRuntime:
         """Kernel-schedule option (include/unet_hip.h unet_set_option); A/B runs and tests."""
         _lib.check(self.lib.unet_set_option(self.ctx, name.encode(), int(value)), self.ctx,
                    f"unet_set_option({name})")
+
+    def reset_options(self):
+        """Every schedule option back to its value at creation (this runtime is shared by
+        every model of its configuration on the device)."""
+        for k, v in self._default_options.items():
+            if self.get_option(k) != v:
+                self.set_option(k, v)
 
     def get_option(self, name):
         v = ctypes.c_int64()
