@@ -837,12 +837,15 @@ __global__ __launch_bounds__((BM / 32) * (BN / 32) * 64, OCC) void wgrad_x3_row3
     for (int s = 0; s < S - 1; ++s)
         if (s < nk) issue(s, s);
     for (int kc = 0; kc < nk; ++kc) {
-        if (kc + S - 1 < nk) issue(kc + S - 1, (kc + S - 1) % S);
-        const int ahead = min(S - 1, nk - 1 - kc);
-        if (S >= 3 && ahead >= 2) x3_wait_vm<(S >= 3 ? 2 : 1) * GPC>();
-        else if (ahead >= 1) x3_wait_vm<GPC>();
+        // one barrier per chunk: wait for chunk kc (chunk kc + 1 may stay in flight with three
+        // stages), barrier -- every wave's DMA has landed and every wave has finished reading
+        // chunk kc - 1 -- then restage that slot with chunk kc + S - 1.  (r04: issuing before
+        // the wait and closing each chunk with a second barrier: the same bits, 0.5 % slower
+        // over the step.)
+        if (S >= 3 && kc + 1 < nk) x3_wait_vm<GPC>();
         else x3_wait_vm<0>();
         x3_barrier();
+        if (kc + S - 1 < nk) issue(kc + S - 1, (kc + S - 1) % S);
         const unsigned sb = x3_lds_u32(smem) + (kc % S) * STAGE;
         x3_short4 fa[2][3][3][2], fb[2][3][2];
         auto load = [&](auto KK) {
@@ -883,7 +886,6 @@ __global__ __launch_bounds__((BM / 32) * (BN / 32) * 64, OCC) void wgrad_x3_row3
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
         mma(std::integral_constant<int, 1>{});
-        x3_barrier();
     }
 
     const int li = lane & 31, lh = lane >> 5;

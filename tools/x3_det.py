@@ -1,6 +1,7 @@
-"""GPU-box check: is the x3 training step deterministic per schedule in a fresh process?
-Runs x3_r3 = 1, 0, 1, 0 (and 2) on the same inputs and reports bitwise equality of repeats
-and the norm-relative gradient gap between schedules (per tensor, worst three)."""
+"""GPU-box check: one training step (B=2, 256x256, model.py UNet) per schedule spec, each
+spec run twice; reports bitwise equality of repeats and against the first spec, and the
+norm-relative gap of the worst three gradient tensors.
+usage: python tools/x3_det.py "" "x3_r3=0" "x3_wob=1 x3_r3=1" ..."""
 import sys
 sys.path[:0] = ["tests", ".", "thyroid-nodule-image-segmentation-unet-ddti_amd"]
 import torch
@@ -10,21 +11,23 @@ from oracle import unet_ref_cpu as O
 
 DEV = torch.device("cuda:0")
 x, t = inputs(29, 2, 256, 256)
+specs = sys.argv[1:] or ["", "x3_r3=0"]
 res = []
-for r3 in (1, 0, 1, 0, 2):
-    m = hip_model(O.make_params(42), DEV)
-    with options(m.flatten_().rt, x3_r3=r3):
-        logits = m(x.to(DEV))
-        l = unet_hip.seg_losses(logits, t.to(DEV))
-        (l[0] + l[1]).backward()
-        torch.cuda.synchronize()
-    res.append((r3, logits.detach().cpu().double(),
-                {k: p.grad.detach().cpu().double() for k, p in m.named_parameters()}))
-    del m
-for i in range(len(res)):
-    for j in range(i):
-        a, b = res[i], res[j]
-        same = torch.equal(a[1], b[1]) and all(torch.equal(a[2][k], b[2][k]) for k in a[2])
-        gaps = sorted(((norm_rel(a[2][k], b[2][k]), k) for k in a[2]), reverse=True)[:3]
-        print(f"run{i}(r3={a[0]}) vs run{j}(r3={b[0]}): bitwise {same} logits {norm_rel(a[1], b[1]):.2e} "
-              f"worst grads {[(f'{g:.1e}', k) for g, k in gaps]}", flush=True)
+for spec in specs:
+    kv = dict((a, int(b)) for a, b in (o.split("=") for o in spec.split()))
+    for rep in range(2):
+        m = hip_model(O.make_params(42), DEV)
+        with options(m.flatten_().rt, **kv):
+            logits = m(x.to(DEV))
+            l = unet_hip.seg_losses(logits, t.to(DEV))
+            (l[0] + l[1]).backward()
+            torch.cuda.synchronize()
+        res.append((f"[{spec}]#{rep}", logits.detach().cpu().double(),
+                    {k: p.grad.detach().cpu().double() for k, p in m.named_parameters()}))
+        del m
+base = res[0]
+for r in res[1:]:
+    same = torch.equal(r[1], base[1]) and all(torch.equal(r[2][k], base[2][k]) for k in r[2])
+    gaps = sorted(((norm_rel(r[2][k], base[2][k]), k) for k in r[2]), reverse=True)[:3]
+    print(f"{r[0]} vs {base[0]}: bitwise {same} logits {norm_rel(r[1], base[1]):.2e} "
+          f"worst grads {[(f'{g:.1e}', k) for g, k in gaps]}", flush=True)
