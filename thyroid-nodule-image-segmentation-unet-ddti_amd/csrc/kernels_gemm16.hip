@@ -340,14 +340,12 @@ __global__ __launch_bounds__(512, 1) void rowgemm16_row3_kernel(RowGemmArgs p) {
     const int ns = 3 * CC;
     issue(0);
     for (int s = 0; s < ns; ++s) {
-        if (s + 1 < ns) {
-            issue(s + 1);
-            if (a3) wait_vm<AI + BI>();
-            else wait_vm<AI - 1 + BI>();
-        } else {
-            wait_vm<0>();
-        }
+        // one barrier per stage: wait for stage s, barrier (every wave's DMA landed, every
+        // wave done reading stage s - 1), then restage s - 1's buffer with s + 1.  (r04: issuing
+        // before the wait and a second barrier after the MFMAs gave the same bits, 3 % slower.)
+        wait_vm<0>();
         block_barrier();
+        if (s + 1 < ns) issue(s + 1);
         const char* base = smem + (s & 1) * STAGE;
 #pragma unroll
         for (int dx = 0; dx < 3; ++dx)
@@ -370,8 +368,8 @@ __global__ __launch_bounds__(512, 1) void rowgemm16_row3_kernel(RowGemmArgs p) {
             }
         // this stage's ds_reads must have returned before any wave restages it
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        block_barrier();
     }
+    block_barrier();  // the epilogue reuses the stage memory
     row_epilogue<EMODE, BM, BN, WM, WN, true>(p, acc, m0, n0, tile_m, wm, wn, lane, tid, (float*)smem);
 }
 
@@ -739,23 +737,23 @@ __global__ __launch_bounds__(512, 1) void wgrad16_row3_kernel(WgradArgs p) {
     for (int s = 0; s < S - 1; ++s)
         if (s < nk) issue(s, s);
     for (int kc = 0; kc < nk; ++kc) {
-        if (kc + S - 1 < nk) issue(kc + S - 1, (kc + S - 1) % S);
-        const int ahead = min(S - 1, nk - 1 - kc);
-        // this wave's pieces per chunk: AI + BI (a3) or AI - 1 + BI
+        // one barrier per chunk: chunks kc + 1 .. kc + S - 2 may stay in flight; then
+        // restage the buffer every wave finished reading in chunk kc - 1.  (r04: issuing
+        // before the wait and a second barrier after the MFMAs, the same bits, 2 % slower.)
+        const int ahead = min(S - 2, nk - 1 - kc);
         if (a3) {
             constexpr int G = AI + BI;
-            if (ahead >= 3) wait_vm<3 * G>();
-            else if (ahead == 2) wait_vm<2 * G>();
+            if (ahead >= 2) wait_vm<2 * G>();
             else if (ahead == 1) wait_vm<G>();
             else wait_vm<0>();
         } else {
             constexpr int G = AI - 1 + BI;
-            if (ahead >= 3) wait_vm<3 * G>();
-            else if (ahead == 2) wait_vm<2 * G>();
+            if (ahead >= 2) wait_vm<2 * G>();
             else if (ahead == 1) wait_vm<G>();
             else wait_vm<0>();
         }
         block_barrier();
+        if (kc + S - 1 < nk) issue(kc + S - 1, (kc + S - 1) % S);
         const unsigned sb = lds_u32(smem) + (kc % S) * STAGE;
         short4v fa[2][3][2], fb[2][NT][2];
         auto load = [&](auto KK) {
@@ -801,7 +799,6 @@ __global__ __launch_bounds__(512, 1) void wgrad16_row3_kernel(WgradArgs p) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
         mma(std::integral_constant<int, 3>{});
-        block_barrier();
     }
 
     const int li = lane & 31, lh = lane >> 5;
