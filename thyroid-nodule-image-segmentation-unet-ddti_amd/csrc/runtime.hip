@@ -94,7 +94,9 @@ struct Options {
                                // 27.1 -> 24.4 ms/step), 2 layers with a 64-channel operand
     int wgrad_row3_tile = -1;  // its tile (>= 20), -1 = by channel counts
     int wgrad_blocks = 2048;       // split-K target (blocks) of the one-tap f32 weight gradients
-    int rg16_bn_k = 8192;          // rg16: E_STORE_BN GEMMs with K below this take the 128x128 tile
+    int rg16_bn_k = 0;             // rg16: E_STORE_BN GEMMs with K below this take the 128x128 tile
+                                   // (8192 until the one-barrier halo kernel, r04: 0 is 1-1.5 %
+                                   // faster on config 4, profiles/r04_c4_barrier_ab.txt)
     int wgrad16_blocks = 1536;     // split-K target (blocks) of the bf16 weight gradients
                                    // (config 4 A/B: 1536 +1.4 % over 2048, 1024 -4.7 %)
     int wgrad_row3_big = 21;       // row3 tile where Cin, Cout % 128 == 0 (-1 = 23)
@@ -680,11 +682,11 @@ bool rg16_on(const unet_ctx* c, int C, int N) {
 // speed only.  Default: the 256x256 tile (8 waves, one block per CU) unless
 //  * it would leave CUs idle: fewer than 256 blocks (the 16x16 / 32x32 levels of config 4:
 //    bottleneck fwd 0.48 -> 0.37 ms, its dgrad 0.90 -> 0.48 ms on the 128x128 tile), or
-//  * the epilogue is the BN-backward-partials one (E_STORE_BN: reads the BN input, writes
-//    f32 and reduces per-channel partials) over a short K < 8192: with one block per CU
-//    nothing hides that epilogue, while two co-resident 128x128 blocks overlap one's
-//    epilogue with the other's MFMAs (level-1 dgrad 1.15 -> 0.80 ms, level-0 ConvT dgrad
-//    0.77 -> 0.37 ms; per-layer sweep in profiles/r01_rg16_tile_sweep.txt).
+//  * option rg16_bn_k > K for a BN-backward-partials GEMM (E_STORE_BN: reads the BN input,
+//    writes f32 and reduces per-channel partials): with one block per CU nothing hides that
+//    epilogue, while two co-resident 128x128 blocks overlap one's epilogue with the other's
+//    MFMAs (r01: level-1 dgrad 1.15 -> 0.80 ms, profiles/r01_rg16_tile_sweep.txt; default 0
+//    since the r04 one-barrier halo kernel made the 256x256 / 512x128 tiles faster overall).
 int rg16_tile(const unet_ctx* c, const RowGemmArgs& g) {
     const int cout = g.emode == E_CONVT ? g.cout : 0;
     auto fits = [&](int t) {
