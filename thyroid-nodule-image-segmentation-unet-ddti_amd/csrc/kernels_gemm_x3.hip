@@ -477,7 +477,8 @@ static int x3_tile(const RowGemmArgs& a, int tile, hipStream_t s) {
         // (r04, not kept: 4-wave 128x64 / 64x128 wave tiles, within noise of 8 waves; B
         // straight from global memory into registers instead of the LDS ring, one barrier per
         // halo group, bit-identical but 222 -> 161 TF/s: the per-wave B loads cost more than
-        // the ring's barriers; 256 x 64 as 4 waves of 64 x 64, bit-identical, 589 -> 584 img/s)
+        // the ring's barriers; 256 x 64 as 4 waves of 64 x 64, bit-identical, 589 -> 584 img/s;
+        // 256 x 64 with a three-slot B ring, B two sub-steps ahead: bit-identical, no gain)
         if constexpr (AMODE == G_CONV3)
             return tile == 4 ? x3r3_go<EMODE, 128>(a, s) : x3r3_go<EMODE, 64>(a, s);
         return -1;
