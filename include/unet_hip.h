@@ -95,10 +95,12 @@ typedef struct {
     int in_channels;   /* models/model.py:6 / mod.py:11 in_channels (default 1; must be 1) */
     int out_channels;  /* models/model.py:6 / mod.py:12 out_channels (default 1; 1..4)   */
     int variant;       /* unet_variant (0 = models/model.py)                               */
-    int base_filters;  /* mod.py:13 (0 = default 64); a multiple of 8, <= 256.  32 / 64 /
-                          128 / 256 run natively; other widths (the reference grid's 16 /
-                          24 / 48) run zero-padded to the next power of two >= 32 inside
-                          the library (the caller's arenas keep the torch layouts) */
+    int base_filters;  /* mod.py:13 (0 = default 64); a multiple of 8, <= 256.  Channels are
+                          padded per level inside the library (the caller's arenas keep the
+                          torch layouts): level 0 runs the next power of two >= 32 of
+                          base_filters, every deeper level the next multiple of 32 of
+                          base_filters << level (base 16: 32, 32, 64, 128, 256 -- only level 0
+                          padded; 24: 32, 64, 96, 192, ...; 48: 64, 96, 192, ...) */
     int depth;         /* mod.py:14 (0 = default 5 for mod, 4 for model); 1..6             */
     int math;          /* unet_math of the conv GEMMs (0 = f32)                            */
 } unet_cfg;
@@ -215,8 +217,10 @@ int unet_resize_u8(unet_ctx* ctx, const uint8_t* src, int h, int w, float* dst, 
  *   tile16_n128_dgrad tile16_n64 rg16 rg16_tile rg16_bn_k rg16_r3 rg16_n128 rg16_n128_bn
  *   rg16_xp wg16 wg16_tile wg16_r3 convt16 wg16t xcd16 xcd_remap dz_in_wgrad x3 x3_tile
  *   x3_wtile x3_wblocks x3_n64 x3_r3
- * Set them between steps, not between a forward and its backward (the workspace plan
- * depends on some of them). */
+ * Set them between steps, not between a forward and its backward: the workspace plan and
+ * which saved images exist depend on them (x3, convt16, the bf16 kernel choices, ...), so
+ * unet_backward returns UNET_ERR_INVALID when any option differs from the last training
+ * unet_forward's (or when no training forward ran on this context). */
 int unet_set_option(unet_ctx* ctx, const char* name, int64_t value);
 int unet_get_option(const unet_ctx* ctx, const char* name, int64_t* value);
 /* i-th option name (0 ..), UNET_ERR_INVALID past the last one; *name is static. */
@@ -238,9 +242,21 @@ int unet_timing_read(unet_ctx* ctx, int i, const char** family, int64_t* launche
  * kind: 0 y[i] (post-ReLU conv output, NHWC, channel stride *ld, channel offset *off),
  *       1 BN scale[i], 2 BN shift[i], 3 BN batch mean[i], 4 BN invstd[i],
  *       5 pooled[l] (NHWC dense), 6 concat buffer[l] (NHWC, 2*64<<l channels),
- *       7 d(concat)[l] of the last backward.  *count = elements (pixels*ld for NHWC). */
+ *       7 d(concat)[l] of the last backward, 8 max-pool winner index[l] (uint8 NHWC dense,
+ *       window position 0..3 in torch's scan order).  *count = elements (pixels*ld for NHWC). */
 int unet_debug_view(unet_ctx* ctx, int N, int H, int W, int training, int kind, int index,
                     int64_t* byte_offset, int64_t* count, int* ld, int* off);
+
+/* Test hooks of the exact three-way bf16 split the x3 GEMMs use (csrc/x3_split.h; no
+ * reference counterpart).  n f32 values (n a multiple of 32) become the x3 image the kernels
+ * stream, bf16 bit patterns [n / 32][3][32]: for v = v[32 r + j], out[96 r + j] = h,
+ * out[96 r + 32 + j] = m, out[96 r + 64 + j] = l, with v = h + m + l exactly for normal and
+ * huge finite v; +-inf / NaN keep h = v, m = l = 0.  unet_x3_split_host runs the shared source on the host (bit-level RNE);
+ * unet_x3_split_device runs the device pass (to_x3_kernel, hardware bf16 conversion) on n
+ * device floats into a device buffer, enqueued on `stream`. */
+int unet_x3_split_host(const float* v, int64_t n, uint16_t* out);
+int unet_x3_split_device(unet_ctx* ctx, const float* v, int64_t n, uint16_t* out,
+                         unet_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -105,17 +105,42 @@ def _bn(x, P, B, name, training):
 
 
 _RECORD = None  # test hook: list collecting the post-ReLU (pre-BN) output of every conv
+# test hook: 18 boolean masks (NCHW, forward order) replacing the ReLU decisions -- ReLU(z)
+# becomes z * mask -- so an fp64 evaluation can follow another evaluation's ReLU branches
+# (tests/test_gpu_x3.py: near-zero pre-activations that round to the other side of 0 in f32
+# would otherwise move whole upstream gradients)
+_RELU_MASKS = None
+
+
+# test hook: 4 max-pool winner indices (N, C, Ho, Wo, window position 0..3 in torch's scan
+# order), so the fp64 evaluation also follows another evaluation's pooling branches (near-ties
+# between BN outputs)
+_POOL_IDX = None
+
+
+def _maxpool(x):
+    if _POOL_IDX is None:
+        return F.max_pool2d(x, 2)
+    N, C, H, W = x.shape
+    win = x.reshape(N, C, H // 2, 2, W // 2, 2).permute(0, 1, 2, 4, 3, 5).reshape(N, C, H // 2, W // 2, 4)
+    return win.gather(-1, _POOL_IDX.pop(0).long().unsqueeze(-1)).squeeze(-1)
+
+
+def _relu(x):
+    if _RELU_MASKS is None:
+        return F.relu(x)
+    return x * _RELU_MASKS.pop(0).to(x.dtype)
 
 
 def _conv_block(x, P, B, prefix, training):
     # models/model.py:33-43
     x = F.conv2d(x, P[f"{prefix}.0.weight"], P[f"{prefix}.0.bias"], padding=1)
-    x = F.relu(x)
+    x = _relu(x)
     if _RECORD is not None:
         _RECORD.append(x.detach())
     x = _bn(x, P, B, f"{prefix}.2", training)
     x = F.conv2d(x, P[f"{prefix}.3.weight"], P[f"{prefix}.3.bias"], padding=1)
-    x = F.relu(x)
+    x = _relu(x)
     if _RECORD is not None:
         _RECORD.append(x.detach())
     x = _bn(x, P, B, f"{prefix}.5", training)
@@ -126,23 +151,29 @@ def _convT(x, P, name):
     return F.conv_transpose2d(x, P[f"{name}.weight"], P[f"{name}.bias"], stride=2)
 
 
-def forward(x, P, B, training=True, record=None):
+def forward(x, P, B, training=True, record=None, relu_masks=None, pool_idx=None):
     """models/model.py:53-73.  P: params (name -> tensor), B: buffers (mutated in train mode).
-    record: optional list that receives the 18 post-ReLU conv outputs (test diagnostics)."""
-    global _RECORD
+    record: optional list that receives the 18 post-ReLU conv outputs (test diagnostics).
+    relu_masks / pool_idx: optional 18 boolean NCHW masks / 4 winner-index tensors that replace
+    the conv ReLUs' / max-pools' decisions (test hook)."""
+    global _RECORD, _RELU_MASKS, _POOL_IDX
     _RECORD = record
+    _RELU_MASKS = None if relu_masks is None else list(relu_masks)
+    _POOL_IDX = None if pool_idx is None else list(pool_idx)
     try:
         return _forward(x, P, B, training)
     finally:
         _RECORD = None
+        _RELU_MASKS = None
+        _POOL_IDX = None
 
 
 def _forward(x, P, B, training):
     enc1 = _conv_block(x, P, B, "encoder1", training)
-    enc2 = _conv_block(F.max_pool2d(enc1, 2), P, B, "encoder2", training)
-    enc3 = _conv_block(F.max_pool2d(enc2, 2), P, B, "encoder3", training)
-    enc4 = _conv_block(F.max_pool2d(enc3, 2), P, B, "encoder4", training)
-    m = F.max_pool2d(enc4, kernel_size=2, stride=2)              # middle.0
+    enc2 = _conv_block(_maxpool(enc1), P, B, "encoder2", training)     # F.max_pool2d(enc1, 2)
+    enc3 = _conv_block(_maxpool(enc2), P, B, "encoder3", training)
+    enc4 = _conv_block(_maxpool(enc3), P, B, "encoder4", training)
+    m = _maxpool(enc4)              # middle.0 nn.MaxPool2d(kernel_size=2, stride=2)
     m = _conv_block(m, P, B, "middle.1", training)
     dec4 = _convT(m, P, "middle.2")
     dec4 = torch.cat([dec4, enc4], dim=1)

@@ -2,12 +2,16 @@
 csrc/kernels_gemm_x3.hip) against the f32-MFMA kernels (option x3 = 0), both measured
 against the oracle evaluated in fp64.
 
-Every f32 operand splits exactly into three bf16 pieces; the kernels form six of the nine
-piece products (the three dropped ones are below 2^-25 |a b| together) and keep the five
-small products in a separate f32 accumulator, so the large accumulator takes one rounding
-per 16 products against the f32 MFMA's one per 2.  The bar here is therefore "no worse than
-the f32 MFMA path", per layer and on the logits; the 1e-4 north-star bars are the other GPU
-tests' (they run the default, x3 on).
+Every f32 operand splits exactly into three bf16 pieces (csrc/x3_split.h); the kernels form
+six of the nine piece products (the three dropped ones are at most ~2^-23 |a b| together) and
+keep the five small products in a separate f32 accumulator, so the large accumulator takes one
+rounding per 16 products against the f32 MFMA's one per 2.  Bars: "no worse than the f32 MFMA
+path" per layer and on the logits, plus ABSOLUTE bars against an fp64 oracle that follows the
+GPU's own branches (oracle/unet_ref_cpu.py relu_masks / pool_idx: a pre-activation within ~1e-6
+of zero rounds to the other side in one f32 evaluation or another, and a near-tie of two BN
+outputs in a max-pool window routes the gradient to another pixel; either moves whole upstream
+gradients, which is what the relative bars used to absorb).  The 1e-4 north-star bars are the
+other GPU tests' (they run the default, x3 on).
 """
 import os
 
@@ -30,6 +34,60 @@ def _threads():
 
 def _to64(d):
     return {k: (v.double() if v.is_floating_point() else v.clone()) for k, v in d.items()}
+
+
+# Absolute bars against the fp64 oracle on the GPU's own ReLU branches (measured r05 on
+# MI355X: profiles/r05_x3_masked_bars.txt).  Conv / ConvT weight gradients carry no
+# cancellation; the conv biases ahead of ReLU -> BN (models/model.py:36-38) get sums that
+# largely cancel (the BN input gradient sums to ~0 over the pixels), so their relative
+# rounding noise is larger; every tensor is held to SURVEY §8c's 1e-2 as well.
+W_BAR, B_BAR, ALL_BAR = 1e-4, 2e-3, 1e-2
+
+
+def _relu_masks(m, x):
+    """The 18 conv ReLU decisions (y > 0, NCHW) and the 4 max-pool winner indices of this
+    path's training forward on x (the forward is deterministic, so they are the ones m(x)
+    takes)."""
+    st = m.flatten_()
+    N, _, H, W = x.shape
+    with torch.no_grad():
+        _, ws = st.rt.forward(st.param_arena, st.bn_arena.clone(), st.nbt_arena.clone(),
+                              x.to(DEV), training=True)
+    masks = []
+    for i in range(18):
+        v, off = st.rt.debug_view(ws, N, H, W, True, 0, i)
+        lvl = {0: 0, 1: 0, 2: 1, 3: 1, 4: 2, 5: 2, 6: 3, 7: 3, 8: 4, 9: 4, 10: 3, 11: 3,
+               12: 2, 13: 2, 14: 1, 15: 1, 16: 0, 17: 0}[i]
+        C = 64 << lvl
+        h, w = H >> lvl, W >> lvl
+        masks.append((v[:, off:off + C] > 0).reshape(N, h, w, C).permute(0, 3, 1, 2).cpu())
+    pools = []
+    for lvl in range(4):
+        v, _ = st.rt.debug_view(ws, N, H, W, True, 8, lvl)
+        C, h, w = 64 << lvl, H >> (lvl + 1), W >> (lvl + 1)
+        pools.append(v.reshape(N, h, w, C).permute(0, 3, 1, 2).cpu())
+    del ws
+    return masks, pools
+
+
+def _masked_fp64_step(P, x, t, branches):
+    masks, pools = branches
+    return O.train_step(_to64(P), _to64(O.init_buffers()), None, x.double(), t.double(),
+                        forward_fn=lambda xx, PP, BB, tr: O.forward(xx, PP, BB, tr, relu_masks=masks,
+                                                                   pool_idx=pools))
+
+
+def _check_masked(grads, ref, tag):
+    """Per-tensor norm-relative gradient errors against the masked fp64 step: weights <=
+    W_BAR, conv / BN biases <= B_BAR, every tensor <= ALL_BAR.  Returns the worst of each."""
+    ew = {k: norm_rel(grads[k], g) for k, g in ref["grads"].items() if g.dim() == 4}
+    eb = {k: norm_rel(grads[k], g) for k, g in ref["grads"].items() if g.dim() != 4}
+    kw, kb = max(ew, key=ew.get), max(eb, key=eb.get)
+    print(f"{tag}: vs masked fp64: worst weight {kw} {ew[kw]:.2e}, worst other {kb} {eb[kb]:.2e}")
+    assert ew[kw] <= W_BAR, (tag, kw, ew[kw])
+    assert max(eb.values()) <= ALL_BAR, (tag, kb, eb[kb])
+    assert all(v <= B_BAR for v in eb.values()), (tag, kb, eb[kb])
+    return ew[kw], eb[kb]
 
 
 def test_x3_forward_no_less_accurate_than_f32_mfma():
@@ -68,19 +126,21 @@ def test_x3_forward_no_less_accurate_than_f32_mfma():
 
 def test_x3_train_step_matches_f32_mfma():
     """One training step (fwd, BCE+Dice, bwd) at B=2 128x128 against the fp64 oracle: logits
-    at least as accurate as the f32-MFMA path's (measured 1.2e-6 vs 3.1e-6), gradients within
-    the spread the f32 path itself shows (a ReLU input within ~1e-6 of zero flips in one
-    evaluation or the other and moves upstream gradients by ~1e-2: measured worst tensor 9.3e-3
-    for x3, 1.5e-2 for f32)."""
+    at least as accurate as the f32-MFMA path's (measured 1.2e-6 vs 3.1e-6); gradients against
+    the fp64 step that follows each path's own ReLU branches at the absolute bars above, and
+    x3's worst tensor no worse than 1.25x the f32 path's on the same footing.  (Against the
+    unmasked fp64 step a ReLU input within ~1e-6 of zero flips in one evaluation or the other
+    and moves upstream gradients by ~1e-2)"""
     import unet_hip
     P = O.make_params(11)
     x, t = inputs(5, 2, 128, 128)
     ref = O.train_step(_to64(P), _to64(O.init_buffers()), None, x.double(), t.double())
-    res = {}
+    res, worst = {}, {}
     from _helpers import options
     for x3 in (1, 0):
         m = hip_model(P, DEV)
         with options(m.flatten_().rt, x3=x3):
+            masks = _relu_masks(m, x)
             logits = m(x.to(DEV))
             losses = unet_hip.seg_losses(logits, t.to(DEV))
             (losses[0] + losses[1]).backward()
@@ -88,12 +148,11 @@ def test_x3_train_step_matches_f32_mfma():
         res[x3] = (logits.detach().cpu().double(),
                    {k: p.grad.detach().cpu().double() for k, p in m.named_parameters()})
         del m
+        worst[x3] = _check_masked(res[x3][1], _masked_fp64_step(P, x, t, masks), f"x3={x3}")
     el = {k: norm_rel(res[k][0], ref["logits"]) for k in res}
     assert el[1] <= 1e-5 and el[1] <= 1.25 * el[0] + 1e-8, el
-    worst = {k: max(norm_rel(res[k][1][n], g) for n, g in ref["grads"].items()) for k in res}
-    print(f"logits vs fp64: x3 {el[1]:.2e} f32 {el[0]:.2e}; worst grad: x3 {worst[1]:.2e} "
-          f"f32 {worst[0]:.2e}")
-    assert worst[1] <= 1.25 * max(worst[0], 1e-2), worst
+    print(f"logits vs fp64: x3 {el[1]:.2e} f32 {el[0]:.2e}")
+    assert worst[1][0] <= 1.25 * worst[0][0] + 1e-7, worst
 
 
 @pytest.mark.parametrize("B,H,W", [(2, 128, 128), (1, 48, 80)])
@@ -198,11 +257,102 @@ def test_x3_halo_tile_no_less_accurate_than_one_tap():
     ref = O.train_step(_to64(P), _to64(O.init_buffers()), None, x.double(), t.double())
     res = {r3: step(x, t, r3) for r3 in (1, 0)}
     el = {k: norm_rel(res[k][0], ref["logits"]) for k in res}
-    worst = {k: max(norm_rel(res[k][1][n], g) for n, g in ref["grads"].items()) for k in res}
-    print(f"vs fp64: logits halo {el[1]:.2e} one-tap {el[0]:.2e}; worst grad halo {worst[1]:.2e} "
-          f"one-tap {worst[0]:.2e}")
+    print(f"vs fp64: logits halo {el[1]:.2e} one-tap {el[0]:.2e}")
     assert el[1] <= 1e-5 and el[1] <= 1.25 * el[0] + 1e-8, el
-    assert worst[1] <= 1.25 * max(worst[0], 1e-2), worst
+    # gradients: absolute bars against the fp64 step on each schedule's own ReLU branches
+    worst = {}
+    for r3 in (1, 0):
+        m = hip_model(P, DEV)
+        with options(m.flatten_().rt, x3_r3=r3):
+            masks = _relu_masks(m, x)
+        del m
+        worst[r3] = _check_masked(res[r3][1], _masked_fp64_step(P, x, t, masks), f"x3_r3={r3}")
+    assert worst[1][0] <= 1.25 * worst[0][0] + 1e-7, worst
     x, t = inputs(29, 1, 48, 80)
     a, b = step(x, t, 1), step(x, t, 0)
     assert torch.equal(a[0], b[0]) and all(torch.equal(a[1][k], b[1][k]) for k in a[1])
+
+
+def test_x3_split_device_matches_restatement():
+    """The device split pass (to_x3_kernel through unet_x3_split_device, hardware bf16
+    conversion) against the NumPy restatement of csrc/x3_split.h: bit-identical over normal
+    values of every exponent, huge finite values around the bf16 overflow threshold (h = the
+    largest finite bf16), +-inf (h = v, m = l = 0), subnormal and tiny values, signed zeros;
+    NaN keeps a NaN h with m = l = 0."""
+    import x3_split_ref as X
+    import unet_hip
+    m = hip_model(O.make_params(42), DEV)
+    rt = m.flatten_().rt
+    v = X.edge_values(2)
+    vd = torch.from_numpy(v).to(DEV)
+    out = torch.zeros(3 * v.size, dtype=torch.int16, device=DEV)
+    rc = rt.lib.unet_x3_split_device(rt.ctx, vd.data_ptr(), v.size, out.data_ptr(),
+                                     unet_hip._lib.stream_ptr(DEV))
+    assert rc == 0
+    got = out.cpu().numpy().view(np.uint16)
+    want = X.to_image(*X.split(v))
+    gh, gm, gl = X.from_image(got)
+    wh, wm, wl = X.from_image(want)
+    nan = np.isnan(v)
+    assert np.array_equal(gm, wm) and np.array_equal(gl, wl)
+    assert np.array_equal(gh[~nan], wh[~nan]), np.flatnonzero(gh != wh)[:8]
+    assert np.all(np.isnan(X.bf16_to_f32(gh[nan])))
+
+
+@pytest.mark.parametrize("beta", [3.395e38, -3.4e38, float("nan"), 1e-39, float("inf"), float("-inf")])
+def test_x3_range_edge_activation_through_one_conv(beta):
+    """An activation at the range edges through one x3 conv: channel 5 of encoder1's first BN
+    gets gamma = 0, beta = `beta`, so encoder1.3 (64 -> 64, the halo x3 GEMM) reads that value
+    at every pixel, split by the forward's to_x3 pass.  Against the f32 MFMA kernels (x3 = 0)
+    on the same input: huge finite values (above bf16's overflow threshold; before r05 their
+    split overflowed to inf and turned the conv into NaN), NaN and subnormal values give the
+    same outputs (finite ones within 1e-5 norm-relative).  +-inf: h = +-inf, m = l = 0, so an
+    output is +-inf or NaN as in f32, except that a weight whose low piece is exactly 0 turns
+    an inf product into inf * 0 = NaN (x3_split.h caveat): after the ReLU (NaN -> 0 on both
+    paths) such outputs read 0 where f32 has +inf; nothing else may differ."""
+    P = O.make_params(42)
+    P["encoder1.2.weight"][5] = 0.0
+    P["encoder1.2.bias"][5] = beta
+    x, _ = inputs(3, 2, 64, 64)
+    from _helpers import options
+    y = {}
+    for x3 in (1, 0):
+        m = hip_model(P, DEV)
+        st = m.flatten_()
+        with options(st.rt, x3=x3), torch.no_grad():
+            _, ws = st.rt.forward(st.param_arena, st.bn_arena, st.nbt_arena, x.to(DEV), training=True)
+            v, off = st.rt.debug_view(ws, 2, 64, 64, True, 0, 1)
+            y[x3] = v[:, off:off + 64].cpu().double()
+        del m, st, ws
+    a, b = y[1], y[0]
+    fa, fb = torch.isfinite(a), torch.isfinite(b)
+    if np.isinf(beta):
+        diff = ~((a == b) | (torch.isnan(a) & torch.isnan(b)))
+        assert torch.all((b[diff] == float("inf")) & (a[diff] == 0)), "x3 differs beyond inf*0"
+        assert diff.double().mean() <= 0.1
+        return
+    assert torch.equal(fa, fb)
+    assert torch.equal(torch.isnan(a), torch.isnan(b))
+    if fa.any():
+        assert norm_rel(a[fa], b[fa]) <= 1e-5, norm_rel(a[fa], b[fa])
+    if abs(beta) > 1e38:
+        assert fa.all() and a.abs().max() > 1e35  # the huge channel reached the outputs
+
+
+def test_backward_refuses_options_changed_since_forward():
+    """unet_backward checks the schedule options against the training forward's
+    (the workspace plan and the saved x3 images depend on x3, convt16, ...): toggling x3
+    between the two raises instead of reading saved activations at shifted offsets."""
+    from _helpers import options
+    from unet_hip._lib import HipError
+    m = hip_model(O.make_params(42), DEV)
+    st = m.flatten_()
+    x, _ = inputs(3, 2, 64, 64)
+    grads = torch.zeros_like(st.param_arena)
+    logits, ws = st.rt.forward(st.param_arena, st.bn_arena, st.nbt_arena, x.to(DEV), training=True)
+    with options(st.rt, x3=0):
+        with pytest.raises(HipError, match="x3"):
+            st.rt.backward(st.param_arena, torch.ones_like(logits), grads, ws)
+    st.rt.backward(st.param_arena, torch.ones_like(logits), grads, ws)  # same options: runs
+    torch.cuda.synchronize()
+    assert torch.isfinite(grads).all()

@@ -370,3 +370,59 @@ def test_res_flop_count_matches_torch_counter():
             MO.make_res_forward(depth)(torch.rand(1, 1, side, side), P, B, True)
         want = 2 * (unet_level_macs(side, side, 1, 1, base, depth) + res_skip_macs(side, side, 1, base, depth))
         assert fc.get_total_flops() == want
+
+
+def test_x3_split_restatement_is_exact_at_the_range_edges():
+    """tests/x3_split_ref.py (the restatement of csrc/x3_split.h): h + m + l == v exactly for
+    normal and huge finite v (|v| >= 0x1.FFp127 would round to inf in bf16: h takes the
+    largest finite bf16 instead), +-inf and NaN keep h = v with m = l = 0, and values with
+    subnormal pieces lose at most 2^-134 (bf16's subnormal quantum is 2^-133)."""
+    import numpy as np
+    import x3_split_ref as X
+    v = X.edge_values()
+    h, m, lo = X.split(v)
+    hf, mf, lf = (X.bf16_to_f32(b).astype(np.float64) for b in (h, m, lo))
+    fin = np.isfinite(v)
+    s = hf + mf + lf
+    exact = fin & (np.abs(v) >= np.ldexp(1.0, -110))
+    assert np.all(s[exact] == v[exact].astype(np.float64))
+    assert np.all(np.abs(s[fin] - v[fin].astype(np.float64)) <= np.ldexp(1.0, -134))
+    assert np.all(np.isfinite(hf[fin])) and np.all(np.isfinite(mf[fin])) and np.all(np.isfinite(lf[fin]))
+    inf = np.isinf(v)
+    assert np.all(hf[inf] == v[inf]) and np.all(m[inf] == 0) and np.all(lo[inf] == 0)
+    nan = np.isnan(v)
+    assert nan.any() and np.all(np.isnan(hf[nan])) and np.all(m[nan] == 0) and np.all(lo[nan] == 0)
+    huge = fin & (np.abs(v) >= X.BF16_OVF)
+    assert huge.sum() >= 6 and np.all(np.abs(hf[huge]) == float(X.BF16_MAX))
+
+
+def test_x3_split_host_hook_matches_restatement():
+    """unet_x3_split_host runs csrc/x3_split.h (the source the device passes use) on the host;
+    its bits equal the NumPy restatement everywhere, the edges included."""
+    import ctypes
+    import numpy as np
+    import x3_split_ref as X
+    from unet_hip import _lib
+    lib = _lib.load()
+    v = np.ascontiguousarray(X.edge_values(1))
+    out = np.zeros(3 * v.size, np.uint16)
+    assert lib.unet_x3_split_host(v.ctypes.data_as(ctypes.c_void_p), v.size,
+                                  out.ctypes.data_as(ctypes.c_void_p)) == 0
+    want = X.to_image(*X.split(v))
+    assert np.array_equal(out, want), np.flatnonzero(out != want)[:8]
+    assert lib.unet_x3_split_host(v.ctypes.data_as(ctypes.c_void_p), 31,
+                                  out.ctypes.data_as(ctypes.c_void_p)) == -1
+
+
+def test_backward_refuses_without_a_training_forward(rt):
+    """the workspace plan depends on the schedule options, so unet_backward checks
+    them against the last training forward's; with no training forward on the context it
+    refuses before touching the device."""
+    import ctypes
+    from unet_hip import _lib
+    from unet_hip.runtime import UNetRuntime
+    fresh = UNetRuntime("cuda:0")
+    d = ctypes.c_void_p(256)
+    rc = fresh.lib.unet_backward(fresh.ctx, d, d, d, d, 1 << 30, 2, 64, 64, None)
+    assert rc == -1
+    assert b"without a training forward" in fresh.lib.unet_last_error(fresh.ctx)

@@ -4,6 +4,7 @@
 // partials, residual close), so every kernel family stores identical results.
 #pragma once
 #include "common.h"
+#include "x3_split.h"
 
 namespace {
 
@@ -332,14 +333,13 @@ __device__ __forceinline__ void row_epilogue(const RowGemmArgs& p, f32x16 (&acc)
 #pragma unroll
                     for (int nt = 0; nt < NT; ++nt) {
                         const float v = acc[mt][nt][r] + bb[nt];
-                        const __bf16 h = (__bf16)v;
-                        const float r1 = v - (float)h;
-                        const __bf16 mm = (__bf16)r1;
+                        uint16_t h, mm, lo;
+                        x3_split(v, X3CvtDev{}, h, mm, lo);
                         const int ch = p.ooff + co_[nt];
-                        __bf16* d = (__bf16*)p.out3 + (ob + coff[nt]) * 3 * (size_t)p.ldo + (ch >> 5) * 96 + (ch & 31);
+                        uint16_t* d = p.out3 + (ob + coff[nt]) * 3 * (size_t)p.ldo + (ch >> 5) * 96 + (ch & 31);
                         d[0] = h;
                         d[32] = mm;
-                        d[64] = (__bf16)(r1 - (float)mm);
+                        d[64] = lo;
                     }
                 } else if (p.out16) {  // bf16 straight into the consumer's operand image (RNE, as k_to_bf16)
 #pragma unroll

@@ -7,8 +7,11 @@
 // last 8, so nothing is left over for normal v).  A product then is the sum of the nine
 // piece products; the six kept here,
 //   Ah*Bh + Ah*Bm + Am*Bh + Ah*Bl + Am*Bm + Al*Bh,
-// drop Am*Bl, Al*Bm, Al*Bl, at most ~2^-25 |a b| together -- below the 2^-24 unit roundoff
-// of one f32 operation.  Each piece product is exact in the MFMA (8 x 8 significand bits)
+// drop Am*Bl, Al*Bm, Al*Bl: with |m| <= 2^-8 |a|, |l| <= 2^-16 |a| they total at most
+// 2^-24 + 2^-24 + 2^-32 ~ 2^-23 |a b| (worst case; the unit roundoff of one f32 operation is
+// 2^-24, and the split accumulators below make the K-long sum ~3x MORE accurate than the f32
+// MFMA kernels' in practice, profiles/r04_x3_probe_splitacc.txt).  Range edges (huge, inf,
+// NaN, subnormal pieces): x3_split.h.  Each piece product is exact in the MFMA (8 x 8 significand bits)
 // and accumulates in f32, so a K-long dot product carries the rounding of an f32
 // accumulation chain, like the f32 MFMA path: this is f32 arithmetic, not a bf16
 // approximation (tests/test_gpu_x3.py holds it to the f32 kernels' own error vs fp64).
@@ -917,20 +920,21 @@ static int wx3_go(const WgradArgs& a, hipStream_t s) {
 
 // exact three-way split of 8 f32 values into their hi / mid / lo bf16 pieces, stored at d,
 // d + 32, d + 64 (one 32-channel group of an x3 row)
+// (x3_split.h: the range edges -- huge, +-inf, NaN -- keep their values)
+typedef uint16_t x3_u16x8 __attribute__((ext_vector_type(8)));
 __device__ __forceinline__ void x3_store8(const float (&v)[8], uint16_t* d) {
-    bf16x8 h, m, l;
+    x3_u16x8 h, m, l;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-        const __bf16 hj = (__bf16)v[j];
-        const float r1 = v[j] - (float)hj;
-        const __bf16 mj = (__bf16)r1;
+        uint16_t hj, mj, lj;
+        x3_split(v[j], X3CvtDev{}, hj, mj, lj);
         h[j] = hj;
         m[j] = mj;
-        l[j] = (__bf16)(r1 - (float)mj);
+        l[j] = lj;
     }
-    *(bf16x8*)d = h;
-    *(bf16x8*)(d + 32) = m;
-    *(bf16x8*)(d + 64) = l;
+    *(x3_u16x8*)d = h;
+    *(x3_u16x8*)(d + 32) = m;
+    *(x3_u16x8*)(d + 64) = l;
 }
 
 // x3 image of op(src) (f32 [P][ld] at channel offset off, C channels; scale / shift: the

@@ -31,6 +31,7 @@
 
 #include "../../include/unet_hip.h"
 #include "kernels_misc.h"
+#include "x3_split.h"
 
 namespace {
 
@@ -261,6 +262,12 @@ struct unet_ctx {
     std::vector<hipEvent_t> ev_pool;
     size_t ev_used = 0;
     Options opt;
+    // the options of the last training forward: the workspace plan and which saved images
+    // exist (x3, convt16, the bf16 kernels, ...) depend on them, so unet_backward refuses to
+    // run under different ones (it would read saved activations at shifted offsets, or an
+    // up half the forward never wrote)
+    Options fwd_opt;
+    bool fwd_opt_set = false;
 
     int nconv() const { return (int)conv.size(); }
     int chl[MAX_DEPTH + 1] = {};                           // kernel (padded) channels per level
@@ -2263,6 +2270,10 @@ int unet_forward(unet_ctx* c, const float* params, float* bn_running, int64_t* b
     make_plan(c, N, H, W, training != 0, (char*)ws, p);
     if (hipSetDevice(c->device) != hipSuccess) return fail(c, UNET_ERR_HIP, "hipSetDevice");
     if (!c->timing) c->ev_used = 0;
+    if (training) {
+        c->fwd_opt = c->opt;
+        c->fwd_opt_set = true;
+    }
     const hipStream_t s = (hipStream_t)stream;
     if (!c->padded)
         return forward_impl(c, params, bn_running, bn_count, x, logits, p, training != 0, s);
@@ -2287,6 +2298,13 @@ int unet_backward(unet_ctx* c, const float* params, const float* dlogits, float*
     ABI_TRY
     if (!c || !params || !dlogits || !grads || !ws) return c ? fail(c, UNET_ERR_INVALID, "null pointer") : UNET_ERR_INVALID;
     if (!shape_ok(c, N, H, W)) return fail(c, UNET_ERR_SHAPE, "bad shape N=%d H=%d W=%d", N, H, W);
+    if (!c->fwd_opt_set) return fail(c, UNET_ERR_INVALID, "backward without a training forward");
+    for (const OptionDesc& d : OPTION_TABLE)
+        if (c->opt.*d.field != c->fwd_opt.*d.field)
+            return fail(c, UNET_ERR_INVALID,
+                        "option '%s' changed between the training forward (%d) and its backward "
+                        "(%d): the workspace plan depends on it",
+                        d.name, c->fwd_opt.*d.field, c->opt.*d.field);
     Plan p;
     make_plan(c, N, H, W, true, nullptr, p);
     if (ws_bytes < p.bytes) return fail(c, UNET_ERR_WORKSPACE, "workspace %zu < %zu", ws_bytes, p.bytes);
@@ -2365,6 +2383,24 @@ int unet_adamw(unet_ctx* c, float* params, const float* grads, float* m, float* 
     a.gscale = (float)gscale;
     int r = k_adamw(params, grads, m, v, n, a, (hipStream_t)stream);
     return r ? fail(c, UNET_ERR_HIP, "adamw launch %d", r) : UNET_OK;
+    ABI_CATCH(c)
+}
+
+int unet_x3_split_host(const float* v, int64_t n, uint16_t* out) {
+    if (!v || !out || n < 0 || n % 32) return UNET_ERR_INVALID;
+    for (int64_t i = 0; i < n; ++i) {
+        const int64_t r = i / 32, j = i % 32;
+        x3_split(v[i], X3CvtHost{}, out[96 * r + j], out[96 * r + 32 + j], out[96 * r + 64 + j]);
+    }
+    return UNET_OK;
+}
+
+int unet_x3_split_device(unet_ctx* c, const float* v, int64_t n, uint16_t* out, unet_stream_t stream) {
+    ABI_TRY
+    if (!c || !v || !out || n < 32 || n % 32) return c ? fail(c, UNET_ERR_INVALID, "x3 split: n") : UNET_ERR_INVALID;
+    if (hipSetDevice(c->device) != hipSuccess) return fail(c, UNET_ERR_HIP, "hipSetDevice");
+    const int r = k_to_x3(v, 32, 0, 32, nullptr, nullptr, 0, n / 32, out, 32, 0, (hipStream_t)stream);
+    return r ? fail(c, UNET_ERR_HIP, "to_x3 launch %d", r) : UNET_OK;
     ABI_CATCH(c)
 }
 
@@ -2554,6 +2590,10 @@ int unet_debug_view(unet_ctx* c, int N, int H, int W, int training, int kind, in
             q = p.dcat[index];
             n = p.P[index] * 2 * C;
             l = 2 * C;
+        } else if (kind == 8) {  // max-pool winner index (uint8, window position 0..3)
+            q = p.idx[index];
+            n = p.P[index + 1] * C;
+            l = C;
         } else {
             return UNET_ERR_INVALID;
         }

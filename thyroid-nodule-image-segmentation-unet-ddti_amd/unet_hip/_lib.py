@@ -87,6 +87,8 @@ SIGNATURES = {
     "unet_resize_plan": (c_int, [c_int, c_int, c_void_p, c_void_p, P(c_int)]),
     "unet_resize_u8": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p,
                                c_void_p, c_int, c_void_p, c_void_p, c_int, c_float, c_void_p]),
+    "unet_x3_split_host": (c_int, [c_void_p, c_int64, c_void_p]),
+    "unet_x3_split_device": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
     "unet_timing_enable": (c_int, [c_void_p, c_int]),
     "unet_timing_filter": (c_int, [c_void_p, c_char_p]),
     "unet_timing_reset": (c_int, [c_void_p]),

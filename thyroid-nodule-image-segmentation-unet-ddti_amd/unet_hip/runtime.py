@@ -198,6 +198,8 @@ class UNetRuntime:
         _lib.check(self.lib.unet_debug_view(self.ctx, N, H, W, int(training), kind, index,
                                             ctypes.byref(bo), ctypes.byref(cnt), ctypes.byref(ld),
                                             ctypes.byref(off)), self.ctx, "unet_debug_view")
+        if kind == 8:  # uint8 max-pool winner index
+            return workspace[bo.value:bo.value + cnt.value].view(-1, ld.value), off.value
         flat = workspace[bo.value:bo.value + 4 * cnt.value].view(torch.float32)
         if kind in (1, 2, 3, 4):
             return flat
