@@ -113,6 +113,30 @@ def launch(n, argv):
                               start_new_session=True)
              for e in rank_envs(n, _free_port())]
     status = 0
+    live = list(procs)
+
+    def stop_ranks(signum, frame):
+        # the ranks run in sessions of their own, so a SIGTERM / SIGHUP to this launcher (a
+        # scheduler's timeout) would not reach them: they would keep their GPUs and wait in a
+        # collective.  Forward it to every rank's process group, give them a moment, exit.
+        for q in live:
+            try:
+                os.killpg(q.pid, signal.SIGTERM)
+            except ProcessLookupError:
+                pass
+        deadline = time.time() + 10
+        for q in live:
+            try:
+                q.wait(timeout=max(0.1, deadline - time.time()))
+            except subprocess.TimeoutExpired:
+                try:
+                    os.killpg(q.pid, signal.SIGKILL)
+                except ProcessLookupError:
+                    pass
+        sys.exit(128 + signum)
+
+    signal.signal(signal.SIGTERM, stop_ranks)
+    signal.signal(signal.SIGHUP, stop_ranks)
     try:
         while procs:
             for p in list(procs):
@@ -120,6 +144,7 @@ def launch(n, argv):
                 if rc is None:
                     continue
                 procs.remove(p)
+                live.remove(p)
                 if rc != 0 and status == 0:
                     status = rc if rc > 0 else 128 - rc
                     print(f"bench.py: rank process {p.pid} exited with {rc}; stopping the "
@@ -254,7 +279,7 @@ def main():
         raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started {world} "
                          f"ranks (WORLD_SIZE); n_gpus must equal the rank count")
     if args.dry_run:
-        print(json.dumps({"dry_run": True, "argv": sys.argv[1:],
+        print(json.dumps({"dry_run": True, "argv": sys.argv[1:], "pid": os.getpid(),
                           **{k: os.environ.get(k) for k in _RANK_ENV}}), flush=True)
         fail = os.environ.get("BENCH_DRY_RUN_FAIL_RANK")  # launcher test: one rank fails,
         if fail is not None:                              # the others wait as if in a collective
@@ -396,8 +421,26 @@ def main():
                  res_train_flops_per_image(S, S, args.base, args.depth) if cres else
                  train_flops_per_image(S, S)) * B
     bf16 = c4 and args.mfma == "bf16"
-    x3 = dom.startswith("x3") or dom.startswith("wx3")
-    peak = BF16_MFMA_PEAK_TFLOPS if bf16 else X3_MFMA_PEAK_TFLOPS if x3 else FP32_MFMA_PEAK_TFLOPS
+
+    def kpeak(k):
+        """MFMA peak of one kernel instance's arithmetic: x3 kernels (exact 3-way splits on
+        the bf16 matrix cores) bf16 / 6; the bf16 network's GEMMs bf16; the rest f32 MFMA."""
+        if k.startswith("x3") or k.startswith("wx3"):
+            return X3_MFMA_PEAK_TFLOPS
+        return BF16_MFMA_PEAK_TFLOPS if bf16 else FP32_MFMA_PEAK_TFLOPS
+    x3 = kpeak(dom) == X3_MFMA_PEAK_TFLOPS
+    peak = kpeak(dom)
+    # the step's conv work runs on several kernel families with different peaks (ResUNet's
+    # 32-channel levels and 1x1 skips stay on f32 MFMA beside the x3 GEMMs): price the step
+    # against the FLOP-weighted peak of the families that ran it (profiling step's FLOPs)
+    fam_flop = {}
+    for k, (_, _, fl) in kern.items():
+        if fl > 0:
+            fam_flop[kpeak(k)] = fam_flop.get(kpeak(k), 0.0) + fl
+    tot_flop = sum(fam_flop.values())
+    step_peak = tot_flop / sum(fl / pk for pk, fl in fam_flop.items()) if tot_flop else peak
+    names = {X3_MFMA_PEAK_TFLOPS: "x3", BF16_MFMA_PEAK_TFLOPS: "bf16", FP32_MFMA_PEAK_TFLOPS: "f32_mfma"}
+    peak_mix = {names[pk]: round(fl / tot_flop, 4) for pk, fl in sorted(fam_flop.items())} if tot_flop else {}
     roofline = {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 3),
                 "peak": peak, "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4),
@@ -405,7 +448,9 @@ def main():
                 "flop_per_launch": per_launch_flop,
                 "kernel_share_of_gpu_time": round(kern[dom][1] / max(1e-9, sum(v[1] for v in kern.values())), 4),
                 "step_conv_tflops": round(conv_flop / (ms * 1e-3) / 1e12, 3),
-                "step_conv_frac": round(conv_flop / (ms * 1e-3) / 1e12 / peak, 4)}
+                "step_conv_frac": round(conv_flop / (ms * 1e-3) / 1e12 / step_peak, 4),
+                "step_peak_tflops": round(step_peak, 2),
+                "step_flop_share_by_arith": peak_mix}
     if x3:
         roofline["peak_note"] = ("f32 GEMM on bf16 MFMA through exact 3-way operand splits: 6 bf16 "
                                  "products per f32 product, so the peak is the bf16 dense peak / 6")

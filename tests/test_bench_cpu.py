@@ -68,3 +68,31 @@ def test_rank_envs():
     envs = bench.rank_envs(2, 12345, base={"X": "1"})
     assert [e["RANK"] for e in envs] == ["0", "1"]
     assert all(e["X"] == "1" and e["MASTER_PORT"] == "12345" for e in envs)
+
+
+def test_launcher_forwards_sigterm_to_ranks():
+    """the ranks run in sessions of their own, so a SIGTERM to the launcher (a
+    scheduler's timeout) must be forwarded to them, or they keep their GPUs and wait in a
+    collective.  Every dry-run rank sleeps (no rank fails); SIGTERM the launcher: it exits
+    128 + 15 and no rank survives it."""
+    import signal
+    p = subprocess.Popen([sys.executable, BENCH, "--gpus", "3", "--dry-run"],
+                         env=_clean_env(BENCH_DRY_RUN_FAIL_RANK="99"), stdout=subprocess.PIPE,
+                         stderr=subprocess.PIPE, text=True)
+    pids = []
+    t0 = time.time()
+    while len(pids) < 3 and time.time() - t0 < 30:
+        line = p.stdout.readline()
+        if line.startswith("{"):
+            pids.append(json.loads(line)["pid"])
+    assert len(pids) == 3
+    p.send_signal(signal.SIGTERM)
+    assert p.wait(timeout=30) == 128 + signal.SIGTERM
+    time.sleep(0.5)
+    for pid in pids:
+        try:
+            os.kill(pid, 0)
+            alive = True
+        except ProcessLookupError:
+            alive = False
+        assert not alive, pid

@@ -181,6 +181,31 @@ def test_x3_row_tile_choice_bit_identical(B, H, W):
         assert torch.equal(outs[0][1], outs[i][1]), (i, (outs[0][1] - outs[i][1]).abs().max().item())
 
 
+@pytest.mark.parametrize("B,H,W", [(2, 128, 128), (1, 256, 256)])
+def test_x3_halo_schedules_bit_identical(B, H, W):
+    """The halo GEMM's wave schedules (option x3_r3_sched, kernels_gemm_x3.hip X3R3Sched: which
+    waves issue the LDS-DMA, the stagger of waves 4..7, where the DMA goes in the sub-step) run
+    the same MFMAs in the same order per accumulator: one training step -- logits and the whole
+    gradient arena -- is bit-identical across all five.  128x128 covers W = 128 .. 16; 256x256 the
+    level-0 256x64 tile at W = 256."""
+    import unet_hip
+    from _helpers import options
+    x, t = inputs(31, B, H, W)
+    outs = []
+    for sched in range(5):
+        m = hip_model(O.make_params(42), DEV)
+        with options(m.flatten_().rt, x3_r3_sched=sched):
+            logits = m(x.to(DEV))
+            l = unet_hip.seg_losses(logits, t.to(DEV))
+            (l[0] + l[1]).backward()
+            torch.cuda.synchronize()
+        outs.append((logits.detach().clone(), m._state.grad_arena.clone()))
+        del m
+    for i in range(1, len(outs)):
+        assert torch.equal(outs[0][0], outs[i][0]), i
+        assert torch.equal(outs[0][1], outs[i][1]), (i, (outs[0][1] - outs[i][1]).abs().max().item())
+
+
 def test_x3_tap_row_wgrad_matches_one_tap():
     """The tap-row x3 weight gradient (wgrad_x3_row3_kernel: three dx taps from one 34-pixel
     halo, default on rows of 32k pixels) against the one-tap x3 kernel (option x3_wtile = 1

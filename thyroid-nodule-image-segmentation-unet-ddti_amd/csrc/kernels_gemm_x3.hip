@@ -100,7 +100,6 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_x3_kernel(RowGemmA
     constexpr int AI = (BM * RB + 1024 * WAVES - 1) / (1024 * WAVES);
     constexpr int BI = (BN * RB + 1024 * WAVES - 1) / (1024 * WAVES);
     constexpr int AREG = AI * WAVES * 1024;  // bytes of the A region of a stage
-    constexpr int GPC = AI + BI;
     constexpr int DIST = S - 1;
     static_assert(DIST >= 1 && DIST <= 3, "stages");
     constexpr int STAGE = AREG + BI * WAVES * 1024;
@@ -290,94 +289,99 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_x3_kernel(RowGemmA
 //   K order: dy, channel group, dx, k -- a reordering of the one-tap kernel's sum, so results
 //   agree with the other tiles to f32 rounding, not bitwise.
 // ------------------------------------------------------------------------------------
-// BN = 128 (8 waves of 64 x 64) or 64 (8 waves of 64 x 32, B pieces padded to 2 per wave);
-// WM / WN: other wave tiles (4 waves of 128 x 64 / 64 x 128 per 256 x 128 block: one wave per
-// SIMD with twice the MFMAs per fragment read; A/B options)
-template <int EMODE, int BN = 128, int WM = 64, int WN = BN / 2>
-__global__ __launch_bounds__((256 / WM) * (BN / WN) * 64, 1) void rowgemm_x3_row3_kernel(RowGemmArgs p) {
-    constexpr int BM = 256, BK = 32, WAVES_N = BN / WN, WAVES = (BM / WM) * WAVES_N;
+// BN = 128 (8 waves of 64 x 64) or 64 (8 waves of 64 x 32, B pieces padded to 2 per wave).
+//
+// Schedule (r05, tools/x3_halo_exp.hip, profiles/r05_halo_sched.txt).  The eight waves pair up on
+// the four SIMDs (wave w and w + 4), and when both run the same program they reach the barrier,
+// the DMA issue (100-185 cycles per LDS-DMA piece inside a busy phase, MI355X_MICROARCH.md) and
+// the post-barrier fragment reads together, leaving the matrix pipe idle.  Template SCHED:
+//   LW   waves that issue the LDS-DMA: 8 (all, each its share) or 4 (waves 0..3 issue twice as
+//        many pieces; waves 4..7 never stall on a DMA issue)
+//   LAG  waves 4..7 run each sub-step's second k-step MFMAs after the next barrier, from
+//        fragments they read before it (held in registers): their pipe work starts while
+//        their partner waits for its first fragments
+//   LATE the DMA of the next sub-step is issued after the first k-step's fragment reads
+// The next group's halo is spread over the current group's three sub-steps (AC pieces each).
+// Every schedule runs the same MFMAs in the same order per accumulator: bit-identical.
+template <int BN, int LW, bool ISSUER, bool LAG, bool LATE>
+__device__ __forceinline__ void x3r3_body(const RowGemmArgs& p, char* smem, int wave, int lane,
+                                          f32x16 (&acc)[2][BN / 64], f32x16 (&acl)[2][BN / 64],
+                                          int m0, int n0) {
+    constexpr int BM = 256, BK = 32, WM = 64, WN = BN / 2, WAVES_N = 2, WAVES = 8;
     constexpr int MT = WM / 32, NT = WN / 32;
-    constexpr int RB = 192;
-    constexpr int AR = 288;                                   // halo rows (W = 16: 16 x 18)
-    constexpr int AI = (AR * RB + 1024 * WAVES - 1) / (1024 * WAVES);  // 7 A pieces per wave
-    constexpr int BI = (BN * RB + 1024 * WAVES - 1) / (1024 * WAVES);  // 3 / 2 B pieces per wave
-    constexpr int AREG = AI * WAVES * 1024, BREG = BI * WAVES * 1024;  // 56 KB, 24 / 16 KB
-    constexpr int SMEM = 2 * AREG + 2 * BREG;                 // 160 KB
-    static_assert(SMEM >= 2 * (BM / 64) * BN * 8, "epilogue scratch");
-    __shared__ __attribute__((aligned(1024))) char smem[SMEM];
+    constexpr int RB = 192, AR = 288;
+    constexpr int AREG = ((AR * RB + 1024 * WAVES - 1) / (1024 * WAVES)) * WAVES * 1024;  // 56 KB
+    constexpr int BREG = ((BN * RB + 1024 * WAVES - 1) / (1024 * WAVES)) * WAVES * 1024;  // 24 / 16 KB
+    constexpr int AI = AREG / (1024 * LW), BI = BREG / (1024 * LW);  // pieces per issuing wave
+    constexpr int AC = (AI + 2) / 3;                                  // halo pieces per sub-step
     auto swz = [](int r) { return (r >> 2) & 3; };
-
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave / WAVES_N, wn = wave % WAVES_N;
-    const int ntn = p.N / BN;
-    const int bid = p.xcd ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
-    const int tile_m = bid / ntn, tile_n = bid - tile_m * ntn;
-    const int m0 = tile_m * BM, n0 = tile_n * BN;
     const int H = p.H, W = p.W, C = p.C, K = p.K;
     const int SEG = W < BM ? W : BM, HW = SEG + 2;
     const int AROWS = (BM / SEG) * HW;
     const size_t rowa = 3 * (size_t)p.lda, rowb = 3 * (size_t)K;
-
-    // A loader: lane of piece j fills halo bytes (j WAVES + wave) KB + 16 lane: halo row h,
-    // 16-B slot w / 16 of its 192 B; pixel of h at dy = 1 (-1: padding column / past the halo)
-    int acen[AI], ayr[AI], ace[AI];
+    // A loader: lane of piece j fills halo bytes (j LW + wave) KB + 16 lane: halo row h, 16-B
+    // slot w / 16 of its 192 B; pixel of h at dy = 1 (-1: padding column / past the halo)
+    int acen[ISSUER ? AI : 1], ayr[ISSUER ? AI : 1], ace[ISSUER ? AI : 1];
+    const uint16_t* bsrc[ISSUER ? BI : 1];
+    bool bok[ISSUER ? BI : 1];
+    if constexpr (ISSUER) {
 #pragma unroll
-    for (int j = 0; j < AI; ++j) {
-        const int o = ((j * WAVES + wave) * 64 + lane) * 16;
-        const int h = o / RB, w = o - h * RB;
-        const int r = h / HW, xl = h - r * HW - 1;
-        const int mrow = m0 + r * SEG;
-        bool ok = h < AROWS && mrow < p.M;
-        const Pix q = decode(ok ? mrow : 0, H, W);
-        ok = ok && q.x + xl >= 0 && q.x + xl < W;
-        acen[j] = ok ? mrow + xl : -1;
-        ayr[j] = q.y;
-        ace[j] = (w >> 6) * 32 + ((((w >> 4) & 3) ^ swz(h)) << 3);
-    }
-    const uint16_t* bsrc[BI];
-    bool bok[BI];
+        for (int j = 0; j < AI; ++j) {
+            const int o = ((j * LW + wave) * 64 + lane) * 16;
+            const int h = o / RB, w = o - h * RB;
+            const int r = h / HW, xl = h - r * HW - 1;
+            const int mrow = m0 + r * SEG;
+            bool ok = h < AROWS && mrow < p.M;
+            const Pix q = decode(ok ? mrow : 0, H, W);
+            ok = ok && q.x + xl >= 0 && q.x + xl < W;
+            acen[j] = ok ? mrow + xl : -1;
+            ayr[j] = q.y;
+            ace[j] = (w >> 6) * 32 + ((((w >> 4) & 3) ^ swz(h)) << 3);
+        }
 #pragma unroll
-    for (int j = 0; j < BI; ++j) {
-        const int o = ((j * WAVES + wave) * 64 + lane) * 16;
-        const int r = o / RB, w = o - r * RB;
-        bok[j] = r < BN;
-        bsrc[j] = p.bt16 + (size_t)(n0 + (bok[j] ? r : 0)) * rowb + (w >> 6) * 32 +
-                  ((((w >> 4) & 3) ^ swz(r)) << 3);
+        for (int j = 0; j < BI; ++j) {
+            const int o = ((j * LW + wave) * 64 + lane) * 16;
+            const int r = o / RB, w = o - r * RB;
+            bok[j] = r < BN;
+            bsrc[j] = p.bt16 + (size_t)(n0 + (bok[j] ? r : 0)) * rowb + (w >> 6) * 32 +
+                      ((((w >> 4) & 3) ^ swz(r)) << 3);
+        }
     }
     const uint16_t* zero = (const uint16_t*)p.zero16;
     const uint16_t* a16 = p.a16 + (size_t)p.aoff * 3;
     const int CC = C / BK;  // channel groups per tap
-    // sub-step s = (dy, group, dx): halo of group g = s / 3 (dy = g / CC), B of tap dy * 3 + dx
-    auto issue_a = [&](int g) {
+    const int NG = 3 * CC;  // halo groups (dy, channel group)
+    const int ns = 9 * CC;  // sub-steps (dy, channel group, dx)
+    // halo pieces [j0, j1) of group g into buffer g & 1
+    auto issue_a = [&](int g, int j0, int j1) {
         const int dy = g / CC, c0 = (g - dy * CC) * BK;
         char* base = smem + (g & 1) * AREG;
 #pragma unroll
         for (int j = 0; j < AI; ++j) {
+            if (j < j0 || j >= j1) continue;
             const int yy = ayr[j] + dy - 1;
             const bool valid = acen[j] >= 0 && yy >= 0 && yy < H;
             const uint16_t* src =
                 valid ? a16 + (size_t)(acen[j] + (dy - 1) * W) * rowa + c0 * 3 + ace[j] : zero;
-            x3_dma16(src, base + (j * WAVES + wave) * 1024);
+            x3_dma16(src, base + (j * LW + wave) * 1024);
         }
     };
-    auto issue_b = [&](int s) {
+    auto issue_b = [&](int s) {  // B rows of tap dy * 3 + dx, channel group, into slot s & 1
         const int g = s / 3, dx = s - g * 3;
         const int dy = g / CC, c0 = (g - dy * CC) * BK;
         const int k0 = (dy * 3 + dx) * C + c0;
         char* base = smem + 2 * AREG + (s & 1) * BREG;
 #pragma unroll
-        for (int j = 0; j < BI; ++j)
-            x3_dma16(bok[j] ? bsrc[j] + k0 * 3 : zero, base + (j * WAVES + wave) * 1024);
+        for (int j = 0; j < BI; ++j) x3_dma16(bok[j] ? bsrc[j] + k0 * 3 : zero, base + (j * LW + wave) * 1024);
     };
-
-    f32x16 acc[MT][NT], acl[MT][NT];
-#pragma unroll
-    for (int i = 0; i < MT; ++i)
-#pragma unroll
-        for (int j = 0; j < NT; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = acl[i][j][r] = 0.f;
+    // during sub-step s: B(s + 1), then the halo pieces [dx AC, (dx + 1) AC) of group g + 1 into
+    // the buffer group g - 1 read (free since the barrier that opened group g)
+    auto issue = [&](int s) {
+        const int g = s / 3, dx = s - g * 3;
+        if (s + 1 < ns) issue_b(s + 1);
+        if (g + 1 < NG) issue_a(g + 1, dx * AC, dx * AC + AC);
+    };
     const int lh = lane >> 5, li = lane & 31;
     int ahb[MT], bro[NT], bfx[NT];  // halo row of output pixel at dx = 0; B row offsets
 #pragma unroll
@@ -392,25 +396,31 @@ __global__ __launch_bounds__((256 / WM) * (BN / WN) * 64, 1) void rowgemm_x3_row
         bro[nt] = r * RB;
         bfx[nt] = swz(r);
     }
-
-    const int ns = 9 * CC;  // sub-steps
-    issue_a(0);
-    issue_b(0);
+    bf16x8 ha[MT][3], hb[NT][3];  // LAG: the previous sub-step's second k-step fragments
+    if constexpr (ISSUER) {
+        issue_a(0, 0, AI);
+        issue_b(0);
+    }
     for (int s = 0; s < ns; ++s) {
         const int g = s / 3, dx = s - g * 3;
-        const bool nb = s + 1 < ns, na = dx == 0 && g + 1 < 3 * CC;
-        const bool pa = dx == 1 && g + 1 < 3 * CC;  // s - 1 issued the next halo after B(s)
-        // one barrier per sub-step: wait for B(s) (in flight after it: the next halo when
-        // s - 1 issued it), barrier -- every wave's DMA has landed and every wave has finished
-        // reading sub-step s - 1 -- then issue B(s + 1) into s - 1's slot and, entering a
-        // group, the next halo into the previous group's buffer.  (r04: issuing before the
-        // wait and closing each sub-step with a second barrier gave the same bits at 2-3 %
-        // lower TF/s, profiles/r04_x3_halo_ab.txt.)
-        if (pa) x3_wait_vm<AI>();
-        else x3_wait_vm<0>();
+        // one barrier per sub-step: the issuing waves wait for B(s) and, entering a group, the
+        // last halo pieces of g (the pieces of g + 1 issued during s - 1, younger than B(s), may
+        // stay in flight); the barrier then also means every wave finished reading s - 1, so
+        // slot (s + 1) & 1 and halo buffer (g + 1) & 1 are free
+        if constexpr (ISSUER) {
+            if (dx >= 1 && g + 1 < NG) x3_wait_vm<AC>();
+            else x3_wait_vm<0>();
+        }
         x3_barrier();
-        if (nb) issue_b(s + 1);
-        if (na) issue_a(g + 1);
+        if constexpr (ISSUER && !LATE) issue(s);
+        if constexpr (LAG) {
+            if (s > 0) {
+#pragma unroll
+                for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                    for (int nt = 0; nt < NT; ++nt) mfma_x3s(ha[mt], hb[nt], acc[mt][nt], acl[mt][nt]);
+            }
+        }
         const char* abase = smem + (g & 1) * AREG;
         const char* bbase = smem + 2 * AREG + (s & 1) * BREG;
 #pragma unroll
@@ -429,13 +439,70 @@ __global__ __launch_bounds__((256 / WM) * (BN / WN) * 64, 1) void rowgemm_x3_row
 #pragma unroll
                 for (int q = 0; q < 3; ++q)
                     bfr[nt][q] = *(const bf16x8*)(bbase + bro[nt] + q * 64 + ((c ^ bfx[nt]) << 4));
+            if constexpr (ISSUER && LATE) {
+                if (kk == 0) issue(s);
+            }
+            if (LAG && kk == 1) {
 #pragma unroll
-            for (int mt = 0; mt < MT; ++mt)
+                for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-                for (int nt = 0; nt < NT; ++nt) mfma_x3s(af[mt], bfr[nt], acc[mt][nt], acl[mt][nt]);
+                    for (int q = 0; q < 3; ++q) ha[mt][q] = af[mt][q];
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+                    for (int q = 0; q < 3; ++q) hb[nt][q] = bfr[nt][q];
+            } else {
+#pragma unroll
+                for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                    for (int nt = 0; nt < NT; ++nt) mfma_x3s(af[mt], bfr[nt], acc[mt][nt], acl[mt][nt]);
+            }
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
+    if constexpr (LAG) {
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) mfma_x3s(ha[mt], hb[nt], acc[mt][nt], acl[mt][nt]);
+    }
+}
+
+// SCHED: 0 = every wave issues its share, no stagger (r04); 1 = + stagger + late DMA;
+// 2 = loader waves 0..3 + stagger; 3 = loader waves + stagger + late DMA; 4 = loader waves only
+template <int SCHED>
+struct X3R3Sched {
+    static constexpr int LW = SCHED >= 2 ? 4 : 8;
+    static constexpr bool LAG = SCHED >= 1 && SCHED <= 3;
+    static constexpr bool LATE = SCHED == 1 || SCHED == 3;
+};
+
+template <int EMODE, int BN = 128, int SCHED = 0>
+__global__ __launch_bounds__(512, 1) void rowgemm_x3_row3_kernel(RowGemmArgs p) {
+    constexpr int BM = 256, WM = 64, WN = BN / 2, MT = 2, NT = WN / 32;
+    constexpr int RB = 192, AR = 288;
+    constexpr int SMEM = 2 * ((AR * RB + 8191) / 8192) * 8192 + 2 * ((BN * RB + 8191) / 8192) * 8192;  // 160 KB
+    static_assert(SMEM >= 2 * (BM / 64) * BN * 8, "epilogue scratch");
+    __shared__ __attribute__((aligned(1024))) char smem[SMEM];
+    using SC = X3R3Sched<SCHED>;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave / 2, wn = wave % 2;
+    const int ntn = p.N / BN;
+    const int bid = p.xcd ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+    const int tile_m = bid / ntn, tile_n = bid - tile_m * ntn;
+    const int m0 = tile_m * BM, n0 = tile_n * BN;
+    f32x16 acc[MT][NT], acl[MT][NT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = acl[i][j][r] = 0.f;
+    if (wave >= 4)
+        x3r3_body<BN, SC::LW, SC::LW == 8, SC::LAG, SC::LATE>(p, smem, wave, lane, acc, acl, m0, n0);
+    else
+        x3r3_body<BN, SC::LW, true, false, SC::LATE>(p, smem, wave, lane, acc, acl, m0, n0);
     x3_barrier();  // the epilogue reuses the stage memory
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
@@ -444,15 +511,20 @@ __global__ __launch_bounds__((256 / WM) * (BN / WN) * 64, 1) void rowgemm_x3_row
     row_epilogue<EMODE, BM, BN, WM, WN, true>(p, acc, m0, n0, tile_m, wm, wn, lane, tid, (float*)smem);
 }
 
-template <int EMODE, int BN, int WM = 64, int WN = BN / 2>
-static int x3r3_go(const RowGemmArgs& a, hipStream_t s) {
+template <int EMODE, int BN>
+static int x3r3_go(const RowGemmArgs& a, int sched, hipStream_t s) {
     // BM % W == 0 or W % BM == 0 keeps a tile on whole rows / row segments; W >= 16 bounds the halo
     if (a.amode != G_CONV3 || a.N % BN || a.C % 32 || a.K != 9 * a.C) return -1;
     if (a.W < 16 || (256 % a.W && a.W % 256)) return -1;
     const dim3 grid(((a.M + 255) / 256) * (a.N / BN));
-    constexpr int threads = (256 / WM) * (BN / WN) * 64;
-    hipLaunchKernelGGL((rowgemm_x3_row3_kernel<EMODE, BN, WM, WN>), grid, dim3(threads), 0, s, a);
-    return (int)hipGetLastError();
+#define X3R3_SCHED(v)                                                                          \
+    if (sched == v) {                                                                         \
+        hipLaunchKernelGGL((rowgemm_x3_row3_kernel<EMODE, BN, v>), grid, dim3(512), 0, s, a); \
+        return (int)hipGetLastError();                                                        \
+    }
+    X3R3_SCHED(0) X3R3_SCHED(1) X3R3_SCHED(2) X3R3_SCHED(3) X3R3_SCHED(4)
+#undef X3R3_SCHED
+    return -1;
 }
 
 // tiles (split accumulators; probe: profiles/r04_x3_probe_*.txt): 0 = 256x128 (8 waves of
@@ -475,7 +547,7 @@ static int x3_go(const RowGemmArgs& a, hipStream_t s) {
 }
 
 template <int AMODE, int EMODE>
-static int x3_tile(const RowGemmArgs& a, int tile, hipStream_t s) {
+static int x3_tile(const RowGemmArgs& a, int tile, hipStream_t s, int sched = 0) {
     if (tile == 4 || tile == 5) {  // tap-row halo kernel (3x3 convs): 256 x 128 / 256 x 64
         // (r04, not kept: 4-wave 128x64 / 64x128 wave tiles, within noise of 8 waves; B
         // straight from global memory into registers instead of the LDS ring, one barrier per
@@ -483,7 +555,7 @@ static int x3_tile(const RowGemmArgs& a, int tile, hipStream_t s) {
         // the ring's barriers; 256 x 64 as 4 waves of 64 x 64, bit-identical, 589 -> 584 img/s;
         // 256 x 64 with a three-slot B ring, B two sub-steps ahead: bit-identical, no gain)
         if constexpr (AMODE == G_CONV3)
-            return tile == 4 ? x3r3_go<EMODE, 128>(a, s) : x3r3_go<EMODE, 64>(a, s);
+            return tile == 4 ? x3r3_go<EMODE, 128>(a, sched, s) : x3r3_go<EMODE, 64>(a, sched, s);
         return -1;
     }
 #define X3_CASE(id, T) \
@@ -1091,17 +1163,17 @@ int rowgemm_x3_tile_dims(int tile, int* bm, int* bn) {
 }
 
 // A: x3 image (a16, lda channels per row, channel offset aoff), Bt: x3 weights [N][K]
-int launch_rowgemm_x3(const RowGemmArgs& a, int tile, hipStream_t s) {
+int launch_rowgemm_x3(const RowGemmArgs& a, int tile, hipStream_t s, int sched) {
     if (!a.a16 || !a.bt16 || !a.zero16 || a.M < 1 || a.K != gather_taps(a.amode) * a.C) return -1;
     if (a.aoff % 32 || a.lda % 32) return -1;
     if ((a.emode == E_STORE_BN || a.emode == E_RESID) != (a.ey != nullptr)) return -1;
     if (a.ascale || a.acoef) return -1;  // the x3 image already holds op(A)
     if (a.amode == G_CONV3) {
-        if (a.emode == E_BIAS_RELU_STATS) return x3_tile<G_CONV3, E_BIAS_RELU_STATS>(a, tile, s);
-        if (a.emode == E_STATS) return x3_tile<G_CONV3, E_STATS>(a, tile, s);
-        if (a.emode == E_STORE) return x3_tile<G_CONV3, E_STORE>(a, tile, s);
-        if (a.emode == E_STORE_BN) return x3_tile<G_CONV3, E_STORE_BN>(a, tile, s);
-        if (a.emode == E_ADD) return x3_tile<G_CONV3, E_ADD>(a, tile, s);
+        if (a.emode == E_BIAS_RELU_STATS) return x3_tile<G_CONV3, E_BIAS_RELU_STATS>(a, tile, s, sched);
+        if (a.emode == E_STATS) return x3_tile<G_CONV3, E_STATS>(a, tile, s, sched);
+        if (a.emode == E_STORE) return x3_tile<G_CONV3, E_STORE>(a, tile, s, sched);
+        if (a.emode == E_STORE_BN) return x3_tile<G_CONV3, E_STORE_BN>(a, tile, s, sched);
+        if (a.emode == E_ADD) return x3_tile<G_CONV3, E_ADD>(a, tile, s, sched);
     }
     if (a.amode == G_UP2) {
         if (a.emode == E_STORE_BN) return x3_tile<G_UP2, E_STORE_BN>(a, tile, s);

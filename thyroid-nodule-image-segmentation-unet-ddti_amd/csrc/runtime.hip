@@ -163,6 +163,8 @@ struct Options {
     int x3_wblocks = 1536;     // split-K target (blocks) of its 128x128 weight gradients
     int x3_n64 = 2;            // its row-GEMM tile for 64 outputs (2 = 128x64, 3 = 256x64)
     int x3_r3 = 1;             // its 256x128 3x3 GEMMs on the tap-row halo kernel (tile 4)
+    int x3_r3_sched = 0;       // the halo kernel's wave schedule (kernels_gemm_x3.hip X3R3Sched:
+                               // who issues the LDS-DMA, stagger of waves 4..7; bit-identical)
 };
 struct OptionDesc {
     const char* name;
@@ -212,6 +214,7 @@ const OptionDesc OPTION_TABLE[] = {
     {"x3_wblocks", &Options::x3_wblocks},
     {"x3_n64", &Options::x3_n64},
     {"x3_r3", &Options::x3_r3},
+    {"x3_r3_sched", &Options::x3_r3_sched},
 };
 
 }  // namespace
@@ -1299,7 +1302,7 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
                 use_x3(p, g, img, C.cin, p.pack3 + 3 * C.pf);
                 const int tile = x3_tile(c, g);
                 R = bn_groups(M);
-                RUN(xlabel("conv_fwd", tile, i), 2.0 * M * C.cout * 9 * C.cin, launch_rowgemm_x3(g, tile, s));
+                RUN(xlabel("conv_fwd", tile, i), 2.0 * M * C.cout * 9 * C.cin, launch_rowgemm_x3(g, tile, s, c->opt.x3_r3_sched));
                 return stats_finalize(c, L, p, i, R, M, training, prm, bn_run, bn_cnt);
             }
             if (rg16_on(c, C.cin, C.cout)) {
@@ -1375,7 +1378,7 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
                 up16[idec] = true;
             }
             const int tile = x3_tile(c, g);
-            RUN(xlabel("convT_fwd", tile, 100 + k), 2.0 * g.M * g.N * g.K, launch_rowgemm_x3(g, tile, s));
+            RUN(xlabel("convT_fwd", tile, 100 + k), 2.0 * g.M * g.N * g.K, launch_rowgemm_x3(g, tile, s, c->opt.x3_r3_sched));
             return 0;
         }
         if (!c->res && rg16_on(c, T.cin, T.cout)) {
@@ -1588,7 +1591,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
             }
             const int tile = x3_tile(c, g);
             if (rows) *rows = bn_groups(P);
-            RUN(xlabel("conv_dgrad", tile, i), 2.0 * P * C.cout * 9 * C.cin, launch_rowgemm_x3(g, tile, s));
+            RUN(xlabel("conv_dgrad", tile, i), 2.0 * P * C.cout * 9 * C.cin, launch_rowgemm_x3(g, tile, s, c->opt.x3_r3_sched));
             return 0;
         }
         // bf16 image of dz: A operand of the LDS-DMA dgrad, B' of the LDS-DMA wgrad; the f32
@@ -1788,7 +1791,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
             const int tile = x3_tile(c, g);
             *rows = bn_groups(Pin);
             RUN(xlabel("convT_dgrad", tile, 100 + k), 2.0 * Pin * T.cin * 4 * T.cout,
-                launch_rowgemm_x3(g, tile, s));
+                launch_rowgemm_x3(g, tile, s, c->opt.x3_r3_sched));
             return 0;
         }
         WgradCfg wc = wgrad_cfg(c, T.cin, 1, T.cout, 4, Pin, c->bf16);

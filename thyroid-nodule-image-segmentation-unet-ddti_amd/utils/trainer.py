@@ -330,8 +330,9 @@ class Trainer:
         if _distributed() and self._can_plot():
             # one set of PNGs over the whole test set, in the reference's sample order: batch
             # by batch, each batch's shards in rank order (DataParallel's gather order)
-            parts = [None] * dist.get_world_size()
-            dist.all_gather_object(parts, keep)
+            # (gather to rank 0 only: it alone plots, so the other ranks need no copies)
+            parts = [None] * dist.get_world_size() if self.rank0 else None
+            dist.gather_object(keep, parts, dst=0)
             keep = ([p[b] for b in range(len(parts[0])) for p in parts if b < len(p)]
                     if self.rank0 else [])
         keep = [k for k in keep if k is not None]
