@@ -206,6 +206,30 @@ def test_x3_halo_schedules_bit_identical(B, H, W):
         assert torch.equal(outs[0][1], outs[i][1]), (i, (outs[0][1] - outs[i][1]).abs().max().item())
 
 
+def test_x3_wgrad_schedules_bit_identical():
+    """The 64x128 tap-row x3 weight gradient's schedules (option x3_wsched: four LDS stages
+    with waves 4..7 half a chunk behind, and the same with waves 0..3 issuing every DMA) run
+    the same MFMAs in the same order per accumulator over the same split partition: one
+    training step is bit-identical to the r04 schedule (B=2 at 128x128; W = 128 .. 32 on the
+    tap-row kernels)."""
+    import unet_hip
+    from _helpers import options
+    x, t = inputs(37, 2, 128, 128)
+    outs = []
+    for sched in (0, 1, 2):
+        m = hip_model(O.make_params(42), DEV)
+        with options(m.flatten_().rt, x3_wsched=sched):
+            logits = m(x.to(DEV))
+            l = unet_hip.seg_losses(logits, t.to(DEV))
+            (l[0] + l[1]).backward()
+            torch.cuda.synchronize()
+        outs.append((logits.detach().clone(), m._state.grad_arena.clone()))
+        del m
+    for i in range(1, len(outs)):
+        assert torch.equal(outs[0][0], outs[i][0]), i
+        assert torch.equal(outs[0][1], outs[i][1]), (i, (outs[0][1] - outs[i][1]).abs().max().item())
+
+
 def test_x3_tap_row_wgrad_matches_one_tap():
     """The tap-row x3 weight gradient (wgrad_x3_row3_kernel: three dx taps from one 34-pixel
     halo, default on rows of 32k pixels) against the one-tap x3 kernel (option x3_wtile = 1

@@ -159,7 +159,9 @@ int wgrad_tile_taps(int tile);  // taps of the M dimension one block covers (3 f
 // sched: schedule of the tap-row halo tiles 4 / 5 (kernels_gemm_x3.hip X3R3Sched; bit-identical)
 int launch_rowgemm_x3(const RowGemmArgs& a, int tile, hipStream_t s, int sched = 0);
 int rowgemm_x3_tile_dims(int tile, int* bm, int* bn);
-int launch_wgrad_x3(const WgradArgs& a, int tile, hipStream_t s);
+// sched: schedule of the tap-row 64x128 tile (2): 0 = r04, 1 = four stages with waves 4..7 half a
+// chunk behind, 2 = 1 with waves 0..3 issuing every DMA (bit-identical)
+int launch_wgrad_x3(const WgradArgs& a, int tile, hipStream_t s, int sched = 0);
 int wgrad_x3_tile_dims(int tile, int* bm, int* bn);
 // x3 image of op(src) (BN affine if scale, ReLU on channels < relu) into dst [P][dld] at
 // channel offset doff

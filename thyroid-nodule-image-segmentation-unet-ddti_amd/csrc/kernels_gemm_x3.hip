@@ -810,23 +810,36 @@ __global__ __launch_bounds__(T::THREADS, 1) void wgrad_x3_kernel(WgradArgs p) {
 // reads feed 18 MFMAs.  Stage: [AR halo rows][6 BM B] + [32 pixel rows][6 BN B]; the loader
 // gives every wave the same instruction count (rows past the halo / chunk read zeros).
 // ------------------------------------------------------------------------------------
-template <int BM, int BN, int S = 3, int OCC = 1>
+//
+// SCHED (r05): 0 = every wave issues its share of the DMA and runs both k-steps of chunk kc in
+// segment kc (r04).  1 = four LDS stages with the DMA two chunks ahead, so a stage stays intact
+// one segment longer: waves 4..7 (each sharing a SIMD with wave w - 4) run half a chunk behind,
+// reading and computing chunk kc - 1's second k-step at the start of segment kc while their
+// partner waits for its first fragments of chunk kc (MI355X_MICROARCH.md "two waves per SIMD"
+// item 9).  2 = 1 with the DMA issued by waves 0..3 only (twice the pieces each).  Same MFMAs
+// in the same order per accumulator, same split partition: bit-identical.
+template <int BM, int BN, int S = 3, int OCC = 1, int SCHED = 0>
 __global__ __launch_bounds__((BM / 32) * (BN / 32) * 64, OCC) void wgrad_x3_row3_kernel(WgradArgs p) {
     constexpr int WAVES = (BM / 32) * (BN / 32), BKP = 32;
     constexpr int WAVES_N = BN / 32;
-    static_assert(S >= 2 && S <= 3, "stages");
+    static_assert(S >= 2 && S <= 4, "stages");
+    static_assert(SCHED == 0 || (S == 4 && WAVES == 8), "the staggered schedules need 4 stages, 8 waves");
+    constexpr int LW = SCHED == 2 ? 4 : WAVES;  // waves issuing the DMA
+    constexpr int DIST = SCHED ? 2 : S - 1;     // chunks the DMA runs ahead
     constexpr int RA = 6 * BM, RBB = 6 * BN;
     constexpr int HALO = BKP + 2;
-    constexpr int AI = (HALO * RA + 1024 * WAVES - 1) / (1024 * WAVES);  // per wave
-    constexpr int BI = (BKP * RBB + 1024 * WAVES - 1) / (1024 * WAVES);
+    constexpr int AREG = (HALO * RA + 1024 * WAVES - 1) / (1024 * WAVES) * WAVES * 1024;  // per stage
+    constexpr int BREG = (BKP * RBB + 1024 * WAVES - 1) / (1024 * WAVES) * WAVES * 1024;
+    constexpr int AI = AREG / (1024 * LW), BI = BREG / (1024 * LW);  // pieces per issuing wave
     constexpr int GPC = AI + BI;
-    constexpr int AREG = AI * WAVES * 1024, BREG = BI * WAVES * 1024;  // bytes per stage
     constexpr int STAGE = AREG + BREG;
     __shared__ __attribute__((aligned(1024))) char smem[STAGE * S];
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+    const bool issuer = wave < LW;
+    const bool lag = SCHED != 0 && wave >= 4;
     const int tiles_n = p.CB / BN, tiles_m = p.CA / BM;
     int idx = p.xcd ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
     const int tn = idx % tiles_n;
@@ -841,20 +854,26 @@ __global__ __launch_bounds__((BM / 32) * (BN / 32) * 64, OCC) void wgrad_x3_row3
     const int pend = min(pbeg + p.pps, p.P);
     const int nk = (pend - pbeg) / BKP;  // pps, P multiples of 32
 
-    int arow[AI], aele[AI], brow[BI], bele[BI];
+    // loader: lane of piece j fills stage byte o = (j LW + wave) KB + 16 lane: pixel row o / RA,
+    // 16-B slot (o % RA) / 16, sourcing slot x3_tswz of it (kept in registers for SCHED 0; the
+    // staggered schedules recompute it per piece to stay within 256 VGPRs)
+    constexpr bool KEEP = SCHED == 0;
+    int arow[KEEP ? AI : 1], aele[KEEP ? AI : 1], brow[KEEP ? BI : 1], bele[KEEP ? BI : 1];
+    auto apiece = [&](int j, int& r, int& e) {
+        const int o = ((j * LW + wave) * 64 + lane) * 16;
+        r = o / RA;
+        e = x3_tswz<RA>((o - r * RA) >> 4, r) * 8;
+    };
+    auto bpiece = [&](int j, int& r, int& e) {
+        const int o = ((j * LW + wave) * 64 + lane) * 16;
+        r = o / RBB;
+        e = x3_tswz<RBB>((o - r * RBB) >> 4, r) * 8;
+    };
+    if constexpr (KEEP) {
 #pragma unroll
-    for (int j = 0; j < AI; ++j) {
-        const int o = ((j * WAVES + wave) * 64 + lane) * 16;
-        const int r = o / RA, sl = (o - r * RA) >> 4;
-        arow[j] = r;
-        aele[j] = x3_tswz<RA>(sl, r) * 8;
-    }
+        for (int j = 0; j < AI; ++j) apiece(j, arow[j], aele[j]);
 #pragma unroll
-    for (int j = 0; j < BI; ++j) {
-        const int o = ((j * WAVES + wave) * 64 + lane) * 16;
-        const int r = o / RBB, sl = (o - r * RBB) >> 4;
-        brow[j] = r;
-        bele[j] = x3_tswz<RBB>(sl, r) * 8;
+        for (int j = 0; j < BI; ++j) bpiece(j, brow[j], bele[j]);
     }
     const uint16_t* a16 = (const uint16_t*)p.a + (size_t)(p.aoff + ca0) * 3;
     const uint16_t* b16 = (const uint16_t*)p.b + (size_t)(p.boff + cb0) * 3;
@@ -871,16 +890,22 @@ __global__ __launch_bounds__((BM / 32) * (BN / 32) * 64, OCC) void wgrad_x3_row3
         char* base = smem + st * STAGE;
 #pragma unroll
         for (int j = 0; j < AI; ++j) {
-            const int xx = x0 - 1 + arow[j];
-            const bool ok = rowok && arow[j] < HALO && xx >= 0 && xx < W;
-            const uint16_t* g = ok ? a16 + (size_t)(rowbase + xx) * rowa + aele[j] : zero;
-            x3_dma16(g, base + (j * WAVES + wave) * 1024);
+            int ar, ae;
+            if constexpr (KEEP) ar = arow[j], ae = aele[j];
+            else apiece(j, ar, ae);
+            const int xx = x0 - 1 + ar;
+            const bool ok = rowok && ar < HALO && xx >= 0 && xx < W;
+            const uint16_t* g = ok ? a16 + (size_t)(rowbase + xx) * rowa + ae : zero;
+            x3_dma16(g, base + (j * LW + wave) * 1024);
         }
 #pragma unroll
         for (int j = 0; j < BI; ++j) {
-            const bool ok = brow[j] < BKP;
-            const uint16_t* g = ok ? b16 + (size_t)(pc + brow[j]) * rowb + bele[j] : zero;
-            x3_dma16(g, base + AREG + (j * WAVES + wave) * 1024);
+            int br, be;
+            if constexpr (KEEP) br = brow[j], be = bele[j];
+            else bpiece(j, br, be);
+            const bool ok = br < BKP;
+            const uint16_t* g = ok ? b16 + (size_t)(pc + br) * rowb + be : zero;
+            x3_dma16(g, base + AREG + (j * LW + wave) * 1024);
         }
     };
 
@@ -909,60 +934,100 @@ __global__ __launch_bounds__((BM / 32) * (BN / 32) * 64, OCC) void wgrad_x3_row3
             boff[q] = AREG + trow * RBB + (x3_tswz<RBB>(slot(colb, q), trow) << 4) + ((colb >> 2) & 1) * 8;
     }
 
+    // fragments of one k-step: A' of the three dx taps, B'; read by ds_read_b64_tr_b16
+    struct Frag {
+        x3_short4 a[3][3][2], b[3][2];
+    };
+    auto load = [&](Frag& f, auto KK, unsigned sb) {
+        constexpr int kk = decltype(KK)::value;
 #pragma unroll
-    for (int s = 0; s < S - 1; ++s)
-        if (s < nk) issue(s, s);
-    for (int kc = 0; kc < nk; ++kc) {
-        // one barrier per chunk: wait for chunk kc (chunk kc + 1 may stay in flight with three
-        // stages), barrier -- every wave's DMA has landed and every wave has finished reading
-        // chunk kc - 1 -- then restage that slot with chunk kc + S - 1.  (r04: issuing before
-        // the wait and closing each chunk with a second barrier: the same bits, 0.5 % slower
-        // over the step.)
-        if (S >= 3 && kc + 1 < nk) x3_wait_vm<GPC>();
-        else x3_wait_vm<0>();
-        x3_barrier();
-        if (kc + S - 1 < nk) issue(kc + S - 1, (kc + S - 1) % S);
-        const unsigned sb = x3_lds_u32(smem) + (kc % S) * STAGE;
-        x3_short4 fa[2][3][3][2], fb[2][3][2];
-        auto load = [&](auto KK) {
-            constexpr int kk = decltype(KK)::value;
-#pragma unroll
-            for (int dx = 0; dx < 3; ++dx)
-#pragma unroll
-                for (int q = 0; q < 3; ++q) {
-                    fa[kk][dx][q][0] = x3_tr16<kk * 16 * RA>(sb + aoff[dx][q]);
-                    fa[kk][dx][q][1] = x3_tr16<kk * 16 * RA + 4 * RA>(sb + aoff[dx][q]);
-                }
+        for (int dx = 0; dx < 3; ++dx)
 #pragma unroll
             for (int q = 0; q < 3; ++q) {
-                fb[kk][q][0] = x3_tr16<kk * 16 * RBB>(sb + boff[q]);
-                fb[kk][q][1] = x3_tr16<kk * 16 * RBB + 4 * RBB>(sb + boff[q]);
+                f.a[dx][q][0] = x3_tr16<kk * 16 * RA>(sb + aoff[dx][q]);
+                f.a[dx][q][1] = x3_tr16<kk * 16 * RA + 4 * RA>(sb + aoff[dx][q]);
             }
-        };
-        auto mma = [&](auto KK) {
-            constexpr int kk = decltype(KK)::value;
-            bf16x8 b3[3];
 #pragma unroll
-            for (int q = 0; q < 3; ++q) b3[q] = *(const bf16x8*)fb[kk][q];
+        for (int q = 0; q < 3; ++q) {
+            f.b[q][0] = x3_tr16<kk * 16 * RBB>(sb + boff[q]);
+            f.b[q][1] = x3_tr16<kk * 16 * RBB + 4 * RBB>(sb + boff[q]);
+        }
+    };
+    auto mma = [&](const Frag& f) {
+        bf16x8 b3[3];
 #pragma unroll
-            for (int dx = 0; dx < 3; ++dx) {
-                bf16x8 a3[3];
+        for (int q = 0; q < 3; ++q) b3[q] = *(const bf16x8*)f.b[q];
 #pragma unroll
-                for (int q = 0; q < 3; ++q) a3[q] = *(const bf16x8*)fa[kk][dx][q];
-                mfma_x3s(a3, b3, acc[dx], acl[dx]);
-            }
-        };
-        load(std::integral_constant<int, 0>{});
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-        load(std::integral_constant<int, 1>{});
-        __builtin_amdgcn_sched_barrier(0);
-        mma(std::integral_constant<int, 0>{});
-        __builtin_amdgcn_sched_barrier(0);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-        mma(std::integral_constant<int, 1>{});
+        for (int dx = 0; dx < 3; ++dx) {
+            bf16x8 a3[3];
+#pragma unroll
+            for (int q = 0; q < 3; ++q) a3[q] = *(const bf16x8*)f.a[dx][q];
+            mfma_x3s(a3, b3, acc[dx], acl[dx]);
+        }
+    };
+    const unsigned sbase = x3_lds_u32(smem);
+    using K0 = std::integral_constant<int, 0>;
+    using K1 = std::integral_constant<int, 1>;
+
+    if (issuer) {
+#pragma unroll
+        for (int s = 0; s < DIST; ++s)
+            if (s < nk) issue(s, s);
     }
+    // one chunk loop per role (separately register-allocated paths)
+    auto run = [&](auto LAGC) {
+        constexpr bool LAG = decltype(LAGC)::value;
+        for (int kc = 0; kc < nk; ++kc) {
+            // one barrier per chunk: the issuing waves wait for chunk kc (chunk kc + 1 may stay
+            // in flight when the DMA runs two ahead), barrier -- every wave's DMA has landed and
+            // every wave has finished the reads of the slot about to be restaged -- then
+            // restage it with chunk kc + DIST
+            if (issuer) {
+                if (DIST >= 2 && kc + 1 < nk) x3_wait_vm<GPC>();
+                else x3_wait_vm<0>();
+            }
+            x3_barrier();
+            if (issuer && kc + DIST < nk) issue(kc + DIST, (kc + DIST) % S);
+            const unsigned sb = sbase + (kc % S) * STAGE;
+            Frag f0, f1;
+            if constexpr (LAG) {  // chunk kc - 1's second k-step, then this chunk's first
+                if (kc > 0) {
+                    load(f1, K1{}, sbase + ((kc + S - 1) % S) * STAGE);
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    __builtin_amdgcn_sched_barrier(0);
+                    load(f0, K0{}, sb);
+                    __builtin_amdgcn_sched_barrier(0);
+                    mma(f1);
+                } else {
+                    load(f0, K0{}, sb);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_sched_barrier(0);
+                mma(f0);
+            } else {
+                load(f0, K0{}, sb);
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_sched_barrier(0);
+                load(f1, K1{}, sb);
+                __builtin_amdgcn_sched_barrier(0);
+                mma(f0);
+                __builtin_amdgcn_sched_barrier(0);
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_sched_barrier(0);
+                mma(f1);
+            }
+        }
+        if (LAG && nk > 0) {  // the last chunk's second k-step (its stage is not restaged any more)
+            Frag f1;
+            load(f1, K1{}, sbase + ((nk - 1) % S) * STAGE);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+            mma(f1);
+        }
+    };
+    if (lag) run(std::true_type{});
+    else run(std::false_type{});
 
     const int li = lane & 31, lh = lane >> 5;
     float* slab = p.slab + (size_t)split * p.Mw * p.Nw;
@@ -1215,7 +1280,7 @@ int wgrad_x3_tile_dims(int tile, int* bm, int* bn) {
 // G_CONV3, B' G_IDENT) and ConvT (A' G_IDENT, B' G_UP2); no bias column sums.
 // (r04, not kept: the tap-row tiles on 64-pixel chunks, four k-steps per barrier pair:
 // bit-identical, config 2 within noise, profiles/r04_x3_halo_ab.txt)
-int launch_wgrad_x3(const WgradArgs& a, int tile, hipStream_t s) {
+int launch_wgrad_x3(const WgradArgs& a, int tile, hipStream_t s, int sched) {
     if (a.ascale || a.bcoef || a.bias_slab || !a.zero16 || a.P < 1) return -1;
     if (a.aoff % 32 || a.boff % 32 || a.lda % 32 || a.ldb % 32) return -1;
     if (tile >= 2 && tile <= 4) {  // tap-row kernel: 3x3 convs, W % 32 == 0
@@ -1225,7 +1290,11 @@ int launch_wgrad_x3(const WgradArgs& a, int tile, hipStream_t s) {
             a.CA % bm || a.CB % bn || a.W % 32 || a.pps % 32 || a.P % 32)
             return -1;
         const dim3 grid((a.CA / bm) * 3 * (a.CB / bn) * a.splits);
-        if (tile == 2)
+        if (tile == 2 && sched == 1)
+            hipLaunchKernelGGL((wgrad_x3_row3_kernel<64, 128, 4, 1, 1>), grid, dim3(512), 0, s, a);
+        else if (tile == 2 && sched == 2)
+            hipLaunchKernelGGL((wgrad_x3_row3_kernel<64, 128, 4, 1, 2>), grid, dim3(512), 0, s, a);
+        else if (tile == 2)
             hipLaunchKernelGGL((wgrad_x3_row3_kernel<64, 128>), grid, dim3(512), 0, s, a);
         else if (tile == 3)
             hipLaunchKernelGGL((wgrad_x3_row3_kernel<128, 64>), grid, dim3(512), 0, s, a);

@@ -165,6 +165,9 @@ struct Options {
     int x3_r3 = 1;             // its 256x128 3x3 GEMMs on the tap-row halo kernel (tile 4)
     int x3_r3_sched = 0;       // the halo kernel's wave schedule (kernels_gemm_x3.hip X3R3Sched:
                                // who issues the LDS-DMA, stagger of waves 4..7; bit-identical)
+    int x3_wsched = 0;         // the 64x128 tap-row weight gradient's schedule (0 = r04, 1 = four
+                               // stages with waves 4..7 half a chunk behind, 2 = 1 with waves
+                               // 0..3 issuing every DMA; bit-identical)
 };
 struct OptionDesc {
     const char* name;
@@ -215,6 +218,7 @@ const OptionDesc OPTION_TABLE[] = {
     {"x3_n64", &Options::x3_n64},
     {"x3_r3", &Options::x3_r3},
     {"x3_r3_sched", &Options::x3_r3_sched},
+    {"x3_wsched", &Options::x3_wsched},
 };
 
 }  // namespace
@@ -1561,7 +1565,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
             w.splits = wc.splits;
             w.slab = p.slab;
             w.zero16 = p.zero16;
-            RUN(x3wlabel("conv_wgrad", wc, i), 2.0 * P * C.cout * 9 * C.cin, launch_wgrad_x3(w, wc.tile, s));
+            RUN(x3wlabel("conv_wgrad", wc, i), 2.0 * P * C.cout * 9 * C.cin, launch_wgrad_x3(w, wc.tile, s, c->opt.x3_wsched));
             RUN("wgrad_reduce", 0,
                 k_slab_reduce(p.slab, wc.splits, w.Mw, w.Nw, 0, C.cin, C.cout, grads + C.w, s));
             if (!dx) return 0;
@@ -1757,7 +1761,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
             w.slab = p.slab;
             w.zero16 = p.zero16;
             RUN(x3wlabel("convT_wgrad", wc, 100 + k), 2.0 * Pin * T.cin * 4 * T.cout,
-                launch_wgrad_x3(w, wc.tile, s));
+                launch_wgrad_x3(w, wc.tile, s, c->opt.x3_wsched));
             RUN("bias_grad", 0, k_up2_bias_partials(p.dcat[lo], ldo, uo, Hi, Wi, Pin, T.cout, wc.pps,
                                                     wc.splits, p.bslab, s));
             RUN("wgrad_reduce", 0,
