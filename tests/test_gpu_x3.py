@@ -186,15 +186,16 @@ def test_x3_halo_schedules_bit_identical(B, H, W):
     """The halo GEMM's wave schedules (option x3_r3_sched, kernels_gemm_x3.hip X3R3Sched: which
     waves issue the LDS-DMA, the stagger of waves 4..7, where the DMA goes in the sub-step) run
     the same MFMAs in the same order per accumulator: one training step -- logits and the whole
-    gradient arena -- is bit-identical across all five.  128x128 covers W = 128 .. 16; 256x256 the
-    level-0 256x64 tile at W = 256."""
+    gradient arena -- is bit-identical across all five, and with the 64-output GEMMs on the
+    128x64 two-blocks-per-CU halo tile (option x3_n64_r3 = 6; same K order, same 128-row BN
+    partial groups).  128x128 covers W = 128 .. 16; 256x256 the level-0 tiles at W = 256."""
     import unet_hip
     from _helpers import options
     x, t = inputs(31, B, H, W)
     outs = []
-    for sched in range(5):
+    for sched, n64 in ((0, 5), (1, 5), (2, 5), (3, 5), (4, 5), (0, 6)):
         m = hip_model(O.make_params(42), DEV)
-        with options(m.flatten_().rt, x3_r3_sched=sched):
+        with options(m.flatten_().rt, x3_r3_sched=sched, x3_n64_r3=n64):
             logits = m(x.to(DEV))
             l = unet_hip.seg_losses(logits, t.to(DEV))
             (l[0] + l[1]).backward()

@@ -303,15 +303,15 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_x3_kernel(RowGemmA
 //   LATE the DMA of the next sub-step is issued after the first k-step's fragment reads
 // The next group's halo is spread over the current group's three sub-steps (AC pieces each).
 // Every schedule runs the same MFMAs in the same order per accumulator: bit-identical.
-template <int BN, int LW, bool ISSUER, bool LAG, bool LATE>
+template <int BM, int BN, int LW, bool ISSUER, bool LAG, bool LATE>
 __device__ __forceinline__ void x3r3_body(const RowGemmArgs& p, char* smem, int wave, int lane,
                                           f32x16 (&acc)[2][BN / 64], f32x16 (&acl)[2][BN / 64],
                                           int m0, int n0) {
-    constexpr int BM = 256, BK = 32, WM = 64, WN = BN / 2, WAVES_N = 2, WAVES = 8;
+    constexpr int BK = 32, WM = 64, WN = BN / 2, WAVES_N = 2, WAVES = (BM / WM) * WAVES_N;
     constexpr int MT = WM / 32, NT = WN / 32;
-    constexpr int RB = 192, AR = 288;
-    constexpr int AREG = ((AR * RB + 1024 * WAVES - 1) / (1024 * WAVES)) * WAVES * 1024;  // 56 KB
-    constexpr int BREG = ((BN * RB + 1024 * WAVES - 1) / (1024 * WAVES)) * WAVES * 1024;  // 24 / 16 KB
+    constexpr int RB = 192, AR = BM / 16 * 18;  // halo rows at W = 16: BM / 16 rows of 18
+    constexpr int AREG = ((AR * RB + 1024 * WAVES - 1) / (1024 * WAVES)) * WAVES * 1024;  // 56 / 28 KB
+    constexpr int BREG = ((BN * RB + 1024 * WAVES - 1) / (1024 * WAVES)) * WAVES * 1024;  // 24 / 16 / 12 KB
     constexpr int AI = AREG / (1024 * LW), BI = BREG / (1024 * LW);  // pieces per issuing wave
     constexpr int AC = (AI + 2) / 3;                                  // halo pieces per sub-step
     auto swz = [](int r) { return (r >> 2) & 3; };
@@ -477,12 +477,16 @@ struct X3R3Sched {
     static constexpr bool LATE = SCHED == 1 || SCHED == 3;
 };
 
-template <int EMODE, int BN = 128, int SCHED = 0>
-__global__ __launch_bounds__(512, 1) void rowgemm_x3_row3_kernel(RowGemmArgs p) {
-    constexpr int BM = 256, WM = 64, WN = BN / 2, MT = 2, NT = WN / 32;
-    constexpr int RB = 192, AR = 288;
-    constexpr int SMEM = 2 * ((AR * RB + 8191) / 8192) * 8192 + 2 * ((BN * RB + 8191) / 8192) * 8192;  // 160 KB
+// BM = 256: 8 waves, one block per CU (160 KB); BM = 128 (tile 6, 128 x 64): 4 waves of 64 x 32,
+// 80 KB, two blocks per CU -- independent blocks run out of phase, so one block's prologue,
+// epilogue and barrier stalls overlap the other's MFMAs (the short-K level-0 GEMMs)
+template <int EMODE, int BN = 128, int SCHED = 0, int BM = 256>
+__global__ __launch_bounds__(BM / 64 * 2 * 64, BM == 256 ? 1 : 2) void rowgemm_x3_row3_kernel(RowGemmArgs p) {
+    constexpr int WM = 64, WN = BN / 2, MT = 2, NT = WN / 32, WAVES = BM / 64 * 2;
+    constexpr int RB = 192, AR = BM / 16 * 18, WB = 1024 * WAVES;
+    constexpr int SMEM = 2 * ((AR * RB + WB - 1) / WB) * WB + 2 * ((BN * RB + WB - 1) / WB) * WB;  // 160 / 80 KB
     static_assert(SMEM >= 2 * (BM / 64) * BN * 8, "epilogue scratch");
+    static_assert(BM == 256 || SCHED == 0, "the staggered schedules pair waves w and w + 4");
     __shared__ __attribute__((aligned(1024))) char smem[SMEM];
     using SC = X3R3Sched<SCHED>;
     const int tid = threadIdx.x, lane = tid & 63;
@@ -499,10 +503,12 @@ __global__ __launch_bounds__(512, 1) void rowgemm_x3_row3_kernel(RowGemmArgs p) 
         for (int j = 0; j < NT; ++j)
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = acl[i][j][r] = 0.f;
-    if (wave >= 4)
-        x3r3_body<BN, SC::LW, SC::LW == 8, SC::LAG, SC::LATE>(p, smem, wave, lane, acc, acl, m0, n0);
+    if constexpr (BM == 128)
+        x3r3_body<BM, BN, 4, true, false, false>(p, smem, wave, lane, acc, acl, m0, n0);
+    else if (wave >= 4)
+        x3r3_body<BM, BN, SC::LW, SC::LW == 8, SC::LAG, SC::LATE>(p, smem, wave, lane, acc, acl, m0, n0);
     else
-        x3r3_body<BN, SC::LW, true, false, SC::LATE>(p, smem, wave, lane, acc, acl, m0, n0);
+        x3r3_body<BM, BN, SC::LW, true, false, SC::LATE>(p, smem, wave, lane, acc, acl, m0, n0);
     x3_barrier();  // the epilogue reuses the stage memory
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
@@ -511,12 +517,16 @@ __global__ __launch_bounds__(512, 1) void rowgemm_x3_row3_kernel(RowGemmArgs p) 
     row_epilogue<EMODE, BM, BN, WM, WN, true>(p, acc, m0, n0, tile_m, wm, wn, lane, tid, (float*)smem);
 }
 
-template <int EMODE, int BN>
+template <int EMODE, int BN, int BM = 256>
 static int x3r3_go(const RowGemmArgs& a, int sched, hipStream_t s) {
     // BM % W == 0 or W % BM == 0 keeps a tile on whole rows / row segments; W >= 16 bounds the halo
     if (a.amode != G_CONV3 || a.N % BN || a.C % 32 || a.K != 9 * a.C) return -1;
-    if (a.W < 16 || (256 % a.W && a.W % 256)) return -1;
-    const dim3 grid(((a.M + 255) / 256) * (a.N / BN));
+    if (a.W < 16 || (BM % a.W && a.W % BM)) return -1;
+    const dim3 grid(((a.M + BM - 1) / BM) * (a.N / BN));
+    if constexpr (BM == 128) {
+        hipLaunchKernelGGL((rowgemm_x3_row3_kernel<EMODE, BN, 0, 128>), grid, dim3(256), 0, s, a);
+        return (int)hipGetLastError();
+    }
 #define X3R3_SCHED(v)                                                                          \
     if (sched == v) {                                                                         \
         hipLaunchKernelGGL((rowgemm_x3_row3_kernel<EMODE, BN, v>), grid, dim3(512), 0, s, a); \
@@ -548,14 +558,16 @@ static int x3_go(const RowGemmArgs& a, hipStream_t s) {
 
 template <int AMODE, int EMODE>
 static int x3_tile(const RowGemmArgs& a, int tile, hipStream_t s, int sched = 0) {
-    if (tile == 4 || tile == 5) {  // tap-row halo kernel (3x3 convs): 256 x 128 / 256 x 64
+    if (tile == 4 || tile == 5 || tile == 6) {  // tap-row halo kernel (3x3 convs): 256 x 128 / 256 x 64 / 128 x 64
         // (r04, not kept: 4-wave 128x64 / 64x128 wave tiles, within noise of 8 waves; B
         // straight from global memory into registers instead of the LDS ring, one barrier per
         // halo group, bit-identical but 222 -> 161 TF/s: the per-wave B loads cost more than
         // the ring's barriers; 256 x 64 as 4 waves of 64 x 64, bit-identical, 589 -> 584 img/s;
         // 256 x 64 with a three-slot B ring, B two sub-steps ahead: bit-identical, no gain)
         if constexpr (AMODE == G_CONV3)
-            return tile == 4 ? x3r3_go<EMODE, 128>(a, sched, s) : x3r3_go<EMODE, 64>(a, sched, s);
+            return tile == 4 ? x3r3_go<EMODE, 128>(a, sched, s)
+                 : tile == 5 ? x3r3_go<EMODE, 64>(a, sched, s)
+                             : x3r3_go<EMODE, 64, 128>(a, sched, s);
         return -1;
     }
 #define X3_CASE(id, T) \
@@ -1211,9 +1223,9 @@ __global__ __launch_bounds__(256) void bn_dz_x3_kernel(const float* __restrict__
 }  // namespace
 
 int rowgemm_x3_tile_dims(int tile, int* bm, int* bn) {
-    if (tile == 4 || tile == 5) {  // tap-row halo 256 x 128 / 256 x 64
-        *bm = 256;
-        *bn = tile == 5 ? 64 : 128;
+    if (tile == 4 || tile == 5 || tile == 6) {  // tap-row halo 256 x 128 / 256 x 64 / 128 x 64
+        *bm = tile == 6 ? 128 : 256;
+        *bn = tile == 4 ? 128 : 64;
         return 0;
     }
 #define X3_DIMS(id, T)  \

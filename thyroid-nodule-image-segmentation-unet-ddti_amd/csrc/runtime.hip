@@ -165,6 +165,8 @@ struct Options {
     int x3_r3 = 1;             // its 256x128 3x3 GEMMs on the tap-row halo kernel (tile 4)
     int x3_r3_sched = 0;       // the halo kernel's wave schedule (kernels_gemm_x3.hip X3R3Sched:
                                // who issues the LDS-DMA, stagger of waves 4..7; bit-identical)
+    int x3_n64_r3 = 5;         // halo tile of the 64-output 3x3 GEMMs: 5 = 256x64 (8 waves, one
+                               // block per CU), 6 = 128x64 (4 waves, two blocks per CU)
     int x3_wsched = 0;         // the 64x128 tap-row weight gradient's schedule (0 = r04, 1 = four
                                // stages with waves 4..7 half a chunk behind, 2 = 1 with waves
                                // 0..3 issuing every DMA; bit-identical)
@@ -218,6 +220,7 @@ const OptionDesc OPTION_TABLE[] = {
     {"x3_n64", &Options::x3_n64},
     {"x3_r3", &Options::x3_r3},
     {"x3_r3_sched", &Options::x3_r3_sched},
+    {"x3_n64_r3", &Options::x3_n64_r3},
     {"x3_wsched", &Options::x3_wsched},
 };
 
@@ -782,8 +785,10 @@ int x3_tile(const unet_ctx* c, const RowGemmArgs& g) {
         if (blocks < 256) return 1;
         return c->opt.x3_r3 && r3ok ? 4 : 0;
     }
-    // 64 outputs: the 256 x 64 halo tile (5) where its grid fills the chip
-    if (c->opt.x3_r3 && r3ok && (int64_t)(g.M + 255) / 256 >= 512) return 5;
+    // 64 outputs: a halo tile (5 = 256 x 64, one block per CU; 6 = 128 x 64, two blocks per
+    // CU: option x3_n64_r3) where the 256-row grid fills the chip
+    if (c->opt.x3_r3 && r3ok && (int64_t)(g.M + 255) / 256 >= 512)
+        return c->opt.x3_n64_r3 == 6 ? 6 : 5;
     return c->opt.x3_n64;
 }
 

@@ -22,6 +22,13 @@ for S in 0 1 2 3 4 0; do
   echo "sched $S rc=$r $(python3 -c "import json;d=json.load(open('gpurun_out/$TAG.bench$S.json'));print(d['value'], d['ms_per_step'], d['roofline']['kernel'], d['roofline']['avg_launch_ms'])" 2>/dev/null)"
   [ $r -ne 0 ] && { tail -20 gpurun_out/$TAG.bench$S.err; exit $r; }
 done
+for S in 6 5; do
+  timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --opt x3_n64_r3=$S \
+    > gpurun_out/$TAG.nbench$S.json 2> gpurun_out/$TAG.nbench$S.err
+  r=$?
+  echo "n64_r3 $S rc=$r $(python3 -c "import json;d=json.load(open('gpurun_out/$TAG.nbench$S.json'));print(d['value'], d['ms_per_step'])" 2>/dev/null)"
+  [ $r -ne 0 ] && { tail -20 gpurun_out/$TAG.nbench$S.err; exit $r; }
+done
 for S in 1 2 0; do
   timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --opt x3_wsched=$S \
     > gpurun_out/$TAG.wbench$S.json 2> gpurun_out/$TAG.wbench$S.err

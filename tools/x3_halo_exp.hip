@@ -556,6 +556,14 @@ int main(int argc, char** argv) {
         std::vector<float> r((size_t)M * N), q((size_t)M * N);
         CK(hipMemcpy(r.data(), yref, r.size() * 4, hipMemcpyDeviceToHost));
         h.out = y;
+        if (bn == 64) {  // the 128 x 64 two-blocks-per-CU halo tile
+            CK(hipMemset(y, 0, (size_t)M * N * 4));
+            const float t = timeit([&] { return launch_rowgemm_x3(h, 6, 0, 0); });
+            CK(hipMemcpy(q.data(), y, q.size() * 4, hipMemcpyDeviceToHost));
+            const bool same = memcmp(q.data(), r.data(), q.size() * 4) == 0;
+            printf("    library tile 6 (128x64, 2/CU): %.3f ms %.1f TF/s  %s\n", t, fl / t / 1e9,
+                   same ? "bit-identical" : "DIFFERS");
+        }
         for (int sc = 0; sc <= 4; ++sc) {  // the library's schedules (X3R3Sched)
             CK(hipMemset(y, 0, (size_t)M * N * 4));
             const float t = timeit([&] { return launch_rowgemm_x3(h, bn == 128 ? 4 : 5, 0, sc); });
