@@ -286,6 +286,23 @@ def test_convt16_bit_identical():
     _assert_same(outs[0], outs[1], "convt16")
 
 
+def test_rg16_halo_schedules_bit_identical():
+    """The bf16 halo GEMM's schedules (option rg16_sched: waves 4..7 run each stage's last tap
+    after the next barrier from held fragments; 2 also moves the DMA after the first tap's
+    reads) run the same MFMAs in the same order per accumulator: one training step of BASELINE
+    config 4's network at 256^2 (tiles 19 / 20 on W = 256 .. 16) is bit-identical to r04's."""
+    x, t = inputs(61, 2, 256, 256)
+    P = MO.make_params(67, 128, 5)
+    outs = {}
+    for sched in (0, 1, 2):
+        m = _bf16_model(P, 128, 5)
+        with options(m.flatten_().rt, rg16_sched=sched):
+            outs[sched] = _bf16_step(m, x, t)
+        del m
+    _assert_same(outs[0], outs[1], "rg16_sched 1")
+    _assert_same(outs[0], outs[2], "rg16_sched 2")
+
+
 def test_wg16_tap_row_bit_identical():
     """The tap-row bf16 weight gradient (kernels_gemm16.hip wgrad16_row3_kernel, option wg16_r3
     = 3 / 4 LDS stages: the three dx taps of one tap row from one halo of 66 pixel rows) runs

@@ -142,7 +142,8 @@ int launch_rowgemm_pipe(const RowGemmArgs& a, int tile, hipStream_t s);
 // 5 = 128x64 four waves, 7 = 64x64 three waves / SIMD, 8 = 64x32, 9 = 32x32;
 // 20.. = one row of 3x3 taps per block (3 accumulator sets; BM = channels of ONE tap):
 // 20 = 64x64, 21 = 128x64, 22 = 64x128, 23 = 128x128
-int launch_rowgemm16(const RowGemmArgs& a, int tile, hipStream_t s);
+// sched: schedule of the tap-row halo tiles 19 / 20 (rowgemm16_row3_kernel SCHED; bit-identical)
+int launch_rowgemm16(const RowGemmArgs& a, int tile, hipStream_t s, int sched = 0);
 // speed-of-light ablations of the forward rg16 GEMM (tile 4): -2 when not applicable
 int launch_rowgemm16_xp(const RowGemmArgs& a, int xp, hipStream_t s);
 int rowgemm16_tile_dims(int tile, int* bm, int* bn, int* stages = nullptr);

@@ -244,7 +244,12 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm16_kernel(RowGemmAr
 // ------------------------------------------------------------------------------------
 // BM x BN block tiles: 256 x 256 (tile 19) and 512 x 128 (tile 20, the 128-output layers of
 // config 4's level 0: 8 waves of 128 x 64 either way).
-template <int EMODE, int BM, int BN>
+// SCHED (r05, option rg16_sched; bit-identical): 0 = r04; 1 = waves 4..7 (each sharing a SIMD
+// with wave w - 4) run the stage's last tap (dx = 2) after the next barrier from fragments held
+// in registers, so that their matrix work opens each segment while their partner waits for its
+// first fragments (MI355X_MICROARCH.md "two waves per SIMD" item 9); 2 = 1 with the next
+// stage's DMA issued after the first tap's fragment reads
+template <int EMODE, int BM, int BN, int SCHED = 0>
 __global__ __launch_bounds__(512, 1) void rowgemm16_row3_kernel(RowGemmArgs p) {
     constexpr int WM = 128, WN = 64, BK = 32, WAVES_N = BN / WN;
     constexpr int WAVES = (BM / WM) * WAVES_N;
@@ -339,47 +344,80 @@ __global__ __launch_bounds__(512, 1) void rowgemm16_row3_kernel(RowGemmArgs p) {
 
     const int ns = 3 * CC;
     issue(0);
-    for (int s = 0; s < ns; ++s) {
-        // one barrier per stage: wait for stage s, barrier (every wave's DMA landed, every
-        // wave done reading stage s - 1), then restage s - 1's buffer with s + 1.  (r04: issuing
-        // before the wait and a second barrier after the MFMAs gave the same bits, 3 % slower.)
-        wait_vm<0>();
-        block_barrier();
-        if (s + 1 < ns) issue(s + 1);
-        const char* base = smem + (s & 1) * STAGE;
+    auto run = [&](auto LAGC) {
+        constexpr bool LAG = decltype(LAGC)::value;
+        bf16x8 ha[BK / 16][MT], hb[BK / 16][NT];  // LAG: the previous stage's dx = 2 fragments
+        auto mm = [&](const bf16x8 (&af)[MT], const bf16x8 (&bfr)[NT]) {
 #pragma unroll
-        for (int dx = 0; dx < 3; ++dx)
+            for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-            for (int kk = 0; kk < BK / 16; ++kk) {
-                const int c = kk * 2 + lh;
-                bf16x8 af[MT], bfr[NT];
+                for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma32_bf16(af[mt], bfr[nt], acc[mt][nt]);
+        };
+        for (int s = 0; s < ns; ++s) {
+            // one barrier per stage: wait for stage s, barrier (every wave's DMA landed, every
+            // wave done reading stage s - 1), then restage s - 1's buffer with s + 1.  (r04:
+            // issuing before the wait and a second barrier after the MFMAs gave the same bits,
+            // 3 % slower.)
+            wait_vm<0>();
+            block_barrier();
+            if (SCHED != 2 && s + 1 < ns) issue(s + 1);
+            if constexpr (LAG) {
+                if (s > 0) {
 #pragma unroll
-                for (int mt = 0; mt < MT; ++mt) {
-                    const int h = ahb[mt] + dx;
-                    af[mt] = *(const bf16x8*)(base + h * RB + ((c ^ swz(h)) << 4));
+                    for (int kk = 0; kk < BK / 16; ++kk) mm(ha[kk], hb[kk]);
                 }
-#pragma unroll
-                for (int nt = 0; nt < NT; ++nt)
-                    bfr[nt] = *(const bf16x8*)(base + bro[nt] + dx * BN * RB + ((c ^ bfx[nt]) << 4));
-#pragma unroll
-                for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-                    for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma32_bf16(af[mt], bfr[nt], acc[mt][nt]);
             }
-        // this stage's ds_reads must have returned before any wave restages it
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    }
+            const char* base = smem + (s & 1) * STAGE;
+#pragma unroll
+            for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+                for (int kk = 0; kk < BK / 16; ++kk) {
+                    const int c = kk * 2 + lh;
+                    bf16x8 af[MT], bfr[NT];
+#pragma unroll
+                    for (int mt = 0; mt < MT; ++mt) {
+                        const int h = ahb[mt] + dx;
+                        af[mt] = *(const bf16x8*)(base + h * RB + ((c ^ swz(h)) << 4));
+                    }
+#pragma unroll
+                    for (int nt = 0; nt < NT; ++nt)
+                        bfr[nt] = *(const bf16x8*)(base + bro[nt] + dx * BN * RB + ((c ^ bfx[nt]) << 4));
+                    if (SCHED == 2 && dx == 0 && kk == 0 && s + 1 < ns) issue(s + 1);
+                    if (LAG && dx == 2) {
+#pragma unroll
+                        for (int mt = 0; mt < MT; ++mt) ha[kk][mt] = af[mt];
+#pragma unroll
+                        for (int nt = 0; nt < NT; ++nt) hb[kk][nt] = bfr[nt];
+                    } else {
+                        mm(af, bfr);
+                    }
+                }
+            // this stage's ds_reads must have returned before any wave restages it
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
+        if constexpr (LAG) {
+#pragma unroll
+            for (int kk = 0; kk < BK / 16; ++kk) mm(ha[kk], hb[kk]);
+        }
+    };
+    if (SCHED != 0 && wave >= 4) run(std::true_type{});
+    else run(std::false_type{});
     block_barrier();  // the epilogue reuses the stage memory
     row_epilogue<EMODE, BM, BN, WM, WN, true>(p, acc, m0, n0, tile_m, wm, wn, lane, tid, (float*)smem);
 }
 
 template <int EMODE, int BM, int BN>
-static int rg16r3_go(const RowGemmArgs& a, hipStream_t s) {
+static int rg16r3_go(const RowGemmArgs& a, hipStream_t s, int sched) {
     // BM % W == 0 or W % BM == 0 keeps a tile on whole rows / row segments; W >= 16 bounds the halo
     if (a.amode != G_CONV3 || a.N % BN || a.C % 32 || a.K != 9 * a.C) return -1;
     if (a.W < 16 || (BM % a.W && a.W % BM)) return -1;
     const dim3 grid(((a.M + BM - 1) / BM) * (a.N / BN));
-    hipLaunchKernelGGL((rowgemm16_row3_kernel<EMODE, BM, BN>), grid, dim3(512), 0, s, a);
+    if (sched == 1)
+        hipLaunchKernelGGL((rowgemm16_row3_kernel<EMODE, BM, BN, 1>), grid, dim3(512), 0, s, a);
+    else if (sched == 2)
+        hipLaunchKernelGGL((rowgemm16_row3_kernel<EMODE, BM, BN, 2>), grid, dim3(512), 0, s, a);
+    else
+        hipLaunchKernelGGL((rowgemm16_row3_kernel<EMODE, BM, BN>), grid, dim3(512), 0, s, a);
     return (int)hipGetLastError();
 }
 
@@ -402,10 +440,10 @@ static int rg16_go(const RowGemmArgs& a, hipStream_t s) {
 }
 
 template <int AMODE, int EMODE>
-static int rg16_tile(const RowGemmArgs& a, int tile, hipStream_t s) {
+static int rg16_tile(const RowGemmArgs& a, int tile, hipStream_t s, int sched) {
     if (tile == 19 || tile == 20) {
         if constexpr (AMODE == G_CONV3)
-            return tile == 19 ? rg16r3_go<EMODE, 256, 256>(a, s) : rg16r3_go<EMODE, 512, 128>(a, s);
+            return tile == 19 ? rg16r3_go<EMODE, 256, 256>(a, s, sched) : rg16r3_go<EMODE, 512, 128>(a, s, sched);
         return -1;
     }
 #define RG16_CASE(id, T) \
@@ -880,16 +918,16 @@ int launch_rowgemm16_xp(const RowGemmArgs& a, int xp, hipStream_t s) {
     return -2;
 }
 
-int launch_rowgemm16(const RowGemmArgs& a, int tile, hipStream_t s) {
+int launch_rowgemm16(const RowGemmArgs& a, int tile, hipStream_t s, int sched) {
     if (a.M < 1 || a.K != gather_taps(a.amode) * a.C || !a.a16 || !a.bt16 || !a.zero16) return -1;
     if (a.ascale || a.acoef || a.arelu) return -1;  // operands arrive prepared (k_to_bf16)
     if ((a.emode == E_STORE_BN) != (a.ey != nullptr)) return -1;
     if ((a.escale != nullptr) != (a.eshift != nullptr)) return -1;
-    if (a.amode == G_CONV3 && a.emode == E_STATS) return rg16_tile<G_CONV3, E_STATS>(a, tile, s);
-    if (a.amode == G_CONV3 && a.emode == E_STORE) return rg16_tile<G_CONV3, E_STORE>(a, tile, s);
-    if (a.amode == G_CONV3 && a.emode == E_STORE_BN) return rg16_tile<G_CONV3, E_STORE_BN>(a, tile, s);
-    if (a.amode == G_IDENT && a.emode == E_CONVT) return rg16_tile<G_IDENT, E_CONVT>(a, tile, s);
-    if (a.amode == G_UP2 && a.emode == E_STORE_BN) return rg16_tile<G_UP2, E_STORE_BN>(a, tile, s);
+    if (a.amode == G_CONV3 && a.emode == E_STATS) return rg16_tile<G_CONV3, E_STATS>(a, tile, s, sched);
+    if (a.amode == G_CONV3 && a.emode == E_STORE) return rg16_tile<G_CONV3, E_STORE>(a, tile, s, sched);
+    if (a.amode == G_CONV3 && a.emode == E_STORE_BN) return rg16_tile<G_CONV3, E_STORE_BN>(a, tile, s, sched);
+    if (a.amode == G_IDENT && a.emode == E_CONVT) return rg16_tile<G_IDENT, E_CONVT>(a, tile, s, sched);
+    if (a.amode == G_UP2 && a.emode == E_STORE_BN) return rg16_tile<G_UP2, E_STORE_BN>(a, tile, s, sched);
     return -1;
 }
 

@@ -133,6 +133,9 @@ struct Options {
                                // halo for 3x3 convs, 6 elsewhere; r04 config 4: 122.7 -> 124.8
                                // img/s with 20, 121.9 with 6)
     int rg16_n128_bn = 0;      // ... also for the short-K E_STORE_BN GEMMs (else 128x128)
+    int rg16_sched = 0;        // the bf16 halo kernel's schedule (0 = r04, 1 = waves 4..7 run each
+                               // stage's last tap after the next barrier, 2 = 1 + the DMA after the
+                               // first tap's reads; bit-identical)
     int rg16_r3 = 1;           // 256x256 3x3-conv GEMMs (W >= 16) on the tap-row halo kernel (tile 19;
                                // config 4: +0.9..1.2 % over three A/B pairs, r03)
     int wg16 = 1;              // bf16 3x3 wgrad on the LDS-DMA transposed-read kernel
@@ -202,6 +205,7 @@ const OptionDesc OPTION_TABLE[] = {
     {"rg16_tile", &Options::rg16_tile},
     {"rg16_bn_k", &Options::rg16_bn_k},
     {"rg16_r3", &Options::rg16_r3},
+    {"rg16_sched", &Options::rg16_sched},
     {"rg16_n128", &Options::rg16_n128},
     {"rg16_n128_bn", &Options::rg16_n128_bn},
     {"rg16_xp", &Options::rg16_xp},
@@ -1330,7 +1334,7 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
                 R = bn_groups(M);
                 const bool xp = c->opt.rg16_xp && tile == 4;
                 RUN(tlabel16("conv_fwd", tile, i), 2.0 * M * C.cout * 9 * C.cin,
-                    xp ? launch_rowgemm16_xp(g, c->opt.rg16_xp, s) : launch_rowgemm16(g, tile, s));
+                    xp ? launch_rowgemm16_xp(g, c->opt.rg16_xp, s) : launch_rowgemm16(g, tile, s, c->opt.rg16_sched));
                 return stats_finalize(c, L, p, i, R, M, training, prm, bn_run, bn_cnt);
             }
             R = bn_groups(M);
@@ -1406,7 +1410,7 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
             }
             const int tile = rg16_tile(c, g);
             RUN(tlabel16("convT_fwd", tile, 100 + k), 2.0 * g.M * g.N * g.K,
-                launch_rowgemm16(g, tile, s));
+                launch_rowgemm16(g, tile, s, c->opt.rg16_sched));
             return 0;
         }
         const int tile = pick_tile(c, T.cout, false, c->bf16, true);  // grid N = 4 cout
@@ -1722,7 +1726,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
                 const int tile = rg16_tile(c, g);
                 if (rows) *rows = bn_groups(P);
                 RUN(tlabel16("conv_dgrad", tile, i), 2.0 * P * C.cout * 9 * C.cin,
-                    launch_rowgemm16(g, tile, s));
+                    launch_rowgemm16(g, tile, s, c->opt.rg16_sched));
                 return 0;
             }
             if (rows) *rows = bn_groups(P);
@@ -1904,7 +1908,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
             const int tile = rg16_tile(c, g);
             *rows = bn_groups(Pin);
             RUN(tlabel16("convT_dgrad", tile, 100 + k), 2.0 * Pin * T.cin * 4 * T.cout,
-                launch_rowgemm16(g, tile, s));
+                launch_rowgemm16(g, tile, s, c->opt.rg16_sched));
             return 0;
         }
         const int tile = pick_tile(c, T.cin, true, c->bf16, true);
