@@ -312,12 +312,12 @@ def test_wg16_tap_row_bit_identical():
     x, t = inputs(43, 2, 256, 256)
     P = MO.make_params(47, 128, 5)
     outs = {}
-    for r3 in (0, 3, 4):
+    for r3 in (0, 3, 4, 5):
         m = _bf16_model(P, 128, 5)
         with options(m.flatten_().rt, wg16_r3=r3):
             outs[r3] = _bf16_step(m, x, t)
         del m
-    for r3 in (3, 4):
+    for r3 in (3, 4, 5):  # 5: four waves of 32 x 128 per tap (r05)
         _assert_same(outs[0], outs[r3], f"wg16_r3={r3} vs one-tap")
 
 

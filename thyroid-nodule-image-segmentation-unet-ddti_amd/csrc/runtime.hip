@@ -144,6 +144,7 @@ struct Options {
                                // decoder's concat straight into that conv's bf16 operand image
                                // (no f32 up half; its prep pass converts the skip half only)
     int wg16_r3 = 4;           // 3x3 layers with W % 64 == 0 on the tap-row bf16 weight gradient
+                               // (5, r05: four waves of 32 x 128 per tap, 3 stages)
                                // (tile 3 / 4 = three / four LDS stages; 0 = off; r04 config 4:
                                // 122.7 -> 124.5 / 125.2 img/s)
     int wg16t = 1;             // bf16 ConvT wgrad on the same kernel
@@ -1674,14 +1675,14 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
             int t = wg16_tile(c, C.cin, C.cout);
             // option wg16_r3: the tap-row kernel (three taps per block from one halo row)
             const int r3 = c->opt.wg16_r3;
-            if ((r3 == 3 || r3 == 4) && Wl % 64 == 0 && C.cin % 128 == 0 && C.cout % 128 == 0 &&
+            if (r3 >= 3 && r3 <= 5 && Wl % 64 == 0 && C.cin % 128 == 0 && C.cout % 128 == 0 &&
                 wc.pps % 64 == 0)
                 t = r3;
             int wbm = 0, wbn = 0, wst = 0;
             wgrad16g_tile_dims(t, &wbm, &wbn, &wst);
             char lb[96];
-            snprintf(lb, sizeof lb, "conv_wgrad/wg16%s_%dx%ds%d|%d", t == 3 || t == 4 ? "r3" : "", wbm,
-                     wbn, wst, i);
+            snprintf(lb, sizeof lb, "conv_wgrad/wg16%s_%dx%ds%d|%d",
+                     t == 3 || t == 4 ? "r3" : t >= 5 ? "r3w" : "", wbm, wbn, wst, i);
             RUN(lb, 2.0 * P * C.cout * 9 * C.cin, launch_wgrad16(w, t, s));
         } else {
             RUN(wlabel("conv_wgrad", wc, i), 2.0 * P * C.cout * 9 * C.cin, launch_wgrad(w, wc.tile, s));
