@@ -476,17 +476,20 @@ def test_mod_narrow_one_step_matches_golden(golden_dir, tag, base):
                       GRAD_TOL, tag)
 
 
+@pytest.mark.parametrize("n32", [0, 1])
 @pytest.mark.parametrize("base,depth,H,W", [(16, 5, 64, 96), (24, 4, 128, 64), (48, 6, 128, 256),
                                             (32, 4, 64, 64)])
-def test_mod_narrow_full_grads_vs_fp64(base, depth, H, W):
+def test_mod_narrow_full_grads_vs_fp64(base, depth, H, W, n32):
     """Every gradient element of narrow networks (base 32 native on the 32-channel tiles;
     16 / 24 padded to 32 and 48 to 64 inside the library) against the
     fp64 oracle, and the padding is invisible in the caller's arenas (torch-layout
     gradients, running stats).  At depth 6 the bottleneck BN sees 16 values per channel,
     where a near-zero ReLU input flips under any fp32 rounding change: the envelope is 2x
     the fp32 oracle's own error over x and x * (1 + 1e-7) (as tests/test_gpu_res.py),
-    floor 1e-2."""
+    floor 1e-2.  n32 = 1 (option x3_n32, r05): the 32- and 96-channel layers on the x3 kernels
+    too (128x32 row tile, 32-wide weight-gradient tiles)."""
     import unet_hip
+    from _helpers import options
     P = MO.make_params(7, base, depth)
     x, t = inputs(33, 2, H, W)
     ref = MO.train_step(P, MO.init_buffers(base, depth), None, x, t, depth=depth)
@@ -496,9 +499,10 @@ def test_mod_narrow_full_grads_vs_fp64(base, depth, H, W):
                          for k, v in MO.init_buffers(base, depth).items()},
                         None, x.double(), t.double(), depth=depth)
     m = hip_mod_model(P, DEV, base, depth)
-    logits = m(x.to(DEV))
-    losses = unet_hip.seg_losses(logits, t.to(DEV))
-    (losses[0] + losses[1]).backward()
+    with options(m.flatten_().rt, x3_n32=n32):
+        logits = m(x.to(DEV))
+        losses = unet_hip.seg_losses(logits, t.to(DEV))
+        (losses[0] + losses[1]).backward()
     assert rel_max(logits.detach().cpu().numpy(), ref["logits"].numpy()) <= LOGIT_TOL
     e32 = {k: max(norm_rel(g, r64["grads"][k]), norm_rel(refp["grads"][k], r64["grads"][k]))
            for k, g in ref["grads"].items()}

@@ -545,7 +545,10 @@ using TX0 = TileX3<256, 128, 64, 64, 2, 1, 1>;
 using TX1 = TileX3<128, 128, 64, 64, 2, 1, 1>;
 using TX2 = TileX3<128, 64, 64, 32, 2, 2, 1>;
 using TX3 = TileX3<256, 64, 64, 32, 2, 1, 1>;
-#define ROWGEMM_X3_TILES(X) X(0, TX0) X(1, TX1) X(2, TX2) X(3, TX3)
+// 7 = 128x32 (2 waves of 64x32, two blocks per CU): the 32-channel layers of the reference
+// grid's narrow widths (option x3_n32, r05)
+using TX7 = TileX3<128, 32, 64, 32, 2, 1, 1>;  // (60 KB: LDS allows two blocks per CU)
+#define ROWGEMM_X3_TILES(X) X(0, TX0) X(1, TX1) X(2, TX2) X(3, TX3) X(7, TX7)
 
 template <int AMODE, int EMODE, class T, int XP = 0>
 static int x3_go(const RowGemmArgs& a, hipStream_t s) {
@@ -1057,7 +1060,11 @@ __global__ __launch_bounds__((BM / 32) * (BN / 32) * 64, OCC) void wgrad_x3_row3
 // three LDS stages of 32 pixels
 using WX0 = WTileX3<128, 128, 64, 32, 3, 1>;
 using WX1 = WTileX3<64, 64, 32, 32, 3, 1>;
-#define WGRAD_X3_TILES(X) X(0, WX0) X(1, WX1)
+// 8 / 9 / 10 = 64x32 / 32x64 / 32x32 (waves of 32x32): 32-channel operands (option x3_n32, r05)
+using WX8 = WTileX3<64, 32, 32, 32, 3, 1>;
+using WX9 = WTileX3<32, 64, 32, 32, 3, 1>;
+using WX10 = WTileX3<32, 32, 32, 32, 3, 1>;
+#define WGRAD_X3_TILES(X) X(0, WX0) X(1, WX1) X(8, WX8) X(9, WX9) X(10, WX10)
 
 template <int AMODE, int BMODE, class T>
 static int wx3_go(const WgradArgs& a, hipStream_t s) {
@@ -1270,10 +1277,14 @@ int k_to_x3(const float* src, int ld, int off, int C, const float* scale, const 
     return (int)hipGetLastError();
 }
 
+// tap-row tiles (BM ci x BN co per tap, three taps per block): 2 = 64x128, 3 = 128x64, 4 = 64x64,
+// 5 = 32x64, 6 = 64x32, 7 = 32x32 (5..7: option x3_n32, r05)
+static const int WX3R3_DIMS[8][2] = {{0, 0}, {0, 0}, {64, 128}, {128, 64}, {64, 64}, {32, 64}, {64, 32}, {32, 32}};
+
 int wgrad_x3_tile_dims(int tile, int* bm, int* bn) {
-    if (tile >= 2 && tile <= 4) {  // tap-row: BM x BN per tap, three taps per block
-        *bm = tile == 3 ? 128 : 64;
-        *bn = tile == 2 ? 128 : 64;
+    if (tile >= 2 && tile <= 7) {
+        *bm = WX3R3_DIMS[tile][0];
+        *bn = WX3R3_DIMS[tile][1];
         return 0;
     }
 #define WX3_DIMS(id, T) \
@@ -1295,7 +1306,7 @@ int wgrad_x3_tile_dims(int tile, int* bm, int* bn) {
 int launch_wgrad_x3(const WgradArgs& a, int tile, hipStream_t s, int sched) {
     if (a.ascale || a.bcoef || a.bias_slab || !a.zero16 || a.P < 1) return -1;
     if (a.aoff % 32 || a.boff % 32 || a.lda % 32 || a.ldb % 32) return -1;
-    if (tile >= 2 && tile <= 4) {  // tap-row kernel: 3x3 convs, W % 32 == 0
+    if (tile >= 2 && tile <= 7) {  // tap-row kernel: 3x3 convs, W % 32 == 0
         int bm = 0, bn = 0;
         wgrad_x3_tile_dims(tile, &bm, &bn);
         if (a.amode != G_CONV3 || a.bmode != G_IDENT || a.Mw != 9 * a.CA || a.Nw != a.CB ||
@@ -1310,15 +1321,24 @@ int launch_wgrad_x3(const WgradArgs& a, int tile, hipStream_t s, int sched) {
             hipLaunchKernelGGL((wgrad_x3_row3_kernel<64, 128>), grid, dim3(512), 0, s, a);
         else if (tile == 3)
             hipLaunchKernelGGL((wgrad_x3_row3_kernel<128, 64>), grid, dim3(512), 0, s, a);
-        else  // 64 x 64: four waves, two LDS stages, two blocks per CU
+        else if (tile == 4)  // 64 x 64: four waves, two LDS stages, two blocks per CU
             hipLaunchKernelGGL((wgrad_x3_row3_kernel<64, 64, 2, 2>), grid, dim3(256), 0, s, a);
+        else if (tile == 5)  // the 32-channel tiles: one or two waves, three stages (LDS: 2-4 blocks per CU)
+            hipLaunchKernelGGL((wgrad_x3_row3_kernel<32, 64, 3, 1>), grid, dim3(128), 0, s, a);
+        else if (tile == 6)
+            hipLaunchKernelGGL((wgrad_x3_row3_kernel<64, 32, 3, 1>), grid, dim3(128), 0, s, a);
+        else
+            hipLaunchKernelGGL((wgrad_x3_row3_kernel<32, 32, 3, 1>), grid, dim3(64), 0, s, a);
         return (int)hipGetLastError();
     }
-#define WX3G(AM, BMD)                                      \
-    do {                                                   \
-        if (tile == 0) return wx3_go<AM, BMD, WX0>(a, s);  \
-        if (tile == 1) return wx3_go<AM, BMD, WX1>(a, s);  \
-        return -1;                                         \
+#define WX3G(AM, BMD)                                        \
+    do {                                                     \
+        if (tile == 0) return wx3_go<AM, BMD, WX0>(a, s);    \
+        if (tile == 1) return wx3_go<AM, BMD, WX1>(a, s);    \
+        if (tile == 8) return wx3_go<AM, BMD, WX8>(a, s);    \
+        if (tile == 9) return wx3_go<AM, BMD, WX9>(a, s);    \
+        if (tile == 10) return wx3_go<AM, BMD, WX10>(a, s);  \
+        return -1;                                           \
     } while (0)
     if (a.amode == G_CONV3 && a.bmode == G_IDENT) WX3G(G_CONV3, G_IDENT);
     if (a.amode == G_IDENT && a.bmode == G_UP2) WX3G(G_IDENT, G_UP2);

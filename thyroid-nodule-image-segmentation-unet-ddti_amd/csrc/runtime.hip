@@ -169,6 +169,7 @@ struct Options {
     int x3_r3 = 1;             // its 256x128 3x3 GEMMs on the tap-row halo kernel (tile 4)
     int x3_r3_sched = 0;       // the halo kernel's wave schedule (kernels_gemm_x3.hip X3R3Sched:
                                // who issues the LDS-DMA, stagger of waves 4..7; bit-identical)
+    int x3_n32 = 0;            // x3 also for 32-multiple channel counts (r05; narrow widths)
     int x3_n64_r3 = 5;         // halo tile of the 64-output 3x3 GEMMs: 5 = 256x64 (8 waves, one
                                // block per CU), 6 = 128x64 (4 waves, two blocks per CU)
     int x3_wsched = 0;         // the 64x128 tap-row weight gradient's schedule (0 = r04, 1 = four
@@ -225,6 +226,7 @@ const OptionDesc OPTION_TABLE[] = {
     {"x3_n64", &Options::x3_n64},
     {"x3_r3", &Options::x3_r3},
     {"x3_r3_sched", &Options::x3_r3_sched},
+    {"x3_n32", &Options::x3_n32},
     {"x3_n64_r3", &Options::x3_n64_r3},
     {"x3_wsched", &Options::x3_wsched},
 };
@@ -768,8 +770,11 @@ bool convt_wg16_on(const unet_ctx* c, int cin, int cout) {
 // weight-gradient GEMMs on x3 images (exact three-way bf16 splits of the f32 operands, six
 // MFMA products, split f32 accumulators: fp64 error ~3x below the f32 MFMA kernels',
 // profiles/r04_x3_probe_*.txt).  The residual network's 1x1 skip GEMMs keep the f32 kernels.
+// Option x3_n32 (r05) extends it to 32-multiple channel counts (the reference grid's narrow
+// widths: 32 / 96 channels) on the 128x32 row tile and the 32-wide weight-gradient tiles.
 bool x3_conv_on(const unet_ctx* c, int cin, int cout) {
-    return c->opt.x3 && !c->bf16 && cin % 64 == 0 && cout % 64 == 0;
+    const int q = c->opt.x3_n32 ? 32 : 64;
+    return c->opt.x3 && !c->bf16 && cin % q == 0 && cout % q == 0;
 }
 bool x3_convt_on(const unet_ctx* c, int cin, int cout) { return x3_conv_on(c, cin, cout); }
 
@@ -783,7 +788,7 @@ int x3_tile(const unet_ctx* c, const RowGemmArgs& g) {
     };
     // tile 4: the tap-row halo kernel (3x3 convs on rows of 16 .. 256k pixels, option x3_r3)
     const bool r3ok = g.amode == G_CONV3 && g.W >= 16 && (256 % g.W == 0 || g.W % 256 == 0);
-    if (c->opt.x3_tile >= 0 && fits(c->opt.x3_tile) && (c->opt.x3_tile < 4 || r3ok))
+    if (c->opt.x3_tile >= 0 && fits(c->opt.x3_tile) && (c->opt.x3_tile < 4 || c->opt.x3_tile > 6 || r3ok))
         return c->opt.x3_tile;
     if (g.N % 128 == 0 && fits(0)) {
         const int64_t blocks = (int64_t)(g.M + 255) / 256 * (g.N / 128);
@@ -792,8 +797,9 @@ int x3_tile(const unet_ctx* c, const RowGemmArgs& g) {
     }
     // 64 outputs: a halo tile (5 = 256 x 64, one block per CU; 6 = 128 x 64, two blocks per
     // CU: option x3_n64_r3) where the 256-row grid fills the chip
-    if (c->opt.x3_r3 && r3ok && (int64_t)(g.M + 255) / 256 >= 512)
+    if (g.N % 64 == 0 && c->opt.x3_r3 && r3ok && (int64_t)(g.M + 255) / 256 >= 512)
         return c->opt.x3_n64_r3 == 6 ? 6 : 5;
+    if (g.N % 64) return 7;  // 32-multiple outputs (option x3_n32): 128 x 32
     return c->opt.x3_n64;
 }
 
@@ -810,17 +816,26 @@ WgradCfg x3_wgrad_cfg(const unet_ctx* c, int CA, int tapsA, int CB, int tapsB, i
     if (r3 && CA % 64 == 0 && CB % 128 == 0) w.tile = 2;
     else if (r3 && CA % 128 == 0 && CB % 64 == 0) w.tile = 3;
     else if (r3 && CA % 64 == 0 && CB % 64 == 0) w.tile = 4;
+    if (CA % 64 || CB % 64) {  // 32-channel operands (option x3_n32): tap-row 32x64 / 64x32 /
+                               // 32x32 (5 / 6 / 7), one-tap 64x32 / 32x64 / 32x32 (8 / 9 / 10)
+        const int k = CA % 64 == 0 ? 1 : CB % 64 == 0 ? 0 : 2;  // 0: BM 32, 1: BN 32, 2: both
+        w.tile = r3 ? (k == 0 ? 5 : k == 1 ? 6 : 7) : (k == 1 ? 8 : k == 0 ? 9 : 10);
+    }
     if (c->opt.x3_wtile >= 0) {
         int bm = 0, bn = 0;
         const int t = c->opt.x3_wtile;
-        if (wgrad_x3_tile_dims(t, &bm, &bn) == 0 && CA % bm == 0 && CB % bn == 0 && (t < 2 || r3))
+        if (wgrad_x3_tile_dims(t, &bm, &bn) == 0 && CA % bm == 0 && CB % bn == 0 && (t < 2 || t > 7 || r3))
             w.tile = t;
     }
     wgrad_x3_tile_dims(w.tile, &w.bm, &w.bn);
     w.bkp = 32;
-    const int64_t tiles = w.tile >= 2 ? (int64_t)(CA / w.bm) * 3 * (CB / w.bn)
-                                      : (int64_t)(tapsA * CA / w.bm) * (tapsB * CB / w.bn);
-    const int64_t target = (int64_t)c->opt.x3_wblocks * (w.tile == 1 ? 4 : w.tile == 4 ? 2 : 1);
+    const bool tap_row = w.tile >= 2 && w.tile <= 7;
+    const int64_t tiles = tap_row ? (int64_t)(CA / w.bm) * 3 * (CB / w.bn)
+                                  : (int64_t)(tapsA * CA / w.bm) * (tapsB * CB / w.bn);
+    // blocks per 128x128 one-tap block of work: by area (one-tap), half that (tap-row)
+    const int area = std::max(1, 16384 / (w.bm * w.bn));
+    const int64_t target = (int64_t)c->opt.x3_wblocks *
+                           (w.tile <= 1 ? area : tap_row ? std::max(1, area / 2) : area);
     int64_t splits = std::max<int64_t>(1, (target + tiles - 1) / tiles);
     int64_t pps = (P + splits - 1) / splits;
     pps = (pps + 255) / 256 * 256;
@@ -846,7 +861,7 @@ void use_x3(const Plan& p, RowGemmArgs& g, const uint16_t* img, int C, const uin
 
 std::string x3wlabel(const char* fam, const WgradCfg& w, int layer) {
     char b[112];
-    snprintf(b, sizeof b, "%s/wx3%s_%dx%d|%d", fam, w.tile >= 2 ? "r3" : "", w.bm, w.bn, layer);
+    snprintf(b, sizeof b, "%s/wx3%s_%dx%d|%d", fam, w.tile >= 2 && w.tile <= 7 ? "r3" : "", w.bm, w.bn, layer);
     return b;
 }
 
@@ -854,7 +869,7 @@ std::string xlabel(const char* fam, int tile, int layer) {
     int bm = 0, bn = 0;
     rowgemm_x3_tile_dims(tile, &bm, &bn);
     char b[112];
-    snprintf(b, sizeof b, "%s/x3%s_%dx%d|%d", fam, tile >= 4 ? "r3" : "", bm, bn, layer);
+    snprintf(b, sizeof b, "%s/x3%s_%dx%d|%d", fam, tile >= 4 && tile <= 6 ? "r3" : "", bm, bn, layer);
     return b;
 }
 
