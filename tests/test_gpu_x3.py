@@ -36,12 +36,13 @@ def _to64(d):
     return {k: (v.double() if v.is_floating_point() else v.clone()) for k, v in d.items()}
 
 
-# Absolute bars against the fp64 oracle on the GPU's own ReLU branches (measured r05 on
-# MI355X: profiles/r05_x3_masked_bars.txt).  Conv / ConvT weight gradients carry no
-# cancellation; the conv biases ahead of ReLU -> BN (models/model.py:36-38) get sums that
-# largely cancel (the BN input gradient sums to ~0 over the pixels), so their relative
-# rounding noise is larger; every tensor is held to SURVEY §8c's 1e-2 as well.
-W_BAR, B_BAR, ALL_BAR = 1e-4, 2e-3, 1e-2
+# Absolute bars against the fp64 oracle on the GPU's own ReLU / max-pool branches (measured r05
+# on MI355X, profiles/r05_x3_masked_bars.txt: worst weight gradient 4.9e-6 (x3) / 1.3e-5 (f32
+# MFMA) at 128^2, 1.3e-5 / 1.4e-5 (halo / one-tap x3) at 256^2; worst bias / BN gradient
+# 6.1e-6 .. 2.4e-5).  The conv biases ahead of ReLU -> BN (models/model.py:36-38) get sums that
+# largely cancel (the BN input gradient sums to ~0 over the pixels), so their relative rounding
+# noise is the larger; every tensor is also held to SURVEY §8c's 1e-2.
+W_BAR, B_BAR, ALL_BAR = 1e-4, 2e-4, 1e-2
 
 
 def _relu_masks(m, x):

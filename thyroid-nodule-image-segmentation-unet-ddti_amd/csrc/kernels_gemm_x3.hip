@@ -1093,20 +1093,28 @@ __device__ __forceinline__ void x3_store8(const float (&v)[8], uint16_t* d) {
     *(x3_u16x8*)(d + 64) = l;
 }
 
+// Rows per block of the two image passes: 256, or fewer where that leaves the grid short of
+// ~1024 blocks (the deep levels: 8k rows x 1024 channels made 32 blocks, 1.2 TB/s;
+// profiles/r05_x3_pass_exp.txt).  bn_dz_x3's bias partials come one row per block, so the
+// caller sizes its reduction with x3_dz_blocks (the same rule).
+__host__ __device__ inline int x3_rows_per_block(int64_t P) {
+    return P >= 256 * 1024 ? 256 : P >= 128 * 1024 ? 128 : 64;
+}
+constexpr int X3_RIF = 4;  // rows in flight per thread (all loads before any arithmetic)
+
 // x3 image of op(src) (f32 [P][ld] at channel offset off, C channels; scale / shift: the
 // BN affine, ReLU on channels < relu) into dst [P][dld / 32][3][32] at channel offset doff.
-// A block covers X3_PREP_RPB rows; thread t handles channel octet t % (C / 8) of rows
-// t / (C / 8) + k 256 / (C / 8), two rows in flight; the affine is loaded once per thread.
-constexpr int X3_PREP_RPB = 256;
+// A block covers rpb rows; thread t handles channel octet t % (C / 8) of rows t / (C / 8) +
+// k 256 / (C / 8), X3_RIF rows in flight; the affine is loaded once per thread.
 __global__ __launch_bounds__(256) void to_x3_kernel(const float* __restrict__ src, int ld, int off, int C,
                                                     const float* __restrict__ scale,
                                                     const float* __restrict__ shift, int relu, int64_t P,
-                                                    uint16_t* __restrict__ dst, int dld, int doff) {
+                                                    uint16_t* __restrict__ dst, int dld, int doff, int rpb) {
     const int g8 = C / 8, G = min(g8, 256);  // octets per pass (C > 2048: several passes)
     const int r0 = threadIdx.x / G, rstep = 256 / G;
     if (r0 >= rstep) return;
-    const int64_t mb = (int64_t)blockIdx.x * X3_PREP_RPB;
-    const int64_t me = min(mb + X3_PREP_RPB, P);
+    const int64_t mb = (int64_t)blockIdx.x * rpb;
+    const int64_t me = min(mb + rpb, P);
     for (int oct = threadIdx.x % G; oct < g8; oct += G) {
         const int c = oct * 8;
         float sc[8], sh[8];
@@ -1123,30 +1131,33 @@ __global__ __launch_bounds__(256) void to_x3_kernel(const float* __restrict__ sr
         }
         const int cc = doff + c;
         uint16_t* dcol = dst + (cc >> 5) * 96 + (cc & 31);
-        auto load = [&](int64_t m, float (&v)[8]) {
-            const float* sp = src + m * ld + off + c;
-            const f32x4 v0 = *(const f32x4*)sp, v1 = *(const f32x4*)(sp + 4);
+        for (int64_t m = mb + r0; m < me; m += X3_RIF * rstep) {
+            f32x4 v[X3_RIF][2];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                v[j] = v0[j];
-                v[4 + j] = v1[j];
-            }
-            if (scale) {
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    float t = __builtin_fmaf(sc[j], v[j], sh[j]);
-                    if (c + j < relu) t = fmaxf(t, 0.f);
-                    v[j] = t;
+            for (int i = 0; i < X3_RIF; ++i) {
+                const int64_t mi = m + i * rstep;
+                if (mi < me) {
+                    const float* sp = src + mi * ld + off + c;
+                    v[i][0] = *(const f32x4*)sp;
+                    v[i][1] = *(const f32x4*)(sp + 4);
                 }
             }
-        };
-        for (int64_t m = mb + r0; m < me; m += 2 * rstep) {
-            const int64_t m2 = m + rstep;
-            float v[8], w[8];
-            load(m, v);
-            if (m2 < me) load(m2, w);
-            x3_store8(v, dcol + m * 3 * (int64_t)dld);
-            if (m2 < me) x3_store8(w, dcol + m2 * 3 * (int64_t)dld);
+#pragma unroll
+            for (int i = 0; i < X3_RIF; ++i) {
+                const int64_t mi = m + i * rstep;
+                if (mi >= me) break;
+                float w[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    float t = v[i][j >> 2][j & 3];
+                    if (scale) {
+                        t = __builtin_fmaf(sc[j], t, sh[j]);
+                        if (c + j < relu) t = fmaxf(t, 0.f);
+                    }
+                    w[j] = t;
+                }
+                x3_store8(w, dcol + mi * 3 * (int64_t)dld);
+            }
         }
     }
 }
@@ -1154,19 +1165,20 @@ __global__ __launch_bounds__(256) void to_x3_kernel(const float* __restrict__ sr
 // dz = [!mask || y > 0] (A do + B (y - mean) + C) per channel (bn_dz4, the f32 path's
 // rounding order) as the x3 image dz3 [P][C / 32][3][32]; with bpart, also the per-block
 // column sums of dz (the conv bias gradient; k_sum_partials adds the G rows in f64).  A
-// block covers RPB rows; thread t handles channel octet t % (C / 8) of rows t / (C / 8) +
-// k 256 / (C / 8).
-constexpr int X3_DZ_RPB = 256;
+// block covers rpb rows (x3_rows_per_block); thread t handles channel octet t % (C / 8) of
+// rows t / (C / 8) + k 256 / (C / 8), X3_RIF rows in flight (the column sums add each thread's
+// rows in ascending order).
 __global__ __launch_bounds__(256) void bn_dz_x3_kernel(const float* __restrict__ d, const float* __restrict__ y,
                                                        int ld, int off, int64_t P, int C,
                                                        const float* __restrict__ coef, int mask,
-                                                       uint16_t* __restrict__ dz3, float* __restrict__ bpart) {
+                                                       uint16_t* __restrict__ dz3, float* __restrict__ bpart,
+                                                       int rpb) {
     __shared__ float red[256 * 8];
     const int g8 = C / 8, G = min(g8, 256);  // octets per pass (bias sums: C <= 2048, one pass)
     const int r0 = threadIdx.x / G, rstep = 256 / G;
     const bool active = r0 < rstep;  // threads past the last complete row group idle
-    const int64_t mb = (int64_t)blockIdx.x * X3_DZ_RPB;
-    const int64_t me = min(mb + X3_DZ_RPB, P);
+    const int64_t mb = (int64_t)blockIdx.x * rpb;
+    const int64_t me = min(mb + rpb, P);
     float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     for (int oct = threadIdx.x % G; active && oct < g8; oct += G) {
         const int c = oct * 8;
@@ -1178,39 +1190,33 @@ __global__ __launch_bounds__(256) void bn_dz_x3_kernel(const float* __restrict__
             kc[h] = *(const f32x4*)(coef + 2 * C + c + 4 * h);
             km[h] = *(const f32x4*)(coef + 3 * C + c + 4 * h);
         }
-        // two rows in flight (loads of both before either's arithmetic); the column sums add
-        // the rows in ascending order either way
-        auto dz8 = [&](const f32x4 (&dv)[2], const f32x4 (&yv)[2], float (&v)[8]) {
+        for (int64_t m = mb + r0; m < me; m += X3_RIF * rstep) {
+            f32x4 dv[X3_RIF][2], yv[X3_RIF][2];
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const f32x4 r = bn_dz4(ka[h], dv[h], kb[h], yv[h], km[h], kc[h]);
+            for (int i = 0; i < X3_RIF; ++i) {
+                const int64_t mi = m + i * rstep;
+                if (mi < me) {
 #pragma unroll
-                for (int j = 0; j < 4; ++j) v[4 * h + j] = (!mask || yv[h][j] > 0.f) ? r[j] : 0.f;
-            }
-        };
-        for (int64_t m = mb + r0; m < me; m += 2 * rstep) {
-            const int64_t m2 = m + rstep;
-            const bool two = m2 < me;
-            f32x4 dv[2], yv[2], dw[2], yw[2];
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                dv[h] = *(const f32x4*)(d + m * C + c + 4 * h);
-                yv[h] = *(const f32x4*)(y + m * ld + off + c + 4 * h);
-                if (two) {
-                    dw[h] = *(const f32x4*)(d + m2 * C + c + 4 * h);
-                    yw[h] = *(const f32x4*)(y + m2 * ld + off + c + 4 * h);
+                    for (int h = 0; h < 2; ++h) {
+                        dv[i][h] = *(const f32x4*)(d + mi * C + c + 4 * h);
+                        yv[i][h] = *(const f32x4*)(y + mi * ld + off + c + 4 * h);
+                    }
                 }
             }
-            float v[8];
-            dz8(dv, yv, v);
 #pragma unroll
-            for (int j = 0; j < 8; ++j) cs[j] += v[j];
-            x3_store8(v, dz3 + m * 3 * (int64_t)C + (c >> 5) * 96 + (c & 31));
-            if (two) {
-                dz8(dw, yw, v);
+            for (int i = 0; i < X3_RIF; ++i) {
+                const int64_t mi = m + i * rstep;
+                if (mi >= me) break;
+                float v[8];
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const f32x4 r = bn_dz4(ka[h], dv[i][h], kb[h], yv[i][h], km[h], kc[h]);
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) v[4 * h + j] = (!mask || yv[i][h][j] > 0.f) ? r[j] : 0.f;
+                }
 #pragma unroll
                 for (int j = 0; j < 8; ++j) cs[j] += v[j];
-                x3_store8(v, dz3 + m2 * 3 * (int64_t)C + (c >> 5) * 96 + (c & 31));
+                x3_store8(v, dz3 + mi * 3 * (int64_t)C + (c >> 5) * 96 + (c & 31));
             }
         }
     }
@@ -1271,9 +1277,10 @@ int k_to_x3(const float* src, int ld, int off, int C, const float* scale, const 
             int relu, int64_t P, uint16_t* dst, int dld, int doff, hipStream_t s) {
     if (C % 32 || dld % 32 || doff % 32 || ld % 4 || off % 4) return -1;
     if (P < 1) return -1;
-    const int blocks = (int)((P + X3_PREP_RPB - 1) / X3_PREP_RPB);
+    const int rpb = x3_rows_per_block(P);
+    const int blocks = (int)((P + rpb - 1) / rpb);
     hipLaunchKernelGGL(to_x3_kernel, dim3(blocks), dim3(256), 0, s, src, ld, off, C, scale, shift,
-                       relu, P, dst, dld, doff);
+                       relu, P, dst, dld, doff, rpb);
     return (int)hipGetLastError();
 }
 
@@ -1346,13 +1353,16 @@ int launch_wgrad_x3(const WgradArgs& a, int tile, hipStream_t s, int sched) {
     return -1;
 }
 
-int x3_dz_blocks(int64_t P) { return (int)((P + X3_DZ_RPB - 1) / X3_DZ_RPB); }
+int x3_dz_blocks(int64_t P) {
+    const int rpb = x3_rows_per_block(P);
+    return (int)((P + rpb - 1) / rpb);
+}
 
 int k_bn_dz_x3(const float* d, const float* y, int ld, int off, int64_t P, int C, const float* coef,
                int mask, uint16_t* dz3, float* bpart, hipStream_t s) {
     if (C % 32 || (bpart && C > 2048) || ld % 4 || off % 4 || P < 1) return -1;
     hipLaunchKernelGGL(bn_dz_x3_kernel, dim3(x3_dz_blocks(P)), dim3(256), 0, s, d, y, ld, off, P, C, coef,
-                       mask, dz3, bpart);
+                       mask, dz3, bpart, x3_rows_per_block(P));
     return (int)hipGetLastError();
 }
 

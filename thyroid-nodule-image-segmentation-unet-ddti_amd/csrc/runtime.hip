@@ -801,7 +801,8 @@ int x3_tile(const unet_ctx* c, const RowGemmArgs& g) {
     // CU: option x3_n64_r3) where the 256-row grid fills the chip
     if (g.N % 64 == 0 && c->opt.x3_r3 && r3ok && (int64_t)(g.M + 255) / 256 >= 512)
         return c->opt.x3_n64_r3 == 6 ? 6 : 5;
-    if (g.N % 64) return 7;  // 32-multiple outputs (option x3_n32): 128 x 32
+    // 32-multiple outputs, or a ConvT whose cout is not a 64-tile fit (option x3_n32): 128 x 32
+    if (g.N % 64 || !fits(c->opt.x3_n64)) return 7;
     return c->opt.x3_n64;
 }
 

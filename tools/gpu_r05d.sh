@@ -9,7 +9,7 @@ timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method threa
 rc=$?
 echo "n32 tests rc=$rc"; grep -E "PASS|FAIL|Error|assert" gpurun_out/$TAG.n32.log | tail -30
 [ $rc -ne 0 ] && [ $rc -ne 1 ] && exit $rc
-for B in 16 24 32 48; do
+for B in ${BASES:-16 24 32 48}; do
   for N in 1 0; do
     timeout -k 10 300 python bench.py --config res --base $B --depth 4 --steps 6 --warmup 2 --opt x3_n32=$N \
       > gpurun_out/$TAG.res${B}n$N.json 2> gpurun_out/$TAG.res${B}n$N.err

@@ -4,7 +4,7 @@ set -u
 cd $GRAFT_REPO_ROOT
 TAG=${1:-suite}
 timeout -k 10 800 python -u -m pytest tests -m gpu -v --timeout 240 --timeout-method thread \
-  -p no:cacheprovider --durations=12 > gpurun_out/$TAG.pytest.log 2>&1
+  -p no:cacheprovider --durations=12 -rP > gpurun_out/$TAG.pytest.log 2>&1
 rc=$?
 echo "pytest rc=$rc"; grep -E "passed|failed|error" gpurun_out/$TAG.pytest.log | tail -3
 grep -E "^FAILED|^ERROR" gpurun_out/$TAG.pytest.log | head -20
