@@ -241,7 +241,9 @@ int unet_timing_read(unet_ctx* ctx, int i, const char** family, int64_t* launche
 /* Debug/test view into a workspace: byte offset of an intermediate tensor.
  * kind: 0 y[i] (post-ReLU conv output, NHWC, channel stride *ld, channel offset *off),
  *       1 BN scale[i], 2 BN shift[i], 3 BN batch mean[i], 4 BN invstd[i],
- *       5 pooled[l] (NHWC dense), 6 concat buffer[l] (NHWC, 2*64<<l channels),
+ *       5 pooled[l] (NHWC dense; not written when the next conv runs on the x3 kernels:
+ *       the max-pool then stores that conv's x3 operand image instead), 6 concat buffer[l]
+ *       (NHWC, 2*64<<l channels),
  *       7 d(concat)[l] of the last backward, 8 max-pool winner index[l] (uint8 NHWC dense,
  *       window position 0..3 in torch's scan order).  *count = elements (pixels*ld for NHWC). */
 int unet_debug_view(unet_ctx* ctx, int N, int H, int W, int training, int kind, int index,

@@ -321,6 +321,38 @@ __device__ __forceinline__ void row_epilogue(const RowGemmArgs& p, f32x16 (&acc)
             co_[nt] = co;
             bb[nt] = p.bias[co];
         }
+        if (p.out3) {
+            // x3 split straight into the consumer's operand image (as k_to_x3), two channels per
+            // store: lanes li, li ^ 1 hold neighbouring columns of the same rows, so for each
+            // pair of accumulator rows (r, r + 1) the even lane stores row r and the odd lane row
+            // r + 1, each for both columns (4-B stores, half the 2-B store instructions)
+            const int odd = li & 1;
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                for (int r2 = 0; r2 < 8; ++r2) {
+                    const int row = 2 * r2 + odd;
+                    const int m = m0 + wm * WM + mt * 32 + (row & 3) + 8 * (row >> 2) + 4 * lh;
+                    const Pix q = decode_fast(m < p.M ? m : 0, H, W, rH, rW);
+                    const size_t ob = (size_t)(q.img * 2 * H + 2 * q.y) * (2 * W) + 2 * q.x;
+#pragma unroll
+                    for (int nt = 0; nt < NT; ++nt) {
+                        const float v0 = acc[mt][nt][2 * r2] + bb[nt], v1 = acc[mt][nt][2 * r2 + 1] + bb[nt];
+                        const float recv = __shfl_xor(odd ? v0 : v1, 1);
+                        const float ve = odd ? recv : v0, vo = odd ? v1 : recv;  // columns li & ~1, li | 1
+                        if (m >= p.M) continue;
+                        uint16_t he, me, le, ho, mo, lo;
+                        x3_split(ve, X3CvtDev{}, he, me, le);
+                        x3_split(vo, X3CvtDev{}, ho, mo, lo);
+                        const int ch = p.ooff + co_[nt] - odd;
+                        uint16_t* d = p.out3 + (ob + coff[nt]) * 3 * (size_t)p.ldo + (ch >> 5) * 96 + (ch & 31);
+                        *(uint32_t*)d = (uint32_t)he | ((uint32_t)ho << 16);
+                        *(uint32_t*)(d + 32) = (uint32_t)me | ((uint32_t)mo << 16);
+                        *(uint32_t*)(d + 64) = (uint32_t)le | ((uint32_t)lo << 16);
+                    }
+                }
+            return;
+        }
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
@@ -329,19 +361,7 @@ __device__ __forceinline__ void row_epilogue(const RowGemmArgs& p, f32x16 (&acc)
                 if (m >= p.M) continue;
                 const Pix q = decode_fast(m, H, W, rH, rW);
                 const size_t ob = (size_t)(q.img * 2 * H + 2 * q.y) * (2 * W) + 2 * q.x;
-                if (p.out3) {  // x3 split straight into the consumer's operand image (as k_to_x3)
-#pragma unroll
-                    for (int nt = 0; nt < NT; ++nt) {
-                        const float v = acc[mt][nt][r] + bb[nt];
-                        uint16_t h, mm, lo;
-                        x3_split(v, X3CvtDev{}, h, mm, lo);
-                        const int ch = p.ooff + co_[nt];
-                        uint16_t* d = p.out3 + (ob + coff[nt]) * 3 * (size_t)p.ldo + (ch >> 5) * 96 + (ch & 31);
-                        d[0] = h;
-                        d[32] = mm;
-                        d[64] = lo;
-                    }
-                } else if (p.out16) {  // bf16 straight into the consumer's operand image (RNE, as k_to_bf16)
+                if (p.out16) {  // bf16 straight into the consumer's operand image (RNE, as k_to_bf16)
 #pragma unroll
                     for (int nt = 0; nt < NT; ++nt)
                         ((__bf16*)p.out16)[(ob + coff[nt]) * p.ldo + p.ooff + co_[nt]] =

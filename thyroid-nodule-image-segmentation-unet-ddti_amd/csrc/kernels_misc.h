@@ -33,7 +33,8 @@ int k_bn_finalize_eval(int C, const float* gamma, const float* beta, const float
                        const float* rvar, float eps, float* scale, float* shift, hipStream_t s);
 // relu / mscale+mshift: BN -> ReLU order (mod.py:46-47), see the kernels.
 int k_maxpool_bn(const float* y, int ld, int off, const float* scale, const float* shift, int relu,
-                 int N, int H, int W, int C, float* out, uint8_t* idx, hipStream_t s);
+                 int N, int H, int W, int C, float* out, uint8_t* idx, hipStream_t s,
+                 uint16_t* out3 = nullptr);
 int k_maxpool_bwd(const float* dp, const uint8_t* idx, const float* dskip, int ldskip, int offskip,
                   const float* y, int ldy, int offy, const float* mscale, const float* mshift,
                   int N, int H, int W, int C, float* dout, float* partial, int G, hipStream_t s);

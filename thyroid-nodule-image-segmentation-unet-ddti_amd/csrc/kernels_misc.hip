@@ -6,7 +6,7 @@
 // reductions (no float atomics), so two runs of the same inputs are bit-identical.
 // Layout everywhere: NHWC, channel stride `ld`, channel offset `off` (concat slices).
 #include "kernels_misc.h"
-#include "gemm_common.h"  // Pix, decode, pix_advance
+#include "gemm_common.h"  // Pix, decode, pix_advance (and x3_split.h)
 
 namespace {
 
@@ -451,7 +451,8 @@ __global__ void bn_finalize_eval_kernel(int C, const float* __restrict__ gamma,
 __device__ __forceinline__ void maxpool_px(const float* __restrict__ y, int ld, int off, f32x4 sc,
                                            f32x4 sh, int relu, int H, int W, int img, int yo,
                                            int xo, int c, float* __restrict__ out,
-                                           uint8_t* __restrict__ idx, int64_t o) {
+                                           uint8_t* __restrict__ idx, int64_t o,
+                                           uint16_t* __restrict__ out3 = nullptr, int C = 0) {
     f32x4 best;
     uint32_t bi = 0;
 #pragma unroll
@@ -472,7 +473,23 @@ __device__ __forceinline__ void maxpool_px(const float* __restrict__ y, int ld, 
     if (relu)
 #pragma unroll
         for (int j = 0; j < 4; ++j) best[j] = fmaxf(best[j], 0.f);
-    *(f32x4*)(out + o) = best;
+    if (out) *(f32x4*)(out + o) = best;
+    if (out3) {  // the x3 split straight into the next conv's operand image [pixels][C / 32][3][32]
+        typedef uint16_t u16x4 __attribute__((ext_vector_type(4)));
+        u16x4 h, m, l;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            uint16_t hj, mj, lj;
+            x3_split(best[j], X3CvtDev{}, hj, mj, lj);
+            h[j] = hj;
+            m[j] = mj;
+            l[j] = lj;
+        }
+        uint16_t* d = out3 + (o / C) * 3 * C + (c >> 5) * 96 + (c & 31);
+        *(u16x4*)d = h;
+        *(u16x4*)(d + 32) = m;
+        *(u16x4*)(d + 64) = l;
+    }
     *(uint32_t*)(idx + o) = bi;
 }
 
@@ -484,7 +501,8 @@ __global__ __launch_bounds__(256) void maxpool_bn_kernel(const float* __restrict
                                                          const float* __restrict__ shift, int relu,
                                                          int N, int H, int W, int C,
                                                          float* __restrict__ out,
-                                                         uint8_t* __restrict__ idx) {
+                                                         uint8_t* __restrict__ idx,
+                                                         uint16_t* __restrict__ out3) {
     const int Ho = H / 2, Wo = W / 2, c4n = C / 4;
     const int tpr = c4n < 256 ? c4n : 256, rpp = 256 / tpr;
     const int PO = N * Ho * Wo;
@@ -502,7 +520,7 @@ __global__ __launch_bounds__(256) void maxpool_bn_kernel(const float* __restrict
         Pix at = decode(min(r0 + g, PO - 1), Ho, Wo);
         for (int po = r0 + g; po < r1; po += rpp) {
             maxpool_px(y, ld, off, sc, sh, relu, H, W, at.img, at.y, at.x, c, out, idx,
-                       (int64_t)po * C + c);
+                       (int64_t)po * C + c, out3, C);
             pix_advance(at, rpp, Ho, Wo);
         }
     }
@@ -513,7 +531,7 @@ __global__ void maxpool_bn_any_kernel(const float* __restrict__ y, int ld, int o
                                       const float* __restrict__ scale,
                                       const float* __restrict__ shift, int relu, int N, int H,
                                       int W, int C, float* __restrict__ out,
-                                      uint8_t* __restrict__ idx) {
+                                      uint8_t* __restrict__ idx, uint16_t* __restrict__ out3) {
     const int Ho = H / 2, Wo = W / 2, c4n = C / 4;
     const int64_t total = (int64_t)N * Ho * Wo * c4n;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
@@ -525,7 +543,7 @@ __global__ void maxpool_bn_any_kernel(const float* __restrict__ y, int ld, int o
         const int yo = (int)(t % Ho), img = (int)(t / Ho);
         const f32x4 sc = scale ? *(const f32x4*)(scale + 4 * c4) : f32x4{1.f, 1.f, 1.f, 1.f};
         const f32x4 sh = shift ? *(const f32x4*)(shift + 4 * c4) : f32x4{0.f, 0.f, 0.f, 0.f};
-        maxpool_px(y, ld, off, sc, sh, relu, H, W, img, yo, xo, 4 * c4, out, idx, po * C + 4 * c4);
+        maxpool_px(y, ld, off, sc, sh, relu, H, W, img, yo, xo, 4 * c4, out, idx, po * C + 4 * c4, out3, C);
     }
 }
 
@@ -1550,15 +1568,16 @@ int k_bn_finalize_eval(int C, const float* gamma, const float* beta, const float
     LAUNCH_CHECK();
 }
 int k_maxpool_bn(const float* y, int ld, int off, const float* scale, const float* shift, int relu,
-                 int N, int H, int W, int C, float* out, uint8_t* idx, hipStream_t s) {
+                 int N, int H, int W, int C, float* out, uint8_t* idx, hipStream_t s, uint16_t* out3) {
     const int64_t n = (int64_t)N * (H / 2) * (W / 2) * (C / 4);
     const int c4n = C / 4;
+    if ((!out && !out3) || (out3 && C % 32)) return -1;
     if (C % 4 == 0 && c4n >= 1 && (int64_t)N * H * W < (1ll << 31))
         hipLaunchKernelGGL(maxpool_bn_kernel, dim3(grid_for(n)), dim3(256), 0, s, y, ld, off, scale,
-                           shift, relu, N, H, W, C, out, idx);
+                           shift, relu, N, H, W, C, out, idx, out3);
     else
         hipLaunchKernelGGL(maxpool_bn_any_kernel, dim3(grid_for(n)), dim3(256), 0, s, y, ld, off,
-                           scale, shift, relu, N, H, W, C, out, idx);
+                           scale, shift, relu, N, H, W, C, out, idx, out3);
     LAUNCH_CHECK();
 }
 int k_maxpool_bwd(const float* dp, const uint8_t* idx, const float* dskip, int ldskip, int offskip,

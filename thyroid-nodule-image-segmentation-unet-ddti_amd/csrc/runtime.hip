@@ -1285,6 +1285,9 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
     const float* xin = p.x_nhwc;
     // decoder convs whose operand image already holds the ConvT's up half (option convt16)
     std::vector<char> up16(NC, 0);
+    // x3: the max-pool wrote the next encoder conv's x3 operand image itself (no f32 pooled
+    // tensor, no prep pass; r05)
+    std::vector<char> pool3(NC, 0);
 
     auto conv = [&](int i) -> int {
         const ConvL& C = c->conv[i];
@@ -1322,7 +1325,9 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
             g.emode = c->bn_relu ? E_STATS : E_BIAS_RELU_STATS;
             if (p.pack3 && x3_conv_on(c, C.cin, C.cout)) {
                 uint16_t* img = p.x3[i] ? p.x3[i] : p.s3;
-                if (up16[i]) {  // the ConvT stored the up half's x3 split: convert the skip half
+                if (pool3[i]) {
+                    // (the max-pool already stored op(pooled) as this conv's x3 image)
+                } else if (up16[i]) {  // the ConvT stored the up half's x3 split: convert the skip half
                     const int l = C.level, so = c->skip_off(l), ch = c->ch(l);
                     const int rl = std::min(std::max(a.relu - so, 0), ch);
                     RUN("prep_x3", 0, k_to_x3(a.ptr, a.ld, a.off + so, ch, a.scale ? a.scale + so : nullptr,
@@ -1488,10 +1493,19 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
                 RUN("maxpool_fwd", 0,
                     k_maxpool_bn(p.out[b], p.ldout[b], p.offout[b], nullptr, nullptr, 0, p.N, H >> b,
                                  W >> b, C, p.pool[b], p.idx[b], s));
-            else
+            else {
+                const int j = 2 * (b + 1);  // the next encoder block's first conv
+                const ConvL& Cj = c->conv[j];
+                uint16_t* out3 = nullptr;
+                if (p.pack3 && x3_conv_on(c, Cj.cin, Cj.cout)) {
+                    out3 = p.x3[j] ? p.x3[j] : p.s3;
+                    pool3[j] = 1;
+                }
                 RUN("maxpool_fwd", 0,
                     k_maxpool_bn(p.y[i], p.ldy[i], p.offy[i], p.scale[i], p.shift[i],
-                                 c->bn_relu ? 1 : 0, p.N, H >> b, W >> b, C, p.pool[b], p.idx[b], s));
+                                 c->bn_relu ? 1 : 0, p.N, H >> b, W >> b, C, out3 ? nullptr : p.pool[b],
+                                 p.idx[b], s, out3));
+            }
         }
     }
     for (int k = 0; k < D; ++k) {
