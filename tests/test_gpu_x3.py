@@ -187,14 +187,16 @@ def test_x3_halo_schedules_bit_identical(B, H, W):
     """The halo GEMM's wave schedules (option x3_r3_sched, kernels_gemm_x3.hip X3R3Sched: which
     waves issue the LDS-DMA, the stagger of waves 4..7, where the DMA goes in the sub-step) run
     the same MFMAs in the same order per accumulator: one training step -- logits and the whole
-    gradient arena -- is bit-identical across all five, and with the 64-output GEMMs on the
+    gradient arena -- is bit-identical across all five, across the 16x16x32 schedules 8..10 (to
+    1e-4 of the largest value vs the 32x32x16 ones), and with the 64-output GEMMs on the
     128x64 two-blocks-per-CU halo tile (option x3_n64_r3 = 6; same K order, same 128-row BN
     partial groups).  128x128 covers W = 128 .. 16; 256x256 the level-0 tiles at W = 256."""
     import unet_hip
     from _helpers import options
     x, t = inputs(31, B, H, W)
     outs = []
-    for sched, n64 in ((0, 5), (1, 5), (2, 5), (3, 5), (4, 5), (0, 6)):
+    runs = ((0, 5), (1, 5), (2, 5), (3, 5), (4, 5), (0, 6), (8, 5), (9, 5), (10, 5))
+    for sched, n64 in runs:
         m = hip_model(O.make_params(42), DEV)
         with options(m.flatten_().rt, x3_r3_sched=sched, x3_n64_r3=n64):
             logits = m(x.to(DEV))
@@ -203,9 +205,17 @@ def test_x3_halo_schedules_bit_identical(B, H, W):
             torch.cuda.synchronize()
         outs.append((logits.detach().clone(), m._state.grad_arena.clone()))
         del m
+    # 0..4 (32x32x16) and 8..10 (16x16x32) are bit-identical within their shape; across shapes
+    # the MFMA sums 32 instead of 16 products per step: f32 rounding apart
+    m16 = [i for i, (sc, _) in enumerate(runs) if sc >= 8]
     for i in range(1, len(outs)):
-        assert torch.equal(outs[0][0], outs[i][0]), i
-        assert torch.equal(outs[0][1], outs[i][1]), (i, (outs[0][1] - outs[i][1]).abs().max().item())
+        j = m16[0] if i in m16 else 0
+        if i == j:
+            continue
+        assert torch.equal(outs[j][0], outs[i][0]), i
+        assert torch.equal(outs[j][1], outs[i][1]), (i, (outs[j][1] - outs[i][1]).abs().max().item())
+    for a, b in ((outs[0][0], outs[m16[0]][0]), (outs[0][1], outs[m16[0]][1])):
+        assert (a - b).abs().max().item() <= 1e-4 * b.abs().max().item()
 
 
 def test_x3_wgrad_schedules_bit_identical():
@@ -218,7 +228,7 @@ def test_x3_wgrad_schedules_bit_identical():
     from _helpers import options
     x, t = inputs(37, 2, 128, 128)
     outs = []
-    for sched in (0, 1, 2):
+    for sched in (0, 1, 2, 3):
         m = hip_model(O.make_params(42), DEV)
         with options(m.flatten_().rt, x3_wsched=sched):
             logits = m(x.to(DEV))

@@ -167,16 +167,19 @@ struct Options {
     int x3_wblocks = 1536;     // split-K target (blocks) of its 128x128 weight gradients
     int x3_n64 = 2;            // its row-GEMM tile for 64 outputs (2 = 128x64, 3 = 256x64)
     int x3_r3 = 1;             // its 256x128 3x3 GEMMs on the tap-row halo kernel (tile 4)
-    int x3_r3_sched = 1;       // the halo kernel's wave schedule (kernels_gemm_x3.hip X3R3Sched:
+    int x3_r3_sched = 9;       // the halo kernel's wave schedule (kernels_gemm_x3.hip X3R3Sched:
                                // who issues the LDS-DMA, stagger of waves 4..7; bit-identical).
                                // r05 (profiles/r05_halo_sched.txt): 1 (stagger + DMA after the
-                               // first k-step's reads) +5..13 % per layer, config 2 591 -> 603 img/s
+                               // first k-step's reads) +5..13 % per layer, config 2 591 -> 603 img/s;
+                               // 8..10 the same on 16x16x32 MFMAs (x3r3_body16), 9 = 1's
+                               // schedule: -4..-13 % per launch vs 1 (profiles/r05_halo_m16.txt)
     int x3_n32 = 0;            // x3 also for 32-multiple channel counts (r05; narrow widths)
     int x3_n64_r3 = 5;         // halo tile of the 64-output 3x3 GEMMs: 5 = 256x64 (8 waves, one
                                // block per CU), 6 = 128x64 (4 waves, two blocks per CU)
-    int x3_wsched = 0;         // the 64x128 tap-row weight gradient's schedule (0 = r04, 1 = four
-                               // stages with waves 4..7 half a chunk behind, 2 = 1 with waves
-                               // 0..3 issuing every DMA; bit-identical)
+    int x3_wsched = 0;         // the tap-row weight gradient's schedule (0 = r04, 1 = four stages
+                               // with waves 4..7 half a chunk behind, 2 = 1 with waves 0..3
+                               // issuing every DMA (64x128 only), 3 = the DMA after the first
+                               // k-step's reads (64x128, 128x64); bit-identical)
 };
 struct OptionDesc {
     const char* name;

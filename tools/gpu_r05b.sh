@@ -29,7 +29,7 @@ for S in 6 5; do
   echo "n64_r3 $S rc=$r $(python3 -c "import json;d=json.load(open('gpurun_out/$TAG.nbench$S.json'));print(d['value'], d['ms_per_step'])" 2>/dev/null)"
   [ $r -ne 0 ] && { tail -20 gpurun_out/$TAG.nbench$S.err; exit $r; }
 done
-for S in 1 2 0; do
+for S in ${WS:-1 2 0}; do
   timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --opt x3_wsched=$S \
     > gpurun_out/$TAG.wbench$S.json 2> gpurun_out/$TAG.wbench$S.err
   r=$?

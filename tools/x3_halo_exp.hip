@@ -10,11 +10,15 @@
 //          1024 / 2048 (timing only): B / A DMA from the same rows every sub-step (always L2 hits)
 //          256 explicit fragment pipeline (k-step 0 reads, then k-step 1 reads one per k-step-0
 //             MFMA, then the k-step-1 MFMAs)
+//          8192 (timing only): each 32x32x16 MFMA replaced by two 16x16x32 MFMAs on slices of
+//             the same accumulators (the same FLOPs in the other shape; MI355X_MICROARCH.md DVFS
+//             item 7: the 16x16x32 loop holds a higher clock)
 //   build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/x3_halo_exp.hip -o /tmp/x3_halo_exp
 //   run:   /tmp/x3_halo_exp [iters] [flag list, e.g. 0,16,64,80]
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <math.h>
 #include <algorithm>
 #include <vector>
 
@@ -30,6 +34,30 @@
     } while (0)
 
 namespace {
+
+__device__ __forceinline__ f32x4 m16(bf16x8 a, bf16x8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+template <int F>
+__device__ __forceinline__ void mx3(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f32x16& hi, f32x16& lo) {
+    if constexpr (F & 8192) {
+        f32x4 l0 = {lo[0], lo[1], lo[2], lo[3]}, l1 = {lo[4], lo[5], lo[6], lo[7]};
+        f32x4 h0 = {hi[0], hi[1], hi[2], hi[3]}, h1 = {hi[4], hi[5], hi[6], hi[7]};
+        l0 = m16(a[2], b[0], l0); l1 = m16(a[2], b[1], l1);
+        l0 = m16(a[1], b[1], l0); l1 = m16(a[1], b[2], l1);
+        l0 = m16(a[0], b[2], l0); l1 = m16(a[0], b[0], l1);
+        l0 = m16(a[1], b[0], l0); l1 = m16(a[1], b[2], l1);
+        l0 = m16(a[0], b[1], l0); l1 = m16(a[0], b[2], l1);
+        h0 = m16(a[0], b[0], h0); h1 = m16(a[0], b[1], h1);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            lo[i] = l0[i]; lo[4 + i] = l1[i]; hi[i] = h0[i]; hi[4 + i] = h1[i];
+        }
+    } else {
+        mfma_x3s(a, b, hi, lo);
+    }
+}
 
 template <int BN, int F, bool LAG>
 __device__ __forceinline__ void halo_body(const RowGemmArgs& p, char* smem, int wave, int lane,
@@ -137,7 +165,7 @@ __device__ __forceinline__ void halo_body(const RowGemmArgs& p, char* smem, int 
 #pragma unroll
                 for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-                    for (int nt = 0; nt < NT; ++nt) mfma_x3s(ha[mt], hb[nt], acc[mt][nt], acl[mt][nt]);
+                    for (int nt = 0; nt < NT; ++nt) mx3<F>(ha[mt], hb[nt], acc[mt][nt], acl[mt][nt]);
             }
         }
         const char* abase = smem + (g & 1) * AREG;
@@ -167,7 +195,7 @@ __device__ __forceinline__ void halo_body(const RowGemmArgs& p, char* smem, int 
 #pragma unroll
                 for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-                    for (int nt = 0; nt < NT; ++nt) mfma_x3s(fa[kk][mt], fb[kk][nt], acc[mt][nt], acl[mt][nt]);
+                    for (int nt = 0; nt < NT; ++nt) mx3<F>(fa[kk][mt], fb[kk][nt], acc[mt][nt], acl[mt][nt]);
             };
             rd(0);
             __builtin_amdgcn_sched_barrier(0);
@@ -250,7 +278,7 @@ __device__ __forceinline__ void halo_body(const RowGemmArgs& p, char* smem, int 
 #pragma unroll
                 for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-                    for (int nt = 0; nt < NT; ++nt) mfma_x3s(af[mt], bfr[nt], acc[mt][nt], acl[mt][nt]);
+                    for (int nt = 0; nt < NT; ++nt) mx3<F>(af[mt], bfr[nt], acc[mt][nt], acl[mt][nt]);
             }
         }
         if constexpr (!(F & 8)) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -259,7 +287,7 @@ __device__ __forceinline__ void halo_body(const RowGemmArgs& p, char* smem, int 
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-            for (int nt = 0; nt < NT; ++nt) mfma_x3s(ha[mt], hb[nt], acc[mt][nt], acl[mt][nt]);
+            for (int nt = 0; nt < NT; ++nt) mx3<F>(ha[mt], hb[nt], acc[mt][nt], acl[mt][nt]);
     }
     if constexpr (F & 8) x3_wait_vm<0>();
 }
@@ -379,7 +407,7 @@ __device__ __forceinline__ void halo_body_ld(const RowGemmArgs& p, char* smem, i
 #pragma unroll
                 for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-                    for (int nt = 0; nt < NT; ++nt) mfma_x3s(ha[mt], hb[nt], acc[mt][nt], acl[mt][nt]);
+                    for (int nt = 0; nt < NT; ++nt) mx3<F>(ha[mt], hb[nt], acc[mt][nt], acl[mt][nt]);
             }
         }
         const char* abase = smem + (g & 1) * AREG;
@@ -416,7 +444,7 @@ __device__ __forceinline__ void halo_body_ld(const RowGemmArgs& p, char* smem, i
 #pragma unroll
                 for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-                    for (int nt = 0; nt < NT; ++nt) mfma_x3s(af[mt], bfr[nt], acc[mt][nt], acl[mt][nt]);
+                    for (int nt = 0; nt < NT; ++nt) mx3<F>(af[mt], bfr[nt], acc[mt][nt], acl[mt][nt]);
             }
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -425,7 +453,7 @@ __device__ __forceinline__ void halo_body_ld(const RowGemmArgs& p, char* smem, i
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-            for (int nt = 0; nt < NT; ++nt) mfma_x3s(ha[mt], hb[nt], acc[mt][nt], acl[mt][nt]);
+            for (int nt = 0; nt < NT; ++nt) mx3<F>(ha[mt], hb[nt], acc[mt][nt], acl[mt][nt]);
     }
 }
 
@@ -475,7 +503,7 @@ int go(const RowGemmArgs& a) {
     return (int)hipGetLastError();
 }
 
-#define FLAG_LIST(X) X(0) X(1) X(2) X(4) X(7) X(16) X(96) X(112) X(4096) X(4112) X(4128) X(4160) X(4176) X(4192) X(4208)
+#define FLAG_LIST(X) X(0) X(1) X(2) X(4) X(7) X(16) X(96) X(112) X(4096) X(4112) X(4128) X(4160) X(4176) X(4192) X(4208) X(8192) X(8199) X(8288)
 
 int run(const RowGemmArgs& a, int bn, int f) {
 #define FCASE(v)                                       \
@@ -564,13 +592,18 @@ int main(int argc, char** argv) {
             printf("    library tile 6 (128x64, 2/CU): %.3f ms %.1f TF/s  %s\n", t, fl / t / 1e9,
                    same ? "bit-identical" : "DIFFERS");
         }
-        for (int sc = 0; sc <= 4; ++sc) {  // the library's schedules (X3R3Sched)
+        const int scheds[] = {1, 8, 9, 10, 12, 13};  // the library's schedules (8.. = 16x16x32)
+        double rmax = 0;
+        for (float v : r) rmax = std::max(rmax, (double)fabsf(v));
+        for (int sc : scheds) {
             CK(hipMemset(y, 0, (size_t)M * N * 4));
             const float t = timeit([&] { return launch_rowgemm_x3(h, bn == 128 ? 4 : 5, 0, sc); });
             CK(hipMemcpy(q.data(), y, q.size() * 4, hipMemcpyDeviceToHost));
             const bool same = memcmp(q.data(), r.data(), q.size() * 4) == 0;
-            printf("    library sched %d: %.3f ms %.1f TF/s  %s\n", sc, t, fl / t / 1e9,
-                   same ? "bit-identical" : "DIFFERS");
+            double dmax = 0;
+            for (size_t i = 0; i < q.size(); ++i) dmax = std::max(dmax, (double)fabsf(q[i] - r[i]));
+            printf("    library sched %2d: %.3f ms %.1f TF/s  %s (max |diff| %.3g of max |y| %.3g)\n", sc, t,
+                   fl / t / 1e9, same ? "bit-identical" : "differs", dmax, rmax);
             fflush(stdout);
         }
         for (int f : flags) {
@@ -583,7 +616,7 @@ int main(int argc, char** argv) {
             CK(hipMemcpy(q.data(), y, q.size() * 4, hipMemcpyDeviceToHost));
             const bool same = memcmp(q.data(), r.data(), q.size() * 4) == 0;
             printf("    flags %3d: %.3f ms %.1f TF/s  %s\n", f, t, fl / t / 1e9,
-                   (f & 3087) ? "(ablation)" : same ? "bit-identical" : "DIFFERS");
+                   (f & (3087 | 8192)) ? "(ablation)" : same ? "bit-identical" : "DIFFERS");
             fflush(stdout);
         }
         CK(hipFree(x)); CK(hipFree(w)); CK(hipFree(yref)); CK(hipFree(y)); CK(hipFree(x3)); CK(hipFree(w3));
