@@ -850,6 +850,19 @@ __device__ __forceinline__ int x3_tswz(int sl, int row) {
     else return sl;
 }
 
+// the same for the 16x16x32 weight gradient (r05): a 32-lane half reads 32 B (16 columns) of
+// eight consecutive pixel rows r0 .. r0 + 7 (and, in its second read, of rows r0 + 16 ..), so
+// the 32-B slot pairs of those rows must fall on eight different 32-B bank sections: RB % 256
+// == 0: XOR the pair by row & 7; == 128: rows of one parity share a 128-B half, XOR the pair by
+// (row >> 1) & 3; 192: rows r, r + 4 share a 64-B quarter, XOR the pair by (row >> 2) & 1.
+// Invariant under row + 16; pairs (and 16-B halves of a plane) stay whole.
+template <int RB>
+__device__ __forceinline__ int x3_tswz16(int sl, int row) {
+    if constexpr (RB % 256 == 0) return sl ^ ((row & 7) << 1);
+    else if constexpr (RB % 256 == 128) return sl ^ (((row >> 1) & 3) << 1);
+    else return sl ^ (((row >> 2) & 1) << 1);
+}
+
 template <int OFF>
 __device__ __forceinline__ x3_short4 x3_tr16(unsigned addr) {
     x3_short4 r;
@@ -1086,10 +1099,11 @@ __global__ __launch_bounds__((BM / 32) * (BN / 32) * 64, OCC) void wgrad_x3_row3
     constexpr int WAVES = (BM / 32) * (BN / 32), BKP = 32;
     constexpr int WAVES_N = BN / 32;
     static_assert(S >= 2 && S <= 4, "stages");
-    static_assert(SCHED == 0 || SCHED == 3 || (S == 4 && WAVES == 8), "the staggered schedules need 4 stages, 8 waves");
+    constexpr bool M16 = SCHED >= 8;  // 16x16x32 MFMAs (8: as 0, 9: as 3)
+    static_assert(SCHED == 0 || SCHED == 3 || M16 || (S == 4 && WAVES == 8), "the staggered schedules need 4 stages, 8 waves");
     constexpr int LW = SCHED == 2 ? 4 : WAVES;  // waves issuing the DMA
     constexpr int DIST = (SCHED == 1 || SCHED == 2) ? 2 : S - 1;  // chunks the DMA runs ahead
-    constexpr bool LATE = SCHED == 3;           // the DMA issued after the first k-step's reads
+    constexpr bool LATE = SCHED == 3 || SCHED == 9;  // the DMA issued after the first k-step's reads
     constexpr int RA = 6 * BM, RBB = 6 * BN;
     constexpr int HALO = BKP + 2;
     constexpr int AREG = (HALO * RA + 1024 * WAVES - 1) / (1024 * WAVES) * WAVES * 1024;  // per stage
@@ -1126,12 +1140,12 @@ __global__ __launch_bounds__((BM / 32) * (BN / 32) * 64, OCC) void wgrad_x3_row3
     auto apiece = [&](int j, int& r, int& e) {
         const int o = ((j * LW + wave) * 64 + lane) * 16;
         r = o / RA;
-        e = x3_tswz<RA>((o - r * RA) >> 4, r) * 8;
+        e = (M16 ? x3_tswz16<RA>((o - r * RA) >> 4, r) : x3_tswz<RA>((o - r * RA) >> 4, r)) * 8;
     };
     auto bpiece = [&](int j, int& r, int& e) {
         const int o = ((j * LW + wave) * 64 + lane) * 16;
         r = o / RBB;
-        e = x3_tswz<RBB>((o - r * RBB) >> 4, r) * 8;
+        e = (M16 ? x3_tswz16<RBB>((o - r * RBB) >> 4, r) : x3_tswz<RBB>((o - r * RBB) >> 4, r)) * 8;
     };
     if constexpr (KEEP) {
 #pragma unroll
@@ -1172,6 +1186,114 @@ __global__ __launch_bounds__((BM / 32) * (BN / 32) * 64, OCC) void wgrad_x3_row3
             x3_dma16(g, base + AREG + (j * LW + wave) * 1024);
         }
     };
+
+    if constexpr (M16) {
+        // 16x16x32: per chunk ONE k-step of 32 pixels; a wave's 32 x 32 x 3-tap tile is 2 x 2
+        // blocks of 16 x 16 per tap.  Lane l of group g = l / 16 supplies the k values 8 g .. 8 g
+        // + 7 = pixel rows 4 g + qq (first transposed read) and 16 + 4 g + qq (second), the same
+        // rows for A' and B' (any k order sums the same products), column l & 15 of its block.
+        f32x4 hi[3][2][2], lo[3][2][2];
+#pragma unroll
+        for (int d = 0; d < 3; ++d)
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) hi[d][b >> 1][b & 1][r] = lo[d][b >> 1][b & 1][r] = 0.f;
+        const int g = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
+        const int trow = 4 * g + qq;
+        auto slot = [](int col, int q) { return (col >> 5) * 12 + q * 4 + ((col & 31) >> 3); };
+        int aoff[3][2][3], boff[2][3];
+#pragma unroll
+        for (int bm = 0; bm < 2; ++bm) {
+            const int col = wm * 32 + 16 * bm + 4 * pp;
+#pragma unroll
+            for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+                for (int q = 0; q < 3; ++q)
+                    aoff[dx][bm][q] = (trow + dx) * RA + (x3_tswz16<RA>(slot(col, q), trow + dx) << 4) + ((col >> 2) & 1) * 8;
+            const int colb = wn * 32 + 16 * bm + 4 * pp;
+#pragma unroll
+            for (int q = 0; q < 3; ++q)
+                boff[bm][q] = AREG + trow * RBB + (x3_tswz16<RBB>(slot(colb, q), trow) << 4) + ((colb >> 2) & 1) * 8;
+        }
+        const unsigned sbase = x3_lds_u32(smem);
+        auto rd = [](x3_short4 (&f)[2], unsigned addr, auto ROWB) {
+            constexpr int rb = decltype(ROWB)::value;
+            f[0] = x3_tr16<0>(addr);
+            f[1] = x3_tr16<16 * rb>(addr);
+        };
+        using IRA = std::integral_constant<int, RA>;
+        using IRB = std::integral_constant<int, RBB>;
+        auto mma = [&](const x3_short4 (&fa)[3][3][2], const x3_short4 (&fb)[2][3][2], int bm) {
+#pragma unroll
+            for (int bn = 0; bn < 2; ++bn) {
+                bf16x8 b3[3];
+#pragma unroll
+                for (int q = 0; q < 3; ++q) b3[q] = *(const bf16x8*)fb[bn][q];
+#pragma unroll
+                for (int dx = 0; dx < 3; ++dx) {
+                    bf16x8 a3[3];
+#pragma unroll
+                    for (int q = 0; q < 3; ++q) a3[q] = *(const bf16x8*)fa[dx][q];
+                    mfma_x3s16(a3, b3, hi[dx][bm][bn], lo[dx][bm][bn]);
+                }
+            }
+        };
+        if (issuer) {
+#pragma unroll
+            for (int s = 0; s < DIST; ++s)
+                if (s < nk) issue(s, s);
+        }
+        for (int kc = 0; kc < nk; ++kc) {
+            if (issuer) {
+                if (DIST >= 2 && kc + 1 < nk) x3_wait_vm<GPC>();
+                else x3_wait_vm<0>();
+            }
+            x3_barrier();
+            if (!LATE && issuer && kc + DIST < nk) issue(kc + DIST, (kc + DIST) % S);
+            const unsigned sb = sbase + (kc % S) * STAGE;
+            x3_short4 fb[2][3][2], fa[3][3][2], fa1[3][3][2];
+#pragma unroll
+            for (int bn = 0; bn < 2; ++bn)
+#pragma unroll
+                for (int q = 0; q < 3; ++q) rd(fb[bn][q], sb + boff[bn][q], IRB{});
+#pragma unroll
+            for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+                for (int q = 0; q < 3; ++q) rd(fa[dx][q], sb + aoff[dx][0][q], IRA{});
+            if (LATE && issuer && kc + DIST < nk) {
+                __builtin_amdgcn_sched_barrier(0);
+                issue(kc + DIST, (kc + DIST) % S);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+                for (int q = 0; q < 3; ++q) rd(fa1[dx][q], sb + aoff[dx][1][q], IRA{});
+            __builtin_amdgcn_sched_barrier(0);
+            mma(fa, fb, 0);
+            __builtin_amdgcn_sched_barrier(0);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+            mma(fa1, fb, 1);
+        }
+        float* slab = p.slab + (size_t)split * p.Mw * p.Nw;
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+            for (int bm = 0; bm < 2; ++bm)
+#pragma unroll
+                for (int bn = 0; bn < 2; ++bn)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int m = (dy * 3 + dx) * p.CA + ca0 + wm * 32 + 16 * bm + 4 * g + i;
+                        const int n = cb0 + wn * 32 + 16 * bn + (lane & 15);
+                        slab[(size_t)m * p.Nw + n] = hi[dx][bm][bn][i] + lo[dx][bm][bn][i];
+                    }
+        return;
+    }
 
     f32x16 acc[3], acl[3];
 #pragma unroll
@@ -1582,6 +1704,14 @@ int launch_wgrad_x3(const WgradArgs& a, int tile, hipStream_t s, int sched) {
             hipLaunchKernelGGL((wgrad_x3_row3_kernel<64, 128, 3, 1, 3>), grid, dim3(512), 0, s, a);
         else if (tile == 3 && sched == 3)
             hipLaunchKernelGGL((wgrad_x3_row3_kernel<128, 64, 3, 1, 3>), grid, dim3(512), 0, s, a);
+        else if (tile == 2 && sched == 8)  // 16x16x32 (r05)
+            hipLaunchKernelGGL((wgrad_x3_row3_kernel<64, 128, 3, 1, 8>), grid, dim3(512), 0, s, a);
+        else if (tile == 2 && sched == 9)
+            hipLaunchKernelGGL((wgrad_x3_row3_kernel<64, 128, 3, 1, 9>), grid, dim3(512), 0, s, a);
+        else if (tile == 3 && sched >= 8)
+            hipLaunchKernelGGL((wgrad_x3_row3_kernel<128, 64, 3, 1, 8>), grid, dim3(512), 0, s, a);
+        else if (tile == 4 && sched >= 8)
+            hipLaunchKernelGGL((wgrad_x3_row3_kernel<64, 64, 2, 2, 8>), grid, dim3(256), 0, s, a);
         else if (tile == 2)
             hipLaunchKernelGGL((wgrad_x3_row3_kernel<64, 128>), grid, dim3(512), 0, s, a);
         else if (tile == 3)

@@ -176,10 +176,12 @@ struct Options {
     int x3_n32 = 0;            // x3 also for 32-multiple channel counts (r05; narrow widths)
     int x3_n64_r3 = 5;         // halo tile of the 64-output 3x3 GEMMs: 5 = 256x64 (8 waves, one
                                // block per CU), 6 = 128x64 (4 waves, two blocks per CU)
-    int x3_wsched = 0;         // the tap-row weight gradient's schedule (0 = r04, 1 = four stages
+    int x3_wsched = 9;         // the tap-row weight gradient's schedule (0 = r04, 1 = four stages
                                // with waves 4..7 half a chunk behind, 2 = 1 with waves 0..3
                                // issuing every DMA (64x128 only), 3 = the DMA after the first
-                               // k-step's reads (64x128, 128x64); bit-identical)
+                               // k-step's reads (64x128, 128x64); bit-identical); 8 / 9 = 0 / 3
+                               // on 16x16x32 MFMAs (64x128, 128x64, 64x64): config 2 +1.6 / +1.9 %
+                               // (profiles/r05_wgrad_m16_ab.txt)
 };
 struct OptionDesc {
     const char* name;
