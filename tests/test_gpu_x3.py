@@ -159,7 +159,8 @@ def test_x3_train_step_matches_f32_mfma():
 @pytest.mark.parametrize("B,H,W", [(2, 128, 128), (1, 48, 80)])
 def test_x3_row_tile_choice_bit_identical(B, H, W):
     """Every x3 row-GEMM tile (0 = 256x128, 1 = 128x128, 2 = 128x64, 3 = 256x64 for the
-    64-output GEMMs; -1 = the per-GEMM choice) walks K in the same chunk order with the same six-product MFMA sequence per
+    64-output GEMMs; -1 = the per-GEMM choice; 32x32x16 MFMAs, and tiles 0 / 1 again on
+    16x16x32) walks K in the same chunk order with the same six-product MFMA sequence per
     element and emits BN partials in the same 128-row groups, so one training step -- logits
     and the whole gradient arena -- is bit-identical across them (48x80: tiles ending past
     M, the guarded epilogue)."""
@@ -167,10 +168,12 @@ def test_x3_row_tile_choice_bit_identical(B, H, W):
     from _helpers import options
     x, t = inputs(13, B, H, W)
     outs = []
-    for tile, n64 in ((-1, 2), (0, 2), (1, 2), (2, 2), (-1, 3)):
+    runs = ((-1, 2, 0), (0, 2, 0), (1, 2, 0), (2, 2, 0), (-1, 3, 0), (0, 2, 1), (1, 2, 1))
+    for tile, n64, m16 in runs:
         m = hip_model(O.make_params(42), DEV)
-        # (the tap-row halo tile sums K in another order: test_x3_halo_tile_matches_one_tap)
-        with options(m.flatten_().rt, x3_tile=tile, x3_n64=n64, x3_r3=0):
+        # (the tap-row halo tile sums K in another order: test_x3_halo_tile_matches_one_tap;
+        # x3_1tap16 = 1 puts tiles 0 / 1 on 16x16x32 MFMAs: bit-identical to each other)
+        with options(m.flatten_().rt, x3_tile=tile, x3_n64=n64, x3_r3=0, x3_1tap16=m16):
             logits = m(x.to(DEV))
             l = unet_hip.seg_losses(logits, t.to(DEV))
             (l[0] + l[1]).backward()
@@ -178,8 +181,12 @@ def test_x3_row_tile_choice_bit_identical(B, H, W):
         outs.append((logits.detach().clone(), m._state.grad_arena.clone()))
         del m
     for i in range(1, len(outs)):
-        assert torch.equal(outs[0][0], outs[i][0]), i
-        assert torch.equal(outs[0][1], outs[i][1]), (i, (outs[0][1] - outs[i][1]).abs().max().item())
+        j = 5 if runs[i][2] else 0
+        if i == j:
+            continue
+        assert torch.equal(outs[j][0], outs[i][0]), i
+        assert torch.equal(outs[j][1], outs[i][1]), (i, (outs[j][1] - outs[i][1]).abs().max().item())
+    assert torch.isfinite(outs[5][1]).all()
 
 
 @pytest.mark.parametrize("B,H,W", [(2, 128, 128), (1, 256, 256)])
@@ -216,6 +223,30 @@ def test_x3_halo_schedules_bit_identical(B, H, W):
         assert torch.equal(outs[j][1], outs[i][1]), (i, (outs[j][1] - outs[i][1]).abs().max().item())
     for a, b in ((outs[0][0], outs[m16[0]][0]), (outs[0][1], outs[m16[0]][1])):
         assert (a - b).abs().max().item() <= 1e-4 * b.abs().max().item()
+
+
+def test_x3_one_tap_m16_close():
+    """Option x3_1tap16 (r05, default off: no gain measured): the one-tap x3 row GEMM and weight
+    gradient tiles (the ConvT layers and the 16x16 bottleneck) on 16x16x32 MFMAs.  One
+    training step at 128x128 stays within f32 rounding of the 32x32x16 one-tap kernels (the
+    masked fp64 tests bound both against the oracle)."""
+    import unet_hip
+    from _helpers import options
+    x, t = inputs(41, 2, 128, 128)
+    outs = []
+    for flag in (0, 1):
+        m = hip_model(O.make_params(43), DEV)
+        with options(m.flatten_().rt, x3_1tap16=flag):
+            logits = m(x.to(DEV))
+            l = unet_hip.seg_losses(logits, t.to(DEV))
+            (l[0] + l[1]).backward()
+            torch.cuda.synchronize()
+        outs.append((logits.detach().clone(), m._state.grad_arena.clone()))
+        del m
+    (l0, g0), (l1, g1) = outs
+    assert not torch.equal(l0, l1)  # the flag reaches the kernels
+    assert (l0 - l1).abs().max().item() <= 1e-5 * l0.abs().max().item()
+    assert torch.allclose(g1, g0, rtol=1e-3, atol=1e-5 * g0.abs().max().item()), (g1 - g0).abs().max().item()
 
 
 def test_x3_wgrad_schedules_bit_identical():

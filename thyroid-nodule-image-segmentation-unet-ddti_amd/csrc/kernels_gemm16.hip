@@ -249,14 +249,21 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm16_kernel(RowGemmAr
 // in registers, so that their matrix work opens each segment while their partner waits for its
 // first fragments (MI355X_MICROARCH.md "two waves per SIMD" item 9); 2 = 1 with the next
 // stage's DMA issued after the first tap's fragment reads
+// SCHED 8 (r05): 0 on 16x16x32 MFMAs (9 / 10 = 1 / 2 spill 22-28 VGPRs, not built) -- per tap ONE k-step of 32 channels, a wave's
+// 128 x 64 tile as 8 x 4 blocks of 16 x 16 (rows via m16_row, acc16_to32 before the epilogue);
+// the 16-B chunk swizzle becomes c ^ ((r >> 1) & 2), conflict-free for that read pattern (the
+// ds_read_b128 lane groups take two chunks of 16 consecutive rows; kernels_gemm_x3.hip
+// x3r3_body16).  Same FLOPs, same LDS bytes; the sums run 32 products per MFMA step.
 template <int EMODE, int BM, int BN, int SCHED = 0>
 __global__ __launch_bounds__(512, 1) void rowgemm16_row3_kernel(RowGemmArgs p) {
+    constexpr bool M16 = SCHED >= 8;
+    constexpr int SC = SCHED & 7;
     constexpr int WM = 128, WN = 64, BK = 32, WAVES_N = BN / WN;
     constexpr int WAVES = (BM / WM) * WAVES_N;
     static_assert(WAVES == 8, "512 threads");
     constexpr int MT = WM / 32, NT = WN / 32;
     constexpr int RB = 2 * BK, LPR = RB / 16, RPI = 64 / LPR;  // 64-B rows, 16 rows / piece
-    auto swz = [](int r) { return (r >> 2) & 3; };
+    auto swz = [](int r) { return M16 ? (r >> 1) & 2 : (r >> 2) & 3; };
     constexpr int AR = (BM / 16) * 18;        // halo rows held (W = 16: BM / 16 rows x 18)
     constexpr int AI = (AR / RPI + WAVES - 1) / WAVES;  // A pieces per wave (w, w + 8, ...)
     constexpr int BR = 3 * BN;                // B rows: taps dx = 0..2 x BN outputs
@@ -321,6 +328,101 @@ __global__ __launch_bounds__(512, 1) void rowgemm16_row3_kernel(RowGemmArgs p) {
     };
 
     f32x16 acc[MT][NT];
+    const int ns = 3 * CC;
+    if constexpr (M16) {
+        f32x4 a16[MT][NT][2][2];
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+#pragma unroll
+            for (int j = 0; j < NT; ++j)
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) a16[i][j][b >> 1][b & 1][r] = 0.f;
+        const int ks = lane >> 4, rs = lane & 15, rp = m16_row(rs);
+        int ahb[MT][2], bro[NT][2], bfx[NT][2];
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+            for (int bm = 0; bm < 2; ++bm) {
+                const int mo = wm * WM + mt * 32 + bm * 16 + rp;
+                const int r = mo / SEG;
+                ahb[mt][bm] = r * HW + (mo - r * SEG);
+            }
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+            for (int bn = 0; bn < 2; ++bn) {
+                const int r = wn * WN + nt * 32 + bn * 16 + rs;
+                bro[nt][bn] = (AR + r) * RB;
+                bfx[nt][bn] = swz(r);
+            }
+        issue(0);
+        auto run16 = [&](auto LAGC) {
+            constexpr bool LAG = decltype(LAGC)::value;
+            bf16x8 ha[MT][2], hb[NT][2];  // LAG: the previous stage's dx = 2 fragments
+            auto mm = [&](const bf16x8 (&af)[MT][2], const bf16x8 (&bfr)[NT][2]) {
+#pragma unroll
+                for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                    for (int bm = 0; bm < 2; ++bm)
+#pragma unroll
+                        for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+                            for (int bn = 0; bn < 2; ++bn)
+                                a16[mt][nt][bm][bn] = mfma16_bf16(af[mt][bm], bfr[nt][bn], a16[mt][nt][bm][bn]);
+            };
+            for (int s = 0; s < ns; ++s) {
+                wait_vm<0>();
+                block_barrier();
+                if (SC != 2 && s + 1 < ns) issue(s + 1);
+                if constexpr (LAG) {
+                    if (s > 0) mm(ha, hb);
+                }
+                const char* base = smem + (s & 1) * STAGE;
+#pragma unroll
+                for (int dx = 0; dx < 3; ++dx) {
+                    bf16x8 af[MT][2], bfr[NT][2];
+#pragma unroll
+                    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                        for (int bm = 0; bm < 2; ++bm) {
+                            const int h = ahb[mt][bm] + dx;
+                            af[mt][bm] = *(const bf16x8*)(base + h * RB + ((ks ^ swz(h)) << 4));
+                        }
+#pragma unroll
+                    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+                        for (int bn = 0; bn < 2; ++bn)
+                            bfr[nt][bn] = *(const bf16x8*)(base + bro[nt][bn] + dx * BN * RB + ((ks ^ bfx[nt][bn]) << 4));
+                    if (SC == 2 && dx == 0 && s + 1 < ns) issue(s + 1);
+                    if (LAG && dx == 2) {
+#pragma unroll
+                        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                            for (int bm = 0; bm < 2; ++bm) ha[mt][bm] = af[mt][bm];
+#pragma unroll
+                        for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+                            for (int bn = 0; bn < 2; ++bn) hb[nt][bn] = bfr[nt][bn];
+                    } else {
+                        mm(af, bfr);
+                    }
+                }
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            }
+            if constexpr (LAG) mm(ha, hb);
+        };
+        if (SC != 0 && wave >= 4) run16(std::true_type{});
+        else run16(std::false_type{});
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) acc16_to32(a16[mt][nt], acc[mt][nt], lane);
+        block_barrier();
+        row_epilogue<EMODE, BM, BN, WM, WN, true>(p, acc, m0, n0, tile_m, wm, wn, lane, tid, (float*)smem);
+        return;
+    }
 #pragma unroll
     for (int i = 0; i < MT; ++i)
 #pragma unroll
@@ -342,7 +444,6 @@ __global__ __launch_bounds__(512, 1) void rowgemm16_row3_kernel(RowGemmArgs p) {
         bfx[nt] = swz(r);  // rows dx * 256 + r share it
     }
 
-    const int ns = 3 * CC;
     issue(0);
     auto run = [&](auto LAGC) {
         constexpr bool LAG = decltype(LAGC)::value;
@@ -360,7 +461,7 @@ __global__ __launch_bounds__(512, 1) void rowgemm16_row3_kernel(RowGemmArgs p) {
             // 3 % slower.)
             wait_vm<0>();
             block_barrier();
-            if (SCHED != 2 && s + 1 < ns) issue(s + 1);
+            if (SC != 2 && s + 1 < ns) issue(s + 1);
             if constexpr (LAG) {
                 if (s > 0) {
 #pragma unroll
@@ -382,7 +483,7 @@ __global__ __launch_bounds__(512, 1) void rowgemm16_row3_kernel(RowGemmArgs p) {
 #pragma unroll
                     for (int nt = 0; nt < NT; ++nt)
                         bfr[nt] = *(const bf16x8*)(base + bro[nt] + dx * BN * RB + ((c ^ bfx[nt]) << 4));
-                    if (SCHED == 2 && dx == 0 && kk == 0 && s + 1 < ns) issue(s + 1);
+                    if (SC == 2 && dx == 0 && kk == 0 && s + 1 < ns) issue(s + 1);
                     if (LAG && dx == 2) {
 #pragma unroll
                         for (int mt = 0; mt < MT; ++mt) ha[kk][mt] = af[mt];
@@ -400,7 +501,7 @@ __global__ __launch_bounds__(512, 1) void rowgemm16_row3_kernel(RowGemmArgs p) {
             for (int kk = 0; kk < BK / 16; ++kk) mm(ha[kk], hb[kk]);
         }
     };
-    if (SCHED != 0 && wave >= 4) run(std::true_type{});
+    if (SC != 0 && wave >= 4) run(std::true_type{});
     else run(std::false_type{});
     block_barrier();  // the epilogue reuses the stage memory
     row_epilogue<EMODE, BM, BN, WM, WN, true>(p, acc, m0, n0, tile_m, wm, wn, lane, tid, (float*)smem);
@@ -416,6 +517,9 @@ static int rg16r3_go(const RowGemmArgs& a, hipStream_t s, int sched) {
         hipLaunchKernelGGL((rowgemm16_row3_kernel<EMODE, BM, BN, 1>), grid, dim3(512), 0, s, a);
     else if (sched == 2)
         hipLaunchKernelGGL((rowgemm16_row3_kernel<EMODE, BM, BN, 2>), grid, dim3(512), 0, s, a);
+    else if (sched == 8)
+        hipLaunchKernelGGL((rowgemm16_row3_kernel<EMODE, BM, BN, 8>), grid, dim3(512), 0, s, a);
+
     else
         hipLaunchKernelGGL((rowgemm16_row3_kernel<EMODE, BM, BN>), grid, dim3(512), 0, s, a);
     return (int)hipGetLastError();

@@ -79,9 +79,6 @@ __device__ __forceinline__ void mfma_x3s(const bf16x8 (&a)[3], const bf16x8 (&b)
 }
 
 // the six products of one 16x16x32 block (the same pieces and order; 32 k per instruction)
-__device__ __forceinline__ f32x4 mfma16_bf16(bf16x8 a, bf16x8 b, f32x4 c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
-}
 
 __device__ __forceinline__ void mfma_x3s16(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f32x4& hi, f32x4& lo) {
     lo = mfma16_bf16(a[2], b[0], lo);
@@ -103,7 +100,9 @@ struct TileX3 {
 // XP: speed-of-light ablations for tools/x3_probe.hip only (results are garbage): bit 0 drops
 // the A DMA, 1 the B DMA, 2 the LDS fragment reads, 3 the loop's waits and barriers; the
 // library instantiates XP = 0.
-template <int AMODE, int EMODE, class T, int XP = 0>
+// M16 (r05): 16x16x32 MFMAs, one k-step of 32 channels per chunk (as x3r3_body16; swizzle
+// c ^ ((r >> 1) & 2), rows via m16_row, acc16_to32 before the epilogue)
+template <int AMODE, int EMODE, class T, int XP = 0, bool M16 = false>
 __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_x3_kernel(RowGemmArgs p) {
     constexpr int BM = T::BM, BN = T::BN, WM = T::WM, WN = T::WN, S = T::S, BK = T::BK;
     constexpr int WAVES = T::WAVES, WAVES_N = BN / WN;
@@ -120,7 +119,8 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_x3_kernel(RowGemmA
     constexpr int RED = 2 * (BM / 64) * BN * 8;
     constexpr int SMEM = STAGE * S > RED ? STAGE * S : RED;
     __shared__ __attribute__((aligned(1024))) char smem[SMEM];
-    auto swz = [](int r) { return (r >> 2) & 3; };
+    auto swz = [](int r) { return M16 ? (r >> 1) & 2 : (r >> 2) & 3; };
+    static_assert(!M16 || (T::SA && XP == 0), "16x16x32: split accumulators, no ablations");
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -209,6 +209,36 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_x3_kernel(RowGemmA
         bfx[nt] = swz(r);
     }
 
+    // M16: [mt][nt][bm][bn] 16x16 blocks, A rows / B columns of lane slot rs
+    f32x4 h16[M16 ? MT : 1][M16 ? NT : 1][2][2], l16[M16 ? MT : 1][M16 ? NT : 1][2][2];
+    int aro16[M16 ? MT : 1][2], afx16[M16 ? MT : 1][2], bro16[M16 ? NT : 1][2], bfx16[M16 ? NT : 1][2];
+    const int ks = lane >> 4;
+    if constexpr (M16) {
+        const int rs = lane & 15;
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                const int ra = wm * WM + mt * 32 + b * 16 + m16_row(rs);
+                aro16[mt][b] = ra * RB;
+                afx16[mt][b] = swz(ra);
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+                    for (int bn = 0; bn < 2; ++bn)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) h16[mt][nt][b][bn][r] = l16[mt][nt][b][bn][r] = 0.f;
+            }
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                const int rb = wn * WN + nt * 32 + b * 16 + rs;
+                bro16[nt][b] = AREG + rb * RB;
+                bfx16[nt][b] = swz(rb);
+            }
+    }
+
     const int nk = K / BK;
     bf16x8 xa;  // XP & 4: a register operand
 #pragma unroll
@@ -235,8 +265,33 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_x3_kernel(RowGemmA
         }
         if constexpr (!(XP & 8)) x3_barrier();
         const char* base = smem + (kc % S) * STAGE;
+        if constexpr (M16) {
+            bf16x8 af[MT][2][3], bfr[NT][2][3];
 #pragma unroll
-        for (int kk = 0; kk < BK / 16; ++kk) {
+            for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+                for (int b = 0; b < 2; ++b)
+#pragma unroll
+                    for (int q = 0; q < 3; ++q)
+                        bfr[nt][b][q] = *(const bf16x8*)(base + bro16[nt][b] + q * 64 + ((ks ^ bfx16[nt][b]) << 4));
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt) {
+#pragma unroll
+                for (int b = 0; b < 2; ++b)
+#pragma unroll
+                    for (int q = 0; q < 3; ++q)
+                        af[mt][b][q] = *(const bf16x8*)(base + aro16[mt][b] + q * 64 + ((ks ^ afx16[mt][b]) << 4));
+#pragma unroll
+                for (int b = 0; b < 2; ++b)
+#pragma unroll
+                    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+                        for (int bn = 0; bn < 2; ++bn)
+                            mfma_x3s16(af[mt][b], bfr[nt][bn], h16[mt][nt][b][bn], l16[mt][nt][b][bn]);
+            }
+        }
+#pragma unroll
+        for (int kk = 0; kk < (M16 ? 0 : BK / 16); ++kk) {
             const int c = kk * 2 + lh;
             bf16x8 af[MT][3], bfr[NT][3];
             if constexpr (XP & 4) {  // operands from registers only (no LDS traffic)
@@ -274,7 +329,17 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_x3_kernel(RowGemmA
         }
     }
     if constexpr (XP & 8) x3_wait_vm<0>();
-    if constexpr (SA) {
+    if constexpr (M16) {
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) {
+                f32x4 a[2][2];
+#pragma unroll
+                for (int b = 0; b < 4; ++b) a[b >> 1][b & 1] = h16[mt][nt][b >> 1][b & 1] + l16[mt][nt][b >> 1][b & 1];
+                acc16_to32(a, acc[mt][nt], lane);
+            }
+    } else if constexpr (SA) {
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
@@ -571,7 +636,7 @@ __device__ __forceinline__ void x3r3_body16(const RowGemmArgs& p, char* smem, in
         if (g + 1 < NG) issue_a(g + 1, dx * AC, dx * AC + AC);
     };
     const int ks = lane >> 4, rs = lane & 15;
-    const int rperm = ((rs >> 2) & 1) * 8 + (rs >> 3) * 4 + (rs & 3);
+    const int rperm = m16_row(rs);
     int ahb[2][2], bro[NT][2], bfx[NT][2];
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt)
@@ -671,21 +736,15 @@ __device__ __forceinline__ void x3r3_body16(const RowGemmArgs& p, char* smem, in
 template <int NT>
 __device__ __forceinline__ void x3_acc16_to32(const f32x4 (&hi)[2][NT][2][2], const f32x4 (&lo)[2][NT][2][2],
                                               f32x16 (&acc)[2][NT], int lane) {
-    const bool odd = (lane >> 4) & 1;
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt)
+        for (int nt = 0; nt < NT; ++nt) {
+            f32x4 a[2][2];
 #pragma unroll
-            for (int bm = 0; bm < 2; ++bm)
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const float v0 = hi[mt][nt][bm][0][i] + lo[mt][nt][bm][0][i];
-                    const float v1 = hi[mt][nt][bm][1][i] + lo[mt][nt][bm][1][i];
-                    const float p0 = __shfl_xor(v0, 16), p1 = __shfl_xor(v1, 16);
-                    acc[mt][nt][8 * bm + i] = odd ? p1 : v0;
-                    acc[mt][nt][8 * bm + 4 + i] = odd ? v1 : p0;
-                }
+            for (int b = 0; b < 4; ++b) a[b >> 1][b & 1] = hi[mt][nt][b >> 1][b & 1] + lo[mt][nt][b >> 1][b & 1];
+            acc16_to32(a, acc[mt][nt], lane);
+        }
 }
 
 // SCHED: 0 = every wave issues its share, no stagger (r04); 1 = + stagger + late DMA;
@@ -796,12 +855,12 @@ using TX3 = TileX3<256, 64, 64, 32, 2, 1, 1>;
 using TX7 = TileX3<128, 32, 64, 32, 2, 1, 1>;  // (60 KB: LDS allows two blocks per CU)
 #define ROWGEMM_X3_TILES(X) X(0, TX0) X(1, TX1) X(2, TX2) X(3, TX3) X(7, TX7)
 
-template <int AMODE, int EMODE, class T, int XP = 0>
+template <int AMODE, int EMODE, class T, int XP = 0, bool M16 = false>
 static int x3_go(const RowGemmArgs& a, hipStream_t s) {
     if (a.N % T::BN || a.C % 32 || a.K % 32) return -1;
     if (EMODE == E_CONVT && (a.cout % T::BN) && (T::BN % a.cout)) return -1;
     const dim3 grid(((a.M + T::BM - 1) / T::BM) * (a.N / T::BN));
-    hipLaunchKernelGGL((rowgemm_x3_kernel<AMODE, EMODE, T, XP>), grid, dim3(T::THREADS), 0, s, a);
+    hipLaunchKernelGGL((rowgemm_x3_kernel<AMODE, EMODE, T, XP, M16>), grid, dim3(T::THREADS), 0, s, a);
     return (int)hipGetLastError();
 }
 
@@ -819,6 +878,9 @@ static int x3_tile(const RowGemmArgs& a, int tile, hipStream_t s, int sched = 0)
                              : x3r3_go<EMODE, 64, 128>(a, sched, s);
         return -1;
     }
+    // schedules >= 8 (16x16x32) also take the one-tap 64 x 64-wave tiles to 16x16x32 (r05)
+    if (sched >= 8 && tile == 0) return x3_go<AMODE, EMODE, TX0, 0, true>(a, s);
+    if (sched >= 8 && tile == 1) return x3_go<AMODE, EMODE, TX1, 0, true>(a, s);
 #define X3_CASE(id, T) \
     if (tile == id) return x3_go<AMODE, EMODE, T>(a, s);
     ROWGEMM_X3_TILES(X3_CASE)
@@ -882,7 +944,9 @@ struct WTileX3 {
     static constexpr int THREADS = 64 * WAVES;
 };
 
-template <int AMODE, int BMODE, class T>
+// M16 (r05): 16x16x32 MFMAs, one k-step of 32 pixels per chunk (as wgrad_x3_row3_kernel's: k
+// 8 g .. 8 g + 7 of lane group g = pixel rows 4 g + qq and 16 + 4 g + qq, swizzle x3_tswz16)
+template <int AMODE, int BMODE, class T, bool M16 = false>
 __global__ __launch_bounds__(T::THREADS, 1) void wgrad_x3_kernel(WgradArgs p) {
     constexpr int BM = T::BM, BN = T::BN, WM = T::WM, WN = T::WN, BKP = T::BKP, S = T::S;
     constexpr int WAVES = T::WAVES, WAVES_N = BN / WN;
@@ -921,14 +985,14 @@ __global__ __launch_bounds__(T::THREADS, 1) void wgrad_x3_kernel(WgradArgs p) {
         const int o = ((j * WAVES + wave) * 64 + lane) * 16;
         const int r = o / RA, sl = (o - r * RA) >> 4;
         arow[j] = r;
-        aele[j] = x3_tswz<RA>(sl, r) * 8;
+        aele[j] = (M16 ? x3_tswz16<RA>(sl, r) : x3_tswz<RA>(sl, r)) * 8;
     }
 #pragma unroll
     for (int j = 0; j < BI; ++j) {
         const int o = ((j * WAVES + wave) * 64 + lane) * 16;
         const int r = o / RBB, sl = (o - r * RBB) >> 4;
         brow[j] = r;
-        bele[j] = x3_tswz<RBB>(sl, r) * 8;
+        bele[j] = (M16 ? x3_tswz16<RBB>(sl, r) : x3_tswz<RBB>(sl, r)) * 8;
     }
     const uint16_t* a16 = (const uint16_t*)p.a + (size_t)(p.aoff + ca0) * 3;
     const uint16_t* b16 = (const uint16_t*)p.b + (size_t)(p.boff + cb0) * 3;
@@ -963,6 +1027,111 @@ __global__ __launch_bounds__(T::THREADS, 1) void wgrad_x3_kernel(WgradArgs p) {
     };
 
     constexpr int SA = T::SA;
+    static_assert(!M16 || SA, "16x16x32: split accumulators");
+    if constexpr (M16) {
+        f32x4 hi[MT][NT][2][2], lo[MT][NT][2][2];
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+#pragma unroll
+            for (int j = 0; j < NT; ++j)
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) hi[i][j][b >> 1][b & 1][r] = lo[i][j][b >> 1][b & 1][r] = 0.f;
+        const int g = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
+        const int trow = 4 * g + qq;
+        auto slot = [](int col, int q) { return (col >> 5) * 12 + q * 4 + ((col & 31) >> 3); };
+        int aoff[MT][2][3], boff[NT][2][3];
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+#pragma unroll
+                for (int mt = 0; mt < MT; ++mt) {
+                    const int col = wm * WM + mt * 32 + 16 * b + 4 * pp;
+                    aoff[mt][b][q] = trow * RA + (x3_tswz16<RA>(slot(col, q), trow) << 4) + ((col >> 2) & 1) * 8;
+                }
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt) {
+                    const int col = wn * WN + nt * 32 + 16 * b + 4 * pp;
+                    boff[nt][b][q] = BKP * RA + trow * RBB + (x3_tswz16<RBB>(slot(col, q), trow) << 4) + ((col >> 2) & 1) * 8;
+                }
+            }
+#pragma unroll
+        for (int s = 0; s < S - 1; ++s)
+            if (s < nk) issue(s, s);
+        for (int kc = 0; kc < nk; ++kc) {
+            if (kc + S - 1 < nk) issue(kc + S - 1, (kc + S - 1) % S);
+            const int ahead = min(S - 1, nk - 1 - kc);
+            if constexpr (S >= 3) {
+                if (ahead >= 2) x3_wait_vm<2 * GPC>();
+                else if (ahead == 1) x3_wait_vm<GPC>();
+                else x3_wait_vm<0>();
+            } else {
+                if (ahead >= 1) x3_wait_vm<GPC>();
+                else x3_wait_vm<0>();
+            }
+            x3_barrier();
+            const unsigned sb = x3_lds_u32(smem) + (kc % S) * STAGE;
+            x3_short4 fa[MT][2][3][2], fb[NT][2][3][2];
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+                for (int b = 0; b < 2; ++b)
+#pragma unroll
+                    for (int q = 0; q < 3; ++q) {
+                        fb[nt][b][q][0] = x3_tr16<0>(sb + boff[nt][b][q]);
+                        fb[nt][b][q][1] = x3_tr16<16 * RBB>(sb + boff[nt][b][q]);
+                    }
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                for (int b = 0; b < 2; ++b)
+#pragma unroll
+                    for (int q = 0; q < 3; ++q) {
+                        fa[mt][b][q][0] = x3_tr16<0>(sb + aoff[mt][b][q]);
+                        fa[mt][b][q][1] = x3_tr16<16 * RA>(sb + aoff[mt][b][q]);
+                    }
+            // the transposed reads are inline asm: their results are only valid after the wait,
+            // so no MFMA may be scheduled above it
+            __builtin_amdgcn_sched_barrier(0);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                for (int b = 0; b < 2; ++b)
+#pragma unroll
+                    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+                        for (int bn = 0; bn < 2; ++bn) {
+                            bf16x8 a3[3], b3[3];
+#pragma unroll
+                            for (int q = 0; q < 3; ++q) {
+                                a3[q] = *(const bf16x8*)fa[mt][b][q];
+                                b3[q] = *(const bf16x8*)fb[nt][bn][q];
+                            }
+                            mfma_x3s16(a3, b3, hi[mt][nt][b][bn], lo[mt][nt][b][bn]);
+                        }
+            x3_barrier();
+        }
+        float* slab = p.slab + (size_t)split * p.Mw * p.Nw;
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+                for (int b = 0; b < 2; ++b)
+#pragma unroll
+                    for (int bn = 0; bn < 2; ++bn)
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            const int m = tm * BM + wm * WM + mt * 32 + 16 * b + 4 * g + i;
+                            const int n = tn * BN + wn * WN + nt * 32 + 16 * bn + (lane & 15);
+                            slab[(size_t)m * p.Nw + n] = hi[mt][nt][b][bn][i] + lo[mt][nt][b][bn][i];
+                        }
+        return;
+    }
     f32x16 acc[MT][NT], acl[SA ? MT : 1][SA ? NT : 1];
 #pragma unroll
     for (int i = 0; i < MT; ++i)
@@ -1442,11 +1611,11 @@ using WX9 = WTileX3<32, 64, 32, 32, 3, 1>;
 using WX10 = WTileX3<32, 32, 32, 32, 3, 1>;
 #define WGRAD_X3_TILES(X) X(0, WX0) X(1, WX1) X(8, WX8) X(9, WX9) X(10, WX10)
 
-template <int AMODE, int BMODE, class T>
+template <int AMODE, int BMODE, class T, bool M16 = false>
 static int wx3_go(const WgradArgs& a, hipStream_t s) {
     if (a.Mw % T::BM || a.Nw % T::BN || a.CA % T::BM || a.CB % T::BN || a.pps % T::BKP) return -1;
     const dim3 grid((a.Mw / T::BM) * (a.Nw / T::BN) * a.splits);
-    hipLaunchKernelGGL((wgrad_x3_kernel<AMODE, BMODE, T>), grid, dim3(T::THREADS), 0, s, a);
+    hipLaunchKernelGGL((wgrad_x3_kernel<AMODE, BMODE, T, M16>), grid, dim3(T::THREADS), 0, s, a);
     return (int)hipGetLastError();
 }
 
@@ -1728,6 +1897,8 @@ int launch_wgrad_x3(const WgradArgs& a, int tile, hipStream_t s, int sched) {
     }
 #define WX3G(AM, BMD)                                        \
     do {                                                     \
+        if (tile == 0 && sched >= 8) return wx3_go<AM, BMD, WX0, true>(a, s); \
+        if (tile == 1 && sched >= 8) return wx3_go<AM, BMD, WX1, true>(a, s); \
         if (tile == 0) return wx3_go<AM, BMD, WX0>(a, s);    \
         if (tile == 1) return wx3_go<AM, BMD, WX1>(a, s);    \
         if (tile == 8) return wx3_go<AM, BMD, WX8>(a, s);    \

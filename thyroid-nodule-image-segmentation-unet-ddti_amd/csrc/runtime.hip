@@ -173,6 +173,9 @@ struct Options {
                                // first k-step's reads) +5..13 % per layer, config 2 591 -> 603 img/s;
                                // 8..10 the same on 16x16x32 MFMAs (x3r3_body16), 9 = 1's
                                // schedule: -4..-13 % per launch vs 1 (profiles/r05_halo_m16.txt)
+    int x3_1tap16 = 0;         // the one-tap x3 tiles (0 / 1 row GEMM, 0 / 1 weight gradient) follow
+                               // the 16x16x32 schedules (x3_r3_sched / x3_wsched >= 8; r05):
+                               // config 2 within noise (profiles/r05_1tap16_ab.txt), so off
     int x3_n32 = 0;            // x3 also for 32-multiple channel counts (r05; narrow widths)
     int x3_n64_r3 = 5;         // halo tile of the 64-output 3x3 GEMMs: 5 = 256x64 (8 waves, one
                                // block per CU), 6 = 128x64 (4 waves, two blocks per CU)
@@ -236,6 +239,7 @@ const OptionDesc OPTION_TABLE[] = {
     {"x3_n32", &Options::x3_n32},
     {"x3_n64_r3", &Options::x3_n64_r3},
     {"x3_wsched", &Options::x3_wsched},
+    {"x3_1tap16", &Options::x3_1tap16},
 };
 
 }  // namespace
@@ -787,6 +791,17 @@ bool x3_convt_on(const unet_ctx* c, int cin, int cout) { return x3_conv_on(c, ci
 
 // row-GEMM tile: 256x128 (one block of 8 waves per CU) unless that grid leaves CUs idle
 // (128x128), 128x64 for the 64-output GEMMs
+// the schedule argument of launch_rowgemm_x3 / launch_wgrad_x3 for a tile: the one-tap tiles
+// take the 16x16x32 kernels from schedules >= 8 unless option x3_1tap16 is off
+int x3_rsched(const unet_ctx* c, int tile) {
+    const int sc = c->opt.x3_r3_sched;
+    return (tile >= 4 && tile <= 6) || c->opt.x3_1tap16 ? sc : 0;
+}
+int x3_wsched(const unet_ctx* c, int tile) {
+    const int sc = c->opt.x3_wsched;
+    return (tile >= 2 && tile <= 7) || c->opt.x3_1tap16 ? sc : 0;
+}
+
 int x3_tile(const unet_ctx* c, const RowGemmArgs& g) {
     auto fits = [&](int t) {
         int bm = 0, bn = 0;
@@ -1344,7 +1359,7 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
                 use_x3(p, g, img, C.cin, p.pack3 + 3 * C.pf);
                 const int tile = x3_tile(c, g);
                 R = bn_groups(M);
-                RUN(xlabel("conv_fwd", tile, i), 2.0 * M * C.cout * 9 * C.cin, launch_rowgemm_x3(g, tile, s, c->opt.x3_r3_sched));
+                RUN(xlabel("conv_fwd", tile, i), 2.0 * M * C.cout * 9 * C.cin, launch_rowgemm_x3(g, tile, s, x3_rsched(c, tile)));
                 return stats_finalize(c, L, p, i, R, M, training, prm, bn_run, bn_cnt);
             }
             if (rg16_on(c, C.cin, C.cout)) {
@@ -1420,7 +1435,7 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
                 up16[idec] = true;
             }
             const int tile = x3_tile(c, g);
-            RUN(xlabel("convT_fwd", tile, 100 + k), 2.0 * g.M * g.N * g.K, launch_rowgemm_x3(g, tile, s, c->opt.x3_r3_sched));
+            RUN(xlabel("convT_fwd", tile, 100 + k), 2.0 * g.M * g.N * g.K, launch_rowgemm_x3(g, tile, s, x3_rsched(c, tile)));
             return 0;
         }
         if (!c->res && rg16_on(c, T.cin, T.cout)) {
@@ -1612,7 +1627,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
             w.splits = wc.splits;
             w.slab = p.slab;
             w.zero16 = p.zero16;
-            RUN(x3wlabel("conv_wgrad", wc, i), 2.0 * P * C.cout * 9 * C.cin, launch_wgrad_x3(w, wc.tile, s, c->opt.x3_wsched));
+            RUN(x3wlabel("conv_wgrad", wc, i), 2.0 * P * C.cout * 9 * C.cin, launch_wgrad_x3(w, wc.tile, s, x3_wsched(c, wc.tile)));
             RUN("wgrad_reduce", 0,
                 k_slab_reduce(p.slab, wc.splits, w.Mw, w.Nw, 0, C.cin, C.cout, grads + C.w, s));
             if (!dx) return 0;
@@ -1642,7 +1657,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
             }
             const int tile = x3_tile(c, g);
             if (rows) *rows = bn_groups(P);
-            RUN(xlabel("conv_dgrad", tile, i), 2.0 * P * C.cout * 9 * C.cin, launch_rowgemm_x3(g, tile, s, c->opt.x3_r3_sched));
+            RUN(xlabel("conv_dgrad", tile, i), 2.0 * P * C.cout * 9 * C.cin, launch_rowgemm_x3(g, tile, s, x3_rsched(c, tile)));
             return 0;
         }
         // bf16 image of dz: A operand of the LDS-DMA dgrad, B' of the LDS-DMA wgrad; the f32
@@ -1808,7 +1823,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
             w.slab = p.slab;
             w.zero16 = p.zero16;
             RUN(x3wlabel("convT_wgrad", wc, 100 + k), 2.0 * Pin * T.cin * 4 * T.cout,
-                launch_wgrad_x3(w, wc.tile, s, c->opt.x3_wsched));
+                launch_wgrad_x3(w, wc.tile, s, x3_wsched(c, wc.tile)));
             RUN("bias_grad", 0, k_up2_bias_partials(p.dcat[lo], ldo, uo, Hi, Wi, Pin, T.cout, wc.pps,
                                                     wc.splits, p.bslab, s));
             RUN("wgrad_reduce", 0,
@@ -1842,7 +1857,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
             const int tile = x3_tile(c, g);
             *rows = bn_groups(Pin);
             RUN(xlabel("convT_dgrad", tile, 100 + k), 2.0 * Pin * T.cin * 4 * T.cout,
-                launch_rowgemm_x3(g, tile, s, c->opt.x3_r3_sched));
+                launch_rowgemm_x3(g, tile, s, x3_rsched(c, tile)));
             return 0;
         }
         WgradCfg wc = wgrad_cfg(c, T.cin, 1, T.cout, 4, Pin, c->bf16);

@@ -7,6 +7,7 @@ TESTS=${2:-tests/test_gpu_x3.py}
 A=${3:-x3_r3_sched=1}
 B=${4:-x3_r3_sched=9}
 CFG=${5:-2}
+EXTRA=${6:-}
 mkdir -p gpurun_out
 if [ "$TESTS" != "none" ]; then
   timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread -p no:cacheprovider \
@@ -16,9 +17,9 @@ if [ "$TESTS" != "none" ]; then
   [ $rc -ne 0 ] && exit $rc
 fi
 for O in "$A" "$B" "$A" "$B"; do
-  timeout -k 10 300 python bench.py --config $CFG --steps 20 --warmup 5 --no-cpu-baseline --opt $O > gpurun_out/$TAG.json 2> gpurun_out/$TAG.err
+  timeout -k 10 300 python bench.py --config $CFG --steps 20 --warmup 5 --no-cpu-baseline $EXTRA --opt $O > gpurun_out/$TAG.json 2> gpurun_out/$TAG.err
   r=$?
-  echo "$O rc=$r $(python3 -c "import json;d=json.load(open('gpurun_out/$TAG.json'));print(d['value'], d['ms_per_step'], d['roofline']['achieved'], d['roofline']['kernel'])" 2>/dev/null)"
+  echo "$O rc=$r $(python3 -c "import json;d=json.load(open('gpurun_out/$TAG.json'));print(d['value'], d['ms_per_step'], d['roofline']['achieved'], d['roofline']['kernel'], d['roofline'].get('step_conv_frac'))" 2>/dev/null)"
   [ $r -ne 0 ] && { tail -5 gpurun_out/$TAG.err; exit $r; }
 done
 exit 0
