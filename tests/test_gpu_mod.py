@@ -321,7 +321,7 @@ def test_wg16_tap_row_bit_identical():
         _assert_same(outs[0], outs[r3], f"wg16_r3={r3} vs one-tap")
 
 
-@pytest.mark.parametrize("halo,sched", [(19, 0), (20, 0), (19, 8), (20, 8)])
+@pytest.mark.parametrize("halo,sched", [(19, 0), (20, 0), (19, 8)])
 def test_rg16_halo_tile_within_bf16_error(halo, sched):
     """Tiles 19 / 20 (the tap-row halo kernel at 256x256 / 512x128, kernels_gemm16.hip
     rowgemm16_row3_kernel) sum K in
