@@ -1263,7 +1263,7 @@ __global__ __launch_bounds__(T::THREADS, 1) void wgrad_x3_kernel(WgradArgs p) {
 // three stages with the next DMA issued behind the first k-step's fragment reads (as the halo
 // GEMM's schedule 1).  Same MFMAs in the same order per accumulator, same split partition:
 // bit-identical.
-template <int BM, int BN, int S = 3, int OCC = 1, int SCHED = 0>
+template <int BM, int BN, int S = 3, int OCC = 1, int SCHED = 0, bool W16 = false>
 __global__ __launch_bounds__((BM / 32) * (BN / 32) * 64, OCC) void wgrad_x3_row3_kernel(WgradArgs p) {
     constexpr int WAVES = (BM / 32) * (BN / 32), BKP = 32;
     constexpr int WAVES_N = BN / 32;
@@ -1274,7 +1274,9 @@ __global__ __launch_bounds__((BM / 32) * (BN / 32) * 64, OCC) void wgrad_x3_row3
     constexpr int DIST = (SCHED == 1 || SCHED == 2) ? 2 : S - 1;  // chunks the DMA runs ahead
     constexpr bool LATE = SCHED == 3 || SCHED == 9;  // the DMA issued after the first k-step's reads
     constexpr int RA = 6 * BM, RBB = 6 * BN;
-    constexpr int HALO = BKP + 2;
+    // halo pixel rows per stage: 34 (one 32-pixel row segment), or with M16 at W = 16 two
+    // image rows of 16 + 2 (r05: the 16x16 level's 3x3 weight gradients on this kernel too)
+    constexpr int HALO = M16 ? BKP + 4 : BKP + 2;
     constexpr int AREG = (HALO * RA + 1024 * WAVES - 1) / (1024 * WAVES) * WAVES * 1024;  // per stage
     constexpr int BREG = (BKP * RBB + 1024 * WAVES - 1) / (1024 * WAVES) * WAVES * 1024;
     constexpr int AI = AREG / (1024 * LW), BI = BREG / (1024 * LW);  // pieces per issuing wave
@@ -1306,10 +1308,15 @@ __global__ __launch_bounds__((BM / 32) * (BN / 32) * 64, OCC) void wgrad_x3_row3
     // staggered schedules recompute it per piece to stay within 256 VGPRs)
     constexpr bool KEEP = SCHED == 0;
     int arow[KEEP ? AI : 1], aele[KEEP ? AI : 1], brow[KEEP ? BI : 1], bele[KEEP ? BI : 1];
-    auto apiece = [&](int j, int& r, int& e) {
+    // W16 (launched for W = 16 only): two 18-row halo segments, swizzle by row mod 18 (its own
+    // instance: one kernel holding both loops costs 1-6 spilled VGPRs)
+    static_assert(!W16 || M16, "W = 16 on the 16x16x32 kernel only");
+    using W16T = std::integral_constant<bool, W16>;
+    auto apiece = [&](int j, int& r, int& e, auto W16C) {
+        constexpr bool TW = decltype(W16C)::value;
         const int o = ((j * LW + wave) * 64 + lane) * 16;
         r = o / RA;
-        e = (M16 ? x3_tswz16<RA>((o - r * RA) >> 4, r) : x3_tswz<RA>((o - r * RA) >> 4, r)) * 8;
+        e = (M16 ? x3_tswz16<RA>((o - r * RA) >> 4, TW ? r % 18 : r) : x3_tswz<RA>((o - r * RA) >> 4, r)) * 8;
     };
     auto bpiece = [&](int j, int& r, int& e) {
         const int o = ((j * LW + wave) * 64 + lane) * 16;
@@ -1318,7 +1325,7 @@ __global__ __launch_bounds__((BM / 32) * (BN / 32) * 64, OCC) void wgrad_x3_row3
     };
     if constexpr (KEEP) {
 #pragma unroll
-        for (int j = 0; j < AI; ++j) apiece(j, arow[j], aele[j]);
+        for (int j = 0; j < AI; ++j) apiece(j, arow[j], aele[j], std::false_type{});
 #pragma unroll
         for (int j = 0; j < BI; ++j) bpiece(j, brow[j], bele[j]);
     }
@@ -1327,7 +1334,8 @@ __global__ __launch_bounds__((BM / 32) * (BN / 32) * 64, OCC) void wgrad_x3_row3
     const size_t rowa = 3 * (size_t)p.lda, rowb = 3 * (size_t)p.ldb;
     const uint16_t* zero = (const uint16_t*)p.zero16;
 
-    auto issue = [&](int kc, int st) {
+    auto issue = [&](int kc, int st, auto W16C) {
+        constexpr bool TW = decltype(W16C)::value;
         const int pc = pbeg + kc * BKP;  // wave-uniform: the chunk's image row and first column
         const int t = pc / W, x0 = pc - t * W;
         const int img = t / H, y = t - img * H;
@@ -1339,10 +1347,14 @@ __global__ __launch_bounds__((BM / 32) * (BN / 32) * 64, OCC) void wgrad_x3_row3
         for (int j = 0; j < AI; ++j) {
             int ar, ae;
             if constexpr (KEEP) ar = arow[j], ae = aele[j];
-            else apiece(j, ar, ae);
-            const int xx = x0 - 1 + ar;
-            const bool ok = rowok && ar < HALO && xx >= 0 && xx < W;
-            const uint16_t* g = ok ? a16 + (size_t)(rowbase + xx) * rowa + ae : zero;
+            else apiece(j, ar, ae, W16C);
+            // W = 16 (w16): halo row ar = 18 seg + xl + 1 holds image row y + seg + dy - 1,
+            // column xl (the chunk is image rows y, y + 1; y even, H even)
+            const int seg = TW ? ar / 18 : 0;
+            const int xx = TW ? ar - seg * 18 - 1 : x0 - 1 + ar;
+            const bool segok = TW ? (seg < 2 && yy + seg >= 0 && yy + seg < H) : (rowok && ar < BKP + 2);
+            const bool ok = segok && xx >= 0 && xx < W;
+            const uint16_t* g = ok ? a16 + (size_t)(rowbase + seg * W + xx) * rowa + ae : zero;
             x3_dma16(g, base + (j * LW + wave) * 1024);
         }
 #pragma unroll
@@ -1380,6 +1392,7 @@ __global__ __launch_bounds__((BM / 32) * (BN / 32) * 64, OCC) void wgrad_x3_row3
 #pragma unroll
                 for (int q = 0; q < 3; ++q)
                     aoff[dx][bm][q] = (trow + dx) * RA + (x3_tswz16<RA>(slot(col, q), trow + dx) << 4) + ((col >> 2) & 1) * 8;
+            // (trow + dx <= 17: the same swizzle row for W = 16's row-mod-18 rule)
             const int colb = wn * 32 + 16 * bm + 4 * pp;
 #pragma unroll
             for (int q = 0; q < 3; ++q)
@@ -1391,7 +1404,13 @@ __global__ __launch_bounds__((BM / 32) * (BN / 32) * 64, OCC) void wgrad_x3_row3
             f[0] = x3_tr16<0>(addr);
             f[1] = x3_tr16<16 * rb>(addr);
         };
-        using IRA = std::integral_constant<int, RA>;
+        // A' second read: pixel rows 16 + 4 g + qq sit 16 halo rows on, or 18 at W = 16 (a
+        // compile-time offset per loop instance: an added address per read costs 18 VGPRs)
+        auto rda = [](x3_short4 (&f)[2], unsigned addr, auto W16C) {
+            constexpr int off = decltype(W16C)::value ? 18 * RA : 16 * RA;
+            f[0] = x3_tr16<0>(addr);
+            f[1] = x3_tr16<off>(addr);
+        };
         using IRB = std::integral_constant<int, RBB>;
         auto mma = [&](const x3_short4 (&fa)[3][3][2], const x3_short4 (&fb)[2][3][2], int bm) {
 #pragma unroll
@@ -1408,10 +1427,11 @@ __global__ __launch_bounds__((BM / 32) * (BN / 32) * 64, OCC) void wgrad_x3_row3
                 }
             }
         };
+        auto loop = [&](auto W16C) {
         if (issuer) {
 #pragma unroll
             for (int s = 0; s < DIST; ++s)
-                if (s < nk) issue(s, s);
+                if (s < nk) issue(s, s, W16C);
         }
         for (int kc = 0; kc < nk; ++kc) {
             if (issuer) {
@@ -1419,7 +1439,7 @@ __global__ __launch_bounds__((BM / 32) * (BN / 32) * 64, OCC) void wgrad_x3_row3
                 else x3_wait_vm<0>();
             }
             x3_barrier();
-            if (!LATE && issuer && kc + DIST < nk) issue(kc + DIST, (kc + DIST) % S);
+            if (!LATE && issuer && kc + DIST < nk) issue(kc + DIST, (kc + DIST) % S, W16C);
             const unsigned sb = sbase + (kc % S) * STAGE;
             x3_short4 fb[2][3][2], fa[3][3][2], fa1[3][3][2];
 #pragma unroll
@@ -1429,10 +1449,10 @@ __global__ __launch_bounds__((BM / 32) * (BN / 32) * 64, OCC) void wgrad_x3_row3
 #pragma unroll
             for (int dx = 0; dx < 3; ++dx)
 #pragma unroll
-                for (int q = 0; q < 3; ++q) rd(fa[dx][q], sb + aoff[dx][0][q], IRA{});
+                for (int q = 0; q < 3; ++q) rda(fa[dx][q], sb + aoff[dx][0][q], W16C);
             if (LATE && issuer && kc + DIST < nk) {
                 __builtin_amdgcn_sched_barrier(0);
-                issue(kc + DIST, (kc + DIST) % S);
+                issue(kc + DIST, (kc + DIST) % S, W16C);
                 __builtin_amdgcn_sched_barrier(0);
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1440,7 +1460,7 @@ __global__ __launch_bounds__((BM / 32) * (BN / 32) * 64, OCC) void wgrad_x3_row3
 #pragma unroll
             for (int dx = 0; dx < 3; ++dx)
 #pragma unroll
-                for (int q = 0; q < 3; ++q) rd(fa1[dx][q], sb + aoff[dx][1][q], IRA{});
+                for (int q = 0; q < 3; ++q) rda(fa1[dx][q], sb + aoff[dx][1][q], W16C);
             __builtin_amdgcn_sched_barrier(0);
             mma(fa, fb, 0);
             __builtin_amdgcn_sched_barrier(0);
@@ -1448,6 +1468,8 @@ __global__ __launch_bounds__((BM / 32) * (BN / 32) * 64, OCC) void wgrad_x3_row3
             __builtin_amdgcn_sched_barrier(0);
             mma(fa1, fb, 1);
         }
+        };
+        loop(W16T{});
         float* slab = p.slab + (size_t)split * p.Mw * p.Nw;
 #pragma unroll
         for (int dx = 0; dx < 3; ++dx)
@@ -1527,7 +1549,7 @@ __global__ __launch_bounds__((BM / 32) * (BN / 32) * 64, OCC) void wgrad_x3_row3
     if (issuer) {
 #pragma unroll
         for (int s = 0; s < DIST; ++s)
-            if (s < nk) issue(s, s);
+            if (s < nk) issue(s, s, std::false_type{});
     }
     // one chunk loop per role (separately register-allocated paths)
     auto run = [&](auto LAGC) {
@@ -1542,7 +1564,7 @@ __global__ __launch_bounds__((BM / 32) * (BN / 32) * 64, OCC) void wgrad_x3_row3
                 else x3_wait_vm<0>();
             }
             x3_barrier();
-            if (!LATE && issuer && kc + DIST < nk) issue(kc + DIST, (kc + DIST) % S);
+            if (!LATE && issuer && kc + DIST < nk) issue(kc + DIST, (kc + DIST) % S, std::false_type{});
             const unsigned sb = sbase + (kc % S) * STAGE;
             Frag f0, f1;
             if constexpr (LAG) {  // chunk kc - 1's second k-step, then this chunk's first
@@ -1564,7 +1586,7 @@ __global__ __launch_bounds__((BM / 32) * (BN / 32) * 64, OCC) void wgrad_x3_row3
                 load(f0, K0{}, sb);
                 if (LATE && issuer && kc + DIST < nk) {  // the DMA behind the first fragment reads
                     __builtin_amdgcn_sched_barrier(0);
-                    issue(kc + DIST, (kc + DIST) % S);
+                    issue(kc + DIST, (kc + DIST) % S, std::false_type{});
                     __builtin_amdgcn_sched_barrier(0);
                 }
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1861,8 +1883,10 @@ int launch_wgrad_x3(const WgradArgs& a, int tile, hipStream_t s, int sched) {
     if (tile >= 2 && tile <= 7) {  // tap-row kernel: 3x3 convs, W % 32 == 0
         int bm = 0, bn = 0;
         wgrad_x3_tile_dims(tile, &bm, &bn);
+        // W % 32 == 0, or (16x16x32 schedules, tiles 2..4) W = 16 with an even H
+        const bool w16ok = a.W == 16 && a.H % 2 == 0 && sched >= 8 && tile <= 4;
         if (a.amode != G_CONV3 || a.bmode != G_IDENT || a.Mw != 9 * a.CA || a.Nw != a.CB ||
-            a.CA % bm || a.CB % bn || a.W % 32 || a.pps % 32 || a.P % 32)
+            a.CA % bm || a.CB % bn || (a.W % 32 && !w16ok) || a.pps % 32 || a.P % 32)
             return -1;
         const dim3 grid((a.CA / bm) * 3 * (a.CB / bn) * a.splits);
         if (tile == 2 && sched == 1)
@@ -1873,6 +1897,12 @@ int launch_wgrad_x3(const WgradArgs& a, int tile, hipStream_t s, int sched) {
             hipLaunchKernelGGL((wgrad_x3_row3_kernel<64, 128, 3, 1, 3>), grid, dim3(512), 0, s, a);
         else if (tile == 3 && sched == 3)
             hipLaunchKernelGGL((wgrad_x3_row3_kernel<128, 64, 3, 1, 3>), grid, dim3(512), 0, s, a);
+        else if (a.W == 16 && tile == 2)  // 16x16x32 at W = 16 (w16ok: sched >= 8)
+            hipLaunchKernelGGL((wgrad_x3_row3_kernel<64, 128, 3, 1, 9, true>), grid, dim3(512), 0, s, a);
+        else if (a.W == 16 && tile == 3)
+            hipLaunchKernelGGL((wgrad_x3_row3_kernel<128, 64, 3, 1, 8, true>), grid, dim3(512), 0, s, a);
+        else if (a.W == 16 && tile == 4)
+            hipLaunchKernelGGL((wgrad_x3_row3_kernel<64, 64, 2, 2, 8, true>), grid, dim3(256), 0, s, a);
         else if (tile == 2 && sched == 8)  // 16x16x32 (r05)
             hipLaunchKernelGGL((wgrad_x3_row3_kernel<64, 128, 3, 1, 8>), grid, dim3(512), 0, s, a);
         else if (tile == 2 && sched == 9)

@@ -832,10 +832,12 @@ int x3_tile(const unet_ctx* c, const RowGemmArgs& g) {
 // 3x3 convs on rows of a multiple of 32 pixels (row_w): the tap-row kernel (tiles 2 = 64x128,
 // 3 = 128x64 per tap, three taps per block)
 WgradCfg x3_wgrad_cfg(const unet_ctx* c, int CA, int tapsA, int CB, int tapsB, int64_t P,
-                      int row_w = 0) {
+                      int row_w = 0, int row_h = 0) {
     WgradCfg w{};
     w.tile = (CA % 128 == 0 && CB % 128 == 0) ? 0 : 1;
-    const bool r3 = tapsA == 9 && tapsB == 1 && row_w % 32 == 0 && row_w > 0;
+    // tap-row kernel: rows of 32k pixels, or (16x16x32 schedules, r05) 16-pixel rows in pairs
+    const bool w16 = row_w == 16 && row_h % 2 == 0 && c->opt.x3_wsched >= 8 && CA % 64 == 0 && CB % 64 == 0;
+    const bool r3 = tapsA == 9 && tapsB == 1 && ((row_w % 32 == 0 && row_w > 0) || w16);
     if (r3 && CA % 64 == 0 && CB % 128 == 0) w.tile = 2;
     else if (r3 && CA % 128 == 0 && CB % 64 == 0) w.tile = 3;
     else if (r3 && CA % 64 == 0 && CB % 64 == 0) w.tile = 4;
@@ -1030,7 +1032,7 @@ void make_plan(unet_ctx* c, int N, int H, int W, bool training, char* base, Plan
         for (int i = 1; i < NC; ++i) {
             const ConvL& L = c->conv[i];
             WgradCfg w = x3_conv_on(c, L.cin, L.cout)
-                             ? x3_wgrad_cfg(c, L.cin, 9, L.cout, 1, p.P[L.level], W >> L.level)
+                             ? x3_wgrad_cfg(c, L.cin, 9, L.cout, 1, p.P[L.level], W >> L.level, H >> L.level)
                              : wgrad_cfg(c, L.cin, 9, L.cout, 1, p.P[L.level], c->bf16, W >> L.level);
             smax = std::max(smax, (int64_t)w.splits * 9 * L.cin * L.cout);
             bmax = std::max(bmax, (int64_t)w.splits * L.cout);
@@ -1607,7 +1609,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
                     RUN("bias_grad", 0, k_sum_partials(p.part, G, C.cout, grads + C.b, s));
                 }
             }
-            const WgradCfg wc = x3_wgrad_cfg(c, C.cin, 9, C.cout, 1, P, Wl);
+            const WgradCfg wc = x3_wgrad_cfg(c, C.cin, 9, C.cout, 1, P, Wl, Hl);
             WgradArgs w{};
             w.xcd = 1;
             w.H = Hl;
