@@ -173,6 +173,9 @@ struct Options {
                                // first k-step's reads) +5..13 % per layer, config 2 591 -> 603 img/s;
                                // 8..10 the same on 16x16x32 MFMAs (x3r3_body16), 9 = 1's
                                // schedule: -4..-13 % per launch vs 1 (profiles/r05_halo_m16.txt)
+    int x3_wwaves = 3;         // tap-row x3 weight gradients: split-K so the grid is this many full
+                               // waves of block slots (0 = the x3_wblocks target; r05,
+                               // profiles/r05_wwaves_ab.txt)
     int x3_1tap16 = 0;         // the one-tap x3 tiles (0 / 1 row GEMM, 0 / 1 weight gradient) follow
                                // the 16x16x32 schedules (x3_r3_sched / x3_wsched >= 8; r05):
                                // config 2 within noise (profiles/r05_1tap16_ab.txt), so off
@@ -240,6 +243,7 @@ const OptionDesc OPTION_TABLE[] = {
     {"x3_n64_r3", &Options::x3_n64_r3},
     {"x3_wsched", &Options::x3_wsched},
     {"x3_1tap16", &Options::x3_1tap16},
+    {"x3_wwaves", &Options::x3_wwaves},
 };
 
 }  // namespace
@@ -864,6 +868,15 @@ WgradCfg x3_wgrad_cfg(const unet_ctx* c, int CA, int tapsA, int CB, int tapsB, i
     int64_t splits = std::max<int64_t>(1, (target + tiles - 1) / tiles);
     int64_t pps = (P + splits - 1) / splits;
     pps = (pps + 255) / 256 * 256;
+    if (tap_row && c->opt.x3_wwaves > 0) {
+        // (r05) exactly x3_wwaves full waves of block slots (256 CUs x blocks per CU): at most
+        // that many blocks, pixel splits in 32-pixel steps.  The 256-pixel rounding above can
+        // land a few blocks past a wave boundary (1024: 2049 blocks on 2048 slots, -4 %)
+        const int64_t slots = 256LL * (w.tile == 4 ? 2 : 1) * c->opt.x3_wwaves;
+        const int64_t s = std::max<int64_t>(1, slots / tiles);
+        pps = (P + s - 1) / s;
+        pps = (pps + 31) / 32 * 32;
+    }
     w.pps = (int)pps;
     w.splits = (int)((P + pps - 1) / pps);
     return w;
