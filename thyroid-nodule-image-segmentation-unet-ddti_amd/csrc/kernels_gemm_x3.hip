@@ -822,6 +822,199 @@ __global__ __launch_bounds__(BM / 64 * 2 * 64, BM == 256 ? 1 : 2) void rowgemm_x
     row_epilogue<EMODE, BM, BN, WM, WN, true>(p, acc, m0, n0, tile_m, wm, wn, lane, tid, (float*)smem);
 }
 
+// ------------------------------------------------------------------------------------
+// Tile 8 (r05): the 64-output 3x3 GEMMs on a 512 x 64 halo tile, 8 waves of 64 x 64 -- the
+// 256 x 128 kernel's wave tile -- over TWO image rows of 256.  A 32-channel halo of two rows
+// (2 x 258 x 192 B) cannot be double-buffered in 160 KB, so the channel group is 16: x3 rows of
+// 96 B ([h | m | l] x 16 channels), a halo stage of 516 rows = 49.5 KB (56 KB region), one
+// 32x32x16 k-step per sub-step (dy, 16-channel group, dx).  Per 768 MFMA cycles a wave issues
+// ~3 LDS-DMA pieces (the 256 x 64 tile: ~4.3) and reads 12 fragments for 24 MFMAs (64 x 32
+// waves: 9 for 12).  LDS: 2 x 56 KB halo + 2 x 8 KB B = 128 KB, one block per CU.
+//   swizzle: 16-B half h of plane q of row r at slot 2 q + (h ^ ((r >> 3) & 1)) -- rows r and
+//   r + 8 share a bank slot (96 B = 6 slots), the 16 rows of a ds_read_b128 lane group then
+//   land on 16 distinct slots.
+//   K order (dy, 16-channel group, dx): results agree with the other tiles to f32 rounding.
+//   LAG (schedule 1, default): waves 4..7 run their second 32-row half's MFMAs after the next
+//   barrier from held fragments; LATE: the next sub-step's DMA after this one's reads.
+// ------------------------------------------------------------------------------------
+template <int EMODE, bool LAG, bool LATE>
+__global__ __launch_bounds__(512, 1) void rowgemm_x3_r3k16_kernel(RowGemmArgs p) {
+    constexpr int BM = 512, BN = 64, BK = 16, WM = 64, WN = 64, WAVES = 8, MT = 2, NT = 2;
+    constexpr int RB = 96, AR = BM / 16 * 18;
+    constexpr int AREG = ((AR * RB + 1024 * WAVES - 1) / (1024 * WAVES)) * WAVES * 1024;  // 56 KB
+    constexpr int BREG = ((BN * RB + 1024 * WAVES - 1) / (1024 * WAVES)) * WAVES * 1024;  // 8 KB
+    constexpr int AI = AREG / (1024 * WAVES), BI = BREG / (1024 * WAVES);
+    constexpr int AC = (AI + 2) / 3;
+    constexpr int SMEM = 2 * AREG + 2 * BREG;
+    static_assert(SMEM >= 2 * (BM / 64) * BN * 8, "epilogue scratch");
+    __shared__ __attribute__((aligned(1024))) char smem[SMEM];
+    auto swz = [](int r) { return (r >> 3) & 1; };
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave, wn = 0;
+    const int ntn = p.N / BN;
+    const int bid = p.xcd ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+    const int tile_m = bid / ntn, tile_n = bid - tile_m * ntn;
+    const int m0 = tile_m * BM, n0 = tile_n * BN;
+    const int H = p.H, W = p.W, C = p.C, K = p.K;
+    const int SEG = W < BM ? W : BM, HW = SEG + 2;
+    const int AROWS = (BM / SEG) * HW;
+    const size_t rowa = 3 * (size_t)p.lda, rowb = 3 * (size_t)K;
+    // A loader: lane of piece j fills halo bytes (j 8 + wave) KB + 16 lane = halo row h, slot k =
+    // w / 16 (plane k / 2, half k & 1) sourcing the (half ^ swz(h)) 8 channels of that plane
+    int acen[AI], apk[AI];
+#pragma unroll
+    for (int j = 0; j < AI; ++j) {
+        const int o = ((j * WAVES + wave) * 64 + lane) * 16;
+        const int h = o / RB, k = (o - h * RB) >> 4;
+        const int r = h / HW, xl = h - r * HW - 1;
+        const int mrow = m0 + r * SEG;
+        bool ok = h < AROWS && mrow < p.M;
+        const Pix q = decode(ok ? mrow : 0, H, W);
+        ok = ok && q.x + xl >= 0 && q.x + xl < W;
+        acen[j] = ok ? mrow + xl : -1;
+        apk[j] = q.y * 128 + (k >> 1) * 32 + (((k & 1) ^ swz(h)) << 3);
+    }
+    int boff[BI];
+#pragma unroll
+    for (int j = 0; j < BI; ++j) {
+        const int o = ((j * WAVES + wave) * 64 + lane) * 16;
+        const int r = o / RB, k = (o - r * RB) >> 4;
+        boff[j] = r < BN ? (int)((n0 + r) * rowb) + (k >> 1) * 32 + (((k & 1) ^ swz(r)) << 3) : -1;
+    }
+    const uint16_t* zero = (const uint16_t*)p.zero16;
+    const uint16_t* a16 = p.a16 + (size_t)p.aoff * 3;
+    const int CC = C / BK;  // 16-channel groups per tap
+    const int NG = 3 * CC;  // halo groups (dy, group)
+    const int ns = 9 * CC;  // sub-steps (dy, group, dx)
+    // element offset of channel c0 (a multiple of 16) inside an x3 row: its 32-channel chunk
+    // of 96 elements, then the 16-channel half of each plane
+    auto chunk = [](int c0) { return (c0 >> 5) * 96 + ((c0 >> 4) & 1) * 16; };
+    auto issue_a = [&](int g, int j0, int j1) {
+        const int dy = g / CC, c0 = (g - dy * CC) * BK;
+        char* base = smem + (g & 1) * AREG;
+        const int ce = chunk(c0);
+#pragma unroll
+        for (int j = 0; j < AI; ++j) {
+            if (j < j0 || j >= j1) continue;
+            const int yy = (apk[j] >> 7) + dy - 1;
+            const bool valid = acen[j] >= 0 && yy >= 0 && yy < H;
+            const uint16_t* src =
+                valid ? a16 + (size_t)(acen[j] + (dy - 1) * W) * rowa + ce + (apk[j] & 127) : zero;
+            x3_dma16(src, base + (j * WAVES + wave) * 1024);
+        }
+    };
+    auto issue_b = [&](int s) {
+        const int g = s / 3, dx = s - g * 3;
+        const int dy = g / CC, c0 = (g - dy * CC) * BK;
+        const int ke = chunk((dy * 3 + dx) * C + c0);
+        char* base = smem + 2 * AREG + (s & 1) * BREG;
+#pragma unroll
+        for (int j = 0; j < BI; ++j)
+            x3_dma16(boff[j] >= 0 ? p.bt16 + boff[j] + ke : zero, base + (j * WAVES + wave) * 1024);
+    };
+    auto issue = [&](int s) {
+        const int g = s / 3, dx = s - g * 3;
+        if (s + 1 < ns) issue_b(s + 1);
+        if (g + 1 < NG) issue_a(g + 1, dx * AC, dx * AC + AC);
+    };
+    const int lh = lane >> 5, li = lane & 31;
+    int ahb[MT], bro[NT], bfx[NT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+        const int mo = wm * WM + mt * 32 + li;
+        const int r = mo / SEG;
+        ahb[mt] = r * HW + (mo - r * SEG);
+    }
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+        const int r = wn * WN + nt * 32 + li;
+        bro[nt] = r * RB;
+        bfx[nt] = swz(r);
+    }
+    f32x16 acc[MT][NT], acl[MT][NT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = acl[i][j][r] = 0.f;
+    auto run = [&](auto LAGC) {
+        constexpr bool LG = decltype(LAGC)::value;
+        bf16x8 ha[3], hb[NT][3];  // LG: the previous sub-step's second-half fragments
+        issue_a(0, 0, AI);
+        issue_b(0);
+        for (int s = 0; s < ns; ++s) {
+            const int g = s / 3, dx = s - g * 3;
+            if (dx >= 1 && g + 1 < NG) x3_wait_vm<AC>();
+            else x3_wait_vm<0>();
+            x3_barrier();
+            if constexpr (!LATE) issue(s);
+            if constexpr (LG) {
+                if (s > 0) {
+#pragma unroll
+                    for (int nt = 0; nt < NT; ++nt) mfma_x3s(ha, hb[nt], acc[1][nt], acl[1][nt]);
+                }
+            }
+            const char* abase = smem + (g & 1) * AREG;
+            const char* bbase = smem + 2 * AREG + (s & 1) * BREG;
+            bf16x8 af[MT][3], bfr[NT][3];
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+                for (int q = 0; q < 3; ++q)
+                    bfr[nt][q] = *(const bf16x8*)(bbase + bro[nt] + q * 32 + ((lh ^ bfx[nt]) << 4));
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt) {
+                const int h = ahb[mt] + dx;
+#pragma unroll
+                for (int q = 0; q < 3; ++q)
+                    af[mt][q] = *(const bf16x8*)(abase + h * RB + q * 32 + ((lh ^ swz(h)) << 4));
+            }
+            if constexpr (LATE) issue(s);
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) mfma_x3s(af[0], bfr[nt], acc[0][nt], acl[0][nt]);
+            if constexpr (LG) {
+#pragma unroll
+                for (int q = 0; q < 3; ++q) ha[q] = af[1][q];
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+                    for (int q = 0; q < 3; ++q) hb[nt][q] = bfr[nt][q];
+            } else {
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt) mfma_x3s(af[1], bfr[nt], acc[1][nt], acl[1][nt]);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
+        if constexpr (LG) {
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) mfma_x3s(ha, hb[nt], acc[1][nt], acl[1][nt]);
+        }
+    };
+    if (LAG && wave >= 4) run(std::true_type{});
+    else run(std::false_type{});
+    x3_barrier();  // the epilogue reuses the stage memory
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) acc[mt][nt] += acl[mt][nt];
+    row_epilogue<EMODE, BM, BN, WM, WN, true>(p, acc, m0, n0, tile_m, wm, wn, lane, tid, (float*)smem);
+}
+
+template <int EMODE>
+static int x3r3k16_go(const RowGemmArgs& a, int sched, hipStream_t s) {
+    if (a.amode != G_CONV3 || a.N % 64 || a.C % 32 || a.K != 9 * a.C) return -1;
+    if (a.W < 16 || (512 % a.W && a.W % 512)) return -1;
+    const dim3 grid(((a.M + 511) / 512) * (a.N / 64));
+    // schedules: 0 = no stagger (DMA after the barrier), 1 (and the others) = stagger + late DMA
+    if (sched == 0)
+        hipLaunchKernelGGL((rowgemm_x3_r3k16_kernel<EMODE, false, false>), grid, dim3(512), 0, s, a);
+    else
+        hipLaunchKernelGGL((rowgemm_x3_r3k16_kernel<EMODE, true, true>), grid, dim3(512), 0, s, a);
+    return (int)hipGetLastError();
+}
+
 template <int EMODE, int BN, int BM = 256>
 static int x3r3_go(const RowGemmArgs& a, int sched, hipStream_t s) {
     // BM % W == 0 or W % BM == 0 keeps a tile on whole rows / row segments; W >= 16 bounds the halo
@@ -866,6 +1059,10 @@ static int x3_go(const RowGemmArgs& a, hipStream_t s) {
 
 template <int AMODE, int EMODE>
 static int x3_tile(const RowGemmArgs& a, int tile, hipStream_t s, int sched = 0) {
+    if (tile == 8) {  // 512 x 64, 16-channel halo groups (r05)
+        if constexpr (AMODE == G_CONV3) return x3r3k16_go<EMODE>(a, sched >= 8 ? 1 : sched, s);
+        return -1;
+    }
     if (tile == 4 || tile == 5 || tile == 6) {  // tap-row halo kernel (3x3 convs): 256 x 128 / 256 x 64 / 128 x 64
         // (r04, not kept: 4-wave 128x64 / 64x128 wave tiles, within noise of 8 waves; B
         // straight from global memory into registers instead of the LDS ring, one barrier per
@@ -1806,6 +2003,11 @@ int rowgemm_x3_tile_dims(int tile, int* bm, int* bn) {
     if (tile == 4 || tile == 5 || tile == 6) {  // tap-row halo 256 x 128 / 256 x 64 / 128 x 64
         *bm = tile == 6 ? 128 : 256;
         *bn = tile == 4 ? 128 : 64;
+        return 0;
+    }
+    if (tile == 8) {  // tap-row halo 512 x 64, 16-channel groups
+        *bm = 512;
+        *bn = 64;
         return 0;
     }
 #define X3_DIMS(id, T)  \

@@ -176,12 +176,16 @@ struct Options {
     int x3_wwaves = 3;         // tap-row x3 weight gradients: split-K so the grid is this many full
                                // waves of block slots (0 = the x3_wblocks target; r05,
                                // profiles/r05_wwaves_ab.txt)
+    int x3_wwaves1 = 3;        // the same for the one-tap x3 weight gradients (ConvT, 8x8):
+                               // +0.45 % (profiles/r05_wwaves_ab.txt)
     int x3_1tap16 = 0;         // the one-tap x3 tiles (0 / 1 row GEMM, 0 / 1 weight gradient) follow
                                // the 16x16x32 schedules (x3_r3_sched / x3_wsched >= 8; r05):
                                // config 2 within noise (profiles/r05_1tap16_ab.txt), so off
     int x3_n32 = 0;            // x3 also for 32-multiple channel counts (r05; narrow widths)
     int x3_n64_r3 = 5;         // halo tile of the 64-output 3x3 GEMMs: 5 = 256x64 (8 waves, one
-                               // block per CU), 6 = 128x64 (4 waves, two blocks per CU)
+                               // block per CU), 6 = 128x64 (4 waves, two blocks per CU), 8 =
+                               // 512x64 over 16-channel groups (r05: 1.103 vs 1.032 ms at level 0,
+                               // profiles/r05_halo_k16.txt -- not faster, kept as an option)
     int x3_wsched = 9;         // the tap-row weight gradient's schedule (0 = r04, 1 = four stages
                                // with waves 4..7 half a chunk behind, 2 = 1 with waves 0..3
                                // issuing every DMA (64x128 only), 3 = the DMA after the first
@@ -244,6 +248,7 @@ const OptionDesc OPTION_TABLE[] = {
     {"x3_wsched", &Options::x3_wsched},
     {"x3_1tap16", &Options::x3_1tap16},
     {"x3_wwaves", &Options::x3_wwaves},
+    {"x3_wwaves1", &Options::x3_wwaves1},
 };
 
 }  // namespace
@@ -814,8 +819,10 @@ int x3_tile(const unet_ctx* c, const RowGemmArgs& g) {
     };
     // tile 4: the tap-row halo kernel (3x3 convs on rows of 16 .. 256k pixels, option x3_r3)
     const bool r3ok = g.amode == G_CONV3 && g.W >= 16 && (256 % g.W == 0 || g.W % 256 == 0);
-    if (c->opt.x3_tile >= 0 && fits(c->opt.x3_tile) && (c->opt.x3_tile < 4 || c->opt.x3_tile > 6 || r3ok))
-        return c->opt.x3_tile;
+    const bool r3ok8 = g.amode == G_CONV3 && g.W >= 16 && (512 % g.W == 0 || g.W % 512 == 0);
+    const int ft = c->opt.x3_tile;
+    if (ft >= 0 && fits(ft) && ((ft < 4 || ft == 7) || (ft >= 4 && ft <= 6 && r3ok) || (ft == 8 && r3ok8)))
+        return ft;
     if (g.N % 128 == 0 && fits(0)) {
         const int64_t blocks = (int64_t)(g.M + 255) / 256 * (g.N / 128);
         if (blocks < 256) return 1;
@@ -823,8 +830,10 @@ int x3_tile(const unet_ctx* c, const RowGemmArgs& g) {
     }
     // 64 outputs: a halo tile (5 = 256 x 64, one block per CU; 6 = 128 x 64, two blocks per
     // CU: option x3_n64_r3) where the 256-row grid fills the chip
-    if (g.N % 64 == 0 && c->opt.x3_r3 && r3ok && (int64_t)(g.M + 255) / 256 >= 512)
+    if (g.N % 64 == 0 && c->opt.x3_r3 && r3ok && (int64_t)(g.M + 255) / 256 >= 512) {
+        if (c->opt.x3_n64_r3 == 8 && r3ok8) return 8;
         return c->opt.x3_n64_r3 == 6 ? 6 : 5;
+    }
     // 32-multiple outputs, or a ConvT whose cout is not a 64-tile fit (option x3_n32): 128 x 32
     if (g.N % 64 || !fits(c->opt.x3_n64)) return 7;
     return c->opt.x3_n64;
@@ -868,11 +877,12 @@ WgradCfg x3_wgrad_cfg(const unet_ctx* c, int CA, int tapsA, int CB, int tapsB, i
     int64_t splits = std::max<int64_t>(1, (target + tiles - 1) / tiles);
     int64_t pps = (P + splits - 1) / splits;
     pps = (pps + 255) / 256 * 256;
-    if (tap_row && c->opt.x3_wwaves > 0) {
-        // (r05) exactly x3_wwaves full waves of block slots (256 CUs x blocks per CU): at most
+    const int ww = tap_row ? c->opt.x3_wwaves : c->opt.x3_wwaves1;
+    if (w.tile <= 4 && ww > 0) {
+        // (r05) exactly `ww` full waves of block slots (256 CUs x blocks per CU): at most
         // that many blocks, pixel splits in 32-pixel steps.  The 256-pixel rounding above can
         // land a few blocks past a wave boundary (1024: 2049 blocks on 2048 slots, -4 %)
-        const int64_t slots = 256LL * (w.tile == 4 ? 2 : 1) * c->opt.x3_wwaves;
+        const int64_t slots = 256LL * (w.tile == 4 || w.tile == 1 ? 2 : 1) * ww;
         const int64_t s = std::max<int64_t>(1, slots / tiles);
         pps = (P + s - 1) / s;
         pps = (pps + 31) / 32 * 32;
@@ -907,7 +917,7 @@ std::string xlabel(const char* fam, int tile, int layer) {
     int bm = 0, bn = 0;
     rowgemm_x3_tile_dims(tile, &bm, &bn);
     char b[112];
-    snprintf(b, sizeof b, "%s/x3%s_%dx%d|%d", fam, tile >= 4 && tile <= 6 ? "r3" : "", bm, bn, layer);
+    snprintf(b, sizeof b, "%s/x3%s_%dx%d|%d", fam, tile == 8 ? "r3k16" : tile >= 4 && tile <= 6 ? "r3" : "", bm, bn, layer);
     return b;
 }
 

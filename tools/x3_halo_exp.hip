@@ -503,7 +503,7 @@ int go(const RowGemmArgs& a) {
     return (int)hipGetLastError();
 }
 
-#define FLAG_LIST(X) X(0) X(1) X(2) X(4) X(7) X(16) X(96) X(112) X(4096) X(4112) X(4128) X(4160) X(4176) X(4192) X(4208) X(8192) X(8199) X(8288)
+#define FLAG_LIST(X) X(0) X(1) X(2) X(4) X(7) X(16) X(96) X(112) X(4096) X(4112) X(4128) X(4160) X(4176) X(4192) X(4208)
 
 int run(const RowGemmArgs& a, int bn, int f) {
 #define FCASE(v)                                       \
@@ -584,6 +584,20 @@ int main(int argc, char** argv) {
         std::vector<float> r((size_t)M * N), q((size_t)M * N);
         CK(hipMemcpy(r.data(), yref, r.size() * 4, hipMemcpyDeviceToHost));
         h.out = y;
+        if (bn == 64) {  // the 512 x 64 16-channel-group halo tile (tile 8), schedules 0 / 1
+            for (int sc = 0; sc < 2; ++sc) {
+                CK(hipMemset(y, 0, (size_t)M * N * 4));
+                const float t = timeit([&] { return launch_rowgemm_x3(h, 8, 0, sc); });
+                CK(hipMemcpy(q.data(), y, q.size() * 4, hipMemcpyDeviceToHost));
+                double dmax = 0, rmx = 0;
+                for (size_t i = 0; i < q.size(); ++i) {
+                    dmax = std::max(dmax, (double)fabsf(q[i] - r[i]));
+                    rmx = std::max(rmx, (double)fabsf(r[i]));
+                }
+                printf("    library tile 8 (512x64 k16) sched %d: %.3f ms %.1f TF/s  (max |diff| %.3g of %.3g)\n", sc,
+                       t, fl / t / 1e9, dmax, rmx);
+            }
+        }
         if (bn == 64) {  // the 128 x 64 two-blocks-per-CU halo tile
             CK(hipMemset(y, 0, (size_t)M * N * 4));
             const float t = timeit([&] { return launch_rowgemm_x3(h, 6, 0, 0); });
@@ -592,7 +606,7 @@ int main(int argc, char** argv) {
             printf("    library tile 6 (128x64, 2/CU): %.3f ms %.1f TF/s  %s\n", t, fl / t / 1e9,
                    same ? "bit-identical" : "DIFFERS");
         }
-        const int scheds[] = {1, 8, 9, 10, 12, 13};  // the library's schedules (8.. = 16x16x32)
+        const int scheds[] = {1, 9};  // the library's schedules (8.. = 16x16x32)
         double rmax = 0;
         for (float v : r) rmax = std::max(rmax, (double)fabsf(v));
         for (int sc : scheds) {
