@@ -252,6 +252,28 @@ def test_x3_one_tap_m16_close():
     assert torch.allclose(g1, g0, rtol=1e-3, atol=1e-5 * g0.abs().max().item()), (g1 - g0).abs().max().item()
 
 
+def test_x3_head_fuse_bit_identical():
+    """Option head_fuse (r05, default on): with one output channel the last conv's x3 dz pass
+    recomputes its `do` = [activation > 0] dl w from the logit gradient (head_bwd's own fma
+    mask and product) instead of reading a full-resolution f32 `do` that head_bwd stored: one
+    training step is bit-identical either way."""
+    import unet_hip
+    from _helpers import options
+    x, t = inputs(47, 2, 128, 128)
+    outs = []
+    for flag in (0, 1):
+        m = hip_model(O.make_params(53), DEV)
+        with options(m.flatten_().rt, head_fuse=flag):
+            logits = m(x.to(DEV))
+            l = unet_hip.seg_losses(logits, t.to(DEV))
+            (l[0] + l[1]).backward()
+            torch.cuda.synchronize()
+        outs.append((logits.detach().clone(), m._state.grad_arena.clone()))
+        del m
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1]), (outs[0][1] - outs[1][1]).abs().max().item()
+
+
 def test_x3_wgrad_schedules_bit_identical():
     """The 64x128 tap-row x3 weight gradient's schedules (option x3_wsched: four LDS stages
     with waves 4..7 half a chunk behind, and the same with waves 0..3 issuing every DMA; 8, 9 the

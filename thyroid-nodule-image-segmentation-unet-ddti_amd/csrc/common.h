@@ -169,8 +169,12 @@ int wgrad_x3_tile_dims(int tile, int* bm, int* bn);
 int k_to_x3(const float* src, int ld, int off, int C, const float* scale, const float* shift,
             int relu, int64_t P, uint16_t* dst, int dld, int doff, hipStream_t s);
 // BN-backward dz (bn_dz4) as an x3 image; bpart (optional): [x3_dz_blocks(P)][C] column sums
+// hdl != null (r05): `d` is not read; do = [hrelu: fma(y, hsc, hsh) > 0] hdl[m] hw[c] (the 1x1
+// head's backward with one output channel, head_bwd's expression)
 int k_bn_dz_x3(const float* d, const float* y, int ld, int off, int64_t P, int C, const float* coef,
-               int mask, uint16_t* dz3, float* bpart, hipStream_t s);
+               int mask, uint16_t* dz3, float* bpart, hipStream_t s, const float* hdl = nullptr,
+               const float* hw = nullptr, const float* hsc = nullptr, const float* hsh = nullptr,
+               int hrelu = 0);
 int x3_dz_blocks(int64_t P);
 // register-staged bf16 wgrad tile ids (a.bf16): 0 = 128x128/32 px, 2 = 64x64/64,
 // 3 = 128x64/64, 4 = 64x128/64

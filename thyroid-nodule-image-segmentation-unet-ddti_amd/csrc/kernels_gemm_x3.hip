@@ -1932,11 +1932,22 @@ __global__ __launch_bounds__(256) void to_x3_kernel(const float* __restrict__ sr
 // block covers rpb rows (x3_rows_per_block); thread t handles channel octet t % (C / 8) of
 // rows t / (C / 8) + k 256 / (C / 8), X3_RIF rows in flight (the column sums add each thread's
 // rows in ascending order).
+// HEAD (r05): the last conv's `do` is not read from memory but recomputed from the 1x1 head:
+// do[m][c] = [BN->ReLU: fma(y, sc, sh) > 0] dl[m] w[c] (head_bwd's expression, bit for bit;
+// out_channels = 1), so head_bwd need not store the 64-channel f32 do at full resolution.
+struct DzHead {
+    const float* dl;     // d logits [P] (NCHW with one channel = pixel order)
+    const float* w;      // head weights [C]
+    const float *sc, *sh;  // the last BN's forward affine
+    int relu;            // BN -> ReLU: mask by the activation
+};
+
+template <bool HEAD>
 __global__ __launch_bounds__(256) void bn_dz_x3_kernel(const float* __restrict__ d, const float* __restrict__ y,
                                                        int ld, int off, int64_t P, int C,
                                                        const float* __restrict__ coef, int mask,
                                                        uint16_t* __restrict__ dz3, float* __restrict__ bpart,
-                                                       int rpb) {
+                                                       int rpb, DzHead hd) {
     __shared__ float red[256 * 8];
     const int g8 = C / 8, G = min(g8, 256);  // octets per pass (bias sums: C <= 2048, one pass)
     const int r0 = threadIdx.x / G, rstep = 256 / G;
@@ -1946,26 +1957,44 @@ __global__ __launch_bounds__(256) void bn_dz_x3_kernel(const float* __restrict__
     float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     for (int oct = threadIdx.x % G; active && oct < g8; oct += G) {
         const int c = oct * 8;
-        f32x4 ka[2], kb[2], kc[2], km[2];
+        f32x4 ka[2], kb[2], kc[2], km[2], hw[2], hs[2], hh[2];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             ka[h] = *(const f32x4*)(coef + c + 4 * h);
             kb[h] = *(const f32x4*)(coef + C + c + 4 * h);
             kc[h] = *(const f32x4*)(coef + 2 * C + c + 4 * h);
             km[h] = *(const f32x4*)(coef + 3 * C + c + 4 * h);
+            if constexpr (HEAD) {
+                hw[h] = *(const f32x4*)(hd.w + c + 4 * h);
+                hs[h] = *(const f32x4*)(hd.sc + c + 4 * h);
+                hh[h] = *(const f32x4*)(hd.sh + c + 4 * h);
+            }
         }
         for (int64_t m = mb + r0; m < me; m += X3_RIF * rstep) {
             f32x4 dv[X3_RIF][2], yv[X3_RIF][2];
+            float dl[X3_RIF];
 #pragma unroll
             for (int i = 0; i < X3_RIF; ++i) {
                 const int64_t mi = m + i * rstep;
                 if (mi < me) {
+                    if constexpr (HEAD) dl[i] = hd.dl[mi];
 #pragma unroll
                     for (int h = 0; h < 2; ++h) {
-                        dv[i][h] = *(const f32x4*)(d + mi * C + c + 4 * h);
+                        if constexpr (!HEAD) dv[i][h] = *(const f32x4*)(d + mi * C + c + 4 * h);
                         yv[i][h] = *(const f32x4*)(y + mi * ld + off + c + 4 * h);
                     }
                 }
+            }
+            if constexpr (HEAD) {
+#pragma unroll
+                for (int i = 0; i < X3_RIF; ++i)
+#pragma unroll
+                    for (int h = 0; h < 2; ++h)
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            const bool on = !hd.relu || __builtin_fmaf(yv[i][h][j], hs[h][j], hh[h][j]) > 0.f;
+                            dv[i][h][j] = on ? dl[i] * hw[h][j] : 0.f;
+                        }
             }
 #pragma unroll
             for (int i = 0; i < X3_RIF; ++i) {
@@ -2150,10 +2179,18 @@ int x3_dz_blocks(int64_t P) {
 }
 
 int k_bn_dz_x3(const float* d, const float* y, int ld, int off, int64_t P, int C, const float* coef,
-               int mask, uint16_t* dz3, float* bpart, hipStream_t s) {
+               int mask, uint16_t* dz3, float* bpart, hipStream_t s, const float* hdl, const float* hw,
+               const float* hsc, const float* hsh, int hrelu) {
     if (C % 32 || (bpart && C > 2048) || ld % 4 || off % 4 || P < 1) return -1;
-    hipLaunchKernelGGL(bn_dz_x3_kernel, dim3(x3_dz_blocks(P)), dim3(256), 0, s, d, y, ld, off, P, C, coef,
-                       mask, dz3, bpart, x3_rows_per_block(P));
+    if (hdl) {
+        if (!hw || !hsc || !hsh) return -1;
+        const DzHead hd{hdl, hw, hsc, hsh, hrelu};
+        hipLaunchKernelGGL(bn_dz_x3_kernel<true>, dim3(x3_dz_blocks(P)), dim3(256), 0, s, d, y, ld, off, P, C,
+                           coef, mask, dz3, bpart, x3_rows_per_block(P), hd);
+    } else {
+        hipLaunchKernelGGL(bn_dz_x3_kernel<false>, dim3(x3_dz_blocks(P)), dim3(256), 0, s, d, y, ld, off, P, C,
+                           coef, mask, dz3, bpart, x3_rows_per_block(P), DzHead{});
+    }
     return (int)hipGetLastError();
 }
 

@@ -1103,7 +1103,9 @@ __global__ void head_fwd_kernel(const float* __restrict__ y, int C, const float*
         for (int u = 0; u < U; ++u) {
             const int pix = pb + u * stride;
             f32x4 a = v[u];
-            if (scale) a = a * sc + sh;
+            if (scale)  // explicit fma: the same activation as the backward's ReLU mask
+#pragma unroll
+                for (int j = 0; j < 4; ++j) a[j] = __builtin_fmaf(a[j], sc[j], sh[j]);
             if (relu)
 #pragma unroll
                 for (int j = 0; j < 4; ++j) a[j] = fmaxf(a[j], 0.f);
@@ -1145,7 +1147,9 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__
     // two pixels per trip, both pixels' loads issued first (P < 2^31: 32-bit pixel math);
     // each thread still accumulates its pixels in increasing m (same partials)
     auto one = [&](int m, const f32x4& yr, const float (&dl)[4]) {
-        f32x4 v = yr * sc + sh;
+        f32x4 v;  // explicit fma: bn_dz_x3's fused head source recomputes this mask (r05)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = __builtin_fmaf(yr[j], sc[j], sh[j]);
         if (relu)
 #pragma unroll
             for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
@@ -1158,7 +1162,7 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__
         if (relu)
 #pragma unroll
             for (int j = 0; j < 4; ++j) d[j] = v[j] > 0.f ? d[j] : 0.f;
-        *(f32x4*)(dout + (int64_t)m * C + 4 * q) = d;
+        if (dout) *(f32x4*)(dout + (int64_t)m * C + 4 * q) = d;  // (null: the dz pass recomputes it)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             bq[0][j] += d[j];

@@ -178,6 +178,8 @@ struct Options {
                                // profiles/r05_wwaves_ab.txt)
     int x3_wwaves1 = 3;        // the same for the one-tap x3 weight gradients (ConvT, 8x8):
                                // +0.45 % (profiles/r05_wwaves_ab.txt)
+    int head_fuse = 1;         // x3 path, one output channel: the last conv's dz pass recomputes
+                               // `do` from the head instead of head_bwd storing it (r05)
     int x3_1tap16 = 0;         // the one-tap x3 tiles (0 / 1 row GEMM, 0 / 1 weight gradient) follow
                                // the 16x16x32 schedules (x3_r3_sched / x3_wsched >= 8; r05):
                                // config 2 within noise (profiles/r05_1tap16_ab.txt), so off
@@ -247,6 +249,7 @@ const OptionDesc OPTION_TABLE[] = {
     {"x3_n64_r3", &Options::x3_n64_r3},
     {"x3_wsched", &Options::x3_wsched},
     {"x3_1tap16", &Options::x3_1tap16},
+    {"head_fuse", &Options::head_fuse},
     {"x3_wwaves", &Options::x3_wwaves},
     {"x3_wwaves1", &Options::x3_wwaves1},
 };
@@ -1602,6 +1605,8 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
     // dz = A do + B (y - mean) + C as one elementwise pass over do, or (option dz_in_wgrad)
     // inside the weight gradient's B' loader, which also stores it for the dgrad
     const int dz_mask = c->bn_relu ? 0 : 1;
+    // conv whose x3 dz pass recomputes `do` from the 1x1 head (set below when it applies)
+    int head_src_conv = -1;
     // conv i backward from do_i (dense [P][cout]).
     // dgrad -> dx (ld ldx).  bn_next: dx is the `do` of BN layer i-1 (second conv of a
     // block), so the epilogue also emits that layer's partials; *rows = their count.
@@ -1621,8 +1626,12 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
             // option x3: dz as an x3 image (and the conv bias's column partials), the weight
             // gradient from the forward's kept input image and dz, the input gradient from dz
             float* bp = C.b >= 0 ? p.part : nullptr;
+            // (r05) the last conv's `do` straight from the 1x1 head (head_bwd stored none)
+            const bool hsrc = i == head_src_conv;
             RUN("bn_dz", 0, k_bn_dz_x3(dout, p.y[i], p.ldy[i], p.offy[i], P, C.cout, p.coef, dz_mask,
-                                      p.s3, bp, s));
+                                      p.s3, bp, s, hsrc ? dlogits : nullptr, hsrc ? prm + c->head_w : nullptr,
+                                      hsrc ? p.scale[i] : nullptr, hsrc ? p.shift[i] : nullptr,
+                                      c->bn_relu ? 1 : 0));
             if (bp) {  // many 256-row partials: one two-level reduction (as the BN statistics)
                 const int G = x3_dz_blocks(P);
                 if (G > STAT_G) {
@@ -2106,10 +2115,15 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
     }
     // ---- head + last decoder block (stage 0) ----
     const int last = NC - 1;
+    // (r05) one output channel on the x3 path: the last conv's dz pass recomputes `do` =
+    // mask * dl * w from the logit gradient, so head_bwd stores no full-resolution f32 `do`
+    const bool head_fuse = c->out_ch == 1 && c->conv[last].cout == c->base && p.pack3 &&
+                           x3_conv_on(c, c->conv[last].cin, c->conv[last].cout) && c->opt.head_fuse;
+    head_src_conv = head_fuse ? last : -1;
     RUN("head_bwd", 2.0 * p.P[0] * c->base * c->out_ch * 2,
         k_head_bwd(p.y[last], c->base, p.scale[last], p.shift[last], c->bn_relu ? 1 : 0,
-                   prm + c->head_w, c->out_ch, (int)p.P[0], H * W, dlogits, G0, p.hpart, p.part,
-                   wide_g(p.P[0]), s));
+                   prm + c->head_w, c->out_ch, (int)p.P[0], H * W, dlogits, head_fuse ? nullptr : G0,
+                   p.hpart, p.part, wide_g(p.P[0]), s));
     RUN("head_grad", 0, k_sum_partials(p.hpart, wide_g(p.P[0]), c->out_ch * c->base + c->out_ch,
                                        grads + c->head_w, s));
     if ((rc = bn_finalize(last, wide_g(p.P[0])))) return rc;
