@@ -765,7 +765,7 @@ __global__ __launch_bounds__(BM / 64 * 2 * 64, BM == 256 ? 1 : 2) void rowgemm_x
     constexpr int RB = 192, AR = BM / 16 * 18, WB = 1024 * WAVES;
     constexpr int SMEM = 2 * ((AR * RB + WB - 1) / WB) * WB + 2 * ((BN * RB + WB - 1) / WB) * WB;  // 160 / 80 KB
     static_assert(SMEM >= 2 * (BM / 64) * BN * 8, "epilogue scratch");
-    static_assert(BM == 256 || SCHED == 0, "the staggered schedules pair waves w and w + 4");
+    static_assert(BM == 256 || SCHED == 0 || SCHED == 9, "the staggered schedules pair waves w and w + 4");
     __shared__ __attribute__((aligned(1024))) char smem[SMEM];
     using SC = X3R3Sched<SCHED & 7>;
     const int tid = threadIdx.x, lane = tid & 63;
@@ -790,8 +790,9 @@ __global__ __launch_bounds__(BM / 64 * 2 * 64, BM == 256 ? 1 : 2) void rowgemm_x
         // stagger + late DMA.  (Measured and dropped: late DMA alone; waves 0..3 issuing every
         // DMA with waves 4..7 staggered -- 17..55 spilled VGPRs.)
         constexpr int SUB = SCHED - 8;
-        constexpr bool LATE16 = SUB >= 1, LAG16 = SUB >= 1, QL16 = SUB == 2;
-        constexpr int LW16 = 8;
+        // (BM = 128, tile 6: four waves, two blocks per CU -- the other block is the stagger)
+        constexpr bool LATE16 = SUB >= 1, LAG16 = SUB >= 1 && BM == 256, QL16 = SUB == 2;
+        constexpr int LW16 = BM / 64 * 2;
         if (wave >= 4)
             x3r3_body16<BM, BN, LW16, LW16 == 8, LAG16, LATE16, QL16>(p, smem, wave, lane, h16, l16, m0, n0);
         else
@@ -1022,7 +1023,10 @@ static int x3r3_go(const RowGemmArgs& a, int sched, hipStream_t s) {
     if (a.W < 16 || (BM % a.W && a.W % BM)) return -1;
     const dim3 grid(((a.M + BM - 1) / BM) * (a.N / BN));
     if constexpr (BM == 128) {
-        hipLaunchKernelGGL((rowgemm_x3_row3_kernel<EMODE, BN, 0, 128>), grid, dim3(256), 0, s, a);
+        if (sched >= 8)  // 16x16x32, DMA after the first reads
+            hipLaunchKernelGGL((rowgemm_x3_row3_kernel<EMODE, BN, 9, 128>), grid, dim3(256), 0, s, a);
+        else
+            hipLaunchKernelGGL((rowgemm_x3_row3_kernel<EMODE, BN, 0, 128>), grid, dim3(256), 0, s, a);
         return (int)hipGetLastError();
     }
 #define X3R3_SCHED(v)                                                                          \

@@ -184,8 +184,9 @@ struct Options {
                                // the 16x16x32 schedules (x3_r3_sched / x3_wsched >= 8; r05):
                                // config 2 within noise (profiles/r05_1tap16_ab.txt), so off
     int x3_n32 = 0;            // x3 also for 32-multiple channel counts (r05; narrow widths)
-    int x3_n64_r3 = 5;         // halo tile of the 64-output 3x3 GEMMs: 5 = 256x64 (8 waves, one
-                               // block per CU), 6 = 128x64 (4 waves, two blocks per CU), 8 =
+    int x3_n64_r3 = 6;         // halo tile of the 64-output 3x3 GEMMs: 5 = 256x64 (8 waves, one
+                               // block per CU), 6 = 128x64 (4 waves, two blocks per CU; on the
+                               // 16x16x32 schedules +0.2 % over 5, profiles/r05_halo_k16.txt), 8 =
                                // 512x64 over 16-channel groups (r05: 1.103 vs 1.032 ms at level 0,
                                // profiles/r05_halo_k16.txt -- not faster, kept as an option)
     int x3_wsched = 9;         // the tap-row weight gradient's schedule (0 = r04, 1 = four stages
