@@ -202,7 +202,7 @@ def test_x3_halo_schedules_bit_identical(B, H, W):
     from _helpers import options
     x, t = inputs(31, B, H, W)
     outs = []
-    runs = ((0, 5), (1, 5), (2, 5), (3, 5), (4, 5), (0, 6), (8, 5), (9, 5), (10, 5), (9, 6), (0, 8), (1, 8))
+    runs = ((0, 5), (1, 5), (2, 5), (3, 5), (4, 5), (0, 6), (8, 5), (9, 5), (10, 5), (12, 5), (9, 6), (0, 8), (1, 8))
     for sched, n64 in runs:
         m = hip_model(O.make_params(42), DEV)
         with options(m.flatten_().rt, x3_r3_sched=sched, x3_n64_r3=n64):

@@ -563,7 +563,13 @@ __device__ __forceinline__ void x3r3_body(const RowGemmArgs& p, char* smem, int 
 //   and this XOR puts them on 16 distinct bank quads for any r0.
 //   Stagger (LAG): waves 4..7 run the second 32-row half's MFMAs after the next barrier.
 // ------------------------------------------------------------------------------------
-template <int BM, int BN, int LW, bool ISSUER, bool LAG, bool LATE, bool QL = false>
+// RA (schedule 11, not built: 52-53 spilled VGPRs): the staggered waves hold only the B
+// fragments and re-read the deferred A half from the halo after the barrier (intact while the
+// next sub-step is in the same halo group: only dx = 0, 1 defer)
+// RC (schedule 12): the loader state is recomputed per DMA piece (f32-reciprocal decode) instead
+// of being held in 17 registers per wave -- for the staggered waves, which hold fragments
+template <int BM, int BN, int LW, bool ISSUER, bool LAG, bool LATE, bool QL = false, bool RA = false,
+          bool RC = false>
 __device__ __forceinline__ void x3r3_body16(const RowGemmArgs& p, char* smem, int wave, int lane,
                                             f32x4 (&hi)[2][BN / 64][2][2], f32x4 (&lo)[2][BN / 64][2][2],
                                             int m0, int n0) {
@@ -582,26 +588,31 @@ __device__ __forceinline__ void x3r3_body16(const RowGemmArgs& p, char* smem, in
     const size_t rowa = 3 * (size_t)p.lda, rowb = 3 * (size_t)K;
     // loader state packed to 3 registers per piece pair (the staggered waves hold a second
     // fragment set): pixel index, y * 128 + element offset in the 192-B row, B element offset
-    int acen[ISSUER ? AI : 1], apk[ISSUER ? AI : 1], boff[ISSUER ? BI : 1];
-    if constexpr (ISSUER) {
+    constexpr bool KEEP = ISSUER && !RC;
+    int acen[KEEP ? AI : 1], apk[KEEP ? AI : 1], boff[KEEP ? BI : 1];
+    const float rHW = 1.f / (float)HW, rW = 1.f / (float)W, rH = 1.f / (float)H;
+    // piece j's A state: pixel at dy = 1 (-1: padding / past the halo), y * 128 + element offset
+    auto apiece = [&](int j, int& cen, int& pk) {
+        const int o = ((j * LW + wave) * 64 + lane) * 16;
+        const int h = o / RB, w = o - h * RB;
+        const int r = RC ? (int)(((float)h + 0.5f) * rHW) : h / HW, xl = h - r * HW - 1;
+        const int mrow = m0 + r * SEG;
+        bool ok = h < AROWS && mrow < p.M;
+        const Pix q = RC ? decode_fast(ok ? mrow : 0, H, W, rH, rW) : decode(ok ? mrow : 0, H, W);
+        ok = ok && q.x + xl >= 0 && q.x + xl < W;
+        cen = ok ? mrow + xl : -1;
+        pk = q.y * 128 + (w >> 6) * 32 + ((((w >> 4) & 3) ^ swz(h)) << 3);
+    };
+    auto bpiece = [&](int j) {
+        const int o = ((j * LW + wave) * 64 + lane) * 16;
+        const int r = o / RB, w = o - r * RB;
+        return r < BN ? (int)((n0 + r) * rowb) + (w >> 6) * 32 + ((((w >> 4) & 3) ^ swz(r)) << 3) : -1;
+    };
+    if constexpr (KEEP) {
 #pragma unroll
-        for (int j = 0; j < AI; ++j) {
-            const int o = ((j * LW + wave) * 64 + lane) * 16;
-            const int h = o / RB, w = o - h * RB;
-            const int r = h / HW, xl = h - r * HW - 1;
-            const int mrow = m0 + r * SEG;
-            bool ok = h < AROWS && mrow < p.M;
-            const Pix q = decode(ok ? mrow : 0, H, W);
-            ok = ok && q.x + xl >= 0 && q.x + xl < W;
-            acen[j] = ok ? mrow + xl : -1;
-            apk[j] = q.y * 128 + (w >> 6) * 32 + ((((w >> 4) & 3) ^ swz(h)) << 3);
-        }
+        for (int j = 0; j < AI; ++j) apiece(j, acen[j], apk[j]);
 #pragma unroll
-        for (int j = 0; j < BI; ++j) {
-            const int o = ((j * LW + wave) * 64 + lane) * 16;
-            const int r = o / RB, w = o - r * RB;
-            boff[j] = r < BN ? (int)((n0 + r) * rowb) + (w >> 6) * 32 + ((((w >> 4) & 3) ^ swz(r)) << 3) : -1;
-        }
+        for (int j = 0; j < BI; ++j) boff[j] = bpiece(j);
     }
     const uint16_t* zero = (const uint16_t*)p.zero16;
     const uint16_t* a16 = p.a16 + (size_t)p.aoff * 3;
@@ -614,10 +625,13 @@ __device__ __forceinline__ void x3r3_body16(const RowGemmArgs& p, char* smem, in
 #pragma unroll
         for (int j = 0; j < AI; ++j) {
             if (j < j0 || j >= j1) continue;
-            const int yy = (apk[j] >> 7) + dy - 1;
-            const bool valid = acen[j] >= 0 && yy >= 0 && yy < H;
+            int cen, pk;
+            if constexpr (KEEP) cen = acen[j], pk = apk[j];
+            else apiece(j, cen, pk);
+            const int yy = (pk >> 7) + dy - 1;
+            const bool valid = cen >= 0 && yy >= 0 && yy < H;
             const uint16_t* src =
-                valid ? a16 + (size_t)(acen[j] + (dy - 1) * W) * rowa + c0 * 3 + (apk[j] & 127) : zero;
+                valid ? a16 + (size_t)(cen + (dy - 1) * W) * rowa + c0 * 3 + (pk & 127) : zero;
             x3_dma16(src, base + (j * LW + wave) * 1024);
         }
     };
@@ -627,8 +641,10 @@ __device__ __forceinline__ void x3r3_body16(const RowGemmArgs& p, char* smem, in
         const int k0 = (dy * 3 + dx) * C + c0;
         char* base = smem + 2 * AREG + (s & 1) * BREG;
 #pragma unroll
-        for (int j = 0; j < BI; ++j)
-            x3_dma16(boff[j] >= 0 ? p.bt16 + boff[j] + k0 * 3 : zero, base + (j * LW + wave) * 1024);
+        for (int j = 0; j < BI; ++j) {
+            const int bo = KEEP ? boff[j] : bpiece(j);
+            x3_dma16(bo >= 0 ? p.bt16 + bo + k0 * 3 : zero, base + (j * LW + wave) * 1024);
+        }
     };
     auto issue = [&](int s) {
         const int g = s / 3, dx = s - g * 3;
@@ -680,12 +696,24 @@ __device__ __forceinline__ void x3r3_body16(const RowGemmArgs& p, char* smem, in
         }
         x3_barrier();
         if constexpr (ISSUER && !LATE) issue(s);
-        if constexpr (LAG) {
+        const char* abase = smem + (g & 1) * AREG;
+        if constexpr (LAG && RA) {
+            if (dx > 0) {  // the previous sub-step (same group, tap dx - 1): its second A half
+                bf16x8 ap[2][3];
+#pragma unroll
+                for (int bm = 0; bm < 2; ++bm) {
+                    const int h = ahb[1][bm] + dx - 1;
+#pragma unroll
+                    for (int q = 0; q < 3; ++q) ap[bm][q] = *(const bf16x8*)(abase + h * RB + q * 64 + ((ks ^ swz(h)) << 4));
+                }
+                mma(ap, &hb[0][0][0], 1, N0, NT);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        } else if constexpr (LAG) {
             if (s > 0) mma(ha, &hb[0][0][0], 1, N0, NT);
             // the held registers free before this sub-step's reads (256 VGPRs at two waves / SIMD)
             __builtin_amdgcn_sched_barrier(0);
         }
-        const char* abase = smem + (g & 1) * AREG;
         const char* bbase = smem + 2 * AREG + (s & 1) * BREG;
         bf16x8 af[2][3], bfr[NT][2][3];
 #pragma unroll
@@ -704,19 +732,7 @@ __device__ __forceinline__ void x3r3_body16(const RowGemmArgs& p, char* smem, in
         if constexpr (ISSUER && LATE) issue(s);
         mma(af, &bfr[0][0][0], 0, 0, NT);
         if constexpr (LAG) __builtin_amdgcn_sched_barrier(0);  // A of the held half after A0 died
-        bf16x8 af1[2][3];
-#pragma unroll
-        for (int bm = 0; bm < 2; ++bm) {
-            const int h = ahb[1][bm] + dx;
-#pragma unroll
-            for (int q = 0; q < 3; ++q) af1[bm][q] = *(const bf16x8*)(abase + h * RB + q * 64 + ((ks ^ swz(h)) << 4));
-        }
-        if constexpr (LAG) {
-            if constexpr (N0 > 0) mma(af1, &bfr[0][0][0], 1, 0, N0);
-#pragma unroll
-            for (int bm = 0; bm < 2; ++bm)
-#pragma unroll
-                for (int q = 0; q < 3; ++q) ha[bm][q] = af1[bm][q];
+        if (LAG && RA && dx < 2) {  // defer the second half: hold B, re-read A after the barrier
 #pragma unroll
             for (int nt = 0; nt < HN; ++nt)
 #pragma unroll
@@ -724,11 +740,32 @@ __device__ __forceinline__ void x3r3_body16(const RowGemmArgs& p, char* smem, in
 #pragma unroll
                     for (int q = 0; q < 3; ++q) hb[nt][bn][q] = bfr[N0 + nt][bn][q];
         } else {
-            mma(af1, &bfr[0][0][0], 1, 0, NT);
+            bf16x8 af1[2][3];
+#pragma unroll
+            for (int bm = 0; bm < 2; ++bm) {
+                const int h = ahb[1][bm] + dx;
+#pragma unroll
+                for (int q = 0; q < 3; ++q) af1[bm][q] = *(const bf16x8*)(abase + h * RB + q * 64 + ((ks ^ swz(h)) << 4));
+            }
+            if constexpr (LAG && !RA) {
+                if constexpr (N0 > 0) mma(af1, &bfr[0][0][0], 1, 0, N0);
+#pragma unroll
+                for (int bm = 0; bm < 2; ++bm)
+#pragma unroll
+                    for (int q = 0; q < 3; ++q) ha[bm][q] = af1[bm][q];
+#pragma unroll
+                for (int nt = 0; nt < HN; ++nt)
+#pragma unroll
+                    for (int bn = 0; bn < 2; ++bn)
+#pragma unroll
+                        for (int q = 0; q < 3; ++q) hb[nt][bn][q] = bfr[N0 + nt][bn][q];
+            } else {
+                mma(af1, &bfr[0][0][0], 1, 0, NT);
+            }
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
-    if constexpr (LAG) mma(ha, &hb[0][0][0], 1, N0, NT);
+    if constexpr (LAG && !RA) mma(ha, &hb[0][0][0], 1, N0, NT);
 }
 
 // the 16x16x32 accumulators (hi + lo) in the 32x32x16 register layout: lanes l and l ^ 16 swap
@@ -791,10 +828,11 @@ __global__ __launch_bounds__(BM / 64 * 2 * 64, BM == 256 ? 1 : 2) void rowgemm_x
         // DMA with waves 4..7 staggered -- 17..55 spilled VGPRs.)
         constexpr int SUB = SCHED - 8;
         // (BM = 128, tile 6: four waves, two blocks per CU -- the other block is the stagger)
-        constexpr bool LATE16 = SUB >= 1, LAG16 = SUB >= 1 && BM == 256, QL16 = SUB == 2;
+        constexpr bool LATE16 = SUB >= 1, LAG16 = SUB >= 1 && BM == 256, QL16 = SUB == 2, RA16 = SUB == 3;
+        constexpr bool RC16 = SUB == 4;
         constexpr int LW16 = BM / 64 * 2;
         if (wave >= 4)
-            x3r3_body16<BM, BN, LW16, LW16 == 8, LAG16, LATE16, QL16>(p, smem, wave, lane, h16, l16, m0, n0);
+            x3r3_body16<BM, BN, LW16, LW16 == 8, LAG16, LATE16, QL16, RA16, RC16>(p, smem, wave, lane, h16, l16, m0, n0);
         else
             x3r3_body16<BM, BN, LW16, true, false, LATE16>(p, smem, wave, lane, h16, l16, m0, n0);
         x3_acc16_to32(h16, l16, acc, lane);
@@ -1034,7 +1072,7 @@ static int x3r3_go(const RowGemmArgs& a, int sched, hipStream_t s) {
         hipLaunchKernelGGL((rowgemm_x3_row3_kernel<EMODE, BN, v>), grid, dim3(512), 0, s, a); \
         return (int)hipGetLastError();                                                        \
     }
-    X3R3_SCHED(0) X3R3_SCHED(1) X3R3_SCHED(2) X3R3_SCHED(3) X3R3_SCHED(4) X3R3_SCHED(8) X3R3_SCHED(9) X3R3_SCHED(10)
+    X3R3_SCHED(0) X3R3_SCHED(1) X3R3_SCHED(2) X3R3_SCHED(3) X3R3_SCHED(4) X3R3_SCHED(8) X3R3_SCHED(9) X3R3_SCHED(10) X3R3_SCHED(12)
 #undef X3R3_SCHED
     return -1;
 }

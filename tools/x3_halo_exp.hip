@@ -606,7 +606,7 @@ int main(int argc, char** argv) {
             printf("    library tile 6 (128x64, 2/CU): %.3f ms %.1f TF/s  %s\n", t, fl / t / 1e9,
                    same ? "bit-identical" : "DIFFERS");
         }
-        const int scheds[] = {1, 9};  // the library's schedules (8.. = 16x16x32)
+        const int scheds[] = {1, 9, 12};  // the library's schedules (8.. = 16x16x32)
         double rmax = 0;
         for (float v : r) rmax = std::max(rmax, (double)fabsf(v));
         for (int sc : scheds) {
