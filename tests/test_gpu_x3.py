@@ -253,17 +253,18 @@ def test_x3_one_tap_m16_close():
 
 
 def test_x3_head_fuse_bit_identical():
-    """Option head_fuse (r05, default on): with one output channel the last conv's x3 dz pass
-    recomputes its `do` = [activation > 0] dl w from the logit gradient (head_bwd's own fma
-    mask and product) instead of reading a full-resolution f32 `do` that head_bwd stored: one
-    training step is bit-identical either way."""
+    """Options head_fuse / pool_fuse (r05, default on): the x3 dz pass of the last conv
+    recomputes its `do` = [activation > 0] dl w from the logit gradient, and that of each
+    encoder block's second conv its `do` = mask (dskip + routed dpool) from the max-pool
+    backward's inputs (the producers' own fma masks and sums), instead of reading a
+    full-resolution f32 `do` the producer stored: one training step is bit-identical."""
     import unet_hip
     from _helpers import options
     x, t = inputs(47, 2, 128, 128)
     outs = []
     for flag in (0, 1):
         m = hip_model(O.make_params(53), DEV)
-        with options(m.flatten_().rt, head_fuse=flag):
+        with options(m.flatten_().rt, head_fuse=flag, pool_fuse=flag):
             logits = m(x.to(DEV))
             l = unet_hip.seg_losses(logits, t.to(DEV))
             (l[0] + l[1]).backward()

@@ -175,6 +175,12 @@ int k_bn_dz_x3(const float* d, const float* y, int ld, int off, int64_t P, int C
                int mask, uint16_t* dz3, float* bpart, hipStream_t s, const float* hdl = nullptr,
                const float* hw = nullptr, const float* hsc = nullptr, const float* hsh = nullptr,
                int hrelu = 0);
+// the same with do = [msc: fma(msc, y, msh) > 0] (dskip + [idx == window position] dp): the
+// encoder block's second conv, maxpool_bwd's expression (r05; dskip offset applied, N H W the
+// full-resolution grid, P = N H W < 2^24 for the f32-reciprocal pixel decode)
+int k_bn_dz_x3_pool(const float* y, int ld, int off, int64_t P, int C, const float* coef, int mask,
+                    uint16_t* dz3, float* bpart, const float* dp, const uint8_t* idx, const float* dskip,
+                    int ldskip, const float* msc, const float* msh, int N, int H, int W, hipStream_t s);
 int x3_dz_blocks(int64_t P);
 // register-staged bf16 wgrad tile ids (a.bf16): 0 = 128x128/32 px, 2 = 64x64/64,
 // 3 = 128x64/64, 4 = 64x128/64

@@ -1983,13 +1983,25 @@ struct DzHead {
     const float *sc, *sh;  // the last BN's forward affine
     int relu;            // BN -> ReLU: mask by the activation
 };
+// POOL (r05): the encoder block's second conv: do = [BN->ReLU: fma(msc, y, msh) > 0] (dskip +
+// [winner == window position] dp) -- maxpool_bwd's expression, so it need not store do
+struct DzPool {
+    const float* dp;       // d pooled [N][H/2][W/2][C]
+    const uint8_t* idx;    // winner index per pooled element
+    const float* dskip;    // the concat gradient's skip half (offset applied), row stride ldskip
+    int ldskip;
+    const float *msc, *msh;  // BN -> ReLU mask affine, or null
+    int H, W;              // full-resolution grid
+    float rH, rW;
+};
 
-template <bool HEAD>
+template <int SRC>  // 0: do from memory, 1: DzHead, 2: DzPool
 __global__ __launch_bounds__(256) void bn_dz_x3_kernel(const float* __restrict__ d, const float* __restrict__ y,
                                                        int ld, int off, int64_t P, int C,
                                                        const float* __restrict__ coef, int mask,
                                                        uint16_t* __restrict__ dz3, float* __restrict__ bpart,
-                                                       int rpb, DzHead hd) {
+                                                       int rpb, DzHead hd, DzPool pl) {
+    constexpr bool HEAD = SRC == 1, POOL = SRC == 2;
     __shared__ float red[256 * 8];
     const int g8 = C / 8, G = min(g8, 256);  // octets per pass (bias sums: C <= 2048, one pass)
     const int r0 = threadIdx.x / G, rstep = 256 / G;
@@ -2015,17 +2027,46 @@ __global__ __launch_bounds__(256) void bn_dz_x3_kernel(const float* __restrict__
         for (int64_t m = mb + r0; m < me; m += X3_RIF * rstep) {
             f32x4 dv[X3_RIF][2], yv[X3_RIF][2];
             float dl[X3_RIF];
+            f32x4 gp[X3_RIF][2];
+            uint32_t wi[X3_RIF][2];
+            int kk[X3_RIF];
 #pragma unroll
             for (int i = 0; i < X3_RIF; ++i) {
                 const int64_t mi = m + i * rstep;
                 if (mi < me) {
                     if constexpr (HEAD) dl[i] = hd.dl[mi];
+                    int64_t po = 0;
+                    if constexpr (POOL) {
+                        const Pix q = decode_fast((int)mi, pl.H, pl.W, pl.rH, pl.rW);
+                        po = ((int64_t)q.img * (pl.H >> 1) + (q.y >> 1)) * (pl.W >> 1) + (q.x >> 1);
+                        kk[i] = (q.y & 1) * 2 + (q.x & 1);
+                        const uint2 w2 = *(const uint2*)(pl.idx + po * C + c);
+                        wi[i][0] = w2.x;
+                        wi[i][1] = w2.y;
+                    }
 #pragma unroll
                     for (int h = 0; h < 2; ++h) {
-                        if constexpr (!HEAD) dv[i][h] = *(const f32x4*)(d + mi * C + c + 4 * h);
+                        if constexpr (POOL) {
+                            dv[i][h] = *(const f32x4*)(pl.dskip + mi * pl.ldskip + c + 4 * h);
+                            gp[i][h] = *(const f32x4*)(pl.dp + po * C + c + 4 * h);
+                        } else if constexpr (!HEAD) {
+                            dv[i][h] = *(const f32x4*)(d + mi * C + c + 4 * h);
+                        }
                         yv[i][h] = *(const f32x4*)(y + mi * ld + off + c + 4 * h);
                     }
                 }
+            }
+            if constexpr (POOL) {
+#pragma unroll
+                for (int i = 0; i < X3_RIF; ++i)
+#pragma unroll
+                    for (int h = 0; h < 2; ++h)
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            if (((wi[i][h] >> (8 * j)) & 0xFF) == (uint32_t)kk[i]) dv[i][h][j] += gp[i][h][j];
+                            if (pl.msc && !(__builtin_fmaf(pl.msc[c + 4 * h + j], yv[i][h][j], pl.msh[c + 4 * h + j]) > 0.f))
+                                dv[i][h][j] = 0.f;
+                        }
             }
             if constexpr (HEAD) {
 #pragma unroll
@@ -2227,12 +2268,23 @@ int k_bn_dz_x3(const float* d, const float* y, int ld, int off, int64_t P, int C
     if (hdl) {
         if (!hw || !hsc || !hsh) return -1;
         const DzHead hd{hdl, hw, hsc, hsh, hrelu};
-        hipLaunchKernelGGL(bn_dz_x3_kernel<true>, dim3(x3_dz_blocks(P)), dim3(256), 0, s, d, y, ld, off, P, C,
-                           coef, mask, dz3, bpart, x3_rows_per_block(P), hd);
+        hipLaunchKernelGGL(bn_dz_x3_kernel<1>, dim3(x3_dz_blocks(P)), dim3(256), 0, s, d, y, ld, off, P, C,
+                           coef, mask, dz3, bpart, x3_rows_per_block(P), hd, DzPool{});
     } else {
-        hipLaunchKernelGGL(bn_dz_x3_kernel<false>, dim3(x3_dz_blocks(P)), dim3(256), 0, s, d, y, ld, off, P, C,
-                           coef, mask, dz3, bpart, x3_rows_per_block(P), DzHead{});
+        hipLaunchKernelGGL(bn_dz_x3_kernel<0>, dim3(x3_dz_blocks(P)), dim3(256), 0, s, d, y, ld, off, P, C,
+                           coef, mask, dz3, bpart, x3_rows_per_block(P), DzHead{}, DzPool{});
     }
+    return (int)hipGetLastError();
+}
+
+int k_bn_dz_x3_pool(const float* y, int ld, int off, int64_t P, int C, const float* coef, int mask,
+                    uint16_t* dz3, float* bpart, const float* dp, const uint8_t* idx, const float* dskip,
+                    int ldskip, const float* msc, const float* msh, int N, int H, int W, hipStream_t s) {
+    if (C % 32 || (bpart && C > 2048) || ld % 4 || off % 4 || ldskip % 4 || P < 1) return -1;
+    if (!dp || !idx || !dskip || H % 2 || W % 2 || (int64_t)N * H * W != P || P >= (1LL << 24)) return -1;
+    const DzPool pl{dp, idx, dskip, ldskip, msc, msh, H, W, 1.f / (float)H, 1.f / (float)W};
+    hipLaunchKernelGGL(bn_dz_x3_kernel<2>, dim3(x3_dz_blocks(P)), dim3(256), 0, s, nullptr, y, ld, off, P, C,
+                       coef, mask, dz3, bpart, x3_rows_per_block(P), DzHead{}, pl);
     return (int)hipGetLastError();
 }
 

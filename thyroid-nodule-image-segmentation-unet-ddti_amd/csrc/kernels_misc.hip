@@ -598,9 +598,10 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const float* __restric
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     if (((bi >> (8 * j)) & 0xFF) == (uint32_t)k) v[j] += gp[j];
-                    if (mscale && !(ms[j] * yv[j] + mb[j] > 0.f)) v[j] = 0.f;
+                    // (explicit fma: bn_dz_x3's fused pool source recomputes this mask, r05)
+                    if (mscale && !(__builtin_fmaf(ms[j], yv[j], mb[j]) > 0.f)) v[j] = 0.f;
                 }
-                *(f32x4*)(dout + pin * C + c) = v;
+                if (dout) *(f32x4*)(dout + pin * C + c) = v;  // (null: the dz pass recomputes it)
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     acc[0][j] += v[j];

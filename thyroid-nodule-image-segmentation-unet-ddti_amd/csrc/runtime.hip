@@ -178,6 +178,9 @@ struct Options {
                                // profiles/r05_wwaves_ab.txt)
     int x3_wwaves1 = 3;        // the same for the one-tap x3 weight gradients (ConvT, 8x8):
                                // +0.45 % (profiles/r05_wwaves_ab.txt)
+    int x3_convt_tile = -1;    // x3 ConvT forward / dgrad tile override (0..3; -1 = x3_tile)
+    int pool_fuse = 1;         // x3 path: the encoder block's second conv recomputes its `do` from
+                               // the max-pool backward's inputs instead of maxpool_bwd storing it
     int head_fuse = 1;         // x3 path, one output channel: the last conv's dz pass recomputes
                                // `do` from the head instead of head_bwd storing it (r05)
     int x3_1tap16 = 0;         // the one-tap x3 tiles (0 / 1 row GEMM, 0 / 1 weight gradient) follow
@@ -251,6 +254,8 @@ const OptionDesc OPTION_TABLE[] = {
     {"x3_wsched", &Options::x3_wsched},
     {"x3_1tap16", &Options::x3_1tap16},
     {"head_fuse", &Options::head_fuse},
+    {"x3_convt_tile", &Options::x3_convt_tile},
+    {"pool_fuse", &Options::pool_fuse},
     {"x3_wwaves", &Options::x3_wwaves},
     {"x3_wwaves1", &Options::x3_wwaves1},
 };
@@ -813,6 +818,18 @@ int x3_rsched(const unet_ctx* c, int tile) {
 int x3_wsched(const unet_ctx* c, int tile) {
     const int sc = c->opt.x3_wsched;
     return (tile >= 2 && tile <= 7) || c->opt.x3_1tap16 ? sc : 0;
+}
+
+int x3_tile(const unet_ctx* c, const RowGemmArgs& g);
+// ConvT forward / dgrad (short K = Cin or 4 Cout): option x3_convt_tile overrides the tile
+// (r05 A/B: the epilogue-heavy ConvT GEMMs on a two-blocks-per-CU tile)
+int x3_convt_tile(const unet_ctx* c, const RowGemmArgs& g) {
+    const int t = c->opt.x3_convt_tile;
+    int bm = 0, bn = 0;
+    if (t >= 0 && t <= 3 && rowgemm_x3_tile_dims(t, &bm, &bn) == 0 && g.N % bn == 0 &&
+        (g.emode != E_CONVT || g.cout % bn == 0 || bn % g.cout == 0))
+        return t;
+    return x3_tile(c, g);
 }
 
 int x3_tile(const unet_ctx* c, const RowGemmArgs& g) {
@@ -1463,7 +1480,7 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
                 g.out3 = p.x3[idec];
                 up16[idec] = true;
             }
-            const int tile = x3_tile(c, g);
+            const int tile = x3_convt_tile(c, g);
             RUN(xlabel("convT_fwd", tile, 100 + k), 2.0 * g.M * g.N * g.K, launch_rowgemm_x3(g, tile, s, x3_rsched(c, tile)));
             return 0;
         }
@@ -1608,6 +1625,16 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
     const int dz_mask = c->bn_relu ? 0 : 1;
     // conv whose x3 dz pass recomputes `do` from the 1x1 head (set below when it applies)
     int head_src_conv = -1;
+    // conv whose x3 dz pass recomputes `do` from the max-pool backward's inputs (option
+    // pool_fuse, r05): the encoder block's second conv
+    struct PoolSrc {
+        int conv = -1;
+        const float* dp = nullptr;
+        const uint8_t* idx = nullptr;
+        const float* dskip = nullptr;
+        int ldskip = 0;
+        const float *msc = nullptr, *msh = nullptr;
+    } pool_src;
     // conv i backward from do_i (dense [P][cout]).
     // dgrad -> dx (ld ldx).  bn_next: dx is the `do` of BN layer i-1 (second conv of a
     // block), so the epilogue also emits that layer's partials; *rows = their count.
@@ -1629,10 +1656,17 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
             float* bp = C.b >= 0 ? p.part : nullptr;
             // (r05) the last conv's `do` straight from the 1x1 head (head_bwd stored none)
             const bool hsrc = i == head_src_conv;
-            RUN("bn_dz", 0, k_bn_dz_x3(dout, p.y[i], p.ldy[i], p.offy[i], P, C.cout, p.coef, dz_mask,
-                                      p.s3, bp, s, hsrc ? dlogits : nullptr, hsrc ? prm + c->head_w : nullptr,
-                                      hsrc ? p.scale[i] : nullptr, hsrc ? p.shift[i] : nullptr,
-                                      c->bn_relu ? 1 : 0));
+            if (i == pool_src.conv) {  // (r05) do straight from the max-pool backward's inputs
+                const PoolSrc& q = pool_src;
+                RUN("bn_dz", 0, k_bn_dz_x3_pool(p.y[i], p.ldy[i], p.offy[i], P, C.cout, p.coef, dz_mask, p.s3,
+                                                bp, q.dp, q.idx, q.dskip, q.ldskip, q.msc, q.msh, p.N, Hl,
+                                                Wl, s));
+            } else {
+                RUN("bn_dz", 0, k_bn_dz_x3(dout, p.y[i], p.ldy[i], p.offy[i], P, C.cout, p.coef, dz_mask,
+                                          p.s3, bp, s, hsrc ? dlogits : nullptr,
+                                          hsrc ? prm + c->head_w : nullptr, hsrc ? p.scale[i] : nullptr,
+                                          hsrc ? p.shift[i] : nullptr, c->bn_relu ? 1 : 0));
+            }
             if (bp) {  // many 256-row partials: one two-level reduction (as the BN statistics)
                 const int G = x3_dz_blocks(P);
                 if (G > STAT_G) {
@@ -1889,7 +1923,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
                 }
                 g.stats = p.part;
             }
-            const int tile = x3_tile(c, g);
+            const int tile = x3_convt_tile(c, g);
             *rows = bn_groups(Pin);
             RUN(xlabel("convT_dgrad", tile, 100 + k), 2.0 * Pin * T.cin * 4 * T.cout,
                 launch_rowgemm_x3(g, tile, s, x3_rsched(c, tile)));
@@ -2158,11 +2192,23 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         // up to 2048 blocks on the large levels (512 left the pass at ~4.7 TB/s); the partial
         // rows fit: p.part holds P/64 + 1 rows of 2C for every conv of the level
         const int Gmp = wide_g(p.P[b]);
+        const bool pool_fuse = c->opt.pool_fuse && p.pack3 && c->conv[i1].cout == C &&
+                               x3_conv_on(c, c->conv[i1].cin, c->conv[i1].cout) && p.P[b] < (1 << 24);
+        pool_src = PoolSrc{};
+        if (pool_fuse) {
+            pool_src.conv = i1;
+            pool_src.dp = cur;
+            pool_src.idx = p.idx[b];
+            pool_src.dskip = p.dcat[b] + c->skip_off(b);
+            pool_src.ldskip = 2 * C;
+            pool_src.msc = c->bn_relu ? p.scale[i1] : nullptr;
+            pool_src.msh = c->bn_relu ? p.shift[i1] : nullptr;
+        }
         RUN("maxpool_bwd", 0,
             k_maxpool_bwd(cur, p.idx[b], p.dcat[b], 2 * C, c->skip_off(b), p.y[i1], p.ldy[i1],
                           p.offy[i1], c->bn_relu ? p.scale[i1] : nullptr,
-                          c->bn_relu ? p.shift[i1] : nullptr, p.N, H >> b, W >> b, C, nxt, p.part,
-                          Gmp, s));
+                          c->bn_relu ? p.shift[i1] : nullptr, p.N, H >> b, W >> b, C,
+                          pool_fuse ? nullptr : nxt, p.part, Gmp, s));
         cur = nxt;
         nxt = cur == G0 ? G1 : G0;
         if ((rc = bn_finalize(i1, Gmp))) return rc;
