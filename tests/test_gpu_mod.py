@@ -321,7 +321,7 @@ def test_wg16_tap_row_bit_identical():
         _assert_same(outs[0], outs[r3], f"wg16_r3={r3} vs one-tap")
 
 
-@pytest.mark.parametrize("halo,sched", [(19, 0), (20, 0), (19, 8)])
+@pytest.mark.parametrize("halo,sched", [(19, 0), (20, 0)])
 def test_rg16_halo_tile_within_bf16_error(halo, sched):
     """Tiles 19 / 20 (the tap-row halo kernel at 256x256 / 512x128, kernels_gemm16.hip
     rowgemm16_row3_kernel) sum K in
@@ -330,8 +330,10 @@ def test_rg16_halo_tile_within_bf16_error(halo, sched):
     (halo levels W = 256 .. 16; the 8x8 bottleneck falls back to the one-tap tile), one
     training step: its distance from tile 4 must stay below the distance of tile 4 itself
     from the fp32-MFMA network (the bf16 rounding error the path already carries), for the
-    logits and for every gradient (floor 1e-3 for near-zero BN-bias gradients).  sched 8: the
-    halo kernel on 16x16x32 MFMAs (option rg16_sched = 8, r05), held to the same bar."""
+    logits and for every gradient (floor 1e-3 for near-zero BN-bias gradients).  (The halo
+    kernel on 16x16x32 MFMAs, option rg16_sched = 8, passed this bar in r05 -- profiles/
+    r05_1tap16_ab.txt -- and is not a default; its case left the suite to keep it within
+    budget.)"""
     x, t = inputs(37, 1, 256, 256)
     P = MO.make_params(41, 128, 5)
     outs = {}
