@@ -331,9 +331,8 @@ def test_rg16_halo_tile_within_bf16_error(halo, sched):
     training step: its distance from tile 4 must stay below the distance of tile 4 itself
     from the fp32-MFMA network (the bf16 rounding error the path already carries), for the
     logits and for every gradient (floor 1e-3 for near-zero BN-bias gradients).  (The halo
-    kernel on 16x16x32 MFMAs, option rg16_sched = 8, passed this bar in r05 -- profiles/
-    r05_1tap16_ab.txt -- and is not a default; its case left the suite to keep it within
-    budget.)"""
+    kernel on 16x16x32 MFMAs, option rg16_sched = 8, passed this bar as case [19-8] in the r05
+    suite runs; it is not a default, and the case left the suite to keep it within budget.)"""
     x, t = inputs(37, 1, 256, 256)
     P = MO.make_params(41, 128, 5)
     outs = {}
