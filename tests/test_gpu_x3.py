@@ -286,7 +286,7 @@ def test_x3_wgrad_schedules_bit_identical():
     from _helpers import options
     x, t = inputs(37, 2, 128, 128)
     outs = []
-    scheds = (0, 1, 2, 3, 8, 9)
+    scheds = (0, 1, 2, 3, 8, 9, 10)
     for sched in scheds:
         m = hip_model(O.make_params(42), DEV)
         with options(m.flatten_().rt, x3_wsched=sched):

@@ -1510,8 +1510,8 @@ __global__ __launch_bounds__((BM / 32) * (BN / 32) * 64, OCC) void wgrad_x3_row3
     constexpr bool M16 = SCHED >= 8;  // 16x16x32 MFMAs (8: as 0, 9: as 3)
     static_assert(SCHED == 0 || SCHED == 3 || M16 || (S == 4 && WAVES == 8), "the staggered schedules need 4 stages, 8 waves");
     constexpr int LW = SCHED == 2 ? 4 : WAVES;  // waves issuing the DMA
-    constexpr int DIST = (SCHED == 1 || SCHED == 2) ? 2 : S - 1;  // chunks the DMA runs ahead
-    constexpr bool LATE = SCHED == 3 || SCHED == 9;  // the DMA issued after the first k-step's reads
+    constexpr int DIST = (SCHED == 1 || SCHED == 2 || SCHED == 10) ? 2 : S - 1;  // chunks the DMA runs ahead
+    constexpr bool LATE = SCHED == 3 || SCHED >= 9;  // the DMA issued after the first k-step's reads
     constexpr int RA = 6 * BM, RBB = 6 * BN;
     // halo pixel rows per stage: 34 (one 32-pixel row segment), or with M16 at W = 16 two
     // image rows of 16 + 2 (r05: the 16x16 level's 3x3 weight gradients on this kernel too)
@@ -1527,7 +1527,8 @@ __global__ __launch_bounds__((BM / 32) * (BN / 32) * 64, OCC) void wgrad_x3_row3
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave / WAVES_N, wn = wave % WAVES_N;
     const bool issuer = wave < LW;
-    const bool lag = (SCHED == 1 || SCHED == 2) && wave >= 4;
+    const bool lag = (SCHED == 1 || SCHED == 2 || SCHED == 10) && wave >= 4;
+    static_assert(SCHED != 10 || (S == 4 && WAVES == 8), "schedule 10: four stages, waves w / w + 4");
     const int tiles_n = p.CB / BN, tiles_m = p.CA / BM;
     int idx = p.xcd ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
     const int tn = idx % tiles_n;
@@ -1666,7 +1667,12 @@ __global__ __launch_bounds__((BM / 32) * (BN / 32) * 64, OCC) void wgrad_x3_row3
                 }
             }
         };
-        auto loop = [&](auto W16C) {
+        // schedule 10 (LG): waves 4..7 run each chunk's second 16-column half (bm = 1) at the
+        // start of the next chunk, re-reading its fragments from the chunk's stage (four
+        // stages, DMA two chunks ahead: a stage stays intact one chunk longer) -- the stagger
+        // of the halo GEMM's schedule 9 without held registers
+        auto loop = [&](auto W16C, auto LGC) {
+        constexpr bool LG = decltype(LGC)::value;
         if (issuer) {
 #pragma unroll
             for (int s = 0; s < DIST; ++s)
@@ -1679,6 +1685,25 @@ __global__ __launch_bounds__((BM / 32) * (BN / 32) * 64, OCC) void wgrad_x3_row3
             }
             x3_barrier();
             if (!LATE && issuer && kc + DIST < nk) issue(kc + DIST, (kc + DIST) % S, W16C);
+            if constexpr (LG) {
+                if (kc > 0) {
+                    const unsigned sp = sbase + ((kc + S - 1) % S) * STAGE;
+                    x3_short4 pb[2][3][2], pa[3][3][2];
+#pragma unroll
+                    for (int bn = 0; bn < 2; ++bn)
+#pragma unroll
+                        for (int q = 0; q < 3; ++q) rd(pb[bn][q], sp + boff[bn][q], IRB{});
+#pragma unroll
+                    for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+                        for (int q = 0; q < 3; ++q) rda(pa[dx][q], sp + aoff[dx][1][q], W16C);
+                    __builtin_amdgcn_sched_barrier(0);
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    __builtin_amdgcn_sched_barrier(0);
+                    mma(pa, pb, 1);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
             const unsigned sb = sbase + (kc % S) * STAGE;
             x3_short4 fb[2][3][2], fa[3][3][2], fa1[3][3][2];
 #pragma unroll
@@ -1696,6 +1721,10 @@ __global__ __launch_bounds__((BM / 32) * (BN / 32) * 64, OCC) void wgrad_x3_row3
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_sched_barrier(0);
+            if constexpr (LG) {
+                mma(fa, fb, 0);
+                continue;
+            }
 #pragma unroll
             for (int dx = 0; dx < 3; ++dx)
 #pragma unroll
@@ -1707,8 +1736,27 @@ __global__ __launch_bounds__((BM / 32) * (BN / 32) * 64, OCC) void wgrad_x3_row3
             __builtin_amdgcn_sched_barrier(0);
             mma(fa1, fb, 1);
         }
+        if constexpr (LG) {
+            if (nk > 0) {  // the last chunk's second half (its stage is not restaged any more)
+                const unsigned sp = sbase + ((nk - 1) % S) * STAGE;
+                x3_short4 pb[2][3][2], pa[3][3][2];
+#pragma unroll
+                for (int bn = 0; bn < 2; ++bn)
+#pragma unroll
+                    for (int q = 0; q < 3; ++q) rd(pb[bn][q], sp + boff[bn][q], IRB{});
+#pragma unroll
+                for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+                    for (int q = 0; q < 3; ++q) rda(pa[dx][q], sp + aoff[dx][1][q], W16C);
+                __builtin_amdgcn_sched_barrier(0);
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_sched_barrier(0);
+                mma(pa, pb, 1);
+            }
+        }
         };
-        loop(W16T{});
+        if (lag) loop(W16T{}, std::true_type{});
+        else loop(W16T{}, std::false_type{});
         float* slab = p.slab + (size_t)split * p.Mw * p.Nw;
 #pragma unroll
         for (int dx = 0; dx < 3; ++dx)
@@ -2211,7 +2259,9 @@ int launch_wgrad_x3(const WgradArgs& a, int tile, hipStream_t s, int sched) {
             hipLaunchKernelGGL((wgrad_x3_row3_kernel<64, 128, 3, 1, 3>), grid, dim3(512), 0, s, a);
         else if (tile == 3 && sched == 3)
             hipLaunchKernelGGL((wgrad_x3_row3_kernel<128, 64, 3, 1, 3>), grid, dim3(512), 0, s, a);
-        else if (a.W == 16 && tile == 2)  // 16x16x32 at W = 16 (w16ok: sched >= 8)
+        else if (a.W == 16 && tile == 2 && sched == 10)  // 16x16x32 at W = 16 (w16ok: sched >= 8)
+            hipLaunchKernelGGL((wgrad_x3_row3_kernel<64, 128, 4, 1, 10, true>), grid, dim3(512), 0, s, a);
+        else if (a.W == 16 && tile == 2)
             hipLaunchKernelGGL((wgrad_x3_row3_kernel<64, 128, 3, 1, 9, true>), grid, dim3(512), 0, s, a);
         else if (a.W == 16 && tile == 3)
             hipLaunchKernelGGL((wgrad_x3_row3_kernel<128, 64, 3, 1, 8, true>), grid, dim3(512), 0, s, a);
@@ -2221,6 +2271,8 @@ int launch_wgrad_x3(const WgradArgs& a, int tile, hipStream_t s, int sched) {
             hipLaunchKernelGGL((wgrad_x3_row3_kernel<64, 128, 3, 1, 8>), grid, dim3(512), 0, s, a);
         else if (tile == 2 && sched == 9)
             hipLaunchKernelGGL((wgrad_x3_row3_kernel<64, 128, 3, 1, 9>), grid, dim3(512), 0, s, a);
+        else if (tile == 2 && sched == 10)  // + waves 4..7 half a chunk behind (re-read)
+            hipLaunchKernelGGL((wgrad_x3_row3_kernel<64, 128, 4, 1, 10>), grid, dim3(512), 0, s, a);
         else if (tile == 3 && sched >= 8)
             hipLaunchKernelGGL((wgrad_x3_row3_kernel<128, 64, 3, 1, 8>), grid, dim3(512), 0, s, a);
         else if (tile == 4 && sched >= 8)

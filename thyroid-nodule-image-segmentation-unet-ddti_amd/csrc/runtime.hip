@@ -192,12 +192,15 @@ struct Options {
                                // 16x16x32 schedules +0.2 % over 5, profiles/r05_halo_k16.txt), 8 =
                                // 512x64 over 16-channel groups (r05: 1.103 vs 1.032 ms at level 0,
                                // profiles/r05_halo_k16.txt -- not faster, kept as an option)
-    int x3_wsched = 9;         // the tap-row weight gradient's schedule (0 = r04, 1 = four stages
+    int x3_wsched = 10;        // the tap-row weight gradient's schedule (0 = r04, 1 = four stages
                                // with waves 4..7 half a chunk behind, 2 = 1 with waves 0..3
                                // issuing every DMA (64x128 only), 3 = the DMA after the first
                                // k-step's reads (64x128, 128x64); bit-identical); 8 / 9 = 0 / 3
                                // on 16x16x32 MFMAs (64x128, 128x64, 64x64): config 2 +1.6 / +1.9 %
-                               // (profiles/r05_wgrad_m16_ab.txt)
+                               // (profiles/r05_wgrad_m16_ab.txt); 10 = 9 with waves 4..7 running
+                               // each chunk's second half after the next barrier from re-read
+                               // fragments (64x128; four stages): +1.5 % over 9
+                               // (profiles/r05_wgrad_sched10_ab.txt)
 };
 struct OptionDesc {
     const char* name;
