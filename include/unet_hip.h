@@ -216,7 +216,7 @@ int unet_resize_u8(unet_ctx* ctx, const uint8_t* src, int h, int w, float* dst, 
  *   tile_n64 tile_n64_dgrad tile_n32 tile_convt64 tile_convt tile_convt_dgrad tile16_n128
  *   tile16_n128_dgrad tile16_n64 rg16 rg16_tile rg16_bn_k rg16_r3 rg16_sched rg16_n128 rg16_n128_bn
  *   rg16_xp wg16 wg16_tile wg16_r3 convt16 wg16t xcd16 xcd_remap dz_in_wgrad x3 x3_tile
- *   x3_wtile x3_wblocks x3_n64 x3_r3 x3_r3_sched x3_n32 x3_n64_r3 x3_wsched x3_1tap16 head_fuse x3_convt_tile pool_fuse x3_wwaves x3_wwaves1
+ *   x3_wtile x3_wblocks x3_n64 x3_r3 x3_r3_sched x3_n32 x3_n64_r3 x3_wsched x3_1tap16 head_fuse x3_convt_tile pool_fuse x3_wwaves x3_wwaves1 tile_group wg16_split
  * Set them between steps, not between a forward and its backward: the workspace plan and
  * which saved images exist depend on them (x3, convt16, the bf16 kernel choices, ...), so
  * unet_backward returns UNET_ERR_INVALID when any option differs from the last training

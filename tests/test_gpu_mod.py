@@ -270,6 +270,21 @@ def test_rg16_tile_choice_is_numerically_invisible(side):
         _assert_same(outs[0], outs[tile], f"{side}^2 tile {tile} vs 0")
 
 
+def test_rg16_tile_group_bit_identical():
+    """Option tile_group (r06): BASELINE config 4's network at 512^2, bs 2 -- the 16^2 / 32^2
+    levels' 2048- and 4096-output GEMMs (128x128 tiles, 16-32 N tiles) walk their tiles in
+    groups of M tiles instead of M-major.  One training step is bit-identical."""
+    x, t = inputs(79, 2, 512, 512)
+    P = MO.make_params(83, 128, 5)
+    outs = {}
+    for flag in (0, 1):
+        m = _bf16_model(P, 128, 5)
+        with options(m.flatten_().rt, tile_group=flag):
+            outs[flag] = _bf16_step(m, x, t)
+        del m
+    _assert_same(outs[0], outs[1], "tile_group")
+
+
 def test_convt16_bit_identical():
     """Option convt16 (default on): in a bf16 training step the ConvT forward stores bf16 of
     its output straight into the decoder conv's kept operand image (the same RNE rounding of
@@ -312,13 +327,23 @@ def test_wg16_tap_row_bit_identical():
     x, t = inputs(43, 2, 256, 256)
     P = MO.make_params(47, 128, 5)
     outs = {}
-    for r3 in (0, 3, 4, 5):
+    for r3 in (0, 3, 4, 5, 6, 7):
         m = _bf16_model(P, 128, 5)
         with options(m.flatten_().rt, wg16_r3=r3):
             outs[r3] = _bf16_step(m, x, t)
         del m
     for r3 in (3, 4, 5):  # 5: four waves of 32 x 128 per tap (r05)
         _assert_same(outs[0], outs[r3], f"wg16_r3={r3} vs one-tap")
+    # 6 / 7 (r06): the 16x16x32 kernel, 7 with the re-read stagger -- the same MFMAs per
+    # accumulator in both (bit-identical); against the 32x32x16 kernels the chunk sums run 32
+    # instead of 16 products per MFMA step: f32 rounding apart (exact bf16 products)
+    _assert_same(outs[6], outs[7], "wg16_r3=7 vs 6")
+    assert torch.equal(outs[6][0], outs[4][0])  # the forward does not change
+    for k, g4 in outs[4][1].items():
+        g6 = outs[6][1][k]
+        assert torch.isfinite(g6).all(), k
+        tol = 2e-5 * max(g4.abs().max().item(), 1e-30)
+        assert (g6 - g4).abs().max().item() <= tol, (k, (g6 - g4).abs().max().item(), tol)
 
 
 @pytest.mark.parametrize("halo,sched", [(19, 0), (20, 0)])

@@ -275,6 +275,29 @@ def test_x3_head_fuse_bit_identical():
     assert torch.equal(outs[0][1], outs[1][1]), (outs[0][1] - outs[1][1]).abs().max().item()
 
 
+def test_tile_group_order_bit_identical():
+    """Option tile_group (r06, default on): the LDS-DMA row GEMMs walk their tiles in groups of M
+    tiles (gemm_common.h tile_mn) where the N tiles are many, so one XCD's resident blocks share
+    fewer weight rows.  A tile computes the same thing wherever it runs: one training step of the
+    model.py network at 256^2, bs 4 (the 16^2 level's 1024-output GEMMs take groups of 2) is
+    bit-identical to the M-major order."""
+    import unet_hip
+    from _helpers import options
+    x, t = inputs(71, 4, 256, 256)
+    outs = []
+    for flag in (0, 1):
+        m = hip_model(O.make_params(73), DEV)
+        with options(m.flatten_().rt, tile_group=flag):
+            logits = m(x.to(DEV))
+            l = unet_hip.seg_losses(logits, t.to(DEV))
+            (l[0] + l[1]).backward()
+            torch.cuda.synchronize()
+        outs.append((logits.detach().clone(), m._state.grad_arena.clone()))
+        del m
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1]), (outs[0][1] - outs[1][1]).abs().max().item()
+
+
 def test_x3_wgrad_schedules_bit_identical():
     """The 64x128 tap-row x3 weight gradient's schedules (option x3_wsched: four LDS stages
     with waves 4..7 half a chunk behind, and the same with waves 0..3 issuing every DMA; 8, 9 the

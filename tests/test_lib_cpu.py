@@ -312,7 +312,7 @@ def test_schedule_option_defaults():
             "rg16_bn_k": 0, "wg16": 1, "wg16_tile": 2, "wgrad16_blocks": 1536,
             "xcd_remap": 1, "xcd16": 1, "tile_convt": -1, "tile_convt_dgrad": 26, "rg16_xp": 0,
             "dz_in_wgrad": 256, "rg16_r3": 1, "rg16_sched": 0, "rg16_n128": 20, "rg16_n128_bn": 0, "wg16_r3": 4,
-            "convt16": 1, "x3": 1, "x3_tile": -1, "x3_wtile": -1, "x3_wblocks": 1536, "x3_n64": 2, "x3_r3": 1, "x3_r3_sched": 9, "x3_n32": 0, "x3_n64_r3": 6, "x3_wsched": 10, "x3_1tap16": 0, "x3_wwaves": 3, "x3_wwaves1": 3, "head_fuse": 1, "x3_convt_tile": -1, "pool_fuse": 1}
+            "convt16": 1, "x3": 1, "x3_tile": -1, "x3_wtile": -1, "x3_wblocks": 1536, "x3_n64": 2, "x3_r3": 1, "x3_r3_sched": 9, "x3_n32": 0, "x3_n64_r3": 6, "x3_wsched": 10, "x3_1tap16": 0, "x3_wwaves": 3, "x3_wwaves1": 3, "head_fuse": 1, "x3_convt_tile": -1, "pool_fuse": 1, "tile_group": 1, "wg16_split": 1}
     got = {k: fresh.get_option(k) for k in want}
     assert got == want
 

@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
@@ -91,7 +93,28 @@ struct RowGemmArgs {
                           // instead of f32 into out (the bf16 consumer's operand image)
     uint16_t* out3;       // E_CONVT: store the x3 split of the result into this x3 image (ldo
                           // channels per row, channel offset ooff) instead of f32 into out
+    int tgm;              // (r06) tile order: 0 / 1 M-major, > 1 groups of tgm M tiles
+                          // (gemm_common.h tile_mn), -1 = the launcher's choice (tile_group_auto)
 };
+
+// (r06) group size of tile_mn for a grid of ntm x ntn tiles whose blocks hold `slots` block
+// slots per XCD: the power of two that minimises the A + B rows one XCD's concurrently resident
+// blocks touch (both operands stream K elements per row, so rows are the cost).  M-major when
+// there are fewer than four N tiles (the weights fit the L2 anyway).
+inline int tile_group_auto(int64_t M, int N, int BM, int BN, int slots) {
+    const int64_t ntm = (M + BM - 1) / BM, ntn = N / BN;
+    if (ntn < 4 || ntm < 2) return 1;
+    const int64_t run = std::min<int64_t>(slots, (ntm * ntn + 7) / 8);
+    int best = 1;
+    int64_t bc = -1;
+    for (int64_t gm = 1; gm <= ntm && gm <= run; gm *= 2) {
+        const int64_t mspan = std::min<int64_t>(ntm, gm * ((run + gm * ntn - 1) / (gm * ntn)));
+        const int64_t nspan = std::min<int64_t>(ntn, (run + gm - 1) / gm);
+        const int64_t cost = mspan * BM + nspan * BN;
+        if (bc < 0 || cost < bc) bc = cost, best = (int)gm;
+    }
+    return best;
+}
 
 struct WgradArgs {
     int H, W;   // pixel grid of the reduction rows (P = Nimg*H*W)

@@ -64,6 +64,26 @@ __device__ __forceinline__ int xcd_remap(int b, int n) {
     return x < r ? x * (q + 1) + i : r * (q + 1) + (x - r) * q + i;
 }
 
+// (r06) remapped block -> (tile_m, tile_n).  gm <= 1: M-major (consecutive blocks walk the N
+// tiles of one M tile).  gm > 1: groups of gm M tiles, each group walking its N tiles with the
+// group's M tiles fastest, so a run of consecutive blocks -- the blocks one XCD holds at once,
+// after xcd_remap -- covers a gm x (run / gm) rectangle of tiles instead of one or two M tiles
+// x every N tile.  Where the weight matrix is large (config 4's 16² / 32² levels: 75-151 MB of
+// bf16 weights, every XCD re-reading all of it under M-major order) that cuts the distinct A and
+// B rows per XCD L2.  The order never changes what a tile computes: bit-identical.
+__device__ __forceinline__ void tile_mn(int bid, int ntm, int ntn, int gm, int& tm, int& tn) {
+    if (gm <= 1) {
+        tm = bid / ntn;
+        tn = bid - tm * ntn;
+        return;
+    }
+    const int per = gm * ntn, grp = bid / per, first = grp * gm;
+    const int gs = min(ntm - first, gm);
+    const int r = bid - grp * per;
+    tn = r / gs;
+    tm = first + (r - tn * gs);
+}
+
 __device__ __forceinline__ Pix decode(int m, int H, int W) {
     Pix r;
     int t = m / W;

@@ -127,7 +127,8 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_x3_kernel(RowGemmA
     const int wm = wave / WAVES_N, wn = wave % WAVES_N;
     const int ntn = p.N / BN;
     const int bid = p.xcd ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
-    const int tile_m = bid / ntn, tile_n = bid - tile_m * ntn;
+    int tile_m, tile_n;
+    tile_mn(bid, (p.M + BM - 1) / BM, ntn, p.tgm, tile_m, tile_n);
     const int m0 = tile_m * BM, n0 = tile_n * BN;
     const int H = p.H, W = p.W, C = p.C, K = p.K;
     const size_t rowa = 3 * (size_t)p.lda, rowb = 3 * (size_t)K;  // x3 row strides (bf16)
@@ -810,7 +811,8 @@ __global__ __launch_bounds__(BM / 64 * 2 * 64, BM == 256 ? 1 : 2) void rowgemm_x
     const int wm = wave / 2, wn = wave % 2;
     const int ntn = p.N / BN;
     const int bid = p.xcd ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
-    const int tile_m = bid / ntn, tile_n = bid - tile_m * ntn;
+    int tile_m, tile_n;
+    tile_mn(bid, (p.M + BM - 1) / BM, ntn, p.tgm, tile_m, tile_n);
     const int m0 = tile_m * BM, n0 = tile_n * BN;
     f32x16 acc[MT][NT];
     if constexpr (SCHED >= 8) {  // the 16x16x32 body (SCHED - 8 = the schedule)
@@ -1100,7 +1102,13 @@ static int x3_go(const RowGemmArgs& a, hipStream_t s) {
 }
 
 template <int AMODE, int EMODE>
-static int x3_tile(const RowGemmArgs& a, int tile, hipStream_t s, int sched = 0) {
+static int x3_tile(const RowGemmArgs& a0, int tile, hipStream_t s, int sched = 0) {
+    RowGemmArgs a = a0;
+    if (a.tgm < 0) {  // tile order: the group size for this tile's grid (two blocks per CU on 128 x 64)
+        int bm = 0, bn = 0;
+        if (rowgemm_x3_tile_dims(tile, &bm, &bn) != 0) return -1;
+        a.tgm = tile_group_auto(a.M, a.N, bm, bn, (tile == 2 || tile == 6 || tile == 7) ? 64 : 32);
+    }
     if (tile == 8) {  // 512 x 64, 16-channel halo groups (r05)
         if constexpr (AMODE == G_CONV3) return x3r3k16_go<EMODE>(a, sched >= 8 ? 1 : sched, s);
         return -1;

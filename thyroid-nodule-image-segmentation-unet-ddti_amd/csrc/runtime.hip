@@ -192,6 +192,11 @@ struct Options {
                                // 16x16x32 schedules +0.2 % over 5, profiles/r05_halo_k16.txt), 8 =
                                // 512x64 over 16-channel groups (r05: 1.103 vs 1.032 ms at level 0,
                                // profiles/r05_halo_k16.txt -- not faster, kept as an option)
+    int wg16_split = 1;        // (r06) bf16 tap-row weight gradients: split-K by whole waves (wgrad_cfg);
+                               // 0 = r05's 1536-block target
+    int tile_group = 1;        // (r06) row-GEMM tile order of the LDS-DMA kernels (rg16, x3): 1 = grouped
+                               // where the N tiles are many (tile_group_auto), 0 = M-major (r05);
+                               // bit-identical
     int x3_wsched = 10;        // the tap-row weight gradient's schedule (0 = r04, 1 = four stages
                                // with waves 4..7 half a chunk behind, 2 = 1 with waves 0..3
                                // issuing every DMA (64x128 only), 3 = the DMA after the first
@@ -261,6 +266,8 @@ const OptionDesc OPTION_TABLE[] = {
     {"pool_fuse", &Options::pool_fuse},
     {"x3_wwaves", &Options::x3_wwaves},
     {"x3_wwaves1", &Options::x3_wwaves1},
+    {"tile_group", &Options::tile_group},
+    {"wg16_split", &Options::wg16_split},
 };
 
 }  // namespace
@@ -721,6 +728,27 @@ WgradCfg wgrad_cfg(const unet_ctx* c, int CA, int tapsA, int CB, int tapsB, int6
     if (s < 1) s = 1;
     int64_t pps = (P + s - 1) / s;
     pps = (pps + 127) / 128 * 128;
+    // (r06) bf16 3x3 weight gradients on the tap-row kernel (W % 64 == 0): the 1536-block target
+    // above, counted in one-tap 128x128 tiles, launches (CA / 128) 3 (CB / 128) tap-row blocks
+    // per split, i.e. 513-576 blocks on 256 one-block-per-CU slots -- a third wave holding 1-64
+    // blocks, and the kernel took three block durations instead of two.  Instead pick the split
+    // count s minimising waves(s) x chunks per block(s) + the slab traffic of s splits (the
+    // one-tap kernel, option wg16_r3 = 0, gets the same partition: bit-identical).
+    if (bf16 && c->opt.wg16_split && tapsA == 9 && tapsB == 1 && row_w > 0 && row_w % 64 == 0 &&
+        CA % 128 == 0 && CB % 128 == 0 && P % 64 == 0) {
+        const int64_t t3 = (int64_t)(CA / 128) * 3 * (CB / 128);
+        const int64_t slots = 256;
+        double best = -1;
+        for (int64_t sc = 1; sc <= maxs; ++sc) {
+            const int64_t waves = (t3 * sc + slots - 1) / slots;
+            const int64_t chunks = (P + 64 * sc - 1) / (64 * sc);
+            // ~1.2 us per 64-pixel chunk of a 128x128x3 block; slabs written and reduced at ~5 TB/s
+            const double cost = waves * chunks * 1.2e-6 + sc * 9.0 * CA * CB * 8 / 5e12;
+            if (best < 0 || cost < best) best = cost, s = sc;
+        }
+        pps = (P + s - 1) / s;
+        pps = (pps + 63) / 64 * 64;
+    }
     w.pps = (int)pps;
     w.splits = (int)((P + pps - 1) / pps);
     return w;
@@ -917,7 +945,7 @@ WgradCfg x3_wgrad_cfg(const unet_ctx* c, int CA, int tapsA, int CB, int tapsB, i
 }
 
 // point g at x3 operands: A image `img` (lda = C channels), weights w3
-void use_x3(const Plan& p, RowGemmArgs& g, const uint16_t* img, int C, const uint16_t* w3) {
+void use_x3(const unet_ctx* c, const Plan& p, RowGemmArgs& g, const uint16_t* img, int C, const uint16_t* w3) {
     g.a = nullptr;
     g.a16 = img;
     g.lda = C;
@@ -929,6 +957,7 @@ void use_x3(const Plan& p, RowGemmArgs& g, const uint16_t* img, int C, const uin
     g.bt16 = w3;
     g.zero16 = p.zero16;
     g.xcd = 1;
+    g.tgm = c->opt.tile_group ? -1 : 0;
 }
 
 std::string x3wlabel(const char* fam, const WgradCfg& w, int layer) {
@@ -1290,6 +1319,7 @@ void use_a16(const unet_ctx* c, const Plan& p, RowGemmArgs& g, int C) {
     g.acoef = nullptr;
     g.zero16 = p.zero16;
     g.xcd = xcd16_on(c);
+    g.tgm = c->opt.tile_group ? -1 : 0;
 }
 
 // device copies of the expand / compact tables (the host tables live in the context, so
@@ -1405,7 +1435,7 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
                     RUN("prep_x3", 0, k_to_x3(a.ptr, a.ld, a.off, C.cin, a.scale, a.shift, a.relu, M, img,
                                               C.cin, 0, s));
                 }
-                use_x3(p, g, img, C.cin, p.pack3 + 3 * C.pf);
+                use_x3(c, p, g, img, C.cin, p.pack3 + 3 * C.pf);
                 const int tile = x3_tile(c, g);
                 R = bn_groups(M);
                 RUN(xlabel("conv_fwd", tile, i), 2.0 * M * C.cout * 9 * C.cin, launch_rowgemm_x3(g, tile, s, x3_rsched(c, tile)));
@@ -1472,7 +1502,7 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
             uint16_t* img = p.t3[k] ? p.t3[k] : p.s3;
             RUN("prep_x3", 0, k_to_x3(g.a, g.lda, g.aoff, T.cin, g.ascale, g.ashift, g.arelu, g.M, img,
                                       T.cin, 0, s));
-            use_x3(p, g, img, T.cin, p.pack3 + 3 * T.pf);
+            use_x3(c, p, g, img, T.cin, p.pack3 + 3 * T.pf);
             // option convt16 (x3 training): the up half of the decoder's concat goes straight
             // into that conv's kept x3 image, its only reader; the conv's prep pass then
             // converts the skip half only
@@ -1711,7 +1741,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
             g.K = 9 * C.cout;
             g.C = C.cout;
             g.amode = G_CONV3;
-            use_x3(p, g, p.s3, C.cout, p.pack3 + 3 * C.pd);
+            use_x3(c, p, g, p.s3, C.cout, p.pack3 + 3 * C.pd);
             g.out = dx;
             g.ldo = ldx;
             g.ooff = 0;
@@ -1799,14 +1829,14 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
             int t = wg16_tile(c, C.cin, C.cout);
             // option wg16_r3: the tap-row kernel (three taps per block from one halo row)
             const int r3 = c->opt.wg16_r3;
-            if (r3 >= 3 && r3 <= 5 && Wl % 64 == 0 && C.cin % 128 == 0 && C.cout % 128 == 0 &&
+            if (r3 >= 3 && r3 <= 7 && Wl % 64 == 0 && C.cin % 128 == 0 && C.cout % 128 == 0 &&
                 wc.pps % 64 == 0)
                 t = r3;
             int wbm = 0, wbn = 0, wst = 0;
             wgrad16g_tile_dims(t, &wbm, &wbn, &wst);
             char lb[96];
             snprintf(lb, sizeof lb, "conv_wgrad/wg16%s_%dx%ds%d|%d",
-                     t == 3 || t == 4 ? "r3" : t >= 5 ? "r3w" : "", wbm, wbn, wst, i);
+                     t == 3 || t == 4 ? "r3" : t == 5 ? "r3w" : t >= 6 ? "r3m" : "", wbm, wbn, wst, i);
             RUN(lb, 2.0 * P * C.cout * 9 * C.cin, launch_wgrad16(w, t, s));
         } else {
             RUN(wlabel("conv_wgrad", wc, i), 2.0 * P * C.cout * 9 * C.cin, launch_wgrad(w, wc.tile, s));
@@ -1909,7 +1939,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
             g.K = 4 * T.cout;
             g.C = T.cout;
             g.amode = G_UP2;
-            use_x3(p, g, p.s3, T.cout, p.pack3 + 3 * T.pd);
+            use_x3(c, p, g, p.s3, T.cout, p.pack3 + 3 * T.pd);
             g.out = dx;
             g.ldo = T.cin;
             g.ooff = 0;
