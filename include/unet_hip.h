@@ -212,11 +212,10 @@ int unet_resize_u8(unet_ctx* ctx, const uint8_t* src, int h, int w, float* dst, 
  * library never reads the environment: an option changes only when set here.
  * Names (runtime.hip OPTION_TABLE, in this order; unet_option_name enumerates them):
  *   wgrad_row3 wgrad_row3_tile wgrad_row3_big wgrad_row3_blocks wgrad_row3_n32 wgrad_blocks
- *   wgrad16_blocks wgrad_tile_w wgrad_tile_n wgrad16_tile tile_n128 tile_n128_dgrad
- *   tile_n64 tile_n64_dgrad tile_n32 tile_convt64 tile_convt tile_convt_dgrad tile16_n128
- *   tile16_n128_dgrad tile16_n64 rg16 rg16_tile rg16_bn_k rg16_r3 rg16_sched rg16_n128 rg16_n128_bn
- *   rg16_xp wg16 wg16_tile wg16_r3 convt16 wg16t xcd16 xcd_remap dz_in_wgrad x3 x3_tile
- *   x3_wtile x3_wblocks x3_n64 x3_r3 x3_r3_sched x3_n32 x3_n64_r3 x3_wsched x3_1tap16 head_fuse x3_convt_tile pool_fuse x3_wwaves x3_wwaves1 tile_group wg16_split
+ *   wgrad16_blocks wgrad_tile_w wgrad_tile_n tile_n128 tile_n128_dgrad tile_n64 tile_n64_dgrad
+ *   tile_n32 tile_convt64 tile_convt tile_convt_dgrad rg16 rg16_tile rg16_bn_k rg16_r3 rg16_n128
+ *   rg16_n128_bn wg16 wg16_tile wg16_r3 convt16 wg16t xcd16 xcd_remap dz_in_wgrad x3 x3_tile
+ *   x3_wtile x3_wblocks x3_n64 x3_r3 head_fuse pool_fuse x3_wwaves x3_wwaves1 tile_group
  * Set them between steps, not between a forward and its backward: the workspace plan and
  * which saved images exist depend on them (x3, convt16, the bf16 kernel choices, ...), so
  * unet_backward returns UNET_ERR_INVALID when any option differs from the last training

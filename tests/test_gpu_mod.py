@@ -301,23 +301,6 @@ def test_convt16_bit_identical():
     _assert_same(outs[0], outs[1], "convt16")
 
 
-def test_rg16_halo_schedules_bit_identical():
-    """The bf16 halo GEMM's schedules (option rg16_sched: waves 4..7 run each stage's last tap
-    after the next barrier from held fragments; 2 also moves the DMA after the first tap's
-    reads) run the same MFMAs in the same order per accumulator: one training step of BASELINE
-    config 4's network at 256^2 (tiles 19 / 20 on W = 256 .. 16) is bit-identical to r04's."""
-    x, t = inputs(61, 2, 256, 256)
-    P = MO.make_params(67, 128, 5)
-    outs = {}
-    for sched in (0, 1, 2):
-        m = _bf16_model(P, 128, 5)
-        with options(m.flatten_().rt, rg16_sched=sched):
-            outs[sched] = _bf16_step(m, x, t)
-        del m
-    _assert_same(outs[0], outs[1], "rg16_sched 1")
-    _assert_same(outs[0], outs[2], "rg16_sched 2")
-
-
 def test_wg16_tap_row_bit_identical():
     """The tap-row bf16 weight gradient (kernels_gemm16.hip wgrad16_row3_kernel, option wg16_r3
     = 3 / 4 LDS stages: the three dx taps of one tap row from one halo of 66 pixel rows) runs
@@ -346,8 +329,8 @@ def test_wg16_tap_row_bit_identical():
         assert (g6 - g4).abs().max().item() <= tol, (k, (g6 - g4).abs().max().item(), tol)
 
 
-@pytest.mark.parametrize("halo,sched", [(19, 0), (20, 0)])
-def test_rg16_halo_tile_within_bf16_error(halo, sched):
+@pytest.mark.parametrize("halo", [19, 20])
+def test_rg16_halo_tile_within_bf16_error(halo):
     """Tiles 19 / 20 (the tap-row halo kernel at 256x256 / 512x128, kernels_gemm16.hip
     rowgemm16_row3_kernel) sum K in
     the order (tap row, channel slice, tap column) instead of the one-tap kernel's (tap,
@@ -355,15 +338,13 @@ def test_rg16_halo_tile_within_bf16_error(halo, sched):
     (halo levels W = 256 .. 16; the 8x8 bottleneck falls back to the one-tap tile), one
     training step: its distance from tile 4 must stay below the distance of tile 4 itself
     from the fp32-MFMA network (the bf16 rounding error the path already carries), for the
-    logits and for every gradient (floor 1e-3 for near-zero BN-bias gradients).  (The halo
-    kernel on 16x16x32 MFMAs, option rg16_sched = 8, passed this bar as case [19-8] in the r05
-    suite runs; it is not a default, and the case left the suite to keep it within budget.)"""
+    logits and for every gradient (floor 1e-3 for near-zero BN-bias gradients)."""
     x, t = inputs(37, 1, 256, 256)
     P = MO.make_params(41, 128, 5)
     outs = {}
     for tile in (4, halo):
         m = _bf16_model(P, 128, 5)
-        with options(m.flatten_().rt, rg16_tile=tile, rg16_sched=sched if tile == halo else 0):
+        with options(m.flatten_().rt, rg16_tile=tile):
             outs[tile] = _bf16_step(m, x, t)
         del m
     import unet_hip
@@ -503,18 +484,16 @@ def test_mod_narrow_one_step_matches_golden(golden_dir, tag, base):
                       GRAD_TOL, tag)
 
 
-@pytest.mark.parametrize("n32", [0, 1])
 @pytest.mark.parametrize("base,depth,H,W", [(16, 5, 64, 96), (24, 4, 128, 64), (48, 6, 128, 256),
                                             (32, 4, 64, 64)])
-def test_mod_narrow_full_grads_vs_fp64(base, depth, H, W, n32):
+def test_mod_narrow_full_grads_vs_fp64(base, depth, H, W):
     """Every gradient element of narrow networks (base 32 native on the 32-channel tiles;
     16 / 24 padded to 32 and 48 to 64 inside the library) against the
     fp64 oracle, and the padding is invisible in the caller's arenas (torch-layout
     gradients, running stats).  At depth 6 the bottleneck BN sees 16 values per channel,
     where a near-zero ReLU input flips under any fp32 rounding change: the envelope is 2x
     the fp32 oracle's own error over x and x * (1 + 1e-7) (as tests/test_gpu_res.py),
-    floor 1e-2.  n32 = 1 (option x3_n32, r05): the 32- and 96-channel layers on the x3 kernels
-    too (128x32 row tile, 32-wide weight-gradient tiles)."""
+    floor 1e-2."""
     import unet_hip
     from _helpers import options
     P = MO.make_params(7, base, depth)
@@ -526,7 +505,7 @@ def test_mod_narrow_full_grads_vs_fp64(base, depth, H, W, n32):
                          for k, v in MO.init_buffers(base, depth).items()},
                         None, x.double(), t.double(), depth=depth)
     m = hip_mod_model(P, DEV, base, depth)
-    with options(m.flatten_().rt, x3_n32=n32):
+    with options(m.flatten_().rt):
         logits = m(x.to(DEV))
         losses = unet_hip.seg_losses(logits, t.to(DEV))
         (losses[0] + losses[1]).backward()

@@ -466,7 +466,7 @@ def test_mask_counts():
     assert torch.equal(mask.bool(), pm)
 
 
-def test_full_size_vs_torch_gpu_reference():
+def test_full_size_vs_cpu_oracle():
     """bs=32, 1x256x256 (BASELINE config 2): forward and gradients vs the CPU oracle's step on
     the box's host threads (~15 s; the same functional graph on the GPU through torch/MIOpen
     spent ~110 s compiling its kernels on every fresh box)."""
@@ -574,8 +574,8 @@ def test_wgrad_row3_matches_one_tap_tiles(variant):
                                            ("model", 1, 48, 80), ("mod", 2, 128, 64),
                                            ("res", 2, 64, 64)])
 def test_pipe_gemm_bit_identical(variant, B, H, W):
-    """Row-GEMM tiles 16..19, 25, 26 (kernels_gemm_pipe.hip: the software-pipelined schedule
-    of the 128x128 / 128x64 f32 tiles, global loads one or two chunks ahead, 18 the default;
+    """Row-GEMM tiles 18, 19, 25, 26 (kernels_gemm_pipe.hip: the software-pipelined schedule
+    of the 128x128 / 128x64 f32 tiles, global loads two chunks ahead, 18 the default;
     25 / 26: 128x64 at three blocks per CU, the N = 64 dgrad / ConvT-dgrad defaults) walk K in
     the same order with the same prologue arithmetic and the same epilogues as the
     register-staged rowgemm_kernel tiles (4, 0, 1), so a training step -- logits and the
@@ -588,8 +588,7 @@ def test_pipe_gemm_bit_identical(variant, B, H, W):
     from oracle import mod_ref_cpu as MO
     x, t = inputs(43, B, H, W)
     outs = []
-    for tiles in ((4, 0, 1, 0), (16, 16, 17, 16), (18, 18, 19, 18), (16, 18, 25, 26),
-                  (18, 16, 26, 25)):
+    for tiles in ((4, 0, 1, 0), (18, 18, 19, 18), (18, 4, 25, 26), (4, 18, 26, 25)):
         if variant == "model":
             m = hip_model(O.make_params(42), DEV)
         elif variant == "mod":

@@ -97,9 +97,8 @@ def _to64(d):
     return {k: (v.double() if v.is_floating_point() else v.clone()) for k, v in d.items()}
 
 
-@pytest.mark.parametrize("base,depth,size,n32", [(64, 3, 64, 0), (64, 5, 128, 0), (32, 4, 64, 0),
-                                                 (32, 4, 64, 1), (16, 4, 64, 1)])
-def test_res_full_grads_vs_oracle(base, depth, size, n32):
+@pytest.mark.parametrize("base,depth,size", [(64, 3, 64), (64, 5, 128), (32, 4, 64), (16, 4, 64)])
+def test_res_full_grads_vs_oracle(base, depth, size):
     """Every element of every gradient vs the oracle (depth 5 = the reference default).
 
     Deep levels are small: at depth 5 the bottleneck's BatchNorm sees (size/32)^2 pixels x
@@ -109,8 +108,7 @@ def test_res_full_grads_vs_oracle(base, depth, size, n32):
     oracle's own worst per-tensor error, floored at the usual 1e-2.  That
     fp32 error is taken over two evaluations, of x and of x * (1 + 1e-7): a 1-ulp-scale
     input change flips such near-zero masks too (base 64 depth 3: the bottleneck's
-    conv.1 bias gradient goes from 2.7e-3 to 1.5e-2 off fp64 in the oracle itself).
-    n32 = 1 (option x3_n32, r05): the 32-channel layers on the x3 kernels too."""
+    conv.1 bias gradient goes from 2.7e-3 to 1.5e-2 off fp64 in the oracle itself)."""
     import unet_hip
     from _helpers import options
     P = MO.res_make_params(9, base, depth)
@@ -121,7 +119,7 @@ def test_res_full_grads_vs_oracle(base, depth, size, n32):
     r64 = MO.res_train_step(_to64(P), _to64(MO.res_init_buffers(base, depth)), None, x.double(),
                             t.double(), depth=depth)
     m = _model(P, base, depth)
-    with options(m.flatten_().rt, x3_n32=n32):
+    with options(m.flatten_().rt):
         logits = m(x.to(DEV))
         losses = unet_hip.seg_losses(logits, t.to(DEV))
         (losses[0] + losses[1]).backward()

@@ -92,6 +92,18 @@ def test_debug_views_inside_workspace(rt):
         assert v.shape[0] * v.shape[1] <= nb // 4
     sc = rt.debug_view(ws, N, H, W, True, 1, 3)
     assert sc.numel() == 128
+    # the f32 pooled buffer (view 5) exists only where the max-pool writes it: on the x3 path
+    # it writes the next conv's x3 image instead, so the view is refused
+    from unet_hip._lib import HipError
+    with pytest.raises(HipError):
+        rt.debug_view(ws, N, H, W, True, 5, 0)
+    try:
+        rt.set_option("x3", 0)
+        ws0 = torch.empty(rt.workspace_bytes(N, H, W, True), dtype=torch.uint8)
+        v, _ = rt.debug_view(ws0, N, H, W, True, 5, 0)
+        assert tuple(v.shape) == (N * (H // 2) * (W // 2), 64)
+    finally:
+        rt.set_option("x3", 1)
 
 
 def test_no_cpu_fallback():
@@ -310,9 +322,9 @@ def test_schedule_option_defaults():
             "tile_n32": 15, "tile_convt64": 1, "wgrad_row3": 1, "wgrad_row3_big": 21,
             "wgrad_row3_blocks": 1536, "wgrad_blocks": 2048, "rg16": 1, "rg16_tile": -1,
             "rg16_bn_k": 0, "wg16": 1, "wg16_tile": 2, "wgrad16_blocks": 1536,
-            "xcd_remap": 1, "xcd16": 1, "tile_convt": -1, "tile_convt_dgrad": 26, "rg16_xp": 0,
-            "dz_in_wgrad": 256, "rg16_r3": 1, "rg16_sched": 0, "rg16_n128": 20, "rg16_n128_bn": 0, "wg16_r3": 4,
-            "convt16": 1, "x3": 1, "x3_tile": -1, "x3_wtile": -1, "x3_wblocks": 1536, "x3_n64": 2, "x3_r3": 1, "x3_r3_sched": 9, "x3_n32": 0, "x3_n64_r3": 6, "x3_wsched": 10, "x3_1tap16": 0, "x3_wwaves": 3, "x3_wwaves1": 3, "head_fuse": 1, "x3_convt_tile": -1, "pool_fuse": 1, "tile_group": 1, "wg16_split": 1}
+            "xcd_remap": 1, "xcd16": 1, "tile_convt": -1, "tile_convt_dgrad": 26,
+            "dz_in_wgrad": 256, "rg16_r3": 1, "rg16_n128": 20, "rg16_n128_bn": 0, "wg16_r3": 4,
+            "convt16": 1, "x3": 1, "x3_tile": -1, "x3_wtile": -1, "x3_wblocks": 1536, "x3_n64": 2, "x3_r3": 1, "x3_wwaves": 3, "x3_wwaves1": 3, "head_fuse": 1, "pool_fuse": 1, "tile_group": 1}
     got = {k: fresh.get_option(k) for k in want}
     assert got == want
 

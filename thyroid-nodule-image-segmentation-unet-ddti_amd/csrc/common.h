@@ -152,23 +152,20 @@ struct WgradArgs {
 // host launchers (kernels_gemm.hip)
 // row-GEMM tile ids: register-staged 0 = 128x128 (two LDS images), 1 = 128x64, 4 = 128x128,
 // 6 = 128x128 64-K chunks (bf16), 13 = 128x32, 14 = 256x32; software-pipelined (kernels_gemm_pipe.hip)
-// 16 = 128x128, 17 = 128x64, 18 / 19 = the same loading two chunks ahead, 25 / 26 = 128x64 at
-// three blocks per CU (one / two chunks ahead)
+// 18 = 128x128, 19 = 128x64 (loading two chunks ahead), 25 / 26 = 128x64 at three blocks per CU
+// (one / two chunks ahead)
 int launch_rowgemm(const RowGemmArgs& a, int tile, hipStream_t s);
 int rowgemm_tile_dims(int tile, int* bm, int* bn, int* bk);
 int rowgemm_tile_dbuf(int tile);
-// software-pipelined f32 row GEMM (kernels_gemm_pipe.hip); tile 0 = 128x128, 1 = 128x64,
-// 2 / 3 = two chunks ahead, 4 / 5 = 128x64 at three blocks per CU
+// software-pipelined f32 row GEMM (kernels_gemm_pipe.hip); tile 2 = 128x128, 3 = 128x64 (two
+// chunks ahead), 4 / 5 = 128x64 at three blocks per CU
 int rowgemm_pipe_ok(const RowGemmArgs& a);
 int launch_rowgemm_pipe(const RowGemmArgs& a, int tile, hipStream_t s);
 // wgrad tile ids (kernels_gemm.hip WGRAD_TILES): 0 = 128x128, 3 = 64x128 two waves,
 // 5 = 128x64 four waves, 7 = 64x64 three waves / SIMD, 8 = 64x32, 9 = 32x32;
 // 20.. = one row of 3x3 taps per block (3 accumulator sets; BM = channels of ONE tap):
 // 20 = 64x64, 21 = 128x64, 22 = 64x128, 23 = 128x128
-// sched: schedule of the tap-row halo tiles 19 / 20 (rowgemm16_row3_kernel SCHED; bit-identical)
-int launch_rowgemm16(const RowGemmArgs& a, int tile, hipStream_t s, int sched = 0);
-// speed-of-light ablations of the forward rg16 GEMM (tile 4): -2 when not applicable
-int launch_rowgemm16_xp(const RowGemmArgs& a, int xp, hipStream_t s);
+int launch_rowgemm16(const RowGemmArgs& a, int tile, hipStream_t s);
 int rowgemm16_tile_dims(int tile, int* bm, int* bn, int* stages = nullptr);
 int wgrad16g_tile_dims(int tile, int* bm, int* bn, int* stages = nullptr);
 int launch_wgrad(const WgradArgs& a, int tile, hipStream_t s);
@@ -178,14 +175,12 @@ int wgrad_tile_taps(int tile);  // taps of the M dimension one block covers (3 f
 // f32 GEMMs on bf16 MFMAs through exact three-way operand splits (kernels_gemm_x3.hip):
 // x3 images bf16 [rows][C / 32][3][32] (hi, mid, lo planes per 32-channel group).  Row GEMM:
 // a16 / bt16 are x3 images (lda channels per A row, aoff a channel offset); tiles 0 =
-// 256x128, 1 = 128x128, 2 = 128x64.  Weight gradient: a / b are x3 images; tiles 0 = 128x128,
-// 1 = 64x64.
-// sched: schedule of the tap-row halo tiles 4 / 5 (kernels_gemm_x3.hip X3R3Sched; bit-identical)
-int launch_rowgemm_x3(const RowGemmArgs& a, int tile, hipStream_t s, int sched = 0);
+// 256x128, 1 = 128x128, 2 = 128x64, 3 = 256x64; tap-row halo tiles 4 = 256x128, 6 = 128x64.
+// Weight gradient: a / b are x3 images; tiles 0 = 128x128, 1 = 64x64; tap-row tiles 2 = 64x128,
+// 3 = 128x64, 4 = 64x64.
+int launch_rowgemm_x3(const RowGemmArgs& a, int tile, hipStream_t s);
 int rowgemm_x3_tile_dims(int tile, int* bm, int* bn);
-// sched: schedule of the tap-row 64x128 tile (2): 0 = r04, 1 = four stages with waves 4..7 half a
-// chunk behind, 2 = 1 with waves 0..3 issuing every DMA (bit-identical)
-int launch_wgrad_x3(const WgradArgs& a, int tile, hipStream_t s, int sched = 0);
+int launch_wgrad_x3(const WgradArgs& a, int tile, hipStream_t s);
 int wgrad_x3_tile_dims(int tile, int* bm, int* bn);
 // x3 image of op(src) (BN affine if scale, ReLU on channels < relu) into dst [P][dld] at
 // channel offset doff

@@ -1098,7 +1098,7 @@ int rowgemm_tile_dims(int tile, int* bm, int* bn, int* bk) {
         *bk = 32;
         return 0;
     }
-    if (tile >= 16 && tile <= 19) {  // rowgemm_pipe_kernel (18, 19: loads two chunks ahead)
+    if (tile == 18 || tile == 19) {  // rowgemm_pipe_kernel (loads two chunks ahead)
         *bm = 128;
         *bn = tile % 2 == 0 ? 128 : 64;
         *bk = 32;
@@ -1124,7 +1124,7 @@ int rowgemm_tile_dims(int tile, int* bm, int* bn, int* bk) {
 
 int rowgemm_tile_dbuf(int tile) {
     if (tile == 15) return 3;  // operands straight from global memory
-    if ((tile >= 16 && tile <= 19) || tile == 25 || tile == 26) return 2;  // pipelined
+    if (tile == 18 || tile == 19 || tile == 25 || tile == 26) return 2;  // pipelined
 #define RG_DB(id, T) \
     if (tile == id) return T::DBUF ? 1 : 0;
     ROWGEMM_TILES(RG_DB)
@@ -1180,12 +1180,12 @@ int launch_rowgemm(const RowGemmArgs& a, int tile, hipStream_t s) {
     if ((a.escale != nullptr) != (a.eshift != nullptr) || (a.arelu && !aff)) return -1;
     if (a.emode == E_RESID && !a.escale) return -1;
     if ((a.bt != nullptr) == (a.bt16 != nullptr)) return -1;  // exactly one weight image
-    // ids 16..19, 25, 26: the software-pipelined f32 kernel (128x128 / 128x64, loads one or
-    // two chunks ahead; 25 / 26: 128x64 at three blocks per CU); operands it does not take
-    // (bf16 weights, > 2 GB offsets) run the same tile shape on the register-staged kernel
-    if ((tile >= 16 && tile <= 19) || tile == 25 || tile == 26) {
+    // ids 18, 19, 25, 26: the software-pipelined f32 kernel (128x128 / 128x64 loading two chunks
+    // ahead; 25 / 26: 128x64 at three blocks per CU); operands it does not take (bf16 weights,
+    // > 2 GB offsets) run the same tile shape on the register-staged kernel
+    if (tile == 18 || tile == 19 || tile == 25 || tile == 26) {
         if (rowgemm_pipe_ok(a)) return launch_rowgemm_pipe(a, tile <= 19 ? tile - 16 : tile - 21, s);
-        tile = (tile <= 19 && tile % 2 == 0) ? 4 : 1;
+        tile = tile == 18 ? 4 : 1;
     }
     return a.bt16 ? rowgemm_dispatch<true>(a, tile, s) : rowgemm_dispatch<false>(a, tile, s);
 }

@@ -62,10 +62,7 @@ struct Tile16 {
     static constexpr int THREADS = 64 * WAVES;
 };
 
-// XP: speed-of-light ablations (option rg16_xp, forward GEMMs on tile 4 only; results are
-// garbage): bit 0 drops the A DMA, 1 the B DMA, 2 the LDS fragment reads, 3 the loop's
-// waits and barriers.  The library's normal path instantiates XP = 0.
-template <int AMODE, int EMODE, class T, int XP = 0>
+template <int AMODE, int EMODE, class T>
 __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm16_kernel(RowGemmArgs p) {
     constexpr int BM = T::BM, BN = T::BN, WM = T::WM, WN = T::WN, S = T::S, BK = T::BK;
     constexpr int WAVES = T::WAVES, WAVES_N = BN / WN;
@@ -128,17 +125,13 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm16_kernel(RowGemmAr
         char* base = smem + st * STAGE;
 #pragma unroll
         for (int j = 0; j < AI; ++j) {
-            if (XP & 1) continue;
             bool valid;
             const int src = gather_src<AMODE>(tap, am[j], aq[j], H, W, valid);
             const uint16_t* g = (valid && aok[j]) ? p.a16 + (size_t)src * p.lda + c0 + ach[j] : zero;
             glds16(g, base + (j * WAVES + wave) * 1024);
         }
 #pragma unroll
-        for (int j = 0; j < BI; ++j) {
-            if (XP & 2) continue;
-            glds16(bsrc[j] + k0, base + BM * RB + (j * WAVES + wave) * 1024);
-        }
+        for (int j = 0; j < BI; ++j) glds16(bsrc[j] + k0, base + BM * RB + (j * WAVES + wave) * 1024);
     };
 
     f32x16 acc[MT][NT];
@@ -166,9 +159,6 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm16_kernel(RowGemmAr
     }
 
     const int nk = K / BK;
-    bf16x8 xa;  // XP & 4: a register operand
-#pragma unroll
-    for (int j = 0; j < 8; ++j) xa[j] = (__bf16)(float)(lane + j);
 #pragma unroll
     for (int s = 0; s < DIST; ++s)
         if (s < nk) issue(s, s);
@@ -177,8 +167,7 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm16_kernel(RowGemmAr
         if (kc + DIST < nk) issue(kc + DIST, (kc + DIST) % S);
         // chunks issued after kc that may stay in flight
         const int ahead = min(INFL, nk - 1 - kc);
-        if constexpr (XP & 8) {
-        } else if constexpr (INFL >= 3) {
+        if constexpr (INFL >= 3) {
             if (ahead >= 3) wait_vm<3 * GPC>();
             else if (ahead == 2) wait_vm<2 * GPC>();
             else if (ahead == 1) wait_vm<GPC>();
@@ -193,35 +182,26 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm16_kernel(RowGemmAr
         } else {
             wait_vm<0>();
         }
-        if constexpr (!(XP & 8)) block_barrier();
+        block_barrier();
         const char* base = smem + (kc % S) * STAGE;
 #pragma unroll
         for (int kk = 0; kk < BK / 16; ++kk) {
             const int c = kk * 2 + lh;
             bf16x8 af[MT], bfr[NT];
-            if constexpr (XP & 4) {  // operands from registers only (no LDS traffic)
 #pragma unroll
-                for (int mt = 0; mt < MT; ++mt) af[mt] = xa;
+            for (int mt = 0; mt < MT; ++mt)
+                af[mt] = *(const bf16x8*)(base + aro[mt] + ((c ^ afx[mt]) << 4));
 #pragma unroll
-                for (int nt = 0; nt < NT; ++nt) bfr[nt] = xa;
-            } else {
-#pragma unroll
-                for (int mt = 0; mt < MT; ++mt)
-                    af[mt] = *(const bf16x8*)(base + aro[mt] + ((c ^ afx[mt]) << 4));
-#pragma unroll
-                for (int nt = 0; nt < NT; ++nt)
-                    bfr[nt] = *(const bf16x8*)(base + bro[nt] + ((c ^ bfx[nt]) << 4));
-            }
+            for (int nt = 0; nt < NT; ++nt)
+                bfr[nt] = *(const bf16x8*)(base + bro[nt] + ((c ^ bfx[nt]) << 4));
 #pragma unroll
             for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
                 for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma32_bf16(af[mt], bfr[nt], acc[mt][nt]);
         }
-        if constexpr (!(XP & 8)) {
-            // this stage's ds_reads must have returned before any wave restages it
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            block_barrier();
-        }
+        // this stage's ds_reads must have returned before any wave restages it
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        block_barrier();
     }
     row_epilogue<EMODE, BM, BN, WM, WN, true>(p, acc, m0, n0, tile_m, wm, wn, lane, tid, (float*)smem);
 }
@@ -245,26 +225,17 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm16_kernel(RowGemmAr
 // ------------------------------------------------------------------------------------
 // BM x BN block tiles: 256 x 256 (tile 19) and 512 x 128 (tile 20, the 128-output layers of
 // config 4's level 0: 8 waves of 128 x 64 either way).
-// SCHED (r05, option rg16_sched; bit-identical): 0 = r04; 1 = waves 4..7 (each sharing a SIMD
-// with wave w - 4) run the stage's last tap (dx = 2) after the next barrier from fragments held
-// in registers, so that their matrix work opens each segment while their partner waits for its
-// first fragments (MI355X_MICROARCH.md "two waves per SIMD" item 9); 2 = 1 with the next
-// stage's DMA issued after the first tap's fragment reads
-// SCHED 8 (r05): 0 on 16x16x32 MFMAs (9 / 10 = 1 / 2 spill 22-28 VGPRs, not built) -- per tap ONE k-step of 32 channels, a wave's
-// 128 x 64 tile as 8 x 4 blocks of 16 x 16 (rows via m16_row, acc16_to32 before the epilogue);
-// the 16-B chunk swizzle becomes c ^ ((r >> 1) & 2), conflict-free for that read pattern (the
-// ds_read_b128 lane groups take two chunks of 16 consecutive rows; kernels_gemm_x3.hip
-// x3r3_body16).  Same FLOPs, same LDS bytes; the sums run 32 products per MFMA step.
-template <int EMODE, int BM, int BN, int SCHED = 0>
+// (r05, removed in r06: waves 4..7 running each stage's last tap after the next barrier, with
+// and without the next DMA behind the first tap's reads; the same kernel on 16x16x32 MFMAs:
+// +1 % kernel, -0.4 % step, profiles/r05_1tap16_ab.txt)
+template <int EMODE, int BM, int BN>
 __global__ __launch_bounds__(512, 1) void rowgemm16_row3_kernel(RowGemmArgs p) {
-    constexpr bool M16 = SCHED >= 8;
-    constexpr int SC = SCHED & 7;
     constexpr int WM = 128, WN = 64, BK = 32, WAVES_N = BN / WN;
     constexpr int WAVES = (BM / WM) * WAVES_N;
     static_assert(WAVES == 8, "512 threads");
     constexpr int MT = WM / 32, NT = WN / 32;
     constexpr int RB = 2 * BK, LPR = RB / 16, RPI = 64 / LPR;  // 64-B rows, 16 rows / piece
-    auto swz = [](int r) { return M16 ? (r >> 1) & 2 : (r >> 2) & 3; };
+    auto swz = [](int r) { return (r >> 2) & 3; };
     constexpr int AR = (BM / 16) * 18;        // halo rows held (W = 16: BM / 16 rows x 18)
     constexpr int AI = (AR / RPI + WAVES - 1) / WAVES;  // A pieces per wave (w, w + 8, ...)
     constexpr int BR = 3 * BN;                // B rows: taps dx = 0..2 x BN outputs
@@ -331,100 +302,6 @@ __global__ __launch_bounds__(512, 1) void rowgemm16_row3_kernel(RowGemmArgs p) {
 
     f32x16 acc[MT][NT];
     const int ns = 3 * CC;
-    if constexpr (M16) {
-        f32x4 a16[MT][NT][2][2];
-#pragma unroll
-        for (int i = 0; i < MT; ++i)
-#pragma unroll
-            for (int j = 0; j < NT; ++j)
-#pragma unroll
-                for (int b = 0; b < 4; ++b)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) a16[i][j][b >> 1][b & 1][r] = 0.f;
-        const int ks = lane >> 4, rs = lane & 15, rp = m16_row(rs);
-        int ahb[MT][2], bro[NT][2], bfx[NT][2];
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-            for (int bm = 0; bm < 2; ++bm) {
-                const int mo = wm * WM + mt * 32 + bm * 16 + rp;
-                const int r = mo / SEG;
-                ahb[mt][bm] = r * HW + (mo - r * SEG);
-            }
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-            for (int bn = 0; bn < 2; ++bn) {
-                const int r = wn * WN + nt * 32 + bn * 16 + rs;
-                bro[nt][bn] = (AR + r) * RB;
-                bfx[nt][bn] = swz(r);
-            }
-        issue(0);
-        auto run16 = [&](auto LAGC) {
-            constexpr bool LAG = decltype(LAGC)::value;
-            bf16x8 ha[MT][2], hb[NT][2];  // LAG: the previous stage's dx = 2 fragments
-            auto mm = [&](const bf16x8 (&af)[MT][2], const bf16x8 (&bfr)[NT][2]) {
-#pragma unroll
-                for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-                    for (int bm = 0; bm < 2; ++bm)
-#pragma unroll
-                        for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-                            for (int bn = 0; bn < 2; ++bn)
-                                a16[mt][nt][bm][bn] = mfma16_bf16(af[mt][bm], bfr[nt][bn], a16[mt][nt][bm][bn]);
-            };
-            for (int s = 0; s < ns; ++s) {
-                wait_vm<0>();
-                block_barrier();
-                if (SC != 2 && s + 1 < ns) issue(s + 1);
-                if constexpr (LAG) {
-                    if (s > 0) mm(ha, hb);
-                }
-                const char* base = smem + (s & 1) * STAGE;
-#pragma unroll
-                for (int dx = 0; dx < 3; ++dx) {
-                    bf16x8 af[MT][2], bfr[NT][2];
-#pragma unroll
-                    for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-                        for (int bm = 0; bm < 2; ++bm) {
-                            const int h = ahb[mt][bm] + dx;
-                            af[mt][bm] = *(const bf16x8*)(base + h * RB + ((ks ^ swz(h)) << 4));
-                        }
-#pragma unroll
-                    for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-                        for (int bn = 0; bn < 2; ++bn)
-                            bfr[nt][bn] = *(const bf16x8*)(base + bro[nt][bn] + dx * BN * RB + ((ks ^ bfx[nt][bn]) << 4));
-                    if (SC == 2 && dx == 0 && s + 1 < ns) issue(s + 1);
-                    if (LAG && dx == 2) {
-#pragma unroll
-                        for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-                            for (int bm = 0; bm < 2; ++bm) ha[mt][bm] = af[mt][bm];
-#pragma unroll
-                        for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-                            for (int bn = 0; bn < 2; ++bn) hb[nt][bn] = bfr[nt][bn];
-                    } else {
-                        mm(af, bfr);
-                    }
-                }
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            }
-            if constexpr (LAG) mm(ha, hb);
-        };
-        if (SC != 0 && wave >= 4) run16(std::true_type{});
-        else run16(std::false_type{});
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-            for (int nt = 0; nt < NT; ++nt) acc16_to32(a16[mt][nt], acc[mt][nt], lane);
-        block_barrier();
-        row_epilogue<EMODE, BM, BN, WM, WN, true>(p, acc, m0, n0, tile_m, wm, wn, lane, tid, (float*)smem);
-        return;
-    }
 #pragma unroll
     for (int i = 0; i < MT; ++i)
 #pragma unroll
@@ -447,83 +324,47 @@ __global__ __launch_bounds__(512, 1) void rowgemm16_row3_kernel(RowGemmArgs p) {
     }
 
     issue(0);
-    auto run = [&](auto LAGC) {
-        constexpr bool LAG = decltype(LAGC)::value;
-        bf16x8 ha[BK / 16][MT], hb[BK / 16][NT];  // LAG: the previous stage's dx = 2 fragments
-        auto mm = [&](const bf16x8 (&af)[MT], const bf16x8 (&bfr)[NT]) {
+    for (int s = 0; s < ns; ++s) {
+        // one barrier per stage: wait for stage s, barrier (every wave's DMA landed, every wave
+        // done reading stage s - 1), then restage s - 1's buffer with s + 1.  (r04: issuing
+        // before the wait and a second barrier after the MFMAs gave the same bits, 3 % slower.)
+        wait_vm<0>();
+        block_barrier();
+        if (s + 1 < ns) issue(s + 1);
+        const char* base = smem + (s & 1) * STAGE;
 #pragma unroll
-            for (int mt = 0; mt < MT; ++mt)
+        for (int dx = 0; dx < 3; ++dx)
 #pragma unroll
-                for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma32_bf16(af[mt], bfr[nt], acc[mt][nt]);
-        };
-        for (int s = 0; s < ns; ++s) {
-            // one barrier per stage: wait for stage s, barrier (every wave's DMA landed, every
-            // wave done reading stage s - 1), then restage s - 1's buffer with s + 1.  (r04:
-            // issuing before the wait and a second barrier after the MFMAs gave the same bits,
-            // 3 % slower.)
-            wait_vm<0>();
-            block_barrier();
-            if (SC != 2 && s + 1 < ns) issue(s + 1);
-            if constexpr (LAG) {
-                if (s > 0) {
+            for (int kk = 0; kk < BK / 16; ++kk) {
+                const int c = kk * 2 + lh;
+                bf16x8 af[MT], bfr[NT];
 #pragma unroll
-                    for (int kk = 0; kk < BK / 16; ++kk) mm(ha[kk], hb[kk]);
+                for (int mt = 0; mt < MT; ++mt) {
+                    const int h = ahb[mt] + dx;
+                    af[mt] = *(const bf16x8*)(base + h * RB + ((c ^ swz(h)) << 4));
                 }
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt)
+                    bfr[nt] = *(const bf16x8*)(base + bro[nt] + dx * BN * RB + ((c ^ bfx[nt]) << 4));
+#pragma unroll
+                for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                    for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma32_bf16(af[mt], bfr[nt], acc[mt][nt]);
             }
-            const char* base = smem + (s & 1) * STAGE;
-#pragma unroll
-            for (int dx = 0; dx < 3; ++dx)
-#pragma unroll
-                for (int kk = 0; kk < BK / 16; ++kk) {
-                    const int c = kk * 2 + lh;
-                    bf16x8 af[MT], bfr[NT];
-#pragma unroll
-                    for (int mt = 0; mt < MT; ++mt) {
-                        const int h = ahb[mt] + dx;
-                        af[mt] = *(const bf16x8*)(base + h * RB + ((c ^ swz(h)) << 4));
-                    }
-#pragma unroll
-                    for (int nt = 0; nt < NT; ++nt)
-                        bfr[nt] = *(const bf16x8*)(base + bro[nt] + dx * BN * RB + ((c ^ bfx[nt]) << 4));
-                    if (SC == 2 && dx == 0 && kk == 0 && s + 1 < ns) issue(s + 1);
-                    if (LAG && dx == 2) {
-#pragma unroll
-                        for (int mt = 0; mt < MT; ++mt) ha[kk][mt] = af[mt];
-#pragma unroll
-                        for (int nt = 0; nt < NT; ++nt) hb[kk][nt] = bfr[nt];
-                    } else {
-                        mm(af, bfr);
-                    }
-                }
-            // this stage's ds_reads must have returned before any wave restages it
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        }
-        if constexpr (LAG) {
-#pragma unroll
-            for (int kk = 0; kk < BK / 16; ++kk) mm(ha[kk], hb[kk]);
-        }
-    };
-    if (SC != 0 && wave >= 4) run(std::true_type{});
-    else run(std::false_type{});
+        // this stage's ds_reads must have returned before any wave restages it
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
     block_barrier();  // the epilogue reuses the stage memory
     row_epilogue<EMODE, BM, BN, WM, WN, true>(p, acc, m0, n0, tile_m, wm, wn, lane, tid, (float*)smem);
 }
 
 template <int EMODE, int BM, int BN>
-static int rg16r3_go(const RowGemmArgs& a, hipStream_t s, int sched) {
+static int rg16r3_go(const RowGemmArgs& a, hipStream_t s) {
     // BM % W == 0 or W % BM == 0 keeps a tile on whole rows / row segments; W >= 16 bounds the halo
     if (a.amode != G_CONV3 || a.N % BN || a.C % 32 || a.K != 9 * a.C) return -1;
     if (a.W < 16 || (BM % a.W && a.W % BM)) return -1;
     const dim3 grid(((a.M + BM - 1) / BM) * (a.N / BN));
-    if (sched == 1)
-        hipLaunchKernelGGL((rowgemm16_row3_kernel<EMODE, BM, BN, 1>), grid, dim3(512), 0, s, a);
-    else if (sched == 2)
-        hipLaunchKernelGGL((rowgemm16_row3_kernel<EMODE, BM, BN, 2>), grid, dim3(512), 0, s, a);
-    else if (sched == 8)
-        hipLaunchKernelGGL((rowgemm16_row3_kernel<EMODE, BM, BN, 8>), grid, dim3(512), 0, s, a);
-
-    else
-        hipLaunchKernelGGL((rowgemm16_row3_kernel<EMODE, BM, BN>), grid, dim3(512), 0, s, a);
+    hipLaunchKernelGGL((rowgemm16_row3_kernel<EMODE, BM, BN>), grid, dim3(512), 0, s, a);
     return (int)hipGetLastError();
 }
 
@@ -536,17 +377,17 @@ using T16_4 = Tile16<256, 256, 128, 64, 2, 1>;
 using T16_6 = Tile16<512, 128, 128, 64, 2, 1>;
 #define ROWGEMM16_TILES(X) X(0, T16_0) X(2, T16_2) X(4, T16_4) X(6, T16_6)
 
-template <int AMODE, int EMODE, class T, int XP = 0>
+template <int AMODE, int EMODE, class T>
 static int rg16_go(const RowGemmArgs& a, hipStream_t s) {
     if (a.N % T::BN || a.C % T::BK || a.K % T::BK) return -1;
     if (EMODE == E_CONVT && (a.cout % T::BN)) return -1;
     const dim3 grid(((a.M + T::BM - 1) / T::BM) * (a.N / T::BN));
-    hipLaunchKernelGGL((rowgemm16_kernel<AMODE, EMODE, T, XP>), grid, dim3(T::THREADS), 0, s, a);
+    hipLaunchKernelGGL((rowgemm16_kernel<AMODE, EMODE, T>), grid, dim3(T::THREADS), 0, s, a);
     return (int)hipGetLastError();
 }
 
 template <int AMODE, int EMODE>
-static int rg16_tile(const RowGemmArgs& a0, int tile, hipStream_t s, int sched) {
+static int rg16_tile(const RowGemmArgs& a0, int tile, hipStream_t s) {
     RowGemmArgs a = a0;
     if (a.tgm < 0) {  // tile order: the group size for this tile's grid (two blocks per CU on tile 0)
         int bm = 0, bn = 0;
@@ -555,7 +396,7 @@ static int rg16_tile(const RowGemmArgs& a0, int tile, hipStream_t s, int sched) 
     }
     if (tile == 19 || tile == 20) {
         if constexpr (AMODE == G_CONV3)
-            return tile == 19 ? rg16r3_go<EMODE, 256, 256>(a, s, sched) : rg16r3_go<EMODE, 512, 128>(a, s, sched);
+            return tile == 19 ? rg16r3_go<EMODE, 256, 256>(a, s) : rg16r3_go<EMODE, 512, 128>(a, s);
         return -1;
     }
 #define RG16_CASE(id, T) \
@@ -1256,25 +1097,16 @@ int rowgemm16_tile_dims(int tile, int* bm, int* bn, int* stages) {
 
 // The combinations of the BN -> ReLU network (models/mod.py): conv forward (E_STATS),
 // conv dgrad (E_STORE / E_STORE_BN), ConvT forward (E_CONVT), ConvT dgrad (G_UP2, E_STORE_BN).
-int launch_rowgemm16_xp(const RowGemmArgs& a, int xp, hipStream_t s) {
-    if (a.amode != G_CONV3 || a.emode != E_STATS) return -2;
-#define XPC(v) \
-    if (xp == v) return rg16_go<G_CONV3, E_STATS, T16_4, v>(a, s);
-    XPC(1) XPC(2) XPC(3) XPC(4) XPC(7) XPC(8) XPC(12) XPC(15)
-#undef XPC
-    return -2;
-}
-
-int launch_rowgemm16(const RowGemmArgs& a, int tile, hipStream_t s, int sched) {
+int launch_rowgemm16(const RowGemmArgs& a, int tile, hipStream_t s) {
     if (a.M < 1 || a.K != gather_taps(a.amode) * a.C || !a.a16 || !a.bt16 || !a.zero16) return -1;
     if (a.ascale || a.acoef || a.arelu) return -1;  // operands arrive prepared (k_to_bf16)
     if ((a.emode == E_STORE_BN) != (a.ey != nullptr)) return -1;
     if ((a.escale != nullptr) != (a.eshift != nullptr)) return -1;
-    if (a.amode == G_CONV3 && a.emode == E_STATS) return rg16_tile<G_CONV3, E_STATS>(a, tile, s, sched);
-    if (a.amode == G_CONV3 && a.emode == E_STORE) return rg16_tile<G_CONV3, E_STORE>(a, tile, s, sched);
-    if (a.amode == G_CONV3 && a.emode == E_STORE_BN) return rg16_tile<G_CONV3, E_STORE_BN>(a, tile, s, sched);
-    if (a.amode == G_IDENT && a.emode == E_CONVT) return rg16_tile<G_IDENT, E_CONVT>(a, tile, s, sched);
-    if (a.amode == G_UP2 && a.emode == E_STORE_BN) return rg16_tile<G_UP2, E_STORE_BN>(a, tile, s, sched);
+    if (a.amode == G_CONV3 && a.emode == E_STATS) return rg16_tile<G_CONV3, E_STATS>(a, tile, s);
+    if (a.amode == G_CONV3 && a.emode == E_STORE) return rg16_tile<G_CONV3, E_STORE>(a, tile, s);
+    if (a.amode == G_CONV3 && a.emode == E_STORE_BN) return rg16_tile<G_CONV3, E_STORE_BN>(a, tile, s);
+    if (a.amode == G_IDENT && a.emode == E_CONVT) return rg16_tile<G_IDENT, E_CONVT>(a, tile, s);
+    if (a.amode == G_UP2 && a.emode == E_STORE_BN) return rg16_tile<G_UP2, E_STORE_BN>(a, tile, s);
     return -1;
 }
 

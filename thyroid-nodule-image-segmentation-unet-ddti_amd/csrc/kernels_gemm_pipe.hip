@@ -301,9 +301,9 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_pipe_kernel(RowGem
     }
 }
 
-using PipeTile0 = PipeTile<128, 128, 64, 64, 2>;  // 4 waves of 64x64, 74 KB LDS
-using PipeTile1 = PipeTile<128, 64, 64, 32, 2>;   // 4 waves of 64x32 (N = 64 outputs)
-using PipeTile2 = PipeTile<128, 128, 64, 64, 2, 2>;  // tile 0, loads two chunks ahead
+// 4 waves of 64x64 (74 KB LDS) / 4 waves of 64x32 (N = 64 outputs), loading two chunks ahead
+// (r02-r03 tiles 0 / 1 loaded one chunk ahead: 1-2 % slower, removed in r06)
+using PipeTile2 = PipeTile<128, 128, 64, 64, 2, 2>;
 using PipeTile3 = PipeTile<128, 64, 64, 32, 2, 2>;
 // N = 64 at three blocks per CU (48 KB of LDS each): a third resident block to overlap the
 // epilogues of the short-K (576) level-0 GEMMs; 5 loads two chunks ahead
@@ -326,8 +326,6 @@ static int pipe_go(const RowGemmArgs& a, hipStream_t s) {
 
 template <int AMODE, int AOP, int EMODE>
 static int pipe_tile(const RowGemmArgs& a, int tile, hipStream_t s) {
-    if (tile == 0) return pipe_go<AMODE, AOP, EMODE, PipeTile0>(a, s);
-    if (tile == 1) return pipe_go<AMODE, AOP, EMODE, PipeTile1>(a, s);
     if (tile == 2) return pipe_go<AMODE, AOP, EMODE, PipeTile2>(a, s);
     if (tile == 3) return pipe_go<AMODE, AOP, EMODE, PipeTile3>(a, s);
     if (tile == 4) return pipe_go<AMODE, AOP, EMODE, PipeTile4>(a, s);
@@ -347,8 +345,8 @@ int rowgemm_pipe_ok(const RowGemmArgs& a) {
     return 1;
 }
 
-// tile: 0 = 128x128, 1 = 128x64, 2 / 3 = those loading two chunks ahead, 4 / 5 = 128x64 at
-// three blocks per CU
+// tile: 2 = 128x128, 3 = 128x64 (loading two chunks ahead), 4 / 5 = 128x64 at three blocks per
+// CU (one / two chunks ahead)
 int launch_rowgemm_pipe(const RowGemmArgs& a, int tile, hipStream_t s) {
     if (!rowgemm_pipe_ok(a) || a.M < 1 || a.K != gather_taps(a.amode) * a.C) return -1;
     const bool aff = a.ascale != nullptr;

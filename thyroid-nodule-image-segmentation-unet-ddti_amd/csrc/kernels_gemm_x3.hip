@@ -97,12 +97,7 @@ struct TileX3 {
     static constexpr int THREADS = 64 * WAVES;
 };
 
-// XP: speed-of-light ablations for tools/x3_probe.hip only (results are garbage): bit 0 drops
-// the A DMA, 1 the B DMA, 2 the LDS fragment reads, 3 the loop's waits and barriers; the
-// library instantiates XP = 0.
-// M16 (r05): 16x16x32 MFMAs, one k-step of 32 channels per chunk (as x3r3_body16; swizzle
-// c ^ ((r >> 1) & 2), rows via m16_row, acc16_to32 before the epilogue)
-template <int AMODE, int EMODE, class T, int XP = 0, bool M16 = false>
+template <int AMODE, int EMODE, class T>
 __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_x3_kernel(RowGemmArgs p) {
     constexpr int BM = T::BM, BN = T::BN, WM = T::WM, WN = T::WN, S = T::S, BK = T::BK;
     constexpr int WAVES = T::WAVES, WAVES_N = BN / WN;
@@ -119,8 +114,7 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_x3_kernel(RowGemmA
     constexpr int RED = 2 * (BM / 64) * BN * 8;
     constexpr int SMEM = STAGE * S > RED ? STAGE * S : RED;
     __shared__ __attribute__((aligned(1024))) char smem[SMEM];
-    auto swz = [](int r) { return M16 ? (r >> 1) & 2 : (r >> 2) & 3; };
-    static_assert(!M16 || (T::SA && XP == 0), "16x16x32: split accumulators, no ablations");
+    auto swz = [](int r) { return (r >> 2) & 3; };
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -169,19 +163,16 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_x3_kernel(RowGemmA
         char* base = smem + st * STAGE;
 #pragma unroll
         for (int j = 0; j < AI; ++j) {
-            if (XP & 1) continue;
             bool valid;
             const int src = gather_src<AMODE>(tap, am[j], aq[j], H, W, valid);
             const uint16_t* g = (valid && aok[j]) ? a16 + (size_t)src * rowa + c0 * 3 + ace[j] : zero;
             x3_dma16(g, base + (j * WAVES + wave) * 1024);
         }
 #pragma unroll
-        for (int j = 0; j < BI; ++j) {
-            if (XP & 2) continue;
+        for (int j = 0; j < BI; ++j)
             x3_dma16(bok[j] ? bsrc[j] + k0 * 3 : zero, base + AREG + (j * WAVES + wave) * 1024);
-        }
     };
-    constexpr int GPCX = ((XP & 1) ? 0 : AI) + ((XP & 2) ? 0 : BI);  // DMA pieces actually issued
+    constexpr int GPC = AI + BI;  // DMA pieces per chunk
 
     constexpr int SA = T::SA;
     f32x16 acc[MT][NT], acl[SA ? MT : 1][SA ? NT : 1];
@@ -210,112 +201,42 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_x3_kernel(RowGemmA
         bfx[nt] = swz(r);
     }
 
-    // M16: [mt][nt][bm][bn] 16x16 blocks, A rows / B columns of lane slot rs
-    f32x4 h16[M16 ? MT : 1][M16 ? NT : 1][2][2], l16[M16 ? MT : 1][M16 ? NT : 1][2][2];
-    int aro16[M16 ? MT : 1][2], afx16[M16 ? MT : 1][2], bro16[M16 ? NT : 1][2], bfx16[M16 ? NT : 1][2];
-    const int ks = lane >> 4;
-    if constexpr (M16) {
-        const int rs = lane & 15;
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-            for (int b = 0; b < 2; ++b) {
-                const int ra = wm * WM + mt * 32 + b * 16 + m16_row(rs);
-                aro16[mt][b] = ra * RB;
-                afx16[mt][b] = swz(ra);
-#pragma unroll
-                for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-                    for (int bn = 0; bn < 2; ++bn)
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) h16[mt][nt][b][bn][r] = l16[mt][nt][b][bn][r] = 0.f;
-            }
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-            for (int b = 0; b < 2; ++b) {
-                const int rb = wn * WN + nt * 32 + b * 16 + rs;
-                bro16[nt][b] = AREG + rb * RB;
-                bfx16[nt][b] = swz(rb);
-            }
-    }
-
     const int nk = K / BK;
-    bf16x8 xa;  // XP & 4: a register operand
-#pragma unroll
-    for (int j = 0; j < 8; ++j) xa[j] = (__bf16)(float)(lane + j);
 #pragma unroll
     for (int s = 0; s < DIST; ++s)
         if (s < nk) issue(s, s);
     for (int kc = 0; kc < nk; ++kc) {
         if (kc + DIST < nk) issue(kc + DIST, (kc + DIST) % S);
         const int ahead = min(DIST, nk - 1 - kc);
-        if constexpr (XP & 8) {
-        } else if constexpr (DIST >= 3) {
-            if (ahead >= 3) x3_wait_vm<3 * GPCX>();
-            else if (ahead == 2) x3_wait_vm<2 * GPCX>();
-            else if (ahead == 1) x3_wait_vm<GPCX>();
+        if constexpr (DIST >= 3) {
+            if (ahead >= 3) x3_wait_vm<3 * GPC>();
+            else if (ahead == 2) x3_wait_vm<2 * GPC>();
+            else if (ahead == 1) x3_wait_vm<GPC>();
             else x3_wait_vm<0>();
         } else if constexpr (DIST == 2) {
-            if (ahead >= 2) x3_wait_vm<2 * GPCX>();
-            else if (ahead == 1) x3_wait_vm<GPCX>();
+            if (ahead >= 2) x3_wait_vm<2 * GPC>();
+            else if (ahead == 1) x3_wait_vm<GPC>();
             else x3_wait_vm<0>();
         } else {
-            if (ahead >= 1) x3_wait_vm<GPCX>();
+            if (ahead >= 1) x3_wait_vm<GPC>();
             else x3_wait_vm<0>();
         }
-        if constexpr (!(XP & 8)) x3_barrier();
+        x3_barrier();
         const char* base = smem + (kc % S) * STAGE;
-        if constexpr (M16) {
-            bf16x8 af[MT][2][3], bfr[NT][2][3];
+#pragma unroll
+        for (int kk = 0; kk < BK / 16; ++kk) {
+            const int c = kk * 2 + lh;
+            bf16x8 af[MT][3], bfr[NT][3];
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                for (int q = 0; q < 3; ++q)
+                    af[mt][q] = *(const bf16x8*)(base + aro[mt] + q * 64 + ((c ^ afx[mt]) << 4));
 #pragma unroll
             for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
-                for (int b = 0; b < 2; ++b)
-#pragma unroll
-                    for (int q = 0; q < 3; ++q)
-                        bfr[nt][b][q] = *(const bf16x8*)(base + bro16[nt][b] + q * 64 + ((ks ^ bfx16[nt][b]) << 4));
-#pragma unroll
-            for (int mt = 0; mt < MT; ++mt) {
-#pragma unroll
-                for (int b = 0; b < 2; ++b)
-#pragma unroll
-                    for (int q = 0; q < 3; ++q)
-                        af[mt][b][q] = *(const bf16x8*)(base + aro16[mt][b] + q * 64 + ((ks ^ afx16[mt][b]) << 4));
-#pragma unroll
-                for (int b = 0; b < 2; ++b)
-#pragma unroll
-                    for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-                        for (int bn = 0; bn < 2; ++bn)
-                            mfma_x3s16(af[mt][b], bfr[nt][bn], h16[mt][nt][b][bn], l16[mt][nt][b][bn]);
-            }
-        }
-#pragma unroll
-        for (int kk = 0; kk < (M16 ? 0 : BK / 16); ++kk) {
-            const int c = kk * 2 + lh;
-            bf16x8 af[MT][3], bfr[NT][3];
-            if constexpr (XP & 4) {  // operands from registers only (no LDS traffic)
-#pragma unroll
-                for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-                    for (int q = 0; q < 3; ++q) af[mt][q] = xa;
-#pragma unroll
-                for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-                    for (int q = 0; q < 3; ++q) bfr[nt][q] = xa;
-            } else {
-#pragma unroll
-                for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-                    for (int q = 0; q < 3; ++q)
-                        af[mt][q] = *(const bf16x8*)(base + aro[mt] + q * 64 + ((c ^ afx[mt]) << 4));
-#pragma unroll
-                for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-                    for (int q = 0; q < 3; ++q)
-                        bfr[nt][q] = *(const bf16x8*)(base + bro[nt] + q * 64 + ((c ^ bfx[nt]) << 4));
-            }
+                for (int q = 0; q < 3; ++q)
+                    bfr[nt][q] = *(const bf16x8*)(base + bro[nt] + q * 64 + ((c ^ bfx[nt]) << 4));
 #pragma unroll
             for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
@@ -324,23 +245,10 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_x3_kernel(RowGemmA
                     else acc[mt][nt] = mfma_x3(af[mt], bfr[nt], acc[mt][nt]);
                 }
         }
-        if constexpr (!(XP & 8)) {
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            x3_barrier();
-        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        x3_barrier();
     }
-    if constexpr (XP & 8) x3_wait_vm<0>();
-    if constexpr (M16) {
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-            for (int nt = 0; nt < NT; ++nt) {
-                f32x4 a[2][2];
-#pragma unroll
-                for (int b = 0; b < 4; ++b) a[b >> 1][b & 1] = h16[mt][nt][b >> 1][b & 1] + l16[mt][nt][b >> 1][b & 1];
-                acc16_to32(a, acc[mt][nt], lane);
-            }
-    } else if constexpr (SA) {
+    if constexpr (SA) {
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
@@ -371,184 +279,19 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void rowgemm_x3_kernel(RowGemmA
 // ------------------------------------------------------------------------------------
 // BN = 128 (8 waves of 64 x 64) or 64 (8 waves of 64 x 32, B pieces padded to 2 per wave).
 //
-// Schedule (r05, tools/x3_halo_exp.hip, profiles/r05_halo_sched.txt).  The eight waves pair up on
-// the four SIMDs (wave w and w + 4), and when both run the same program they reach the barrier,
-// the DMA issue (100-185 cycles per LDS-DMA piece inside a busy phase, MI355X_MICROARCH.md) and
-// the post-barrier fragment reads together, leaving the matrix pipe idle.  Template SCHED:
-//   LW   waves that issue the LDS-DMA: 8 (all, each its share) or 4 (waves 0..3 issue twice as
-//        many pieces; waves 4..7 never stall on a DMA issue)
-//   LAG  waves 4..7 run each sub-step's second k-step MFMAs after the next barrier, from
-//        fragments they read before it (held in registers): their pipe work starts while
-//        their partner waits for its first fragments
-//   LATE the DMA of the next sub-step is issued after the first k-step's fragment reads
+// Schedule (r05, profiles/r05_halo_sched.txt, r05_halo_m16.txt).  The eight waves pair up on the
+// four SIMDs (wave w and w + 4), and when both run the same program they reach the barrier, the
+// DMA issue (100-185 cycles per LDS-DMA piece inside a busy phase, MI355X_MICROARCH.md) and the
+// post-barrier fragment reads together, leaving the matrix pipe idle.  So:
+//   LAG  waves 4..7 run each sub-step's second 32-row half after the next barrier, from
+//        fragments they read before it (held in registers): their pipe work starts while their
+//        partner waits for its first fragments
+//   LATE the DMA of the next sub-step is issued after the first fragment reads
 // The next group's halo is spread over the current group's three sub-steps (AC pieces each).
-// Every schedule runs the same MFMAs in the same order per accumulator: bit-identical.
-template <int BM, int BN, int LW, bool ISSUER, bool LAG, bool LATE>
-__device__ __forceinline__ void x3r3_body(const RowGemmArgs& p, char* smem, int wave, int lane,
-                                          f32x16 (&acc)[2][BN / 64], f32x16 (&acl)[2][BN / 64],
-                                          int m0, int n0) {
-    constexpr int BK = 32, WM = 64, WN = BN / 2, WAVES_N = 2, WAVES = (BM / WM) * WAVES_N;
-    constexpr int MT = WM / 32, NT = WN / 32;
-    constexpr int RB = 192, AR = BM / 16 * 18;  // halo rows at W = 16: BM / 16 rows of 18
-    constexpr int AREG = ((AR * RB + 1024 * WAVES - 1) / (1024 * WAVES)) * WAVES * 1024;  // 56 / 28 KB
-    constexpr int BREG = ((BN * RB + 1024 * WAVES - 1) / (1024 * WAVES)) * WAVES * 1024;  // 24 / 16 / 12 KB
-    constexpr int AI = AREG / (1024 * LW), BI = BREG / (1024 * LW);  // pieces per issuing wave
-    constexpr int AC = (AI + 2) / 3;                                  // halo pieces per sub-step
-    auto swz = [](int r) { return (r >> 2) & 3; };
-    const int wm = wave / WAVES_N, wn = wave % WAVES_N;
-    const int H = p.H, W = p.W, C = p.C, K = p.K;
-    const int SEG = W < BM ? W : BM, HW = SEG + 2;
-    const int AROWS = (BM / SEG) * HW;
-    const size_t rowa = 3 * (size_t)p.lda, rowb = 3 * (size_t)K;
-    // A loader: lane of piece j fills halo bytes (j LW + wave) KB + 16 lane: halo row h, 16-B
-    // slot w / 16 of its 192 B; pixel of h at dy = 1 (-1: padding column / past the halo)
-    int acen[ISSUER ? AI : 1], ayr[ISSUER ? AI : 1], ace[ISSUER ? AI : 1];
-    const uint16_t* bsrc[ISSUER ? BI : 1];
-    bool bok[ISSUER ? BI : 1];
-    if constexpr (ISSUER) {
-#pragma unroll
-        for (int j = 0; j < AI; ++j) {
-            const int o = ((j * LW + wave) * 64 + lane) * 16;
-            const int h = o / RB, w = o - h * RB;
-            const int r = h / HW, xl = h - r * HW - 1;
-            const int mrow = m0 + r * SEG;
-            bool ok = h < AROWS && mrow < p.M;
-            const Pix q = decode(ok ? mrow : 0, H, W);
-            ok = ok && q.x + xl >= 0 && q.x + xl < W;
-            acen[j] = ok ? mrow + xl : -1;
-            ayr[j] = q.y;
-            ace[j] = (w >> 6) * 32 + ((((w >> 4) & 3) ^ swz(h)) << 3);
-        }
-#pragma unroll
-        for (int j = 0; j < BI; ++j) {
-            const int o = ((j * LW + wave) * 64 + lane) * 16;
-            const int r = o / RB, w = o - r * RB;
-            bok[j] = r < BN;
-            bsrc[j] = p.bt16 + (size_t)(n0 + (bok[j] ? r : 0)) * rowb + (w >> 6) * 32 +
-                      ((((w >> 4) & 3) ^ swz(r)) << 3);
-        }
-    }
-    const uint16_t* zero = (const uint16_t*)p.zero16;
-    const uint16_t* a16 = p.a16 + (size_t)p.aoff * 3;
-    const int CC = C / BK;  // channel groups per tap
-    const int NG = 3 * CC;  // halo groups (dy, channel group)
-    const int ns = 9 * CC;  // sub-steps (dy, channel group, dx)
-    // halo pieces [j0, j1) of group g into buffer g & 1
-    auto issue_a = [&](int g, int j0, int j1) {
-        const int dy = g / CC, c0 = (g - dy * CC) * BK;
-        char* base = smem + (g & 1) * AREG;
-#pragma unroll
-        for (int j = 0; j < AI; ++j) {
-            if (j < j0 || j >= j1) continue;
-            const int yy = ayr[j] + dy - 1;
-            const bool valid = acen[j] >= 0 && yy >= 0 && yy < H;
-            const uint16_t* src =
-                valid ? a16 + (size_t)(acen[j] + (dy - 1) * W) * rowa + c0 * 3 + ace[j] : zero;
-            x3_dma16(src, base + (j * LW + wave) * 1024);
-        }
-    };
-    auto issue_b = [&](int s) {  // B rows of tap dy * 3 + dx, channel group, into slot s & 1
-        const int g = s / 3, dx = s - g * 3;
-        const int dy = g / CC, c0 = (g - dy * CC) * BK;
-        const int k0 = (dy * 3 + dx) * C + c0;
-        char* base = smem + 2 * AREG + (s & 1) * BREG;
-#pragma unroll
-        for (int j = 0; j < BI; ++j) x3_dma16(bok[j] ? bsrc[j] + k0 * 3 : zero, base + (j * LW + wave) * 1024);
-    };
-    // during sub-step s: B(s + 1), then the halo pieces [dx AC, (dx + 1) AC) of group g + 1 into
-    // the buffer group g - 1 read (free since the barrier that opened group g)
-    auto issue = [&](int s) {
-        const int g = s / 3, dx = s - g * 3;
-        if (s + 1 < ns) issue_b(s + 1);
-        if (g + 1 < NG) issue_a(g + 1, dx * AC, dx * AC + AC);
-    };
-    const int lh = lane >> 5, li = lane & 31;
-    int ahb[MT], bro[NT], bfx[NT];  // halo row of output pixel at dx = 0; B row offsets
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-        const int mo = wm * WM + mt * 32 + li;
-        const int r = mo / SEG;
-        ahb[mt] = r * HW + (mo - r * SEG);
-    }
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-        const int r = wn * WN + nt * 32 + li;
-        bro[nt] = r * RB;
-        bfx[nt] = swz(r);
-    }
-    bf16x8 ha[MT][3], hb[NT][3];  // LAG: the previous sub-step's second k-step fragments
-    if constexpr (ISSUER) {
-        issue_a(0, 0, AI);
-        issue_b(0);
-    }
-    for (int s = 0; s < ns; ++s) {
-        const int g = s / 3, dx = s - g * 3;
-        // one barrier per sub-step: the issuing waves wait for B(s) and, entering a group, the
-        // last halo pieces of g (the pieces of g + 1 issued during s - 1, younger than B(s), may
-        // stay in flight); the barrier then also means every wave finished reading s - 1, so
-        // slot (s + 1) & 1 and halo buffer (g + 1) & 1 are free
-        if constexpr (ISSUER) {
-            if (dx >= 1 && g + 1 < NG) x3_wait_vm<AC>();
-            else x3_wait_vm<0>();
-        }
-        x3_barrier();
-        if constexpr (ISSUER && !LATE) issue(s);
-        if constexpr (LAG) {
-            if (s > 0) {
-#pragma unroll
-                for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-                    for (int nt = 0; nt < NT; ++nt) mfma_x3s(ha[mt], hb[nt], acc[mt][nt], acl[mt][nt]);
-            }
-        }
-        const char* abase = smem + (g & 1) * AREG;
-        const char* bbase = smem + 2 * AREG + (s & 1) * BREG;
-#pragma unroll
-        for (int kk = 0; kk < BK / 16; ++kk) {
-            const int c = kk * 2 + lh;
-            bf16x8 af[MT][3], bfr[NT][3];
-#pragma unroll
-            for (int mt = 0; mt < MT; ++mt) {
-                const int h = ahb[mt] + dx;
-#pragma unroll
-                for (int q = 0; q < 3; ++q)
-                    af[mt][q] = *(const bf16x8*)(abase + h * RB + q * 64 + ((c ^ swz(h)) << 4));
-            }
-#pragma unroll
-            for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-                for (int q = 0; q < 3; ++q)
-                    bfr[nt][q] = *(const bf16x8*)(bbase + bro[nt] + q * 64 + ((c ^ bfx[nt]) << 4));
-            if constexpr (ISSUER && LATE) {
-                if (kk == 0) issue(s);
-            }
-            if (LAG && kk == 1) {
-#pragma unroll
-                for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-                    for (int q = 0; q < 3; ++q) ha[mt][q] = af[mt][q];
-#pragma unroll
-                for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-                    for (int q = 0; q < 3; ++q) hb[nt][q] = bfr[nt][q];
-            } else {
-#pragma unroll
-                for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-                    for (int nt = 0; nt < NT; ++nt) mfma_x3s(af[mt], bfr[nt], acc[mt][nt], acl[mt][nt]);
-            }
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    }
-    if constexpr (LAG) {
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-            for (int nt = 0; nt < NT; ++nt) mfma_x3s(ha[mt], hb[nt], acc[mt][nt], acl[mt][nt]);
-    }
-}
-
-// ------------------------------------------------------------------------------------
+// Same MFMAs in the same order per accumulator with or without them: bit-identical.
+// (r04-r05, measured and removed in r06: the 32x32x16 body of the same kernel, 5-18 % slower per
+// launch; waves 0..3 issuing every DMA; a quarter stagger; re-reading the deferred A half; the
+// loader state recomputed per piece; a 512 x 64 tile over 16-channel groups, 1.103 vs 1.032 ms.)
 // The same halo GEMM on v_mfma_f32_16x16x32_bf16 (r05).  Under load the chip holds a higher clock
 // on the 16x16x32 shape than on 32x32x16 at equal cycles per FLOP (MI355X_MICROARCH.md, DVFS
 // item 7); with this kernel's LDS traffic and DMA unchanged, swapping the shape alone measured
@@ -564,13 +307,7 @@ __device__ __forceinline__ void x3r3_body(const RowGemmArgs& p, char* smem, int 
 //   and this XOR puts them on 16 distinct bank quads for any r0.
 //   Stagger (LAG): waves 4..7 run the second 32-row half's MFMAs after the next barrier.
 // ------------------------------------------------------------------------------------
-// RA (schedule 11, not built: 52-53 spilled VGPRs): the staggered waves hold only the B
-// fragments and re-read the deferred A half from the halo after the barrier (intact while the
-// next sub-step is in the same halo group: only dx = 0, 1 defer)
-// RC (schedule 12): the loader state is recomputed per DMA piece (f32-reciprocal decode) instead
-// of being held in 17 registers per wave -- for the staggered waves, which hold fragments
-template <int BM, int BN, int LW, bool ISSUER, bool LAG, bool LATE, bool QL = false, bool RA = false,
-          bool RC = false>
+template <int BM, int BN, bool LAG>
 __device__ __forceinline__ void x3r3_body16(const RowGemmArgs& p, char* smem, int wave, int lane,
                                             f32x4 (&hi)[2][BN / 64][2][2], f32x4 (&lo)[2][BN / 64][2][2],
                                             int m0, int n0) {
@@ -579,7 +316,7 @@ __device__ __forceinline__ void x3r3_body16(const RowGemmArgs& p, char* smem, in
     constexpr int RB = 192, AR = BM / 16 * 18;
     constexpr int AREG = ((AR * RB + 1024 * WAVES - 1) / (1024 * WAVES)) * WAVES * 1024;
     constexpr int BREG = ((BN * RB + 1024 * WAVES - 1) / (1024 * WAVES)) * WAVES * 1024;
-    constexpr int AI = AREG / (1024 * LW), BI = BREG / (1024 * LW);
+    constexpr int AI = AREG / (1024 * WAVES), BI = BREG / (1024 * WAVES);  // pieces per wave
     constexpr int AC = (AI + 2) / 3;
     auto swz = [](int r) { return (r >> 1) & 2; };
     const int wm = wave / WAVES_N, wn = wave % WAVES_N;
@@ -589,31 +326,24 @@ __device__ __forceinline__ void x3r3_body16(const RowGemmArgs& p, char* smem, in
     const size_t rowa = 3 * (size_t)p.lda, rowb = 3 * (size_t)K;
     // loader state packed to 3 registers per piece pair (the staggered waves hold a second
     // fragment set): pixel index, y * 128 + element offset in the 192-B row, B element offset
-    constexpr bool KEEP = ISSUER && !RC;
-    int acen[KEEP ? AI : 1], apk[KEEP ? AI : 1], boff[KEEP ? BI : 1];
-    const float rHW = 1.f / (float)HW, rW = 1.f / (float)W, rH = 1.f / (float)H;
-    // piece j's A state: pixel at dy = 1 (-1: padding / past the halo), y * 128 + element offset
-    auto apiece = [&](int j, int& cen, int& pk) {
-        const int o = ((j * LW + wave) * 64 + lane) * 16;
+    int acen[AI], apk[AI], boff[BI];
+#pragma unroll
+    for (int j = 0; j < AI; ++j) {  // piece j's A state: pixel at dy = 1 (-1: padding / past the halo)
+        const int o = ((j * WAVES + wave) * 64 + lane) * 16;
         const int h = o / RB, w = o - h * RB;
-        const int r = RC ? (int)(((float)h + 0.5f) * rHW) : h / HW, xl = h - r * HW - 1;
+        const int r = h / HW, xl = h - r * HW - 1;
         const int mrow = m0 + r * SEG;
         bool ok = h < AROWS && mrow < p.M;
-        const Pix q = RC ? decode_fast(ok ? mrow : 0, H, W, rH, rW) : decode(ok ? mrow : 0, H, W);
+        const Pix q = decode(ok ? mrow : 0, H, W);
         ok = ok && q.x + xl >= 0 && q.x + xl < W;
-        cen = ok ? mrow + xl : -1;
-        pk = q.y * 128 + (w >> 6) * 32 + ((((w >> 4) & 3) ^ swz(h)) << 3);
-    };
-    auto bpiece = [&](int j) {
-        const int o = ((j * LW + wave) * 64 + lane) * 16;
+        acen[j] = ok ? mrow + xl : -1;
+        apk[j] = q.y * 128 + (w >> 6) * 32 + ((((w >> 4) & 3) ^ swz(h)) << 3);
+    }
+#pragma unroll
+    for (int j = 0; j < BI; ++j) {
+        const int o = ((j * WAVES + wave) * 64 + lane) * 16;
         const int r = o / RB, w = o - r * RB;
-        return r < BN ? (int)((n0 + r) * rowb) + (w >> 6) * 32 + ((((w >> 4) & 3) ^ swz(r)) << 3) : -1;
-    };
-    if constexpr (KEEP) {
-#pragma unroll
-        for (int j = 0; j < AI; ++j) apiece(j, acen[j], apk[j]);
-#pragma unroll
-        for (int j = 0; j < BI; ++j) boff[j] = bpiece(j);
+        boff[j] = r < BN ? (int)((n0 + r) * rowb) + (w >> 6) * 32 + ((((w >> 4) & 3) ^ swz(r)) << 3) : -1;
     }
     const uint16_t* zero = (const uint16_t*)p.zero16;
     const uint16_t* a16 = p.a16 + (size_t)p.aoff * 3;
@@ -626,14 +356,11 @@ __device__ __forceinline__ void x3r3_body16(const RowGemmArgs& p, char* smem, in
 #pragma unroll
         for (int j = 0; j < AI; ++j) {
             if (j < j0 || j >= j1) continue;
-            int cen, pk;
-            if constexpr (KEEP) cen = acen[j], pk = apk[j];
-            else apiece(j, cen, pk);
-            const int yy = (pk >> 7) + dy - 1;
-            const bool valid = cen >= 0 && yy >= 0 && yy < H;
+            const int yy = (apk[j] >> 7) + dy - 1;
+            const bool valid = acen[j] >= 0 && yy >= 0 && yy < H;
             const uint16_t* src =
-                valid ? a16 + (size_t)(cen + (dy - 1) * W) * rowa + c0 * 3 + (pk & 127) : zero;
-            x3_dma16(src, base + (j * LW + wave) * 1024);
+                valid ? a16 + (size_t)(acen[j] + (dy - 1) * W) * rowa + c0 * 3 + (apk[j] & 127) : zero;
+            x3_dma16(src, base + (j * WAVES + wave) * 1024);
         }
     };
     auto issue_b = [&](int s) {
@@ -642,11 +369,11 @@ __device__ __forceinline__ void x3r3_body16(const RowGemmArgs& p, char* smem, in
         const int k0 = (dy * 3 + dx) * C + c0;
         char* base = smem + 2 * AREG + (s & 1) * BREG;
 #pragma unroll
-        for (int j = 0; j < BI; ++j) {
-            const int bo = KEEP ? boff[j] : bpiece(j);
-            x3_dma16(bo >= 0 ? p.bt16 + bo + k0 * 3 : zero, base + (j * LW + wave) * 1024);
-        }
+        for (int j = 0; j < BI; ++j)
+            x3_dma16(boff[j] >= 0 ? p.bt16 + boff[j] + k0 * 3 : zero, base + (j * WAVES + wave) * 1024);
     };
+    // during sub-step s: B(s + 1), then the halo pieces [dx AC, (dx + 1) AC) of group g + 1 into
+    // the buffer group g - 1 read (free since the barrier that opened group g)
     auto issue = [&](int s) {
         const int g = s / 3, dx = s - g * 3;
         if (s + 1 < ns) issue_b(s + 1);
@@ -671,47 +398,32 @@ __device__ __forceinline__ void x3r3_body16(const RowGemmArgs& p, char* smem, in
             bro[nt][bn] = r * RB;
             bfx[nt][bn] = swz(r);
         }
-    // LAG: the previous sub-step's deferred fragments -- the second 32-row half (QL: only its
-    // last 32-column block, a quarter of the MFMAs and fewer held registers)
-    constexpr int HN = QL ? 1 : NT, N0 = NT - HN;
-    bf16x8 ha[2][3], hb[HN][2][3];
-    auto mma = [&](const bf16x8 (&af)[2][3], const bf16x8* bf, int mt, int nt0, int nt1) {
+    // LAG: the previous sub-step's deferred fragments (the second 32-row half)
+    bf16x8 ha[2][3], hb[NT][2][3];
+    auto mma = [&](const bf16x8 (&af)[2][3], const bf16x8* bf, int mt) {
 #pragma unroll
         for (int bm = 0; bm < 2; ++bm)
 #pragma unroll
-            for (int nt = nt0; nt < nt1; ++nt)
+            for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
                 for (int bn = 0; bn < 2; ++bn)
-                    mfma_x3s16(af[bm], *(const bf16x8(*)[3])(bf + ((nt - nt0) * 2 + bn) * 3),
-                               hi[mt][nt][bm][bn], lo[mt][nt][bm][bn]);
+                    mfma_x3s16(af[bm], *(const bf16x8(*)[3])(bf + (nt * 2 + bn) * 3), hi[mt][nt][bm][bn],
+                               lo[mt][nt][bm][bn]);
     };
-    if constexpr (ISSUER) {
-        issue_a(0, 0, AI);
-        issue_b(0);
-    }
+    issue_a(0, 0, AI);
+    issue_b(0);
     for (int s = 0; s < ns; ++s) {
         const int g = s / 3, dx = s - g * 3;
-        if constexpr (ISSUER) {
-            if (dx >= 1 && g + 1 < NG) x3_wait_vm<AC>();
-            else x3_wait_vm<0>();
-        }
+        // one barrier per sub-step: wait for B(s) and, entering a group, the last halo pieces of
+        // g (the pieces of g + 1 issued during s - 1, younger than B(s), may stay in flight); the
+        // barrier then also means every wave finished reading s - 1, so slot (s + 1) & 1 and
+        // halo buffer (g + 1) & 1 are free
+        if (dx >= 1 && g + 1 < NG) x3_wait_vm<AC>();
+        else x3_wait_vm<0>();
         x3_barrier();
-        if constexpr (ISSUER && !LATE) issue(s);
         const char* abase = smem + (g & 1) * AREG;
-        if constexpr (LAG && RA) {
-            if (dx > 0) {  // the previous sub-step (same group, tap dx - 1): its second A half
-                bf16x8 ap[2][3];
-#pragma unroll
-                for (int bm = 0; bm < 2; ++bm) {
-                    const int h = ahb[1][bm] + dx - 1;
-#pragma unroll
-                    for (int q = 0; q < 3; ++q) ap[bm][q] = *(const bf16x8*)(abase + h * RB + q * 64 + ((ks ^ swz(h)) << 4));
-                }
-                mma(ap, &hb[0][0][0], 1, N0, NT);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-        } else if constexpr (LAG) {
-            if (s > 0) mma(ha, &hb[0][0][0], 1, N0, NT);
+        if constexpr (LAG) {
+            if (s > 0) mma(ha, &hb[0][0][0], 1);
             // the held registers free before this sub-step's reads (256 VGPRs at two waves / SIMD)
             __builtin_amdgcn_sched_barrier(0);
         }
@@ -730,43 +442,33 @@ __device__ __forceinline__ void x3r3_body16(const RowGemmArgs& p, char* smem, in
 #pragma unroll
             for (int q = 0; q < 3; ++q) af[bm][q] = *(const bf16x8*)(abase + h * RB + q * 64 + ((ks ^ swz(h)) << 4));
         }
-        if constexpr (ISSUER && LATE) issue(s);
-        mma(af, &bfr[0][0][0], 0, 0, NT);
+        issue(s);  // LATE: the next sub-step's DMA behind the first fragment reads
+        mma(af, &bfr[0][0][0], 0);
         if constexpr (LAG) __builtin_amdgcn_sched_barrier(0);  // A of the held half after A0 died
-        if (LAG && RA && dx < 2) {  // defer the second half: hold B, re-read A after the barrier
+        bf16x8 af1[2][3];
 #pragma unroll
-            for (int nt = 0; nt < HN; ++nt)
+        for (int bm = 0; bm < 2; ++bm) {
+            const int h = ahb[1][bm] + dx;
+#pragma unroll
+            for (int q = 0; q < 3; ++q) af1[bm][q] = *(const bf16x8*)(abase + h * RB + q * 64 + ((ks ^ swz(h)) << 4));
+        }
+        if constexpr (LAG) {
+#pragma unroll
+            for (int bm = 0; bm < 2; ++bm)
+#pragma unroll
+                for (int q = 0; q < 3; ++q) ha[bm][q] = af1[bm][q];
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
                 for (int bn = 0; bn < 2; ++bn)
 #pragma unroll
-                    for (int q = 0; q < 3; ++q) hb[nt][bn][q] = bfr[N0 + nt][bn][q];
+                    for (int q = 0; q < 3; ++q) hb[nt][bn][q] = bfr[nt][bn][q];
         } else {
-            bf16x8 af1[2][3];
-#pragma unroll
-            for (int bm = 0; bm < 2; ++bm) {
-                const int h = ahb[1][bm] + dx;
-#pragma unroll
-                for (int q = 0; q < 3; ++q) af1[bm][q] = *(const bf16x8*)(abase + h * RB + q * 64 + ((ks ^ swz(h)) << 4));
-            }
-            if constexpr (LAG && !RA) {
-                if constexpr (N0 > 0) mma(af1, &bfr[0][0][0], 1, 0, N0);
-#pragma unroll
-                for (int bm = 0; bm < 2; ++bm)
-#pragma unroll
-                    for (int q = 0; q < 3; ++q) ha[bm][q] = af1[bm][q];
-#pragma unroll
-                for (int nt = 0; nt < HN; ++nt)
-#pragma unroll
-                    for (int bn = 0; bn < 2; ++bn)
-#pragma unroll
-                        for (int q = 0; q < 3; ++q) hb[nt][bn][q] = bfr[N0 + nt][bn][q];
-            } else {
-                mma(af1, &bfr[0][0][0], 1, 0, NT);
-            }
+            mma(af1, &bfr[0][0][0], 1);
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
-    if constexpr (LAG && !RA) mma(ha, &hb[0][0][0], 1, N0, NT);
+    if constexpr (LAG) mma(ha, &hb[0][0][0], 1);
 }
 
 // the 16x16x32 accumulators (hi + lo) in the 32x32x16 register layout: lanes l and l ^ 16 swap
@@ -785,27 +487,17 @@ __device__ __forceinline__ void x3_acc16_to32(const f32x4 (&hi)[2][NT][2][2], co
         }
 }
 
-// SCHED: 0 = every wave issues its share, no stagger (r04); 1 = + stagger + late DMA;
-// 2 = loader waves 0..3 + stagger; 3 = loader waves + stagger + late DMA; 4 = loader waves only
-template <int SCHED>
-struct X3R3Sched {
-    static constexpr int LW = SCHED >= 2 ? 4 : 8;
-    static constexpr bool LAG = SCHED >= 1 && SCHED <= 3;
-    static constexpr bool LATE = SCHED == 1 || SCHED == 3;
-};
-
-// BM = 256: 8 waves, one block per CU (160 KB); BM = 128 (tile 6, 128 x 64): 4 waves of 64 x 32,
-// 80 KB, two blocks per CU -- independent blocks run out of phase, so one block's prologue,
-// epilogue and barrier stalls overlap the other's MFMAs (the short-K level-0 GEMMs)
-template <int EMODE, int BN = 128, int SCHED = 0, int BM = 256>
+// BM = 256 (tile 4 / 256 x 128): 8 waves, one block per CU (160 KB), staggered; BM = 128 (tile 6,
+// 128 x 64): 4 waves of 64 x 32, 80 KB, two blocks per CU -- independent blocks run out of phase,
+// so one block's prologue, epilogue and barrier stalls overlap the other's MFMAs (the short-K
+// level-0 GEMMs), and no wave holds deferred fragments
+template <int EMODE, int BN = 128, int BM = 256>
 __global__ __launch_bounds__(BM / 64 * 2 * 64, BM == 256 ? 1 : 2) void rowgemm_x3_row3_kernel(RowGemmArgs p) {
-    constexpr int WM = 64, WN = BN / 2, MT = 2, NT = WN / 32, WAVES = BM / 64 * 2;
+    constexpr int WM = 64, WN = BN / 2, NT = WN / 32, WAVES = BM / 64 * 2;
     constexpr int RB = 192, AR = BM / 16 * 18, WB = 1024 * WAVES;
     constexpr int SMEM = 2 * ((AR * RB + WB - 1) / WB) * WB + 2 * ((BN * RB + WB - 1) / WB) * WB;  // 160 / 80 KB
     static_assert(SMEM >= 2 * (BM / 64) * BN * 8, "epilogue scratch");
-    static_assert(BM == 256 || SCHED == 0 || SCHED == 9, "the staggered schedules pair waves w and w + 4");
     __shared__ __attribute__((aligned(1024))) char smem[SMEM];
-    using SC = X3R3Sched<SCHED & 7>;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave / 2, wn = wave % 2;
@@ -814,271 +506,34 @@ __global__ __launch_bounds__(BM / 64 * 2 * 64, BM == 256 ? 1 : 2) void rowgemm_x
     int tile_m, tile_n;
     tile_mn(bid, (p.M + BM - 1) / BM, ntn, p.tgm, tile_m, tile_n);
     const int m0 = tile_m * BM, n0 = tile_n * BN;
-    f32x16 acc[MT][NT];
-    if constexpr (SCHED >= 8) {  // the 16x16x32 body (SCHED - 8 = the schedule)
-        f32x4 h16[2][NT][2][2], l16[2][NT][2][2];
+    f32x16 acc[2][NT];
+    f32x4 h16[2][NT][2][2], l16[2][NT][2][2];
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int j = 0; j < NT; ++j)
-#pragma unroll
-                for (int b = 0; b < 4; ++b)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) h16[i][j][b >> 1][b & 1][r] = l16[i][j][b >> 1][b & 1][r] = 0.f;
-        // SCHED 8: every wave issues, no stagger; 9: + half stagger + late DMA; 10: + quarter
-        // stagger + late DMA.  (Measured and dropped: late DMA alone; waves 0..3 issuing every
-        // DMA with waves 4..7 staggered -- 17..55 spilled VGPRs.)
-        constexpr int SUB = SCHED - 8;
-        // (BM = 128, tile 6: four waves, two blocks per CU -- the other block is the stagger)
-        constexpr bool LATE16 = SUB >= 1, LAG16 = SUB >= 1 && BM == 256, QL16 = SUB == 2, RA16 = SUB == 3;
-        constexpr bool RC16 = SUB == 4;
-        constexpr int LW16 = BM / 64 * 2;
-        if (wave >= 4)
-            x3r3_body16<BM, BN, LW16, LW16 == 8, LAG16, LATE16, QL16, RA16, RC16>(p, smem, wave, lane, h16, l16, m0, n0);
-        else
-            x3r3_body16<BM, BN, LW16, true, false, LATE16>(p, smem, wave, lane, h16, l16, m0, n0);
-        x3_acc16_to32(h16, l16, acc, lane);
-        x3_barrier();
-        row_epilogue<EMODE, BM, BN, WM, WN, true>(p, acc, m0, n0, tile_m, wm, wn, lane, tid, (float*)smem);
-        return;
-    }
-    f32x16 acl[MT][NT];
-#pragma unroll
-    for (int i = 0; i < MT; ++i)
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < NT; ++j)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = acl[i][j][r] = 0.f;
-    if constexpr (BM == 128)
-        x3r3_body<BM, BN, 4, true, false, false>(p, smem, wave, lane, acc, acl, m0, n0);
-    else if (wave >= 4)
-        x3r3_body<BM, BN, SC::LW, SC::LW == 8, SC::LAG, SC::LATE>(p, smem, wave, lane, acc, acl, m0, n0);
+            for (int b = 0; b < 4; ++b)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) h16[i][j][b >> 1][b & 1][r] = l16[i][j][b >> 1][b & 1][r] = 0.f;
+    if (BM == 256 && wave >= 4)
+        x3r3_body16<BM, BN, BM == 256>(p, smem, wave, lane, h16, l16, m0, n0);
     else
-        x3r3_body<BM, BN, SC::LW, true, false, SC::LATE>(p, smem, wave, lane, acc, acl, m0, n0);
+        x3r3_body16<BM, BN, false>(p, smem, wave, lane, h16, l16, m0, n0);
+    x3_acc16_to32(h16, l16, acc, lane);
     x3_barrier();  // the epilogue reuses the stage memory
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt) acc[mt][nt] += acl[mt][nt];
     row_epilogue<EMODE, BM, BN, WM, WN, true>(p, acc, m0, n0, tile_m, wm, wn, lane, tid, (float*)smem);
-}
-
-// ------------------------------------------------------------------------------------
-// Tile 8 (r05): the 64-output 3x3 GEMMs on a 512 x 64 halo tile, 8 waves of 64 x 64 -- the
-// 256 x 128 kernel's wave tile -- over TWO image rows of 256.  A 32-channel halo of two rows
-// (2 x 258 x 192 B) cannot be double-buffered in 160 KB, so the channel group is 16: x3 rows of
-// 96 B ([h | m | l] x 16 channels), a halo stage of 516 rows = 49.5 KB (56 KB region), one
-// 32x32x16 k-step per sub-step (dy, 16-channel group, dx).  Per 768 MFMA cycles a wave issues
-// ~3 LDS-DMA pieces (the 256 x 64 tile: ~4.3) and reads 12 fragments for 24 MFMAs (64 x 32
-// waves: 9 for 12).  LDS: 2 x 56 KB halo + 2 x 8 KB B = 128 KB, one block per CU.
-//   swizzle: 16-B half h of plane q of row r at slot 2 q + (h ^ ((r >> 3) & 1)) -- rows r and
-//   r + 8 share a bank slot (96 B = 6 slots), the 16 rows of a ds_read_b128 lane group then
-//   land on 16 distinct slots.
-//   K order (dy, 16-channel group, dx): results agree with the other tiles to f32 rounding.
-//   LAG (schedule 1, default): waves 4..7 run their second 32-row half's MFMAs after the next
-//   barrier from held fragments; LATE: the next sub-step's DMA after this one's reads.
-// ------------------------------------------------------------------------------------
-template <int EMODE, bool LAG, bool LATE>
-__global__ __launch_bounds__(512, 1) void rowgemm_x3_r3k16_kernel(RowGemmArgs p) {
-    constexpr int BM = 512, BN = 64, BK = 16, WM = 64, WN = 64, WAVES = 8, MT = 2, NT = 2;
-    constexpr int RB = 96, AR = BM / 16 * 18;
-    constexpr int AREG = ((AR * RB + 1024 * WAVES - 1) / (1024 * WAVES)) * WAVES * 1024;  // 56 KB
-    constexpr int BREG = ((BN * RB + 1024 * WAVES - 1) / (1024 * WAVES)) * WAVES * 1024;  // 8 KB
-    constexpr int AI = AREG / (1024 * WAVES), BI = BREG / (1024 * WAVES);
-    constexpr int AC = (AI + 2) / 3;
-    constexpr int SMEM = 2 * AREG + 2 * BREG;
-    static_assert(SMEM >= 2 * (BM / 64) * BN * 8, "epilogue scratch");
-    __shared__ __attribute__((aligned(1024))) char smem[SMEM];
-    auto swz = [](int r) { return (r >> 3) & 1; };
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = wave, wn = 0;
-    const int ntn = p.N / BN;
-    const int bid = p.xcd ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
-    const int tile_m = bid / ntn, tile_n = bid - tile_m * ntn;
-    const int m0 = tile_m * BM, n0 = tile_n * BN;
-    const int H = p.H, W = p.W, C = p.C, K = p.K;
-    const int SEG = W < BM ? W : BM, HW = SEG + 2;
-    const int AROWS = (BM / SEG) * HW;
-    const size_t rowa = 3 * (size_t)p.lda, rowb = 3 * (size_t)K;
-    // A loader: lane of piece j fills halo bytes (j 8 + wave) KB + 16 lane = halo row h, slot k =
-    // w / 16 (plane k / 2, half k & 1) sourcing the (half ^ swz(h)) 8 channels of that plane
-    int acen[AI], apk[AI];
-#pragma unroll
-    for (int j = 0; j < AI; ++j) {
-        const int o = ((j * WAVES + wave) * 64 + lane) * 16;
-        const int h = o / RB, k = (o - h * RB) >> 4;
-        const int r = h / HW, xl = h - r * HW - 1;
-        const int mrow = m0 + r * SEG;
-        bool ok = h < AROWS && mrow < p.M;
-        const Pix q = decode(ok ? mrow : 0, H, W);
-        ok = ok && q.x + xl >= 0 && q.x + xl < W;
-        acen[j] = ok ? mrow + xl : -1;
-        apk[j] = q.y * 128 + (k >> 1) * 32 + (((k & 1) ^ swz(h)) << 3);
-    }
-    int boff[BI];
-#pragma unroll
-    for (int j = 0; j < BI; ++j) {
-        const int o = ((j * WAVES + wave) * 64 + lane) * 16;
-        const int r = o / RB, k = (o - r * RB) >> 4;
-        boff[j] = r < BN ? (int)((n0 + r) * rowb) + (k >> 1) * 32 + (((k & 1) ^ swz(r)) << 3) : -1;
-    }
-    const uint16_t* zero = (const uint16_t*)p.zero16;
-    const uint16_t* a16 = p.a16 + (size_t)p.aoff * 3;
-    const int CC = C / BK;  // 16-channel groups per tap
-    const int NG = 3 * CC;  // halo groups (dy, group)
-    const int ns = 9 * CC;  // sub-steps (dy, group, dx)
-    // element offset of channel c0 (a multiple of 16) inside an x3 row: its 32-channel chunk
-    // of 96 elements, then the 16-channel half of each plane
-    auto chunk = [](int c0) { return (c0 >> 5) * 96 + ((c0 >> 4) & 1) * 16; };
-    auto issue_a = [&](int g, int j0, int j1) {
-        const int dy = g / CC, c0 = (g - dy * CC) * BK;
-        char* base = smem + (g & 1) * AREG;
-        const int ce = chunk(c0);
-#pragma unroll
-        for (int j = 0; j < AI; ++j) {
-            if (j < j0 || j >= j1) continue;
-            const int yy = (apk[j] >> 7) + dy - 1;
-            const bool valid = acen[j] >= 0 && yy >= 0 && yy < H;
-            const uint16_t* src =
-                valid ? a16 + (size_t)(acen[j] + (dy - 1) * W) * rowa + ce + (apk[j] & 127) : zero;
-            x3_dma16(src, base + (j * WAVES + wave) * 1024);
-        }
-    };
-    auto issue_b = [&](int s) {
-        const int g = s / 3, dx = s - g * 3;
-        const int dy = g / CC, c0 = (g - dy * CC) * BK;
-        const int ke = chunk((dy * 3 + dx) * C + c0);
-        char* base = smem + 2 * AREG + (s & 1) * BREG;
-#pragma unroll
-        for (int j = 0; j < BI; ++j)
-            x3_dma16(boff[j] >= 0 ? p.bt16 + boff[j] + ke : zero, base + (j * WAVES + wave) * 1024);
-    };
-    auto issue = [&](int s) {
-        const int g = s / 3, dx = s - g * 3;
-        if (s + 1 < ns) issue_b(s + 1);
-        if (g + 1 < NG) issue_a(g + 1, dx * AC, dx * AC + AC);
-    };
-    const int lh = lane >> 5, li = lane & 31;
-    int ahb[MT], bro[NT], bfx[NT];
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-        const int mo = wm * WM + mt * 32 + li;
-        const int r = mo / SEG;
-        ahb[mt] = r * HW + (mo - r * SEG);
-    }
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-        const int r = wn * WN + nt * 32 + li;
-        bro[nt] = r * RB;
-        bfx[nt] = swz(r);
-    }
-    f32x16 acc[MT][NT], acl[MT][NT];
-#pragma unroll
-    for (int i = 0; i < MT; ++i)
-#pragma unroll
-        for (int j = 0; j < NT; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = acl[i][j][r] = 0.f;
-    auto run = [&](auto LAGC) {
-        constexpr bool LG = decltype(LAGC)::value;
-        bf16x8 ha[3], hb[NT][3];  // LG: the previous sub-step's second-half fragments
-        issue_a(0, 0, AI);
-        issue_b(0);
-        for (int s = 0; s < ns; ++s) {
-            const int g = s / 3, dx = s - g * 3;
-            if (dx >= 1 && g + 1 < NG) x3_wait_vm<AC>();
-            else x3_wait_vm<0>();
-            x3_barrier();
-            if constexpr (!LATE) issue(s);
-            if constexpr (LG) {
-                if (s > 0) {
-#pragma unroll
-                    for (int nt = 0; nt < NT; ++nt) mfma_x3s(ha, hb[nt], acc[1][nt], acl[1][nt]);
-                }
-            }
-            const char* abase = smem + (g & 1) * AREG;
-            const char* bbase = smem + 2 * AREG + (s & 1) * BREG;
-            bf16x8 af[MT][3], bfr[NT][3];
-#pragma unroll
-            for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-                for (int q = 0; q < 3; ++q)
-                    bfr[nt][q] = *(const bf16x8*)(bbase + bro[nt] + q * 32 + ((lh ^ bfx[nt]) << 4));
-#pragma unroll
-            for (int mt = 0; mt < MT; ++mt) {
-                const int h = ahb[mt] + dx;
-#pragma unroll
-                for (int q = 0; q < 3; ++q)
-                    af[mt][q] = *(const bf16x8*)(abase + h * RB + q * 32 + ((lh ^ swz(h)) << 4));
-            }
-            if constexpr (LATE) issue(s);
-#pragma unroll
-            for (int nt = 0; nt < NT; ++nt) mfma_x3s(af[0], bfr[nt], acc[0][nt], acl[0][nt]);
-            if constexpr (LG) {
-#pragma unroll
-                for (int q = 0; q < 3; ++q) ha[q] = af[1][q];
-#pragma unroll
-                for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-                    for (int q = 0; q < 3; ++q) hb[nt][q] = bfr[nt][q];
-            } else {
-#pragma unroll
-                for (int nt = 0; nt < NT; ++nt) mfma_x3s(af[1], bfr[nt], acc[1][nt], acl[1][nt]);
-            }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        }
-        if constexpr (LG) {
-#pragma unroll
-            for (int nt = 0; nt < NT; ++nt) mfma_x3s(ha, hb[nt], acc[1][nt], acl[1][nt]);
-        }
-    };
-    if (LAG && wave >= 4) run(std::true_type{});
-    else run(std::false_type{});
-    x3_barrier();  // the epilogue reuses the stage memory
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt) acc[mt][nt] += acl[mt][nt];
-    row_epilogue<EMODE, BM, BN, WM, WN, true>(p, acc, m0, n0, tile_m, wm, wn, lane, tid, (float*)smem);
-}
-
-template <int EMODE>
-static int x3r3k16_go(const RowGemmArgs& a, int sched, hipStream_t s) {
-    if (a.amode != G_CONV3 || a.N % 64 || a.C % 32 || a.K != 9 * a.C) return -1;
-    if (a.W < 16 || (512 % a.W && a.W % 512)) return -1;
-    const dim3 grid(((a.M + 511) / 512) * (a.N / 64));
-    // schedules: 0 = no stagger (DMA after the barrier), 1 (and the others) = stagger + late DMA
-    if (sched == 0)
-        hipLaunchKernelGGL((rowgemm_x3_r3k16_kernel<EMODE, false, false>), grid, dim3(512), 0, s, a);
-    else
-        hipLaunchKernelGGL((rowgemm_x3_r3k16_kernel<EMODE, true, true>), grid, dim3(512), 0, s, a);
-    return (int)hipGetLastError();
 }
 
 template <int EMODE, int BN, int BM = 256>
-static int x3r3_go(const RowGemmArgs& a, int sched, hipStream_t s) {
+static int x3r3_go(const RowGemmArgs& a, hipStream_t s) {
     // BM % W == 0 or W % BM == 0 keeps a tile on whole rows / row segments; W >= 16 bounds the halo
     if (a.amode != G_CONV3 || a.N % BN || a.C % 32 || a.K != 9 * a.C) return -1;
     if (a.W < 16 || (BM % a.W && a.W % BM)) return -1;
     const dim3 grid(((a.M + BM - 1) / BM) * (a.N / BN));
-    if constexpr (BM == 128) {
-        if (sched >= 8)  // 16x16x32, DMA after the first reads
-            hipLaunchKernelGGL((rowgemm_x3_row3_kernel<EMODE, BN, 9, 128>), grid, dim3(256), 0, s, a);
-        else
-            hipLaunchKernelGGL((rowgemm_x3_row3_kernel<EMODE, BN, 0, 128>), grid, dim3(256), 0, s, a);
-        return (int)hipGetLastError();
-    }
-#define X3R3_SCHED(v)                                                                          \
-    if (sched == v) {                                                                         \
-        hipLaunchKernelGGL((rowgemm_x3_row3_kernel<EMODE, BN, v>), grid, dim3(512), 0, s, a); \
-        return (int)hipGetLastError();                                                        \
-    }
-    X3R3_SCHED(0) X3R3_SCHED(1) X3R3_SCHED(2) X3R3_SCHED(3) X3R3_SCHED(4) X3R3_SCHED(8) X3R3_SCHED(9) X3R3_SCHED(10) X3R3_SCHED(12)
-#undef X3R3_SCHED
-    return -1;
+    hipLaunchKernelGGL((rowgemm_x3_row3_kernel<EMODE, BN, BM>), grid, dim3(BM / 64 * 2 * 64), 0, s, a);
+    return (int)hipGetLastError();
 }
-
 // tiles (split accumulators; probe: profiles/r04_x3_probe_*.txt): 0 = 256x128 (8 waves of
 // 64x64, 2 stages, 144 KB, one block per CU), 1 = 128x128 (4 waves, 2 stages: grids below 256
 // blocks of tile 0), 2 = 128x64 (4 waves of 64x32, two blocks per CU: the 64-output layers),
@@ -1087,47 +542,39 @@ using TX0 = TileX3<256, 128, 64, 64, 2, 1, 1>;
 using TX1 = TileX3<128, 128, 64, 64, 2, 1, 1>;
 using TX2 = TileX3<128, 64, 64, 32, 2, 2, 1>;
 using TX3 = TileX3<256, 64, 64, 32, 2, 1, 1>;
-// 7 = 128x32 (2 waves of 64x32, two blocks per CU): the 32-channel layers of the reference
-// grid's narrow widths (option x3_n32, r05)
-using TX7 = TileX3<128, 32, 64, 32, 2, 1, 1>;  // (60 KB: LDS allows two blocks per CU)
-#define ROWGEMM_X3_TILES(X) X(0, TX0) X(1, TX1) X(2, TX2) X(3, TX3) X(7, TX7)
+#define ROWGEMM_X3_TILES(X) X(0, TX0) X(1, TX1) X(2, TX2) X(3, TX3)
 
-template <int AMODE, int EMODE, class T, int XP = 0, bool M16 = false>
+template <int AMODE, int EMODE, class T>
 static int x3_go(const RowGemmArgs& a, hipStream_t s) {
     if (a.N % T::BN || a.C % 32 || a.K % 32) return -1;
     if (EMODE == E_CONVT && (a.cout % T::BN) && (T::BN % a.cout)) return -1;
     const dim3 grid(((a.M + T::BM - 1) / T::BM) * (a.N / T::BN));
-    hipLaunchKernelGGL((rowgemm_x3_kernel<AMODE, EMODE, T, XP, M16>), grid, dim3(T::THREADS), 0, s, a);
+    hipLaunchKernelGGL((rowgemm_x3_kernel<AMODE, EMODE, T>), grid, dim3(T::THREADS), 0, s, a);
     return (int)hipGetLastError();
 }
 
 template <int AMODE, int EMODE>
-static int x3_tile(const RowGemmArgs& a0, int tile, hipStream_t s, int sched = 0) {
+static int x3_tile(const RowGemmArgs& a0, int tile, hipStream_t s) {
     RowGemmArgs a = a0;
     if (a.tgm < 0) {  // tile order: the group size for this tile's grid (two blocks per CU on 128 x 64)
         int bm = 0, bn = 0;
         if (rowgemm_x3_tile_dims(tile, &bm, &bn) != 0) return -1;
-        a.tgm = tile_group_auto(a.M, a.N, bm, bn, (tile == 2 || tile == 6 || tile == 7) ? 64 : 32);
+        a.tgm = tile_group_auto(a.M, a.N, bm, bn, (tile == 2 || tile == 6) ? 64 : 32);
     }
-    if (tile == 8) {  // 512 x 64, 16-channel halo groups (r05)
-        if constexpr (AMODE == G_CONV3) return x3r3k16_go<EMODE>(a, sched >= 8 ? 1 : sched, s);
-        return -1;
-    }
-    if (tile == 4 || tile == 5 || tile == 6) {  // tap-row halo kernel (3x3 convs): 256 x 128 / 256 x 64 / 128 x 64
+    if (tile == 4 || tile == 6) {  // tap-row halo kernel (3x3 convs): 256 x 128 / 128 x 64
         // (r04, not kept: 4-wave 128x64 / 64x128 wave tiles, within noise of 8 waves; B
         // straight from global memory into registers instead of the LDS ring, one barrier per
         // halo group, bit-identical but 222 -> 161 TF/s: the per-wave B loads cost more than
         // the ring's barriers; 256 x 64 as 4 waves of 64 x 64, bit-identical, 589 -> 584 img/s;
-        // 256 x 64 with a three-slot B ring, B two sub-steps ahead: bit-identical, no gain)
+        // 256 x 64 with a three-slot B ring, B two sub-steps ahead: bit-identical, no gain;
+        // r05: 256 x 64 on 8 waves, 0.2 % slower than 128 x 64, removed in r06)
         if constexpr (AMODE == G_CONV3)
-            return tile == 4 ? x3r3_go<EMODE, 128>(a, sched, s)
-                 : tile == 5 ? x3r3_go<EMODE, 64>(a, sched, s)
-                             : x3r3_go<EMODE, 64, 128>(a, sched, s);
+            return tile == 4 ? x3r3_go<EMODE, 128>(a, s) : x3r3_go<EMODE, 64, 128>(a, s);
         return -1;
     }
-    // schedules >= 8 (16x16x32) also take the one-tap 64 x 64-wave tiles to 16x16x32 (r05)
-    if (sched >= 8 && tile == 0) return x3_go<AMODE, EMODE, TX0, 0, true>(a, s);
-    if (sched >= 8 && tile == 1) return x3_go<AMODE, EMODE, TX1, 0, true>(a, s);
+    // (r05, removed in r06: the one-tap tiles on 16x16x32, config 2 within noise,
+    // profiles/r05_1tap16_ab.txt; a 128 x 32 tile for the narrow widths' 32-channel layers, slower
+    // than the f32 MFMA kernels there, profiles/r05_x3_n32_ab.txt)
 #define X3_CASE(id, T) \
     if (tile == id) return x3_go<AMODE, EMODE, T>(a, s);
     ROWGEMM_X3_TILES(X3_CASE)
@@ -1191,9 +638,7 @@ struct WTileX3 {
     static constexpr int THREADS = 64 * WAVES;
 };
 
-// M16 (r05): 16x16x32 MFMAs, one k-step of 32 pixels per chunk (as wgrad_x3_row3_kernel's: k
-// 8 g .. 8 g + 7 of lane group g = pixel rows 4 g + qq and 16 + 4 g + qq, swizzle x3_tswz16)
-template <int AMODE, int BMODE, class T, bool M16 = false>
+template <int AMODE, int BMODE, class T>
 __global__ __launch_bounds__(T::THREADS, 1) void wgrad_x3_kernel(WgradArgs p) {
     constexpr int BM = T::BM, BN = T::BN, WM = T::WM, WN = T::WN, BKP = T::BKP, S = T::S;
     constexpr int WAVES = T::WAVES, WAVES_N = BN / WN;
@@ -1232,14 +677,14 @@ __global__ __launch_bounds__(T::THREADS, 1) void wgrad_x3_kernel(WgradArgs p) {
         const int o = ((j * WAVES + wave) * 64 + lane) * 16;
         const int r = o / RA, sl = (o - r * RA) >> 4;
         arow[j] = r;
-        aele[j] = (M16 ? x3_tswz16<RA>(sl, r) : x3_tswz<RA>(sl, r)) * 8;
+        aele[j] = x3_tswz<RA>(sl, r) * 8;
     }
 #pragma unroll
     for (int j = 0; j < BI; ++j) {
         const int o = ((j * WAVES + wave) * 64 + lane) * 16;
         const int r = o / RBB, sl = (o - r * RBB) >> 4;
         brow[j] = r;
-        bele[j] = (M16 ? x3_tswz16<RBB>(sl, r) : x3_tswz<RBB>(sl, r)) * 8;
+        bele[j] = x3_tswz<RBB>(sl, r) * 8;
     }
     const uint16_t* a16 = (const uint16_t*)p.a + (size_t)(p.aoff + ca0) * 3;
     const uint16_t* b16 = (const uint16_t*)p.b + (size_t)(p.boff + cb0) * 3;
@@ -1274,111 +719,6 @@ __global__ __launch_bounds__(T::THREADS, 1) void wgrad_x3_kernel(WgradArgs p) {
     };
 
     constexpr int SA = T::SA;
-    static_assert(!M16 || SA, "16x16x32: split accumulators");
-    if constexpr (M16) {
-        f32x4 hi[MT][NT][2][2], lo[MT][NT][2][2];
-#pragma unroll
-        for (int i = 0; i < MT; ++i)
-#pragma unroll
-            for (int j = 0; j < NT; ++j)
-#pragma unroll
-                for (int b = 0; b < 4; ++b)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) hi[i][j][b >> 1][b & 1][r] = lo[i][j][b >> 1][b & 1][r] = 0.f;
-        const int g = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
-        const int trow = 4 * g + qq;
-        auto slot = [](int col, int q) { return (col >> 5) * 12 + q * 4 + ((col & 31) >> 3); };
-        int aoff[MT][2][3], boff[NT][2][3];
-#pragma unroll
-        for (int b = 0; b < 2; ++b)
-#pragma unroll
-            for (int q = 0; q < 3; ++q) {
-#pragma unroll
-                for (int mt = 0; mt < MT; ++mt) {
-                    const int col = wm * WM + mt * 32 + 16 * b + 4 * pp;
-                    aoff[mt][b][q] = trow * RA + (x3_tswz16<RA>(slot(col, q), trow) << 4) + ((col >> 2) & 1) * 8;
-                }
-#pragma unroll
-                for (int nt = 0; nt < NT; ++nt) {
-                    const int col = wn * WN + nt * 32 + 16 * b + 4 * pp;
-                    boff[nt][b][q] = BKP * RA + trow * RBB + (x3_tswz16<RBB>(slot(col, q), trow) << 4) + ((col >> 2) & 1) * 8;
-                }
-            }
-#pragma unroll
-        for (int s = 0; s < S - 1; ++s)
-            if (s < nk) issue(s, s);
-        for (int kc = 0; kc < nk; ++kc) {
-            if (kc + S - 1 < nk) issue(kc + S - 1, (kc + S - 1) % S);
-            const int ahead = min(S - 1, nk - 1 - kc);
-            if constexpr (S >= 3) {
-                if (ahead >= 2) x3_wait_vm<2 * GPC>();
-                else if (ahead == 1) x3_wait_vm<GPC>();
-                else x3_wait_vm<0>();
-            } else {
-                if (ahead >= 1) x3_wait_vm<GPC>();
-                else x3_wait_vm<0>();
-            }
-            x3_barrier();
-            const unsigned sb = x3_lds_u32(smem) + (kc % S) * STAGE;
-            x3_short4 fa[MT][2][3][2], fb[NT][2][3][2];
-#pragma unroll
-            for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-                for (int b = 0; b < 2; ++b)
-#pragma unroll
-                    for (int q = 0; q < 3; ++q) {
-                        fb[nt][b][q][0] = x3_tr16<0>(sb + boff[nt][b][q]);
-                        fb[nt][b][q][1] = x3_tr16<16 * RBB>(sb + boff[nt][b][q]);
-                    }
-#pragma unroll
-            for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-                for (int b = 0; b < 2; ++b)
-#pragma unroll
-                    for (int q = 0; q < 3; ++q) {
-                        fa[mt][b][q][0] = x3_tr16<0>(sb + aoff[mt][b][q]);
-                        fa[mt][b][q][1] = x3_tr16<16 * RA>(sb + aoff[mt][b][q]);
-                    }
-            // the transposed reads are inline asm: their results are only valid after the wait,
-            // so no MFMA may be scheduled above it
-            __builtin_amdgcn_sched_barrier(0);
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-                for (int b = 0; b < 2; ++b)
-#pragma unroll
-                    for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-                        for (int bn = 0; bn < 2; ++bn) {
-                            bf16x8 a3[3], b3[3];
-#pragma unroll
-                            for (int q = 0; q < 3; ++q) {
-                                a3[q] = *(const bf16x8*)fa[mt][b][q];
-                                b3[q] = *(const bf16x8*)fb[nt][bn][q];
-                            }
-                            mfma_x3s16(a3, b3, hi[mt][nt][b][bn], lo[mt][nt][b][bn]);
-                        }
-            x3_barrier();
-        }
-        float* slab = p.slab + (size_t)split * p.Mw * p.Nw;
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-            for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-                for (int b = 0; b < 2; ++b)
-#pragma unroll
-                    for (int bn = 0; bn < 2; ++bn)
-#pragma unroll
-                        for (int i = 0; i < 4; ++i) {
-                            const int m = tm * BM + wm * WM + mt * 32 + 16 * b + 4 * g + i;
-                            const int n = tn * BN + wn * WN + nt * 32 + 16 * bn + (lane & 15);
-                            slab[(size_t)m * p.Nw + n] = hi[mt][nt][b][bn][i] + lo[mt][nt][b][bn][i];
-                        }
-        return;
-    }
     f32x16 acc[MT][NT], acl[SA ? MT : 1][SA ? NT : 1];
 #pragma unroll
     for (int i = 0; i < MT; ++i)
@@ -1496,34 +836,32 @@ __global__ __launch_bounds__(T::THREADS, 1) void wgrad_x3_kernel(WgradArgs p) {
 // chunk never crosses an image row, so the A' operands of the three taps are the same 34
 // halo pixels of source row y + dy - 1 (columns x0 - 1 .. x0 + 32, zero outside the image),
 // read at row offsets dx = 0, 1, 2: a third of the one-tap kernel's A' staging per MFMA.
-// 8 waves, each 32 ci x 32 co x 3 taps (3 accumulator pairs); per k-step 18 + 6 transposed
-// reads feed 18 MFMAs.  Stage: [AR halo rows][6 BM B] + [32 pixel rows][6 BN B]; the loader
-// gives every wave the same instruction count (rows past the halo / chunk read zeros).
+// 16x16x32 MFMAs (r05): the chip holds a higher clock on that shape at equal cycles per FLOP.
+// Stage: [AR halo rows][6 BM B] + [32 pixel rows][6 BN B]; the loader gives every wave the same
+// instruction count (rows past the halo / chunk read zeros).
 // ------------------------------------------------------------------------------------
 //
-// SCHED (r05): 0 = every wave issues its share of the DMA and runs both k-steps of chunk kc in
-// segment kc (r04).  1 = four LDS stages with the DMA two chunks ahead, so a stage stays intact
-// one segment longer: waves 4..7 (each sharing a SIMD with wave w - 4) run half a chunk behind,
-// reading and computing chunk kc - 1's second k-step at the start of segment kc while their
-// partner waits for its first fragments of chunk kc (MI355X_MICROARCH.md "two waves per SIMD"
-// item 9).  2 = 1 with the DMA issued by waves 0..3 only (twice the pieces each).  3 = r04's
-// three stages with the next DMA issued behind the first k-step's fragment reads (as the halo
-// GEMM's schedule 1).  Same MFMAs in the same order per accumulator, same split partition:
-// bit-identical.
-template <int BM, int BN, int S = 3, int OCC = 1, int SCHED = 0, bool W16 = false>
+// LAG (r05 schedule 10, the 64 x 128 tile): four LDS stages with the DMA two chunks ahead, so a
+// stage stays intact one chunk longer; waves 4..7 (each sharing a SIMD with wave w - 4) run each
+// chunk's second 16-column half at the start of the next chunk, re-reading its fragments from
+// that stage, while their partner waits for its first fragments (MI355X_MICROARCH.md "two waves
+// per SIMD" item 9); the next DMA goes behind the first fragment reads.  Without LAG (the 128 x
+// 64 and 64 x 64 tiles) the DMA runs S - 1 chunks ahead.  Same MFMAs in the same order per
+// accumulator, same split partition: bit-identical.  (r04-r05, removed in r06: the 32x32x16
+// body, 1.6-1.9 % slower over the step, and its staggered / late-DMA variants.)
+template <int BM, int BN, int S = 3, int OCC = 1, bool LAG = false, bool W16 = false>
 __global__ __launch_bounds__((BM / 32) * (BN / 32) * 64, OCC) void wgrad_x3_row3_kernel(WgradArgs p) {
     constexpr int WAVES = (BM / 32) * (BN / 32), BKP = 32;
     constexpr int WAVES_N = BN / 32;
     static_assert(S >= 2 && S <= 4, "stages");
-    constexpr bool M16 = SCHED >= 8;  // 16x16x32 MFMAs (8: as 0, 9: as 3)
-    static_assert(SCHED == 0 || SCHED == 3 || M16 || (S == 4 && WAVES == 8), "the staggered schedules need 4 stages, 8 waves");
-    constexpr int LW = SCHED == 2 ? 4 : WAVES;  // waves issuing the DMA
-    constexpr int DIST = (SCHED == 1 || SCHED == 2 || SCHED == 10) ? 2 : S - 1;  // chunks the DMA runs ahead
-    constexpr bool LATE = SCHED == 3 || SCHED >= 9;  // the DMA issued after the first k-step's reads
+    static_assert(!LAG || (S == 4 && WAVES == 8), "the stagger: four stages, waves w / w + 4");
+    constexpr int LW = WAVES;                   // waves issuing the DMA
+    constexpr int DIST = LAG ? 2 : S - 1;       // chunks the DMA runs ahead
+    constexpr bool LATE = LAG;                  // the DMA issued after the first fragment reads
     constexpr int RA = 6 * BM, RBB = 6 * BN;
-    // halo pixel rows per stage: 34 (one 32-pixel row segment), or with M16 at W = 16 two
-    // image rows of 16 + 2 (r05: the 16x16 level's 3x3 weight gradients on this kernel too)
-    constexpr int HALO = M16 ? BKP + 4 : BKP + 2;
+    // halo pixel rows per stage: 34 (one 32-pixel row segment) plus room for W = 16's two image
+    // rows of 16 + 2 (r05: the 16x16 level's 3x3 weight gradients on this kernel too)
+    constexpr int HALO = BKP + 4;
     constexpr int AREG = (HALO * RA + 1024 * WAVES - 1) / (1024 * WAVES) * WAVES * 1024;  // per stage
     constexpr int BREG = (BKP * RBB + 1024 * WAVES - 1) / (1024 * WAVES) * WAVES * 1024;
     constexpr int AI = AREG / (1024 * LW), BI = BREG / (1024 * LW);  // pieces per issuing wave
@@ -1535,8 +873,7 @@ __global__ __launch_bounds__((BM / 32) * (BN / 32) * 64, OCC) void wgrad_x3_row3
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave / WAVES_N, wn = wave % WAVES_N;
     const bool issuer = wave < LW;
-    const bool lag = (SCHED == 1 || SCHED == 2 || SCHED == 10) && wave >= 4;
-    static_assert(SCHED != 10 || (S == 4 && WAVES == 8), "schedule 10: four stages, waves w / w + 4");
+    const bool lag = LAG && wave >= 4;
     const int tiles_n = p.CB / BN, tiles_m = p.CA / BM;
     int idx = p.xcd ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
     const int tn = idx % tiles_n;
@@ -1552,31 +889,22 @@ __global__ __launch_bounds__((BM / 32) * (BN / 32) * 64, OCC) void wgrad_x3_row3
     const int nk = (pend - pbeg) / BKP;  // pps, P multiples of 32
 
     // loader: lane of piece j fills stage byte o = (j LW + wave) KB + 16 lane: pixel row o / RA,
-    // 16-B slot (o % RA) / 16, sourcing slot x3_tswz of it (kept in registers for SCHED 0; the
-    // staggered schedules recompute it per piece to stay within 256 VGPRs)
-    constexpr bool KEEP = SCHED == 0;
-    int arow[KEEP ? AI : 1], aele[KEEP ? AI : 1], brow[KEEP ? BI : 1], bele[KEEP ? BI : 1];
+    // 16-B slot (o % RA) / 16, sourcing slot x3_tswz16 of it (recomputed per piece to stay
+    // within 256 VGPRs)
     // W16 (launched for W = 16 only): two 18-row halo segments, swizzle by row mod 18 (its own
     // instance: one kernel holding both loops costs 1-6 spilled VGPRs)
-    static_assert(!W16 || M16, "W = 16 on the 16x16x32 kernel only");
     using W16T = std::integral_constant<bool, W16>;
     auto apiece = [&](int j, int& r, int& e, auto W16C) {
         constexpr bool TW = decltype(W16C)::value;
         const int o = ((j * LW + wave) * 64 + lane) * 16;
         r = o / RA;
-        e = (M16 ? x3_tswz16<RA>((o - r * RA) >> 4, TW ? r % 18 : r) : x3_tswz<RA>((o - r * RA) >> 4, r)) * 8;
+        e = x3_tswz16<RA>((o - r * RA) >> 4, TW ? r % 18 : r) * 8;
     };
     auto bpiece = [&](int j, int& r, int& e) {
         const int o = ((j * LW + wave) * 64 + lane) * 16;
         r = o / RBB;
-        e = (M16 ? x3_tswz16<RBB>((o - r * RBB) >> 4, r) : x3_tswz<RBB>((o - r * RBB) >> 4, r)) * 8;
+        e = x3_tswz16<RBB>((o - r * RBB) >> 4, r) * 8;
     };
-    if constexpr (KEEP) {
-#pragma unroll
-        for (int j = 0; j < AI; ++j) apiece(j, arow[j], aele[j], std::false_type{});
-#pragma unroll
-        for (int j = 0; j < BI; ++j) bpiece(j, brow[j], bele[j]);
-    }
     const uint16_t* a16 = (const uint16_t*)p.a + (size_t)(p.aoff + ca0) * 3;
     const uint16_t* b16 = (const uint16_t*)p.b + (size_t)(p.boff + cb0) * 3;
     const size_t rowa = 3 * (size_t)p.lda, rowb = 3 * (size_t)p.ldb;
@@ -1594,8 +922,7 @@ __global__ __launch_bounds__((BM / 32) * (BN / 32) * 64, OCC) void wgrad_x3_row3
 #pragma unroll
         for (int j = 0; j < AI; ++j) {
             int ar, ae;
-            if constexpr (KEEP) ar = arow[j], ae = aele[j];
-            else apiece(j, ar, ae, W16C);
+            apiece(j, ar, ae, W16C);
             // W = 16 (w16): halo row ar = 18 seg + xl + 1 holds image row y + seg + dy - 1,
             // column xl (the chunk is image rows y, y + 1; y even, H even)
             const int seg = TW ? ar / 18 : 0;
@@ -1608,145 +935,92 @@ __global__ __launch_bounds__((BM / 32) * (BN / 32) * 64, OCC) void wgrad_x3_row3
 #pragma unroll
         for (int j = 0; j < BI; ++j) {
             int br, be;
-            if constexpr (KEEP) br = brow[j], be = bele[j];
-            else bpiece(j, br, be);
+            bpiece(j, br, be);
             const bool ok = br < BKP;
             const uint16_t* g = ok ? b16 + (size_t)(pc + br) * rowb + be : zero;
             x3_dma16(g, base + AREG + (j * LW + wave) * 1024);
         }
     };
 
-    if constexpr (M16) {
-        // 16x16x32: per chunk ONE k-step of 32 pixels; a wave's 32 x 32 x 3-tap tile is 2 x 2
-        // blocks of 16 x 16 per tap.  Lane l of group g = l / 16 supplies the k values 8 g .. 8 g
-        // + 7 = pixel rows 4 g + qq (first transposed read) and 16 + 4 g + qq (second), the same
-        // rows for A' and B' (any k order sums the same products), column l & 15 of its block.
-        f32x4 hi[3][2][2], lo[3][2][2];
+    // 16x16x32: per chunk ONE k-step of 32 pixels; a wave's 32 x 32 x 3-tap tile is 2 x 2
+    // blocks of 16 x 16 per tap.  Lane l of group g = l / 16 supplies the k values 8 g .. 8 g
+    // + 7 = pixel rows 4 g + qq (first transposed read) and 16 + 4 g + qq (second), the same
+    // rows for A' and B' (any k order sums the same products), column l & 15 of its block.
+    f32x4 hi[3][2][2], lo[3][2][2];
 #pragma unroll
-        for (int d = 0; d < 3; ++d)
+    for (int d = 0; d < 3; ++d)
 #pragma unroll
-            for (int b = 0; b < 4; ++b)
+        for (int b = 0; b < 4; ++b)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) hi[d][b >> 1][b & 1][r] = lo[d][b >> 1][b & 1][r] = 0.f;
-        const int g = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
-        const int trow = 4 * g + qq;
-        auto slot = [](int col, int q) { return (col >> 5) * 12 + q * 4 + ((col & 31) >> 3); };
-        int aoff[3][2][3], boff[2][3];
+            for (int r = 0; r < 4; ++r) hi[d][b >> 1][b & 1][r] = lo[d][b >> 1][b & 1][r] = 0.f;
+    const int g = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
+    const int trow = 4 * g + qq;
+    auto slot = [](int col, int q) { return (col >> 5) * 12 + q * 4 + ((col & 31) >> 3); };
+    int aoff[3][2][3], boff[2][3];
 #pragma unroll
-        for (int bm = 0; bm < 2; ++bm) {
-            const int col = wm * 32 + 16 * bm + 4 * pp;
+    for (int bm = 0; bm < 2; ++bm) {
+        const int col = wm * 32 + 16 * bm + 4 * pp;
 #pragma unroll
-            for (int dx = 0; dx < 3; ++dx)
-#pragma unroll
-                for (int q = 0; q < 3; ++q)
-                    aoff[dx][bm][q] = (trow + dx) * RA + (x3_tswz16<RA>(slot(col, q), trow + dx) << 4) + ((col >> 2) & 1) * 8;
-            // (trow + dx <= 17: the same swizzle row for W = 16's row-mod-18 rule)
-            const int colb = wn * 32 + 16 * bm + 4 * pp;
+        for (int dx = 0; dx < 3; ++dx)
 #pragma unroll
             for (int q = 0; q < 3; ++q)
-                boff[bm][q] = AREG + trow * RBB + (x3_tswz16<RBB>(slot(colb, q), trow) << 4) + ((colb >> 2) & 1) * 8;
-        }
-        const unsigned sbase = x3_lds_u32(smem);
-        auto rd = [](x3_short4 (&f)[2], unsigned addr, auto ROWB) {
-            constexpr int rb = decltype(ROWB)::value;
-            f[0] = x3_tr16<0>(addr);
-            f[1] = x3_tr16<16 * rb>(addr);
-        };
-        // A' second read: pixel rows 16 + 4 g + qq sit 16 halo rows on, or 18 at W = 16 (a
-        // compile-time offset per loop instance: an added address per read costs 18 VGPRs)
-        auto rda = [](x3_short4 (&f)[2], unsigned addr, auto W16C) {
-            constexpr int off = decltype(W16C)::value ? 18 * RA : 16 * RA;
-            f[0] = x3_tr16<0>(addr);
-            f[1] = x3_tr16<off>(addr);
-        };
-        using IRB = std::integral_constant<int, RBB>;
-        auto mma = [&](const x3_short4 (&fa)[3][3][2], const x3_short4 (&fb)[2][3][2], int bm) {
+                aoff[dx][bm][q] = (trow + dx) * RA + (x3_tswz16<RA>(slot(col, q), trow + dx) << 4) + ((col >> 2) & 1) * 8;
+        // (trow + dx <= 17: the same swizzle row for W = 16's row-mod-18 rule)
+        const int colb = wn * 32 + 16 * bm + 4 * pp;
 #pragma unroll
-            for (int bn = 0; bn < 2; ++bn) {
-                bf16x8 b3[3];
+        for (int q = 0; q < 3; ++q)
+            boff[bm][q] = AREG + trow * RBB + (x3_tswz16<RBB>(slot(colb, q), trow) << 4) + ((colb >> 2) & 1) * 8;
+    }
+    const unsigned sbase = x3_lds_u32(smem);
+    auto rd = [](x3_short4 (&f)[2], unsigned addr, auto ROWB) {
+        constexpr int rb = decltype(ROWB)::value;
+        f[0] = x3_tr16<0>(addr);
+        f[1] = x3_tr16<16 * rb>(addr);
+    };
+    // A' second read: pixel rows 16 + 4 g + qq sit 16 halo rows on, or 18 at W = 16 (a
+    // compile-time offset per loop instance: an added address per read costs 18 VGPRs)
+    auto rda = [](x3_short4 (&f)[2], unsigned addr, auto W16C) {
+        constexpr int off = decltype(W16C)::value ? 18 * RA : 16 * RA;
+        f[0] = x3_tr16<0>(addr);
+        f[1] = x3_tr16<off>(addr);
+    };
+    using IRB = std::integral_constant<int, RBB>;
+    auto mma = [&](const x3_short4 (&fa)[3][3][2], const x3_short4 (&fb)[2][3][2], int bm) {
 #pragma unroll
-                for (int q = 0; q < 3; ++q) b3[q] = *(const bf16x8*)fb[bn][q];
+        for (int bn = 0; bn < 2; ++bn) {
+            bf16x8 b3[3];
 #pragma unroll
-                for (int dx = 0; dx < 3; ++dx) {
-                    bf16x8 a3[3];
+            for (int q = 0; q < 3; ++q) b3[q] = *(const bf16x8*)fb[bn][q];
 #pragma unroll
-                    for (int q = 0; q < 3; ++q) a3[q] = *(const bf16x8*)fa[dx][q];
-                    mfma_x3s16(a3, b3, hi[dx][bm][bn], lo[dx][bm][bn]);
-                }
+            for (int dx = 0; dx < 3; ++dx) {
+                bf16x8 a3[3];
+#pragma unroll
+                for (int q = 0; q < 3; ++q) a3[q] = *(const bf16x8*)fa[dx][q];
+                mfma_x3s16(a3, b3, hi[dx][bm][bn], lo[dx][bm][bn]);
             }
-        };
-        // schedule 10 (LG): waves 4..7 run each chunk's second 16-column half (bm = 1) at the
-        // start of the next chunk, re-reading its fragments from the chunk's stage (four
-        // stages, DMA two chunks ahead: a stage stays intact one chunk longer) -- the stagger
-        // of the halo GEMM's schedule 9 without held registers
-        auto loop = [&](auto W16C, auto LGC) {
-        constexpr bool LG = decltype(LGC)::value;
+        }
+    };
+    // schedule 10 (LG): waves 4..7 run each chunk's second 16-column half (bm = 1) at the
+    // start of the next chunk, re-reading its fragments from the chunk's stage (four
+    // stages, DMA two chunks ahead: a stage stays intact one chunk longer) -- the stagger
+    // of the halo GEMM's schedule 9 without held registers
+    auto loop = [&](auto W16C, auto LGC) {
+    constexpr bool LG = decltype(LGC)::value;
+    if (issuer) {
+#pragma unroll
+        for (int s = 0; s < DIST; ++s)
+            if (s < nk) issue(s, s, W16C);
+    }
+    for (int kc = 0; kc < nk; ++kc) {
         if (issuer) {
-#pragma unroll
-            for (int s = 0; s < DIST; ++s)
-                if (s < nk) issue(s, s, W16C);
+            if (DIST >= 2 && kc + 1 < nk) x3_wait_vm<GPC>();
+            else x3_wait_vm<0>();
         }
-        for (int kc = 0; kc < nk; ++kc) {
-            if (issuer) {
-                if (DIST >= 2 && kc + 1 < nk) x3_wait_vm<GPC>();
-                else x3_wait_vm<0>();
-            }
-            x3_barrier();
-            if (!LATE && issuer && kc + DIST < nk) issue(kc + DIST, (kc + DIST) % S, W16C);
-            if constexpr (LG) {
-                if (kc > 0) {
-                    const unsigned sp = sbase + ((kc + S - 1) % S) * STAGE;
-                    x3_short4 pb[2][3][2], pa[3][3][2];
-#pragma unroll
-                    for (int bn = 0; bn < 2; ++bn)
-#pragma unroll
-                        for (int q = 0; q < 3; ++q) rd(pb[bn][q], sp + boff[bn][q], IRB{});
-#pragma unroll
-                    for (int dx = 0; dx < 3; ++dx)
-#pragma unroll
-                        for (int q = 0; q < 3; ++q) rda(pa[dx][q], sp + aoff[dx][1][q], W16C);
-                    __builtin_amdgcn_sched_barrier(0);
-                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                    __builtin_amdgcn_sched_barrier(0);
-                    mma(pa, pb, 1);
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-            }
-            const unsigned sb = sbase + (kc % S) * STAGE;
-            x3_short4 fb[2][3][2], fa[3][3][2], fa1[3][3][2];
-#pragma unroll
-            for (int bn = 0; bn < 2; ++bn)
-#pragma unroll
-                for (int q = 0; q < 3; ++q) rd(fb[bn][q], sb + boff[bn][q], IRB{});
-#pragma unroll
-            for (int dx = 0; dx < 3; ++dx)
-#pragma unroll
-                for (int q = 0; q < 3; ++q) rda(fa[dx][q], sb + aoff[dx][0][q], W16C);
-            if (LATE && issuer && kc + DIST < nk) {
-                __builtin_amdgcn_sched_barrier(0);
-                issue(kc + DIST, (kc + DIST) % S, W16C);
-                __builtin_amdgcn_sched_barrier(0);
-            }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_sched_barrier(0);
-            if constexpr (LG) {
-                mma(fa, fb, 0);
-                continue;
-            }
-#pragma unroll
-            for (int dx = 0; dx < 3; ++dx)
-#pragma unroll
-                for (int q = 0; q < 3; ++q) rda(fa1[dx][q], sb + aoff[dx][1][q], W16C);
-            __builtin_amdgcn_sched_barrier(0);
-            mma(fa, fb, 0);
-            __builtin_amdgcn_sched_barrier(0);
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_sched_barrier(0);
-            mma(fa1, fb, 1);
-        }
+        x3_barrier();
+        if (!LATE && issuer && kc + DIST < nk) issue(kc + DIST, (kc + DIST) % S, W16C);
         if constexpr (LG) {
-            if (nk > 0) {  // the last chunk's second half (its stage is not restaged any more)
-                const unsigned sp = sbase + ((nk - 1) % S) * STAGE;
+            if (kc > 0) {
+                const unsigned sp = sbase + ((kc + S - 1) % S) * STAGE;
                 x3_short4 pb[2][3][2], pa[3][3][2];
 #pragma unroll
                 for (int bn = 0; bn < 2; ++bn)
@@ -1760,179 +1034,88 @@ __global__ __launch_bounds__((BM / 32) * (BN / 32) * 64, OCC) void wgrad_x3_row3
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                 __builtin_amdgcn_sched_barrier(0);
                 mma(pa, pb, 1);
+                __builtin_amdgcn_sched_barrier(0);
             }
         }
-        };
-        if (lag) loop(W16T{}, std::true_type{});
-        else loop(W16T{}, std::false_type{});
-        float* slab = p.slab + (size_t)split * p.Mw * p.Nw;
+        const unsigned sb = sbase + (kc % S) * STAGE;
+        x3_short4 fb[2][3][2], fa[3][3][2], fa1[3][3][2];
+#pragma unroll
+        for (int bn = 0; bn < 2; ++bn)
+#pragma unroll
+            for (int q = 0; q < 3; ++q) rd(fb[bn][q], sb + boff[bn][q], IRB{});
 #pragma unroll
         for (int dx = 0; dx < 3; ++dx)
 #pragma unroll
-            for (int bm = 0; bm < 2; ++bm)
-#pragma unroll
-                for (int bn = 0; bn < 2; ++bn)
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const int m = (dy * 3 + dx) * p.CA + ca0 + wm * 32 + 16 * bm + 4 * g + i;
-                        const int n = cb0 + wn * 32 + 16 * bn + (lane & 15);
-                        slab[(size_t)m * p.Nw + n] = hi[dx][bm][bn][i] + lo[dx][bm][bn][i];
-                    }
-        return;
-    }
-
-    f32x16 acc[3], acl[3];
-#pragma unroll
-    for (int i = 0; i < 3; ++i)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[i][r] = acl[i][r] = 0.f;
-
-    // transposed-read addresses (k-step 0): lane l of group g = l / 16 supplies row
-    // 8 (g >> 1) + qq (+ dx for A'), columns 16 (g & 1) + 4 pp of plane q
-    const int g = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
-    const int trow = 8 * (g >> 1) + qq;
-    auto slot = [](int col, int q) { return (col >> 5) * 12 + q * 4 + ((col & 31) >> 3); };
-    int aoff[3][3], boff[3];
-    {
-        const int col = wm * 32 + 16 * (g & 1) + 4 * pp;
+            for (int q = 0; q < 3; ++q) rda(fa[dx][q], sb + aoff[dx][0][q], W16C);
+        if (LATE && issuer && kc + DIST < nk) {
+            __builtin_amdgcn_sched_barrier(0);
+            issue(kc + DIST, (kc + DIST) % S, W16C);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (LG) {
+            mma(fa, fb, 0);
+            continue;
+        }
 #pragma unroll
         for (int dx = 0; dx < 3; ++dx)
 #pragma unroll
-            for (int q = 0; q < 3; ++q)
-                aoff[dx][q] = (trow + dx) * RA + (x3_tswz<RA>(slot(col, q), trow + dx) << 4) + ((col >> 2) & 1) * 8;
-        const int colb = wn * 32 + 16 * (g & 1) + 4 * pp;
-#pragma unroll
-        for (int q = 0; q < 3; ++q)
-            boff[q] = AREG + trow * RBB + (x3_tswz<RBB>(slot(colb, q), trow) << 4) + ((colb >> 2) & 1) * 8;
+            for (int q = 0; q < 3; ++q) rda(fa1[dx][q], sb + aoff[dx][1][q], W16C);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(fa, fb, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        mma(fa1, fb, 1);
     }
-
-    // fragments of one k-step: A' of the three dx taps, B'; read by ds_read_b64_tr_b16
-    struct Frag {
-        x3_short4 a[3][3][2], b[3][2];
-    };
-    auto load = [&](Frag& f, auto KK, unsigned sb) {
-        constexpr int kk = decltype(KK)::value;
+    if constexpr (LG) {
+        if (nk > 0) {  // the last chunk's second half (its stage is not restaged any more)
+            const unsigned sp = sbase + ((nk - 1) % S) * STAGE;
+            x3_short4 pb[2][3][2], pa[3][3][2];
 #pragma unroll
-        for (int dx = 0; dx < 3; ++dx)
+            for (int bn = 0; bn < 2; ++bn)
 #pragma unroll
-            for (int q = 0; q < 3; ++q) {
-                f.a[dx][q][0] = x3_tr16<kk * 16 * RA>(sb + aoff[dx][q]);
-                f.a[dx][q][1] = x3_tr16<kk * 16 * RA + 4 * RA>(sb + aoff[dx][q]);
-            }
+                for (int q = 0; q < 3; ++q) rd(pb[bn][q], sp + boff[bn][q], IRB{});
 #pragma unroll
-        for (int q = 0; q < 3; ++q) {
-            f.b[q][0] = x3_tr16<kk * 16 * RBB>(sb + boff[q]);
-            f.b[q][1] = x3_tr16<kk * 16 * RBB + 4 * RBB>(sb + boff[q]);
-        }
-    };
-    auto mma = [&](const Frag& f) {
-        bf16x8 b3[3];
+            for (int dx = 0; dx < 3; ++dx)
 #pragma unroll
-        for (int q = 0; q < 3; ++q) b3[q] = *(const bf16x8*)f.b[q];
-#pragma unroll
-        for (int dx = 0; dx < 3; ++dx) {
-            bf16x8 a3[3];
-#pragma unroll
-            for (int q = 0; q < 3; ++q) a3[q] = *(const bf16x8*)f.a[dx][q];
-            mfma_x3s(a3, b3, acc[dx], acl[dx]);
-        }
-    };
-    const unsigned sbase = x3_lds_u32(smem);
-    using K0 = std::integral_constant<int, 0>;
-    using K1 = std::integral_constant<int, 1>;
-
-    if (issuer) {
-#pragma unroll
-        for (int s = 0; s < DIST; ++s)
-            if (s < nk) issue(s, s, std::false_type{});
-    }
-    // one chunk loop per role (separately register-allocated paths)
-    auto run = [&](auto LAGC) {
-        constexpr bool LAG = decltype(LAGC)::value;
-        for (int kc = 0; kc < nk; ++kc) {
-            // one barrier per chunk: the issuing waves wait for chunk kc (chunk kc + 1 may stay
-            // in flight when the DMA runs two ahead), barrier -- every wave's DMA has landed and
-            // every wave has finished the reads of the slot about to be restaged -- then
-            // restage it with chunk kc + DIST
-            if (issuer) {
-                if (DIST >= 2 && kc + 1 < nk) x3_wait_vm<GPC>();
-                else x3_wait_vm<0>();
-            }
-            x3_barrier();
-            if (!LATE && issuer && kc + DIST < nk) issue(kc + DIST, (kc + DIST) % S, std::false_type{});
-            const unsigned sb = sbase + (kc % S) * STAGE;
-            Frag f0, f1;
-            if constexpr (LAG) {  // chunk kc - 1's second k-step, then this chunk's first
-                if (kc > 0) {
-                    load(f1, K1{}, sbase + ((kc + S - 1) % S) * STAGE);
-                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                    __builtin_amdgcn_sched_barrier(0);
-                    load(f0, K0{}, sb);
-                    __builtin_amdgcn_sched_barrier(0);
-                    mma(f1);
-                } else {
-                    load(f0, K0{}, sb);
-                }
-                __builtin_amdgcn_sched_barrier(0);
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                __builtin_amdgcn_sched_barrier(0);
-                mma(f0);
-            } else {
-                load(f0, K0{}, sb);
-                if (LATE && issuer && kc + DIST < nk) {  // the DMA behind the first fragment reads
-                    __builtin_amdgcn_sched_barrier(0);
-                    issue(kc + DIST, (kc + DIST) % S, std::false_type{});
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                __builtin_amdgcn_sched_barrier(0);
-                load(f1, K1{}, sb);
-                __builtin_amdgcn_sched_barrier(0);
-                mma(f0);
-                __builtin_amdgcn_sched_barrier(0);
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                __builtin_amdgcn_sched_barrier(0);
-                mma(f1);
-            }
-        }
-        if (LAG && nk > 0) {  // the last chunk's second k-step (its stage is not restaged any more)
-            Frag f1;
-            load(f1, K1{}, sbase + ((nk - 1) % S) * STAGE);
+                for (int q = 0; q < 3; ++q) rda(pa[dx][q], sp + aoff[dx][1][q], W16C);
+            __builtin_amdgcn_sched_barrier(0);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_sched_barrier(0);
-            mma(f1);
+            mma(pa, pb, 1);
         }
+    }
     };
-    if (lag) run(std::true_type{});
-    else run(std::false_type{});
-
-    const int li = lane & 31, lh = lane >> 5;
+    if (lag) loop(W16T{}, std::true_type{});
+    else loop(W16T{}, std::false_type{});
     float* slab = p.slab + (size_t)split * p.Mw * p.Nw;
 #pragma unroll
     for (int dx = 0; dx < 3; ++dx)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int m = (dy * 3 + dx) * p.CA + ca0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-            const int n = cb0 + wn * 32 + li;
-            slab[(size_t)m * p.Nw + n] = acc[dx][r] + acl[dx][r];
-        }
+        for (int bm = 0; bm < 2; ++bm)
+#pragma unroll
+            for (int bn = 0; bn < 2; ++bn)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int m = (dy * 3 + dx) * p.CA + ca0 + wm * 32 + 16 * bm + 4 * g + i;
+                    const int n = cb0 + wn * 32 + 16 * bn + (lane & 15);
+                    slab[(size_t)m * p.Nw + n] = hi[dx][bm][bn][i] + lo[dx][bm][bn][i];
+                }
 }
 
 // tiles (split accumulators): 0 = 128x128 (8 waves of 64x32), 1 = 64x64 (4 waves of 32x32);
 // three LDS stages of 32 pixels
 using WX0 = WTileX3<128, 128, 64, 32, 3, 1>;
 using WX1 = WTileX3<64, 64, 32, 32, 3, 1>;
-// 8 / 9 / 10 = 64x32 / 32x64 / 32x32 (waves of 32x32): 32-channel operands (option x3_n32, r05)
-using WX8 = WTileX3<64, 32, 32, 32, 3, 1>;
-using WX9 = WTileX3<32, 64, 32, 32, 3, 1>;
-using WX10 = WTileX3<32, 32, 32, 32, 3, 1>;
-#define WGRAD_X3_TILES(X) X(0, WX0) X(1, WX1) X(8, WX8) X(9, WX9) X(10, WX10)
+#define WGRAD_X3_TILES(X) X(0, WX0) X(1, WX1)
 
-template <int AMODE, int BMODE, class T, bool M16 = false>
+template <int AMODE, int BMODE, class T>
 static int wx3_go(const WgradArgs& a, hipStream_t s) {
     if (a.Mw % T::BM || a.Nw % T::BN || a.CA % T::BM || a.CB % T::BN || a.pps % T::BKP) return -1;
     const dim3 grid((a.Mw / T::BM) * (a.Nw / T::BN) * a.splits);
-    hipLaunchKernelGGL((wgrad_x3_kernel<AMODE, BMODE, T, M16>), grid, dim3(T::THREADS), 0, s, a);
+    hipLaunchKernelGGL((wgrad_x3_kernel<AMODE, BMODE, T>), grid, dim3(T::THREADS), 0, s, a);
     return (int)hipGetLastError();
 }
 
@@ -2168,14 +1351,9 @@ __global__ __launch_bounds__(256) void bn_dz_x3_kernel(const float* __restrict__
 }  // namespace
 
 int rowgemm_x3_tile_dims(int tile, int* bm, int* bn) {
-    if (tile == 4 || tile == 5 || tile == 6) {  // tap-row halo 256 x 128 / 256 x 64 / 128 x 64
+    if (tile == 4 || tile == 6) {  // tap-row halo 256 x 128 / 128 x 64
         *bm = tile == 6 ? 128 : 256;
         *bn = tile == 4 ? 128 : 64;
-        return 0;
-    }
-    if (tile == 8) {  // tap-row halo 512 x 64, 16-channel groups
-        *bm = 512;
-        *bn = 64;
         return 0;
     }
 #define X3_DIMS(id, T)  \
@@ -2190,17 +1368,17 @@ int rowgemm_x3_tile_dims(int tile, int* bm, int* bn) {
 }
 
 // A: x3 image (a16, lda channels per row, channel offset aoff), Bt: x3 weights [N][K]
-int launch_rowgemm_x3(const RowGemmArgs& a, int tile, hipStream_t s, int sched) {
+int launch_rowgemm_x3(const RowGemmArgs& a, int tile, hipStream_t s) {
     if (!a.a16 || !a.bt16 || !a.zero16 || a.M < 1 || a.K != gather_taps(a.amode) * a.C) return -1;
     if (a.aoff % 32 || a.lda % 32) return -1;
     if ((a.emode == E_STORE_BN || a.emode == E_RESID) != (a.ey != nullptr)) return -1;
     if (a.ascale || a.acoef) return -1;  // the x3 image already holds op(A)
     if (a.amode == G_CONV3) {
-        if (a.emode == E_BIAS_RELU_STATS) return x3_tile<G_CONV3, E_BIAS_RELU_STATS>(a, tile, s, sched);
-        if (a.emode == E_STATS) return x3_tile<G_CONV3, E_STATS>(a, tile, s, sched);
-        if (a.emode == E_STORE) return x3_tile<G_CONV3, E_STORE>(a, tile, s, sched);
-        if (a.emode == E_STORE_BN) return x3_tile<G_CONV3, E_STORE_BN>(a, tile, s, sched);
-        if (a.emode == E_ADD) return x3_tile<G_CONV3, E_ADD>(a, tile, s, sched);
+        if (a.emode == E_BIAS_RELU_STATS) return x3_tile<G_CONV3, E_BIAS_RELU_STATS>(a, tile, s);
+        if (a.emode == E_STATS) return x3_tile<G_CONV3, E_STATS>(a, tile, s);
+        if (a.emode == E_STORE) return x3_tile<G_CONV3, E_STORE>(a, tile, s);
+        if (a.emode == E_STORE_BN) return x3_tile<G_CONV3, E_STORE_BN>(a, tile, s);
+        if (a.emode == E_ADD) return x3_tile<G_CONV3, E_ADD>(a, tile, s);
     }
     if (a.amode == G_UP2) {
         if (a.emode == E_STORE_BN) return x3_tile<G_UP2, E_STORE_BN>(a, tile, s);
@@ -2221,12 +1399,11 @@ int k_to_x3(const float* src, int ld, int off, int C, const float* scale, const 
     return (int)hipGetLastError();
 }
 
-// tap-row tiles (BM ci x BN co per tap, three taps per block): 2 = 64x128, 3 = 128x64, 4 = 64x64,
-// 5 = 32x64, 6 = 64x32, 7 = 32x32 (5..7: option x3_n32, r05)
-static const int WX3R3_DIMS[8][2] = {{0, 0}, {0, 0}, {64, 128}, {128, 64}, {64, 64}, {32, 64}, {64, 32}, {32, 32}};
+// tap-row tiles (BM ci x BN co per tap, three taps per block): 2 = 64x128, 3 = 128x64, 4 = 64x64
+static const int WX3R3_DIMS[5][2] = {{0, 0}, {0, 0}, {64, 128}, {128, 64}, {64, 64}};
 
 int wgrad_x3_tile_dims(int tile, int* bm, int* bn) {
-    if (tile >= 2 && tile <= 7) {
+    if (tile >= 2 && tile <= 4) {
         *bm = WX3R3_DIMS[tile][0];
         *bn = WX3R3_DIMS[tile][1];
         return 0;
@@ -2247,67 +1424,36 @@ int wgrad_x3_tile_dims(int tile, int* bm, int* bn) {
 // G_CONV3, B' G_IDENT) and ConvT (A' G_IDENT, B' G_UP2); no bias column sums.
 // (r04, not kept: the tap-row tiles on 64-pixel chunks, four k-steps per barrier pair:
 // bit-identical, config 2 within noise, profiles/r04_x3_halo_ab.txt)
-int launch_wgrad_x3(const WgradArgs& a, int tile, hipStream_t s, int sched) {
+int launch_wgrad_x3(const WgradArgs& a, int tile, hipStream_t s) {
     if (a.ascale || a.bcoef || a.bias_slab || !a.zero16 || a.P < 1) return -1;
     if (a.aoff % 32 || a.boff % 32 || a.lda % 32 || a.ldb % 32) return -1;
-    if (tile >= 2 && tile <= 7) {  // tap-row kernel: 3x3 convs, W % 32 == 0
+    if (tile >= 2 && tile <= 4) {  // tap-row kernel: 3x3 convs, W % 32 == 0 or W = 16 with an even H
         int bm = 0, bn = 0;
         wgrad_x3_tile_dims(tile, &bm, &bn);
-        // W % 32 == 0, or (16x16x32 schedules, tiles 2..4) W = 16 with an even H
-        const bool w16ok = a.W == 16 && a.H % 2 == 0 && sched >= 8 && tile <= 4;
+        const bool w16 = a.W == 16 && a.H % 2 == 0;
         if (a.amode != G_CONV3 || a.bmode != G_IDENT || a.Mw != 9 * a.CA || a.Nw != a.CB ||
-            a.CA % bm || a.CB % bn || (a.W % 32 && !w16ok) || a.pps % 32 || a.P % 32)
+            a.CA % bm || a.CB % bn || (a.W % 32 && !w16) || a.pps % 32 || a.P % 32)
             return -1;
         const dim3 grid((a.CA / bm) * 3 * (a.CB / bn) * a.splits);
-        if (tile == 2 && sched == 1)
-            hipLaunchKernelGGL((wgrad_x3_row3_kernel<64, 128, 4, 1, 1>), grid, dim3(512), 0, s, a);
-        else if (tile == 2 && sched == 2)
-            hipLaunchKernelGGL((wgrad_x3_row3_kernel<64, 128, 4, 1, 2>), grid, dim3(512), 0, s, a);
-        else if (tile == 2 && sched == 3)
-            hipLaunchKernelGGL((wgrad_x3_row3_kernel<64, 128, 3, 1, 3>), grid, dim3(512), 0, s, a);
-        else if (tile == 3 && sched == 3)
-            hipLaunchKernelGGL((wgrad_x3_row3_kernel<128, 64, 3, 1, 3>), grid, dim3(512), 0, s, a);
-        else if (a.W == 16 && tile == 2 && sched == 10)  // 16x16x32 at W = 16 (w16ok: sched >= 8)
-            hipLaunchKernelGGL((wgrad_x3_row3_kernel<64, 128, 4, 1, 10, true>), grid, dim3(512), 0, s, a);
-        else if (a.W == 16 && tile == 2)
-            hipLaunchKernelGGL((wgrad_x3_row3_kernel<64, 128, 3, 1, 9, true>), grid, dim3(512), 0, s, a);
-        else if (a.W == 16 && tile == 3)
-            hipLaunchKernelGGL((wgrad_x3_row3_kernel<128, 64, 3, 1, 8, true>), grid, dim3(512), 0, s, a);
-        else if (a.W == 16 && tile == 4)
-            hipLaunchKernelGGL((wgrad_x3_row3_kernel<64, 64, 2, 2, 8, true>), grid, dim3(256), 0, s, a);
-        else if (tile == 2 && sched == 8)  // 16x16x32 (r05)
-            hipLaunchKernelGGL((wgrad_x3_row3_kernel<64, 128, 3, 1, 8>), grid, dim3(512), 0, s, a);
-        else if (tile == 2 && sched == 9)
-            hipLaunchKernelGGL((wgrad_x3_row3_kernel<64, 128, 3, 1, 9>), grid, dim3(512), 0, s, a);
-        else if (tile == 2 && sched == 10)  // + waves 4..7 half a chunk behind (re-read)
-            hipLaunchKernelGGL((wgrad_x3_row3_kernel<64, 128, 4, 1, 10>), grid, dim3(512), 0, s, a);
-        else if (tile == 3 && sched >= 8)
-            hipLaunchKernelGGL((wgrad_x3_row3_kernel<128, 64, 3, 1, 8>), grid, dim3(512), 0, s, a);
-        else if (tile == 4 && sched >= 8)
-            hipLaunchKernelGGL((wgrad_x3_row3_kernel<64, 64, 2, 2, 8>), grid, dim3(256), 0, s, a);
+        // 64 x 128: four stages with the stagger (r05 schedule 10); 128 x 64 / 64 x 64 without it
+        if (tile == 2 && w16)
+            hipLaunchKernelGGL((wgrad_x3_row3_kernel<64, 128, 4, 1, true, true>), grid, dim3(512), 0, s, a);
         else if (tile == 2)
-            hipLaunchKernelGGL((wgrad_x3_row3_kernel<64, 128>), grid, dim3(512), 0, s, a);
+            hipLaunchKernelGGL((wgrad_x3_row3_kernel<64, 128, 4, 1, true>), grid, dim3(512), 0, s, a);
+        else if (tile == 3 && w16)
+            hipLaunchKernelGGL((wgrad_x3_row3_kernel<128, 64, 3, 1, false, true>), grid, dim3(512), 0, s, a);
         else if (tile == 3)
-            hipLaunchKernelGGL((wgrad_x3_row3_kernel<128, 64>), grid, dim3(512), 0, s, a);
-        else if (tile == 4)  // 64 x 64: four waves, two LDS stages, two blocks per CU
-            hipLaunchKernelGGL((wgrad_x3_row3_kernel<64, 64, 2, 2>), grid, dim3(256), 0, s, a);
-        else if (tile == 5)  // the 32-channel tiles: one or two waves, three stages (LDS: 2-4 blocks per CU)
-            hipLaunchKernelGGL((wgrad_x3_row3_kernel<32, 64, 3, 1>), grid, dim3(128), 0, s, a);
-        else if (tile == 6)
-            hipLaunchKernelGGL((wgrad_x3_row3_kernel<64, 32, 3, 1>), grid, dim3(128), 0, s, a);
+            hipLaunchKernelGGL((wgrad_x3_row3_kernel<128, 64, 3, 1>), grid, dim3(512), 0, s, a);
+        else if (w16)  // 64 x 64: four waves, two LDS stages, two blocks per CU
+            hipLaunchKernelGGL((wgrad_x3_row3_kernel<64, 64, 2, 2, false, true>), grid, dim3(256), 0, s, a);
         else
-            hipLaunchKernelGGL((wgrad_x3_row3_kernel<32, 32, 3, 1>), grid, dim3(64), 0, s, a);
+            hipLaunchKernelGGL((wgrad_x3_row3_kernel<64, 64, 2, 2>), grid, dim3(256), 0, s, a);
         return (int)hipGetLastError();
     }
 #define WX3G(AM, BMD)                                        \
     do {                                                     \
-        if (tile == 0 && sched >= 8) return wx3_go<AM, BMD, WX0, true>(a, s); \
-        if (tile == 1 && sched >= 8) return wx3_go<AM, BMD, WX1, true>(a, s); \
         if (tile == 0) return wx3_go<AM, BMD, WX0>(a, s);    \
         if (tile == 1) return wx3_go<AM, BMD, WX1>(a, s);    \
-        if (tile == 8) return wx3_go<AM, BMD, WX8>(a, s);    \
-        if (tile == 9) return wx3_go<AM, BMD, WX9>(a, s);    \
-        if (tile == 10) return wx3_go<AM, BMD, WX10>(a, s);  \
         return -1;                                           \
     } while (0)
     if (a.amode == G_CONV3 && a.bmode == G_IDENT) WX3G(G_CONV3, G_IDENT);
@@ -2346,15 +1492,4 @@ int k_bn_dz_x3_pool(const float* y, int ld, int off, int64_t P, int C, const flo
     hipLaunchKernelGGL(bn_dz_x3_kernel<2>, dim3(x3_dz_blocks(P)), dim3(256), 0, s, nullptr, y, ld, off, P, C,
                        coef, mask, dz3, bpart, x3_rows_per_block(P), DzHead{}, pl);
     return (int)hipGetLastError();
-}
-
-// speed-of-light ablations of tile 0 on the E_STORE 3x3 GEMM (tools/x3_probe.hip): -2 when
-// not applicable
-int launch_rowgemm_x3_xp(const RowGemmArgs& a, int xp, hipStream_t s) {
-    if (a.amode != G_CONV3 || a.emode != E_STORE) return -2;
-#define XPX(v) \
-    if (xp == v) return x3_go<G_CONV3, E_STORE, TX0, v>(a, s);
-    XPX(1) XPX(2) XPX(3) XPX(4) XPX(8) XPX(12) XPX(15) XPX(7)
-#undef XPX
-    return -2;
 }

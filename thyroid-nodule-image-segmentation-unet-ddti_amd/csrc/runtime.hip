@@ -107,7 +107,6 @@ struct Options {
                                    // (r02 sweep 512..2048: 1536 best, 391 vs 386 img/s)
     int wgrad_tile_w = 0;      // f32 wgrad tile, both channel counts multiples of 128
     int wgrad_tile_n = 7;      // ... 64-channel layers (64x64, 3 waves/SIMD)
-    int wgrad16_tile = 0;      // register-staged bf16 wgrad tile (128-multiples)
     int tile_n128 = -1;        // f32 row-GEMM tile, N % 128 == 0 (-1 = pick_tile's default)
     int tile_n128_dgrad = -1;  // ... dgrad-type
     int tile_n64 = 19;         // ... N = 64 outputs (forward-type)
@@ -121,21 +120,13 @@ struct Options {
     int tile_convt_dgrad = 26; // ConvT input gradient (-1 = tile_n128_dgrad's; 26 = pipelined
                                // 128x64 at three blocks per CU: the K = 4 Cout short-K GEMMs
                                // with their BN-partials epilogue, 1.33 -> 1.15 ms per step)
-    int tile16_n128 = 6;       // register-staged bf16 row-GEMM tiles
-    int tile16_n128_dgrad = 6;
-    int tile16_n64 = 1;
     int rg16 = 1;              // bf16 row GEMMs on the LDS-DMA kernel (0: register-staged)
     int rg16_tile = -1;        // its tile (-1 = per GEMM, rg16_tile())
-    int rg16_xp = 0;           // speed-of-light ablation of the forward rg16 GEMMs (garbage
-                               // results; A/B timing only, kernels_gemm16.hip XP)
     int rg16_n128 = 20;        // rg16 tile of the GEMMs whose N is not a multiple of 256 (the
                                // 128-output layers; -1 = 128x128, 6 = 512x128, 20 = 512x128 tap-row
                                // halo for 3x3 convs, 6 elsewhere; r04 config 4: 122.7 -> 124.8
                                // img/s with 20, 121.9 with 6)
     int rg16_n128_bn = 0;      // ... also for the short-K E_STORE_BN GEMMs (else 128x128)
-    int rg16_sched = 0;        // the bf16 halo kernel's schedule (0 = r04, 1 = waves 4..7 run each
-                               // stage's last tap after the next barrier, 2 = 1 + the DMA after the
-                               // first tap's reads; bit-identical)
     int rg16_r3 = 1;           // 256x256 3x3-conv GEMMs (W >= 16) on the tap-row halo kernel (tile 19;
                                // config 4: +0.9..1.2 % over three A/B pairs, r03)
     int wg16 = 1;              // bf16 3x3 wgrad on the LDS-DMA transposed-read kernel
@@ -167,45 +158,18 @@ struct Options {
     int x3_wblocks = 1536;     // split-K target (blocks) of its 128x128 weight gradients
     int x3_n64 = 2;            // its row-GEMM tile for 64 outputs (2 = 128x64, 3 = 256x64)
     int x3_r3 = 1;             // its 256x128 3x3 GEMMs on the tap-row halo kernel (tile 4)
-    int x3_r3_sched = 9;       // the halo kernel's wave schedule (kernels_gemm_x3.hip X3R3Sched:
-                               // who issues the LDS-DMA, stagger of waves 4..7; bit-identical).
-                               // r05 (profiles/r05_halo_sched.txt): 1 (stagger + DMA after the
-                               // first k-step's reads) +5..13 % per layer, config 2 591 -> 603 img/s;
-                               // 8..10 the same on 16x16x32 MFMAs (x3r3_body16), 9 = 1's
-                               // schedule: -4..-13 % per launch vs 1 (profiles/r05_halo_m16.txt)
     int x3_wwaves = 3;         // tap-row x3 weight gradients: split-K so the grid is this many full
                                // waves of block slots (0 = the x3_wblocks target; r05,
                                // profiles/r05_wwaves_ab.txt)
     int x3_wwaves1 = 3;        // the same for the one-tap x3 weight gradients (ConvT, 8x8):
                                // +0.45 % (profiles/r05_wwaves_ab.txt)
-    int x3_convt_tile = -1;    // x3 ConvT forward / dgrad tile override (0..3; -1 = x3_tile)
     int pool_fuse = 1;         // x3 path: the encoder block's second conv recomputes its `do` from
                                // the max-pool backward's inputs instead of maxpool_bwd storing it
     int head_fuse = 1;         // x3 path, one output channel: the last conv's dz pass recomputes
                                // `do` from the head instead of head_bwd storing it (r05)
-    int x3_1tap16 = 0;         // the one-tap x3 tiles (0 / 1 row GEMM, 0 / 1 weight gradient) follow
-                               // the 16x16x32 schedules (x3_r3_sched / x3_wsched >= 8; r05):
-                               // config 2 within noise (profiles/r05_1tap16_ab.txt), so off
-    int x3_n32 = 0;            // x3 also for 32-multiple channel counts (r05; narrow widths)
-    int x3_n64_r3 = 6;         // halo tile of the 64-output 3x3 GEMMs: 5 = 256x64 (8 waves, one
-                               // block per CU), 6 = 128x64 (4 waves, two blocks per CU; on the
-                               // 16x16x32 schedules +0.2 % over 5, profiles/r05_halo_k16.txt), 8 =
-                               // 512x64 over 16-channel groups (r05: 1.103 vs 1.032 ms at level 0,
-                               // profiles/r05_halo_k16.txt -- not faster, kept as an option)
-    int wg16_split = 1;        // (r06) bf16 tap-row weight gradients: split-K by whole waves (wgrad_cfg);
-                               // 0 = r05's 1536-block target
     int tile_group = 1;        // (r06) row-GEMM tile order of the LDS-DMA kernels (rg16, x3): 1 = grouped
                                // where the N tiles are many (tile_group_auto), 0 = M-major (r05);
                                // bit-identical
-    int x3_wsched = 10;        // the tap-row weight gradient's schedule (0 = r04, 1 = four stages
-                               // with waves 4..7 half a chunk behind, 2 = 1 with waves 0..3
-                               // issuing every DMA (64x128 only), 3 = the DMA after the first
-                               // k-step's reads (64x128, 128x64); bit-identical); 8 / 9 = 0 / 3
-                               // on 16x16x32 MFMAs (64x128, 128x64, 64x64): config 2 +1.6 / +1.9 %
-                               // (profiles/r05_wgrad_m16_ab.txt); 10 = 9 with waves 4..7 running
-                               // each chunk's second half after the next barrier from re-read
-                               // fragments (64x128; four stages): +1.5 % over 9
-                               // (profiles/r05_wgrad_sched10_ab.txt)
 };
 struct OptionDesc {
     const char* name;
@@ -222,7 +186,6 @@ const OptionDesc OPTION_TABLE[] = {
     {"wgrad16_blocks", &Options::wgrad16_blocks},
     {"wgrad_tile_w", &Options::wgrad_tile_w},
     {"wgrad_tile_n", &Options::wgrad_tile_n},
-    {"wgrad16_tile", &Options::wgrad16_tile},
     {"tile_n128", &Options::tile_n128},
     {"tile_n128_dgrad", &Options::tile_n128_dgrad},
     {"tile_n64", &Options::tile_n64},
@@ -231,17 +194,12 @@ const OptionDesc OPTION_TABLE[] = {
     {"tile_convt64", &Options::tile_convt64},
     {"tile_convt", &Options::tile_convt},
     {"tile_convt_dgrad", &Options::tile_convt_dgrad},
-    {"tile16_n128", &Options::tile16_n128},
-    {"tile16_n128_dgrad", &Options::tile16_n128_dgrad},
-    {"tile16_n64", &Options::tile16_n64},
     {"rg16", &Options::rg16},
     {"rg16_tile", &Options::rg16_tile},
     {"rg16_bn_k", &Options::rg16_bn_k},
     {"rg16_r3", &Options::rg16_r3},
-    {"rg16_sched", &Options::rg16_sched},
     {"rg16_n128", &Options::rg16_n128},
     {"rg16_n128_bn", &Options::rg16_n128_bn},
-    {"rg16_xp", &Options::rg16_xp},
     {"wg16", &Options::wg16},
     {"wg16_tile", &Options::wg16_tile},
     {"wg16_r3", &Options::wg16_r3},
@@ -256,24 +214,18 @@ const OptionDesc OPTION_TABLE[] = {
     {"x3_wblocks", &Options::x3_wblocks},
     {"x3_n64", &Options::x3_n64},
     {"x3_r3", &Options::x3_r3},
-    {"x3_r3_sched", &Options::x3_r3_sched},
-    {"x3_n32", &Options::x3_n32},
-    {"x3_n64_r3", &Options::x3_n64_r3},
-    {"x3_wsched", &Options::x3_wsched},
-    {"x3_1tap16", &Options::x3_1tap16},
     {"head_fuse", &Options::head_fuse},
-    {"x3_convt_tile", &Options::x3_convt_tile},
     {"pool_fuse", &Options::pool_fuse},
     {"x3_wwaves", &Options::x3_wwaves},
     {"x3_wwaves1", &Options::x3_wwaves1},
     {"tile_group", &Options::tile_group},
-    {"wg16_split", &Options::wg16_split},
 };
 
 }  // namespace
 
 struct unet_ctx {
     int device = 0;
+    int cus = 256;  // compute units of the device (split-K sizing by whole waves of block slots)
     int in_ch = 1, out_ch = 1;
     int variant = UNET_VARIANT_MODEL;
     int base = 64, depth = 4;  // base: channels of level 0 as the kernels see them (padded)
@@ -680,10 +632,10 @@ struct WgradCfg {
 WgradCfg wgrad_cfg(const unet_ctx* c, int CA, int tapsA, int CB, int tapsB, int64_t P, bool bf16,
                    int row_w = 0) {
     const int r3 = c->opt.wgrad_row3, r3t = c->opt.wgrad_row3_tile;
-    const int tw = c->opt.wgrad_tile_w, tn = c->opt.wgrad_tile_n, t16 = c->opt.wgrad16_tile;
+    const int tw = c->opt.wgrad_tile_w, tn = c->opt.wgrad_tile_n;
     WgradCfg w;
     if (bf16) {  // kernels_gemm.hip WGRAD16_TILES
-        w.tile = (CA % 128 == 0 && CB % 128 == 0) ? t16 : CA % 128 == 0 ? 3 : CB % 128 == 0 ? 4 : 2;
+        w.tile = (CA % 128 == 0 && CB % 128 == 0) ? 0 : CA % 128 == 0 ? 3 : CB % 128 == 0 ? 4 : 2;
         wgrad16_tile_dims(w.tile, &w.bm, &w.bn, &w.bkp);
     } else {
         if (CA % 128 == 0 && CB % 128 == 0)
@@ -734,10 +686,10 @@ WgradCfg wgrad_cfg(const unet_ctx* c, int CA, int tapsA, int CB, int tapsB, int6
     // blocks, and the kernel took three block durations instead of two.  Instead pick the split
     // count s minimising waves(s) x chunks per block(s) + the slab traffic of s splits (the
     // one-tap kernel, option wg16_r3 = 0, gets the same partition: bit-identical).
-    if (bf16 && c->opt.wg16_split && tapsA == 9 && tapsB == 1 && row_w > 0 && row_w % 64 == 0 &&
+    if (bf16 && tapsA == 9 && tapsB == 1 && row_w > 0 && row_w % 64 == 0 &&
         CA % 128 == 0 && CB % 128 == 0 && P % 64 == 0) {
         const int64_t t3 = (int64_t)(CA / 128) * 3 * (CB / 128);
-        const int64_t slots = 256;
+        const int64_t slots = c->cus;
         double best = -1;
         for (int64_t sc = 1; sc <= maxs; ++sc) {
             const int64_t waves = (t3 * sc + slots - 1) / slots;
@@ -830,65 +782,37 @@ bool convt_wg16_on(const unet_ctx* c, int cin, int cout) {
 // weight-gradient GEMMs on x3 images (exact three-way bf16 splits of the f32 operands, six
 // MFMA products, split f32 accumulators: fp64 error ~3x below the f32 MFMA kernels',
 // profiles/r04_x3_probe_*.txt).  The residual network's 1x1 skip GEMMs keep the f32 kernels.
-// Option x3_n32 (r05) extends it to 32-multiple channel counts (the reference grid's narrow
-// widths: 32 / 96 channels) on the 128x32 row tile and the 32-wide weight-gradient tiles.
+// (r05, removed in r06: option x3_n32, x3 for the 32-multiple channel counts of the reference
+// grid's narrow widths on a 128 x 32 row tile and 32-wide weight-gradient tiles -- slower than the
+// f32 MFMA kernels there, profiles/r05_x3_n32_ab.txt.)
 bool x3_conv_on(const unet_ctx* c, int cin, int cout) {
-    const int q = c->opt.x3_n32 ? 32 : 64;
-    return c->opt.x3 && !c->bf16 && cin % q == 0 && cout % q == 0;
+    return c->opt.x3 && !c->bf16 && cin % 64 == 0 && cout % 64 == 0;
 }
 bool x3_convt_on(const unet_ctx* c, int cin, int cout) { return x3_conv_on(c, cin, cout); }
 
-// row-GEMM tile: 256x128 (one block of 8 waves per CU) unless that grid leaves CUs idle
-// (128x128), 128x64 for the 64-output GEMMs
-// the schedule argument of launch_rowgemm_x3 / launch_wgrad_x3 for a tile: the one-tap tiles
-// take the 16x16x32 kernels from schedules >= 8 unless option x3_1tap16 is off
-int x3_rsched(const unet_ctx* c, int tile) {
-    const int sc = c->opt.x3_r3_sched;
-    return (tile >= 4 && tile <= 6) || c->opt.x3_1tap16 ? sc : 0;
-}
-int x3_wsched(const unet_ctx* c, int tile) {
-    const int sc = c->opt.x3_wsched;
-    return (tile >= 2 && tile <= 7) || c->opt.x3_1tap16 ? sc : 0;
-}
-
-int x3_tile(const unet_ctx* c, const RowGemmArgs& g);
-// ConvT forward / dgrad (short K = Cin or 4 Cout): option x3_convt_tile overrides the tile
-// (r05 A/B: the epilogue-heavy ConvT GEMMs on a two-blocks-per-CU tile)
-int x3_convt_tile(const unet_ctx* c, const RowGemmArgs& g) {
-    const int t = c->opt.x3_convt_tile;
-    int bm = 0, bn = 0;
-    if (t >= 0 && t <= 3 && rowgemm_x3_tile_dims(t, &bm, &bn) == 0 && g.N % bn == 0 &&
-        (g.emode != E_CONVT || g.cout % bn == 0 || bn % g.cout == 0))
-        return t;
-    return x3_tile(c, g);
-}
-
+// row-GEMM tile: the tap-row halo kernel for 3x3 convs (4 = 256 x 128, one block of 8 waves per
+// CU; 6 = 128 x 64 for the 64-output GEMMs, two blocks per CU); otherwise the one-tap tiles
+// (0 = 256 x 128, 1 = 128 x 128 where the 256-row grid would leave CUs idle, 2 / 3 = 128 x 64 /
+// 256 x 64: option x3_n64)
 int x3_tile(const unet_ctx* c, const RowGemmArgs& g) {
     auto fits = [&](int t) {
         int bm = 0, bn = 0;
         if (rowgemm_x3_tile_dims(t, &bm, &bn) != 0 || g.N % bn) return false;
         return g.emode != E_CONVT || g.cout % bn == 0 || bn % g.cout == 0;
     };
-    // tile 4: the tap-row halo kernel (3x3 convs on rows of 16 .. 256k pixels, option x3_r3)
+    // the halo tiles: 3x3 convs on rows of 16 .. 256k pixels (option x3_r3)
     const bool r3ok = g.amode == G_CONV3 && g.W >= 16 && (256 % g.W == 0 || g.W % 256 == 0);
-    const bool r3ok8 = g.amode == G_CONV3 && g.W >= 16 && (512 % g.W == 0 || g.W % 512 == 0);
     const int ft = c->opt.x3_tile;
-    if (ft >= 0 && fits(ft) && ((ft < 4 || ft == 7) || (ft >= 4 && ft <= 6 && r3ok) || (ft == 8 && r3ok8)))
-        return ft;
+    if (ft >= 0 && fits(ft) && (ft < 4 || r3ok)) return ft;
     if (g.N % 128 == 0 && fits(0)) {
         const int64_t blocks = (int64_t)(g.M + 255) / 256 * (g.N / 128);
         if (blocks < 256) return 1;
         return c->opt.x3_r3 && r3ok ? 4 : 0;
     }
-    // 64 outputs: a halo tile (5 = 256 x 64, one block per CU; 6 = 128 x 64, two blocks per
-    // CU: option x3_n64_r3) where the 256-row grid fills the chip
-    if (g.N % 64 == 0 && c->opt.x3_r3 && r3ok && (int64_t)(g.M + 255) / 256 >= 512) {
-        if (c->opt.x3_n64_r3 == 8 && r3ok8) return 8;
-        return c->opt.x3_n64_r3 == 6 ? 6 : 5;
-    }
-    // 32-multiple outputs, or a ConvT whose cout is not a 64-tile fit (option x3_n32): 128 x 32
-    if (g.N % 64 || !fits(c->opt.x3_n64)) return 7;
-    return c->opt.x3_n64;
+    // 64 outputs: the 128 x 64 halo tile where the 256-row grid fills the chip (r05: 0.2 % over
+    // a 256 x 64 halo tile, 1.032 vs 1.103 ms for a 512 x 64 one, profiles/r05_halo_k16.txt)
+    if (g.N % 64 == 0 && c->opt.x3_r3 && r3ok && (int64_t)(g.M + 255) / 256 >= 512) return 6;
+    return fits(c->opt.x3_n64) ? c->opt.x3_n64 : -1;
 }
 
 // weight gradient: 128x128 tile where both channel counts allow it, else 64x64; split-K over
@@ -900,26 +824,21 @@ WgradCfg x3_wgrad_cfg(const unet_ctx* c, int CA, int tapsA, int CB, int tapsB, i
                       int row_w = 0, int row_h = 0) {
     WgradCfg w{};
     w.tile = (CA % 128 == 0 && CB % 128 == 0) ? 0 : 1;
-    // tap-row kernel: rows of 32k pixels, or (16x16x32 schedules, r05) 16-pixel rows in pairs
-    const bool w16 = row_w == 16 && row_h % 2 == 0 && c->opt.x3_wsched >= 8 && CA % 64 == 0 && CB % 64 == 0;
+    // tap-row kernel: rows of 32k pixels, or (r05) 16-pixel rows in pairs
+    const bool w16 = row_w == 16 && row_h % 2 == 0 && CA % 64 == 0 && CB % 64 == 0;
     const bool r3 = tapsA == 9 && tapsB == 1 && ((row_w % 32 == 0 && row_w > 0) || w16);
     if (r3 && CA % 64 == 0 && CB % 128 == 0) w.tile = 2;
     else if (r3 && CA % 128 == 0 && CB % 64 == 0) w.tile = 3;
     else if (r3 && CA % 64 == 0 && CB % 64 == 0) w.tile = 4;
-    if (CA % 64 || CB % 64) {  // 32-channel operands (option x3_n32): tap-row 32x64 / 64x32 /
-                               // 32x32 (5 / 6 / 7), one-tap 64x32 / 32x64 / 32x32 (8 / 9 / 10)
-        const int k = CA % 64 == 0 ? 1 : CB % 64 == 0 ? 0 : 2;  // 0: BM 32, 1: BN 32, 2: both
-        w.tile = r3 ? (k == 0 ? 5 : k == 1 ? 6 : 7) : (k == 1 ? 8 : k == 0 ? 9 : 10);
-    }
     if (c->opt.x3_wtile >= 0) {
         int bm = 0, bn = 0;
         const int t = c->opt.x3_wtile;
-        if (wgrad_x3_tile_dims(t, &bm, &bn) == 0 && CA % bm == 0 && CB % bn == 0 && (t < 2 || t > 7 || r3))
+        if (wgrad_x3_tile_dims(t, &bm, &bn) == 0 && CA % bm == 0 && CB % bn == 0 && (t < 2 || r3))
             w.tile = t;
     }
     wgrad_x3_tile_dims(w.tile, &w.bm, &w.bn);
     w.bkp = 32;
-    const bool tap_row = w.tile >= 2 && w.tile <= 7;
+    const bool tap_row = w.tile >= 2 && w.tile <= 4;
     const int64_t tiles = tap_row ? (int64_t)(CA / w.bm) * 3 * (CB / w.bn)
                                   : (int64_t)(tapsA * CA / w.bm) * (tapsB * CB / w.bn);
     // blocks per 128x128 one-tap block of work: by area (one-tap), half that (tap-row)
@@ -931,10 +850,10 @@ WgradCfg x3_wgrad_cfg(const unet_ctx* c, int CA, int tapsA, int CB, int tapsB, i
     pps = (pps + 255) / 256 * 256;
     const int ww = tap_row ? c->opt.x3_wwaves : c->opt.x3_wwaves1;
     if (w.tile <= 4 && ww > 0) {
-        // (r05) exactly `ww` full waves of block slots (256 CUs x blocks per CU): at most
-        // that many blocks, pixel splits in 32-pixel steps.  The 256-pixel rounding above can
-        // land a few blocks past a wave boundary (1024: 2049 blocks on 2048 slots, -4 %)
-        const int64_t slots = 256LL * (w.tile == 4 || w.tile == 1 ? 2 : 1) * ww;
+        // (r05) exactly `ww` full waves of block slots (CUs x blocks per CU): at most that many
+        // blocks, pixel splits in 32-pixel steps.  The 256-pixel rounding above can land a few
+        // blocks past a wave boundary (1024: 2049 blocks on 2048 slots, -4 %)
+        const int64_t slots = (int64_t)c->cus * (w.tile == 4 || w.tile == 1 ? 2 : 1) * ww;
         const int64_t s = std::max<int64_t>(1, slots / tiles);
         pps = (P + s - 1) / s;
         pps = (pps + 31) / 32 * 32;
@@ -962,7 +881,7 @@ void use_x3(const unet_ctx* c, const Plan& p, RowGemmArgs& g, const uint16_t* im
 
 std::string x3wlabel(const char* fam, const WgradCfg& w, int layer) {
     char b[112];
-    snprintf(b, sizeof b, "%s/wx3%s_%dx%d|%d", fam, w.tile >= 2 && w.tile <= 7 ? "r3" : "", w.bm, w.bn, layer);
+    snprintf(b, sizeof b, "%s/wx3%s_%dx%d|%d", fam, w.tile >= 2 ? "r3" : "", w.bm, w.bn, layer);
     return b;
 }
 
@@ -970,7 +889,7 @@ std::string xlabel(const char* fam, int tile, int layer) {
     int bm = 0, bn = 0;
     rowgemm_x3_tile_dims(tile, &bm, &bn);
     char b[112];
-    snprintf(b, sizeof b, "%s/x3%s_%dx%d|%d", fam, tile == 8 ? "r3k16" : tile >= 4 && tile <= 6 ? "r3" : "", bm, bn, layer);
+    snprintf(b, sizeof b, "%s/x3%s_%dx%d|%d", fam, tile >= 4 ? "r3" : "", bm, bn, layer);
     return b;
 }
 
@@ -1179,21 +1098,22 @@ struct Launcher {
 };
 
 // Row-GEMM tile choice for an output width N (tile ids: kernels_gemm.hip ROWGEMM_TILES,
-// 16..19 = kernels_gemm_pipe.hip).
+// 18, 19, 25, 26 = kernels_gemm_pipe.hip).
 //  * f32, N % 128 == 0: the software-pipelined 128x128 kernel, forward with its global loads
-//    two chunks ahead (18), dgrad one chunk ahead (16).  r02 A/B (tools/gpu_ab.sh, config 2):
+//    two chunks ahead (18), dgrad too since r03 (one chunk ahead, tile 16, removed in r06).  r02
+//    A/B (config 2):
 //    401 img/s against 390 for the register-staged tiles (t7 / t4 / t0 by grid size), the
 //    dominant kernel 128.9 vs 122.2 TF/s; the two schedules store identical bits
 //    (tests/test_gpu_parity.py::test_pipe_gemm_bit_identical);
 //  * f32, N = 64 outputs: the pipelined 128x64 with loads two chunks ahead (19) on the
 //    forward GEMMs (level-0 128 -> 64 conv 112 -> 117 TF/s), the register-staged 128x64
-//    (t1) on the dgrads and the level-0 ConvT forward, where 17 / 19 measured slower
+//    (t1) on the ConvT forward and since r03 the three-blocks-per-CU 25 / 26 on the dgrads
 //    (options tile_n64 / tile_n64_dgrad / tile_convt64; profiles/r02_pipe_exp.txt).
 // bf16 MFMA (register-staged): a chunk of 64 K per barrier (4 MFMA k-steps) by default.
 // Options tile_* override (tuning runs; -1 = automatic).
 int pick_tile(const unet_ctx* c, int N, bool dgrad, bool bf16, bool convt = false) {
     const Options& o = c->opt;
-    if (bf16) return N % 128 == 0 ? (dgrad ? o.tile16_n128_dgrad : o.tile16_n128) : o.tile16_n64;
+    if (bf16) return N % 128 == 0 ? 6 : 1;  // register-staged bf16 tiles (kernels_gemm.hip)
     if (N % 64) return o.tile_n32;  // 32 outputs (narrow networks' level 0)
     if (N % 128) return convt && !dgrad ? o.tile_convt64 : (dgrad ? o.tile_n64_dgrad : o.tile_n64);
     if (convt && !dgrad && o.tile_convt >= 0) return o.tile_convt;
@@ -1438,7 +1358,7 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
                 use_x3(c, p, g, img, C.cin, p.pack3 + 3 * C.pf);
                 const int tile = x3_tile(c, g);
                 R = bn_groups(M);
-                RUN(xlabel("conv_fwd", tile, i), 2.0 * M * C.cout * 9 * C.cin, launch_rowgemm_x3(g, tile, s, x3_rsched(c, tile)));
+                RUN(xlabel("conv_fwd", tile, i), 2.0 * M * C.cout * 9 * C.cin, launch_rowgemm_x3(g, tile, s));
                 return stats_finalize(c, L, p, i, R, M, training, prm, bn_run, bn_cnt);
             }
             if (rg16_on(c, C.cin, C.cout)) {
@@ -1455,9 +1375,7 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
                 g.a16 = img;
                 const int tile = rg16_tile(c, g);
                 R = bn_groups(M);
-                const bool xp = c->opt.rg16_xp && tile == 4;
-                RUN(tlabel16("conv_fwd", tile, i), 2.0 * M * C.cout * 9 * C.cin,
-                    xp ? launch_rowgemm16_xp(g, c->opt.rg16_xp, s) : launch_rowgemm16(g, tile, s, c->opt.rg16_sched));
+                RUN(tlabel16("conv_fwd", tile, i), 2.0 * M * C.cout * 9 * C.cin, launch_rowgemm16(g, tile, s));
                 return stats_finalize(c, L, p, i, R, M, training, prm, bn_run, bn_cnt);
             }
             R = bn_groups(M);
@@ -1513,8 +1431,8 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
                 g.out3 = p.x3[idec];
                 up16[idec] = true;
             }
-            const int tile = x3_convt_tile(c, g);
-            RUN(xlabel("convT_fwd", tile, 100 + k), 2.0 * g.M * g.N * g.K, launch_rowgemm_x3(g, tile, s, x3_rsched(c, tile)));
+            const int tile = x3_tile(c, g);
+            RUN(xlabel("convT_fwd", tile, 100 + k), 2.0 * g.M * g.N * g.K, launch_rowgemm_x3(g, tile, s));
             return 0;
         }
         if (!c->res && rg16_on(c, T.cin, T.cout)) {
@@ -1533,7 +1451,7 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
             }
             const int tile = rg16_tile(c, g);
             RUN(tlabel16("convT_fwd", tile, 100 + k), 2.0 * g.M * g.N * g.K,
-                launch_rowgemm16(g, tile, s, c->opt.rg16_sched));
+                launch_rowgemm16(g, tile, s));
             return 0;
         }
         const int tile = pick_tile(c, T.cout, false, c->bf16, true);  // grid N = 4 cout
@@ -1729,7 +1647,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
             w.splits = wc.splits;
             w.slab = p.slab;
             w.zero16 = p.zero16;
-            RUN(x3wlabel("conv_wgrad", wc, i), 2.0 * P * C.cout * 9 * C.cin, launch_wgrad_x3(w, wc.tile, s, x3_wsched(c, wc.tile)));
+            RUN(x3wlabel("conv_wgrad", wc, i), 2.0 * P * C.cout * 9 * C.cin, launch_wgrad_x3(w, wc.tile, s));
             RUN("wgrad_reduce", 0,
                 k_slab_reduce(p.slab, wc.splits, w.Mw, w.Nw, 0, C.cin, C.cout, grads + C.w, s));
             if (!dx) return 0;
@@ -1759,7 +1677,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
             }
             const int tile = x3_tile(c, g);
             if (rows) *rows = bn_groups(P);
-            RUN(xlabel("conv_dgrad", tile, i), 2.0 * P * C.cout * 9 * C.cin, launch_rowgemm_x3(g, tile, s, x3_rsched(c, tile)));
+            RUN(xlabel("conv_dgrad", tile, i), 2.0 * P * C.cout * 9 * C.cin, launch_rowgemm_x3(g, tile, s));
             return 0;
         }
         // bf16 image of dz: A operand of the LDS-DMA dgrad, B' of the LDS-DMA wgrad; the f32
@@ -1881,7 +1799,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
                 const int tile = rg16_tile(c, g);
                 if (rows) *rows = bn_groups(P);
                 RUN(tlabel16("conv_dgrad", tile, i), 2.0 * P * C.cout * 9 * C.cin,
-                    launch_rowgemm16(g, tile, s, c->opt.rg16_sched));
+                    launch_rowgemm16(g, tile, s));
                 return 0;
             }
             if (rows) *rows = bn_groups(P);
@@ -1925,7 +1843,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
             w.slab = p.slab;
             w.zero16 = p.zero16;
             RUN(x3wlabel("convT_wgrad", wc, 100 + k), 2.0 * Pin * T.cin * 4 * T.cout,
-                launch_wgrad_x3(w, wc.tile, s, x3_wsched(c, wc.tile)));
+                launch_wgrad_x3(w, wc.tile, s));
             RUN("bias_grad", 0, k_up2_bias_partials(p.dcat[lo], ldo, uo, Hi, Wi, Pin, T.cout, wc.pps,
                                                     wc.splits, p.bslab, s));
             RUN("wgrad_reduce", 0,
@@ -1956,10 +1874,10 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
                 }
                 g.stats = p.part;
             }
-            const int tile = x3_convt_tile(c, g);
+            const int tile = x3_tile(c, g);
             *rows = bn_groups(Pin);
             RUN(xlabel("convT_dgrad", tile, 100 + k), 2.0 * Pin * T.cin * 4 * T.cout,
-                launch_rowgemm_x3(g, tile, s, x3_rsched(c, tile)));
+                launch_rowgemm_x3(g, tile, s));
             return 0;
         }
         WgradCfg wc = wgrad_cfg(c, T.cin, 1, T.cout, 4, Pin, c->bf16);
@@ -2063,7 +1981,7 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
             const int tile = rg16_tile(c, g);
             *rows = bn_groups(Pin);
             RUN(tlabel16("convT_dgrad", tile, 100 + k), 2.0 * Pin * T.cin * 4 * T.cout,
-                launch_rowgemm16(g, tile, s, c->opt.rg16_sched));
+                launch_rowgemm16(g, tile, s));
             return 0;
         }
         const int tile = pick_tile(c, T.cin, true, c->bf16, true);
@@ -2317,6 +2235,11 @@ int unet_create(const unet_cfg* cfg, int device, unet_ctx** out) {
     try {
         std::unique_ptr<unet_ctx> c(new unet_ctx());
         c->device = device;
+        int cus = 0;  // (no device in a CPU-only process: keep the MI355X's 256)
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
+            c->cus = cus;
+        else
+            (void)hipGetLastError();
         if (cfg) {
             c->in_ch = cfg->in_channels;
             c->out_ch = cfg->out_channels;
@@ -2766,6 +2689,11 @@ int unet_debug_view(unet_ctx* c, int N, int H, int W, int training, int kind, in
         if (index < 0 || index >= c->depth) return UNET_ERR_INVALID;
         const int C = c->ch(index);
         if (kind == 5) {
+            // the x3 path's max-pool writes the next conv's x3 image instead (forward_impl):
+            // the f32 pooled buffer is never written there
+            const ConvL& Cj = c->conv[2 * (index + 1)];
+            if (!c->res && p.pack3 && x3_conv_on(c, Cj.cin, Cj.cout))
+                return fail(c, UNET_ERR_INVALID, "debug view 5: level %d pools into an x3 image", index);
             q = p.pool[index];
             n = p.P[index + 1] * C;
             l = C;
