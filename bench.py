@@ -64,6 +64,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=3)
     ap.add_argument("--verbose", action="store_true")
+    ap.add_argument("--adamw", default="fused", choices=("fused", "plain"),
+                    help="fused: AdamW with the next forward's weight repack (unet_adamw_repack, "
+                         "the default); plain: unet_adamw + the forward's repack (A/B runs)")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="kernel-schedule option of the native context (unet_set_option; "
                          "A/B runs), repeatable")
@@ -340,6 +343,9 @@ def main():
     else:
         model = unet_hip.UNet(1, 1).to(dev).train()
     opt = unet_hip.HipAdamW(model.parameters(), lr=1e-5)
+    if args.adamw == "plain":
+        import unet_hip.module as UM
+        UM.arena_owner = lambda flat: None
     ddp = DistributedUNet(model, opt) if world > 1 else None
     for kv in args.opt:
         name, _, val = kv.partition("=")

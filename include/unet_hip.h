@@ -171,6 +171,21 @@ int unet_adamw(unet_ctx* ctx, float* params, const float* grads, float* exp_avg,
                float* exp_avg_sq, int64_t n, int step, double lr, double beta1, double beta2,
                double eps, double weight_decay, double grad_scale, unet_stream_t stream);
 
+/* (r06) The same AdamW step (utils/trainer.py:41,92 AdamW(...).step()) over the whole parameter
+ * arena of this context (n == the unet_num_params float count), fused with the weight repack
+ * the next forward needs: every 3x3 conv / ConvT weight tile is updated and packed into the
+ * context's own GEMM images in one pass, the other tensors are updated elementwise.  Results
+ * are bit-identical to unet_adamw.  The next unet_forward on the same `params` pointer reads
+ * those images instead of repacking, until unet_params_changed (the caller changed the
+ * parameters by other means: load_state_dict, another optimizer) or the next repack.  A
+ * training forward that read them refuses its backward (UNET_ERR_INVALID) if they were rewritten
+ * in between.  Another n, or a channel-padded network, runs the plain unet_adamw. */
+int unet_adamw_repack(unet_ctx* ctx, float* params, const float* grads, float* exp_avg,
+                      float* exp_avg_sq, int64_t n, int step, double lr, double beta1, double beta2,
+                      double eps, double weight_decay, double grad_scale, unet_stream_t stream);
+/* The caller changed the parameter arena outside unet_adamw_repack: the next forward repacks. */
+int unet_params_changed(unet_ctx* ctx);
+
 /* Mask readout + confusion counts, utils/trainer.py:101-107,217-242, utils/utils.py:225-251.
  * counts (device int64[6]) += {TP, FP, FN, TN} of (sigmoid(logits) > 0.5) vs targets cast to
  * an integer (== 1 is positive), then {|pred AND t!=0|, |pred OR t!=0|} (the bool cast of

@@ -285,48 +285,49 @@ def test_rg16_tile_group_bit_identical():
     _assert_same(outs[0], outs[1], "tile_group")
 
 
-def test_convt16_bit_identical():
-    """Option convt16 (default on): in a bf16 training step the ConvT forward stores bf16 of
-    its output straight into the decoder conv's kept operand image (the same RNE rounding of
-    the same f32 value k_to_bf16 applies) and that conv's prep pass converts the skip half
-    only.  BASELINE config 4's network, one step at 128^2: bit-identical to convt16 = 0."""
+def test_convt16_and_pool_fuse_bit_identical():
+    """Options convt16 and pool_fuse (default on) in a bf16 training step.  convt16: the ConvT
+    forward stores bf16 of its output straight into the decoder conv's kept operand image (the
+    same RNE rounding of the same f32 value k_to_bf16 applies) and that conv's prep pass
+    converts the skip half only.  pool_fuse (r06 on the bf16 path): each encoder block's second
+    conv forms its `do` = mask (dskip + routed dpool) inside its bf16 dz pass from the max-pool
+    backward's inputs instead of reading a full-resolution do that maxpool_bwd stored.  BASELINE
+    config 4's network, one step at 128^2: each off is bit-identical to both on."""
     x, t = inputs(53, 2, 128, 128)
     P = MO.make_params(59, 128, 5)
     outs = {}
-    for flag in (0, 1):
+    for flags in ((1, 1), (0, 1), (1, 0)):
         m = _bf16_model(P, 128, 5)
-        with options(m.flatten_().rt, convt16=flag):
-            outs[flag] = _bf16_step(m, x, t)
+        with options(m.flatten_().rt, convt16=flags[0], pool_fuse=flags[1]):
+            outs[flags] = _bf16_step(m, x, t)
         del m
-    _assert_same(outs[0], outs[1], "convt16")
+    _assert_same(outs[(1, 1)], outs[(0, 1)], "convt16")
+    _assert_same(outs[(1, 1)], outs[(1, 0)], "pool_fuse")
 
 
 def test_wg16_tap_row_bit_identical():
     """The tap-row bf16 weight gradient (kernels_gemm16.hip wgrad16_row3_kernel, option wg16_r3
-    = 3 / 4 LDS stages: the three dx taps of one tap row from one halo of 66 pixel rows) runs
-    the same MFMA sequence per weight element as the one-tap kernel (same operands, pixel
-    chunks, k-steps and split partition), so one training step of BASELINE config 4's network
-    at 256^2 (tap-row levels W = 256, 128, 64; the rest fall back) is bit-identical."""
+    = 4: the three dx taps of one tap row from one halo of 66 pixel rows) runs the same MFMA
+    sequence per weight element as the one-tap kernel (same operands, pixel chunks, k-steps and
+    split partition), so one training step of BASELINE config 4's network at 256^2 (tap-row
+    levels W = 256, 128, 64; the rest fall back) is bit-identical.  The default, wg16_r3 = 7
+    (r06: the 16x16x32 kernel with the re-read stagger), sums 32 instead of 16 exact bf16
+    products per MFMA step: f32 rounding apart from those."""
     x, t = inputs(43, 2, 256, 256)
     P = MO.make_params(47, 128, 5)
     outs = {}
-    for r3 in (0, 3, 4, 5, 6, 7):
+    for r3 in (0, 4, 7):
         m = _bf16_model(P, 128, 5)
         with options(m.flatten_().rt, wg16_r3=r3):
             outs[r3] = _bf16_step(m, x, t)
         del m
-    for r3 in (3, 4, 5):  # 5: four waves of 32 x 128 per tap (r05)
-        _assert_same(outs[0], outs[r3], f"wg16_r3={r3} vs one-tap")
-    # 6 / 7 (r06): the 16x16x32 kernel, 7 with the re-read stagger -- the same MFMAs per
-    # accumulator in both (bit-identical); against the 32x32x16 kernels the chunk sums run 32
-    # instead of 16 products per MFMA step: f32 rounding apart (exact bf16 products)
-    _assert_same(outs[6], outs[7], "wg16_r3=7 vs 6")
-    assert torch.equal(outs[6][0], outs[4][0])  # the forward does not change
+    _assert_same(outs[0], outs[4], "wg16_r3=4 vs one-tap")
+    assert torch.equal(outs[7][0], outs[4][0])  # the forward does not change
     for k, g4 in outs[4][1].items():
-        g6 = outs[6][1][k]
-        assert torch.isfinite(g6).all(), k
+        g7 = outs[7][1][k]
+        assert torch.isfinite(g7).all(), k
         tol = 2e-5 * max(g4.abs().max().item(), 1e-30)
-        assert (g6 - g4).abs().max().item() <= tol, (k, (g6 - g4).abs().max().item(), tol)
+        assert (g7 - g4).abs().max().item() <= tol, (k, (g7 - g4).abs().max().item(), tol)
 
 
 @pytest.mark.parametrize("halo", [19, 20])

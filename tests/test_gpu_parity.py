@@ -723,3 +723,90 @@ def test_bucket_event_exported_for_non_torch_callers():
     torch.cuda.synchronize()
     for (off, n), c in zip(rt.buckets, copies):
         assert torch.equal(c, arena[off:off + n])
+
+
+def _train_steps(m, opt, batches):
+    import unet_hip
+    out = []
+    for x, t in batches:
+        opt.zero_grad()
+        logits = m(x.to(DEV))
+        losses = unet_hip.seg_losses(logits, t.to(DEV))
+        (losses[0] + losses[1]).backward()
+        opt.step()
+        torch.cuda.synchronize()
+        out.append(logits.detach().clone())
+    return out
+
+
+@pytest.mark.parametrize("variant", ["model", "mod_bf16"])
+def test_adamw_repack_bit_identical(variant, monkeypatch):
+    """unet_adamw_repack (r06): HipAdamW over a HIP model's whole arena updates each 3x3 / ConvT
+    weight tile and packs it into the context's GEMM images in one pass, and the next forward
+    reads those images instead of repacking.  Three training steps must be bit-identical --
+    logits of every step, the parameter arena, exp_avg and exp_avg_sq -- to the unfused path
+    (unet_adamw, then the forward's own repack): models/model.py UNet (f32 on the x3 images) and
+    config 4's mod.py UNet(128, 5) on bf16 images."""
+    import unet_hip
+    import unet_hip.module as UM
+    from oracle import mod_ref_cpu as MO
+    H = 64 if variant == "model" else 128
+    batches = [inputs(90 + k, 2, H, H) for k in range(3)]
+    res = {}
+    for fused in (1, 0):
+        if not fused:
+            monkeypatch.setattr(UM, "arena_owner", lambda flat: None)
+        if variant == "model":
+            m = hip_model(O.make_params(42), DEV)
+        else:
+            m = unet_hip.ModUNet(1, 1, base_filters=128, depth=5, mfma_dtype="bf16")
+            sd = m.state_dict()
+            sd.update({k: v.clone() for k, v in MO.make_params(61, 128, 5).items()})
+            m.load_state_dict(sd)
+            m = m.to(DEV).train()
+        opt = unet_hip.HipAdamW(m.parameters(), lr=1e-3)
+        lg = _train_steps(m, opt, batches)
+        st = m.flatten_()
+        p0 = next(m.parameters())
+        res[fused] = (lg, st.param_arena.clone(), opt.state[p0]["exp_avg"].clone(),
+                      opt.state[p0]["exp_avg_sq"].clone())
+        del m, opt
+    for k, (a, b) in enumerate(zip(res[1][0], res[0][0])):
+        assert torch.equal(a, b), f"step {k} logits"
+    assert torch.equal(res[1][1], res[0][1]), (res[1][1] - res[0][1]).abs().max().item()
+    assert torch.equal(res[1][2], res[0][2]) and torch.equal(res[1][3], res[0][3])
+
+
+def test_adamw_repack_invalidation():
+    """The fused path's weight images follow the parameters: a torch in-place write after a
+    fused step (load_state_dict-style; the parameter's version counter moves) is seen by the
+    next forward (it repacks), so is a write through `.data` declared with params_changed(), and
+    a backward whose forward read the images refuses to run after another fused step rewrote
+    them."""
+    import unet_hip
+    from unet_hip._lib import HipError
+    x, t = inputs(95, 2, 64, 64)
+    m = hip_model(O.make_params(42), DEV)
+    opt = unet_hip.HipAdamW(m.parameters(), lr=1e-3)
+    _train_steps(m, opt, [(x, t)])
+    # forward on the fused images, then a fused step in between, then its backward
+    logits = m(x.to(DEV))
+    losses = unet_hip.seg_losses(logits, t.to(DEV))
+    opt.step()  # the grads of the first step are still there: a fused repack
+    with pytest.raises(HipError):
+        (losses[0] + losses[1]).backward()
+    with torch.no_grad():
+        m.encoder2[0].weight.mul_(0.5)  # bumps the arena's version counter
+    got = m(x.to(DEV)).detach().clone()
+    ref = hip_model({k: v.detach().cpu() for k, v in m.named_parameters()}, DEV)
+    want = ref(x.to(DEV)).detach()
+    assert torch.equal(got, want)
+    del ref
+    # writes through .data bypass the version counters: declared with params_changed()
+    _train_steps(m, opt, [(x, t)])
+    m.encoder3[0].weight.data.mul_(-1.0)
+    m.params_changed()
+    got = m(x.to(DEV)).detach().clone()
+    ref = hip_model({k: v.detach().cpu() for k, v in m.named_parameters()}, DEV)
+    want = ref(x.to(DEV)).detach()
+    assert torch.equal(got, want)

@@ -184,18 +184,25 @@ def test_x3_row_tile_choice_bit_identical(B, H, W):
     assert torch.isfinite(outs[0][1]).all()
 
 
-def test_x3_head_fuse_bit_identical():
+@pytest.mark.parametrize("variant", ["model", "mod"])
+def test_x3_head_fuse_bit_identical(variant):
     """Options head_fuse / pool_fuse (r05, default on): the x3 dz pass of the last conv
     recomputes its `do` = [activation > 0] dl w from the logit gradient, and that of each
     encoder block's second conv its `do` = mask (dskip + routed dpool) from the max-pool
     backward's inputs (the producers' own fma masks and sums), instead of reading a
-    full-resolution f32 `do` the producer stored: one training step is bit-identical."""
+    full-resolution f32 `do` the producer stored: one training step is bit-identical.  "mod"
+    (ADVICE r05): models/mod.py UNet(64, 3) in f32, whose BN -> ReLU order takes the mask
+    branches (the head's fma(y, sc, sh) > 0 and the pool's fma(msc, y, msh) > 0)."""
     import unet_hip
-    from _helpers import options
+    from _helpers import hip_mod_model, options
+    from oracle import mod_ref_cpu as MO
     x, t = inputs(47, 2, 128, 128)
     outs = []
     for flag in (0, 1):
-        m = hip_model(O.make_params(53), DEV)
+        if variant == "model":
+            m = hip_model(O.make_params(53), DEV)
+        else:
+            m = hip_mod_model(MO.make_params(53, 64, 3), DEV, 64, 3)
         with options(m.flatten_().rt, head_fuse=flag, pool_fuse=flag):
             logits = m(x.to(DEV))
             l = unet_hip.seg_losses(logits, t.to(DEV))

@@ -323,7 +323,7 @@ def test_schedule_option_defaults():
             "wgrad_row3_blocks": 1536, "wgrad_blocks": 2048, "rg16": 1, "rg16_tile": -1,
             "rg16_bn_k": 0, "wg16": 1, "wg16_tile": 2, "wgrad16_blocks": 1536,
             "xcd_remap": 1, "xcd16": 1, "tile_convt": -1, "tile_convt_dgrad": 26,
-            "dz_in_wgrad": 256, "rg16_r3": 1, "rg16_n128": 20, "rg16_n128_bn": 0, "wg16_r3": 4,
+            "dz_in_wgrad": 256, "rg16_r3": 1, "rg16_n128": 20, "rg16_n128_bn": 0, "wg16_r3": 7,
             "convt16": 1, "x3": 1, "x3_tile": -1, "x3_wtile": -1, "x3_wblocks": 1536, "x3_n64": 2, "x3_r3": 1, "x3_wwaves": 3, "x3_wwaves1": 3, "head_fuse": 1, "pool_fuse": 1, "tile_group": 1}
     got = {k: fresh.get_option(k) for k in want}
     assert got == want

@@ -375,6 +375,8 @@ using T16_0 = Tile16<128, 128, 64, 64, 2, 2>;
 using T16_2 = Tile16<256, 128, 64, 64, 2, 1>;
 using T16_4 = Tile16<256, 256, 128, 64, 2, 1>;
 using T16_6 = Tile16<512, 128, 128, 64, 2, 1>;
+// (r06, not kept: 128x128 with three / four stages at one block per CU for the deep levels' small
+// grids, config 4 -1.2 %, profiles/r06_c4_ab.txt)
 #define ROWGEMM16_TILES(X) X(0, T16_0) X(2, T16_2) X(4, T16_4) X(6, T16_6)
 
 template <int AMODE, int EMODE, class T>
@@ -631,13 +633,11 @@ __global__ __launch_bounds__(T::THREADS, T::OCC) void wgrad16_kernel(WgradArgs p
 // Same operands, pixel chunks, k-steps and split partition as wgrad16_kernel, so every
 // element's sum is the same sequence of MFMAs: bit-identical to the one-tap tiles.
 // ------------------------------------------------------------------------------------
-// WN = 128 (r05, tile 5): four waves of 32 (ci) x 128 (co) per tap, 12 accumulators (in AGPRs)
-// and 14 transposed reads per 12 MFMAs (30 % fewer LDS reads per MFMA than 32 x 64); one block
-// of four waves per CU at 3 stages (up to 512 registers a wave; two blocks per CU at 2 stages
-// spill 350 VGPRs).  Same MFMAs per accumulator element as 32 x 64: bit-identical.
-template <int S, int WN = 64, int OCC = 1>
-__global__ __launch_bounds__((128 / 32) * (128 / WN) * 64, OCC) void wgrad16_row3_kernel(WgradArgs p) {
-    constexpr int BM = 128, BN = 128, WM = 32, BKP = 64;
+// (r05-r06, removed: four waves of 32 x 128 per tap at 3 stages, and 3 stages of this tile --
+// bit-identical, slower)
+template <int S>
+__global__ __launch_bounds__(512, 1) void wgrad16_row3_kernel(WgradArgs p) {
+    constexpr int BM = 128, BN = 128, WM = 32, WN = 64, BKP = 64;
     constexpr int WAVES_N = BN / WN, WAVES = (BM / WM) * WAVES_N;  // 4 x 2 / 4 x 1 waves
     constexpr int NT = WN / 32;
     constexpr int RA = 2 * BM, RBB = 2 * BN;    // 256-B pixel rows
@@ -1059,9 +1059,9 @@ static int wg16_go(const WgradArgs& a, hipStream_t s) {
 }  // namespace
 
 int wgrad16g_tile_dims(int tile, int* bm, int* bn, int* stages) {
-    if (tile >= 3 && tile <= 7) {  // tap-row: 128 x 128 per tap, three taps per block
+    if (tile == 4 || tile == 7) {  // tap-row: 128 x 128 per tap, three taps per block, 4 stages
         *bm = *bn = 128;
-        if (stages) *stages = tile == 3 || tile == 5 ? 3 : 4;
+        if (stages) *stages = 4;
         return 0;
     }
 #define WG16_DIMS(id, T)          \
@@ -1115,23 +1115,16 @@ int launch_rowgemm16(const RowGemmArgs& a, int tile, hipStream_t s) {
 // 3x3 conv (A' G_CONV3, B' G_IDENT) and ConvT (A' G_IDENT, B' G_UP2); no bias column sums.
 int launch_wgrad16(const WgradArgs& a, int tile, hipStream_t s) {
     if (a.aoff || a.boff || a.ascale || a.bcoef || a.bias_slab || !a.zero16 || a.P < 1) return -1;
-    if (tile >= 3 && tile <= 7) {  // tap-row kernel: 3x3 conv layers, W % 64 == 0 (3 / 4: 8 waves,
-                                   // 3 / 4 LDS stages; 5: 4 waves of 32 x 128, 3 stages; 6 / 7:
-                                   // 16x16x32, 4 stages, 7 with the re-read stagger)
+    if (tile == 4 || tile == 7) {  // tap-row kernel: 3x3 conv layers, W % 64 == 0 (4: 32x32x16, 4 LDS
+                                   // stages; 7: 16x16x32 with the re-read stagger, r06)
         if (a.amode != G_CONV3 || a.bmode != G_IDENT || a.Mw != 9 * a.CA || a.Nw != a.CB ||
             a.CA % 128 || a.CB % 128 || a.W % 64 || a.pps % 64)
             return -1;
         const dim3 grid((a.CA / 128) * 3 * (a.Nw / 128) * a.splits);
-        if (tile == 6)
-            hipLaunchKernelGGL((wgrad16_row3_m16_kernel<4, false>), grid, dim3(512), 0, s, a);
-        else if (tile == 7)
+        if (tile == 7)
             hipLaunchKernelGGL((wgrad16_row3_m16_kernel<4, true>), grid, dim3(512), 0, s, a);
-        else if (tile == 3)
-            hipLaunchKernelGGL((wgrad16_row3_kernel<3>), grid, dim3(512), 0, s, a);
-        else if (tile == 4)
-            hipLaunchKernelGGL((wgrad16_row3_kernel<4>), grid, dim3(512), 0, s, a);
         else
-            hipLaunchKernelGGL((wgrad16_row3_kernel<3, 128, 1>), grid, dim3(256), 0, s, a);
+            hipLaunchKernelGGL((wgrad16_row3_kernel<4>), grid, dim3(512), 0, s, a);
         return (int)hipGetLastError();
     }
 #define WG16G(AM, BMD)                                   \

@@ -1250,9 +1250,13 @@ __global__ __launch_bounds__(256) void bn_dz_x3_kernel(const float* __restrict__
     float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     for (int oct = threadIdx.x % G; active && oct < g8; oct += G) {
         const int c = oct * 8;
-        f32x4 ka[2], kb[2], kc[2], km[2], hw[2], hs[2], hh[2];
+        f32x4 ka[2], kb[2], kc[2], km[2], hw[2], hs[2], hh[2], msc[2], msh[2];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
+            if (POOL && pl.msc) {  // the BN -> ReLU mask affine, in registers (r06)
+                msc[h] = *(const f32x4*)(pl.msc + c + 4 * h);
+                msh[h] = *(const f32x4*)(pl.msh + c + 4 * h);
+            }
             ka[h] = *(const f32x4*)(coef + c + 4 * h);
             kb[h] = *(const f32x4*)(coef + C + c + 4 * h);
             kc[h] = *(const f32x4*)(coef + 2 * C + c + 4 * h);
@@ -1303,7 +1307,7 @@ __global__ __launch_bounds__(256) void bn_dz_x3_kernel(const float* __restrict__
 #pragma unroll
                         for (int j = 0; j < 4; ++j) {
                             if (((wi[i][h] >> (8 * j)) & 0xFF) == (uint32_t)kk[i]) dv[i][h][j] += gp[i][h][j];
-                            if (pl.msc && !(__builtin_fmaf(pl.msc[c + 4 * h + j], yv[i][h][j], pl.msh[c + 4 * h + j]) > 0.f))
+                            if (pl.msc && !(__builtin_fmaf(msc[h][j], yv[i][h][j], msh[h][j]) > 0.f))
                                 dv[i][h][j] = 0.f;
                         }
             }

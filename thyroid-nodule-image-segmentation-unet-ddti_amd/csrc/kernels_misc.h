@@ -17,6 +17,18 @@ struct PackJobs {
     PackJob j[MAX_PACK_JOBS];
 };
 int k_pack_all(const PackJobs& jobs, const float* prm, float* pack, int bf16, hipStream_t s);
+// (r06) AdamW fused into the weight repack (unet_adamw_repack): the pack jobs' weight tensors
+// are updated in place and packed from the updated values; `rest` lists the other arena ranges
+// (elementwise AdamW).  Bit-identical to k_adamw over the whole arena followed by k_pack_all.
+constexpr int MAX_ADAM_RANGES = 120;
+struct AdamRanges {
+    int n;
+    int64_t off[MAX_ADAM_RANGES];      // arena offset of range k
+    int64_t cum[MAX_ADAM_RANGES + 1];  // elements before range k (cum[n] = total)
+};
+struct AdamwScalars;
+int k_pack_adamw(const PackJobs& jobs, const AdamRanges& rest, float* p, const float* g, float* m, float* v,
+                 const AdamwScalars& a, float* pack, int bf16, hipStream_t s);
 // conv_first: relu = ReLU after (+bias) (model.py order); b may be null (mod.py, bias-free).
 // wgrad: mask = dz masked by [y > 0] (ReLU before the BN, model.py order); gb may be null.
 int k_conv_first_fwd(const float* x, const float* w, const float* b, float* y, int P, int H, int W,
@@ -50,6 +62,11 @@ int k_to_bf16(const float* src, int ld, int off, int C, const float* scale, cons
 // bn_dz writing the dense bf16 image of dz (and the f32 dz in place when f32 != 0)
 int k_bn_dz16(float* d, const float* y, int ld, int off, int64_t P, int C, const float* coef,
               int mask, uint16_t* dz16, int f32, hipStream_t s);
+// (r06) the same with `do` recomputed from the max-pool backward's inputs (option pool_fuse):
+// do = [msc: fma(msc, y, msh) > 0] (dskip + [idx == window position] dp); no f32 dz
+int k_bn_dz16_pool(const float* y, int ld, int off, int64_t P, int C, const float* coef, int mask,
+                   uint16_t* dz16, const float* dp, const uint8_t* idx, const float* dskip, int ldskip,
+                   const float* msc, const float* msh, int N, int H, int W, hipStream_t s);
 int k_bias_reduce(const float* slab, int S, int taps, int C, float* out, hipStream_t s);
 // ConvT bias partials [splits][4][C] from the up half of the concat gradient (LDS-DMA wgrad)
 int k_up2_bias_partials(const float* d, int ld, int off, int H, int W, int64_t P, int C, int pps,

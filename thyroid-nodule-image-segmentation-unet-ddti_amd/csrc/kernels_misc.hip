@@ -10,6 +10,44 @@
 
 namespace {
 
+// one AdamW element (torch optim/adam.py _single_tensor_adam, documented at adamw_kernel below)
+__device__ __forceinline__ void adamw_elem(float& p, float g, float& m, float& v,
+                                           const AdamwScalars& a) {
+#pragma clang fp contract(off)
+    if (a.gscale != 1.f) g = g * a.gscale;
+    p = p * a.decay;
+    const float d = g - m;
+    m = a.lerp_small ? __builtin_fmaf(a.w1, d, m) : __builtin_fmaf(a.w1 - 1.f, d, g);
+    v = v * a.b2;
+    v = __builtin_fmaf(a.w2 * g, g, v);
+    const float den = __builtin_sqrtf(v) / a.bc2_sqrt + a.eps;
+    p = p + (a.neg_step * m) / den;
+}
+
+// (r06) the fused AdamW of the packed weights (unet_adamw_repack): the pack kernel updates
+// each weight tile from the arena-shaped p / g / m / v before it packs it, so the forward reads
+// no f32 weight again.  Pointers point at the tensor's first element.
+struct AdamTile {
+    float* p;
+    const float* g;
+    float* m;
+    float* v;
+    AdamwScalars a;
+};
+template <bool ADAM>
+__device__ __forceinline__ float pack_load(const float* __restrict__ w, const AdamTile& t, int64_t i) {
+    if constexpr (ADAM) {
+        float p = t.p[i], m = t.m[i], v = t.v[i];
+        adamw_elem(p, t.g[i], m, v, t.a);
+        t.p[i] = p;
+        t.m[i] = m;
+        t.v[i] = v;
+        return p;
+    } else {
+        return w[i];
+    }
+}
+
 // -------------------------------------------------------------------------------------
 // Weight packing.  torch Conv2d weight W[co][ci][ky][kx] (models/model.py:36,39):
 //   fwd  : Wf[co][tap][ci]                    (Bt of the forward row-GEMM, k = tap*Cin+ci)
@@ -23,10 +61,10 @@ namespace {
 // contiguous) are read with unit stride, and both images are written as 32-element runs
 // (ci runs of Wf, co runs of Wd) rather than an element-wise stride-9 / stride-9*Cout
 // scatter.  Row stride 289 floats: both LDS read patterns are conflict-free.
-template <class OUT>
+template <class OUT, bool ADAM = false>
 __device__ void pack_conv3_tile(const float* __restrict__ w, OUT* __restrict__ wf,
                                 OUT* __restrict__ wd, int cin, int cout, int ci0, int co0,
-                                float* tile) {
+                                float* tile, const AdamTile& at = AdamTile{}) {
     constexpr int T = 32, RS = T * 9 + 1;
     const int nci = min(T, cin - ci0), nco = min(T, cout - co0);
     const int tid = threadIdx.x;
@@ -37,7 +75,7 @@ __device__ void pack_conv3_tile(const float* __restrict__ w, OUT* __restrict__ w
         for (int k = 0; k < T * T * 9 / 256; ++k) {
             const int e = tid + 256 * k;  // e = co_l * 288 + (ci_l * 9 + tap)
             const int co_l = e / (T * 9), r = e - co_l * (T * 9);
-            v[k] = w[((int64_t)(co0 + co_l) * cin + ci0) * 9 + r];
+            v[k] = pack_load<ADAM>(w, at, ((int64_t)(co0 + co_l) * cin + ci0) * 9 + r);
         }
 #pragma unroll
         for (int k = 0; k < T * T * 9 / 256; ++k) {
@@ -49,7 +87,7 @@ __device__ void pack_conv3_tile(const float* __restrict__ w, OUT* __restrict__ w
         for (int e = tid; e < T * T * 9; e += 256) {  // e = co_l * 288 + (ci_l * 9 + tap)
             const int co_l = e / (T * 9), r = e - co_l * (T * 9);
             if (co_l < nco && r < nci * 9)
-                tile[co_l * RS + r] = w[((int64_t)(co0 + co_l) * cin + ci0) * 9 + r];
+                tile[co_l * RS + r] = pack_load<ADAM>(w, at, ((int64_t)(co0 + co_l) * cin + ci0) * 9 + r);
         }
     }
     __syncthreads();
@@ -77,17 +115,17 @@ __device__ void pack_conv3_tile(const float* __restrict__ w, OUT* __restrict__ w
 // the fill (lanes over (co_l, ab)), the Tf read (lanes over ci) and the Td read (lanes over
 // co) are all conflict-free (the r02 [ci_l][co_l * 4 + ab] image read Td at a 4-float lane
 // stride: 4-way conflicts, 4.19 M extra LDS cycles per config-4 repack).
-template <class OUT>
+template <class OUT, bool ADAM = false>
 __device__ void pack_convT_tile(const float* __restrict__ w, OUT* __restrict__ tf,
                                 OUT* __restrict__ td, int cin, int cout, int co0, int ci0,
-                                float* tile) {
+                                float* tile, const AdamTile& at = AdamTile{}) {
     constexpr int T = 32, AS = 40, RS = 4 * AS + 1;  // tile: [ci_l][ab][co_l]
     const int nci = min(T, cin - ci0), nco = min(T, cout - co0);
     const int tid = threadIdx.x;
     for (int e = tid; e < T * T * 4; e += 256) {  // e = ci_l * 128 + (co_l * 4 + ab)
         const int ci_l = e / (T * 4), r = e - ci_l * (T * 4);
         if (ci_l < nci && r < nco * 4)
-            tile[ci_l * RS + (r & 3) * AS + (r >> 2)] = w[((int64_t)(ci0 + ci_l) * cout + co0) * 4 + r];
+            tile[ci_l * RS + (r & 3) * AS + (r >> 2)] = pack_load<ADAM>(w, at, ((int64_t)(ci0 + ci_l) * cout + co0) * 4 + r);
     }
     __syncthreads();
     const int l = tid & 31, g = tid >> 5;  // 8 groups of 32 lanes
@@ -109,9 +147,19 @@ __device__ void pack_convT_tile(const float* __restrict__ w, OUT* __restrict__ t
 // Every 3x3 / ConvT weight image of the network in ONE launch (the per-layer launches were
 // 21 small grids per step, most of them too small to fill the chip): block b runs tile
 // b - block0 of the last job with block0 <= b; the job table travels as a kernel argument.
-template <class OUT>
+// ADAM (r06, unet_adamw_repack): each tile is first AdamW-updated in place (p, m, v of the
+// arena-shaped pointers in `ad`, the same adamw_elem as adamw_kernel: bit-identical), and the
+// updated values are what it packs.
+struct AdamArena {
+    float* p;
+    const float* g;
+    float* m;
+    float* v;
+};
+template <class OUT, bool ADAM = false>
 __global__ __launch_bounds__(256) void pack_all_kernel(PackJobs jobs, const float* __restrict__ prm,
-                                                       float* __restrict__ pack) {
+                                                       float* __restrict__ pack, AdamArena ad,
+                                                       AdamwScalars a) {
     __shared__ float tile[32 * (32 * 9 + 1)];
     const int b = blockIdx.x;
     int j = 0;
@@ -121,10 +169,35 @@ __global__ __launch_bounds__(256) void pack_all_kernel(PackJobs jobs, const floa
     const int local = b - J.block0, ix = local % J.tx, iy = local / J.tx;
     OUT* f = (OUT*)(pack + J.f);
     OUT* d = J.d >= 0 ? (OUT*)(pack + J.d) : nullptr;
+    AdamTile at{};
+    if constexpr (ADAM) at = AdamTile{ad.p + J.w, ad.g + J.w, ad.m + J.w, ad.v + J.w, a};
+    const float* w = ADAM ? nullptr : prm + J.w;
     if (J.kind == 0)
-        pack_conv3_tile<OUT>(prm + J.w, f, d, J.cin, J.cout, ix * 32, iy * 32, tile);
+        pack_conv3_tile<OUT, ADAM>(w, f, d, J.cin, J.cout, ix * 32, iy * 32, tile, at);
     else
-        pack_convT_tile<OUT>(prm + J.w, f, d, J.cin, J.cout, ix * 32, iy * 32, tile);
+        pack_convT_tile<OUT, ADAM>(w, f, d, J.cin, J.cout, ix * 32, iy * 32, tile, at);
+}
+
+// (r06) AdamW of the arena elements the fused pack does not cover (biases, BN affine, the
+// first conv and the head): a grid-stride walk over the concatenation of the ranges, each
+// index mapped to its range by binary search in the table (the kernel argument)
+__global__ __launch_bounds__(256) void adamw_ranges_kernel(AdamRanges t, AdamArena ad, AdamwScalars a) {
+    const int64_t total = t.cum[t.n];
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        int lo = 0, hi = t.n - 1;
+        while (lo < hi) {  // the last range with cum <= i
+            const int mid = (lo + hi + 1) >> 1;
+            if (t.cum[mid] <= i) lo = mid;
+            else hi = mid - 1;
+        }
+        const int64_t e = t.off[lo] + (i - t.cum[lo]);
+        float p = ad.p[e], m = ad.m[e], v = ad.v[e];
+        adamw_elem(p, ad.g[e], m, v, a);
+        ad.p[e] = p;
+        ad.m[e] = m;
+        ad.v[e] = v;
+    }
 }
 
 // 1x1 conv weight W[co][ci] -> its dgrad image Wt[ci][co] (models/mod.py:83 skip)
@@ -682,10 +755,23 @@ __global__ __launch_bounds__(256) void bn_dz_rows_kernel(float* __restrict__ d,
 // bn_dz for the bf16 GEMMs: dz as the dense bf16 image the LDS-DMA dgrad / wgrad read
 // (round to nearest even, as k_to_bf16), and the f32 dz in place only when another consumer
 // still reads it (f32 != 0).  8 channels per thread.
+// POOL (r06, option pool_fuse on the bf16 path): `d` is not read; do = [fma(msc, y, msh) > 0]
+// (dskip + [winner == window position] dpool), the max-pool backward's sum recomputed from its
+// inputs (as kernels_gemm_x3.hip bn_dz_x3_kernel<2>), so maxpool_bwd stores no full-resolution do
+struct Dz16Pool {
+    const float* dp;       // d pooled [N][H/2][W/2][C]
+    const uint8_t* idx;    // winner index per pooled element
+    const float* dskip;    // the concat gradient's skip half (offset applied), row stride ldskip
+    int ldskip;
+    const float *msc, *msh;  // BN -> ReLU mask affine, or null
+    int H, W;              // full-resolution grid
+    float rH, rW;
+};
+template <bool POOL>
 __global__ __launch_bounds__(256) void bn_dz16_kernel(float* __restrict__ d, const float* __restrict__ y,
                                                       int ld, int off, int64_t P, int C,
                                                       const float* __restrict__ coef, int mask,
-                                                      int tpr, __bf16* __restrict__ dz16, int f32) {
+                                                      int tpr, __bf16* __restrict__ dz16, int f32, Dz16Pool pl) {
     typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
     constexpr int U = 4;  // rows per thread per trip: 16 independent 16-B loads in flight
     const int rpp = 256 / tpr;
@@ -693,17 +779,56 @@ __global__ __launch_bounds__(256) void bn_dz16_kernel(float* __restrict__ d, con
     for (int64_t m0 = (int64_t)blockIdx.x * rpp * U + threadIdx.x / tpr; m0 < P;
          m0 += (int64_t)gridDim.x * rpp * U) {
         for (int c = c_first; c < C; c += tpr * 8) {
+            // the BN -> ReLU mask affine of this thread's 8 channels, in registers (loaded per
+            // element inside the row loop, the fused pass ran 1.5x slower than the unfused pair)
+            f32x4 msc[2], msh[2];
+            if (POOL && pl.msc) {
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    msc[h] = *(const f32x4*)(pl.msc + c + 4 * h);
+                    msh[h] = *(const f32x4*)(pl.msh + c + 4 * h);
+                }
+            }
             f32x4 dv[U][2], yv[U][2];
+            f32x4 gp[U][2];
+            uint32_t wi[U][2];
+            int kk[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const int64_t m = m0 + u * rpp;
                 if (m < P) {
+                    int64_t po = 0;
+                    if constexpr (POOL) {
+                        const Pix q = decode_fast((int)m, pl.H, pl.W, pl.rH, pl.rW);
+                        po = ((int64_t)q.img * (pl.H >> 1) + (q.y >> 1)) * (pl.W >> 1) + (q.x >> 1);
+                        kk[u] = (q.y & 1) * 2 + (q.x & 1);
+                        const uint2 w2 = *(const uint2*)(pl.idx + po * C + c);
+                        wi[u][0] = w2.x;
+                        wi[u][1] = w2.y;
+                    }
 #pragma unroll
                     for (int h = 0; h < 2; ++h) {
-                        dv[u][h] = *(const f32x4*)(d + m * C + c + 4 * h);
+                        if constexpr (POOL) {
+                            dv[u][h] = *(const f32x4*)(pl.dskip + m * pl.ldskip + c + 4 * h);
+                            gp[u][h] = *(const f32x4*)(pl.dp + po * C + c + 4 * h);
+                        } else {
+                            dv[u][h] = *(const f32x4*)(d + m * C + c + 4 * h);
+                        }
                         yv[u][h] = *(const f32x4*)(y + m * ld + off + c + 4 * h);
                     }
                 }
+            }
+            if constexpr (POOL) {
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+#pragma unroll
+                    for (int h = 0; h < 2; ++h)
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            if (((wi[u][h] >> (8 * j)) & 0xFF) == (uint32_t)kk[u]) dv[u][h][j] += gp[u][h][j];
+                            if (pl.msc && !(__builtin_fmaf(msc[h][j], yv[u][h][j], msh[h][j]) > 0.f))
+                                dv[u][h][j] = 0.f;
+                        }
             }
             f32x4 ka[2], kb[2], kc[2], km[2];
 #pragma unroll
@@ -728,7 +853,7 @@ __global__ __launch_bounds__(256) void bn_dz16_kernel(float* __restrict__ d, con
                         o[j] = (!mask || v[j] > 0.f) ? r[j] : 0.f;
                         o16[4 * h + j] = (__bf16)o[j];
                     }
-                    if (f32) *(f32x4*)(d + m * C + c + 4 * h) = o;
+                    if (!POOL && f32) *(f32x4*)(d + m * C + c + 4 * h) = o;
                 }
                 *(bf16x8*)(dz16 + m * C + c) = o16;
             }
@@ -1421,19 +1546,6 @@ __global__ void loss_bwd_kernel(const float* __restrict__ x, const float* __rest
 // bit for bit except where the host's vectorised sqrtf is not correctly rounded
 // (tests/test_gpu_parity.py::test_adamw_bitwise_vs_oracle).
 // -------------------------------------------------------------------------------------
-__device__ __forceinline__ void adamw_elem(float& p, float g, float& m, float& v,
-                                           const AdamwScalars& a) {
-#pragma clang fp contract(off)
-    if (a.gscale != 1.f) g = g * a.gscale;
-    p = p * a.decay;
-    const float d = g - m;
-    m = a.lerp_small ? __builtin_fmaf(a.w1, d, m) : __builtin_fmaf(a.w1 - 1.f, d, g);
-    v = v * a.b2;
-    v = __builtin_fmaf(a.w2 * g, g, v);
-    const float den = __builtin_sqrtf(v) / a.bc2_sqrt + a.eps;
-    p = p + (a.neg_step * m) / den;
-}
-
 __global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
                              float* __restrict__ m, float* __restrict__ v, int64_t n,
                              AdamwScalars a) {
@@ -1525,9 +1637,27 @@ int k_pack_all(const PackJobs& jobs, const float* prm, float* pack, int bf16, hi
     const PackJob& last = jobs.j[jobs.n - 1];
     const int blocks = last.block0 + last.tx * last.ty;
     if (bf16)
-        hipLaunchKernelGGL(pack_all_kernel<__bf16>, dim3(blocks), dim3(256), 0, s, jobs, prm, pack);
+        hipLaunchKernelGGL(pack_all_kernel<__bf16>, dim3(blocks), dim3(256), 0, s, jobs, prm, pack, AdamArena{},
+                           AdamwScalars{});
     else
-        hipLaunchKernelGGL(pack_all_kernel<float>, dim3(blocks), dim3(256), 0, s, jobs, prm, pack);
+        hipLaunchKernelGGL(pack_all_kernel<float>, dim3(blocks), dim3(256), 0, s, jobs, prm, pack, AdamArena{},
+                           AdamwScalars{});
+    LAUNCH_CHECK();
+}
+int k_pack_adamw(const PackJobs& jobs, const AdamRanges& rest, float* p, const float* g, float* m, float* v,
+                 const AdamwScalars& a, float* pack, int bf16, hipStream_t s) {
+    if (jobs.n < 1 || jobs.n > MAX_PACK_JOBS || rest.n < 0 || rest.n > MAX_ADAM_RANGES) return -1;
+    const PackJob& last = jobs.j[jobs.n - 1];
+    const int blocks = last.block0 + last.tx * last.ty;
+    const AdamArena ad{p, g, m, v};
+    if (bf16)
+        hipLaunchKernelGGL((pack_all_kernel<__bf16, true>), dim3(blocks), dim3(256), 0, s, jobs, nullptr, pack, ad, a);
+    else
+        hipLaunchKernelGGL((pack_all_kernel<float, true>), dim3(blocks), dim3(256), 0, s, jobs, nullptr, pack, ad, a);
+    HIP_OK(hipGetLastError());
+    if (rest.n > 0 && rest.cum[rest.n] > 0)
+        hipLaunchKernelGGL(adamw_ranges_kernel, dim3(grid_for(rest.cum[rest.n], 256, 1024)), dim3(256), 0, s, rest,
+                           ad, a);
     LAUNCH_CHECK();
 }
 int k_conv_first_fwd(const float* x, const float* w, const float* b, float* y, int P, int H, int W,
@@ -1628,8 +1758,21 @@ int k_bn_dz16(float* d, const float* y, int ld, int off, int64_t P, int C, const
     const int c8 = C / 8;
     const int tpr = c8 >= 256 ? 256 : c8;
     if (256 % tpr || (c8 > 256 && c8 % 256)) return -1;
-    hipLaunchKernelGGL(bn_dz16_kernel, dim3(grid_for((P + 3) / 4 * tpr)), dim3(256), 0, s, d, y, ld, off, P, C,
-                       coef, mask, tpr, (__bf16*)dz16, f32);
+    hipLaunchKernelGGL(bn_dz16_kernel<false>, dim3(grid_for((P + 3) / 4 * tpr)), dim3(256), 0, s, d, y, ld, off,
+                       P, C, coef, mask, tpr, (__bf16*)dz16, f32, Dz16Pool{});
+    LAUNCH_CHECK();
+}
+int k_bn_dz16_pool(const float* y, int ld, int off, int64_t P, int C, const float* coef, int mask,
+                   uint16_t* dz16, const float* dp, const uint8_t* idx, const float* dskip, int ldskip,
+                   const float* msc, const float* msh, int N, int H, int W, hipStream_t s) {
+    if (C % 8 || ld % 4 || off % 4 || ldskip % 4) return -1;
+    if (!dp || !idx || !dskip || H % 2 || W % 2 || (int64_t)N * H * W != P || P >= (1LL << 24)) return -1;
+    const int c8 = C / 8;
+    const int tpr = c8 >= 256 ? 256 : c8;
+    if (256 % tpr || (c8 > 256 && c8 % 256)) return -1;
+    const Dz16Pool pl{dp, idx, dskip, ldskip, msc, msh, H, W, 1.f / (float)H, 1.f / (float)W};
+    hipLaunchKernelGGL(bn_dz16_kernel<true>, dim3(grid_for((P + 3) / 4 * tpr)), dim3(256), 0, s, nullptr, y, ld,
+                       off, P, C, coef, mask, tpr, (__bf16*)dz16, 0, pl);
     LAUNCH_CHECK();
 }
 int k_bias_reduce(const float* slab, int S, int taps, int C, float* out, hipStream_t s) {

@@ -134,10 +134,10 @@ struct Options {
     int convt16 = 1;           // bf16 training: the ConvT forward stores the up half of the
                                // decoder's concat straight into that conv's bf16 operand image
                                // (no f32 up half; its prep pass converts the skip half only)
-    int wg16_r3 = 4;           // 3x3 layers with W % 64 == 0 on the tap-row bf16 weight gradient
-                               // (5, r05: four waves of 32 x 128 per tap, 3 stages)
-                               // (tile 3 / 4 = three / four LDS stages; 0 = off; r04 config 4:
-                               // 122.7 -> 124.5 / 125.2 img/s)
+    int wg16_r3 = 7;           // 3x3 layers with W % 64 == 0 on the tap-row bf16 weight gradient:
+                               // 7 = 16x16x32 MFMAs with the re-read stagger (r06, config 4
+                               // +1.3 % over 4, profiles/r06_c4_wg16_ab.txt), 4 = 32x32x16, four
+                               // LDS stages (r04: 122.7 -> 125.2 img/s), 0 = off (one-tap kernel)
     int wg16t = 1;             // bf16 ConvT wgrad on the same kernel
     int xcd16 = 1;             // XCD-contiguous block order, LDS-DMA kernels
     int xcd_remap = 1;         // ... f32 GEMMs: 0 none, 1 both (default: r03 PMC, HBM bytes
@@ -163,7 +163,7 @@ struct Options {
                                // profiles/r05_wwaves_ab.txt)
     int x3_wwaves1 = 3;        // the same for the one-tap x3 weight gradients (ConvT, 8x8):
                                // +0.45 % (profiles/r05_wwaves_ab.txt)
-    int pool_fuse = 1;         // x3 path: the encoder block's second conv recomputes its `do` from
+    int pool_fuse = 1;         // x3 and (r06) bf16 paths: the encoder block's second conv recomputes its `do` from
                                // the max-pool backward's inputs instead of maxpool_bwd storing it
     int head_fuse = 1;         // x3 path, one output channel: the last conv's dz pass recomputes
                                // `do` from the head instead of head_bwd storing it (r05)
@@ -276,6 +276,17 @@ struct unet_ctx {
     // up half the forward never wrote)
     Options fwd_opt;
     bool fwd_opt_set = false;
+    // (r06) weight images written by unet_adamw_repack (AdamW fused into the repack): device
+    // buffers owned by the context, valid for the parameter arena `pp_src` until
+    // unet_params_changed or another repack; pp_gen counts repacks, and a training forward that
+    // read them records the generation its backward must still see
+    float* pp = nullptr;
+    uint16_t* pp3 = nullptr;
+    const float* pp_src = nullptr;
+    bool pp_ok = false;
+    uint64_t pp_gen = 0;
+    bool fwd_used_pp = false;
+    uint64_t fwd_pp_gen = 0;
 
     int nconv() const { return (int)conv.size(); }
     int chl[MAX_DEPTH + 1] = {};                           // kernel (padded) channels per level
@@ -1253,35 +1264,63 @@ int upload_pad_tables(unet_ctx* c, Plan& p, hipStream_t s) {
     return (int)e;
 }
 
+// the pack job table of every 3x3 conv (but the Cin = in_channels first conv) and ConvT weight
+// (dgrad images too when `dgrad`); false when the table overflows
+bool build_pack_jobs(const unet_ctx* c, bool dgrad, PackJobs& jobs) {
+    jobs.n = 0;
+    int blocks = 0;
+    auto add = [&](int64_t w, int64_t f, int64_t d, int cin, int cout, int kind) {
+        PackJob& J = jobs.j[jobs.n++];
+        J.w = w;
+        J.f = f;
+        J.d = dgrad ? d : -1;
+        J.cin = cin;
+        J.cout = cout;
+        J.kind = kind;
+        J.tx = ((kind == 0 ? cin : cout) + 31) / 32;
+        J.ty = ((kind == 0 ? cout : cin) + 31) / 32;
+        J.block0 = blocks;
+        blocks += J.tx * J.ty;
+    };
+    for (const ConvL& C : c->conv) {
+        if (C.pf < 0) continue;
+        if (jobs.n >= MAX_PACK_JOBS) return false;
+        add(C.w, C.pf, C.pd, C.cin, C.cout, 0);
+    }
+    for (const ConvTL& T : c->convt) {
+        if (jobs.n >= MAX_PACK_JOBS) return false;
+        add(T.w, T.pf, T.pd, T.cin, T.cout, 1);
+    }
+    return true;
+}
+
+// whether the plan of this context carries x3 weight images (make_plan's pack3)
+bool plan_has_pack3(const unet_ctx* c) {
+    for (const ConvL& L : c->conv)
+        if (L.pf >= 0 && x3_conv_on(c, L.cin, L.cout)) return true;
+    for (const ConvTL& T : c->convt)
+        if (x3_convt_on(c, T.cin, T.cout)) return true;
+    return false;
+}
+
 int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, const float* x,
                  float* logits, Plan& p, bool training, hipStream_t s) {
     Launcher L{c, s};
     const int H = p.H, W = p.W, D = c->depth, NC = c->nconv();
-    // 1. weight images for the row GEMMs (re-packed every call: params may have changed
-    //    through the optimizer or load_state_dict; ~0.1 ms of HBM traffic per step)
-    {
+    // 1. weight images for the row GEMMs: re-packed every call (params may have changed through
+    //    the optimizer or load_state_dict; ~0.1 ms of HBM traffic per step at config 2) unless
+    //    the fused AdamW of unet_adamw_repack wrote them for exactly these parameters (r06)
+    const bool use_pp = c->pp_ok && c->pp_src == prm && c->pp && (!p.pack3 || c->pp3);
+    if (training) {
+        c->fwd_used_pp = use_pp;
+        c->fwd_pp_gen = c->pp_gen;
+    }
+    if (use_pp) {
+        p.pack = c->pp;
+        if (p.pack3) p.pack3 = c->pp3;
+    } else {
         PackJobs jobs{};
-        int blocks = 0;
-        auto add = [&](int64_t w, int64_t f, int64_t d, int cin, int cout, int kind) {
-            PackJob& J = jobs.j[jobs.n++];
-            J.w = w;
-            J.f = f;
-            J.d = training ? d : -1;
-            J.cin = cin;
-            J.cout = cout;
-            J.kind = kind;
-            J.tx = ((kind == 0 ? cin : cout) + 31) / 32;
-            J.ty = ((kind == 0 ? cout : cin) + 31) / 32;
-            J.block0 = blocks;
-            blocks += J.tx * J.ty;
-        };
-        for (int i = 0; i < NC; ++i) {
-            const ConvL& C = c->conv[i];
-            if (C.pf >= 0 && jobs.n < MAX_PACK_JOBS) add(C.w, C.pf, C.pd, C.cin, C.cout, 0);
-        }
-        for (const ConvTL& T : c->convt)
-            if (jobs.n < MAX_PACK_JOBS) add(T.w, T.pf, T.pd, T.cin, T.cout, 1);
-        if (jobs.n >= MAX_PACK_JOBS) return fail(c, UNET_ERR_INTERNAL, "pack job table full");
+        if (!build_pack_jobs(c, training, jobs)) return fail(c, UNET_ERR_INTERNAL, "pack job table full");
         if (jobs.n) RUN("pack", 0, k_pack_all(jobs, prm, p.pack, c->bf16, s));
         // option x3: the whole region as rows of 32 floats (every image 32-aligned)
         if (p.pack3)
@@ -1694,8 +1733,16 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         if (dzw) {
         } else if (dz16) {
             const bool f32 = !p.x16[i] || !(dx && rg16_on(c, C.cout, C.cin));
-            RUN("bn_dz", 0, k_bn_dz16(const_cast<float*>(dout), p.y[i], p.ldy[i], p.offy[i], P, C.cout,
-                                      p.coef, dz_mask, p.s16, f32 ? 1 : 0, s));
+            if (i == pool_src.conv && !f32) {  // (r06) do straight from the max-pool backward's inputs
+                const PoolSrc& q = pool_src;
+                RUN("bn_dz", 0, k_bn_dz16_pool(p.y[i], p.ldy[i], p.offy[i], P, C.cout, p.coef, dz_mask, p.s16,
+                                               q.dp, q.idx, q.dskip, q.ldskip, q.msc, q.msh, p.N, Hl, Wl, s));
+            } else if (i == pool_src.conv) {
+                return fail(c, UNET_ERR_INTERNAL, "pool_fuse: conv %d needs an f32 dz", i);
+            } else {
+                RUN("bn_dz", 0, k_bn_dz16(const_cast<float*>(dout), p.y[i], p.ldy[i], p.offy[i], P, C.cout,
+                                          p.coef, dz_mask, p.s16, f32 ? 1 : 0, s));
+            }
         } else {
             RUN("bn_dz", 0, k_bn_dz(const_cast<float*>(dout), p.y[i], p.ldy[i], p.offy[i], P, C.cout,
                                     p.coef, dz_mask, s));
@@ -1747,14 +1794,14 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
             int t = wg16_tile(c, C.cin, C.cout);
             // option wg16_r3: the tap-row kernel (three taps per block from one halo row)
             const int r3 = c->opt.wg16_r3;
-            if (r3 >= 3 && r3 <= 7 && Wl % 64 == 0 && C.cin % 128 == 0 && C.cout % 128 == 0 &&
+            if ((r3 == 4 || r3 == 7) && Wl % 64 == 0 && C.cin % 128 == 0 && C.cout % 128 == 0 &&
                 wc.pps % 64 == 0)
                 t = r3;
             int wbm = 0, wbn = 0, wst = 0;
             wgrad16g_tile_dims(t, &wbm, &wbn, &wst);
             char lb[96];
             snprintf(lb, sizeof lb, "conv_wgrad/wg16%s_%dx%ds%d|%d",
-                     t == 3 || t == 4 ? "r3" : t == 5 ? "r3w" : t >= 6 ? "r3m" : "", wbm, wbn, wst, i);
+                     t == 4 ? "r3" : t == 7 ? "r3m" : "", wbm, wbn, wst, i);
             RUN(lb, 2.0 * P * C.cout * 9 * C.cin, launch_wgrad16(w, t, s));
         } else {
             RUN(wlabel("conv_wgrad", wc, i), 2.0 * P * C.cout * 9 * C.cin, launch_wgrad(w, wc.tile, s));
@@ -2143,8 +2190,13 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
         // up to 2048 blocks on the large levels (512 left the pass at ~4.7 TB/s); the partial
         // rows fit: p.part holds P/64 + 1 rows of 2C for every conv of the level
         const int Gmp = wide_g(p.P[b]);
-        const bool pool_fuse = c->opt.pool_fuse && p.pack3 && c->conv[i1].cout == C &&
-                               x3_conv_on(c, c->conv[i1].cin, c->conv[i1].cout) && p.P[b] < (1 << 24);
+        const ConvL& C1 = c->conv[i1];
+        // x3: the conv's x3 dz pass; bf16 (r06): its bf16 dz pass, where no f32 dz is needed
+        // (the LDS-DMA dgrad and weight gradient read the bf16 image only)
+        const bool pool_fuse =
+            c->opt.pool_fuse && !c->res && C1.cout == C && p.P[b] < (1 << 24) &&
+            ((p.pack3 && x3_conv_on(c, C1.cin, C1.cout)) ||
+             (c->bf16 && p.x16[i1] && rg16_on(c, C1.cout, C1.cin)));
         pool_src = PoolSrc{};
         if (pool_fuse) {
             pool_src.conv = i1;
@@ -2265,20 +2317,27 @@ int unet_create(const unet_cfg* cfg, int device, unet_ctx** out) {
         // handles up to 4 classes.
         // Per level: level 0 runs the next power of two >= 32 channels (the head and
         // first-conv kernels want a power-of-two channel-quad count), every deeper level the
-        // next multiple of 32 of base_filters << l (a K-chunk is 32 channels of one tap; the
-        // 32-column row tiles and 32-channel wgrad tiles cover 96, 192, ... natively), so
-        // base 16 pads level 0 only (16 -> 32, then 32, 64, ...: r03 padded every level 2x),
-        // base 48 level 0 only (48 -> 64, then 96, 192, ...), base 24 levels 0 and 1.
+        // next multiple of 32 of base_filters << l (a K-chunk is 32 channels of one tap), and
+        // since r06 an odd multiple of 32 from 96 on the next multiple of 64 (below), so base
+        // 16 pads level 0 only (16 -> 32, then 32, 64, ...: r03 padded every level 2x), base 48
+        // levels 0 and 1 (48 -> 64, 96 -> 128, then 192, 384, ...), base 24 levels 0..2 (24 ->
+        // 32, 48 -> 64, 96 -> 128).
         c->rbase = c->base;
         if (c->base < 8 || c->base > 256 || c->base % 8 || c->depth < 1 || c->depth > MAX_DEPTH)
             return UNET_ERR_UNSUPPORTED;
         c->padded = false;
         for (int l = 0; l <= c->depth; ++l) {
             int pc = 32;
-            if (l == 0)
+            if (l == 0) {
                 while (pc < c->rbase) pc <<= 1;
-            else
+            } else {
                 pc = ((c->rbase << l) + 31) / 32 * 32;
+                // (r06) 96, 160, 224, ... channels run padded to the next multiple of 64: the
+                // x3 GEMMs (f32 math on the bf16 matrix cores) take 64-multiples, and padded x3
+                // beats the native f32 MFMA kernels (96 -> 128: 1.78x the FLOPs at ~2.2x the
+                // rate; base 48's 96-channel level 1 and base 24's level 2)
+                if (pc % 64 == 32 && pc >= 96) pc += 32;
+            }
             c->chl[l] = pc;
             c->padded = c->padded || pc != (c->rbase << l);
         }
@@ -2309,6 +2368,11 @@ int unet_destroy(unet_ctx* c) {
     if (!c) return UNET_ERR_INVALID;
     for (auto e : c->bucket_ev) (void)hipEventDestroy(e);
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
+    if (c->pp || c->pp3) {
+        (void)hipSetDevice(c->device);
+        if (c->pp) (void)hipFree(c->pp);
+        if (c->pp3) (void)hipFree(c->pp3);
+    }
     delete c;
     return UNET_OK;
     ABI_CATCH(c)
@@ -2420,6 +2484,14 @@ int unet_backward(unet_ctx* c, const float* params, const float* dlogits, float*
     make_plan(c, N, H, W, true, nullptr, p);
     if (ws_bytes < p.bytes) return fail(c, UNET_ERR_WORKSPACE, "workspace %zu < %zu", ws_bytes, p.bytes);
     make_plan(c, N, H, W, true, (char*)ws, p);
+    if (c->fwd_used_pp) {  // (r06) the forward read the fused AdamW's weight images
+        if (c->pp_gen != c->fwd_pp_gen || !c->pp_ok)
+            return fail(c, UNET_ERR_INVALID,
+                        "the weight images the training forward used were rewritten before its "
+                        "backward (unet_adamw_repack / unet_params_changed in between)");
+        p.pack = c->pp;
+        if (p.pack3) p.pack3 = c->pp3;
+    }
     if (hipSetDevice(c->device) != hipSuccess) return fail(c, UNET_ERR_HIP, "hipSetDevice");
     if (c->bucket_ev.empty()) {
         c->bucket_ev.resize(c->bucket_off.size());
@@ -2495,6 +2567,84 @@ int unet_adamw(unet_ctx* c, float* params, const float* grads, float* m, float* 
     int r = k_adamw(params, grads, m, v, n, a, (hipStream_t)stream);
     return r ? fail(c, UNET_ERR_HIP, "adamw launch %d", r) : UNET_OK;
     ABI_CATCH(c)
+}
+
+int unet_adamw_repack(unet_ctx* c, float* params, const float* grads, float* m, float* v, int64_t n,
+                      int step, double lr, double b1, double b2, double eps, double wd, double gscale,
+                      unet_stream_t stream) {
+    ABI_TRY
+    if (!c || !params || !grads || !m || !v || n < 0 || step < 1) return UNET_ERR_INVALID;
+    // a narrow (channel-padded) network packs from its padded arena: the plain update, and the
+    // next forward repacks
+    if (n != c->n_param_floats || c->padded) {
+        c->pp_ok = false;
+        return unet_adamw(c, params, grads, m, v, n, step, lr, b1, b2, eps, wd, gscale, stream);
+    }
+    if (hipSetDevice(c->device) != hipSuccess) return fail(c, UNET_ERR_HIP, "hipSetDevice");
+    const bool x3 = plan_has_pack3(c);
+    if (!c->pp && hipMalloc((void**)&c->pp, sizeof(float) * (size_t)std::max<int64_t>(c->pack_floats, 32)) != hipSuccess) {
+        c->pp = nullptr;
+        return fail(c, UNET_ERR_HIP, "hipMalloc: weight images: %lld floats", (long long)c->pack_floats);
+    }
+    if (x3 && !c->pp3 &&
+        hipMalloc((void**)&c->pp3, 3 * sizeof(uint16_t) * (size_t)std::max<int64_t>(c->pack_floats, 32)) != hipSuccess) {
+        c->pp3 = nullptr;
+        return fail(c, UNET_ERR_HIP, "hipMalloc: x3 weight images: %lld floats", (long long)c->pack_floats);
+    }
+    PackJobs jobs{};
+    if (!build_pack_jobs(c, true, jobs)) return fail(c, UNET_ERR_INTERNAL, "pack job table full");
+    // the arena ranges the pack jobs do not cover, in order
+    std::vector<std::pair<int64_t, int64_t>> wr;  // [begin, end) of the packed weight tensors
+    for (int k = 0; k < jobs.n; ++k) {
+        const PackJob& J = jobs.j[k];
+        wr.push_back({J.w, J.w + (int64_t)J.cin * J.cout * (J.kind == 0 ? 9 : 4)});
+    }
+    std::sort(wr.begin(), wr.end());
+    AdamRanges rest{};
+    int64_t at = 0, cum = 0;
+    auto gap = [&](int64_t b, int64_t e) -> bool {
+        if (e <= b) return true;
+        if (rest.n >= MAX_ADAM_RANGES) return false;
+        rest.off[rest.n] = b;
+        rest.cum[rest.n] = cum;
+        cum += e - b;
+        ++rest.n;
+        return true;
+    };
+    for (auto& r : wr) {
+        if (!gap(at, r.first)) return fail(c, UNET_ERR_INTERNAL, "adamw range table full");
+        at = std::max(at, r.second);
+    }
+    if (!gap(at, n)) return fail(c, UNET_ERR_INTERNAL, "adamw range table full");
+    rest.cum[rest.n] = cum;
+    AdamwScalars a;  // (as unet_adamw)
+    a.decay = (float)(1.0 - lr * wd);
+    a.w1 = (float)(1.0 - b1);
+    a.lerp_small = fabs(1.0 - b1) < 0.5 ? 1 : 0;
+    a.b2 = (float)b2;
+    a.w2 = (float)(1.0 - b2);
+    const double bc1 = 1.0 - pow(b1, (double)step);
+    const double bc2 = 1.0 - pow(b2, (double)step);
+    a.neg_step = (float)(-(lr / bc1));
+    a.bc2_sqrt = (float)pow(bc2, 0.5);
+    a.eps = (float)eps;
+    a.gscale = (float)gscale;
+    const hipStream_t s = (hipStream_t)stream;
+    c->pp_ok = false;
+    ++c->pp_gen;
+    int r = k_pack_adamw(jobs, rest, params, grads, m, v, a, c->pp, c->bf16 ? 1 : 0, s);
+    if (!r && x3) r = k_to_x3(c->pp, 32, 0, 32, nullptr, nullptr, 0, c->pack_floats / 32, c->pp3, 32, 0, s);
+    if (r) return fail(c, UNET_ERR_HIP, "adamw repack launch %d", r);
+    c->pp_src = params;
+    c->pp_ok = true;
+    return UNET_OK;
+    ABI_CATCH(c)
+}
+
+int unet_params_changed(unet_ctx* c) {
+    if (!c) return UNET_ERR_INVALID;
+    c->pp_ok = false;
+    return UNET_OK;
 }
 
 int unet_x3_split_host(const float* v, int64_t n, uint16_t* out) {

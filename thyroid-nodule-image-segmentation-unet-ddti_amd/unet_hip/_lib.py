@@ -73,6 +73,9 @@ SIGNATURES = {
                               c_void_p, c_void_p, c_void_p, c_float, c_float, c_float, c_void_p]),
     "unet_adamw": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int,
                            c_double, c_double, c_double, c_double, c_double, c_double, c_void_p]),
+    "unet_adamw_repack": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int,
+                                  c_double, c_double, c_double, c_double, c_double, c_double, c_void_p]),
+    "unet_params_changed": (c_int, [c_void_p]),
     "unet_set_option": (c_int, [c_void_p, c_char_p, c_int64]),
     "unet_get_option": (c_int, [c_void_p, c_char_p, P(c_int64)]),
     "unet_mask_counts": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p,

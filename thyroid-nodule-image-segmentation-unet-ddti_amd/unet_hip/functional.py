@@ -20,6 +20,7 @@ from ._lib import HipUnavailable
 class UNetFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, state, *params):
+        state.sync_params()
         logits, ws = state.rt.forward(state.param_arena, state.bn_arena, state.nbt_arena, x,
                                       training=True)
         ctx.state = state

@@ -20,6 +20,8 @@ num_batches_tracked) and the whole network runs as one native call.  Moving the 
 (``.to()``, ``.cuda()``) re-flattens lazily.  CPU tensors raise ``HipUnavailable``:
 there is no silent CPU fallback.
 """
+import weakref
+
 import torch
 import torch.nn as nn
 
@@ -43,6 +45,19 @@ def _upconv_block(cin, cout):
                          nn.ConvTranspose2d(cin // 2, cout, kernel_size=2, stride=2))
 
 
+# parameter arena (data_ptr, numel) -> its _ArenaState, so HipAdamW finds the context whose
+# fused AdamW + repack (unet_adamw_repack) knows the arena's layout
+_ARENAS = weakref.WeakValueDictionary()
+
+
+def arena_owner(flat):
+    """The _ArenaState whose parameter arena is exactly `flat` (same storage span), or None."""
+    st = _ARENAS.get((flat.data_ptr(), flat.numel()))
+    if st is None or st.param_arena.data_ptr() != flat.data_ptr():
+        return None
+    return st
+
+
 class _ArenaState:
     """Flat device arenas shared by the module and the autograd function."""
 
@@ -53,6 +68,27 @@ class _ArenaState:
         self.bn_arena = bn_arena
         self.nbt_arena = nbt_arena
         self.grad_arena = None
+        # the torch version counters (the arena's plus every parameter's: a Parameter whose
+        # .data was re-pointed into the arena keeps its own counter) when the native weight
+        # images were last known to match the parameters: None = never (the first forward
+        # repacks).  Any torch in-place write to a parameter (load_state_dict, a torch optimizer,
+        # user code under no_grad) bumps one of them; the native AdamW writes through the
+        # pointer and bumps none.  Writes through `.data` bypass every counter, as they bypass
+        # autograd: call the module's params_changed() after those.
+        self.native_version = None
+        _ARENAS[(param_arena.data_ptr(), param_arena.numel())] = self
+        # a new arena may reuse the address of one whose images the (shared) context holds
+        rt.params_changed()
+
+    def version(self):
+        return self.param_arena._version + sum(p._version for p, _, _ in self.params)
+
+    def sync_params(self):
+        """Tell the native side when the parameters changed outside unet_adamw_repack."""
+        v = self.version()
+        if v != self.native_version:
+            self.rt.params_changed()
+            self.native_version = v
 
     def grad_arena_for_backward(self):
         # gradients are written with '=' semantics (zero_grad(set_to_none) is the reference's
@@ -155,9 +191,18 @@ class _HipUNet(nn.Module):
             p.requires_grad for p, _, _ in st.params)
         if need_grad:
             return UNetFunction.apply(x, st, *[p for p, _, _ in st.params])
+        st.sync_params()
         logits, _ = st.rt.forward(st.param_arena, st.bn_arena, st.nbt_arena, x,
                                   training=self.training)
         return logits
+
+    def params_changed(self):
+        """Declare parameter writes the version counters cannot see (through `.data`): the next
+        forward repacks the native weight images."""
+        st = self._state
+        if st is not None:
+            st.rt.params_changed()
+            st.native_version = None
 
     @property
     def flat_params(self):

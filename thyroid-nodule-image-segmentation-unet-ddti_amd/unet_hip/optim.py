@@ -102,7 +102,15 @@ class HipAdamW(torch.optim.Optimizer):
                 if m is None or not self._views_of(params, m, v):
                     m, v = self._rebuild_flat(params, fp)
                     self._flat = {key: (m, v)}
-                rt.adamw(fp, fg, m, v, step, lr, b1, b2, eps, wd, self.grad_scale)
+                # (r06) the whole arena of a HIP model: AdamW fused with its next forward's
+                # weight repack (unet_adamw_repack, bit-identical to unet_adamw)
+                from .module import arena_owner
+                st = arena_owner(fp)
+                if st is not None and fg.numel() == fp.numel():
+                    st.rt.adamw_repack(fp, fg, m, v, step, lr, b1, b2, eps, wd, self.grad_scale)
+                    st.native_version = st.version()  # the images match the parameters
+                else:
+                    rt.adamw(fp, fg, m, v, step, lr, b1, b2, eps, wd, self.grad_scale)
             else:
                 for p in params:
                     s = self.state[p]

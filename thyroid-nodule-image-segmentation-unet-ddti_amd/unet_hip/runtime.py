@@ -136,6 +136,19 @@ class UNetRuntime:
                                  _lib.stream_ptr(params.device))
         _lib.check(rc, self.ctx, "unet_adamw")
 
+    def adamw_repack(self, params, grads, m, v, step, lr, beta1, beta2, eps, wd, grad_scale=1.0):
+        """AdamW over this context's whole parameter arena fused with the next forward's weight
+        repack (unet_adamw_repack; bit-identical to adamw)."""
+        rc = self.lib.unet_adamw_repack(self.ctx, _lib.ptr(params), _lib.ptr(grads), _lib.ptr(m),
+                                        _lib.ptr(v), params.numel(), step, float(lr), float(beta1),
+                                        float(beta2), float(eps), float(wd), float(grad_scale),
+                                        _lib.stream_ptr(params.device))
+        _lib.check(rc, self.ctx, "unet_adamw_repack")
+
+    def params_changed(self):
+        """The parameter arena changed outside adamw_repack: the next forward repacks."""
+        _lib.check(self.lib.unet_params_changed(self.ctx), self.ctx, "unet_params_changed")
+
     # ------------------------------------------------------------------ schedule options
     def set_option(self, name, value):
         """Kernel-schedule option (include/unet_hip.h unet_set_option); A/B runs and tests."""
