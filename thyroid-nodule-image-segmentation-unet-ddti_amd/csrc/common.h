@@ -177,7 +177,7 @@ int wgrad_tile_taps(int tile);  // taps of the M dimension one block covers (3 f
 // a16 / bt16 are x3 images (lda channels per A row, aoff a channel offset); tiles 0 =
 // 256x128, 1 = 128x128, 2 = 128x64, 3 = 256x64; tap-row halo tiles 4 = 256x128, 6 = 128x64.
 // Weight gradient: a / b are x3 images; tiles 0 = 128x128, 1 = 64x64; tap-row tiles 2 = 64x128,
-// 3 = 128x64, 4 = 64x64.
+// 4 = 64x64.
 int launch_rowgemm_x3(const RowGemmArgs& a, int tile, hipStream_t s);
 int rowgemm_x3_tile_dims(int tile, int* bm, int* bn);
 int launch_wgrad_x3(const WgradArgs& a, int tile, hipStream_t s);

@@ -1403,11 +1403,12 @@ int k_to_x3(const float* src, int ld, int off, int C, const float* scale, const 
     return (int)hipGetLastError();
 }
 
-// tap-row tiles (BM ci x BN co per tap, three taps per block): 2 = 64x128, 3 = 128x64, 4 = 64x64
-static const int WX3R3_DIMS[5][2] = {{0, 0}, {0, 0}, {64, 128}, {128, 64}, {64, 64}};
+// tap-row tiles (BM ci x BN co per tap, three taps per block): 2 = 64x128, 4 = 64x64 (r05-r06
+// tile 3, 128x64, measured 20 % slower than 4 on config 2's 128 -> 64 conv and was removed)
+static const int WX3R3_DIMS[5][2] = {{0, 0}, {0, 0}, {64, 128}, {0, 0}, {64, 64}};
 
 int wgrad_x3_tile_dims(int tile, int* bm, int* bn) {
-    if (tile >= 2 && tile <= 4) {
+    if (tile == 2 || tile == 4) {
         *bm = WX3R3_DIMS[tile][0];
         *bn = WX3R3_DIMS[tile][1];
         return 0;
@@ -1431,7 +1432,7 @@ int wgrad_x3_tile_dims(int tile, int* bm, int* bn) {
 int launch_wgrad_x3(const WgradArgs& a, int tile, hipStream_t s) {
     if (a.ascale || a.bcoef || a.bias_slab || !a.zero16 || a.P < 1) return -1;
     if (a.aoff % 32 || a.boff % 32 || a.lda % 32 || a.ldb % 32) return -1;
-    if (tile >= 2 && tile <= 4) {  // tap-row kernel: 3x3 convs, W % 32 == 0 or W = 16 with an even H
+    if (tile == 2 || tile == 4) {  // tap-row kernel: 3x3 convs, W % 32 == 0 or W = 16 with an even H
         int bm = 0, bn = 0;
         wgrad_x3_tile_dims(tile, &bm, &bn);
         const bool w16 = a.W == 16 && a.H % 2 == 0;
@@ -1439,15 +1440,11 @@ int launch_wgrad_x3(const WgradArgs& a, int tile, hipStream_t s) {
             a.CA % bm || a.CB % bn || (a.W % 32 && !w16) || a.pps % 32 || a.P % 32)
             return -1;
         const dim3 grid((a.CA / bm) * 3 * (a.CB / bn) * a.splits);
-        // 64 x 128: four stages with the stagger (r05 schedule 10); 128 x 64 / 64 x 64 without it
+        // 64 x 128: four stages with the stagger (r05 schedule 10); 64 x 64 without it
         if (tile == 2 && w16)
             hipLaunchKernelGGL((wgrad_x3_row3_kernel<64, 128, 4, 1, true, true>), grid, dim3(512), 0, s, a);
         else if (tile == 2)
             hipLaunchKernelGGL((wgrad_x3_row3_kernel<64, 128, 4, 1, true>), grid, dim3(512), 0, s, a);
-        else if (tile == 3 && w16)
-            hipLaunchKernelGGL((wgrad_x3_row3_kernel<128, 64, 3, 1, false, true>), grid, dim3(512), 0, s, a);
-        else if (tile == 3)
-            hipLaunchKernelGGL((wgrad_x3_row3_kernel<128, 64, 3, 1>), grid, dim3(512), 0, s, a);
         else if (w16)  // 64 x 64: four waves, two LDS stages, two blocks per CU
             hipLaunchKernelGGL((wgrad_x3_row3_kernel<64, 64, 2, 2, false, true>), grid, dim3(256), 0, s, a);
         else

@@ -34,6 +34,31 @@ struct AdamTile {
     float* v;
     AdamwScalars a;
 };
+// N elements of one thread at once: every load of the batch issues before the first store
+// (element by element, each element's p / m / v stores held the next element's loads back:
+// the fused kernel then ran slower than unet_adamw + the repack)
+template <int N>
+__device__ __forceinline__ void adam_batch(const AdamTile& t, const int64_t (&ix)[N], const bool (&ok)[N],
+                                           float (&out)[N]) {
+    float p[N], g[N], m[N], v[N];
+#pragma unroll
+    for (int k = 0; k < N; ++k)
+        if (ok[k]) {
+            p[k] = t.p[ix[k]];
+            g[k] = t.g[ix[k]];
+            m[k] = t.m[ix[k]];
+            v[k] = t.v[ix[k]];
+        }
+#pragma unroll
+    for (int k = 0; k < N; ++k)
+        if (ok[k]) {
+            adamw_elem(p[k], g[k], m[k], v[k], t.a);
+            t.p[ix[k]] = p[k];
+            t.m[ix[k]] = m[k];
+            t.v[ix[k]] = v[k];
+            out[k] = p[k];
+        }
+}
 template <bool ADAM>
 __device__ __forceinline__ float pack_load(const float* __restrict__ w, const AdamTile& t, int64_t i) {
     if constexpr (ADAM) {
@@ -70,12 +95,33 @@ __device__ void pack_conv3_tile(const float* __restrict__ w, OUT* __restrict__ w
     const int tid = threadIdx.x;
     if (nci == T && nco == T) {
         // full tile: 36 independent loads per thread in flight before the LDS stores
-        float v[T * T * 9 / 256];
+        constexpr int NK = T * T * 9 / 256;
+        float v[NK];
+        if constexpr (ADAM) {
+            constexpr int CH = 12;  // 48 loads in flight per thread
 #pragma unroll
-        for (int k = 0; k < T * T * 9 / 256; ++k) {
-            const int e = tid + 256 * k;  // e = co_l * 288 + (ci_l * 9 + tap)
-            const int co_l = e / (T * 9), r = e - co_l * (T * 9);
-            v[k] = pack_load<ADAM>(w, at, ((int64_t)(co0 + co_l) * cin + ci0) * 9 + r);
+            for (int k0 = 0; k0 < NK; k0 += CH) {
+                int64_t ix[CH];
+                bool ok[CH];
+                float o[CH];
+#pragma unroll
+                for (int k = 0; k < CH; ++k) {
+                    const int e = tid + 256 * (k0 + k);
+                    const int co_l = e / (T * 9), r = e - co_l * (T * 9);
+                    ix[k] = ((int64_t)(co0 + co_l) * cin + ci0) * 9 + r;
+                    ok[k] = true;
+                }
+                adam_batch<CH>(at, ix, ok, o);
+#pragma unroll
+                for (int k = 0; k < CH; ++k) v[k0 + k] = o[k];
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < NK; ++k) {
+                const int e = tid + 256 * k;  // e = co_l * 288 + (ci_l * 9 + tap)
+                const int co_l = e / (T * 9), r = e - co_l * (T * 9);
+                v[k] = w[((int64_t)(co0 + co_l) * cin + ci0) * 9 + r];
+            }
         }
 #pragma unroll
         for (int k = 0; k < T * T * 9 / 256; ++k) {
@@ -122,10 +168,31 @@ __device__ void pack_convT_tile(const float* __restrict__ w, OUT* __restrict__ t
     constexpr int T = 32, AS = 40, RS = 4 * AS + 1;  // tile: [ci_l][ab][co_l]
     const int nci = min(T, cin - ci0), nco = min(T, cout - co0);
     const int tid = threadIdx.x;
-    for (int e = tid; e < T * T * 4; e += 256) {  // e = ci_l * 128 + (co_l * 4 + ab)
-        const int ci_l = e / (T * 4), r = e - ci_l * (T * 4);
-        if (ci_l < nci && r < nco * 4)
-            tile[ci_l * RS + (r & 3) * AS + (r >> 2)] = pack_load<ADAM>(w, at, ((int64_t)(ci0 + ci_l) * cout + co0) * 4 + r);
+    if constexpr (ADAM) {  // 16 elements per thread, loads batched (adam_batch)
+        constexpr int NK = T * T * 4 / 256;
+        int64_t ix[NK];
+        bool ok[NK];
+        float o[NK];
+#pragma unroll
+        for (int k = 0; k < NK; ++k) {
+            const int e = tid + 256 * k;
+            const int ci_l = e / (T * 4), r = e - ci_l * (T * 4);
+            ok[k] = ci_l < nci && r < nco * 4;
+            ix[k] = ((int64_t)(ci0 + ci_l) * cout + co0) * 4 + r;
+        }
+        adam_batch<NK>(at, ix, ok, o);
+#pragma unroll
+        for (int k = 0; k < NK; ++k) {
+            const int e = tid + 256 * k;
+            const int ci_l = e / (T * 4), r = e - ci_l * (T * 4);
+            if (ok[k]) tile[ci_l * RS + (r & 3) * AS + (r >> 2)] = o[k];
+        }
+    } else {
+        for (int e = tid; e < T * T * 4; e += 256) {  // e = ci_l * 128 + (co_l * 4 + ab)
+            const int ci_l = e / (T * 4), r = e - ci_l * (T * 4);
+            if (ci_l < nci && r < nco * 4)
+                tile[ci_l * RS + (r & 3) * AS + (r >> 2)] = w[((int64_t)(ci0 + ci_l) * cout + co0) * 4 + r];
+        }
     }
     __syncthreads();
     const int l = tid & 31, g = tid >> 5;  // 8 groups of 32 lanes

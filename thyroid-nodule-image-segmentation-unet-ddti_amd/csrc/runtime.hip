@@ -830,7 +830,7 @@ int x3_tile(const unet_ctx* c, const RowGemmArgs& g) {
 // pixels so the grid has >= x3_wblocks 128x128 blocks (4x that of 64x64 ones); pixels per
 // split a multiple of 256
 // 3x3 convs on rows of a multiple of 32 pixels (row_w): the tap-row kernel (tiles 2 = 64x128,
-// 3 = 128x64 per tap, three taps per block)
+// 4 = 64x64 per tap, three taps per block)
 WgradCfg x3_wgrad_cfg(const unet_ctx* c, int CA, int tapsA, int CB, int tapsB, int64_t P,
                       int row_w = 0, int row_h = 0) {
     WgradCfg w{};
@@ -838,8 +838,9 @@ WgradCfg x3_wgrad_cfg(const unet_ctx* c, int CA, int tapsA, int CB, int tapsB, i
     // tap-row kernel: rows of 32k pixels, or (r05) 16-pixel rows in pairs
     const bool w16 = row_w == 16 && row_h % 2 == 0 && CA % 64 == 0 && CB % 64 == 0;
     const bool r3 = tapsA == 9 && tapsB == 1 && ((row_w % 32 == 0 && row_w > 0) || w16);
+    // (r06: 64 x 64 rather than 128 x 64 where only the input channels divide 128 -- config 2's
+    // 128 -> 64 level-0 conv 1.53 -> 1.24 ms, profiles/r06_c2_wtile_ab.txt; tile 3 removed)
     if (r3 && CA % 64 == 0 && CB % 128 == 0) w.tile = 2;
-    else if (r3 && CA % 128 == 0 && CB % 64 == 0) w.tile = 3;
     else if (r3 && CA % 64 == 0 && CB % 64 == 0) w.tile = 4;
     if (c->opt.x3_wtile >= 0) {
         int bm = 0, bn = 0;
@@ -849,7 +850,7 @@ WgradCfg x3_wgrad_cfg(const unet_ctx* c, int CA, int tapsA, int CB, int tapsB, i
     }
     wgrad_x3_tile_dims(w.tile, &w.bm, &w.bn);
     w.bkp = 32;
-    const bool tap_row = w.tile >= 2 && w.tile <= 4;
+    const bool tap_row = w.tile == 2 || w.tile == 4;
     const int64_t tiles = tap_row ? (int64_t)(CA / w.bm) * 3 * (CB / w.bn)
                                   : (int64_t)(tapsA * CA / w.bm) * (tapsB * CB / w.bn);
     // blocks per 128x128 one-tap block of work: by area (one-tap), half that (tap-row)
