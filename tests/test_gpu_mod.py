@@ -239,13 +239,16 @@ def test_rg16_bit_identical_to_register_staged(tile, wtile):
     Cin = 1 first conv takes the new path: the same bf16 roundings of the same f32 values,
     the same K order, split-K partition and 128-row BN partial groups, so one training step
     gives bit-identical logits, gradients and BN statistics for every row tile (256-row
-    tiles included) and every weight-gradient tile."""
+    tiles included) and every weight-gradient tile.  The tap-row weight gradient (wg16_r3,
+    default 7 since r06) sums K in another order and is pinned to the one-tap kernel here
+    (its own test: test_wg16_tap_row_bit_identical)."""
     x, t = inputs(23, 2, 128, 128)
     P = MO.make_params(9, 128, 3)
     outs = []
     for flag in (0, 1):
         m = _bf16_model(P, 128, 3)
-        with options(m.flatten_().rt, rg16=flag, wg16=flag, rg16_tile=tile, wg16_tile=wtile):
+        with options(m.flatten_().rt, rg16=flag, wg16=flag, rg16_tile=tile, wg16_tile=wtile,
+                     wg16_r3=0):
             outs.append(_bf16_step(m, x, t))
     _assert_same(outs[0], outs[1], f"tile {tile}/{wtile}")
 

@@ -14,7 +14,7 @@ if [ "$K" != "-" ]; then
   grep -E "^FAILED|^ERROR" gpurun_out/$TAG.pytest.log | head
   [ $rc -ne 0 ] && exit $rc
 fi
-for cfg in c4 c2; do
+for cfg in ${CFGS:-c4 c2}; do
   if [ $cfg = c4 ]; then BA="--config 4 --mfma bf16 --steps 6 --warmup 2"; else BA="--steps 10 --warmup 3"; fi
   for r in $(seq 1 $N); do
     i=0
