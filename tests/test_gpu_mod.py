@@ -288,24 +288,27 @@ def test_rg16_tile_group_bit_identical():
     _assert_same(outs[0], outs[1], "tile_group")
 
 
-def test_convt16_and_pool_fuse_bit_identical():
-    """Options convt16 and pool_fuse (default on) in a bf16 training step.  convt16: the ConvT
-    forward stores bf16 of its output straight into the decoder conv's kept operand image (the
-    same RNE rounding of the same f32 value k_to_bf16 applies) and that conv's prep pass
-    converts the skip half only.  pool_fuse (r06 on the bf16 path): each encoder block's second
-    conv forms its `do` = mask (dskip + routed dpool) inside its bf16 dz pass from the max-pool
-    backward's inputs instead of reading a full-resolution do that maxpool_bwd stored.  BASELINE
-    config 4's network, one step at 128^2: each off is bit-identical to both on."""
+def test_convt16_pool_and_head_fuse_bit_identical():
+    """Options convt16, pool_fuse and head_fuse (default on) in a bf16 training step.  convt16:
+    the ConvT forward stores bf16 of its output straight into the decoder conv's kept operand
+    image (the same RNE rounding of the same f32 value k_to_bf16 applies) and that conv's prep
+    pass converts the skip half only.  pool_fuse (r06 on the bf16 path): each encoder block's
+    second conv forms its `do` = mask (dskip + routed dpool) inside its bf16 dz pass from the
+    max-pool backward's inputs instead of reading a full-resolution do that maxpool_bwd stored.
+    head_fuse (r06 on the bf16 path): the last conv's bf16 dz pass forms its `do` = [fma(y, sc,
+    sh) > 0] dl w from the logit gradient, so head_bwd stores none.  BASELINE config 4's
+    network, one step at 128^2: each off is bit-identical to all on."""
     x, t = inputs(53, 2, 128, 128)
     P = MO.make_params(59, 128, 5)
     outs = {}
-    for flags in ((1, 1), (0, 1), (1, 0)):
+    for flags in ((1, 1, 1), (0, 1, 1), (1, 0, 1), (1, 1, 0)):
         m = _bf16_model(P, 128, 5)
-        with options(m.flatten_().rt, convt16=flags[0], pool_fuse=flags[1]):
+        with options(m.flatten_().rt, convt16=flags[0], pool_fuse=flags[1], head_fuse=flags[2]):
             outs[flags] = _bf16_step(m, x, t)
         del m
-    _assert_same(outs[(1, 1)], outs[(0, 1)], "convt16")
-    _assert_same(outs[(1, 1)], outs[(1, 0)], "pool_fuse")
+    _assert_same(outs[(1, 1, 1)], outs[(0, 1, 1)], "convt16")
+    _assert_same(outs[(1, 1, 1)], outs[(1, 0, 1)], "pool_fuse")
+    _assert_same(outs[(1, 1, 1)], outs[(1, 1, 0)], "head_fuse")
 
 
 def test_wg16_tap_row_bit_identical():

@@ -251,17 +251,20 @@ def test_negative_gamma_matches_golden(golden_dir):
         assert abs(n - f["grad_norm"][ti]) <= GRAD_TOL * f["grad_norm"][ti], name
 
 
-def test_losses_and_grads_vs_torch():
-    """Fused BCE/Dice/FocalTversky kernel vs torch fp32 ops (incl. soft targets, mixup)."""
+@pytest.mark.parametrize("shape", [(4, 1, 96, 80), (3, 1, 97, 101), (2, 1, 512, 512)])
+def test_losses_and_grads_vs_torch(shape):
+    """Fused BCE/Dice/FocalTversky kernel vs torch fp32 ops (incl. soft targets, mixup).  Shapes:
+    one chunk per sample; (r06) two chunks of an odd size (the scalar loop); 64 chunks per
+    sample (config 4's 512^2 logits)."""
     import unet_hip
     g = torch.Generator().manual_seed(3)
-    x = (torch.randn(4, 1, 96, 80, generator=g) * 4).to(DEV)
-    t = torch.rand(4, 1, 96, 80, generator=g).to(DEV)  # soft targets
+    x = (torch.randn(*shape, generator=g) * 4).to(DEV)
+    t = torch.rand(*shape, generator=g).to(DEV)  # soft targets
     w = torch.tensor([0.7, 1.3, 0.5], device=DEV)
     xr = x.clone().requires_grad_(True)
     pr = torch.sigmoid(xr)
     bce = torch.nn.functional.binary_cross_entropy_with_logits(xr, t)
-    pf, tf = pr.view(4, -1), t.view(4, -1)
+    pf, tf = pr.view(shape[0], -1), t.view(shape[0], -1)
     dice = 1 - ((2 * (pf * tf).sum(1) + 1) / (pf.sum(1) + tf.sum(1) + 1)).mean()
     TP = (pr * t).sum()
     FP = (pr * (1 - t)).sum()

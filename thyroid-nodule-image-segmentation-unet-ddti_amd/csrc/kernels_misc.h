@@ -60,8 +60,12 @@ int k_bn_dz(float* d, const float* y, int ld, int off, int64_t P, int C, const f
 int k_to_bf16(const float* src, int ld, int off, int C, const float* scale, const float* shift,
               int relu, int64_t P, uint16_t* dst, hipStream_t s, int dld = 0);
 // bn_dz writing the dense bf16 image of dz (and the f32 dz in place when f32 != 0)
+// (r06) hdl != null (option head_fuse, one output channel): do = [hrelu: fma(y, hsc, hsh) > 0]
+// hdl[m] hw[c] recomputed from the head (d unused, f32 must be 0)
 int k_bn_dz16(float* d, const float* y, int ld, int off, int64_t P, int C, const float* coef,
-              int mask, uint16_t* dz16, int f32, hipStream_t s);
+              int mask, uint16_t* dz16, int f32, hipStream_t s, const float* hdl = nullptr,
+              const float* hw = nullptr, const float* hsc = nullptr, const float* hsh = nullptr,
+              int hrelu = 0);
 // (r06) the same with `do` recomputed from the max-pool backward's inputs (option pool_fuse):
 // do = [msc: fma(msc, y, msh) > 0] (dskip + [idx == window position] dp); no f32 dz
 int k_bn_dz16_pool(const float* y, int ld, int off, int64_t P, int C, const float* coef, int mask,
@@ -104,8 +108,10 @@ struct PadDesc {
 int k_pad_copy(const PadDesc* table, int n, int64_t max_numel, const float* src, float* dst,
                int expand, hipStream_t s);
 // Losses: per-sample stats fp32[4N] + batch sums fp64[8] (see kernels_misc.hip)
+// (r06) chunks per sample of loss_stats_kernel; part holds 4 * N * loss_groups(per) floats
+int loss_groups(int64_t per);
 int k_loss_stats(const float* x, const float* t, int N, int64_t per, float* stats, double* sums,
-                 hipStream_t s);
+                 float* part, hipStream_t s);
 int k_loss_finalize(const double* sums, float alpha, float beta, float gamma, float* losses,
                     hipStream_t s);
 int k_loss_bwd(const float* x, const float* t, int N, int64_t per, const float* stats,

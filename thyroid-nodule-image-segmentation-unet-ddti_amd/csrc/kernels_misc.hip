@@ -834,12 +834,23 @@ struct Dz16Pool {
     int H, W;              // full-resolution grid
     float rH, rW;
 };
-template <bool POOL>
+// HEAD (r06, option head_fuse on the bf16 path): the last conv's do = [BN -> ReLU: fma(y, sc, sh)
+// > 0] dl[m] w[c], head_bwd's expression bit for bit (one output channel), as
+// kernels_gemm_x3.hip bn_dz_x3_kernel<1>: head_bwd stores no full-resolution f32 do
+struct Dz16Head {
+    const float* dl;       // d logits [P]
+    const float* w;        // head weights [C]
+    const float *sc, *sh;  // the last BN's forward affine
+    int relu;
+};
+template <int SRC>  // 0: do from memory, 1: Dz16Head, 2: Dz16Pool
 __global__ __launch_bounds__(256) void bn_dz16_kernel(float* __restrict__ d, const float* __restrict__ y,
                                                       int ld, int off, int64_t P, int C,
                                                       const float* __restrict__ coef, int mask,
-                                                      int tpr, __bf16* __restrict__ dz16, int f32, Dz16Pool pl) {
+                                                      int tpr, __bf16* __restrict__ dz16, int f32, Dz16Pool pl,
+                                                      Dz16Head hd) {
     typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+    constexpr bool POOL = SRC == 2, HEAD = SRC == 1;
     constexpr int U = 4;  // rows per thread per trip: 16 independent 16-B loads in flight
     const int rpp = 256 / tpr;
     const int c_first = (threadIdx.x % tpr) * 8;
@@ -848,7 +859,7 @@ __global__ __launch_bounds__(256) void bn_dz16_kernel(float* __restrict__ d, con
         for (int c = c_first; c < C; c += tpr * 8) {
             // the BN -> ReLU mask affine of this thread's 8 channels, in registers (loaded per
             // element inside the row loop, the fused pass ran 1.5x slower than the unfused pair)
-            f32x4 msc[2], msh[2];
+            f32x4 msc[2], msh[2], hw[2], hs[2], hh[2];
             if (POOL && pl.msc) {
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
@@ -856,8 +867,17 @@ __global__ __launch_bounds__(256) void bn_dz16_kernel(float* __restrict__ d, con
                     msh[h] = *(const f32x4*)(pl.msh + c + 4 * h);
                 }
             }
+            if constexpr (HEAD) {
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    hw[h] = *(const f32x4*)(hd.w + c + 4 * h);
+                    hs[h] = *(const f32x4*)(hd.sc + c + 4 * h);
+                    hh[h] = *(const f32x4*)(hd.sh + c + 4 * h);
+                }
+            }
             f32x4 dv[U][2], yv[U][2];
             f32x4 gp[U][2];
+            float dl[U];
             uint32_t wi[U][2];
             int kk[U];
 #pragma unroll
@@ -865,6 +885,7 @@ __global__ __launch_bounds__(256) void bn_dz16_kernel(float* __restrict__ d, con
                 const int64_t m = m0 + u * rpp;
                 if (m < P) {
                     int64_t po = 0;
+                    if constexpr (HEAD) dl[u] = hd.dl[m];
                     if constexpr (POOL) {
                         const Pix q = decode_fast((int)m, pl.H, pl.W, pl.rH, pl.rW);
                         po = ((int64_t)q.img * (pl.H >> 1) + (q.y >> 1)) * (pl.W >> 1) + (q.x >> 1);
@@ -878,7 +899,7 @@ __global__ __launch_bounds__(256) void bn_dz16_kernel(float* __restrict__ d, con
                         if constexpr (POOL) {
                             dv[u][h] = *(const f32x4*)(pl.dskip + m * pl.ldskip + c + 4 * h);
                             gp[u][h] = *(const f32x4*)(pl.dp + po * C + c + 4 * h);
-                        } else {
+                        } else if constexpr (!HEAD) {
                             dv[u][h] = *(const f32x4*)(d + m * C + c + 4 * h);
                         }
                         yv[u][h] = *(const f32x4*)(y + m * ld + off + c + 4 * h);
@@ -895,6 +916,17 @@ __global__ __launch_bounds__(256) void bn_dz16_kernel(float* __restrict__ d, con
                             if (((wi[u][h] >> (8 * j)) & 0xFF) == (uint32_t)kk[u]) dv[u][h][j] += gp[u][h][j];
                             if (pl.msc && !(__builtin_fmaf(msc[h][j], yv[u][h][j], msh[h][j]) > 0.f))
                                 dv[u][h][j] = 0.f;
+                        }
+            }
+            if constexpr (HEAD) {
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+#pragma unroll
+                    for (int h = 0; h < 2; ++h)
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            const bool on = !hd.relu || __builtin_fmaf(yv[u][h][j], hs[h][j], hh[h][j]) > 0.f;
+                            dv[u][h][j] = on ? dl[u] * hw[h][j] : 0.f;
                         }
             }
             f32x4 ka[2], kb[2], kc[2], km[2];
@@ -920,7 +952,7 @@ __global__ __launch_bounds__(256) void bn_dz16_kernel(float* __restrict__ d, con
                         o[j] = (!mask || v[j] > 0.f) ? r[j] : 0.f;
                         o16[4 * h + j] = (__bf16)o[j];
                     }
-                    if (!POOL && f32) *(f32x4*)(d + m * C + c + 4 * h) = o;
+                    if (SRC == 0 && f32) *(f32x4*)(d + m * C + c + 4 * h) = o;
                 }
                 *(bf16x8*)(dz16 + m * C + c) = o16;
             }
@@ -1188,6 +1220,39 @@ __global__ __launch_bounds__(256) void slab_reduce_wide_kernel(const float* __re
         }
         grad[o] = s4[j];
     }
+}
+
+// (r06) 2x2 ConvT weight gradient, slab rows m = ci, columns n = ab * cout + co ->
+// grad[ci][co][ab]: one thread per (ci, co) reads its four ab columns (coalesced along co) and
+// stores one float4 (slab_reduce_kernel wrote each float 16 B from the next, which on the
+// 4096 -> 2048 ConvT of config 4 ran its 268 MB at 1.3 TB/s).  Per element the S slabs are
+// summed in exactly slab_reduce_kernel's association: identical bits.
+__global__ __launch_bounds__(256) void slab_reduce_convT_kernel(const float* __restrict__ slab, int S,
+                                                                int cin, int cout,
+                                                                float* __restrict__ grad) {
+    const int64_t total = (int64_t)cin * 4 * cout;
+    const int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (q >= (int64_t)cin * cout) return;
+    const int ci = (int)(q / cout), co = (int)(q - (int64_t)ci * cout);
+    f32x4 r;
+#pragma unroll
+    for (int ab = 0; ab < 4; ++ab) {
+        const float* sp = slab + (int64_t)ci * 4 * cout + ab * cout + co;
+        float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+        int k = 0;
+        for (; k + 8 <= S; k += 8) {
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = sp[(int64_t)(k + u) * total];
+            a0 += v[0] + v[4];
+            a1 += v[1] + v[5];
+            a2 += v[2] + v[6];
+            a3 += v[3] + v[7];
+        }
+        for (; k < S; ++k) a0 += sp[(int64_t)k * total];
+        r[ab] = (a0 + a1) + (a2 + a3);
+    }
+    *(f32x4*)(grad + q * 4) = r;
 }
 
 // 3x3 weight gradient, slab rows m = tap * cin + ci, columns n = co -> grad[co][ci][tap]
@@ -1482,28 +1547,44 @@ __global__ __launch_bounds__(256) void res_first_wgrad_kernel(const float* __res
 }
 
 // -------------------------------------------------------------------------------------
-// Losses (utils/trainer.py:85-88; models/loss.py:13-46).  One block per sample:
+// Losses (utils/trainer.py:85-88; models/loss.py:13-46).  Per sample:
 //   stats[n] = {I = sum p t, Sp = sum p, St = sum t, Sbce = sum bce_elem}
 // bce_elem = (1 - t) x - log_sigmoid(x), log_sigmoid(x) = min(x,0) - log1p(exp(-|x|))
 // (ATen binary_cross_entropy_with_logits), p = 1 / (1 + exp(-x)).
+// (r06) G = loss_groups(per) blocks per sample (a function of the sample size only, so a
+// sample's statistics carry the same bits whatever the batch or its split over ranks) each
+// write the four sums of one contiguous chunk to part[n][g]; loss_sums_kernel adds the G
+// chunks of a sample in order.  One block per sample left 8 CUs streaming config 4's logits
+// (0.31 ms for 17 MB).
 // -------------------------------------------------------------------------------------
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + expf(-x)); }
 
-__global__ __launch_bounds__(1024) void loss_stats_kernel(const float* __restrict__ x,
-                                                         const float* __restrict__ t, int64_t per,
-                                                         float* __restrict__ stats) {
-    __shared__ float red[4][32];
-    const int n = blockIdx.x;
+__device__ __forceinline__ void loss_elem(float xv, float tv, float (&a)[4]) {
+    const float pv = sigmoidf_(xv);
+    a[0] += pv * tv;
+    a[1] += pv;
+    a[2] += tv;
+    a[3] += (1.f - tv) * xv - (fminf(xv, 0.f) - log1pf(expf(-fabsf(xv))));
+}
+
+__global__ __launch_bounds__(256) void loss_stats_kernel(const float* __restrict__ x,
+                                                        const float* __restrict__ t, int64_t per,
+                                                        int G, float* __restrict__ part) {
+    __shared__ float red[4][4];
+    const int n = blockIdx.x / G, g = blockIdx.x - n * G;
+    const int64_t chunk = (per + G - 1) / G;
+    const int64_t i0 = g * chunk, i1 = min(per, i0 + chunk);
     const float* xs = x + n * per;
     const float* ts = t + n * per;
     float a[4] = {0, 0, 0, 0};
-    for (int64_t i = threadIdx.x; i < per; i += blockDim.x) {
-        const float xv = xs[i], tv = ts[i];
-        const float pv = sigmoidf_(xv);
-        a[0] += pv * tv;
-        a[1] += pv;
-        a[2] += tv;
-        a[3] += (1.f - tv) * xv - (fminf(xv, 0.f) - log1pf(expf(-fabsf(xv))));
+    if ((per & 3) == 0 && (chunk & 3) == 0 && ((((uintptr_t)x) | ((uintptr_t)t)) & 15) == 0) {
+        for (int64_t i = i0 + 4 * threadIdx.x; i < i1; i += 4 * blockDim.x) {
+            const f32x4 xv = *(const f32x4*)(xs + i), tv = *(const f32x4*)(ts + i);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) loss_elem(xv[j], tv[j], a);
+        }
+    } else {
+        for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) loss_elem(xs[i], ts[i], a);
     }
     for (int k = 0; k < 4; ++k)
         for (int d = 32; d >= 1; d >>= 1) a[k] += __shfl_xor(a[k], d);
@@ -1511,11 +1592,9 @@ __global__ __launch_bounds__(1024) void loss_stats_kernel(const float* __restric
     if (ln == 0)
         for (int k = 0; k < 4; ++k) red[k][wv] = a[k];
     __syncthreads();
-    if (threadIdx.x < 4) {
-        float s = 0.f;
-        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) s += red[threadIdx.x][w];
-        stats[4 * n + threadIdx.x] = s;
-    }
+    if (threadIdx.x < 4)
+        part[4 * (int64_t)blockIdx.x + threadIdx.x] =
+            (red[threadIdx.x][0] + red[threadIdx.x][1]) + (red[threadIdx.x][2] + red[threadIdx.x][3]);
 }
 
 // Batch sums of the per-sample statistics (double, fixed sample order):
@@ -1524,9 +1603,17 @@ __global__ __launch_bounds__(1024) void loss_stats_kernel(const float* __restric
 // parallelism an all-reduce (SUM) of `sums` turns every rank's local batch into the
 // reference's gathered batch (nn.DataParallel computes the loss on the gathered logits,
 // utils/trainer.py:28-30,85-90; FocalTversky's TP/FP/FN are global, models/loss.py:41-45).
-__global__ void loss_sums_kernel(const float* __restrict__ stats, int N, int64_t per,
-                                 double* __restrict__ sums) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+__global__ __launch_bounds__(256) void loss_sums_kernel(const float* __restrict__ part, int G,
+                                                       float* __restrict__ stats, int N,
+                                                       int64_t per, double* __restrict__ sums) {
+    for (int j = threadIdx.x; j < 4 * N; j += blockDim.x) {  // a sample's chunks, in order
+        const int n = j >> 2, k = j & 3;
+        float v = 0.f;
+        for (int g = 0; g < G; ++g) v += part[4 * ((int64_t)n * G + g) + k];
+        stats[j] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
     double bce = 0, dice = 0, tp = 0, sp = 0, st = 0;
     for (int n = 0; n < N; ++n) {
         const double I = stats[4 * n], P = stats[4 * n + 1], T = stats[4 * n + 2];
@@ -1820,13 +1907,21 @@ int k_to_bf16(const float* src, int ld, int off, int C, const float* scale, cons
     LAUNCH_CHECK();
 }
 int k_bn_dz16(float* d, const float* y, int ld, int off, int64_t P, int C, const float* coef,
-              int mask, uint16_t* dz16, int f32, hipStream_t s) {
+              int mask, uint16_t* dz16, int f32, hipStream_t s, const float* hdl, const float* hw,
+              const float* hsc, const float* hsh, int hrelu) {
     if (C % 8 || ld % 4 || off % 4) return -1;
     const int c8 = C / 8;
     const int tpr = c8 >= 256 ? 256 : c8;
     if (256 % tpr || (c8 > 256 && c8 % 256)) return -1;
-    hipLaunchKernelGGL(bn_dz16_kernel<false>, dim3(grid_for((P + 3) / 4 * tpr)), dim3(256), 0, s, d, y, ld, off,
-                       P, C, coef, mask, tpr, (__bf16*)dz16, f32, Dz16Pool{});
+    if (hdl) {  // do recomputed from the head: no do to read, none to write back
+        if (!hw || !hsc || !hsh || f32) return -1;
+        hipLaunchKernelGGL(bn_dz16_kernel<1>, dim3(grid_for((P + 3) / 4 * tpr)), dim3(256), 0, s, nullptr, y, ld,
+                           off, P, C, coef, mask, tpr, (__bf16*)dz16, 0, Dz16Pool{},
+                           Dz16Head{hdl, hw, hsc, hsh, hrelu});
+        LAUNCH_CHECK();
+    }
+    hipLaunchKernelGGL(bn_dz16_kernel<0>, dim3(grid_for((P + 3) / 4 * tpr)), dim3(256), 0, s, d, y, ld, off,
+                       P, C, coef, mask, tpr, (__bf16*)dz16, f32, Dz16Pool{}, Dz16Head{});
     LAUNCH_CHECK();
 }
 int k_bn_dz16_pool(const float* y, int ld, int off, int64_t P, int C, const float* coef, int mask,
@@ -1838,8 +1933,8 @@ int k_bn_dz16_pool(const float* y, int ld, int off, int64_t P, int C, const floa
     const int tpr = c8 >= 256 ? 256 : c8;
     if (256 % tpr || (c8 > 256 && c8 % 256)) return -1;
     const Dz16Pool pl{dp, idx, dskip, ldskip, msc, msh, H, W, 1.f / (float)H, 1.f / (float)W};
-    hipLaunchKernelGGL(bn_dz16_kernel<true>, dim3(grid_for((P + 3) / 4 * tpr)), dim3(256), 0, s, nullptr, y, ld,
-                       off, P, C, coef, mask, tpr, (__bf16*)dz16, 0, pl);
+    hipLaunchKernelGGL(bn_dz16_kernel<2>, dim3(grid_for((P + 3) / 4 * tpr)), dim3(256), 0, s, nullptr, y, ld,
+                       off, P, C, coef, mask, tpr, (__bf16*)dz16, 0, pl, Dz16Head{});
     LAUNCH_CHECK();
 }
 int k_bias_reduce(const float* slab, int S, int taps, int C, float* out, hipStream_t s) {
@@ -1869,6 +1964,11 @@ int k_slab_reduce(const float* slab, int S, int Mw, int Nw, int kind, int cin, i
     if (kind == 0 && S > 1 && S < 32 && cin % 8 == 0 && cout % 32 == 0 && (cin / 8) * (cout / 32) >= 256) {
         hipLaunchKernelGGL(slab_reduce_conv3_kernel<8>, dim3(cout / 32, cin / 8), dim3(256), 0, s, slab,
                            S, cin, cout, grad);
+        LAUNCH_CHECK();
+    }
+    if (kind == 1 && S < 32 && Mw == cin && Nw == 4 * cout && ((uintptr_t)grad & 15) == 0) {
+        hipLaunchKernelGGL(slab_reduce_convT_kernel, dim3((int)(((int64_t)cin * cout + 255) / 256)), dim3(256),
+                           0, s, slab, S, cin, cout, grad);
         LAUNCH_CHECK();
     }
     if (Nw % 4) return -1;
@@ -1927,11 +2027,13 @@ int k_head_bwd(const float* y, int C, const float* scale, const float* shift, in
                        HW, dlog, dout, partial, bnpart);
     LAUNCH_CHECK();
 }
+int loss_groups(int64_t per) { return (int)std::min<int64_t>(256, std::max<int64_t>(1, per / 4096)); }
 int k_loss_stats(const float* x, const float* t, int N, int64_t per, float* stats, double* sums,
-                 hipStream_t s) {
-    hipLaunchKernelGGL(loss_stats_kernel, dim3(N), dim3(1024), 0, s, x, t, per, stats);
+                 float* part, hipStream_t s) {
+    const int G = loss_groups(per);
+    hipLaunchKernelGGL(loss_stats_kernel, dim3(N * G), dim3(256), 0, s, x, t, per, G, part);
     HIP_OK(hipGetLastError());
-    hipLaunchKernelGGL(loss_sums_kernel, dim3(1), dim3(64), 0, s, stats, N, per, sums);
+    hipLaunchKernelGGL(loss_sums_kernel, dim3(1), dim3(256), 0, s, part, G, stats, N, per, sums);
     LAUNCH_CHECK();
 }
 int k_loss_finalize(const double* sums, float alpha, float beta, float gamma, float* losses,

@@ -165,8 +165,8 @@ struct Options {
                                // +0.45 % (profiles/r05_wwaves_ab.txt)
     int pool_fuse = 1;         // x3 and (r06) bf16 paths: the encoder block's second conv recomputes its `do` from
                                // the max-pool backward's inputs instead of maxpool_bwd storing it
-    int head_fuse = 1;         // x3 path, one output channel: the last conv's dz pass recomputes
-                               // `do` from the head instead of head_bwd storing it (r05)
+    int head_fuse = 1;         // x3 (r05) and bf16 (r06) paths, one output channel: the last conv's dz
+                               // pass recomputes `do` from the head instead of head_bwd storing it
     int tile_group = 1;        // (r06) row-GEMM tile order of the LDS-DMA kernels (rg16, x3): 1 = grouped
                                // where the N tiles are many (tile_group_auto), 0 = M-major (r05);
                                // bit-identical
@@ -282,6 +282,9 @@ struct unet_ctx {
     // read them records the generation its backward must still see
     float* pp = nullptr;
     uint16_t* pp3 = nullptr;
+    // (r06) per-chunk loss statistics of unet_loss_stats (4 floats per chunk, grown on demand)
+    float* lpart = nullptr;
+    int64_t lpart_n = 0;
     const float* pp_src = nullptr;
     bool pp_ok = false;
     uint64_t pp_gen = 0;
@@ -1740,6 +1743,11 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
                                                q.dp, q.idx, q.dskip, q.ldskip, q.msc, q.msh, p.N, Hl, Wl, s));
             } else if (i == pool_src.conv) {
                 return fail(c, UNET_ERR_INTERNAL, "pool_fuse: conv %d needs an f32 dz", i);
+            } else if (i == head_src_conv) {  // (r06) do straight from the 1x1 head
+                if (f32) return fail(c, UNET_ERR_INTERNAL, "head_fuse: conv %d needs an f32 dz", i);
+                RUN("bn_dz", 0, k_bn_dz16(nullptr, p.y[i], p.ldy[i], p.offy[i], P, C.cout, p.coef, dz_mask,
+                                          p.s16, 0, s, dlogits, prm + c->head_w, p.scale[i], p.shift[i],
+                                          c->bn_relu ? 1 : 0));
             } else {
                 RUN("bn_dz", 0, k_bn_dz16(const_cast<float*>(dout), p.y[i], p.ldy[i], p.offy[i], P, C.cout,
                                           p.coef, dz_mask, p.s16, f32 ? 1 : 0, s));
@@ -2149,10 +2157,13 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
     }
     // ---- head + last decoder block (stage 0) ----
     const int last = NC - 1;
-    // (r05) one output channel on the x3 path: the last conv's dz pass recomputes `do` =
-    // mask * dl * w from the logit gradient, so head_bwd stores no full-resolution f32 `do`
-    const bool head_fuse = c->out_ch == 1 && c->conv[last].cout == c->base && p.pack3 &&
-                           x3_conv_on(c, c->conv[last].cin, c->conv[last].cout) && c->opt.head_fuse;
+    // (r05) one output channel on the x3 path (r06: and on the bf16 path's LDS-DMA GEMMs): the
+    // last conv's dz pass recomputes `do` = mask * dl * w from the logit gradient, so head_bwd
+    // stores no full-resolution f32 `do`
+    const ConvL& CL = c->conv[last];
+    const bool head_fuse = c->out_ch == 1 && CL.cout == c->base && c->opt.head_fuse &&
+                           ((p.pack3 && x3_conv_on(c, CL.cin, CL.cout)) ||
+                            (c->bf16 && p.x16[last] && rg16_on(c, CL.cout, CL.cin)));
     head_src_conv = head_fuse ? last : -1;
     RUN("head_bwd", 2.0 * p.P[0] * c->base * c->out_ch * 2,
         k_head_bwd(p.y[last], c->base, p.scale[last], p.shift[last], c->bn_relu ? 1 : 0,
@@ -2369,10 +2380,11 @@ int unet_destroy(unet_ctx* c) {
     if (!c) return UNET_ERR_INVALID;
     for (auto e : c->bucket_ev) (void)hipEventDestroy(e);
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
-    if (c->pp || c->pp3) {
+    if (c->pp || c->pp3 || c->lpart) {
         (void)hipSetDevice(c->device);
         if (c->pp) (void)hipFree(c->pp);
         if (c->pp3) (void)hipFree(c->pp3);
+        if (c->lpart) (void)hipFree(c->lpart);
     }
     delete c;
     return UNET_OK;
@@ -2513,7 +2525,21 @@ int unet_loss_stats(unet_ctx* c, const float* logits, const float* targets, int 
     ABI_TRY
     if (!c || !logits || !targets || !stats || !sums) return UNET_ERR_INVALID;
     if (N < 1 || C < 1 || H < 1 || W < 1) return fail(c, UNET_ERR_SHAPE, "bad loss shape");
-    int r = k_loss_stats(logits, targets, N, (int64_t)C * H * W, stats, sums, (hipStream_t)stream);
+    const int64_t per = (int64_t)C * H * W, need = 4 * (int64_t)N * loss_groups(per);
+    if (need > c->lpart_n) {
+        if (hipSetDevice(c->device) != hipSuccess) return fail(c, UNET_ERR_HIP, "hipSetDevice");
+        if (c->lpart) {  // a loss pass of an earlier call may still read it
+            (void)hipDeviceSynchronize();
+            (void)hipFree(c->lpart);
+        }
+        c->lpart_n = 0;
+        if (hipMalloc((void**)&c->lpart, sizeof(float) * (size_t)need) != hipSuccess) {
+            c->lpart = nullptr;
+            return fail(c, UNET_ERR_HIP, "hipMalloc: loss partials: %lld floats", (long long)need);
+        }
+        c->lpart_n = need;
+    }
+    int r = k_loss_stats(logits, targets, N, per, stats, sums, c->lpart, (hipStream_t)stream);
     return r ? fail(c, UNET_ERR_HIP, "loss_stats launch %d", r) : UNET_OK;
     ABI_CATCH(c)
 }
