@@ -358,8 +358,10 @@ __device__ __forceinline__ void x3r3_body16(const RowGemmArgs& p, char* smem, in
             if (j < j0 || j >= j1) continue;
             const int yy = (apk[j] >> 7) + dy - 1;
             const bool valid = acen[j] >= 0 && yy >= 0 && yy < H;
-            const uint16_t* src =
-                valid ? a16 + (size_t)(acen[j] + (dy - 1) * W) * rowa + c0 * 3 + (apk[j] & 127) : zero;
+            // 32 x 32 -> 64-bit row offset plus a 32-bit in-row offset (no 64-bit loop invariants)
+            const uint64_t off = (uint64_t)(uint32_t)(acen[j] + (dy - 1) * W) * (uint32_t)rowa +
+                                 (uint32_t)(c0 * 3 + (apk[j] & 127));
+            const uint16_t* src = valid ? a16 + off : zero;
             x3_dma16(src, base + (j * WAVES + wave) * 1024);
         }
     };
@@ -381,7 +383,9 @@ __device__ __forceinline__ void x3r3_body16(const RowGemmArgs& p, char* smem, in
     };
     const int ks = lane >> 4, rs = lane & 15;
     const int rperm = m16_row(rs);
-    int ahb[2][2], bro[NT][2], bfx[NT][2];
+    // B rows wn WN + nt 32 + bn 16 + rs: one swizzle for all of them, bit 2 of rs
+    const int bfx = (rs >> 1) & 2;
+    int ahb[2][2], bro[NT][2];
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
@@ -396,7 +400,6 @@ __device__ __forceinline__ void x3r3_body16(const RowGemmArgs& p, char* smem, in
         for (int bn = 0; bn < 2; ++bn) {
             const int r = wn * WN + nt * 32 + bn * 16 + rs;
             bro[nt][bn] = r * RB;
-            bfx[nt][bn] = swz(r);
         }
     // LAG: the previous sub-step's deferred fragments (the second 32-row half)
     bf16x8 ha[2][3], hb[NT][2][3];
@@ -435,7 +438,7 @@ __device__ __forceinline__ void x3r3_body16(const RowGemmArgs& p, char* smem, in
             for (int bn = 0; bn < 2; ++bn)
 #pragma unroll
                 for (int q = 0; q < 3; ++q)
-                    bfr[nt][bn][q] = *(const bf16x8*)(bbase + bro[nt][bn] + q * 64 + ((ks ^ bfx[nt][bn]) << 4));
+                    bfr[nt][bn][q] = *(const bf16x8*)(bbase + bro[nt][bn] + q * 64 + ((ks ^ bfx) << 4));
 #pragma unroll
         for (int bm = 0; bm < 2; ++bm) {
             const int h = ahb[0][bm] + dx;

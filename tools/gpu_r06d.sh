@@ -1,6 +1,6 @@
 # GPU-box script (r06): selected GPU tests (-k, "-" = none), then bench A/B rounds of config 4
 # and config 2 over bench.py argument sets (SET: space-free, comma-separated args, "-" = none;
-# e.g. "--adamw=plain" or "--opt=pool_fuse=0").
+# e.g. "--adamw=plain", "--opt=pool_fuse=0" or "--lib=$PWD/ab_base.so").
 #   usage: bash tools/gpu_r06d.sh TAG "PYTEST_K" ROUNDS "SET1" "SET2" ...
 set -u
 cd $GRAFT_REPO_ROOT
@@ -20,8 +20,11 @@ for cfg in ${CFGS:-c4 c2}; do
     i=0
     for S in "$@"; do
       i=$((i+1))
-      EXTRA=""
+      EXTRA=""; LIBV=""
       [ "$S" != "-" ] && EXTRA=$(echo "$S" | tr ',' ' ' | sed 's/--opt=/--opt /g; s/--adamw=/--adamw /g')
+      # "--lib=PATH": run this set against another build of the library (UNET_HIP_LIB)
+      case "$EXTRA" in *--lib=*) LIBV=$(echo "$EXTRA" | sed 's/.*--lib=\([^ ]*\).*/\1/'); EXTRA=$(echo "$EXTRA" | sed 's/--lib=[^ ]*//');; esac
+      UNET_HIP_LIB=${LIBV:-$GRAFT_REPO_ROOT/thyroid-nodule-image-segmentation-unet-ddti_amd/lib/libunet_hip.so} \
       timeout -k 10 300 python bench.py --no-cpu-baseline --verbose $BA $EXTRA \
         > gpurun_out/$TAG.$cfg.r$r.s$i.json 2> gpurun_out/$TAG.$cfg.r$r.s$i.err
       rc=$?
