@@ -311,15 +311,17 @@ def test_convt16_pool_and_head_fuse_bit_identical():
     _assert_same(outs[(1, 1, 1)], outs[(1, 1, 0)], "head_fuse")
 
 
-def test_wg16_tap_row_bit_identical():
+@pytest.mark.parametrize("side", [256, 128])
+def test_wg16_tap_row_bit_identical(side):
     """The tap-row bf16 weight gradient (kernels_gemm16.hip wgrad16_row3_kernel, option wg16_r3
     = 4: the three dx taps of one tap row from one halo of 66 pixel rows) runs the same MFMA
     sequence per weight element as the one-tap kernel (same operands, pixel chunks, k-steps and
-    split partition), so one training step of BASELINE config 4's network at 256^2 (tap-row
+    split partition), so one training step of BASELINE config 4's network (256^2: tap-row
     levels W = 256, 128, 64; the rest fall back) is bit-identical.  The default, wg16_r3 = 7
-    (r06: the 16x16x32 kernel with the re-read stagger), sums 32 instead of 16 exact bf16
-    products per MFMA step: f32 rounding apart from those."""
-    x, t = inputs(43, 2, 256, 256)
+    (r06: the 16x16x32 kernel with the re-read stagger, also at W = 32 / 16 as 2 / 4 halo
+    segments per 64-pixel chunk: at 128^2 the levels W = 32, 16), sums 32 instead of 16 exact
+    bf16 products per MFMA step: f32 rounding apart from those."""
+    x, t = inputs(43, 2, side, side)
     P = MO.make_params(47, 128, 5)
     outs = {}
     for r3 in (0, 4, 7):

@@ -830,15 +830,24 @@ __global__ __launch_bounds__(512, 1) void wgrad16_row3_kernel(WgradArgs p) {
 //   work opens the segment while their partner waits for its first fragments.
 //   The sums run 32 products per MFMA step (16 on the 32x32x16 kernel): f32 rounding apart from
 //   tiles 3..5, bit-identical between 6 and 7 (same MFMAs in the same order per accumulator).
-template <int S, bool LAG>
+//   SEGW (r06): W % 64 == 0 (64), or the deep levels' W = 32 / 16 (config 4's 32^2 level and
+//   16^2 bottleneck, which ran the one-tap kernel): a 64-pixel chunk is then 64 / W whole image
+//   rows (H W % 64 == 0, so it never leaves its image), staged as 64 / W halo segments of W + 2
+//   pixels at a segment stride of 40 / 24 rows -- multiples of 8, so the row & 7 swizzle of a
+//   fragment read is the same in every segment -- and a k-step's 32 pixels read segment rows
+//   (one segment of 32, or two of 16).
+template <int S, bool LAG, int SEGW = 64>
 __global__ __launch_bounds__(512, 1) void wgrad16_row3_m16_kernel(WgradArgs p) {
     constexpr int BM = 128, BN = 128, WM = 32, WN = 64, BKP = 64;
     constexpr int WAVES_N = BN / WN, WAVES = (BM / WM) * WAVES_N;  // 4 x 2
     constexpr int RA = 2 * BM, RBB = 2 * BN;     // 256-B pixel rows
     constexpr int LA = RA / 16, LB = RBB / 16;   // 16 lanes per row in a DMA instruction
     constexpr int PA = 64 / LA, PB = 64 / LB;    // 4 rows per DMA instruction
-    constexpr int AROWS = BKP + 2;               // halo rows
-    constexpr int NA = (AROWS + PA - 1) / PA;    // 17 A' pieces
+    static_assert(SEGW == 64 || SEGW == 32 || SEGW == 16, "segment width");
+    constexpr int NSEG = BKP / SEGW;             // image rows per chunk (W < 64)
+    constexpr int SS = SEGW == 64 ? BKP : SEGW == 32 ? 40 : 24;  // halo segment stride (rows)
+    constexpr int AROWS = (NSEG - 1) * SS + SEGW + 2;            // halo rows: 66 / 74 / 90
+    constexpr int NA = (AROWS + PA - 1) / PA;    // 17 / 19 / 23 A' pieces
     constexpr int AI = (NA + WAVES - 1) / WAVES;  // 3 (the third: wave 0 only)
     constexpr int BI = BKP / (PB * WAVES);       // 2
     static_assert(BI * PB * WAVES == BKP && (AI - 1) * WAVES < NA, "loader shape");
@@ -876,20 +885,20 @@ __global__ __launch_bounds__(512, 1) void wgrad16_row3_m16_kernel(WgradArgs p) {
     auto swz = [](int sl, int row) { return sl ^ ((row & 7) << 1); };
 
     auto issue = [&](int kc, int st) {
-        const int pc = pbeg + kc * BKP;  // first output pixel of the chunk (one image row)
+        const int pc = pbeg + kc * BKP;  // first output pixel of the chunk (one image row / NSEG rows)
         const Pix q = decode_fast(pc, H, W, rH, rW);
-        const int yy = q.y + dy - 1;
-        const bool rowok = yy >= 0 && yy < H;
-        const int srow = (q.img * H + yy) * W;
         char* base = smem + st * STAGE;
 #pragma unroll
         for (int j = 0; j < AI; ++j) {
             if (j == AI - 1 && !a3) continue;
-            const int row = (j * WAVES + wave) * PA + lra;  // halo row: column x0 - 1 + row
+            const int row = (j * WAVES + wave) * PA + lra;  // halo row
             const int gcha = swz(lane % LA, row) * 8;
-            const int xx = q.x - 1 + row;
-            const bool ok = rowok && row < AROWS && xx >= 0 && xx < W;
-            const uint16_t* g = ok ? a16 + (size_t)(srow + xx) * p.lda + ca0 + gcha : zero;
+            // segment sg (image row q.y + sg), column xx of halo row `row` (segment offset - 1)
+            const int sg = SEGW == 64 ? 0 : row / SS;
+            const int xx = (SEGW == 64 ? q.x : 0) - 1 + row - sg * SS;
+            const int yy = q.y + sg + dy - 1;
+            const bool ok = row < AROWS && sg < NSEG && xx >= 0 && xx < W && yy >= 0 && yy < H;
+            const uint16_t* g = ok ? a16 + (size_t)((q.img * H + yy) * W + xx) * p.lda + ca0 + gcha : zero;
             glds16(g, base + (j * WAVES + wave) * 1024);
         }
 #pragma unroll
@@ -938,12 +947,15 @@ __global__ __launch_bounds__(512, 1) void wgrad16_row3_m16_kernel(WgradArgs p) {
             f.b[bn][0] = ds_tr16<kk * 32 * RBB>(sb + boff[bn]);
             f.b[bn][1] = ds_tr16<kk * 32 * RBB + 16 * RBB>(sb + boff[bn]);
         }
+        // halo rows of the k-step's two 16-pixel halves (the same row & 7 as kk = 0's)
+        constexpr int R0 = SEGW == 64 ? kk * 32 : SEGW == 32 ? kk * SS : 2 * kk * SS;
+        constexpr int R1 = SEGW == 16 ? R0 + SS : R0 + 16;
 #pragma unroll
         for (int dx = 0; dx < 3; ++dx)
 #pragma unroll
             for (int bm = 0; bm < 2; ++bm) {
-                f.a[dx][bm][0] = ds_tr16<kk * 32 * RA>(sb + aoff[dx][bm]);
-                f.a[dx][bm][1] = ds_tr16<kk * 32 * RA + 16 * RA>(sb + aoff[dx][bm]);
+                f.a[dx][bm][0] = ds_tr16<R0 * RA>(sb + aoff[dx][bm]);
+                f.a[dx][bm][1] = ds_tr16<R1 * RA>(sb + aoff[dx][bm]);
             }
     };
     auto mma = [&](const Frag& f) {
@@ -1116,12 +1128,18 @@ int launch_rowgemm16(const RowGemmArgs& a, int tile, hipStream_t s) {
 int launch_wgrad16(const WgradArgs& a, int tile, hipStream_t s) {
     if (a.aoff || a.boff || a.ascale || a.bcoef || a.bias_slab || !a.zero16 || a.P < 1) return -1;
     if (tile == 4 || tile == 7) {  // tap-row kernel: 3x3 conv layers, W % 64 == 0 (4: 32x32x16, 4 LDS
-                                   // stages; 7: 16x16x32 with the re-read stagger, r06)
+                                   // stages; 7: 16x16x32 with the re-read stagger, r06, and also
+                                   // W = 32 / 16 with H W % 64 == 0)
+        const bool deep = tile == 7 && (a.W == 32 || a.W == 16) && (a.H * a.W) % 64 == 0;
         if (a.amode != G_CONV3 || a.bmode != G_IDENT || a.Mw != 9 * a.CA || a.Nw != a.CB ||
-            a.CA % 128 || a.CB % 128 || a.W % 64 || a.pps % 64)
+            a.CA % 128 || a.CB % 128 || (a.W % 64 && !deep) || a.pps % 64 || a.P % 64)
             return -1;
         const dim3 grid((a.CA / 128) * 3 * (a.Nw / 128) * a.splits);
-        if (tile == 7)
+        if (tile == 7 && a.W == 32)
+            hipLaunchKernelGGL((wgrad16_row3_m16_kernel<4, true, 32>), grid, dim3(512), 0, s, a);
+        else if (tile == 7 && a.W == 16)
+            hipLaunchKernelGGL((wgrad16_row3_m16_kernel<4, true, 16>), grid, dim3(512), 0, s, a);
+        else if (tile == 7)
             hipLaunchKernelGGL((wgrad16_row3_m16_kernel<4, true>), grid, dim3(512), 0, s, a);
         else
             hipLaunchKernelGGL((wgrad16_row3_kernel<4>), grid, dim3(512), 0, s, a);

@@ -700,7 +700,8 @@ WgradCfg wgrad_cfg(const unet_ctx* c, int CA, int tapsA, int CB, int tapsB, int6
     // blocks, and the kernel took three block durations instead of two.  Instead pick the split
     // count s minimising waves(s) x chunks per block(s) + the slab traffic of s splits (the
     // one-tap kernel, option wg16_r3 = 0, gets the same partition: bit-identical).
-    if (bf16 && tapsA == 9 && tapsB == 1 && row_w > 0 && row_w % 64 == 0 &&
+    // (W = 32 / 16: the deep levels' tap-row instances, wg16_r3 = 7, r06)
+    if (bf16 && tapsA == 9 && tapsB == 1 && row_w > 0 && (row_w % 64 == 0 || row_w == 32 || row_w == 16) &&
         CA % 128 == 0 && CB % 128 == 0 && P % 64 == 0) {
         const int64_t t3 = (int64_t)(CA / 128) * 3 * (CB / 128);
         const int64_t slots = c->cus;
@@ -1803,7 +1804,9 @@ int backward_impl(unet_ctx* c, const float* prm, const float* dlogits, float* gr
             int t = wg16_tile(c, C.cin, C.cout);
             // option wg16_r3: the tap-row kernel (three taps per block from one halo row)
             const int r3 = c->opt.wg16_r3;
-            if ((r3 == 4 || r3 == 7) && Wl % 64 == 0 && C.cin % 128 == 0 && C.cout % 128 == 0 &&
+            // (r06) tile 7 also at W = 32 / 16 (the 32^2 level and the 16^2 bottleneck)
+            const bool deep = r3 == 7 && (Wl == 32 || Wl == 16) && (Hl * Wl) % 64 == 0 && P % 64 == 0;
+            if ((r3 == 4 || r3 == 7) && (Wl % 64 == 0 || deep) && C.cin % 128 == 0 && C.cout % 128 == 0 &&
                 wc.pps % 64 == 0)
                 t = r3;
             int wbm = 0, wbn = 0, wst = 0;
