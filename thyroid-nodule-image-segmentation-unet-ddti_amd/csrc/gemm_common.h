@@ -399,6 +399,31 @@ __device__ __forceinline__ void row_epilogue(const RowGemmArgs& p, f32x16 (&acc)
                 }
             return;
         }
+        if (p.out16 && ((p.ldo | p.ooff | p.cout) & 1) == 0) {
+            // bf16 straight into the consumer's operand image (RNE, as k_to_bf16), two channels
+            // per 4-B store with the out3 pairing above (r06: half the store instructions)
+            const int odd = li & 1;
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                for (int r2 = 0; r2 < 8; ++r2) {
+                    const int row = 2 * r2 + odd;
+                    const int m = m0 + wm * WM + mt * 32 + (row & 3) + 8 * (row >> 2) + 4 * lh;
+                    const Pix q = decode_fast(m < p.M ? m : 0, H, W, rH, rW);
+                    const size_t ob = (size_t)(q.img * 2 * H + 2 * q.y) * (2 * W) + 2 * q.x;
+#pragma unroll
+                    for (int nt = 0; nt < NT; ++nt) {
+                        const float v0 = acc[mt][nt][2 * r2] + bb[nt], v1 = acc[mt][nt][2 * r2 + 1] + bb[nt];
+                        const float recv = __shfl_xor(odd ? v0 : v1, 1);
+                        const float ve = odd ? recv : v0, vo = odd ? v1 : recv;  // columns li & ~1, li | 1
+                        if (m >= p.M) continue;
+                        const uint32_t be = __builtin_bit_cast(uint16_t, (__bf16)ve);
+                        const uint32_t bo = __builtin_bit_cast(uint16_t, (__bf16)vo);
+                        *(uint32_t*)(p.out16 + (ob + coff[nt]) * p.ldo + p.ooff + co_[nt] - odd) = be | (bo << 16);
+                    }
+                }
+            return;
+        }
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
@@ -407,7 +432,7 @@ __device__ __forceinline__ void row_epilogue(const RowGemmArgs& p, f32x16 (&acc)
                 if (m >= p.M) continue;
                 const Pix q = decode_fast(m, H, W, rH, rW);
                 const size_t ob = (size_t)(q.img * 2 * H + 2 * q.y) * (2 * W) + 2 * q.x;
-                if (p.out16) {  // bf16 straight into the consumer's operand image (RNE, as k_to_bf16)
+                if (p.out16) {  // (odd ld / offset / cout: one 2-B store per element)
 #pragma unroll
                     for (int nt = 0; nt < NT; ++nt)
                         ((__bf16*)p.out16)[(ob + coff[nt]) * p.ldo + p.ooff + co_[nt]] =
