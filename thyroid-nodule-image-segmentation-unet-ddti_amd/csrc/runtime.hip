@@ -136,8 +136,9 @@ struct Options {
                                // (no f32 up half; its prep pass converts the skip half only)
     int wg16_r3 = 7;           // 3x3 layers with W % 64 == 0 on the tap-row bf16 weight gradient:
                                // 7 = 16x16x32 MFMAs with the re-read stagger (r06, config 4
-                               // +1.3 % over 4, profiles/r06_c4_wg16_ab.txt), 4 = 32x32x16, four
-                               // LDS stages (r04: 122.7 -> 125.2 img/s), 0 = off (one-tap kernel)
+                               // +1.3 % over 4, profiles/r06_c4_wg16_ab.txt; also at W = 32 / 16,
+                               // +1.4 %, r06_c4_deep_wgrad_ab.txt), 4 = 32x32x16, four LDS stages
+                               // (r04: 122.7 -> 125.2 img/s), 0 = off (one-tap kernel)
     int wg16t = 1;             // bf16 ConvT wgrad on the same kernel
     int xcd16 = 1;             // XCD-contiguous block order, LDS-DMA kernels
     int xcd_remap = 1;         // ... f32 GEMMs: 0 none, 1 both (default: r03 PMC, HBM bytes
