@@ -147,7 +147,10 @@ int unet_backward(unet_ctx* ctx, const float* params, const float* dlogits, floa
  *        TP/FP/FN are batch-global (models/loss.py:41-45)]
  *   unet_loss_finalize  losses (device fp32[3]) <- {bce_mean, dice_loss, focal_tversky}
  * unet_loss_fwd = unet_loss_stats + unet_loss_finalize (single process).
- * focal uses (alpha, beta, gamma) of utils/trainer.py:38 / models/loss.py:27 defaults. */
+ * focal uses (alpha, beta, gamma) of utils/trainer.py:38 / models/loss.py:27 defaults.
+ * (r06) unet_loss_stats sums each sample in chunks into a context-owned scratch (grown on
+ * demand, synchronising the device when it grows): one loss pass per context in flight at a
+ * time, i.e. issue a context's loss calls on one stream. */
 int unet_loss_stats(unet_ctx* ctx, const float* logits, const float* targets, int N, int C, int H,
                     int W, float* stats, double* sums, unet_stream_t stream);
 int unet_loss_finalize(unet_ctx* ctx, const double* sums, float* losses, float focal_alpha,
