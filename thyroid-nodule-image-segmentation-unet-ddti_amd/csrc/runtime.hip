@@ -763,7 +763,9 @@ int rg16_tile(const unet_ctx* c, const RowGemmArgs& g) {
         return tn;
     }
     const int64_t blocks = (g.M + 255) / 256 * (g.N / 256);
-    if (blocks < 256) return t0;
+    // (r06) a grid too small for 256x256 that fills the CUs with 256x128 takes it (the 16^2
+    // bottleneck's 4096-output GEMMs of config 4) instead of 128x128 at two blocks per CU
+    if (blocks < 256) return (g.M + 255) / 256 * (g.N / 128) >= 256 && fits(2) ? 2 : t0;
     if (g.emode == E_STORE_BN && g.K < c->opt.rg16_bn_k) return t0;
     return t4;
 }
