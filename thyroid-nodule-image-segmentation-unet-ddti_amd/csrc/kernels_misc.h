@@ -44,9 +44,13 @@ int k_bn_finalize_train(const float* part, int G, int C, double count, const flo
 int k_bn_finalize_eval(int C, const float* gamma, const float* beta, const float* rmean,
                        const float* rvar, float eps, float* scale, float* shift, hipStream_t s);
 // relu / mscale+mshift: BN -> ReLU order (mod.py:46-47), see the kernels.
+// (r06) pool16: the pooled values as the next conv's bf16 image [pooled pixels][C]; skip16 / skip3:
+// op(BN(y)) at full resolution as bf16 / x3 into the decoder conv's kept image (ldk channels per
+// pixel, channel offset so) -- what k_to_bf16 / k_to_x3 would write there
 int k_maxpool_bn(const float* y, int ld, int off, const float* scale, const float* shift, int relu,
                  int N, int H, int W, int C, float* out, uint8_t* idx, hipStream_t s,
-                 uint16_t* out3 = nullptr);
+                 uint16_t* out3 = nullptr, uint16_t* pool16 = nullptr, uint16_t* skip16 = nullptr,
+                 uint16_t* skip3 = nullptr, int ldk = 0, int so = 0);
 int k_maxpool_bwd(const float* dp, const uint8_t* idx, const float* dskip, int ldskip, int offskip,
                   const float* y, int ldy, int offy, const float* mscale, const float* mshift,
                   int N, int H, int W, int C, float* dout, float* partial, int G, hipStream_t s);

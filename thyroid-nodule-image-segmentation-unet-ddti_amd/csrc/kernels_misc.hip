@@ -588,17 +588,62 @@ __global__ void bn_finalize_eval_kernel(int C, const float* __restrict__ gamma,
 // relu: BN -> ReLU order (mod.py:46-47); the max of ReLU(v) is ReLU(max v) and the winner
 // only differs where every candidate is <= 0, where the ReLU blocks its gradient anyway.
 // One pooled pixel: BN affine of the four window values, torch's tie rule, optional ReLU.
+// (r06) PoolImg: operand images the pass also writes from the values it forms anyway -- the
+// bf16 pooled image of the next encoder conv (pool16, [pooled pixels][C]) and, at full
+// resolution, the skip half of the decoder conv's kept image of this level (skip16: bf16
+// [pixels][ldk] at channel offset so; skip3: its x3 split, [pixels][ldk / 32][3][32]) with the
+// affine and ReLU k_to_bf16 / k_to_x3 would apply (same fma, same RNE): their prep passes then
+// have nothing left to convert.
+struct PoolImg {
+    uint16_t* pool16;
+    uint16_t* skip16;
+    uint16_t* skip3;
+    int ldk, so;
+};
 __device__ __forceinline__ void maxpool_px(const float* __restrict__ y, int ld, int off, f32x4 sc,
                                            f32x4 sh, int relu, int H, int W, int img, int yo,
                                            int xo, int c, float* __restrict__ out,
                                            uint8_t* __restrict__ idx, int64_t o,
-                                           uint16_t* __restrict__ out3 = nullptr, int C = 0) {
+                                           uint16_t* __restrict__ out3 = nullptr, int C = 0,
+                                           PoolImg pi = PoolImg{}) {
+    typedef uint16_t u16x4 __attribute__((ext_vector_type(4)));
     f32x4 best;
     uint32_t bi = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const int64_t pin = ((int64_t)img * H + 2 * yo + (k >> 1)) * W + 2 * xo + (k & 1);
-        const f32x4 v = *(const f32x4*)(y + pin * ld + off + c) * sc + sh;
+        const f32x4 yv = *(const f32x4*)(y + pin * ld + off + c);
+        f32x4 v;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = __builtin_fmaf(yv[j], sc[j], sh[j]);
+        if (pi.skip16 || pi.skip3) {  // the skip half's operand image: op(BN(y)) at this pixel
+            f32x4 t = v;
+            if (relu)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) t[j] = fmaxf(t[j], 0.f);
+            const int cc = pi.so + c;
+            if (pi.skip16) {
+                u16x4 b;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) b[j] = __builtin_bit_cast(uint16_t, (__bf16)t[j]);
+                *(u16x4*)(pi.skip16 + pin * pi.ldk + cc) = b;
+            }
+            if (pi.skip3) {
+                u16x4 h, m, l;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    uint16_t hj, mj, lj;
+                    x3_split(t[j], X3CvtDev{}, hj, mj, lj);
+                    h[j] = hj;
+                    m[j] = mj;
+                    l[j] = lj;
+                }
+                uint16_t* d = pi.skip3 + pin * 3 * pi.ldk + (cc >> 5) * 96 + (cc & 31);
+                *(u16x4*)d = h;
+                *(u16x4*)(d + 32) = m;
+                *(u16x4*)(d + 64) = l;
+            }
+        }
         if (k == 0) {
             best = v;
         } else {
@@ -614,8 +659,13 @@ __device__ __forceinline__ void maxpool_px(const float* __restrict__ y, int ld, 
 #pragma unroll
         for (int j = 0; j < 4; ++j) best[j] = fmaxf(best[j], 0.f);
     if (out) *(f32x4*)(out + o) = best;
+    if (pi.pool16) {  // bf16 (RNE) straight into the next conv's operand image [pixels][C]
+        u16x4 b;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) b[j] = __builtin_bit_cast(uint16_t, (__bf16)best[j]);
+        *(u16x4*)(pi.pool16 + o) = b;
+    }
     if (out3) {  // the x3 split straight into the next conv's operand image [pixels][C / 32][3][32]
-        typedef uint16_t u16x4 __attribute__((ext_vector_type(4)));
         u16x4 h, m, l;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -642,7 +692,7 @@ __global__ __launch_bounds__(256) void maxpool_bn_kernel(const float* __restrict
                                                          int N, int H, int W, int C,
                                                          float* __restrict__ out,
                                                          uint8_t* __restrict__ idx,
-                                                         uint16_t* __restrict__ out3) {
+                                                         uint16_t* __restrict__ out3, PoolImg pi) {
     const int Ho = H / 2, Wo = W / 2, c4n = C / 4;
     const int tpr = c4n < 256 ? c4n : 256, rpp = 256 / tpr;
     const int PO = N * Ho * Wo;
@@ -660,7 +710,7 @@ __global__ __launch_bounds__(256) void maxpool_bn_kernel(const float* __restrict
         Pix at = decode(min(r0 + g, PO - 1), Ho, Wo);
         for (int po = r0 + g; po < r1; po += rpp) {
             maxpool_px(y, ld, off, sc, sh, relu, H, W, at.img, at.y, at.x, c, out, idx,
-                       (int64_t)po * C + c, out3, C);
+                       (int64_t)po * C + c, out3, C, pi);
             pix_advance(at, rpp, Ho, Wo);
         }
     }
@@ -671,7 +721,7 @@ __global__ void maxpool_bn_any_kernel(const float* __restrict__ y, int ld, int o
                                       const float* __restrict__ scale,
                                       const float* __restrict__ shift, int relu, int N, int H,
                                       int W, int C, float* __restrict__ out,
-                                      uint8_t* __restrict__ idx, uint16_t* __restrict__ out3) {
+                                      uint8_t* __restrict__ idx, uint16_t* __restrict__ out3, PoolImg pi) {
     const int Ho = H / 2, Wo = W / 2, c4n = C / 4;
     const int64_t total = (int64_t)N * Ho * Wo * c4n;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
@@ -683,7 +733,7 @@ __global__ void maxpool_bn_any_kernel(const float* __restrict__ y, int ld, int o
         const int yo = (int)(t % Ho), img = (int)(t / Ho);
         const f32x4 sc = scale ? *(const f32x4*)(scale + 4 * c4) : f32x4{1.f, 1.f, 1.f, 1.f};
         const f32x4 sh = shift ? *(const f32x4*)(shift + 4 * c4) : f32x4{0.f, 0.f, 0.f, 0.f};
-        maxpool_px(y, ld, off, sc, sh, relu, H, W, img, yo, xo, 4 * c4, out, idx, po * C + 4 * c4, out3, C);
+        maxpool_px(y, ld, off, sc, sh, relu, H, W, img, yo, xo, 4 * c4, out, idx, po * C + 4 * c4, out3, C, pi);
     }
 }
 
@@ -1857,16 +1907,20 @@ int k_bn_finalize_eval(int C, const float* gamma, const float* beta, const float
     LAUNCH_CHECK();
 }
 int k_maxpool_bn(const float* y, int ld, int off, const float* scale, const float* shift, int relu,
-                 int N, int H, int W, int C, float* out, uint8_t* idx, hipStream_t s, uint16_t* out3) {
+                 int N, int H, int W, int C, float* out, uint8_t* idx, hipStream_t s, uint16_t* out3,
+                 uint16_t* pool16, uint16_t* skip16, uint16_t* skip3, int ldk, int so) {
     const int64_t n = (int64_t)N * (H / 2) * (W / 2) * (C / 4);
     const int c4n = C / 4;
-    if ((!out && !out3) || (out3 && C % 32)) return -1;
+    if ((!out && !out3 && !pool16) || (out3 && C % 32)) return -1;
+    if ((skip16 || skip3) && (so % 4 || ldk % 4 || so + C > ldk || (skip3 && (so % 32 || ldk % 32))))
+        return -1;
+    const PoolImg pi{pool16, skip16, skip3, ldk, so};
     if (C % 4 == 0 && c4n >= 1 && (int64_t)N * H * W < (1ll << 31))
         hipLaunchKernelGGL(maxpool_bn_kernel, dim3(grid_for(n)), dim3(256), 0, s, y, ld, off, scale,
-                           shift, relu, N, H, W, C, out, idx, out3);
+                           shift, relu, N, H, W, C, out, idx, out3, pi);
     else
         hipLaunchKernelGGL(maxpool_bn_any_kernel, dim3(grid_for(n)), dim3(256), 0, s, y, ld, off,
-                           scale, shift, relu, N, H, W, C, out, idx, out3);
+                           scale, shift, relu, N, H, W, C, out, idx, out3, pi);
     LAUNCH_CHECK();
 }
 int k_maxpool_bwd(const float* dp, const uint8_t* idx, const float* dskip, int ldskip, int offskip,

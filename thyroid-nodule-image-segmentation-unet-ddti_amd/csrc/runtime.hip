@@ -1354,6 +1354,9 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
     // x3: the max-pool wrote the next encoder conv's x3 operand image itself (no f32 pooled
     // tensor, no prep pass; r05)
     std::vector<char> pool3(NC, 0);
+    // (r06) bf16: the max-pool wrote the next encoder conv's bf16 operand image (pool16); both
+    // paths: the max-pool wrote the decoder conv's skip half of its kept image (skipimg)
+    std::vector<char> pool16(NC, 0), skipimg(NC, 0);
 
     auto conv = [&](int i) -> int {
         const ConvL& C = c->conv[i];
@@ -1393,6 +1396,8 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
                 uint16_t* img = p.x3[i] ? p.x3[i] : p.s3;
                 if (pool3[i]) {
                     // (the max-pool already stored op(pooled) as this conv's x3 image)
+                } else if (up16[i] && skipimg[i]) {
+                    // (the ConvT stored the up half, the max-pool the skip half)
                 } else if (up16[i]) {  // the ConvT stored the up half's x3 split: convert the skip half
                     const int l = C.level, so = c->skip_off(l), ch = c->ch(l);
                     const int rl = std::min(std::max(a.relu - so, 0), ch);
@@ -1410,7 +1415,9 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
             }
             if (rg16_on(c, C.cin, C.cout)) {
                 uint16_t* img = p.x16[i] ? p.x16[i] : p.s16;
-                if (up16[i]) {  // the ConvT stored the up half already: convert the skip half
+                if (pool16[i] || (up16[i] && skipimg[i])) {
+                    // (the max-pool / the ConvT and the max-pool stored the whole image)
+                } else if (up16[i]) {  // the ConvT stored the up half already: convert the skip half
                     const int l = C.level, so = c->skip_off(l);
                     RUN("prep16", 0, k_to_bf16(a.ptr, a.ld, a.off + so, c->ch(l), a.scale + so,
                                                a.shift + so, a.relu, M, img + so, s, C.cin));
@@ -1561,14 +1568,29 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
                 const int j = 2 * (b + 1);  // the next encoder block's first conv
                 const ConvL& Cj = c->conv[j];
                 uint16_t* out3 = nullptr;
+                uint16_t *o16 = nullptr, *s16 = nullptr, *s3 = nullptr;
                 if (p.pack3 && x3_conv_on(c, Cj.cin, Cj.cout)) {
                     out3 = p.x3[j] ? p.x3[j] : p.s3;
                     pool3[j] = 1;
+                } else if (p.x16[j] && rg16_on(c, Cj.cin, Cj.cout)) {  // (r06) training, bf16
+                    o16 = p.x16[j];
+                    pool16[j] = 1;
                 }
+                // (r06) the skip half of the decoder conv at this level (its ConvT stores the
+                // up half, option convt16): op(BN(y)) as that conv's kept operand image
+                const int idec = 2 * (2 * D - b);
+                const ConvL& Cd = c->conv[idec];
+                if (c->opt.convt16) {
+                    if (p.pack3 && p.x3[idec] && x3_conv_on(c, Cd.cin, Cd.cout))
+                        s3 = p.x3[idec];
+                    else if (c->bf16 && c->skip_first && p.x16[idec] && rg16_on(c, Cd.cin, Cd.cout))
+                        s16 = p.x16[idec];
+                }
+                skipimg[idec] = s3 || s16;
                 RUN("maxpool_fwd", 0,
                     k_maxpool_bn(p.y[i], p.ldy[i], p.offy[i], p.scale[i], p.shift[i],
                                  c->bn_relu ? 1 : 0, p.N, H >> b, W >> b, C, out3 ? nullptr : p.pool[b],
-                                 p.idx[b], s, out3));
+                                 p.idx[b], s, out3, o16, s16, s3, Cd.cin, c->skip_off(b)));
             }
         }
     }
