@@ -1589,7 +1589,8 @@ int forward_impl(unet_ctx* c, const float* prm, float* bn_run, int64_t* bn_cnt, 
                 skipimg[idec] = s3 || s16;
                 RUN("maxpool_fwd", 0,
                     k_maxpool_bn(p.y[i], p.ldy[i], p.offy[i], p.scale[i], p.shift[i],
-                                 c->bn_relu ? 1 : 0, p.N, H >> b, W >> b, C, out3 ? nullptr : p.pool[b],
+                                 c->bn_relu ? 1 : 0, p.N, H >> b, W >> b, C,
+                                 out3 || o16 ? nullptr : p.pool[b],  // (its images are the only readers)
                                  p.idx[b], s, out3, o16, s16, s3, Cd.cin, c->skip_off(b)));
             }
         }
@@ -2899,6 +2900,9 @@ int unet_debug_view(unet_ctx* c, int N, int H, int W, int training, int kind, in
             const ConvL& Cj = c->conv[2 * (index + 1)];
             if (!c->res && p.pack3 && x3_conv_on(c, Cj.cin, Cj.cout))
                 return fail(c, UNET_ERR_INVALID, "debug view 5: level %d pools into an x3 image", index);
+            // (r06) ... and a bf16 training pass pools into the next conv's bf16 image
+            if (!c->res && training && c->bf16 && wg16_on(c, Cj.cin, Cj.cout) && rg16_on(c, Cj.cin, Cj.cout))
+                return fail(c, UNET_ERR_INVALID, "debug view 5: level %d pools into a bf16 image", index);
             q = p.pool[index];
             n = p.P[index + 1] * C;
             l = C;
